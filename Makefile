@@ -1,0 +1,67 @@
+# Build libgachain (HIP/gfx950 kernels + C ABI + C host core), the drop-in
+# CLI tools, and the test-only oracle.  In-tree outputs (git-ignored, but they
+# travel to the GPU box with gpurun snapshots).
+#
+#   make            product: lib + tools
+#   make oracle     oracle/_build/libgacoracle.so (CPU restatement, tests only)
+#   make ref        oracle/_ref/* from /root/reference (needs the reference tree)
+
+HIPCC    ?= /opt/rocm/bin/hipcc
+CC       ?= gcc
+PKG      := genomealignmenttools_amd
+CSRC     := $(PKG)/csrc
+LIBDIR   := $(PKG)/lib
+BINDIR   := $(PKG)/bin
+OBJDIR   := build/obj
+
+ARCH     := gfx950
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
+            -Iinclude -I$(CSRC) -Wall -Wno-unused-result -Wno-unused-value
+CFLAGS   := -O2 -std=gnu11 -fPIC -Wall -Iinclude -I$(CSRC)
+
+HOST_SRC := $(wildcard $(CSRC)/host/*.c)
+HOST_OBJ := $(patsubst $(CSRC)/host/%.c,$(OBJDIR)/host/%.o,$(HOST_SRC))
+HIP_SRC  := $(CSRC)/gac_kernels.hip $(CSRC)/gac_device.hip
+HIP_OBJ  := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRC))
+HDRS     := include/gachain.h $(CSRC)/gac_kernels.h $(wildcard $(CSRC)/host/*.h)
+
+TOOLS    := $(patsubst $(CSRC)/tools/%.c,$(BINDIR)/%,$(wildcard $(CSRC)/tools/*.c))
+TOOL_LIB_SRC := $(wildcard $(CSRC)/tools/lib/*.c)
+TOOL_LIB_OBJ := $(patsubst $(CSRC)/tools/lib/%.c,$(OBJDIR)/tools/lib/%.o,$(TOOL_LIB_SRC))
+
+all: $(LIBDIR)/libgachain.so $(TOOLS)
+
+$(OBJDIR)/host/%.o: $(CSRC)/host/%.c $(HDRS)
+	@mkdir -p $(dir $@)
+	$(CC) $(CFLAGS) -c $< -o $@
+
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/libgachain.so: $(HIP_OBJ) $(HOST_OBJ)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,libgachain.so
+
+$(OBJDIR)/tools/lib/%.o: $(CSRC)/tools/lib/%.c $(HDRS) $(wildcard $(CSRC)/tools/lib/*.h)
+	@mkdir -p $(dir $@)
+	$(CC) $(CFLAGS) -I$(CSRC)/tools/lib -c $< -o $@
+
+$(BINDIR)/%: $(CSRC)/tools/%.c $(TOOL_LIB_OBJ) $(LIBDIR)/libgachain.so $(HDRS)
+	@mkdir -p $(BINDIR)
+	$(CC) $(CFLAGS) -I$(CSRC)/tools/lib $< $(TOOL_LIB_OBJ) -o $@ -L$(LIBDIR) -lgachain \
+	    -Wl,-rpath,'$$ORIGIN/../lib' -lm -lpthread
+
+oracle: oracle/_build/libgacoracle.so
+
+oracle/_build/libgacoracle.so: oracle/gac_oracle.c
+	@mkdir -p oracle/_build
+	$(CC) -O2 -std=gnu11 -fPIC -shared -Wall $< -o $@ -lm
+
+ref:
+	$(MAKE) -f oracle/ref.mk -j8
+
+clean:
+	rm -rf build $(LIBDIR) $(BINDIR) oracle/_build
+
+.PHONY: all oracle ref clean

@@ -1,0 +1,163 @@
+"""ctypes binding of libgachain (include/gachain.h).
+
+The library is built in-tree by ``make`` (``genomealignmenttools_amd/lib/
+libgachain.so``).  Loading fails loudly when it is missing or unbuildable:
+there is no Python or CPU fallback for any scoring entry point.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import threading
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libgachain.so")
+BIN_DIR = os.path.join(PKG_DIR, "bin")
+
+GAC_OK = 0
+GAC_T = 0
+GAC_Q = 1
+GAC_WANT_LOCAL = 1
+GAC_K_PLAN, GAC_K_TILE, GAC_K_COMBINE = 0, 1, 2
+
+_lock = threading.Lock()
+_lib = None
+
+
+class GacError(RuntimeError):
+    """Error returned by libgachain (message from gac_last_error())."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libgachain error {code}: {msg}")
+        self.code = code
+
+
+class GapCalc(C.Structure):
+    _fields_ = [
+        ("small_size", C.c_int32),
+        ("long_count", C.c_int32),
+        ("q_small", C.POINTER(C.c_int32)),
+        ("t_small", C.POINTER(C.c_int32)),
+        ("b_small", C.POINTER(C.c_int32)),
+        ("long_pos", C.POINTER(C.c_int32)),
+        ("q_long", C.POINTER(C.c_double)),
+        ("t_long", C.POINTER(C.c_double)),
+        ("b_long", C.POINTER(C.c_double)),
+        ("q_last_pos", C.c_int32),
+        ("t_last_pos", C.c_int32),
+        ("b_last_pos", C.c_int32),
+        ("q_last_val", C.c_double),
+        ("t_last_val", C.c_double),
+        ("b_last_val", C.c_double),
+        ("q_last_slope", C.c_double),
+        ("t_last_slope", C.c_double),
+        ("b_last_slope", C.c_double),
+    ]
+
+
+class ChainsetDesc(C.Structure):
+    _fields_ = [
+        ("n_chains", C.c_int64),
+        ("t_seq", C.c_void_p),
+        ("q_seq", C.c_void_p),
+        ("q_strand", C.c_void_p),
+        ("blk_off", C.c_void_p),
+        ("n_blocks", C.c_int64),
+        ("blk_t", C.c_void_p),
+        ("blk_q", C.c_void_p),
+        ("blk_size", C.c_void_p),
+    ]
+
+
+# name -> (restype, argtypes)
+_PROTOS = {
+    "gac_abi_version": (C.c_int, []),
+    "gac_last_error": (C.c_char_p, []),
+    "gac_open": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "gac_close": (None, [C.c_void_p]),
+    "gac_device_arch": (C.c_char_p, [C.c_void_p]),
+    "gac_gapcalc_build": (C.c_int, [C.c_char_p, C.POINTER(C.POINTER(GapCalc))]),
+    "gac_gapcalc_free": (None, [C.POINTER(GapCalc)]),
+    "gac_scheme_read": (
+        C.c_int,
+        [C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+         C.POINTER(C.c_void_p)],
+    ),
+    "gac_set_scoring": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(GapCalc)]),
+    "gac_genome_load_2bit": (C.c_int, [C.c_void_p, C.c_int, C.c_char_p]),
+    "gac_genome_add_seq": (
+        C.c_int,
+        [C.c_void_p, C.c_int, C.c_char_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p,
+         C.c_void_p],
+    ),
+    "gac_genome_finalize": (C.c_int, [C.c_void_p, C.c_int]),
+    "gac_genome_seq_count": (C.c_int32, [C.c_void_p, C.c_int]),
+    "gac_genome_seq_index": (C.c_int32, [C.c_void_p, C.c_int, C.c_char_p]),
+    "gac_genome_seq_size": (C.c_int32, [C.c_void_p, C.c_int, C.c_int32]),
+    "gac_genome_seq_name": (C.c_char_p, [C.c_void_p, C.c_int, C.c_int32]),
+    "gac_genome_decode": (
+        C.c_int, [C.c_void_p, C.c_int, C.c_int32, C.c_int32, C.c_int32, C.c_char_p]),
+    "gac_chains_upload": (C.c_int, [C.c_void_p, C.POINTER(ChainsetDesc), C.POINTER(C.c_void_p)]),
+    "gac_chains_free": (None, [C.c_void_p]),
+    "gac_chains_block_count": (C.c_int64, [C.c_void_p]),
+    "gac_score_ranges": (
+        C.c_int,
+        [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_uint32, C.c_void_p, C.c_void_p,
+         C.c_void_p],
+    ),
+    "gac_score_ranges_device": (
+        C.c_int,
+        [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_uint32, C.c_void_p, C.c_void_p,
+         C.c_void_p, C.c_void_p],
+    ),
+    "gac_dev_alloc": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
+    "gac_dev_free": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gac_memcpy_h2d": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
+    "gac_memcpy_d2h": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
+    "gac_synchronize": (C.c_int, [C.c_void_p]),
+    "gac_prof_enable": (C.c_int, [C.c_void_p, C.c_int]),
+    "gac_prof_read": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
+    "gac_prof_reset": (C.c_int, [C.c_void_p]),
+}
+
+EXPORTED = tuple(_PROTOS)
+
+
+def build(quiet: bool = True) -> None:
+    """Build libgachain + tools in-tree with make (hipcc --offload-arch=gfx950)."""
+    out = subprocess.run(
+        ["make", "-C", REPO_DIR, "-j8", "all"],
+        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if out.returncode != 0:
+        raise RuntimeError("building libgachain failed:\n" + out.stdout[-4000:])
+    if not quiet:
+        print(out.stdout)
+
+
+def lib() -> C.CDLL:
+    """Load libgachain.so (building it first if it is absent)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            build()
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: the HIP extension is required")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _PROTOS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.gac_abi_version() != 1:
+            raise RuntimeError("libgachain ABI mismatch")
+        _lib = L
+        return L
+
+
+def check(rc: int) -> None:
+    if rc != GAC_OK:
+        msg = lib().gac_last_error()
+        raise GacError(rc, msg.decode() if msg else "")

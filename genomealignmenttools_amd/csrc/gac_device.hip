@@ -1,0 +1,747 @@
+// gac_device.hip -- C-ABI implementation of libgachain (include/gachain.h):
+// device context, resident genomes, chainsets, batched sub-chain scoring.
+// There is deliberately no host fallback: every scoring entry point runs the
+// HIP kernels of gac_kernels.hip on a gfx950 device or returns an error.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "gac_kernels.h"
+#include "gachain.h"
+#include "host/gac_host.h"
+
+namespace gac {
+size_t scan_temp_bytes(int64_t n);
+hipError_t launch_plan(const ScoreArgs &a, hipStream_t s);
+hipError_t launch_scan_total(const ScoreArgs &a, void *temp, size_t temp_bytes, hipStream_t s);
+hipError_t launch_scatter(const ScoreArgs &a, hipStream_t s);
+hipError_t launch_tile(const ScoreArgs &a, int grid, hipStream_t s);
+hipError_t launch_combine(const ScoreArgs &a, int grid, hipStream_t s);
+struct SeqDev {
+    int64_t byte_off;
+    int64_t word_off;
+    int32_t size;
+    int32_t pad;
+};
+struct NPiece {
+    int64_t bit0;
+    int32_t len;
+    int32_t pad;
+};
+hipError_t launch_relayout(const uint8_t *raw, const SeqDev *seqs, int nseq, int64_t nwords,
+                           uint2 *planes, uint32_t *nmask, hipStream_t s);
+hipError_t launch_nruns(const NPiece *p, int64_t n, uint32_t *nmask, hipStream_t s);
+}  // namespace gac
+
+using namespace gac;
+
+#define HIPCHK(expr)                                                                        \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess)                                                               \
+            return gac_fail(GAC_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), \
+                            __FILE__, __LINE__);                                            \
+    } while (0)
+
+namespace {
+
+struct Genome {
+    // host-side staging until finalize
+    std::vector<std::string> names;
+    std::vector<int32_t> sizes;
+    std::unordered_map<std::string, int32_t> index;
+    std::vector<uint8_t> raw;       // concatenated packed payloads, 8-B aligned
+    std::vector<int64_t> raw_off;   // per seq
+    std::vector<NPiece> npieces;    // bit0 relative to the seq start until finalize
+    std::vector<int32_t> npiece_seq;
+    // device
+    bool final = false;
+    std::vector<int64_t> woff;      // host copy of word offsets
+    int64_t n_words = 0;
+    uint2 *planes = nullptr;
+    uint32_t *nmask = nullptr;
+    int64_t *d_woff = nullptr;
+};
+
+struct Prof {
+    int kernel;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct gac_ctx {
+    int device = 0;
+    char arch[64] = {0};
+    hipStream_t stream = nullptr;
+    Genome g[2];
+    bool scoring = false;
+    int32_t coef[16];
+    GapDev gap;
+    int32_t *d_small = nullptr;
+    int small_in_lds = 0;
+    // workspace
+    int64_t ws_n = 0;
+    int64_t *plan_b0 = nullptr;
+    int32_t *plan_n = nullptr, *ntiles = nullptr, *tile_off = nullptr, *total_tiles = nullptr;
+    int64_t ws_tiles = 0;
+    int32_t *tile_q = nullptr;
+    TileSum *tsum = nullptr;
+    void *scan_tmp = nullptr;
+    size_t scan_bytes = 0;
+    // staging for the host API
+    int64_t io_n = 0;
+    Range *d_ranges = nullptr;
+    long long *d_g = nullptr, *d_l = nullptr;
+    int32_t *d_ali = nullptr;
+    int32_t *h_total = nullptr;  // pinned
+    int tile_grid = 2048;
+    int combine_grid = 512;
+    // profiling
+    bool prof = false;
+    std::vector<Prof> prof_pending;
+    std::vector<hipEvent_t> prof_free;
+    double prof_ms[GAC_K_COUNT] = {0};
+    int64_t prof_n[GAC_K_COUNT] = {0};
+};
+
+struct gac_chainset {
+    gac_ctx *ctx;
+    int64_t n_chains;
+    int64_t n_blocks;
+    DChain *chains = nullptr;
+    int32_t *bt = nullptr, *bq = nullptr, *bs = nullptr;
+};
+
+// ----------------------------------------------------------------- context
+extern "C" int gac_open(int device, gac_ctx **out) {
+    gac_clear_error();
+    if (!out) return gac_fail(GAC_E_ARG, "gac_open: NULL out");
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0)
+        return gac_fail(GAC_E_HIP, "no HIP device available (%s); libgachain has no CPU fallback",
+                        hipGetErrorString(e));
+    if (device < 0 || device >= n)
+        return gac_fail(GAC_E_ARG, "device %d out of range (%d devices)", device, n);
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return gac_fail(GAC_E_HIP, "device %d is %s; libgachain is built for gfx950 only", device,
+                        prop.gcnArchName);
+    HIPCHK(hipSetDevice(device));
+    gac_ctx *c = new gac_ctx();
+    c->device = device;
+    snprintf(c->arch, sizeof(c->arch), "%s", prop.gcnArchName);
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return gac_fail(GAC_E_HIP, "hipStreamCreate failed");
+    }
+    // persistent tile grid: 8 workgroups (32 waves) per CU
+    c->tile_grid = prop.multiProcessorCount * 8;
+    c->tile_grid = (c->tile_grid + 7) / 8 * 8;
+    c->combine_grid = prop.multiProcessorCount * 2;
+    if (hipHostMalloc((void **)&c->h_total, 16, hipHostMallocDefault) != hipSuccess) {
+        hipStreamDestroy(c->stream);
+        delete c;
+        return gac_fail(GAC_E_HIP, "hipHostMalloc failed");
+    }
+    *out = c;
+    return GAC_OK;
+}
+
+static void free_genome(Genome &g) {
+    if (g.planes) hipFree(g.planes);
+    if (g.nmask) hipFree(g.nmask);
+    if (g.d_woff) hipFree(g.d_woff);
+    g = Genome();
+}
+
+extern "C" void gac_close(gac_ctx *c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    free_genome(c->g[0]);
+    free_genome(c->g[1]);
+    void *bufs[] = {c->d_small, c->plan_b0, c->plan_n,  c->ntiles, c->tile_off, c->total_tiles,
+                    c->tile_q,  c->tsum,    c->scan_tmp, c->d_ranges, c->d_g,   c->d_l,
+                    c->d_ali};
+    for (void *p : bufs)
+        if (p) hipFree(p);
+    for (auto &p : c->prof_pending) {
+        hipEventDestroy(p.a);
+        hipEventDestroy(p.b);
+    }
+    for (auto ev : c->prof_free) hipEventDestroy(ev);
+    if (c->h_total) hipHostFree(c->h_total);
+    hipStreamDestroy(c->stream);
+    delete c;
+}
+
+extern "C" const char *gac_device_arch(gac_ctx *c) { return c ? c->arch : ""; }
+
+// ----------------------------------------------------------------- scoring
+static int acgt_of_code(int code) {  // 2bit code T=0 C=1 A=2 G=3 -> A,C,G,T index
+    static const int m[4] = {3, 1, 0, 2};
+    return m[code];
+}
+
+extern "C" int gac_set_scoring(gac_ctx *c, const int32_t mat[16], const gac_gapcalc *g) {
+    gac_clear_error();
+    if (!c || !mat || !g) return gac_fail(GAC_E_ARG, "gac_set_scoring: NULL argument");
+    if (g->long_count < 2 || g->long_count > kMaxLong)
+        return gac_fail(GAC_E_ARG, "gap table has %d long positions (2..%d supported)",
+                        g->long_count, kMaxLong);
+    if (g->small_size < 1 || g->small_size != g->long_pos[0])
+        return gac_fail(GAC_E_ARG, "inconsistent gap table (smallSize %d)", g->small_size);
+    HIPCHK(hipSetDevice(c->device));
+    for (int qc = 0; qc < 4; ++qc)
+        for (int tc = 0; tc < 4; ++tc)
+            c->coef[qc * 4 + tc] = mat[acgt_of_code(qc) * 4 + acgt_of_code(tc)];
+    GapDev &d = c->gap;
+    memset(&d, 0, sizeof(d));
+    d.small_size = g->small_size;
+    d.long_count = g->long_count;
+    d.last_pos[0] = g->q_last_pos;
+    d.last_pos[1] = g->t_last_pos;
+    d.last_pos[2] = g->b_last_pos;
+    d.last_val[0] = g->q_last_val;
+    d.last_val[1] = g->t_last_val;
+    d.last_val[2] = g->b_last_val;
+    d.last_slope[0] = g->q_last_slope;
+    d.last_slope[1] = g->t_last_slope;
+    d.last_slope[2] = g->b_last_slope;
+    for (int i = 0; i < g->long_count; ++i) {
+        d.long_pos[i] = g->long_pos[i];
+        d.long_val[0][i] = g->q_long[i];
+        d.long_val[1][i] = g->t_long[i];
+        d.long_val[2][i] = g->b_long[i];
+    }
+    std::vector<int32_t> small(3 * (size_t)g->small_size);
+    memcpy(small.data(), g->q_small, g->small_size * 4);
+    memcpy(small.data() + g->small_size, g->t_small, g->small_size * 4);
+    memcpy(small.data() + 2 * g->small_size, g->b_small, g->small_size * 4);
+    if (c->d_small) hipFree(c->d_small);
+    c->d_small = nullptr;
+    HIPCHK(hipMalloc(&c->d_small, small.size() * 4));
+    HIPCHK(hipMemcpy(c->d_small, small.data(), small.size() * 4, hipMemcpyHostToDevice));
+    c->small_in_lds = g->small_size <= kSmallCap;
+    c->scoring = true;
+    return GAC_OK;
+}
+
+// ----------------------------------------------------------------- genomes
+static Genome *side_of(gac_ctx *c, int side) {
+    if (!c || (side != GAC_T && side != GAC_Q)) return nullptr;
+    return &c->g[side];
+}
+
+extern "C" int gac_genome_add_seq(gac_ctx *c, int side, const char *name, int32_t size,
+                                  const uint8_t *packed, int32_t n_nblocks,
+                                  const int32_t *n_starts, const int32_t *n_sizes) {
+    Genome *g = side_of(c, side);
+    if (!g || !name || size < 0 || (size > 0 && !packed) || n_nblocks < 0)
+        return gac_fail(GAC_E_ARG, "gac_genome_add_seq: bad argument");
+    if (g->final) return gac_fail(GAC_E_STATE, "genome side %d already finalized", side);
+    if (g->index.count(name)) return gac_fail(GAC_E_ARG, "duplicate sequence %s", name);
+    int32_t idx = (int32_t)g->names.size();
+    g->index[name] = idx;
+    g->names.push_back(name);
+    g->sizes.push_back(size);
+    size_t off = (g->raw.size() + 7) & ~(size_t)7;
+    size_t nbytes = ((size_t)size + 3) / 4;
+    g->raw.resize(off + nbytes);
+    if (nbytes) memcpy(g->raw.data() + off, packed, nbytes);
+    g->raw_off.push_back((int64_t)off);
+    for (int32_t i = 0; i < n_nblocks; ++i) {
+        int64_t s = n_starts[i], len = n_sizes[i];
+        if (s < 0 || len < 0 || s + len > size)
+            return gac_fail(GAC_E_FORMAT, "N block %d of %s out of range", i, name);
+        while (len > 0) {
+            int32_t piece = (int32_t)(len < 1024 ? len : 1024);
+            g->npieces.push_back(NPiece{s, piece, 0});
+            g->npiece_seq.push_back(idx);
+            s += piece;
+            len -= piece;
+        }
+    }
+    return GAC_OK;
+}
+
+extern "C" int gac_genome_finalize(gac_ctx *c, int side) {
+    gac_clear_error();
+    Genome *g = side_of(c, side);
+    if (!g) return gac_fail(GAC_E_ARG, "gac_genome_finalize: bad side");
+    if (g->final) return gac_fail(GAC_E_STATE, "genome side %d already finalized", side);
+    HIPCHK(hipSetDevice(c->device));
+    const int nseq = (int)g->names.size();
+    std::vector<SeqDev> seqs(nseq);
+    g->woff.resize(nseq);
+    int64_t w = 0;
+    for (int i = 0; i < nseq; ++i) {
+        seqs[i].byte_off = g->raw_off[i];
+        seqs[i].word_off = w;
+        seqs[i].size = g->sizes[i];
+        g->woff[i] = w;
+        w += ((int64_t)g->sizes[i] + 31) / 32;
+    }
+    g->n_words = w;
+    const int64_t alloc_words = w + 4;  // padding: windows read word w+1
+    HIPCHK(hipMalloc(&g->planes, alloc_words * sizeof(uint2)));
+    HIPCHK(hipMalloc(&g->nmask, alloc_words * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&g->d_woff, (nseq ? nseq : 1) * sizeof(int64_t)));
+    HIPCHK(hipMemsetAsync(g->planes, 0, alloc_words * sizeof(uint2), c->stream));
+    HIPCHK(hipMemsetAsync(g->nmask, 0xff, alloc_words * sizeof(uint32_t), c->stream));
+    if (nseq) {
+        HIPCHK(hipMemcpyAsync(g->d_woff, g->woff.data(), nseq * sizeof(int64_t),
+                              hipMemcpyHostToDevice, c->stream));
+        uint8_t *d_raw = nullptr;
+        SeqDev *d_seqs = nullptr;
+        NPiece *d_np = nullptr;
+        const size_t raw_bytes = g->raw.size() + 16;
+        HIPCHK(hipMalloc(&d_raw, raw_bytes));
+        HIPCHK(hipMalloc(&d_seqs, nseq * sizeof(SeqDev)));
+        HIPCHK(hipMemcpyAsync(d_raw, g->raw.data(), g->raw.size(), hipMemcpyHostToDevice,
+                              c->stream));
+        HIPCHK(hipMemcpyAsync(d_seqs, seqs.data(), nseq * sizeof(SeqDev), hipMemcpyHostToDevice,
+                              c->stream));
+        HIPCHK(launch_relayout(d_raw, d_seqs, nseq, w, g->planes, g->nmask, c->stream));
+        const int64_t np = (int64_t)g->npieces.size();
+        if (np) {
+            for (int64_t i = 0; i < np; ++i)
+                g->npieces[i].bit0 += g->woff[g->npiece_seq[i]] * 32;
+            HIPCHK(hipMalloc(&d_np, np * sizeof(NPiece)));
+            HIPCHK(hipMemcpyAsync(d_np, g->npieces.data(), np * sizeof(NPiece),
+                                  hipMemcpyHostToDevice, c->stream));
+            HIPCHK(launch_nruns(d_np, np, g->nmask, c->stream));
+        }
+        HIPCHK(hipStreamSynchronize(c->stream));
+        hipFree(d_raw);
+        hipFree(d_seqs);
+        if (d_np) hipFree(d_np);
+    } else {
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    std::vector<uint8_t>().swap(g->raw);
+    std::vector<NPiece>().swap(g->npieces);
+    std::vector<int32_t>().swap(g->npiece_seq);
+    g->final = true;
+    return GAC_OK;
+}
+
+extern "C" int gac_genome_load_2bit(gac_ctx *c, int side, const char *path) {
+    gac_clear_error();
+    if (!side_of(c, side) || !path) return gac_fail(GAC_E_ARG, "gac_genome_load_2bit: bad argument");
+    gac_twobit tb;
+    int rc = gac_twobit_open(path, &tb);
+    if (rc != GAC_OK) return rc;
+    std::vector<int32_t> ns, nz;
+    for (uint32_t i = 0; i < tb.seq_count && rc == GAC_OK; ++i) {
+        const gac_twobit_seq &s = tb.seqs[i];
+        ns.resize(s.n_count);
+        nz.resize(s.n_count);
+        for (uint32_t k = 0; k < s.n_count; ++k) {
+            ns[k] = (int32_t)gac_twobit_u32(&tb, s.n_starts_raw + 4 * k);
+            nz[k] = (int32_t)gac_twobit_u32(&tb, s.n_sizes_raw + 4 * k);
+        }
+        rc = gac_genome_add_seq(c, side, s.name, (int32_t)s.size, s.packed, (int32_t)s.n_count,
+                                ns.data(), nz.data());
+    }
+    gac_twobit_close(&tb);
+    if (rc != GAC_OK) return rc;
+    return gac_genome_finalize(c, side);
+}
+
+extern "C" int32_t gac_genome_seq_count(gac_ctx *c, int side) {
+    Genome *g = side_of(c, side);
+    return g ? (int32_t)g->names.size() : -1;
+}
+
+extern "C" int32_t gac_genome_seq_index(gac_ctx *c, int side, const char *name) {
+    Genome *g = side_of(c, side);
+    if (!g || !name) return -1;
+    auto it = g->index.find(name);
+    return it == g->index.end() ? -1 : it->second;
+}
+
+extern "C" int32_t gac_genome_seq_size(gac_ctx *c, int side, int32_t i) {
+    Genome *g = side_of(c, side);
+    if (!g || i < 0 || i >= (int32_t)g->sizes.size()) return -1;
+    return g->sizes[i];
+}
+
+extern "C" const char *gac_genome_seq_name(gac_ctx *c, int side, int32_t i) {
+    Genome *g = side_of(c, side);
+    if (!g || i < 0 || i >= (int32_t)g->names.size()) return nullptr;
+    return g->names[i].c_str();
+}
+
+extern "C" int gac_genome_decode(gac_ctx *c, int side, int32_t i, int32_t start, int32_t end,
+                                 char *out) {
+    gac_clear_error();
+    Genome *g = side_of(c, side);
+    if (!g || !g->final || i < 0 || i >= (int32_t)g->sizes.size() || start < 0 ||
+        end > g->sizes[i] || start > end || !out)
+        return gac_fail(GAC_E_ARG, "gac_genome_decode: bad argument");
+    if (start == end) return GAC_OK;
+    HIPCHK(hipSetDevice(c->device));
+    const int64_t w0 = g->woff[i] + start / 32, w1 = g->woff[i] + (end - 1) / 32 + 1;
+    std::vector<uint2> pl(w1 - w0);
+    std::vector<uint32_t> nm(w1 - w0);
+    HIPCHK(hipMemcpy(pl.data(), g->planes + w0, pl.size() * sizeof(uint2), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(nm.data(), g->nmask + w0, nm.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    static const char nt[4] = {'t', 'c', 'a', 'g'};
+    for (int32_t p = start; p < end; ++p) {
+        const int64_t w = g->woff[i] + p / 32 - w0;
+        const int b = p & 31;
+        if ((nm[w] >> b) & 1u) {
+            out[p - start] = 'n';
+        } else {
+            const int code = (int)(((pl[w].y >> b) & 1u) << 1 | ((pl[w].x >> b) & 1u));
+            out[p - start] = nt[code];
+        }
+    }
+    return GAC_OK;
+}
+
+// ----------------------------------------------------------------- chains
+extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_chainset **out) {
+    gac_clear_error();
+    if (!c || !d || !out) return gac_fail(GAC_E_ARG, "gac_chains_upload: NULL argument");
+    *out = nullptr;
+    if (!c->g[0].final || !c->g[1].final)
+        return gac_fail(GAC_E_STATE, "load both genomes before uploading chains");
+    if (d->n_chains < 0 || d->n_blocks < 0 || (d->n_chains && (!d->t_seq || !d->q_seq ||
+                                                                !d->q_strand || !d->blk_off)))
+        return gac_fail(GAC_E_ARG, "gac_chains_upload: bad descriptor");
+    if (d->n_chains && d->blk_off[d->n_chains] != d->n_blocks)
+        return gac_fail(GAC_E_ARG, "blk_off[n_chains] != n_blocks");
+    std::vector<DChain> ch(d->n_chains ? d->n_chains : 1);
+    for (int64_t i = 0; i < d->n_chains; ++i) {
+        const int32_t ts = d->t_seq[i], qs = d->q_seq[i];
+        if (ts < 0 || ts >= (int32_t)c->g[0].sizes.size() || qs < 0 ||
+            qs >= (int32_t)c->g[1].sizes.size())
+            return gac_fail(GAC_E_ARG, "chain %lld: sequence index out of range", (long long)i);
+        const int64_t b0 = d->blk_off[i], b1 = d->blk_off[i + 1];
+        if (b0 < 0 || b1 < b0 || b1 > d->n_blocks || b1 - b0 > INT32_MAX)
+            return gac_fail(GAC_E_ARG, "chain %lld: bad block offsets", (long long)i);
+        const int32_t tsize = c->g[0].sizes[ts], qsize = c->g[1].sizes[qs];
+        int64_t pt = 0, pq = 0;
+        for (int64_t b = b0; b < b1; ++b) {
+            const int64_t t = d->blk_t[b], q = d->blk_q[b], z = d->blk_size[b];
+            if (z < 0 || t < 0 || q < 0 || t + z > tsize || q + z > qsize)
+                return gac_fail(GAC_E_FORMAT,
+                                "chain %lld block %lld [t %lld q %lld size %lld] outside its "
+                                "sequences (tSize %d qSize %d)",
+                                (long long)i, (long long)(b - b0), (long long)t, (long long)q,
+                                (long long)z, tsize, qsize);
+            if (b > b0 && (t < pt || q < pq))
+                return gac_fail(GAC_E_FORMAT, "chain %lld: blocks not ascending (negative gap)",
+                                (long long)i);
+            pt = t + z;
+            pq = q + z;
+        }
+        ch[i].blk_off = b0;
+        ch[i].nblk = (int32_t)(b1 - b0);
+        ch[i].t_seq = ts;
+        ch[i].q_seq = qs;
+        ch[i].strand = d->q_strand[i] ? 1 : 0;
+        ch[i].q_size = qsize;
+        ch[i].pad = 0;
+    }
+    HIPCHK(hipSetDevice(c->device));
+    gac_chainset *cs = new gac_chainset();
+    cs->ctx = c;
+    cs->n_chains = d->n_chains;
+    cs->n_blocks = d->n_blocks;
+    const size_t nb = (size_t)(d->n_blocks ? d->n_blocks : 1) + 1;  // +1: k_tile reads blk+1 only when not last
+    hipError_t e = hipMalloc(&cs->chains, ch.size() * sizeof(DChain));
+    if (e == hipSuccess) e = hipMalloc(&cs->bt, nb * 4);
+    if (e == hipSuccess) e = hipMalloc(&cs->bq, nb * 4);
+    if (e == hipSuccess) e = hipMalloc(&cs->bs, nb * 4);
+    if (e == hipSuccess)
+        e = hipMemcpy(cs->chains, ch.data(), ch.size() * sizeof(DChain), hipMemcpyHostToDevice);
+    if (e == hipSuccess && d->n_blocks) {
+        e = hipMemcpy(cs->bt, d->blk_t, d->n_blocks * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(cs->bq, d->blk_q, d->n_blocks * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpy(cs->bs, d->blk_size, d->n_blocks * 4, hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess) {
+        gac_chains_free(cs);
+        return gac_fail(GAC_E_HIP, "chain upload failed: %s", hipGetErrorString(e));
+    }
+    *out = cs;
+    return GAC_OK;
+}
+
+extern "C" void gac_chains_free(gac_chainset *cs) {
+    if (!cs) return;
+    hipSetDevice(cs->ctx->device);
+    if (cs->chains) hipFree(cs->chains);
+    if (cs->bt) hipFree(cs->bt);
+    if (cs->bq) hipFree(cs->bq);
+    if (cs->bs) hipFree(cs->bs);
+    delete cs;
+}
+
+extern "C" int64_t gac_chains_block_count(const gac_chainset *cs) { return cs ? cs->n_blocks : -1; }
+
+// ----------------------------------------------------------------- launch
+static int ensure_ws(gac_ctx *c, int64_t n, int64_t max_tiles) {
+    if (n > c->ws_n) {
+        int64_t cap = n + n / 2 + 1024;
+        void *bufs[] = {c->plan_b0, c->plan_n, c->ntiles, c->tile_off, c->total_tiles, c->scan_tmp};
+        for (void *p : bufs)
+            if (p) hipFree(p);
+        c->plan_b0 = nullptr;
+        c->plan_n = c->ntiles = c->tile_off = c->total_tiles = nullptr;
+        c->scan_tmp = nullptr;
+        HIPCHK(hipMalloc(&c->plan_b0, cap * 8));
+        HIPCHK(hipMalloc(&c->plan_n, cap * 4));
+        HIPCHK(hipMalloc(&c->ntiles, cap * 4));
+        HIPCHK(hipMalloc(&c->tile_off, cap * 4));
+        HIPCHK(hipMalloc(&c->total_tiles, 16));
+        c->scan_bytes = scan_temp_bytes(cap);
+        HIPCHK(hipMalloc(&c->scan_tmp, c->scan_bytes ? c->scan_bytes : 16));
+        c->ws_n = cap;
+    }
+    if (max_tiles > c->ws_tiles) {
+        int64_t cap = max_tiles + max_tiles / 4 + 1024;
+        if (c->tile_q) hipFree(c->tile_q);
+        if (c->tsum) hipFree(c->tsum);
+        c->tile_q = nullptr;
+        c->tsum = nullptr;
+        HIPCHK(hipMalloc(&c->tile_q, cap * 4));
+        HIPCHK(hipMalloc(&c->tsum, cap * sizeof(TileSum)));
+        c->ws_tiles = cap;
+    }
+    return GAC_OK;
+}
+
+static hipEvent_t prof_event(gac_ctx *c) {
+    if (!c->prof_free.empty()) {
+        hipEvent_t e = c->prof_free.back();
+        c->prof_free.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    hipEventCreate(&e);
+    return e;
+}
+
+#define PROF_BEGIN(k)                                   \
+    hipEvent_t _pa = nullptr, _pb = nullptr;            \
+    if (c->prof) {                                      \
+        _pa = prof_event(c);                            \
+        _pb = prof_event(c);                            \
+        hipEventRecord(_pa, s);                         \
+    }
+#define PROF_END(k)                                     \
+    if (c->prof) {                                      \
+        hipEventRecord(_pb, s);                         \
+        c->prof_pending.push_back(Prof{(k), _pa, _pb}); \
+    }
+
+static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_ranges, int64_t n,
+                        uint32_t flags, long long *d_g, long long *d_l, int32_t *d_ali,
+                        hipStream_t s) {
+    if (!c->scoring) return gac_fail(GAC_E_STATE, "gac_set_scoring() not called");
+    if (!cs || cs->ctx != c) return gac_fail(GAC_E_ARG, "chainset does not belong to this context");
+    if (n < 0 || n > INT32_MAX / 2) return gac_fail(GAC_E_ARG, "bad range count %lld", (long long)n);
+    if (n == 0) return GAC_OK;
+    if ((flags & GAC_WANT_LOCAL) && !d_l) return gac_fail(GAC_E_ARG, "GAC_WANT_LOCAL needs local output");
+    int rc = ensure_ws(c, n, 0);
+    if (rc != GAC_OK) return rc;
+    ScoreArgs a;
+    memset(&a, 0, sizeof(a));
+    const Genome &T = c->g[0], &Q = c->g[1];
+    a.t_planes = T.planes;
+    a.t_nmask = T.nmask;
+    a.t_woff = T.d_woff;
+    a.q_planes = Q.planes;
+    a.q_nmask = Q.nmask;
+    a.q_woff = Q.d_woff;
+    a.chains = cs->chains;
+    a.n_chains = cs->n_chains;
+    a.bt = cs->bt;
+    a.bq = cs->bq;
+    a.bs = cs->bs;
+    a.ranges = d_ranges;
+    a.n = n;
+    a.plan_b0 = c->plan_b0;
+    a.plan_n = c->plan_n;
+    a.ntiles = c->ntiles;
+    a.tile_off = c->tile_off;
+    a.tile_q = c->tile_q;
+    a.total_tiles = c->total_tiles;
+    a.tsum = c->tsum;
+    a.out_g = d_g;
+    a.out_l = d_l;
+    a.out_ali = d_ali;
+    a.want_local = (flags & GAC_WANT_LOCAL) ? 1 : 0;
+    a.small_in_lds = c->small_in_lds;
+    a.small_tab = c->d_small;
+    memcpy(a.coef, c->coef, sizeof(a.coef));
+    a.gap = c->gap;
+    {
+        PROF_BEGIN(GAC_K_PLAN);
+        HIPCHK(launch_plan(a, s));
+        HIPCHK(launch_scan_total(a, c->scan_tmp, c->scan_bytes, s));
+        PROF_END(GAC_K_PLAN);
+    }
+    // tiles are only known after the scan: read the 4-byte total back so the
+    // tile workspace is always large enough (ranges may overlap arbitrarily).
+    HIPCHK(hipMemcpyAsync(c->h_total, c->total_tiles, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const int64_t total = *c->h_total;
+    rc = ensure_ws(c, n, total);
+    if (rc != GAC_OK) return rc;
+    a.tile_q = c->tile_q;
+    a.tsum = c->tsum;
+    if (total == 0) return GAC_OK;
+    HIPCHK(launch_scatter(a, s));
+    {
+        PROF_BEGIN(GAC_K_TILE);
+        HIPCHK(launch_tile(a, c->tile_grid, s));
+        PROF_END(GAC_K_TILE);
+    }
+    {
+        PROF_BEGIN(GAC_K_COMBINE);
+        HIPCHK(launch_combine(a, c->combine_grid, s));
+        PROF_END(GAC_K_COMBINE);
+    }
+    return GAC_OK;
+}
+
+extern "C" int gac_score_ranges_device(gac_ctx *c, const gac_chainset *cs, const gac_range *d_ranges,
+                                       int64_t n, uint32_t flags, int64_t *d_g, int64_t *d_l,
+                                       int32_t *d_ali, void *stream) {
+    gac_clear_error();
+    if (!c) return gac_fail(GAC_E_ARG, "NULL context");
+    if (n > 0 && (!d_ranges || !d_g || !d_ali)) return gac_fail(GAC_E_ARG, "NULL buffer");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return score_device(c, cs, (const Range *)d_ranges, n, flags, (long long *)d_g,
+                        (long long *)d_l, d_ali, s);
+}
+
+extern "C" int gac_score_ranges(gac_ctx *c, const gac_chainset *cs, const gac_range *ranges,
+                                int64_t n, uint32_t flags, int64_t *global, int64_t *local,
+                                int32_t *ali) {
+    gac_clear_error();
+    if (!c) return gac_fail(GAC_E_ARG, "NULL context");
+    if (n < 0) return gac_fail(GAC_E_ARG, "negative range count");
+    if (n == 0) return GAC_OK;
+    if (!ranges || !global || !ali || ((flags & GAC_WANT_LOCAL) && !local))
+        return gac_fail(GAC_E_ARG, "NULL buffer");
+    if (!cs) return gac_fail(GAC_E_ARG, "NULL chainset");
+    for (int64_t i = 0; i < n; ++i)
+        if (ranges[i].chain < 0 || ranges[i].chain >= cs->n_chains)
+            return gac_fail(GAC_E_ARG, "range %lld: chain %d out of range", (long long)i,
+                            ranges[i].chain);
+    HIPCHK(hipSetDevice(c->device));
+    if (n > c->io_n) {
+        int64_t cap = n + n / 2 + 1024;
+        if (c->d_ranges) hipFree(c->d_ranges);
+        if (c->d_g) hipFree(c->d_g);
+        if (c->d_l) hipFree(c->d_l);
+        if (c->d_ali) hipFree(c->d_ali);
+        c->d_ranges = nullptr;
+        c->d_g = c->d_l = nullptr;
+        c->d_ali = nullptr;
+        HIPCHK(hipMalloc(&c->d_ranges, cap * sizeof(Range)));
+        HIPCHK(hipMalloc(&c->d_g, cap * 8));
+        HIPCHK(hipMalloc(&c->d_l, cap * 8));
+        HIPCHK(hipMalloc(&c->d_ali, cap * 4));
+        c->io_n = cap;
+    }
+    hipStream_t s = c->stream;
+    HIPCHK(hipMemcpyAsync(c->d_ranges, ranges, n * sizeof(Range), hipMemcpyHostToDevice, s));
+    int rc = score_device(c, cs, c->d_ranges, n, flags, c->d_g, c->d_l, c->d_ali, s);
+    if (rc != GAC_OK) return rc;
+    HIPCHK(hipMemcpyAsync(global, c->d_g, n * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(ali, c->d_ali, n * 4, hipMemcpyDeviceToHost, s));
+    if (flags & GAC_WANT_LOCAL)
+        HIPCHK(hipMemcpyAsync(local, c->d_l, n * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return GAC_OK;
+}
+
+// ----------------------------------------------------------------- memory
+extern "C" int gac_dev_alloc(gac_ctx *c, size_t bytes, void **p) {
+    if (!c || !p) return gac_fail(GAC_E_ARG, "NULL argument");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMalloc(p, bytes ? bytes : 16));
+    return GAC_OK;
+}
+extern "C" int gac_dev_free(gac_ctx *c, void *p) {
+    if (!c) return gac_fail(GAC_E_ARG, "NULL context");
+    if (p) HIPCHK(hipFree(p));
+    return GAC_OK;
+}
+extern "C" int gac_memcpy_h2d(gac_ctx *c, void *dst, const void *src, size_t n) {
+    if (!c) return gac_fail(GAC_E_ARG, "NULL context");
+    HIPCHK(hipMemcpy(dst, src, n, hipMemcpyHostToDevice));
+    return GAC_OK;
+}
+extern "C" int gac_memcpy_d2h(gac_ctx *c, void *dst, const void *src, size_t n) {
+    if (!c) return gac_fail(GAC_E_ARG, "NULL context");
+    HIPCHK(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost));
+    return GAC_OK;
+}
+extern "C" int gac_synchronize(gac_ctx *c) {
+    if (!c) return gac_fail(GAC_E_ARG, "NULL context");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipDeviceSynchronize());
+    return GAC_OK;
+}
+
+// ----------------------------------------------------------------- profiling
+extern "C" int gac_prof_enable(gac_ctx *c, int on) {
+    if (!c) return gac_fail(GAC_E_ARG, "NULL context");
+    c->prof = on != 0;
+    return GAC_OK;
+}
+
+static int prof_fold(gac_ctx *c) {
+    for (auto &p : c->prof_pending) {
+        HIPCHK(hipEventSynchronize(p.b));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, p.a, p.b));
+        c->prof_ms[p.kernel] += ms;
+        c->prof_n[p.kernel] += 1;
+        c->prof_free.push_back(p.a);
+        c->prof_free.push_back(p.b);
+    }
+    c->prof_pending.clear();
+    return GAC_OK;
+}
+
+extern "C" int gac_prof_read(gac_ctx *c, int k, double *ms, int64_t *n) {
+    if (!c || k < 0 || k >= GAC_K_COUNT) return gac_fail(GAC_E_ARG, "bad argument");
+    int rc = prof_fold(c);
+    if (rc != GAC_OK) return rc;
+    if (ms) *ms = c->prof_ms[k];
+    if (n) *n = c->prof_n[k];
+    return GAC_OK;
+}
+
+extern "C" int gac_prof_reset(gac_ctx *c) {
+    if (!c) return gac_fail(GAC_E_ARG, "NULL context");
+    int rc = prof_fold(c);
+    if (rc != GAC_OK) return rc;
+    for (int k = 0; k < GAC_K_COUNT; ++k) {
+        c->prof_ms[k] = 0;
+        c->prof_n[k] = 0;
+    }
+    return GAC_OK;
+}

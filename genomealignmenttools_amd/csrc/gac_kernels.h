@@ -1,0 +1,89 @@
+// gac_kernels.h -- device data layout shared by the HIP kernels and the
+// C-ABI implementation (gac_device.hip).  gfx950 only.
+//
+// HBM layout (see DESIGN.md "Data layout in HBM"):
+//   genome side (T or Q): 32 bases per "word"
+//     planes[w] : uint2 {x = bit0 plane, y = bit1 plane} of 2-bit codes
+//                 T=0 C=1 A=2 G=3 (the .2bit code; kent dnautil.h:23-28),
+//                 base 32w+i at bit i of each plane
+//     nmask[w]  : uint32, bit i set = base 32w+i is N (or padding)
+//     every sequence starts on a word boundary; word_off[s] = first word
+//   chains: DChain[c] + blocks bt/bq/bs (int32 tStart, qStart, size)
+#pragma once
+#include <stdint.h>
+
+namespace gac {
+
+constexpr int kWave = 64;        // CDNA wavefront
+constexpr int kTileBlocks = 64;  // blocks per tile (one per lane)
+constexpr int kWavesPerWG = 4;   // 256-thread workgroups
+constexpr int kSmallCap = 256;   // gap small-table entries staged in LDS
+constexpr int kMaxLong = 32;     // long gap positions
+constexpr long long kNeg = -(1LL << 61);  // -inf of the local-score monoid
+
+struct DChain {
+    int64_t blk_off;
+    int32_t nblk;
+    int32_t t_seq;
+    int32_t q_seq;
+    int32_t strand;  // 0 '+', 1 '-'
+    int32_t q_size;  // sequence size of q_seq (reverse-complement index base)
+    int32_t pad;
+};
+static_assert(sizeof(DChain) == 32, "DChain layout");
+
+struct GapDev {
+    int32_t small_size;
+    int32_t long_count;
+    int32_t last_pos[3];  // q, t, both
+    int32_t pad;
+    double last_val[3];
+    double last_slope[3];
+    int32_t long_pos[kMaxLong];
+    double long_val[3][kMaxLong];
+};
+
+// Per-tile partial result: additive parts + the local-score max-plus element
+//   s_out = max(s_in + A, B);  m_out = max(m_in, s_in + C, D)
+struct TileSum {
+    long long g;   // sum(block) - sum(gap)
+    long long ali; // aligned bases
+    long long A, B, C, D;
+};
+
+struct Range {
+    int32_t chain, t_start, t_end;
+};
+
+struct ScoreArgs {
+    const uint2 *t_planes;
+    const uint32_t *t_nmask;
+    const int64_t *t_woff;
+    const uint2 *q_planes;
+    const uint32_t *q_nmask;
+    const int64_t *q_woff;
+    const DChain *chains;
+    int64_t n_chains;
+    const int32_t *bt, *bq, *bs;
+    const Range *ranges;
+    int64_t n;
+    // workspace
+    int64_t *plan_b0;
+    int32_t *plan_n;
+    int32_t *ntiles;
+    int32_t *tile_off;
+    int32_t *tile_q;
+    int32_t *total_tiles;
+    TileSum *tsum;
+    // outputs
+    long long *out_g;
+    long long *out_l;
+    int32_t *out_ali;
+    int32_t want_local;
+    int32_t small_in_lds;
+    const int32_t *small_tab;  // [3][small_size] q, t, both
+    int32_t coef[16];          // score of (query code << 2 | target code)
+    GapDev gap;
+};
+
+}  // namespace gac

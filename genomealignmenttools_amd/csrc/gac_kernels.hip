@@ -1,0 +1,510 @@
+// gac_kernels.hip -- CDNA4 (gfx950) kernels of libgachain.
+//
+// The reference hot path (single-threaded C) is, per sub-chain:
+//   chainSubsetOnT   kent/src/lib/chain.c:471-558      clip blocks to [s, e)
+//   chainCalcScore   kent/src/lib/chainConnect.c:24-40  sum(block) - sum(gap)
+//   chainScoreBlock  kent/src/lib/chainConnect.c:14-22  sum matrix[q][t] per base
+//   gapCalcCost      kent/src/lib/gapCalc.c:298-331      piecewise-linear gap cost
+//   chainCalcScoreLocal src/scoreChain/scoreChain.c:176-198  max-plus local score
+// Here one launch scores a whole batch of sub-chains:
+//   k_plan    one lane per range: binary-search the block window (replaces
+//             the O(blocks) list walks of chainSubsetOnT / chainBaseCountSubT)
+//   (scan)    hipcub exclusive sum of tiles per range
+//   k_scatter tile -> range map
+//   k_tile    one wave per tile of <= 64 blocks: lanes score 32-base chunks of
+//             2-bit packed T and Q straight from HBM (bit-plane popcounts, the
+//             4x4 matrix in SGPRs), LDS atomics fold chunks into blocks, lanes
+//             evaluate gapCalcCost in exact f64, and an ordered wave reduction
+//             folds the tile's max-plus local-score element
+//   k_combine one wave per range spanning > 1 tile: ordered fold of tiles
+// All sums are int64: every addend of the reference's double accumulation is
+// an integer, so integer arithmetic is exact and bit-identical.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gac_kernels.h"
+
+#pragma clang fp contract(off)
+
+namespace gac {
+
+// ------------------------------------------------------------ gap cost ---
+// gapCalcCost (kent/src/lib/gapCalc.c:298-331) with interpolate (:82-104),
+// same double operation order, no FMA contraction, truncation to int.
+__device__ __forceinline__ int interp_long(int x, const GapDev &g, int which) {
+    const int n = g.long_count;
+    const double *v = g.long_val[which];
+    for (int i = 0; i < n; ++i) {
+        const int ss = g.long_pos[i];
+        if (x == ss) return (int)v[i];
+        if (x < ss) {
+            const int ds = ss - g.long_pos[i - 1];
+            const double dv = v[i] - v[i - 1];
+            const double prod = __dmul_rn(dv, (double)(x - g.long_pos[i - 1]));
+            return (int)__dadd_rn(v[i - 1], __ddiv_rn(prod, (double)ds));
+        }
+    }
+    const int ds = g.long_pos[n - 1] - g.long_pos[n - 2];
+    const double dv = v[n - 1] - v[n - 2];
+    const double prod = __dmul_rn(dv, (double)(x - g.long_pos[n - 2]));
+    return (int)__dadd_rn(v[n - 2], __ddiv_rn(prod, (double)ds));
+}
+
+__device__ __forceinline__ int gap_cost(const GapDev &g, const int32_t *small, int dq, int dt) {
+    if (dt < 0) dt = 0;
+    if (dq < 0) dq = 0;
+    int which, d;
+    if (dt == 0) {
+        which = 0;
+        d = dq;
+    } else if (dq == 0) {
+        which = 1;
+        d = dt;
+    } else {
+        which = 2;
+        d = dq + dt;
+    }
+    if (d < g.small_size) return small[which * g.small_size + d];
+    if (d >= g.last_pos[which])
+        return (int)__dadd_rn(g.last_val[which],
+                              __dmul_rn(g.last_slope[which], (double)(d - g.last_pos[which])));
+    return interp_long(d, g, which);
+}
+
+// ------------------------------------------------------------ helpers ----
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, int sh) {
+    return __builtin_amdgcn_alignbit(hi, lo, (uint32_t)sh);
+}
+
+// Load 32 bases starting at base index p of the side whose words start at
+// woff: returns the two code planes and the N mask, bit i = base p+i.
+__device__ __forceinline__ void load_window(const uint2 *planes, const uint32_t *nmask,
+                                            int64_t woff, int64_t p, uint32_t &b0,
+                                            uint32_t &b1, uint32_t &nm) {
+    const int64_t w = woff + (p >> 5);
+    const int sh = (int)(p & 31);
+    const uint2 lo = planes[w];
+    const uint2 hi = planes[w + 1];
+    const uint32_t nlo = nmask[w];
+    const uint32_t nhi = nmask[w + 1];
+    b0 = funnel(hi.x, lo.x, sh);
+    b1 = funnel(hi.y, lo.y, sh);
+    nm = funnel(nhi, nlo, sh);
+}
+
+struct Elem {
+    long long A, B, C, D;
+};
+
+__device__ __forceinline__ long long max2(long long a, long long b) { return a > b ? a : b; }
+
+// x then y
+__device__ __forceinline__ Elem compose(const Elem &x, const Elem &y) {
+    Elem r;
+    r.A = x.A + y.A;
+    r.B = max2(x.B + y.A, y.B);
+    r.C = max2(x.C, x.A + y.C);
+    r.D = max2(max2(x.D, x.B + y.C), y.D);
+    return r;
+}
+
+__device__ __forceinline__ long long shfl_down64(long long v, int d) {
+    return __shfl_down(v, d, kWave);
+}
+
+// ordered (non-commutative) wave reduction; lane 0 ends with e_0 . e_1 ... e_63
+__device__ __forceinline__ Elem wave_fold(Elem e, int lane) {
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        Elem o;
+        o.A = shfl_down64(e.A, d);
+        o.B = shfl_down64(e.B, d);
+        o.C = shfl_down64(e.C, d);
+        o.D = shfl_down64(e.D, d);
+        if ((lane & (2 * d - 1)) == 0 && lane + d < kWave) e = compose(e, o);
+    }
+    return e;
+}
+
+__device__ __forceinline__ long long wave_sum(long long v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, kWave);
+    return v;
+}
+
+// ------------------------------------------------------------ k_plan -----
+// One lane per range: window of blocks [b0, b0+n) with tEnd > s and tStart < e.
+__global__ void __launch_bounds__(256) k_plan(ScoreArgs a) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const Range r = a.ranges[i];
+    int n = 0;
+    int64_t b0 = 0;
+    if (r.chain >= 0 && r.chain < a.n_chains && r.t_start < r.t_end) {
+        const DChain c = a.chains[r.chain];
+        const int32_t *bt = a.bt + c.blk_off;
+        const int32_t *bs = a.bs + c.blk_off;
+        // first block with tEnd > s
+        int lo = 0, hi = c.nblk;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (bt[mid] + bs[mid] > r.t_start) hi = mid;
+            else lo = mid + 1;
+        }
+        const int first = lo;
+        // first block with tStart >= e
+        hi = c.nblk;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (bt[mid] >= r.t_end) hi = mid;
+            else lo = mid + 1;
+        }
+        n = lo - first;
+        b0 = c.blk_off + first;
+    }
+    a.plan_b0[i] = b0;
+    a.plan_n[i] = n;
+    a.ntiles[i] = (n + kTileBlocks - 1) / kTileBlocks;
+    if (n == 0) {
+        a.out_g[i] = 0;
+        a.out_ali[i] = 0;
+        if (a.want_local) a.out_l[i] = 0;
+    }
+}
+
+// ------------------------------------------------------------ k_scatter --
+__global__ void __launch_bounds__(256) k_scatter(ScoreArgs a) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const int t0 = a.tile_off[i];
+    const int nt = a.ntiles[i];
+    for (int k = 0; k < nt; ++k) a.tile_q[t0 + k] = (int32_t)i;
+}
+
+__global__ void k_total(ScoreArgs a) {
+    if (threadIdx.x == 0) *a.total_tiles = a.tile_off[a.n - 1] + a.ntiles[a.n - 1];
+}
+
+// ------------------------------------------------------------ k_tile -----
+struct WaveLds {
+    int coff[kTileBlocks + 1];
+    int ts[kTileBlocks];
+    int qs[kTileBlocks];
+    int len[kTileBlocks];
+    unsigned long long acc[kTileBlocks];
+};
+
+__global__ void __launch_bounds__(256) k_tile(ScoreArgs a) {
+    __shared__ int32_t s_small[3 * kSmallCap];
+    __shared__ WaveLds s_w[kWavesPerWG];
+
+    if (a.small_in_lds) {
+        for (int i = threadIdx.x; i < 3 * a.gap.small_size; i += blockDim.x)
+            s_small[i] = a.small_tab[i];
+    }
+    __syncthreads();
+    const int32_t *small = a.small_in_lds ? s_small : a.small_tab;
+
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    WaveLds &L = s_w[wave];
+    const int total = *a.total_tiles;
+
+    // XCD-aware logical id: workgroups b and b+8 share an XCD (round-robin
+    // dispatch), so give them adjacent super-tiles (speed only).
+    const int G = gridDim.x;
+    const int b = blockIdx.x;
+    const int L8 = (G % 8 == 0) ? ((b % 8) * (G / 8) + b / 8) : b;
+
+    for (int st = L8; st * kWavesPerWG < total; st += G) {
+        const int tile = st * kWavesPerWG + wave;
+        if (tile >= total) break;
+        const int qi = __builtin_amdgcn_readfirstlane(a.tile_q[tile]);
+        const int ti = tile - a.tile_off[qi];
+        const Range r = a.ranges[qi];
+        const int nb_q = a.plan_n[qi];
+        const int64_t b0 = a.plan_b0[qi];
+        const DChain c = a.chains[r.chain];
+        const int nt = a.ntiles[qi];
+        const int base_k = ti * kTileBlocks;
+        const int nb = min(kTileBlocks, nb_q - base_k);
+
+        // ---- per-lane block: clip to [s, e), gap to the next block
+        const bool active = lane < nb;
+        int cts = 0, cqs = 0, len = 0, g = 0;
+        bool last = false;
+        if (active) {
+            const int64_t blk = b0 + base_k + lane;
+            const int ts = a.bt[blk], qs = a.bq[blk], sz = a.bs[blk];
+            const int te = ts + sz, qe = qs + sz;
+            cts = ts;
+            cqs = qs;
+            int cte = te;
+            if (cts < r.t_start) {
+                cqs += r.t_start - cts;
+                cts = r.t_start;
+            }
+            if (cte > r.t_end) cte = r.t_end;
+            len = cte - cts;
+            last = (base_k + lane == nb_q - 1);
+            if (!last) {
+                const int nts = a.bt[blk + 1], nqs = a.bq[blk + 1];
+                g = gap_cost(a.gap, small, nqs - qe, nts - te);
+            }
+        }
+        // ---- chunk prefix (32 bases per chunk)
+        const int nch = (len + 31) >> 5;
+        int incl = nch;
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const int o = __shfl_up(incl, d, kWave);
+            if (lane >= d) incl += o;
+        }
+        const int C = __shfl(incl, kWave - 1, kWave);
+        L.coff[lane] = incl - nch;
+        L.ts[lane] = cts;
+        L.qs[lane] = cqs;
+        L.len[lane] = len;
+        L.acc[lane] = 0ull;
+        wave_sync();
+
+        const int64_t twoff = a.t_woff[c.t_seq];
+        const int64_t qwoff = a.q_woff[c.q_seq];
+        const bool minus = c.strand != 0;
+        for (int c0 = 0; c0 < C; c0 += kWave) {
+            const int j = c0 + lane;
+            if (j < C) {
+                int k = 0;
+#pragma unroll
+                for (int step = 32; step > 0; step >>= 1)
+                    if (k + step < nb && L.coff[k + step] <= j) k += step;
+                const int off = (j - L.coff[k]) << 5;
+                const int n = min(32, L.len[k] - off);
+                uint32_t t0, t1, tn, q0, q1, qn;
+                load_window(a.t_planes, a.t_nmask, twoff, (int64_t)L.ts[k] + off, t0, t1, tn);
+                const int qp = L.qs[k] + off;
+                if (!minus) {
+                    load_window(a.q_planes, a.q_nmask, qwoff, qp, q0, q1, qn);
+                } else {
+                    // reverse-complement: rc base j = comp(fwd[qSize-1-(qp+j)])
+                    const int64_t F = (int64_t)c.q_size - qp - n;
+                    uint32_t f0, f1, fn;
+                    load_window(a.q_planes, a.q_nmask, qwoff, F, f0, f1, fn);
+                    const int sh = 32 - n;
+                    q0 = __builtin_bitreverse32(f0) >> sh;
+                    q1 = ~(__builtin_bitreverse32(f1) >> sh);  // complement: code ^ 2
+                    qn = __builtin_bitreverse32(fn) >> sh;
+                }
+                const uint32_t valid = (n >= 32 ? 0xffffffffu : ((1u << n) - 1u)) & ~tn & ~qn;
+                const uint32_t tm[4] = {~t1 & ~t0, ~t1 & t0, t1 & ~t0, t1 & t0};
+                const uint32_t qm[4] = {valid & ~q1 & ~q0, valid & ~q1 & q0, valid & q1 & ~q0,
+                                        valid & q1 & q0};
+                int sc = 0;
+#pragma unroll
+                for (int qc = 0; qc < 4; ++qc)
+#pragma unroll
+                    for (int tc = 0; tc < 4; ++tc)
+                        sc += a.coef[qc * 4 + tc] * __builtin_popcount(qm[qc] & tm[tc]);
+                atomicAdd(&L.acc[k], (unsigned long long)(long long)sc);
+            }
+        }
+        wave_sync();
+
+        // ---- block-level: global sum, ali, max-plus local element
+        long long bsc = active ? (long long)L.acc[lane] : 0;
+        long long gsum = active ? bsc - g : 0;
+        long long ali = active ? len : 0;
+        Elem e;
+        if (active) {
+            e.A = last ? bsc : bsc - g;
+            e.B = last ? kNeg : 0;
+            e.C = bsc;
+            e.D = kNeg;
+        } else {
+            e.A = 0;
+            e.B = kNeg;
+            e.C = kNeg;
+            e.D = kNeg;
+        }
+        gsum = wave_sum(gsum);
+        ali = wave_sum(ali);
+        if (a.want_local) e = wave_fold(e, lane);
+        if (lane == 0) {
+            if (nt == 1) {
+                a.out_g[qi] = gsum;
+                a.out_ali[qi] = (int32_t)ali;
+                if (a.want_local) a.out_l[qi] = max2(0, max2(e.C, e.D));
+            } else {
+                TileSum ts;
+                ts.g = gsum;
+                ts.ali = ali;
+                ts.A = e.A;
+                ts.B = e.B;
+                ts.C = e.C;
+                ts.D = e.D;
+                a.tsum[tile] = ts;
+            }
+        }
+        wave_sync();
+    }
+}
+
+// ------------------------------------------------------------ k_combine --
+__global__ void __launch_bounds__(256) k_combine(ScoreArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave_id = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t qi = wave_id; qi < a.n; qi += nwaves) {
+        const int nt = a.ntiles[qi];
+        if (nt <= 1) continue;
+        const int t0 = a.tile_off[qi];
+        const int per = (nt + kWave - 1) / kWave;
+        const int lo = min(nt, lane * per), hi = min(nt, lo + per);
+        long long g = 0, ali = 0;
+        Elem e = {0, kNeg, kNeg, kNeg};
+        for (int t = lo; t < hi; ++t) {
+            const TileSum s = a.tsum[t0 + t];
+            g += s.g;
+            ali += s.ali;
+            Elem y = {s.A, s.B, s.C, s.D};
+            e = compose(e, y);
+        }
+        g = wave_sum(g);
+        ali = wave_sum(ali);
+        if (a.want_local) e = wave_fold(e, lane);
+        if (lane == 0) {
+            a.out_g[qi] = g;
+            a.out_ali[qi] = (int32_t)ali;
+            if (a.want_local) a.out_l[qi] = max2(0, max2(e.C, e.D));
+        }
+    }
+}
+
+// ------------------------------------------------------------ genome -----
+// Raw .2bit payload (2 bits/base, MSB first in each byte) -> bit planes.
+struct SeqDev {
+    int64_t byte_off;  // into staging
+    int64_t word_off;  // into planes
+    int32_t size;
+    int32_t pad;
+};
+
+__global__ void __launch_bounds__(256) k_relayout(const uint8_t *raw, const SeqDev *seqs,
+                                                  int nseq, int64_t nwords, uint2 *planes,
+                                                  uint32_t *nmask) {
+    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nwords) return;
+    int lo = 0, hi = nseq - 1;
+    while (lo < hi) {  // last seq with word_off <= w
+        const int mid = (lo + hi + 1) >> 1;
+        if (seqs[mid].word_off <= w) lo = mid;
+        else hi = mid - 1;
+    }
+    const SeqDev s = seqs[lo];
+    const int64_t base0 = (w - s.word_off) * 32;
+    uint32_t p0 = 0, p1 = 0, pad = 0;
+    const uint8_t *src = raw + s.byte_off + (base0 >> 2);
+    for (int i = 0; i < 32; ++i) {
+        if (base0 + i >= s.size) {
+            pad |= 1u << i;  // padding scores 0 like an N
+            continue;
+        }
+        const uint32_t code = ((uint32_t)src[i >> 2] >> (6 - 2 * (i & 3))) & 3u;
+        p0 |= (code & 1u) << i;
+        p1 |= (code >> 1) << i;
+    }
+    planes[w] = make_uint2(p0, p1);
+    nmask[w] = pad;
+}
+
+// N runs, pre-split on the host into pieces of <= 1024 bases.
+struct NPiece {
+    int64_t bit0;  // global base index (word_off*32 + start)
+    int32_t len;
+    int32_t pad;
+};
+
+__global__ void __launch_bounds__(256) k_nruns(const NPiece *pieces, int64_t n, uint32_t *nmask) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const NPiece p = pieces[i];
+    int64_t b = p.bit0;
+    const int64_t e = p.bit0 + p.len;
+    while (b < e) {
+        const int64_t w = b >> 5;
+        const int lo = (int)(b & 31);
+        const int64_t wend = (w + 1) << 5;
+        const int hi = (int)((e < wend ? e : wend) - (w << 5));  // exclusive bit
+        const uint32_t m = (hi >= 32 ? 0xffffffffu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+        atomicOr(&nmask[w], m);
+        b = w * 32 + hi;
+    }
+}
+
+}  // namespace gac
+
+// ---------------------------------------------------------------- launch --
+#include <hipcub/hipcub.hpp>
+
+namespace gac {
+
+size_t scan_temp_bytes(int64_t n) {
+    size_t bytes = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (int32_t *)nullptr, (int32_t *)nullptr,
+                                     (int)n, (hipStream_t)0);
+    return bytes;
+}
+
+hipError_t launch_plan(const ScoreArgs &a, hipStream_t s) {
+    const int64_t nb = (a.n + 255) / 256;
+    hipLaunchKernelGGL(k_plan, dim3((unsigned)nb), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_total(const ScoreArgs &a, void *temp, size_t temp_bytes, hipStream_t s) {
+    hipError_t e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, a.ntiles, a.tile_off,
+                                                    (int)a.n, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_total, dim3(1), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter(const ScoreArgs &a, hipStream_t s) {
+    const int64_t nb = (a.n + 255) / 256;
+    hipLaunchKernelGGL(k_scatter, dim3((unsigned)nb), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile(const ScoreArgs &a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_tile, dim3(grid), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_combine(const ScoreArgs &a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_combine, dim3(grid), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_relayout(const uint8_t *raw, const SeqDev *seqs, int nseq, int64_t nwords,
+                           uint2 *planes, uint32_t *nmask, hipStream_t s) {
+    const int64_t nb = (nwords + 255) / 256;
+    if (nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_relayout, dim3((unsigned)nb), dim3(256), 0, s, raw, seqs, nseq, nwords,
+                       planes, nmask);
+    return hipGetLastError();
+}
+
+hipError_t launch_nruns(const NPiece *p, int64_t n, uint32_t *nmask, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const int64_t nb = (n + 255) / 256;
+    hipLaunchKernelGGL(k_nruns, dim3((unsigned)nb), dim3(256), 0, s, p, n, nmask);
+    return hipGetLastError();
+}
+
+}  // namespace gac

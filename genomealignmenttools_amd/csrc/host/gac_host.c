@@ -1,0 +1,639 @@
+/* gac_host.c -- host-side parsing for libgachain (C11).
+ *
+ * Restates, with the same observable results, the kent routines the scoring
+ * path needs before any device work:
+ *   gapCalcRead / gapCalcFromFile / interpolate / calcSlope
+ *       kent/src/lib/gapCalc.c:82-255   (gap tables; built-in loose/medium :40-73)
+ *   axtScoreSchemeReadLf / axtScoreSchemeDefault
+ *       kent/src/lib/axt.c:423-458,692-819
+ *   twoBitOpen / readTwoBitSeqHeader (index only; decoding is on the device)
+ *       kent/src/lib/twoBit.c:420-635
+ */
+#define _GNU_SOURCE
+#include "gac_host.h"
+
+#include <ctype.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+/* ------------------------------------------------------------------ errors */
+static __thread char g_err[1024];
+
+int gac_fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+void gac_clear_error(void) { g_err[0] = 0; }
+
+const char *gac_last_error(void) { return g_err; }
+
+int gac_abi_version(void) { return GAC_ABI_VERSION; }
+
+/* ------------------------------------------------------------- file mapping */
+int gac_map_file(const char *path, gac_map *m) {
+    memset(m, 0, sizeof(*m));
+    m->fd = -1;
+    int fd = (strcmp(path, "stdin") == 0) ? 0 : open(path, O_RDONLY);
+    if (fd < 0)
+        return gac_fail(GAC_E_IO, "can't open %s: %s", path, strerror(errno));
+    struct stat st;
+    if (fd != 0 && fstat(fd, &st) == 0 && S_ISREG(st.st_mode)) {
+        m->size = (size_t)st.st_size;
+        if (m->size == 0) {
+            m->data = (const uint8_t *)"";
+            m->fd = fd;
+            m->mapped = 0;
+            close(fd);
+            m->fd = -1;
+            return GAC_OK;
+        }
+        void *p = mmap(NULL, m->size, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (p == MAP_FAILED) {
+            close(fd);
+            return gac_fail(GAC_E_IO, "can't mmap %s: %s", path, strerror(errno));
+        }
+        madvise(p, m->size, MADV_SEQUENTIAL);
+        m->data = p;
+        m->fd = fd;
+        m->mapped = 1;
+        return GAC_OK;
+    }
+    /* pipe / stdin: slurp */
+    size_t cap = 1 << 20, len = 0;
+    uint8_t *buf = malloc(cap);
+    if (!buf)
+        return gac_fail(GAC_E_IO, "out of memory reading %s", path);
+    for (;;) {
+        if (len == cap) {
+            cap *= 2;
+            uint8_t *nb = realloc(buf, cap);
+            if (!nb) {
+                free(buf);
+                return gac_fail(GAC_E_IO, "out of memory reading %s", path);
+            }
+            buf = nb;
+        }
+        ssize_t r = read(fd, buf + len, cap - len);
+        if (r < 0) {
+            free(buf);
+            return gac_fail(GAC_E_IO, "read error on %s", path);
+        }
+        if (r == 0)
+            break;
+        len += (size_t)r;
+    }
+    if (fd != 0)
+        close(fd);
+    m->data = buf;
+    m->size = len;
+    m->mapped = 0;
+    m->fd = -2; /* heap-owned */
+    return GAC_OK;
+}
+
+void gac_unmap_file(gac_map *m) {
+    if (m->mapped) {
+        munmap((void *)m->data, m->size);
+        close(m->fd);
+    } else if (m->fd == -2) {
+        free((void *)m->data);
+    }
+    memset(m, 0, sizeof(*m));
+}
+
+/* ------------------------------------------------------------ word helpers */
+int gac_chop_white(char *s, char **words, int max) {
+    int n = 0;
+    while (n < max) {
+        while (*s && isspace((unsigned char)*s))
+            ++s;
+        if (*s == 0)
+            break;
+        words[n++] = s;
+        while (*s && !isspace((unsigned char)*s))
+            ++s;
+        if (*s == 0)
+            break;
+        *s++ = 0;
+    }
+    return n;
+}
+
+int gac_same_word(const char *a, const char *b) { return strcasecmp(a, b) == 0; }
+
+/* ------------------------------------------------------------------ gapCalc */
+/* Built-in tables, same numbers as kent/src/lib/gapCalc.c:40-73. */
+static const char *k_gap_loose =
+    "tablesize 11\n"
+    "smallSize 111\n"
+    "position 1 2 3 11 111 2111 12111 32111 72111 152111 252111\n"
+    "qGap 325 360 400 450 600 1100 3600 7600 15600 31600 56600\n"
+    "tGap 325 360 400 450 600 1100 3600 7600 15600 31600 56600\n"
+    "bothGap 625 660 700 750 900 1400 4000 8000 16000 32000 57000\n";
+static const char *k_gap_medium =
+    "tableSize 11\n"
+    "smallSize 111\n"
+    "position 1 2 3 11 111 2111 12111 32111 72111 152111 252111\n"
+    "qGap 350 425 450 600 900 2900 22900 57900 117900 217900 317900\n"
+    "tGap 350 425 450 600 900 2900 22900 57900 117900 217900 317900\n"
+    "bothGap 750 825 850 1000 1300 3300 23300 58300 118300 218300 318300\n";
+
+/* kent interpolate(): linear interpolation between table points, evaluated in
+ * double with the reference's operation order, truncated to int on return. */
+static int gc_interp(int x, const int *s, const double *v, int n) {
+    for (int i = 0; i < n; ++i) {
+        if (x == s[i])
+            return (int)v[i];
+        if (x < s[i]) {
+            int ds = s[i] - s[i - 1];
+            double dv = v[i] - v[i - 1];
+            volatile double prod = dv * (x - s[i - 1]); /* no contraction */
+            return (int)(v[i - 1] + prod / ds);
+        }
+    }
+    int ds = s[n - 1] - s[n - 2];
+    double dv = v[n - 1] - v[n - 2];
+    volatile double prod = dv * (x - s[n - 2]);
+    return (int)(v[n - 2] + prod / ds);
+}
+
+typedef struct gc_text {
+    char *buf;
+    char *cur;
+    const char *name;
+    int line;
+} gc_text;
+
+/* Next line that is not blank and not a comment (kent lineFileNextReal). */
+static char *gc_next_real(gc_text *t) {
+    while (t->cur && *t->cur) {
+        char *line = t->cur;
+        char *nl = strchr(line, '\n');
+        if (nl) {
+            *nl = 0;
+            t->cur = nl + 1;
+        } else {
+            t->cur = line + strlen(line);
+        }
+        ++t->line;
+        char *p = line;
+        while (*p && isspace((unsigned char)*p))
+            ++p;
+        if (*p != 0 && *p != '#')
+            return line;
+    }
+    return NULL;
+}
+
+/* kent readTaggedNumLine (gapCalc.c:112-144). */
+static int gc_tagged(gc_text *t, const char *tag, int count, int *iout, double *fout) {
+    char *line = gc_next_real(t);
+    if (!line)
+        return gac_fail(GAC_E_FORMAT, "Unexpected end of file in %s", t->name);
+    char *w[512];
+    int nw = gac_chop_white(line, w, 512);
+    if (nw == 0 || !gac_same_word(tag, w[0]))
+        return gac_fail(GAC_E_FORMAT, "Expecting %s got %s line %d of %s", tag,
+                        nw ? w[0] : "", t->line, t->name);
+    if (nw - 1 < count)
+        return gac_fail(GAC_E_FORMAT, "Not enough numbers line %d of %s", t->line, t->name);
+    if (nw - 1 > count)
+        return gac_fail(GAC_E_FORMAT, "Too many numbers line %d of %s", t->line, t->name);
+    for (int i = 0; i < count; ++i) {
+        const char *word = w[i + 1];
+        if (!isdigit((unsigned char)word[0]))
+            return gac_fail(GAC_E_FORMAT, "Expecting number got %s line %d of %s", word,
+                            t->line, t->name);
+        if (iout)
+            iout[i] = atoi(word);
+        if (fout)
+            fout[i] = atof(word);
+    }
+    return GAC_OK;
+}
+
+void gac_gapcalc_free(gac_gapcalc *g) {
+    if (!g)
+        return;
+    free(g->q_small);
+    free(g->t_small);
+    free(g->b_small);
+    free(g->long_pos);
+    free(g->q_long);
+    free(g->t_long);
+    free(g->b_long);
+    free(g);
+}
+
+static int gc_parse(char *text, const char *name, gac_gapcalc **out) {
+    gc_text t = {text, text, name, 0};
+    int table_size = 0, small_size = 0, rc;
+    if ((rc = gc_tagged(&t, "tableSize", 1, &table_size, NULL)) != GAC_OK)
+        return rc;
+    if ((rc = gc_tagged(&t, "smallSize", 1, &small_size, NULL)) != GAC_OK)
+        return rc;
+    if (table_size < 2 || table_size > 4096 || small_size < 1)
+        return gac_fail(GAC_E_FORMAT, "bad tableSize/smallSize in %s", name);
+    int *pos = calloc(table_size, sizeof(int));
+    double *qg = calloc(table_size, sizeof(double));
+    double *tg = calloc(table_size, sizeof(double));
+    double *bg = calloc(table_size, sizeof(double));
+    gac_gapcalc *g = calloc(1, sizeof(*g));
+    if (!pos || !qg || !tg || !bg || !g) {
+        rc = gac_fail(GAC_E_ARG, "out of memory");
+        goto done;
+    }
+    if ((rc = gc_tagged(&t, "position", table_size, pos, NULL)) != GAC_OK ||
+        (rc = gc_tagged(&t, "qGap", table_size, NULL, qg)) != GAC_OK ||
+        (rc = gc_tagged(&t, "tGap", table_size, NULL, tg)) != GAC_OK ||
+        (rc = gc_tagged(&t, "bothGap", table_size, NULL, bg)) != GAC_OK)
+        goto done;
+    g->small_size = small_size;
+    g->q_small = calloc(small_size, sizeof(int32_t));
+    g->t_small = calloc(small_size, sizeof(int32_t));
+    g->b_small = calloc(small_size, sizeof(int32_t));
+    /* small tables for 1..smallSize-1; index 0 stays 0 (gapCalc.c:174-182) */
+    for (int i = 1; i < small_size; ++i) {
+        g->q_small[i] = gc_interp(i, pos, qg, table_size);
+        g->t_small[i] = gc_interp(i, pos, tg, table_size);
+        g->b_small[i] = gc_interp(i, pos, bg, table_size);
+    }
+    int start_long = -1;
+    for (int i = 0; i < table_size; ++i)
+        if (pos[i] == small_size) {
+            start_long = i;
+            break;
+        }
+    if (start_long < 0) {
+        rc = gac_fail(GAC_E_FORMAT, "No position %d in gapCalcRead()", small_size);
+        goto done;
+    }
+    int lc = table_size - start_long;
+    if (lc < 2) {
+        rc = gac_fail(GAC_E_FORMAT, "need >= 2 long positions in %s", name);
+        goto done;
+    }
+    g->long_count = lc;
+    g->long_pos = malloc(lc * sizeof(int32_t));
+    g->q_long = malloc(lc * sizeof(double));
+    g->t_long = malloc(lc * sizeof(double));
+    g->b_long = malloc(lc * sizeof(double));
+    for (int i = 0; i < lc; ++i) {
+        g->long_pos[i] = pos[start_long + i];
+        g->q_long[i] = qg[start_long + i];
+        g->t_long[i] = tg[start_long + i];
+        g->b_long[i] = bg[start_long + i];
+    }
+    g->q_last_pos = g->t_last_pos = g->b_last_pos = g->long_pos[lc - 1];
+    g->q_last_val = g->q_long[lc - 1];
+    g->t_last_val = g->t_long[lc - 1];
+    g->b_last_val = g->b_long[lc - 1];
+    /* calcSlope (gapCalc.c:106-110): (y2-y1)/(x2-x1) in double */
+    double dx = (double)g->long_pos[lc - 1] - (double)g->long_pos[lc - 2];
+    g->q_last_slope = (g->q_last_val - g->q_long[lc - 2]) / dx;
+    g->t_last_slope = (g->t_last_val - g->t_long[lc - 2]) / dx;
+    g->b_last_slope = (g->b_last_val - g->b_long[lc - 2]) / dx;
+    *out = g;
+    g = NULL;
+    rc = GAC_OK;
+done:
+    free(pos);
+    free(qg);
+    free(tg);
+    free(bg);
+    gac_gapcalc_free(g);
+    return rc;
+}
+
+int gac_gapcalc_build(const char *name, gac_gapcalc **out) {
+    if (!name || !out)
+        return gac_fail(GAC_E_ARG, "gac_gapcalc_build: NULL argument");
+    *out = NULL;
+    char *text = NULL;
+    int rc;
+    if (strcmp(name, "loose") == 0)
+        text = strdup(k_gap_loose);
+    else if (strcmp(name, "medium") == 0)
+        text = strdup(k_gap_medium);
+    else {
+        gac_map m;
+        if ((rc = gac_map_file(name, &m)) != GAC_OK)
+            return rc;
+        text = malloc(m.size + 1);
+        memcpy(text, m.data, m.size);
+        text[m.size] = 0;
+        gac_unmap_file(&m);
+    }
+    rc = gc_parse(text, name, out);
+    free(text);
+    return rc;
+}
+
+/* --------------------------------------------------------- score matrix */
+/* blastz default (axt.c:423-458), A,C,G,T order, [query][target] */
+static const int32_t k_blastz[16] = {91, -114, -31, -123, -114, 100, -125, -31,
+                                     -31, -125, 100, -114, -123, -31, -114, 91};
+
+typedef struct sc_lines {
+    char *cur;
+    int line;
+} sc_lines;
+
+/* raw next line (kent lineFileNext) */
+static char *sc_next(sc_lines *l) {
+    if (!l->cur || !*l->cur)
+        return NULL;
+    char *line = l->cur;
+    char *nl = strchr(line, '\n');
+    if (nl) {
+        *nl = 0;
+        l->cur = nl + 1;
+    } else {
+        l->cur = line + strlen(line);
+    }
+    ++l->line;
+    return line;
+}
+
+/* kent lineFileChopNext: skip lines starting with '#' and blank lines */
+static int sc_chop_next(sc_lines *l, char **row, int max) {
+    char *line;
+    while ((line = sc_next(l)) != NULL) {
+        if (line[0] == '#')
+            continue;
+        int n = gac_chop_white(line, row, max);
+        if (n)
+            return n;
+    }
+    return 0;
+}
+
+static void sc_append(char **buf, size_t *len, size_t *cap, const char *s) {
+    size_t n = strlen(s);
+    if (*len + n + 1 > *cap) {
+        *cap = (*len + n + 1) * 2;
+        *buf = realloc(*buf, *cap);
+    }
+    memcpy(*buf + *len, s, n + 1);
+    *len += n;
+}
+
+/* split on any char of seps, dropping empty fields (kent chopString) */
+static int sc_chop_string(char *s, const char *seps, char **parts, int max) {
+    int n = 0;
+    while (*s && n < max) {
+        while (*s && strchr(seps, *s))
+            ++s;
+        if (!*s)
+            break;
+        parts[n++] = s;
+        while (*s && !strchr(seps, *s))
+            ++s;
+        if (*s)
+            *s++ = 0;
+    }
+    return n;
+}
+
+int gac_scheme_read(const char *path, int32_t mat[16], int32_t *gap_open,
+                    int32_t *gap_extend, char **extra) {
+    if (extra)
+        *extra = NULL;
+    if (!path) {
+        memcpy(mat, k_blastz, sizeof(k_blastz));
+        if (gap_open)
+            *gap_open = 400;
+        if (gap_extend)
+            *gap_extend = 30;
+        return GAC_OK;
+    }
+    gac_map m;
+    int rc = gac_map_file(path, &m);
+    if (rc != GAC_OK)
+        return rc;
+    char *text = malloc(m.size + 1);
+    memcpy(text, m.data, m.size);
+    text[m.size] = 0;
+    gac_unmap_file(&m);
+
+    sc_lines l = {text, 0};
+    char *row[6];
+    char *ex = calloc(1, 64);
+    size_t exlen = 0, excap = 64;
+    int go = 400, ge = 30;
+    int wc = sc_chop_next(&l, row, 6);
+    if (!wc) {
+        rc = gac_fail(GAC_E_FORMAT, "Scoring matrix file %s too short", path);
+        goto out;
+    }
+    for (;;) {
+        if (strchr(row[0], '=') || (wc > 1 && strchr(row[1], '='))) {
+            char joined[4096];
+            joined[0] = 0;
+            for (int i = 0; i < wc; ++i)
+                strncat(joined, row[i], sizeof(joined) - strlen(joined) - 1);
+            char *hash = strchr(joined, '#');
+            if (hash)
+                *hash = 0;
+            char *parts[32];
+            int np = sc_chop_string(joined, "=", parts, 32);
+            if (np >= 2 && !(strcmp(parts[0], "O") == 0 || strcmp(parts[0], "E") == 0)) {
+                sc_append(&ex, &exlen, &excap, parts[0]);
+                sc_append(&ex, &exlen, &excap, "=");
+                sc_append(&ex, &exlen, &excap, parts[1]);
+                sc_append(&ex, &exlen, &excap, ",");
+            }
+            wc = sc_chop_next(&l, row, 6);
+            if (!wc) {
+                rc = gac_fail(GAC_E_FORMAT, "Scoring matrix file %s too short", path);
+                goto out;
+            }
+            continue;
+        }
+        if (wc < 4 || row[0][0] != 'A' || row[1][0] != 'C' || row[2][0] != 'G' ||
+            row[3][0] != 'T') {
+            rc = gac_fail(GAC_E_FORMAT, "%s doesn't seem to be a score matrix file", path);
+            goto out;
+        }
+        for (int i = 0; i < 4; ++i) {
+            wc = sc_chop_next(&l, row, 6);
+            if (!wc) {
+                rc = gac_fail(GAC_E_FORMAT, "Scoring matrix file %s too short", path);
+                goto out;
+            }
+            int c0 = (wc == 5) ? 1 : 0;
+            if (wc < c0 + 4) {
+                rc = gac_fail(GAC_E_FORMAT, "short matrix row line %d of %s", l.line, path);
+                goto out;
+            }
+            for (int j = 0; j < 4; ++j) {
+                char *end;
+                const char *w = row[c0 + j];
+                long v = strtol(w, &end, 10);
+                if (end == w || *end != 0) {
+                    rc = gac_fail(GAC_E_FORMAT, "Expecting number got %s line %d of %s", w,
+                                  l.line, path);
+                    goto out;
+                }
+                mat[i * 4 + j] = (int32_t)v;
+            }
+        }
+        char *line = sc_next(&l);
+        if (line) {
+            sc_append(&ex, &exlen, &excap, line);
+            sc_append(&ex, &exlen, &excap, ",");
+            char *parts[32];
+            int np = sc_chop_string(line, " =,\t", parts, 32);
+            int got_o = 0, got_e = 0;
+            for (int i = 0; i < np - 1; i += 2) {
+                if (strcmp(parts[i], "O") == 0) {
+                    got_o = 1;
+                    go = atoi(parts[i + 1]);
+                }
+                if (strcmp(parts[i], "E") == 0) {
+                    got_e = 1;
+                    ge = atoi(parts[i + 1]);
+                }
+            }
+            if (!got_o || !got_e) {
+                rc = gac_fail(GAC_E_FORMAT, "Expecting O = and E = in last line of %s", path);
+                goto out;
+            }
+            if (go <= 0 || ge <= 0) {
+                rc = gac_fail(GAC_E_FORMAT, "Must have positive gap scores");
+                goto out;
+            }
+        }
+        break;
+    }
+    if (exlen && ex[exlen - 1] == ',')
+        ex[--exlen] = 0;
+    if (gap_open)
+        *gap_open = go;
+    if (gap_extend)
+        *gap_extend = ge;
+    if (extra) {
+        *extra = ex;
+        ex = NULL;
+    }
+    rc = GAC_OK;
+out:
+    free(ex);
+    free(text);
+    return rc;
+}
+
+/* ------------------------------------------------------------------- 2bit */
+#define TWOBIT_SIG 0x1A412743u
+#define TWOBIT_SIG_SWAP 0x4327411Au
+
+uint32_t gac_twobit_u32(const gac_twobit *tb, const uint8_t *p) {
+    uint32_t v;
+    memcpy(&v, p, 4);
+    return tb->swapped ? __builtin_bswap32(v) : v;
+}
+
+static uint64_t tb_u64(const gac_twobit *tb, const uint8_t *p) {
+    uint64_t v;
+    memcpy(&v, p, 8);
+    return tb->swapped ? __builtin_bswap64(v) : v;
+}
+
+int gac_is_twobit_file(const char *path) {
+    size_t n = strlen(path);
+    return n >= 5 && strcmp(path + n - 5, ".2bit") == 0;
+}
+
+void gac_twobit_close(gac_twobit *tb) {
+    if (tb->seqs) {
+        for (uint32_t i = 0; i < tb->seq_count; ++i)
+            free(tb->seqs[i].name);
+        free(tb->seqs);
+    }
+    gac_unmap_file(&tb->map);
+    memset(tb, 0, sizeof(*tb));
+}
+
+int gac_twobit_open(const char *path, gac_twobit *tb) {
+    memset(tb, 0, sizeof(*tb));
+    int rc = gac_map_file(path, &tb->map);
+    if (rc != GAC_OK)
+        return rc;
+    const uint8_t *d = tb->map.data;
+    size_t sz = tb->map.size;
+    if (sz < 16) {
+        gac_twobit_close(tb);
+        return gac_fail(GAC_E_FORMAT, "%s doesn't have a valid twoBitSig", path);
+    }
+    uint32_t sig;
+    memcpy(&sig, d, 4);
+    if (sig == TWOBIT_SIG_SWAP)
+        tb->swapped = 1;
+    else if (sig != TWOBIT_SIG) {
+        gac_twobit_close(tb);
+        return gac_fail(GAC_E_FORMAT, "%s doesn't have a valid twoBitSig", path);
+    }
+    tb->version = gac_twobit_u32(tb, d + 4);
+    if (tb->version != 0 && tb->version != 1) {
+        gac_twobit_close(tb);
+        return gac_fail(GAC_E_FORMAT,
+                        "Can only handle version 0 or version 1 of this file. This is version %u",
+                        tb->version);
+    }
+    tb->seq_count = gac_twobit_u32(tb, d + 8);
+    tb->seqs = calloc(tb->seq_count ? tb->seq_count : 1, sizeof(gac_twobit_seq));
+    size_t off = 16;
+    for (uint32_t i = 0; i < tb->seq_count; ++i) {
+        if (off + 1 > sz)
+            goto trunc;
+        uint32_t nl = d[off++];
+        if (off + nl + (tb->version == 1 ? 8 : 4) > sz)
+            goto trunc;
+        tb->seqs[i].name = strndup((const char *)d + off, nl);
+        off += nl;
+        uint64_t so;
+        if (tb->version == 1) {
+            so = tb_u64(tb, d + off);
+            off += 8;
+        } else {
+            so = gac_twobit_u32(tb, d + off);
+            off += 4;
+        }
+        /* sequence record */
+        size_t p = (size_t)so;
+        if (p + 8 > sz)
+            goto trunc;
+        gac_twobit_seq *s = &tb->seqs[i];
+        s->size = gac_twobit_u32(tb, d + p);
+        p += 4;
+        s->n_count = gac_twobit_u32(tb, d + p);
+        p += 4;
+        if (p + 8ull * s->n_count + 4 > sz)
+            goto trunc;
+        s->n_starts_raw = d + p;
+        p += 4ull * s->n_count;
+        s->n_sizes_raw = d + p;
+        p += 4ull * s->n_count;
+        uint32_t mc = gac_twobit_u32(tb, d + p);
+        p += 4 + 8ull * mc;
+        p += 4; /* reserved */
+        if (p + ((size_t)s->size + 3) / 4 > sz)
+            goto trunc;
+        s->packed = d + p;
+    }
+    return GAC_OK;
+trunc:
+    gac_twobit_close(tb);
+    return gac_fail(GAC_E_FORMAT, "%s is truncated", path);
+}

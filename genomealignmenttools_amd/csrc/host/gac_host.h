@@ -1,0 +1,64 @@
+/* gac_host.h -- internal host-side (C11) helpers of libgachain: error state,
+ * file mapping, word splitting, 2bit index, gap-table and score-matrix
+ * parsing.  Not part of the public ABI (see include/gachain.h). */
+#ifndef GAC_HOST_H
+#define GAC_HOST_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "gachain.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- errors: thread-local last message ---- */
+int gac_fail(int code, const char *fmt, ...)
+#ifdef __GNUC__
+    __attribute__((format(printf, 2, 3)))
+#endif
+    ;
+void gac_clear_error(void);
+
+/* ---- read-only whole-file mapping ---- */
+typedef struct gac_map {
+    const uint8_t *data;
+    size_t size;
+    int fd;
+    int mapped; /* 1 = mmap, 0 = heap (pipes / stdin) */
+} gac_map;
+int gac_map_file(const char *path, gac_map *m);
+void gac_unmap_file(gac_map *m);
+
+/* ---- line / word helpers (kent chopByWhite semantics) ---- */
+/* Split s (modified in place) on whitespace into at most max words. */
+int gac_chop_white(char *s, char **words, int max);
+/* Case-insensitive string equality (kent sameWord). */
+int gac_same_word(const char *a, const char *b);
+
+/* ---- 2bit index (kent/src/lib/twoBit.c:420-635) ---- */
+typedef struct gac_twobit_seq {
+    char *name;
+    uint32_t size;
+    uint32_t n_count;
+    const uint8_t *n_starts_raw, *n_sizes_raw; /* file order, maybe byte-swapped */
+    const uint8_t *packed;                     /* (size+3)/4 bytes */
+} gac_twobit_seq;
+
+typedef struct gac_twobit {
+    gac_map map;
+    int swapped;
+    uint32_t version;
+    uint32_t seq_count;
+    gac_twobit_seq *seqs;
+} gac_twobit;
+
+int gac_twobit_open(const char *path, gac_twobit *tb);
+void gac_twobit_close(gac_twobit *tb);
+uint32_t gac_twobit_u32(const gac_twobit *tb, const uint8_t *p);
+int gac_is_twobit_file(const char *path);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

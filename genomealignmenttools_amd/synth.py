@@ -1,0 +1,342 @@
+"""Seeded synthetic genomes and chain sets.
+
+Genomes are produced directly in the .2bit code (T=0 C=1 A=2 G=3), with N
+runs and soft-mask runs, and can be written as real .2bit files.  Chains are
+planted homology: query bases under each block are a mutated copy of the
+target (12% substitutions, transitions:transversions 2:1), '-' strand chains
+write the reverse complement.  Everything is numpy-vectorised so the C2 set
+(~2e5 chains, ~2e8 aligned bases, hg38 chr1 x mm10) builds in seconds.
+"""
+from __future__ import annotations
+
+import os
+import struct
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+from .chainfile import ChainArrays
+
+_NT = np.frombuffer(b"tcag", dtype=np.uint8)
+
+# loose gap table (kent/src/lib/gapCalc.c:51-57) -- only used for the
+# approximate synthetic header score, never for scoring
+_LOOSE_POS = np.array([1, 2, 3, 11, 111, 2111, 12111, 32111, 72111, 152111, 252111], float)
+_LOOSE_Q = np.array([325, 360, 400, 450, 600, 1100, 3600, 7600, 15600, 31600, 56600], float)
+_LOOSE_B = np.array([625, 660, 700, 750, 900, 1400, 4000, 8000, 16000, 32000, 57000], float)
+
+# blastz default, [query][target] in 2bit code order (T, C, A, G)
+_BLASTZ_ACGT = np.array([[91, -114, -31, -123], [-114, 100, -125, -31],
+                         [-31, -125, 100, -114], [-123, -31, -114, 91]], np.int64)
+_CODE2ACGT = np.array([3, 1, 0, 2])
+
+
+def matrix_by_code(mat_acgt: np.ndarray) -> np.ndarray:
+    m = np.asarray(mat_acgt, np.int64)
+    return m[np.ix_(_CODE2ACGT, _CODE2ACGT)]
+
+
+@dataclass
+class Genome:
+    names: List[str]
+    codes: List[np.ndarray]                      # uint8 per base, 0..3
+    nruns: List[Tuple[np.ndarray, np.ndarray]]   # (starts, sizes) int32
+    mruns: List[Tuple[np.ndarray, np.ndarray]] = field(default_factory=list)
+
+    @property
+    def sizes(self) -> Dict[str, int]:
+        return {n: len(c) for n, c in zip(self.names, self.codes)}
+
+    def index(self, name: str) -> int:
+        return self.names.index(name)
+
+    def packed(self, i: int) -> np.ndarray:
+        """.2bit payload bytes (2 bits/base, MSB first)."""
+        c = self.codes[i]
+        n = len(c)
+        pad = (-n) % 4
+        if pad:
+            c = np.concatenate([c, np.zeros(pad, np.uint8)])
+        c = c.reshape(-1, 4)
+        return ((c[:, 0] << 6) | (c[:, 1] << 4) | (c[:, 2] << 2) | c[:, 3]).astype(np.uint8)
+
+    def text(self, i: int) -> str:
+        """Decoded 'acgtn' text (reference twoBitReadSeqFrag without mask case)."""
+        s = _NT[self.codes[i]].copy()
+        st, sz = self.nruns[i]
+        for a, b in zip(st, sz):
+            s[a:a + b] = ord("n")
+        return s.tobytes().decode()
+
+    def seq_records(self):
+        """(name, size, packed, n_starts, n_sizes) for Engine.add_sequences."""
+        for i, n in enumerate(self.names):
+            yield n, len(self.codes[i]), self.packed(i), self.nruns[i][0], self.nruns[i][1]
+
+
+def random_runs(rng, size: int, frac: float, mean_len: int) -> Tuple[np.ndarray, np.ndarray]:
+    if frac <= 0 or size < 4:
+        return np.zeros(0, np.int32), np.zeros(0, np.int32)
+    k = max(1, int(size * frac / mean_len))
+    starts = np.sort(rng.integers(0, size, k))
+    lens = rng.geometric(1.0 / mean_len, k)
+    ends = np.minimum(starts + lens, size)
+    # merge overlaps -> disjoint sorted runs
+    out_s, out_e = [], []
+    cs, ce = int(starts[0]), int(ends[0])
+    for s, e in zip(starts[1:], ends[1:]):
+        if s <= ce:
+            ce = max(ce, int(e))
+        else:
+            out_s.append(cs)
+            out_e.append(ce)
+            cs, ce = int(s), int(e)
+    out_s.append(cs)
+    out_e.append(ce)
+    s = np.asarray(out_s, np.int32)
+    return s, (np.asarray(out_e, np.int32) - s)
+
+
+def random_genome(sizes: Dict[str, int], seed: int, n_frac: float = 0.005,
+                  n_mean: int = 2000, mask_frac: float = 0.0) -> Genome:
+    rng = np.random.default_rng(seed)
+    names, codes, nr, mr = [], [], [], []
+    for name, size in sizes.items():
+        names.append(name)
+        b = np.frombuffer(rng.bytes((size + 3) // 4), dtype=np.uint8)
+        c = np.empty(b.size * 4, np.uint8)
+        c[0::4] = b >> 6
+        c[1::4] = (b >> 4) & 3
+        c[2::4] = (b >> 2) & 3
+        c[3::4] = b & 3
+        c = c[:size].copy()
+        ns, nz = random_runs(rng, size, n_frac, n_mean)
+        for a, l in zip(ns, nz):
+            c[a:a + l] = 0  # .2bit stores N as T
+        codes.append(c)
+        nr.append((ns, nz))
+        mr.append(random_runs(rng, size, mask_frac, 300) if mask_frac > 0 else
+                  (np.zeros(0, np.int32), np.zeros(0, np.int32)))
+    return Genome(names, codes, nr, mr)
+
+
+def write_2bit(g: Genome, path: str) -> None:
+    """Write a version-0 .2bit file (kent twoBit.c layout)."""
+    n = len(g.names)
+    header = struct.pack("<IIII", 0x1A412743, 0, n, 0)
+    index_size = sum(1 + len(nm.encode()) + 4 for nm in g.names)
+    off = len(header) + index_size
+    recs, index = [], []
+    for i, nm in enumerate(g.names):
+        size = len(g.codes[i])
+        ns, nz = g.nruns[i]
+        ms, mz = g.mruns[i] if i < len(g.mruns) else (np.zeros(0, np.int32),) * 2
+        rec = struct.pack("<II", size, len(ns)) + np.asarray(ns, "<u4").tobytes() + \
+            np.asarray(nz, "<u4").tobytes() + struct.pack("<I", len(ms)) + \
+            np.asarray(ms, "<u4").tobytes() + np.asarray(mz, "<u4").tobytes() + \
+            struct.pack("<I", 0) + g.packed(i).tobytes()
+        index.append(struct.pack("<B", len(nm.encode())) + nm.encode() + struct.pack("<I", off))
+        if off + len(rec) >= 1 << 32:
+            raise ValueError("2bit v0 limited to 4 GB")
+        recs.append(rec)
+        off += len(rec)
+    with open(path, "wb") as f:
+        f.write(header)
+        for x in index:
+            f.write(x)
+        for r in recs:
+            f.write(r)
+
+
+def read_sizes(path: str) -> Dict[str, int]:
+    out = {}
+    with open(path) as f:
+        for line in f:
+            w = line.split()
+            if len(w) >= 2:
+                out[w[0]] = int(w[1])
+    return out
+
+
+def write_sizes(sizes: Dict[str, int], path: str) -> None:
+    with open(path, "w") as f:
+        for k, v in sizes.items():
+            f.write(f"{k}\t{v}\n")
+
+
+# ---------------------------------------------------------------- chains
+def _gap_mixture(rng, n: int) -> np.ndarray:
+    r = rng.random(n)
+    small = rng.integers(1, 30, n)
+    med = np.exp(rng.uniform(np.log(30), np.log(10_000), n)).astype(np.int64)
+    big = np.exp(rng.uniform(np.log(10_000), np.log(1_000_000), n)).astype(np.int64)
+    return np.where(r < 0.70, small, np.where(r < 0.98, med, big)).astype(np.int64)
+
+
+def _approx_gap_cost(dq: np.ndarray, dt: np.ndarray) -> np.ndarray:
+    both = (dq > 0) & (dt > 0)
+    d = np.where(both, dq + dt, np.maximum(dq, dt)).astype(float)
+    q = np.interp(d, _LOOSE_POS, _LOOSE_Q, right=np.nan)
+    b = np.interp(d, _LOOSE_POS, _LOOSE_B, right=np.nan)
+    q = np.where(np.isnan(q), 56600 + 0.25 * (d - 252111), q)
+    b = np.where(np.isnan(b), 57000 + 0.25 * (d - 252111), b)
+    return np.where(both, b, q)
+
+
+@dataclass
+class SynthConfig:
+    n_chains: int = 200_000
+    alpha: float = 1.8
+    max_blocks: int = 100_000
+    block_mean: int = 40
+    sub_rate: float = 0.12
+    minus_frac: float = 0.5
+    spurious_frac: float = 0.2
+    max_span_frac: float = 0.5
+    seed: int = 42
+
+
+def make_chains(tgen: Genome, tname: str, qgen: Genome, cfg: SynthConfig,
+                mutate_query: bool = True) -> ChainArrays:
+    """Plant chains target tname x all query sequences; mutates qgen in place
+    (query bases under blocks := mutated target).  Returns chains sorted by
+    (approximate) score, descending, ids 1..n in that order."""
+    rng = np.random.default_rng(cfg.seed)
+    ti = tgen.index(tname)
+    tcodes = tgen.codes[ti]
+    tsize = len(tcodes)
+    qsizes = np.array([len(c) for c in qgen.codes], np.int64)
+    n = cfg.n_chains
+    spur = rng.random(n) < cfg.spurious_frac
+    u = rng.random(n)
+    a1 = 1.0 - cfg.alpha
+    nb = np.floor((1 + u * (cfg.max_blocks ** a1 - 1)) ** (1 / a1)).astype(np.int64)
+    nb = np.clip(nb, 1, cfg.max_blocks)
+    nb[spur] = rng.integers(1, 6, spur.sum())
+    qc = rng.choice(len(qsizes), n, p=qsizes / qsizes.sum())
+    strand = (rng.random(n) < cfg.minus_frac).astype(np.uint8)
+    tot = int(nb.sum())
+    sizes = rng.geometric(1.0 / cfg.block_mean, tot).astype(np.int64)
+    g1 = _gap_mixture(rng, tot)
+    g2 = _gap_mixture(rng, tot)
+    mode = rng.integers(0, 3, tot)
+    dt = np.where(mode == 1, 0, g1)
+    dq = np.where(mode == 0, 0, np.where(mode == 1, g1, g2))
+    off = np.zeros(n + 1, np.int64)
+    off[1:] = np.cumsum(nb)
+    first = off[:-1]
+    # last block of each chain has no gap after it
+    last_idx = off[1:] - 1
+    dt[last_idx] = 0
+    dq[last_idx] = 0
+    # truncate chains to fit max_span_frac of their sequences
+    seg = np.repeat(np.arange(n), nb)
+    tstep = sizes + dt
+    qstep = sizes + dq
+    tcum = np.cumsum(tstep) - np.repeat(np.concatenate([[0], np.cumsum(tstep)[off[1:-1] - 1]]), nb)
+    qcum = np.cumsum(qstep) - np.repeat(np.concatenate([[0], np.cumsum(qstep)[off[1:-1] - 1]]), nb)
+    tlim = cfg.max_span_frac * tsize
+    qlim = cfg.max_span_frac * qsizes[qc][seg]
+    keep = (tcum <= tlim) & (qcum <= qlim)
+    keep[first] = True
+    # keep must be a prefix per chain
+    bad = ~keep
+    firstbad = np.full(n, np.iinfo(np.int64).max)
+    np.minimum.at(firstbad, seg[bad], np.nonzero(bad)[0])
+    keep &= np.arange(tot) < firstbad[seg]
+    sizes, dt, dq, seg = sizes[keep], dt[keep], dq[keep], seg[keep]
+    nb = np.bincount(seg, minlength=n).astype(np.int64)
+    off = np.zeros(n + 1, np.int64)
+    off[1:] = np.cumsum(nb)
+    last_idx = off[1:] - 1
+    dt[last_idx] = 0
+    dq[last_idx] = 0
+    # clamp block sizes so that the chain fits the sequences
+    size_t = np.add.reduceat(sizes + dt, off[:-1])
+    size_q = np.add.reduceat(sizes + dq, off[:-1])
+    ts = (rng.random(n) * (tsize - size_t)).astype(np.int64)
+    qs = (rng.random(n) * (qsizes[qc] - size_q)).astype(np.int64)
+    # block starts
+    tstep = sizes + dt
+    qstep = sizes + dq
+    excl_t = np.cumsum(tstep) - tstep
+    excl_q = np.cumsum(qstep) - qstep
+    bt = ts[seg] + excl_t - excl_t[off[:-1]][seg]
+    bq = qs[seg] + excl_q - excl_q[off[:-1]][seg]
+    te = bt[last_idx] + sizes[last_idx]
+    qe = bq[last_idx] + sizes[last_idx]
+
+    # ---- plant homology & compute block scores (blastz default matrix)
+    mat = matrix_by_code(_BLASTZ_ACGT)
+    blk_score = np.zeros(len(sizes), np.int64)
+    if mutate_query:
+        order = np.argsort(qc[seg], kind="stable")
+        qc_blk = qc[seg]
+        for qi in np.unique(qc):
+            sel = order[np.searchsorted(qc_blk[order], qi):np.searchsorted(qc_blk[order], qi, "right")]
+            qcodes = qgen.codes[qi]
+            qsize = len(qcodes)
+            for chunk in np.array_split(sel, max(1, int(sizes[sel].sum() // 20_000_000) + 1)):
+                if len(chunk) == 0:
+                    continue
+                lens = sizes[chunk]
+                rep = np.repeat(np.arange(len(chunk)), lens)
+                within = np.arange(lens.sum()) - np.repeat(np.cumsum(lens) - lens, lens)
+                tpos = bt[chunk][rep] + within
+                rpos = bq[chunk][rep] + within
+                minus = strand[seg[chunk]][rep].astype(bool)
+                tcode = tcodes[tpos]
+                r = rng.random(len(tpos))
+                q = tcode.copy()
+                q = np.where(r < cfg.sub_rate * 2 / 3, q ^ 1, q)
+                q = np.where((r >= cfg.sub_rate * 2 / 3) & (r < cfg.sub_rate * 5 / 6), q ^ 2, q)
+                q = np.where((r >= cfg.sub_rate * 5 / 6) & (r < cfg.sub_rate), q ^ 3, q)
+                fpos = np.where(minus, qsize - 1 - rpos, rpos)
+                qcodes[fpos] = np.where(minus, q ^ 2, q).astype(np.uint8)
+                blk_score[chunk] += np.bincount(rep, weights=mat[q, tcode],
+                                                minlength=len(chunk)).astype(np.int64)
+    gap_cost = _approx_gap_cost(dq, dt)
+    gap_cost[last_idx] = 0
+    score = np.add.reduceat(blk_score - gap_cost, off[:-1]).astype(np.float64)
+    score = np.round(score)
+    order = np.argsort(-score, kind="stable")
+
+    tname_l = [tname] * n
+    qname_l = [qgen.names[i] for i in qc]
+    ca = ChainArrays(
+        score=score, tname=tname_l, tsize=np.full(n, tsize, np.int32),
+        tstart=ts.astype(np.int32), tend=te.astype(np.int32), qname=qname_l,
+        qsize=qsizes[qc].astype(np.int32), qstrand=strand, qstart=qs.astype(np.int32),
+        qend=qe.astype(np.int32), id=np.arange(1, n + 1, dtype=np.int64),
+        blk_off=off, blk_t=bt.astype(np.int32), blk_q=bq.astype(np.int32),
+        blk_size=sizes.astype(np.int32))
+    ca = ca.subset(order)
+    ca.id = np.arange(1, n + 1, dtype=np.int64)
+    return ca
+
+
+def small_case(seed: int = 1, n_chains: int = 300, tsize: int = 400_000,
+               qsizes=(150_000, 90_000, 60_000), max_blocks: int = 400,
+               n_frac: float = 0.01) -> Tuple[Genome, Genome, ChainArrays]:
+    """A tiny, fast, edge-case-rich set for parity tests."""
+    tg = random_genome({"chrT1": tsize}, seed, n_frac=n_frac, n_mean=200, mask_frac=0.2)
+    qg = random_genome({f"chrQ{i + 1}": s for i, s in enumerate(qsizes)}, seed + 1000,
+                       n_frac=n_frac, n_mean=200, mask_frac=0.2)
+    cfg = SynthConfig(n_chains=n_chains, max_blocks=max_blocks, seed=seed)
+    ca = make_chains(tg, "chrT1", qg, cfg)
+    return tg, qg, ca
+
+
+def c2_case(seed: int = 42, n_chains: int = 200_000, sizes_dir: Optional[str] = None,
+            query_limit: Optional[int] = None):
+    """target hg38 chr1, query all mm10 sequences."""
+    here = sizes_dir or os.path.join(os.path.dirname(__file__), "data")
+    hg = read_sizes(os.path.join(here, "hg38.chrom.sizes"))
+    mm = read_sizes(os.path.join(here, "mm10.chrom.sizes"))
+    if query_limit:
+        mm = dict(list(mm.items())[:query_limit])
+    tg = random_genome({"chr1": hg["chr1"]}, seed, n_frac=0.005, n_mean=20_000)
+    qg = random_genome(mm, seed + 1, n_frac=0.005, n_mean=20_000)
+    ca = make_chains(tg, "chr1", qg, SynthConfig(n_chains=n_chains, seed=seed))
+    return tg, qg, ca

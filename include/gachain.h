@@ -1,0 +1,191 @@
+/* gachain.h -- C ABI of libgachain, the MI355X-native chain-scoring engine.
+ *
+ * This is the drop-in boundary for the reference's chain-scoring hot path
+ * (hillerlab/GenomeAlignmentTools: scoreChain, chainNet -rescore,
+ * chainCleaner suspect rescoring).  The reference is single-threaded C whose
+ * tools call the kent library one chain / one sub-chain at a time; this ABI
+ * is the batch, struct-of-arrays replacement for those calls.  Plain C types
+ * only: no torch, no HIP types in any signature.  Every entry point returns
+ * GAC_OK (0) or a negative GAC_E* code; gac_last_error() gives the message.
+ * There is NO CPU fallback: if the HIP runtime or an MI355X (gfx950) device
+ * is unavailable, gac_open() fails and every call on a NULL context fails.
+ *
+ * Reference interfaces replaced (paths relative to the reference root):
+ *   gac_score_ranges      <- chainSubsetOnT      kent/src/lib/chain.c:471-558
+ *                          + chainCalcScore       kent/src/lib/chainConnect.c:24-40
+ *                          + chainScoreBlock      kent/src/lib/chainConnect.c:14-22
+ *                          + gapCalcCost          kent/src/lib/gapCalc.c:298-331
+ *                          + chainCalcScoreLocal  src/scoreChain/scoreChain.c:176-198
+ *                                                 (= src/chainCleaner/chainCleaner.c:531-551)
+ *                          + chainBaseCountSubT   src/chainNet/chainNet.c:773-782
+ *                          (one call scores a whole batch of (chain, tStart, tEnd)
+ *                           sub-chains; a range covering the chain is the full chain)
+ *   gac_set_scoring       <- axtScoreSchemeDefault / axtScoreSchemeReadLf
+ *                                                 kent/src/lib/axt.c:423-458,692-819
+ *                          + gapCalcFromFile      kent/src/lib/gapCalc.c:233-255
+ *   gac_genome_load_2bit  <- twoBitOpen + twoBitReadSeqFrag(tbf, name, 0, 0)
+ *                                                 kent/src/lib/twoBit.c:482-513,725-888
+ *                          + reverseComplement    kent/src/lib/dnautil.c:404-462
+ *                          (genomes stay resident 2-bit packed; '-' query strand is
+ *                           index arithmetic, not a reverse-complemented copy)
+ *   gac_chains_upload     <- chainRead            kent/src/lib/chain.c:256-346
+ *                          (the caller hands over parsed chains as SoA arrays)
+ */
+#ifndef GACHAIN_H
+#define GACHAIN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GAC_ABI_VERSION 1
+
+/* return codes */
+#define GAC_OK 0
+#define GAC_E_ARG (-1)     /* bad argument / shape */
+#define GAC_E_HIP (-2)     /* HIP runtime error (device fault, OOM, no device) */
+#define GAC_E_IO (-3)      /* file open/read error */
+#define GAC_E_FORMAT (-4)  /* malformed input file */
+#define GAC_E_STATE (-5)   /* call out of order (e.g. scoring before set_scoring) */
+
+/* genome sides */
+#define GAC_T 0 /* target / reference genome */
+#define GAC_Q 1 /* query genome */
+
+/* gac_score_ranges flags */
+#define GAC_WANT_LOCAL 1u /* also compute the scoreChain/chainCleaner local score */
+
+typedef struct gac_ctx gac_ctx;
+typedef struct gac_chainset gac_chainset;
+
+/* Piecewise-linear gap cost tables exactly as kent's struct gapCalc
+ * (kent/src/lib/gapCalc.c:12-37).  small tables have small_size entries,
+ * entry 0 unused (0).  Build one with gac_gapcalc_build(). */
+typedef struct gac_gapcalc {
+    int32_t small_size;
+    int32_t long_count;
+    int32_t *q_small, *t_small, *b_small; /* [small_size] */
+    int32_t *long_pos;                    /* [long_count] */
+    double *q_long, *t_long, *b_long;     /* [long_count] */
+    int32_t q_last_pos, t_last_pos, b_last_pos;
+    double q_last_val, t_last_val, b_last_val;
+    double q_last_slope, t_last_slope, b_last_slope;
+} gac_gapcalc;
+
+/* One sub-chain query: chain index in the chainset and a half-open target
+ * range.  [t_start, t_end) covering the whole chain scores the full chain. */
+typedef struct gac_range {
+    int32_t chain;
+    int32_t t_start;
+    int32_t t_end;
+} gac_range;
+
+/* Parsed chains, struct-of-arrays.  Blocks of chain c are
+ * blk_*[blk_off[c] .. blk_off[c+1]), in chain order (ascending t and q;
+ * q in the chain's strand coordinates, as in the .chain file). */
+typedef struct gac_chainset_desc {
+    int64_t n_chains;
+    const int32_t *t_seq;    /* [n_chains] index into the T genome (gac_genome_seq_index) */
+    const int32_t *q_seq;    /* [n_chains] index into the Q genome */
+    const uint8_t *q_strand; /* [n_chains] 0 = '+', 1 = '-' */
+    const int64_t *blk_off;  /* [n_chains + 1] */
+    int64_t n_blocks;
+    const int32_t *blk_t;    /* [n_blocks] tStart */
+    const int32_t *blk_q;    /* [n_blocks] qStart */
+    const int32_t *blk_size; /* [n_blocks] size (tEnd - tStart == qEnd - qStart) */
+} gac_chainset_desc;
+
+/* ---- library / context ------------------------------------------------ */
+int gac_abi_version(void);
+/* Human-readable message of the last error on this thread. */
+const char *gac_last_error(void);
+/* Open a context on HIP device `device`.  Fails (GAC_E_HIP) if there is no
+ * usable gfx950 device: the library never falls back to the CPU. */
+int gac_open(int device, gac_ctx **out);
+void gac_close(gac_ctx *ctx);
+/* Name of the device architecture the context runs on (e.g. "gfx950"). */
+const char *gac_device_arch(gac_ctx *ctx);
+
+/* ---- scoring scheme (host-side parsing, no device needed) -------------- */
+/* Build gap tables from "loose", "medium" or a linearGap file
+ * (gapCalcFromFile, kent/src/lib/gapCalc.c:233-255).  Free with gac_gapcalc_free. */
+int gac_gapcalc_build(const char *name_or_file, gac_gapcalc **out);
+void gac_gapcalc_free(gac_gapcalc *g);
+/* Read a blastz/lastz matrix file (axtScoreSchemeReadLf, axt.c:692-819), or the
+ * blastz default when path is NULL (axtScoreSchemeDefault, axt.c:423-458).
+ * mat[i*4+j] = matrix[query base i][target base j], i,j in A,C,G,T order.
+ * gap_open/gap_extend/extra may be NULL; extra (malloc'd, caller frees) is the
+ * "##blastzParms" text. */
+int gac_scheme_read(const char *path, int32_t mat[16], int32_t *gap_open,
+                    int32_t *gap_extend, char **extra);
+/* Install matrix + gap tables on the device. */
+int gac_set_scoring(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g);
+
+/* ---- genomes ------------------------------------------------------------ */
+/* Load every sequence of a .2bit file onto the device for side T or Q. */
+int gac_genome_load_2bit(gac_ctx *ctx, int side, const char *path);
+/* Or add sequences one by one from a raw .2bit payload (2 bits/base, MSB
+ * first, T=0 C=1 A=2 G=3) plus N runs, then gac_genome_finalize(). */
+int gac_genome_add_seq(gac_ctx *ctx, int side, const char *name, int32_t size,
+                       const uint8_t *packed, int32_t n_nblocks,
+                       const int32_t *n_starts, const int32_t *n_sizes);
+int gac_genome_finalize(gac_ctx *ctx, int side);
+int32_t gac_genome_seq_count(gac_ctx *ctx, int side);
+/* Sequence index by name, or -1. */
+int32_t gac_genome_seq_index(gac_ctx *ctx, int side, const char *name);
+int32_t gac_genome_seq_size(gac_ctx *ctx, int side, int32_t index);
+const char *gac_genome_seq_name(gac_ctx *ctx, int side, int32_t index);
+/* Decode [start, end) of a resident sequence back to 'acgtn' text (test aid:
+ * proves the resident layout round-trips; out must hold end-start bytes). */
+int gac_genome_decode(gac_ctx *ctx, int side, int32_t index, int32_t start,
+                      int32_t end, char *out);
+
+/* ---- chains ------------------------------------------------------------- */
+int gac_chains_upload(gac_ctx *ctx, const gac_chainset_desc *d, gac_chainset **out);
+void gac_chains_free(gac_chainset *cs);
+int64_t gac_chains_block_count(const gac_chainset *cs);
+
+/* ---- scoring ------------------------------------------------------------ */
+/* Score n sub-chains.  Host buffers; synchronous.  For range r of chain c the
+ * sub-chain is chainSubsetOnT(c, r.t_start, r.t_end) and
+ *   global[r] = chainCalcScore(sub)            (exact; reference's double is integral)
+ *   local[r]  = chainCalcScoreLocal(sub)       (only with GAC_WANT_LOCAL; may be NULL otherwise)
+ *   ali[r]    = sum of clipped block sizes     (chainBaseCountSubT)
+ * A range selecting no block yields 0, 0, 0. */
+int gac_score_ranges(gac_ctx *ctx, const gac_chainset *cs, const gac_range *ranges,
+                     int64_t n, uint32_t flags, int64_t *global, int64_t *local,
+                     int32_t *ali);
+/* Same on device-resident buffers, enqueued on `stream` (a hipStream_t, or
+ * NULL for the context's own stream); returns without synchronising.
+ * d_local may be NULL unless GAC_WANT_LOCAL. */
+int gac_score_ranges_device(gac_ctx *ctx, const gac_chainset *cs,
+                            const gac_range *d_ranges, int64_t n, uint32_t flags,
+                            int64_t *d_global, int64_t *d_local, int32_t *d_ali,
+                            void *stream);
+
+/* ---- device memory helpers (for callers without their own allocator) ---- */
+int gac_dev_alloc(gac_ctx *ctx, size_t bytes, void **dptr);
+int gac_dev_free(gac_ctx *ctx, void *dptr);
+int gac_memcpy_h2d(gac_ctx *ctx, void *dst, const void *src, size_t bytes);
+int gac_memcpy_d2h(gac_ctx *ctx, void *dst, const void *src, size_t bytes);
+int gac_synchronize(gac_ctx *ctx);
+
+/* ---- kernel timing (HIP events on the launch stream) -------------------- */
+#define GAC_K_PLAN 0     /* per-range block-window search */
+#define GAC_K_TILE 1     /* tile scoring: bases, gaps, per-tile scan (dominant) */
+#define GAC_K_COMBINE 2  /* multi-tile range combine */
+#define GAC_K_COUNT 3
+/* Enable (1) / disable (0) event timing of each launch. */
+int gac_prof_enable(gac_ctx *ctx, int on);
+/* Synchronise, fold recorded events, and return total ms + launch count of
+ * kernel `k` since the last reset. */
+int gac_prof_read(gac_ctx *ctx, int k, double *total_ms, int64_t *launches);
+int gac_prof_reset(gac_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GACHAIN_H */

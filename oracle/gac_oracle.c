@@ -1,0 +1,405 @@
+/* oracle/gac_oracle.c -- CPU ORACLE: TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C restatement of the reference's chain-scoring hot path, used only
+ * by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the
+ * CHECKER.  The product (genomealignmenttools_amd/, libgachain.so) never
+ * links, loads or calls this file.
+ *
+ * Pinned against: the reference tools compiled from /root/reference by
+ * oracle/ref.mk (scoreChain / chainNet -rescore outputs on the committed
+ * fixtures in tests/golden/, and the reference's own gapCalc via
+ * oracle/_ref/libkentref.so), plus the axtChain known-answer chains of
+ * kent/src/hg/mouseStuff/axtChain/tests (see tests/test_oracle.py).
+ *
+ * Restated functions (reference file:line):
+ *   or_gap_*          gapCalcRead/interpolate/calcSlope/gapCalcCost
+ *                     kent/src/lib/gapCalc.c:82-110,146-222,298-331
+ *   or_block_score    chainScoreBlock  kent/src/lib/chainConnect.c:14-22
+ *   or_subchain       chainSubsetOnT   kent/src/lib/chain.c:471-558
+ *                     chainCalcScore   kent/src/lib/chainConnect.c:24-40
+ *                     chainCalcScoreLocal src/scoreChain/scoreChain.c:176-198
+ *                     chainBaseCountSubT  src/chainNet/chainNet.c:773-782
+ *   or_twobit_*       twoBitReadSeqFragExt (whole sequence, N runs -> 'n')
+ *                     kent/src/lib/twoBit.c:725-878
+ *   or_revcomp        reverseComplement kent/src/lib/dnautil.c:404-462
+ * Sequences are plain 1-byte-per-base text ("acgtn"), the matrix a 256x256
+ * int table like struct axtScoreScheme (kent/src/inc/axt.h:83-91).
+ */
+#include <ctype.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------- gap costs */
+typedef struct or_gap {
+    int small_size;
+    int *qs, *ts, *bs;
+    int long_count;
+    int *lpos;
+    double *ql, *tl, *bl;
+    int qlast, tlast, blast;
+    double qlastv, tlastv, blastv, qslope, tslope, bslope;
+} or_gap;
+
+static int or_interp(int x, const int *s, const double *v, int n) {
+    int i;
+    for (i = 0; i < n; ++i) {
+        if (x == s[i])
+            return v[i];
+        if (x < s[i]) {
+            int ds = s[i] - s[i - 1];
+            double dv = v[i] - v[i - 1];
+            return v[i - 1] + dv * (x - s[i - 1]) / ds;
+        }
+    }
+    {
+        int ds = s[n - 1] - s[n - 2];
+        double dv = v[n - 1] - v[n - 2];
+        return v[n - 2] + dv * (x - s[n - 2]) / ds;
+    }
+}
+
+static const char *or_loose =
+    "tablesize 11\nsmallSize 111\n"
+    "position 1 2 3 11 111 2111 12111 32111 72111 152111 252111\n"
+    "qGap 325 360 400 450 600 1100 3600 7600 15600 31600 56600\n"
+    "tGap 325 360 400 450 600 1100 3600 7600 15600 31600 56600\n"
+    "bothGap 625 660 700 750 900 1400 4000 8000 16000 32000 57000\n";
+static const char *or_medium =
+    "tableSize 11\nsmallSize 111\n"
+    "position 1 2 3 11 111 2111 12111 32111 72111 152111 252111\n"
+    "qGap 350 425 450 600 900 2900 22900 57900 117900 217900 317900\n"
+    "tGap 350 425 450 600 900 2900 22900 57900 117900 217900 317900\n"
+    "bothGap 750 825 850 1000 1300 3300 23300 58300 118300 218300 318300\n";
+
+/* next non-blank, non-'#' line's numbers after its tag */
+static int or_line_nums(char **cur, int count, double *out) {
+    while (**cur) {
+        char *line = *cur;
+        char *nl = strchr(line, '\n');
+        if (nl) {
+            *nl = 0;
+            *cur = nl + 1;
+        } else
+            *cur = line + strlen(line);
+        char *p = line;
+        while (*p && isspace((unsigned char)*p))
+            ++p;
+        if (*p == 0 || *p == '#')
+            continue;
+        while (*p && !isspace((unsigned char)*p))
+            ++p; /* tag */
+        int i;
+        for (i = 0; i < count; ++i) {
+            char *end;
+            out[i] = strtod(p, &end);
+            if (end == p)
+                return -1;
+            p = end;
+        }
+        return 0;
+    }
+    return -1;
+}
+
+void *or_gap_new(const char *name) {
+    char *text = NULL;
+    if (strcmp(name, "loose") == 0)
+        text = strdup(or_loose);
+    else if (strcmp(name, "medium") == 0)
+        text = strdup(or_medium);
+    else {
+        FILE *f = fopen(name, "rb");
+        if (!f)
+            return NULL;
+        fseek(f, 0, SEEK_END);
+        long n = ftell(f);
+        fseek(f, 0, SEEK_SET);
+        text = calloc(n + 1, 1);
+        if (fread(text, 1, n, f) != (size_t)n) {
+            fclose(f);
+            free(text);
+            return NULL;
+        }
+        fclose(f);
+    }
+    char *cur = text;
+    double tmp[1];
+    or_gap *g = calloc(1, sizeof(*g));
+    if (or_line_nums(&cur, 1, tmp))
+        goto bad;
+    int n = (int)tmp[0];
+    if (or_line_nums(&cur, 1, tmp))
+        goto bad;
+    g->small_size = (int)tmp[0];
+    double *pos = calloc(n, sizeof(double)), *q = calloc(n, sizeof(double)),
+           *t = calloc(n, sizeof(double)), *b = calloc(n, sizeof(double));
+    if (or_line_nums(&cur, n, pos) || or_line_nums(&cur, n, q) || or_line_nums(&cur, n, t) ||
+        or_line_nums(&cur, n, b))
+        goto bad;
+    int *ipos = calloc(n, sizeof(int)), i;
+    for (i = 0; i < n; ++i)
+        ipos[i] = (int)pos[i];
+    g->qs = calloc(g->small_size, sizeof(int));
+    g->ts = calloc(g->small_size, sizeof(int));
+    g->bs = calloc(g->small_size, sizeof(int));
+    for (i = 1; i < g->small_size; ++i) {
+        g->qs[i] = or_interp(i, ipos, q, n);
+        g->ts[i] = or_interp(i, ipos, t, n);
+        g->bs[i] = or_interp(i, ipos, b, n);
+    }
+    int sl = -1;
+    for (i = 0; i < n; ++i)
+        if (ipos[i] == g->small_size) {
+            sl = i;
+            break;
+        }
+    if (sl < 0)
+        goto bad;
+    g->long_count = n - sl;
+    g->lpos = ipos + sl;
+    g->ql = q + sl;
+    g->tl = t + sl;
+    g->bl = b + sl;
+    int lc = g->long_count;
+    g->qlast = g->tlast = g->blast = g->lpos[lc - 1];
+    g->qlastv = g->ql[lc - 1];
+    g->tlastv = g->tl[lc - 1];
+    g->blastv = g->bl[lc - 1];
+    g->qslope = (g->qlastv - g->ql[lc - 2]) / ((double)g->qlast - (double)g->lpos[lc - 2]);
+    g->tslope = (g->tlastv - g->tl[lc - 2]) / ((double)g->tlast - (double)g->lpos[lc - 2]);
+    g->bslope = (g->blastv - g->bl[lc - 2]) / ((double)g->blast - (double)g->lpos[lc - 2]);
+    free(text);
+    return g;
+bad:
+    free(text);
+    free(g);
+    return NULL;
+}
+
+int or_gap_cost(void *vg, int dq, int dt) {
+    or_gap *g = vg;
+    if (dt < 0)
+        dt = 0;
+    if (dq < 0)
+        dq = 0;
+    if (dt == 0) {
+        if (dq < g->small_size)
+            return g->qs[dq];
+        if (dq >= g->qlast)
+            return g->qlastv + g->qslope * (dq - g->qlast);
+        return or_interp(dq, g->lpos, g->ql, g->long_count);
+    }
+    if (dq == 0) {
+        if (dt < g->small_size)
+            return g->ts[dt];
+        if (dt >= g->tlast)
+            return g->tlastv + g->tslope * (dt - g->tlast);
+        return or_interp(dt, g->lpos, g->tl, g->long_count);
+    }
+    int both = dq + dt;
+    if (both < g->small_size)
+        return g->bs[both];
+    if (both >= g->blast)
+        return g->blastv + g->bslope * (both - g->blast);
+    return or_interp(both, g->lpos, g->bl, g->long_count);
+}
+
+void or_gap_costs(void *g, int n, const int *dq, const int *dt, int *out) {
+    int i;
+    for (i = 0; i < n; ++i)
+        out[i] = or_gap_cost(g, dq[i], dt[i]);
+}
+
+/* ----------------------------------------------------------- score matrix */
+/* mat16[i*4+j] = score(query base i, target base j), A,C,G,T order; both
+ * cases get the value, everything else (N) 0 -- propagateCase, axt.c:402-421 */
+typedef struct or_matrix {
+    int m[256][256];
+} or_matrix;
+
+void *or_matrix_new(const int *mat16) {
+    static const char lc[4] = {'a', 'c', 'g', 't'}, uc[4] = {'A', 'C', 'G', 'T'};
+    or_matrix *m = calloc(1, sizeof(*m));
+    int i, j;
+    for (i = 0; i < 4; ++i)
+        for (j = 0; j < 4; ++j) {
+            int v = mat16[i * 4 + j];
+            m->m[(int)lc[i]][(int)lc[j]] = v;
+            m->m[(int)uc[i]][(int)lc[j]] = v;
+            m->m[(int)lc[i]][(int)uc[j]] = v;
+            m->m[(int)uc[i]][(int)uc[j]] = v;
+        }
+    return m;
+}
+
+void or_free(void *p) { free(p); }
+
+static double or_block_score(const char *q, const char *t, int size, const or_matrix *m) {
+    double s = 0;
+    int i;
+    for (i = 0; i < size; ++i)
+        s += m->m[(unsigned char)q[i]][(unsigned char)t[i]];
+    return s;
+}
+
+/* -------------------------------------------------------------- scoring */
+/* Score chainSubsetOnT(chain, s, e): blocks bt/bq/bs (chain order, q in the
+ * chain's strand coordinates); qseq is the query sequence already in the
+ * chain's strand (reverse-complemented for '-').  Returns number of blocks kept. */
+int or_subchain(const char *tseq, const char *qseq, const int *bt, const int *bq,
+                const int *bs, int nb, int s, int e, const void *vm, void *g,
+                long long *glob, long long *loc, int *ali) {
+    const or_matrix *m = vm;
+    int k, first = -1;
+    for (k = 0; k < nb; ++k)
+        if (bt[k] + bs[k] > s) {
+            first = k;
+            break;
+        }
+    double score = 0, lscore = 0, lmax = 0;
+    int aliBases = 0, kept = 0;
+    int prevTe = 0, prevQe = 0;
+    for (k = first; k >= 0 && k < nb; ++k) {
+        int ts = bt[k], qs = bq[k], te = bt[k] + bs[k], qe = bq[k] + bs[k];
+        if (ts >= e)
+            break;
+        if (ts < s) {
+            qs += s - ts;
+            ts = s;
+        }
+        if (te > e) {
+            qe -= te - e;
+            te = e;
+        }
+        if (kept > 0) {
+            int gc = or_gap_cost(g, qs - prevQe, ts - prevTe);
+            score -= gc;
+            lscore -= gc;
+            if (lscore < 0)
+                lscore = 0;
+        }
+        double b = or_block_score(qseq + qs, tseq + ts, te - ts, m);
+        score += b;
+        lscore += b;
+        if (lscore > lmax)
+            lmax = lscore;
+        aliBases += te - ts;
+        prevTe = te;
+        prevQe = qe;
+        ++kept;
+    }
+    *glob = (long long)score;
+    *loc = (long long)lmax;
+    *ali = aliBases;
+    return kept;
+}
+
+/* ---------------------------------------------------------------- 2bit */
+typedef struct or_tb {
+    int n;
+    char **names;
+    int *sizes;
+    char **seqs;
+} or_tb;
+
+static uint32_t rd32(const unsigned char *p, int sw) {
+    uint32_t v;
+    memcpy(&v, p, 4);
+    return sw ? __builtin_bswap32(v) : v;
+}
+
+void *or_twobit_load(const char *path) {
+    FILE *f = fopen(path, "rb");
+    if (!f)
+        return NULL;
+    fseek(f, 0, SEEK_END);
+    long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    unsigned char *d = malloc(n);
+    if (fread(d, 1, n, f) != (size_t)n) {
+        fclose(f);
+        free(d);
+        return NULL;
+    }
+    fclose(f);
+    uint32_t sig;
+    memcpy(&sig, d, 4);
+    int sw = (sig == 0x4327411Au);
+    if (!sw && sig != 0x1A412743u) {
+        free(d);
+        return NULL;
+    }
+    uint32_t ver = rd32(d + 4, sw), cnt = rd32(d + 8, sw);
+    or_tb *tb = calloc(1, sizeof(*tb));
+    tb->n = cnt;
+    tb->names = calloc(cnt, sizeof(char *));
+    tb->sizes = calloc(cnt, sizeof(int));
+    tb->seqs = calloc(cnt, sizeof(char *));
+    static const char nt[4] = {'t', 'c', 'a', 'g'};
+    size_t off = 16;
+    uint32_t i, k;
+    for (i = 0; i < cnt; ++i) {
+        int nl = d[off++];
+        tb->names[i] = strndup((char *)d + off, nl);
+        off += nl;
+        uint64_t so;
+        if (ver == 1) {
+            uint64_t v;
+            memcpy(&v, d + off, 8);
+            so = sw ? __builtin_bswap64(v) : v;
+            off += 8;
+        } else {
+            so = rd32(d + off, sw);
+            off += 4;
+        }
+        size_t p = so;
+        uint32_t size = rd32(d + p, sw);
+        p += 4;
+        uint32_t nc = rd32(d + p, sw);
+        p += 4;
+        const unsigned char *ns = d + p, *nz = d + p + 4ull * nc;
+        p += 8ull * nc;
+        uint32_t mc = rd32(d + p, sw);
+        p += 4 + 8ull * mc + 4;
+        char *s = malloc(size + 1);
+        for (k = 0; k < size; ++k)
+            s[k] = nt[(d[p + k / 4] >> (6 - 2 * (k % 4))) & 3];
+        s[size] = 0;
+        for (k = 0; k < nc; ++k) {
+            uint32_t st = rd32(ns + 4 * k, sw), sz = rd32(nz + 4 * k, sw), j;
+            for (j = st; j < st + sz && j < size; ++j)
+                s[j] = 'n';
+        }
+        tb->sizes[i] = size;
+        tb->seqs[i] = s;
+    }
+    free(d);
+    return tb;
+}
+
+int or_twobit_count(void *v) { return ((or_tb *)v)->n; }
+const char *or_twobit_name(void *v, int i) { return ((or_tb *)v)->names[i]; }
+int or_twobit_size(void *v, int i) { return ((or_tb *)v)->sizes[i]; }
+const char *or_twobit_seq(void *v, int i) { return ((or_tb *)v)->seqs[i]; }
+
+/* ntCompTable semantics for acgtn (dnautil.c:404-462) */
+void or_revcomp(const char *in, int n, char *out) {
+    int i;
+    for (i = 0; i < n; ++i) {
+        char c = in[n - 1 - i], r;
+        switch (c) {
+        case 'a': r = 't'; break;
+        case 'c': r = 'g'; break;
+        case 'g': r = 'c'; break;
+        case 't': r = 'a'; break;
+        case 'A': r = 'T'; break;
+        case 'C': r = 'G'; break;
+        case 'G': r = 'C'; break;
+        case 'T': r = 'A'; break;
+        default: r = c; break;
+        }
+        out[i] = r;
+    }
+}

@@ -1,0 +1,158 @@
+"""GPU parity: libgachain (HIP, gfx950) vs the CPU oracle on the same seeded
+inputs.  Integer scores must be bit-exact (the reference accumulates integer
+addends in double; see include/gachain.h)."""
+import numpy as np
+import pytest
+
+from conftest import BLASTZ
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(engine_factory, tg, qg, ca, mat=BLASTZ, gap="loose"):
+    from genomealignmenttools_amd.gachain import GAC_Q, GAC_T, Engine, GapCosts
+    e = Engine(0)
+    e.add_sequences(GAC_T, tg.seq_records())
+    e.add_sequences(GAC_Q, qg.seq_records())
+    e.set_scoring(np.asarray(mat, np.int32), GapCosts(gap))
+    cs = e.upload_chains(ca)
+    return e, cs
+
+
+def _oracle(tg, qg, mat=BLASTZ, gap="loose"):
+    from oracle.oracle import OracleScorer, genome_text
+    return OracleScorer(genome_text(tg), genome_text(qg), mat, gap)
+
+
+def _ranges(ca, rng, per_chain=3):
+    R = []
+    for c in range(ca.n):
+        R.append((c, ca.tstart[c], ca.tend[c]))
+        for _ in range(per_chain):
+            a, b = sorted(rng.integers(ca.tstart[c] - 50, ca.tend[c] + 50, 2))
+            if a < b:
+                R.append((c, a, b))
+    return np.asarray(R, np.int64)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_ranges_vs_oracle(seed):
+    from genomealignmenttools_amd import synth
+    tg, qg, ca = synth.small_case(seed=seed, n_chains=400, max_blocks=600)
+    e, cs = _setup(None, tg, qg, ca)
+    R = _ranges(ca, np.random.default_rng(seed))
+    g, l, a = e.score_ranges(cs, R, want_local=True)
+    og, ol, oa = _oracle(tg, qg).score_ranges(ca, R)
+    assert np.array_equal(g, og)
+    assert np.array_equal(l, ol)
+    assert np.array_equal(a, oa)
+
+
+def test_long_chains_multi_tile():
+    """Chains of thousands of blocks: ranges span many 64-block tiles."""
+    from genomealignmenttools_amd import synth
+    tg = synth.random_genome({"chrT1": 3_000_000}, 11, n_frac=0.01, n_mean=300)
+    qg = synth.random_genome({"q1": 2_000_000, "q2": 1_500_000}, 12, n_frac=0.01, n_mean=300)
+    cfg = synth.SynthConfig(n_chains=60, alpha=1.1, max_blocks=20_000, seed=5)
+    ca = synth.make_chains(tg, "chrT1", qg, cfg)
+    assert ca.blk_off[1:].max() > 0
+    e, cs = _setup(None, tg, qg, ca)
+    R = _ranges(ca, np.random.default_rng(9), per_chain=6)
+    g, l, a = e.score_ranges(cs, R, want_local=True)
+    og, ol, oa = _oracle(tg, qg).score_ranges(ca, R)
+    assert int(np.diff(ca.blk_off).max()) > 64 * 10
+    assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
+
+
+def test_edge_ranges():
+    """Empty windows, single-base windows, ranges ending inside blocks,
+    1-bp blocks, ranges beyond the chain."""
+    from genomealignmenttools_amd import synth
+    from genomealignmenttools_amd.chainfile import ChainArrays
+    tg = synth.random_genome({"t": 5000}, 3, n_frac=0.02, n_mean=20)
+    qg = synth.random_genome({"q": 6000}, 4, n_frac=0.02, n_mean=20)
+    # hand-made chains: 1-bp blocks, zero gaps on one side, both strands
+    blocks = [
+        [(10, 20, 1), (11, 22, 1), (40, 30, 5), (45, 35, 100), (200, 300, 1)],
+        [(0, 0, 4999)],
+        [(100, 5, 33), (133, 38, 31), (170, 70, 65), (300, 100, 64), (400, 200, 129)],
+    ]
+    offs, bt, bq, bs = [0], [], [], []
+    for bl in blocks:
+        for t, q, s in bl:
+            bt.append(t), bq.append(q), bs.append(s)
+        offs.append(len(bs))
+    n = len(blocks)
+    ts = [bl[0][0] for bl in blocks]
+    te = [bl[-1][0] + bl[-1][2] for bl in blocks]
+    qs = [bl[0][1] for bl in blocks]
+    qe = [bl[-1][1] + bl[-1][2] for bl in blocks]
+    mk = lambda: None
+    ca = ChainArrays(score=np.zeros(n), tname=["t"] * n, tsize=np.full(n, 5000, np.int32),
+                     tstart=np.asarray(ts, np.int32), tend=np.asarray(te, np.int32),
+                     qname=["q"] * n, qsize=np.full(n, 6000, np.int32),
+                     qstrand=np.asarray([0, 1, 1], np.uint8), qstart=np.asarray(qs, np.int32),
+                     qend=np.asarray(qe, np.int32), id=np.arange(1, n + 1),
+                     blk_off=np.asarray(offs, np.int64), blk_t=np.asarray(bt, np.int32),
+                     blk_q=np.asarray(bq, np.int32), blk_size=np.asarray(bs, np.int32))
+    e, cs = _setup(None, tg, qg, ca)
+    R = []
+    for c in range(n):
+        lo, hi = int(ts[c]), int(te[c])
+        for s in range(lo - 3, hi + 3, max(1, (hi - lo) // 25)):
+            for d in (1, 2, 7, 33, 64, 65, 500):
+                R.append((c, s, s + d))
+        R.append((c, lo, hi))
+        R.append((c, hi, hi + 10))   # empty window after
+        R.append((c, 0, lo))         # empty window before
+    R = np.asarray(R, np.int64)
+    g, l, a = e.score_ranges(cs, R, want_local=True)
+    og, ol, oa = _oracle(tg, qg).score_ranges(ca, R)
+    assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
+
+
+@pytest.mark.parametrize("gap", ["loose", "medium"])
+def test_gap_costs_exhaustive(gap):
+    """All-N genomes score every block 0, so a 2-block chain scores exactly
+    -gapCalcCost(dq, dt): checks the device gap path (small tables, f64
+    interpolation, huge-gap slope) against the oracle for ~300k gap shapes."""
+    from genomealignmenttools_amd import synth
+    from genomealignmenttools_amd.chainfile import ChainArrays
+    from oracle.oracle import OracleGap
+    T = 60_000_000
+    tg = synth.Genome(["t"], [np.zeros(T, np.uint8)], [(np.array([0], np.int32), np.array([T], np.int32))])
+    qg = synth.Genome(["q"], [np.zeros(T, np.uint8)], [(np.array([0], np.int32), np.array([T], np.int32))])
+    rng = np.random.default_rng(7)
+    d = np.arange(0, 120_000)
+    big = rng.integers(1, 29_000_000, 60_000)
+    dq = np.concatenate([d, np.zeros_like(d), d // 2, big, rng.integers(0, 3, 60_000) * big // 3])
+    dt = np.concatenate([np.zeros_like(d), d, d - d // 2, rng.integers(0, 2, 60_000) * big // 2, big])
+    keep = (dq + dt) > 0
+    dq, dt = dq[keep], dt[keep]
+    n = len(dq)
+    bt = np.stack([np.zeros(n), 1 + dt], 1).reshape(-1).astype(np.int32)
+    bq = np.stack([np.zeros(n), 1 + dq], 1).reshape(-1).astype(np.int32)
+    bs = np.ones(2 * n, np.int32)
+    ca = ChainArrays(score=np.zeros(n), tname=["t"] * n, tsize=np.full(n, T, np.int32),
+                     tstart=np.zeros(n, np.int32), tend=(2 + dt).astype(np.int32),
+                     qname=["q"] * n, qsize=np.full(n, T, np.int32),
+                     qstrand=np.zeros(n, np.uint8), qstart=np.zeros(n, np.int32),
+                     qend=(2 + dq).astype(np.int32), id=np.arange(1, n + 1),
+                     blk_off=np.arange(0, 2 * n + 1, 2, dtype=np.int64), blk_t=bt, blk_q=bq,
+                     blk_size=bs)
+    e, cs = _setup(None, tg, qg, ca, gap=gap)
+    g, _, a = e.score_ranges(cs, e.full_ranges(ca))
+    want = -OracleGap(gap).costs(dq, dt).astype(np.int64)
+    assert np.array_equal(a, np.full(n, 2))
+    bad = np.nonzero(g != want)[0]
+    assert len(bad) == 0, (dq[bad[:5]], dt[bad[:5]], g[bad[:5]], want[bad[:5]])
+
+
+def test_genome_roundtrip():
+    from genomealignmenttools_amd import synth
+    from genomealignmenttools_amd.gachain import GAC_T, Engine
+    tg = synth.random_genome({"a": 1001, "b": 64, "c": 33, "d": 5}, 5, n_frac=0.05, n_mean=10)
+    e = Engine(0)
+    e.add_sequences(GAC_T, tg.seq_records())
+    for i, n in enumerate(tg.names):
+        assert e.decode(GAC_T, e.seq_index(GAC_T, n), 0, len(tg.codes[i])) == tg.text(i)
