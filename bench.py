@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""bench.py -- aligned Gbases scored/sec, chainNet -rescore (BASELINE.json).
+
+Workload (synthetic, seeded): target = hg38 chr1
+(248,956,422 bp), query = all 66 mm10 sequences (2.73 Gb), ~2e5 planted
+chains (power-law blocks/chain, geometric 40-bp blocks, 12% substitutions,
+50% '-' strand, 20% short spurious chains), netted on the host by the
+product's chainNet engine.  One step = the GPU rescoring of every partial
+T-net fill (chainNet -rescore's subchainInfo -> chainSubsetOnT +
+chainCalcScore, src/chainNet/chainNet.c:795-843) with genomes, chains and
+the fill list already resident in HBM.  value = aligned bases of the
+rescored fills (all ranks) / max-over-ranks wall time.
+
+N>1: one process per GPU; every rank nets and rescores its own independent
+C2 set (seed + rank): chains shard by independent chain set, there is no
+data-path collective (scaling "weak").  torch.distributed (RCCL) is used for
+the barrier and the max-over-ranks timing only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BLASTZ = np.array([[91, -114, -31, -123], [-114, 100, -125, -31], [-31, -125, 100, -114],
+                   [-123, -31, -114, 91]], np.int32)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--chains", type=int, default=200_000)
+    p.add_argument("--seed", type=int, default=42)
+    p.add_argument("--workload", choices=["rescore", "scorechain"], default="rescore")
+    p.add_argument("--cpu-seconds", type=float, default=15.0,
+                   help="target CPU seconds for the cpu_baseline sample")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--tmp", default=os.environ.get("TMPDIR", "/tmp"))
+    return p.parse_args()
+
+
+def make_workload(args, rank):
+    from genomealignmenttools_amd import synth
+    t0 = time.time()
+    tg, qg, ca = synth.c2_case(seed=args.seed + rank, n_chains=args.chains)
+    log(f"[rank {rank}] synthetic C2: {ca.n} chains, {len(ca.blk_size)} blocks, "
+        f"{ca.aligned_bases() / 1e6:.1f} M aligned bases ({time.time() - t0:.1f}s)")
+    if args.workload == "scorechain":
+        ranges = np.stack([np.arange(ca.n, dtype=np.int32), ca.tstart, ca.tend], 1)
+        info = {"netted_chains": ca.n}
+    else:
+        from genomealignmenttools_amd.chainnet import net_fills
+        t1 = time.time()
+        fills = net_fills(ca, tg.sizes, qg.sizes, min_score=0.0)
+        part = fills["partial"]
+        ranges = np.stack([fills["chain"][part], fills["start"][part], fills["end"][part]], 1)
+        info = {"netted_chains": int(fills["netted_chains"]), "tnet_fills": int(len(part)),
+                "partial_fills": int(part.sum())}
+        log(f"[rank {rank}] host netting: {info} ({time.time() - t1:.1f}s)")
+    return tg, qg, ca, np.ascontiguousarray(ranges, np.int32), info
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device(f"cuda:{local}"))
+
+    from genomealignmenttools_amd._lib import GAC_K_TILE
+    from genomealignmenttools_amd.gachain import GAC_Q, GAC_T, Engine, GapCosts
+
+    tg, qg, ca, ranges, info = make_workload(args, rank)
+    e = Engine(local)
+    t0 = time.time()
+    e.add_sequences(GAC_T, tg.seq_records())
+    e.add_sequences(GAC_Q, qg.seq_records())
+    e.set_scoring(BLASTZ, GapCosts("loose"))
+    cs = e.upload_chains(ca)
+    n = len(ranges)
+    d_r = e.dev_alloc(ranges.nbytes)
+    e.h2d(d_r, ranges)
+    d_g = e.dev_alloc(8 * n)
+    d_a = e.dev_alloc(4 * n)
+    log(f"[rank {rank}] upload {time.time() - t0:.1f}s; {n} ranges")
+
+    # bytes/blocks of the scored windows (for the roofline) from one host pass
+    ali = np.zeros(n, np.int32)
+    e.score_ranges_device(cs, d_r, n, d_g, d_a)
+    e.synchronize()
+    e.d2h(ali, d_a)
+    bases = int(ali.sum(dtype=np.int64))
+    nblk = _window_blocks(ca, ranges)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        e.score_ranges_device(cs, d_r, n, d_g, d_a)
+    e.synchronize()
+    e.prof_reset()
+    e.prof_enable(True)
+    barrier()
+    e.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        e.score_ranges_device(cs, d_r, n, d_g, d_a)
+    e.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    e.prof_enable(False)
+    tile_ms, tile_n = e.prof_read(GAC_K_TILE)
+    step_s = dt / args.steps
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt, float(bases)], dtype=torch.float64, device=f"cuda:{local}")
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = t.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        dt_max = float(mx[0])
+        total_bases = float(sm[1])
+    else:
+        dt_max, total_bases = dt, float(bases)
+
+    # roofline of the dominant kernel (k_tile): algorithmic bytes per launch
+    # = 0.75 B/base (t+q 2-bit + t+q N-mask bits) + 12 B/block + 44 B/range
+    algo_bytes = 0.75 * bases + 12.0 * nblk + 44.0 * n
+    tile_avg_s = (tile_ms / 1e3) / max(tile_n, 1)
+    achieved = algo_bytes / tile_avg_s / 1e9
+    out = {
+        "metric": "aligned Gbases scored/sec, chainNet -rescore hg38-mm10, 1/2/4/8 MI355X",
+        "value": total_bases * args.steps / dt_max / 1e9,
+        "unit": "Gbases/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt_max / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (seeded C2: hg38 chr1 x mm10 sizes, planted chains; no real genomes)",
+        "config": {
+            "workload": ("chainNet -rescore T-net partial-fill rescoring" if args.workload == "rescore"
+                         else "scoreChain full-chain global+local"),
+            "chains": ca.n, "blocks": int(len(ca.blk_size)),
+            "chain_aligned_bases": ca.aligned_bases(),
+            "ranges_per_gpu": n, "scored_bases_per_gpu": bases, "scored_blocks_per_gpu": nblk,
+            "parallelism": f"chain-set shard x{world}", **info,
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "kernel": "k_tile", "kernel_avg_ms": tile_avg_s * 1e3,
+            "algo_bytes_per_launch": algo_bytes,
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(args, tg, qg, ca, ranges, ali)
+        except Exception as ex:  # reported, never fatal
+            out["cpu_baseline"] = {"error": str(ex)[:300]}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def _window_blocks(ca, ranges):
+    """Blocks selected by each range (host binary search, for the byte model)."""
+    tot = 0
+    for c, s, e in ranges:
+        bt, _, bs = ca.blocks(int(c))
+        lo = np.searchsorted(bt + bs, s, side="right")
+        hi = np.searchsorted(bt, e, side="left")
+        tot += max(0, int(hi - lo))
+    return tot
+
+
+def cpu_baseline(args, tg, qg, ca, ranges, ali):
+    """Reference CPU timing: oracle/_ref/kentref (the reference's own kent
+    chainSubsetOnT + chainCalcScore, as chainNet -rescore runs them per fill)
+    on a bounded random sample of the same fills, one core."""
+    from genomealignmenttools_amd import chainfile, synth
+    from oracle.oracle import KentRef, have_ref
+    if not have_ref():
+        return {"error": "oracle/_ref/kentref not built"}
+    import tempfile
+    d = tempfile.mkdtemp(dir=args.tmp)
+    t0 = time.time()
+    rng = np.random.default_rng(0)
+    order = rng.permutation(len(ranges))
+    frac0 = min(1.0, 4000 / max(len(ranges), 1))
+    def run(frac):
+        sel = np.sort(order[: max(1, int(len(ranges) * frac))])
+        chains = np.unique(ranges[sel, 0])
+        sub = ca.subset(chains)
+        remap = {int(c): i for i, c in enumerate(chains)}
+        r = np.array([(remap[int(c)], s, e) for c, s, e in ranges[sel]], np.int32)
+        cf = os.path.join(d, "s.chain")
+        chainfile.write_chains(sub, cf)
+        kr = KentRef(cf, os.path.join(d, "t.2bit"), os.path.join(d, "q.2bit"), None, "loose")
+        kr.rescore_fills(r)
+        return kr.last_seconds, int(ali[sel].sum(dtype=np.int64)), len(sel)
+    synth.write_2bit(tg, os.path.join(d, "t.2bit"))
+    synth.write_2bit(qg, os.path.join(d, "q.2bit"))
+    sec, b, k = run(frac0)
+    frac = frac0
+    if sec < args.cpu_seconds * 0.5 and frac0 < 1.0:
+        frac = min(1.0, frac0 * args.cpu_seconds / max(sec, 1e-3))
+        sec, b, k = run(frac)
+    import shutil
+    shutil.rmtree(d, ignore_errors=True)
+    log(f"cpu baseline: {k} fills, {b} bases, {sec:.2f}s ({time.time() - t0:.0f}s wall)")
+    return {"value": b / sec / 1e9, "unit": "Gbases/s", "cores": 1, "kind": "reference",
+            "sample": f"{k} of {len(ranges)} partial T-net fills (random, seed 0), {b} aligned "
+                      f"bases, {sec:.2f}s in kent chainSubsetOnT+chainCalcScore+base counts"}
+
+
+if __name__ == "__main__":
+    main()

@@ -71,6 +71,24 @@ class ChainsetDesc(C.Structure):
     ]
 
 
+class NetInput(C.Structure):
+    _fields_ = [
+        ("n_chains", C.c_int64),
+        ("score", C.c_void_p), ("id", C.c_void_p), ("t_seq", C.c_void_p),
+        ("q_seq", C.c_void_p), ("q_strand", C.c_void_p),
+        ("t_start", C.c_void_p), ("t_end", C.c_void_p), ("q_start", C.c_void_p),
+        ("q_end", C.c_void_p), ("blk_off", C.c_void_p), ("blk_t", C.c_void_p),
+        ("blk_q", C.c_void_p), ("blk_size", C.c_void_p),
+        ("n_tseq", C.c_int32), ("t_names", C.c_void_p), ("t_sizes", C.c_void_p),
+        ("n_qseq", C.c_int32), ("q_names", C.c_void_p), ("q_sizes", C.c_void_p),
+    ]
+
+
+class NetOpts(C.Structure):
+    _fields_ = [("min_space", C.c_int32), ("min_fill", C.c_int32), ("min_score", C.c_double),
+                ("incl_hap", C.c_int32)]
+
+
 # name -> (restype, argtypes)
 _PROTOS = {
     "gac_abi_version": (C.c_int, []),
@@ -112,6 +130,14 @@ _PROTOS = {
         [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_uint32, C.c_void_p, C.c_void_p,
          C.c_void_p, C.c_void_p],
     ),
+    "gac_net_build": (C.c_int, [C.POINTER(NetInput), C.POINTER(NetOpts), C.POINTER(C.c_void_p)]),
+    "gac_net_free": (None, [C.c_void_p]),
+    "gac_net_netted": (C.c_int64, [C.c_void_p]),
+    "gac_net_fill_count": (C.c_int64, [C.c_void_p, C.c_int]),
+    "gac_net_get_fills": (
+        C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "gac_net_write": (
+        C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_char_p, C.c_void_p, C.c_int32]),
     "gac_dev_alloc": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
     "gac_dev_free": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gac_memcpy_h2d": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),

@@ -19,9 +19,8 @@
 
 namespace gac {
 size_t scan_temp_bytes(int64_t n);
-hipError_t launch_plan(const ScoreArgs &a, hipStream_t s);
-hipError_t launch_scan_total(const ScoreArgs &a, void *temp, size_t temp_bytes, hipStream_t s);
-hipError_t launch_scatter(const ScoreArgs &a, hipStream_t s);
+hipError_t launch_plan(const ScoreArgs &a, void *temp, size_t temp_bytes, hipStream_t s);
+hipError_t launch_mark(const ScoreArgs &a, hipStream_t s);
 hipError_t launch_tile(const ScoreArgs &a, int grid, hipStream_t s);
 hipError_t launch_combine(const ScoreArgs &a, int grid, hipStream_t s);
 struct SeqDev {
@@ -89,11 +88,11 @@ struct gac_ctx {
     int small_in_lds = 0;
     // workspace
     int64_t ws_n = 0;
-    int64_t *plan_b0 = nullptr;
-    int32_t *plan_n = nullptr, *ntiles = nullptr, *tile_off = nullptr, *total_tiles = nullptr;
+    RangeDesc *rdesc = nullptr;
+    int32_t *nblk = nullptr, *goff = nullptr, *total = nullptr;
     int64_t ws_tiles = 0;
-    int32_t *tile_q = nullptr;
-    TileSum *tsum = nullptr;
+    int32_t *tile_r0 = nullptr;
+    SegSum *sum_head = nullptr, *sum_tail = nullptr;
     void *scan_tmp = nullptr;
     size_t scan_bytes = 0;
     // staging for the host API
@@ -171,9 +170,9 @@ extern "C" void gac_close(gac_ctx *c) {
     hipStreamSynchronize(c->stream);
     free_genome(c->g[0]);
     free_genome(c->g[1]);
-    void *bufs[] = {c->d_small, c->plan_b0, c->plan_n,  c->ntiles, c->tile_off, c->total_tiles,
-                    c->tile_q,  c->tsum,    c->scan_tmp, c->d_ranges, c->d_g,   c->d_l,
-                    c->d_ali};
+    void *bufs[] = {c->d_small, c->rdesc,    c->nblk,     c->goff,     c->total,
+                    c->tile_r0, c->sum_head, c->sum_tail, c->scan_tmp, c->d_ranges,
+                    c->d_g,     c->d_l,      c->d_ali};
     for (void *p : bufs)
         if (p) hipFree(p);
     for (auto &p : c->prof_pending) {
@@ -499,29 +498,30 @@ extern "C" int64_t gac_chains_block_count(const gac_chainset *cs) { return cs ? 
 static int ensure_ws(gac_ctx *c, int64_t n, int64_t max_tiles) {
     if (n > c->ws_n) {
         int64_t cap = n + n / 2 + 1024;
-        void *bufs[] = {c->plan_b0, c->plan_n, c->ntiles, c->tile_off, c->total_tiles, c->scan_tmp};
+        void *bufs[] = {c->rdesc, c->nblk, c->goff, c->total, c->scan_tmp};
         for (void *p : bufs)
             if (p) hipFree(p);
-        c->plan_b0 = nullptr;
-        c->plan_n = c->ntiles = c->tile_off = c->total_tiles = nullptr;
+        c->rdesc = nullptr;
+        c->nblk = c->goff = c->total = nullptr;
         c->scan_tmp = nullptr;
-        HIPCHK(hipMalloc(&c->plan_b0, cap * 8));
-        HIPCHK(hipMalloc(&c->plan_n, cap * 4));
-        HIPCHK(hipMalloc(&c->ntiles, cap * 4));
-        HIPCHK(hipMalloc(&c->tile_off, cap * 4));
-        HIPCHK(hipMalloc(&c->total_tiles, 16));
+        HIPCHK(hipMalloc(&c->rdesc, cap * sizeof(RangeDesc)));
+        HIPCHK(hipMalloc(&c->nblk, cap * 4));
+        HIPCHK(hipMalloc(&c->goff, (cap + 1) * 4));
+        HIPCHK(hipMalloc(&c->total, 16));
         c->scan_bytes = scan_temp_bytes(cap);
         HIPCHK(hipMalloc(&c->scan_tmp, c->scan_bytes ? c->scan_bytes : 16));
         c->ws_n = cap;
     }
     if (max_tiles > c->ws_tiles) {
         int64_t cap = max_tiles + max_tiles / 4 + 1024;
-        if (c->tile_q) hipFree(c->tile_q);
-        if (c->tsum) hipFree(c->tsum);
-        c->tile_q = nullptr;
-        c->tsum = nullptr;
-        HIPCHK(hipMalloc(&c->tile_q, cap * 4));
-        HIPCHK(hipMalloc(&c->tsum, cap * sizeof(TileSum)));
+        if (c->tile_r0) hipFree(c->tile_r0);
+        if (c->sum_head) hipFree(c->sum_head);
+        if (c->sum_tail) hipFree(c->sum_tail);
+        c->tile_r0 = nullptr;
+        c->sum_head = c->sum_tail = nullptr;
+        HIPCHK(hipMalloc(&c->tile_r0, cap * 4));
+        HIPCHK(hipMalloc(&c->sum_head, cap * sizeof(SegSum)));
+        HIPCHK(hipMalloc(&c->sum_tail, cap * sizeof(SegSum)));
         c->ws_tiles = cap;
     }
     return GAC_OK;
@@ -577,13 +577,10 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
     a.bs = cs->bs;
     a.ranges = d_ranges;
     a.n = n;
-    a.plan_b0 = c->plan_b0;
-    a.plan_n = c->plan_n;
-    a.ntiles = c->ntiles;
-    a.tile_off = c->tile_off;
-    a.tile_q = c->tile_q;
-    a.total_tiles = c->total_tiles;
-    a.tsum = c->tsum;
+    a.rdesc = c->rdesc;
+    a.nblk = c->nblk;
+    a.goff = c->goff;
+    a.total = c->total;
     a.out_g = d_g;
     a.out_l = d_l;
     a.out_ali = d_ali;
@@ -594,21 +591,24 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
     a.gap = c->gap;
     {
         PROF_BEGIN(GAC_K_PLAN);
-        HIPCHK(launch_plan(a, s));
-        HIPCHK(launch_scan_total(a, c->scan_tmp, c->scan_bytes, s));
+        HIPCHK(launch_plan(a, c->scan_tmp, c->scan_bytes, s));
         PROF_END(GAC_K_PLAN);
     }
-    // tiles are only known after the scan: read the 4-byte total back so the
-    // tile workspace is always large enough (ranges may overlap arbitrarily).
-    HIPCHK(hipMemcpyAsync(c->h_total, c->total_tiles, 4, hipMemcpyDeviceToHost, s));
+    // the flat block count W is only known after the scan: read {W, T} back
+    // (8 bytes) so the tile workspace always fits (ranges may overlap).
+    HIPCHK(hipMemcpyAsync(c->h_total, c->total, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    const int64_t total = *c->h_total;
-    rc = ensure_ws(c, n, total);
+    const int64_t W = c->h_total[0], NT = c->h_total[1];
+    if (W < 0) return gac_fail(GAC_E_ARG, "window block total overflows int32");
+    if (NT == 0) return GAC_OK;
+    rc = ensure_ws(c, n, NT);
     if (rc != GAC_OK) return rc;
-    a.tile_q = c->tile_q;
-    a.tsum = c->tsum;
-    if (total == 0) return GAC_OK;
-    HIPCHK(launch_scatter(a, s));
+    a.tile_r0 = c->tile_r0;
+    a.sum_head = c->sum_head;
+    a.sum_tail = c->sum_tail;
+    a.n_tiles = (int32_t)NT;
+    a.n_flat = (int32_t)W;
+    HIPCHK(launch_mark(a, s));
     {
         PROF_BEGIN(GAC_K_TILE);
         HIPCHK(launch_tile(a, c->tile_grid, s));

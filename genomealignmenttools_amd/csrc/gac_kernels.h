@@ -43,11 +43,22 @@ struct GapDev {
     double long_val[3][kMaxLong];
 };
 
-// Per-tile partial result: additive parts + the local-score max-plus element
-//   s_out = max(s_in + A, B);  m_out = max(m_in, s_in + C, D)
-struct TileSum {
-    long long g;   // sum(block) - sum(gap)
-    long long ali; // aligned bases
+// Per-range descriptor written by k_plan (one load per lane in k_tile).
+struct RangeDesc {
+    int64_t b0;      // first block of the window (global block index)
+    int64_t twoff;   // first genome word of the target sequence
+    int64_t qwoff;   // first genome word of the query sequence
+    int32_t nblk;    // blocks in the window
+    int32_t s, e;    // target clip range
+    int32_t qinfo;   // query sequence size | (strand << 31)
+};
+static_assert(sizeof(RangeDesc) == 40, "RangeDesc layout");
+
+// Partial result of a range segment inside one tile: additive parts + the
+// local-score max-plus element  s_out = max(s_in + A, B); m_out = max(m_in, s_in + C, D)
+struct SegSum {
+    long long g;    // sum(block) - sum(gap)
+    long long ali;  // aligned bases
     long long A, B, C, D;
 };
 
@@ -68,13 +79,15 @@ struct ScoreArgs {
     const Range *ranges;
     int64_t n;
     // workspace
-    int64_t *plan_b0;
-    int32_t *plan_n;
-    int32_t *ntiles;
-    int32_t *tile_off;
-    int32_t *tile_q;
-    int32_t *total_tiles;
-    TileSum *tsum;
+    RangeDesc *rdesc;    // [n]
+    int32_t *nblk;       // [n]   window blocks per range
+    int32_t *goff;       // [n+1] exclusive scan of nblk (flat block offset)
+    int32_t *tile_r0;    // [T]   range owning the tile's first flat block
+    SegSum *sum_head;    // [T]   partial segment containing the tile's first block
+    SegSum *sum_tail;    // [T]   partial segment containing the tile's last block
+    int32_t *total;      // [2]   W (flat blocks), T (tiles)
+    int32_t n_tiles;     // host copy of T (grid sizing / bounds)
+    int32_t n_flat;      // host copy of W
     // outputs
     long long *out_g;
     long long *out_l;

@@ -6,17 +6,20 @@
 //   chainScoreBlock  kent/src/lib/chainConnect.c:14-22  sum matrix[q][t] per base
 //   gapCalcCost      kent/src/lib/gapCalc.c:298-331      piecewise-linear gap cost
 //   chainCalcScoreLocal src/scoreChain/scoreChain.c:176-198  max-plus local score
-// Here one launch scores a whole batch of sub-chains:
+// Here one batch of sub-chains ("ranges") is scored by:
 //   k_plan    one lane per range: binary-search the block window (replaces
 //             the O(blocks) list walks of chainSubsetOnT / chainBaseCountSubT)
-//   (scan)    hipcub exclusive sum of tiles per range
-//   k_scatter tile -> range map
-//   k_tile    one wave per tile of <= 64 blocks: lanes score 32-base chunks of
+//             and write a 40-byte range descriptor
+//   (scan)    hipcub exclusive sum of window blocks -> flat block offsets
+//   k_mark    tile -> range owning its first flat block
+//   k_tile    one wave per tile of 64 consecutive flat blocks (ranges packed
+//             densely, many ranges per tile): lanes score 32-base chunks of
 //             2-bit packed T and Q straight from HBM (bit-plane popcounts, the
 //             4x4 matrix in SGPRs), LDS atomics fold chunks into blocks, lanes
-//             evaluate gapCalcCost in exact f64, and an ordered wave reduction
-//             folds the tile's max-plus local-score element
-//   k_combine one wave per range spanning > 1 tile: ordered fold of tiles
+//             evaluate gapCalcCost in exact f64, and segmented (by range)
+//             wave scans fold sums and the max-plus local-score element;
+//             ranges complete inside the tile are written directly
+//   k_combine ranges spanning > 1 tile: ordered fold of tile segments
 // All sums are int64: every addend of the reference's double accumulation is
 // an integer, so integer arithmetic is exact and bit-identical.
 #include <hip/hip_runtime.h>
@@ -139,66 +142,134 @@ __device__ __forceinline__ long long wave_sum(long long v) {
 }
 
 // ------------------------------------------------------------ k_plan -----
-// One lane per range: window of blocks [b0, b0+n) with tEnd > s and tStart < e.
+// One lane per range: window of blocks [b0, b0+n) with tEnd > s and tStart < e
+// (chainSubsetOnT's first-block walk and stop condition, chain.c:481-500),
+// plus the per-range descriptor the tile kernel needs.
 __global__ void __launch_bounds__(256) k_plan(ScoreArgs a) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
     const Range r = a.ranges[i];
-    int n = 0;
-    int64_t b0 = 0;
+    RangeDesc d;
+    d.b0 = 0;
+    d.twoff = 0;
+    d.qwoff = 0;
+    d.nblk = 0;
+    d.s = r.t_start;
+    d.e = r.t_end;
+    d.qinfo = 0;
     if (r.chain >= 0 && r.chain < a.n_chains && r.t_start < r.t_end) {
         const DChain c = a.chains[r.chain];
         const int32_t *bt = a.bt + c.blk_off;
         const int32_t *bs = a.bs + c.blk_off;
-        // first block with tEnd > s
         int lo = 0, hi = c.nblk;
-        while (lo < hi) {
+        while (lo < hi) {  // first block with tEnd > s
             const int mid = (lo + hi) >> 1;
             if (bt[mid] + bs[mid] > r.t_start) hi = mid;
             else lo = mid + 1;
         }
         const int first = lo;
-        // first block with tStart >= e
         hi = c.nblk;
-        while (lo < hi) {
+        while (lo < hi) {  // first block with tStart >= e
             const int mid = (lo + hi) >> 1;
             if (bt[mid] >= r.t_end) hi = mid;
             else lo = mid + 1;
         }
-        n = lo - first;
-        b0 = c.blk_off + first;
+        d.nblk = lo - first;
+        d.b0 = c.blk_off + first;
+        d.twoff = a.t_woff[c.t_seq];
+        d.qwoff = a.q_woff[c.q_seq];
+        d.qinfo = c.q_size | (c.strand ? (int32_t)0x80000000 : 0);
     }
-    a.plan_b0[i] = b0;
-    a.plan_n[i] = n;
-    a.ntiles[i] = (n + kTileBlocks - 1) / kTileBlocks;
-    if (n == 0) {
+    a.rdesc[i] = d;
+    a.nblk[i] = d.nblk;
+    if (d.nblk == 0) {
         a.out_g[i] = 0;
         a.out_ali[i] = 0;
         if (a.want_local) a.out_l[i] = 0;
     }
 }
 
-// ------------------------------------------------------------ k_scatter --
-__global__ void __launch_bounds__(256) k_scatter(ScoreArgs a) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n) return;
-    const int t0 = a.tile_off[i];
-    const int nt = a.ntiles[i];
-    for (int k = 0; k < nt; ++k) a.tile_q[t0 + k] = (int32_t)i;
+__global__ void k_total(ScoreArgs a) {
+    if (threadIdx.x == 0) {
+        const int32_t w = a.goff[a.n - 1] + a.nblk[a.n - 1];
+        a.goff[a.n] = w;
+        a.total[0] = w;
+        a.total[1] = (w + kTileBlocks - 1) / kTileBlocks;
+    }
 }
 
-__global__ void k_total(ScoreArgs a) {
-    if (threadIdx.x == 0) *a.total_tiles = a.tile_off[a.n - 1] + a.ntiles[a.n - 1];
+// ------------------------------------------------------------ k_mark -----
+// tile_r0[t] = range owning flat block 64t.
+__global__ void __launch_bounds__(256) k_mark(ScoreArgs a) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const int nb = a.nblk[i];
+    if (nb == 0) return;
+    const int g0 = a.goff[i];
+    const int t0 = (g0 + kTileBlocks - 1) / kTileBlocks;
+    const int t1 = (g0 + nb - 1) / kTileBlocks;
+    for (int t = t0; t <= t1; ++t) a.tile_r0[t] = (int32_t)i;
 }
 
 // ------------------------------------------------------------ k_tile -----
+// One wave per tile of 64 consecutive flat blocks (ranges packed densely).
 struct WaveLds {
-    int coff[kTileBlocks + 1];
+    int goff[2 * kTileBlocks];  // candidate range offsets of this tile
+    int coff[kTileBlocks];      // exclusive chunk prefix per lane-block
     int ts[kTileBlocks];
     int qs[kTileBlocks];
     int len[kTileBlocks];
+    int qinfo[kTileBlocks];
+    long long twoff[kTileBlocks];
+    long long qwoff[kTileBlocks];
     unsigned long long acc[kTileBlocks];
 };
+
+__device__ __forceinline__ int chunk_score(const ScoreArgs &a, const WaveLds &L, int k, int off,
+                                           int n) {
+    uint32_t t0, t1, tn, q0, q1, qn;
+    load_window(a.t_planes, a.t_nmask, L.twoff[k], (int64_t)L.ts[k] + off, t0, t1, tn);
+    const int qi = L.qinfo[k];
+    const int qp = L.qs[k] + off;
+    if (qi >= 0) {
+        load_window(a.q_planes, a.q_nmask, L.qwoff[k], qp, q0, q1, qn);
+    } else {
+        // '-' strand: rc base j = comp(fwd[qSize-1-(qp+j)]), comp = code ^ 2
+        const int64_t F = (int64_t)(qi & 0x7fffffff) - qp - n;
+        uint32_t f0, f1, fn;
+        load_window(a.q_planes, a.q_nmask, L.qwoff[k], F, f0, f1, fn);
+        const int sh = 32 - n;
+        q0 = __builtin_bitreverse32(f0) >> sh;
+        q1 = ~(__builtin_bitreverse32(f1) >> sh);
+        qn = __builtin_bitreverse32(fn) >> sh;
+    }
+    const uint32_t valid = (n >= 32 ? 0xffffffffu : ((1u << n) - 1u)) & ~tn & ~qn;
+    const uint32_t tm[4] = {~t1 & ~t0, ~t1 & t0, t1 & ~t0, t1 & t0};
+    const uint32_t qm[4] = {valid & ~q1 & ~q0, valid & ~q1 & q0, valid & q1 & ~q0, valid & q1 & q0};
+    int sc = 0;
+#pragma unroll
+    for (int qc = 0; qc < 4; ++qc)
+#pragma unroll
+        for (int tc = 0; tc < 4; ++tc)
+            sc += a.coef[qc * 4 + tc] * __builtin_popcount(qm[qc] & tm[tc]);
+    return sc;
+}
+
+__device__ __forceinline__ int find_chunk_block(const WaveLds &L, int nact, int j) {
+    int k = 0;
+#pragma unroll
+    for (int step = 32; step > 0; step >>= 1)
+        if (k + step < nact && L.coff[k + step] <= j) k += step;
+    return k;
+}
+
+__device__ __forceinline__ void seg_store(const ScoreArgs &a, long long *dst_g, int32_t *dst_a,
+                                          long long *dst_l, long long g, long long ali,
+                                          const Elem &e) {
+    *dst_g = g;
+    *dst_a = (int32_t)ali;
+    if (a.want_local) *dst_l = max2(0, max2(e.C, e.D));
+}
 
 __global__ void __launch_bounds__(256) k_tile(ScoreArgs a) {
     __shared__ int32_t s_small[3 * kSmallCap];
@@ -214,49 +285,77 @@ __global__ void __launch_bounds__(256) k_tile(ScoreArgs a) {
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     WaveLds &L = s_w[wave];
-    const int total = *a.total_tiles;
+    const int T = a.n_tiles;
+    const int W = a.n_flat;
 
     // XCD-aware logical id: workgroups b and b+8 share an XCD (round-robin
-    // dispatch), so give them adjacent super-tiles (speed only).
+    // dispatch), so give them adjacent tiles (speed only).
     const int G = gridDim.x;
     const int b = blockIdx.x;
     const int L8 = (G % 8 == 0) ? ((b % 8) * (G / 8) + b / 8) : b;
 
-    for (int st = L8; st * kWavesPerWG < total; st += G) {
+    for (int st = L8; st * kWavesPerWG < T; st += G) {
         const int tile = st * kWavesPerWG + wave;
-        if (tile >= total) break;
-        const int qi = __builtin_amdgcn_readfirstlane(a.tile_q[tile]);
-        const int ti = tile - a.tile_off[qi];
-        const Range r = a.ranges[qi];
-        const int nb_q = a.plan_n[qi];
-        const int64_t b0 = a.plan_b0[qi];
-        const DChain c = a.chains[r.chain];
-        const int nt = a.ntiles[qi];
-        const int base_k = ti * kTileBlocks;
-        const int nb = min(kTileBlocks, nb_q - base_k);
+        if (tile >= T) break;
+        const int j0 = tile * kTileBlocks;
+        const int r0 = a.tile_r0[tile];
+        const int rend = (tile + 1 < T) ? a.tile_r0[tile + 1] : (int)(a.n - 1);
+        const int span = rend - r0 + 1;
+        const int j = j0 + lane;
+        const bool active = j < W;
+
+        // ---- which range owns flat block j
+        if (span <= 2 * kTileBlocks) {
+            L.goff[lane] = (lane < span) ? a.goff[r0 + lane] : 0x7fffffff;
+            L.goff[kTileBlocks + lane] =
+                (kTileBlocks + lane < span) ? a.goff[r0 + kTileBlocks + lane] : 0x7fffffff;
+        }
+        wave_sync();
+        int lo = 0, hi = span - 1;
+        if (span <= 2 * kTileBlocks) {
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (L.goff[mid] <= j) lo = mid;
+                else hi = mid - 1;
+            }
+        } else {
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (a.goff[r0 + mid] <= j) lo = mid;
+                else hi = mid - 1;
+            }
+        }
+        const int ri = r0 + lo;
+        const int gstart = (span <= 2 * kTileBlocks) ? L.goff[lo] : a.goff[ri];
 
         // ---- per-lane block: clip to [s, e), gap to the next block
-        const bool active = lane < nb;
-        int cts = 0, cqs = 0, len = 0, g = 0;
+        int cts = 0, cqs = 0, len = 0, g = 0, k = 0;
         bool last = false;
+        int qinfo = 0;
+        long long twoff = 0, qwoff = 0;
         if (active) {
-            const int64_t blk = b0 + base_k + lane;
+            const RangeDesc d = a.rdesc[ri];
+            k = j - gstart;
+            const int64_t blk = d.b0 + k;
             const int ts = a.bt[blk], qs = a.bq[blk], sz = a.bs[blk];
             const int te = ts + sz, qe = qs + sz;
             cts = ts;
             cqs = qs;
             int cte = te;
-            if (cts < r.t_start) {
-                cqs += r.t_start - cts;
-                cts = r.t_start;
+            if (cts < d.s) {
+                cqs += d.s - cts;
+                cts = d.s;
             }
-            if (cte > r.t_end) cte = r.t_end;
+            if (cte > d.e) cte = d.e;
             len = cte - cts;
-            last = (base_k + lane == nb_q - 1);
+            last = (k == d.nblk - 1);
             if (!last) {
                 const int nts = a.bt[blk + 1], nqs = a.bq[blk + 1];
                 g = gap_cost(a.gap, small, nqs - qe, nts - te);
             }
+            qinfo = d.qinfo;
+            twoff = d.twoff;
+            qwoff = d.qwoff;
         }
         // ---- chunk prefix (32 bases per chunk)
         const int nch = (len + 31) >> 5;
@@ -267,59 +366,39 @@ __global__ void __launch_bounds__(256) k_tile(ScoreArgs a) {
             if (lane >= d) incl += o;
         }
         const int C = __shfl(incl, kWave - 1, kWave);
+        const int nact = min(kTileBlocks, W - j0);
         L.coff[lane] = incl - nch;
         L.ts[lane] = cts;
         L.qs[lane] = cqs;
         L.len[lane] = len;
+        L.qinfo[lane] = qinfo;
+        L.twoff[lane] = twoff;
+        L.qwoff[lane] = qwoff;
         L.acc[lane] = 0ull;
         wave_sync();
 
-        const int64_t twoff = a.t_woff[c.t_seq];
-        const int64_t qwoff = a.q_woff[c.q_seq];
-        const bool minus = c.strand != 0;
-        for (int c0 = 0; c0 < C; c0 += kWave) {
-            const int j = c0 + lane;
-            if (j < C) {
-                int k = 0;
-#pragma unroll
-                for (int step = 32; step > 0; step >>= 1)
-                    if (k + step < nb && L.coff[k + step] <= j) k += step;
-                const int off = (j - L.coff[k]) << 5;
-                const int n = min(32, L.len[k] - off);
-                uint32_t t0, t1, tn, q0, q1, qn;
-                load_window(a.t_planes, a.t_nmask, twoff, (int64_t)L.ts[k] + off, t0, t1, tn);
-                const int qp = L.qs[k] + off;
-                if (!minus) {
-                    load_window(a.q_planes, a.q_nmask, qwoff, qp, q0, q1, qn);
-                } else {
-                    // reverse-complement: rc base j = comp(fwd[qSize-1-(qp+j)])
-                    const int64_t F = (int64_t)c.q_size - qp - n;
-                    uint32_t f0, f1, fn;
-                    load_window(a.q_planes, a.q_nmask, qwoff, F, f0, f1, fn);
-                    const int sh = 32 - n;
-                    q0 = __builtin_bitreverse32(f0) >> sh;
-                    q1 = ~(__builtin_bitreverse32(f1) >> sh);  // complement: code ^ 2
-                    qn = __builtin_bitreverse32(fn) >> sh;
-                }
-                const uint32_t valid = (n >= 32 ? 0xffffffffu : ((1u << n) - 1u)) & ~tn & ~qn;
-                const uint32_t tm[4] = {~t1 & ~t0, ~t1 & t0, t1 & ~t0, t1 & t0};
-                const uint32_t qm[4] = {valid & ~q1 & ~q0, valid & ~q1 & q0, valid & q1 & ~q0,
-                                        valid & q1 & q0};
-                int sc = 0;
-#pragma unroll
-                for (int qc = 0; qc < 4; ++qc)
-#pragma unroll
-                    for (int tc = 0; tc < 4; ++tc)
-                        sc += a.coef[qc * 4 + tc] * __builtin_popcount(qm[qc] & tm[tc]);
-                atomicAdd(&L.acc[k], (unsigned long long)(long long)sc);
+        for (int c0 = 0; c0 < C; c0 += 2 * kWave) {
+            const int ja = c0 + lane, jb = ja + kWave;
+            int ka = 0, kb = 0, sa = 0, sb = 0;
+            if (ja < C) {
+                ka = find_chunk_block(L, nact, ja);
+                const int off = (ja - L.coff[ka]) << 5;
+                sa = chunk_score(a, L, ka, off, min(32, L.len[ka] - off));
             }
+            if (jb < C) {
+                kb = find_chunk_block(L, nact, jb);
+                const int off = (jb - L.coff[kb]) << 5;
+                sb = chunk_score(a, L, kb, off, min(32, L.len[kb] - off));
+            }
+            if (ja < C) atomicAdd(&L.acc[ka], (unsigned long long)(long long)sa);
+            if (jb < C) atomicAdd(&L.acc[kb], (unsigned long long)(long long)sb);
         }
         wave_sync();
 
-        // ---- block-level: global sum, ali, max-plus local element
-        long long bsc = active ? (long long)L.acc[lane] : 0;
-        long long gsum = active ? bsc - g : 0;
-        long long ali = active ? len : 0;
+        // ---- segmented (by range) inclusive scans over the tile's lanes
+        const long long bsc = active ? (long long)L.acc[lane] : 0;
+        long long vg = active ? bsc - g : 0;
+        long long va = active ? len : 0;
         Elem e;
         if (active) {
             e.A = last ? bsc : bsc - g;
@@ -332,23 +411,49 @@ __global__ void __launch_bounds__(256) k_tile(ScoreArgs a) {
             e.C = kNeg;
             e.D = kNeg;
         }
-        gsum = wave_sum(gsum);
-        ali = wave_sum(ali);
-        if (a.want_local) e = wave_fold(e, lane);
-        if (lane == 0) {
-            if (nt == 1) {
-                a.out_g[qi] = gsum;
-                a.out_ali[qi] = (int32_t)ali;
-                if (a.want_local) a.out_l[qi] = max2(0, max2(e.C, e.D));
+        const bool head = !active || lane == 0 || k == 0;
+        int f = head ? 1 : 0;
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const long long og = __shfl_up(vg, d, kWave);
+            const long long oa = __shfl_up(va, d, kWave);
+            Elem o;
+            if (a.want_local) {
+                o.A = __shfl_up(e.A, d, kWave);
+                o.B = __shfl_up(e.B, d, kWave);
+                o.C = __shfl_up(e.C, d, kWave);
+                o.D = __shfl_up(e.D, d, kWave);
+            }
+            const int of = __shfl_up(f, d, kWave);
+            if (lane >= d) {
+                if (!f) {
+                    vg += og;
+                    va += oa;
+                    if (a.want_local) e = compose(o, e);
+                }
+                f |= of;
+            }
+        }
+        const bool next_head = __shfl_down((int)head, 1, kWave) != 0;
+        const bool seg_end = active && (lane == kWave - 1 || next_head);
+        const int r_lane0 = __shfl(ri, 0, kWave);
+        const int k_lane0 = __shfl(k, 0, kWave);
+        if (seg_end) {
+            const bool has0 = (ri == r_lane0);
+            const bool starts = !has0 || k_lane0 == 0;
+            if (starts && last) {
+                seg_store(a, &a.out_g[ri], &a.out_ali[ri], a.out_l ? &a.out_l[ri] : nullptr, vg,
+                          va, e);
             } else {
-                TileSum ts;
-                ts.g = gsum;
-                ts.ali = ali;
-                ts.A = e.A;
-                ts.B = e.B;
-                ts.C = e.C;
-                ts.D = e.D;
-                a.tsum[tile] = ts;
+                SegSum ssum;
+                ssum.g = vg;
+                ssum.ali = va;
+                ssum.A = e.A;
+                ssum.B = e.B;
+                ssum.C = e.C;
+                ssum.D = e.D;
+                if (has0 && !starts) a.sum_head[tile] = ssum;
+                if (!last && (lane == kWave - 1 || j + 1 == W)) a.sum_tail[tile] = ssum;
             }
         }
         wave_sync();
@@ -356,32 +461,54 @@ __global__ void __launch_bounds__(256) k_tile(ScoreArgs a) {
 }
 
 // ------------------------------------------------------------ k_combine --
+// Ranges spanning > 1 tile: tail segment of the first tile, then the head
+// segments of the following tiles, folded in order.
 __global__ void __launch_bounds__(256) k_combine(ScoreArgs a) {
     const int lane = threadIdx.x & 63;
     const int64_t wave_id = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    for (int64_t qi = wave_id; qi < a.n; qi += nwaves) {
-        const int nt = a.ntiles[qi];
-        if (nt <= 1) continue;
-        const int t0 = a.tile_off[qi];
-        const int per = (nt + kWave - 1) / kWave;
-        const int lo = min(nt, lane * per), hi = min(nt, lo + per);
-        long long g = 0, ali = 0;
-        Elem e = {0, kNeg, kNeg, kNeg};
-        for (int t = lo; t < hi; ++t) {
-            const TileSum s = a.tsum[t0 + t];
-            g += s.g;
-            ali += s.ali;
-            Elem y = {s.A, s.B, s.C, s.D};
-            e = compose(e, y);
+    for (int64_t base = wave_id * kWave; base < a.n; base += nwaves * kWave) {
+        const int64_t my = base + lane;
+        bool multi = false;
+        int tf = 0, tl = 0;
+        if (my < a.n) {
+            const int nb = a.nblk[my];
+            if (nb > 0) {
+                const int g0 = a.goff[my];
+                tf = g0 / kTileBlocks;
+                tl = (g0 + nb - 1) / kTileBlocks;
+                multi = tf != tl;
+            }
         }
-        g = wave_sum(g);
-        ali = wave_sum(ali);
-        if (a.want_local) e = wave_fold(e, lane);
-        if (lane == 0) {
-            a.out_g[qi] = g;
-            a.out_ali[qi] = (int32_t)ali;
-            if (a.want_local) a.out_l[qi] = max2(0, max2(e.C, e.D));
+        unsigned long long mask = __ballot(multi);
+        while (mask) {
+            const int src = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            const int64_t ri = base + src;
+            const int f0 = __shfl(tf, src, kWave);
+            const int f1 = __shfl(tl, src, kWave);
+            const int nt = f1 - f0;  // head segments in tiles f0+1 .. f1
+            const int per = (nt + kWave - 1) / kWave;
+            const int lo = min(nt, lane * per), hi = min(nt, lo + per);
+            long long g = 0, ali = 0;
+            Elem e = {0, kNeg, kNeg, kNeg};
+            for (int t = lo; t < hi; ++t) {
+                const SegSum s = a.sum_head[f0 + 1 + t];
+                g += s.g;
+                ali += s.ali;
+                const Elem y = {s.A, s.B, s.C, s.D};
+                e = compose(e, y);
+            }
+            g = wave_sum(g);
+            ali = wave_sum(ali);
+            if (a.want_local) e = wave_fold(e, lane);
+            if (lane == 0) {
+                const SegSum s0 = a.sum_tail[f0];
+                const Elem x = {s0.A, s0.B, s0.C, s0.D};
+                e = compose(x, e);
+                seg_store(a, &a.out_g[ri], &a.out_ali[ri], a.out_l ? &a.out_l[ri] : nullptr,
+                          s0.g + g, s0.ali + ali, e);
+            }
         }
     }
 }
@@ -461,23 +588,20 @@ size_t scan_temp_bytes(int64_t n) {
     return bytes;
 }
 
-hipError_t launch_plan(const ScoreArgs &a, hipStream_t s) {
+hipError_t launch_plan(const ScoreArgs &a, void *temp, size_t temp_bytes, hipStream_t s) {
     const int64_t nb = (a.n + 255) / 256;
     hipLaunchKernelGGL(k_plan, dim3((unsigned)nb), dim3(256), 0, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_scan_total(const ScoreArgs &a, void *temp, size_t temp_bytes, hipStream_t s) {
-    hipError_t e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, a.ntiles, a.tile_off,
-                                                    (int)a.n, s);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, a.nblk, a.goff, (int)a.n, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_total, dim3(1), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_scatter(const ScoreArgs &a, hipStream_t s) {
+hipError_t launch_mark(const ScoreArgs &a, hipStream_t s) {
     const int64_t nb = (a.n + 255) / 256;
-    hipLaunchKernelGGL(k_scatter, dim3((unsigned)nb), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_mark, dim3((unsigned)nb), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -1,0 +1,846 @@
+/* gac_net.c -- host netting engine of chainNet (C11), array-indexed.
+ *
+ * Same fill/gap trees, same .net text as the reference's
+ * src/chainNet/chainNet.c, without its O(fills x blocks) list rescans:
+ *   makeChroms / addSpaceForGap / findSpaces   :328-354, :289-300, :527-544
+ *       -> per-chromosome treap of disjoint spaces, in-order range query
+ *   addChainT / addChainQ / fillSpace / innerBounds / strictlyInside
+ *       :557-679, :487-523, :356-391, :321-325
+ *       -> identical decisions; the gap scan stops at the first gap that
+ *          ends past the space (gaps are monotone), instead of walking the
+ *          rest of the chain for every space
+ *   sortNet / rCalcOtherFill / t,qFillOtherRange  :694-723, :393-484
+ *       -> fills/gaps sorted once into arrays; other-side ranges by binary
+ *          search to the first block of the fill
+ *   rOutputFill / rOutputGap / fillOut / subchainInfo / outputNetSide
+ *       :747-896 -> same traversal and printf formats; chainBaseCount and
+ *          chainBaseCountSubT/SubQ come from per-chain prefix sums
+ * Rescored T-side sub-chain scores are supplied by the caller (computed on
+ * the GPU through gac_score_ranges); this file never scores bases.
+ */
+#define _GNU_SOURCE
+#include "gac_host.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define BIGNUM 0x3fffffff /* kent common.h:117 */
+
+typedef struct ngap ngap;
+typedef struct nfill nfill;
+
+struct ngap {
+    int start, end, o_start, o_end;
+    nfill *fill_head; /* slAddHead order until sorted */
+    nfill **fills;
+    int n_fills;
+    ngap *next; /* in parent fill's list */
+};
+
+struct nfill {
+    int start, end, o_start, o_end;
+    int32_t chain;
+    ngap *gap_head;
+    ngap **gaps;
+    int n_gaps;
+    nfill *next;
+    int64_t ord; /* pre-order index on its side */
+};
+
+typedef struct tnode {
+    int start, end;
+    ngap *gap;
+    uint32_t prio;
+    int32_t l, r;
+} tnode;
+
+typedef struct nchrom {
+    const char *name;
+    int size;
+    ngap *root;
+    int32_t troot;
+} nchrom;
+
+/* ------------------------------------------------------------ arena */
+typedef struct arena {
+    char **blocks;
+    size_t n, cap, used, bsize;
+} arena;
+
+static void *arena_alloc(arena *a, size_t sz) {
+    sz = (sz + 15) & ~(size_t)15;
+    if (a->n == 0 || a->used + sz > a->bsize) {
+        if (a->n == a->cap) {
+            a->cap = a->cap ? a->cap * 2 : 64;
+            a->blocks = realloc(a->blocks, a->cap * sizeof(char *));
+        }
+        size_t bs = sz > (1u << 22) ? sz : (1u << 22);
+        a->blocks[a->n++] = calloc(1, bs);
+        a->bsize = bs;
+        a->used = 0;
+    }
+    void *p = a->blocks[a->n - 1] + a->used;
+    a->used += sz;
+    return p;
+}
+
+static void arena_free(arena *a) {
+    for (size_t i = 0; i < a->n; ++i)
+        free(a->blocks[i]);
+    free(a->blocks);
+    memset(a, 0, sizeof(*a));
+}
+
+struct gac_net {
+    gac_net_input in;
+    gac_net_opts opt;
+    int64_t n_netted;
+    nchrom *chroms[2]; /* [GAC_T], [GAC_Q] */
+    int32_t n_chroms[2];
+    arena ar;
+    tnode *tn;
+    int32_t tn_n, tn_cap, tn_free;
+    uint32_t rng;
+    int64_t *ali_prefix; /* per block prefix of sizes, per chain offset by blk_off */
+    /* pre-order fill index per side */
+    nfill **order[2];
+    int64_t n_order[2];
+    /* scratch for findSpaces */
+    int32_t *fs;
+    int64_t fs_n, fs_cap;
+    /* scratch for reversed blocks */
+    int32_t *rs, *re, *ros, *roe;
+    int64_t r_cap;
+};
+
+/* ------------------------------------------------------------ treap */
+static uint32_t net_rand(gac_net *n) {
+    n->rng ^= n->rng << 13;
+    n->rng ^= n->rng >> 17;
+    n->rng ^= n->rng << 5;
+    return n->rng;
+}
+
+static int32_t tn_new(gac_net *n, int start, int end, ngap *gap) {
+    int32_t i;
+    if (n->tn_free >= 0) {
+        i = n->tn_free;
+        n->tn_free = n->tn[i].l;
+    } else {
+        if (n->tn_n == n->tn_cap) {
+            n->tn_cap = n->tn_cap ? n->tn_cap * 2 : 1 << 16;
+            n->tn = realloc(n->tn, (size_t)n->tn_cap * sizeof(tnode));
+        }
+        i = n->tn_n++;
+    }
+    tnode *t = &n->tn[i];
+    t->start = start;
+    t->end = end;
+    t->gap = gap;
+    t->prio = net_rand(n);
+    t->l = t->r = -1;
+    return i;
+}
+
+static void tn_release(gac_net *n, int32_t i) {
+    n->tn[i].l = n->tn_free;
+    n->tn_free = i;
+}
+
+/* split by start: l gets starts < key, r gets starts >= key */
+static void tn_split(gac_net *n, int32_t t, int key, int32_t *l, int32_t *r) {
+    if (t < 0) {
+        *l = *r = -1;
+        return;
+    }
+    if (n->tn[t].start < key) {
+        tn_split(n, n->tn[t].r, key, &n->tn[t].r, r);
+        *l = t;
+    } else {
+        tn_split(n, n->tn[t].l, key, l, &n->tn[t].l);
+        *r = t;
+    }
+}
+
+static int32_t tn_merge(gac_net *n, int32_t a, int32_t b) {
+    if (a < 0)
+        return b;
+    if (b < 0)
+        return a;
+    if (n->tn[a].prio > n->tn[b].prio) {
+        n->tn[a].r = tn_merge(n, n->tn[a].r, b);
+        return a;
+    }
+    n->tn[b].l = tn_merge(n, a, n->tn[b].l);
+    return b;
+}
+
+static void tn_insert(gac_net *n, int32_t *root, int32_t node) {
+    int32_t l, r;
+    tn_split(n, *root, n->tn[node].start, &l, &r);
+    *root = tn_merge(n, tn_merge(n, l, node), r);
+}
+
+static void tn_erase(gac_net *n, int32_t *root, int key) {
+    /* spaces are disjoint: start is a unique key */
+    int32_t *p = root;
+    while (*p >= 0) {
+        tnode *t = &n->tn[*p];
+        if (t->start == key) {
+            *p = tn_merge(n, t->l, t->r);
+            return;
+        }
+        p = (key < t->start) ? &t->l : &t->r;
+    }
+}
+
+static void fs_push(gac_net *n, int32_t v) {
+    if (n->fs_n == n->fs_cap) {
+        n->fs_cap = n->fs_cap ? n->fs_cap * 2 : 1024;
+        n->fs = realloc(n->fs, n->fs_cap * sizeof(int32_t));
+    }
+    n->fs[n->fs_n++] = v;
+}
+
+/* in-order spaces overlapping [qs, qe) (spaceCmp == 0, chainNet.c:277-287) */
+static void tn_range(gac_net *n, int32_t t, int qs, int qe) {
+    while (t >= 0) {
+        tnode *x = &n->tn[t];
+        if (x->end > qs)
+            tn_range(n, x->l, qs, qe);
+        if (x->end > qs && x->start < qe)
+            fs_push(n, t);
+        if (x->start < qe)
+            t = x->r;
+        else
+            break;
+    }
+}
+
+static void add_space_for_gap(gac_net *n, nchrom *c, ngap *g) {
+    tn_insert(n, &c->troot, tn_new(n, g->start, g->end, g));
+}
+
+static ngap *gap_new(gac_net *n, int s, int e, int os, int oe) {
+    ngap *g = arena_alloc(&n->ar, sizeof(ngap));
+    g->start = s;
+    g->end = e;
+    g->o_start = os;
+    g->o_end = oe;
+    return g;
+}
+
+/* ------------------------------------------------------------ netting */
+static int strictly_inside(const gac_net *n, int min_start, int max_end, int start, int end) {
+    return min_start < start && start + n->opt.min_space <= end && end < max_end;
+}
+
+/* Generic addChainT/addChainQ on one side.  s[],e[] = this side's block
+ * coordinates in list order (+ strand coords), os_gap/oe_gap = other-side
+ * gap bounds per block (gap between block b and b+1). */
+static void add_chain_side(gac_net *n, nchrom *c, int32_t chain, int nb, const int32_t *s,
+                           const int32_t *e, const int32_t *gos, const int32_t *goe,
+                           int cstart, int cend) {
+    n->fs_n = 0;
+    tn_range(n, c->troot, cstart, cend);
+    int64_t nsp = n->fs_n;
+    if (nsp == 0)
+        return;
+    int32_t *sp = malloc(nsp * sizeof(int32_t));
+    memcpy(sp, n->fs, nsp * sizeof(int32_t));
+    int k = 0;
+    for (int64_t si = 0; si < nsp; ++si) {
+        int32_t ti = sp[si];
+        const int sstart = n->tn[ti].start, send = n->tn[ti].end;
+        ngap *sgap = n->tn[ti].gap;
+        while (k + 1 < nb && s[k + 1] <= sstart)
+            ++k;
+        /* innerBounds (chainNet.c:356-391) */
+        int start = BIGNUM, end = -BIGNUM;
+        for (int b = k; b < nb; ++b) {
+            int bs = s[b], be = e[b];
+            if (be <= sstart)
+                continue;
+            if (bs >= send)
+                break;
+            if (bs < sstart)
+                bs = sstart;
+            if (be > send)
+                be = send;
+            if (start > bs)
+                start = bs;
+            if (end < be)
+                end = be;
+        }
+        if (end < 0 || end - start < n->opt.min_fill)
+            continue;
+        /* fillSpace (chainNet.c:487-523) */
+        nfill *f = arena_alloc(&n->ar, sizeof(nfill));
+        f->start = start;
+        f->end = end;
+        f->chain = chain;
+        tn_erase(n, &c->troot, sstart);
+        if (start - sstart >= n->opt.min_space)
+            tn_insert(n, &c->troot, tn_new(n, sstart, start, sgap));
+        if (send - end >= n->opt.min_space)
+            tn_insert(n, &c->troot, tn_new(n, end, send, sgap));
+        f->next = sgap->fill_head;
+        sgap->fill_head = f;
+        /* gaps strictly inside the space */
+        for (int b = k; b + 1 < nb; ++b) {
+            int gs = e[b], ge = s[b + 1];
+            if (ge >= send)
+                break;
+            if (strictly_inside(n, sstart, send, gs, ge)) {
+                ngap *g = gap_new(n, gs, ge, gos[b], goe[b]);
+                add_space_for_gap(n, c, g);
+                g->next = f->gap_head;
+                f->gap_head = g;
+            }
+        }
+        tn_release(n, ti);
+    }
+    free(sp);
+}
+
+static void ensure_rev(gac_net *n, int64_t nb) {
+    if (nb > n->r_cap) {
+        n->r_cap = nb * 2;
+        n->rs = realloc(n->rs, n->r_cap * 4);
+        n->re = realloc(n->re, n->r_cap * 4);
+        n->ros = realloc(n->ros, n->r_cap * 4);
+        n->roe = realloc(n->roe, n->r_cap * 4);
+    }
+}
+
+static int is_haplotype(const char *name) {
+    return strstr(name, "_hap") != NULL || strstr(name, "_alt") != NULL;
+}
+
+static void add_chain(gac_net *n, int64_t c) {
+    const gac_net_input *in = &n->in;
+    const int64_t b0 = in->blk_off[c];
+    const int nb = (int)(in->blk_off[c + 1] - b0);
+    const int32_t *bt = in->blk_t + b0, *bq = in->blk_q + b0, *bs = in->blk_size + b0;
+    const int minus = in->q_strand[c] != 0;
+    const int qsize = in->q_sizes[in->q_seq[c]];
+    ensure_rev(n, nb);
+    /* ---- addChainQ (chainNet.c:610-679) */
+    {
+        nchrom *qc = &n->chroms[GAC_Q][in->q_seq[c]];
+        int qs = in->q_start[c], qe = in->q_end[c];
+        if (!minus) {
+            for (int b = 0; b < nb; ++b) {
+                n->rs[b] = bq[b];
+                n->re[b] = bq[b] + bs[b];
+                if (b + 1 < nb) {
+                    n->ros[b] = bt[b] + bs[b];
+                    n->roe[b] = bt[b + 1];
+                }
+            }
+        } else {
+            int t = qs;
+            qs = qsize - qe;
+            qe = qsize - t;
+            for (int i = 0; i < nb; ++i) {
+                int j = nb - 1 - i; /* original index */
+                n->rs[i] = qsize - (bq[j] + bs[j]);
+                n->re[i] = qsize - bq[j];
+                if (i + 1 < nb) { /* block = j, next = j-1 */
+                    n->ros[i] = bt[j - 1];
+                    n->roe[i] = bt[j] + bs[j];
+                }
+            }
+        }
+        add_chain_side(n, qc, (int32_t)c, nb, n->rs, n->re, n->ros, n->roe, qs, qe);
+    }
+    /* ---- addChainT (chainNet.c:557-608) */
+    {
+        nchrom *tc = &n->chroms[GAC_T][in->t_seq[c]];
+        for (int b = 0; b < nb; ++b) {
+            n->rs[b] = bt[b];
+            n->re[b] = bt[b] + bs[b];
+            if (b + 1 < nb) {
+                int qs = bq[b] + bs[b], qe = bq[b + 1];
+                if (minus) {
+                    int t = qs;
+                    qs = qsize - qe;
+                    qe = qsize - t;
+                }
+                n->ros[b] = qs;
+                n->roe[b] = qe;
+            }
+        }
+        add_chain_side(n, tc, (int32_t)c, nb, n->rs, n->re, n->ros, n->roe, in->t_start[c],
+                       in->t_end[c]);
+    }
+}
+
+/* ------------------------------------------------------------ finish */
+static int cmp_fill(const void *a, const void *b) {
+    const nfill *x = *(nfill *const *)a, *y = *(nfill *const *)b;
+    return (x->start > y->start) - (x->start < y->start);
+}
+
+static int cmp_gap(const void *a, const void *b) {
+    const ngap *x = *(ngap *const *)a, *y = *(ngap *const *)b;
+    return (x->start > y->start) - (x->start < y->start);
+}
+
+/* first block index with value[k] + size[k] > v (blocks monotone) */
+static int first_end_after(const int32_t *st, const int32_t *sz, int nb, int v) {
+    int lo = 0, hi = nb;
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (st[mid] + sz[mid] > v)
+            hi = mid;
+        else
+            lo = mid + 1;
+    }
+    return lo;
+}
+
+/* tFillOtherRange / qFillOtherRange (chainNet.c:393-484) */
+static void fill_other_range(gac_net *n, nfill *f, int is_q) {
+    const gac_net_input *in = &n->in;
+    const int64_t c = f->chain, b0 = in->blk_off[c];
+    const int nb = (int)(in->blk_off[c + 1] - b0);
+    const int32_t *bt = in->blk_t + b0, *bq = in->blk_q + b0, *bs = in->blk_size + b0;
+    const int minus = in->q_strand[c] != 0;
+    const int qsize = in->q_sizes[in->q_seq[c]];
+    int clip_s = f->start, clip_e = f->end;
+    int tmin = BIGNUM, tmax = -BIGNUM, qmin = BIGNUM, qmax = -BIGNUM;
+    if (is_q) {
+        if (minus) {
+            int t = clip_s;
+            clip_s = qsize - clip_e;
+            clip_e = qsize - t;
+        }
+        for (int b = first_end_after(bq, bs, nb, clip_s); b < nb; ++b) {
+            int qs = bq[b], qe = bq[b] + bs[b], ts = bt[b], te = bt[b] + bs[b];
+            if (qe <= clip_s)
+                continue;
+            if (qs >= clip_e)
+                break;
+            if (qs < clip_s) {
+                ts += clip_s - qs;
+                qs = clip_s;
+            }
+            if (qe > clip_e) {
+                te -= qe - clip_e;
+                qe = clip_e;
+            }
+            if (qmin > qs) qmin = qs;
+            if (qmax < qe) qmax = qe;
+            if (tmin > ts) tmin = ts;
+            if (tmax < te) tmax = te;
+        }
+        if (minus) {
+            int t = qmin;
+            qmin = qsize - qmax;
+            qmax = qsize - t;
+        }
+        f->start = qmin;
+        f->end = qmax;
+        f->o_start = tmin;
+        f->o_end = tmax;
+    } else {
+        for (int b = first_end_after(bt, bs, nb, clip_s); b < nb; ++b) {
+            int ts = bt[b], te = bt[b] + bs[b], qs = bq[b], qe = bq[b] + bs[b];
+            if (te <= clip_s)
+                continue;
+            if (ts >= clip_e)
+                break;
+            if (ts < clip_s) {
+                qs += clip_s - ts;
+                ts = clip_s;
+            }
+            if (te > clip_e) {
+                qe -= te - clip_e;
+                te = clip_e;
+            }
+            if (qmin > qs) qmin = qs;
+            if (qmax < qe) qmax = qe;
+            if (tmin > ts) tmin = ts;
+            if (tmax < te) tmax = te;
+        }
+        if (minus) {
+            int t = qmin;
+            qmin = qsize - qmax;
+            qmax = qsize - t;
+        }
+        f->start = tmin;
+        f->end = tmax;
+        f->o_start = qmin;
+        f->o_end = qmax;
+    }
+}
+
+static void order_push(gac_net *n, int side, nfill *f, int64_t *cap) {
+    if (n->n_order[side] == *cap) {
+        *cap = *cap ? *cap * 2 : 4096;
+        n->order[side] = realloc(n->order[side], *cap * sizeof(nfill *));
+    }
+    f->ord = n->n_order[side];
+    n->order[side][n->n_order[side]++] = f;
+}
+
+static void finish_gap(gac_net *n, int side, ngap *g, int64_t *cap);
+
+static void finish_fill(gac_net *n, int side, nfill *f, int64_t *cap) {
+    fill_other_range(n, f, side == GAC_Q);
+    order_push(n, side, f, cap);
+    int cnt = 0;
+    for (ngap *g = f->gap_head; g; g = g->next)
+        ++cnt;
+    f->n_gaps = cnt;
+    f->gaps = cnt ? arena_alloc(&n->ar, cnt * sizeof(ngap *)) : NULL;
+    cnt = 0;
+    for (ngap *g = f->gap_head; g; g = g->next)
+        f->gaps[cnt++] = g;
+    qsort(f->gaps, f->n_gaps, sizeof(ngap *), cmp_gap);
+    for (int i = 0; i < f->n_gaps; ++i)
+        finish_gap(n, side, f->gaps[i], cap);
+}
+
+static void finish_gap(gac_net *n, int side, ngap *g, int64_t *cap) {
+    int cnt = 0;
+    for (nfill *f = g->fill_head; f; f = f->next)
+        ++cnt;
+    g->n_fills = cnt;
+    g->fills = cnt ? arena_alloc(&n->ar, cnt * sizeof(nfill *)) : NULL;
+    cnt = 0;
+    for (nfill *f = g->fill_head; f; f = f->next)
+        g->fills[cnt++] = f;
+    qsort(g->fills, g->n_fills, sizeof(nfill *), cmp_fill);
+    for (int i = 0; i < g->n_fills; ++i)
+        finish_fill(n, side, g->fills[i], cap);
+}
+
+/* ------------------------------------------------------------ API */
+void gac_net_free(gac_net *n) {
+    if (!n)
+        return;
+    arena_free(&n->ar);
+    free(n->tn);
+    free(n->chroms[0]);
+    free(n->chroms[1]);
+    free(n->order[0]);
+    free(n->order[1]);
+    free(n->fs);
+    free(n->rs);
+    free(n->re);
+    free(n->ros);
+    free(n->roe);
+    free(n->ali_prefix);
+    free(n);
+}
+
+int gac_net_build(const gac_net_input *in, const gac_net_opts *opt, gac_net **out) {
+    gac_clear_error();
+    if (!in || !opt || !out)
+        return gac_fail(GAC_E_ARG, "gac_net_build: NULL argument");
+    *out = NULL;
+    gac_net *n = calloc(1, sizeof(*n));
+    n->in = *in;
+    n->opt = *opt;
+    n->tn_free = -1;
+    n->rng = 0x9E3779B9u;
+    for (int side = 0; side < 2; ++side) {
+        int32_t cnt = side == GAC_T ? in->n_tseq : in->n_qseq;
+        const char *const *names = side == GAC_T ? in->t_names : in->q_names;
+        const int32_t *sizes = side == GAC_T ? in->t_sizes : in->q_sizes;
+        n->n_chroms[side] = cnt;
+        n->chroms[side] = calloc(cnt ? cnt : 1, sizeof(nchrom));
+        for (int32_t i = 0; i < cnt; ++i) {
+            nchrom *c = &n->chroms[side][i];
+            c->name = names[i];
+            c->size = sizes[i];
+            c->root = gap_new(n, 0, sizes[i], 0, 0);
+            c->troot = -1;
+            add_space_for_gap(n, c, c->root);
+        }
+    }
+    double last = -1;
+    int64_t i;
+    for (i = 0; i < in->n_chains; ++i) {
+        const double sc = in->score[i];
+        if (last >= 0 && sc > last) {
+            gac_net_free(n);
+            return gac_fail(GAC_E_FORMAT, "input must be sorted in order of score");
+        }
+        last = sc;
+        if (sc < opt->min_score)
+            break;
+        if (in->t_seq[i] < 0 || in->t_seq[i] >= in->n_tseq || in->q_seq[i] < 0 ||
+            in->q_seq[i] >= in->n_qseq) {
+            gac_net_free(n);
+            return gac_fail(GAC_E_ARG, "chain %lld: sequence index out of range", (long long)i);
+        }
+        if (!opt->incl_hap && is_haplotype(in->q_names[in->q_seq[i]]))
+            continue;
+        add_chain(n, i);
+    }
+    n->n_netted = i;
+    /* finishNet: Q then T (order irrelevant), sort + other ranges + pre-order index */
+    for (int side = 1; side >= 0; --side) {
+        int64_t cap = 0;
+        for (int32_t k = 0; k < n->n_chroms[side]; ++k) {
+            nchrom *c = &n->chroms[side][k];
+            if (c->root->fill_head)
+                finish_gap(n, side, c->root, &cap);
+        }
+    }
+    /* aligned-base prefix per block for chainBaseCount / SubT / SubQ */
+    n->ali_prefix = malloc((in->blk_off[in->n_chains] + 1) * sizeof(int64_t));
+    int64_t acc = 0;
+    for (int64_t b = 0; b < in->blk_off[in->n_chains]; ++b) {
+        n->ali_prefix[b] = acc;
+        acc += in->blk_size[b];
+    }
+    n->ali_prefix[in->blk_off[in->n_chains]] = acc;
+    *out = n;
+    return GAC_OK;
+}
+
+int64_t gac_net_netted(const gac_net *n) { return n ? n->n_netted : -1; }
+
+int64_t gac_net_fill_count(const gac_net *n, int side) {
+    if (!n || (side != GAC_T && side != GAC_Q))
+        return -1;
+    return n->n_order[side];
+}
+
+/* aligned bases of chain c inside [s, e) on one side (chainBaseCountSubT/Q) */
+static int sub_size(const gac_net *n, int64_t c, int s, int e, int is_q) {
+    const gac_net_input *in = &n->in;
+    const int64_t b0 = in->blk_off[c];
+    const int nb = (int)(in->blk_off[c + 1] - b0);
+    const int32_t *st = (is_q ? in->blk_q : in->blk_t) + b0, *sz = in->blk_size + b0;
+    int lo = first_end_after(st, sz, nb, s);
+    /* first block with start >= e */
+    int a = lo, hi = nb;
+    while (a < hi) {
+        int mid = (a + hi) >> 1;
+        if (st[mid] >= e)
+            hi = mid;
+        else
+            a = mid + 1;
+    }
+    if (a <= lo)
+        return 0;
+    int64_t tot = n->ali_prefix[b0 + a] - n->ali_prefix[b0 + lo];
+    /* clip the first and last block */
+    int fs = st[lo], fe = st[lo] + sz[lo];
+    if (fs < s)
+        tot -= s - fs;
+    int ls = st[a - 1], le = st[a - 1] + sz[a - 1];
+    if (le > e)
+        tot -= le - e;
+    (void)fe;
+    (void)ls;
+    return (int)tot;
+}
+
+static int full_size(const gac_net *n, int64_t c) {
+    const gac_net_input *in = &n->in;
+    return (int)(n->ali_prefix[in->blk_off[c + 1]] - n->ali_prefix[in->blk_off[c]]);
+}
+
+/* visibility of each fill: reached by rOutputFill and passing its filters
+ * given the score rule; for the T side with rescore the score filter always
+ * passes (partial scores are >= 1, netted chains >= minScore = 0). */
+int gac_net_get_fills(const gac_net *n, int side, int32_t *chain, int32_t *start, int32_t *end,
+                      int32_t *ali, uint8_t *flags) {
+    if (!n || (side != GAC_T && side != GAC_Q))
+        return gac_fail(GAC_E_ARG, "gac_net_get_fills: bad argument");
+    const gac_net_input *in = &n->in;
+    for (int64_t i = 0; i < n->n_order[side]; ++i) {
+        const nfill *f = n->order[side][i];
+        int64_t c = f->chain;
+        int s = f->start, e = f->end;
+        int full, sz;
+        if (side == GAC_Q) {
+            if (in->q_strand[c]) {
+                int qsize = in->q_sizes[in->q_seq[c]];
+                int t = s;
+                s = qsize - e;
+                e = qsize - t;
+            }
+            full = (s <= in->q_start[c] && e >= in->q_end[c]);
+        } else {
+            full = (s <= in->t_start[c] && e >= in->t_end[c]);
+        }
+        sz = full ? full_size(n, c) : sub_size(n, c, s, e, side == GAC_Q);
+        if (chain)
+            chain[i] = (int32_t)c;
+        if (start)
+            start[i] = f->start;
+        if (end)
+            end[i] = f->end;
+        if (ali)
+            ali[i] = sz;
+        if (flags)
+            flags[i] = (uint8_t)(full ? 0 : 1);
+    }
+    /* visibility pass (pre-order: parents precede children) */
+    if (flags) {
+        for (int32_t k = 0; k < n->n_chroms[side]; ++k) {
+            /* iterative DFS */
+            const nchrom *c = &n->chroms[side][k];
+            if (!c->root->fill_head)
+                continue;
+            typedef struct {
+                const nfill *f;
+                int vis;
+            } item;
+            int64_t cap = 1024, top = 0;
+            item *st = malloc(cap * sizeof(item));
+            for (int i = c->root->n_fills - 1; i >= 0; --i)
+                st[top++] = (item){c->root->fills[i], 1};
+            while (top) {
+                item it = st[--top];
+                const nfill *f = it.f;
+                int sz = ali ? ali[f->ord] : 0;
+                int vis = it.vis && sz >= n->opt.min_fill;
+                if (vis)
+                    flags[f->ord] |= 2;
+                for (int g = f->n_gaps - 1; g >= 0; --g) {
+                    const ngap *gp = f->gaps[g];
+                    for (int j = gp->n_fills - 1; j >= 0; --j) {
+                        if (top == cap) {
+                            cap *= 2;
+                            st = realloc(st, cap * sizeof(item));
+                        }
+                        st[top++] = (item){gp->fills[j], vis};
+                    }
+                }
+            }
+            free(st);
+        }
+    }
+    return GAC_OK;
+}
+
+/* ------------------------------------------------------------ output */
+typedef struct wctx {
+    const gac_net *n;
+    FILE *f;
+    int side;
+    const int64_t *tscore; /* per T fill (pre-order), GPU-rescored partial scores */
+    int depth;
+    char *buf;
+} wctx;
+
+static void spaces(FILE *f, int k) {
+    while (k-- > 0)
+        fputc(' ', f);
+}
+
+static void out_fill(wctx *w, const nfill *f);
+
+static void out_gap(wctx *w, const nfill *parent, const ngap *g) {
+    const gac_net_input *in = &w->n->in;
+    const int64_t c = parent->chain;
+    const char *ochrom = w->side == GAC_Q ? in->t_names[in->t_seq[c]] : in->q_names[in->q_seq[c]];
+    ++w->depth;
+    spaces(w->f, w->depth);
+    fprintf(w->f, "gap %d %d %s %c %d %d\n", g->start, g->end - g->start, ochrom,
+            in->q_strand[c] ? '-' : '+', g->o_start, g->o_end - g->o_start);
+    for (int i = 0; i < g->n_fills; ++i)
+        out_fill(w, g->fills[i]);
+    --w->depth;
+}
+
+static void out_fill(wctx *w, const nfill *f) {
+    const gac_net *n = w->n;
+    const gac_net_input *in = &n->in;
+    const int64_t c = f->chain;
+    int s = f->start, e = f->end;
+    int sub;
+    double score;
+    /* subchainInfo (chainNet.c:795-843) */
+    const int fullsz = full_size(n, c);
+    if (w->side == GAC_Q) {
+        if (in->q_strand[c]) {
+            int qsize = in->q_sizes[in->q_seq[c]];
+            int t = s;
+            s = qsize - e;
+            e = qsize - t;
+        }
+        if (s <= in->q_start[c] && e >= in->q_end[c]) {
+            score = in->score[c];
+            sub = fullsz;
+        } else {
+            sub = sub_size(n, c, s, e, 1);
+            score = in->score[c] * sub / fullsz;
+        }
+    } else {
+        if (s <= in->t_start[c] && e >= in->t_end[c]) {
+            score = in->score[c];
+            sub = fullsz;
+        } else {
+            sub = sub_size(n, c, s, e, 0);
+            if (w->tscore) {
+                double r = (double)w->tscore[f->ord];
+                score = r <= 0 ? 1 : r; /* chainNet.c:244-245 */
+            } else {
+                score = in->score[c] * sub / fullsz;
+            }
+        }
+    }
+    if (score >= n->opt.min_score && sub >= n->opt.min_fill) {
+        ++w->depth;
+        spaces(w->f, w->depth);
+        const char *ochrom = w->side == GAC_Q ? in->t_names[in->t_seq[c]] : in->q_names[in->q_seq[c]];
+        fprintf(w->f, "fill %d %d %s %c %d %d id %d score %1.0f ali %d\n", f->start,
+                f->end - f->start, ochrom, in->q_strand[c] ? '-' : '+', f->o_start,
+                f->o_end - f->o_start, in->id[c], score, sub);
+        for (int i = 0; i < f->n_gaps; ++i)
+            out_gap(w, f, f->gaps[i]);
+        --w->depth;
+    }
+}
+
+int gac_net_write(const gac_net *n, int side, const int64_t *tscores, const char *path,
+                  const char *const *meta, int32_t n_meta) {
+    if (!n || !path || (side != GAC_T && side != GAC_Q))
+        return gac_fail(GAC_E_ARG, "gac_net_write: bad argument");
+    FILE *f;
+    int close_it = 1;
+    if (strcmp(path, "stdout") == 0) {
+        f = stdout;
+        close_it = 0;
+    } else {
+        f = fopen(path, "w");
+        if (!f)
+            return gac_fail(GAC_E_IO, "Can't open %s to write", path);
+    }
+    char *buf = malloc(1 << 22);
+    setvbuf(f, buf, _IOFBF, 1 << 22);
+    for (int32_t i = 0; i < n_meta; ++i)
+        fprintf(f, "%s\n", meta[i]);
+    wctx w = {n, f, side, side == GAC_T ? tscores : NULL, 0, buf};
+    for (int32_t k = 0; k < n->n_chroms[side]; ++k) {
+        const nchrom *c = &n->chroms[side][k];
+        w.depth = 0;
+        if (c->root->fill_head) {
+            fprintf(f, "net %s %d\n", c->name, c->size);
+            for (int i = 0; i < c->root->n_fills; ++i)
+                out_fill(&w, c->root->fills[i]);
+        }
+    }
+    int bad = ferror(f);
+    if (close_it) {
+        if (fclose(f) != 0)
+            bad = 1;
+    } else {
+        fflush(f);
+        setvbuf(f, NULL, _IOLBF, 0);
+    }
+    free(buf);
+    if (bad)
+        return gac_fail(GAC_E_IO, "write error on %s", path);
+    return GAC_OK;
+}

@@ -166,12 +166,12 @@ def write_sizes(sizes: Dict[str, int], path: str) -> None:
 
 
 # ---------------------------------------------------------------- chains
-def _gap_mixture(rng, n: int) -> np.ndarray:
+def _gap_mixture(rng, n: int, p_small: float = 0.70, p_med: float = 0.28) -> np.ndarray:
     r = rng.random(n)
     small = rng.integers(1, 30, n)
     med = np.exp(rng.uniform(np.log(30), np.log(10_000), n)).astype(np.int64)
     big = np.exp(rng.uniform(np.log(10_000), np.log(1_000_000), n)).astype(np.int64)
-    return np.where(r < 0.70, small, np.where(r < 0.98, med, big)).astype(np.int64)
+    return np.where(r < p_small, small, np.where(r < p_small + p_med, med, big)).astype(np.int64)
 
 
 def _approx_gap_cost(dq: np.ndarray, dt: np.ndarray) -> np.ndarray:
@@ -194,6 +194,8 @@ class SynthConfig:
     minus_frac: float = 0.5
     spurious_frac: float = 0.2
     max_span_frac: float = 0.5
+    gap_p_small: float = 0.70   # gaps < 30 bp
+    gap_p_med: float = 0.28     # 30 bp .. 10 kb (rest: 10 kb .. 1 Mb)
     seed: int = 42
 
 
@@ -218,8 +220,8 @@ def make_chains(tgen: Genome, tname: str, qgen: Genome, cfg: SynthConfig,
     strand = (rng.random(n) < cfg.minus_frac).astype(np.uint8)
     tot = int(nb.sum())
     sizes = rng.geometric(1.0 / cfg.block_mean, tot).astype(np.int64)
-    g1 = _gap_mixture(rng, tot)
-    g2 = _gap_mixture(rng, tot)
+    g1 = _gap_mixture(rng, tot, cfg.gap_p_small, cfg.gap_p_med)
+    g2 = _gap_mixture(rng, tot, cfg.gap_p_small, cfg.gap_p_med)
     mode = rng.integers(0, 3, tot)
     dt = np.where(mode == 1, 0, g1)
     dq = np.where(mode == 0, 0, np.where(mode == 1, g1, g2))

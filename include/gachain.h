@@ -166,6 +166,62 @@ int gac_score_ranges_device(gac_ctx *ctx, const gac_chainset *cs,
                             int64_t *d_global, int64_t *d_local, int32_t *d_ali,
                             void *stream);
 
+/* ---- chainNet netting engine (host, no device needed) -------------------
+ * Replaces chainNet's netting and output (src/chainNet/chainNet.c:328-896):
+ * makeChroms/addChainT/addChainQ/fillSpace/finishNet/rOutputFill/...
+ * Same fills, gaps and .net text; no per-fill O(blocks) list rescans.  For
+ * -rescore the caller scores the partial T fills with gac_score_ranges and
+ * hands the scores to gac_net_write (subchainInfo's rescoring branch,
+ * chainNet.c:826-836).  Input arrays are borrowed and must outlive the net. */
+typedef struct gac_net gac_net;
+
+typedef struct gac_net_input {
+    int64_t n_chains;        /* in file order (chainNet requires descending score) */
+    const double *score;     /* header score */
+    const int32_t *id;       /* chain id */
+    const int32_t *t_seq;    /* index into t_names/t_sizes */
+    const int32_t *q_seq;    /* index into q_names/q_sizes */
+    const uint8_t *q_strand; /* 0 '+', 1 '-' */
+    const int32_t *t_start, *t_end, *q_start, *q_end;
+    const int64_t *blk_off;  /* [n_chains + 1] */
+    const int32_t *blk_t, *blk_q, *blk_size;
+    int32_t n_tseq;          /* target chrom.sizes, file order */
+    const char *const *t_names;
+    const int32_t *t_sizes;
+    int32_t n_qseq;          /* query chrom.sizes, file order */
+    const char *const *q_names;
+    const int32_t *q_sizes;
+} gac_net_input;
+
+typedef struct gac_net_opts {
+    int32_t min_space; /* -minSpace, default 25 */
+    int32_t min_fill;  /* -minFill, default min_space / 2 */
+    double min_score;  /* -minScore, default 2000; 0 with -rescore */
+    int32_t incl_hap;  /* -inclHap */
+} gac_net_opts;
+
+/* Net chains in order until the first one with score < min_score (error if
+ * scores increase).  Chains on *_hap* / *_alt* queries are skipped unless
+ * incl_hap. */
+int gac_net_build(const gac_net_input *in, const gac_net_opts *opts, gac_net **out);
+void gac_net_free(gac_net *net);
+/* number of input chains consumed (netted or skipped) before stopping */
+int64_t gac_net_netted(const gac_net *net);
+/* fills of one side, in .net output (pre-order) order */
+int64_t gac_net_fill_count(const gac_net *net, int side);
+/* Per fill: chain index, start, end (own side, + strand), aligned bases
+ * (subchainInfo's subSize) and flags: bit0 = partial (rescored on T with
+ * -rescore), bit1 = printed by rOutputFill under -rescore (the fill and all
+ * its ancestors have ali >= min_fill).  Any pointer may be NULL. */
+int gac_net_get_fills(const gac_net *net, int side, int32_t *chain, int32_t *start,
+                      int32_t *end, int32_t *ali, uint8_t *flags);
+/* Write one side's .net (outputNetSide) to path ("stdout" allowed) after the
+ * n_meta '#' metadata lines.  t_scores (T side only, may be NULL): per fill
+ * in gac_net_get_fills order, the rescored global score of partial fills
+ * (<= 0 prints as 1); NULL = reference's proportional approximation. */
+int gac_net_write(const gac_net *net, int side, const int64_t *t_scores, const char *path,
+                  const char *const *meta, int32_t n_meta);
+
 /* ---- device memory helpers (for callers without their own allocator) ---- */
 int gac_dev_alloc(gac_ctx *ctx, size_t bytes, void **dptr);
 int gac_dev_free(gac_ctx *ctx, void *dptr);

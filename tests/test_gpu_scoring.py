@@ -53,7 +53,8 @@ def test_long_chains_multi_tile():
     from genomealignmenttools_amd import synth
     tg = synth.random_genome({"chrT1": 3_000_000}, 11, n_frac=0.01, n_mean=300)
     qg = synth.random_genome({"q1": 2_000_000, "q2": 1_500_000}, 12, n_frac=0.01, n_mean=300)
-    cfg = synth.SynthConfig(n_chains=60, alpha=1.1, max_blocks=20_000, seed=5)
+    cfg = synth.SynthConfig(n_chains=60, alpha=1.1, max_blocks=20_000, seed=5,
+                            gap_p_small=0.97, gap_p_med=0.03)
     ca = synth.make_chains(tg, "chrT1", qg, cfg)
     assert ca.blk_off[1:].max() > 0
     e, cs = _setup(None, tg, qg, ca)
@@ -75,7 +76,7 @@ def test_edge_ranges():
     blocks = [
         [(10, 20, 1), (11, 22, 1), (40, 30, 5), (45, 35, 100), (200, 300, 1)],
         [(0, 0, 4999)],
-        [(100, 5, 33), (133, 38, 31), (170, 70, 65), (300, 100, 64), (400, 200, 129)],
+        [(100, 5, 33), (133, 38, 31), (170, 70, 65), (300, 140, 64), (400, 210, 129)],
     ]
     offs, bt, bq, bs = [0], [], [], []
     for bl in blocks:
