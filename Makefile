@@ -50,7 +50,7 @@ $(OBJDIR)/tools/lib/%.o: $(CSRC)/tools/lib/%.c $(HDRS) $(wildcard $(CSRC)/tools/
 $(BINDIR)/%: $(CSRC)/tools/%.c $(TOOL_LIB_OBJ) $(LIBDIR)/libgachain.so $(HDRS)
 	@mkdir -p $(BINDIR)
 	$(CC) $(CFLAGS) -I$(CSRC)/tools/lib $< $(TOOL_LIB_OBJ) -o $@ -L$(LIBDIR) -lgachain \
-	    -Wl,-rpath,'$$ORIGIN/../lib' -lm -lpthread
+	    -Wl,-rpath,'$$ORIGIN/../lib' -lz -lm -lpthread
 
 oracle: oracle/_build/libgacoracle.so
 

@@ -1,0 +1,260 @@
+/* chainNet -- make alignment nets out of chains (with -rescore on an MI355X).
+ *
+ * Drop-in for the reference's src/chainNet/chainNet.c (Hiller version with
+ * -rescore): same command line, options, defaults, error checks and .net
+ * output.  Netting runs on the host (libgachain gac_net_*, array-indexed,
+ * no O(fills x blocks) rescans); with -rescore every printed partial
+ * target-side fill is rescored in ONE batched GPU call (gac_score_ranges),
+ * replacing the per-fill chainSubsetOnT + chainCalcScore of subchainInfo
+ * (:795-843). */
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "gac_tool.h"
+#include "gachain.h"
+#include "host/gac_host.h"
+
+static const gt_spec k_opts[] = {
+    {"minSpace", GT_INT},      {"minFill", GT_INT},      {"minScore", GT_DOUBLE},
+    {"inclHap", GT_BOOL},      {"rescore", GT_BOOL},     {"tNibDir", GT_STRING},
+    {"qNibDir", GT_STRING},    {"scoreScheme", GT_STRING}, {"linearGap", GT_STRING},
+    {NULL, 0},
+};
+
+static void usage(int min_space, double min_score) {
+    gt_abort(
+        "chainNet - Make alignment nets out of chains (MI355X / libgachain)\n"
+        "usage:\n"
+        "   chainNet in.chain target.sizes query.sizes target.net query.net\n"
+        "where:\n"
+        "   in.chain is the chain file sorted by score\n"
+        "   target.sizes contains the size of the target sequences\n"
+        "   query.sizes contains the size of the query sequences\n"
+        "   target.net is the output over the target genome\n"
+        "   query.net is the output over the query genome\n"
+        "options:\n"
+        "   -minSpace=N - minimum gap size to fill, default %d\n"
+        "   -minFill=N  - default half of minSpace\n"
+        "   -minScore=N - minimum chain score to consider, default %.1lf\n"
+        "   -verbose=N - Alter verbosity (default 1)\n"
+        "   -inclHap - include query sequences name in the form *_hap*|*_alt*.\n"
+        "              Normally these are excluded from nets as being haplotype\n"
+        "              pseudochromosomes\n"
+        "   -rescore                    compute the real score of the sub-net (on the GPU)\n"
+        "   -tNibDir=fileName           target genome file (2bit)\n"
+        "   -qNibDir=fileName           query genome file (2bit)\n"
+        "   -scoreScheme=fileName       Read the scoring matrix from a blastz-format file\n"
+        "   -linearGap=<medium|loose|filename> Specify type of linearGap to use.\n",
+        min_space, min_score);
+}
+
+int main(int argc, char *argv[]) {
+    int min_space = 25;
+    double min_score = 2000;
+    gt_options(&argc, argv, k_opts);
+    if (argc != 6)
+        usage(min_space, min_score);
+    min_space = gt_opt_int("minSpace", min_space);
+    const int min_fill = gt_opt_int("minFill", min_space / 2);
+    min_score = gt_opt_int("minScore", (int)min_score); /* optionInt, chainNet.c:1015 */
+    const int incl_hap = gt_opt_exists("inclHap");
+    const int rescore = gt_opt_exists("rescore");
+    const char *tnib = NULL, *qnib = NULL;
+    int32_t mat[16];
+    gac_gapcalc *gap = NULL;
+    if (rescore) {
+        min_score = 0;
+        tnib = gt_opt_str("tNibDir", NULL);
+        qnib = gt_opt_str("qNibDir", NULL);
+        if (tnib == NULL)
+            gt_abort("With -rescore you must specify the target genome file (parameter -tNibDir)\n");
+        if (qnib == NULL)
+            gt_abort("With -rescore you must specify the query genome file (parameter -qNibDir)\n");
+        const char *gap_name = gt_opt_str("linearGap", NULL);
+        const char *scheme = gt_opt_str("scoreScheme", NULL);
+        if (scheme)
+            gt_verbose(1, "Reading scoring matrix from %s\n", scheme);
+        gt_check(gac_scheme_read(scheme, mat, NULL, NULL, NULL));
+        if (gap_name == NULL)
+            gt_abort("Must specify linear gap costs.  Use 'loose' or 'medium' for defaults\n");
+        gt_check(gac_gapcalc_build(gap_name, &gap));
+        gt_verbose(1, "-rescore is set: read target/query genome from %s and %s. scoreSchemeName %s. gap costs %s.\n",
+                   tnib, qnib, scheme ? scheme : "default", gap_name);
+        if (!gac_is_twobit_file(tnib) || !gac_is_twobit_file(qnib))
+            gt_abort("ERROR: only 2bit genome files are supported (got %s, %s)\n", tnib, qnib);
+    }
+    const char *chain_file = argv[1], *tsizes_file = argv[2], *qsizes_file = argv[3];
+    const char *tnet = argv[4], *qnet = argv[5];
+
+    gt_sizes qs, ts;
+    gt_read_sizes(qsizes_file, &qs);
+    gt_read_sizes(tsizes_file, &ts);
+    gt_verbose(1, "Got %d chroms in %s, %d in %s\n", ts.names.n, tsizes_file, qs.names.n,
+               qsizes_file);
+    /* open outputs like mustOpen before reading */
+    FILE *tf = gt_must_open(tnet, "w");
+    FILE *qf = gt_must_open(qnet, "w");
+    if (tf != stdout)
+        fclose(tf);
+    if (qf != stdout)
+        fclose(qf);
+
+    gt_chains c;
+    gt_read_chains(chain_file, &c, min_score, 1);
+    int32_t *tix = malloc((c.n ? c.n : 1) * 4), *qix = malloc((c.n ? c.n : 1) * 4);
+    double last = -1;
+    for (int64_t i = 0; i < c.n; ++i) {
+        if (last >= 0 && c.score[i] > last)
+            gt_abort("%s must be sorted in order of score", chain_file);
+        last = c.score[i];
+        const char *qn = c.qnames.names[c.qname[i]], *tn = c.tnames.names[c.tname[i]];
+        qix[i] = gt_names_find(&qs.names, qn);
+        if (qix[i] < 0)
+            gt_abort("hashMustFindVal: '%s' not found", qn);
+        if (qs.size[qix[i]] != c.qsize[i])
+            gt_abort("%s is %d in %s but %d in %s", qn, c.qsize[i], chain_file, qs.size[qix[i]],
+                     qsizes_file);
+        tix[i] = gt_names_find(&ts.names, tn);
+        if (tix[i] < 0)
+            gt_abort("hashMustFindVal: '%s' not found", tn);
+        if (ts.size[tix[i]] != c.tsize[i])
+            gt_abort("%s is %d in %s but %d in %s", tn, c.tsize[i], chain_file, ts.size[tix[i]],
+                     tsizes_file);
+    }
+    gac_net_input in;
+    memset(&in, 0, sizeof(in));
+    in.n_chains = c.n;
+    in.score = c.score;
+    in.id = c.id;
+    in.t_seq = tix;
+    in.q_seq = qix;
+    in.q_strand = c.qstrand;
+    in.t_start = c.tstart;
+    in.t_end = c.tend;
+    in.q_start = c.qstart;
+    in.q_end = c.qend;
+    in.blk_off = c.blk_off;
+    in.blk_t = c.bt;
+    in.blk_q = c.bq;
+    in.blk_size = c.bs;
+    in.n_tseq = ts.names.n;
+    in.t_names = (const char *const *)ts.names.names;
+    in.t_sizes = ts.size;
+    in.n_qseq = qs.names.n;
+    in.q_names = (const char *const *)qs.names.names;
+    in.q_sizes = qs.size;
+    gac_net_opts opt = {min_space, min_fill, min_score, incl_hap};
+    gac_net *net = NULL;
+    gt_check(gac_net_build(&in, &opt, &net));
+    gt_verbose(1, "Finishing nets\n");
+
+    int64_t *tscores = NULL;
+    if (rescore) {
+        const int64_t nf = gac_net_fill_count(net, GAC_T);
+        int32_t *fc = malloc((nf ? nf : 1) * 4), *fs = malloc((nf ? nf : 1) * 4),
+                *fe = malloc((nf ? nf : 1) * 4);
+        uint8_t *fl = malloc(nf ? nf : 1);
+        int32_t *fa = malloc((nf ? nf : 1) * 4);
+        gt_check(gac_net_get_fills(net, GAC_T, fc, fs, fe, fa, fl));
+        gac_range *r = malloc((nf ? nf : 1) * sizeof(gac_range));
+        int64_t *rix = malloc((nf ? nf : 1) * 8);
+        int64_t nr = 0;
+        for (int64_t i = 0; i < nf; ++i)
+            if ((fl[i] & 3) == 3) { /* partial and printed */
+                r[nr].chain = fc[i];
+                r[nr].t_start = fs[i];
+                r[nr].t_end = fe[i];
+                rix[nr++] = i;
+            }
+        tscores = calloc(nf ? nf : 1, 8);
+        if (nr) {
+            gac_ctx *ctx = NULL;
+            gt_check(gac_open(0, &ctx));
+            gt_check(gac_set_scoring(ctx, mat, gap));
+            gt_check(gac_genome_load_2bit(ctx, GAC_T, tnib));
+            gt_check(gac_genome_load_2bit(ctx, GAC_Q, qnib));
+            /* upload only the chains owning a rescored fill (their sequences
+             * must be in the 2bit files; others are never looked up) */
+            int32_t *remap = malloc(c.n * 4);
+            for (int64_t i = 0; i < c.n; ++i)
+                remap[i] = -1;
+            int64_t nsub = 0, nbsub = 0;
+            for (int64_t k = 0; k < nr; ++k)
+                if (remap[r[k].chain] < 0) {
+                    remap[r[k].chain] = (int32_t)nsub++;
+                    nbsub += c.blk_off[r[k].chain + 1] - c.blk_off[r[k].chain];
+                }
+            int32_t *gts = malloc(nsub * 4), *gqs = malloc(nsub * 4);
+            uint8_t *gst = malloc(nsub);
+            int64_t *goff = malloc((nsub + 1) * 8);
+            int32_t *gbt = malloc((nbsub ? nbsub : 1) * 4), *gbq = malloc((nbsub ? nbsub : 1) * 4),
+                    *gbs = malloc((nbsub ? nbsub : 1) * 4);
+            int64_t *src = malloc(nsub * 8);
+            for (int64_t i = 0; i < c.n; ++i)
+                if (remap[i] >= 0)
+                    src[remap[i]] = i;
+            goff[0] = 0;
+            for (int64_t j = 0; j < nsub; ++j) {
+                const int64_t i = src[j];
+                const char *tn = c.tnames.names[c.tname[i]], *qn = c.qnames.names[c.qname[i]];
+                gts[j] = gac_genome_seq_index(ctx, GAC_T, tn);
+                if (gts[j] < 0)
+                    gt_abort("%s is not in %s", tn, tnib);
+                gqs[j] = gac_genome_seq_index(ctx, GAC_Q, qn);
+                if (gqs[j] < 0)
+                    gt_abort("%s is not in %s", qn, qnib);
+                gst[j] = c.qstrand[i];
+                const int64_t b0 = c.blk_off[i], nb = c.blk_off[i + 1] - b0;
+                memcpy(gbt + goff[j], c.bt + b0, nb * 4);
+                memcpy(gbq + goff[j], c.bq + b0, nb * 4);
+                memcpy(gbs + goff[j], c.bs + b0, nb * 4);
+                goff[j + 1] = goff[j] + nb;
+            }
+            for (int64_t k = 0; k < nr; ++k)
+                r[k].chain = remap[r[k].chain];
+            gac_chainset_desc d = {nsub, gts, gqs, gst, goff, nbsub, gbt, gbq, gbs};
+            gac_chainset *cs = NULL;
+            gt_check(gac_chains_upload(ctx, &d, &cs));
+            int64_t *g = malloc(nr * 8);
+            int32_t *ali = malloc(nr * 4);
+            gt_check(gac_score_ranges(ctx, cs, r, nr, 0, g, NULL, ali));
+            for (int64_t k = 0; k < nr; ++k)
+                tscores[rix[k]] = g[k];
+            free(g);
+            free(ali);
+            free(gts);
+            free(gqs);
+            free(gst);
+            free(goff);
+            free(gbt);
+            free(gbq);
+            free(gbs);
+            free(src);
+            free(remap);
+            gac_chains_free(cs);
+            gac_close(ctx);
+        }
+        free(fc);
+        free(fs);
+        free(fe);
+        free(fl);
+        free(fa);
+        free(r);
+        free(rix);
+    }
+    gt_verbose(1, "writing %s\n", tnet);
+    gt_check(gac_net_write(net, GAC_T, tscores, tnet, (const char *const *)c.meta, c.n_meta));
+    gt_verbose(1, "writing %s\n", qnet);
+    gt_check(gac_net_write(net, GAC_Q, NULL, qnet, (const char *const *)c.meta, c.n_meta));
+    free(tscores);
+    gac_net_free(net);
+    gac_gapcalc_free(gap);
+    gt_chains_free(&c);
+    gt_sizes_free(&qs);
+    gt_sizes_free(&ts);
+    free(tix);
+    free(qix);
+    return 0;
+}

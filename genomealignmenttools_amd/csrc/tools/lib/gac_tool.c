@@ -1,0 +1,549 @@
+/* gac_tool.c -- shared host code of the drop-in CLI tools (see gac_tool.h). */
+#define _GNU_SOURCE
+#include "gac_tool.h"
+#include "host/gac_host.h"
+
+#include <ctype.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+#include <zlib.h>
+
+/* ------------------------------------------------------------ errors */
+static int g_verbose = 1;
+
+void gt_abort(const char *fmt, ...) {
+    va_list ap;
+    fflush(stdout);
+    va_start(ap, fmt);
+    vfprintf(stderr, fmt, ap);
+    va_end(ap);
+    size_t n = strlen(fmt);
+    if (n == 0 || fmt[n - 1] != '\n')
+        fputc('\n', stderr);
+    exit(255); /* errAbort -> exit(-1) */
+}
+
+void gt_verbose(int level, const char *fmt, ...) {
+    if (level > g_verbose)
+        return;
+    va_list ap;
+    va_start(ap, fmt);
+    vfprintf(stderr, fmt, ap);
+    va_end(ap);
+}
+
+int gt_verbosity(void) { return g_verbose; }
+
+void gt_check(int rc) {
+    if (rc != GAC_OK)
+        gt_abort("%s", gac_last_error());
+}
+
+/* ------------------------------------------------------------ options */
+typedef struct gt_optval {
+    char *name, *val;
+} gt_optval;
+static gt_optval *g_opts;
+static int g_nopts, g_capopts;
+
+static const gt_spec *spec_find(const gt_spec *spec, const char *name) {
+    for (; spec && spec->name; ++spec)
+        if (strcmp(spec->name, name) == 0)
+            return spec;
+    return NULL;
+}
+
+static void validate(const gt_spec *spec, const char *name, const char *val) {
+    static const gt_spec common[] = {{"verbose", GT_INT}, {NULL, 0}};
+    const gt_spec *s = spec_find(spec, name);
+    if (!s)
+        s = spec_find(common, name);
+    if (!s)
+        gt_abort("-%s is not a valid option", name);
+    char *end;
+    switch (s->type) {
+    case GT_BOOL:
+        if (val)
+            gt_abort("boolean option -%s must not have value", name);
+        break;
+    case GT_STRING:
+        if (!val)
+            gt_abort("string option -%s must have a value", name);
+        break;
+    case GT_INT:
+        if (!val)
+            gt_abort("int option -%s must have a value", name);
+        (void)strtol(val, &end, 10);
+        if (*val == 0 || *end != 0)
+            gt_abort("value of -%s is not a valid integer: \"%s\"", name, val);
+        break;
+    case GT_DOUBLE:
+        if (!val)
+            gt_abort("double option -%s must have a value", name);
+        (void)strtod(val, &end);
+        if (*val == 0 || *end != 0)
+            gt_abort("value of -%s is not a valid double: \"%s\"", name, val);
+        break;
+    }
+}
+
+/* parseAnOption (kent/src/lib/options.c:121-190) */
+static int parse_one(const gt_spec *spec, char *arg) {
+    char *eq = strchr(arg, '=');
+    if (!(eq || arg[0] == '-'))
+        return 0;
+    if (arg[0] == '-' && (arg[1] == 0 || isspace((unsigned char)arg[1])))
+        return 0;
+    if (eq) {
+        for (char *s = arg; s < eq; ++s)
+            if (*s != '_' && *s != '-' && !isalnum((unsigned char)*s))
+                return 0;
+    }
+    char *name = arg[0] == '-' ? arg + 1 : arg;
+    char *val = NULL;
+    if (eq) {
+        *eq = 0;
+        val = eq + 1;
+    }
+    validate(spec, name, val);
+    if (g_nopts == g_capopts) {
+        g_capopts = g_capopts ? g_capopts * 2 : 16;
+        g_opts = realloc(g_opts, g_capopts * sizeof(gt_optval));
+    }
+    g_opts[g_nopts].name = strdup(name);
+    g_opts[g_nopts].val = strdup(val ? val : "on");
+    ++g_nopts;
+    if (eq)
+        *eq = '=';
+    return 1;
+}
+
+void gt_options(int *argc, char **argv, const gt_spec *spec) {
+    int orig = *argc, n = 1, i;
+    char **rd = argv + 1, **wr = argv + 1;
+    for (i = 1; i < orig; ++i) {
+        if (strcmp(*rd, "--") == 0) {
+            rd++;
+            i++;
+            break;
+        }
+        if (!parse_one(spec, *rd)) {
+            *wr++ = *rd;
+            n++;
+        }
+        rd++;
+    }
+    for (; i < orig; ++i) {
+        *wr++ = *rd++;
+        n++;
+    }
+    *argc = n;
+    *wr = NULL;
+    g_verbose = gt_opt_int("verbose", 1);
+}
+
+const char *gt_opt_str(const char *name, const char *def) {
+    for (int i = g_nopts - 1; i >= 0; --i) /* last occurrence wins */
+        if (strcmp(g_opts[i].name, name) == 0)
+            return g_opts[i].val;
+    return def;
+}
+
+int gt_opt_exists(const char *name) { return gt_opt_str(name, NULL) != NULL; }
+
+/* optionInt (kent/src/lib/options.c:359-378) */
+int gt_opt_int(const char *name, int def) {
+    const char *s = gt_opt_str(name, NULL);
+    if (!s || strcmp(s, "on") == 0)
+        return def;
+    char *end;
+    long v = strtol(s, &end, 10);
+    if (*s == 0 || *end != 0)
+        gt_abort("value of -%s is not a valid integer: \"%s\"", name, s);
+    return (int)v;
+}
+
+/* ------------------------------------------------------------ names */
+static uint32_t hash_str(const char *s, size_t n) {
+    uint32_t h = 2166136261u;
+    for (size_t i = 0; i < n; ++i)
+        h = (h ^ (uint8_t)s[i]) * 16777619u;
+    return h;
+}
+
+static void names_rehash(gt_names *t, int32_t nslot) {
+    free(t->slots);
+    t->nslot = nslot;
+    t->slots = malloc(nslot * sizeof(int32_t));
+    memset(t->slots, 0xff, nslot * sizeof(int32_t));
+    for (int32_t i = 0; i < t->n; ++i) {
+        uint32_t h = hash_str(t->names[i], strlen(t->names[i])) & (nslot - 1);
+        while (t->slots[h] >= 0)
+            h = (h + 1) & (nslot - 1);
+        t->slots[h] = i;
+    }
+}
+
+int32_t gt_names_find(const gt_names *t, const char *s) {
+    if (!t->nslot)
+        return -1;
+    size_t n = strlen(s);
+    uint32_t h = hash_str(s, n) & (t->nslot - 1);
+    while (t->slots[h] >= 0) {
+        if (strcmp(t->names[t->slots[h]], s) == 0)
+            return t->slots[h];
+        h = (h + 1) & (t->nslot - 1);
+    }
+    return -1;
+}
+
+int32_t gt_names_add(gt_names *t, const char *s, size_t len) {
+    if (t->nslot) {
+        uint32_t h = hash_str(s, len) & (t->nslot - 1);
+        while (t->slots[h] >= 0) {
+            const char *x = t->names[t->slots[h]];
+            if (strncmp(x, s, len) == 0 && x[len] == 0)
+                return t->slots[h];
+            h = (h + 1) & (t->nslot - 1);
+        }
+    }
+    if (t->n == t->cap) {
+        t->cap = t->cap ? t->cap * 2 : 64;
+        t->names = realloc(t->names, t->cap * sizeof(char *));
+    }
+    t->names[t->n] = strndup(s, len);
+    int32_t id = t->n++;
+    if (t->n * 2 > t->nslot)
+        names_rehash(t, t->nslot ? t->nslot * 2 : 256);
+    else {
+        uint32_t h = hash_str(s, len) & (t->nslot - 1);
+        while (t->slots[h] >= 0)
+            h = (h + 1) & (t->nslot - 1);
+        t->slots[h] = id;
+    }
+    return id;
+}
+
+void gt_names_free(gt_names *t) {
+    for (int32_t i = 0; i < t->n; ++i)
+        free(t->names[i]);
+    free(t->names);
+    free(t->slots);
+    memset(t, 0, sizeof(*t));
+}
+
+/* ------------------------------------------------------------ files */
+FILE *gt_must_open(const char *path, const char *mode) {
+    if (strcmp(path, "stdout") == 0)
+        return stdout;
+    if (strcmp(path, "stdin") == 0)
+        return stdin;
+    FILE *f = fopen(path, mode);
+    if (!f)
+        gt_abort("Can't open %s to %s: %s", path, mode[0] == 'w' ? "write" : "read",
+                 strerror(errno));
+    return f;
+}
+
+void gt_careful_close(FILE *f, const char *path) {
+    if (f == stdout || f == stdin) {
+        if (fflush(f) != 0)
+            gt_abort("write error on %s", path);
+        return;
+    }
+    if (fclose(f) != 0)
+        gt_abort("close failed on %s", path);
+}
+
+int gt_file_exists(const char *path) {
+    struct stat st;
+    return strcmp(path, "stdin") == 0 || stat(path, &st) == 0;
+}
+
+/* whole file into a NUL-terminated heap buffer (.gz decompressed) */
+static char *slurp(const char *path, size_t *len) {
+    size_t n = strlen(path);
+    int gz = n > 3 && strcmp(path + n - 3, ".gz") == 0;
+    size_t cap = 1 << 20, l = 0;
+    char *buf = NULL;
+    if (gz) {
+        gzFile g = gzopen(path, "rb");
+        if (!g)
+            gt_abort("Couldn't open %s , %s", path, strerror(errno));
+        gzbuffer(g, 1 << 20);
+        buf = malloc(cap + 1);
+        for (;;) {
+            if (l == cap) {
+                cap *= 2;
+                buf = realloc(buf, cap + 1);
+            }
+            int r = gzread(g, buf + l, (unsigned)((cap - l) > (1u << 30) ? (1u << 30) : (cap - l)));
+            if (r < 0)
+                gt_abort("gzip read error on %s", path);
+            if (r == 0)
+                break;
+            l += (size_t)r;
+        }
+        gzclose(g);
+    } else {
+        int fd = strcmp(path, "stdin") == 0 ? 0 : open(path, O_RDONLY);
+        if (fd < 0)
+            gt_abort("Couldn't open %s , %s", path, strerror(errno));
+        struct stat st;
+        if (fd != 0 && fstat(fd, &st) == 0 && S_ISREG(st.st_mode))
+            cap = (size_t)st.st_size + 1;
+        buf = malloc(cap + 1);
+        for (;;) {
+            if (l == cap) {
+                cap *= 2;
+                buf = realloc(buf, cap + 1);
+            }
+            ssize_t r = read(fd, buf + l, cap - l);
+            if (r < 0)
+                gt_abort("read error on %s", path);
+            if (r == 0)
+                break;
+            l += (size_t)r;
+        }
+        if (fd != 0)
+            close(fd);
+    }
+    buf[l] = 0;
+    *len = l;
+    return buf;
+}
+
+/* ------------------------------------------------------------ chains */
+typedef struct lf {
+    char *cur, *end;
+    const char *path;
+    int line;
+    gt_chains *meta_to;
+} lf;
+
+static char *lf_next(lf *f) {
+    if (f->cur >= f->end)
+        return NULL;
+    char *line = f->cur;
+    char *nl = memchr(line, '\n', f->end - line);
+    if (nl) {
+        *nl = 0;
+        f->cur = nl + 1;
+    } else {
+        f->cur = f->end;
+    }
+    ++f->line;
+    return line;
+}
+
+static void add_meta(gt_chains *c, const char *line) {
+    if (c->n_meta == c->meta_cap) {
+        c->meta_cap = c->meta_cap ? c->meta_cap * 2 : 16;
+        c->meta = realloc(c->meta, c->meta_cap * sizeof(char *));
+    }
+    c->meta[c->n_meta++] = strdup(line);
+}
+
+/* lineFileChopNext: next non-blank, non-'#' line chopped into <= max words */
+static int lf_chop(lf *f, char **row, int max) {
+    char *line;
+    while ((line = lf_next(f)) != NULL) {
+        if (line[0] == '#') {
+            if (f->meta_to)
+                add_meta(f->meta_to, line);
+            continue;
+        }
+        int n = gac_chop_white(line, row, max);
+        if (n)
+            return n;
+    }
+    return 0;
+}
+
+static int need_num(lf *f, char **row, int ix) {
+    char c = row[ix][0];
+    if (c != '-' && !isdigit((unsigned char)c))
+        gt_abort("Expecting number field %d line %d of %s, got %s", ix + 1, f->line, f->path,
+                 row[ix]);
+    return atoi(row[ix]);
+}
+
+#define GROW(ptr, cap, n, type)                                   \
+    do {                                                          \
+        if ((n) >= (cap)) {                                       \
+            (cap) = (cap) ? (cap) * 2 : 1024;                      \
+            (ptr) = realloc((ptr), (size_t)(cap) * sizeof(type)); \
+        }                                                         \
+    } while (0)
+
+static void chains_reserve(gt_chains *c) {
+    if (c->n + 1 >= c->cap) {
+        int64_t cap = c->cap ? c->cap * 2 : 4096;
+        c->score = realloc(c->score, cap * sizeof(double));
+        c->tname = realloc(c->tname, cap * 4);
+        c->tsize = realloc(c->tsize, cap * 4);
+        c->tstart = realloc(c->tstart, cap * 4);
+        c->tend = realloc(c->tend, cap * 4);
+        c->qname = realloc(c->qname, cap * 4);
+        c->qsize = realloc(c->qsize, cap * 4);
+        c->qstart = realloc(c->qstart, cap * 4);
+        c->qend = realloc(c->qend, cap * 4);
+        c->qstrand = realloc(c->qstrand, cap);
+        c->id = realloc(c->id, cap * 4);
+        c->blk_off = realloc(c->blk_off, (cap + 1) * 8);
+        c->cap = cap;
+    }
+}
+
+static int g_next_id = 1; /* chainIdNext (chain.c:180-198) */
+
+void gt_read_chains(const char *path, gt_chains *c, double stop_below, int keep_meta) {
+    memset(c, 0, sizeof(*c));
+    size_t len;
+    char *buf = slurp(path, &len);
+    lf f = {buf, buf + len, path, 0, keep_meta ? c : NULL};
+    c->blk_off = malloc(8);
+    c->blk_off[0] = 0;
+    char *row[13];
+    for (;;) {
+        int wc = lf_chop(&f, row, 13);
+        if (wc == 0)
+            break;
+        if (wc < 12)
+            gt_abort("Expecting at least 12 words line %d of %s", f.line, path);
+        if (strcmp(row[0], "chain") != 0)
+            gt_abort("Expecting 'chain' line %d of %s", f.line, path);
+        chains_reserve(c);
+        int64_t i = c->n;
+        c->score[i] = atof(row[1]);
+        c->tname[i] = gt_names_add(&c->tnames, row[2], strlen(row[2]));
+        c->tsize[i] = need_num(&f, row, 3);
+        c->id[i] = wc >= 13 ? need_num(&f, row, 12) : g_next_id++;
+        c->tstart[i] = need_num(&f, row, 5);
+        c->tend[i] = need_num(&f, row, 6);
+        c->qname[i] = gt_names_add(&c->qnames, row[7], strlen(row[7]));
+        c->qsize[i] = need_num(&f, row, 8);
+        c->qstrand[i] = row[9][0] == '-' ? 1 : 0;
+        c->qstart[i] = need_num(&f, row, 10);
+        c->qend[i] = need_num(&f, row, 11);
+        if (c->qstart[i] >= c->qend[i] || c->tstart[i] >= c->tend[i])
+            gt_abort("End before start line %d of %s", f.line, path);
+        if (c->qstart[i] < 0 || c->tstart[i] < 0)
+            gt_abort("Start before zero line %d of %s", f.line, path);
+        if (c->qend[i] > c->qsize[i] || c->tend[i] > c->tsize[i])
+            gt_abort("Past end of sequence line %d of %s", f.line, path);
+        /* chainReadBlocks (chain.c:301-335) */
+        int q = c->qstart[i], t = c->tstart[i];
+        int64_t nb0 = c->nb;
+        for (;;) {
+            char *brow[3];
+            int bw = lf_chop(&f, brow, 3);
+            if (bw == 0)
+                gt_abort("Unexpected end of file in %s", path);
+            int size = need_num(&f, brow, 0);
+            if (c->nb + 1 >= c->bcap) {
+                c->bcap = c->bcap ? c->bcap * 2 : 1 << 16;
+                c->bt = realloc(c->bt, c->bcap * 4);
+                c->bq = realloc(c->bq, c->bcap * 4);
+                c->bs = realloc(c->bs, c->bcap * 4);
+            }
+            c->bt[c->nb] = t;
+            c->bq[c->nb] = q;
+            c->bs[c->nb] = size;
+            c->nb++;
+            q += size;
+            t += size;
+            if (bw == 1)
+                break;
+            if (bw < 3)
+                gt_abort("Expecting 1 or 3 words line %d of %s\n", f.line, path);
+            t += need_num(&f, brow, 1);
+            q += need_num(&f, brow, 2);
+        }
+        if (q != c->qend[i])
+            gt_abort("q end mismatch %d vs %d line %d of %s\n", q, c->qend[i], f.line, path);
+        if (t != c->tend[i])
+            gt_abort("t end mismatch %d vs %d line %d of %s\n", t, c->tend[i], f.line, path);
+        if (c->score[i] < stop_below) { /* read, not kept (chainNet.c:949-952) */
+            c->nb = nb0;
+            break;
+        }
+        c->n++;
+        c->blk_off[c->n] = c->nb;
+    }
+    free(buf);
+}
+
+void gt_chains_free(gt_chains *c) {
+    free(c->score);
+    free(c->tname);
+    free(c->tsize);
+    free(c->tstart);
+    free(c->tend);
+    free(c->qname);
+    free(c->qsize);
+    free(c->qstart);
+    free(c->qend);
+    free(c->qstrand);
+    free(c->id);
+    free(c->blk_off);
+    free(c->bt);
+    free(c->bq);
+    free(c->bs);
+    gt_names_free(&c->tnames);
+    gt_names_free(&c->qnames);
+    for (int32_t i = 0; i < c->n_meta; ++i)
+        free(c->meta[i]);
+    free(c->meta);
+    memset(c, 0, sizeof(*c));
+}
+
+int gt_next_chain_id(void) { return g_next_id++; }
+
+void gt_write_chain(FILE *f, const gt_chains *c, int64_t i, double score, int32_t id) {
+    fprintf(f, "chain %1.0f %s %d + %d %d %s %d %c %d %d %d\n", score, c->tnames.names[c->tname[i]],
+            c->tsize[i], c->tstart[i], c->tend[i], c->qnames.names[c->qname[i]], c->qsize[i],
+            c->qstrand[i] ? '-' : '+', c->qstart[i], c->qend[i], id);
+    const int64_t b0 = c->blk_off[i], b1 = c->blk_off[i + 1];
+    for (int64_t b = b0; b < b1; ++b) {
+        if (b + 1 < b1)
+            fprintf(f, "%d\t%d\t%d\n", c->bs[b], c->bt[b + 1] - (c->bt[b] + c->bs[b]),
+                    c->bq[b + 1] - (c->bq[b] + c->bs[b]));
+        else
+            fprintf(f, "%d\n", c->bs[b]);
+    }
+    fputc('\n', f);
+}
+
+/* ------------------------------------------------------------ sizes */
+void gt_read_sizes(const char *path, gt_sizes *s) {
+    memset(s, 0, sizeof(*s));
+    size_t len;
+    char *buf = slurp(path, &len);
+    lf f = {buf, buf + len, path, 0, NULL};
+    int32_t cap = 0;
+    char *row[3];
+    int wc;
+    while ((wc = lf_chop(&f, row, 3)) != 0) {
+        if (wc != 2)
+            gt_abort("Expecting 2 words line %d of %s got %d", f.line, path, wc);
+        if (gt_names_find(&s->names, row[0]) >= 0)
+            gt_abort("Duplicate %s in %s", row[0], path);
+        int32_t id = gt_names_add(&s->names, row[0], strlen(row[0]));
+        GROW(s->size, cap, id, int32_t);
+        s->size[id] = need_num(&f, row, 1);
+    }
+    free(buf);
+}
+
+void gt_sizes_free(gt_sizes *s) {
+    gt_names_free(&s->names);
+    free(s->size);
+    memset(s, 0, sizeof(*s));
+}

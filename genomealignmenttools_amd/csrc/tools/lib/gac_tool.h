@@ -1,0 +1,87 @@
+/* gac_tool.h -- shared host code of the drop-in CLI tools (C11):
+ * kent-compatible option parsing (kent/src/lib/options.c:121-378),
+ * errAbort semantics (message to stderr, exit 255; kent/src/lib/errAbort.c),
+ * .chain reading/writing (kent/src/lib/chain.c:200-346) and chrom.sizes. */
+#ifndef GAC_TOOL_H
+#define GAC_TOOL_H
+
+#include <stdint.h>
+#include <stdio.h>
+
+#include "gachain.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+void gt_abort(const char *fmt, ...) __attribute__((noreturn, format(printf, 1, 2)));
+void gt_verbose(int level, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+int gt_verbosity(void);
+void gt_check(int rc); /* abort with gac_last_error() unless GAC_OK */
+
+/* ---- options ---- */
+enum { GT_BOOL, GT_INT, GT_DOUBLE, GT_STRING };
+typedef struct gt_spec {
+    const char *name;
+    int type;
+} gt_spec;
+/* Parse and remove options from argv (kent optionInit); "verbose" is always
+ * accepted.  Unknown options abort. */
+void gt_options(int *argc, char **argv, const gt_spec *spec);
+const char *gt_opt_str(const char *name, const char *def);
+int gt_opt_exists(const char *name);
+int gt_opt_int(const char *name, int def);
+
+/* ---- string table ---- */
+typedef struct gt_names {
+    char **names;
+    int32_t n, cap;
+    int32_t *slots;  /* open addressing, -1 = empty */
+    int32_t nslot;
+} gt_names;
+int32_t gt_names_add(gt_names *t, const char *s, size_t len);
+int32_t gt_names_find(const gt_names *t, const char *s);
+void gt_names_free(gt_names *t);
+
+/* ---- chains (struct of arrays) ---- */
+typedef struct gt_chains {
+    int64_t n, cap;
+    double *score;
+    int32_t *tname, *tsize, *tstart, *tend; /* tname: index into tnames */
+    int32_t *qname, *qsize, *qstart, *qend;
+    uint8_t *qstrand;
+    int32_t *id;
+    int64_t *blk_off; /* n + 1 */
+    int64_t nb, bcap;
+    int32_t *bt, *bq, *bs;
+    gt_names tnames, qnames;
+    char **meta; /* '#' lines in order */
+    int32_t n_meta, meta_cap;
+} gt_chains;
+
+/* stop_below: stop after reading the first chain whose score is < stop_below
+ * (that chain is read, like chainNet's loop, but not kept); pass -HUGE_VAL
+ * to read everything.  Reads .gz transparently, "stdin" allowed. */
+void gt_read_chains(const char *path, gt_chains *c, double stop_below, int keep_meta);
+void gt_chains_free(gt_chains *c);
+/* chainIdNext (chain.c:180-198): the shared "next id" counter */
+int gt_next_chain_id(void);
+/* chainWrite (chain.c:200-227) of chain i with the given score and id */
+void gt_write_chain(FILE *f, const gt_chains *c, int64_t i, double score, int32_t id);
+
+/* ---- chrom.sizes ---- */
+typedef struct gt_sizes {
+    gt_names names;
+    int32_t *size;
+} gt_sizes;
+void gt_read_sizes(const char *path, gt_sizes *s);
+void gt_sizes_free(gt_sizes *s);
+
+FILE *gt_must_open(const char *path, const char *mode);
+void gt_careful_close(FILE *f, const char *path);
+int gt_file_exists(const char *path);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,143 @@
+/* scoreChain -- (re)score existing chains on an MI355X.
+ *
+ * Drop-in for the reference's src/scoreChain/scoreChain.c: same command
+ * line, options and output formats (chain, -returnOnlyScore,
+ * -returnOnlyScoreAndCoords; :42-79, :301-331).  Genomes are loaded once,
+ * resident 2-bit packed on the GPU; every chain's global score
+ * (chainCalcScore), local score (chainCalcScoreLocal, :176-198) and aligned
+ * bases are computed in one batched GPU call (gac_score_ranges). */
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "gac_tool.h"
+#include "gachain.h"
+#include "host/gac_host.h"
+
+static const gt_spec k_opts[] = {
+    {"scoreScheme", GT_STRING},
+    {"linearGap", GT_STRING},
+    {"doLocalScore", GT_BOOL},
+    {"forceLocalScore", GT_BOOL},
+    {"returnOnlyScore", GT_BOOL},
+    {"returnOnlyScoreAndCoords", GT_BOOL},
+    {NULL, 0},
+};
+
+static void usage(void) {
+    gt_abort(
+        "scoreChain - (re)score existing chains (MI355X / libgachain)\n"
+        "usage:\n"
+        "   scoreChain in.chainFile reference.2bit query.2bit out.chain  -linearGap=loose|medium|filename\n"
+        "Where reference.2bit and query.2bit are the names of a .2bit files for the reference and query\n"
+        "options:\n"
+        " Local score = we set score = 0 if score < 0 and return the max of the score that we reach for a chain\n"
+        "   -returnOnlyScore             default=FALSE. Just return chain ID{tab}globalScore{tab}localScore{tab}totalAligningBases, not the entire chain\n"
+        "   -returnOnlyScoreAndCoords    default=FALSE. Just return chain ID{tab}chainStartInRef{tab}chainEndInRef{tab}localScore{tab}totalAligningBases, not the entire chain\n"
+        "   -doLocalScore                default=FALSE. Only if the global score of a chain is negative, compute and output the local score in the chain file.\n"
+        "   -forceLocalScore             default=FALSE. Always output the local score in the chain file.\n"
+        "   -scoreScheme=fileName        Read the scoring matrix from a blastz-format file\n"
+        "   -linearGap=<medium|loose|filename>    Specify type of linearGap to use.\n"
+        "              *Must* specify this argument to one of these choices.\n");
+}
+
+int main(int argc, char *argv[]) {
+    gt_options(&argc, argv, k_opts);
+    const char *gap_name = gt_opt_str("linearGap", NULL);
+    const char *scheme_name = gt_opt_str("scoreScheme", NULL);
+    const int do_local = gt_opt_exists("doLocalScore");
+    const int force_local = gt_opt_exists("forceLocalScore");
+    const int only_score = gt_opt_exists("returnOnlyScore");
+    const int only_coords = gt_opt_exists("returnOnlyScoreAndCoords");
+    if (argc != 5)
+        usage();
+    if (only_score && only_coords)
+        gt_abort("ERROR: You cannot specify both returnOnlyScore and returnOnlyScoreAndCoords\n");
+
+    int32_t mat[16];
+    gt_check(gac_scheme_read(scheme_name, mat, NULL, NULL, NULL));
+    if (gap_name == NULL)
+        gt_abort("Must specify linear gap costs.  Use 'loose' or 'medium' for defaults\n");
+    gac_gapcalc *gap = NULL;
+    gt_check(gac_gapcalc_build(gap_name, &gap));
+
+    const char *t2bit = argv[2], *q2bit = argv[3];
+    if (!gt_file_exists(t2bit))
+        gt_abort("ERROR: target 2bit file or nib directory %s does not exist\n", t2bit);
+    if (!gt_file_exists(q2bit))
+        gt_abort("ERROR: query 2bit file or nib directory %s does not exist\n", q2bit);
+    if (!gac_is_twobit_file(t2bit))
+        gt_abort("ERROR: only 2bit files are supported, not %s\n", t2bit);
+    if (!gac_is_twobit_file(q2bit))
+        gt_abort("ERROR: only 2bit files are supported, not %s\n", q2bit);
+
+    gac_ctx *ctx = NULL;
+    gt_check(gac_open(0, &ctx));
+    gt_check(gac_set_scoring(ctx, mat, gap));
+    gt_check(gac_genome_load_2bit(ctx, GAC_T, t2bit));
+    gt_check(gac_genome_load_2bit(ctx, GAC_Q, q2bit));
+
+    FILE *out = gt_must_open(argv[4], "w");
+    gt_chains c;
+    gt_read_chains(argv[1], &c, -HUGE_VAL, 0);
+
+    /* resolve sequence names (twoBitReadSeqFrag aborts on unknown names) */
+    int32_t *tseq = malloc((c.n ? c.n : 1) * 4), *qseq = malloc((c.n ? c.n : 1) * 4);
+    for (int64_t i = 0; i < c.n; ++i) {
+        tseq[i] = gac_genome_seq_index(ctx, GAC_T, c.tnames.names[c.tname[i]]);
+        if (tseq[i] < 0)
+            gt_abort("%s is not in %s", c.tnames.names[c.tname[i]], t2bit);
+        qseq[i] = gac_genome_seq_index(ctx, GAC_Q, c.qnames.names[c.qname[i]]);
+        if (qseq[i] < 0)
+            gt_abort("%s is not in %s", c.qnames.names[c.qname[i]], q2bit);
+    }
+    gac_chainset_desc d = {c.n, tseq, qseq, c.qstrand, c.blk_off, c.nb, c.bt, c.bq, c.bs};
+    gac_chainset *cs = NULL;
+    gt_check(gac_chains_upload(ctx, &d, &cs));
+    gac_range *r = malloc((c.n ? c.n : 1) * sizeof(gac_range));
+    for (int64_t i = 0; i < c.n; ++i) {
+        r[i].chain = (int32_t)i;
+        r[i].t_start = c.tstart[i];
+        r[i].t_end = c.tend[i];
+    }
+    int64_t *glob = malloc((c.n ? c.n : 1) * 8), *loc = malloc((c.n ? c.n : 1) * 8);
+    int32_t *ali = malloc((c.n ? c.n : 1) * 4);
+    gt_check(gac_score_ranges(ctx, cs, r, c.n, GAC_WANT_LOCAL, glob, loc, ali));
+
+    static char obuf[1 << 22];
+    setvbuf(out, obuf, _IOFBF, sizeof(obuf));
+    for (int64_t i = 0; i < c.n; ++i) {
+        const double g = (double)glob[i], l = (double)loc[i];
+        double score;
+        if (force_local) {
+            score = l;
+        } else {
+            score = g;
+            if (score <= 0 && do_local)
+                score = l;
+        }
+        int32_t id = c.id[i];
+        if (only_score) {
+            fprintf(out, "%d\t%1.0f\t%1.0f\t%d\n", id, g, l, ali[i]);
+        } else if (only_coords) {
+            fprintf(out, "%d\t%d\t%d\t%1.0f\t%1.0f\t%d\n", id, c.tstart[i], c.tend[i], g, l, ali[i]);
+        } else {
+            if (id == 0) /* chainWriteHead assigns an id (chain.c:203-204) */
+                id = gt_next_chain_id();
+            gt_write_chain(out, &c, i, score, id);
+        }
+    }
+    gt_careful_close(out, argv[4]);
+    free(r);
+    free(glob);
+    free(loc);
+    free(ali);
+    free(tseq);
+    free(qseq);
+    gac_chains_free(cs);
+    gac_gapcalc_free(gap);
+    gt_chains_free(&c);
+    gac_close(ctx);
+    return 0;
+}

@@ -1,0 +1,107 @@
+"""GPU end-to-end parity of the drop-in tools against the reference's own
+outputs (tests/golden, generated with the tools compiled from
+/root/reference): byte-identical files."""
+import filecmp
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import BLASTZ, GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _bin(name):
+    from genomealignmenttools_amd._lib import BIN_DIR
+    return os.path.join(BIN_DIR, name)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    return r
+
+
+@pytest.mark.parametrize("case", ["newStyleLastz", "oldStyleBlastz"])
+@pytest.mark.parametrize("gap", ["loose", "medium"])
+@pytest.mark.parametrize("mode,flag", [("score", "-returnOnlyScore"),
+                                       ("coords", "-returnOnlyScoreAndCoords"),
+                                       ("chain", None), ("local", "-forceLocalScore")])
+def test_scorechain_chrM(case, gap, mode, flag, tmp_path):
+    d = os.path.join(GOLDEN, "chrM")
+    out = tmp_path / "out"
+    cmd = [_bin("scoreChain"), os.path.join(d, f"{case}.chain"), os.path.join(d, "hg19.chrM.2bit"),
+           os.path.join(d, "susScr3.chrM.2bit"), str(out), f"-linearGap={gap}",
+           f"-scoreScheme={os.path.join(d, case + '.Q.txt')}"]
+    if flag:
+        cmd.append(flag)
+    _run(cmd)
+    assert filecmp.cmp(out, os.path.join(d, f"{case}.{gap}.{mode}.out"), shallow=False)
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_scorechain_synth(seed, tmp_path):
+    d = os.path.join(GOLDEN, f"synth{seed}")
+    p = lambda x: os.path.join(d, x)
+    _run([_bin("scoreChain"), p("in.chain"), p("t.2bit"), p("q.2bit"), str(tmp_path / "a"),
+          "-linearGap=loose", "-returnOnlyScoreAndCoords"])
+    assert filecmp.cmp(tmp_path / "a", p("score.out"), shallow=False)
+    _run([_bin("scoreChain"), p("in.chain"), p("t.2bit"), p("q.2bit"), str(tmp_path / "b"),
+          "-linearGap=medium", "-doLocalScore"])
+    assert filecmp.cmp(tmp_path / "b", p("rescored.chain"), shallow=False)
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_chainnet_rescore_synth(seed, tmp_path):
+    d = os.path.join(GOLDEN, f"synth{seed}")
+    p = lambda x: os.path.join(d, x)
+    _run([_bin("chainNet"), p("in.chain"), p("t.sizes"), p("q.sizes"), str(tmp_path / "t.net"),
+          str(tmp_path / "q.net"), "-rescore", f"-tNibDir={p('t.2bit')}",
+          f"-qNibDir={p('q.2bit')}", "-linearGap=loose"])
+    assert filecmp.cmp(tmp_path / "t.net", p("rescore.t.net"), shallow=False)
+    assert filecmp.cmp(tmp_path / "q.net", p("rescore.q.net"), shallow=False)
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_api_subchains_vs_reference(seed):
+    """The C ABI's batched sub-chain scores == reference chainSubsetOnT +
+    chainCalcScore (+ scoreChain local loop) on 3000 random ranges."""
+    from genomealignmenttools_amd.chainfile import read_chains
+    from genomealignmenttools_amd.gachain import GAC_Q, GAC_T, Engine, GapCosts
+    d = os.path.join(GOLDEN, f"synth{seed}")
+    z = np.load(os.path.join(d, "subchain.npz"))
+    ca = read_chains(os.path.join(d, "in.chain"))
+    e = Engine(0)
+    e.load_2bit(GAC_T, os.path.join(d, "t.2bit"))
+    e.load_2bit(GAC_Q, os.path.join(d, "q.2bit"))
+    e.set_scoring(np.asarray(BLASTZ, np.int32), GapCosts("loose"))
+    cs = e.upload_chains(ca)
+    g, l, a = e.score_ranges(cs, z["ranges"], want_local=True)
+    assert np.array_equal(g, z["glob"]) and np.array_equal(l, z["loc"])
+    assert np.array_equal(a, z["ali"])
+
+
+def test_scorechain_c1_example(tmp_path):
+    """Config C1: example/hg38.danRer10.chain with HoxD55.q against the seeded
+    synthetic hg38 chr2 / danRer10 chr22 genomes (regenerated here)."""
+    from genomealignmenttools_amd import synth
+    d = os.path.join(GOLDEN, "c1")
+    cfg = json.load(open(os.path.join(d, "seed.json")))
+    s = cfg["seed"]
+    tg = synth.random_genome(cfg["t"], s, n_frac=cfg["n_frac"], n_mean=cfg["n_mean"],
+                             mask_frac=cfg["mask_frac"])
+    qg = synth.random_genome(cfg["q"], s + 1, n_frac=cfg["n_frac"], n_mean=cfg["n_mean"],
+                             mask_frac=cfg["mask_frac"])
+    synth.write_2bit(tg, str(tmp_path / "t.2bit"))
+    synth.write_2bit(qg, str(tmp_path / "q.2bit"))
+    for mode, flag in [("score", "-returnOnlyScore"), ("chain", None)]:
+        cmd = [_bin("scoreChain"), os.path.join(d, "hg38.danRer10.chain"), str(tmp_path / "t.2bit"),
+               str(tmp_path / "q.2bit"), str(tmp_path / mode), "-linearGap=loose",
+               "-scoreScheme=" + os.path.join(d, "HoxD55.q")]
+        if flag:
+            cmd.append(flag)
+        _run(cmd)
+        assert filecmp.cmp(tmp_path / mode, os.path.join(d, f"c1.{mode}.out"), shallow=False)
