@@ -91,7 +91,8 @@ struct gac_ctx {
     RangeDesc *rdesc = nullptr;
     int32_t *nblk = nullptr, *goff = nullptr, *total = nullptr;
     int64_t ws_tiles = 0;
-    int32_t *tile_r0 = nullptr;
+    int32_t *ridx = nullptr;
+    int64_t ws_flat = 0;
     SegSum *sum_head = nullptr, *sum_tail = nullptr;
     void *scan_tmp = nullptr;
     size_t scan_bytes = 0;
@@ -171,7 +172,7 @@ extern "C" void gac_close(gac_ctx *c) {
     free_genome(c->g[0]);
     free_genome(c->g[1]);
     void *bufs[] = {c->d_small, c->rdesc,    c->nblk,     c->goff,     c->total,
-                    c->tile_r0, c->sum_head, c->sum_tail, c->scan_tmp, c->d_ranges,
+                    c->ridx,    c->sum_head, c->sum_tail, c->scan_tmp, c->d_ranges,
                     c->d_g,     c->d_l,      c->d_ali};
     for (void *p : bufs)
         if (p) hipFree(p);
@@ -495,7 +496,7 @@ extern "C" void gac_chains_free(gac_chainset *cs) {
 extern "C" int64_t gac_chains_block_count(const gac_chainset *cs) { return cs ? cs->n_blocks : -1; }
 
 // ----------------------------------------------------------------- launch
-static int ensure_ws(gac_ctx *c, int64_t n, int64_t max_tiles) {
+static int ensure_ws(gac_ctx *c, int64_t n, int64_t max_tiles, int64_t flat = 0) {
     if (n > c->ws_n) {
         int64_t cap = n + n / 2 + 1024;
         void *bufs[] = {c->rdesc, c->nblk, c->goff, c->total, c->scan_tmp};
@@ -512,14 +513,18 @@ static int ensure_ws(gac_ctx *c, int64_t n, int64_t max_tiles) {
         HIPCHK(hipMalloc(&c->scan_tmp, c->scan_bytes ? c->scan_bytes : 16));
         c->ws_n = cap;
     }
+    if (flat > c->ws_flat) {
+        int64_t cap = flat + flat / 4 + 4096;
+        if (c->ridx) hipFree(c->ridx);
+        c->ridx = nullptr;
+        HIPCHK(hipMalloc(&c->ridx, cap * 4));
+        c->ws_flat = cap;
+    }
     if (max_tiles > c->ws_tiles) {
         int64_t cap = max_tiles + max_tiles / 4 + 1024;
-        if (c->tile_r0) hipFree(c->tile_r0);
         if (c->sum_head) hipFree(c->sum_head);
         if (c->sum_tail) hipFree(c->sum_tail);
-        c->tile_r0 = nullptr;
         c->sum_head = c->sum_tail = nullptr;
-        HIPCHK(hipMalloc(&c->tile_r0, cap * 4));
         HIPCHK(hipMalloc(&c->sum_head, cap * sizeof(SegSum)));
         HIPCHK(hipMalloc(&c->sum_tail, cap * sizeof(SegSum)));
         c->ws_tiles = cap;
@@ -601,9 +606,9 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
     const int64_t W = c->h_total[0], NT = c->h_total[1];
     if (W < 0) return gac_fail(GAC_E_ARG, "window block total overflows int32");
     if (NT == 0) return GAC_OK;
-    rc = ensure_ws(c, n, NT);
+    rc = ensure_ws(c, n, NT, W);
     if (rc != GAC_OK) return rc;
-    a.tile_r0 = c->tile_r0;
+    a.ridx = c->ridx;
     a.sum_head = c->sum_head;
     a.sum_tail = c->sum_tail;
     a.n_tiles = (int32_t)NT;

@@ -11,7 +11,7 @@
 //             the O(blocks) list walks of chainSubsetOnT / chainBaseCountSubT)
 //             and write a 40-byte range descriptor
 //   (scan)    hipcub exclusive sum of window blocks -> flat block offsets
-//   k_mark    tile -> range owning its first flat block
+//   k_mark    flat block -> owning range id
 //   k_tile    one wave per tile of 64 consecutive flat blocks (ranges packed
 //             densely, many ranges per tile): lanes score 32-base chunks of
 //             2-bit packed T and Q straight from HBM (bit-plane popcounts, the
@@ -199,30 +199,28 @@ __global__ void k_total(ScoreArgs a) {
 }
 
 // ------------------------------------------------------------ k_mark -----
-// tile_r0[t] = range owning flat block 64t.
+// ridx[j] = range owning flat block j (lets a tile map lanes -> ranges with
+// one coalesced load instead of a dependent search).
 __global__ void __launch_bounds__(256) k_mark(ScoreArgs a) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
     const int nb = a.nblk[i];
-    if (nb == 0) return;
     const int g0 = a.goff[i];
-    const int t0 = (g0 + kTileBlocks - 1) / kTileBlocks;
-    const int t1 = (g0 + nb - 1) / kTileBlocks;
-    for (int t = t0; t <= t1; ++t) a.tile_r0[t] = (int32_t)i;
+    for (int k = 0; k < nb; ++k) a.ridx[g0 + k] = (int32_t)i;
 }
 
 // ------------------------------------------------------------ k_tile -----
 // One wave per tile of 64 consecutive flat blocks (ranges packed densely).
 struct WaveLds {
-    int goff[2 * kTileBlocks];  // candidate range offsets of this tile
-    int coff[kTileBlocks];      // exclusive chunk prefix per lane-block
+    int coff[kTileBlocks];  // exclusive chunk prefix per lane-block
     int ts[kTileBlocks];
     int qs[kTileBlocks];
     int len[kTileBlocks];
     int qinfo[kTileBlocks];
     long long twoff[kTileBlocks];
     long long qwoff[kTileBlocks];
-    unsigned long long acc[kTileBlocks];
+    int acc[kTileBlocks];   // block score (per 64-chunk pass sums fit int32;
+                            // blocks > 2^31/100 bases are rejected at upload)
 };
 
 __device__ __forceinline__ int chunk_score(const ScoreArgs &a, const WaveLds &L, int k, int off,
@@ -263,14 +261,15 @@ __device__ __forceinline__ int find_chunk_block(const WaveLds &L, int nact, int 
     return k;
 }
 
-__device__ __forceinline__ void seg_store(const ScoreArgs &a, long long *dst_g, int32_t *dst_a,
-                                          long long *dst_l, long long g, long long ali,
+template <bool LOCAL>
+__device__ __forceinline__ void seg_store(const ScoreArgs &a, int ri, long long g, int ali,
                                           const Elem &e) {
-    *dst_g = g;
-    *dst_a = (int32_t)ali;
-    if (a.want_local) *dst_l = max2(0, max2(e.C, e.D));
+    a.out_g[ri] = g;
+    a.out_ali[ri] = ali;
+    if (LOCAL) a.out_l[ri] = max2(0, max2(e.C, e.D));
 }
 
+template <bool LOCAL>
 __global__ void __launch_bounds__(256) k_tile(ScoreArgs a) {
     __shared__ int32_t s_small[3 * kSmallCap];
     __shared__ WaveLds s_w[kWavesPerWG];
@@ -287,46 +286,27 @@ __global__ void __launch_bounds__(256) k_tile(ScoreArgs a) {
     WaveLds &L = s_w[wave];
     const int T = a.n_tiles;
     const int W = a.n_flat;
+    const unsigned long long lanemask_le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
 
     // XCD-aware logical id: workgroups b and b+8 share an XCD (round-robin
     // dispatch), so give them adjacent tiles (speed only).
     const int G = gridDim.x;
     const int b = blockIdx.x;
     const int L8 = (G % 8 == 0) ? ((b % 8) * (G / 8) + b / 8) : b;
+    const int stride = G * kWavesPerWG;
 
-    for (int st = L8; st * kWavesPerWG < T; st += G) {
-        const int tile = st * kWavesPerWG + wave;
-        if (tile >= T) break;
-        const int j0 = tile * kTileBlocks;
-        const int r0 = a.tile_r0[tile];
-        const int rend = (tile + 1 < T) ? a.tile_r0[tile + 1] : (int)(a.n - 1);
-        const int span = rend - r0 + 1;
-        const int j = j0 + lane;
+    int tile = L8 * kWavesPerWG + wave;
+    // software pipeline: the lane->range map of the next tile is loaded while
+    // the current tile is scored
+    int ri_next = (tile < T && tile * kTileBlocks + lane < W) ? a.ridx[tile * kTileBlocks + lane] : 0;
+    for (; tile < T; tile += stride) {
+        const int j = tile * kTileBlocks + lane;
         const bool active = j < W;
-
-        // ---- which range owns flat block j
-        if (span <= 2 * kTileBlocks) {
-            L.goff[lane] = (lane < span) ? a.goff[r0 + lane] : 0x7fffffff;
-            L.goff[kTileBlocks + lane] =
-                (kTileBlocks + lane < span) ? a.goff[r0 + kTileBlocks + lane] : 0x7fffffff;
+        const int ri = ri_next;
+        {
+            const int jn = j + stride * kTileBlocks;
+            ri_next = (jn < W) ? a.ridx[jn] : 0;
         }
-        wave_sync();
-        int lo = 0, hi = span - 1;
-        if (span <= 2 * kTileBlocks) {
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (L.goff[mid] <= j) lo = mid;
-                else hi = mid - 1;
-            }
-        } else {
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (a.goff[r0 + mid] <= j) lo = mid;
-                else hi = mid - 1;
-            }
-        }
-        const int ri = r0 + lo;
-        const int gstart = (span <= 2 * kTileBlocks) ? L.goff[lo] : a.goff[ri];
 
         // ---- per-lane block: clip to [s, e), gap to the next block
         int cts = 0, cqs = 0, len = 0, g = 0, k = 0;
@@ -335,9 +315,15 @@ __global__ void __launch_bounds__(256) k_tile(ScoreArgs a) {
         long long twoff = 0, qwoff = 0;
         if (active) {
             const RangeDesc d = a.rdesc[ri];
-            k = j - gstart;
+            k = j - a.goff[ri];
             const int64_t blk = d.b0 + k;
             const int ts = a.bt[blk], qs = a.bq[blk], sz = a.bs[blk];
+            last = (k == d.nblk - 1);
+            int nts = 0, nqs = 0;
+            if (!last) {
+                nts = a.bt[blk + 1];
+                nqs = a.bq[blk + 1];
+            }
             const int te = ts + sz, qe = qs + sz;
             cts = ts;
             cqs = qs;
@@ -348,11 +334,7 @@ __global__ void __launch_bounds__(256) k_tile(ScoreArgs a) {
             }
             if (cte > d.e) cte = d.e;
             len = cte - cts;
-            last = (k == d.nblk - 1);
-            if (!last) {
-                const int nts = a.bt[blk + 1], nqs = a.bq[blk + 1];
-                g = gap_cost(a.gap, small, nqs - qe, nts - te);
-            }
+            if (!last) g = gap_cost(a.gap, small, nqs - qe, nts - te);
             qinfo = d.qinfo;
             twoff = d.twoff;
             qwoff = d.qwoff;
@@ -366,7 +348,7 @@ __global__ void __launch_bounds__(256) k_tile(ScoreArgs a) {
             if (lane >= d) incl += o;
         }
         const int C = __shfl(incl, kWave - 1, kWave);
-        const int nact = min(kTileBlocks, W - j0);
+        const int nact = min(kTileBlocks, W - tile * kTileBlocks);
         L.coff[lane] = incl - nch;
         L.ts[lane] = cts;
         L.qs[lane] = cqs;
@@ -374,7 +356,7 @@ __global__ void __launch_bounds__(256) k_tile(ScoreArgs a) {
         L.qinfo[lane] = qinfo;
         L.twoff[lane] = twoff;
         L.qwoff[lane] = qwoff;
-        L.acc[lane] = 0ull;
+        L.acc[lane] = 0;
         wave_sync();
 
         for (int c0 = 0; c0 < C; c0 += 2 * kWave) {
@@ -390,68 +372,68 @@ __global__ void __launch_bounds__(256) k_tile(ScoreArgs a) {
                 const int off = (jb - L.coff[kb]) << 5;
                 sb = chunk_score(a, L, kb, off, min(32, L.len[kb] - off));
             }
-            if (ja < C) atomicAdd(&L.acc[ka], (unsigned long long)(long long)sa);
-            if (jb < C) atomicAdd(&L.acc[kb], (unsigned long long)(long long)sb);
+            if (ja < C) atomicAdd(&L.acc[ka], sa);
+            if (jb < C) atomicAdd(&L.acc[kb], sb);
         }
         wave_sync();
 
         // ---- segmented (by range) inclusive scans over the tile's lanes
         const long long bsc = active ? (long long)L.acc[lane] : 0;
         long long vg = active ? bsc - g : 0;
-        long long va = active ? len : 0;
+        int va = active ? len : 0;
         Elem e;
-        if (active) {
-            e.A = last ? bsc : bsc - g;
-            e.B = last ? kNeg : 0;
-            e.C = bsc;
-            e.D = kNeg;
-        } else {
-            e.A = 0;
-            e.B = kNeg;
-            e.C = kNeg;
-            e.D = kNeg;
+        if (LOCAL) {
+            if (active) {
+                e.A = last ? bsc : bsc - g;
+                e.B = last ? kNeg : 0;
+                e.C = bsc;
+                e.D = kNeg;
+            } else {
+                e.A = 0;
+                e.B = kNeg;
+                e.C = kNeg;
+                e.D = kNeg;
+            }
         }
         const bool head = !active || lane == 0 || k == 0;
-        int f = head ? 1 : 0;
+        const unsigned long long heads = __ballot(head);
+        const int seg0 = 63 - __builtin_clzll(heads & lanemask_le);  // my segment's first lane
 #pragma unroll
         for (int d = 1; d < kWave; d <<= 1) {
             const long long og = __shfl_up(vg, d, kWave);
-            const long long oa = __shfl_up(va, d, kWave);
+            const int oa = __shfl_up(va, d, kWave);
             Elem o;
-            if (a.want_local) {
+            if (LOCAL) {
                 o.A = __shfl_up(e.A, d, kWave);
                 o.B = __shfl_up(e.B, d, kWave);
                 o.C = __shfl_up(e.C, d, kWave);
                 o.D = __shfl_up(e.D, d, kWave);
             }
-            const int of = __shfl_up(f, d, kWave);
-            if (lane >= d) {
-                if (!f) {
-                    vg += og;
-                    va += oa;
-                    if (a.want_local) e = compose(o, e);
-                }
-                f |= of;
+            if (lane - d >= seg0) {
+                vg += og;
+                va += oa;
+                if (LOCAL) e = compose(o, e);
             }
         }
-        const bool next_head = __shfl_down((int)head, 1, kWave) != 0;
-        const bool seg_end = active && (lane == kWave - 1 || next_head);
-        const int r_lane0 = __shfl(ri, 0, kWave);
-        const int k_lane0 = __shfl(k, 0, kWave);
+        const bool seg_end = active && (lane == kWave - 1 || ((heads >> (lane + 1)) & 1ull));
+        const int r_lane0 = __builtin_amdgcn_readfirstlane(ri);
+        const int k_lane0 = __builtin_amdgcn_readfirstlane(k);
         if (seg_end) {
-            const bool has0 = (ri == r_lane0);
+            const bool has0 = (seg0 == 0);
             const bool starts = !has0 || k_lane0 == 0;
+            (void)r_lane0;
             if (starts && last) {
-                seg_store(a, &a.out_g[ri], &a.out_ali[ri], a.out_l ? &a.out_l[ri] : nullptr, vg,
-                          va, e);
+                seg_store<LOCAL>(a, ri, vg, va, e);
             } else {
                 SegSum ssum;
                 ssum.g = vg;
                 ssum.ali = va;
-                ssum.A = e.A;
-                ssum.B = e.B;
-                ssum.C = e.C;
-                ssum.D = e.D;
+                if (LOCAL) {
+                    ssum.A = e.A;
+                    ssum.B = e.B;
+                    ssum.C = e.C;
+                    ssum.D = e.D;
+                }
                 if (has0 && !starts) a.sum_head[tile] = ssum;
                 if (!last && (lane == kWave - 1 || j + 1 == W)) a.sum_tail[tile] = ssum;
             }
@@ -462,14 +444,17 @@ __global__ void __launch_bounds__(256) k_tile(ScoreArgs a) {
 
 // ------------------------------------------------------------ k_combine --
 // Ranges spanning > 1 tile: tail segment of the first tile, then the head
-// segments of the following tiles, folded in order.
+// segments of the following tiles, folded in order.  Short spans are folded
+// by one lane; long spans (> kLaneFold tiles) by the whole wave.
+constexpr int kLaneFold = 16;
+
+template <bool LOCAL>
 __global__ void __launch_bounds__(256) k_combine(ScoreArgs a) {
     const int lane = threadIdx.x & 63;
     const int64_t wave_id = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     for (int64_t base = wave_id * kWave; base < a.n; base += nwaves * kWave) {
         const int64_t my = base + lane;
-        bool multi = false;
         int tf = 0, tl = 0;
         if (my < a.n) {
             const int nb = a.nblk[my];
@@ -477,37 +462,53 @@ __global__ void __launch_bounds__(256) k_combine(ScoreArgs a) {
                 const int g0 = a.goff[my];
                 tf = g0 / kTileBlocks;
                 tl = (g0 + nb - 1) / kTileBlocks;
-                multi = tf != tl;
             }
         }
-        unsigned long long mask = __ballot(multi);
+        const int nt = tl - tf;
+        if (nt > 0 && nt <= kLaneFold) {
+            SegSum s0 = a.sum_tail[tf];
+            Elem e = {s0.A, s0.B, s0.C, s0.D};
+            long long g = s0.g, ali = s0.ali;
+            for (int t = tf + 1; t <= tl; ++t) {
+                const SegSum s = a.sum_head[t];
+                g += s.g;
+                ali += s.ali;
+                if (LOCAL) {
+                    const Elem y = {s.A, s.B, s.C, s.D};
+                    e = compose(e, y);
+                }
+            }
+            seg_store<LOCAL>(a, (int)my, g, (int)ali, e);
+        }
+        unsigned long long mask = __ballot(nt > kLaneFold);
         while (mask) {
             const int src = __builtin_ctzll(mask);
             mask &= mask - 1;
             const int64_t ri = base + src;
             const int f0 = __shfl(tf, src, kWave);
             const int f1 = __shfl(tl, src, kWave);
-            const int nt = f1 - f0;  // head segments in tiles f0+1 .. f1
-            const int per = (nt + kWave - 1) / kWave;
-            const int lo = min(nt, lane * per), hi = min(nt, lo + per);
+            const int cnt = f1 - f0;  // head segments in tiles f0+1 .. f1
+            const int per = (cnt + kWave - 1) / kWave;
+            const int lo = min(cnt, lane * per), hi = min(cnt, lo + per);
             long long g = 0, ali = 0;
             Elem e = {0, kNeg, kNeg, kNeg};
             for (int t = lo; t < hi; ++t) {
                 const SegSum s = a.sum_head[f0 + 1 + t];
                 g += s.g;
                 ali += s.ali;
-                const Elem y = {s.A, s.B, s.C, s.D};
-                e = compose(e, y);
+                if (LOCAL) {
+                    const Elem y = {s.A, s.B, s.C, s.D};
+                    e = compose(e, y);
+                }
             }
             g = wave_sum(g);
             ali = wave_sum(ali);
-            if (a.want_local) e = wave_fold(e, lane);
+            if (LOCAL) e = wave_fold(e, lane);
             if (lane == 0) {
                 const SegSum s0 = a.sum_tail[f0];
                 const Elem x = {s0.A, s0.B, s0.C, s0.D};
-                e = compose(x, e);
-                seg_store(a, &a.out_g[ri], &a.out_ali[ri], a.out_l ? &a.out_l[ri] : nullptr,
-                          s0.g + g, s0.ali + ali, e);
+                if (LOCAL) e = compose(x, e);
+                seg_store<LOCAL>(a, (int)ri, s0.g + g, (int)(s0.ali + ali), e);
             }
         }
     }
@@ -606,12 +607,18 @@ hipError_t launch_mark(const ScoreArgs &a, hipStream_t s) {
 }
 
 hipError_t launch_tile(const ScoreArgs &a, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_tile, dim3(grid), dim3(256), 0, s, a);
+    if (a.want_local)
+        hipLaunchKernelGGL(k_tile<true>, dim3(grid), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_tile<false>, dim3(grid), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_combine(const ScoreArgs &a, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_combine, dim3(grid), dim3(256), 0, s, a);
+    if (a.want_local)
+        hipLaunchKernelGGL(k_combine<true>, dim3(grid), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_combine<false>, dim3(grid), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
