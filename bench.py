@@ -132,14 +132,8 @@ def main():
     tile_ms, tile_n = e.prof_read(GAC_K_TILE)
     step_s = dt / args.steps
     if dist is not None:
-        import torch
-        t = torch.tensor([dt, float(bases)], dtype=torch.float64, device=f"cuda:{local}")
-        mx = t.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = t.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        dt_max = float(mx[0])
-        total_bases = float(sm[1])
+        from genomealignmenttools_amd.shard import reduce_time_and_work
+        dt_max, total_bases = reduce_time_and_work(dist, dt, float(bases), device=f"cuda:{local}")
     else:
         dt_max, total_bases = dt, float(bases)
 

@@ -453,9 +453,9 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
         ch[i].nblk = (int32_t)(b1 - b0);
         ch[i].t_seq = ts;
         ch[i].q_seq = qs;
-        ch[i].strand = d->q_strand[i] ? 1 : 0;
-        ch[i].q_size = qsize;
-        ch[i].pad = 0;
+        ch[i].qinfo = qsize | (d->q_strand[i] ? (int32_t)0x80000000 : 0);
+        ch[i].tstart = b1 > b0 ? d->blk_t[b0] : 0;
+        ch[i].tend = b1 > b0 ? d->blk_t[b1 - 1] + d->blk_size[b1 - 1] : 0;
     }
     HIPCHK(hipSetDevice(c->device));
     gac_chainset *cs = new gac_chainset();

@@ -26,9 +26,9 @@ struct DChain {
     int32_t nblk;
     int32_t t_seq;
     int32_t q_seq;
-    int32_t strand;  // 0 '+', 1 '-'
-    int32_t q_size;  // sequence size of q_seq (reverse-complement index base)
-    int32_t pad;
+    int32_t qinfo;   // q_seq size (reverse-complement index base) | strand << 31
+    int32_t tstart;  // target span of the blocks (interpolation guesses)
+    int32_t tend;
 };
 static_assert(sizeof(DChain) == 32, "DChain layout");
 

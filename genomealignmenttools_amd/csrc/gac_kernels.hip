@@ -142,6 +142,42 @@ __device__ __forceinline__ long long wave_sum(long long v) {
 }
 
 // ------------------------------------------------------------ k_plan -----
+// First k in [0, n) with pred(k) true (pred monotone false..true), n if none:
+// gallop from guess g, then binary search the bracket.  Blocks are close to
+// uniformly spread along a chain, so an interpolated guess needs few probes
+// (each probe is a dependent load).
+template <class P>
+__device__ __forceinline__ int gallop_first(int n, int g, P pred) {
+    if (n <= 0) return 0;
+    g = g < 0 ? 0 : (g > n - 1 ? n - 1 : g);
+    int lo, hi;
+    if (pred(g)) {
+        hi = g;
+        int x = g - 1, step = 1;
+        while (x >= 0 && pred(x)) {
+            hi = x;
+            x -= step;
+            step <<= 1;
+        }
+        lo = x + 1 > 0 ? x + 1 : 0;
+    } else {
+        lo = g + 1;
+        int x = g + 1, step = 1;
+        while (x < n && !pred(x)) {
+            lo = x + 1;
+            x += step;
+            step <<= 1;
+        }
+        hi = x < n ? x : n;
+    }
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (pred(mid)) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+
 // One lane per range: window of blocks [b0, b0+n) with tEnd > s and tStart < e
 // (chainSubsetOnT's first-block walk and stop condition, chain.c:481-500),
 // plus the per-range descriptor the tile kernel needs.
@@ -161,24 +197,20 @@ __global__ void __launch_bounds__(256) k_plan(ScoreArgs a) {
         const DChain c = a.chains[r.chain];
         const int32_t *bt = a.bt + c.blk_off;
         const int32_t *bs = a.bs + c.blk_off;
-        int lo = 0, hi = c.nblk;
-        while (lo < hi) {  // first block with tEnd > s
-            const int mid = (lo + hi) >> 1;
-            if (bt[mid] + bs[mid] > r.t_start) hi = mid;
-            else lo = mid + 1;
-        }
-        const int first = lo;
-        hi = c.nblk;
-        while (lo < hi) {  // first block with tStart >= e
-            const int mid = (lo + hi) >> 1;
-            if (bt[mid] >= r.t_end) hi = mid;
-            else lo = mid + 1;
-        }
-        d.nblk = lo - first;
+        const int n = c.nblk;
+        const int64_t span = c.tend > c.tstart ? (int64_t)(c.tend - c.tstart) : 1;
+        // first block with tEnd > s, galloping from an interpolated guess
+        const int g1 = (int)(((int64_t)r.t_start - c.tstart) * n / span);
+        const int first = gallop_first(n, g1, [&](int k) { return bt[k] + bs[k] > r.t_start; });
+        // first block with tStart >= e
+        const int g2 = (int)(((int64_t)r.t_end - c.tstart) * n / span);
+        const int stop = first + gallop_first(n - first, g2 - first,
+                                              [&](int k) { return bt[first + k] >= r.t_end; });
+        d.nblk = stop - first;
         d.b0 = c.blk_off + first;
         d.twoff = a.t_woff[c.t_seq];
         d.qwoff = a.q_woff[c.q_seq];
-        d.qinfo = c.q_size | (c.strand ? (int32_t)0x80000000 : 0);
+        d.qinfo = c.qinfo;
     }
     a.rdesc[i] = d;
     a.nblk[i] = d.nblk;
@@ -202,11 +234,25 @@ __global__ void k_total(ScoreArgs a) {
 // ridx[j] = range owning flat block j (lets a tile map lanes -> ranges with
 // one coalesced load instead of a dependent search).
 __global__ void __launch_bounds__(256) k_mark(ScoreArgs a) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n) return;
-    const int nb = a.nblk[i];
-    const int g0 = a.goff[i];
-    for (int k = 0; k < nb; ++k) a.ridx[g0 + k] = (int32_t)i;
+    const int lane = threadIdx.x & 63;
+    const int64_t base = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) - lane;
+    const int64_t i = base + lane;
+    int nb = 0, g0 = 0;
+    if (i < a.n) {
+        nb = a.nblk[i];
+        g0 = a.goff[i];
+    }
+    // short windows: one lane each; long windows: the whole wave, coalesced
+    constexpr int kShort = 16;
+    if (nb <= kShort)
+        for (int k = 0; k < nb; ++k) a.ridx[g0 + k] = (int32_t)i;
+    unsigned long long mask = __ballot(nb > kShort);
+    while (mask) {
+        const int src = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        const int n = __shfl(nb, src, kWave), o = __shfl(g0, src, kWave);
+        for (int k = lane; k < n; k += kWave) a.ridx[o + k] = (int32_t)(base + src);
+    }
 }
 
 // ------------------------------------------------------------ k_tile -----
