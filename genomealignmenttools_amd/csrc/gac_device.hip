@@ -91,7 +91,7 @@ struct gac_ctx {
     RangeDesc *rdesc = nullptr;
     int32_t *nblk = nullptr, *goff = nullptr, *total = nullptr;
     int64_t ws_tiles = 0;
-    int32_t *ridx = nullptr;
+    int32_t *ridx = nullptr, *bidx = nullptr;
     int64_t ws_flat = 0;
     SegSum *sum_head = nullptr, *sum_tail = nullptr;
     void *scan_tmp = nullptr;
@@ -172,7 +172,7 @@ extern "C" void gac_close(gac_ctx *c) {
     free_genome(c->g[0]);
     free_genome(c->g[1]);
     void *bufs[] = {c->d_small, c->rdesc,    c->nblk,     c->goff,     c->total,
-                    c->ridx,    c->sum_head, c->sum_tail, c->scan_tmp, c->d_ranges,
+                    c->ridx,    c->bidx, c->sum_head, c->sum_tail, c->scan_tmp, c->d_ranges,
                     c->d_g,     c->d_l,      c->d_ali};
     for (void *p : bufs)
         if (p) hipFree(p);
@@ -516,8 +516,10 @@ static int ensure_ws(gac_ctx *c, int64_t n, int64_t max_tiles, int64_t flat = 0)
     if (flat > c->ws_flat) {
         int64_t cap = flat + flat / 4 + 4096;
         if (c->ridx) hipFree(c->ridx);
-        c->ridx = nullptr;
+        if (c->bidx) hipFree(c->bidx);
+        c->ridx = c->bidx = nullptr;
         HIPCHK(hipMalloc(&c->ridx, cap * 4));
+        HIPCHK(hipMalloc(&c->bidx, cap * 4));
         c->ws_flat = cap;
     }
     if (max_tiles > c->ws_tiles) {
@@ -609,6 +611,7 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
     rc = ensure_ws(c, n, NT, W);
     if (rc != GAC_OK) return rc;
     a.ridx = c->ridx;
+    a.bidx = c->bidx;
     a.sum_head = c->sum_head;
     a.sum_tail = c->sum_tail;
     a.n_tiles = (int32_t)NT;

@@ -83,6 +83,7 @@ struct ScoreArgs {
     int32_t *nblk;       // [n]   window blocks per range
     int32_t *goff;       // [n+1] exclusive scan of nblk (flat block offset)
     int32_t *ridx;       // [W]   range owning each flat block
+    int32_t *bidx;       // [W]   global block index of each flat block
     SegSum *sum_head;    // [T]   partial segment containing the tile's first block
     SegSum *sum_tail;    // [T]   partial segment containing the tile's last block
     int32_t *total;      // [2]   W (flat blocks), T (tiles)

@@ -198,14 +198,23 @@ __global__ void __launch_bounds__(256) k_plan(ScoreArgs a) {
         const int32_t *bt = a.bt + c.blk_off;
         const int32_t *bs = a.bs + c.blk_off;
         const int n = c.nblk;
-        const int64_t span = c.tend > c.tstart ? (int64_t)(c.tend - c.tstart) : 1;
-        // first block with tEnd > s, galloping from an interpolated guess
-        const int g1 = (int)(((int64_t)r.t_start - c.tstart) * n / span);
-        const int first = gallop_first(n, g1, [&](int k) { return bt[k] + bs[k] > r.t_start; });
-        // first block with tStart >= e
-        const int g2 = (int)(((int64_t)r.t_end - c.tstart) * n / span);
-        const int stop = first + gallop_first(n - first, g2 - first,
-                                              [&](int k) { return bt[first + k] >= r.t_end; });
+        // first block with tEnd > s (binary search; block spans are too
+        // irregular -- heavy-tailed gaps -- for interpolation to pay)
+        int lo = 0, hi = n;
+        if (r.t_start >= c.tstart) {
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (bt[mid] + bs[mid] > r.t_start) hi = mid;
+                else lo = mid + 1;
+            }
+        }
+        const int first = lo;
+        // first block with tStart >= e: windows are short, gallop from `first`
+        const int stop = r.t_end > c.tend
+                             ? n
+                             : first + gallop_first(n - first, 0, [&](int k) {
+                                   return bt[first + k] >= r.t_end;
+                               });
         d.nblk = stop - first;
         d.b0 = c.blk_off + first;
         d.twoff = a.t_woff[c.t_seq];
@@ -231,57 +240,72 @@ __global__ void k_total(ScoreArgs a) {
 }
 
 // ------------------------------------------------------------ k_mark -----
-// ridx[j] = range owning flat block j (lets a tile map lanes -> ranges with
-// one coalesced load instead of a dependent search).
+// For every flat block j: ridx[j] = owning range, bidx[j] = global block
+// index.  A tile then maps lanes to ranges and blocks with one coalesced
+// (prefetched) load and issues the range-descriptor and block loads together.
 __global__ void __launch_bounds__(256) k_mark(ScoreArgs a) {
     const int lane = threadIdx.x & 63;
     const int64_t base = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) - lane;
     const int64_t i = base + lane;
     int nb = 0, g0 = 0;
+    int64_t b0 = 0;
     if (i < a.n) {
         nb = a.nblk[i];
         g0 = a.goff[i];
+        if (nb > 0) b0 = a.rdesc[i].b0;
     }
     // short windows: one lane each; long windows: the whole wave, coalesced
     constexpr int kShort = 16;
     if (nb <= kShort)
-        for (int k = 0; k < nb; ++k) a.ridx[g0 + k] = (int32_t)i;
+        for (int k = 0; k < nb; ++k) {
+            a.ridx[g0 + k] = (int32_t)i;
+            a.bidx[g0 + k] = (int32_t)(b0 + k);
+        }
     unsigned long long mask = __ballot(nb > kShort);
     while (mask) {
         const int src = __builtin_ctzll(mask);
         mask &= mask - 1;
         const int n = __shfl(nb, src, kWave), o = __shfl(g0, src, kWave);
-        for (int k = lane; k < n; k += kWave) a.ridx[o + k] = (int32_t)(base + src);
+        const int64_t bb = __shfl(b0, src, kWave);
+        for (int k = lane; k < n; k += kWave) {
+            a.ridx[o + k] = (int32_t)(base + src);
+            a.bidx[o + k] = (int32_t)(bb + k);
+        }
     }
 }
 
 // ------------------------------------------------------------ k_tile -----
-// One wave per tile of 64 consecutive flat blocks (ranges packed densely).
+// One wave scores a PAIR of tiles (2 x 64 consecutive flat blocks; ranges
+// packed densely, many per tile) per iteration: one round trip for the
+// range descriptors + blocks of both tiles, chunk loads of both tiles in
+// flight together, then the per-tile segmented reductions.
+constexpr int kPair = 2 * kTileBlocks;
+
 struct WaveLds {
-    int coff[kTileBlocks];  // exclusive chunk prefix per lane-block
-    int ts[kTileBlocks];
-    int qs[kTileBlocks];
-    int len[kTileBlocks];
-    int qinfo[kTileBlocks];
-    long long twoff[kTileBlocks];
-    long long qwoff[kTileBlocks];
-    int acc[kTileBlocks];   // block score (per 64-chunk pass sums fit int32;
-                            // blocks > 2^31/100 bases are rejected at upload)
+    int coff[kPair];        // exclusive chunk prefix per block
+    long long tpos[kPair];  // global base index of the clipped target start
+    long long qpos[kPair];  // '+': global base index of the clipped query start
+                            // '-': global base index of (qSize - clipped qStart)
+    int lenq[kPair];        // clipped length | strand << 31
+    int acc[kPair];         // block scores
+};
+
+struct BlkInfo {
+    long long tpos, qpos;
+    int len, g, lenq;
+    bool active, first, last;
 };
 
 __device__ __forceinline__ int chunk_score(const ScoreArgs &a, const WaveLds &L, int k, int off,
                                            int n) {
     uint32_t t0, t1, tn, q0, q1, qn;
-    load_window(a.t_planes, a.t_nmask, L.twoff[k], (int64_t)L.ts[k] + off, t0, t1, tn);
-    const int qi = L.qinfo[k];
-    const int qp = L.qs[k] + off;
-    if (qi >= 0) {
-        load_window(a.q_planes, a.q_nmask, L.qwoff[k], qp, q0, q1, qn);
+    load_window(a.t_planes, a.t_nmask, 0, L.tpos[k] + off, t0, t1, tn);
+    if (L.lenq[k] >= 0) {
+        load_window(a.q_planes, a.q_nmask, 0, L.qpos[k] + off, q0, q1, qn);
     } else {
         // '-' strand: rc base j = comp(fwd[qSize-1-(qp+j)]), comp = code ^ 2
-        const int64_t F = (int64_t)(qi & 0x7fffffff) - qp - n;
         uint32_t f0, f1, fn;
-        load_window(a.q_planes, a.q_nmask, L.qwoff[k], F, f0, f1, fn);
+        load_window(a.q_planes, a.q_nmask, 0, L.qpos[k] - off - n, f0, f1, fn);
         const int sh = 32 - n;
         q0 = __builtin_bitreverse32(f0) >> sh;
         q1 = ~(__builtin_bitreverse32(f1) >> sh);
@@ -302,7 +326,7 @@ __device__ __forceinline__ int chunk_score(const ScoreArgs &a, const WaveLds &L,
 __device__ __forceinline__ int find_chunk_block(const WaveLds &L, int nact, int j) {
     int k = 0;
 #pragma unroll
-    for (int step = 32; step > 0; step >>= 1)
+    for (int step = 64; step > 0; step >>= 1)
         if (k + step < nact && L.coff[k + step] <= j) k += step;
     return k;
 }
@@ -313,6 +337,94 @@ __device__ __forceinline__ void seg_store(const ScoreArgs &a, int ri, long long 
     a.out_g[ri] = g;
     a.out_ali[ri] = ali;
     if (LOCAL) a.out_l[ri] = max2(0, max2(e.C, e.D));
+}
+
+// clip block bi of range ri to [s, e) and evaluate its gap to the next block
+__device__ __forceinline__ BlkInfo block_info(const ScoreArgs &a, const int32_t *small,
+                                              const RangeDesc &d, int bi, int ts, int qs, int sz,
+                                              int nts, int nqs) {
+    BlkInfo o;
+    o.active = true;
+    o.first = (bi == d.b0);
+    o.last = (bi == d.b0 + d.nblk - 1);
+    const int te = ts + sz, qe = qs + sz;
+    int cts = ts, cqs = qs, cte = te;
+    if (cts < d.s) {
+        cqs += d.s - cts;
+        cts = d.s;
+    }
+    if (cte > d.e) cte = d.e;
+    o.len = cte - cts;
+    o.g = o.last ? 0 : gap_cost(a.gap, small, nqs - qe, nts - te);
+    o.tpos = d.twoff * 32 + cts;
+    const bool minus = d.qinfo < 0;
+    o.qpos = minus ? d.qwoff * 32 + ((d.qinfo & 0x7fffffff) - cqs) : d.qwoff * 32 + cqs;
+    o.lenq = o.len | (minus ? (int)0x80000000 : 0);
+    return o;
+}
+
+// per-tile segmented reductions (v: lane's block of this tile)
+template <bool LOCAL>
+__device__ __forceinline__ void tile_reduce(const ScoreArgs &a, int tile, int lane, int ri,
+                                            const BlkInfo &v, long long bsc, int j, int W,
+                                            unsigned long long lanemask_le) {
+    long long vg = v.active ? bsc - v.g : 0;
+    int va = v.active ? v.len : 0;
+    Elem e;
+    if (LOCAL) {
+        if (v.active) {
+            e.A = v.last ? bsc : bsc - v.g;
+            e.B = v.last ? kNeg : 0;
+            e.C = bsc;
+            e.D = kNeg;
+        } else {
+            e.A = 0;
+            e.B = kNeg;
+            e.C = kNeg;
+            e.D = kNeg;
+        }
+    }
+    const bool head = !v.active || lane == 0 || v.first;
+    const unsigned long long heads = __ballot(head);
+    const int seg0 = 63 - __builtin_clzll(heads & lanemask_le);  // my segment's first lane
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const long long og = __shfl_up(vg, d, kWave);
+        const int oa = __shfl_up(va, d, kWave);
+        Elem o;
+        if (LOCAL) {
+            o.A = __shfl_up(e.A, d, kWave);
+            o.B = __shfl_up(e.B, d, kWave);
+            o.C = __shfl_up(e.C, d, kWave);
+            o.D = __shfl_up(e.D, d, kWave);
+        }
+        if (lane - d >= seg0) {
+            vg += og;
+            va += oa;
+            if (LOCAL) e = compose(o, e);
+        }
+    }
+    const bool seg_end = v.active && (lane == kWave - 1 || ((heads >> (lane + 1)) & 1ull));
+    const bool first0 = __builtin_amdgcn_readfirstlane(v.first ? 1 : 0) != 0;
+    if (seg_end) {
+        const bool has0 = (seg0 == 0);
+        const bool starts = !has0 || first0;
+        if (starts && v.last) {
+            seg_store<LOCAL>(a, ri, vg, va, e);
+        } else {
+            SegSum ssum;
+            ssum.g = vg;
+            ssum.ali = va;
+            if (LOCAL) {
+                ssum.A = e.A;
+                ssum.B = e.B;
+                ssum.C = e.C;
+                ssum.D = e.D;
+            }
+            if (has0 && !starts) a.sum_head[tile] = ssum;
+            if (!v.last && (lane == kWave - 1 || j + 1 == W)) a.sum_tail[tile] = ssum;
+        }
+    }
 }
 
 template <bool LOCAL>
@@ -330,79 +442,79 @@ __global__ void __launch_bounds__(256) k_tile(ScoreArgs a) {
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     WaveLds &L = s_w[wave];
-    const int T = a.n_tiles;
     const int W = a.n_flat;
+    const int NP = (a.n_tiles + 1) / 2;  // tile pairs
     const unsigned long long lanemask_le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
 
     // XCD-aware logical id: workgroups b and b+8 share an XCD (round-robin
-    // dispatch), so give them adjacent tiles (speed only).
+    // dispatch), so give them adjacent pairs (speed only).
     const int G = gridDim.x;
     const int b = blockIdx.x;
     const int L8 = (G % 8 == 0) ? ((b % 8) * (G / 8) + b / 8) : b;
     const int stride = G * kWavesPerWG;
 
-    int tile = L8 * kWavesPerWG + wave;
-    // software pipeline: the lane->range map of the next tile is loaded while
-    // the current tile is scored
-    int ri_next = (tile < T && tile * kTileBlocks + lane < W) ? a.ridx[tile * kTileBlocks + lane] : 0;
-    for (; tile < T; tile += stride) {
-        const int j = tile * kTileBlocks + lane;
-        const bool active = j < W;
-        const int ri = ri_next;
+    int pair = L8 * kWavesPerWG + wave;
+    // software pipeline: lane -> (range, block) maps of the next pair are
+    // loaded while the current pair is scored
+    int jn = pair * kPair + lane;
+    int riA = 0, biA = 0, riB = 0, biB = 0;
+    if (pair < NP) {
+        if (jn < W) { riA = a.ridx[jn]; biA = a.bidx[jn]; }
+        if (jn + kTileBlocks < W) { riB = a.ridx[jn + kTileBlocks]; biB = a.bidx[jn + kTileBlocks]; }
+    }
+    for (; pair < NP; pair += stride) {
+        const int jA = pair * kPair + lane, jB = jA + kTileBlocks;
+        const bool actA = jA < W, actB = jB < W;
+        const int cA = riA, cB = riB, bA = biA, bB = biB;
         {
-            const int jn = j + stride * kTileBlocks;
-            ri_next = (jn < W) ? a.ridx[jn] : 0;
+            const int j2 = jA + stride * kPair;
+            riA = biA = riB = biB = 0;
+            if (j2 < W) { riA = a.ridx[j2]; biA = a.bidx[j2]; }
+            if (j2 + kTileBlocks < W) { riB = a.ridx[j2 + kTileBlocks]; biB = a.bidx[j2 + kTileBlocks]; }
         }
+        // ---- one round trip: both tiles' range descriptors + blocks (+ next block)
+        RangeDesc dA, dB;
+        int tsA = 0, qsA = 0, szA = 0, ntsA = 0, nqsA = 0;
+        int tsB = 0, qsB = 0, szB = 0, ntsB = 0, nqsB = 0;
+        if (actA) {
+            dA = a.rdesc[cA];
+            tsA = a.bt[bA]; qsA = a.bq[bA]; szA = a.bs[bA];
+            ntsA = a.bt[bA + 1]; nqsA = a.bq[bA + 1];  // blocks array is padded by one
+        }
+        if (actB) {
+            dB = a.rdesc[cB];
+            tsB = a.bt[bB]; qsB = a.bq[bB]; szB = a.bs[bB];
+            ntsB = a.bt[bB + 1]; nqsB = a.bq[bB + 1];
+        }
+        BlkInfo vA = {}, vB = {};
+        if (actA) vA = block_info(a, small, dA, bA, tsA, qsA, szA, ntsA, nqsA);
+        if (actB) vB = block_info(a, small, dB, bB, tsB, qsB, szB, ntsB, nqsB);
 
-        // ---- per-lane block: clip to [s, e), gap to the next block
-        int cts = 0, cqs = 0, len = 0, g = 0, k = 0;
-        bool last = false;
-        int qinfo = 0;
-        long long twoff = 0, qwoff = 0;
-        if (active) {
-            const RangeDesc d = a.rdesc[ri];
-            k = j - a.goff[ri];
-            const int64_t blk = d.b0 + k;
-            const int ts = a.bt[blk], qs = a.bq[blk], sz = a.bs[blk];
-            last = (k == d.nblk - 1);
-            int nts = 0, nqs = 0;
-            if (!last) {
-                nts = a.bt[blk + 1];
-                nqs = a.bq[blk + 1];
-            }
-            const int te = ts + sz, qe = qs + sz;
-            cts = ts;
-            cqs = qs;
-            int cte = te;
-            if (cts < d.s) {
-                cqs += d.s - cts;
-                cts = d.s;
-            }
-            if (cte > d.e) cte = d.e;
-            len = cte - cts;
-            if (!last) g = gap_cost(a.gap, small, nqs - qe, nts - te);
-            qinfo = d.qinfo;
-            twoff = d.twoff;
-            qwoff = d.qwoff;
-        }
-        // ---- chunk prefix (32 bases per chunk)
-        const int nch = (len + 31) >> 5;
-        int incl = nch;
+        // ---- chunk prefix over the 128 blocks (32 bases per chunk)
+        const int nchA = (vA.len + 31) >> 5, nchB = (vB.len + 31) >> 5;
+        int incA = nchA, incB = nchB;
 #pragma unroll
         for (int d = 1; d < kWave; d <<= 1) {
-            const int o = __shfl_up(incl, d, kWave);
-            if (lane >= d) incl += o;
+            const int oA = __shfl_up(incA, d, kWave);
+            const int oB = __shfl_up(incB, d, kWave);
+            if (lane >= d) {
+                incA += oA;
+                incB += oB;
+            }
         }
-        const int C = __shfl(incl, kWave - 1, kWave);
-        const int nact = min(kTileBlocks, W - tile * kTileBlocks);
-        L.coff[lane] = incl - nch;
-        L.ts[lane] = cts;
-        L.qs[lane] = cqs;
-        L.len[lane] = len;
-        L.qinfo[lane] = qinfo;
-        L.twoff[lane] = twoff;
-        L.qwoff[lane] = qwoff;
+        const int CA = __shfl(incA, kWave - 1, kWave);
+        const int C = CA + __shfl(incB, kWave - 1, kWave);
+        const int nact = min(kPair, W - pair * kPair);
+        L.coff[lane] = incA - nchA;
+        L.coff[kTileBlocks + lane] = CA + incB - nchB;
+        L.tpos[lane] = vA.tpos;
+        L.tpos[kTileBlocks + lane] = vB.tpos;
+        L.qpos[lane] = vA.qpos;
+        L.qpos[kTileBlocks + lane] = vB.qpos;
+        L.lenq[lane] = vA.lenq;
+        L.lenq[kTileBlocks + lane] = vB.lenq;
         L.acc[lane] = 0;
+        L.acc[kTileBlocks + lane] = 0;
         wave_sync();
 
         for (int c0 = 0; c0 < C; c0 += 2 * kWave) {
@@ -411,79 +523,23 @@ __global__ void __launch_bounds__(256) k_tile(ScoreArgs a) {
             if (ja < C) {
                 ka = find_chunk_block(L, nact, ja);
                 const int off = (ja - L.coff[ka]) << 5;
-                sa = chunk_score(a, L, ka, off, min(32, L.len[ka] - off));
+                sa = chunk_score(a, L, ka, off, min(32, (L.lenq[ka] & 0x7fffffff) - off));
             }
             if (jb < C) {
                 kb = find_chunk_block(L, nact, jb);
                 const int off = (jb - L.coff[kb]) << 5;
-                sb = chunk_score(a, L, kb, off, min(32, L.len[kb] - off));
+                sb = chunk_score(a, L, kb, off, min(32, (L.lenq[kb] & 0x7fffffff) - off));
             }
             if (ja < C) atomicAdd(&L.acc[ka], sa);
             if (jb < C) atomicAdd(&L.acc[kb], sb);
         }
         wave_sync();
 
-        // ---- segmented (by range) inclusive scans over the tile's lanes
-        const long long bsc = active ? (long long)L.acc[lane] : 0;
-        long long vg = active ? bsc - g : 0;
-        int va = active ? len : 0;
-        Elem e;
-        if (LOCAL) {
-            if (active) {
-                e.A = last ? bsc : bsc - g;
-                e.B = last ? kNeg : 0;
-                e.C = bsc;
-                e.D = kNeg;
-            } else {
-                e.A = 0;
-                e.B = kNeg;
-                e.C = kNeg;
-                e.D = kNeg;
-            }
-        }
-        const bool head = !active || lane == 0 || k == 0;
-        const unsigned long long heads = __ballot(head);
-        const int seg0 = 63 - __builtin_clzll(heads & lanemask_le);  // my segment's first lane
-#pragma unroll
-        for (int d = 1; d < kWave; d <<= 1) {
-            const long long og = __shfl_up(vg, d, kWave);
-            const int oa = __shfl_up(va, d, kWave);
-            Elem o;
-            if (LOCAL) {
-                o.A = __shfl_up(e.A, d, kWave);
-                o.B = __shfl_up(e.B, d, kWave);
-                o.C = __shfl_up(e.C, d, kWave);
-                o.D = __shfl_up(e.D, d, kWave);
-            }
-            if (lane - d >= seg0) {
-                vg += og;
-                va += oa;
-                if (LOCAL) e = compose(o, e);
-            }
-        }
-        const bool seg_end = active && (lane == kWave - 1 || ((heads >> (lane + 1)) & 1ull));
-        const int r_lane0 = __builtin_amdgcn_readfirstlane(ri);
-        const int k_lane0 = __builtin_amdgcn_readfirstlane(k);
-        if (seg_end) {
-            const bool has0 = (seg0 == 0);
-            const bool starts = !has0 || k_lane0 == 0;
-            (void)r_lane0;
-            if (starts && last) {
-                seg_store<LOCAL>(a, ri, vg, va, e);
-            } else {
-                SegSum ssum;
-                ssum.g = vg;
-                ssum.ali = va;
-                if (LOCAL) {
-                    ssum.A = e.A;
-                    ssum.B = e.B;
-                    ssum.C = e.C;
-                    ssum.D = e.D;
-                }
-                if (has0 && !starts) a.sum_head[tile] = ssum;
-                if (!last && (lane == kWave - 1 || j + 1 == W)) a.sum_tail[tile] = ssum;
-            }
-        }
+        const long long bscA = L.acc[lane], bscB = L.acc[kTileBlocks + lane];
+        const int tA = 2 * pair;
+        tile_reduce<LOCAL>(a, tA, lane, cA, vA, bscA, jA, W, lanemask_le);
+        if (tA + 1 < a.n_tiles)
+            tile_reduce<LOCAL>(a, tA + 1, lane, cB, vB, bscB, jB, W, lanemask_le);
         wave_sync();
     }
 }

@@ -77,6 +77,8 @@ def test_edge_ranges():
         [(10, 20, 1), (11, 22, 1), (40, 30, 5), (45, 35, 100), (200, 300, 1)],
         [(0, 0, 4999)],
         [(100, 5, 33), (133, 38, 31), (170, 70, 65), (300, 140, 64), (400, 210, 129)],
+        # zero-size blocks (legal in .chain files) at both ends and inside
+        [(50, 60, 0), (50, 61, 10), (70, 80, 0), (75, 85, 20), (100, 110, 0)],
     ]
     offs, bt, bq, bs = [0], [], [], []
     for bl in blocks:
@@ -92,7 +94,7 @@ def test_edge_ranges():
     ca = ChainArrays(score=np.zeros(n), tname=["t"] * n, tsize=np.full(n, 5000, np.int32),
                      tstart=np.asarray(ts, np.int32), tend=np.asarray(te, np.int32),
                      qname=["q"] * n, qsize=np.full(n, 6000, np.int32),
-                     qstrand=np.asarray([0, 1, 1], np.uint8), qstart=np.asarray(qs, np.int32),
+                     qstrand=np.asarray([0, 1, 1, 0], np.uint8)[:n], qstart=np.asarray(qs, np.int32),
                      qend=np.asarray(qe, np.int32), id=np.arange(1, n + 1),
                      blk_off=np.asarray(offs, np.int64), blk_t=np.asarray(bt, np.int32),
                      blk_q=np.asarray(bq, np.int32), blk_size=np.asarray(bs, np.int32))
