@@ -36,6 +36,9 @@ struct NPiece {
 };
 hipError_t launch_relayout(const uint8_t *raw, const SeqDev *seqs, int nseq, int64_t nwords,
                            uint2 *planes, uint32_t *nmask, hipStream_t s);
+hipError_t launch_nflags(const DChain *chains, int64_t n_chains, int4 *blk,
+                         const uint32_t *t_nmask, const int64_t *t_woff, const uint32_t *q_nmask,
+                         const int64_t *q_woff, hipStream_t s);
 hipError_t launch_nruns(const NPiece *p, int64_t n, uint32_t *nmask, hipStream_t s);
 }  // namespace gac
 
@@ -117,7 +120,7 @@ struct gac_chainset {
     int64_t n_chains;
     int64_t n_blocks;
     DChain *chains = nullptr;
-    int32_t *bt = nullptr, *bq = nullptr, *bs = nullptr;
+    int4 *blk = nullptr;  // {tStart, qStart, size, nflags}, padded by one entry
 };
 
 // ----------------------------------------------------------------- context
@@ -437,7 +440,7 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
         int64_t pt = 0, pq = 0;
         for (int64_t b = b0; b < b1; ++b) {
             const int64_t t = d->blk_t[b], q = d->blk_q[b], z = d->blk_size[b];
-            if (z < 0 || t < 0 || q < 0 || t + z > tsize || q + z > qsize)
+            if (z < 0 || z >= (1 << 29) || t < 0 || q < 0 || t + z > tsize || q + z > qsize)
                 return gac_fail(GAC_E_FORMAT,
                                 "chain %lld block %lld [t %lld q %lld size %lld] outside its "
                                 "sequences (tSize %d qSize %d)",
@@ -458,23 +461,25 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
         ch[i].tend = b1 > b0 ? d->blk_t[b1 - 1] + d->blk_size[b1 - 1] : 0;
     }
     HIPCHK(hipSetDevice(c->device));
+    std::vector<int4> blk((size_t)d->n_blocks + 1);
+    for (int64_t b = 0; b < d->n_blocks; ++b)
+        blk[b] = make_int4(d->blk_t[b], d->blk_q[b], d->blk_size[b], 0);
+    blk[d->n_blocks] = make_int4(0, 0, 0, 0);
     gac_chainset *cs = new gac_chainset();
     cs->ctx = c;
     cs->n_chains = d->n_chains;
     cs->n_blocks = d->n_blocks;
-    const size_t nb = (size_t)(d->n_blocks ? d->n_blocks : 1) + 1;  // +1: k_tile reads blk+1 only when not last
     hipError_t e = hipMalloc(&cs->chains, ch.size() * sizeof(DChain));
-    if (e == hipSuccess) e = hipMalloc(&cs->bt, nb * 4);
-    if (e == hipSuccess) e = hipMalloc(&cs->bq, nb * 4);
-    if (e == hipSuccess) e = hipMalloc(&cs->bs, nb * 4);
+    if (e == hipSuccess) e = hipMalloc(&cs->blk, blk.size() * sizeof(int4));
     if (e == hipSuccess)
         e = hipMemcpy(cs->chains, ch.data(), ch.size() * sizeof(DChain), hipMemcpyHostToDevice);
-    if (e == hipSuccess && d->n_blocks) {
-        e = hipMemcpy(cs->bt, d->blk_t, d->n_blocks * 4, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(cs->bq, d->blk_q, d->n_blocks * 4, hipMemcpyHostToDevice);
-        if (e == hipSuccess)
-            e = hipMemcpy(cs->bs, d->blk_size, d->n_blocks * 4, hipMemcpyHostToDevice);
-    }
+    if (e == hipSuccess)
+        e = hipMemcpy(cs->blk, blk.data(), blk.size() * sizeof(int4), hipMemcpyHostToDevice);
+    // per-block N flags (scoring skips N-mask loads of N-free blocks)
+    if (e == hipSuccess)
+        e = launch_nflags(cs->chains, cs->n_chains, cs->blk, c->g[0].nmask, c->g[0].d_woff,
+                          c->g[1].nmask, c->g[1].d_woff, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) {
         gac_chains_free(cs);
         return gac_fail(GAC_E_HIP, "chain upload failed: %s", hipGetErrorString(e));
@@ -487,9 +492,7 @@ extern "C" void gac_chains_free(gac_chainset *cs) {
     if (!cs) return;
     hipSetDevice(cs->ctx->device);
     if (cs->chains) hipFree(cs->chains);
-    if (cs->bt) hipFree(cs->bt);
-    if (cs->bq) hipFree(cs->bq);
-    if (cs->bs) hipFree(cs->bs);
+    if (cs->blk) hipFree(cs->blk);
     delete cs;
 }
 
@@ -579,9 +582,7 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
     a.q_woff = Q.d_woff;
     a.chains = cs->chains;
     a.n_chains = cs->n_chains;
-    a.bt = cs->bt;
-    a.bq = cs->bq;
-    a.bs = cs->bs;
+    a.blk = cs->blk;
     a.ranges = d_ranges;
     a.n = n;
     a.rdesc = c->rdesc;

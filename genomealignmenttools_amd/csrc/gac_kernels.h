@@ -8,7 +8,9 @@
 //                 base 32w+i at bit i of each plane
 //     nmask[w]  : uint32, bit i set = base 32w+i is N (or padding)
 //     every sequence starts on a word boundary; word_off[s] = first word
-//   chains: DChain[c] + blocks bt/bq/bs (int32 tStart, qStart, size)
+//   chains: DChain[c] + blocks blk[b] = int4 {tStart, qStart, size, nflags}
+//     nflags bit0/bit1: the block's target/query bases contain an N
+//     (precomputed at upload; blocks without N skip the N-mask loads)
 #pragma once
 #include <stdint.h>
 
@@ -43,16 +45,16 @@ struct GapDev {
     double long_val[3][kMaxLong];
 };
 
-// Per-range descriptor written by k_plan (one load per lane in k_tile).
+// Per-range descriptor written by k_plan (two 16-B loads in k_tile).
 struct RangeDesc {
-    int64_t b0;      // first block of the window (global block index)
-    int64_t twoff;   // first genome word of the target sequence
-    int64_t qwoff;   // first genome word of the query sequence
+    int64_t tbase;   // global base index of the target sequence start (word_off * 32)
+    int64_t qbase;   // '+': global base index of the query sequence start
+                     // '-': ~(word_off * 32 + qSize)  (negative)
+    int32_t b0;      // first block of the window (global block index)
     int32_t nblk;    // blocks in the window
     int32_t s, e;    // target clip range
-    int32_t qinfo;   // query sequence size | (strand << 31)
 };
-static_assert(sizeof(RangeDesc) == 40, "RangeDesc layout");
+static_assert(sizeof(RangeDesc) == 32, "RangeDesc layout");
 
 // Partial result of a range segment inside one tile: additive parts + the
 // local-score max-plus element  s_out = max(s_in + A, B); m_out = max(m_in, s_in + C, D)
@@ -75,7 +77,7 @@ struct ScoreArgs {
     const int64_t *q_woff;
     const DChain *chains;
     int64_t n_chains;
-    const int32_t *bt, *bq, *bs;
+    const int4 *blk;     // [n_blocks + 1] {tStart, qStart, size, nflags}
     const Range *ranges;
     int64_t n;
     // workspace

@@ -85,20 +85,24 @@ __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, int sh) {
     return __builtin_amdgcn_alignbit(hi, lo, (uint32_t)sh);
 }
 
-// Load 32 bases starting at base index p of the side whose words start at
-// woff: returns the two code planes and the N mask, bit i = base p+i.
-__device__ __forceinline__ void load_window(const uint2 *planes, const uint32_t *nmask,
-                                            int64_t woff, int64_t p, uint32_t &b0,
-                                            uint32_t &b1, uint32_t &nm) {
-    const int64_t w = woff + (p >> 5);
+typedef uint32_t u32x4a8 __attribute__((ext_vector_type(4), aligned(8)));
+typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
+
+// 32 bases starting at global base index p: the two code planes (bit i = base
+// p+i) with ONE 16-byte load of words w, w+1 ({p0,p1} each; 8-byte aligned).
+__device__ __forceinline__ void load_planes(const uint2 *planes, int64_t p, uint32_t &b0,
+                                            uint32_t &b1) {
+    const int64_t w = p >> 5;
     const int sh = (int)(p & 31);
-    const uint2 lo = planes[w];
-    const uint2 hi = planes[w + 1];
-    const uint32_t nlo = nmask[w];
-    const uint32_t nhi = nmask[w + 1];
-    b0 = funnel(hi.x, lo.x, sh);
-    b1 = funnel(hi.y, lo.y, sh);
-    nm = funnel(nhi, nlo, sh);
+    const u32x4a8 v = *reinterpret_cast<const u32x4a8 *>(planes + w);
+    b0 = funnel(v.z, v.x, sh);
+    b1 = funnel(v.w, v.y, sh);
+}
+
+__device__ __forceinline__ uint32_t load_nmask(const uint32_t *nmask, int64_t p) {
+    const int64_t w = p >> 5;
+    const u32x2a4 v = *reinterpret_cast<const u32x2a4 *>(nmask + w);
+    return funnel(v.y, v.x, (int)(p & 31));
 }
 
 struct Elem {
@@ -141,11 +145,49 @@ __device__ __forceinline__ long long wave_sum(long long v) {
     return v;
 }
 
+// ------------------------------------------------------------ k_nflags ---
+// At chain upload: flag blocks whose target / query bases contain an N, so
+// the scoring kernel can skip N-mask loads for all other blocks.  One wave
+// per chain, lanes over blocks.
+__device__ __forceinline__ bool range_has_n(const uint32_t *nmask, int64_t p, int len) {
+    if (len <= 0) return false;
+    int64_t w = p >> 5;
+    const int64_t we = (p + len - 1) >> 5;
+    const int lo = (int)(p & 31);
+    const int hi = (int)((p + len - 1) & 31);
+    for (; w <= we; ++w) {
+        uint32_t m = nmask[w];
+        if (w == (p >> 5)) m &= ~((1u << lo) - 1u);
+        if (w == we) m &= (hi == 31) ? 0xffffffffu : ((2u << hi) - 1u);
+        if (m) return true;
+    }
+    return false;
+}
+
+__global__ void __launch_bounds__(256) k_nflags(const DChain *chains, int64_t n_chains, int4 *blk,
+                                                const uint32_t *t_nmask, const int64_t *t_woff,
+                                                const uint32_t *q_nmask, const int64_t *q_woff) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave_id = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t c = wave_id; c < n_chains; c += nwaves) {
+        const DChain ch = chains[c];
+        const int64_t tb = t_woff[ch.t_seq] * 32, qb = q_woff[ch.q_seq] * 32;
+        const bool minus = ch.qinfo < 0;
+        const int qsize = ch.qinfo & 0x7fffffff;
+        for (int k = lane; k < ch.nblk; k += kWave) {
+            int4 b = blk[ch.blk_off + k];
+            const int64_t qf = minus ? (int64_t)qsize - b.y - b.z : b.y;
+            b.w = (range_has_n(t_nmask, tb + b.x, b.z) ? 1 : 0) |
+                  (range_has_n(q_nmask, qb + qf, b.z) ? 2 : 0);
+            blk[ch.blk_off + k] = b;
+        }
+    }
+}
+
 // ------------------------------------------------------------ k_plan -----
 // First k in [0, n) with pred(k) true (pred monotone false..true), n if none:
-// gallop from guess g, then binary search the bracket.  Blocks are close to
-// uniformly spread along a chain, so an interpolated guess needs few probes
-// (each probe is a dependent load).
+// gallop from guess g, then binary search the bracket.
 template <class P>
 __device__ __forceinline__ int gallop_first(int n, int g, P pred) {
     if (n <= 0) return 0;
@@ -186,17 +228,15 @@ __global__ void __launch_bounds__(256) k_plan(ScoreArgs a) {
     if (i >= a.n) return;
     const Range r = a.ranges[i];
     RangeDesc d;
+    d.tbase = 0;
+    d.qbase = 0;
     d.b0 = 0;
-    d.twoff = 0;
-    d.qwoff = 0;
     d.nblk = 0;
     d.s = r.t_start;
     d.e = r.t_end;
-    d.qinfo = 0;
     if (r.chain >= 0 && r.chain < a.n_chains && r.t_start < r.t_end) {
         const DChain c = a.chains[r.chain];
-        const int32_t *bt = a.bt + c.blk_off;
-        const int32_t *bs = a.bs + c.blk_off;
+        const int4 *bk = a.blk + c.blk_off;
         const int n = c.nblk;
         // first block with tEnd > s (binary search; block spans are too
         // irregular -- heavy-tailed gaps -- for interpolation to pay)
@@ -204,7 +244,8 @@ __global__ void __launch_bounds__(256) k_plan(ScoreArgs a) {
         if (r.t_start >= c.tstart) {
             while (lo < hi) {
                 const int mid = (lo + hi) >> 1;
-                if (bt[mid] + bs[mid] > r.t_start) hi = mid;
+                const int4 b = bk[mid];
+                if (b.x + b.z > r.t_start) hi = mid;
                 else lo = mid + 1;
             }
         }
@@ -213,13 +254,13 @@ __global__ void __launch_bounds__(256) k_plan(ScoreArgs a) {
         const int stop = r.t_end > c.tend
                              ? n
                              : first + gallop_first(n - first, 0, [&](int k) {
-                                   return bt[first + k] >= r.t_end;
+                                   return bk[first + k].x >= r.t_end;
                                });
         d.nblk = stop - first;
-        d.b0 = c.blk_off + first;
-        d.twoff = a.t_woff[c.t_seq];
-        d.qwoff = a.q_woff[c.q_seq];
-        d.qinfo = c.qinfo;
+        d.b0 = (int32_t)(c.blk_off + first);
+        d.tbase = a.t_woff[c.t_seq] * 32;
+        const int64_t qw = a.q_woff[c.q_seq] * 32;
+        d.qbase = c.qinfo < 0 ? ~(qw + (c.qinfo & 0x7fffffff)) : qw;
     }
     a.rdesc[i] = d;
     a.nblk[i] = d.nblk;
@@ -247,8 +288,7 @@ __global__ void __launch_bounds__(256) k_mark(ScoreArgs a) {
     const int lane = threadIdx.x & 63;
     const int64_t base = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) - lane;
     const int64_t i = base + lane;
-    int nb = 0, g0 = 0;
-    int64_t b0 = 0;
+    int nb = 0, g0 = 0, b0 = 0;
     if (i < a.n) {
         nb = a.nblk[i];
         g0 = a.goff[i];
@@ -259,57 +299,58 @@ __global__ void __launch_bounds__(256) k_mark(ScoreArgs a) {
     if (nb <= kShort)
         for (int k = 0; k < nb; ++k) {
             a.ridx[g0 + k] = (int32_t)i;
-            a.bidx[g0 + k] = (int32_t)(b0 + k);
+            a.bidx[g0 + k] = b0 + k;
         }
     unsigned long long mask = __ballot(nb > kShort);
     while (mask) {
         const int src = __builtin_ctzll(mask);
         mask &= mask - 1;
         const int n = __shfl(nb, src, kWave), o = __shfl(g0, src, kWave);
-        const int64_t bb = __shfl(b0, src, kWave);
+        const int bb = __shfl(b0, src, kWave);
         for (int k = lane; k < n; k += kWave) {
             a.ridx[o + k] = (int32_t)(base + src);
-            a.bidx[o + k] = (int32_t)(bb + k);
+            a.bidx[o + k] = bb + k;
         }
     }
 }
 
 // ------------------------------------------------------------ k_tile -----
-// One wave scores a PAIR of tiles (2 x 64 consecutive flat blocks; ranges
-// packed densely, many per tile) per iteration: one round trip for the
-// range descriptors + blocks of both tiles, chunk loads of both tiles in
-// flight together, then the per-tile segmented reductions.
-constexpr int kPair = 2 * kTileBlocks;
-
+// One wave per tile of 64 consecutive flat blocks (ranges packed densely,
+// many per tile).  Per tile: one round trip for the range descriptors and
+// blocks (the lane -> (range, block) map was prefetched during the previous
+// tile), one for the 2-bit windows (16-byte loads; N masks only for blocks
+// flagged at upload), then segmented per-range scans.
 struct WaveLds {
-    int coff[kPair];        // exclusive chunk prefix per block
-    long long tpos[kPair];  // global base index of the clipped target start
-    long long qpos[kPair];  // '+': global base index of the clipped query start
-                            // '-': global base index of (qSize - clipped qStart)
-    int lenq[kPair];        // clipped length | strand << 31
-    int acc[kPair];         // block scores
+    int coff[kTileBlocks];        // exclusive chunk prefix per lane-block
+    long long tpos[kTileBlocks];  // global base index of the clipped target start
+    long long qpos[kTileBlocks];  // '+': global base index of the clipped query start
+                                  // '-': global base index of (qSize - clipped qStart)
+    int lenq[kTileBlocks];        // clipped length | minus << 31 | tN << 30 | qN << 29
+    unsigned long long acc[kTileBlocks];  // block scores (int64: a block may be huge)
 };
 
-struct BlkInfo {
-    long long tpos, qpos;
-    int len, g, lenq;
-    bool active, first, last;
-};
+constexpr int kLenMask = (1 << 29) - 1;
 
 __device__ __forceinline__ int chunk_score(const ScoreArgs &a, const WaveLds &L, int k, int off,
                                            int n) {
-    uint32_t t0, t1, tn, q0, q1, qn;
-    load_window(a.t_planes, a.t_nmask, 0, L.tpos[k] + off, t0, t1, tn);
-    if (L.lenq[k] >= 0) {
-        load_window(a.q_planes, a.q_nmask, 0, L.qpos[k] + off, q0, q1, qn);
+    const int lq = L.lenq[k];
+    uint32_t t0, t1, q0, q1, tn = 0, qn = 0;
+    const int64_t tp = L.tpos[k] + off;
+    load_planes(a.t_planes, tp, t0, t1);
+    if (lq & (1 << 30)) tn = load_nmask(a.t_nmask, tp);
+    if (lq >= 0) {
+        const int64_t qp = L.qpos[k] + off;
+        load_planes(a.q_planes, qp, q0, q1);
+        if (lq & (1 << 29)) qn = load_nmask(a.q_nmask, qp);
     } else {
         // '-' strand: rc base j = comp(fwd[qSize-1-(qp+j)]), comp = code ^ 2
-        uint32_t f0, f1, fn;
-        load_window(a.q_planes, a.q_nmask, 0, L.qpos[k] - off - n, f0, f1, fn);
+        const int64_t F = L.qpos[k] - off - n;
+        uint32_t f0, f1;
+        load_planes(a.q_planes, F, f0, f1);
         const int sh = 32 - n;
         q0 = __builtin_bitreverse32(f0) >> sh;
         q1 = ~(__builtin_bitreverse32(f1) >> sh);
-        qn = __builtin_bitreverse32(fn) >> sh;
+        if (lq & (1 << 29)) qn = __builtin_bitreverse32(load_nmask(a.q_nmask, F)) >> sh;
     }
     const uint32_t valid = (n >= 32 ? 0xffffffffu : ((1u << n) - 1u)) & ~tn & ~qn;
     const uint32_t tm[4] = {~t1 & ~t0, ~t1 & t0, t1 & ~t0, t1 & t0};
@@ -326,7 +367,7 @@ __device__ __forceinline__ int chunk_score(const ScoreArgs &a, const WaveLds &L,
 __device__ __forceinline__ int find_chunk_block(const WaveLds &L, int nact, int j) {
     int k = 0;
 #pragma unroll
-    for (int step = 64; step > 0; step >>= 1)
+    for (int step = 32; step > 0; step >>= 1)
         if (k + step < nact && L.coff[k + step] <= j) k += step;
     return k;
 }
@@ -337,94 +378,6 @@ __device__ __forceinline__ void seg_store(const ScoreArgs &a, int ri, long long 
     a.out_g[ri] = g;
     a.out_ali[ri] = ali;
     if (LOCAL) a.out_l[ri] = max2(0, max2(e.C, e.D));
-}
-
-// clip block bi of range ri to [s, e) and evaluate its gap to the next block
-__device__ __forceinline__ BlkInfo block_info(const ScoreArgs &a, const int32_t *small,
-                                              const RangeDesc &d, int bi, int ts, int qs, int sz,
-                                              int nts, int nqs) {
-    BlkInfo o;
-    o.active = true;
-    o.first = (bi == d.b0);
-    o.last = (bi == d.b0 + d.nblk - 1);
-    const int te = ts + sz, qe = qs + sz;
-    int cts = ts, cqs = qs, cte = te;
-    if (cts < d.s) {
-        cqs += d.s - cts;
-        cts = d.s;
-    }
-    if (cte > d.e) cte = d.e;
-    o.len = cte - cts;
-    o.g = o.last ? 0 : gap_cost(a.gap, small, nqs - qe, nts - te);
-    o.tpos = d.twoff * 32 + cts;
-    const bool minus = d.qinfo < 0;
-    o.qpos = minus ? d.qwoff * 32 + ((d.qinfo & 0x7fffffff) - cqs) : d.qwoff * 32 + cqs;
-    o.lenq = o.len | (minus ? (int)0x80000000 : 0);
-    return o;
-}
-
-// per-tile segmented reductions (v: lane's block of this tile)
-template <bool LOCAL>
-__device__ __forceinline__ void tile_reduce(const ScoreArgs &a, int tile, int lane, int ri,
-                                            const BlkInfo &v, long long bsc, int j, int W,
-                                            unsigned long long lanemask_le) {
-    long long vg = v.active ? bsc - v.g : 0;
-    int va = v.active ? v.len : 0;
-    Elem e;
-    if (LOCAL) {
-        if (v.active) {
-            e.A = v.last ? bsc : bsc - v.g;
-            e.B = v.last ? kNeg : 0;
-            e.C = bsc;
-            e.D = kNeg;
-        } else {
-            e.A = 0;
-            e.B = kNeg;
-            e.C = kNeg;
-            e.D = kNeg;
-        }
-    }
-    const bool head = !v.active || lane == 0 || v.first;
-    const unsigned long long heads = __ballot(head);
-    const int seg0 = 63 - __builtin_clzll(heads & lanemask_le);  // my segment's first lane
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        const long long og = __shfl_up(vg, d, kWave);
-        const int oa = __shfl_up(va, d, kWave);
-        Elem o;
-        if (LOCAL) {
-            o.A = __shfl_up(e.A, d, kWave);
-            o.B = __shfl_up(e.B, d, kWave);
-            o.C = __shfl_up(e.C, d, kWave);
-            o.D = __shfl_up(e.D, d, kWave);
-        }
-        if (lane - d >= seg0) {
-            vg += og;
-            va += oa;
-            if (LOCAL) e = compose(o, e);
-        }
-    }
-    const bool seg_end = v.active && (lane == kWave - 1 || ((heads >> (lane + 1)) & 1ull));
-    const bool first0 = __builtin_amdgcn_readfirstlane(v.first ? 1 : 0) != 0;
-    if (seg_end) {
-        const bool has0 = (seg0 == 0);
-        const bool starts = !has0 || first0;
-        if (starts && v.last) {
-            seg_store<LOCAL>(a, ri, vg, va, e);
-        } else {
-            SegSum ssum;
-            ssum.g = vg;
-            ssum.ali = va;
-            if (LOCAL) {
-                ssum.A = e.A;
-                ssum.B = e.B;
-                ssum.C = e.C;
-                ssum.D = e.D;
-            }
-            if (has0 && !starts) a.sum_head[tile] = ssum;
-            if (!v.last && (lane == kWave - 1 || j + 1 == W)) a.sum_tail[tile] = ssum;
-        }
-    }
 }
 
 template <bool LOCAL>
@@ -442,79 +395,78 @@ __global__ void __launch_bounds__(256) k_tile(ScoreArgs a) {
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     WaveLds &L = s_w[wave];
+    const int T = a.n_tiles;
     const int W = a.n_flat;
-    const int NP = (a.n_tiles + 1) / 2;  // tile pairs
     const unsigned long long lanemask_le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
 
     // XCD-aware logical id: workgroups b and b+8 share an XCD (round-robin
-    // dispatch), so give them adjacent pairs (speed only).
+    // dispatch), so give them adjacent tiles (speed only).
     const int G = gridDim.x;
     const int b = blockIdx.x;
     const int L8 = (G % 8 == 0) ? ((b % 8) * (G / 8) + b / 8) : b;
     const int stride = G * kWavesPerWG;
 
-    int pair = L8 * kWavesPerWG + wave;
-    // software pipeline: lane -> (range, block) maps of the next pair are
-    // loaded while the current pair is scored
-    int jn = pair * kPair + lane;
-    int riA = 0, biA = 0, riB = 0, biB = 0;
-    if (pair < NP) {
-        if (jn < W) { riA = a.ridx[jn]; biA = a.bidx[jn]; }
-        if (jn + kTileBlocks < W) { riB = a.ridx[jn + kTileBlocks]; biB = a.bidx[jn + kTileBlocks]; }
+    int tile = L8 * kWavesPerWG + wave;
+    int ri_next = 0, bi_next = 0;
+    {
+        const int j = tile * kTileBlocks + lane;
+        if (tile < T && j < W) {
+            ri_next = a.ridx[j];
+            bi_next = a.bidx[j];
+        }
     }
-    for (; pair < NP; pair += stride) {
-        const int jA = pair * kPair + lane, jB = jA + kTileBlocks;
-        const bool actA = jA < W, actB = jB < W;
-        const int cA = riA, cB = riB, bA = biA, bB = biB;
+    for (; tile < T; tile += stride) {
+        const int j = tile * kTileBlocks + lane;
+        const bool active = j < W;
+        const int ri = ri_next, bi = bi_next;
         {
-            const int j2 = jA + stride * kPair;
-            riA = biA = riB = biB = 0;
-            if (j2 < W) { riA = a.ridx[j2]; biA = a.bidx[j2]; }
-            if (j2 + kTileBlocks < W) { riB = a.ridx[j2 + kTileBlocks]; biB = a.bidx[j2 + kTileBlocks]; }
-        }
-        // ---- one round trip: both tiles' range descriptors + blocks (+ next block)
-        RangeDesc dA, dB;
-        int tsA = 0, qsA = 0, szA = 0, ntsA = 0, nqsA = 0;
-        int tsB = 0, qsB = 0, szB = 0, ntsB = 0, nqsB = 0;
-        if (actA) {
-            dA = a.rdesc[cA];
-            tsA = a.bt[bA]; qsA = a.bq[bA]; szA = a.bs[bA];
-            ntsA = a.bt[bA + 1]; nqsA = a.bq[bA + 1];  // blocks array is padded by one
-        }
-        if (actB) {
-            dB = a.rdesc[cB];
-            tsB = a.bt[bB]; qsB = a.bq[bB]; szB = a.bs[bB];
-            ntsB = a.bt[bB + 1]; nqsB = a.bq[bB + 1];
-        }
-        BlkInfo vA = {}, vB = {};
-        if (actA) vA = block_info(a, small, dA, bA, tsA, qsA, szA, ntsA, nqsA);
-        if (actB) vB = block_info(a, small, dB, bB, tsB, qsB, szB, ntsB, nqsB);
-
-        // ---- chunk prefix over the 128 blocks (32 bases per chunk)
-        const int nchA = (vA.len + 31) >> 5, nchB = (vB.len + 31) >> 5;
-        int incA = nchA, incB = nchB;
-#pragma unroll
-        for (int d = 1; d < kWave; d <<= 1) {
-            const int oA = __shfl_up(incA, d, kWave);
-            const int oB = __shfl_up(incB, d, kWave);
-            if (lane >= d) {
-                incA += oA;
-                incB += oB;
+            const int jn = j + stride * kTileBlocks;
+            ri_next = bi_next = 0;
+            if (jn < W) {
+                ri_next = a.ridx[jn];
+                bi_next = a.bidx[jn];
             }
         }
-        const int CA = __shfl(incA, kWave - 1, kWave);
-        const int C = CA + __shfl(incB, kWave - 1, kWave);
-        const int nact = min(kPair, W - pair * kPair);
-        L.coff[lane] = incA - nchA;
-        L.coff[kTileBlocks + lane] = CA + incB - nchB;
-        L.tpos[lane] = vA.tpos;
-        L.tpos[kTileBlocks + lane] = vB.tpos;
-        L.qpos[lane] = vA.qpos;
-        L.qpos[kTileBlocks + lane] = vB.qpos;
-        L.lenq[lane] = vA.lenq;
-        L.lenq[kTileBlocks + lane] = vB.lenq;
-        L.acc[lane] = 0;
-        L.acc[kTileBlocks + lane] = 0;
+
+        // ---- per-lane block: clip to [s, e), gap to the next block
+        int len = 0, g = 0, lenq = 0;
+        bool first = false, last = false;
+        long long tpos = 0, qpos = 0;
+        if (active) {
+            const RangeDesc d = a.rdesc[ri];
+            const int4 bk = a.blk[bi];
+            const int4 nx = a.blk[bi + 1];  // the block array is padded by one
+            first = (bi == d.b0);
+            last = (bi == d.b0 + d.nblk - 1);
+            const int te = bk.x + bk.z, qe = bk.y + bk.z;
+            int cts = bk.x, cqs = bk.y, cte = te;
+            if (cts < d.s) {
+                cqs += d.s - cts;
+                cts = d.s;
+            }
+            if (cte > d.e) cte = d.e;
+            len = cte - cts;
+            if (!last) g = gap_cost(a.gap, small, nx.y - qe, nx.x - te);
+            tpos = d.tbase + cts;
+            const bool minus = d.qbase < 0;
+            qpos = minus ? ~d.qbase - cqs : d.qbase + cqs;
+            lenq = len | (minus ? (int)0x80000000 : 0) | ((bk.w & 1) << 30) | ((bk.w & 2) << 28);
+        }
+        // ---- chunk prefix (32 bases per chunk)
+        const int nch = (len + 31) >> 5;
+        int incl = nch;
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const int o = __shfl_up(incl, d, kWave);
+            if (lane >= d) incl += o;
+        }
+        const int C = __shfl(incl, kWave - 1, kWave);
+        const int nact = min(kTileBlocks, W - tile * kTileBlocks);
+        L.coff[lane] = incl - nch;
+        L.tpos[lane] = tpos;
+        L.qpos[lane] = qpos;
+        L.lenq[lane] = lenq;
+        L.acc[lane] = 0ull;
         wave_sync();
 
         for (int c0 = 0; c0 < C; c0 += 2 * kWave) {
@@ -523,23 +475,77 @@ __global__ void __launch_bounds__(256) k_tile(ScoreArgs a) {
             if (ja < C) {
                 ka = find_chunk_block(L, nact, ja);
                 const int off = (ja - L.coff[ka]) << 5;
-                sa = chunk_score(a, L, ka, off, min(32, (L.lenq[ka] & 0x7fffffff) - off));
+                sa = chunk_score(a, L, ka, off, min(32, (L.lenq[ka] & kLenMask) - off));
             }
             if (jb < C) {
                 kb = find_chunk_block(L, nact, jb);
                 const int off = (jb - L.coff[kb]) << 5;
-                sb = chunk_score(a, L, kb, off, min(32, (L.lenq[kb] & 0x7fffffff) - off));
+                sb = chunk_score(a, L, kb, off, min(32, (L.lenq[kb] & kLenMask) - off));
             }
-            if (ja < C) atomicAdd(&L.acc[ka], sa);
-            if (jb < C) atomicAdd(&L.acc[kb], sb);
+            if (ja < C) atomicAdd(&L.acc[ka], (unsigned long long)(long long)sa);
+            if (jb < C) atomicAdd(&L.acc[kb], (unsigned long long)(long long)sb);
         }
         wave_sync();
 
-        const long long bscA = L.acc[lane], bscB = L.acc[kTileBlocks + lane];
-        const int tA = 2 * pair;
-        tile_reduce<LOCAL>(a, tA, lane, cA, vA, bscA, jA, W, lanemask_le);
-        if (tA + 1 < a.n_tiles)
-            tile_reduce<LOCAL>(a, tA + 1, lane, cB, vB, bscB, jB, W, lanemask_le);
+        // ---- segmented (by range) inclusive scans over the tile's lanes
+        const long long bsc = active ? (long long)L.acc[lane] : 0;
+        long long vg = active ? bsc - g : 0;
+        int va = active ? len : 0;
+        Elem e;
+        if (LOCAL) {
+            if (active) {
+                e.A = last ? bsc : bsc - g;
+                e.B = last ? kNeg : 0;
+                e.C = bsc;
+                e.D = kNeg;
+            } else {
+                e.A = 0;
+                e.B = kNeg;
+                e.C = kNeg;
+                e.D = kNeg;
+            }
+        }
+        const bool head = !active || lane == 0 || first;
+        const unsigned long long heads = __ballot(head);
+        const int seg0 = 63 - __builtin_clzll(heads & lanemask_le);  // my segment's first lane
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const long long og = __shfl_up(vg, d, kWave);
+            const int oa = __shfl_up(va, d, kWave);
+            Elem o;
+            if (LOCAL) {
+                o.A = __shfl_up(e.A, d, kWave);
+                o.B = __shfl_up(e.B, d, kWave);
+                o.C = __shfl_up(e.C, d, kWave);
+                o.D = __shfl_up(e.D, d, kWave);
+            }
+            if (lane - d >= seg0) {
+                vg += og;
+                va += oa;
+                if (LOCAL) e = compose(o, e);
+            }
+        }
+        const bool seg_end = active && (lane == kWave - 1 || ((heads >> (lane + 1)) & 1ull));
+        const bool first0 = __builtin_amdgcn_readfirstlane(first ? 1 : 0) != 0;
+        if (seg_end) {
+            const bool has0 = (seg0 == 0);
+            const bool starts = !has0 || first0;
+            if (starts && last) {
+                seg_store<LOCAL>(a, ri, vg, va, e);
+            } else {
+                SegSum ssum;
+                ssum.g = vg;
+                ssum.ali = va;
+                if (LOCAL) {
+                    ssum.A = e.A;
+                    ssum.B = e.B;
+                    ssum.C = e.C;
+                    ssum.D = e.D;
+                }
+                if (has0 && !starts) a.sum_head[tile] = ssum;
+                if (!last && (lane == kWave - 1 || j + 1 == W)) a.sum_tail[tile] = ssum;
+            }
+        }
         wave_sync();
     }
 }
@@ -721,6 +727,16 @@ hipError_t launch_combine(const ScoreArgs &a, int grid, hipStream_t s) {
         hipLaunchKernelGGL(k_combine<true>, dim3(grid), dim3(256), 0, s, a);
     else
         hipLaunchKernelGGL(k_combine<false>, dim3(grid), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_nflags(const DChain *chains, int64_t n_chains, int4 *blk,
+                         const uint32_t *t_nmask, const int64_t *t_woff, const uint32_t *q_nmask,
+                         const int64_t *q_woff, hipStream_t s) {
+    if (n_chains == 0) return hipSuccess;
+    const int64_t waves = n_chains < 65536 ? n_chains : 65536;
+    hipLaunchKernelGGL(k_nflags, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, chains,
+                       n_chains, blk, t_nmask, t_woff, q_nmask, q_woff);
     return hipGetLastError();
 }
 
