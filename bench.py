@@ -86,7 +86,7 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world,
                                 device_id=torch.device(f"cuda:{local}"))
 
-    from genomealignmenttools_amd._lib import GAC_K_TILE
+    from genomealignmenttools_amd._lib import GAC_K_COMBINE, GAC_K_PLAN, GAC_K_TILE
     from genomealignmenttools_amd.gachain import GAC_Q, GAC_T, Engine, GapCosts
 
     tg, qg, ca, ranges, info = make_workload(args, rank)
@@ -130,6 +130,9 @@ def main():
     dt = time.perf_counter() - t0
     e.prof_enable(False)
     tile_ms, tile_n = e.prof_read(GAC_K_TILE)
+    kern_ms = {name: e.prof_read(k)[0] / max(e.prof_read(k)[1], 1)
+               for name, k in (("plan+mark", GAC_K_PLAN), ("tile", GAC_K_TILE),
+                               ("combine", GAC_K_COMBINE))}
     step_s = dt / args.steps
     if dist is not None:
         from genomealignmenttools_amd.shard import reduce_time_and_work
@@ -169,6 +172,7 @@ def main():
             "kernel": "k_tile", "kernel_avg_ms": tile_avg_s * 1e3,
             "algo_bytes_per_launch": algo_bytes,
         },
+        "kernel_ms_per_step": kern_ms,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -18,9 +18,11 @@
 #include "host/gac_host.h"
 
 namespace gac {
-size_t scan_temp_bytes(int64_t n);
-hipError_t launch_plan(const ScoreArgs &a, void *temp, size_t temp_bytes, hipStream_t s);
-hipError_t launch_mark(const ScoreArgs &a, hipStream_t s);
+int plan_grid(int64_t n);
+int tile_blocks_per_cu(bool local);
+hipError_t launch_plan(const ScoreArgs &a, hipStream_t s);
+int mark_chunks_bound(int64_t flat, int64_t n);
+hipError_t launch_mark(const ScoreArgs &a, int grid, hipStream_t s);
 hipError_t launch_tile(const ScoreArgs &a, int grid, hipStream_t s);
 hipError_t launch_combine(const ScoreArgs &a, int grid, hipStream_t s);
 struct SeqDev {
@@ -79,6 +81,9 @@ struct Prof {
 
 }  // namespace
 
+// status[0..8) + 9 arrival counters on their own 128-byte lines
+constexpr size_t kStatusBytes = 128 + 9 * 128;
+
 struct gac_ctx {
     int device = 0;
     char arch[64] = {0};
@@ -92,20 +97,27 @@ struct gac_ctx {
     // workspace
     int64_t ws_n = 0;
     RangeDesc *rdesc = nullptr;
-    int32_t *nblk = nullptr, *goff = nullptr, *total = nullptr;
+    int32_t *nblk = nullptr, *goff = nullptr;
+    int32_t *pb0 = nullptr;                  // [ws_n]
+    unsigned long long *gran = nullptr;      // [plan workgroups]
+    int32_t *plan_off = nullptr, *chunk_off = nullptr;  // [plan workgroups]
+    int32_t *chunk_wg = nullptr;             // [ws_chunks]
+    int64_t ws_chunks = 0;
+    int32_t *status = nullptr;               // [8] status, then the arrival counters
+    uint32_t epoch = 0;
     int64_t ws_tiles = 0;
     int32_t *ridx = nullptr, *bidx = nullptr;
     int64_t ws_flat = 0;
     SegSum *sum_head = nullptr, *sum_tail = nullptr;
-    void *scan_tmp = nullptr;
-    size_t scan_bytes = 0;
     // staging for the host API
     int64_t io_n = 0;
     Range *d_ranges = nullptr;
     long long *d_g = nullptr, *d_l = nullptr;
     int32_t *d_ali = nullptr;
-    int32_t *h_total = nullptr;  // pinned
-    int tile_grid = 2048;
+    int32_t *h_total = nullptr;  // pinned [8]
+    int tile_grid = 2048;       // k_mark grid
+    int tile_grid_g = 2048;     // k_tile<false> grid (resident workgroups)
+    int tile_grid_l = 2048;     // k_tile<true> grid
     int combine_grid = 512;
     // profiling
     bool prof = false;
@@ -121,6 +133,7 @@ struct gac_chainset {
     int64_t n_blocks;
     DChain *chains = nullptr;
     int4 *blk = nullptr;  // {tStart, qStart, size, nflags}, padded by one entry
+    int2 *tspan = nullptr;  // {tStart, tEnd}
 };
 
 // ----------------------------------------------------------------- context
@@ -151,8 +164,10 @@ extern "C" int gac_open(int device, gac_ctx **out) {
     // persistent tile grid: 8 workgroups (32 waves) per CU
     c->tile_grid = prop.multiProcessorCount * 8;
     c->tile_grid = (c->tile_grid + 7) / 8 * 8;
-    c->combine_grid = prop.multiProcessorCount * 2;
-    if (hipHostMalloc((void **)&c->h_total, 16, hipHostMallocDefault) != hipSuccess) {
+    c->combine_grid = prop.multiProcessorCount * 8;  // one 64-range group per wave
+    c->tile_grid_g = prop.multiProcessorCount * tile_blocks_per_cu(false);
+    c->tile_grid_l = prop.multiProcessorCount * tile_blocks_per_cu(true);
+    if (hipHostMalloc((void **)&c->h_total, 32, hipHostMallocDefault) != hipSuccess) {
         hipStreamDestroy(c->stream);
         delete c;
         return gac_fail(GAC_E_HIP, "hipHostMalloc failed");
@@ -174,9 +189,9 @@ extern "C" void gac_close(gac_ctx *c) {
     hipStreamSynchronize(c->stream);
     free_genome(c->g[0]);
     free_genome(c->g[1]);
-    void *bufs[] = {c->d_small, c->rdesc,    c->nblk,     c->goff,     c->total,
-                    c->ridx,    c->bidx, c->sum_head, c->sum_tail, c->scan_tmp, c->d_ranges,
-                    c->d_g,     c->d_l,      c->d_ali};
+    void *bufs[] = {c->d_small,  c->rdesc,    c->nblk,     c->goff, c->pb0, c->gran, c->plan_off, c->chunk_off, c->chunk_wg,
+                    c->status,   c->ridx,     c->bidx,     c->sum_head, c->sum_tail,
+                    c->d_ranges, c->d_g,      c->d_l,      c->d_ali};
     for (void *p : bufs)
         if (p) hipFree(p);
     for (auto &p : c->prof_pending) {
@@ -465,6 +480,10 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
     for (int64_t b = 0; b < d->n_blocks; ++b)
         blk[b] = make_int4(d->blk_t[b], d->blk_q[b], d->blk_size[b], 0);
     blk[d->n_blocks] = make_int4(0, 0, 0, 0);
+    std::vector<int2> tspan((size_t)d->n_blocks + 1);
+    for (int64_t b = 0; b < d->n_blocks; ++b)
+        tspan[b] = make_int2(d->blk_t[b], d->blk_t[b] + d->blk_size[b]);
+    tspan[d->n_blocks] = make_int2(0, 0);
     gac_chainset *cs = new gac_chainset();
     cs->ctx = c;
     cs->n_chains = d->n_chains;
@@ -475,6 +494,9 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
         e = hipMemcpy(cs->chains, ch.data(), ch.size() * sizeof(DChain), hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipMemcpy(cs->blk, blk.data(), blk.size() * sizeof(int4), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&cs->tspan, tspan.size() * sizeof(int2));
+    if (e == hipSuccess)
+        e = hipMemcpy(cs->tspan, tspan.data(), tspan.size() * sizeof(int2), hipMemcpyHostToDevice);
     // per-block N flags (scoring skips N-mask loads of N-free blocks)
     if (e == hipSuccess)
         e = launch_nflags(cs->chains, cs->n_chains, cs->blk, c->g[0].nmask, c->g[0].d_woff,
@@ -493,37 +515,53 @@ extern "C" void gac_chains_free(gac_chainset *cs) {
     hipSetDevice(cs->ctx->device);
     if (cs->chains) hipFree(cs->chains);
     if (cs->blk) hipFree(cs->blk);
+    if (cs->tspan) hipFree(cs->tspan);
     delete cs;
 }
 
 extern "C" int64_t gac_chains_block_count(const gac_chainset *cs) { return cs ? cs->n_blocks : -1; }
 
 // ----------------------------------------------------------------- launch
-static int ensure_ws(gac_ctx *c, int64_t n, int64_t max_tiles, int64_t flat = 0) {
+static int ensure_ws(gac_ctx *c, int64_t n, int64_t max_tiles, int64_t flat, hipStream_t s) {
     if (n > c->ws_n) {
         int64_t cap = n + n / 2 + 1024;
-        void *bufs[] = {c->rdesc, c->nblk, c->goff, c->total, c->scan_tmp};
+        void *bufs[] = {c->rdesc, c->nblk, c->goff, c->pb0, c->gran, c->plan_off, c->chunk_off};
         for (void *p : bufs)
             if (p) hipFree(p);
         c->rdesc = nullptr;
-        c->nblk = c->goff = c->total = nullptr;
-        c->scan_tmp = nullptr;
+        c->nblk = c->goff = c->pb0 = c->plan_off = c->chunk_off = nullptr;
+        c->gran = nullptr;
+        const int64_t G = plan_grid(cap) + 2;
         HIPCHK(hipMalloc(&c->rdesc, cap * sizeof(RangeDesc)));
         HIPCHK(hipMalloc(&c->nblk, cap * 4));
-        HIPCHK(hipMalloc(&c->goff, (cap + 1) * 4));
-        HIPCHK(hipMalloc(&c->total, 16));
-        c->scan_bytes = scan_temp_bytes(cap);
-        HIPCHK(hipMalloc(&c->scan_tmp, c->scan_bytes ? c->scan_bytes : 16));
+        HIPCHK(hipMalloc(&c->goff, cap * 4));
+        HIPCHK(hipMalloc(&c->pb0, cap * 4));
+        HIPCHK(hipMalloc(&c->gran, G * 8));
+        HIPCHK(hipMemsetAsync(c->gran, 0, G * 8, s));  // epoch 0 is never used
+        HIPCHK(hipMalloc(&c->plan_off, G * 4));
+        HIPCHK(hipMalloc(&c->chunk_off, G * 4));
         c->ws_n = cap;
+    }
+    if (!c->status) {
+        HIPCHK(hipMalloc(&c->status, kStatusBytes));
+        HIPCHK(hipMemsetAsync(c->status, 0, kStatusBytes, s));
     }
     if (flat > c->ws_flat) {
         int64_t cap = flat + flat / 4 + 4096;
+        if (cap > INT32_MAX) cap = INT32_MAX;
         if (c->ridx) hipFree(c->ridx);
         if (c->bidx) hipFree(c->bidx);
         c->ridx = c->bidx = nullptr;
         HIPCHK(hipMalloc(&c->ridx, cap * 4));
         HIPCHK(hipMalloc(&c->bidx, cap * 4));
         c->ws_flat = cap;
+    }
+    const int64_t nq = mark_chunks_bound(c->ws_flat, c->ws_n);
+    if (nq > c->ws_chunks) {
+        if (c->chunk_wg) hipFree(c->chunk_wg);
+        c->chunk_wg = nullptr;
+        HIPCHK(hipMalloc(&c->chunk_wg, nq * 4));
+        c->ws_chunks = nq;
     }
     if (max_tiles > c->ws_tiles) {
         int64_t cap = max_tiles + max_tiles / 4 + 1024;
@@ -561,6 +599,12 @@ static hipEvent_t prof_event(gac_ctx *c) {
         c->prof_pending.push_back(Prof{(k), _pa, _pb}); \
     }
 
+// One call = 4 launches (k_plan, k_mark, k_tile, k_combine) and a 32-byte
+// status readback.  The flat block count W is only known on the
+// device (ranges may overlap), so the kernels check the workspace capacity
+// themselves; on overflow k_tile / k_combine do nothing and the call grows the
+// workspace to the reported {W, T} and runs once more (first call or a larger
+// batch only).
 static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_ranges, int64_t n,
                         uint32_t flags, long long *d_g, long long *d_l, int32_t *d_ali,
                         hipStream_t s) {
@@ -569,7 +613,9 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
     if (n < 0 || n > INT32_MAX / 2) return gac_fail(GAC_E_ARG, "bad range count %lld", (long long)n);
     if (n == 0) return GAC_OK;
     if ((flags & GAC_WANT_LOCAL) && !d_l) return gac_fail(GAC_E_ARG, "GAC_WANT_LOCAL needs local output");
-    int rc = ensure_ws(c, n, 0);
+    // first guess for an empty workspace: 8 window blocks per range
+    const int64_t guess = c->ws_flat ? 0 : 8 * n;
+    int rc = ensure_ws(c, n, guess / kTileBlocks + 1, guess, s);
     if (rc != GAC_OK) return rc;
     ScoreArgs a;
     memset(&a, 0, sizeof(a));
@@ -583,12 +629,9 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
     a.chains = cs->chains;
     a.n_chains = cs->n_chains;
     a.blk = cs->blk;
+    a.tspan = cs->tspan;
     a.ranges = d_ranges;
     a.n = n;
-    a.rdesc = c->rdesc;
-    a.nblk = c->nblk;
-    a.goff = c->goff;
-    a.total = c->total;
     a.out_g = d_g;
     a.out_l = d_l;
     a.out_ali = d_ali;
@@ -597,38 +640,59 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
     a.small_tab = c->d_small;
     memcpy(a.coef, c->coef, sizeof(a.coef));
     a.gap = c->gap;
-    {
-        PROF_BEGIN(GAC_K_PLAN);
-        HIPCHK(launch_plan(a, c->scan_tmp, c->scan_bytes, s));
-        PROF_END(GAC_K_PLAN);
+    for (int pass = 0; pass < 2; ++pass) {
+        a.rdesc = c->rdesc;
+        a.nblk = c->nblk;
+        a.goff = c->goff;
+        if (++c->epoch == 0) {  // granule tags wrapped: clear them
+            HIPCHK(hipMemsetAsync(c->gran, 0, (plan_grid(c->ws_n) + 2) * 8, s));
+            c->epoch = 1;
+        }
+        a.pb0 = c->pb0;
+        a.gran = c->gran;
+        a.plan_off = c->plan_off;
+        a.chunk_off = c->chunk_off;
+        a.chunk_wg = c->chunk_wg;
+        a.cap_chunks = (int32_t)(c->ws_chunks < INT32_MAX ? c->ws_chunks : INT32_MAX);
+        a.epoch = c->epoch;
+        a.status = c->status;
+        a.ticket = (uint32_t *)(c->status + 32);
+        a.ridx = c->ridx;
+        a.bidx = c->bidx;
+        a.sum_head = c->sum_head;
+        a.sum_tail = c->sum_tail;
+        a.cap_flat = (int32_t)c->ws_flat;
+        a.cap_tiles = (int32_t)(c->ws_tiles < INT32_MAX ? c->ws_tiles : INT32_MAX);
+        {
+            PROF_BEGIN(GAC_K_PLAN);
+            HIPCHK(launch_plan(a, s));
+            HIPCHK(launch_mark(a, c->tile_grid, s));
+            PROF_END(GAC_K_PLAN);
+        }
+        {
+            PROF_BEGIN(GAC_K_TILE);
+            HIPCHK(launch_tile(a, a.want_local ? c->tile_grid_l : c->tile_grid_g, s));
+            PROF_END(GAC_K_TILE);
+        }
+        {
+            PROF_BEGIN(GAC_K_COMBINE);
+            HIPCHK(launch_combine(a, c->combine_grid, s));
+            PROF_END(GAC_K_COMBINE);
+        }
+        HIPCHK(hipMemcpyAsync(c->h_total, c->status, 32, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        const int32_t W = c->h_total[0], NT = c->h_total[1];
+        if (c->h_total[4]) {
+            HIPCHK(hipMemsetAsync(c->status, 0, kStatusBytes, s));
+            HIPCHK(hipStreamSynchronize(s));
+            return gac_fail(GAC_E_HIP, "k_plan: a workgroup total never became visible");
+        }
+        if (W == INT32_MAX) return gac_fail(GAC_E_ARG, "window block total overflows int32");
+        if (!c->h_total[2]) return GAC_OK;
+        rc = ensure_ws(c, n, NT, W, s);
+        if (rc != GAC_OK) return rc;
     }
-    // the flat block count W is only known after the scan: read {W, T} back
-    // (8 bytes) so the tile workspace always fits (ranges may overlap).
-    HIPCHK(hipMemcpyAsync(c->h_total, c->total, 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    const int64_t W = c->h_total[0], NT = c->h_total[1];
-    if (W < 0) return gac_fail(GAC_E_ARG, "window block total overflows int32");
-    if (NT == 0) return GAC_OK;
-    rc = ensure_ws(c, n, NT, W);
-    if (rc != GAC_OK) return rc;
-    a.ridx = c->ridx;
-    a.bidx = c->bidx;
-    a.sum_head = c->sum_head;
-    a.sum_tail = c->sum_tail;
-    a.n_tiles = (int32_t)NT;
-    a.n_flat = (int32_t)W;
-    HIPCHK(launch_mark(a, s));
-    {
-        PROF_BEGIN(GAC_K_TILE);
-        HIPCHK(launch_tile(a, c->tile_grid, s));
-        PROF_END(GAC_K_TILE);
-    }
-    {
-        PROF_BEGIN(GAC_K_COMBINE);
-        HIPCHK(launch_combine(a, c->combine_grid, s));
-        PROF_END(GAC_K_COMBINE);
-    }
-    return GAC_OK;
+    return gac_fail(GAC_E_STATE, "scoring workspace still too small after growing it");
 }
 
 extern "C" int gac_score_ranges_device(gac_ctx *c, const gac_chainset *cs, const gac_range *d_ranges,

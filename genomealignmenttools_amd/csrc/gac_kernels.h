@@ -78,19 +78,29 @@ struct ScoreArgs {
     const DChain *chains;
     int64_t n_chains;
     const int4 *blk;     // [n_blocks + 1] {tStart, qStart, size, nflags}
+    const int2 *tspan;   // [n_blocks]     {tStart, tEnd} (window searches)
     const Range *ranges;
     int64_t n;
     // workspace
     RangeDesc *rdesc;    // [n]
     int32_t *nblk;       // [n]   window blocks per range
-    int32_t *goff;       // [n+1] exclusive scan of nblk (flat block offset)
+    int32_t *goff;       // [n]   exclusive scan of nblk inside the plan workgroup
+    int32_t *pb0;        // [n]   first window block (compact copy of rdesc.b0)
     int32_t *ridx;       // [W]   range owning each flat block
     int32_t *bidx;       // [W]   global block index of each flat block
     SegSum *sum_head;    // [T]   partial segment containing the tile's first block
     SegSum *sum_tail;    // [T]   partial segment containing the tile's last block
-    int32_t *total;      // [2]   W (flat blocks), T (tiles)
-    int32_t n_tiles;     // host copy of T (grid sizing / bounds)
-    int32_t n_flat;      // host copy of W
+    unsigned long long *gran;  // [G] {epoch, window-block total} of each plan workgroup
+    uint32_t *ticket;    // plan workgroups done: 8 XCD shards + top, 128 B apart (self-resetting)
+    int32_t *plan_off;   // [G]   flat offset of plan workgroup w
+    int32_t *chunk_off;  // [G]   first mark chunk of plan workgroup w
+    int32_t *chunk_wg;   // [cap_chunks] plan workgroup of each mark chunk
+    int32_t *status;     // [8]   W (flat blocks, saturated), T (tiles), 1 = workspace too
+                         //       small, mark chunks, error bits (1 = granule never seen)
+    uint32_t epoch;      // tag of this call's granules
+    int32_t cap_chunks;
+    int32_t cap_flat;    // ridx/bidx capacity
+    int32_t cap_tiles;   // sum_head/sum_tail capacity
     // outputs
     long long *out_g;
     long long *out_l;

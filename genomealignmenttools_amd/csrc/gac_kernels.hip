@@ -8,10 +8,10 @@
 //   chainCalcScoreLocal src/scoreChain/scoreChain.c:176-198  max-plus local score
 // Here one batch of sub-chains ("ranges") is scored by:
 //   k_plan    one lane per range: binary-search the block window (replaces
-//             the O(blocks) list walks of chainSubsetOnT / chainBaseCountSubT)
-//             and write a 40-byte range descriptor
-//   (scan)    hipcub exclusive sum of window blocks -> flat block offsets
-//   k_mark    flat block -> owning range id
+//             the O(blocks) list walks of chainSubsetOnT / chainBaseCountSubT),
+//             write a 32-byte range descriptor; workgroup scan of window
+//             blocks, the last workgroup scans the workgroup totals
+//   k_mark    flat block -> (range, block) map, in balanced chunks
 //   k_tile    one wave per tile of 64 consecutive flat blocks (ranges packed
 //             densely, many ranges per tile): lanes score 32-base chunks of
 //             2-bit packed T and Q straight from HBM (bit-plane popcounts, the
@@ -220,13 +220,10 @@ __device__ __forceinline__ int gallop_first(int n, int g, P pred) {
     return lo;
 }
 
-// One lane per range: window of blocks [b0, b0+n) with tEnd > s and tStart < e
+// Window of blocks [b0, b0+n) of range r: tEnd > s and tStart < e
 // (chainSubsetOnT's first-block walk and stop condition, chain.c:481-500),
 // plus the per-range descriptor the tile kernel needs.
-__global__ void __launch_bounds__(256) k_plan(ScoreArgs a) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n) return;
-    const Range r = a.ranges[i];
+__device__ __forceinline__ RangeDesc plan_range(const ScoreArgs &a, const Range r) {
     RangeDesc d;
     d.tbase = 0;
     d.qbase = 0;
@@ -236,7 +233,9 @@ __global__ void __launch_bounds__(256) k_plan(ScoreArgs a) {
     d.e = r.t_end;
     if (r.chain >= 0 && r.chain < a.n_chains && r.t_start < r.t_end) {
         const DChain c = a.chains[r.chain];
-        const int4 *bk = a.blk + c.blk_off;
+        // {tStart, tEnd} per block, 8 bytes: the last probes of a search fall
+        // in one 128-byte line
+        const int2 *sp = a.tspan + c.blk_off;
         const int n = c.nblk;
         // first block with tEnd > s (binary search; block spans are too
         // irregular -- heavy-tailed gaps -- for interpolation to pay)
@@ -244,8 +243,7 @@ __global__ void __launch_bounds__(256) k_plan(ScoreArgs a) {
         if (r.t_start >= c.tstart) {
             while (lo < hi) {
                 const int mid = (lo + hi) >> 1;
-                const int4 b = bk[mid];
-                if (b.x + b.z > r.t_start) hi = mid;
+                if (sp[mid].y > r.t_start) hi = mid;
                 else lo = mid + 1;
             }
         }
@@ -254,7 +252,7 @@ __global__ void __launch_bounds__(256) k_plan(ScoreArgs a) {
         const int stop = r.t_end > c.tend
                              ? n
                              : first + gallop_first(n - first, 0, [&](int k) {
-                                   return bk[first + k].x >= r.t_end;
+                                   return sp[first + k].x >= r.t_end;
                                });
         d.nblk = stop - first;
         d.b0 = (int32_t)(c.blk_off + first);
@@ -262,55 +260,203 @@ __global__ void __launch_bounds__(256) k_plan(ScoreArgs a) {
         const int64_t qw = a.q_woff[c.q_seq] * 32;
         d.qbase = c.qinfo < 0 ? ~(qw + (c.qinfo & 0x7fffffff)) : qw;
     }
-    a.rdesc[i] = d;
-    a.nblk[i] = d.nblk;
-    if (d.nblk == 0) {
-        a.out_g[i] = 0;
-        a.out_ali[i] = 0;
-        if (a.want_local) a.out_l[i] = 0;
-    }
+    return d;
 }
 
-__global__ void k_total(ScoreArgs a) {
-    if (threadIdx.x == 0) {
-        const int32_t w = a.goff[a.n - 1] + a.nblk[a.n - 1];
-        a.goff[a.n] = w;
-        a.total[0] = w;
-        a.total[1] = (w + kTileBlocks - 1) / kTileBlocks;
+// ------------------------------------------------------------ k_plan -----
+// One lane per range: plan, then a workgroup scan of the window blocks:
+// goff[i] = exclusive prefix inside the plan workgroup w = i / 256, pb0[i] =
+// first window block, and the workgroup total published as ONE 8-byte
+// {epoch, total} granule (sc1 store; needs no ordering against anything).
+// Workgroups then add to a counter; the last to add reads every granule
+// (spinning on any whose tag is not yet visible), scans the totals into
+// P[w] (flat offset of workgroup w) and CP[w] (its first mark chunk), writes
+// the mark-chunk table, and publishes {W, T, overflow, chunks} in status[].
+// No fences: on gfx950 an agent release/acquire per workgroup costs an L2
+// writeback/invalidate each (measured: +75 us on this kernel).
+constexpr int kPlanWG = 256;
+constexpr int kMarkChunk = 1024;  // flat blocks per k_mark work item
+constexpr int kSpinLimit = 1 << 22;
+
+__device__ __forceinline__ long long wg_exclusive_scan(long long v, long long *s_wsum,
+                                                      long long &total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    long long incl = v;
+#pragma unroll
+    for (int k = 1; k < kWave; k <<= 1) {
+        const long long o = __shfl_up(incl, k, kWave);
+        if (lane >= k) incl += o;
+    }
+    if (lane == kWave - 1) s_wsum[wave] = incl;
+    __syncthreads();
+    long long pre = 0;
+    total = 0;
+#pragma unroll
+    for (int w = 0; w < kPlanWG / kWave; ++w) {
+        const long long x = s_wsum[w];
+        if (w < wave) pre += x;
+        total += x;
+    }
+    __syncthreads();
+    return pre + incl - v;
+}
+
+__device__ __forceinline__ unsigned long long gran_load(const unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void __launch_bounds__(kPlanWG, 8) k_plan(ScoreArgs a) {
+    __shared__ long long s_wsum[kPlanWG / kWave];
+    __shared__ int s_last;
+    __shared__ uint32_t s_val[16 * kPlanWG];  // last workgroup: one batch of totals
+    const int tid = threadIdx.x;
+    const int64_t i = (int64_t)blockIdx.x * kPlanWG + tid;
+    int nb = 0;
+    if (i < a.n) {
+        const RangeDesc d = plan_range(a, a.ranges[i]);
+        a.rdesc[i] = d;
+        a.nblk[i] = nb = d.nblk;
+        a.pb0[i] = d.b0;
+        if (nb == 0) {
+            a.out_g[i] = 0;
+            a.out_ali[i] = 0;
+            if (a.want_local) a.out_l[i] = 0;
+        }
+    }
+    // 64-bit: 256 windows of a huge chain may exceed int32 (saturated; the
+    // host reports it)
+    long long agg;
+    const long long excl = wg_exclusive_scan(nb, s_wsum, agg);
+    if (agg > 0x7fffffffLL) agg = 0x7fffffffLL;
+    if (i < a.n) a.goff[i] = (int32_t)(excl < 0x7fffffffLL ? excl : 0x7fffffffLL);
+    const unsigned long long tag = (unsigned long long)a.epoch << 32;
+    if (tid == 0) {
+        __hip_atomic_store(&a.gran[blockIdx.x], tag | (uint32_t)agg, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        // arrival counter sharded by XCD (one word takes ~88 adds/us): the
+        // last arrival of each shard adds to the top counter
+        const int G = gridDim.x, x = blockIdx.x & 7;
+        const unsigned nx = (unsigned)((G - x + 7) >> 3), nshard = G < 8 ? G : 8;
+        uint32_t *sh = a.ticket + 32 * x, *top = a.ticket + 32 * 8;
+        bool last = false;
+        if (__hip_atomic_fetch_add(sh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nx - 1) {
+            *sh = 0u;  // every arrival of this shard is in: reset for the next call
+            last = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   nshard - 1;
+        }
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // ---- last workgroup: scan the totals, 4096 workgroups per batch (all
+    // granule loads of a batch in flight at once, coalesced; spin only on
+    // the rare granule whose tag is not visible yet)
+    constexpr int kPer = 16;
+    const int G = gridDim.x;
+    bool late = false;
+    long long carry = 0, ccarry = 0;
+    for (int b0 = 0; b0 < G; b0 += kPer * kPlanWG) {
+        // 4 loads in flight per lane (keeps the kernel at <= 64 VGPRs)
+#pragma unroll 1
+        for (int k0 = 0; k0 < kPer; k0 += 4) {
+            unsigned long long g[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int w = b0 + (k0 + k) * kPlanWG + tid;
+                g[k] = w < G ? gran_load(&a.gran[w]) : tag;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int w = b0 + (k0 + k) * kPlanWG + tid;
+                for (int spin = 0; (g[k] & ~0xffffffffull) != tag; ++spin) {
+                    if (spin > kSpinLimit) {
+                        late = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    g[k] = gran_load(&a.gran[w]);
+                }
+                s_val[(k0 + k) * kPlanWG + tid] = (uint32_t)g[k];
+            }
+        }
+        __syncthreads();
+        // thread t owns workgroups b0 + [kPer t, kPer t + kPer)
+        long long mine = 0, mch = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const long long v = s_val[kPer * tid + k];
+            mine += v;
+            mch += (v + kMarkChunk - 1) / kMarkChunk;
+        }
+        long long bt, bc;
+        long long run = carry + wg_exclusive_scan(mine, s_wsum, bt);
+        long long crun = ccarry + wg_exclusive_scan(mch, s_wsum, bc);
+        carry += bt;
+        ccarry += bc;
+        const bool fits = ccarry <= a.cap_chunks;
+#pragma unroll 1
+        for (int k = 0; k < kPer; ++k) {
+            const int w = b0 + kPer * tid + k;
+            if (w >= G) break;
+            const long long v = s_val[kPer * tid + k];
+            const long long ch = (v + kMarkChunk - 1) / kMarkChunk;
+            a.plan_off[w] = (int32_t)(run < 0x7fffffffLL ? run : 0x7fffffffLL);
+            a.chunk_off[w] = (int32_t)(crun < 0x7fffffffLL ? crun : 0x7fffffffLL);
+            if (fits)
+                for (long long c = 0; c < ch; ++c) a.chunk_wg[crun + c] = w;
+            run += v;
+            crun += ch;
+        }
+        __syncthreads();
+    }
+    long long W = carry;
+    const long long NQ = ccarry;
+    const bool sat = W >= 0x7fffffffLL;
+    if (sat) W = 0x7fffffffLL;
+    const long long T = (W + kTileBlocks - 1) / kTileBlocks;
+    const bool over = sat || W > a.cap_flat || T > a.cap_tiles || NQ > a.cap_chunks;
+    if (late) atomicOr(&a.status[4], 1);
+    if (tid == 0) {
+        a.ticket[32 * 8] = 0u;  // for the next call
+        a.status[0] = (int32_t)W;
+        a.status[1] = (int32_t)T;
+        a.status[2] = over ? 1 : 0;
+        a.status[3] = (int32_t)(NQ < 0x7fffffffLL ? NQ : 0x7fffffffLL);
     }
 }
 
 // ------------------------------------------------------------ k_mark -----
-// For every flat block j: ridx[j] = owning range, bidx[j] = global block
-// index.  A tile then maps lanes to ranges and blocks with one coalesced
-// (prefetched) load and issues the range-descriptor and block loads together.
-__global__ void __launch_bounds__(256) k_mark(ScoreArgs a) {
-    const int lane = threadIdx.x & 63;
-    const int64_t base = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) - lane;
-    const int64_t i = base + lane;
-    int nb = 0, g0 = 0, b0 = 0;
-    if (i < a.n) {
-        nb = a.nblk[i];
-        g0 = a.goff[i];
-        if (nb > 0) b0 = a.rdesc[i].b0;
-    }
-    // short windows: one lane each; long windows: the whole wave, coalesced
-    constexpr int kShort = 16;
-    if (nb <= kShort)
-        for (int k = 0; k < nb; ++k) {
-            a.ridx[g0 + k] = (int32_t)i;
-            a.bidx[g0 + k] = b0 + k;
+// Flat block -> (range, block) map.  Work item = one chunk of <= 1024 flat
+// blocks of one plan workgroup (balanced however long the windows are);
+// persistent grid over the chunk table.  The workgroup's 256 local offsets
+// go to LDS; each flat block finds its owner by an 8-step LDS search, and
+// the ridx/bidx stores are coalesced.
+__global__ void __launch_bounds__(kPlanWG) k_mark(ScoreArgs a) {
+    __shared__ int s_excl[kPlanWG];
+    __shared__ int s_b0[kPlanWG];
+    if (a.status[2]) return;  // workspace overflow: the host grows it and reruns
+    const int NQ = a.status[3], W = a.status[0];
+    const int G = (int)((a.n + kPlanWG - 1) / kPlanWG);
+    const int tid = threadIdx.x;
+    for (int q = blockIdx.x; q < NQ; q += gridDim.x) {
+        const int w = a.chunk_wg[q];
+        const int c = q - a.chunk_off[w];
+        const int base = a.plan_off[w];
+        const int tot = (w + 1 < G ? a.plan_off[w + 1] : W) - base;
+        const int64_t i = (int64_t)w * kPlanWG + tid;
+        s_excl[tid] = i < a.n ? a.goff[i] : 0x7fffffff;
+        s_b0[tid] = i < a.n ? a.pb0[i] : 0;
+        __syncthreads();
+        const int f1 = min(tot, (c + 1) * kMarkChunk);
+        for (int f = c * kMarkChunk + tid; f < f1; f += kPlanWG) {
+            int r = 0;
+#pragma unroll
+            for (int step = kPlanWG / 2; step > 0; step >>= 1)
+                if (s_excl[r + step] <= f) r += step;
+            a.ridx[base + f] = w * kPlanWG + r;
+            a.bidx[base + f] = s_b0[r] + (f - s_excl[r]);
         }
-    unsigned long long mask = __ballot(nb > kShort);
-    while (mask) {
-        const int src = __builtin_ctzll(mask);
-        mask &= mask - 1;
-        const int n = __shfl(nb, src, kWave), o = __shfl(g0, src, kWave);
-        const int bb = __shfl(b0, src, kWave);
-        for (int k = lane; k < n; k += kWave) {
-            a.ridx[o + k] = (int32_t)(base + src);
-            a.bidx[o + k] = bb + k;
-        }
+        __syncthreads();
     }
 }
 
@@ -381,7 +527,7 @@ __device__ __forceinline__ void seg_store(const ScoreArgs &a, int ri, long long 
 }
 
 template <bool LOCAL>
-__global__ void __launch_bounds__(256) k_tile(ScoreArgs a) {
+__global__ void __launch_bounds__(256, LOCAL ? 7 : 8) k_tile(ScoreArgs a) {
     __shared__ int32_t s_small[3 * kSmallCap];
     __shared__ WaveLds s_w[kWavesPerWG];
 
@@ -395,8 +541,9 @@ __global__ void __launch_bounds__(256) k_tile(ScoreArgs a) {
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     WaveLds &L = s_w[wave];
-    const int T = a.n_tiles;
-    const int W = a.n_flat;
+    if (a.status[2]) return;  // workspace overflow: the host grows it and reruns
+    const int T = a.status[1];
+    const int W = a.status[0];
     const unsigned long long lanemask_le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
 
     // XCD-aware logical id: workgroups b and b+8 share an XCD (round-robin
@@ -558,6 +705,7 @@ constexpr int kLaneFold = 16;
 
 template <bool LOCAL>
 __global__ void __launch_bounds__(256) k_combine(ScoreArgs a) {
+    if (a.status[2]) return;
     const int lane = threadIdx.x & 63;
     const int64_t wave_id = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -567,7 +715,7 @@ __global__ void __launch_bounds__(256) k_combine(ScoreArgs a) {
         if (my < a.n) {
             const int nb = a.nblk[my];
             if (nb > 0) {
-                const int g0 = a.goff[my];
+                const int g0 = a.plan_off[my / kPlanWG] + a.goff[my];
                 tf = g0 / kTileBlocks;
                 tl = (g0 + nb - 1) / kTileBlocks;
             }
@@ -686,32 +834,29 @@ __global__ void __launch_bounds__(256) k_nruns(const NPiece *pieces, int64_t n, 
 }  // namespace gac
 
 // ---------------------------------------------------------------- launch --
-#include <hipcub/hipcub.hpp>
-
 namespace gac {
 
-size_t scan_temp_bytes(int64_t n) {
-    size_t bytes = 0;
-    hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (int32_t *)nullptr, (int32_t *)nullptr,
-                                     (int)n, (hipStream_t)0);
-    return bytes;
-}
+int plan_grid(int64_t n) { return (int)((n + kPlanWG - 1) / kPlanWG); }
 
-hipError_t launch_plan(const ScoreArgs &a, void *temp, size_t temp_bytes, hipStream_t s) {
-    const int64_t nb = (a.n + 255) / 256;
-    hipLaunchKernelGGL(k_plan, dim3((unsigned)nb), dim3(256), 0, s, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, a.nblk, a.goff, (int)a.n, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_total, dim3(1), dim3(64), 0, s, a);
+hipError_t launch_plan(const ScoreArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(k_plan, dim3((unsigned)plan_grid(a.n)), dim3(kPlanWG), 0, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_mark(const ScoreArgs &a, hipStream_t s) {
-    const int64_t nb = (a.n + 255) / 256;
-    hipLaunchKernelGGL(k_mark, dim3((unsigned)nb), dim3(256), 0, s, a);
+int mark_chunks_bound(int64_t flat, int64_t n) { return (int)(flat / kMarkChunk + plan_grid(n) + 2); }
+
+hipError_t launch_mark(const ScoreArgs &a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_mark, dim3(grid), dim3(kPlanWG), 0, s, a);
     return hipGetLastError();
+}
+
+// Resident workgroups per CU of the persistent tile kernel (the grid must not
+// exceed what fits at once, or the last workgroups run as a second wave).
+int tile_blocks_per_cu(bool local) {
+    int nb = 0;
+    hipError_t e = local ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<true>, 256, 0)
+                         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<false>, 256, 0);
+    return (e == hipSuccess && nb > 0) ? nb : 4;
 }
 
 hipError_t launch_tile(const ScoreArgs &a, int grid, hipStream_t s) {

@@ -159,8 +159,10 @@ int gac_score_ranges(gac_ctx *ctx, const gac_chainset *cs, const gac_range *rang
                      int64_t n, uint32_t flags, int64_t *global, int64_t *local,
                      int32_t *ali);
 /* Same on device-resident buffers, enqueued on `stream` (a hipStream_t, or
- * NULL for the context's own stream); returns without synchronising.
- * d_local may be NULL unless GAC_WANT_LOCAL. */
+ * NULL for the context's own stream).  Four kernel launches; the call then
+ * waits for `stream` to read back a 32-byte status (the scoring workspace is
+ * sized on the device and grown + rerun here when a batch outgrows it), so
+ * results are ready on return.  d_local may be NULL unless GAC_WANT_LOCAL. */
 int gac_score_ranges_device(gac_ctx *ctx, const gac_chainset *cs,
                             const gac_range *d_ranges, int64_t n, uint32_t flags,
                             int64_t *d_global, int64_t *d_local, int32_t *d_ali,
@@ -230,7 +232,7 @@ int gac_memcpy_d2h(gac_ctx *ctx, void *dst, const void *src, size_t bytes);
 int gac_synchronize(gac_ctx *ctx);
 
 /* ---- kernel timing (HIP events on the launch stream) -------------------- */
-#define GAC_K_PLAN 0     /* per-range block-window search */
+#define GAC_K_PLAN 0     /* block-window search + scan + flat-block map (k_plan, k_mark) */
 #define GAC_K_TILE 1     /* tile scoring: bases, gaps, per-tile scan (dominant) */
 #define GAC_K_COMBINE 2  /* multi-tile range combine */
 #define GAC_K_COUNT 3

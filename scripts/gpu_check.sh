@@ -9,8 +9,11 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 make -j16 all oracle > "$OUT/build.log" 2>&1 || { echo "build failed"; exit 1; }
 timeout -k 10 900 python -m pytest tests -x -q -m gpu > "$OUT/tests.log" 2>&1
-echo "pytest rc=$?" >> "$OUT/tests.log"
+rc=$?
+echo "pytest rc=$rc" >> "$OUT/tests.log"
 tail -3 "$OUT/tests.log"
+# 0 = pass, 1 = a test failed; anything else (abort, fault, time limit): stop here
+[ $rc -le 1 ] || exit $rc
 timeout -k 10 900 python bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench failed"; tail -20 "$OUT/bench.err"; exit 1; }
 cat "$OUT/bench.json"
 cd /tmp && export TMPDIR=/tmp

@@ -1,0 +1,53 @@
+"""Summarise rocprofv3 --pmc passes (scripts/gpu_counters.sh output) into one
+JSON: per kernel, the mean counter value per dispatch, plus derived figures
+(FETCH_SIZE/WRITE_SIZE in bytes, waves and wait fractions).
+
+usage: python scripts/pmc_summary.py gpurun_out/TAG > profiles/rNN_pmc_summary.json
+
+FETCH_SIZE / WRITE_SIZE are reported by rocprofv3 in KiB; per
+/opt/skills/guides/MI355X_MICROARCH.md the gfx950 FETCH_SIZE derivation counts
+64-byte requests at 128 bytes, so reads made only of wide (128-B) requests are
+exact and the figure is an upper bound otherwise.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def short(name):
+    name = name.split("(")[0]
+    return name.replace("void ", "").strip()
+
+
+def main(root):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for path in sorted(glob.glob(os.path.join(root, "pmc*", "*counter_collection.csv"))):
+        per = collections.defaultdict(float)
+        meta = {}
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                key = (r["Dispatch_Id"], short(r["Kernel_Name"]), r["Counter_Name"])
+                per[key] += float(r["Counter_Value"])  # summed over dimensions
+                meta[r["Dispatch_Id"]] = (r["VGPR_Count"], r["SGPR_Count"], r["LDS_Block_Size"])
+        for (_, k, c), v in per.items():
+            acc[k][c].append(v)
+    out = {}
+    for k, cs in sorted(acc.items()):
+        d = {c: sum(v) / len(v) for c, v in sorted(cs.items())}
+        d["dispatches"] = max(len(v) for v in cs.values())
+        if "FETCH_SIZE" in d:
+            d["fetch_bytes"] = d["FETCH_SIZE"] * 1024.0
+        if "WRITE_SIZE" in d:
+            d["write_bytes"] = d["WRITE_SIZE"] * 1024.0
+        if d.get("SQ_WAVE_CYCLES"):
+            d["wait_any_frac"] = d.get("SQ_WAIT_ANY", 0.0) / d["SQ_WAVE_CYCLES"]
+        out[k] = d
+    json.dump(out, sys.stdout, indent=1, sort_keys=True)
+    print()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

@@ -48,6 +48,44 @@ def test_ranges_vs_oracle(seed):
     assert np.array_equal(a, oa)
 
 
+def test_workspace_growth_and_lookback():
+    """One engine, batches of growing size: the first call's workspace guess
+    is outgrown (device-side overflow flag -> grow -> rerun), k_plan's
+    look-back crosses many 64-workgroup windows (60k ranges = 235 plan
+    workgroups), empty windows are interleaved, and repeated calls (new
+    look-back epochs) give identical results."""
+    from genomealignmenttools_amd import synth
+    tg, qg, ca = synth.small_case(seed=4, n_chains=300, max_blocks=2000)
+    e, cs = _setup(None, tg, qg, ca)
+    orc = _oracle(tg, qg)
+    rng = np.random.default_rng(4)
+    full = np.stack([np.arange(ca.n), ca.tstart, ca.tend], 1).astype(np.int64)
+    # 1) tiny batch, then full chains (many more window blocks per range)
+    for R in (full[:3], full):
+        g, l, a = e.score_ranges(cs, R, want_local=True)
+        og, ol, oa = orc.score_ranges(ca, R)
+        assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
+    # 2) 60k short ranges, a third of them selecting nothing
+    c = rng.integers(0, ca.n, 60_000)
+    s = rng.integers(ca.tstart[c] - 100, ca.tend[c])
+    ln = rng.integers(1, 3000, len(c))
+    R = np.stack([c, s, s + ln], 1).astype(np.int64)
+    R[::3, 2] = R[::3, 1]  # empty
+    og, ol, oa = orc.score_ranges(ca, R)
+    for _ in range(3):
+        g, l, a = e.score_ranges(cs, R, want_local=True)
+        assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
+    # 3) > 4096 plan workgroups (1.14M ranges): the pre-scanned offsets path
+    RR = np.tile(R, (19, 1))
+    g, l, a = e.score_ranges(cs, RR, want_local=True)
+    assert np.array_equal(g, np.tile(og, 19)) and np.array_equal(l, np.tile(ol, 19))
+    assert np.array_equal(a, np.tile(oa, 19))
+    # 4) back to the full chains with the grown workspace
+    g, _, a = e.score_ranges(cs, full)
+    og, _, oa = orc.score_ranges(ca, full)
+    assert np.array_equal(g, og) and np.array_equal(a, oa)
+
+
 def test_long_chains_multi_tile():
     """Chains of thousands of blocks: ranges span many 64-block tiles."""
     from genomealignmenttools_amd import synth
