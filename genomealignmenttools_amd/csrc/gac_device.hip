@@ -9,6 +9,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -38,6 +39,8 @@ struct NPiece {
 };
 hipError_t launch_relayout(const uint8_t *raw, const SeqDev *seqs, int nseq, int64_t nwords,
                            uint2 *planes, uint32_t *nmask, hipStream_t s);
+hipError_t launch_gap_table(const GapDev &g, const int32_t *small, int len, int32_t *tab,
+                            hipStream_t s);
 hipError_t launch_nflags(const DChain *chains, int64_t n_chains, int4 *blk,
                          const uint32_t *t_nmask, const int64_t *t_woff, const uint32_t *q_nmask,
                          const int64_t *q_woff, hipStream_t s);
@@ -93,7 +96,8 @@ struct gac_ctx {
     int32_t coef[16];
     GapDev gap;
     int32_t *d_small = nullptr;
-    int small_in_lds = 0;
+    int32_t *d_gap_tab = nullptr;  // [3][gap_len]
+    int gap_len = 0;
     // workspace
     int64_t ws_n = 0;
     RangeDesc *rdesc = nullptr;
@@ -189,7 +193,7 @@ extern "C" void gac_close(gac_ctx *c) {
     hipStreamSynchronize(c->stream);
     free_genome(c->g[0]);
     free_genome(c->g[1]);
-    void *bufs[] = {c->d_small,  c->rdesc,    c->nblk,     c->goff, c->pb0, c->gran, c->plan_off, c->chunk_off, c->chunk_wg,
+    void *bufs[] = {c->d_small,  c->d_gap_tab, c->rdesc,    c->nblk,     c->goff, c->pb0, c->gran, c->plan_off, c->chunk_off, c->chunk_wg,
                     c->status,   c->ridx,     c->bidx,     c->sum_head, c->sum_tail,
                     c->d_ranges, c->d_g,      c->d_l,      c->d_ali};
     for (void *p : bufs)
@@ -221,6 +225,9 @@ extern "C" int gac_set_scoring(gac_ctx *c, const int32_t mat[16], const gac_gapc
     if (g->small_size < 1 || g->small_size != g->long_pos[0])
         return gac_fail(GAC_E_ARG, "inconsistent gap table (smallSize %d)", g->small_size);
     HIPCHK(hipSetDevice(c->device));
+    for (int i = 0; i < 16; ++i)  // the kernel multiplies in 24 bits (v_mad_i32_i24)
+        if (mat[i] <= -(1 << 22) || mat[i] >= (1 << 22))
+            return gac_fail(GAC_E_ARG, "score matrix entry %d out of range (|s| < 2^22)", mat[i]);
     for (int qc = 0; qc < 4; ++qc)
         for (int tc = 0; tc < 4; ++tc)
             c->coef[qc * 4 + tc] = mat[acgt_of_code(qc) * 4 + acgt_of_code(tc)];
@@ -251,7 +258,19 @@ extern "C" int gac_set_scoring(gac_ctx *c, const int32_t mat[16], const gac_gapc
     c->d_small = nullptr;
     HIPCHK(hipMalloc(&c->d_small, small.size() * 4));
     HIPCHK(hipMemcpy(c->d_small, small.data(), small.size() * 4, hipMemcpyHostToDevice));
-    c->small_in_lds = g->small_size <= kSmallCap;
+    // gap-cost table up to the last table position (everything beyond is the
+    // slope branch); capped at GAC_GAP_TABLE_MAX entries per kind (default
+    // 2^22) -- lengths past a capped table are evaluated in the kernel
+    int64_t len = std::max(std::max(g->q_last_pos, g->t_last_pos), g->b_last_pos);
+    int64_t cap = 1 << 22;
+    if (const char *env = getenv("GAC_GAP_TABLE_MAX")) cap = std::max(1LL, atoll(env));
+    len = std::max<int64_t>(g->small_size, std::min(len, cap));
+    if (c->d_gap_tab) hipFree(c->d_gap_tab);
+    c->d_gap_tab = nullptr;
+    HIPCHK(hipMalloc(&c->d_gap_tab, 3 * len * 4));
+    HIPCHK(launch_gap_table(d, c->d_small, (int)len, c->d_gap_tab, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->gap_len = (int)len;
     c->scoring = true;
     return GAC_OK;
 }
@@ -636,7 +655,8 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
     a.out_l = d_l;
     a.out_ali = d_ali;
     a.want_local = (flags & GAC_WANT_LOCAL) ? 1 : 0;
-    a.small_in_lds = c->small_in_lds;
+    a.gap_len = c->gap_len;
+    a.gap_tab = c->d_gap_tab;
     a.small_tab = c->d_small;
     memcpy(a.coef, c->coef, sizeof(a.coef));
     a.gap = c->gap;

@@ -19,7 +19,6 @@ namespace gac {
 constexpr int kWave = 64;        // CDNA wavefront
 constexpr int kTileBlocks = 64;  // blocks per tile (one per lane)
 constexpr int kWavesPerWG = 4;   // 256-thread workgroups
-constexpr int kSmallCap = 256;   // gap small-table entries staged in LDS
 constexpr int kMaxLong = 32;     // long gap positions
 constexpr long long kNeg = -(1LL << 61);  // -inf of the local-score monoid
 
@@ -106,7 +105,8 @@ struct ScoreArgs {
     long long *out_l;
     int32_t *out_ali;
     int32_t want_local;
-    int32_t small_in_lds;
+    int32_t gap_len;           // gap_tab entries per kind
+    const int32_t *gap_tab;    // [3][gap_len] gapCalcCost by kind (q, t, both) and length
     const int32_t *small_tab;  // [3][small_size] q, t, both
     int32_t coef[16];          // score of (query code << 2 | target code)
     GapDev gap;

@@ -53,25 +53,43 @@ __device__ __forceinline__ int interp_long(int x, const GapDev &g, int which) {
     return (int)__dadd_rn(v[n - 2], __ddiv_rn(prod, (double)ds));
 }
 
-__device__ __forceinline__ int gap_cost(const GapDev &g, const int32_t *small, int dq, int dt) {
-    if (dt < 0) dt = 0;
-    if (dq < 0) dq = 0;
-    int which, d;
-    if (dt == 0) {
-        which = 0;
-        d = dq;
-    } else if (dq == 0) {
-        which = 1;
-        d = dt;
-    } else {
-        which = 2;
-        d = dq + dt;
-    }
+// Cost of a gap of kind `which` (0 = query-only, 1 = target-only, 2 = both)
+// and length d, the three branches of gapCalcCost.
+__device__ __forceinline__ int gap_cost_wd(const GapDev &g, const int32_t *small, int which,
+                                           int d) {
     if (d < g.small_size) return small[which * g.small_size + d];
     if (d >= g.last_pos[which])
         return (int)__dadd_rn(g.last_val[which],
                               __dmul_rn(g.last_slope[which], (double)(d - g.last_pos[which])));
     return interp_long(d, g, which);
+}
+
+// gapCalcCost's kind/length from (dq, dt)
+__device__ __forceinline__ int gap_kind(int dq, int dt, int &d) {
+    if (dt < 0) dt = 0;
+    if (dq < 0) dq = 0;
+    if (dt == 0) {
+        d = dq;
+        return 0;
+    }
+    if (dq == 0) {
+        d = dt;
+        return 1;
+    }
+    d = dq + dt;
+    return 2;
+}
+
+// Gap-cost table [3][len] built once per scoring setup from gap_cost_wd (the
+// scoring kernel then needs one load per gap; lengths >= len, i.e. beyond the
+// last table position, take the slope branch or, past a capped table, the
+// interpolation).
+__global__ void __launch_bounds__(256) k_gap_table(GapDev g, const int32_t *small, int len,
+                                                   int32_t *tab) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 3 * (int64_t)len) return;
+    const int which = (int)(i / len), d = (int)(i % len);
+    tab[i] = gap_cost_wd(g, small, which, d);
 }
 
 // ------------------------------------------------------------ helpers ----
@@ -506,15 +524,21 @@ __device__ __forceinline__ int chunk_score(const ScoreArgs &a, const WaveLds &L,
     for (int qc = 0; qc < 4; ++qc)
 #pragma unroll
         for (int tc = 0; tc < 4; ++tc)
-            sc += a.coef[qc * 4 + tc] * __builtin_popcount(qm[qc] & tm[tc]);
+            sc += __mul24(a.coef[qc * 4 + tc], (int)__builtin_popcount(qm[qc] & tm[tc]));
     return sc;
 }
 
-__device__ __forceinline__ int find_chunk_block(const WaveLds &L, int nact, int j) {
+// Block owning chunk j: the largest k with coff[k] <= j (coff is
+// non-decreasing; blocks without chunks share the next block's offset and
+// lanes past the tile's end hold the chunk total, so no bounds are needed).
+// 4-ary: three rounds of three independent LDS reads.
+__device__ __forceinline__ int find_chunk_block(const WaveLds &L, int j) {
     int k = 0;
 #pragma unroll
-    for (int step = 32; step > 0; step >>= 1)
-        if (k + step < nact && L.coff[k + step] <= j) k += step;
+    for (int step = 16; step > 0; step >>= 2) {
+        const int c1 = L.coff[k + step], c2 = L.coff[k + 2 * step], c3 = L.coff[k + 3 * step];
+        k += step * ((c1 <= j) + (c2 <= j) + (c3 <= j));
+    }
     return k;
 }
 
@@ -528,15 +552,7 @@ __device__ __forceinline__ void seg_store(const ScoreArgs &a, int ri, long long 
 
 template <bool LOCAL>
 __global__ void __launch_bounds__(256, LOCAL ? 7 : 8) k_tile(ScoreArgs a) {
-    __shared__ int32_t s_small[3 * kSmallCap];
     __shared__ WaveLds s_w[kWavesPerWG];
-
-    if (a.small_in_lds) {
-        for (int i = threadIdx.x; i < 3 * a.gap.small_size; i += blockDim.x)
-            s_small[i] = a.small_tab[i];
-    }
-    __syncthreads();
-    const int32_t *small = a.small_in_lds ? s_small : a.small_tab;
 
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
@@ -593,7 +609,12 @@ __global__ void __launch_bounds__(256, LOCAL ? 7 : 8) k_tile(ScoreArgs a) {
             }
             if (cte > d.e) cte = d.e;
             len = cte - cts;
-            if (!last) g = gap_cost(a.gap, small, nx.y - qe, nx.x - te);
+            if (!last) {
+                int d;
+                const int which = gap_kind(nx.y - qe, nx.x - te, d);
+                g = d < a.gap_len ? a.gap_tab[which * a.gap_len + d]
+                                  : gap_cost_wd(a.gap, a.small_tab, which, d);
+            }
             tpos = d.tbase + cts;
             const bool minus = d.qbase < 0;
             qpos = minus ? ~d.qbase - cqs : d.qbase + cqs;
@@ -608,7 +629,6 @@ __global__ void __launch_bounds__(256, LOCAL ? 7 : 8) k_tile(ScoreArgs a) {
             if (lane >= d) incl += o;
         }
         const int C = __shfl(incl, kWave - 1, kWave);
-        const int nact = min(kTileBlocks, W - tile * kTileBlocks);
         L.coff[lane] = incl - nch;
         L.tpos[lane] = tpos;
         L.qpos[lane] = qpos;
@@ -620,12 +640,12 @@ __global__ void __launch_bounds__(256, LOCAL ? 7 : 8) k_tile(ScoreArgs a) {
             const int ja = c0 + lane, jb = ja + kWave;
             int ka = 0, kb = 0, sa = 0, sb = 0;
             if (ja < C) {
-                ka = find_chunk_block(L, nact, ja);
+                ka = find_chunk_block(L, ja);
                 const int off = (ja - L.coff[ka]) << 5;
                 sa = chunk_score(a, L, ka, off, min(32, (L.lenq[ka] & kLenMask) - off));
             }
             if (jb < C) {
-                kb = find_chunk_block(L, nact, jb);
+                kb = find_chunk_block(L, jb);
                 const int off = (jb - L.coff[kb]) << 5;
                 sb = chunk_score(a, L, kb, off, min(32, (L.lenq[kb] & kLenMask) - off));
             }
@@ -872,6 +892,13 @@ hipError_t launch_combine(const ScoreArgs &a, int grid, hipStream_t s) {
         hipLaunchKernelGGL(k_combine<true>, dim3(grid), dim3(256), 0, s, a);
     else
         hipLaunchKernelGGL(k_combine<false>, dim3(grid), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_gap_table(const GapDev &g, const int32_t *small, int len, int32_t *tab,
+                            hipStream_t s) {
+    const int64_t nb = (3 * (int64_t)len + 255) / 256;
+    hipLaunchKernelGGL(k_gap_table, dim3((unsigned)nb), dim3(256), 0, s, g, small, len, tab);
     return hipGetLastError();
 }
 

@@ -152,11 +152,16 @@ def test_edge_ranges():
     assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
 
 
-@pytest.mark.parametrize("gap", ["loose", "medium"])
-def test_gap_costs_exhaustive(gap):
+@pytest.mark.parametrize("gap,table_max", [("loose", None), ("medium", None),
+                                           ("loose", "150"), ("medium", "5000")])
+def test_gap_costs_exhaustive(gap, table_max, monkeypatch):
     """All-N genomes score every block 0, so a 2-block chain scores exactly
-    -gapCalcCost(dq, dt): checks the device gap path (small tables, f64
-    interpolation, huge-gap slope) against the oracle for ~300k gap shapes."""
+    -gapCalcCost(dq, dt): checks the device gap path (the per-setup gap-cost
+    table, and with a capped table the in-kernel small-table / f64
+    interpolation / huge-gap slope branches) against the oracle for ~300k
+    gap shapes."""
+    if table_max:
+        monkeypatch.setenv("GAC_GAP_TABLE_MAX", table_max)
     from genomealignmenttools_amd import synth
     from genomealignmenttools_amd.chainfile import ChainArrays
     from oracle.oracle import OracleGap
