@@ -47,6 +47,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0,
                    help="target CPU seconds for the cpu_baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--prof", choices=["tile", "all", "none"], default="tile",
+                   help="kernels bracketed by HIP events inside the timed region "
+                        "(the roofline needs k_tile's)")
     p.add_argument("--tmp", default=os.environ.get("TMPDIR", "/tmp"))
     return p.parse_args()
 
@@ -119,7 +122,8 @@ def main():
         e.score_ranges_device(cs, d_r, n, d_g, d_a)
     e.synchronize()
     e.prof_reset()
-    e.prof_enable(True)
+    if args.prof != "none":
+        e.prof_enable(True, None if args.prof == "all" else [GAC_K_TILE])
     barrier()
     e.synchronize()
     t0 = time.perf_counter()
@@ -130,9 +134,18 @@ def main():
     dt = time.perf_counter() - t0
     e.prof_enable(False)
     tile_ms, tile_n = e.prof_read(GAC_K_TILE)
+    # per-kernel breakdown: a separate, untimed pass with every kernel bracketed
+    e.prof_reset()
+    e.prof_enable(True)
+    for _ in range(min(args.steps, 5)):
+        e.score_ranges_device(cs, d_r, n, d_g, d_a)
+    e.synchronize()
+    e.prof_enable(False)
     kern_ms = {name: e.prof_read(k)[0] / max(e.prof_read(k)[1], 1)
                for name, k in (("plan+mark", GAC_K_PLAN), ("tile", GAC_K_TILE),
                                ("combine", GAC_K_COMBINE))}
+    if args.prof == "none":  # roofline from the breakdown pass
+        tile_ms, tile_n = kern_ms["tile"], 1
     step_s = dt / args.steps
     if dist is not None:
         from genomealignmenttools_amd.shard import reduce_time_and_work

@@ -84,8 +84,8 @@ struct Prof {
 
 }  // namespace
 
-// status[0..8) + 9 arrival counters on their own 128-byte lines
-constexpr size_t kStatusBytes = 128 + 9 * 128;
+// status[0..8) + 33 arrival counters (32 shards + top), each on its own 128-byte line
+constexpr size_t kStatusBytes = 128 + 33 * 128;
 
 struct gac_ctx {
     int device = 0;
@@ -124,7 +124,7 @@ struct gac_ctx {
     int tile_grid_l = 2048;     // k_tile<true> grid
     int combine_grid = 512;
     // profiling
-    bool prof = false;
+    int prof = 0;  // mask of timed kernels
     std::vector<Prof> prof_pending;
     std::vector<hipEvent_t> prof_free;
     double prof_ms[GAC_K_COUNT] = {0};
@@ -138,6 +138,7 @@ struct gac_chainset {
     DChain *chains = nullptr;
     int4 *blk = nullptr;  // {tStart, qStart, size, nflags}, padded by one entry
     int2 *tspan = nullptr;  // {tStart, tEnd}
+    uint32_t *bucket = nullptr;  // per-chain bucket indexes
 };
 
 // ----------------------------------------------------------------- context
@@ -499,10 +500,38 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
     for (int64_t b = 0; b < d->n_blocks; ++b)
         blk[b] = make_int4(d->blk_t[b], d->blk_q[b], d->blk_size[b], 0);
     blk[d->n_blocks] = make_int4(0, 0, 0, 0);
-    std::vector<int2> tspan((size_t)d->n_blocks + 1);
+    // per-chain bucket indexes (layout: gac_kernels.h, DChain)
+    int64_t idx_n = 0;
+    for (int64_t i = 0; i < d->n_chains; ++i) {
+        const int64_t nb = ch[i].nblk;
+        const int64_t span = (int64_t)ch[i].tend - ch[i].tstart;
+        int shift = 0;
+        while (span > 0 && (((span - 1) >> shift) + 1) > std::max<int64_t>(2 * nb, 1)) ++shift;
+        ch[i].shift = shift;
+        ch[i].pad = 0;
+        ch[i].idx_off = idx_n;
+        idx_n += (span > 0 ? ((span - 1) >> shift) + 1 : 0) + 1;
+        ch[i].tbase = c->g[0].woff[ch[i].t_seq] * 32;
+        const int64_t qw = c->g[1].woff[ch[i].q_seq] * 32;
+        ch[i].qbase = ch[i].qinfo < 0 ? ~(qw + (ch[i].qinfo & 0x7fffffff)) : qw;
+    }
+    std::vector<uint32_t> bucket((size_t)std::max<int64_t>(idx_n, 1));
+    for (int64_t i = 0; i < d->n_chains; ++i) {
+        const int64_t b0 = ch[i].blk_off, nb = ch[i].nblk;
+        const int64_t span = (int64_t)ch[i].tend - ch[i].tstart;
+        const int64_t nbk = span > 0 ? ((span - 1) >> ch[i].shift) + 1 : 0;
+        uint32_t *bk = bucket.data() + ch[i].idx_off;
+        int64_t b = 0;
+        for (int64_t k = 0; k < nbk; ++k) {
+            const int64_t pos = ch[i].tstart + (k << ch[i].shift);
+            while (b < nb && (int64_t)d->blk_t[b0 + b] + d->blk_size[b0 + b] <= pos) ++b;
+            bk[k] = (uint32_t)b;
+        }
+        bk[nbk] = (uint32_t)nb;
+    }
+    std::vector<int2> tspan((size_t)d->n_blocks + 8, make_int2(INT32_MAX, INT32_MAX));
     for (int64_t b = 0; b < d->n_blocks; ++b)
         tspan[b] = make_int2(d->blk_t[b], d->blk_t[b] + d->blk_size[b]);
-    tspan[d->n_blocks] = make_int2(0, 0);
     gac_chainset *cs = new gac_chainset();
     cs->ctx = c;
     cs->n_chains = d->n_chains;
@@ -513,6 +542,9 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
         e = hipMemcpy(cs->chains, ch.data(), ch.size() * sizeof(DChain), hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipMemcpy(cs->blk, blk.data(), blk.size() * sizeof(int4), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&cs->bucket, bucket.size() * 4);
+    if (e == hipSuccess)
+        e = hipMemcpy(cs->bucket, bucket.data(), bucket.size() * 4, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&cs->tspan, tspan.size() * sizeof(int2));
     if (e == hipSuccess)
         e = hipMemcpy(cs->tspan, tspan.data(), tspan.size() * sizeof(int2), hipMemcpyHostToDevice);
@@ -535,6 +567,7 @@ extern "C" void gac_chains_free(gac_chainset *cs) {
     if (cs->chains) hipFree(cs->chains);
     if (cs->blk) hipFree(cs->blk);
     if (cs->tspan) hipFree(cs->tspan);
+    if (cs->bucket) hipFree(cs->bucket);
     delete cs;
 }
 
@@ -607,13 +640,13 @@ static hipEvent_t prof_event(gac_ctx *c) {
 
 #define PROF_BEGIN(k)                                   \
     hipEvent_t _pa = nullptr, _pb = nullptr;            \
-    if (c->prof) {                                      \
+    if (c->prof & (1 << (k))) {                         \
         _pa = prof_event(c);                            \
         _pb = prof_event(c);                            \
         hipEventRecord(_pa, s);                         \
     }
 #define PROF_END(k)                                     \
-    if (c->prof) {                                      \
+    if (_pa) {                                          \
         hipEventRecord(_pb, s);                         \
         c->prof_pending.push_back(Prof{(k), _pa, _pb}); \
     }
@@ -649,6 +682,7 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
     a.n_chains = cs->n_chains;
     a.blk = cs->blk;
     a.tspan = cs->tspan;
+    a.bucket = cs->bucket;
     a.ranges = d_ranges;
     a.n = n;
     a.out_g = d_g;
@@ -801,7 +835,7 @@ extern "C" int gac_synchronize(gac_ctx *c) {
 // ----------------------------------------------------------------- profiling
 extern "C" int gac_prof_enable(gac_ctx *c, int on) {
     if (!c) return gac_fail(GAC_E_ARG, "NULL context");
-    c->prof = on != 0;
+    c->prof = on & GAC_PROF_ALL;
     return GAC_OK;
 }
 

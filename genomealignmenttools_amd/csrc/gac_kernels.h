@@ -27,11 +27,26 @@ struct DChain {
     int32_t nblk;
     int32_t t_seq;
     int32_t q_seq;
-    int32_t qinfo;   // q_seq size (reverse-complement index base) | strand << 31
-    int32_t tstart;  // target span of the blocks (interpolation guesses)
+    int32_t qinfo;     // q_seq size (reverse-complement index base) | strand << 31
+    int32_t tstart;    // target span of the blocks
     int32_t tend;
+    int64_t idx_off;   // this chain's bucket index in ScoreArgs::bucket
+    int32_t shift;     // bucket width = 2^shift target bases
+    int32_t pad;
+    int64_t tbase;     // global base index of the target sequence start (word_off * 32)
+    int64_t qbase;     // '+': global base index of the query sequence start;
+                       // '-': ~(word_off * 32 + qSize)  (as RangeDesc::qbase)
 };
-static_assert(sizeof(DChain) == 32, "DChain layout");
+static_assert(sizeof(DChain) == 64, "DChain layout: one 64-byte record");
+
+// Bucket index of a chain (built at upload): the target span [tstart, tend)
+// is cut into nb = ((tend - tstart - 1) >> shift) + 1 buckets of 2^shift
+// bases (shift chosen so that nb <= 2 * blocks), and
+//   bucket[idx_off + k] = first block with tEnd > tstart + (k << shift),
+//   bucket[idx_off + nb] = blocks.
+// The first block with tEnd > s then lies in [bucket[k], bucket[k + 1]],
+// k = (s - tstart) >> shift: one 8-byte load plus a search of that bracket
+// (usually one or two blocks) replaces a log2(blocks) binary search.
 
 struct GapDev {
     int32_t small_size;
@@ -77,7 +92,8 @@ struct ScoreArgs {
     const DChain *chains;
     int64_t n_chains;
     const int4 *blk;     // [n_blocks + 1] {tStart, qStart, size, nflags}
-    const int2 *tspan;   // [n_blocks]     {tStart, tEnd} (window searches)
+    const int2 *tspan;   // [n_blocks + 8] {tStart, tEnd} (window ends; padded)
+    const uint32_t *bucket;  // chain bucket indexes (see DChain)
     const Range *ranges;
     int64_t n;
     // workspace
@@ -90,7 +106,7 @@ struct ScoreArgs {
     SegSum *sum_head;    // [T]   partial segment containing the tile's first block
     SegSum *sum_tail;    // [T]   partial segment containing the tile's last block
     unsigned long long *gran;  // [G] {epoch, window-block total} of each plan workgroup
-    uint32_t *ticket;    // plan workgroups done: 8 XCD shards + top, 128 B apart (self-resetting)
+    uint32_t *ticket;    // plan workgroups done: 32 shards + top, 128 B apart (self-resetting)
     int32_t *plan_off;   // [G]   flat offset of plan workgroup w
     int32_t *chunk_off;  // [G]   first mark chunk of plan workgroup w
     int32_t *chunk_wg;   // [cap_chunks] plan workgroup of each mark chunk

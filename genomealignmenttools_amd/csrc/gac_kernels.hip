@@ -238,9 +238,13 @@ __device__ __forceinline__ int gallop_first(int n, int g, P pred) {
     return lo;
 }
 
-// Window of blocks [b0, b0+n) of range r: tEnd > s and tStart < e
+// Window of blocks [first, stop) of range r: tEnd > s and tStart < e
 // (chainSubsetOnT's first-block walk and stop condition, chain.c:481-500),
-// plus the per-range descriptor the tile kernel needs.
+// plus the descriptor k_tile needs.  Planning is a chain of dependent random
+// accesses, so it is built for few of them: the 64-byte chain record, then
+// the chain's bucket index (upload-time; bucket k of 2^shift target bases
+// holds the first block ending past its start), which brackets the first
+// block to one or two spans, then a gallop for the (short) window end.
 __device__ __forceinline__ RangeDesc plan_range(const ScoreArgs &a, const Range r) {
     RangeDesc d;
     d.tbase = 0;
@@ -249,35 +253,37 @@ __device__ __forceinline__ RangeDesc plan_range(const ScoreArgs &a, const Range 
     d.nblk = 0;
     d.s = r.t_start;
     d.e = r.t_end;
-    if (r.chain >= 0 && r.chain < a.n_chains && r.t_start < r.t_end) {
-        const DChain c = a.chains[r.chain];
-        // {tStart, tEnd} per block, 8 bytes: the last probes of a search fall
-        // in one 128-byte line
-        const int2 *sp = a.tspan + c.blk_off;
-        const int n = c.nblk;
-        // first block with tEnd > s (binary search; block spans are too
-        // irregular -- heavy-tailed gaps -- for interpolation to pay)
-        int lo = 0, hi = n;
-        if (r.t_start >= c.tstart) {
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (sp[mid].y > r.t_start) hi = mid;
-                else lo = mid + 1;
-            }
+    if (r.chain < 0 || r.chain >= a.n_chains || r.t_start >= r.t_end) return d;
+    const DChain c = a.chains[r.chain];
+    d.tbase = c.tbase;
+    d.qbase = c.qbase;
+    const int n = c.nblk;
+    if (n == 0) return d;
+    const int2 *sp = a.tspan + c.blk_off;
+    int first;
+    if (r.t_start < c.tstart) {
+        first = 0;
+    } else if (r.t_start >= c.tend) {
+        first = n;
+    } else {
+        const int k = (r.t_start - c.tstart) >> c.shift;
+        const u32x2a4 br = *reinterpret_cast<const u32x2a4 *>(a.bucket + c.idx_off + k);
+        int lo = (int)br.x, hi = (int)br.y;  // first block with tEnd > s is in [lo, hi]
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (sp[mid].y > r.t_start) hi = mid;
+            else lo = mid + 1;
         }
-        const int first = lo;
-        // first block with tStart >= e: windows are short, gallop from `first`
-        const int stop = r.t_end > c.tend
-                             ? n
-                             : first + gallop_first(n - first, 0, [&](int k) {
-                                   return sp[first + k].x >= r.t_end;
-                               });
-        d.nblk = stop - first;
-        d.b0 = (int32_t)(c.blk_off + first);
-        d.tbase = a.t_woff[c.t_seq] * 32;
-        const int64_t qw = a.q_woff[c.q_seq] * 32;
-        d.qbase = c.qinfo < 0 ? ~(qw + (c.qinfo & 0x7fffffff)) : qw;
+        first = lo;
     }
+    // first block with tStart >= e: windows are short, gallop from `first`
+    const int stop = r.t_end > c.tend
+                         ? n
+                         : first + gallop_first(n - first, 0, [&](int k) {
+                               return sp[first + k].x >= r.t_end;
+                           });
+    d.nblk = stop - first;
+    d.b0 = (int32_t)(c.blk_off + first);
     return d;
 }
 
@@ -295,6 +301,7 @@ __device__ __forceinline__ RangeDesc plan_range(const ScoreArgs &a, const Range 
 constexpr int kPlanWG = 256;
 constexpr int kMarkChunk = 1024;  // flat blocks per k_mark work item
 constexpr int kSpinLimit = 1 << 22;
+constexpr int kFanShards = 32;  // arrival counter shards
 
 __device__ __forceinline__ long long wg_exclusive_scan(long long v, long long *s_wsum,
                                                       long long &total) {
@@ -351,11 +358,12 @@ __global__ void __launch_bounds__(kPlanWG, 8) k_plan(ScoreArgs a) {
     if (tid == 0) {
         __hip_atomic_store(&a.gran[blockIdx.x], tag | (uint32_t)agg, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-        // arrival counter sharded by XCD (one word takes ~88 adds/us): the
-        // last arrival of each shard adds to the top counter
-        const int G = gridDim.x, x = blockIdx.x & 7;
-        const unsigned nx = (unsigned)((G - x + 7) >> 3), nshard = G < 8 ? G : 8;
-        uint32_t *sh = a.ticket + 32 * x, *top = a.ticket + 32 * 8;
+        // arrival counter sharded (one word takes ~88 adds/us): the last
+        // arrival of each shard adds to the top counter
+        const int G = gridDim.x, x = blockIdx.x & (kFanShards - 1);
+        const unsigned nx = (unsigned)((G - x + kFanShards - 1) / kFanShards);
+        const unsigned nshard = G < kFanShards ? G : kFanShards;
+        uint32_t *sh = a.ticket + 32 * x, *top = a.ticket + 32 * kFanShards;
         bool last = false;
         if (__hip_atomic_fetch_add(sh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nx - 1) {
             *sh = 0u;  // every arrival of this shard is in: reset for the next call
@@ -435,7 +443,7 @@ __global__ void __launch_bounds__(kPlanWG, 8) k_plan(ScoreArgs a) {
     const bool over = sat || W > a.cap_flat || T > a.cap_tiles || NQ > a.cap_chunks;
     if (late) atomicOr(&a.status[4], 1);
     if (tid == 0) {
-        a.ticket[32 * 8] = 0u;  // for the next call
+        a.ticket[32 * kFanShards] = 0u;  // for the next call
         a.status[0] = (int32_t)W;
         a.status[1] = (int32_t)T;
         a.status[2] = over ? 1 : 0;

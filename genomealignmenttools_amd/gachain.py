@@ -226,8 +226,13 @@ class Engine:
     def synchronize(self) -> None:
         check(lib().gac_synchronize(self.h))
 
-    def prof_enable(self, on: bool = True) -> None:
-        check(lib().gac_prof_enable(self.h, 1 if on else 0))
+    def prof_enable(self, on: bool = True, kernels=None) -> None:
+        """Time launches with HIP events: all kernels, or those in `kernels`
+        (GAC_K_* ids)."""
+        mask = 0
+        if on:
+            mask = (1 << 3) - 1 if kernels is None else sum(1 << k for k in kernels)
+        check(lib().gac_prof_enable(self.h, mask))
 
     def prof_reset(self) -> None:
         check(lib().gac_prof_reset(self.h))

@@ -236,8 +236,11 @@ int gac_synchronize(gac_ctx *ctx);
 #define GAC_K_TILE 1     /* tile scoring: bases, gaps, per-tile scan (dominant) */
 #define GAC_K_COMBINE 2  /* multi-tile range combine */
 #define GAC_K_COUNT 3
-/* Enable (1) / disable (0) event timing of each launch. */
-int gac_prof_enable(gac_ctx *ctx, int on);
+#define GAC_PROF_ALL ((1 << GAC_K_COUNT) - 1)
+/* Event timing of each launch of the kernels in `mask` (bits 1 << GAC_K_*;
+ * 0 = off, GAC_PROF_ALL = all).  Each timed kernel adds two event markers
+ * to the stream. */
+int gac_prof_enable(gac_ctx *ctx, int mask);
 /* Synchronise, fold recorded events, and return total ms + launch count of
  * kernel `k` since the last reset. */
 int gac_prof_read(gac_ctx *ctx, int k, double *total_ms, int64_t *launches);
