@@ -20,7 +20,7 @@
 
 namespace gac {
 int plan_grid(int64_t n);
-int tile_blocks_per_cu(bool local);
+int persistent_blocks_per_cu(int which);
 hipError_t launch_plan(const ScoreArgs &a, hipStream_t s);
 int mark_chunks_bound(int64_t flat, int64_t n);
 hipError_t launch_mark(const ScoreArgs &a, int grid, hipStream_t s);
@@ -84,8 +84,7 @@ struct Prof {
 
 }  // namespace
 
-// status[0..8) + 33 arrival counters (32 shards + top), each on its own 128-byte line
-constexpr size_t kStatusBytes = 128 + 33 * 128;
+constexpr size_t kStatusBytes = 128;  // status[0..8)
 
 struct gac_ctx {
     int device = 0;
@@ -103,12 +102,11 @@ struct gac_ctx {
     RangeDesc *rdesc = nullptr;
     int32_t *nblk = nullptr, *goff = nullptr;
     int32_t *pb0 = nullptr;                  // [ws_n]
-    unsigned long long *gran = nullptr;      // [plan workgroups]
+    int32_t *agg = nullptr;                  // [plan workgroups]
     int32_t *plan_off = nullptr, *chunk_off = nullptr;  // [plan workgroups]
     int32_t *chunk_wg = nullptr;             // [ws_chunks]
     int64_t ws_chunks = 0;
-    int32_t *status = nullptr;               // [8] status, then the arrival counters
-    uint32_t epoch = 0;
+    int32_t *status = nullptr;               // [8]
     int64_t ws_tiles = 0;
     int32_t *ridx = nullptr, *bidx = nullptr;
     int64_t ws_flat = 0;
@@ -119,7 +117,7 @@ struct gac_ctx {
     long long *d_g = nullptr, *d_l = nullptr;
     int32_t *d_ali = nullptr;
     int32_t *h_total = nullptr;  // pinned [8]
-    int tile_grid = 2048;       // k_mark grid
+    int tile_grid = 2048;       // k_mark grid (resident workgroups)
     int tile_grid_g = 2048;     // k_tile<false> grid (resident workgroups)
     int tile_grid_l = 2048;     // k_tile<true> grid
     int combine_grid = 512;
@@ -167,11 +165,10 @@ extern "C" int gac_open(int device, gac_ctx **out) {
         return gac_fail(GAC_E_HIP, "hipStreamCreate failed");
     }
     // persistent tile grid: 8 workgroups (32 waves) per CU
-    c->tile_grid = prop.multiProcessorCount * 8;
-    c->tile_grid = (c->tile_grid + 7) / 8 * 8;
+    c->tile_grid = prop.multiProcessorCount * persistent_blocks_per_cu(2);  // k_mark
     c->combine_grid = prop.multiProcessorCount * 8;  // one 64-range group per wave
-    c->tile_grid_g = prop.multiProcessorCount * tile_blocks_per_cu(false);
-    c->tile_grid_l = prop.multiProcessorCount * tile_blocks_per_cu(true);
+    c->tile_grid_g = prop.multiProcessorCount * persistent_blocks_per_cu(0);
+    c->tile_grid_l = prop.multiProcessorCount * persistent_blocks_per_cu(1);
     if (hipHostMalloc((void **)&c->h_total, 32, hipHostMallocDefault) != hipSuccess) {
         hipStreamDestroy(c->stream);
         delete c;
@@ -194,7 +191,7 @@ extern "C" void gac_close(gac_ctx *c) {
     hipStreamSynchronize(c->stream);
     free_genome(c->g[0]);
     free_genome(c->g[1]);
-    void *bufs[] = {c->d_small,  c->d_gap_tab, c->rdesc,    c->nblk,     c->goff, c->pb0, c->gran, c->plan_off, c->chunk_off, c->chunk_wg,
+    void *bufs[] = {c->d_small,  c->d_gap_tab, c->rdesc,    c->nblk,     c->goff, c->pb0, c->agg, c->plan_off, c->chunk_off, c->chunk_wg,
                     c->status,   c->ridx,     c->bidx,     c->sum_head, c->sum_tail,
                     c->d_ranges, c->d_g,      c->d_l,      c->d_ali};
     for (void *p : bufs)
@@ -577,19 +574,18 @@ extern "C" int64_t gac_chains_block_count(const gac_chainset *cs) { return cs ? 
 static int ensure_ws(gac_ctx *c, int64_t n, int64_t max_tiles, int64_t flat, hipStream_t s) {
     if (n > c->ws_n) {
         int64_t cap = n + n / 2 + 1024;
-        void *bufs[] = {c->rdesc, c->nblk, c->goff, c->pb0, c->gran, c->plan_off, c->chunk_off};
+        void *bufs[] = {c->rdesc, c->nblk, c->goff, c->pb0, c->agg, c->plan_off, c->chunk_off};
         for (void *p : bufs)
             if (p) hipFree(p);
         c->rdesc = nullptr;
         c->nblk = c->goff = c->pb0 = c->plan_off = c->chunk_off = nullptr;
-        c->gran = nullptr;
+        c->agg = nullptr;
         const int64_t G = plan_grid(cap) + 2;
         HIPCHK(hipMalloc(&c->rdesc, cap * sizeof(RangeDesc)));
         HIPCHK(hipMalloc(&c->nblk, cap * 4));
         HIPCHK(hipMalloc(&c->goff, cap * 4));
         HIPCHK(hipMalloc(&c->pb0, cap * 4));
-        HIPCHK(hipMalloc(&c->gran, G * 8));
-        HIPCHK(hipMemsetAsync(c->gran, 0, G * 8, s));  // epoch 0 is never used
+        HIPCHK(hipMalloc(&c->agg, G * 4));
         HIPCHK(hipMalloc(&c->plan_off, G * 4));
         HIPCHK(hipMalloc(&c->chunk_off, G * 4));
         c->ws_n = cap;
@@ -698,19 +694,13 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
         a.rdesc = c->rdesc;
         a.nblk = c->nblk;
         a.goff = c->goff;
-        if (++c->epoch == 0) {  // granule tags wrapped: clear them
-            HIPCHK(hipMemsetAsync(c->gran, 0, (plan_grid(c->ws_n) + 2) * 8, s));
-            c->epoch = 1;
-        }
         a.pb0 = c->pb0;
-        a.gran = c->gran;
+        a.agg = c->agg;
         a.plan_off = c->plan_off;
         a.chunk_off = c->chunk_off;
         a.chunk_wg = c->chunk_wg;
         a.cap_chunks = (int32_t)(c->ws_chunks < INT32_MAX ? c->ws_chunks : INT32_MAX);
-        a.epoch = c->epoch;
         a.status = c->status;
-        a.ticket = (uint32_t *)(c->status + 32);
         a.ridx = c->ridx;
         a.bidx = c->bidx;
         a.sum_head = c->sum_head;
@@ -736,11 +726,6 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
         HIPCHK(hipMemcpyAsync(c->h_total, c->status, 32, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         const int32_t W = c->h_total[0], NT = c->h_total[1];
-        if (c->h_total[4]) {
-            HIPCHK(hipMemsetAsync(c->status, 0, kStatusBytes, s));
-            HIPCHK(hipStreamSynchronize(s));
-            return gac_fail(GAC_E_HIP, "k_plan: a workgroup total never became visible");
-        }
         if (W == INT32_MAX) return gac_fail(GAC_E_ARG, "window block total overflows int32");
         if (!c->h_total[2]) return GAC_OK;
         rc = ensure_ws(c, n, NT, W, s);

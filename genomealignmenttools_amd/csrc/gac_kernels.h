@@ -92,7 +92,7 @@ struct ScoreArgs {
     const DChain *chains;
     int64_t n_chains;
     const int4 *blk;     // [n_blocks + 1] {tStart, qStart, size, nflags}
-    const int2 *tspan;   // [n_blocks + 8] {tStart, tEnd} (window ends; padded)
+    const int2 *tspan;   // [n_blocks + 8] {tStart, tEnd} (window searches; padded)
     const uint32_t *bucket;  // chain bucket indexes (see DChain)
     const Range *ranges;
     int64_t n;
@@ -105,14 +105,12 @@ struct ScoreArgs {
     int32_t *bidx;       // [W]   global block index of each flat block
     SegSum *sum_head;    // [T]   partial segment containing the tile's first block
     SegSum *sum_tail;    // [T]   partial segment containing the tile's last block
-    unsigned long long *gran;  // [G] {epoch, window-block total} of each plan workgroup
-    uint32_t *ticket;    // plan workgroups done: 32 shards + top, 128 B apart (self-resetting)
-    int32_t *plan_off;   // [G]   flat offset of plan workgroup w
-    int32_t *chunk_off;  // [G]   first mark chunk of plan workgroup w
-    int32_t *chunk_wg;   // [cap_chunks] plan workgroup of each mark chunk
+    int32_t *agg;        // [G]   window blocks of each plan workgroup (k_plan; saturated)
+    int32_t *plan_off;   // [G+1] flat offset of plan workgroup w
+    int32_t *chunk_off;  // [G+1] first mark chunk of plan workgroup w (large batches)
+    int32_t *chunk_wg;   // [cap_chunks] plan workgroup of each mark chunk (large batches)
     int32_t *status;     // [8]   W (flat blocks, saturated), T (tiles), 1 = workspace too
-                         //       small, mark chunks, error bits (1 = granule never seen)
-    uint32_t epoch;      // tag of this call's granules
+                         //       small, mark chunks
     int32_t cap_chunks;
     int32_t cap_flat;    // ridx/bidx capacity
     int32_t cap_tiles;   // sum_head/sum_tail capacity

@@ -105,6 +105,7 @@ __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, int sh) {
 
 typedef uint32_t u32x4a8 __attribute__((ext_vector_type(4), aligned(8)));
 typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
+typedef int32_t i32x4a8 __attribute__((ext_vector_type(4), aligned(8)));
 
 // 32 bases starting at global base index p: the two code planes (bit i = base
 // p+i) with ONE 16-byte load of words w, w+1 ({p0,p1} each; 8-byte aligned).
@@ -241,10 +242,11 @@ __device__ __forceinline__ int gallop_first(int n, int g, P pred) {
 // Window of blocks [first, stop) of range r: tEnd > s and tStart < e
 // (chainSubsetOnT's first-block walk and stop condition, chain.c:481-500),
 // plus the descriptor k_tile needs.  Planning is a chain of dependent random
-// accesses, so it is built for few of them: the 64-byte chain record, then
-// the chain's bucket index (upload-time; bucket k of 2^shift target bases
-// holds the first block ending past its start), which brackets the first
-// block to one or two spans, then a gallop for the (short) window end.
+// accesses, so it is built for few of them: the 64-byte chain record, the
+// chain's bucket index (upload-time; bucket k of 2^shift target bases holds
+// the first block ending past its start), which brackets the first block,
+// then ONE 64-byte load of 8 block spans that settles the window start and,
+// for most windows, its end.
 __device__ __forceinline__ RangeDesc plan_range(const ScoreArgs &a, const Range r) {
     RangeDesc d;
     d.tbase = 0;
@@ -260,48 +262,69 @@ __device__ __forceinline__ RangeDesc plan_range(const ScoreArgs &a, const Range 
     const int n = c.nblk;
     if (n == 0) return d;
     const int2 *sp = a.tspan + c.blk_off;
-    int first;
-    if (r.t_start < c.tstart) {
-        first = 0;
-    } else if (r.t_start >= c.tend) {
-        first = n;
+    const int s = r.t_start, e = r.t_end;
+    int lo, hi;  // the first block with tEnd > s is in [lo, hi]
+    if (s < c.tstart) {
+        lo = hi = 0;
+    } else if (s >= c.tend) {
+        lo = hi = n;
     } else {
-        const int k = (r.t_start - c.tstart) >> c.shift;
+        const int k = (s - c.tstart) >> c.shift;
         const u32x2a4 br = *reinterpret_cast<const u32x2a4 *>(a.bucket + c.idx_off + k);
-        int lo = (int)br.x, hi = (int)br.y;  // first block with tEnd > s is in [lo, hi]
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (sp[mid].y > r.t_start) hi = mid;
-            else lo = mid + 1;
-        }
-        first = lo;
+        lo = (int)br.x;
+        hi = (int)br.y;
     }
-    // first block with tStart >= e: windows are short, gallop from `first`
-    const int stop = r.t_end > c.tend
-                         ? n
-                         : first + gallop_first(n - first, 0, [&](int k) {
-                               return sp[first + k].x >= r.t_end;
-                           });
+    // spans of blocks lo .. lo+7 (the span array is padded by 8 entries, so
+    // reading past this chain is safe; those entries are masked)
+    int2 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+        const i32x4a8 x = *reinterpret_cast<const i32x4a8 *>(sp + lo + j);
+        v[j] = make_int2(x.x, x.y);
+        v[j + 1] = make_int2(x.z, x.w);
+    }
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cnt += (lo + j < hi && v[j].y <= s) ? 1 : 0;
+    int first = lo + cnt;
+    if (cnt == 8 && first < hi) {  // dense bucket: binary search the rest
+        int l2 = first, h2 = hi;
+        while (l2 < h2) {
+            const int mid = (l2 + h2) >> 1;
+            if (sp[mid].y > s) h2 = mid;
+            else l2 = mid + 1;
+        }
+        first = l2;
+    }
+    // first block >= first with tStart >= e (or n)
+    int stop = -1;
+    if (e > c.tend) {
+        stop = n;
+    } else {
+#pragma unroll
+        for (int j = 7; j >= 0; --j) {
+            const int bj = lo + j;
+            if (bj >= first && (bj >= n || v[j].x >= e)) stop = bj < n ? bj : n;
+        }
+        if (stop < 0) {  // long window: gallop on
+            const int from = max(first, lo + 8);
+            stop = from + gallop_first(n - from, 0, [&](int k) { return sp[from + k].x >= e; });
+        }
+    }
     d.nblk = stop - first;
     d.b0 = (int32_t)(c.blk_off + first);
     return d;
 }
 
 // ------------------------------------------------------------ k_plan -----
-// One lane per range: plan, then a workgroup scan of the window blocks:
-// goff[i] = exclusive prefix inside the plan workgroup w = i / 256, pb0[i] =
-// first window block, and the workgroup total published as ONE 8-byte
-// {epoch, total} granule (sc1 store; needs no ordering against anything).
-// Workgroups then add to a counter; the last to add reads every granule
-// (spinning on any whose tag is not yet visible), scans the totals into
-// P[w] (flat offset of workgroup w) and CP[w] (its first mark chunk), writes
-// the mark-chunk table, and publishes {W, T, overflow, chunks} in status[].
-// No fences: on gfx950 an agent release/acquire per workgroup costs an L2
-// writeback/invalidate each (measured: +75 us on this kernel).
+// One lane per range: plan, then the workgroup's scan of its window blocks:
+// goff[i] = exclusive prefix inside plan workgroup w = i / 256, pb0[i] =
+// first window block, agg[w] = the workgroup's total.  Nothing crosses
+// workgroups here (an in-kernel hand-off of the totals -- counter fan-in and
+// a last-arriver scan -- cost more than the separate one-workgroup
+// k_scan_agg launch).
 constexpr int kPlanWG = 256;
 constexpr int kMarkChunk = 1024;  // flat blocks per k_mark work item
-constexpr int kSpinLimit = 1 << 22;
-constexpr int kFanShards = 32;  // arrival counter shards
 
 __device__ __forceinline__ long long wg_exclusive_scan(long long v, long long *s_wsum,
                                                       long long &total) {
@@ -326,14 +349,8 @@ __device__ __forceinline__ long long wg_exclusive_scan(long long v, long long *s
     return pre + incl - v;
 }
 
-__device__ __forceinline__ unsigned long long gran_load(const unsigned long long *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 __global__ void __launch_bounds__(kPlanWG, 8) k_plan(ScoreArgs a) {
     __shared__ long long s_wsum[kPlanWG / kWave];
-    __shared__ int s_last;
-    __shared__ uint32_t s_val[16 * kPlanWG];  // last workgroup: one batch of totals
     const int tid = threadIdx.x;
     const int64_t i = (int64_t)blockIdx.x * kPlanWG + tid;
     int nb = 0;
@@ -348,116 +365,88 @@ __global__ void __launch_bounds__(kPlanWG, 8) k_plan(ScoreArgs a) {
             if (a.want_local) a.out_l[i] = 0;
         }
     }
-    // 64-bit: 256 windows of a huge chain may exceed int32 (saturated; the
-    // host reports it)
+    // 64-bit: 256 windows of a huge chain may exceed int32 (saturated in
+    // k_mark; the host reports it)
     long long agg;
     const long long excl = wg_exclusive_scan(nb, s_wsum, agg);
-    if (agg > 0x7fffffffLL) agg = 0x7fffffffLL;
     if (i < a.n) a.goff[i] = (int32_t)(excl < 0x7fffffffLL ? excl : 0x7fffffffLL);
-    const unsigned long long tag = (unsigned long long)a.epoch << 32;
-    if (tid == 0) {
-        __hip_atomic_store(&a.gran[blockIdx.x], tag | (uint32_t)agg, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        // arrival counter sharded (one word takes ~88 adds/us): the last
-        // arrival of each shard adds to the top counter
-        const int G = gridDim.x, x = blockIdx.x & (kFanShards - 1);
-        const unsigned nx = (unsigned)((G - x + kFanShards - 1) / kFanShards);
-        const unsigned nshard = G < kFanShards ? G : kFanShards;
-        uint32_t *sh = a.ticket + 32 * x, *top = a.ticket + 32 * kFanShards;
-        bool last = false;
-        if (__hip_atomic_fetch_add(sh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nx - 1) {
-            *sh = 0u;  // every arrival of this shard is in: reset for the next call
-            last = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                   nshard - 1;
-        }
-        s_last = last;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    // ---- last workgroup: scan the totals, 4096 workgroups per batch (all
-    // granule loads of a batch in flight at once, coalesced; spin only on
-    // the rare granule whose tag is not visible yet)
-    constexpr int kPer = 16;
-    const int G = gridDim.x;
-    bool late = false;
-    long long carry = 0, ccarry = 0;
-    for (int b0 = 0; b0 < G; b0 += kPer * kPlanWG) {
-        // 4 loads in flight per lane (keeps the kernel at <= 64 VGPRs)
-#pragma unroll 1
-        for (int k0 = 0; k0 < kPer; k0 += 4) {
-            unsigned long long g[4];
+    if (tid == 0) a.agg[blockIdx.x] = (int32_t)(agg < 0x7fffffffLL ? agg : 0x7fffffffLL);
+}
+
+// Scan of the plan workgroups' totals by one workgroup (k_scan_agg): flat
+// offsets (plan_off), mark-chunk offsets (chunk_off) and, when it fits, the
+// chunk table (chunk_wg).  Thread t owns workgroups [8t, 8t + 8) of each
+// batch of 2048, loaded all at once.  Returns {W, chunks} (W saturated at
+// INT32_MAX).
+struct AggScan {
+    long long W, NQ;
+};
+
+__device__ AggScan scan_totals(const ScoreArgs &a, int G, long long *s_wsum) {
+    constexpr int kPer = 8, kBatch = kPer * kPlanWG;
+    const int tid = threadIdx.x;
+    AggScan t = {0, 0};
+    for (int b0 = 0; b0 < G; b0 += kBatch) {
+        int32_t v[kPer];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int w = b0 + (k0 + k) * kPlanWG + tid;
-                g[k] = w < G ? gran_load(&a.gran[w]) : tag;
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int w = b0 + (k0 + k) * kPlanWG + tid;
-                for (int spin = 0; (g[k] & ~0xffffffffull) != tag; ++spin) {
-                    if (spin > kSpinLimit) {
-                        late = true;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    g[k] = gran_load(&a.gran[w]);
-                }
-                s_val[(k0 + k) * kPlanWG + tid] = (uint32_t)g[k];
-            }
+        for (int k = 0; k < kPer; ++k) {
+            const int w = b0 + tid * kPer + k;
+            v[k] = w < G ? a.agg[w] : 0;
         }
-        __syncthreads();
-        // thread t owns workgroups b0 + [kPer t, kPer t + kPer)
         long long mine = 0, mch = 0;
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
-            const long long v = s_val[kPer * tid + k];
-            mine += v;
-            mch += (v + kMarkChunk - 1) / kMarkChunk;
+            mine += v[k];
+            mch += ((long long)v[k] + kMarkChunk - 1) / kMarkChunk;
         }
-        long long bt, bc;
-        long long run = carry + wg_exclusive_scan(mine, s_wsum, bt);
-        long long crun = ccarry + wg_exclusive_scan(mch, s_wsum, bc);
-        carry += bt;
-        ccarry += bc;
-        const bool fits = ccarry <= a.cap_chunks;
-#pragma unroll 1
+        long long bw, bq;
+        long long run = t.W + wg_exclusive_scan(mine, s_wsum, bw);
+        long long crun = t.NQ + wg_exclusive_scan(mch, s_wsum, bq);
+        t.W += bw;
+        t.NQ += bq;
+        const bool fits = t.NQ <= a.cap_chunks;
+#pragma unroll
         for (int k = 0; k < kPer; ++k) {
-            const int w = b0 + kPer * tid + k;
-            if (w >= G) break;
-            const long long v = s_val[kPer * tid + k];
-            const long long ch = (v + kMarkChunk - 1) / kMarkChunk;
-            a.plan_off[w] = (int32_t)(run < 0x7fffffffLL ? run : 0x7fffffffLL);
-            a.chunk_off[w] = (int32_t)(crun < 0x7fffffffLL ? crun : 0x7fffffffLL);
-            if (fits)
-                for (long long c = 0; c < ch; ++c) a.chunk_wg[crun + c] = w;
-            run += v;
+            const int w = b0 + tid * kPer + k;
+            const long long ch = ((long long)v[k] + kMarkChunk - 1) / kMarkChunk;
+            if (w < G) {
+                a.plan_off[w] = (int32_t)(run < 0x7fffffffLL ? run : 0x7fffffffLL);
+                a.chunk_off[w] = (int32_t)(crun < 0x7fffffffLL ? crun : 0x7fffffffLL);
+                if (fits)
+                    for (long long c = 0; c < ch; ++c) a.chunk_wg[crun + c] = w;
+            }
+            run += v[k];
             crun += ch;
         }
-        __syncthreads();
     }
-    long long W = carry;
-    const long long NQ = ccarry;
-    const bool sat = W >= 0x7fffffffLL;
-    if (sat) W = 0x7fffffffLL;
-    const long long T = (W + kTileBlocks - 1) / kTileBlocks;
-    const bool over = sat || W > a.cap_flat || T > a.cap_tiles || NQ > a.cap_chunks;
-    if (late) atomicOr(&a.status[4], 1);
-    if (tid == 0) {
-        a.ticket[32 * kFanShards] = 0u;  // for the next call
-        a.status[0] = (int32_t)W;
-        a.status[1] = (int32_t)T;
-        a.status[2] = over ? 1 : 0;
-        a.status[3] = (int32_t)(NQ < 0x7fffffffLL ? NQ : 0x7fffffffLL);
-    }
+    if (t.W > 0x7fffffffLL) t.W = 0x7fffffffLL;
+    return t;
+}
+
+__device__ __forceinline__ void publish_status(const ScoreArgs &a, AggScan t) {
+    const long long T = (t.W + kTileBlocks - 1) / kTileBlocks;
+    const bool over = t.W >= 0x7fffffffLL || t.W > a.cap_flat || T > a.cap_tiles ||
+                      t.NQ > a.cap_chunks;
+    a.status[0] = (int32_t)t.W;
+    a.status[1] = (int32_t)T;
+    a.status[2] = over ? 1 : 0;
+    a.status[3] = (int32_t)(t.NQ < 0x7fffffffLL ? t.NQ : 0x7fffffffLL);
+}
+
+__global__ void __launch_bounds__(kPlanWG) k_scan_agg(ScoreArgs a) {
+    __shared__ long long s_wsum[kPlanWG / kWave];
+    const int G = (int)((a.n + kPlanWG - 1) / kPlanWG);
+    const AggScan t = scan_totals(a, G, s_wsum);
+    if (threadIdx.x == 0) publish_status(a, t);
 }
 
 // ------------------------------------------------------------ k_mark -----
 // Flat block -> (range, block) map.  Work item = one chunk of <= 1024 flat
-// blocks of one plan workgroup (balanced however long the windows are);
-// persistent grid over the chunk table.  The workgroup's 256 local offsets
-// go to LDS; each flat block finds its owner by an 8-step LDS search, and
-// the ridx/bidx stores are coalesced.
-__global__ void __launch_bounds__(kPlanWG) k_mark(ScoreArgs a) {
+// blocks of one plan workgroup (balanced however long the windows are; the
+// chunk table comes from k_scan_agg); persistent grid.  The plan workgroup's
+// 256 local offsets go to LDS; each flat block finds its owner by an 8-step
+// LDS search; the ridx/bidx stores are coalesced.
+__global__ void __launch_bounds__(kPlanWG, 8) k_mark(ScoreArgs a) {
     __shared__ int s_excl[kPlanWG];
     __shared__ int s_b0[kPlanWG];
     if (a.status[2]) return;  // workspace overflow: the host grows it and reruns
@@ -874,16 +863,19 @@ hipError_t launch_plan(const ScoreArgs &a, hipStream_t s) {
 int mark_chunks_bound(int64_t flat, int64_t n) { return (int)(flat / kMarkChunk + plan_grid(n) + 2); }
 
 hipError_t launch_mark(const ScoreArgs &a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_scan_agg, dim3(1), dim3(kPlanWG), 0, s, a);
     hipLaunchKernelGGL(k_mark, dim3(grid), dim3(kPlanWG), 0, s, a);
     return hipGetLastError();
 }
 
-// Resident workgroups per CU of the persistent tile kernel (the grid must not
-// exceed what fits at once, or the last workgroups run as a second wave).
-int tile_blocks_per_cu(bool local) {
+// Resident workgroups per CU of the persistent kernels (a grid must not
+// exceed what fits at once, or the last workgroups run as a second wave):
+// 0 = k_tile<false>, 1 = k_tile<true>, 2 = k_mark.
+int persistent_blocks_per_cu(int which) {
     int nb = 0;
-    hipError_t e = local ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<true>, 256, 0)
-                         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<false>, 256, 0);
+    hipError_t e = which == 0   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<false>, 256, 0)
+                   : which == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<true>, 256, 0)
+                                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_mark, 256, 0);
     return (e == hipSuccess && nb > 0) ? nb : 4;
 }
 

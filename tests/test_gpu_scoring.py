@@ -75,7 +75,7 @@ def test_workspace_growth_and_lookback():
     for _ in range(3):
         g, l, a = e.score_ranges(cs, R, want_local=True)
         assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
-    # 3) > 4096 plan workgroups (1.14M ranges): the pre-scanned offsets path
+    # 3) 1.14M ranges: 4456 plan workgroups, three k_scan_agg batches
     RR = np.tile(R, (19, 1))
     g, l, a = e.score_ranges(cs, RR, want_local=True)
     assert np.array_equal(g, np.tile(og, 19)) and np.array_equal(l, np.tile(ol, 19))
