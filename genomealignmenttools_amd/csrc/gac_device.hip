@@ -92,7 +92,8 @@ struct gac_ctx {
     hipStream_t stream = nullptr;
     Genome g[2];
     bool scoring = false;
-    int32_t coef[16];
+    int32_t coef[16];  // multilinear basis (ScoreArgs::coef)
+    int sym = 0;
     GapDev gap;
     int32_t *d_small = nullptr;
     int32_t *d_gap_tab = nullptr;  // [3][gap_len]
@@ -223,12 +224,27 @@ extern "C" int gac_set_scoring(gac_ctx *c, const int32_t mat[16], const gac_gapc
     if (g->small_size < 1 || g->small_size != g->long_pos[0])
         return gac_fail(GAC_E_ARG, "inconsistent gap table (smallSize %d)", g->small_size);
     HIPCHK(hipSetDevice(c->device));
-    for (int i = 0; i < 16; ++i)  // the kernel multiplies in 24 bits (v_mad_i32_i24)
-        if (mat[i] <= -(1 << 22) || mat[i] >= (1 << 22))
-            return gac_fail(GAC_E_ARG, "score matrix entry %d out of range (|s| < 2^22)", mat[i]);
-    for (int qc = 0; qc < 4; ++qc)
-        for (int tc = 0; tc < 4; ++tc)
-            c->coef[qc * 4 + tc] = mat[acgt_of_code(qc) * 4 + acgt_of_code(tc)];
+    // the kernel multiplies basis coefficients (|c| <= 16 max|s|) by counts
+    // <= 32 in 24 bits (v_mad_i32_i24) and sums 16 terms in int32
+    for (int i = 0; i < 16; ++i)
+        if (mat[i] <= -(1 << 17) || mat[i] >= (1 << 17))
+            return gac_fail(GAC_E_ARG, "score matrix entry %d out of range (|s| < 2^17)", mat[i]);
+    // f(S) = M[q][t] at t1,t0,d1,d0 = bits of S (q = t ^ d); Moebius transform
+    // to the multilinear coefficients
+    int32_t f[16];
+    for (int S = 0; S < 16; ++S) {
+        const int t = S >> 2, q = t ^ (S & 3);
+        f[S] = mat[acgt_of_code(q) * 4 + acgt_of_code(t)];
+    }
+    for (int S = 0; S < 16; ++S) {
+        int32_t cs = 0;
+        for (int T = 0; T < 16; ++T)
+            if ((T & S) == T) cs += (__builtin_popcount(S ^ T) & 1) ? -f[T] : f[T];
+        c->coef[S] = cs;
+    }
+    c->sym = 1;
+    for (int S = 8; S < 16; ++S)
+        if (c->coef[S]) c->sym = 0;
     GapDev &d = c->gap;
     memset(&d, 0, sizeof(d));
     d.small_size = g->small_size;
@@ -689,6 +705,7 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
     a.gap_tab = c->d_gap_tab;
     a.small_tab = c->d_small;
     memcpy(a.coef, c->coef, sizeof(a.coef));
+    a.sym = c->sym;
     a.gap = c->gap;
     for (int pass = 0; pass < 2; ++pass) {
         a.rdesc = c->rdesc;

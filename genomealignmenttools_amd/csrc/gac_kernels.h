@@ -122,7 +122,10 @@ struct ScoreArgs {
     int32_t gap_len;           // gap_tab entries per kind
     const int32_t *gap_tab;    // [3][gap_len] gapCalcCost by kind (q, t, both) and length
     const int32_t *small_tab;  // [3][small_size] q, t, both
-    int32_t coef[16];          // score of (query code << 2 | target code)
+    int32_t coef[16];          // score matrix in the multilinear basis of the bits
+                               // (t1, t0, d1, d0), d = q ^ t: coef[S], S = t1<<3 |
+                               // t0<<2 | d1<<1 | d0 (set bits = factors)
+    int32_t sym;               // matrix is strand-symmetric: coef[8..15] == 0
     GapDev gap;
 };
 

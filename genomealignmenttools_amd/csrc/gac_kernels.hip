@@ -492,6 +492,7 @@ struct WaveLds {
 
 constexpr int kLenMask = (1 << 29) - 1;
 
+template <bool SYM>
 __device__ __forceinline__ int chunk_score(const ScoreArgs &a, const WaveLds &L, int k, int off,
                                            int n) {
     const int lq = L.lenq[k];
@@ -513,15 +514,34 @@ __device__ __forceinline__ int chunk_score(const ScoreArgs &a, const WaveLds &L,
         q1 = ~(__builtin_bitreverse32(f1) >> sh);
         if (lq & (1 << 29)) qn = __builtin_bitreverse32(load_nmask(a.q_nmask, F)) >> sh;
     }
-    const uint32_t valid = (n >= 32 ? 0xffffffffu : ((1u << n) - 1u)) & ~tn & ~qn;
-    const uint32_t tm[4] = {~t1 & ~t0, ~t1 & t0, t1 & ~t0, t1 & t0};
-    const uint32_t qm[4] = {valid & ~q1 & ~q0, valid & ~q1 & q0, valid & q1 & ~q0, valid & q1 & q0};
-    int sc = 0;
-#pragma unroll
-    for (int qc = 0; qc < 4; ++qc)
-#pragma unroll
-        for (int tc = 0; tc < 4; ++tc)
-            sc += __mul24(a.coef[qc * 4 + tc], (int)__builtin_popcount(qm[qc] & tm[tc]));
+    const uint32_t v = (n >= 32 ? 0xffffffffu : ((1u << n) - 1u)) & ~tn & ~qn;
+    // score = sum over positions of coef[S] * prod(S) in the basis
+    // (t1, t0, d1, d0), d = q ^ t (multilinear form of the 4x4 matrix, see
+    // ScoreArgs::coef): one AND + popcount + 24-bit multiply-add per term.
+    // Strand-symmetric matrices (M[comp q][comp t] = M[q][t]; comp flips
+    // bit 1) have no t1 terms: 8 instead of 16.
+    const uint32_t d0 = q0 ^ t0, d1 = q1 ^ t1;
+    const uint32_t m2 = v & d1, m1 = v & d0, m4 = v & t0;
+    const uint32_t m3 = m2 & d0, m6 = m4 & d1, m5 = m4 & d0, m7 = m6 & d0;
+    int sc = __mul24(a.coef[0], (int)__builtin_popcount(v));
+    sc += __mul24(a.coef[1], (int)__builtin_popcount(m1));
+    sc += __mul24(a.coef[2], (int)__builtin_popcount(m2));
+    sc += __mul24(a.coef[3], (int)__builtin_popcount(m3));
+    sc += __mul24(a.coef[4], (int)__builtin_popcount(m4));
+    sc += __mul24(a.coef[5], (int)__builtin_popcount(m5));
+    sc += __mul24(a.coef[6], (int)__builtin_popcount(m6));
+    sc += __mul24(a.coef[7], (int)__builtin_popcount(m7));
+    if (!SYM) {
+        const uint32_t u = v & t1;
+        sc += __mul24(a.coef[8], (int)__builtin_popcount(u));
+        sc += __mul24(a.coef[9], (int)__builtin_popcount(u & d0));
+        sc += __mul24(a.coef[10], (int)__builtin_popcount(u & d1));
+        sc += __mul24(a.coef[11], (int)__builtin_popcount(u & d1 & d0));
+        sc += __mul24(a.coef[12], (int)__builtin_popcount(u & t0));
+        sc += __mul24(a.coef[13], (int)__builtin_popcount(u & t0 & d0));
+        sc += __mul24(a.coef[14], (int)__builtin_popcount(u & t0 & d1));
+        sc += __mul24(a.coef[15], (int)__builtin_popcount(u & m7));
+    }
     return sc;
 }
 
@@ -547,7 +567,7 @@ __device__ __forceinline__ void seg_store(const ScoreArgs &a, int ri, long long 
     if (LOCAL) a.out_l[ri] = max2(0, max2(e.C, e.D));
 }
 
-template <bool LOCAL>
+template <bool LOCAL, bool SYM>
 __global__ void __launch_bounds__(256, LOCAL ? 7 : 8) k_tile(ScoreArgs a) {
     __shared__ WaveLds s_w[kWavesPerWG];
 
@@ -639,12 +659,12 @@ __global__ void __launch_bounds__(256, LOCAL ? 7 : 8) k_tile(ScoreArgs a) {
             if (ja < C) {
                 ka = find_chunk_block(L, ja);
                 const int off = (ja - L.coff[ka]) << 5;
-                sa = chunk_score(a, L, ka, off, min(32, (L.lenq[ka] & kLenMask) - off));
+                sa = chunk_score<SYM>(a, L, ka, off, min(32, (L.lenq[ka] & kLenMask) - off));
             }
             if (jb < C) {
                 kb = find_chunk_block(L, jb);
                 const int off = (jb - L.coff[kb]) << 5;
-                sb = chunk_score(a, L, kb, off, min(32, (L.lenq[kb] & kLenMask) - off));
+                sb = chunk_score<SYM>(a, L, kb, off, min(32, (L.lenq[kb] & kLenMask) - off));
             }
             if (ja < C) atomicAdd(&L.acc[ka], (unsigned long long)(long long)sa);
             if (jb < C) atomicAdd(&L.acc[kb], (unsigned long long)(long long)sb);
@@ -873,17 +893,23 @@ hipError_t launch_mark(const ScoreArgs &a, int grid, hipStream_t s) {
 // 0 = k_tile<false>, 1 = k_tile<true>, 2 = k_mark.
 int persistent_blocks_per_cu(int which) {
     int nb = 0;
-    hipError_t e = which == 0   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<false>, 256, 0)
-                   : which == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<true>, 256, 0)
-                                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_mark, 256, 0);
+    // (the symmetric and general variants differ by a few registers; size
+    // for the general one)
+    hipError_t e =
+        which == 0   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<false, false>, 256, 0)
+        : which == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<true, false>, 256, 0)
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_mark, 256, 0);
     return (e == hipSuccess && nb > 0) ? nb : 4;
 }
 
 hipError_t launch_tile(const ScoreArgs &a, int grid, hipStream_t s) {
-    if (a.want_local)
-        hipLaunchKernelGGL(k_tile<true>, dim3(grid), dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL(k_tile<false>, dim3(grid), dim3(256), 0, s, a);
+    if (a.want_local) {
+        if (a.sym) hipLaunchKernelGGL((k_tile<true, true>), dim3(grid), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_tile<true, false>), dim3(grid), dim3(256), 0, s, a);
+    } else {
+        if (a.sym) hipLaunchKernelGGL((k_tile<false, true>), dim3(grid), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_tile<false, false>), dim3(grid), dim3(256), 0, s, a);
+    }
     return hipGetLastError();
 }
 

@@ -48,6 +48,28 @@ def test_ranges_vs_oracle(seed):
     assert np.array_equal(a, oa)
 
 
+@pytest.mark.parametrize("lim", [300, (1 << 17) - 1])
+def test_asymmetric_matrix(lim):
+    """A random, strand-asymmetric score matrix takes the 16-term scoring
+    path; entries up to the accepted limit (|s| < 2^17) must not overflow."""
+    from genomealignmenttools_amd import synth
+    from genomealignmenttools_amd._lib import GacError
+    rng = np.random.default_rng(lim)
+    mat = rng.integers(-lim, lim + 1, 16).astype(np.int32)
+    mat[0] = lim  # an extreme entry for sure
+    tg, qg, ca = synth.small_case(seed=5, n_chains=200, max_blocks=400)
+    e, cs = _setup(None, tg, qg, ca, mat=mat)
+    R = _ranges(ca, np.random.default_rng(5))
+    g, l, a = e.score_ranges(cs, R, want_local=True)
+    og, ol, oa = _oracle(tg, qg, mat=mat).score_ranges(ca, R)
+    assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
+    from genomealignmenttools_amd.gachain import GapCosts
+    bad = mat.copy()
+    bad[3] = 1 << 17
+    with pytest.raises(GacError):
+        e.set_scoring(bad, GapCosts("loose"))
+
+
 def test_workspace_growth_and_lookback():
     """One engine, batches of growing size: the first call's workspace guess
     is outgrown (device-side overflow flag -> grow -> rerun), k_plan's
