@@ -41,6 +41,8 @@ hipError_t launch_relayout(const uint8_t *raw, const SeqDev *seqs, int nseq, int
                            uint2 *planes, uint32_t *nmask, hipStream_t s);
 hipError_t launch_gap_table(const GapDev &g, const int32_t *small, int len, int32_t *tab,
                             hipStream_t s);
+hipError_t launch_block_gaps(const DChain *chains, int64_t n_chains, int4 *blk, const GapDev &g,
+                             const int32_t *small, const int32_t *tab, int len, hipStream_t s);
 hipError_t launch_nflags(const DChain *chains, int64_t n_chains, int4 *blk,
                          const uint32_t *t_nmask, const int64_t *t_woff, const uint32_t *q_nmask,
                          const int64_t *q_woff, hipStream_t s);
@@ -93,6 +95,7 @@ struct gac_ctx {
     Genome g[2];
     bool scoring = false;
     int32_t coef[16];  // multilinear basis (ScoreArgs::coef)
+    uint32_t gap_version = 0;  // bumped by every gac_set_scoring
     int sym = 0;
     GapDev gap;
     int32_t *d_small = nullptr;
@@ -135,7 +138,8 @@ struct gac_chainset {
     int64_t n_chains;
     int64_t n_blocks;
     DChain *chains = nullptr;
-    int4 *blk = nullptr;  // {tStart, qStart, size, nflags}, padded by one entry
+    int4 *blk = nullptr;  // {tStart, qStart, size | N flags, gap}, padded by one entry
+    uint32_t gap_version = 0;  // scoring setup the blk[].w gaps were computed for
     int2 *tspan = nullptr;  // {tStart, tEnd}
     uint32_t *bucket = nullptr;  // per-chain bucket indexes
 };
@@ -285,6 +289,7 @@ extern "C" int gac_set_scoring(gac_ctx *c, const int32_t mat[16], const gac_gapc
     HIPCHK(launch_gap_table(d, c->d_small, (int)len, c->d_gap_tab, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->gap_len = (int)len;
+    ++c->gap_version;
     c->scoring = true;
     return GAC_OK;
 }
@@ -677,6 +682,11 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
     if (n < 0 || n > INT32_MAX / 2) return gac_fail(GAC_E_ARG, "bad range count %lld", (long long)n);
     if (n == 0) return GAC_OK;
     if ((flags & GAC_WANT_LOCAL) && !d_l) return gac_fail(GAC_E_ARG, "GAC_WANT_LOCAL needs local output");
+    if (cs->gap_version != c->gap_version) {  // blk[].w for this scoring setup
+        HIPCHK(launch_block_gaps(cs->chains, cs->n_chains, cs->blk, c->gap, c->d_small,
+                                 c->d_gap_tab, c->gap_len, s));
+        const_cast<gac_chainset *>(cs)->gap_version = c->gap_version;
+    }
     // first guess for an empty workspace: 8 window blocks per range
     const int64_t guess = c->ws_flat ? 0 : 8 * n;
     int rc = ensure_ws(c, n, guess / kTileBlocks + 1, guess, s);

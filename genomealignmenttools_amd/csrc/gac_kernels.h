@@ -8,9 +8,11 @@
 //                 base 32w+i at bit i of each plane
 //     nmask[w]  : uint32, bit i set = base 32w+i is N (or padding)
 //     every sequence starts on a word boundary; word_off[s] = first word
-//   chains: DChain[c] + blocks blk[b] = int4 {tStart, qStart, size, nflags}
-//     nflags bit0/bit1: the block's target/query bases contain an N
+//   chains: DChain[c] + blocks blk[b] = int4 {tStart, qStart, size | flags, gap}
+//     flags (bits 29/30 of .z): the block's target/query bases contain an N
 //     (precomputed at upload; blocks without N skip the N-mask loads)
+//     gap: gapCalcCost to the chain's next block (k_block_gaps, per scoring
+//     setup; 0 after the last block)
 #pragma once
 #include <stdint.h>
 
@@ -21,6 +23,9 @@ constexpr int kTileBlocks = 64;  // blocks per tile (one per lane)
 constexpr int kWavesPerWG = 4;   // 256-thread workgroups
 constexpr int kMaxLong = 32;     // long gap positions
 constexpr long long kNeg = -(1LL << 61);  // -inf of the local-score monoid
+constexpr int kSizeMask = (1 << 29) - 1;  // block size field of blk[].z
+constexpr int kTHasN = 1 << 29;           // blk[].z: target bases contain an N
+constexpr int kQHasN = 1 << 30;           // blk[].z: query bases contain an N
 
 struct DChain {
     int64_t blk_off;
@@ -91,7 +96,7 @@ struct ScoreArgs {
     const int64_t *q_woff;
     const DChain *chains;
     int64_t n_chains;
-    const int4 *blk;     // [n_blocks + 1] {tStart, qStart, size, nflags}
+    const int4 *blk;     // [n_blocks + 1] {tStart, qStart, size | N flags, gap to next}
     const int2 *tspan;   // [n_blocks + 8] {tStart, tEnd} (window searches; padded)
     const uint32_t *bucket;  // chain bucket indexes (see DChain)
     const Range *ranges;

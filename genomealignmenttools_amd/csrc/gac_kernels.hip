@@ -196,10 +196,40 @@ __global__ void __launch_bounds__(256) k_nflags(const DChain *chains, int64_t n_
         const int qsize = ch.qinfo & 0x7fffffff;
         for (int k = lane; k < ch.nblk; k += kWave) {
             int4 b = blk[ch.blk_off + k];
-            const int64_t qf = minus ? (int64_t)qsize - b.y - b.z : b.y;
-            b.w = (range_has_n(t_nmask, tb + b.x, b.z) ? 1 : 0) |
-                  (range_has_n(q_nmask, qb + qf, b.z) ? 2 : 0);
+            const int z = b.z & kSizeMask;
+            const int64_t qf = minus ? (int64_t)qsize - b.y - z : b.y;
+            b.z = z | (range_has_n(t_nmask, tb + b.x, z) ? kTHasN : 0) |
+                  (range_has_n(q_nmask, qb + qf, z) ? kQHasN : 0);
             blk[ch.blk_off + k] = b;
+        }
+    }
+}
+
+// ------------------------------------------------------------ k_block_gaps
+// Per scoring setup and chain set: blk[b].w = gapCalcCost of the gap from
+// block b to block b+1 of the same chain (0 after a chain's last block).  A
+// gap inside a scored window is always between two unclipped block ends
+// (clipping only moves the first block's start and the last block's end), so
+// the tile kernel reads it with the block instead of evaluating it.
+__global__ void __launch_bounds__(256) k_block_gaps(const DChain *chains, int64_t n_chains,
+                                                    int4 *blk, GapDev g, const int32_t *small,
+                                                    const int32_t *tab, int len) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave_id = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t c = wave_id; c < n_chains; c += nwaves) {
+        const DChain ch = chains[c];
+        for (int k = lane; k < ch.nblk; k += kWave) {
+            int4 *b = blk + ch.blk_off + k;
+            int cost = 0;
+            if (k + 1 < ch.nblk) {
+                const int4 x = b[0], y = b[1];
+                const int z = x.z & kSizeMask;
+                int d;
+                const int which = gap_kind(y.y - (x.y + z), y.x - (x.x + z), d);
+                cost = d < len ? tab[which * len + d] : gap_cost_wd(g, small, which, d);
+            }
+            b->w = cost;
         }
     }
 }
@@ -486,11 +516,11 @@ struct WaveLds {
     long long tpos[kTileBlocks];  // global base index of the clipped target start
     long long qpos[kTileBlocks];  // '+': global base index of the clipped query start
                                   // '-': global base index of (qSize - clipped qStart)
-    int lenq[kTileBlocks];        // clipped length | minus << 31 | tN << 30 | qN << 29
+    int lenq[kTileBlocks];        // clipped length | minus << 31 | qN << 30 | tN << 29
     unsigned long long acc[kTileBlocks];  // block scores (int64: a block may be huge)
 };
 
-constexpr int kLenMask = (1 << 29) - 1;
+constexpr int kLenMask = kSizeMask;  // lenq: len | tN (bit 29) | qN (bit 30) | minus (bit 31)
 
 template <bool SYM>
 __device__ __forceinline__ int chunk_score(const ScoreArgs &a, const WaveLds &L, int k, int off,
@@ -499,11 +529,11 @@ __device__ __forceinline__ int chunk_score(const ScoreArgs &a, const WaveLds &L,
     uint32_t t0, t1, q0, q1, tn = 0, qn = 0;
     const int64_t tp = L.tpos[k] + off;
     load_planes(a.t_planes, tp, t0, t1);
-    if (lq & (1 << 30)) tn = load_nmask(a.t_nmask, tp);
+    if (lq & kTHasN) tn = load_nmask(a.t_nmask, tp);
     if (lq >= 0) {
         const int64_t qp = L.qpos[k] + off;
         load_planes(a.q_planes, qp, q0, q1);
-        if (lq & (1 << 29)) qn = load_nmask(a.q_nmask, qp);
+        if (lq & kQHasN) qn = load_nmask(a.q_nmask, qp);
     } else {
         // '-' strand: rc base j = comp(fwd[qSize-1-(qp+j)]), comp = code ^ 2
         const int64_t F = L.qpos[k] - off - n;
@@ -512,7 +542,7 @@ __device__ __forceinline__ int chunk_score(const ScoreArgs &a, const WaveLds &L,
         const int sh = 32 - n;
         q0 = __builtin_bitreverse32(f0) >> sh;
         q1 = ~(__builtin_bitreverse32(f1) >> sh);
-        if (lq & (1 << 29)) qn = __builtin_bitreverse32(load_nmask(a.q_nmask, F)) >> sh;
+        if (lq & kQHasN) qn = __builtin_bitreverse32(load_nmask(a.q_nmask, F)) >> sh;
     }
     const uint32_t v = (n >= 32 ? 0xffffffffu : ((1u << n) - 1u)) & ~tn & ~qn;
     // score = sum over positions of coef[S] * prod(S) in the basis
@@ -614,28 +644,22 @@ __global__ void __launch_bounds__(256, LOCAL ? 7 : 8) k_tile(ScoreArgs a) {
         long long tpos = 0, qpos = 0;
         if (active) {
             const RangeDesc d = a.rdesc[ri];
-            const int4 bk = a.blk[bi];
-            const int4 nx = a.blk[bi + 1];  // the block array is padded by one
+            const int4 bk = a.blk[bi];  // {tStart, qStart, size | N flags, gap to next}
             first = (bi == d.b0);
             last = (bi == d.b0 + d.nblk - 1);
-            const int te = bk.x + bk.z, qe = bk.y + bk.z;
-            int cts = bk.x, cqs = bk.y, cte = te;
+            const int z = bk.z & kSizeMask;
+            int cts = bk.x, cqs = bk.y, cte = bk.x + z;
             if (cts < d.s) {
                 cqs += d.s - cts;
                 cts = d.s;
             }
             if (cte > d.e) cte = d.e;
             len = cte - cts;
-            if (!last) {
-                int d;
-                const int which = gap_kind(nx.y - qe, nx.x - te, d);
-                g = d < a.gap_len ? a.gap_tab[which * a.gap_len + d]
-                                  : gap_cost_wd(a.gap, a.small_tab, which, d);
-            }
+            if (!last) g = bk.w;
             tpos = d.tbase + cts;
             const bool minus = d.qbase < 0;
             qpos = minus ? ~d.qbase - cqs : d.qbase + cqs;
-            lenq = len | (minus ? (int)0x80000000 : 0) | ((bk.w & 1) << 30) | ((bk.w & 2) << 28);
+            lenq = len | (minus ? (int)0x80000000 : 0) | (bk.z & (kTHasN | kQHasN));
         }
         // ---- chunk prefix (32 bases per chunk)
         const int nch = (len + 31) >> 5;
@@ -925,6 +949,15 @@ hipError_t launch_gap_table(const GapDev &g, const int32_t *small, int len, int3
                             hipStream_t s) {
     const int64_t nb = (3 * (int64_t)len + 255) / 256;
     hipLaunchKernelGGL(k_gap_table, dim3((unsigned)nb), dim3(256), 0, s, g, small, len, tab);
+    return hipGetLastError();
+}
+
+hipError_t launch_block_gaps(const DChain *chains, int64_t n_chains, int4 *blk, const GapDev &g,
+                             const int32_t *small, const int32_t *tab, int len, hipStream_t s) {
+    if (n_chains == 0) return hipSuccess;
+    const int64_t waves = n_chains < 65536 ? n_chains : 65536;
+    hipLaunchKernelGGL(k_block_gaps, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, chains,
+                       n_chains, blk, g, small, tab, len);
     return hipGetLastError();
 }
 
