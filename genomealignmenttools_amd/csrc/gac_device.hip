@@ -120,7 +120,9 @@ struct gac_ctx {
     Range *d_ranges = nullptr;
     long long *d_g = nullptr, *d_l = nullptr;
     int32_t *d_ali = nullptr;
-    int32_t *h_total = nullptr;  // pinned [8]
+    int32_t *h_stat = nullptr;   // pinned, coherent host words written by k_scan_agg [8]
+    int32_t *d_h_stat = nullptr; // its device address
+    int32_t call_seq = 0;
     int tile_grid = 2048;       // k_mark grid (resident workgroups)
     int tile_grid_g = 2048;     // k_tile<false> grid (resident workgroups)
     int tile_grid_l = 2048;     // k_tile<true> grid
@@ -174,7 +176,9 @@ extern "C" int gac_open(int device, gac_ctx **out) {
     c->combine_grid = prop.multiProcessorCount * 8;  // one 64-range group per wave
     c->tile_grid_g = prop.multiProcessorCount * persistent_blocks_per_cu(0);
     c->tile_grid_l = prop.multiProcessorCount * persistent_blocks_per_cu(1);
-    if (hipHostMalloc((void **)&c->h_total, 32, hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc((void **)&c->h_stat, 64, hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess ||
+        hipHostGetDevicePointer((void **)&c->d_h_stat, c->h_stat, 0) != hipSuccess) {
         hipStreamDestroy(c->stream);
         delete c;
         return gac_fail(GAC_E_HIP, "hipHostMalloc failed");
@@ -206,7 +210,7 @@ extern "C" void gac_close(gac_ctx *c) {
         hipEventDestroy(p.b);
     }
     for (auto ev : c->prof_free) hipEventDestroy(ev);
-    if (c->h_total) hipHostFree(c->h_total);
+    if (c->h_stat) hipHostFree(c->h_stat);
     hipStreamDestroy(c->stream);
     delete c;
 }
@@ -593,6 +597,9 @@ extern "C" int64_t gac_chains_block_count(const gac_chainset *cs) { return cs ? 
 
 // ----------------------------------------------------------------- launch
 static int ensure_ws(gac_ctx *c, int64_t n, int64_t max_tiles, int64_t flat, hipStream_t s) {
+    // buffers may still be in use by calls in flight on the stream
+    if (n > c->ws_n || flat > c->ws_flat || max_tiles > c->ws_tiles || !c->status)
+        HIPCHK(hipStreamSynchronize(s));
     if (n > c->ws_n) {
         int64_t cap = n + n / 2 + 1024;
         void *bufs[] = {c->rdesc, c->nblk, c->goff, c->pb0, c->agg, c->plan_off, c->chunk_off};
@@ -668,8 +675,30 @@ static hipEvent_t prof_event(gac_ctx *c) {
         c->prof_pending.push_back(Prof{(k), _pa, _pb}); \
     }
 
-// One call = 4 launches (k_plan, k_mark, k_tile, k_combine) and a 32-byte
-// status readback.  The flat block count W is only known on the
+// Spin on the pinned status words until k_scan_agg of call `tag` has written
+// them (checking now and then that the stream is still busy).
+static int wait_status(gac_ctx *c, hipStream_t s, int32_t tag, int32_t st[4]) {
+    volatile int32_t *h = c->h_stat;
+    for (uint64_t spin = 0;; ++spin) {
+        if (h[4] == tag) {
+            __atomic_thread_fence(__ATOMIC_ACQUIRE);
+            for (int k = 0; k < 4; ++k) st[k] = h[k];
+            return GAC_OK;
+        }
+        if ((spin & 1023) == 1023) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipSuccess && h[4] != tag)
+                return gac_fail(GAC_E_HIP, "scoring status never arrived (call %d)", tag);
+            if (q != hipSuccess && q != hipErrorNotReady)
+                return gac_fail(GAC_E_HIP, "scoring failed: %s", hipGetErrorString(q));
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+// One call = 5 launches (k_plan, k_scan_agg, k_mark, k_tile, k_combine); the
+// host waits only for k_scan_agg's status words (pinned memory), not for the
+// scoring itself.  The flat block count W is only known on the
 // device (ranges may overlap), so the kernels check the workspace capacity
 // themselves; on overflow k_tile / k_combine do nothing and the call grows the
 // workspace to the reported {W, T} and runs once more (first call or a larger
@@ -732,6 +761,9 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
         a.bidx = c->bidx;
         a.sum_head = c->sum_head;
         a.sum_tail = c->sum_tail;
+        a.host_status = c->d_h_stat;
+        a.call_tag = ++c->call_seq;
+        if (a.call_tag <= 0) a.call_tag = c->call_seq = 1;
         a.cap_flat = (int32_t)c->ws_flat;
         a.cap_tiles = (int32_t)(c->ws_tiles < INT32_MAX ? c->ws_tiles : INT32_MAX);
         {
@@ -750,12 +782,16 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
             HIPCHK(launch_combine(a, c->combine_grid, s));
             PROF_END(GAC_K_COMBINE);
         }
-        HIPCHK(hipMemcpyAsync(c->h_total, c->status, 32, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        const int32_t W = c->h_total[0], NT = c->h_total[1];
-        if (W == INT32_MAX) return gac_fail(GAC_E_ARG, "window block total overflows int32");
-        if (!c->h_total[2]) return GAC_OK;
-        rc = ensure_ws(c, n, NT, W, s);
+        // wait for k_scan_agg's status words only; the rest runs on
+        int32_t st[4];
+        rc = wait_status(c, s, a.call_tag, st);
+        if (rc != GAC_OK) return rc;
+        if (st[0] == INT32_MAX) {
+            HIPCHK(hipStreamSynchronize(s));
+            return gac_fail(GAC_E_ARG, "window block total overflows int32");
+        }
+        if (!st[2]) return GAC_OK;
+        rc = ensure_ws(c, n, st[1], st[0], s);  // (synchronises before growing)
         if (rc != GAC_OK) return rc;
     }
     return gac_fail(GAC_E_STATE, "scoring workspace still too small after growing it");
@@ -829,12 +865,14 @@ extern "C" int gac_dev_free(gac_ctx *c, void *p) {
 }
 extern "C" int gac_memcpy_h2d(gac_ctx *c, void *dst, const void *src, size_t n) {
     if (!c) return gac_fail(GAC_E_ARG, "NULL context");
-    HIPCHK(hipMemcpy(dst, src, n, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     return GAC_OK;
 }
 extern "C" int gac_memcpy_d2h(gac_ctx *c, void *dst, const void *src, size_t n) {
     if (!c) return gac_fail(GAC_E_ARG, "NULL context");
-    HIPCHK(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     return GAC_OK;
 }
 extern "C" int gac_synchronize(gac_ctx *c) {

@@ -116,6 +116,8 @@ struct ScoreArgs {
     int32_t *chunk_wg;   // [cap_chunks] plan workgroup of each mark chunk (large batches)
     int32_t *status;     // [8]   W (flat blocks, saturated), T (tiles), 1 = workspace too
                          //       small, mark chunks
+    int32_t *host_status;  // pinned host words: status[0..4) + call_tag (k_scan_agg)
+    int32_t call_tag;
     int32_t cap_chunks;
     int32_t cap_flat;    // ridx/bidx capacity
     int32_t cap_tiles;   // sum_head/sum_tail capacity

@@ -453,14 +453,22 @@ __device__ AggScan scan_totals(const ScoreArgs &a, int G, long long *s_wsum) {
     return t;
 }
 
+// {W, T, overflow, chunks} for the later kernels, and the same, tagged with
+// the call's sequence number, straight into the host's pinned status words:
+// the host learns whether the workspace sufficed as soon as this kernel ends,
+// while k_mark / k_tile / k_combine still run.
 __device__ __forceinline__ void publish_status(const ScoreArgs &a, AggScan t) {
     const long long T = (t.W + kTileBlocks - 1) / kTileBlocks;
     const bool over = t.W >= 0x7fffffffLL || t.W > a.cap_flat || T > a.cap_tiles ||
                       t.NQ > a.cap_chunks;
-    a.status[0] = (int32_t)t.W;
-    a.status[1] = (int32_t)T;
-    a.status[2] = over ? 1 : 0;
-    a.status[3] = (int32_t)(t.NQ < 0x7fffffffLL ? t.NQ : 0x7fffffffLL);
+    const int32_t st[4] = {(int32_t)t.W, (int32_t)T, over ? 1 : 0,
+                           (int32_t)(t.NQ < 0x7fffffffLL ? t.NQ : 0x7fffffffLL)};
+    for (int k = 0; k < 4; ++k) {
+        a.status[k] = st[k];
+        __hip_atomic_store(&a.host_status[k], st[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: values before the tag
+    __hip_atomic_store(&a.host_status[4], a.call_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ void __launch_bounds__(kPlanWG) k_scan_agg(ScoreArgs a) {

@@ -159,10 +159,13 @@ int gac_score_ranges(gac_ctx *ctx, const gac_chainset *cs, const gac_range *rang
                      int64_t n, uint32_t flags, int64_t *global, int64_t *local,
                      int32_t *ali);
 /* Same on device-resident buffers, enqueued on `stream` (a hipStream_t, or
- * NULL for the context's own stream).  Four kernel launches; the call then
- * waits for `stream` to read back a 32-byte status (the scoring workspace is
- * sized on the device and grown + rerun here when a batch outgrows it), so
- * results are ready on return.  d_local may be NULL unless GAC_WANT_LOCAL. */
+ * NULL for the context's own stream).  Returns as soon as the batch is known
+ * to fit the scoring workspace (the first kernels write a status word to
+ * pinned host memory; on the rare call that outgrows the workspace it is
+ * grown and the batch rerun before returning); the scoring itself completes
+ * asynchronously -- synchronise the stream (or gac_synchronize /
+ * gac_memcpy_d2h, which are ordered after it) before reading results.
+ * d_local may be NULL unless GAC_WANT_LOCAL. */
 int gac_score_ranges_device(gac_ctx *ctx, const gac_chainset *cs,
                             const gac_range *d_ranges, int64_t n, uint32_t flags,
                             int64_t *d_global, int64_t *d_local, int32_t *d_ali,
@@ -227,6 +230,7 @@ int gac_net_write(const gac_net *net, int side, const int64_t *t_scores, const c
 /* ---- device memory helpers (for callers without their own allocator) ---- */
 int gac_dev_alloc(gac_ctx *ctx, size_t bytes, void **dptr);
 int gac_dev_free(gac_ctx *ctx, void *dptr);
+/* Synchronous copies, ordered after all work enqueued on the context's stream. */
 int gac_memcpy_h2d(gac_ctx *ctx, void *dst, const void *src, size_t bytes);
 int gac_memcpy_d2h(gac_ctx *ctx, void *dst, const void *src, size_t bytes);
 int gac_synchronize(gac_ctx *ctx);

@@ -108,6 +108,38 @@ def test_workspace_growth_and_lookback():
     assert np.array_equal(g, og) and np.array_equal(a, oa)
 
 
+def test_device_api_async_batches():
+    """gac_score_ranges_device returns before the scoring completes: several
+    batches enqueued back to back (the second outgrows the workspace), each
+    into its own output buffers, then read after one synchronisation."""
+    from genomealignmenttools_amd import synth
+    tg, qg, ca = synth.small_case(seed=6, n_chains=300, max_blocks=1500)
+    e, cs = _setup(None, tg, qg, ca)
+    orc = _oracle(tg, qg)
+    rng = np.random.default_rng(6)
+    full = np.stack([np.arange(ca.n), ca.tstart, ca.tend], 1)
+    batches = [_ranges(ca, rng, per_chain=1)[:50], np.tile(full, (4, 1)), _ranges(ca, rng)]
+    bufs = []
+    for R in batches:
+        R32 = np.ascontiguousarray(R, np.int32)
+        n = len(R32)
+        d_r, d_g, d_l, d_a = (e.dev_alloc(max(1, n * k)) for k in (12, 8, 8, 4))
+        e.h2d(d_r, R32)
+        e.score_ranges_device(cs, d_r, n, d_g, d_a, d_l=d_l, want_local=True)
+        bufs.append((R, d_r, d_g, d_l, d_a))
+    e.synchronize()
+    for R, d_r, d_g, d_l, d_a in bufs:
+        n = len(R)
+        g, l, a = np.zeros(n, np.int64), np.zeros(n, np.int64), np.zeros(n, np.int32)
+        e.d2h(g, d_g)
+        e.d2h(l, d_l)
+        e.d2h(a, d_a)
+        og, ol, oa = orc.score_ranges(ca, R)
+        assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
+        for p in (d_r, d_g, d_l, d_a):
+            e.dev_free(p)
+
+
 def test_long_chains_multi_tile():
     """Chains of thousands of blocks: ranges span many 64-block tiles."""
     from genomealignmenttools_amd import synth
