@@ -530,35 +530,37 @@ struct WaveLds {
 
 constexpr int kLenMask = kSizeMask;  // lenq: len | tN (bit 29) | qN (bit 30) | minus (bit 31)
 
+// One 32-base chunk of a tile, split into address preparation, loads and
+// evaluation so that the loads of a lane's two chunks are issued together,
+// with no branch between them (a branch makes the compiler wait for every
+// load in flight).
+struct ChunkRef {
+    int64_t tp, qp;  // first word-aligned window of the target / query planes
+    int k;           // block (lane of the tile)
+    int n;           // bases in the chunk (<= 0: no chunk; loads stay in bounds)
+    int lq;          // the block's lenq
+};
+
+__device__ __forceinline__ ChunkRef chunk_prep(const WaveLds &L, int j);
+
+struct ChunkRaw {
+    u32x4a8 t, q;  // plane words w, w+1 ({p0, p1} each)
+};
+
+__device__ __forceinline__ ChunkRaw chunk_load(const ScoreArgs &a, const ChunkRef &c) {
+    ChunkRaw r;
+    r.t = *reinterpret_cast<const u32x4a8 *>(a.t_planes + (c.tp >> 5));
+    r.q = *reinterpret_cast<const u32x4a8 *>(a.q_planes + (c.qp >> 5));
+    return r;
+}
+
+// sum over the positions in v of the matrix score, in the multilinear basis
+// (t1, t0, d1, d0), d = q ^ t (see ScoreArgs::coef): one AND + popcount +
+// 24-bit multiply-add per term.  Strand-symmetric matrices (M[comp q][comp t]
+// = M[q][t]; comp flips bit 1) have no t1 terms: 8 instead of 16.
 template <bool SYM>
-__device__ __forceinline__ int chunk_score(const ScoreArgs &a, const WaveLds &L, int k, int off,
-                                           int n) {
-    const int lq = L.lenq[k];
-    uint32_t t0, t1, q0, q1, tn = 0, qn = 0;
-    const int64_t tp = L.tpos[k] + off;
-    load_planes(a.t_planes, tp, t0, t1);
-    if (lq & kTHasN) tn = load_nmask(a.t_nmask, tp);
-    if (lq >= 0) {
-        const int64_t qp = L.qpos[k] + off;
-        load_planes(a.q_planes, qp, q0, q1);
-        if (lq & kQHasN) qn = load_nmask(a.q_nmask, qp);
-    } else {
-        // '-' strand: rc base j = comp(fwd[qSize-1-(qp+j)]), comp = code ^ 2
-        const int64_t F = L.qpos[k] - off - n;
-        uint32_t f0, f1;
-        load_planes(a.q_planes, F, f0, f1);
-        const int sh = 32 - n;
-        q0 = __builtin_bitreverse32(f0) >> sh;
-        q1 = ~(__builtin_bitreverse32(f1) >> sh);
-        if (lq & kQHasN) qn = __builtin_bitreverse32(load_nmask(a.q_nmask, F)) >> sh;
-    }
-    const uint32_t v = (n >= 32 ? 0xffffffffu : ((1u << n) - 1u)) & ~tn & ~qn;
-    // score = sum over positions of coef[S] * prod(S) in the basis
-    // (t1, t0, d1, d0), d = q ^ t (multilinear form of the 4x4 matrix, see
-    // ScoreArgs::coef): one AND + popcount + 24-bit multiply-add per term.
-    // Strand-symmetric matrices (M[comp q][comp t] = M[q][t]; comp flips
-    // bit 1) have no t1 terms: 8 instead of 16.
-    const uint32_t d0 = q0 ^ t0, d1 = q1 ^ t1;
+__device__ __forceinline__ int score_bits(const ScoreArgs &a, uint32_t v, uint32_t t0,
+                                          uint32_t t1, uint32_t d0, uint32_t d1) {
     const uint32_t m2 = v & d1, m1 = v & d0, m4 = v & t0;
     const uint32_t m3 = m2 & d0, m6 = m4 & d1, m5 = m4 & d0, m7 = m6 & d0;
     int sc = __mul24(a.coef[0], (int)__builtin_popcount(v));
@@ -583,6 +585,39 @@ __device__ __forceinline__ int chunk_score(const ScoreArgs &a, const WaveLds &L,
     return sc;
 }
 
+// Score of a chunk: all positions first; N positions (blocks flagged at
+// upload only -- rare) are then subtracted, so the common path carries no
+// N-mask loads.
+template <bool SYM>
+__device__ __forceinline__ int chunk_eval(const ScoreArgs &a, const ChunkRef &c,
+                                          const ChunkRaw &r) {
+    const int n = c.n;
+    const int sht = (int)(c.tp & 31), shq = (int)(c.qp & 31);
+    const uint32_t t0 = funnel(r.t.z, r.t.x, sht), t1 = funnel(r.t.w, r.t.y, sht);
+    uint32_t q0 = funnel(r.q.z, r.q.x, shq), q1 = funnel(r.q.w, r.q.y, shq);
+    const bool minus = c.lq < 0;
+    const int sh = 32 - n;
+    if (minus) {
+        // '-' strand: rc base j = comp(fwd[qSize-1-(qp+j)]), comp = code ^ 2;
+        // the window was read at the forward position of the chunk's end
+        q0 = __builtin_bitreverse32(q0) >> sh;
+        q1 = ~(__builtin_bitreverse32(q1) >> sh);
+    }
+    const uint32_t v = n <= 0 ? 0u : n >= 32 ? 0xffffffffu : ((1u << n) - 1u);
+    const uint32_t d0 = q0 ^ t0, d1 = q1 ^ t1;
+    int sc = score_bits<SYM>(a, v, t0, t1, d0, d1);
+    if (c.lq & (kTHasN | kQHasN)) {
+        uint32_t nm = 0;
+        if (c.lq & kTHasN) nm = load_nmask(a.t_nmask, c.tp);
+        if (c.lq & kQHasN) {
+            const uint32_t qn = load_nmask(a.q_nmask, c.qp);
+            nm |= minus ? __builtin_bitreverse32(qn) >> sh : qn;
+        }
+        sc -= score_bits<SYM>(a, v & nm, t0, t1, d0, d1);
+    }
+    return sc;
+}
+
 // Block owning chunk j: the largest k with coff[k] <= j (coff is
 // non-decreasing; blocks without chunks share the next block's offset and
 // lanes past the tile's end hold the chunk total, so no bounds are needed).
@@ -597,6 +632,21 @@ __device__ __forceinline__ int find_chunk_block(const WaveLds &L, int j) {
     return k;
 }
 
+// Chunk j of the tile: its block, base count and plane positions.  j past
+// the tile's chunks yields n <= 0 with in-bounds positions.
+__device__ __forceinline__ ChunkRef chunk_prep(const WaveLds &L, int j) {
+    ChunkRef c;
+    c.k = find_chunk_block(L, j);
+    c.lq = L.lenq[c.k];
+    int off = (j - L.coff[c.k]) << 5;
+    c.n = min(32, (c.lq & kLenMask) - off);
+    if (c.n <= 0) off = 0;
+    c.tp = L.tpos[c.k] + off;
+    // '-': read the forward window that ends where the chunk starts
+    c.qp = c.lq < 0 ? L.qpos[c.k] - off - max(c.n, 0) : L.qpos[c.k] + off;
+    return c;
+}
+
 template <bool LOCAL>
 __device__ __forceinline__ void seg_store(const ScoreArgs &a, int ri, long long g, int ali,
                                           const Elem &e) {
@@ -606,7 +656,7 @@ __device__ __forceinline__ void seg_store(const ScoreArgs &a, int ri, long long 
 }
 
 template <bool LOCAL, bool SYM>
-__global__ void __launch_bounds__(256, LOCAL ? 7 : 8) k_tile(ScoreArgs a) {
+__global__ void __launch_bounds__(256, 6) k_tile(ScoreArgs a) {
     __shared__ WaveLds s_w[kWavesPerWG];
 
     const int wave = threadIdx.x >> 6;
@@ -686,20 +736,14 @@ __global__ void __launch_bounds__(256, LOCAL ? 7 : 8) k_tile(ScoreArgs a) {
         wave_sync();
 
         for (int c0 = 0; c0 < C; c0 += 2 * kWave) {
-            const int ja = c0 + lane, jb = ja + kWave;
-            int ka = 0, kb = 0, sa = 0, sb = 0;
-            if (ja < C) {
-                ka = find_chunk_block(L, ja);
-                const int off = (ja - L.coff[ka]) << 5;
-                sa = chunk_score<SYM>(a, L, ka, off, min(32, (L.lenq[ka] & kLenMask) - off));
-            }
-            if (jb < C) {
-                kb = find_chunk_block(L, jb);
-                const int off = (jb - L.coff[kb]) << 5;
-                sb = chunk_score<SYM>(a, L, kb, off, min(32, (L.lenq[kb] & kLenMask) - off));
-            }
-            if (ja < C) atomicAdd(&L.acc[ka], (unsigned long long)(long long)sa);
-            if (jb < C) atomicAdd(&L.acc[kb], (unsigned long long)(long long)sb);
+            const ChunkRef ca = chunk_prep(L, c0 + lane);
+            const ChunkRef cb = chunk_prep(L, c0 + kWave + lane);
+            const ChunkRaw ra = chunk_load(a, ca);
+            const ChunkRaw rb = chunk_load(a, cb);
+            const int sa = chunk_eval<SYM>(a, ca, ra);
+            const int sb = chunk_eval<SYM>(a, cb, rb);
+            if (ca.n > 0) atomicAdd(&L.acc[ca.k], (unsigned long long)(long long)sa);
+            if (cb.n > 0) atomicAdd(&L.acc[cb.k], (unsigned long long)(long long)sb);
         }
         wave_sync();
 
