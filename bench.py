@@ -181,7 +181,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc_traffic(args, n, nblk),
             "kernel": "k_tile", "kernel_avg_ms": tile_avg_s * 1e3,
             "algo_bytes_per_launch": algo_bytes,
         },
@@ -197,6 +197,25 @@ def main():
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                            "k_tile_traffic.json")
+
+
+def _pmc_traffic(args, n, nblk):
+    """HBM bytes per k_tile launch from the committed PMC profile of this same
+    workload (scripts/gpu_counters.sh + scripts/pmc_summary.py: request
+    counters by size), or None when no profile matches the workload."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if (t.get("workload") != args.workload or t.get("ranges") != n or t.get("blocks") != nblk
+            or t.get("chains") != args.chains or t.get("seed") != args.seed):
+        return None
+    return t.get("hbm_bytes_per_launch")
 
 
 def _window_blocks(ca, ranges):

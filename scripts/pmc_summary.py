@@ -4,10 +4,14 @@ JSON: per kernel, the mean counter value per dispatch, plus derived figures
 
 usage: python scripts/pmc_summary.py gpurun_out/TAG > profiles/rNN_pmc_summary.json
 
-FETCH_SIZE / WRITE_SIZE are reported by rocprofv3 in KiB; per
-/opt/skills/guides/MI355X_MICROARCH.md the gfx950 FETCH_SIZE derivation counts
-64-byte requests at 128 bytes, so reads made only of wide (128-B) requests are
-exact and the figure is an upper bound otherwise.
+FETCH_SIZE / WRITE_SIZE are reported by rocprofv3 in KiB, but on gfx950
+FETCH_SIZE tallies every memory-side read request at 64 B whatever its size
+(MI355X_MICROARCH.md, HBM section), so the HBM bytes are taken from the
+request counters by size instead: hbm_read_bytes = 32 n32 + 64 n64 + 128 n128
+(TCC_EA0_RDREQ_{32,64,128}B), hbm_write_bytes = 64 n64 + 32 (n - n64)
+(TCC_EA0_WRREQ, _64B).  Infinity-cache hits are counted by these counters
+too (same section), so the figure is traffic leaving L2, an upper bound on
+DRAM bytes.
 """
 import collections
 import csv
@@ -42,6 +46,15 @@ def main(root):
             d["fetch_bytes"] = d["FETCH_SIZE"] * 1024.0
         if "WRITE_SIZE" in d:
             d["write_bytes"] = d["WRITE_SIZE"] * 1024.0
+        # HBM-side bytes by request size (the traffic figure bench.py reports)
+        if "TCC_EA0_RDREQ_32B_sum" in d:
+            d["hbm_read_bytes"] = (32.0 * d["TCC_EA0_RDREQ_32B_sum"] + 64.0 * d["TCC_EA0_RDREQ_64B_sum"]
+                                   + 128.0 * d["TCC_EA0_RDREQ_128B_sum"])
+        if "TCC_EA0_WRREQ_sum" in d:
+            w64 = d["TCC_EA0_WRREQ_64B_sum"]
+            d["hbm_write_bytes"] = 64.0 * w64 + 32.0 * (d["TCC_EA0_WRREQ_sum"] - w64)
+        if "hbm_read_bytes" in d and "hbm_write_bytes" in d:
+            d["hbm_bytes"] = d["hbm_read_bytes"] + d["hbm_write_bytes"]
         if d.get("SQ_WAVE_CYCLES"):
             d["wait_any_frac"] = d.get("SQ_WAIT_ANY", 0.0) / d["SQ_WAVE_CYCLES"]
         out[k] = d
