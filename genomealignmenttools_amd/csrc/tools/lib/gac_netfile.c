@@ -1,0 +1,341 @@
+/* gac_netfile.c -- .net text: kent net reader tree and NetFilterNonNested
+ * (see gac_netfile.h for the reference semantics restated here). */
+#define _GNU_SOURCE
+#include "gac_netfile.h"
+
+#include <ctype.h>
+#include <limits.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "gac_tool.h"
+#include "host/gac_host.h"
+
+/* ------------------------------------------------------------ lines */
+void gt_lines_push(gt_lines *l, char *s) {
+    if (l->n == l->cap) {
+        l->cap = l->cap ? l->cap * 2 : 1024;
+        l->line = realloc(l->line, (size_t)l->cap * sizeof(char *));
+    }
+    l->line[l->n++] = s;
+}
+
+void gt_lines_read(const char *path, gt_lines *l) {
+    memset(l, 0, sizeof(*l));
+    FILE *f = gt_must_open(path, "r");
+    size_t cap = 1 << 20, len = 0;
+    char *buf = malloc(cap + 1);
+    size_t r;
+    while ((r = fread(buf + len, 1, cap - len, f)) > 0) {
+        len += r;
+        if (len == cap) {
+            cap *= 2;
+            buf = realloc(buf, cap + 1);
+        }
+    }
+    if (f != stdin)
+        fclose(f);
+    buf[len] = 0;
+    l->buf = buf;
+    char *p = buf, *end = buf + len;
+    while (p < end) {
+        char *nl = memchr(p, '\n', end - p);
+        if (nl)
+            *nl = 0;
+        if (l->n == l->cap) {
+            l->cap = l->cap ? l->cap * 2 : 1024;
+            l->line = realloc(l->line, (size_t)l->cap * sizeof(char *));
+        }
+        l->line[l->n++] = p;
+        p = nl ? nl + 1 : end;
+    }
+}
+
+void gt_lines_free(gt_lines *l) {
+    if (!l->buf)
+        for (int64_t i = 0; i < l->n; ++i)
+            free(l->line[i]);
+    free(l->line);
+    free(l->buf);
+    memset(l, 0, sizeof(*l));
+}
+
+/* ------------------------------------------------------------ net tree */
+typedef struct reader {
+    const gt_lines *l;
+    int64_t pos;
+    const char *what;
+    gt_netset *ns;
+} reader;
+
+/* lineFileNextReal: skip blank lines and lines whose first non-blank is '#' */
+static char *next_real(reader *r) {
+    while (r->pos < r->l->n) {
+        char *s = r->l->line[r->pos++];
+        const char *p = s;
+        while (isspace((unsigned char)*p))
+            ++p;
+        if (*p != 0 && *p != '#')
+            return s;
+    }
+    return NULL;
+}
+
+static int32_t need_num(reader *r, char **w, int i) {
+    char *end;
+    long v = strtol(w[i], &end, 10);
+    if (*w[i] == 0 || *end != 0)
+        gt_abort("Expecting number field %d line %lld of %s, got %s", i + 1, (long long)r->pos,
+                 r->what, w[i]);
+    return (int32_t)v;
+}
+
+/* cnFillFromLine (chainNet.c:86-150): the fields chainCleaner uses */
+static int32_t fill_from_line(reader *r, char *line) {
+    char *w[64];
+    char *copy = strdup(line);
+    int wc = gac_chop_white(copy, w, 64);
+    if (wc < 7)
+        gt_abort("Expecting 7 words line %lld of %s got %d", (long long)r->pos, r->what, wc);
+    gt_netset *ns = r->ns;
+    if (ns->nf == ns->fcap) {
+        ns->fcap = ns->fcap ? ns->fcap * 2 : 4096;
+        ns->fills = realloc(ns->fills, (size_t)ns->fcap * sizeof(gt_fill));
+    }
+    gt_fill *f = &ns->fills[ns->nf];
+    memset(f, 0, sizeof(*f));
+    f->child = f->next = -1;
+    f->tstart = need_num(r, w, 1);
+    f->tsize = need_num(r, w, 2);
+    need_num(r, w, 5);
+    need_num(r, w, 6);
+    for (int i = 7; i < wc; i += 2) {
+        if (i + 1 >= wc)
+            break;
+        if (strcmp(w[i], "score") == 0)
+            f->score = atof(w[i + 1]);
+        else if (strcmp(w[i], "type") == 0)
+            ;
+        else {
+            int32_t v = need_num(r, w, i + 1);
+            if (strcmp(w[i], "id") == 0)
+                f->chain_id = v;
+        }
+    }
+    free(copy);
+    return (int32_t)ns->nf++;
+}
+
+static int lead_spaces(const char *s) {
+    int d = 0;
+    while (s[d] == ' ')
+        ++d;
+    return d;
+}
+
+/* cnFillRead (chainNet.c:152-178) */
+static int32_t read_list(reader *r) {
+    int depth = 0;
+    int32_t head = -1, tail = -1, fill = -1;
+    for (;;) {
+        char *line = next_real(r);
+        if (!line)
+            break;
+        const int d = lead_spaces(line);
+        if (fill < 0)
+            depth = d;
+        if (d < depth) {
+            --r->pos; /* lineFileReuse */
+            break;
+        }
+        if (d > depth) {
+            --r->pos;
+            const int32_t c = read_list(r);
+            r->ns->fills[fill].child = c;
+        } else {
+            fill = fill_from_line(r, line);
+            if (tail < 0)
+                head = fill;
+            else
+                r->ns->fills[tail].next = fill;
+            tail = fill;
+        }
+    }
+    return head;
+}
+
+void gt_net_parse(const gt_lines *l, const char *what, gt_netset *ns) {
+    memset(ns, 0, sizeof(*ns));
+    reader r = {l, 0, what, ns};
+    char *line;
+    while ((line = next_real(&r)) != NULL) {
+        if (strncmp(line, "net ", 4) != 0)
+            gt_abort("Expecting 'net' first word of line %lld of %s", (long long)r.pos, what);
+        char *w[3];
+        char *copy = strdup(line);
+        int wc = gac_chop_white(copy, w, 3);
+        if (wc < 3)
+            gt_abort("Expecting 3 words line %lld of %s got %d", (long long)r.pos, what, wc);
+        if (ns->n == ns->cap) {
+            ns->cap = ns->cap ? ns->cap * 2 : 64;
+            ns->nets = realloc(ns->nets, (size_t)ns->cap * sizeof(gt_net1));
+        }
+        gt_net1 *n = &ns->nets[ns->n++];
+        n->name = strdup(w[1]);
+        n->size = need_num(&r, w, 2);
+        free(copy);
+        n->first = read_list(&r);
+    }
+}
+
+void gt_netset_free(gt_netset *ns) {
+    for (int32_t i = 0; i < ns->n; ++i)
+        free(ns->nets[i].name);
+    free(ns->nets);
+    free(ns->fills);
+    memset(ns, 0, sizeof(*ns));
+}
+
+/* ------------------------------------------------------------ NetFilterNonNested */
+/* the script's fill/gap pattern /^([ ]+)([fill|gap].*)/: spaces, then one of
+ * the characters f i l | g a p; returns the space count or -1 */
+static int level_of(const char *s) {
+    int d = lead_spaces(s);
+    if (d == 0 || !strchr("fil|gap", s[d]) || s[d] == 0)
+        return -1;
+    return d;
+}
+
+/* Perl's numeric value of a decimal field (as used by the script's >=) */
+static double field_num(const char *s) { return atof(s); }
+
+void gt_netfilter_nonnested(const gt_lines *in, const char *what, double s1, double t1,
+                            double q1, double s2, double t2, double q2, gt_lines *out) {
+    memset(out, 0, sizeof(*out));
+    /* mode "12": an unset set 2 (all zero) -> INT_MAX; an unset set 1 -> INT_MAX */
+    if (s2 == 0 && t2 == 0 && q2 == 0)
+        s2 = t2 = q2 = INT_MAX;
+    if (s1 == 0 && t1 == 0 && q1 == 0)
+        s1 = t1 = q1 = INT_MAX;
+    const int64_t n = in->n;
+    char *skip = calloc(n ? n : 1, 1);
+    int *minus = calloc(n ? n : 1, sizeof(int));
+    /* the script keys its per-net counter by the net line's text */
+    gt_names netkey;
+    memset(&netkey, 0, sizeof(netkey));
+    int64_t *kept = calloc(n ? n : 1, sizeof(int64_t)); /* per distinct net line */
+    int64_t i = 0;
+    for (; i < n; ++i) {
+        if (in->line[i][0] == '#')
+            continue;
+        if (strncmp(in->line[i], "net ", 4) != 0)
+            gt_abort("ERROR: expect file to start with net, but got this line instead: %s\n",
+                     in->line[i]);
+        break;
+    }
+    int64_t cur = 0;
+    if (i < n) {
+        cur = gt_names_add(&netkey, in->line[i], strlen(in->line[i]));
+        kept[cur] = 0;
+    }
+    for (int64_t k = i + 1; k < n; ++k) {
+        const char *line = in->line[k];
+        if (strstr(line, " gap "))
+            continue;
+        if (strncmp(line, "net ", 4) == 0) {
+            cur = gt_names_add(&netkey, line, strlen(line));
+            kept[cur] = 0;
+            continue;
+        }
+        const int level = level_of(line);
+        if (level < 0)
+            gt_abort("ERROR: expect fill or gap in %s\n", line);
+        if (!strstr(line, " fill "))
+            continue;
+        const char *rest = line + level;
+        const char *sc = strstr(rest, "score ");
+        /* /score (\d+) /: digits followed by a space */
+        double score = -1;
+        while (sc) {
+            const char *p = sc + 6;
+            const char *q = p;
+            while (isdigit((unsigned char)*q))
+                ++q;
+            if (q > p && *q == ' ') {
+                score = atof(p);
+                break;
+            }
+            sc = strstr(sc + 1, "score ");
+        }
+        if (score < 0)
+            gt_abort("ERROR: no score field is given in this fill line: %s\n", rest);
+        /* split / / of the rest: f[2] = tSize, f[6] = qSize */
+        char *copy = strdup(rest);
+        char *f[8] = {0};
+        int nf = 0;
+        for (char *tok = copy;;) {
+            char *sp = strchr(tok, ' ');
+            if (nf < 8)
+                f[nf] = tok;
+            ++nf;
+            if (!sp)
+                break;
+            *sp = 0;
+            tok = sp + 1;
+        }
+        const double tsz = nf > 2 ? field_num(f[2]) : 0, qsz = nf > 6 ? field_num(f[6]) : 0;
+        free(copy);
+        const int pass = (score >= s1 && tsz >= t1 && qsz >= q1) ||
+                         (score >= s2 && tsz >= t2 && qsz >= q2);
+        if (pass) {
+            kept[cur]++;
+        } else {
+            skip[k] = 1;
+            /* eraseGapsMarkSkip(k + 1, level) */
+            for (int64_t j = k + 1; j < n; ++j) {
+                const char *lj = in->line[j];
+                if (strncmp(lj, "net ", 4) == 0)
+                    break;
+                const int cl = level_of(lj);
+                if (cl < 0)
+                    gt_abort("ERROR: expect fill or gap in %s\n", lj);
+                if (cl <= level)
+                    break;
+                if (cl == level + 1)
+                    skip[j] = 1;
+                else
+                    minus[j] += 2;
+            }
+        }
+    }
+    (void)what;
+    /* output(): net lines if a fill of theirs is kept, then kept fill/gap
+     * lines re-indented */
+    for (int64_t k = 0; k < n; ++k) {
+        const char *line = in->line[k];
+        if (strncmp(line, "net ", 4) == 0) {
+            const int32_t key = gt_names_find(&netkey, line);
+            if (key >= 0 && kept[key] > 0)
+                gt_lines_push(out, strdup(line));
+        }
+        if (!skip[k]) {
+            const int level = level_of(line);
+            if (level >= 0) {
+                const int cl = level - minus[k];
+                const char *rest = line + level;
+                const size_t rl = strlen(rest);
+                char *s = malloc((size_t)(cl > 0 ? cl : 0) + rl + 1);
+                int p = 0;
+                for (; p < cl; ++p)
+                    s[p] = ' ';
+                memcpy(s + p, rest, rl + 1);
+                gt_lines_push(out, s);
+            }
+        }
+    }
+    free(skip);
+    free(minus);
+    free(kept);
+    gt_names_free(&netkey);
+}

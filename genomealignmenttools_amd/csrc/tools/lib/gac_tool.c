@@ -169,6 +169,116 @@ int gt_opt_int(const char *name, int def) {
     return (int)v;
 }
 
+/* optionDouble (kent/src/lib/options.c:426-439) */
+double gt_opt_double(const char *name, double def) {
+    const char *s = gt_opt_str(name, NULL);
+    if (!s)
+        return def;
+    char *end;
+    double v = strtod(s, &end);
+    if (*s == 0 || *end != 0)
+        gt_abort("value of -%s is not a valid double: \"%s\"", name, s);
+    return v;
+}
+
+/* ------------------------------------------------------------ kent hash order */
+static uint32_t kent_hash_string(const char *s) {
+    uint32_t r = 0;
+    int c;
+    while ((c = *s++) != 0)
+        r += (r << 3) + (uint32_t)c;
+    return r;
+}
+
+void gt_khash_init(gt_khash *h, int pow) {
+    memset(h, 0, sizeof(*h));
+    h->pow = pow ? pow : 12;
+    h->mask = (1u << h->pow) - 1;
+    h->head = malloc(((size_t)1 << h->pow) * sizeof(int32_t));
+    memset(h->head, 0xff, ((size_t)1 << h->pow) * sizeof(int32_t));
+}
+
+int32_t gt_khash_find(const gt_khash *h, int32_t key) {
+    char buf[16];
+    snprintf(buf, sizeof(buf), "%d", key);
+    for (int32_t e = h->head[kent_hash_string(buf) & h->mask]; e >= 0; e = h->next[e])
+        if (h->key[e] == key)
+            return e;
+    return -1;
+}
+
+static void khash_resize(gt_khash *h, int pow) {
+    if (pow > 30)
+        pow = 30;
+    if (pow == h->pow)
+        return;
+    const uint32_t old_size = 1u << h->pow;
+    int32_t *old = h->head;
+    h->pow = pow;
+    h->mask = (1u << pow) - 1;
+    h->head = malloc(((size_t)1 << pow) * sizeof(int32_t));
+    memset(h->head, 0xff, ((size_t)1 << pow) * sizeof(int32_t));
+    for (uint32_t i = 0; i < old_size; ++i) {
+        int32_t e = old[i];
+        while (e >= 0) {
+            const int32_t nx = h->next[e];
+            const uint32_t b = h->hv[e] & h->mask;
+            h->next[e] = h->head[b];
+            h->head[b] = e;
+            e = nx;
+        }
+    }
+    /* hashReverseAllBucketLists */
+    for (uint32_t b = 0; b <= h->mask; ++b) {
+        int32_t prev = -1, e = h->head[b];
+        while (e >= 0) {
+            const int32_t nx = h->next[e];
+            h->next[e] = prev;
+            prev = e;
+            e = nx;
+        }
+        h->head[b] = prev;
+    }
+    free(old);
+}
+
+int32_t gt_khash_add(gt_khash *h, int32_t key) {
+    if (h->n == h->cap) {
+        h->cap = h->cap ? h->cap * 2 : 1024;
+        h->next = realloc(h->next, (size_t)h->cap * sizeof(int32_t));
+        h->hv = realloc(h->hv, (size_t)h->cap * sizeof(uint32_t));
+        h->key = realloc(h->key, (size_t)h->cap * sizeof(int32_t));
+    }
+    char buf[16];
+    snprintf(buf, sizeof(buf), "%d", key);
+    const int32_t e = h->n++;
+    h->key[e] = key;
+    h->hv[e] = kent_hash_string(buf);
+    const uint32_t b = h->hv[e] & h->mask;
+    h->next[e] = h->head[b];
+    h->head[b] = e;
+    /* autoExpand: elCount > size * 1.0 -> digitsBaseTwo(size) = pow + 1 */
+    if ((int64_t)h->n > ((int64_t)1 << h->pow))
+        khash_resize(h, h->pow + 1);
+    return e;
+}
+
+int32_t gt_khash_order(const gt_khash *h, int32_t *out) {
+    int32_t k = 0;
+    for (uint32_t b = 0; b <= h->mask; ++b)
+        for (int32_t e = h->head[b]; e >= 0; e = h->next[e])
+            out[k++] = e;
+    return k;
+}
+
+void gt_khash_free(gt_khash *h) {
+    free(h->head);
+    free(h->next);
+    free(h->hv);
+    free(h->key);
+    memset(h, 0, sizeof(*h));
+}
+
 /* ------------------------------------------------------------ names */
 static uint32_t hash_str(const char *s, size_t n) {
     uint32_t h = 2166136261u;
@@ -517,6 +627,22 @@ void gt_write_chain(FILE *f, const gt_chains *c, int64_t i, double score, int32_
                     c->bq[b + 1] - (c->bq[b] + c->bs[b]));
         else
             fprintf(f, "%d\n", c->bs[b]);
+    }
+    fputc('\n', f);
+}
+
+void gt_write_chain_raw(FILE *f, double score, const char *tname, int32_t tsize, int32_t tstart,
+                        int32_t tend, const char *qname, int32_t qsize, int qminus,
+                        int32_t qstart, int32_t qend, int32_t id, const int32_t *bt,
+                        const int32_t *bq, const int32_t *bs, int64_t nb) {
+    fprintf(f, "chain %1.0f %s %d + %d %d %s %d %c %d %d %d\n", score, tname, tsize, tstart, tend,
+            qname, qsize, qminus ? '-' : '+', qstart, qend, id);
+    for (int64_t b = 0; b < nb; ++b) {
+        if (b + 1 < nb)
+            fprintf(f, "%d\t%d\t%d\n", bs[b], bt[b + 1] - (bt[b] + bs[b]),
+                    bq[b + 1] - (bq[b] + bs[b]));
+        else
+            fprintf(f, "%d\n", bs[b]);
     }
     fputc('\n', f);
 }

@@ -31,6 +31,30 @@ void gt_options(int *argc, char **argv, const gt_spec *spec);
 const char *gt_opt_str(const char *name, const char *def);
 int gt_opt_exists(const char *name);
 int gt_opt_int(const char *name, int def);
+double gt_opt_double(const char *name, double def);
+
+/* ---- kent hash iteration order (kent/src/lib/hash.c) ----
+ * Tools whose output order follows a kent hash traversal (hashTraverseEls,
+ * hashElListHash) keep the same order by replaying the hash: hashString of
+ * the key text (:41-53), head insertion into bucket hashVal & mask
+ * (:115-141), doubling when elCount > size (defaultExpansionFactor 1.0) with
+ * the bucket lists re-reversed into insertion order (:424-470), default size
+ * 2^12 (:355-367).  Keys here are ints printed "%d" (chainCleaner's keys). */
+typedef struct gt_khash {
+    int pow;
+    uint32_t mask;
+    int32_t *head;  /* [1 << pow] first element of each bucket, -1 = empty */
+    int32_t *next;  /* per element */
+    uint32_t *hv;   /* per element: hashString of the key text */
+    int32_t *key;   /* per element */
+    int32_t n, cap;
+} gt_khash;
+void gt_khash_init(gt_khash *h, int pow); /* pow 0 = kent's default 12 */
+int32_t gt_khash_find(const gt_khash *h, int32_t key); /* element or -1 */
+int32_t gt_khash_add(gt_khash *h, int32_t key);        /* new element (no dedupe) */
+/* elements in hashTraverseEls order; returns the count */
+int32_t gt_khash_order(const gt_khash *h, int32_t *out);
+void gt_khash_free(gt_khash *h);
 
 /* ---- string table ---- */
 typedef struct gt_names {
@@ -68,6 +92,11 @@ void gt_chains_free(gt_chains *c);
 int gt_next_chain_id(void);
 /* chainWrite (chain.c:200-227) of chain i with the given score and id */
 void gt_write_chain(FILE *f, const gt_chains *c, int64_t i, double score, int32_t id);
+/* chainWrite of an explicit header and block list */
+void gt_write_chain_raw(FILE *f, double score, const char *tname, int32_t tsize, int32_t tstart,
+                        int32_t tend, const char *qname, int32_t qsize, int qminus,
+                        int32_t qstart, int32_t qend, int32_t id, const int32_t *bt,
+                        const int32_t *bq, const int32_t *bs, int64_t nb);
 
 /* ---- chrom.sizes ---- */
 typedef struct gt_sizes {

@@ -342,3 +342,222 @@ def c2_case(seed: int = 42, n_chains: int = 200_000, sizes_dir: Optional[str] = 
     qg = random_genome(mm, seed + 1, n_frac=0.005, n_mean=20_000)
     ca = make_chains(tg, "chr1", qg, SynthConfig(n_chains=n_chains, seed=seed))
     return tg, qg, ca
+
+
+# ---------------------------------------------------------------- chainCleaner loci
+def _mutate(rng, codes: np.ndarray, div: float) -> np.ndarray:
+    r = rng.random(len(codes))
+    q = codes.copy()
+    q = np.where(r < div * 2 / 3, q ^ 1, q)
+    q = np.where((r >= div * 2 / 3) & (r < div * 5 / 6), q ^ 2, q)
+    q = np.where((r >= div * 5 / 6) & (r < div), q ^ 3, q)
+    return q.astype(np.uint8)
+
+
+class _Chain:
+    def __init__(self, tname: str, qname: str, strand: int):
+        self.tname, self.qname, self.strand = tname, qname, strand
+        self.blocks: List[Tuple[int, int, int, float]] = []  # (t, q, size, div)
+
+    def add_run(self, rng, t: int, q: int, length: int, div: float, bmin=80, bmax=600,
+                gmax=40) -> Tuple[int, int]:
+        """Blocks covering about `length` target bases from (t, q) with small
+        gaps (one- or two-sided); returns the end (t, q)."""
+        end = t + length
+        while True:
+            size = int(rng.integers(bmin, bmax + 1))
+            if t + size >= end:
+                size = max(1, end - t)
+                self.blocks.append((t, q, size, div))
+                return t + size, q + size
+            self.blocks.append((t, q, size, div))
+            t += size
+            q += size
+            mode = int(rng.integers(0, 3))
+            g1, g2 = int(rng.integers(1, gmax + 1)), int(rng.integers(1, gmax + 1))
+            t += 0 if mode == 1 else g1
+            q += 0 if mode == 0 else g2
+            if t >= end - 10:
+                return t, q
+
+
+def cleaner_case(seed: int = 7, n_loci: int = 24):
+    """Planted chain-breaking alignments (chainCleaner).
+
+    Per locus a high-scoring chain P (the would-be breaking chain) has two
+    long anchors and, between them, 1-3 short "suspect" runs separated by
+    large gaps; a lower-scoring chain B aligns a different query region to
+    the target inside those gaps, so in the nets B is split by P's suspects
+    (1-3 breaks, adjacent pairs for -doPairs).  Suspect size/divergence and
+    B's piece sizes/divergence are drawn so that some suspects pass the
+    default thresholds and others fail one (LR ratio, broken-chain score,
+    gap size); extra chains sometimes sit between B's pieces (breaks that
+    stay broken by another higher-scoring chain), B is on either strand, and
+    unrelated noise chains (with exact score ties) fill the space between
+    loci.  Header scores are left 0: the caller rescores the chains with the
+    reference scoreChain, sorts them and assigns ids.
+    Returns (target Genome, query Genome, list of _Chain)."""
+    rng = np.random.default_rng(seed)
+    span = 56_000
+    tsizes = {"chrT1": (n_loci // 2 + 1) * span + 20_000,
+              "chrT2": (n_loci - n_loci // 2 + 1) * span + 20_000}
+    qsizes = {"chrQ1": sum(tsizes.values()) + 40_000, "chrQ2": n_loci * 36_000 + 20_000,
+              "chrQ3": n_loci * 30_000 + 20_000}
+    tg = random_genome(tsizes, seed, n_frac=0.0)
+    qg = random_genome(qsizes, seed + 1, n_frac=0.0)
+    chains: List[_Chain] = []
+    qcur = {"chrQ1": 1000, "chrQ2": 1000, "chrQ3": 1000}  # forward allocation cursors
+
+    def q_alloc(qname: str, length: int, strand: int) -> int:
+        """Allocate `length` forward bases; return the start in strand coords."""
+        f = qcur[qname]
+        qcur[qname] = f + length + int(rng.integers(200, 2000))
+        assert qcur[qname] < qsizes[qname], qname
+        return f if strand == 0 else qsizes[qname] - (f + length)
+
+    locus_t = {"chrT1": 5_000, "chrT2": 5_000}
+    for li in range(n_loci):
+        tname = "chrT1" if li % 2 == 0 else "chrT2"
+        x = locus_t[tname]
+        locus_t[tname] += span
+        # every 4th locus: two strong suspects around a tiny divergent middle
+        # piece of B -- both singles fail on that side, the pair can pass
+        pair_locus = li % 4 == 3
+        k = 2 if pair_locus else int(rng.choice([1, 1, 2, 2, 3]))
+        a_lo, a_hi = (8000, 10000) if pair_locus else (2500, 5000)
+        a_l, a_r = int(rng.integers(a_lo, a_hi)), int(rng.integers(a_lo, a_hi))
+        gaps = [int(rng.integers(6000, 11000)) for _ in range(k + 1)]
+        susp = [int(rng.choice([150, 250] if pair_locus else [20, 40, 80, 150, 300, 700]))
+                for _ in range(k)]
+        # ---- P on chrQ1 '+': anchors, gaps (two-sided), suspects
+        p = _Chain(tname, "chrQ1", 0)
+        total_t = a_l + sum(gaps) + sum(susp) + a_r
+        q0 = q_alloc("chrQ1", total_t + 600 * (k + 1), 0)
+        t, q = p.add_run(rng, x, q0, a_l, 0.04)
+        gap_iv, susp_iv = [], []
+        for j in range(k + 1):
+            g_t = gaps[j]
+            g_q = max(50, g_t + int(rng.integers(-400, 400)))
+            gap_iv.append((t, t + g_t))
+            t += g_t
+            q += g_q
+            if j < k:
+                sdiv = 0.05 if pair_locus else float(rng.choice([0.05, 0.15, 0.25, 0.35]))
+                s0 = t
+                t, q = p.add_run(rng, t, q, susp[j], sdiv, bmin=20, bmax=400, gmax=30)
+                susp_iv.append((s0, t))
+        t, q = p.add_run(rng, t, q, a_r, 0.04)
+        chains.append(p)
+        # ---- B: one piece per P gap, on chrQ2 either strand
+        strand = int(rng.integers(0, 2))
+        bdiv = 0.06 if pair_locus else float(rng.choice([0.06, 0.1, 0.14, 0.3]))
+        pieces = []
+        for (g0, g1) in gap_iv:
+            glen = g1 - g0
+            m1 = int(rng.integers(100, glen // 3))
+            m2 = int(rng.integers(100, glen // 3))
+            inner = 0 < len(pieces) < len(gap_iv) - 1
+            if pair_locus:
+                length = 120 if inner else min(2500, glen - m1 - m2 - 50)
+            else:
+                length = int(rng.choice([120, 200, 400] if inner and rng.random() < 0.5 else
+                                        [300, 800, 1500, 2500, glen - m1 - m2 - 50]))
+            length = max(100, min(length, glen - m1 - m2 - 50))
+            # the piece hugs the suspect side of the gap
+            pieces.append((g0 + m1, g0 + m1 + length) if len(pieces) == len(gap_iv) - 1
+                          else (g1 - m2 - length, g1 - m2))
+        # first piece sits at the right end of the first gap (next to the
+        # suspect), the last at the left end of the last gap
+        qlen = sum(b - a for a, b in pieces) + 400 * len(pieces) + 5000
+        bq = q_alloc("chrQ2", qlen, strand)
+        b = _Chain(tname, "chrQ2", strand)
+        qb = bq
+        for pi, (a0, a1) in enumerate(pieces):
+            tiny = pair_locus and 0 < pi < len(pieces) - 1
+            _, qb = b.add_run(rng, a0, qb, a1 - a0, 0.3 if tiny else bdiv)
+            qb += int(rng.integers(5, 300))
+        chains.append(b)
+        # ---- sometimes a third chain inside a gap, next to one of B's pieces
+        if rng.random() < 0.3:
+            j = int(rng.integers(0, len(gap_iv)))
+            g0, g1 = gap_iv[j]
+            a0, a1 = pieces[j]
+            lo, hi = (g0 + 20, a0 - 20) if a0 - g0 > g1 - a1 else (a1 + 20, g1 - 20)
+            if hi - lo > 200:
+                c = _Chain(tname, "chrQ3", int(rng.integers(0, 2)))
+                clen = int(rng.integers(150, hi - lo))
+                c0 = int(rng.integers(lo, hi - clen + 1))
+                cq = q_alloc("chrQ3", clen + 200, c.strand)
+                c.add_run(rng, c0, cq, clen, float(rng.choice([0.02, 0.1, 0.2])))
+                chains.append(c)
+        # ---- noise chains in the spacer after the locus
+        t_sp = x + total_t + 200
+        n_noise = 0
+        while t_sp + 900 < x + span - 200 and n_noise < 10:
+            n_noise += 1
+            n_len = int(rng.integers(60, 700))
+            c = _Chain(tname, "chrQ3", int(rng.integers(0, 2)))
+            cq = q_alloc("chrQ3", n_len + 100, c.strand)
+            c.add_run(rng, t_sp, cq, n_len, float(rng.choice([0.0, 0.1, 0.3])), bmin=30,
+                      bmax=300)
+            chains.append(c)
+            t_sp += n_len + int(rng.integers(50, 800))
+    # ---- plant homology
+    for c in chains:
+        ti, qi = tg.index(c.tname), qg.index(c.qname)
+        qcodes = qg.codes[qi]
+        qsize = len(qcodes)
+        for (t, q, size, div) in c.blocks:
+            m = _mutate(rng, tg.codes[ti][t:t + size], div)
+            if c.strand == 0:
+                qcodes[q:q + size] = m
+            else:
+                f0 = qsize - (q + size)
+                qcodes[f0:f0 + size] = (m ^ 2)[::-1]
+    # ---- exact score ties: duplicate a few noise chains' target and query text
+    noise = [c for c in chains if c.qname == "chrQ3" and len(c.blocks) == 1 and c.blocks[0][3] == 0.0]
+    for a, b2 in zip(noise[0::2], noise[1::2]):
+        (ta, qa, sa, _), (tb, qb, sb, _) = a.blocks[0], b2.blocks[0]
+        s = min(sa, sb)
+        a.blocks[0] = (ta, qa, s, 0.0)
+        b2.blocks[0] = (tb, qb, s, 0.0)
+        ti = tg.index(a.tname)
+        tg.codes[tg.index(b2.tname)][tb:tb + s] = tg.codes[ti][ta:ta + s]
+        for c in (a, b2):
+            t, q, size, _ = c.blocks[0]
+            qcodes = qg.codes[qg.index(c.qname)]
+            m = tg.codes[tg.index(c.tname)][t:t + size]
+            if c.strand == 0:
+                qcodes[q:q + size] = m
+            else:
+                f0 = len(qcodes) - (q + size)
+                qcodes[f0:f0 + size] = (m ^ 2)[::-1]
+    return tg, qg, chains
+
+
+def chains_to_arrays(tg: Genome, qg: Genome, chains) -> ChainArrays:
+    """_Chain list -> ChainArrays (score 0, ids 1..n in list order)."""
+    n = len(chains)
+    offs = [0]
+    bt, bq, bs = [], [], []
+    ts, te, qs, qe = [], [], [], []
+    for c in chains:
+        for (t, q, s, _) in c.blocks:
+            bt.append(t)
+            bq.append(q)
+            bs.append(s)
+        offs.append(len(bs))
+        ts.append(c.blocks[0][0])
+        qs.append(c.blocks[0][1])
+        te.append(c.blocks[-1][0] + c.blocks[-1][2])
+        qe.append(c.blocks[-1][1] + c.blocks[-1][2])
+    tsz, qsz = tg.sizes, qg.sizes
+    return ChainArrays(
+        score=np.zeros(n), tname=[c.tname for c in chains],
+        tsize=np.array([tsz[c.tname] for c in chains], np.int32),
+        tstart=np.array(ts, np.int32), tend=np.array(te, np.int32),
+        qname=[c.qname for c in chains], qsize=np.array([qsz[c.qname] for c in chains], np.int32),
+        qstrand=np.array([c.strand for c in chains], np.uint8), qstart=np.array(qs, np.int32),
+        qend=np.array(qe, np.int32), id=np.arange(1, n + 1, dtype=np.int64),
+        blk_off=np.array(offs, np.int64), blk_t=np.array(bt, np.int32),
+        blk_q=np.array(bq, np.int32), blk_size=np.array(bs, np.int32))

@@ -105,3 +105,45 @@ def test_scorechain_c1_example(tmp_path):
             cmd.append(flag)
         _run(cmd)
         assert filecmp.cmp(tmp_path / mode, os.path.join(d, f"c1.{mode}.out"), shallow=False)
+
+
+# ---------------------------------------------------------------- chainCleaner
+def _cleaner_cases():
+    with open(os.path.join(GOLDEN, "cleaner", "cases.json")) as f:
+        return json.load(f)
+
+
+def _cleaner_outputs(opts):
+    files = ["out.chain", "out.bed"]
+    for o in opts:
+        if o.startswith("-newChainIDDict=") or o.startswith("-suspectDataFile="):
+            files.append(o.split("=", 1)[1])
+    if "-debug" in opts:
+        files += _cleaner_cases()["debug_files"]
+    return files
+
+
+def _run_cleaner(case, tmp_path, net):
+    d = os.path.join(GOLDEN, "cleaner")
+    opts = _cleaner_cases()["cases"][case]
+    p = lambda x: os.path.join(d, x)
+    cmd = [_bin("chainCleaner"), p("in.chain"), p("t.2bit"), p("q.2bit"), "out.chain", "out.bed"]
+    cmd += [f"-net={p('in.net')}"] if net else [f"-tSizes={p('t.sizes')}", f"-qSizes={p('q.sizes')}"]
+    r = subprocess.run(cmd + opts, capture_output=True, text=True, timeout=600, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr
+    for f in _cleaner_outputs(opts):
+        assert filecmp.cmp(tmp_path / f, os.path.join(d, case, f), shallow=False), (case, f)
+
+
+@pytest.mark.parametrize("case", ["default", "pairs", "lowfold", "filters", "sdata", "debug"])
+def test_chaincleaner_net(case, tmp_path):
+    """chainCleaner -net=in.net: every output byte-identical to the reference."""
+    _run_cleaner(case, tmp_path, net=True)
+
+
+@pytest.mark.parametrize("case", ["default", "lowfold"])
+def test_chaincleaner_nonet(case, tmp_path):
+    """Without -net the tool nets in-process (chainNet -minScore=0 |
+    NetFilterNonNested.perl -minScore1 3000); same outputs as the reference
+    run on that pipeline's net."""
+    _run_cleaner(case, tmp_path, net=False)

@@ -118,6 +118,32 @@ def test_tool_errors(tmp_path):
     assert r.returncode == 255 and "-tNibDir" in r.stderr
 
 
+def test_chaincleaner_errors(tmp_path):
+    """chainCleaner argument checks (errAbort, exit 255) -- all before any
+    device work."""
+    from genomealignmenttools_amd._lib import BIN_DIR
+    cc = os.path.join(BIN_DIR, "chainCleaner")
+    d = os.path.join(GOLDEN, "cleaner")
+    p = lambda x: os.path.join(d, x)
+    r = subprocess.run([cc], capture_output=True, text=True)
+    assert r.returncode == 255 and "usage" in r.stderr and "-LRfoldThreshold" in r.stderr
+    args = [p("in.chain"), p("t.2bit"), p("q.2bit"), str(tmp_path / "o.chain"),
+            str(tmp_path / "o.bed")]
+    r = subprocess.run([cc] + args + [f"-net={p('in.net')}"], capture_output=True, text=True)
+    assert r.returncode == 255 and "Must specify linear gap costs" in r.stderr
+    r = subprocess.run([cc] + args + ["-linearGap=loose"], capture_output=True, text=True)
+    assert r.returncode == 255 and "You must specifiy -tSizes" in r.stderr
+    r = subprocess.run([cc] + args + ["-linearGap=loose", f"-tSizes={p('t.sizes')}"],
+                       capture_output=True, text=True)
+    assert r.returncode == 255 and "You must specifiy -qSizes" in r.stderr
+    r = subprocess.run([cc] + args + ["-linearGap=loose", "-LRfoldThreshold=x"],
+                       capture_output=True, text=True)
+    assert r.returncode == 255
+    r = subprocess.run([cc, p("in.chain"), "/nonexistent.2bit", p("q.2bit"), "a", "b",
+                        "-linearGap=loose"], capture_output=True, text=True)
+    assert r.returncode == 255 and "does not exist" in r.stderr
+
+
 def test_no_cpu_fallback_without_gpu():
     """On a box without a usable gfx950 device every scoring entry point must
     fail loudly (there is no CPU path to fall back to)."""
