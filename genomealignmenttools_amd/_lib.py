@@ -89,6 +89,21 @@ class NetOpts(C.Structure):
                 ("incl_hap", C.c_int32)]
 
 
+class AxtInput(C.Structure):
+    _fields_ = [("n_pairs", C.c_int64), ("t_seq", C.c_void_p), ("q_seq", C.c_void_p),
+                ("q_strand", C.c_void_p), ("blk_off", C.c_void_p), ("blk_t", C.c_void_p),
+                ("blk_q", C.c_void_p), ("blk_size", C.c_void_p)]
+
+
+class AxtChains(C.Structure):
+    _fields_ = [("n_chains", C.c_int64), ("score", C.POINTER(C.c_double)),
+                ("pair", C.POINTER(C.c_int32)), ("t_start", C.POINTER(C.c_int32)),
+                ("t_end", C.POINTER(C.c_int32)), ("q_start", C.POINTER(C.c_int32)),
+                ("q_end", C.POINTER(C.c_int32)), ("blk_off", C.POINTER(C.c_int64)),
+                ("n_blocks", C.c_int64), ("blk_t", C.POINTER(C.c_int32)),
+                ("blk_q", C.POINTER(C.c_int32)), ("blk_size", C.POINTER(C.c_int32))]
+
+
 # name -> (restype, argtypes)
 _PROTOS = {
     "gac_abi_version": (C.c_int, []),
@@ -103,6 +118,7 @@ _PROTOS = {
         [C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
          C.POINTER(C.c_void_p)],
     ),
+    "gac_gap_cost": (C.c_int, [C.POINTER(GapCalc), C.c_int, C.c_int]),
     "gac_set_scoring": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(GapCalc)]),
     "gac_genome_load_2bit": (C.c_int, [C.c_void_p, C.c_int, C.c_char_p]),
     "gac_genome_add_seq": (
@@ -130,6 +146,17 @@ _PROTOS = {
         [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_uint32, C.c_void_p, C.c_void_p,
          C.c_void_p, C.c_void_p],
     ),
+    "gac_score_blocks": (
+        C.c_int,
+        [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+         C.c_void_p, C.c_void_p, C.c_void_p],
+    ),
+    "gac_axt_chain": (
+        C.c_int,
+        [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(GapCalc), C.POINTER(AxtInput), C.c_double,
+         C.c_int, C.c_char_p, C.POINTER(C.POINTER(AxtChains))],
+    ),
+    "gac_axt_chains_free": (None, [C.POINTER(AxtChains)]),
     "gac_net_build": (C.c_int, [C.POINTER(NetInput), C.POINTER(NetOpts), C.POINTER(C.c_void_p)]),
     "gac_net_free": (None, [C.c_void_p]),
     "gac_net_netted": (C.c_int64, [C.c_void_p]),

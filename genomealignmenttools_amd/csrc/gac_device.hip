@@ -47,6 +47,8 @@ hipError_t launch_nflags(const DChain *chains, int64_t n_chains, int4 *blk,
                          const uint32_t *t_nmask, const int64_t *t_woff, const uint32_t *q_nmask,
                          const int64_t *q_woff, hipStream_t s);
 hipError_t launch_nruns(const NPiece *p, int64_t n, uint32_t *nmask, hipStream_t s);
+hipError_t launch_blocks(const ScoreArgs &a, const BlockJob *jobs, int64_t n, int32_t *out,
+                         hipStream_t s);
 }  // namespace gac
 
 using namespace gac;
@@ -70,6 +72,10 @@ struct Genome {
     std::vector<int64_t> raw_off;   // per seq
     std::vector<NPiece> npieces;    // bit0 relative to the seq start until finalize
     std::vector<int32_t> npiece_seq;
+    // host copy kept after finalize (raw stays): merged, sorted N runs per
+    // sequence, CSR by nrun_off -- host-side base access (gac_genome_view)
+    std::vector<int64_t> nrun_off{0};
+    std::vector<int32_t> nrun_start, nrun_size;
     // device
     bool final = false;
     std::vector<int64_t> woff;      // host copy of word offsets
@@ -321,6 +327,24 @@ extern "C" int gac_genome_add_seq(gac_ctx *c, int side, const char *name, int32_
     g->raw.resize(off + nbytes);
     if (nbytes) memcpy(g->raw.data() + off, packed, nbytes);
     g->raw_off.push_back((int64_t)off);
+    {
+        std::vector<std::pair<int32_t, int32_t>> runs;
+        for (int32_t i = 0; i < n_nblocks; ++i)
+            if (n_sizes[i] > 0) runs.emplace_back(n_starts[i], n_starts[i] + n_sizes[i]);
+        std::sort(runs.begin(), runs.end());
+        size_t k0 = g->nrun_start.size();
+        for (const auto &r : runs) {
+            const size_t k = g->nrun_start.size();
+            if (k > k0 && r.first <= g->nrun_start[k - 1] + g->nrun_size[k - 1]) {
+                const int32_t e = std::max(g->nrun_start[k - 1] + g->nrun_size[k - 1], r.second);
+                g->nrun_size[k - 1] = e - g->nrun_start[k - 1];
+            } else {
+                g->nrun_start.push_back(r.first);
+                g->nrun_size.push_back(r.second - r.first);
+            }
+        }
+        g->nrun_off.push_back((int64_t)g->nrun_start.size());
+    }
     for (int32_t i = 0; i < n_nblocks; ++i) {
         int64_t s = n_starts[i], len = n_sizes[i];
         if (s < 0 || len < 0 || s + len > size)
@@ -390,7 +414,6 @@ extern "C" int gac_genome_finalize(gac_ctx *c, int side) {
     } else {
         HIPCHK(hipStreamSynchronize(c->stream));
     }
-    std::vector<uint8_t>().swap(g->raw);
     std::vector<NPiece>().swap(g->npieces);
     std::vector<int32_t>().swap(g->npiece_seq);
     g->final = true;
@@ -469,6 +492,76 @@ extern "C" int gac_genome_decode(gac_ctx *c, int side, int32_t i, int32_t start,
             out[p - start] = nt[code];
         }
     }
+    return GAC_OK;
+}
+
+extern "C" int gac_genome_view(gac_ctx *c, int side, int32_t i, gac_seq_view *v) {
+    Genome *g = side_of(c, side);
+    if (!g || !g->final || i < 0 || i >= (int32_t)g->sizes.size() || !v)
+        return gac_fail(GAC_E_ARG, "gac_genome_view: bad argument");
+    v->packed = g->raw.data() + g->raw_off[i];
+    v->size = g->sizes[i];
+    v->n_start = g->nrun_start.data() + g->nrun_off[i];
+    v->n_size = g->nrun_size.data() + g->nrun_off[i];
+    v->n_count = (int32_t)(g->nrun_off[i + 1] - g->nrun_off[i]);
+    return GAC_OK;
+}
+
+extern "C" int gac_score_blocks(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq,
+                                const int32_t *q_seq, const uint8_t *q_strand,
+                                const int64_t *blk_off, const int32_t *blk_t,
+                                const int32_t *blk_q, const int32_t *blk_size, int32_t *score) {
+    gac_clear_error();
+    if (!c || n_pairs < 0 || (n_pairs && (!t_seq || !q_seq || !q_strand || !blk_off)))
+        return gac_fail(GAC_E_ARG, "gac_score_blocks: bad argument");
+    if (!c->scoring) return gac_fail(GAC_E_STATE, "gac_score_blocks before gac_set_scoring");
+    if (!c->g[0].final || !c->g[1].final)
+        return gac_fail(GAC_E_STATE, "load both genomes before scoring blocks");
+    const int64_t n = n_pairs ? blk_off[n_pairs] : 0;
+    if (n == 0) return GAC_OK;
+    if (!blk_t || !blk_q || !blk_size || !score)
+        return gac_fail(GAC_E_ARG, "gac_score_blocks: NULL block array");
+    std::vector<BlockJob> jobs(n);
+    const Genome &T = c->g[0], &Q = c->g[1];
+    for (int64_t p = 0; p < n_pairs; ++p) {
+        const int32_t ts = t_seq[p], qs = q_seq[p];
+        if (ts < 0 || ts >= (int32_t)T.sizes.size() || qs < 0 || qs >= (int32_t)Q.sizes.size())
+            return gac_fail(GAC_E_ARG, "gac_score_blocks: pair %lld: bad sequence index",
+                            (long long)p);
+        const int64_t tw = T.woff[ts] * 32, qw = Q.woff[qs] * 32;
+        const int32_t tsize = T.sizes[ts], qsize = Q.sizes[qs];
+        for (int64_t b = blk_off[p]; b < blk_off[p + 1]; ++b) {
+            const int32_t bt = blk_t[b], bq = blk_q[b], sz = blk_size[b];
+            if (bt < 0 || bq < 0 || sz < 0 || (int64_t)bt + sz > tsize || (int64_t)bq + sz > qsize)
+                return gac_fail(GAC_E_ARG, "block %lld (%d %d %d) outside %s/%s", (long long)b,
+                                bt, bq, sz, T.names[ts].c_str(), Q.names[qs].c_str());
+            BlockJob &j = jobs[b];
+            j.tp = tw + bt;
+            j.minus = q_strand[p] ? 1 : 0;
+            j.qp = j.minus ? qw + (qsize - bq) : qw + bq;
+            j.n = sz;
+        }
+    }
+    HIPCHK(hipSetDevice(c->device));
+    BlockJob *d_jobs = nullptr;
+    int32_t *d_out = nullptr;
+    HIPCHK(hipMalloc((void **)&d_jobs, n * sizeof(BlockJob)));
+    HIPCHK(hipMalloc((void **)&d_out, n * sizeof(int32_t)));
+    HIPCHK(hipMemcpyAsync(d_jobs, jobs.data(), n * sizeof(BlockJob), hipMemcpyHostToDevice,
+                          c->stream));
+    ScoreArgs a;
+    memset(&a, 0, sizeof(a));
+    a.t_planes = T.planes;
+    a.t_nmask = T.nmask;
+    a.q_planes = Q.planes;
+    a.q_nmask = Q.nmask;
+    memcpy(a.coef, c->coef, sizeof(a.coef));
+    a.sym = c->sym;
+    HIPCHK(launch_blocks(a, d_jobs, n, d_out, c->stream));
+    HIPCHK(hipMemcpyAsync(score, d_out, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    hipFree(d_jobs);
+    hipFree(d_out);
     return GAC_OK;
 }
 

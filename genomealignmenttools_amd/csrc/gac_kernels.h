@@ -136,4 +136,13 @@ struct ScoreArgs {
     GapDev gap;
 };
 
+// One ungapped block for k_blocks (axtScoreUngapped): global plane positions
+// of its first target base and, for the query, of its first base ('+') or
+// one past its last base on the forward strand ('-').
+struct BlockJob {
+    int64_t tp, qp;
+    int32_t n;
+    int32_t minus;
+};
+
 }  // namespace gac

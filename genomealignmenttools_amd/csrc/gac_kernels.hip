@@ -1032,6 +1032,48 @@ hipError_t launch_relayout(const uint8_t *raw, const SeqDev *seqs, int nseq, int
     return hipGetLastError();
 }
 
+// axtScoreUngapped (kent/src/lib/axt.c:186-194) for a batch of ungapped
+// blocks -- axtChain's per-block scores (chainPair, axtChain.c:276-282).  One
+// lane per block, 32 bases per step through the same plane windows and
+// multilinear matrix basis as k_tile; N positions are subtracted with the N
+// masks (matrix entries of N are 0).
+__global__ void __launch_bounds__(256) k_blocks(ScoreArgs a, const BlockJob *jobs, int64_t n,
+                                                int32_t *out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const BlockJob j = jobs[i];
+    int sc = 0;
+    for (int off = 0; off < j.n; off += 32) {
+        const int m = min(32, j.n - off);
+        const int64_t tp = j.tp + off;
+        const int64_t qp = j.minus ? j.qp - off - m : j.qp + off;
+        uint32_t t0, t1, q0, q1;
+        load_planes(a.t_planes, tp, t0, t1);
+        load_planes(a.q_planes, qp, q0, q1);
+        uint32_t qn = load_nmask(a.q_nmask, qp);
+        if (j.minus) {
+            const int sh = 32 - m;
+            q0 = __builtin_bitreverse32(q0) >> sh;
+            q1 = ~(__builtin_bitreverse32(q1) >> sh);
+            qn = __builtin_bitreverse32(qn) >> sh;
+        }
+        const uint32_t v = m >= 32 ? 0xffffffffu : ((1u << m) - 1u);
+        const uint32_t d0 = q0 ^ t0, d1 = q1 ^ t1;
+        sc += score_bits<false>(a, v, t0, t1, d0, d1);
+        const uint32_t nm = (load_nmask(a.t_nmask, tp) | qn) & v;
+        if (nm) sc -= score_bits<false>(a, nm, t0, t1, d0, d1);
+    }
+    out[i] = sc;
+}
+
+hipError_t launch_blocks(const ScoreArgs &a, const BlockJob *jobs, int64_t n, int32_t *out,
+                         hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const int64_t nb = (n + 255) / 256;
+    hipLaunchKernelGGL(k_blocks, dim3((unsigned)nb), dim3(256), 0, s, a, jobs, n, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_nruns(const NPiece *p, int64_t n, uint32_t *nmask, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const int64_t nb = (n + 255) / 256;

@@ -1,0 +1,1042 @@
+/* gac_axtchain.c -- axtChain's chaining (gac_axt_chain, include/gachain.h).
+ *
+ * The reference chains the blocks of one (query, strand, target) pair at a
+ * time, single-threaded (kent/src/hg/mouseStuff/axtChain/axtChain.c:250-309,
+ * 452-470; kent/src/lib/chainBlock.c; kent/src/lib/chainConnect.c).  Here:
+ *   1. removeExactOverlaps for every pair (host);
+ *   2. every block's axtScoreUngapped in ONE GPU batch (gac_score_blocks);
+ *   3. the kd-tree DP of chainBlocks per pair on host threads -- pairs are
+ *      independent, so they run concurrently, largest first;
+ *   4. chainRemovePartialOverlaps + chainMergeAbutting per chain (host);
+ *   5. every chain's chainCalcScore in ONE GPU batch (gac_score_ranges over
+ *      whole chains);
+ *   6. minScore filter and the final stable score sort.
+ *
+ * Step 3 is a sequential dynamic programme: each leaf's best predecessor is
+ * a branch-and-bound DFS of the kd-tree whose bounds depend on every leaf
+ * before it, and whose pruning order decides ties (first in DFS order wins)
+ * and -- because the overlap-adjusted connect cost can fall below the
+ * gapCost bound -- even which predecessor is found.  Bit-exact output needs
+ * that exact search, so the tree, the split rules, the visiting order, the
+ * strict/non-strict comparisons and the double arithmetic all follow
+ * chainBlock.c line by line (the sums are integral, so double is exact). */
+#define _GNU_SOURCE
+#include <pthread.h>
+#include <stdarg.h>
+#include <stdatomic.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include "gac_host.h"
+#include "gachain.h"
+
+/* ------------------------------------------------------------------ env */
+typedef struct ax_env {
+    const gac_gapcalc *g;
+    int32_t m5[25];    /* [q code * 5 + t code], codes T C A G = 0..3, N = 4 */
+    int32_t *gtab;     /* [3][gtab_len] gapCalcCost by kind and distance */
+    int gtab_len;
+} ax_env;
+
+/* chainConnectGapCost = gapCalcCost (chainConnect.c:108-112) */
+static inline int gap_cost(const ax_env *e, int dq, int dt) {
+    if (dt < 0)
+        dt = 0;
+    if (dq < 0)
+        dq = 0;
+    int kind, d;
+    if (dt == 0) {
+        kind = 0;
+        d = dq;
+    } else if (dq == 0) {
+        kind = 1;
+        d = dt;
+    } else {
+        kind = 2;
+        d = dq + dt;
+    }
+    if (d >= 0 && d < e->gtab_len)
+        return e->gtab[kind * e->gtab_len + d];
+    return gac_gap_cost(e->g, dq, dt);
+}
+
+/* ------------------------------------------------------------------ sequences */
+typedef struct ax_seq {
+    gac_seq_view v;
+    int minus; /* query on '-': coordinates on the reverse complement */
+} ax_seq;
+
+/* codes of strand positions [start, start + len) (N = 4) */
+static void seq_codes(const ax_seq *s, int32_t start, int32_t len, uint8_t *out) {
+    const int32_t size = s->v.size;
+    for (int32_t i = 0; i < len; ++i) {
+        const int32_t f = s->minus ? size - 1 - (start + i) : start + i;
+        const int c = (s->v.packed[f >> 2] >> (6 - 2 * (f & 3))) & 3;
+        out[i] = (uint8_t)(s->minus ? c ^ 2 : c);
+    }
+    if (s->v.n_count == 0 || len <= 0)
+        return;
+    const int32_t flo = s->minus ? size - (start + len) : start, fhi = flo + len;
+    int32_t lo = 0, hi = s->v.n_count; /* first run ending after flo */
+    while (lo < hi) {
+        const int32_t mid = (lo + hi) / 2;
+        if (s->v.n_start[mid] + s->v.n_size[mid] > flo)
+            hi = mid;
+        else
+            lo = mid + 1;
+    }
+    for (int32_t k = lo; k < s->v.n_count && s->v.n_start[k] < fhi; ++k) {
+        const int32_t a = s->v.n_start[k] > flo ? s->v.n_start[k] : flo;
+        const int32_t b = s->v.n_start[k] + s->v.n_size[k] < fhi ? s->v.n_start[k] + s->v.n_size[k]
+                                                                  : fhi;
+        for (int32_t f = a; f < b; ++f)
+            out[s->minus ? (size - 1 - f) - start : f - start] = 4;
+    }
+}
+
+/* ------------------------------------------------------------------ per-thread work */
+typedef struct ax_node { /* struct kdBranch (chainBlock.c:17-28) */
+    int32_t lo, hi, leaf, cut;
+    double max_score;
+    int32_t max_q, max_t;
+} ax_node;
+
+typedef struct ax_out { /* one pair's result */
+    int32_t n_chains;
+    int32_t *coff;           /* [n_chains + 1] */
+    int32_t *bt, *bq, *bs;   /* blocks after overlap removal + merge */
+    char *details;
+    size_t details_len;
+    int err;
+    char msg[512];
+} ax_out;
+
+typedef struct ax_work {
+    const ax_env *e;
+    ax_seq q, t;
+    /* the pair's blocks (after removeExactOverlaps) */
+    int32_t n;
+    const int32_t *qs, *qe, *ts, *te, *score;
+    /* leaves (indexed by block) */
+    double *total;
+    int32_t *pred; /* best predecessor: node index or -1 */
+    uint8_t *hit;
+    int32_t *tord, *qord, *tmp;
+    int32_t nl;
+    ax_node *nodes;
+    int32_t nn;
+    /* crossover scratch */
+    uint8_t *xs;
+    int32_t xcap;
+    /* error */
+    int err;
+    char msg[512];
+    size_t cap_n;
+} ax_work;
+
+static void w_fail(ax_work *w, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+static void w_fail(ax_work *w, const char *fmt, ...) {
+    if (w->err)
+        return;
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(w->msg, sizeof(w->msg), fmt, ap);
+    va_end(ap);
+    w->err = 1;
+}
+
+/* cBlockFindCrossover (chainConnect.c:61-105) on blocks (qs,qe,ts,te) */
+static void crossover(ax_work *w, int32_t lqs, int32_t lqe, int32_t lts, int32_t lte,
+                      int32_t rqs, int32_t rqe, int32_t rts, int32_t rte, int overlap,
+                      int *ret_pos, int *ret_adj) {
+    (void)lqs;
+    (void)rqe;
+    if (overlap > (lte - lts) || overlap > (rte - rts)) {
+        w_fail(w, "overlap is %d -- too large for one of these:\nqSize=%d  tSize=%d\n", overlap,
+               w->q.v.size, w->t.v.size);
+        *ret_pos = 0;
+        *ret_adj = 0;
+        return;
+    }
+    if (4 * overlap > w->xcap) {
+        w->xcap = 4 * overlap + 1024;
+        w->xs = realloc(w->xs, (size_t)w->xcap);
+    }
+    uint8_t *rq = w->xs, *lq = rq + overlap, *rt = lq + overlap, *lt = rt + overlap;
+    seq_codes(&w->q, rqs, overlap, rq);
+    seq_codes(&w->q, lqe - overlap, overlap, lq);
+    seq_codes(&w->t, rts, overlap, rt);
+    seq_codes(&w->t, lte - overlap, overlap, lt);
+    const int32_t *m = w->e->m5;
+    int64_t r_score = 0, l_score = 0;
+    for (int i = 0; i < overlap; ++i) {
+        r_score += m[rq[i] * 5 + rt[i]];
+        l_score += m[lq[i] * 5 + lt[i]];
+    }
+    int64_t score = r_score, best = r_score;
+    int best_pos = 0;
+    for (int i = 0; i < overlap; ++i) {
+        score += m[lq[i] * 5 + lt[i]];
+        score -= m[rq[i] * 5 + rt[i]];
+        if (score > best) {
+            best = score;
+            best_pos = i + 1;
+        }
+    }
+    *ret_pos = best_pos;
+    *ret_adj = (int)(r_score + l_score - best);
+}
+
+/* chainConnectCost (chainConnect.c:114-149) of block a then block b */
+static int connect_cost(ax_work *w, int32_t a, int32_t b) {
+    int dq = w->qs[b] - w->qe[a];
+    int dt = w->ts[b] - w->te[a];
+    int adj = 0;
+    if (w->qs[a] >= w->qs[b] || w->ts[a] >= w->ts[b]) {
+        w_fail(w, "a (%d %d) not strictly before b (%d %d)", w->qs[a], w->ts[a], w->qs[b],
+               w->ts[b]);
+        return 0;
+    }
+    if (dq < 0 || dt < 0) {
+        const int b_size = w->qe[b] - w->qs[b];
+        const int a_size = w->qe[a] - w->qs[a];
+        const int overlap = -(dq < dt ? dq : dt);
+        if (overlap >= b_size || overlap >= a_size) {
+            adj = 100000000;
+        } else {
+            int cross;
+            crossover(w, w->qs[a], w->qe[a], w->ts[a], w->te[a], w->qs[b], w->qe[b], w->ts[b],
+                      w->te[b], overlap, &cross, &adj);
+            dq += overlap;
+            dt += overlap;
+        }
+    }
+    return adj + gap_cost(w->e, dq, dt);
+}
+
+/* stable partition of a[0..n) into hit-first order (splitList, chainBlock.c:92-110) */
+static void partition(int32_t *a, int32_t n, const uint8_t *hit, int32_t *tmp) {
+    int32_t k = 0;
+    for (int32_t i = 0; i < n; ++i)
+        if (hit[a[i]])
+            tmp[k++] = a[i];
+    for (int32_t i = 0; i < n; ++i)
+        if (!hit[a[i]])
+            tmp[k++] = a[i];
+    memcpy(a, tmp, (size_t)n * sizeof(int32_t));
+}
+
+/* kdBuild (chainBlock.c:124-164): Q in query order, T in target order */
+static int32_t kd_build(ax_work *w, int32_t *Q, int32_t *T, int32_t n, int dim) {
+    const int32_t id = w->nn++;
+    if (n == 1) {
+        const int32_t l = Q[0];
+        w->nodes[id] = (ax_node){-1, -1, l, 0, 0.0, w->qe[l], w->te[l]};
+        return id;
+    }
+    const int32_t half = n / 2;
+    for (int32_t i = 0; i < n; ++i) /* clearHits(lists[0]) */
+        w->hit[Q[i]] = 0;
+    const int32_t *D = dim == 0 ? Q : T; /* medianVal: first n/2 marked */
+    for (int32_t i = 0; i < half; ++i)
+        w->hit[D[i]] = 1;
+    const int32_t ml = D[half - 1];
+    const int32_t cut = dim == 0 ? w->qs[ml] : w->ts[ml];
+    partition(Q, n, w->hit, w->tmp);
+    partition(T, n, w->hit, w->tmp);
+    const int32_t lo = kd_build(w, Q, T, half, 1 - dim);
+    const int32_t hi = kd_build(w, Q + half, T + half, n - half, 1 - dim);
+    ax_node *nd = &w->nodes[id];
+    nd->lo = lo;
+    nd->hi = hi;
+    nd->leaf = -1;
+    nd->cut = cut;
+    nd->max_score = 0.0;
+    nd->max_q = w->nodes[lo].max_q > w->nodes[hi].max_q ? w->nodes[lo].max_q : w->nodes[hi].max_q;
+    nd->max_t = w->nodes[lo].max_t > w->nodes[hi].max_t ? w->nodes[lo].max_t : w->nodes[hi].max_t;
+    return id;
+}
+
+enum { kStack = 512 };
+
+/* bestPredecessor (chainBlock.c:207-263), iterative with the same order:
+ * the hi subtree (only when the lonely leaf lies past the cut) before lo */
+static void best_predecessor(ax_work *w, int32_t lonely, double *ret_score, int32_t *ret_pred) {
+    const int32_t lq = w->qs[lonely], lt = w->ts[lonely];
+    const double lscore = w->score[lonely];
+    double best = 0.0;
+    int32_t best_node = -1;
+    int32_t st_node[kStack];
+    uint8_t st_dim[kStack];
+    int sp = 0;
+    st_node[sp] = 0;
+    st_dim[sp++] = 0;
+    while (sp > 0) {
+        --sp;
+        const int32_t b = st_node[sp];
+        const int dim = st_dim[sp];
+        const ax_node *nd = &w->nodes[b];
+        double max_score = nd->max_score + lscore;
+        if (max_score < best)
+            continue;
+        max_score -= gap_cost(w->e, lq - nd->max_q, lt - nd->max_t);
+        if (max_score < best)
+            continue;
+        if (nd->leaf >= 0) {
+            const int32_t l = nd->leaf;
+            if (w->qs[l] < lq && w->ts[l] < lt) {
+                const double s = w->total[l] + lscore - connect_cost(w, l, lonely);
+                if (s > best) {
+                    best = s;
+                    best_node = b;
+                }
+            }
+            continue;
+        }
+        if (sp + 2 > kStack) {
+            w_fail(w, "kd-tree deeper than %d", kStack / 2);
+            break;
+        }
+        const int32_t coord = dim == 0 ? lq : lt;
+        st_node[sp] = nd->lo;
+        st_dim[sp++] = (uint8_t)(1 - dim);
+        if (coord > nd->cut) {
+            st_node[sp] = nd->hi;
+            st_dim[sp++] = (uint8_t)(1 - dim);
+        }
+    }
+    *ret_score = best;
+    *ret_pred = best_node;
+}
+
+/* updateScoresOnWay (chainBlock.c:265-279): both sides on a tie with the cut */
+static void update_scores(ax_work *w, int32_t leaf) {
+    const double total = w->total[leaf];
+    const int32_t lq = w->qs[leaf], lt = w->ts[leaf];
+    int32_t st_node[kStack];
+    uint8_t st_dim[kStack];
+    int sp = 0;
+    st_node[sp] = 0;
+    st_dim[sp++] = 0;
+    while (sp > 0) {
+        --sp;
+        const int32_t b = st_node[sp];
+        const int dim = st_dim[sp];
+        ax_node *nd = &w->nodes[b];
+        if (nd->max_score < total)
+            nd->max_score = total;
+        if (nd->leaf < 0) {
+            if (sp + 2 > kStack) {
+                w_fail(w, "kd-tree deeper than %d", kStack / 2);
+                return;
+            }
+            const int32_t coord = dim == 0 ? lq : lt;
+            if (coord <= nd->cut) {
+                st_node[sp] = nd->lo;
+                st_dim[sp++] = (uint8_t)(1 - dim);
+            }
+            if (coord >= nd->cut) {
+                st_node[sp] = nd->hi;
+                st_dim[sp++] = (uint8_t)(1 - dim);
+            }
+        }
+    }
+}
+
+/* ---- sorts (glibc qsort is a stable merge sort here; ranks make it explicit) */
+typedef struct ikey {
+    int64_t k;
+    int32_t rank, v;
+} ikey;
+
+static int ikey_cmp(const void *a, const void *b) {
+    const ikey *x = a, *y = b;
+    if (x->k != y->k)
+        return x->k < y->k ? -1 : 1;
+    return (x->rank > y->rank) - (x->rank < y->rank);
+}
+
+typedef struct dkey {
+    double k;
+    int32_t rank, v;
+} dkey;
+
+/* descending by k (kdLeafCmpTotal / chainCmpScore: sign of b - a) */
+static int dkey_cmp_desc(const void *a, const void *b) {
+    const dkey *x = a, *y = b;
+    const double diff = y->k - x->k;
+    if (diff < 0)
+        return -1;
+    if (diff > 0)
+        return 1;
+    return (x->rank > y->rank) - (x->rank < y->rank);
+}
+
+/* ---- chain post-processing on a block list (linked by next[]) ---- */
+typedef struct ax_cb {
+    int32_t qs, qe, ts, te;
+    int32_t next;
+} ax_cb;
+
+static void xover_cb(ax_work *w, const ax_cb *a, const ax_cb *b, int overlap, int *pos, int *adj) {
+    crossover(w, a->qs, a->qe, a->ts, a->te, b->qs, b->qe, b->ts, b->te, overlap, pos, adj);
+}
+
+/* chainRemovePartialOverlaps (chainConnect.c:255-344) + chainMergeAbutting
+ * (:346-368); returns the new head (blocks in cb[], list by next) */
+static int32_t remove_partial_overlaps(ax_work *w, ax_cb *cb, int32_t head) {
+    for (int32_t a = head, b = cb[a].next; b >= 0; a = b, b = cb[b].next)
+        if (cb[a].qs >= cb[b].qs || cb[a].ts >= cb[b].ts) {
+            w_fail(w, "a (%d %d) not before b (%d %d) before removePartialOverlaps", cb[a].qs,
+                   cb[a].ts, cb[b].qs, cb[b].ts);
+            return head;
+        }
+    for (;;) {
+        int trim_a = 0, trim_b = 0;
+        int32_t a = head, b = cb[a].next;
+        for (;;) {
+            if (b < 0)
+                break;
+            const int dq = cb[b].qs - cb[a].qe, dt = cb[b].ts - cb[a].te;
+            if (dq < 0 || dt < 0) {
+                const int overlap = -(dq < dt ? dq : dt);
+                const int a_size = cb[a].qe - cb[a].qs, b_size = cb[b].qe - cb[b].qs;
+                if (overlap >= a_size || overlap >= b_size) {
+                    trim_b = 1;
+                } else {
+                    int cross, adj;
+                    xover_cb(w, &cb[a], &cb[b], overlap, &cross, &adj);
+                    cb[b].qs += cross;
+                    cb[b].ts += cross;
+                    const int inv = overlap - cross;
+                    cb[a].qe -= inv;
+                    cb[a].te -= inv;
+                    if (cb[b].qe <= cb[b].qs)
+                        trim_b = 1;
+                    else if (cb[a].qe <= cb[a].qs)
+                        trim_a = 1;
+                }
+            }
+            if (trim_a) {
+                /* removeNegativeBlocks */
+                int32_t nh = -1, tail = -1;
+                for (int32_t x = head; x >= 0; x = cb[x].next) {
+                    if (cb[x].qs >= cb[x].qe || cb[x].ts >= cb[x].te)
+                        continue;
+                    if (tail < 0)
+                        nh = x;
+                    else
+                        cb[tail].next = x;
+                    tail = x;
+                }
+                if (tail >= 0)
+                    cb[tail].next = -1;
+                head = nh;
+                break;
+            } else if (trim_b) {
+                b = cb[b].next;
+                cb[a].next = b;
+                trim_b = 0;
+            } else {
+                a = b;
+                b = cb[b].next;
+            }
+        }
+        if (!trim_a)
+            break;
+        if (head < 0)
+            break;
+    }
+    /* checkChainGaps / checkStartBeforeEnd */
+    for (int32_t a = head, b = head >= 0 ? cb[head].next : -1; b >= 0; a = b, b = cb[b].next)
+        if (cb[a].qe > cb[b].qs || cb[a].te > cb[b].ts) {
+            w_fail(w, "Negative gap between (%d %d - %d %d) and (%d %d - %d %d) after removePartialOverlaps",
+                   cb[a].qs, cb[a].ts, cb[a].qe, cb[a].te, cb[b].qs, cb[b].ts, cb[b].qe, cb[b].te);
+            return head;
+        }
+    for (int32_t x = head; x >= 0; x = cb[x].next)
+        if (cb[x].qs >= cb[x].qe || cb[x].ts >= cb[x].te) {
+            w_fail(w, "Start after end in (%d %d) to (%d %d) after removePartialOverlaps",
+                   cb[x].qs, cb[x].ts, cb[x].qe, cb[x].te);
+            return head;
+        }
+    /* chainMergeAbutting */
+    int32_t last = -1;
+    for (int32_t x = head; x >= 0;) {
+        const int32_t nx = cb[x].next;
+        if (last < 0 || cb[last].qe != cb[x].qs || cb[last].te != cb[x].ts) {
+            last = x;
+        } else {
+            cb[last].qe = cb[x].qe;
+            cb[last].te = cb[x].te;
+            cb[last].next = nx;
+        }
+        x = nx;
+    }
+    return head;
+}
+
+/* ------------------------------------------------------------------ one pair */
+typedef struct ax_pairinfo {
+    const char *tname, *qname;
+    int32_t tsize, qsize;
+    char strand;
+} ax_pairinfo;
+
+static void chain_pair(ax_work *w, const ax_pairinfo *pi, FILE *details, ax_out *out) {
+    const int32_t nb = w->n;
+    memset(out, 0, sizeof(*out));
+    /* leaves: slAddHead over the block list (reversed), zero-length blocks
+     * skipped, then slSort by tStart (stable) */
+    ikey *k = malloc((size_t)(nb ? nb : 1) * sizeof(ikey));
+    int32_t nl = 0;
+    for (int32_t i = nb - 1; i >= 0; --i) {
+        if (w->ts[i] == w->te[i])
+            continue;
+        k[nl] = (ikey){w->ts[i], nl, i};
+        ++nl;
+    }
+    w->nl = nl;
+    if (nl == 0) {
+        free(k);
+        out->coff = calloc(1, sizeof(int32_t));
+        return;
+    }
+    qsort(k, (size_t)nl, sizeof(ikey), ikey_cmp);
+    for (int32_t i = 0; i < nl; ++i)
+        w->tord[i] = k[i].v;
+    /* query-ordered copy: dlSort by qStart of the target-ordered list */
+    for (int32_t i = 0; i < nl; ++i)
+        k[i] = (ikey){w->qs[w->tord[i]], i, w->tord[i]};
+    qsort(k, (size_t)nl, sizeof(ikey), ikey_cmp);
+    for (int32_t i = 0; i < nl; ++i)
+        w->qord[i] = k[i].v;
+    free(k);
+    for (int32_t i = 0; i < nb; ++i) {
+        w->total[i] = w->score[i];
+        w->pred[i] = -1;
+    }
+    /* the tree is built from copies: kd_build permutes its lists */
+    int32_t *Q = malloc((size_t)nl * sizeof(int32_t)), *T = malloc((size_t)nl * sizeof(int32_t));
+    memcpy(Q, w->qord, (size_t)nl * sizeof(int32_t));
+    memcpy(T, w->tord, (size_t)nl * sizeof(int32_t));
+    w->nn = 0;
+    kd_build(w, Q, T, nl, 0);
+    free(Q);
+    free(T);
+    /* findBestPredecessors (chainBlock.c:281-300) */
+    for (int32_t i = 0; i < nl && !w->err; ++i) {
+        const int32_t l = w->tord[i];
+        double s;
+        int32_t p;
+        best_predecessor(w, l, &s, &p);
+        if (s > w->total[l]) {
+            w->total[l] = s;
+            w->pred[l] = p;
+        }
+        update_scores(w, l);
+    }
+    if (w->err)
+        return;
+    /* peelChains (chainBlock.c:311-373) in totalScore order */
+    dkey *dk = malloc((size_t)nl * sizeof(dkey));
+    for (int32_t i = 0; i < nl; ++i)
+        dk[i] = (dkey){w->total[w->tord[i]], i, w->tord[i]};
+    qsort(dk, (size_t)nl, sizeof(dkey), dkey_cmp_desc);
+    for (int32_t i = 0; i < nb; ++i)
+        w->hit[i] = 0;
+    int32_t *cblk = malloc((size_t)nl * sizeof(int32_t)); /* chain blocks, chain by chain */
+    int32_t *cstart = malloc((size_t)(nl + 1) * sizeof(int32_t));
+    int32_t nc = 0, nbk = 0;
+    for (int32_t i = 0; i < nl; ++i) {
+        const int32_t leaf = dk[i].v;
+        if (w->hit[leaf])
+            continue;
+        if (details)
+            fprintf(details, "chain %1.0f %s %d + %d %d %s %d %c %d %d %d\n", w->total[leaf],
+                    pi->tname, pi->tsize, 0, w->te[leaf], pi->qname, pi->qsize, pi->strand, 0,
+                    w->qe[leaf], -1);
+        cstart[nc] = nbk;
+        const int32_t first = nbk;
+        for (int32_t lf = leaf;;) {
+            w->hit[lf] = 1;
+            cblk[nbk++] = lf;
+            if (details)
+                fprintf(details, "%d\t%f\t%d\t%d\t%d\n", w->score[lf], w->total[lf], w->ts[lf],
+                        w->qs[lf], w->qe[lf] - w->qs[lf]);
+            if (w->pred[lf] < 0)
+                break;
+            const int32_t pl = w->nodes[w->pred[lf]].leaf;
+            if (details)
+                fprintf(details, " gap %d\t%d\n", w->ts[lf] - w->te[pl], w->qs[lf] - w->qe[pl]);
+            lf = pl;
+            if (w->hit[lf])
+                break;
+        }
+        /* slAddHead built the list from the end: reverse to ascending */
+        for (int32_t a = first, b = nbk - 1; a < b; ++a, --b) {
+            const int32_t x = cblk[a];
+            cblk[a] = cblk[b];
+            cblk[b] = x;
+        }
+        ++nc;
+    }
+    cstart[nc] = nbk;
+    free(dk);
+    /* scoreBlocks (chainBlock.c:296-309), then slSort(chainCmpScore) */
+    dkey *ck = malloc((size_t)(nc ? nc : 1) * sizeof(dkey));
+    for (int32_t c = 0; c < nc && !w->err; ++c) {
+        double s = 0;
+        for (int32_t j = cstart[c]; j < cstart[c + 1]; ++j) {
+            s += w->score[cblk[j]];
+            if (j > cstart[c])
+                s -= connect_cost(w, cblk[j - 1], cblk[j]);
+        }
+        ck[c] = (dkey){s, c, c};
+    }
+    qsort(ck, (size_t)nc, sizeof(dkey), dkey_cmp_desc);
+    /* removePartialOverlaps + mergeAbutting per chain, in that order */
+    ax_cb *cb = malloc((size_t)(nbk ? nbk : 1) * sizeof(ax_cb));
+    out->coff = malloc((size_t)(nc + 1) * sizeof(int32_t));
+    out->bt = malloc((size_t)(nbk ? nbk : 1) * sizeof(int32_t));
+    out->bq = malloc((size_t)(nbk ? nbk : 1) * sizeof(int32_t));
+    out->bs = malloc((size_t)(nbk ? nbk : 1) * sizeof(int32_t));
+    int32_t no = 0, nob = 0;
+    for (int32_t r = 0; r < nc && !w->err; ++r) {
+        const int32_t c = ck[r].v, b0 = cstart[c], b1 = cstart[c + 1];
+        for (int32_t j = b0; j < b1; ++j) {
+            const int32_t x = cblk[j];
+            cb[j] = (ax_cb){w->qs[x], w->qe[x], w->ts[x], w->te[x], j + 1 < b1 ? j + 1 : -1};
+        }
+        const int32_t head = remove_partial_overlaps(w, cb, b0);
+        out->coff[no] = nob;
+        for (int32_t x = head; x >= 0; x = cb[x].next) {
+            out->bt[nob] = cb[x].ts;
+            out->bq[nob] = cb[x].qs;
+            out->bs[nob] = cb[x].qe - cb[x].qs;
+            ++nob;
+        }
+        if (nob > out->coff[no])
+            ++no;
+    }
+    out->coff[no] = nob;
+    out->n_chains = no;
+    free(ck);
+    free(cb);
+    free(cblk);
+    free(cstart);
+}
+
+/* ------------------------------------------------------------------ threads */
+typedef struct ax_job {
+    const ax_env *e;
+    gac_ctx *ctx;
+    const gac_axt_input *in;
+    /* folded blocks per pair: [poff[p], poff[p+1]) */
+    const int64_t *poff;
+    const int32_t *qs, *qe, *ts, *te, *score;
+    const ax_pairinfo *info;
+    const int32_t *order; /* pairs, largest first */
+    int64_t n_pairs;
+    _Atomic int64_t next;
+    ax_out *out;
+    int want_details;
+} ax_job;
+
+static void work_reserve(ax_work *w, int32_t n) {
+    if ((size_t)n <= w->cap_n)
+        return;
+    const size_t c = (size_t)n + 16;
+    w->total = realloc(w->total, c * sizeof(double));
+    w->pred = realloc(w->pred, c * sizeof(int32_t));
+    w->hit = realloc(w->hit, c);
+    w->tord = realloc(w->tord, c * sizeof(int32_t));
+    w->qord = realloc(w->qord, c * sizeof(int32_t));
+    w->tmp = realloc(w->tmp, c * sizeof(int32_t));
+    w->nodes = realloc(w->nodes, 2 * c * sizeof(ax_node));
+    w->cap_n = c;
+}
+
+static void *ax_thread(void *arg) {
+    ax_job *J = arg;
+    ax_work w;
+    memset(&w, 0, sizeof(w));
+    w.e = J->e;
+    for (;;) {
+        const int64_t k = atomic_fetch_add(&J->next, 1);
+        if (k >= J->n_pairs)
+            break;
+        const int32_t p = J->order[k];
+        const int64_t b0 = J->poff[p];
+        const int32_t n = (int32_t)(J->poff[p + 1] - b0);
+        ax_out *o = &J->out[p];
+        w.err = 0;
+        w.msg[0] = 0;
+        if (gac_genome_view(J->ctx, GAC_Q, J->in->q_seq[p], &w.q.v) != GAC_OK ||
+            gac_genome_view(J->ctx, GAC_T, J->in->t_seq[p], &w.t.v) != GAC_OK) {
+            memset(o, 0, sizeof(*o));
+            o->err = 1;
+            snprintf(o->msg, sizeof(o->msg), "pair %d: no host sequence", p);
+            continue;
+        }
+        w.q.minus = J->in->q_strand[p] ? 1 : 0;
+        w.t.minus = 0;
+        w.n = n;
+        w.qs = J->qs + b0;
+        w.qe = J->qe + b0;
+        w.ts = J->ts + b0;
+        w.te = J->te + b0;
+        w.score = J->score + b0;
+        work_reserve(&w, n);
+        char *dbuf = NULL;
+        size_t dlen = 0;
+        FILE *df = J->want_details ? open_memstream(&dbuf, &dlen) : NULL;
+        chain_pair(&w, &J->info[p], df, o);
+        if (df) {
+            fclose(df);
+            o->details = dbuf;
+            o->details_len = dlen;
+        }
+        if (w.err) {
+            o->err = 1;
+            memcpy(o->msg, w.msg, sizeof(o->msg));
+        }
+    }
+    free(w.total);
+    free(w.pred);
+    free(w.hit);
+    free(w.tord);
+    free(w.qord);
+    free(w.tmp);
+    free(w.nodes);
+    free(w.xs);
+    return NULL;
+}
+
+static int thread_count(int req) {
+    if (req > 0)
+        return req > 256 ? 256 : req;
+    const char *s = getenv("GAC_THREADS");
+    if (!s || !*s)
+        s = getenv("OMP_NUM_THREADS");
+    int n = s && *s ? atoi(s) : 0;
+    if (n <= 0) {
+        const long c = sysconf(_SC_NPROCESSORS_ONLN);
+        n = c > 0 ? (int)c : 1;
+    }
+    return n > 64 ? 64 : n;
+}
+
+/* ------------------------------------------------------------------ entry */
+static int cmp_i64_desc_pair(const void *a, const void *b, void *arg) {
+    const int64_t *sz = arg;
+    const int32_t x = *(const int32_t *)a, y = *(const int32_t *)b;
+    if (sz[x] != sz[y])
+        return sz[x] > sz[y] ? -1 : 1;
+    return (x > y) - (x < y);
+}
+
+void gac_axt_chains_free(gac_axt_chains *c) {
+    if (!c)
+        return;
+    free(c->score);
+    free(c->pair);
+    free(c->t_start);
+    free(c->t_end);
+    free(c->q_start);
+    free(c->q_end);
+    free(c->blk_off);
+    free(c->blk_t);
+    free(c->blk_q);
+    free(c->blk_size);
+    free(c);
+}
+
+typedef struct bkey { /* removeExactOverlaps: slSort(cBlockCmpBoth) */
+    int32_t qs, ts, rank, qe, te;
+} bkey;
+
+static int bkey_cmp(const void *a, const void *b) {
+    const bkey *x = a, *y = b;
+    if (x->qs != y->qs)
+        return x->qs < y->qs ? -1 : 1;
+    if (x->ts != y->ts)
+        return x->ts < y->ts ? -1 : 1;
+    return (x->rank > y->rank) - (x->rank < y->rank);
+}
+
+int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
+                  const gac_axt_input *in, double min_score, int n_threads,
+                  const char *details_path, gac_axt_chains **out) {
+    gac_clear_error();
+    if (!ctx || !mat || !g || !in || !out || in->n_pairs < 0 ||
+        (in->n_pairs && (!in->t_seq || !in->q_seq || !in->q_strand || !in->blk_off)))
+        return gac_fail(GAC_E_ARG, "gac_axt_chain: bad argument");
+    *out = NULL;
+    int rc = gac_set_scoring(ctx, mat, g);
+    if (rc != GAC_OK)
+        return rc;
+    const int64_t np = in->n_pairs;
+    const int64_t nin = np ? in->blk_off[np] : 0;
+    /* ---- removeExactOverlaps per pair (axtChain.c:173-197) */
+    int64_t *poff = malloc((size_t)(np + 1) * sizeof(int64_t));
+    int32_t *qs = malloc((size_t)(nin ? nin : 1) * 4), *qe = malloc((size_t)(nin ? nin : 1) * 4);
+    int32_t *ts = malloc((size_t)(nin ? nin : 1) * 4), *te = malloc((size_t)(nin ? nin : 1) * 4);
+    int32_t *bsz = malloc((size_t)(nin ? nin : 1) * 4);
+    ax_pairinfo *info = calloc((size_t)(np ? np : 1), sizeof(ax_pairinfo));
+    poff[0] = 0;
+    int64_t nb = 0;
+    for (int64_t p = 0; p < np; ++p) {
+        const int64_t a = in->blk_off[p], b = in->blk_off[p + 1];
+        info[p].tname = gac_genome_seq_name(ctx, GAC_T, in->t_seq[p]);
+        info[p].qname = gac_genome_seq_name(ctx, GAC_Q, in->q_seq[p]);
+        info[p].tsize = gac_genome_seq_size(ctx, GAC_T, in->t_seq[p]);
+        info[p].qsize = gac_genome_seq_size(ctx, GAC_Q, in->q_seq[p]);
+        info[p].strand = in->q_strand[p] ? '-' : '+';
+        if (!info[p].tname || !info[p].qname) {
+            rc = gac_fail(GAC_E_ARG, "gac_axt_chain: pair %lld: bad sequence index", (long long)p);
+            goto fail;
+        }
+        bkey *k = malloc((size_t)(b > a ? b - a : 1) * sizeof(bkey));
+        for (int64_t i = a; i < b; ++i)
+            k[i - a] = (bkey){in->blk_q[i], in->blk_t[i], (int32_t)(i - a),
+                              in->blk_q[i] + in->blk_size[i], in->blk_t[i] + in->blk_size[i]};
+        qsort(k, (size_t)(b - a), sizeof(bkey), bkey_cmp);
+        const int64_t first = nb;
+        for (int64_t i = 0; i < b - a; ++i) {
+            if (nb > first && k[i].qs == qs[nb - 1] && k[i].ts == ts[nb - 1]) {
+                if (qe[nb - 1] < k[i].qe)
+                    qe[nb - 1] = k[i].qe;
+                if (te[nb - 1] < k[i].te)
+                    te[nb - 1] = k[i].te;
+                continue;
+            }
+            qs[nb] = k[i].qs;
+            qe[nb] = k[i].qe;
+            ts[nb] = k[i].ts;
+            te[nb] = k[i].te;
+            ++nb;
+        }
+        free(k);
+        poff[p + 1] = nb;
+        /* checkBlockRange (axtChain.c:242-248), query then target per block */
+        for (int64_t i = first; i < nb; ++i) {
+            if (qe[i] > info[p].qsize) {
+                rc = gac_fail(GAC_E_ARG, "query %s block %d-%d exceeds sequence length %d",
+                              info[p].qname, qs[i], qe[i], info[p].qsize);
+                goto fail;
+            }
+            if (te[i] > info[p].tsize) {
+                rc = gac_fail(GAC_E_ARG, "target %s block %d-%d exceeds sequence length %d",
+                              info[p].tname, ts[i], te[i], info[p].tsize);
+                goto fail;
+            }
+        }
+    }
+    /* ---- axtScoreUngapped of every block: one GPU batch */
+    int32_t *score = malloc((size_t)(nb ? nb : 1) * 4);
+    for (int64_t i = 0; i < nb; ++i)
+        bsz[i] = qe[i] - qs[i];
+    rc = gac_score_blocks(ctx, np, in->t_seq, in->q_seq, in->q_strand, poff, ts, qs, bsz, score);
+    if (rc != GAC_OK) {
+        free(score);
+        goto fail;
+    }
+    /* ---- host gap-cost table + code matrix */
+    ax_env env;
+    memset(&env, 0, sizeof(env));
+    env.g = g;
+    {
+        static const int acgt_of_code[4] = {3, 1, 0, 2}; /* T C A G -> index in ACGT */
+        for (int qc = 0; qc < 5; ++qc)
+            for (int tc = 0; tc < 5; ++tc)
+                env.m5[qc * 5 + tc] =
+                    (qc == 4 || tc == 4) ? 0 : mat[acgt_of_code[qc] * 4 + acgt_of_code[tc]];
+        int len = 1 << 20;
+        env.gtab_len = len;
+        env.gtab = malloc((size_t)3 * len * sizeof(int32_t));
+        for (int d = 0; d < len; ++d) {
+            env.gtab[d] = gac_gap_cost(g, d, 0);
+            env.gtab[len + d] = gac_gap_cost(g, 0, d);
+            env.gtab[2 * len + d] = d >= 2 ? gac_gap_cost(g, 1, d - 1) : gac_gap_cost(g, 0, 0);
+        }
+    }
+    /* ---- chainBlocks + overlap removal per pair on host threads */
+    ax_out *po = calloc((size_t)(np ? np : 1), sizeof(ax_out));
+    int32_t *order = malloc((size_t)(np ? np : 1) * sizeof(int32_t));
+    int64_t *psize = malloc((size_t)(np ? np : 1) * sizeof(int64_t));
+    for (int64_t p = 0; p < np; ++p) {
+        order[p] = (int32_t)p;
+        psize[p] = poff[p + 1] - poff[p];
+    }
+    qsort_r(order, (size_t)np, sizeof(int32_t), cmp_i64_desc_pair, psize);
+    ax_job J;
+    memset(&J, 0, sizeof(J));
+    J.e = &env;
+    J.ctx = ctx;
+    J.in = in;
+    J.poff = poff;
+    J.qs = qs;
+    J.qe = qe;
+    J.ts = ts;
+    J.te = te;
+    J.score = score;
+    J.info = info;
+    J.order = order;
+    J.n_pairs = np;
+    atomic_init(&J.next, 0);
+    J.out = po;
+    J.want_details = details_path != NULL;
+    int nt = thread_count(n_threads);
+    if (nt > np)
+        nt = np > 0 ? (int)np : 1;
+    pthread_t *th = malloc((size_t)nt * sizeof(pthread_t));
+    for (int i = 1; i < nt; ++i)
+        pthread_create(&th[i], NULL, ax_thread, &J);
+    ax_thread(&J);
+    for (int i = 1; i < nt; ++i)
+        pthread_join(th[i], NULL);
+    free(th);
+    free(env.gtab);
+    free(score);
+    free(order);
+    free(psize);
+    for (int64_t p = 0; p < np; ++p)
+        if (po[p].err) {
+            rc = gac_fail(GAC_E_FORMAT, "%s", po[p].msg);
+            break;
+        }
+    if (rc == GAC_OK && details_path) {
+        FILE *f = fopen(details_path, "w");
+        if (!f) {
+            rc = gac_fail(GAC_E_IO, "Can't open %s to write", details_path);
+        } else {
+            for (int64_t p = 0; p < np; ++p)
+                if (po[p].details_len)
+                    fwrite(po[p].details, 1, po[p].details_len, f);
+            if (fclose(f) != 0)
+                rc = gac_fail(GAC_E_IO, "Can't close %s", details_path);
+        }
+    }
+    gac_axt_chains *R = NULL;
+    if (rc == GAC_OK) {
+        /* ---- chainCalcScore of every chain: one GPU batch */
+        int64_t nc = 0, ncb = 0;
+        for (int64_t p = 0; p < np; ++p) {
+            nc += po[p].n_chains;
+            ncb += po[p].coff ? po[p].coff[po[p].n_chains] : 0;
+        }
+        int32_t *ct = malloc((size_t)(nc ? nc : 1) * 4), *cq = malloc((size_t)(nc ? nc : 1) * 4);
+        uint8_t *cs = malloc((size_t)(nc ? nc : 1));
+        int32_t *cpair = malloc((size_t)(nc ? nc : 1) * 4);
+        int64_t *coff = malloc((size_t)(nc + 1) * 8);
+        int32_t *bt = malloc((size_t)(ncb ? ncb : 1) * 4), *bq = malloc((size_t)(ncb ? ncb : 1) * 4),
+                *bs = malloc((size_t)(ncb ? ncb : 1) * 4);
+        gac_range *rg = malloc((size_t)(nc ? nc : 1) * sizeof(gac_range));
+        int64_t *gsc = malloc((size_t)(nc ? nc : 1) * 8);
+        int32_t *gali = malloc((size_t)(nc ? nc : 1) * 4);
+        int64_t c = 0, x = 0;
+        coff[0] = 0;
+        for (int64_t p = 0; p < np; ++p) {
+            const ax_out *o = &po[p];
+            for (int32_t k = 0; k < o->n_chains; ++k) {
+                ct[c] = in->t_seq[p];
+                cq[c] = in->q_seq[p];
+                cs[c] = in->q_strand[p] ? 1 : 0;
+                cpair[c] = (int32_t)p;
+                const int32_t b0 = o->coff[k], b1 = o->coff[k + 1];
+                memcpy(bt + x, o->bt + b0, (size_t)(b1 - b0) * 4);
+                memcpy(bq + x, o->bq + b0, (size_t)(b1 - b0) * 4);
+                memcpy(bs + x, o->bs + b0, (size_t)(b1 - b0) * 4);
+                rg[c] = (gac_range){(int32_t)c, o->bt[b0], o->bt[b1 - 1] + o->bs[b1 - 1]};
+                x += b1 - b0;
+                coff[++c] = x;
+            }
+        }
+        gac_chainset_desc d = {nc, ct, cq, cs, coff, ncb, bt, bq, bs};
+        gac_chainset *set = NULL;
+        if (nc > 0) {
+            rc = gac_chains_upload(ctx, &d, &set);
+            if (rc == GAC_OK)
+                rc = gac_score_ranges(ctx, set, rg, nc, 0, gsc, NULL, gali);
+            gac_chains_free(set);
+        }
+        if (rc == GAC_OK) {
+            /* minScore filter; slAddHead onto the master list (reversed),
+             * then slSort(chainCmpScore) -- stable */
+            dkey *k = malloc((size_t)(nc ? nc : 1) * sizeof(dkey));
+            int64_t nk = 0;
+            for (int64_t i = nc - 1; i >= 0; --i)
+                if ((double)gsc[i] >= min_score) {
+                    k[nk] = (dkey){(double)gsc[i], (int32_t)nk, (int32_t)i};
+                    ++nk;
+                }
+            qsort(k, (size_t)nk, sizeof(dkey), dkey_cmp_desc);
+            R = calloc(1, sizeof(*R));
+            R->n_chains = nk;
+            R->score = malloc((size_t)(nk ? nk : 1) * sizeof(double));
+            R->pair = malloc((size_t)(nk ? nk : 1) * 4);
+            R->t_start = malloc((size_t)(nk ? nk : 1) * 4);
+            R->t_end = malloc((size_t)(nk ? nk : 1) * 4);
+            R->q_start = malloc((size_t)(nk ? nk : 1) * 4);
+            R->q_end = malloc((size_t)(nk ? nk : 1) * 4);
+            R->blk_off = malloc((size_t)(nk + 1) * 8);
+            int64_t tb = 0;
+            for (int64_t j = 0; j < nk; ++j)
+                tb += coff[k[j].v + 1] - coff[k[j].v];
+            R->n_blocks = tb;
+            R->blk_t = malloc((size_t)(tb ? tb : 1) * 4);
+            R->blk_q = malloc((size_t)(tb ? tb : 1) * 4);
+            R->blk_size = malloc((size_t)(tb ? tb : 1) * 4);
+            R->blk_off[0] = 0;
+            for (int64_t j = 0; j < nk; ++j) {
+                const int32_t i = k[j].v;
+                const int64_t b0 = coff[i], b1 = coff[i + 1], o = R->blk_off[j];
+                R->score[j] = (double)gsc[i];
+                R->pair[j] = cpair[i];
+                R->t_start[j] = bt[b0];
+                R->q_start[j] = bq[b0];
+                R->t_end[j] = bt[b1 - 1] + bs[b1 - 1];
+                R->q_end[j] = bq[b1 - 1] + bs[b1 - 1];
+                memcpy(R->blk_t + o, bt + b0, (size_t)(b1 - b0) * 4);
+                memcpy(R->blk_q + o, bq + b0, (size_t)(b1 - b0) * 4);
+                memcpy(R->blk_size + o, bs + b0, (size_t)(b1 - b0) * 4);
+                R->blk_off[j + 1] = o + (b1 - b0);
+            }
+            free(k);
+        }
+        free(ct);
+        free(cq);
+        free(cs);
+        free(cpair);
+        free(coff);
+        free(bt);
+        free(bq);
+        free(bs);
+        free(rg);
+        free(gsc);
+        free(gali);
+    }
+    for (int64_t p = 0; p < np; ++p) {
+        free(po[p].coff);
+        free(po[p].bt);
+        free(po[p].bq);
+        free(po[p].bs);
+        free(po[p].details);
+    }
+    free(po);
+    if (rc == GAC_OK)
+        *out = R;
+fail:
+    free(poff);
+    free(qs);
+    free(qe);
+    free(ts);
+    free(te);
+    free(bsz);
+    free(info);
+    return rc;
+}

@@ -223,6 +223,44 @@ static int gc_tagged(gc_text *t, const char *tag, int count, int *iout, double *
     return GAC_OK;
 }
 
+/* interpolate() over the long positions (gapCalc.c:82-104) */
+static int gc_long(const gac_gapcalc *g, const double *v, int x) {
+    return gc_interp(x, g->long_pos, v, g->long_count);
+}
+
+int gac_gap_cost(const gac_gapcalc *g, int dq, int dt) {
+    if (dt < 0)
+        dt = 0;
+    if (dq < 0)
+        dq = 0;
+    if (dt == 0) {
+        if (dq < g->small_size)
+            return g->q_small[dq];
+        if (dq >= g->q_last_pos) {
+            volatile double prod = g->q_last_slope * (dq - g->q_last_pos);
+            return (int)(g->q_last_val + prod);
+        }
+        return gc_long(g, g->q_long, dq);
+    }
+    if (dq == 0) {
+        if (dt < g->small_size)
+            return g->t_small[dt];
+        if (dt >= g->t_last_pos) {
+            volatile double prod = g->t_last_slope * (dt - g->t_last_pos);
+            return (int)(g->t_last_val + prod);
+        }
+        return gc_long(g, g->t_long, dt);
+    }
+    const int both = dq + dt;
+    if (both < g->small_size)
+        return g->b_small[both];
+    if (both >= g->b_last_pos) {
+        volatile double prod = g->b_last_slope * (both - g->b_last_pos);
+        return (int)(g->b_last_val + prod);
+    }
+    return gc_long(g, g->b_long, both);
+}
+
 void gac_gapcalc_free(gac_gapcalc *g) {
     if (!g)
         return;

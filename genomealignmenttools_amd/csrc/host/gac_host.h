@@ -58,6 +58,16 @@ void gac_twobit_close(gac_twobit *tb);
 uint32_t gac_twobit_u32(const gac_twobit *tb, const uint8_t *p);
 int gac_is_twobit_file(const char *path);
 
+/* ---- host view of a resident sequence (kept after gac_genome_finalize) ----
+ * packed: 2 bits/base MSB-first (T=0 C=1 A=2 G=3); N runs merged and sorted. */
+typedef struct gac_seq_view {
+    const uint8_t *packed;
+    int32_t size;
+    const int32_t *n_start, *n_size;
+    int32_t n_count;
+} gac_seq_view;
+int gac_genome_view(gac_ctx *ctx, int side, int32_t index, gac_seq_view *v);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,547 @@
+/* axtChain -- drop-in for kent/src/hg/mouseStuff/axtChain/axtChain.c: chain
+ * together axt (or -psl) alignments.
+ *
+ * Same command line (kent optionHash: any option is accepted), same output
+ * text.  Input parsing, seqPair grouping and output follow the reference
+ * (readPslBlocks :345-377, readAxtBlocks :311-343, axtChain :379-470):
+ *   - pairs keyed by qName + strand + tName; PSL pairs stay in reverse
+ *     first-seen order (slAddHead), axt pairs are sorted by seqPairCmp;
+ *   - blocks of a pair in input order (slAddHead per block, then
+ *     slReverse);
+ *   - output: the ##matrix / ##gapPenalties / ##blastzParms header
+ *     (axtScoreSchemeDnaWrite, axt.c:836-872), the input's '#' lines
+ *     (unique), then the chains in chainCmpScore order with ids 1..n.
+ * The chaining itself -- removeExactOverlaps, block scores, chainBlocks'
+ * kd-tree DP, overlap removal, chainCalcScore, the minScore filter and the
+ * final sort -- is one libgachain call, gac_axt_chain (GPU block and chain
+ * scoring, host-threaded DP).  Genomes must be .2bit files (-faQ/-faT fasta
+ * inputs are read and uploaded as sequences). */
+#define _GNU_SOURCE
+#include <ctype.h>
+#include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "gac_tool.h"
+#include "gachain.h"
+#include "host/gac_host.h"
+
+static void usage(int min_score) {
+    gt_abort(
+        "axtChain - Chain together axt alignments.\n"
+        "usage:\n"
+        "   axtChain [options] -linearGap=loose in.axt tNibDir qNibDir out.chain\n"
+        "Where tNibDir/qNibDir are either directories full of nib files, the name\n"
+        "of a .2bit file, or a single fasta file with additional -faQ or -faT options.\n"
+        "options:\n"
+        "   -psl Use psl instead of axt format for input\n"
+        "   -faQ The specified qNibDir is a fasta file with multiple sequences for query\n"
+        "   -faT The specified tNibDir is a fasta file with multiple sequences for target\n"
+        "                NOTE: will not work with gzipped fasta files\n"
+        "   -minScore=N  Minimum score for chain, default %d\n"
+        "   -details=fileName Output some additional chain details\n"
+        "   -scoreScheme=fileName Read the scoring matrix from a blastz-format file\n"
+        "   -linearGap=<medium|loose|filename> Specify type of linearGap to use.\n"
+        "              *Must* specify this argument to one of these choices.\n"
+        "              loose is chicken/human linear gap costs.\n"
+        "              medium is mouse/human linear gap costs.\n"
+        "              Or specify a piecewise linearGap tab delimited file.\n"
+        "   (this build reads .2bit genomes, or fasta with -faQ/-faT; not nib directories)\n",
+        min_score);
+}
+
+/* ------------------------------------------------------------ kent lineFile */
+typedef struct rd {
+    char *buf, *cur, *end;
+    const char *path;
+    int line;
+    FILE *meta;       /* lineFileSetMetaDataOutput */
+    gt_names seen;    /* lineFileSetUniqueMetaData */
+    char *last;       /* last line returned (for lineFileReuse) */
+    int reuse;
+} rd;
+
+static void rd_open(rd *r, const char *path, FILE *meta) {
+    memset(r, 0, sizeof(*r));
+    size_t len;
+    r->buf = gt_slurp(path, &len);
+    r->cur = r->buf;
+    r->end = r->buf + len;
+    r->path = path;
+    r->meta = meta;
+}
+
+static void rd_meta(rd *r, const char *line) {
+    if (!r->meta || line[0] != '#')
+        return;
+    if (gt_names_find(&r->seen, line) >= 0)
+        return;
+    gt_names_add(&r->seen, line, strlen(line));
+    fprintf(r->meta, "%s\n", line);
+}
+
+/* lineFileNext */
+static char *rd_next(rd *r) {
+    if (r->reuse) {
+        r->reuse = 0;
+        rd_meta(r, r->last);
+        return r->last;
+    }
+    if (r->cur >= r->end)
+        return NULL;
+    char *line = r->cur;
+    char *nl = memchr(line, '\n', (size_t)(r->end - line));
+    if (nl) {
+        *nl = 0;
+        r->cur = nl + 1;
+    } else {
+        r->cur = r->end;
+    }
+    ++r->line;
+    r->last = line;
+    rd_meta(r, line);
+    return line;
+}
+
+/* lineFileNextReal: not blank, not starting (after spaces) with '#' */
+static char *rd_next_real(rd *r) {
+    char *line;
+    while ((line = rd_next(r)) != NULL) {
+        const char *s = line;
+        while (isspace((unsigned char)*s))
+            ++s;
+        if (*s != 0 && *s != '#')
+            return line;
+    }
+    return NULL;
+}
+
+/* kent chopByWhite into at most max words (modifies s) */
+static int chop(char *s, char **w, int max) {
+    return gac_chop_white(s, w, max);
+}
+
+static unsigned sql_unsigned(const char *s) {
+    char *end;
+    if (!isdigit((unsigned char)*s))
+        gt_abort("invalid unsigned integer: \"%s\"", s);
+    unsigned long v = strtoul(s, &end, 10);
+    if (*end != 0)
+        gt_abort("invalid unsigned integer: \"%s\"", s);
+    return (unsigned)v;
+}
+
+/* sqlUnsignedDynamicArray: comma-separated, optional trailing comma */
+static int32_t *sql_uarray(char *s, int *count) {
+    int n = 0, cap = 16;
+    int32_t *a = malloc(cap * sizeof(int32_t));
+    while (*s) {
+        char *c = strchr(s, ',');
+        if (c)
+            *c = 0;
+        if (n == cap) {
+            cap *= 2;
+            a = realloc(a, cap * sizeof(int32_t));
+        }
+        a[n++] = (int32_t)sql_unsigned(s);
+        if (!c)
+            break;
+        s = c + 1;
+    }
+    *count = n;
+    return a;
+}
+
+/* ------------------------------------------------------------ seqPairs */
+typedef struct pair {
+    char *qname, *tname;
+    char strand;
+    int64_t nb, cap;
+    int32_t *bt, *bq, *bs;
+} pair;
+
+typedef struct pairs {
+    gt_names keys;   /* "qName<strand>tName" -> index (hashAddSaveName) */
+    pair *p;
+    int32_t n, cap;
+} pairs;
+
+static pair *pair_get(pairs *P, const char *qname, const char *strand, const char *tname) {
+    char key[4096];
+    snprintf(key, sizeof(key), "%s%s%s", qname, strand, tname);
+    int32_t i = gt_names_find(&P->keys, key);
+    if (i < 0) {
+        i = gt_names_add(&P->keys, key, strlen(key));
+        if (P->n == P->cap) {
+            P->cap = P->cap ? P->cap * 2 : 64;
+            P->p = realloc(P->p, (size_t)P->cap * sizeof(pair));
+        }
+        pair *p = &P->p[P->n++];
+        memset(p, 0, sizeof(*p));
+        p->qname = strdup(qname);
+        p->tname = strdup(tname);
+        p->strand = strand[0];
+    }
+    return &P->p[i];
+}
+
+static void pair_add(pair *p, int32_t t, int32_t q, int32_t size) {
+    if (p->nb == p->cap) {
+        p->cap = p->cap ? p->cap * 2 : 256;
+        p->bt = realloc(p->bt, (size_t)p->cap * 4);
+        p->bq = realloc(p->bq, (size_t)p->cap * 4);
+        p->bs = realloc(p->bs, (size_t)p->cap * 4);
+    }
+    p->bt[p->nb] = t;
+    p->bq[p->nb] = q;
+    p->bs[p->nb] = size;
+    ++p->nb;
+}
+
+/* readPslBlocks (:345-377) with pslxFileOpenWithUniqueMeta (psl.c:547-612) */
+static void read_psl(const char *path, pairs *P, FILE *out) {
+    rd r;
+    rd_open(&r, path, out);
+    char *line = rd_next(&r);
+    if (!line) {
+        fprintf(stderr, "%s is empty\n", path);
+    } else if (strncmp(line, "psLayout version", 16) == 0) {
+        char *copy = strdup(line), *w[32];
+        const int wc = chop(copy, w, 32);
+        if (wc < 3)
+            gt_abort("%s is not a psLayout file", path);
+        if (strcmp(w[2], "3") != 0 && strcmp(w[2], "4") != 0)
+            gt_abort("%s is version %s of psLayout, this program can only handle through version 4",
+                     path, w[2]);
+        free(copy);
+        for (int i = 0; i < 4; ++i)
+            if (!rd_next(&r))
+                gt_abort("%s severely truncated", path);
+    } else {
+        int eof = 0;
+        while (line[0] == '#' && !eof) {
+            char *nx = rd_next(&r);
+            if (!nx)
+                eof = 1;
+            else
+                line = nx;
+        }
+        char *copy = strdup(line), *w[32];
+        const int wc = chop(copy, w, 32);
+        if ((wc < 21 || wc > 23 || (w[8][0] != '+' && w[8][0] != '-')) && !eof)
+            gt_abort("%s is not a psLayout file", path);
+        else if (!eof)
+            r.reuse = 1;
+        free(copy);
+    }
+    while ((line = rd_next_real(&r)) != NULL) {
+        char *w[32];
+        const int wc = chop(line, w, 32);
+        if (wc != 21 && wc != 23)
+            gt_abort("Bad line %d of %s wordCount is %d instead of 21 or 23\n", r.line, path, wc);
+        const unsigned block_count = sql_unsigned(w[17]);
+        for (int i = 0; i < 8; ++i)
+            (void)sql_unsigned(w[i][0] == '-' ? w[i] + 1 : w[i]);
+        const char *strand = w[8];
+        (void)sql_unsigned(w[10]);
+        (void)sql_unsigned(w[14]);
+        int n1, n2, n3;
+        int32_t *sizes = sql_uarray(w[18], &n1);
+        int32_t *qstarts = sql_uarray(w[19], &n2);
+        int32_t *tstarts = sql_uarray(w[20], &n3);
+        if ((unsigned)n1 != block_count || (unsigned)n2 != block_count ||
+            (unsigned)n3 != block_count)
+            gt_abort("Assertion `sizeOne == ret->blockCount' failed (line %d of %s)", r.line, path);
+        if (strand[1] != '\0')
+            gt_abort("requires PSLs to have implicit positive strand, found `%s'", strand);
+        pair *p = pair_get(P, w[9], strand, w[13]);
+        for (unsigned i = 0; i < block_count; ++i)
+            pair_add(p, tstarts[i], qstarts[i], sizes[i]);
+        free(sizes);
+        free(qstarts);
+        free(tstarts);
+    }
+    gt_names_free(&r.seen);
+    free(r.buf);
+}
+
+static int need_num(rd *r, char **w, int i) {
+    char *end;
+    const char *s = w[i];
+    long v = strtol(s, &end, 10);
+    if (*s == 0 || *end != 0 || !(isdigit((unsigned char)s[0]) || s[0] == '-'))
+        gt_abort("Expecting number field %d line %d of %s, got %s", i + 1, r->line, r->path, s);
+    return (int)v;
+}
+
+/* readAxtBlocks (:311-343): axtRead (axt.c:52-92) + axtAddBlocksToBoxInList
+ * (axt.c:929-970) */
+static void read_axt(const char *path, pairs *P, FILE *out) {
+    rd r;
+    rd_open(&r, path, out);
+    for (;;) {
+        char *w[10];
+        int wc = 0;
+        char *line;
+        while ((line = rd_next(&r)) != NULL) { /* lineFileChopNext */
+            if (line[0] == '#')
+                continue;
+            wc = chop(line, w, 10);
+            if (wc != 0)
+                break;
+        }
+        if (!line || wc <= 0)
+            break;
+        if (wc < 8)
+            gt_abort("Expecting at least 8 words line %d of %s got %d\n", r.line, path, wc);
+        const int qstart = need_num(&r, w, 5) - 1, qend = need_num(&r, w, 6);
+        const int tstart = need_num(&r, w, 2) - 1, tend = need_num(&r, w, 3);
+        (void)qend;
+        (void)tend;
+        if (wc > 8)
+            (void)need_num(&r, w, 8);
+        char strand[2] = {w[7][0], 0};
+        char *qname = w[4], *tname = w[1];
+        char *tsym = rd_next(&r);
+        if (!tsym)
+            gt_abort("Premature end of file in %s", path);
+        char *qsym = rd_next(&r);
+        if (!qsym)
+            gt_abort("Premature end of file in %s", path);
+        const size_t sym = strlen(tsym);
+        if (strlen(qsym) != sym)
+            gt_abort("Symbol count %d != %d inconsistent between sequences line %d and prev line of %s",
+                     (int)sym, (int)strlen(qsym), r.line, path);
+        rd_next(&r); /* blank line */
+        pair *p = pair_get(P, qname, strand, tname);
+        int q_pos = qstart, t_pos = tstart, qs = 0, ts = 0, last_in = 0;
+        for (size_t i = 0; i <= sym; ++i) {
+            const int aq = isalpha((unsigned char)qsym[i]) ? 1 : 0;
+            const int at = isalpha((unsigned char)tsym[i]) ? 1 : 0;
+            const int this_in = aq && at;
+            if (this_in) {
+                if (!last_in) {
+                    qs = q_pos;
+                    ts = t_pos;
+                }
+            } else if (last_in) {
+                const int size = q_pos - qs;
+                if (size > 0)
+                    pair_add(p, ts, qs, size);
+            }
+            last_in = this_in;
+            q_pos += aq;
+            t_pos += at;
+        }
+    }
+    gt_names_free(&r.seen);
+    free(r.buf);
+}
+
+/* seqPairCmp (:71-83) */
+static int pair_cmp(const void *a, const void *b) {
+    const pair *x = *(pair *const *)a, *y = *(pair *const *)b;
+    int d = strcmp(x->tname, y->tname);
+    if (d == 0)
+        d = strcmp(x->qname, y->qname);
+    if (d == 0)
+        d = (int)x->strand - (int)y->strand;
+    return d;
+}
+
+/* ------------------------------------------------------------ fasta (-faQ/-faT) */
+static void load_fasta(gac_ctx *ctx, int side, const char *path) {
+    size_t len;
+    char *buf = gt_slurp(path, &len);
+    char *p = buf, *end = buf + len;
+    int nseq = 0;
+    while (p < end) {
+        if (*p != '>') {
+            char *nl = memchr(p, '\n', (size_t)(end - p));
+            p = nl ? nl + 1 : end;
+            continue;
+        }
+        char *nl = memchr(p, '\n', (size_t)(end - p));
+        char *hdr_end = nl ? nl : end;
+        char *name = p + 1;
+        while (name < hdr_end && isspace((unsigned char)*name))
+            ++name;
+        char *ne = name;
+        while (ne < hdr_end && !isspace((unsigned char)*ne))
+            ++ne;
+        char saved = *ne;
+        *ne = 0;
+        char *seqname = strdup(name);
+        *ne = saved;
+        p = nl ? nl + 1 : end;
+        /* sequence lines until the next '>' */
+        size_t cap = 1 << 16, n = 0;
+        uint8_t *codes = malloc(cap);
+        while (p < end && *p != '>') {
+            const char c = *p++;
+            if (isspace((unsigned char)c))
+                continue;
+            if (n == cap) {
+                cap *= 2;
+                codes = realloc(codes, cap);
+            }
+            switch (c) {
+            case 't': case 'T': codes[n++] = 0; break;
+            case 'c': case 'C': codes[n++] = 1; break;
+            case 'a': case 'A': codes[n++] = 2; break;
+            case 'g': case 'G': codes[n++] = 3; break;
+            default: codes[n++] = 4; break;
+            }
+        }
+        uint8_t *packed = calloc((n + 3) / 4 + 1, 1);
+        int32_t *ns = malloc((n + 1) * sizeof(int32_t)), *nz = malloc((n + 1) * sizeof(int32_t));
+        int32_t nn = 0;
+        for (size_t i = 0; i < n; ++i) {
+            const int c = codes[i] == 4 ? 0 : codes[i];
+            packed[i >> 2] |= (uint8_t)(c << (6 - 2 * (i & 3)));
+            if (codes[i] == 4) {
+                if (nn > 0 && (size_t)(ns[nn - 1] + nz[nn - 1]) == i)
+                    ++nz[nn - 1];
+                else {
+                    ns[nn] = (int32_t)i;
+                    nz[nn] = 1;
+                    ++nn;
+                }
+            }
+        }
+        gt_check(gac_genome_add_seq(ctx, side, seqname, (int32_t)n, packed, nn, ns, nz));
+        gt_verbose(2, "read %s: %zu bases from %s\n", seqname, n, path);
+        free(seqname);
+        free(codes);
+        free(packed);
+        free(ns);
+        free(nz);
+        ++nseq;
+    }
+    free(buf);
+    gt_check(gac_genome_finalize(ctx, side));
+}
+
+/* ------------------------------------------------------------ main */
+int main(int argc, char *argv[]) {
+    gt_options_hash(&argc, argv);
+    int min_score = gt_opt_int("minScore", 1000);
+    const char *details = gt_opt_str("details", NULL);
+    const char *gap_name = gt_opt_str("linearGap", NULL);
+    const char *scheme = gt_opt_str("scoreScheme", NULL);
+    if (argc != 5)
+        usage(min_score);
+    const char *in = argv[1], *tnib = argv[2], *qnib = argv[3], *out_path = argv[4];
+    int32_t mat[16], gap_open = 0, gap_extend = 0;
+    char *extra = NULL;
+    if (scheme)
+        gt_verbose(1, "Reading scoring matrix from %s\n", scheme);
+    gt_check(gac_scheme_read(scheme, mat, &gap_open, &gap_extend, &extra));
+    if (gap_name == NULL)
+        gt_abort("Must specify linear gap costs.  Use 'loose' or 'medium' for defaults\n");
+    gac_gapcalc *gap = NULL;
+    gt_check(gac_gapcalc_build(gap_name, &gap));
+    const int fa_q = gt_opt_exists("faQ"), fa_t = gt_opt_exists("faT");
+
+    FILE *f = gt_must_open(out_path, "w");
+    /* axtScoreSchemeDnaWrite (axt.c:836-872): matrix in ACGT x ACGT order */
+    fprintf(f, "##matrix=axtChain 16");
+    for (int i = 0; i < 16; ++i)
+        fprintf(f, "%c%d", i ? ',' : ' ', mat[i]);
+    fprintf(f, "\n##gapPenalties=axtChain O=%d E=%d\n", gap_open, gap_extend);
+    if (extra) {
+        char *w = extra;
+        for (char *r = extra; *r; ++r)
+            if (*r != ' ' && *r != '"')
+                *w++ = *r;
+        *w = 0;
+        fprintf(f, "##blastzParms=%s\n", extra);
+    }
+    if (details) {
+        FILE *d = gt_must_open(details, "w");
+        fclose(d);
+    }
+    pairs P;
+    memset(&P, 0, sizeof(P));
+    const int psl = gt_opt_exists("psl");
+    if (psl)
+        read_psl(in, &P, f);
+    else
+        read_axt(in, &P, f);
+    /* pair order: PSL slAddHead (reverse first-seen); axt also sorted */
+    pair **ord = malloc((size_t)(P.n ? P.n : 1) * sizeof(pair *));
+    for (int32_t i = 0; i < P.n; ++i)
+        ord[i] = &P.p[P.n - 1 - i];
+    if (!psl)
+        qsort(ord, (size_t)P.n, sizeof(pair *), pair_cmp); /* keys are distinct */
+
+    gac_ctx *ctx = NULL;
+    gt_check(gac_open(0, &ctx));
+    if (fa_t) {
+        load_fasta(ctx, GAC_T, tnib);
+    } else {
+        if (!gac_is_twobit_file(tnib))
+            gt_abort("given tNibDir argument: '%s' is not a 2bit file (nib directories are not supported)\n",
+                     tnib);
+        gt_check(gac_genome_load_2bit(ctx, GAC_T, tnib));
+    }
+    if (fa_q) {
+        load_fasta(ctx, GAC_Q, qnib);
+    } else {
+        if (!gac_is_twobit_file(qnib))
+            gt_abort("given qNibDir argument: '%s' is not a 2bit file (nib directories are not supported)\n",
+                     qnib);
+        gt_check(gac_genome_load_2bit(ctx, GAC_Q, qnib));
+    }
+    /* sequences in the order the reference loads them (q, then t, per pair) */
+    const int64_t np = P.n;
+    int32_t *tseq = malloc((size_t)(np ? np : 1) * 4), *qseq = malloc((size_t)(np ? np : 1) * 4);
+    uint8_t *strand = malloc((size_t)(np ? np : 1));
+    int64_t *boff = malloc((size_t)(np + 1) * 8);
+    boff[0] = 0;
+    for (int64_t i = 0; i < np; ++i) {
+        const pair *p = ord[i];
+        qseq[i] = gac_genome_seq_index(ctx, GAC_Q, p->qname);
+        if (qseq[i] < 0) {
+            if (fa_q)
+                gt_abort("ERROR: can not find sequence name '%s' from fasta file '%s'\n", p->qname, qnib);
+            gt_abort("%s is not in %s", p->qname, qnib);
+        }
+        tseq[i] = gac_genome_seq_index(ctx, GAC_T, p->tname);
+        if (tseq[i] < 0) {
+            if (fa_t)
+                gt_abort("ERROR: can not find sequence name '%s' from fasta file '%s'\n", p->tname, tnib);
+            gt_abort("%s is not in %s", p->tname, tnib);
+        }
+        strand[i] = p->strand == '-' ? 1 : 0;
+        boff[i + 1] = boff[i] + p->nb;
+    }
+    const int64_t nb = boff[np];
+    int32_t *bt = malloc((size_t)(nb ? nb : 1) * 4), *bq = malloc((size_t)(nb ? nb : 1) * 4),
+            *bs = malloc((size_t)(nb ? nb : 1) * 4);
+    for (int64_t i = 0; i < np; ++i) {
+        const pair *p = ord[i];
+        memcpy(bt + boff[i], p->bt, (size_t)p->nb * 4);
+        memcpy(bq + boff[i], p->bq, (size_t)p->nb * 4);
+        memcpy(bs + boff[i], p->bs, (size_t)p->nb * 4);
+    }
+    gac_axt_input ai = {np, tseq, qseq, strand, boff, bt, bq, bs};
+    gac_axt_chains *ch = NULL;
+    gt_check(gac_axt_chain(ctx, mat, gap, &ai, (double)min_score, 0, details, &ch));
+    for (int64_t c = 0; c < ch->n_chains; ++c) {
+        const int32_t p = ch->pair[c];
+        const int64_t b0 = ch->blk_off[c];
+        gt_write_chain_raw(f, ch->score[c], ord[p]->tname, gac_genome_seq_size(ctx, GAC_T, tseq[p]),
+                           ch->t_start[c], ch->t_end[c], ord[p]->qname,
+                           gac_genome_seq_size(ctx, GAC_Q, qseq[p]), strand[p], ch->q_start[c],
+                           ch->q_end[c], (int32_t)(c + 1), ch->blk_t + b0, ch->blk_q + b0,
+                           ch->blk_size + b0, ch->blk_off[c + 1] - b0);
+    }
+    gt_careful_close(f, out_path);
+    gt_verbose(2, "%lld pairs, %lld blocks, %lld chains\n", (long long)np, (long long)nb,
+               (long long)ch->n_chains);
+    gac_axt_chains_free(ch);
+    gac_close(ctx);
+    return 0;
+}

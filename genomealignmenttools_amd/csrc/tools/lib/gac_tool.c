@@ -59,8 +59,12 @@ static const gt_spec *spec_find(const gt_spec *spec, const char *name) {
     return NULL;
 }
 
+static int g_any_option = 0; /* optionHash: every option accepted */
+
 static void validate(const gt_spec *spec, const char *name, const char *val) {
     static const gt_spec common[] = {{"verbose", GT_INT}, {NULL, 0}};
+    if (g_any_option)
+        return;
     const gt_spec *s = spec_find(spec, name);
     if (!s)
         s = spec_find(common, name);
@@ -146,6 +150,11 @@ void gt_options(int *argc, char **argv, const gt_spec *spec) {
     *argc = n;
     *wr = NULL;
     g_verbose = gt_opt_int("verbose", 1);
+}
+
+void gt_options_hash(int *argc, char **argv) {
+    g_any_option = 1;
+    gt_options(argc, argv, NULL);
 }
 
 const char *gt_opt_str(const char *name, const char *def) {
@@ -377,7 +386,7 @@ int gt_file_exists(const char *path) {
 }
 
 /* whole file into a NUL-terminated heap buffer (.gz decompressed) */
-static char *slurp(const char *path, size_t *len) {
+char *gt_slurp(const char *path, size_t *len) {
     size_t n = strlen(path);
     int gz = n > 3 && strcmp(path + n - 3, ".gz") == 0;
     size_t cap = 1 << 20, l = 0;
@@ -516,7 +525,7 @@ static int g_next_id = 1; /* chainIdNext (chain.c:180-198) */
 void gt_read_chains(const char *path, gt_chains *c, double stop_below, int keep_meta) {
     memset(c, 0, sizeof(*c));
     size_t len;
-    char *buf = slurp(path, &len);
+    char *buf = gt_slurp(path, &len);
     lf f = {buf, buf + len, path, 0, keep_meta ? c : NULL};
     c->blk_off = malloc(8);
     c->blk_off[0] = 0;
@@ -651,7 +660,7 @@ void gt_write_chain_raw(FILE *f, double score, const char *tname, int32_t tsize,
 void gt_read_sizes(const char *path, gt_sizes *s) {
     memset(s, 0, sizeof(*s));
     size_t len;
-    char *buf = slurp(path, &len);
+    char *buf = gt_slurp(path, &len);
     lf f = {buf, buf + len, path, 0, NULL};
     int32_t cap = 0;
     char *row[3];

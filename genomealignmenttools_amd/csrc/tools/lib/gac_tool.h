@@ -28,6 +28,9 @@ typedef struct gt_spec {
 /* Parse and remove options from argv (kent optionInit); "verbose" is always
  * accepted.  Unknown options abort. */
 void gt_options(int *argc, char **argv, const gt_spec *spec);
+/* optionHash (kent/src/lib/options.c:200-214): the same parsing, but any
+ * option name is accepted (axtChain) */
+void gt_options_hash(int *argc, char **argv);
 const char *gt_opt_str(const char *name, const char *def);
 int gt_opt_exists(const char *name);
 int gt_opt_int(const char *name, int def);
@@ -107,6 +110,8 @@ void gt_read_sizes(const char *path, gt_sizes *s);
 void gt_sizes_free(gt_sizes *s);
 
 FILE *gt_must_open(const char *path, const char *mode);
+/* whole file (".gz" decompressed, "stdin" allowed) into a NUL-terminated buffer */
+char *gt_slurp(const char *path, size_t *len);
 void gt_careful_close(FILE *f, const char *path);
 int gt_file_exists(const char *path);
 

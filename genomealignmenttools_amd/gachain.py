@@ -39,6 +39,10 @@ class GapCosts:
     def ptr(self):
         return self._ptr
 
+    def cost(self, dq: int, dt: int) -> int:
+        """gapCalcCost on the host (gac_gap_cost)."""
+        return int(lib().gac_gap_cost(self._ptr, int(dq), int(dt)))
+
     def tables(self):
         g = self._ptr.contents
         n, m = g.small_size, g.long_count

@@ -561,3 +561,109 @@ def chains_to_arrays(tg: Genome, qg: Genome, chains) -> ChainArrays:
         qend=np.array(qe, np.int32), id=np.arange(1, n + 1, dtype=np.int64),
         blk_off=np.array(offs, np.int64), blk_t=np.array(bt, np.int32),
         blk_q=np.array(bq, np.int32), blk_size=np.array(bs, np.int32))
+
+
+# ---------------------------------------------------------------- axtChain PSL input
+def psl_case(seed: int = 5, tsizes=(300_000, 120_000), qsizes=(250_000, 90_000),
+             paths_per_pair: int = 6, noise_frac: float = 0.2):
+    """Seeded PSL blocks for axtChain (small): per
+    (target, query, strand) pair a few planted collinear alignment paths --
+    ungapped blocks (geometric sizes) separated by q/t/both gaps, query bases a
+    mutated copy of the target -- cut into PSL records of 1-8 blocks; then
+    the awkward cases the DP has to get right: records re-emitted with a
+    diagonal shift (partially overlapping blocks -> crossovers), records
+    re-emitted from the same start with another length (removeExactOverlaps
+    folds), blocks overlapping the previous block on one side only, and
+    random unrelated blocks (noise_frac).  Both strands; N runs in both
+    genomes.  Returns (target Genome, query Genome, list of PSL records as
+    (qName, strand, tName, [(tStart, qStart, size)...]))."""
+    rng = np.random.default_rng(seed)
+    tg = random_genome({f"chrT{i + 1}": s for i, s in enumerate(tsizes)}, seed, n_frac=0.002,
+                       n_mean=300)
+    qg = random_genome({f"chrQ{i + 1}": s for i, s in enumerate(qsizes)}, seed + 1, n_frac=0.002,
+                       n_mean=300)
+    recs = []
+    for ti, tname in enumerate(tg.names):
+        tcodes = tg.codes[ti]
+        for qi, qname in enumerate(qg.names):
+            qcodes = qg.codes[qi]
+            qsize = len(qcodes)
+            for strand in (0, 1):
+                sname = "+-"[strand]
+                for _ in range(paths_per_pair):
+                    nblk = int(rng.integers(3, 60))
+                    t = int(rng.integers(0, len(tcodes) // 2))
+                    q = int(rng.integers(0, qsize // 2))
+                    div = float(rng.choice([0.05, 0.12, 0.2]))
+                    path = []
+                    for _b in range(nblk):
+                        size = int(min(rng.geometric(1 / 60), 400))
+                        if t + size >= len(tcodes) or q + size >= qsize:
+                            break
+                        path.append((t, q, size))
+                        m = _mutate(rng, tcodes[t:t + size], div)
+                        if strand == 0:
+                            qcodes[q:q + size] = m
+                        else:
+                            f0 = qsize - (q + size)
+                            qcodes[f0:f0 + size] = (m ^ 2)[::-1]
+                        mode = int(rng.integers(0, 3))
+                        g = int(rng.choice([1, 3, 10, 40, 200, 1500, 8000]))
+                        t += size + (0 if mode == 1 else g)
+                        q += size + (0 if mode == 0 else int(rng.integers(1, 2 * g + 2)))
+                    # cut into records
+                    i = 0
+                    while i < len(path):
+                        k = int(rng.integers(1, 9))
+                        rec = path[i:i + k]
+                        recs.append((qname, sname, tname, list(rec)))
+                        r = rng.random()
+                        if r < 0.15:     # diagonal shift: partial overlaps
+                            d = int(rng.integers(1, 25))
+                            shifted = [(a + d, b + d, s) for a, b, s in rec
+                                       if a + d + s < len(tcodes) and b + d + s < qsize]
+                            if shifted:
+                                recs.append((qname, sname, tname, shifted))
+                        elif r < 0.25:   # same starts, other length
+                            recs.append((qname, sname, tname,
+                                         [(a, b, max(1, s + int(rng.integers(-20, 20))))
+                                          for a, b, s in rec]))
+                        elif r < 0.32:   # one-sided overlap with the previous block
+                            a, b, s = rec[0]
+                            if s > 30:
+                                recs.append((qname, sname, tname, [(a + 10, b + 5, s - 15)]))
+                        i += k
+                # noise blocks
+                nn = int(noise_frac * paths_per_pair * 20)
+                for _ in range(nn):
+                    size = int(rng.integers(20, 200))
+                    t = int(rng.integers(0, len(tcodes) - size))
+                    q = int(rng.integers(0, qsize - size))
+                    recs.append((qname, sname, tname, [(t, q, size)]))
+    order = rng.permutation(len(recs))
+    return tg, qg, [recs[i] for i in order]
+
+
+def write_psl(tg: Genome, qg: Genome, recs, path: str, header: bool = True) -> None:
+    """PSL text (psLayout version 3): only strand, names, sizes and the
+    block lists matter to axtChain; match counts are left 0."""
+    tsz, qsz = tg.sizes, qg.sizes
+    with open(path, "w") as f:
+        if header:
+            f.write("psLayout version 3\n\nmatch\tmis-\trep.\tN's\tQ gap\tQ gap\tT gap\tT gap\t"
+                    "strand\tQ\t\tQ\tQ\tQ\tT\t\tT\tT\tT\tblock\tblockSizes\tqStarts\t tStarts\n"
+                    "\tmatch\tmatch\t\tcount\tbases\tcount\tbases\t\tname\t\tsize\tstart\tend\t"
+                    "name\t\tsize\tstart\tend\tcount\n" + "-" * 159 + "\n")
+        for qname, strand, tname, blocks in recs:
+            blocks = sorted(blocks, key=lambda b: (b[0], b[1]))
+            ts = blocks[0][0]
+            te = max(a + s for a, b, s in blocks)
+            qs = min(b for a, b, s in blocks)
+            qe = max(b + s for a, b, s in blocks)
+            if strand == "-":
+                qs, qe = qsz[qname] - qe, qsz[qname] - qs
+            f.write("\t".join(str(x) for x in [0, 0, 0, 0, 0, 0, 0, 0, strand, qname, qsz[qname], qs,
+                                                qe, tname, tsz[tname], ts, te, len(blocks)]))
+            f.write("\t" + "".join(f"{s}," for a, b, s in blocks))
+            f.write("\t" + "".join(f"{b}," for a, b, s in blocks))
+            f.write("\t" + "".join(f"{a}," for a, b, s in blocks) + "\n")

@@ -114,6 +114,10 @@ const char *gac_device_arch(gac_ctx *ctx);
  * (gapCalcFromFile, kent/src/lib/gapCalc.c:233-255).  Free with gac_gapcalc_free. */
 int gac_gapcalc_build(const char *name_or_file, gac_gapcalc **out);
 void gac_gapcalc_free(gac_gapcalc *g);
+/* gapCalcCost (kent/src/lib/gapCalc.c:298-331) on the host: negative
+ * distances clamp to 0, q / t / both tables, interpolation in double with
+ * the reference's operation order, truncated to int. */
+int gac_gap_cost(const gac_gapcalc *g, int dq, int dt);
 /* Read a blastz/lastz matrix file (axtScoreSchemeReadLf, axt.c:692-819), or the
  * blastz default when path is NULL (axtScoreSchemeDefault, axt.c:423-458).
  * mat[i*4+j] = matrix[query base i][target base j], i,j in A,C,G,T order.
@@ -170,6 +174,58 @@ int gac_score_ranges_device(gac_ctx *ctx, const gac_chainset *cs,
                             const gac_range *d_ranges, int64_t n, uint32_t flags,
                             int64_t *d_global, int64_t *d_local, int32_t *d_ali,
                             void *stream);
+
+/* ---- axtChain ------------------------------------------------------------
+ * Per-block scores: axtScoreUngapped (kent/src/lib/axt.c:186-194) of every
+ * block, the scores chainPair gives the kd-tree (axtChain.c:276-282).  Pairs
+ * share a target / query sequence and strand ('-': query coordinates on the
+ * reverse strand, as in PSL/axt).  Blocks must lie inside their sequences. */
+int gac_score_blocks(gac_ctx *ctx, int64_t n_pairs, const int32_t *t_seq, const int32_t *q_seq,
+                     const uint8_t *q_strand, const int64_t *blk_off, const int32_t *blk_t,
+                     const int32_t *blk_q, const int32_t *blk_size, int32_t *score);
+
+/* axtChain's chaining of every seqPair (axtChain.c:250-309 chainPair and
+ * :452-470 the final sort), replacing
+ *   removeExactOverlaps          axtChain.c:173-197
+ *   axtScoreUngapped per block   axt.c:186-194              (GPU, gac_score_blocks)
+ *   chainBlocks                  kent/src/lib/chainBlock.c:400-452: the kd-tree
+ *                                (kdBuild :124-164), bestPredecessor (:207-263),
+ *                                updateScoresOnWay (:265-279), peelChains
+ *                                (:311-373), scoreBlocks (:296-309)
+ *   chainConnectCost             kent/src/lib/chainConnect.c:114-149 (+ cBlockFindCrossover :61-105)
+ *   chainRemovePartialOverlaps   chainConnect.c:255-344, chainMergeAbutting :346-368
+ *   chainCalcScore               chainConnect.c:24-40       (GPU, gac_score_ranges)
+ *   minScore filter + slSort(chainCmpScore)
+ * Blocks of pair p are [blk_off[p], blk_off[p+1]) in the order axtChain holds
+ * them before removeExactOverlaps (input order: the PSL/axt records and their
+ * blocks as read).  Pairs are processed in the given order (spList order);
+ * the kd-tree DP runs on host threads (n_threads, 0 = all cores), one pair at
+ * a time per thread.  Output chains are in chainWrite order; ids are 1..n.
+ * details_path (may be NULL): axtChain -details text.  Installs mat/g on
+ * the context (gac_set_scoring). */
+typedef struct gac_axt_input {
+    int64_t n_pairs;
+    const int32_t *t_seq;    /* [n_pairs] gac_genome_seq_index(GAC_T) */
+    const int32_t *q_seq;    /* [n_pairs] gac_genome_seq_index(GAC_Q) */
+    const uint8_t *q_strand; /* [n_pairs] 0 '+', 1 '-' */
+    const int64_t *blk_off;  /* [n_pairs + 1] */
+    const int32_t *blk_t, *blk_q, *blk_size;
+} gac_axt_input;
+
+typedef struct gac_axt_chains {
+    int64_t n_chains;
+    double *score;           /* chainCalcScore (integral) */
+    int32_t *pair;           /* seqPair index of each chain */
+    int32_t *t_start, *t_end, *q_start, *q_end;
+    int64_t *blk_off;        /* [n_chains + 1] */
+    int64_t n_blocks;
+    int32_t *blk_t, *blk_q, *blk_size;
+} gac_axt_chains;
+
+int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
+                  const gac_axt_input *in, double min_score, int n_threads,
+                  const char *details_path, gac_axt_chains **out);
+void gac_axt_chains_free(gac_axt_chains *c);
 
 /* ---- chainNet netting engine (host, no device needed) -------------------
  * Replaces chainNet's netting and output (src/chainNet/chainNet.c:328-896):

@@ -147,3 +147,57 @@ def test_chaincleaner_nonet(case, tmp_path):
     NetFilterNonNested.perl -minScore1 3000); same outputs as the reference
     run on that pipeline's net."""
     _run_cleaner(case, tmp_path, net=False)
+
+
+# ---------------------------------------------------------------- axtChain
+@pytest.mark.parametrize("case", ["newStyleLastz", "oldStyleBlastz"])
+def test_axtchain_kat(case, tmp_path):
+    """The reference's own axtChain known-answer test
+    (kent/src/hg/mouseStuff/axtChain/tests/makefile): -psl input, real chrM
+    DNA, lastz matrices; byte-identical to tests/expected."""
+    d = os.path.join(GOLDEN, "chrM")
+    out = tmp_path / "out.chain"
+    _run([_bin("axtChain"), "-psl", os.path.join(d, f"{case}.psl"), "-minScore=3000",
+          "-linearGap=loose", os.path.join(d, "hg19.chrM.2bit"),
+          f"-scoreScheme={os.path.join(d, case + '.Q.txt')}", os.path.join(d, "susScr3.chrM.2bit"),
+          str(out)])
+    assert filecmp.cmp(out, os.path.join(d, f"{case}.chain"), shallow=False)
+
+
+def test_axtchain_kat_fasta(tmp_path):
+    """-faQ/-faT: the same known answer with fasta genomes."""
+    from oracle.oracle import read_2bit_text
+    d = os.path.join(GOLDEN, "chrM")
+    for name in ["hg19", "susScr3"]:
+        seqs = read_2bit_text(os.path.join(d, f"{name}.chrM.2bit"))
+        with open(tmp_path / f"{name}.fa", "w") as f:
+            for k, v in seqs.items():
+                f.write(f">{k}\n{v.decode()}\n")
+    out = tmp_path / "out.chain"
+    _run([_bin("axtChain"), "-psl", "-faQ", "-faT", os.path.join(d, "newStyleLastz.psl"),
+          "-minScore=3000", "-linearGap=loose", str(tmp_path / "hg19.fa"),
+          f"-scoreScheme={os.path.join(d, 'newStyleLastz.Q.txt')}", str(tmp_path / "susScr3.fa"),
+          str(out)])
+    assert filecmp.cmp(out, os.path.join(d, "newStyleLastz.chain"), shallow=False)
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+@pytest.mark.parametrize("case", ["loose", "medium0", "hoxd", "axt"])
+def test_axtchain_synth(seed, case, tmp_path):
+    """Planted PSL/axt blocks with partial, exact and one-sided overlaps,
+    noise, both strands: chains (and -details) byte-identical to the
+    reference axtChain."""
+    d = os.path.join(GOLDEN, "axtchain", f"s{seed}")
+    with open(os.path.join(GOLDEN, "axtchain", "cases.json")) as f:
+        opts = json.load(f)[case]
+    inp = "in.psl" if "-psl" in opts else "in.axt.gz"
+    opts = [o.replace("../../chrM", os.path.join(GOLDEN, "chrM")) for o in opts]
+    r = subprocess.run([_bin("axtChain")] + opts + [os.path.join(d, inp), os.path.join(d, "t.2bit"),
+                                                    os.path.join(d, "q.2bit"), "out.chain"],
+                       capture_output=True, text=True, timeout=600, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert filecmp.cmp(tmp_path / "out.chain", os.path.join(d, f"{case}.chain"), shallow=False)
+    for o in opts:
+        if o.startswith("-details="):
+            fn = o.split("=", 1)[1]
+            assert filecmp.cmp(tmp_path / fn, os.path.join(d, fn), shallow=False)

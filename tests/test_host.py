@@ -39,6 +39,21 @@ def test_gapcalc_tables_match_oracle():
         assert list(t["b_small"][2:]) == [og.cost(i // 2, i - i // 2) for i in range(2, n)]
 
 
+def test_host_gap_cost_vs_reference():
+    """gac_gap_cost (the host gapCalcCost axtChain's DP uses) against the
+    reference's own gapCalcCost on 5.6k (dq, dt) shapes x 3 tables
+    (tests/golden/gapcalc.json, generated with the reference objects)."""
+    import json
+    from genomealignmenttools_amd.gachain import GapCosts
+    with open(os.path.join(GOLDEN, "gapcalc.json")) as f:
+        d = json.load(f)
+    for key, name in [("loose", "loose"), ("medium", "medium"),
+                      ("file", os.path.join(GOLDEN, "linearGap.txt"))]:
+        g = GapCosts(name)
+        got = [g.cost(dq, dt) for dq, dt in d["pairs"]]
+        assert got == d[key], key
+
+
 def test_score_scheme_reader():
     from genomealignmenttools_amd.gachain import read_score_scheme
     m, go, ge, ex = read_score_scheme(os.path.join(GOLDEN, "c1", "HoxD55.q"))
@@ -142,6 +157,36 @@ def test_chaincleaner_errors(tmp_path):
     r = subprocess.run([cc, p("in.chain"), "/nonexistent.2bit", p("q.2bit"), "a", "b",
                         "-linearGap=loose"], capture_output=True, text=True)
     assert r.returncode == 255 and "does not exist" in r.stderr
+
+
+def test_axtchain_errors(tmp_path):
+    """axtChain argument and input checks (errAbort, exit 255) -- all before
+    any device work."""
+    from genomealignmenttools_amd._lib import BIN_DIR
+    ax = os.path.join(BIN_DIR, "axtChain")
+    d = os.path.join(GOLDEN, "chrM")
+    r = subprocess.run([ax], capture_output=True, text=True)
+    assert r.returncode == 255 and "usage" in r.stderr and "-minScore=N" in r.stderr
+    args = [os.path.join(d, "newStyleLastz.psl"), os.path.join(d, "hg19.chrM.2bit"),
+            os.path.join(d, "susScr3.chrM.2bit"), str(tmp_path / "o.chain")]
+    r = subprocess.run([ax, "-psl"] + args, capture_output=True, text=True)
+    assert r.returncode == 255 and "Must specify linear gap costs" in r.stderr
+    r = subprocess.run([ax, "-psl", "-minScore=x", "-linearGap=loose"] + args,
+                       capture_output=True, text=True)
+    assert r.returncode == 255 and "not a valid integer" in r.stderr
+    bad = tmp_path / "bad.psl"
+    bad.write_text("#c\n1\t2\t3\n")
+    r = subprocess.run([ax, "-psl", "-linearGap=loose", str(bad)] + args[1:],
+                       capture_output=True, text=True)
+    assert r.returncode == 255 and "is not a psLayout file" in r.stderr
+    lines = open(os.path.join(d, "newStyleLastz.psl")).read().split("\n")
+    body = [l for l in lines if l and not l.startswith("#")]
+    w = body[0].split("\t")
+    w[8] = "++"
+    bad.write_text("\t".join(w) + "\n")
+    r = subprocess.run([ax, "-psl", "-linearGap=loose", str(bad)] + args[1:],
+                       capture_output=True, text=True)
+    assert r.returncode == 255 and "requires PSLs to have implicit positive strand" in r.stderr
 
 
 def test_no_cpu_fallback_without_gpu():
