@@ -65,3 +65,16 @@ clean:
 	rm -rf build $(LIBDIR) $(BINDIR) oracle/_build
 
 .PHONY: all oracle ref clean
+
+# TEST INFRASTRUCTURE: axtChain's host half (front end + kd-tree DP) on a CPU
+# stand-in of the device ABI, for profiling in GPU-less containers.  Not part
+# of `all`; never shipped (oracle/cpu_gac_stub.c).
+cpu-axtchain: oracle/_build/axtChain_cpu
+
+oracle/_build/axtChain_cpu: $(CSRC)/tools/axtChain.c $(CSRC)/host/gac_axtchain.c \
+		$(CSRC)/host/gac_host.c oracle/cpu_gac_stub.c $(TOOL_LIB_SRC)
+	@mkdir -p oracle/_build
+	$(CC) -O2 -g -std=gnu11 -Wall -Iinclude -I$(CSRC) -I$(CSRC)/host -I$(CSRC)/tools/lib $^ \
+	    -o $@ -lz -lm -lpthread $(CPU_EXTRA)
+
+.PHONY: cpu-axtchain

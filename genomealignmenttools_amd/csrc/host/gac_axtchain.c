@@ -28,6 +28,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <unistd.h>
 
 #include "gac_host.h"
@@ -112,6 +113,7 @@ typedef struct ax_out { /* one pair's result */
     size_t details_len;
     int err;
     char msg[512];
+    double secs; /* wall time of this pair's chaining */
 } ax_out;
 
 typedef struct ax_work {
@@ -234,7 +236,8 @@ static int32_t kd_build(ax_work *w, int32_t *Q, int32_t *T, int32_t n, int dim) 
     const int32_t id = w->nn++;
     if (n == 1) {
         const int32_t l = Q[0];
-        w->nodes[id] = (ax_node){-1, -1, l, 0, 0.0, w->qe[l], w->te[l]};
+        /* leaf node: lo/hi carry the leaf's qStart/tStart */
+        w->nodes[id] = (ax_node){w->qs[l], w->ts[l], l, 0, 0.0, w->qe[l], w->te[l]};
         return id;
     }
     const int32_t half = n / 2;
@@ -247,8 +250,10 @@ static int32_t kd_build(ax_work *w, int32_t *Q, int32_t *T, int32_t n, int dim) 
     const int32_t cut = dim == 0 ? w->qs[ml] : w->ts[ml];
     partition(Q, n, w->hit, w->tmp);
     partition(T, n, w->hit, w->tmp);
-    const int32_t lo = kd_build(w, Q, T, half, 1 - dim);
+    /* hi first: nodes land in the DFS's usual visiting order (pre-order,
+     * hi before lo), so a search walks memory forward */
     const int32_t hi = kd_build(w, Q + half, T + half, n - half, 1 - dim);
+    const int32_t lo = kd_build(w, Q, T, half, 1 - dim);
     ax_node *nd = &w->nodes[id];
     nd->lo = lo;
     nd->hi = hi;
@@ -287,7 +292,7 @@ static void best_predecessor(ax_work *w, int32_t lonely, double *ret_score, int3
             continue;
         if (nd->leaf >= 0) {
             const int32_t l = nd->leaf;
-            if (w->qs[l] < lq && w->ts[l] < lt) {
+            if (nd->lo < lq && nd->hi < lt) {
                 const double s = w->total[l] + lscore - connect_cost(w, l, lonely);
                 if (s > best) {
                     best = s;
@@ -694,7 +699,11 @@ static void *ax_thread(void *arg) {
         char *dbuf = NULL;
         size_t dlen = 0;
         FILE *df = J->want_details ? open_memstream(&dbuf, &dlen) : NULL;
+        struct timespec t0, t1;
+        clock_gettime(CLOCK_MONOTONIC, &t0);
         chain_pair(&w, &J->info[p], df, o);
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        o->secs = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
         if (df) {
             fclose(df);
             o->details = dbuf;
@@ -730,7 +739,101 @@ static int thread_count(int req) {
     return n > 64 ? 64 : n;
 }
 
+/* ------------------------------------------------------------------ parallel helpers */
+static void run_threads(int nt, void *(*fn)(void *), void *arg) {
+    if (nt < 1)
+        nt = 1;
+    pthread_t *th = malloc((size_t)nt * sizeof(pthread_t));
+    for (int i = 1; i < nt; ++i)
+        pthread_create(&th[i], NULL, fn, arg);
+    fn(arg);
+    for (int i = 1; i < nt; ++i)
+        pthread_join(th[i], NULL);
+    free(th);
+}
+
+typedef struct bkey { /* removeExactOverlaps: slSort(cBlockCmpBoth) */
+    int32_t qs, ts, rank, qe, te;
+} bkey;
+
+static int bkey_cmp(const void *a, const void *b) {
+    const bkey *x = a, *y = b;
+    if (x->qs != y->qs)
+        return x->qs < y->qs ? -1 : 1;
+    if (x->ts != y->ts)
+        return x->ts < y->ts ? -1 : 1;
+    return (x->rank > y->rank) - (x->rank < y->rank);
+}
+
+typedef struct fold_job {
+    const gac_axt_input *in;
+    int32_t *qs, *qe, *ts, *te;
+    int64_t *poff; /* poff[p + 1] = folded count of pair p */
+    int64_t np;
+    _Atomic int64_t next;
+} fold_job;
+
+/* removeExactOverlaps (axtChain.c:173-197): slSort by (qStart, tStart),
+ * stable; blocks with both starts equal fold into the first (max ends) */
+static void *fold_thread(void *arg) {
+    fold_job *F = arg;
+    const gac_axt_input *in = F->in;
+    bkey *k = NULL;
+    int64_t kcap = 0;
+    for (;;) {
+        const int64_t p = atomic_fetch_add(&F->next, 1);
+        if (p >= F->np)
+            break;
+        const int64_t a = in->blk_off[p], b = in->blk_off[p + 1];
+        if (b - a > kcap) {
+            kcap = b - a;
+            k = realloc(k, (size_t)kcap * sizeof(bkey));
+        }
+        for (int64_t i = a; i < b; ++i)
+            k[i - a] = (bkey){in->blk_q[i], in->blk_t[i], (int32_t)(i - a),
+                              in->blk_q[i] + in->blk_size[i], in->blk_t[i] + in->blk_size[i]};
+        qsort(k, (size_t)(b - a), sizeof(bkey), bkey_cmp);
+        int64_t n = a;
+        for (int64_t i = 0; i < b - a; ++i) {
+            if (n > a && k[i].qs == F->qs[n - 1] && k[i].ts == F->ts[n - 1]) {
+                if (F->qe[n - 1] < k[i].qe)
+                    F->qe[n - 1] = k[i].qe;
+                if (F->te[n - 1] < k[i].te)
+                    F->te[n - 1] = k[i].te;
+                continue;
+            }
+            F->qs[n] = k[i].qs;
+            F->qe[n] = k[i].qe;
+            F->ts[n] = k[i].ts;
+            F->te[n] = k[i].te;
+            ++n;
+        }
+        F->poff[p + 1] = n - a;
+    }
+    free(k);
+    return NULL;
+}
+
 /* ------------------------------------------------------------------ entry */
+/* GAC_TIMING=1: stage wall times on stderr */
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+static void stage(const char *what, double *t) {
+    static int on = -1;
+    if (on < 0) {
+        const char *e = getenv("GAC_TIMING");
+        on = e && *e && *e != '0';
+    }
+    const double n = now_s();
+    if (on)
+        fprintf(stderr, "[gac_axt_chain] %-28s %8.3f s\n", what, n - *t);
+    *t = n;
+}
+
 static int cmp_i64_desc_pair(const void *a, const void *b, void *arg) {
     const int64_t *sz = arg;
     const int32_t x = *(const int32_t *)a, y = *(const int32_t *)b;
@@ -755,19 +858,6 @@ void gac_axt_chains_free(gac_axt_chains *c) {
     free(c);
 }
 
-typedef struct bkey { /* removeExactOverlaps: slSort(cBlockCmpBoth) */
-    int32_t qs, ts, rank, qe, te;
-} bkey;
-
-static int bkey_cmp(const void *a, const void *b) {
-    const bkey *x = a, *y = b;
-    if (x->qs != y->qs)
-        return x->qs < y->qs ? -1 : 1;
-    if (x->ts != y->ts)
-        return x->ts < y->ts ? -1 : 1;
-    return (x->rank > y->rank) - (x->rank < y->rank);
-}
-
 int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
                   const gac_axt_input *in, double min_score, int n_threads,
                   const char *details_path, gac_axt_chains **out) {
@@ -776,9 +866,11 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
         (in->n_pairs && (!in->t_seq || !in->q_seq || !in->q_strand || !in->blk_off)))
         return gac_fail(GAC_E_ARG, "gac_axt_chain: bad argument");
     *out = NULL;
+    double tclock = now_s();
     int rc = gac_set_scoring(ctx, mat, g);
     if (rc != GAC_OK)
         return rc;
+    stage("set scoring", &tclock);
     const int64_t np = in->n_pairs;
     const int64_t nin = np ? in->blk_off[np] : 0;
     /* ---- removeExactOverlaps per pair (axtChain.c:173-197) */
@@ -787,10 +879,7 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
     int32_t *ts = malloc((size_t)(nin ? nin : 1) * 4), *te = malloc((size_t)(nin ? nin : 1) * 4);
     int32_t *bsz = malloc((size_t)(nin ? nin : 1) * 4);
     ax_pairinfo *info = calloc((size_t)(np ? np : 1), sizeof(ax_pairinfo));
-    poff[0] = 0;
-    int64_t nb = 0;
     for (int64_t p = 0; p < np; ++p) {
-        const int64_t a = in->blk_off[p], b = in->blk_off[p + 1];
         info[p].tname = gac_genome_seq_name(ctx, GAC_T, in->t_seq[p]);
         info[p].qname = gac_genome_seq_name(ctx, GAC_Q, in->q_seq[p]);
         info[p].tsize = gac_genome_seq_size(ctx, GAC_T, in->t_seq[p]);
@@ -800,28 +889,24 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
             rc = gac_fail(GAC_E_ARG, "gac_axt_chain: pair %lld: bad sequence index", (long long)p);
             goto fail;
         }
-        bkey *k = malloc((size_t)(b > a ? b - a : 1) * sizeof(bkey));
-        for (int64_t i = a; i < b; ++i)
-            k[i - a] = (bkey){in->blk_q[i], in->blk_t[i], (int32_t)(i - a),
-                              in->blk_q[i] + in->blk_size[i], in->blk_t[i] + in->blk_size[i]};
-        qsort(k, (size_t)(b - a), sizeof(bkey), bkey_cmp);
+    }
+    const int nthreads = thread_count(n_threads);
+    {
+        /* every pair folds in parallel into its own input slot, then the
+         * slots are compacted in pair order */
+        fold_job F = {in, qs, qe, ts, te, poff, np, 0};
+        atomic_init(&F.next, 0);
+        run_threads(nthreads < np ? nthreads : (int)(np ? np : 1), fold_thread, &F);
+    }
+    int64_t nb = 0;
+    for (int64_t p = 0; p < np; ++p) {
+        const int64_t a = in->blk_off[p], c = poff[p + 1]; /* c: folded count of pair p */
+        memmove(qs + nb, qs + a, (size_t)c * 4);
+        memmove(qe + nb, qe + a, (size_t)c * 4);
+        memmove(ts + nb, ts + a, (size_t)c * 4);
+        memmove(te + nb, te + a, (size_t)c * 4);
         const int64_t first = nb;
-        for (int64_t i = 0; i < b - a; ++i) {
-            if (nb > first && k[i].qs == qs[nb - 1] && k[i].ts == ts[nb - 1]) {
-                if (qe[nb - 1] < k[i].qe)
-                    qe[nb - 1] = k[i].qe;
-                if (te[nb - 1] < k[i].te)
-                    te[nb - 1] = k[i].te;
-                continue;
-            }
-            qs[nb] = k[i].qs;
-            qe[nb] = k[i].qe;
-            ts[nb] = k[i].ts;
-            te[nb] = k[i].te;
-            ++nb;
-        }
-        free(k);
-        poff[p + 1] = nb;
+        nb += c;
         /* checkBlockRange (axtChain.c:242-248), query then target per block */
         for (int64_t i = first; i < nb; ++i) {
             if (qe[i] > info[p].qsize) {
@@ -836,6 +921,10 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
             }
         }
     }
+    poff[0] = 0;
+    for (int64_t p = 0; p < np; ++p)
+        poff[p + 1] += poff[p];
+    stage("removeExactOverlaps", &tclock);
     /* ---- axtScoreUngapped of every block: one GPU batch */
     int32_t *score = malloc((size_t)(nb ? nb : 1) * 4);
     for (int64_t i = 0; i < nb; ++i)
@@ -845,6 +934,7 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
         free(score);
         goto fail;
     }
+    stage("GPU block scores", &tclock);
     /* ---- host gap-cost table + code matrix */
     ax_env env;
     memset(&env, 0, sizeof(env));
@@ -855,7 +945,7 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
             for (int tc = 0; tc < 5; ++tc)
                 env.m5[qc * 5 + tc] =
                     (qc == 4 || tc == 4) ? 0 : mat[acgt_of_code[qc] * 4 + acgt_of_code[tc]];
-        int len = 1 << 20;
+        int len = 1 << 15;
         env.gtab_len = len;
         env.gtab = malloc((size_t)3 * len * sizeof(int32_t));
         for (int d = 0; d < len; ++d) {
@@ -864,6 +954,7 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
             env.gtab[2 * len + d] = d >= 2 ? gac_gap_cost(g, 1, d - 1) : gac_gap_cost(g, 0, 0);
         }
     }
+    stage("host gap table", &tclock);
     /* ---- chainBlocks + overlap removal per pair on host threads */
     ax_out *po = calloc((size_t)(np ? np : 1), sizeof(ax_out));
     int32_t *order = malloc((size_t)(np ? np : 1) * sizeof(int32_t));
@@ -890,16 +981,25 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
     atomic_init(&J.next, 0);
     J.out = po;
     J.want_details = details_path != NULL;
-    int nt = thread_count(n_threads);
+    int nt = nthreads;
     if (nt > np)
         nt = np > 0 ? (int)np : 1;
-    pthread_t *th = malloc((size_t)nt * sizeof(pthread_t));
-    for (int i = 1; i < nt; ++i)
-        pthread_create(&th[i], NULL, ax_thread, &J);
-    ax_thread(&J);
-    for (int i = 1; i < nt; ++i)
-        pthread_join(th[i], NULL);
-    free(th);
+    run_threads(nt, ax_thread, &J);
+    stage("kd-tree DP (threads)", &tclock);
+    if (getenv("GAC_TIMING")) {
+        double sum = 0, mx = 0;
+        int64_t imx = 0;
+        for (int64_t p = 0; p < np; ++p) {
+            sum += po[p].secs;
+            if (po[p].secs > mx) {
+                mx = po[p].secs;
+                imx = p;
+            }
+        }
+        fprintf(stderr, "[gac_axt_chain] %d threads, %lld pairs, %lld blocks: sum %.3f s, largest "
+                        "pair %lld (%lld blocks) %.3f s\n", nt, (long long)np, (long long)nb, sum,
+                (long long)imx, (long long)(poff[imx + 1] - poff[imx]), mx);
+    }
     free(env.gtab);
     free(score);
     free(order);
@@ -964,6 +1064,7 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
                 rc = gac_score_ranges(ctx, set, rg, nc, 0, gsc, NULL, gali);
             gac_chains_free(set);
         }
+        stage("GPU chain scores", &tclock);
         if (rc == GAC_OK) {
             /* minScore filter; slAddHead onto the master list (reversed),
              * then slSort(chainCmpScore) -- stable */
@@ -1028,6 +1129,7 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
         free(po[p].details);
     }
     free(po);
+    stage("filter + sort", &tclock);
     if (rc == GAC_OK)
         *out = R;
 fail:

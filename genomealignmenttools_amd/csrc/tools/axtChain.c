@@ -22,6 +22,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "gac_tool.h"
 #include "gachain.h"
@@ -423,6 +424,12 @@ static void load_fasta(gac_ctx *ctx, int side, const char *path) {
     gt_check(gac_genome_finalize(ctx, side));
 }
 
+static double wall(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
 /* ------------------------------------------------------------ main */
 int main(int argc, char *argv[]) {
     gt_options_hash(&argc, argv);
@@ -462,6 +469,7 @@ int main(int argc, char *argv[]) {
         FILE *d = gt_must_open(details, "w");
         fclose(d);
     }
+    double t0 = wall();
     pairs P;
     memset(&P, 0, sizeof(P));
     const int psl = gt_opt_exists("psl");
@@ -476,6 +484,8 @@ int main(int argc, char *argv[]) {
     if (!psl)
         qsort(ord, (size_t)P.n, sizeof(pair *), pair_cmp); /* keys are distinct */
 
+    gt_verbose(2, "read %d pairs from %s in %.3f s\n", P.n, in, wall() - t0);
+    t0 = wall();
     gac_ctx *ctx = NULL;
     gt_check(gac_open(0, &ctx));
     if (fa_t) {
@@ -526,6 +536,8 @@ int main(int argc, char *argv[]) {
         memcpy(bq + boff[i], p->bq, (size_t)p->nb * 4);
         memcpy(bs + boff[i], p->bs, (size_t)p->nb * 4);
     }
+    gt_verbose(2, "device + genomes in %.3f s\n", wall() - t0);
+    t0 = wall();
     gac_axt_input ai = {np, tseq, qseq, strand, boff, bt, bq, bs};
     gac_axt_chains *ch = NULL;
     gt_check(gac_axt_chain(ctx, mat, gap, &ai, (double)min_score, 0, details, &ch));
@@ -539,6 +551,7 @@ int main(int argc, char *argv[]) {
                            ch->blk_size + b0, ch->blk_off[c + 1] - b0);
     }
     gt_careful_close(f, out_path);
+    gt_verbose(2, "chaining + writing in %.3f s\n", wall() - t0);
     gt_verbose(2, "%lld pairs, %lld blocks, %lld chains\n", (long long)np, (long long)nb,
                (long long)ch->n_chains);
     gac_axt_chains_free(ch);

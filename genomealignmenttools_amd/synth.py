@@ -667,3 +667,118 @@ def write_psl(tg: Genome, qg: Genome, recs, path: str, header: bool = True) -> N
             f.write("\t" + "".join(f"{s}," for a, b, s in blocks))
             f.write("\t" + "".join(f"{b}," for a, b, s in blocks))
             f.write("\t" + "".join(f"{a}," for a, b, s in blocks) + "\n")
+
+
+def psl_c4(seed: int = 7, n_blocks: int = 2_000_000, n_t: int = 4, n_q: int = 3,
+           tsize: int = 60_000_000, qsize: int = 50_000_000, collinear: float = 0.8,
+           alpha: float = 1.2):
+    """SURVEY §8(d) C4 at a chosen size: n_blocks PSL blocks over n_t x n_q
+    chromosome pairs x 2 strands, power-law blocks per pair, `collinear` of
+    them on planted collinear paths (mutated copies, gaps mostly short) and
+    the rest random.  Vectorised; returns (tg, qg, recs-as-arrays) where
+    recs = dict(pair arrays: qname, strand, tname; per-block arrays:
+    rec (record id), t, q, size; per-record pair index)."""
+    rng = np.random.default_rng(seed)
+    tg = random_genome({f"chr{i + 1}": tsize for i in range(n_t)}, seed, n_frac=0.001,
+                       n_mean=2000)
+    qg = random_genome({f"chrQ{i + 1}": qsize for i in range(n_q)}, seed + 1, n_frac=0.001,
+                       n_mean=2000)
+    pairs = [(ti, qi, s) for ti in range(n_t) for qi in range(n_q) for s in (0, 1)]
+    w = 1.0 / np.arange(1, len(pairs) + 1) ** alpha
+    w = w[rng.permutation(len(pairs))]
+    per_pair = np.maximum(50, (w / w.sum() * n_blocks).astype(np.int64))
+    out_t, out_q, out_s, out_pair, out_rec = [], [], [], [], []
+    rec_base = 0
+    mat = matrix_by_code(_BLASTZ_ACGT)
+    for pi, (ti, qi, strand) in enumerate(pairs):
+        nb = int(per_pair[pi])
+        ncol = int(nb * collinear)
+        # collinear paths of ~200 blocks each
+        npath = max(1, ncol // 200)
+        sizes = np.minimum(rng.geometric(1 / 50, ncol), 500).astype(np.int64)
+        mode = rng.integers(0, 3, ncol)
+        g = np.where(rng.random(ncol) < 0.8, rng.integers(1, 60, ncol),
+                     rng.integers(60, 5000, ncol))
+        dt = np.where(mode == 1, 0, g)
+        dq = np.where(mode == 0, 0, np.maximum(1, g + rng.integers(-20, 20, ncol)))
+        path = np.minimum(np.arange(ncol) * npath // max(ncol, 1), npath - 1)
+        first = np.r_[True, path[1:] != path[:-1]]
+        tstep = np.where(first, 0, np.r_[0, (sizes + dt)[:-1]])
+        qstep = np.where(first, 0, np.r_[0, (sizes + dq)[:-1]])
+        # path origins
+        span_t = np.bincount(path, weights=sizes + dt, minlength=npath)
+        span_q = np.bincount(path, weights=sizes + dq, minlength=npath)
+        t0 = (rng.random(npath) * np.maximum(1, tsize - span_t - 1)).astype(np.int64)
+        q0 = (rng.random(npath) * np.maximum(1, qsize - span_q - 1)).astype(np.int64)
+        ct = np.cumsum(tstep) - np.repeat(np.cumsum(tstep)[first], np.bincount(path))
+        cq = np.cumsum(qstep) - np.repeat(np.cumsum(qstep)[first], np.bincount(path))
+        bt = t0[path] + ct
+        bq = q0[path] + cq
+        ok = (bt + sizes < tsize) & (bq + sizes < qsize)
+        bt, bq, sizes, path = bt[ok], bq[ok], sizes[ok], path[ok]
+        # plant homology (12% substitutions)
+        tc = tg.codes[ti]
+        qc = qg.codes[qi]
+        rep = np.repeat(np.arange(len(sizes)), sizes)
+        within = np.arange(sizes.sum()) - np.repeat(np.cumsum(sizes) - sizes, sizes)
+        tpos = bt[rep] + within
+        rpos = bq[rep] + within
+        m = _mutate(rng, tc[tpos], 0.12)
+        fpos = rpos if strand == 0 else qsize - 1 - rpos
+        qc[fpos] = m if strand == 0 else m ^ 2
+        # random blocks
+        nr = nb - ncol
+        rs = rng.integers(20, 300, nr)
+        rt = rng.integers(0, tsize - 400, nr)
+        rq = rng.integers(0, qsize - 400, nr)
+        # records: collinear blocks in runs of 1..8 consecutive blocks
+        k = rng.integers(1, 9, len(sizes))
+        rec_c = np.cumsum(np.r_[0, (np.arange(1, len(sizes)) % 5 == 0) |
+                                (path[1:] != path[:-1])]) if len(sizes) else np.zeros(0, np.int64)
+        del k
+        rec_r = np.arange(nr) + (rec_c[-1] + 1 if len(rec_c) else 0)
+        out_t += [bt, rt]
+        out_q += [bq, rq]
+        out_s += [sizes, rs]
+        out_pair += [np.full(len(sizes) + nr, pi, np.int32)]
+        out_rec += [rec_base + rec_c, rec_base + rec_r]
+        rec_base += int((rec_r[-1] + 1) if nr else (rec_c[-1] + 1 if len(rec_c) else 0))
+    blocks = dict(t=np.concatenate(out_t).astype(np.int64), q=np.concatenate(out_q).astype(np.int64),
+                  size=np.concatenate(out_s).astype(np.int64),
+                  pair=np.concatenate(out_pair), rec=np.concatenate(out_rec).astype(np.int64))
+    return tg, qg, pairs, blocks
+
+
+def write_psl_c4(tg: Genome, qg: Genome, pairs, blocks, path: str, seed: int = 7) -> int:
+    """PSL text of psl_c4 blocks: one line per record, records in a seeded
+    random order (as lastz output of many jobs would be concatenated)."""
+    rng = np.random.default_rng(seed + 99)
+    rec = blocks["rec"]
+    order = np.argsort(rec, kind="stable")
+    rec_s = rec[order]
+    starts = np.r_[0, np.nonzero(rec_s[1:] != rec_s[:-1])[0] + 1]
+    ends = np.r_[starts[1:], len(rec_s)]
+    perm = rng.permutation(len(starts))
+    tnames = tg.names
+    qnames = qg.names
+    tsz = tg.sizes
+    qsz = qg.sizes
+    with open(path, "w") as f:
+        for r in perm:
+            idx = order[starts[r]:ends[r]]
+            pi = int(blocks["pair"][idx[0]])
+            ti, qi, strand = pairs[pi]
+            bt = blocks["t"][idx]
+            bq = blocks["q"][idx]
+            bs = blocks["size"][idx]
+            o = np.lexsort((bq, bt))
+            bt, bq, bs = bt[o], bq[o], bs[o]
+            tn, qn = tnames[ti], qnames[qi]
+            qs, qe = int(bq.min()), int((bq + bs).max())
+            if strand:
+                qs, qe = qsz[qn] - qe, qsz[qn] - qs
+            f.write(f"0\t0\t0\t0\t0\t0\t0\t0\t{'+-'[strand]}\t{qn}\t{qsz[qn]}\t{qs}\t{qe}\t{tn}\t"
+                    f"{tsz[tn]}\t{int(bt[0])}\t{int((bt + bs).max())}\t{len(bt)}\t"
+                    + "".join(f"{x}," for x in bs) + "\t" + "".join(f"{x}," for x in bq)
+                    + "\t" + "".join(f"{x}," for x in bt) + "\n")
+    return len(starts)

@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""End-to-end tool timings beside the reference binaries (SURVEY §8(d)
+configs C3/C4), on the GPU box's own host.
+
+  python scripts/bench_tools.py axtchain --blocks 5000000
+  python scripts/bench_tools.py cleaner --loci 2000
+
+axtchain: synth.psl_c4 (seeded C4-like PSL: power-law blocks per chromosome
+pair, 80% planted collinear, 20% random), run by bin/axtChain and by the
+reference axtChain compiled from /root/reference (oracle/_ref/axtChain,
+test infrastructure; timed as the CPU baseline), outputs compared byte for
+byte.  cleaner: synth.cleaner_case at scale, chainNet -minScore=0 + the
+in-process filter via bin/chainCleaner without -net vs the reference
+chainCleaner given the reference chainNet|NetFilterNonNested net (timed
+separately).  Prints one JSON line per run; files go to --tmp.
+"""
+import argparse
+import filecmp
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+from genomealignmenttools_amd import chainfile, synth  # noqa: E402
+
+BIN = os.path.join(REPO, "genomealignmenttools_amd", "bin")
+REF = os.path.join(REPO, "oracle", "_ref")
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def timed(cmd, cwd=None, env=None, timeout=3000):
+    t = time.time()
+    r = subprocess.run(cmd, capture_output=True, text=True, cwd=cwd, env=env, timeout=timeout)
+    dt = time.time() - t
+    if r.returncode != 0:
+        raise RuntimeError(f"{cmd} failed rc={r.returncode}: {r.stderr[-3000:]}")
+    return dt, r
+
+
+def sha(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for b in iter(lambda: f.read(1 << 20), b""):
+            h.update(b)
+    return h.hexdigest()[:16]
+
+
+def axtchain(a):
+    d = os.path.join(a.tmp, f"c4_{a.blocks}")
+    os.makedirs(d, exist_ok=True)
+    psl = os.path.join(d, "in.psl")
+    if not os.path.exists(psl):
+        t = time.time()
+        tg, qg, pairs, b = synth.psl_c4(a.seed, a.blocks, tsize=a.tsize, qsize=a.qsize)
+        synth.write_2bit(tg, os.path.join(d, "t.2bit"))
+        synth.write_2bit(qg, os.path.join(d, "q.2bit"))
+        nrec = synth.write_psl_c4(tg, qg, pairs, b, psl, a.seed)
+        log(f"generated {len(b['t'])} blocks, {nrec} records in {time.time() - t:.1f}s")
+    env = dict(os.environ, GAC_TIMING="1")
+    args = ["-psl", psl, os.path.join(d, "t.2bit"), os.path.join(d, "q.2bit")]
+    ours = os.path.join(d, "ours.chain")
+    t_ours, r = timed([os.path.join(BIN, "axtChain"), "-linearGap=loose", "-verbose=0"] + args +
+                      [ours], env=env)
+    log(r.stderr)
+    res = {"tool": "axtChain", "blocks": a.blocks, "seed": a.seed, "ours_s": round(t_ours, 3),
+           "ours_sha": sha(ours), "timing": [l for l in r.stderr.splitlines() if "gac_axt" in l]}
+    refbin = os.path.join(REF, "axtChain")
+    if os.path.exists(refbin) and not a.no_ref:
+        ref = os.path.join(d, "ref.chain")
+        t_ref, _ = timed([refbin, "-linearGap=loose", "-verbose=0"] + args + [ref])
+        res.update(ref_s=round(t_ref, 3), ref_cores=1, identical=filecmp.cmp(ours, ref, False),
+                   speedup=round(t_ref / t_ours, 2))
+    res["chains"] = sum(1 for line in open(ours) if line.startswith("chain"))
+    print(json.dumps(res), flush=True)
+
+
+def cleaner(a):
+    d = os.path.join(a.tmp, f"c3_{a.loci}")
+    os.makedirs(d, exist_ok=True)
+    inc = os.path.join(d, "in.chain")
+    if not os.path.exists(inc):
+        t = time.time()
+        tg, qg, chains = synth.cleaner_case(a.seed, a.loci)
+        synth.write_2bit(tg, os.path.join(d, "t.2bit"))
+        synth.write_2bit(qg, os.path.join(d, "q.2bit"))
+        synth.write_sizes(tg.sizes, os.path.join(d, "t.sizes"))
+        synth.write_sizes(qg.sizes, os.path.join(d, "q.sizes"))
+        ca = synth.chains_to_arrays(tg, qg, chains)
+        chainfile.write_chains(ca, os.path.join(d, "unscored.chain"))
+        # header scores from our own scoreChain (byte-identical to the reference's)
+        timed([os.path.join(BIN, "scoreChain"), os.path.join(d, "unscored.chain"),
+               os.path.join(d, "t.2bit"), os.path.join(d, "q.2bit"), os.path.join(d, "sc.chain"),
+               "-linearGap=loose"])
+        sc = chainfile.read_chains(os.path.join(d, "sc.chain"))
+        import numpy as np
+        order = np.argsort(-sc.score, kind="stable")
+        sc = sc.subset(order)
+        sc.id = np.arange(1, sc.n + 1, dtype=np.int64)
+        chainfile.write_chains(sc, inc)
+        log(f"generated {sc.n} chains in {time.time() - t:.1f}s")
+    p = lambda x: os.path.join(d, x)
+    t_ours, r = timed([os.path.join(BIN, "chainCleaner"), inc, p("t.2bit"), p("q.2bit"),
+                       p("ours.chain"), p("ours.bed"), f"-tSizes={p('t.sizes')}",
+                       f"-qSizes={p('q.sizes')}", "-linearGap=loose", "-verbose=1"], cwd=d)
+    res = {"tool": "chainCleaner", "loci": a.loci, "seed": a.seed, "ours_s": round(t_ours, 3),
+           "removed": sum(1 for _ in open(p("ours.bed"))),
+           "gpu": [l for l in r.stderr.splitlines() if l.startswith("GPU:")]}
+    if os.path.exists(os.path.join(REF, "chainCleaner")) and not a.no_ref:
+        env = dict(os.environ, PATH=REF + os.pathsep + os.environ.get("PATH", ""))
+        t_net, rn = timed([os.path.join(REF, "chainNet"), "-minScore=0", inc, p("t.sizes"),
+                           p("q.sizes"), "stdout", "/dev/null"])
+        t0 = time.time()
+        # the reference's perl filter when /root/reference is present (build
+        # container), else the product's C port (bin/NetFilterNonNested)
+        perl = "/root/reference/src/NetFilterNonNested.perl"
+        filt = (["perl", perl] if os.path.exists(perl) else
+                [os.path.join(BIN, "NetFilterNonNested")])
+        net = subprocess.run(filt + ["/dev/stdin", "-minScore1", "3000"], input=rn.stdout,
+                             capture_output=True, text=True)
+        res["ref_filter"] = "perl" if filt[0] == "perl" else "bin/NetFilterNonNested"
+        t_filter = time.time() - t0
+        if net.returncode == 0:
+            with open(p("ref.net"), "w") as f:
+                f.write(net.stdout)
+            t_ref, _ = timed([os.path.join(REF, "chainCleaner"), inc, p("t.2bit"), p("q.2bit"),
+                              p("ref.chain"), p("ref.bed"), f"-net={p('ref.net')}",
+                              "-linearGap=loose", "-verbose=0"], cwd=d, env=env)
+            res.update(ref_s=round(t_net + t_filter + t_ref, 3), ref_net_s=round(t_net, 3),
+                       ref_filter_s=round(t_filter, 3), ref_clean_s=round(t_ref, 3), ref_cores=1,
+                       identical=filecmp.cmp(p("ours.chain"), p("ref.chain"), False)
+                       and filecmp.cmp(p("ours.bed"), p("ref.bed"), False))
+            res["speedup"] = round(res["ref_s"] / t_ours, 2)
+        else:
+            res["ref_error"] = "perl filter unavailable: " + net.stderr[-200:]
+    print(json.dumps(res), flush=True)
+
+
+def c2_files(a):
+    """C2: hg38 chr1 x all mm10, ~2e5 planted chains, seed 42,
+    written once under --tmp (2bit genomes, chrom.sizes, chains)."""
+    d = os.path.join(a.tmp, f"c2_{a.chains}_{a.seed}")
+    os.makedirs(d, exist_ok=True)
+    if not os.path.exists(os.path.join(d, "in.chain")):
+        t = time.time()
+        tg, qg, ca = synth.c2_case(a.seed, a.chains)
+        synth.write_2bit(tg, os.path.join(d, "t.2bit"))
+        synth.write_2bit(qg, os.path.join(d, "q.2bit"))
+        synth.write_sizes(tg.sizes, os.path.join(d, "t.sizes"))
+        synth.write_sizes(qg.sizes, os.path.join(d, "q.sizes"))
+        chainfile.write_chains(ca, os.path.join(d, "in.chain"))
+        log(f"C2: {ca.n} chains, {ca.aligned_bases()} aligned bases, {time.time() - t:.1f}s")
+    return d
+
+
+def scorechain(a):
+    d = c2_files(a)
+    p = lambda x: os.path.join(d, x)
+    args = [p("in.chain"), p("t.2bit"), p("q.2bit")]
+    t_ours, r = timed([os.path.join(BIN, "scoreChain")] + args + [p("ours.chain"), "-linearGap=loose",
+                                                                  "-verbose=2"])
+    res = {"tool": "scoreChain", "chains": a.chains, "seed": a.seed, "ours_s": round(t_ours, 3),
+           "stages": [l for l in r.stderr.splitlines() if " s" in l][-8:]}
+    if os.path.exists(os.path.join(REF, "scoreChain")) and not a.no_ref:
+        t_ref, _ = timed([os.path.join(REF, "scoreChain")] + args + [p("ref.chain"),
+                                                                     "-linearGap=loose"])
+        res.update(ref_s=round(t_ref, 3), ref_cores=1, speedup=round(t_ref / t_ours, 2),
+                   identical=filecmp.cmp(p("ours.chain"), p("ref.chain"), False))
+    print(json.dumps(res), flush=True)
+
+
+def chainnet(a):
+    d = c2_files(a)
+    p = lambda x: os.path.join(d, x)
+    args = [p("in.chain"), p("t.sizes"), p("q.sizes")]
+    opts = ["-rescore", f"-tNibDir={p('t.2bit')}", f"-qNibDir={p('q.2bit')}", "-linearGap=loose"]
+    t_ours, r = timed([os.path.join(BIN, "chainNet")] + args + [p("ours.t.net"), p("ours.q.net")] +
+                      opts + ["-verbose=2"])
+    res = {"tool": "chainNet -rescore", "chains": a.chains, "seed": a.seed,
+           "ours_s": round(t_ours, 3),
+           "stages": [l for l in r.stderr.splitlines() if " s" in l][-8:]}
+    if os.path.exists(os.path.join(REF, "chainNet")) and not a.no_ref:
+        t_ref, _ = timed([os.path.join(REF, "chainNet")] + args + [p("ref.t.net"), p("ref.q.net")] +
+                         opts)
+        res.update(ref_s=round(t_ref, 3), ref_cores=1, speedup=round(t_ref / t_ours, 2),
+                   identical=filecmp.cmp(p("ours.t.net"), p("ref.t.net"), False)
+                   and filecmp.cmp(p("ours.q.net"), p("ref.q.net"), False))
+    print(json.dumps(res), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tool", choices=["axtchain", "cleaner", "scorechain", "chainnet"])
+    ap.add_argument("--chains", type=int, default=200_000)
+    ap.add_argument("--blocks", type=int, default=2_000_000)
+    ap.add_argument("--tsize", type=int, default=60_000_000)
+    ap.add_argument("--qsize", type=int, default=50_000_000)
+    ap.add_argument("--loci", type=int, default=2000)
+    ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--no-ref", action="store_true")
+    ap.add_argument("--tmp", default=os.environ.get("TMPDIR", "/tmp"))
+    a = ap.parse_args()
+    if a.seed is None:
+        a.seed = 42 if a.tool in ("scorechain", "chainnet") else 7
+    {"axtchain": axtchain, "cleaner": cleaner, "scorechain": scorechain,
+     "chainnet": chainnet}[a.tool](a)
+
+
+if __name__ == "__main__":
+    main()
