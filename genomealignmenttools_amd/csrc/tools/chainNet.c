@@ -89,6 +89,7 @@ int main(int argc, char *argv[]) {
     const char *tnet = argv[4], *qnet = argv[5];
 
     gt_sizes qs, ts;
+    gt_stage(NULL);
     gt_read_sizes(qsizes_file, &qs);
     gt_read_sizes(tsizes_file, &ts);
     gt_verbose(1, "Got %d chroms in %s, %d in %s\n", ts.names.n, tsizes_file, qs.names.n,
@@ -103,6 +104,7 @@ int main(int argc, char *argv[]) {
 
     gt_chains c;
     gt_read_chains(chain_file, &c, min_score, 1);
+    gt_stage("read chains");
     int32_t *tix = malloc((c.n ? c.n : 1) * 4), *qix = malloc((c.n ? c.n : 1) * 4);
     double last = -1;
     for (int64_t i = 0; i < c.n; ++i) {
@@ -148,6 +150,7 @@ int main(int argc, char *argv[]) {
     gac_net_opts opt = {min_space, min_fill, min_score, incl_hap};
     gac_net *net = NULL;
     gt_check(gac_net_build(&in, &opt, &net));
+    gt_stage("netting");
     gt_verbose(1, "Finishing nets\n");
 
     int64_t *tscores = NULL;
@@ -171,10 +174,13 @@ int main(int argc, char *argv[]) {
         tscores = calloc(nf ? nf : 1, 8);
         if (nr) {
             gac_ctx *ctx = NULL;
+            gt_stage(NULL);
             gt_check(gac_open(0, &ctx));
+            gt_stage("device open");
             gt_check(gac_set_scoring(ctx, mat, gap));
             gt_check(gac_genome_load_2bit(ctx, GAC_T, tnib));
             gt_check(gac_genome_load_2bit(ctx, GAC_Q, qnib));
+            gt_stage("2bit genomes to HBM");
             /* upload only the chains owning a rescored fill (their sequences
              * must be in the 2bit files; others are never looked up) */
             int32_t *remap = malloc(c.n * 4);
@@ -217,9 +223,11 @@ int main(int argc, char *argv[]) {
             gac_chainset_desc d = {nsub, gts, gqs, gst, goff, nbsub, gbt, gbq, gbs};
             gac_chainset *cs = NULL;
             gt_check(gac_chains_upload(ctx, &d, &cs));
+            gt_stage("chains to HBM");
             int64_t *g = malloc(nr * 8);
             int32_t *ali = malloc(nr * 4);
             gt_check(gac_score_ranges(ctx, cs, r, nr, 0, g, NULL, ali));
+            gt_stage("GPU fill rescoring");
             for (int64_t k = 0; k < nr; ++k)
                 tscores[rix[k]] = g[k];
             free(g);
@@ -248,6 +256,7 @@ int main(int argc, char *argv[]) {
     gt_check(gac_net_write(net, GAC_T, tscores, tnet, (const char *const *)c.meta, c.n_meta));
     gt_verbose(1, "writing %s\n", qnet);
     gt_check(gac_net_write(net, GAC_Q, NULL, qnet, (const char *const *)c.meta, c.n_meta));
+    gt_stage("write nets");
     free(tscores);
     gac_net_free(net);
     gac_gapcalc_free(gap);

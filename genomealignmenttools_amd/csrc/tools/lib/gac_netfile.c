@@ -212,12 +212,18 @@ static double field_num(const char *s) { return atof(s); }
 
 void gt_netfilter_nonnested(const gt_lines *in, const char *what, double s1, double t1,
                             double q1, double s2, double t2, double q2, gt_lines *out) {
-    memset(out, 0, sizeof(*out));
     /* mode "12": an unset set 2 (all zero) -> INT_MAX; an unset set 1 -> INT_MAX */
     if (s2 == 0 && t2 == 0 && q2 == 0)
         s2 = t2 = q2 = INT_MAX;
     if (s1 == 0 && t1 == 0 && q1 == 0)
         s1 = t1 = q1 = INT_MAX;
+    const double sc[2] = {s1, s2}, ts[2] = {t1, t2}, qs[2] = {q1, q2};
+    gt_netfilter_sets(in, what, 2, sc, ts, qs, out);
+}
+
+void gt_netfilter_sets(const gt_lines *in, const char *what, int nsets, const double *set_score,
+                       const double *set_t, const double *set_q, gt_lines *out) {
+    memset(out, 0, sizeof(*out));
     const int64_t n = in->n;
     char *skip = calloc(n ? n : 1, 1);
     int *minus = calloc(n ? n : 1, sizeof(int));
@@ -286,8 +292,9 @@ void gt_netfilter_nonnested(const gt_lines *in, const char *what, double s1, dou
         }
         const double tsz = nf > 2 ? field_num(f[2]) : 0, qsz = nf > 6 ? field_num(f[6]) : 0;
         free(copy);
-        const int pass = (score >= s1 && tsz >= t1 && qsz >= q1) ||
-                         (score >= s2 && tsz >= t2 && qsz >= q2);
+        int pass = 0;
+        for (int k = 0; k < nsets && !pass; ++k)
+            pass = score >= set_score[k] && tsz >= set_t[k] && qsz >= set_q[k];
         if (pass) {
             kept[cur]++;
         } else {

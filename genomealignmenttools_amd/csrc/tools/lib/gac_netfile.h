@@ -58,6 +58,11 @@ void gt_netset_free(gt_netset *ns);
  * filtered lines (new strings). */
 void gt_netfilter_nonnested(const gt_lines *in, const char *what, double s1, double t1,
                             double q1, double s2, double t2, double q2, gt_lines *out);
+/* the same filter with any number of (score, tSize, qSize) sets: a fill is
+ * kept if it passes all three thresholds of at least one set ("batch" mode,
+ * NetFilterNonNested.perl:368-374; "12" mode is two sets) */
+void gt_netfilter_sets(const gt_lines *in, const char *what, int nsets, const double *set_score,
+                       const double *set_t, const double *set_q, gt_lines *out);
 
 #ifdef __cplusplus
 }

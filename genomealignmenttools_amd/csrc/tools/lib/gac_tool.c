@@ -12,6 +12,7 @@
 #include <string.h>
 #include <sys/stat.h>
 #include <unistd.h>
+#include <time.h>
 #include <zlib.h>
 
 /* ------------------------------------------------------------ errors */
@@ -39,6 +40,16 @@ void gt_verbose(int level, const char *fmt, ...) {
 }
 
 int gt_verbosity(void) { return g_verbose; }
+
+void gt_stage(const char *what) {
+    static double last = -1;
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    const double now = ts.tv_sec + 1e-9 * ts.tv_nsec;
+    if (last >= 0 && what && g_verbose >= 2)
+        fprintf(stderr, "[stage] %-32s %8.3f s\n", what, now - last);
+    last = now;
+}
 
 void gt_check(int rc) {
     if (rc != GAC_OK)

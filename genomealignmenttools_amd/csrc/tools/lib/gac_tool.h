@@ -17,6 +17,8 @@ extern "C" {
 void gt_abort(const char *fmt, ...) __attribute__((noreturn, format(printf, 1, 2)));
 void gt_verbose(int level, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 int gt_verbosity(void);
+/* -verbose>=2: wall time since the previous gt_stage call, labelled */
+void gt_stage(const char *what);
 void gt_check(int rc); /* abort with gac_last_error() unless GAC_OK */
 
 /* ---- options ---- */

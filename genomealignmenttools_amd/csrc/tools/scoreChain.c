@@ -73,14 +73,18 @@ int main(int argc, char *argv[]) {
         gt_abort("ERROR: only 2bit files are supported, not %s\n", q2bit);
 
     gac_ctx *ctx = NULL;
+    gt_stage(NULL);
     gt_check(gac_open(0, &ctx));
+    gt_stage("device open");
     gt_check(gac_set_scoring(ctx, mat, gap));
     gt_check(gac_genome_load_2bit(ctx, GAC_T, t2bit));
     gt_check(gac_genome_load_2bit(ctx, GAC_Q, q2bit));
+    gt_stage("2bit genomes to HBM");
 
     FILE *out = gt_must_open(argv[4], "w");
     gt_chains c;
     gt_read_chains(argv[1], &c, -HUGE_VAL, 0);
+    gt_stage("read chains");
 
     /* resolve sequence names (twoBitReadSeqFrag aborts on unknown names) */
     int32_t *tseq = malloc((c.n ? c.n : 1) * 4), *qseq = malloc((c.n ? c.n : 1) * 4);
@@ -95,6 +99,7 @@ int main(int argc, char *argv[]) {
     gac_chainset_desc d = {c.n, tseq, qseq, c.qstrand, c.blk_off, c.nb, c.bt, c.bq, c.bs};
     gac_chainset *cs = NULL;
     gt_check(gac_chains_upload(ctx, &d, &cs));
+    gt_stage("chains to HBM");
     gac_range *r = malloc((c.n ? c.n : 1) * sizeof(gac_range));
     for (int64_t i = 0; i < c.n; ++i) {
         r[i].chain = (int32_t)i;
@@ -104,6 +109,7 @@ int main(int argc, char *argv[]) {
     int64_t *glob = malloc((c.n ? c.n : 1) * 8), *loc = malloc((c.n ? c.n : 1) * 8);
     int32_t *ali = malloc((c.n ? c.n : 1) * 4);
     gt_check(gac_score_ranges(ctx, cs, r, c.n, GAC_WANT_LOCAL, glob, loc, ali));
+    gt_stage("GPU scoring");
 
     static char obuf[1 << 22];
     setvbuf(out, obuf, _IOFBF, sizeof(obuf));
@@ -129,6 +135,7 @@ int main(int argc, char *argv[]) {
         }
     }
     gt_careful_close(out, argv[4]);
+    gt_stage("write output");
     free(r);
     free(glob);
     free(loc);

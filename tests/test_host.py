@@ -199,3 +199,19 @@ def test_no_cpu_fallback_without_gpu():
         pytest.skip("GPU present")
     with pytest.raises(GacError, match="no CPU fallback"):
         Engine(0)
+
+
+@pytest.mark.parametrize("net", ["synth11", "synth12q", "cleaner"])
+@pytest.mark.parametrize("case", ["s3000", "two_sets", "eq", "batch"])
+def test_netfilter_nonnested_vs_reference(net, case):
+    """bin/NetFilterNonNested.perl (native, host only) byte-identical to the
+    reference perl script on reference chainNet nets ("12" and batch modes)."""
+    import json
+    from genomealignmenttools_amd._lib import BIN_DIR
+    d = os.path.join(GOLDEN, "netfilter")
+    with open(os.path.join(d, "cases.json")) as f:
+        opts = json.load(f)[case]
+    r = subprocess.run([os.path.join(BIN_DIR, "NetFilterNonNested.perl"),
+                        os.path.join(d, f"{net}.net")] + opts, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout == open(os.path.join(d, f"{net}.{case}.out")).read()
