@@ -122,10 +122,10 @@ def cleaner(a):
         # container), else the product's C port (bin/NetFilterNonNested)
         perl = "/root/reference/src/NetFilterNonNested.perl"
         filt = (["perl", perl] if os.path.exists(perl) else
-                [os.path.join(BIN, "NetFilterNonNested")])
+                [os.path.join(BIN, "NetFilterNonNested.perl")])
         net = subprocess.run(filt + ["/dev/stdin", "-minScore1", "3000"], input=rn.stdout,
                              capture_output=True, text=True)
-        res["ref_filter"] = "perl" if filt[0] == "perl" else "bin/NetFilterNonNested"
+        res["ref_filter"] = "perl" if filt[0] == "perl" else "bin/NetFilterNonNested.perl"
         t_filter = time.time() - t0
         if net.returncode == 0:
             with open(p("ref.net"), "w") as f:
