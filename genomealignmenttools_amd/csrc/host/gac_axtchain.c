@@ -728,29 +728,11 @@ static void *ax_thread(void *arg) {
 static int thread_count(int req) {
     if (req > 0)
         return req > 256 ? 256 : req;
-    const char *s = getenv("GAC_THREADS");
-    if (!s || !*s)
-        s = getenv("OMP_NUM_THREADS");
-    int n = s && *s ? atoi(s) : 0;
-    if (n <= 0) {
-        const long c = sysconf(_SC_NPROCESSORS_ONLN);
-        n = c > 0 ? (int)c : 1;
-    }
-    return n > 64 ? 64 : n;
+    return gac_host_threads();
 }
 
 /* ------------------------------------------------------------------ parallel helpers */
-static void run_threads(int nt, void *(*fn)(void *), void *arg) {
-    if (nt < 1)
-        nt = 1;
-    pthread_t *th = malloc((size_t)nt * sizeof(pthread_t));
-    for (int i = 1; i < nt; ++i)
-        pthread_create(&th[i], NULL, fn, arg);
-    fn(arg);
-    for (int i = 1; i < nt; ++i)
-        pthread_join(th[i], NULL);
-    free(th);
-}
+#define run_threads gac_run_threads
 
 typedef struct bkey { /* removeExactOverlaps: slSort(cBlockCmpBoth) */
     int32_t qs, ts, rank, qe, te;

@@ -12,6 +12,9 @@
 #define _GNU_SOURCE
 #include "gac_host.h"
 
+#include <pthread.h>
+#include <unistd.h>
+
 #include <ctype.h>
 #include <errno.h>
 #include <fcntl.h>
@@ -674,4 +677,29 @@ int gac_twobit_open(const char *path, gac_twobit *tb) {
 trunc:
     gac_twobit_close(tb);
     return gac_fail(GAC_E_FORMAT, "%s is truncated", path);
+}
+
+/* ------------------------------------------------------------------- threads */
+int gac_host_threads(void) {
+    const char *s = getenv("GAC_THREADS");
+    if (!s || !*s)
+        s = getenv("OMP_NUM_THREADS");
+    int n = s && *s ? atoi(s) : 0;
+    if (n <= 0) {
+        const long c = sysconf(_SC_NPROCESSORS_ONLN);
+        n = c > 0 ? (int)c : 1;
+    }
+    return n > 64 ? 64 : n;
+}
+
+void gac_run_threads(int n, void *(*fn)(void *), void *arg) {
+    if (n < 1)
+        n = 1;
+    pthread_t *th = malloc((size_t)n * sizeof(pthread_t));
+    for (int i = 1; i < n; ++i)
+        pthread_create(&th[i], NULL, fn, arg);
+    fn(arg);
+    for (int i = 1; i < n; ++i)
+        pthread_join(th[i], NULL);
+    free(th);
 }

@@ -58,6 +58,11 @@ void gac_twobit_close(gac_twobit *tb);
 uint32_t gac_twobit_u32(const gac_twobit *tb, const uint8_t *p);
 int gac_is_twobit_file(const char *path);
 
+/* ---- host threads: GAC_THREADS, else OMP_NUM_THREADS, else all cores (<= 64) */
+int gac_host_threads(void);
+/* fn(arg) on n threads (one of them the caller); fn pulls work itself */
+void gac_run_threads(int n, void *(*fn)(void *), void *arg);
+
 /* ---- host view of a resident sequence (kept after gac_genome_finalize) ----
  * packed: 2 bits/base MSB-first (T=0 C=1 A=2 G=3); N runs merged and sorted. */
 typedef struct gac_seq_view {

@@ -21,7 +21,9 @@
 #define _GNU_SOURCE
 #include "gac_host.h"
 
+#include <stdatomic.h>
 #include <stdio.h>
+#include <time.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -92,37 +94,47 @@ static void arena_free(arena *a) {
     memset(a, 0, sizeof(*a));
 }
 
-struct gac_net {
-    gac_net_input in;
-    gac_net_opts opt;
-    int64_t n_netted;
-    nchrom *chroms[2]; /* [GAC_T], [GAC_Q] */
-    int32_t n_chroms[2];
+/* One netting worker: the side trees of the chromosomes it nets live in its
+ * own space pool and arena (chromosomes are independent: every chain is
+ * added to its target chromosome's tree and to its query chromosome's tree,
+ * each in score order, and nothing else is shared). */
+typedef struct nwork {
     arena ar;
     tnode *tn;
     int32_t tn_n, tn_cap, tn_free;
     uint32_t rng;
-    int64_t *ali_prefix; /* per block prefix of sizes, per chain offset by blk_off */
-    /* pre-order fill index per side */
-    nfill **order[2];
-    int64_t n_order[2];
     /* scratch for findSpaces */
     int32_t *fs;
     int64_t fs_n, fs_cap;
     /* scratch for reversed blocks */
     int32_t *rs, *re, *ros, *roe;
     int64_t r_cap;
+    char pad[64]; /* keep workers' hot fields on separate cache lines */
+} nwork;
+
+struct gac_net {
+    gac_net_input in;
+    gac_net_opts opt;
+    int64_t n_netted;
+    nchrom *chroms[2]; /* [GAC_T], [GAC_Q] */
+    int32_t n_chroms[2];
+    nwork *w;          /* [n_w]; w[0] also holds the finishNet arrays */
+    int n_w;
+    int64_t *ali_prefix; /* per block prefix of sizes, per chain offset by blk_off */
+    /* pre-order fill index per side */
+    nfill **order[2];
+    int64_t n_order[2];
 };
 
 /* ------------------------------------------------------------ treap */
-static uint32_t net_rand(gac_net *n) {
+static uint32_t net_rand(nwork *n) {
     n->rng ^= n->rng << 13;
     n->rng ^= n->rng >> 17;
     n->rng ^= n->rng << 5;
     return n->rng;
 }
 
-static int32_t tn_new(gac_net *n, int start, int end, ngap *gap) {
+static int32_t tn_new(nwork *n, int start, int end, ngap *gap) {
     int32_t i;
     if (n->tn_free >= 0) {
         i = n->tn_free;
@@ -143,13 +155,13 @@ static int32_t tn_new(gac_net *n, int start, int end, ngap *gap) {
     return i;
 }
 
-static void tn_release(gac_net *n, int32_t i) {
+static void tn_release(nwork *n, int32_t i) {
     n->tn[i].l = n->tn_free;
     n->tn_free = i;
 }
 
 /* split by start: l gets starts < key, r gets starts >= key */
-static void tn_split(gac_net *n, int32_t t, int key, int32_t *l, int32_t *r) {
+static void tn_split(nwork *n, int32_t t, int key, int32_t *l, int32_t *r) {
     if (t < 0) {
         *l = *r = -1;
         return;
@@ -163,7 +175,7 @@ static void tn_split(gac_net *n, int32_t t, int key, int32_t *l, int32_t *r) {
     }
 }
 
-static int32_t tn_merge(gac_net *n, int32_t a, int32_t b) {
+static int32_t tn_merge(nwork *n, int32_t a, int32_t b) {
     if (a < 0)
         return b;
     if (b < 0)
@@ -176,13 +188,13 @@ static int32_t tn_merge(gac_net *n, int32_t a, int32_t b) {
     return b;
 }
 
-static void tn_insert(gac_net *n, int32_t *root, int32_t node) {
+static void tn_insert(nwork *n, int32_t *root, int32_t node) {
     int32_t l, r;
     tn_split(n, *root, n->tn[node].start, &l, &r);
     *root = tn_merge(n, tn_merge(n, l, node), r);
 }
 
-static void tn_erase(gac_net *n, int32_t *root, int key) {
+static void tn_erase(nwork *n, int32_t *root, int key) {
     /* spaces are disjoint: start is a unique key */
     int32_t *p = root;
     while (*p >= 0) {
@@ -195,7 +207,7 @@ static void tn_erase(gac_net *n, int32_t *root, int key) {
     }
 }
 
-static void fs_push(gac_net *n, int32_t v) {
+static void fs_push(nwork *n, int32_t v) {
     if (n->fs_n == n->fs_cap) {
         n->fs_cap = n->fs_cap ? n->fs_cap * 2 : 1024;
         n->fs = realloc(n->fs, n->fs_cap * sizeof(int32_t));
@@ -204,7 +216,7 @@ static void fs_push(gac_net *n, int32_t v) {
 }
 
 /* in-order spaces overlapping [qs, qe) (spaceCmp == 0, chainNet.c:277-287) */
-static void tn_range(gac_net *n, int32_t t, int qs, int qe) {
+static void tn_range(nwork *n, int32_t t, int qs, int qe) {
     while (t >= 0) {
         tnode *x = &n->tn[t];
         if (x->end > qs)
@@ -218,11 +230,11 @@ static void tn_range(gac_net *n, int32_t t, int qs, int qe) {
     }
 }
 
-static void add_space_for_gap(gac_net *n, nchrom *c, ngap *g) {
+static void add_space_for_gap(nwork *n, nchrom *c, ngap *g) {
     tn_insert(n, &c->troot, tn_new(n, g->start, g->end, g));
 }
 
-static ngap *gap_new(gac_net *n, int s, int e, int os, int oe) {
+static ngap *gap_new(nwork *n, int s, int e, int os, int oe) {
     ngap *g = arena_alloc(&n->ar, sizeof(ngap));
     g->start = s;
     g->end = e;
@@ -239,9 +251,9 @@ static int strictly_inside(const gac_net *n, int min_start, int max_end, int sta
 /* Generic addChainT/addChainQ on one side.  s[],e[] = this side's block
  * coordinates in list order (+ strand coords), os_gap/oe_gap = other-side
  * gap bounds per block (gap between block b and b+1). */
-static void add_chain_side(gac_net *n, nchrom *c, int32_t chain, int nb, const int32_t *s,
-                           const int32_t *e, const int32_t *gos, const int32_t *goe,
-                           int cstart, int cend) {
+static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int32_t chain, int nb,
+                           const int32_t *s, const int32_t *e, const int32_t *gos,
+                           const int32_t *goe, int cstart, int cend) {
     n->fs_n = 0;
     tn_range(n, c->troot, cstart, cend);
     int64_t nsp = n->fs_n;
@@ -273,7 +285,7 @@ static void add_chain_side(gac_net *n, nchrom *c, int32_t chain, int nb, const i
             if (end < be)
                 end = be;
         }
-        if (end < 0 || end - start < n->opt.min_fill)
+        if (end < 0 || end - start < net->opt.min_fill)
             continue;
         /* fillSpace (chainNet.c:487-523) */
         nfill *f = arena_alloc(&n->ar, sizeof(nfill));
@@ -281,9 +293,9 @@ static void add_chain_side(gac_net *n, nchrom *c, int32_t chain, int nb, const i
         f->end = end;
         f->chain = chain;
         tn_erase(n, &c->troot, sstart);
-        if (start - sstart >= n->opt.min_space)
+        if (start - sstart >= net->opt.min_space)
             tn_insert(n, &c->troot, tn_new(n, sstart, start, sgap));
-        if (send - end >= n->opt.min_space)
+        if (send - end >= net->opt.min_space)
             tn_insert(n, &c->troot, tn_new(n, end, send, sgap));
         f->next = sgap->fill_head;
         sgap->fill_head = f;
@@ -292,7 +304,7 @@ static void add_chain_side(gac_net *n, nchrom *c, int32_t chain, int nb, const i
             int gs = e[b], ge = s[b + 1];
             if (ge >= send)
                 break;
-            if (strictly_inside(n, sstart, send, gs, ge)) {
+            if (strictly_inside(net, sstart, send, gs, ge)) {
                 ngap *g = gap_new(n, gs, ge, gos[b], goe[b]);
                 add_space_for_gap(n, c, g);
                 g->next = f->gap_head;
@@ -304,7 +316,7 @@ static void add_chain_side(gac_net *n, nchrom *c, int32_t chain, int nb, const i
     free(sp);
 }
 
-static void ensure_rev(gac_net *n, int64_t nb) {
+static void ensure_rev(nwork *n, int64_t nb) {
     if (nb > n->r_cap) {
         n->r_cap = nb * 2;
         n->rs = realloc(n->rs, n->r_cap * 4);
@@ -318,63 +330,69 @@ static int is_haplotype(const char *name) {
     return strstr(name, "_hap") != NULL || strstr(name, "_alt") != NULL;
 }
 
-static void add_chain(gac_net *n, int64_t c) {
-    const gac_net_input *in = &n->in;
+/* addChainQ (chainNet.c:610-679) */
+static void add_chain_q(const gac_net *net, nwork *n, int64_t c) {
+    const gac_net_input *in = &net->in;
     const int64_t b0 = in->blk_off[c];
     const int nb = (int)(in->blk_off[c + 1] - b0);
     const int32_t *bt = in->blk_t + b0, *bq = in->blk_q + b0, *bs = in->blk_size + b0;
     const int minus = in->q_strand[c] != 0;
     const int qsize = in->q_sizes[in->q_seq[c]];
     ensure_rev(n, nb);
-    /* ---- addChainQ (chainNet.c:610-679) */
-    {
-        nchrom *qc = &n->chroms[GAC_Q][in->q_seq[c]];
-        int qs = in->q_start[c], qe = in->q_end[c];
-        if (!minus) {
-            for (int b = 0; b < nb; ++b) {
-                n->rs[b] = bq[b];
-                n->re[b] = bq[b] + bs[b];
-                if (b + 1 < nb) {
-                    n->ros[b] = bt[b] + bs[b];
-                    n->roe[b] = bt[b + 1];
-                }
-            }
-        } else {
-            int t = qs;
-            qs = qsize - qe;
-            qe = qsize - t;
-            for (int i = 0; i < nb; ++i) {
-                int j = nb - 1 - i; /* original index */
-                n->rs[i] = qsize - (bq[j] + bs[j]);
-                n->re[i] = qsize - bq[j];
-                if (i + 1 < nb) { /* block = j, next = j-1 */
-                    n->ros[i] = bt[j - 1];
-                    n->roe[i] = bt[j] + bs[j];
-                }
-            }
-        }
-        add_chain_side(n, qc, (int32_t)c, nb, n->rs, n->re, n->ros, n->roe, qs, qe);
-    }
-    /* ---- addChainT (chainNet.c:557-608) */
-    {
-        nchrom *tc = &n->chroms[GAC_T][in->t_seq[c]];
+    nchrom *qc = &net->chroms[GAC_Q][in->q_seq[c]];
+    int qs = in->q_start[c], qe = in->q_end[c];
+    if (!minus) {
         for (int b = 0; b < nb; ++b) {
-            n->rs[b] = bt[b];
-            n->re[b] = bt[b] + bs[b];
+            n->rs[b] = bq[b];
+            n->re[b] = bq[b] + bs[b];
             if (b + 1 < nb) {
-                int qs = bq[b] + bs[b], qe = bq[b + 1];
-                if (minus) {
-                    int t = qs;
-                    qs = qsize - qe;
-                    qe = qsize - t;
-                }
-                n->ros[b] = qs;
-                n->roe[b] = qe;
+                n->ros[b] = bt[b] + bs[b];
+                n->roe[b] = bt[b + 1];
             }
         }
-        add_chain_side(n, tc, (int32_t)c, nb, n->rs, n->re, n->ros, n->roe, in->t_start[c],
-                       in->t_end[c]);
+    } else {
+        int t = qs;
+        qs = qsize - qe;
+        qe = qsize - t;
+        for (int i = 0; i < nb; ++i) {
+            int j = nb - 1 - i; /* original index */
+            n->rs[i] = qsize - (bq[j] + bs[j]);
+            n->re[i] = qsize - bq[j];
+            if (i + 1 < nb) { /* block = j, next = j-1 */
+                n->ros[i] = bt[j - 1];
+                n->roe[i] = bt[j] + bs[j];
+            }
+        }
     }
+    add_chain_side(net, n, qc, (int32_t)c, nb, n->rs, n->re, n->ros, n->roe, qs, qe);
+}
+
+/* addChainT (chainNet.c:557-608) */
+static void add_chain_t(const gac_net *net, nwork *n, int64_t c) {
+    const gac_net_input *in = &net->in;
+    const int64_t b0 = in->blk_off[c];
+    const int nb = (int)(in->blk_off[c + 1] - b0);
+    const int32_t *bt = in->blk_t + b0, *bq = in->blk_q + b0, *bs = in->blk_size + b0;
+    const int minus = in->q_strand[c] != 0;
+    const int qsize = in->q_sizes[in->q_seq[c]];
+    ensure_rev(n, nb);
+    nchrom *tc = &net->chroms[GAC_T][in->t_seq[c]];
+    for (int b = 0; b < nb; ++b) {
+        n->rs[b] = bt[b];
+        n->re[b] = bt[b] + bs[b];
+        if (b + 1 < nb) {
+            int qs = bq[b] + bs[b], qe = bq[b + 1];
+            if (minus) {
+                int t = qs;
+                qs = qsize - qe;
+                qe = qsize - t;
+            }
+            n->ros[b] = qs;
+            n->roe[b] = qe;
+        }
+    }
+    add_chain_side(net, n, tc, (int32_t)c, nb, n->rs, n->re, n->ros, n->roe, in->t_start[c],
+                   in->t_end[c]);
 }
 
 /* ------------------------------------------------------------ finish */
@@ -477,64 +495,149 @@ static void fill_other_range(gac_net *n, nfill *f, int is_q) {
     }
 }
 
-static void order_push(gac_net *n, int side, nfill *f, int64_t *cap) {
-    if (n->n_order[side] == *cap) {
-        *cap = *cap ? *cap * 2 : 4096;
-        n->order[side] = realloc(n->order[side], *cap * sizeof(nfill *));
+/* finishNet per chromosome (sortNet + rCalcOtherFill, chainNet.c:694-723):
+ * fills/gaps into sorted arrays, other-side ranges, and the chromosome's
+ * fills in pre-order (numbered globally afterwards, in chromosome order) */
+typedef struct fin_ctx {
+    gac_net *n;
+    nwork *w;
+    int side;
+    nfill **ord;
+    int64_t n_ord, cap;
+} fin_ctx;
+
+static void finish_gap(fin_ctx *x, ngap *g);
+
+static void finish_fill(fin_ctx *x, nfill *f) {
+    fill_other_range(x->n, f, x->side == GAC_Q);
+    if (x->n_ord == x->cap) {
+        x->cap = x->cap ? x->cap * 2 : 256;
+        x->ord = realloc(x->ord, (size_t)x->cap * sizeof(nfill *));
     }
-    f->ord = n->n_order[side];
-    n->order[side][n->n_order[side]++] = f;
-}
-
-static void finish_gap(gac_net *n, int side, ngap *g, int64_t *cap);
-
-static void finish_fill(gac_net *n, int side, nfill *f, int64_t *cap) {
-    fill_other_range(n, f, side == GAC_Q);
-    order_push(n, side, f, cap);
+    x->ord[x->n_ord++] = f;
     int cnt = 0;
     for (ngap *g = f->gap_head; g; g = g->next)
         ++cnt;
     f->n_gaps = cnt;
-    f->gaps = cnt ? arena_alloc(&n->ar, cnt * sizeof(ngap *)) : NULL;
+    f->gaps = cnt ? arena_alloc(&x->w->ar, cnt * sizeof(ngap *)) : NULL;
     cnt = 0;
     for (ngap *g = f->gap_head; g; g = g->next)
         f->gaps[cnt++] = g;
     qsort(f->gaps, f->n_gaps, sizeof(ngap *), cmp_gap);
     for (int i = 0; i < f->n_gaps; ++i)
-        finish_gap(n, side, f->gaps[i], cap);
+        finish_gap(x, f->gaps[i]);
 }
 
-static void finish_gap(gac_net *n, int side, ngap *g, int64_t *cap) {
+static void finish_gap(fin_ctx *x, ngap *g) {
     int cnt = 0;
     for (nfill *f = g->fill_head; f; f = f->next)
         ++cnt;
     g->n_fills = cnt;
-    g->fills = cnt ? arena_alloc(&n->ar, cnt * sizeof(nfill *)) : NULL;
+    g->fills = cnt ? arena_alloc(&x->w->ar, cnt * sizeof(nfill *)) : NULL;
     cnt = 0;
     for (nfill *f = g->fill_head; f; f = f->next)
         g->fills[cnt++] = f;
     qsort(g->fills, g->n_fills, sizeof(nfill *), cmp_fill);
     for (int i = 0; i < g->n_fills; ++i)
-        finish_fill(n, side, g->fills[i], cap);
+        finish_fill(x, g->fills[i]);
 }
 
 /* ------------------------------------------------------------ API */
 void gac_net_free(gac_net *n) {
     if (!n)
         return;
-    arena_free(&n->ar);
-    free(n->tn);
+    for (int i = 0; i < n->n_w; ++i) {
+        nwork *w = &n->w[i];
+        arena_free(&w->ar);
+        free(w->tn);
+        free(w->fs);
+        free(w->rs);
+        free(w->re);
+        free(w->ros);
+        free(w->roe);
+    }
+    free(n->w);
     free(n->chroms[0]);
     free(n->chroms[1]);
     free(n->order[0]);
     free(n->order[1]);
-    free(n->fs);
-    free(n->rs);
-    free(n->re);
-    free(n->ros);
-    free(n->roe);
     free(n->ali_prefix);
     free(n);
+}
+
+typedef struct fin_job {
+    gac_net *n;
+    fin_ctx *x; /* [T chromosomes..., Q chromosomes...] */
+    int64_t nc;
+    _Atomic int64_t next;
+    _Atomic int wid;
+} fin_job;
+
+static void *fin_thread(void *arg) {
+    fin_job *F = arg;
+    nwork *w = &F->n->w[atomic_fetch_add(&F->wid, 1)];
+    for (;;) {
+        const int64_t k = atomic_fetch_add(&F->next, 1);
+        if (k >= F->nc)
+            break;
+        const int side = k < F->n->n_chroms[GAC_T] ? GAC_T : GAC_Q;
+        const int32_t ci = (int32_t)(side == GAC_T ? k : k - F->n->n_chroms[GAC_T]);
+        nchrom *c = &F->n->chroms[side][ci];
+        fin_ctx *x = &F->x[k];
+        x->n = F->n;
+        x->w = w;
+        x->side = side;
+        if (c->root->fill_head)
+            finish_gap(x, c->root);
+    }
+    return NULL;
+}
+
+typedef struct net_task {
+    int side;
+    int32_t chrom;
+    const int64_t *chains;
+    int64_t n;
+} net_task;
+
+static int net_task_cmp(const void *a, const void *b) {
+    const net_task *x = a, *y = b;
+    if (x->n != y->n)
+        return x->n > y->n ? -1 : 1;
+    if (x->side != y->side)
+        return x->side - y->side;
+    return (x->chrom > y->chrom) - (x->chrom < y->chrom);
+}
+
+typedef struct net_job {
+    gac_net *n;
+    net_task *task;
+    int64_t ntask;
+    _Atomic int64_t next;
+    _Atomic int wid;
+} net_job;
+
+static void *net_thread(void *arg) {
+    net_job *J = arg;
+    nwork *w = &J->n->w[atomic_fetch_add(&J->wid, 1)];
+    for (;;) {
+        const int64_t k = atomic_fetch_add(&J->next, 1);
+        if (k >= J->ntask)
+            break;
+        const net_task *t = &J->task[k];
+        nchrom *c = &J->n->chroms[t->side][t->chrom];
+        /* makeChroms (chainNet.c:328-354): one gap = one space over the
+         * whole sequence */
+        c->root = gap_new(w, 0, c->size, 0, 0);
+        add_space_for_gap(w, c, c->root);
+        for (int64_t i = 0; i < t->n; ++i) {
+            if (t->side == GAC_T)
+                add_chain_t(J->n, w, t->chains[i]);
+            else
+                add_chain_q(J->n, w, t->chains[i]);
+        }
+    }
+    return NULL;
 }
 
 int gac_net_build(const gac_net_input *in, const gac_net_opts *opt, gac_net **out) {
@@ -545,23 +648,16 @@ int gac_net_build(const gac_net_input *in, const gac_net_opts *opt, gac_net **ou
     gac_net *n = calloc(1, sizeof(*n));
     n->in = *in;
     n->opt = *opt;
-    n->tn_free = -1;
-    n->rng = 0x9E3779B9u;
-    for (int side = 0; side < 2; ++side) {
-        int32_t cnt = side == GAC_T ? in->n_tseq : in->n_qseq;
-        const char *const *names = side == GAC_T ? in->t_names : in->q_names;
-        const int32_t *sizes = side == GAC_T ? in->t_sizes : in->q_sizes;
-        n->n_chroms[side] = cnt;
-        n->chroms[side] = calloc(cnt ? cnt : 1, sizeof(nchrom));
-        for (int32_t i = 0; i < cnt; ++i) {
-            nchrom *c = &n->chroms[side][i];
-            c->name = names[i];
-            c->size = sizes[i];
-            c->root = gap_new(n, 0, sizes[i], 0, 0);
-            c->troot = -1;
-            add_space_for_gap(n, c, c->root);
-        }
+    n->n_w = gac_host_threads();
+    n->w = calloc((size_t)n->n_w, sizeof(nwork));
+    for (int k = 0; k < n->n_w; ++k) {
+        n->w[k].tn_free = -1;
+        /* xorshift seeds must be non-zero (a zero seed stays zero and
+         * degenerates the treap into a list) */
+        n->w[k].rng = (0x9E3779B9u ^ (0x85EBCA6Bu * (uint32_t)(k + 1))) | 1u;
     }
+    /* chains to net: in order until the first below minScore (must be
+     * sorted), haplotype queries skipped unless incl_hap */
     double last = -1;
     int64_t i;
     for (i = 0; i < in->n_chains; ++i) {
@@ -578,20 +674,102 @@ int gac_net_build(const gac_net_input *in, const gac_net_opts *opt, gac_net **ou
             gac_net_free(n);
             return gac_fail(GAC_E_ARG, "chain %lld: sequence index out of range", (long long)i);
         }
-        if (!opt->incl_hap && is_haplotype(in->q_names[in->q_seq[i]]))
-            continue;
-        add_chain(n, i);
     }
-    n->n_netted = i;
-    /* finishNet: Q then T (order irrelevant), sort + other ranges + pre-order index */
-    for (int side = 1; side >= 0; --side) {
-        int64_t cap = 0;
-        for (int32_t k = 0; k < n->n_chroms[side]; ++k) {
+    const int64_t nn = i;
+    /* per (side, chromosome): its chains in order (counting sort) */
+    int32_t nt = in->n_tseq, nq = in->n_qseq;
+    int64_t *toff = calloc((size_t)nt + 1, 8), *qoff = calloc((size_t)nq + 1, 8);
+    int64_t *tl = malloc((size_t)(nn ? nn : 1) * 8), *ql = malloc((size_t)(nn ? nn : 1) * 8);
+    int64_t *tfill = malloc((size_t)(nt ? nt : 1) * 8), *qfill = malloc((size_t)(nq ? nq : 1) * 8);
+    for (int64_t c = 0; c < nn; ++c) {
+        if (!opt->incl_hap && is_haplotype(in->q_names[in->q_seq[c]]))
+            continue;
+        ++toff[in->t_seq[c] + 1];
+        ++qoff[in->q_seq[c] + 1];
+    }
+    for (int32_t k = 0; k < nt; ++k)
+        toff[k + 1] += toff[k];
+    for (int32_t k = 0; k < nq; ++k)
+        qoff[k + 1] += qoff[k];
+    memcpy(tfill, toff, (size_t)nt * 8);
+    memcpy(qfill, qoff, (size_t)nq * 8);
+    for (int64_t c = 0; c < nn; ++c) {
+        if (!opt->incl_hap && is_haplotype(in->q_names[in->q_seq[c]]))
+            continue;
+        tl[tfill[in->t_seq[c]]++] = c;
+        ql[qfill[in->q_seq[c]]++] = c;
+    }
+    for (int side = 0; side < 2; ++side) {
+        int32_t cnt = side == GAC_T ? nt : nq;
+        const char *const *names = side == GAC_T ? in->t_names : in->q_names;
+        const int32_t *sizes = side == GAC_T ? in->t_sizes : in->q_sizes;
+        n->n_chroms[side] = cnt;
+        n->chroms[side] = calloc(cnt ? cnt : 1, sizeof(nchrom));
+        for (int32_t k = 0; k < cnt; ++k) {
             nchrom *c = &n->chroms[side][k];
-            if (c->root->fill_head)
-                finish_gap(n, side, c->root, &cap);
+            c->name = names[k];
+            c->size = sizes[k];
+            c->troot = -1;
         }
     }
+    /* tasks, largest first; every task nets one chromosome of one side */
+    net_job J;
+    memset(&J, 0, sizeof(J));
+    J.n = n;
+    J.ntask = nt + nq;
+    J.task = malloc((size_t)(J.ntask ? J.ntask : 1) * sizeof(net_task));
+    for (int32_t k = 0; k < nt; ++k)
+        J.task[k] = (net_task){GAC_T, k, tl + toff[k], toff[k + 1] - toff[k]};
+    for (int32_t k = 0; k < nq; ++k)
+        J.task[nt + k] = (net_task){GAC_Q, k, ql + qoff[k], qoff[k + 1] - qoff[k]};
+    qsort(J.task, (size_t)J.ntask, sizeof(net_task), net_task_cmp);
+    atomic_init(&J.next, 0);
+    atomic_init(&J.wid, 0);
+    gac_run_threads(n->n_w < J.ntask ? n->n_w : (J.ntask ? J.ntask : 1), net_thread, &J);
+    free(J.task);
+    free(toff);
+    free(qoff);
+    free(tl);
+    free(ql);
+    free(tfill);
+    free(qfill);
+    n->n_netted = i;
+    struct timespec t_fin0, t_fin1;
+    clock_gettime(CLOCK_MONOTONIC, &t_fin0);
+    /* finishNet: chromosomes in parallel, then the pre-order index per side
+     * in chromosome order */
+    {
+        fin_job F;
+        memset(&F, 0, sizeof(F));
+        F.n = n;
+        F.nc = n->n_chroms[0] + n->n_chroms[1];
+        F.x = calloc((size_t)(F.nc ? F.nc : 1), sizeof(fin_ctx));
+        atomic_init(&F.next, 0);
+        atomic_init(&F.wid, 0);
+        gac_run_threads(n->n_w < F.nc ? n->n_w : (F.nc ? (int)F.nc : 1), fin_thread, &F);
+        for (int side = 0; side < 2; ++side) {
+            int64_t tot = 0;
+            const int64_t base = side == GAC_T ? 0 : n->n_chroms[GAC_T];
+            for (int32_t k = 0; k < n->n_chroms[side]; ++k)
+                tot += F.x[base + k].n_ord;
+            n->order[side] = malloc((size_t)(tot ? tot : 1) * sizeof(nfill *));
+            int64_t o = 0;
+            for (int32_t k = 0; k < n->n_chroms[side]; ++k) {
+                fin_ctx *x = &F.x[base + k];
+                for (int64_t j = 0; j < x->n_ord; ++j) {
+                    x->ord[j]->ord = o;
+                    n->order[side][o++] = x->ord[j];
+                }
+                free(x->ord);
+            }
+            n->n_order[side] = o;
+        }
+        free(F.x);
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t_fin1);
+    if (getenv("GAC_TIMING"))
+        fprintf(stderr, "[gac_net_build] finishNet %.3f s\n",
+                (t_fin1.tv_sec - t_fin0.tv_sec) + 1e-9 * (t_fin1.tv_nsec - t_fin0.tv_nsec));
     /* aligned-base prefix per block for chainBaseCount / SubT / SubQ */
     n->ali_prefix = malloc((in->blk_off[in->n_chains] + 1) * sizeof(int64_t));
     int64_t acc = 0;
@@ -803,6 +981,47 @@ static void out_fill(wctx *w, const nfill *f) {
     }
 }
 
+/* Parallel output: the top-level fills of every chromosome (in output
+ * order) are cut into contiguous ranges; each thread prints its range into
+ * its own memory stream (a range that starts a chromosome also prints the
+ * "net" line), and the buffers are written in order. */
+typedef struct witem {
+    int32_t chrom, fill;
+} witem;
+
+typedef struct wjob {
+    const gac_net *n;
+    int side;
+    const int64_t *tscore;
+    const witem *items;
+    int64_t n_items, per;
+    _Atomic int64_t next;
+    char **buf;
+    size_t *len;
+} wjob;
+
+static void *write_thread(void *arg) {
+    wjob *J = arg;
+    for (;;) {
+        const int64_t r = atomic_fetch_add(&J->next, 1);
+        const int64_t a = r * J->per;
+        if (a >= J->n_items)
+            break;
+        const int64_t b = a + J->per < J->n_items ? a + J->per : J->n_items;
+        FILE *f = open_memstream(&J->buf[r], &J->len[r]);
+        wctx w = {J->n, f, J->side, J->tscore, 0, NULL};
+        for (int64_t i = a; i < b; ++i) {
+            const nchrom *c = &J->n->chroms[J->side][J->items[i].chrom];
+            if (J->items[i].fill == 0)
+                fprintf(f, "net %s %d\n", c->name, c->size);
+            w.depth = 0;
+            out_fill(&w, c->root->fills[J->items[i].fill]);
+        }
+        fclose(f);
+    }
+    return NULL;
+}
+
 int gac_net_write(const gac_net *n, int side, const int64_t *tscores, const char *path,
                   const char *const *meta, int32_t n_meta) {
     if (!n || !path || (side != GAC_T && side != GAC_Q))
@@ -817,29 +1036,45 @@ int gac_net_write(const gac_net *n, int side, const int64_t *tscores, const char
         if (!f)
             return gac_fail(GAC_E_IO, "Can't open %s to write", path);
     }
-    char *buf = malloc(1 << 22);
-    setvbuf(f, buf, _IOFBF, 1 << 22);
     for (int32_t i = 0; i < n_meta; ++i)
         fprintf(f, "%s\n", meta[i]);
-    wctx w = {n, f, side, side == GAC_T ? tscores : NULL, 0, buf};
+    int64_t ni = 0;
     for (int32_t k = 0; k < n->n_chroms[side]; ++k) {
         const nchrom *c = &n->chroms[side][k];
-        w.depth = 0;
-        if (c->root->fill_head) {
-            fprintf(f, "net %s %d\n", c->name, c->size);
-            for (int i = 0; i < c->root->n_fills; ++i)
-                out_fill(&w, c->root->fills[i]);
-        }
+        if (c->root->fill_head)
+            ni += c->root->n_fills;
     }
+    witem *items = malloc((size_t)(ni ? ni : 1) * sizeof(witem));
+    ni = 0;
+    for (int32_t k = 0; k < n->n_chroms[side]; ++k) {
+        const nchrom *c = &n->chroms[side][k];
+        if (c->root->fill_head)
+            for (int i = 0; i < c->root->n_fills; ++i)
+                items[ni++] = (witem){k, i};
+    }
+    const int nt = gac_host_threads();
+    int64_t per = ni / (8 * (int64_t)nt) + 1;
+    const int64_t nr = (ni + per - 1) / per;
+    wjob J = {n, side, side == GAC_T ? tscores : NULL, items, ni, per, 0, NULL, NULL};
+    atomic_init(&J.next, 0);
+    J.buf = calloc((size_t)(nr ? nr : 1), sizeof(char *));
+    J.len = calloc((size_t)(nr ? nr : 1), sizeof(size_t));
+    gac_run_threads(nt < nr ? nt : (int)(nr ? nr : 1), write_thread, &J);
+    for (int64_t r = 0; r < nr; ++r) {
+        if (J.len[r])
+            fwrite(J.buf[r], 1, J.len[r], f);
+        free(J.buf[r]);
+    }
+    free(J.buf);
+    free(J.len);
+    free(items);
     int bad = ferror(f);
     if (close_it) {
         if (fclose(f) != 0)
             bad = 1;
     } else {
         fflush(f);
-        setvbuf(f, NULL, _IOLBF, 0);
     }
-    free(buf);
     if (bad)
         return gac_fail(GAC_E_IO, "write error on %s", path);
     return GAC_OK;

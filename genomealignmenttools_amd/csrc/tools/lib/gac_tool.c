@@ -12,6 +12,7 @@
 #include <string.h>
 #include <sys/stat.h>
 #include <unistd.h>
+#include <pthread.h>
 #include <time.h>
 #include <zlib.h>
 
@@ -449,12 +450,24 @@ char *gt_slurp(const char *path, size_t *len) {
     return buf;
 }
 
-/* ------------------------------------------------------------ chains */
+/* ------------------------------------------------------------ chains
+ * gt_read_chains parses in parallel: the text is cut into chunks at lines
+ * that start with "chain" (only a header can), every chunk is parsed by its
+ * own thread with the sequential rules (chainReadChainLine /
+ * chainReadBlocks, chain.c:229-335), and the chunks are stitched in order.
+ * Everything order-dependent is replayed after the fact: the first error
+ * in file order (line numbers from per-chunk newline counts), the first
+ * chain scoring below stop_below (the read stops there, as chainNet's loop
+ * does, chainNet.c:949-952), chainIdNext ids of id-less headers, and the
+ * '#' metadata lines. */
 typedef struct lf {
     char *cur, *end;
     const char *path;
-    int line;
+    int64_t line;
     gt_chains *meta_to;
+    /* first error of the chunk: message, byte position */
+    int err;
+    char msg[512];
 } lf;
 
 static char *lf_next(lf *f) {
@@ -496,25 +509,26 @@ static int lf_chop(lf *f, char **row, int max) {
     return 0;
 }
 
-static int need_num(lf *f, char **row, int ix) {
-    char c = row[ix][0];
-    if (c != '-' && !isdigit((unsigned char)c))
-        gt_abort("Expecting number field %d line %d of %s, got %s", ix + 1, f->line, f->path,
-                 row[ix]);
-    return atoi(row[ix]);
-}
-
-#define GROW(ptr, cap, n, type)                                   \
-    do {                                                          \
-        if ((n) >= (cap)) {                                       \
-            (cap) = (cap) ? (cap) * 2 : 1024;                      \
-            (ptr) = realloc((ptr), (size_t)(cap) * sizeof(type)); \
-        }                                                         \
+/* messages keep "\001" for the line number and "\002" for the path; both
+ * are filled in once the chunk's first line is known */
+#define LF_FAIL(f, ...)                                                        \
+    do {                                                                       \
+        snprintf((f)->msg, sizeof((f)->msg), __VA_ARGS__);                     \
+        (f)->err = 1;                                                          \
+        return -1;                                                             \
     } while (0)
 
-static void chains_reserve(gt_chains *c) {
-    if (c->n + 1 >= c->cap) {
-        int64_t cap = c->cap ? c->cap * 2 : 4096;
+/* lineFileNeedNum; the message takes the chunk-local line, fixed up later */
+static int need_num(lf *f, char **row, int ix, int *out) {
+    char c = row[ix][0];
+    if (c != '-' && !isdigit((unsigned char)c))
+        LF_FAIL(f, "Expecting number field %d line \001 of \002, got %s", ix + 1, row[ix]);
+    *out = atoi(row[ix]);
+    return 0;
+}
+
+static void chains_grow(gt_chains *c, int64_t cap) {
+    {
         c->score = realloc(c->score, cap * sizeof(double));
         c->tname = realloc(c->tname, cap * 4);
         c->tsize = realloc(c->tsize, cap * 4);
@@ -531,82 +545,289 @@ static void chains_reserve(gt_chains *c) {
     }
 }
 
+static void chains_reserve(gt_chains *c) {
+    if (c->n + 1 >= c->cap)
+        chains_grow(c, c->cap ? c->cap * 2 : 4096);
+}
+
+/* room for `need` chains (and need + 1 block offsets) */
+static void chains_reserve_n(gt_chains *c, int64_t need) {
+    if (c->cap < need)
+        chains_grow(c, need > 2 * c->cap ? need : 2 * c->cap);
+}
+
 static int g_next_id = 1; /* chainIdNext (chain.c:180-198) */
+
+typedef struct chunk {
+    lf f;
+    gt_chains c;       /* local: names local, id -1 = assign later */
+    int64_t stop;      /* first chain (local index) scoring below stop_below, or -1 */
+    int64_t lines;     /* newlines in the chunk */
+    int64_t err_line;  /* local line of the error */
+    double stop_below;
+} chunk;
+
+/* parse one record; 0 = ok, 1 = end of chunk, -1 = error (f->msg) */
+static int parse_chain(chunk *k) {
+    lf *f = &k->f;
+    gt_chains *c = &k->c;
+    char *row[13];
+    int wc = lf_chop(f, row, 13);
+    if (wc == 0)
+        return 1;
+    if (wc < 12)
+        LF_FAIL(f, "Expecting at least 12 words line \001 of \002");
+    if (strcmp(row[0], "chain") != 0)
+        LF_FAIL(f, "Expecting 'chain' line \001 of \002");
+    chains_reserve(c);
+    int64_t i = c->n;
+    int v;
+    c->score[i] = atof(row[1]);
+    c->tname[i] = gt_names_add(&c->tnames, row[2], strlen(row[2]));
+    if (need_num(f, row, 3, &v))
+        return -1;
+    c->tsize[i] = v;
+    if (wc >= 13) {
+        if (need_num(f, row, 12, &v))
+            return -1;
+        c->id[i] = v;
+    } else {
+        c->id[i] = INT32_MIN; /* chainIdNext, assigned in file order later */
+    }
+    if (need_num(f, row, 5, &c->tstart[i]) || need_num(f, row, 6, &c->tend[i]))
+        return -1;
+    c->qname[i] = gt_names_add(&c->qnames, row[7], strlen(row[7]));
+    if (need_num(f, row, 8, &c->qsize[i]))
+        return -1;
+    c->qstrand[i] = row[9][0] == '-' ? 1 : 0;
+    if (need_num(f, row, 10, &c->qstart[i]) || need_num(f, row, 11, &c->qend[i]))
+        return -1;
+    if (c->qstart[i] >= c->qend[i] || c->tstart[i] >= c->tend[i])
+        LF_FAIL(f, "End before start line \001 of \002");
+    if (c->qstart[i] < 0 || c->tstart[i] < 0)
+        LF_FAIL(f, "Start before zero line \001 of \002");
+    if (c->qend[i] > c->qsize[i] || c->tend[i] > c->tsize[i])
+        LF_FAIL(f, "Past end of sequence line \001 of \002");
+    /* chainReadBlocks (chain.c:301-335) */
+    int q = c->qstart[i], t = c->tstart[i];
+    for (;;) {
+        char *brow[3];
+        int bw = lf_chop(f, brow, 3);
+        if (bw == 0)
+            LF_FAIL(f, "Unexpected end of file in \002");
+        int size;
+        if (need_num(f, brow, 0, &size))
+            return -1;
+        if (c->nb + 1 >= c->bcap) {
+            c->bcap = c->bcap ? c->bcap * 2 : 1 << 16;
+            c->bt = realloc(c->bt, c->bcap * 4);
+            c->bq = realloc(c->bq, c->bcap * 4);
+            c->bs = realloc(c->bs, c->bcap * 4);
+        }
+        c->bt[c->nb] = t;
+        c->bq[c->nb] = q;
+        c->bs[c->nb] = size;
+        c->nb++;
+        q += size;
+        t += size;
+        if (bw == 1)
+            break;
+        if (bw < 3)
+            LF_FAIL(f, "Expecting 1 or 3 words line \001 of \002\n");
+        int dt, dq;
+        if (need_num(f, brow, 1, &dt) || need_num(f, brow, 2, &dq))
+            return -1;
+        t += dt;
+        q += dq;
+    }
+    if (q != c->qend[i])
+        LF_FAIL(f, "q end mismatch %d vs %d line \001 of \002\n", q, c->qend[i]);
+    if (t != c->tend[i])
+        LF_FAIL(f, "t end mismatch %d vs %d line \001 of \002\n", t, c->tend[i]);
+    c->n++;
+    c->blk_off[c->n] = c->nb;
+    if (c->score[i] < k->stop_below) { /* read, not kept (chainNet.c:949-952) */
+        k->stop = i;
+        return 1;
+    }
+    return 0;
+}
+
+static void *parse_chunk(void *arg) {
+    chunk *k = arg;
+    k->c.blk_off = malloc(8);
+    k->c.blk_off[0] = 0;
+    int r;
+    while ((r = parse_chain(k)) == 0)
+        ;
+    if (r < 0)
+        k->err_line = k->f.line;
+    /* newlines of the whole chunk (for the next chunks' line numbers) */
+    return NULL;
+}
+
+typedef struct nl_job {
+    const char *a, *b;
+    int64_t n;
+} nl_job;
+
+static void *count_newlines(void *arg) {
+    nl_job *j = arg;
+    int64_t n = 0;
+    for (const char *p = j->a; p < j->b;) {
+        const char *q = memchr(p, '\n', (size_t)(j->b - p));
+        if (!q)
+            break;
+        ++n;
+        p = q + 1;
+    }
+    j->n = n;
+    return NULL;
+}
+
+int gt_threads(void) {
+    const char *s = getenv("GAC_THREADS");
+    if (!s || !*s)
+        s = getenv("OMP_NUM_THREADS");
+    int n = s && *s ? atoi(s) : 0;
+    if (n <= 0) {
+        long c = sysconf(_SC_NPROCESSORS_ONLN);
+        n = c > 0 ? (int)c : 1;
+    }
+    return n > 64 ? 64 : n;
+}
+
+void gt_parallel(int n, void *(*fn)(void *), void *args, size_t stride) {
+    pthread_t *th = malloc((size_t)(n > 0 ? n : 1) * sizeof(pthread_t));
+    for (int i = 1; i < n; ++i)
+        pthread_create(&th[i], NULL, fn, (char *)args + (size_t)i * stride);
+    if (n > 0)
+        fn(args);
+    for (int i = 1; i < n; ++i)
+        pthread_join(th[i], NULL);
+    free(th);
+}
 
 void gt_read_chains(const char *path, gt_chains *c, double stop_below, int keep_meta) {
     memset(c, 0, sizeof(*c));
     size_t len;
     char *buf = gt_slurp(path, &len);
-    lf f = {buf, buf + len, path, 0, keep_meta ? c : NULL};
+    /* chunk boundaries at "\nchain" */
+    int nt = len < (8u << 20) ? 1 : gt_threads();
+    char **cut = malloc((size_t)(nt + 1) * sizeof(char *));
+    cut[0] = buf;
+    int nk = 1;
+    for (int k = 1; k < nt; ++k) {
+        char *p = buf + len / nt * k;
+        if (p < cut[nk - 1])
+            p = cut[nk - 1];
+        char *h = NULL;
+        while (p < buf + len) {
+            char *nl = memchr(p, '\n', (size_t)(buf + len - p));
+            if (!nl)
+                break;
+            if ((size_t)(buf + len - (nl + 1)) >= 5 && memcmp(nl + 1, "chain", 5) == 0) {
+                h = nl + 1;
+                break;
+            }
+            p = nl + 1;
+        }
+        if (h && h > cut[nk - 1])
+            cut[nk++] = h;
+    }
+    cut[nk] = buf + len;
+    chunk *K = calloc((size_t)nk, sizeof(chunk));
+    nl_job *NL = calloc((size_t)nk, sizeof(nl_job));
+    for (int k = 0; k < nk; ++k) {
+        K[k].f = (lf){cut[k], cut[k + 1], path, 0, keep_meta ? &K[k].c : NULL, 0, {0}};
+        K[k].stop = -1;
+        K[k].stop_below = stop_below;
+        NL[k] = (nl_job){cut[k], cut[k + 1], 0};
+    }
+    gt_parallel(nk, count_newlines, NL, sizeof(nl_job)); /* before parsing cuts lines */
+    gt_parallel(nk, parse_chunk, K, sizeof(chunk));
+    /* stitch in file order up to the first error or stop */
     c->blk_off = malloc(8);
     c->blk_off[0] = 0;
-    char *row[13];
-    for (;;) {
-        int wc = lf_chop(&f, row, 13);
-        if (wc == 0)
-            break;
-        if (wc < 12)
-            gt_abort("Expecting at least 12 words line %d of %s", f.line, path);
-        if (strcmp(row[0], "chain") != 0)
-            gt_abort("Expecting 'chain' line %d of %s", f.line, path);
-        chains_reserve(c);
-        int64_t i = c->n;
-        c->score[i] = atof(row[1]);
-        c->tname[i] = gt_names_add(&c->tnames, row[2], strlen(row[2]));
-        c->tsize[i] = need_num(&f, row, 3);
-        c->id[i] = wc >= 13 ? need_num(&f, row, 12) : g_next_id++;
-        c->tstart[i] = need_num(&f, row, 5);
-        c->tend[i] = need_num(&f, row, 6);
-        c->qname[i] = gt_names_add(&c->qnames, row[7], strlen(row[7]));
-        c->qsize[i] = need_num(&f, row, 8);
-        c->qstrand[i] = row[9][0] == '-' ? 1 : 0;
-        c->qstart[i] = need_num(&f, row, 10);
-        c->qend[i] = need_num(&f, row, 11);
-        if (c->qstart[i] >= c->qend[i] || c->tstart[i] >= c->tend[i])
-            gt_abort("End before start line %d of %s", f.line, path);
-        if (c->qstart[i] < 0 || c->tstart[i] < 0)
-            gt_abort("Start before zero line %d of %s", f.line, path);
-        if (c->qend[i] > c->qsize[i] || c->tend[i] > c->tsize[i])
-            gt_abort("Past end of sequence line %d of %s", f.line, path);
-        /* chainReadBlocks (chain.c:301-335) */
-        int q = c->qstart[i], t = c->tstart[i];
-        int64_t nb0 = c->nb;
-        for (;;) {
-            char *brow[3];
-            int bw = lf_chop(&f, brow, 3);
-            if (bw == 0)
-                gt_abort("Unexpected end of file in %s", path);
-            int size = need_num(&f, brow, 0);
-            if (c->nb + 1 >= c->bcap) {
-                c->bcap = c->bcap ? c->bcap * 2 : 1 << 16;
+    int64_t line0 = 0;
+    for (int k = 0; k < nk; ++k) {
+        chunk *ch = &K[k];
+        const int64_t take = ch->stop >= 0 ? ch->stop : ch->c.n; /* the stop chain is dropped */
+        /* metadata: all '#' lines the chunk consumed (a stop drops the rest) */
+        for (int32_t m = 0; m < ch->c.n_meta; ++m) {
+            add_meta(c, ch->c.meta[m]);
+        }
+        int32_t *tmap = malloc((size_t)(ch->c.tnames.n ? ch->c.tnames.n : 1) * 4);
+        int32_t *qmap = malloc((size_t)(ch->c.qnames.n ? ch->c.qnames.n : 1) * 4);
+        for (int32_t i = 0; i < ch->c.tnames.n; ++i)
+            tmap[i] = gt_names_add(&c->tnames, ch->c.tnames.names[i], strlen(ch->c.tnames.names[i]));
+        for (int32_t i = 0; i < ch->c.qnames.n; ++i)
+            qmap[i] = gt_names_add(&c->qnames, ch->c.qnames.names[i], strlen(ch->c.qnames.names[i]));
+        /* ids: every header read so far consumes chainIdNext, kept or not */
+        const int64_t nread = ch->c.n;
+        for (int64_t i = 0; i < nread; ++i)
+            if (ch->c.id[i] == INT32_MIN)
+                ch->c.id[i] = g_next_id++;
+        if (take > 0) {
+            const int64_t nb = ch->c.blk_off[take];
+            chains_reserve_n(c, c->n + take + 1);
+            for (int64_t i = 0; i < take; ++i) {
+                const int64_t j = c->n + i;
+                c->score[j] = ch->c.score[i];
+                c->tname[j] = tmap[ch->c.tname[i]];
+                c->tsize[j] = ch->c.tsize[i];
+                c->tstart[j] = ch->c.tstart[i];
+                c->tend[j] = ch->c.tend[i];
+                c->qname[j] = qmap[ch->c.qname[i]];
+                c->qsize[j] = ch->c.qsize[i];
+                c->qstart[j] = ch->c.qstart[i];
+                c->qend[j] = ch->c.qend[i];
+                c->qstrand[j] = ch->c.qstrand[i];
+                c->id[j] = ch->c.id[i];
+                c->blk_off[j + 1] = c->nb + ch->c.blk_off[i + 1];
+            }
+            c->n += take;
+            if (c->nb + nb + 1 > c->bcap) {
+                c->bcap = c->nb + nb + 1;
                 c->bt = realloc(c->bt, c->bcap * 4);
                 c->bq = realloc(c->bq, c->bcap * 4);
                 c->bs = realloc(c->bs, c->bcap * 4);
             }
-            c->bt[c->nb] = t;
-            c->bq[c->nb] = q;
-            c->bs[c->nb] = size;
-            c->nb++;
-            q += size;
-            t += size;
-            if (bw == 1)
-                break;
-            if (bw < 3)
-                gt_abort("Expecting 1 or 3 words line %d of %s\n", f.line, path);
-            t += need_num(&f, brow, 1);
-            q += need_num(&f, brow, 2);
+            memcpy(c->bt + c->nb, ch->c.bt, (size_t)nb * 4);
+            memcpy(c->bq + c->nb, ch->c.bq, (size_t)nb * 4);
+            memcpy(c->bs + c->nb, ch->c.bs, (size_t)nb * 4);
+            c->nb += nb;
         }
-        if (q != c->qend[i])
-            gt_abort("q end mismatch %d vs %d line %d of %s\n", q, c->qend[i], f.line, path);
-        if (t != c->tend[i])
-            gt_abort("t end mismatch %d vs %d line %d of %s\n", t, c->tend[i], f.line, path);
-        if (c->score[i] < stop_below) { /* read, not kept (chainNet.c:949-952) */
-            c->nb = nb0;
+        free(tmap);
+        free(qmap);
+        const int err = ch->f.err && ch->stop < 0;
+        if (err) {
+            char msg[2048];
+            size_t o = 0;
+            for (const char *m = ch->f.msg; *m && o + 1 < sizeof(msg); ++m) {
+                if (*m == '\001')
+                    o += snprintf(msg + o, sizeof(msg) - o, "%lld", (long long)(line0 + ch->err_line));
+                else if (*m == '\002')
+                    o += snprintf(msg + o, sizeof(msg) - o, "%s", path);
+                else
+                    msg[o++] = *m;
+                if (o >= sizeof(msg))
+                    o = sizeof(msg) - 1;
+            }
+            msg[o] = 0;
+            for (int j = 0; j < nk; ++j)
+                gt_chains_free(&K[j].c);
+            gt_abort("%s", msg);
+        }
+        line0 += NL[k].n;
+        if (ch->stop >= 0)
             break;
-        }
-        c->n++;
-        c->blk_off[c->n] = c->nb;
     }
+    for (int k = 0; k < nk; ++k)
+        gt_chains_free(&K[k].c);
+    free(K);
+    free(NL);
+    free(cut);
     free(buf);
 }
 
@@ -672,18 +893,25 @@ void gt_read_sizes(const char *path, gt_sizes *s) {
     memset(s, 0, sizeof(*s));
     size_t len;
     char *buf = gt_slurp(path, &len);
-    lf f = {buf, buf + len, path, 0, NULL};
+    lf f = {buf, buf + len, path, 0, NULL, 0, {0}};
     int32_t cap = 0;
     char *row[3];
     int wc;
     while ((wc = lf_chop(&f, row, 3)) != 0) {
         if (wc != 2)
-            gt_abort("Expecting 2 words line %d of %s got %d", f.line, path, wc);
+            gt_abort("Expecting 2 words line %lld of %s got %d", (long long)f.line, path, wc);
         if (gt_names_find(&s->names, row[0]) >= 0)
             gt_abort("Duplicate %s in %s", row[0], path);
         int32_t id = gt_names_add(&s->names, row[0], strlen(row[0]));
-        GROW(s->size, cap, id, int32_t);
-        s->size[id] = need_num(&f, row, 1);
+        if (id >= cap) {
+            cap = cap ? cap * 2 : 1024;
+            s->size = realloc(s->size, (size_t)cap * sizeof(int32_t));
+        }
+        int v;
+        if (need_num(&f, row, 1, &v))
+            gt_abort("Expecting number field 2 line %lld of %s, got %s", (long long)f.line, path,
+                     row[1]);
+        s->size[id] = v;
     }
     free(buf);
 }

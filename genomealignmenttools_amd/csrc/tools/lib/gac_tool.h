@@ -17,6 +17,11 @@ extern "C" {
 void gt_abort(const char *fmt, ...) __attribute__((noreturn, format(printf, 1, 2)));
 void gt_verbose(int level, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 int gt_verbosity(void);
+/* worker threads for host stages (GAC_THREADS, else OMP_NUM_THREADS, else
+ * all cores; at most 64) */
+int gt_threads(void);
+/* run fn(args + i * stride) for i in [0, n) on n threads (0 on the caller) */
+void gt_parallel(int n, void *(*fn)(void *), void *args, size_t stride);
 /* -verbose>=2: wall time since the previous gt_stage call, labelled */
 void gt_stage(const char *what);
 void gt_check(int rc); /* abort with gac_last_error() unless GAC_OK */
