@@ -50,6 +50,8 @@ def parse():
     p.add_argument("--prof", choices=["tile", "all", "none"], default="tile",
                    help="kernels bracketed by HIP events inside the timed region "
                         "(the roofline needs k_tile's)")
+    p.add_argument("--order", choices=["net", "chain", "t"], default="net",
+                   help="range order handed to the GPU: .net output order, (chain, tStart), or tStart")
     p.add_argument("--tmp", default=os.environ.get("TMPDIR", "/tmp"))
     return p.parse_args()
 
@@ -72,6 +74,10 @@ def make_workload(args, rank):
         info = {"netted_chains": int(fills["netted_chains"]), "tnet_fills": int(len(part)),
                 "partial_fills": int(part.sum())}
         log(f"[rank {rank}] host netting: {info} ({time.time() - t1:.1f}s)")
+    if args.order == "chain":
+        ranges = ranges[np.lexsort((ranges[:, 1], ranges[:, 0]))]
+    elif args.order == "t":
+        ranges = ranges[np.argsort(ranges[:, 1], kind="stable")]
     return tg, qg, ca, np.ascontiguousarray(ranges, np.int32), info
 
 

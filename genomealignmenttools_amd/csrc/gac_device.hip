@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -68,8 +69,11 @@ struct Genome {
     std::vector<std::string> names;
     std::vector<int32_t> sizes;
     std::unordered_map<std::string, int32_t> index;
-    std::vector<uint8_t> raw;       // concatenated packed payloads, 8-B aligned
-    std::vector<int64_t> raw_off;   // per seq
+    std::vector<uint8_t> raw;       // payloads copied by gac_genome_add_seq, 8-B aligned
+    std::vector<int64_t> raw_off;   // per seq: offset into raw (-1: payload is ext[i])
+    std::vector<const uint8_t *> ext;  // per seq: payload inside the mapped .2bit file
+    gac_twobit tb{};                // mapping kept open for ext (gac_genome_load_2bit)
+    bool tb_open = false;
     std::vector<NPiece> npieces;    // bit0 relative to the seq start until finalize
     std::vector<int32_t> npiece_seq;
     // host copy kept after finalize (raw stays): merged, sorted N runs per
@@ -83,6 +87,7 @@ struct Genome {
     uint2 *planes = nullptr;
     uint32_t *nmask = nullptr;
     int64_t *d_woff = nullptr;
+    const uint8_t *packed(int i) const { return ext[i] ? ext[i] : raw.data() + raw_off[i]; }
 };
 
 struct Prof {
@@ -133,6 +138,9 @@ struct gac_ctx {
     int tile_grid_g = 2048;     // k_tile<false> grid (resident workgroups)
     int tile_grid_l = 2048;     // k_tile<true> grid
     int combine_grid = 512;
+    // pinned staging for genome uploads (two buffers, alternating)
+    uint8_t *pin[2] = {nullptr, nullptr};
+    hipEvent_t pin_ev[2] = {nullptr, nullptr};
     // profiling
     int prof = 0;  // mask of timed kernels
     std::vector<Prof> prof_pending;
@@ -194,6 +202,7 @@ extern "C" int gac_open(int device, gac_ctx **out) {
 }
 
 static void free_genome(Genome &g) {
+    if (g.tb_open) gac_twobit_close(&g.tb);
     if (g.planes) hipFree(g.planes);
     if (g.nmask) hipFree(g.nmask);
     if (g.d_woff) hipFree(g.d_woff);
@@ -217,6 +226,10 @@ extern "C" void gac_close(gac_ctx *c) {
     }
     for (auto ev : c->prof_free) hipEventDestroy(ev);
     if (c->h_stat) hipHostFree(c->h_stat);
+    for (int k = 0; k < 2; ++k) {
+        if (c->pin[k]) hipHostFree(c->pin[k]);
+        if (c->pin_ev[k]) hipEventDestroy(c->pin_ev[k]);
+    }
     hipStreamDestroy(c->stream);
     delete c;
 }
@@ -310,9 +323,11 @@ static Genome *side_of(gac_ctx *c, int side) {
     return &c->g[side];
 }
 
-extern "C" int gac_genome_add_seq(gac_ctx *c, int side, const char *name, int32_t size,
-                                  const uint8_t *packed, int32_t n_nblocks,
-                                  const int32_t *n_starts, const int32_t *n_sizes) {
+// copy = false: the payload stays where it is (a mapped .2bit file kept open
+// by the genome) and is read straight into pinned staging at finalize.
+static int add_seq(gac_ctx *c, int side, const char *name, int32_t size, const uint8_t *packed,
+                   bool copy, int32_t n_nblocks, const int32_t *n_starts,
+                   const int32_t *n_sizes) {
     Genome *g = side_of(c, side);
     if (!g || !name || size < 0 || (size > 0 && !packed) || n_nblocks < 0)
         return gac_fail(GAC_E_ARG, "gac_genome_add_seq: bad argument");
@@ -322,11 +337,17 @@ extern "C" int gac_genome_add_seq(gac_ctx *c, int side, const char *name, int32_
     g->index[name] = idx;
     g->names.push_back(name);
     g->sizes.push_back(size);
-    size_t off = (g->raw.size() + 7) & ~(size_t)7;
     size_t nbytes = ((size_t)size + 3) / 4;
-    g->raw.resize(off + nbytes);
-    if (nbytes) memcpy(g->raw.data() + off, packed, nbytes);
-    g->raw_off.push_back((int64_t)off);
+    if (copy) {
+        size_t off = (g->raw.size() + 7) & ~(size_t)7;
+        g->raw.resize(off + nbytes);
+        if (nbytes) memcpy(g->raw.data() + off, packed, nbytes);
+        g->raw_off.push_back((int64_t)off);
+        g->ext.push_back(nullptr);
+    } else {
+        g->raw_off.push_back(-1);
+        g->ext.push_back(packed);
+    }
     {
         std::vector<std::pair<int32_t, int32_t>> runs;
         for (int32_t i = 0; i < n_nblocks; ++i)
@@ -360,6 +381,91 @@ extern "C" int gac_genome_add_seq(gac_ctx *c, int side, const char *name, int32_
     return GAC_OK;
 }
 
+extern "C" int gac_genome_add_seq(gac_ctx *c, int side, const char *name, int32_t size,
+                                  const uint8_t *packed, int32_t n_nblocks,
+                                  const int32_t *n_starts, const int32_t *n_sizes) {
+    return add_seq(c, side, name, size, packed, true, n_nblocks, n_starts, n_sizes);
+}
+
+// Staged upload of the packed payloads to d_raw (layout: seqs[i].byte_off,
+// 8-byte aligned): host threads copy 32 MB windows into two alternating
+// pinned buffers while the previous window's DMA runs.
+constexpr size_t kPinBytes = 32u << 20;
+
+struct StageJob {
+    const Genome *g;
+    const SeqDev *seqs;
+    int nseq;
+    size_t lo, hi;   // window of the staging layout
+    uint8_t *dst;    // pinned buffer (window start)
+    int nt;
+};
+
+static void *stage_thread_body(StageJob *J, int t) {
+    const size_t len = J->hi - J->lo, per = (len + J->nt - 1) / J->nt;
+    const size_t a = J->lo + std::min(len, per * t), b = J->lo + std::min(len, per * (t + 1));
+    if (a >= b) return nullptr;
+    // sequences overlapping [a, b): binary search the first
+    int lo = 0, hi = J->nseq;
+    while (lo < hi) {
+        const int m = (lo + hi) / 2;
+        const size_t end = (size_t)J->seqs[m].byte_off + ((size_t)J->seqs[m].size + 3) / 4;
+        if (end <= a) lo = m + 1;
+        else hi = m;
+    }
+    size_t pos = a;
+    for (int i = lo; i < J->nseq && pos < b; ++i) {
+        const size_t s0 = (size_t)J->seqs[i].byte_off;
+        const size_t s1 = s0 + ((size_t)J->seqs[i].size + 3) / 4;
+        if (s0 > pos) {  // alignment padding
+            const size_t z = std::min(s0, b) - pos;
+            memset(J->dst + (pos - J->lo), 0, z);
+            pos += z;
+            if (pos >= b) break;
+        }
+        const size_t e = std::min(s1, b);
+        if (e > pos) {
+            memcpy(J->dst + (pos - J->lo), J->g->packed(i) + (pos - s0), e - pos);
+            pos = e;
+        }
+    }
+    if (pos < b) memset(J->dst + (pos - J->lo), 0, b - pos);
+    return nullptr;
+}
+
+struct StageArg {
+    StageJob *J;
+    std::atomic<int> next;
+};
+
+static void *stage_thread(void *p) {
+    StageArg *A = (StageArg *)p;
+    for (int t; (t = A->next.fetch_add(1)) < A->J->nt;) stage_thread_body(A->J, t);
+    return nullptr;
+}
+
+static int upload_payloads(gac_ctx *c, const Genome *g, const SeqDev *seqs, int nseq,
+                           uint8_t *d_raw, size_t raw_bytes) {
+    for (int k = 0; k < 2; ++k) {
+        if (!c->pin[k]) HIPCHK(hipHostMalloc((void **)&c->pin[k], kPinBytes, hipHostMallocDefault));
+        if (!c->pin_ev[k]) HIPCHK(hipEventCreateWithFlags(&c->pin_ev[k], hipEventDisableTiming));
+    }
+    const int nt = std::max(1, std::min(16, gac_host_threads()));
+    int k = 0;
+    for (size_t lo = 0; lo < raw_bytes; lo += kPinBytes, k ^= 1) {
+        const size_t hi = std::min(raw_bytes, lo + kPinBytes);
+        HIPCHK(hipEventSynchronize(c->pin_ev[k]));  // its previous DMA is done
+        StageJob J = {g, seqs, nseq, lo, hi, c->pin[k], nt};
+        StageArg A;
+        A.J = &J;
+        A.next = 0;
+        gac_run_threads(nt, stage_thread, &A);
+        HIPCHK(hipMemcpyAsync(d_raw + lo, c->pin[k], hi - lo, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipEventRecord(c->pin_ev[k], c->stream));
+    }
+    return GAC_OK;
+}
+
 extern "C" int gac_genome_finalize(gac_ctx *c, int side) {
     gac_clear_error();
     Genome *g = side_of(c, side);
@@ -370,8 +476,11 @@ extern "C" int gac_genome_finalize(gac_ctx *c, int side) {
     std::vector<SeqDev> seqs(nseq);
     g->woff.resize(nseq);
     int64_t w = 0;
+    size_t raw_bytes = 0;  // staging layout: payloads 8-byte aligned, in sequence order
     for (int i = 0; i < nseq; ++i) {
-        seqs[i].byte_off = g->raw_off[i];
+        raw_bytes = (raw_bytes + 7) & ~(size_t)7;
+        seqs[i].byte_off = (int64_t)raw_bytes;
+        raw_bytes += ((size_t)g->sizes[i] + 3) / 4;
         seqs[i].word_off = w;
         seqs[i].size = g->sizes[i];
         g->woff[i] = w;
@@ -390,11 +499,10 @@ extern "C" int gac_genome_finalize(gac_ctx *c, int side) {
         uint8_t *d_raw = nullptr;
         SeqDev *d_seqs = nullptr;
         NPiece *d_np = nullptr;
-        const size_t raw_bytes = g->raw.size() + 16;
-        HIPCHK(hipMalloc(&d_raw, raw_bytes));
+        HIPCHK(hipMalloc(&d_raw, raw_bytes + 16));
         HIPCHK(hipMalloc(&d_seqs, nseq * sizeof(SeqDev)));
-        HIPCHK(hipMemcpyAsync(d_raw, g->raw.data(), g->raw.size(), hipMemcpyHostToDevice,
-                              c->stream));
+        int rc = upload_payloads(c, g, seqs.data(), nseq, d_raw, raw_bytes);
+        if (rc != GAC_OK) return rc;
         HIPCHK(hipMemcpyAsync(d_seqs, seqs.data(), nseq * sizeof(SeqDev), hipMemcpyHostToDevice,
                               c->stream));
         HIPCHK(launch_relayout(d_raw, d_seqs, nseq, w, g->planes, g->nmask, c->stream));
@@ -435,11 +543,18 @@ extern "C" int gac_genome_load_2bit(gac_ctx *c, int side, const char *path) {
             ns[k] = (int32_t)gac_twobit_u32(&tb, s.n_starts_raw + 4 * k);
             nz[k] = (int32_t)gac_twobit_u32(&tb, s.n_sizes_raw + 4 * k);
         }
-        rc = gac_genome_add_seq(c, side, s.name, (int32_t)s.size, s.packed, (int32_t)s.n_count,
-                                ns.data(), nz.data());
+        rc = add_seq(c, side, s.name, (int32_t)s.size, s.packed, false, (int32_t)s.n_count,
+                     ns.data(), nz.data());
     }
-    gac_twobit_close(&tb);
-    if (rc != GAC_OK) return rc;
+    if (rc != GAC_OK) {  // the side holds pointers into tb: drop it whole
+        free_genome(*side_of(c, side));
+        gac_twobit_close(&tb);
+        return rc;
+    }
+    // the payloads are read from the mapping at finalize and by gac_genome_view
+    Genome *g = side_of(c, side);
+    g->tb = tb;
+    g->tb_open = true;
     return gac_genome_finalize(c, side);
 }
 
@@ -499,7 +614,7 @@ extern "C" int gac_genome_view(gac_ctx *c, int side, int32_t i, gac_seq_view *v)
     Genome *g = side_of(c, side);
     if (!g || !g->final || i < 0 || i >= (int32_t)g->sizes.size() || !v)
         return gac_fail(GAC_E_ARG, "gac_genome_view: bad argument");
-    v->packed = g->raw.data() + g->raw_off[i];
+    v->packed = g->packed(i);
     v->size = g->sizes[i];
     v->n_start = g->nrun_start.data() + g->nrun_off[i];
     v->n_size = g->nrun_size.data() + g->nrun_off[i];

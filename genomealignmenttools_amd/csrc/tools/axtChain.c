@@ -469,6 +469,13 @@ int main(int argc, char *argv[]) {
         FILE *d = gt_must_open(details, "w");
         fclose(d);
     }
+    /* 2bit genomes: device + genomes come up on a helper thread while the
+     * alignments are read (scoring is set later, by gac_axt_chain) */
+    gt_device dev;
+    memset(&dev, 0, sizeof(dev));
+    const int early_dev = !fa_t && !fa_q && gac_is_twobit_file(tnib) && gac_is_twobit_file(qnib);
+    if (early_dev)
+        gt_device_start(&dev, tnib, qnib, NULL, NULL);
     double t0 = wall();
     pairs P;
     memset(&P, 0, sizeof(P));
@@ -487,22 +494,26 @@ int main(int argc, char *argv[]) {
     gt_verbose(2, "read %d pairs from %s in %.3f s\n", P.n, in, wall() - t0);
     t0 = wall();
     gac_ctx *ctx = NULL;
-    gt_check(gac_open(0, &ctx));
-    if (fa_t) {
-        load_fasta(ctx, GAC_T, tnib);
+    if (early_dev) {
+        ctx = gt_device_join(&dev);
     } else {
-        if (!gac_is_twobit_file(tnib))
-            gt_abort("given tNibDir argument: '%s' is not a 2bit file (nib directories are not supported)\n",
-                     tnib);
-        gt_check(gac_genome_load_2bit(ctx, GAC_T, tnib));
-    }
-    if (fa_q) {
-        load_fasta(ctx, GAC_Q, qnib);
-    } else {
-        if (!gac_is_twobit_file(qnib))
-            gt_abort("given qNibDir argument: '%s' is not a 2bit file (nib directories are not supported)\n",
-                     qnib);
-        gt_check(gac_genome_load_2bit(ctx, GAC_Q, qnib));
+        gt_check(gac_open(0, &ctx));
+        if (fa_t) {
+            load_fasta(ctx, GAC_T, tnib);
+        } else {
+            if (!gac_is_twobit_file(tnib))
+                gt_abort("given tNibDir argument: '%s' is not a 2bit file (nib directories are not supported)\n",
+                         tnib);
+            gt_check(gac_genome_load_2bit(ctx, GAC_T, tnib));
+        }
+        if (fa_q) {
+            load_fasta(ctx, GAC_Q, qnib);
+        } else {
+            if (!gac_is_twobit_file(qnib))
+                gt_abort("given qNibDir argument: '%s' is not a 2bit file (nib directories are not supported)\n",
+                         qnib);
+            gt_check(gac_genome_load_2bit(ctx, GAC_Q, qnib));
+        }
     }
     /* sequences in the order the reference loads them (q, then t, per pair) */
     const int64_t np = P.n;

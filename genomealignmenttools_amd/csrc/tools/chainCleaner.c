@@ -1230,6 +1230,9 @@ int main(int argc, char *argv[]) {
         gt_abort("ERROR: query 2bit file or nib directory %s does not exist\n", qnib);
     if (!gac_is_twobit_file(tnib) || !gac_is_twobit_file(qnib))
         gt_abort("ERROR: only 2bit genome files are supported (got %s, %s)\n", tnib, qnib);
+    /* device + genomes come up on a helper thread during steps 0-2 */
+    gt_device dev;
+    gt_device_start(&dev, tnib, qnib, mat, gap);
 
     /* ---- 0. net the chains if no net is given */
     gt_lines net_lines;
@@ -1387,10 +1390,7 @@ int main(int argc, char *argv[]) {
                          interest.key[order[oi]]);
         free(order);
     }
-    gt_check(gac_open(0, &S.ctx));
-    gt_check(gac_set_scoring(S.ctx, mat, gap));
-    gt_check(gac_genome_load_2bit(S.ctx, GAC_T, tnib));
-    gt_check(gac_genome_load_2bit(S.ctx, GAC_Q, qnib));
+    S.ctx = gt_device_join(&dev);
     {
         const size_t nn = (size_t)(S.nich ? S.nich : 1);
         S.t_seq = malloc(nn * 4);

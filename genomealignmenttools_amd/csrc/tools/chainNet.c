@@ -88,6 +88,13 @@ int main(int argc, char *argv[]) {
     const char *chain_file = argv[1], *tsizes_file = argv[2], *qsizes_file = argv[3];
     const char *tnet = argv[4], *qnet = argv[5];
 
+    /* with -rescore the device and both genomes come up on a helper thread
+     * while the chains are read and netted */
+    gt_device dev;
+    memset(&dev, 0, sizeof(dev));
+    if (rescore)
+        gt_device_start(&dev, tnib, qnib, mat, gap);
+
     gt_sizes qs, ts;
     gt_stage(NULL);
     gt_read_sizes(qsizes_file, &qs);
@@ -173,14 +180,9 @@ int main(int argc, char *argv[]) {
             }
         tscores = calloc(nf ? nf : 1, 8);
         if (nr) {
-            gac_ctx *ctx = NULL;
             gt_stage(NULL);
-            gt_check(gac_open(0, &ctx));
-            gt_stage("device open");
-            gt_check(gac_set_scoring(ctx, mat, gap));
-            gt_check(gac_genome_load_2bit(ctx, GAC_T, tnib));
-            gt_check(gac_genome_load_2bit(ctx, GAC_Q, qnib));
-            gt_stage("2bit genomes to HBM");
+            gac_ctx *ctx = gt_device_join(&dev);
+            gt_stage("device open + 2bit genomes (rest)");
             /* upload only the chains owning a rescored fill (their sequences
              * must be in the 2bit files; others are never looked up) */
             int32_t *remap = malloc(c.n * 4);
@@ -243,6 +245,11 @@ int main(int argc, char *argv[]) {
             free(remap);
             gac_chains_free(cs);
             gac_close(ctx);
+        }
+        if (dev.started) { /* nothing to rescore: the genomes were never needed */
+            gac_ctx *ctx = gt_device_wait(&dev);
+            if (ctx)
+                gac_close(ctx);
         }
         free(fc);
         free(fs);

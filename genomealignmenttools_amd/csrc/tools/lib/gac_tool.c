@@ -18,9 +18,12 @@
 
 /* ------------------------------------------------------------ errors */
 static int g_verbose = 1;
+static void *g_live_dev; /* gt_device whose helper thread may still run HIP calls */
+static void join_live_device(void);
 
 void gt_abort(const char *fmt, ...) {
     va_list ap;
+    join_live_device(); /* never exit under a thread that is inside the HIP runtime */
     fflush(stdout);
     va_start(ap, fmt);
     vfprintf(stderr, fmt, ap);
@@ -50,6 +53,74 @@ void gt_stage(const char *what) {
     if (last >= 0 && what && g_verbose >= 2)
         fprintf(stderr, "[stage] %-32s %8.3f s\n", what, now - last);
     last = now;
+}
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+static void *device_thread(void *arg) {
+    gt_device *d = arg;
+    const double t0 = now_s();
+    d->rc = gac_open(0, &d->ctx);
+    d->open_s = now_s() - t0;
+    if (d->rc == GAC_OK && d->mat)
+        d->rc = gac_set_scoring(d->ctx, d->mat, d->gap);
+    if (d->rc == GAC_OK)
+        d->rc = gac_genome_load_2bit(d->ctx, GAC_T, d->t2bit);
+    if (d->rc == GAC_OK)
+        d->rc = gac_genome_load_2bit(d->ctx, GAC_Q, d->q2bit);
+    d->load_s = now_s() - t0 - d->open_s;
+    if (d->rc != GAC_OK) /* the error text is thread-local */
+        snprintf(d->err, sizeof(d->err), "%s", gac_last_error());
+    return NULL;
+}
+
+void gt_device_start(gt_device *d, const char *t2bit, const char *q2bit, const int32_t mat[16],
+                     const gac_gapcalc *gap) {
+    memset(d, 0, sizeof(*d));
+    d->t2bit = t2bit;
+    d->q2bit = q2bit;
+    d->mat = mat;
+    d->gap = gap;
+    pthread_t th;
+    if (pthread_create(&th, NULL, device_thread, d) != 0)
+        gt_abort("can't start the device thread\n");
+    d->th = (unsigned long)th;
+    d->started = 1;
+    g_live_dev = d;
+}
+
+static void join_live_device(void) {
+    gt_device *d = g_live_dev;
+    if (d && d->started && !pthread_equal(pthread_self(), (pthread_t)d->th)) {
+        pthread_join((pthread_t)d->th, NULL);
+        d->started = 0;
+    }
+    g_live_dev = NULL;
+}
+
+gac_ctx *gt_device_wait(gt_device *d) {
+    if (d->started) {
+        pthread_join((pthread_t)d->th, NULL);
+        d->started = 0;
+    }
+    if (g_live_dev == d)
+        g_live_dev = NULL;
+    return d->rc == GAC_OK ? d->ctx : NULL;
+}
+
+gac_ctx *gt_device_join(gt_device *d) {
+    if (!d->started)
+        gt_abort("gt_device_join: not started\n");
+    gt_device_wait(d);
+    if (d->rc != GAC_OK)
+        gt_abort("%s\n", d->err);
+    gt_verbose(2, "[stage] (overlapped) device open %.3f s, 2bit genomes to HBM %.3f s\n",
+               d->open_s, d->load_s);
+    return d->ctx;
 }
 
 void gt_check(int rc) {
@@ -886,6 +957,54 @@ void gt_write_chain_raw(FILE *f, double score, const char *tname, int32_t tsize,
             fprintf(f, "%d\n", bs[b]);
     }
     fputc('\n', f);
+}
+
+typedef struct pw_job {
+    int64_t n, per;
+    void (*fn)(FILE *, int64_t, void *);
+    void *arg;
+    int64_t next; /* atomic */
+    char **buf;
+    size_t *len;
+} pw_job;
+
+static void *pw_thread(void *p) {
+    pw_job *J = *(pw_job **)p;
+    for (;;) {
+        const int64_t r = __atomic_fetch_add(&J->next, 1, __ATOMIC_RELAXED);
+        const int64_t a = r * J->per;
+        if (a >= J->n)
+            break;
+        const int64_t b = a + J->per < J->n ? a + J->per : J->n;
+        FILE *f = open_memstream(&J->buf[r], &J->len[r]);
+        if (!f)
+            gt_abort("out of memory formatting output\n");
+        for (int64_t i = a; i < b; ++i)
+            J->fn(f, i, J->arg);
+        fclose(f);
+    }
+    return NULL;
+}
+
+void gt_par_write(FILE *out, int64_t n, void (*fn)(FILE *f, int64_t i, void *arg), void *arg) {
+    if (n <= 0)
+        return;
+    const int nt = gt_threads();
+    const int64_t per = n / (8 * (int64_t)nt) + 1, nr = (n + per - 1) / per;
+    pw_job J = {n, per, fn, arg, 0, calloc((size_t)nr, sizeof(char *)),
+                calloc((size_t)nr, sizeof(size_t))};
+    pw_job **args = malloc((size_t)nt * sizeof(pw_job *));
+    for (int t = 0; t < nt; ++t)
+        args[t] = &J;
+    gt_parallel(nt < nr ? nt : (int)nr, pw_thread, args, sizeof(pw_job *));
+    for (int64_t r = 0; r < nr; ++r) {
+        if (J.len[r])
+            fwrite(J.buf[r], 1, J.len[r], out);
+        free(J.buf[r]);
+    }
+    free(args);
+    free(J.buf);
+    free(J.len);
 }
 
 /* ------------------------------------------------------------ sizes */

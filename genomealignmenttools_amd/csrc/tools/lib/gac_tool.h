@@ -26,6 +26,28 @@ void gt_parallel(int n, void *(*fn)(void *), void *args, size_t stride);
 void gt_stage(const char *what);
 void gt_check(int rc); /* abort with gac_last_error() unless GAC_OK */
 
+/* ---- device bring-up off the critical path ----
+ * gt_device_start opens device 0, sets the scoring scheme and uploads both
+ * .2bit genomes on a helper thread, so that HIP runtime start-up and the
+ * genome upload overlap the host's chain parsing / netting; gt_device_join
+ * waits for it and returns the context (aborting with its error, like
+ * gt_check).  mat and gap must stay valid until the join. */
+typedef struct gt_device {
+    const char *t2bit, *q2bit;
+    const int32_t *mat;
+    const gac_gapcalc *gap;
+    gac_ctx *ctx;
+    int rc, started;
+    double open_s, load_s;
+    char err[1024];
+    unsigned long th; /* pthread_t */
+} gt_device;
+void gt_device_start(gt_device *d, const char *t2bit, const char *q2bit, const int32_t mat[16],
+                     const gac_gapcalc *gap);
+gac_ctx *gt_device_join(gt_device *d);
+/* the same wait without the abort: NULL if the bring-up failed */
+gac_ctx *gt_device_wait(gt_device *d);
+
 /* ---- options ---- */
 enum { GT_BOOL, GT_INT, GT_DOUBLE, GT_STRING };
 typedef struct gt_spec {
@@ -107,6 +129,12 @@ void gt_write_chain_raw(FILE *f, double score, const char *tname, int32_t tsize,
                         int32_t tend, const char *qname, int32_t qsize, int qminus,
                         int32_t qstart, int32_t qend, int32_t id, const int32_t *bt,
                         const int32_t *bq, const int32_t *bs, int64_t nb);
+
+/* Ordered parallel output: items [0, n) are cut into contiguous runs, each
+ * printed by fn(f, i, arg) into a per-run memory stream on gt_threads()
+ * threads, and the runs are written to out in order (the bytes equal a
+ * sequential loop's). */
+void gt_par_write(FILE *out, int64_t n, void (*fn)(FILE *f, int64_t i, void *arg), void *arg);
 
 /* ---- chrom.sizes ---- */
 typedef struct gt_sizes {

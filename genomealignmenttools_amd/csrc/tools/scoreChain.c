@@ -42,6 +42,35 @@ static void usage(void) {
         "              *Must* specify this argument to one of these choices.\n");
 }
 
+typedef struct sc_out {
+    const gt_chains *c;
+    const int64_t *glob, *loc;
+    const int32_t *ali, *id;
+    int do_local, force_local, only_score, only_coords;
+} sc_out;
+
+/* one output record (scoreChain.c:301-331) */
+static void write_one(FILE *out, int64_t i, void *arg) {
+    const sc_out *o = arg;
+    const gt_chains *c = o->c;
+    const double g = (double)o->glob[i], l = (double)o->loc[i];
+    double score;
+    if (o->force_local) {
+        score = l;
+    } else {
+        score = g;
+        if (score <= 0 && o->do_local)
+            score = l;
+    }
+    if (o->only_score)
+        fprintf(out, "%d\t%1.0f\t%1.0f\t%d\n", o->id[i], g, l, o->ali[i]);
+    else if (o->only_coords)
+        fprintf(out, "%d\t%d\t%d\t%1.0f\t%1.0f\t%d\n", o->id[i], c->tstart[i], c->tend[i], g, l,
+                o->ali[i]);
+    else
+        gt_write_chain(out, c, i, score, o->id[i]);
+}
+
 int main(int argc, char *argv[]) {
     gt_options(&argc, argv, k_opts);
     const char *gap_name = gt_opt_str("linearGap", NULL);
@@ -72,19 +101,17 @@ int main(int argc, char *argv[]) {
     if (!gac_is_twobit_file(q2bit))
         gt_abort("ERROR: only 2bit files are supported, not %s\n", q2bit);
 
-    gac_ctx *ctx = NULL;
+    /* device open + genome upload run on a helper thread beside the parse */
+    gt_device dev;
     gt_stage(NULL);
-    gt_check(gac_open(0, &ctx));
-    gt_stage("device open");
-    gt_check(gac_set_scoring(ctx, mat, gap));
-    gt_check(gac_genome_load_2bit(ctx, GAC_T, t2bit));
-    gt_check(gac_genome_load_2bit(ctx, GAC_Q, q2bit));
-    gt_stage("2bit genomes to HBM");
+    gt_device_start(&dev, t2bit, q2bit, mat, gap);
 
     FILE *out = gt_must_open(argv[4], "w");
     gt_chains c;
     gt_read_chains(argv[1], &c, -HUGE_VAL, 0);
     gt_stage("read chains");
+    gac_ctx *ctx = gt_device_join(&dev);
+    gt_stage("device open + 2bit genomes (rest)");
 
     /* resolve sequence names (twoBitReadSeqFrag aborts on unknown names) */
     int32_t *tseq = malloc((c.n ? c.n : 1) * 4), *qseq = malloc((c.n ? c.n : 1) * 4);
@@ -111,29 +138,14 @@ int main(int argc, char *argv[]) {
     gt_check(gac_score_ranges(ctx, cs, r, c.n, GAC_WANT_LOCAL, glob, loc, ali));
     gt_stage("GPU scoring");
 
-    static char obuf[1 << 22];
-    setvbuf(out, obuf, _IOFBF, sizeof(obuf));
-    for (int64_t i = 0; i < c.n; ++i) {
-        const double g = (double)glob[i], l = (double)loc[i];
-        double score;
-        if (force_local) {
-            score = l;
-        } else {
-            score = g;
-            if (score <= 0 && do_local)
-                score = l;
-        }
-        int32_t id = c.id[i];
-        if (only_score) {
-            fprintf(out, "%d\t%1.0f\t%1.0f\t%d\n", id, g, l, ali[i]);
-        } else if (only_coords) {
-            fprintf(out, "%d\t%d\t%d\t%1.0f\t%1.0f\t%d\n", id, c.tstart[i], c.tend[i], g, l, ali[i]);
-        } else {
-            if (id == 0) /* chainWriteHead assigns an id (chain.c:203-204) */
-                id = gt_next_chain_id();
-            gt_write_chain(out, &c, i, score, id);
-        }
-    }
+    /* chainWriteHead assigns ids to id-less chains in output order
+     * (chain.c:203-204): fix them before the parallel formatting */
+    int32_t *ids = malloc((c.n ? c.n : 1) * 4);
+    for (int64_t i = 0; i < c.n; ++i)
+        ids[i] = (c.id[i] == 0 && !only_score && !only_coords) ? gt_next_chain_id() : c.id[i];
+    sc_out so = {&c, glob, loc, ali, ids, do_local, force_local, only_score, only_coords};
+    gt_par_write(out, c.n, write_one, &so);
+    free(ids);
     gt_careful_close(out, argv[4]);
     gt_stage("write output");
     free(r);
