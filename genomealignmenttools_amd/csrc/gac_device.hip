@@ -47,6 +47,9 @@ hipError_t launch_block_gaps(const DChain *chains, int64_t n_chains, int4 *blk, 
 hipError_t launch_nflags(const DChain *chains, int64_t n_chains, int4 *blk,
                          const uint32_t *t_nmask, const int64_t *t_woff, const uint32_t *q_nmask,
                          const int64_t *q_woff, hipStream_t s);
+hipError_t launch_build(const int32_t *bt, const int32_t *bq, const int32_t *bs, int64_t nb,
+                        const DChain *chains, int64_t n_chains, int4 *blk, int2 *tspan,
+                        uint32_t *bucket, hipStream_t s);
 hipError_t launch_nruns(const NPiece *p, int64_t n, uint32_t *nmask, hipStream_t s);
 hipError_t launch_blocks(const ScoreArgs &a, const BlockJob *jobs, int64_t n, int32_t *out,
                          hipStream_t s);
@@ -444,12 +447,18 @@ static void *stage_thread(void *p) {
     return nullptr;
 }
 
-static int upload_payloads(gac_ctx *c, const Genome *g, const SeqDev *seqs, int nseq,
-                           uint8_t *d_raw, size_t raw_bytes) {
+static int ensure_pinned(gac_ctx *c) {
     for (int k = 0; k < 2; ++k) {
         if (!c->pin[k]) HIPCHK(hipHostMalloc((void **)&c->pin[k], kPinBytes, hipHostMallocDefault));
         if (!c->pin_ev[k]) HIPCHK(hipEventCreateWithFlags(&c->pin_ev[k], hipEventDisableTiming));
     }
+    return GAC_OK;
+}
+
+static int upload_payloads(gac_ctx *c, const Genome *g, const SeqDev *seqs, int nseq,
+                           uint8_t *d_raw, size_t raw_bytes) {
+    int rc = ensure_pinned(c);
+    if (rc != GAC_OK) return rc;
     const int nt = std::max(1, std::min(16, gac_host_threads()));
     int k = 0;
     for (size_t lo = 0; lo < raw_bytes; lo += kPinBytes, k ^= 1) {
@@ -681,6 +690,117 @@ extern "C" int gac_score_blocks(gac_ctx *c, int64_t n_pairs, const int32_t *t_se
 }
 
 // ----------------------------------------------------------------- chains
+// Host-side build of the device chain set, in parallel over chain ranges
+// balanced by blocks: validation + DChain records (pass 1), bucket-index
+// offsets (serial prefix), then blocks / spans / bucket indexes (pass 2).
+struct UploadJob {
+    gac_ctx *c;
+    const gac_chainset_desc *d;
+    DChain *ch;
+    const int64_t *cut;  // chain ranges per task
+    std::atomic<int> next;
+    int ntask;
+    std::atomic<long long> err_chain;  // first failing chain (pass 1), -1 if none
+};
+
+static void upload_pass1(UploadJob *J, int64_t i0, int64_t i1) {
+    const gac_chainset_desc *d = J->d;
+    gac_ctx *c = J->c;
+    for (int64_t i = i0; i < i1; ++i) {
+        const int32_t ts = d->t_seq[i], qs = d->q_seq[i];
+        DChain &x = J->ch[i];
+        bool bad = ts < 0 || ts >= (int32_t)c->g[0].sizes.size() || qs < 0 ||
+                   qs >= (int32_t)c->g[1].sizes.size();
+        const int64_t b0 = d->blk_off[i], b1 = d->blk_off[i + 1];
+        bad = bad || b0 < 0 || b1 < b0 || b1 > d->n_blocks || b1 - b0 > INT32_MAX;
+        if (!bad) {
+            const int32_t tsize = c->g[0].sizes[ts], qsize = c->g[1].sizes[qs];
+            int64_t pt = 0, pq = 0;
+            for (int64_t b = b0; b < b1 && !bad; ++b) {
+                const int64_t t = d->blk_t[b], q = d->blk_q[b], z = d->blk_size[b];
+                bad = z < 0 || z >= (1 << 29) || t < 0 || q < 0 || t + z > tsize || q + z > qsize ||
+                      (b > b0 && (t < pt || q < pq));
+                pt = t + z;
+                pq = q + z;
+            }
+            x.qinfo = qsize | (d->q_strand[i] ? (int32_t)0x80000000 : 0);
+        }
+        if (bad) {  // reported (with the serial check's message) by the caller
+            long long cur = J->err_chain.load();
+            while ((cur < 0 || i < cur) && !J->err_chain.compare_exchange_weak(cur, i)) {
+            }
+            return;
+        }
+        x.blk_off = b0;
+        x.nblk = (int32_t)(b1 - b0);
+        x.t_seq = ts;
+        x.q_seq = qs;
+        x.tstart = b1 > b0 ? d->blk_t[b0] : 0;
+        x.tend = b1 > b0 ? d->blk_t[b1 - 1] + d->blk_size[b1 - 1] : 0;
+        const int64_t span = (int64_t)x.tend - x.tstart;
+        int shift = 0;
+        while (span > 0 && (((span - 1) >> shift) + 1) > std::max<int64_t>(2 * x.nblk, 1)) ++shift;
+        x.shift = shift;
+        x.pad = 0;
+        x.idx_off = (span > 0 ? ((span - 1) >> shift) + 1 : 0) + 1;  // count until the prefix
+        x.tbase = c->g[0].woff[ts] * 32;
+        const int64_t qw = c->g[1].woff[qs] * 32;
+        x.qbase = x.qinfo < 0 ? ~(qw + (x.qinfo & 0x7fffffff)) : qw;
+    }
+}
+
+static void *upload_thread(void *p) {
+    UploadJob *J = (UploadJob *)p;
+    for (int t; (t = J->next.fetch_add(1)) < J->ntask;) {
+        upload_pass1(J, J->cut[t], J->cut[t + 1]);
+    }
+    return nullptr;
+}
+
+// Pageable host array -> device through the context's pinned staging buffers
+// (threaded copies into one buffer while the other one's DMA runs).
+struct CopyJob {
+    const uint8_t *src;
+    uint8_t *dst;
+    size_t len;
+    int nt;
+    std::atomic<int> next;
+};
+
+static void *copy_thread(void *p) {
+    CopyJob *J = (CopyJob *)p;
+    const size_t per = (J->len + J->nt - 1) / J->nt;
+    for (int t; (t = J->next.fetch_add(1)) < J->nt;) {
+        const size_t a = std::min(J->len, per * t), b = std::min(J->len, per * (t + 1));
+        if (b > a) memcpy(J->dst + a, J->src + a, b - a);
+    }
+    return nullptr;
+}
+
+static int ensure_pinned(gac_ctx *c);
+
+static int upload_staged(gac_ctx *c, void *d_dst, const void *h_src, size_t bytes) {
+    int rc = ensure_pinned(c);
+    if (rc != GAC_OK) return rc;
+    const int nt = std::max(1, std::min(16, gac_host_threads()));
+    int k = 0;
+    for (size_t lo = 0; lo < bytes; lo += kPinBytes, k ^= 1) {
+        const size_t hi = std::min(bytes, lo + kPinBytes);
+        HIPCHK(hipEventSynchronize(c->pin_ev[k]));
+        CopyJob J;
+        J.src = (const uint8_t *)h_src + lo;
+        J.dst = c->pin[k];
+        J.len = hi - lo;
+        J.nt = (hi - lo) >= (4u << 20) ? nt : 1;
+        J.next = 0;
+        gac_run_threads(J.nt, copy_thread, &J);
+        HIPCHK(hipMemcpyAsync((uint8_t *)d_dst + lo, c->pin[k], hi - lo, hipMemcpyHostToDevice,
+                              c->stream));
+        HIPCHK(hipEventRecord(c->pin_ev[k], c->stream));
+    }
+    return GAC_OK;
+}
+
 extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_chainset **out) {
     gac_clear_error();
     if (!c || !d || !out) return gac_fail(GAC_E_ARG, "gac_chains_upload: NULL argument");
@@ -692,8 +812,34 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
         return gac_fail(GAC_E_ARG, "gac_chains_upload: bad descriptor");
     if (d->n_chains && d->blk_off[d->n_chains] != d->n_blocks)
         return gac_fail(GAC_E_ARG, "blk_off[n_chains] != n_blocks");
-    std::vector<DChain> ch(d->n_chains ? d->n_chains : 1);
-    for (int64_t i = 0; i < d->n_chains; ++i) {
+    const int64_t n = d->n_chains;
+    std::vector<DChain> ch(n ? n : 1);
+    // tasks: contiguous chain ranges of about equal blocks + chains
+    const int nt = std::max(1, std::min(64, gac_host_threads()));
+    const int ntask = (int)std::min<int64_t>(std::max<int64_t>(n, 1), 8 * nt);
+    std::vector<int64_t> cut(ntask + 1, n);
+    {
+        const int64_t work = d->n_blocks + n;
+        int64_t i = 0;
+        cut[0] = 0;
+        for (int t = 1; t < ntask; ++t) {
+            const int64_t target = work * t / ntask;
+            while (i < n && d->blk_off[i] + i < target) ++i;
+            cut[t] = i;
+        }
+        cut[ntask] = n;
+    }
+    UploadJob J;
+    J.c = c;
+    J.d = d;
+    J.ch = ch.data();
+    J.cut = cut.data();
+    J.ntask = ntask;
+    J.next = 0;
+    J.err_chain = -1;
+    gac_run_threads(std::min(nt, ntask), upload_thread, &J);
+    if (J.err_chain.load() >= 0) {  // the first bad chain: the serial checks, for the message
+        const int64_t i = J.err_chain.load();
         const int32_t ts = d->t_seq[i], qs = d->q_seq[i];
         if (ts < 0 || ts >= (int32_t)c->g[0].sizes.size() || qs < 0 ||
             qs >= (int32_t)c->g[1].sizes.size())
@@ -717,74 +863,44 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
             pt = t + z;
             pq = q + z;
         }
-        ch[i].blk_off = b0;
-        ch[i].nblk = (int32_t)(b1 - b0);
-        ch[i].t_seq = ts;
-        ch[i].q_seq = qs;
-        ch[i].qinfo = qsize | (d->q_strand[i] ? (int32_t)0x80000000 : 0);
-        ch[i].tstart = b1 > b0 ? d->blk_t[b0] : 0;
-        ch[i].tend = b1 > b0 ? d->blk_t[b1 - 1] + d->blk_size[b1 - 1] : 0;
+        return gac_fail(GAC_E_FORMAT, "chain %lld: invalid", (long long)i);
+    }
+    int64_t idx_n = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t k = ch[i].idx_off;
+        ch[i].idx_off = idx_n;
+        idx_n += k;
     }
     HIPCHK(hipSetDevice(c->device));
-    std::vector<int4> blk((size_t)d->n_blocks + 1);
-    for (int64_t b = 0; b < d->n_blocks; ++b)
-        blk[b] = make_int4(d->blk_t[b], d->blk_q[b], d->blk_size[b], 0);
-    blk[d->n_blocks] = make_int4(0, 0, 0, 0);
-    // per-chain bucket indexes (layout: gac_kernels.h, DChain)
-    int64_t idx_n = 0;
-    for (int64_t i = 0; i < d->n_chains; ++i) {
-        const int64_t nb = ch[i].nblk;
-        const int64_t span = (int64_t)ch[i].tend - ch[i].tstart;
-        int shift = 0;
-        while (span > 0 && (((span - 1) >> shift) + 1) > std::max<int64_t>(2 * nb, 1)) ++shift;
-        ch[i].shift = shift;
-        ch[i].pad = 0;
-        ch[i].idx_off = idx_n;
-        idx_n += (span > 0 ? ((span - 1) >> shift) + 1 : 0) + 1;
-        ch[i].tbase = c->g[0].woff[ch[i].t_seq] * 32;
-        const int64_t qw = c->g[1].woff[ch[i].q_seq] * 32;
-        ch[i].qbase = ch[i].qinfo < 0 ? ~(qw + (ch[i].qinfo & 0x7fffffff)) : qw;
-    }
-    std::vector<uint32_t> bucket((size_t)std::max<int64_t>(idx_n, 1));
-    for (int64_t i = 0; i < d->n_chains; ++i) {
-        const int64_t b0 = ch[i].blk_off, nb = ch[i].nblk;
-        const int64_t span = (int64_t)ch[i].tend - ch[i].tstart;
-        const int64_t nbk = span > 0 ? ((span - 1) >> ch[i].shift) + 1 : 0;
-        uint32_t *bk = bucket.data() + ch[i].idx_off;
-        int64_t b = 0;
-        for (int64_t k = 0; k < nbk; ++k) {
-            const int64_t pos = ch[i].tstart + (k << ch[i].shift);
-            while (b < nb && (int64_t)d->blk_t[b0 + b] + d->blk_size[b0 + b] <= pos) ++b;
-            bk[k] = (uint32_t)b;
-        }
-        bk[nbk] = (uint32_t)nb;
-    }
-    std::vector<int2> tspan((size_t)d->n_blocks + 8, make_int2(INT32_MAX, INT32_MAX));
-    for (int64_t b = 0; b < d->n_blocks; ++b)
-        tspan[b] = make_int2(d->blk_t[b], d->blk_t[b] + d->blk_size[b]);
     gac_chainset *cs = new gac_chainset();
     cs->ctx = c;
     cs->n_chains = d->n_chains;
     cs->n_blocks = d->n_blocks;
+    const size_t nb = (size_t)d->n_blocks;
+    int32_t *d_bt = nullptr;  // caller's block arrays, staged; blocks / spans / buckets are
+                              // built from them on the device (k_build_*)
     hipError_t e = hipMalloc(&cs->chains, ch.size() * sizeof(DChain));
-    if (e == hipSuccess) e = hipMalloc(&cs->blk, blk.size() * sizeof(int4));
-    if (e == hipSuccess)
-        e = hipMemcpy(cs->chains, ch.data(), ch.size() * sizeof(DChain), hipMemcpyHostToDevice);
-    if (e == hipSuccess)
-        e = hipMemcpy(cs->blk, blk.data(), blk.size() * sizeof(int4), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&cs->bucket, bucket.size() * 4);
-    if (e == hipSuccess)
-        e = hipMemcpy(cs->bucket, bucket.data(), bucket.size() * 4, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&cs->tspan, tspan.size() * sizeof(int2));
-    if (e == hipSuccess)
-        e = hipMemcpy(cs->tspan, tspan.data(), tspan.size() * sizeof(int2), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&cs->blk, (nb + 1) * sizeof(int4));
+    if (e == hipSuccess) e = hipMalloc(&cs->bucket, (size_t)std::max<int64_t>(idx_n, 1) * 4);
+    if (e == hipSuccess) e = hipMalloc(&cs->tspan, (nb + 8) * sizeof(int2));
+    if (e == hipSuccess) e = hipMalloc(&d_bt, std::max<size_t>(3 * nb, 1) * 4);
+    int rc = GAC_OK;
+    if (e == hipSuccess) rc = upload_staged(c, cs->chains, ch.data(), ch.size() * sizeof(DChain));
+    if (e == hipSuccess && rc == GAC_OK && nb) rc = upload_staged(c, d_bt, d->blk_t, nb * 4);
+    if (e == hipSuccess && rc == GAC_OK && nb) rc = upload_staged(c, d_bt + nb, d->blk_q, nb * 4);
+    if (e == hipSuccess && rc == GAC_OK && nb) rc = upload_staged(c, d_bt + 2 * nb, d->blk_size, nb * 4);
+    if (e == hipSuccess && rc == GAC_OK)
+        e = launch_build(d_bt, d_bt + nb, d_bt + 2 * nb, (int64_t)nb, cs->chains, cs->n_chains,
+                         cs->blk, cs->tspan, cs->bucket, c->stream);
     // per-block N flags (scoring skips N-mask loads of N-free blocks)
-    if (e == hipSuccess)
+    if (e == hipSuccess && rc == GAC_OK)
         e = launch_nflags(cs->chains, cs->n_chains, cs->blk, c->g[0].nmask, c->g[0].d_woff,
                           c->g[1].nmask, c->g[1].d_woff, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    if (e != hipSuccess) {
+    if (d_bt) hipFree(d_bt);
+    if (e != hipSuccess || rc != GAC_OK) {
         gac_chains_free(cs);
+        if (rc != GAC_OK) return rc;
         return gac_fail(GAC_E_HIP, "chain upload failed: %s", hipGetErrorString(e));
     }
     *out = cs;

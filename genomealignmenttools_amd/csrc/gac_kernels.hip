@@ -205,6 +205,53 @@ __global__ void __launch_bounds__(256) k_nflags(const DChain *chains, int64_t n_
     }
 }
 
+// ------------------------------------------------------------ k_build ----
+// Chain upload, device side: blocks {tStart, qStart, size, 0} and target
+// spans from the caller's plain block arrays (one lane per block), then every
+// chain's bucket index (one wave per chain, one lane per bucket: the first
+// block ending past the bucket's start, by binary search over the spans).
+__global__ void __launch_bounds__(256) k_build_blocks(const int32_t *bt, const int32_t *bq,
+                                                      const int32_t *bs, int64_t nb, int4 *blk,
+                                                      int2 *tspan) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < nb) {
+        const int t = bt[b], z = bs[b];
+        blk[b] = make_int4(t, bq[b], z, 0);
+        tspan[b] = make_int2(t, t + z);
+    } else if (b < nb + 8) {
+        tspan[b] = make_int2(0x7fffffff, 0x7fffffff);
+        if (b == nb) blk[b] = make_int4(0, 0, 0, 0);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_build_buckets(const DChain *chains, int64_t n_chains,
+                                                       const int2 *tspan, uint32_t *bucket) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave_id = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t c = wave_id; c < n_chains; c += nwaves) {
+        const DChain ch = chains[c];
+        const int2 *sp = tspan + ch.blk_off;
+        const int64_t span = (int64_t)ch.tend - ch.tstart;
+        const int64_t nbk = span > 0 ? ((span - 1) >> ch.shift) + 1 : 0;
+        uint32_t *bk = bucket + ch.idx_off;
+        for (int64_t k = lane; k <= nbk; k += kWave) {
+            if (k == nbk) {
+                bk[k] = (uint32_t)ch.nblk;
+                continue;
+            }
+            const int64_t pos = ch.tstart + (k << ch.shift);
+            int lo = 0, hi = ch.nblk;  // first block with tEnd > pos
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if ((int64_t)sp[mid].y > pos) hi = mid;
+                else lo = mid + 1;
+            }
+            bk[k] = (uint32_t)lo;
+        }
+    }
+}
+
 // ------------------------------------------------------------ k_block_gaps
 // Per scoring setup and chain set: blk[b].w = gapCalcCost of the gap from
 // block b to block b+1 of the same chain (0 after a chain's last block).  A
@@ -1010,6 +1057,20 @@ hipError_t launch_block_gaps(const DChain *chains, int64_t n_chains, int4 *blk, 
     const int64_t waves = n_chains < 65536 ? n_chains : 65536;
     hipLaunchKernelGGL(k_block_gaps, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, chains,
                        n_chains, blk, g, small, tab, len);
+    return hipGetLastError();
+}
+
+hipError_t launch_build(const int32_t *bt, const int32_t *bq, const int32_t *bs, int64_t nb,
+                        const DChain *chains, int64_t n_chains, int4 *blk, int2 *tspan,
+                        uint32_t *bucket, hipStream_t s) {
+    const int64_t g = (nb + 8 + 255) / 256;
+    hipLaunchKernelGGL(k_build_blocks, dim3((unsigned)g), dim3(256), 0, s, bt, bq, bs, nb, blk,
+                       tspan);
+    if (n_chains > 0) {
+        const int64_t waves = n_chains < 65536 ? n_chains : 65536;
+        hipLaunchKernelGGL(k_build_buckets, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s,
+                           chains, n_chains, tspan, bucket);
+    }
     return hipGetLastError();
 }
 

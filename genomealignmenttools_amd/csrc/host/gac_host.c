@@ -11,6 +11,7 @@
  */
 #define _GNU_SOURCE
 #include "gac_host.h"
+#include <stdatomic.h>
 
 #include <pthread.h>
 #include <unistd.h>
@@ -702,4 +703,71 @@ void gac_run_threads(int n, void *(*fn)(void *), void *arg) {
     for (int i = 1; i < n; ++i)
         pthread_join(th[i], NULL);
     free(th);
+}
+
+/* ------------------------------------------------------------ output */
+typedef struct po_job {
+    int64_t nr;
+    void (*fn)(FILE *, int64_t, void *);
+    void *arg;
+    char **buf;
+    size_t *len;
+    _Atomic int *ready;
+    _Atomic int64_t next;
+    _Atomic int oom;
+} po_job;
+
+static void *po_thread(void *p) {
+    po_job *J = p;
+    for (;;) {
+        const int64_t r = atomic_fetch_add(&J->next, 1);
+        if (r >= J->nr)
+            break;
+        FILE *f = open_memstream(&J->buf[r], &J->len[r]);
+        if (!f) {
+            atomic_store(&J->oom, 1);
+        } else {
+            J->fn(f, r, J->arg);
+            fclose(f);
+        }
+        atomic_store_explicit(&J->ready[r], 1, memory_order_release);
+    }
+    return NULL;
+}
+
+int gac_par_output(FILE *out, int64_t nr, void (*fn)(FILE *f, int64_t r, void *arg), void *arg) {
+    if (nr <= 0)
+        return 0;
+    po_job J;
+    J.nr = nr;
+    J.fn = fn;
+    J.arg = arg;
+    J.buf = calloc((size_t)nr, sizeof(char *));
+    J.len = calloc((size_t)nr, sizeof(size_t));
+    J.ready = calloc((size_t)nr, sizeof(_Atomic int));
+    atomic_init(&J.next, 0);
+    atomic_init(&J.oom, 0);
+    int nt = gac_host_threads() - 1;
+    if (nt < 1)
+        nt = 1;
+    if (nt > nr)
+        nt = (int)nr;
+    pthread_t *th = malloc((size_t)nt * sizeof(pthread_t));
+    for (int i = 0; i < nt; ++i)
+        pthread_create(&th[i], NULL, po_thread, &J);
+    int bad = 0;
+    for (int64_t r = 0; r < nr; ++r) {
+        while (!atomic_load_explicit(&J.ready[r], memory_order_acquire))
+            usleep(20);
+        if (J.len[r] && fwrite(J.buf[r], 1, J.len[r], out) != J.len[r])
+            bad = 1;
+        free(J.buf[r]);
+    }
+    for (int i = 0; i < nt; ++i)
+        pthread_join(th[i], NULL);
+    free(th);
+    free(J.buf);
+    free(J.len);
+    free((void *)J.ready);
+    return (bad || atomic_load(&J.oom)) ? -1 : 0;
 }

@@ -6,6 +6,7 @@
 
 #include <stddef.h>
 #include <stdint.h>
+#include <stdio.h>
 #include "gachain.h"
 
 #ifdef __cplusplus
@@ -62,6 +63,11 @@ int gac_is_twobit_file(const char *path);
 int gac_host_threads(void);
 /* fn(arg) on n threads (one of them the caller); fn pulls work itself */
 void gac_run_threads(int n, void *(*fn)(void *), void *arg);
+/* Ordered parallel output with formatting and writing overlapped: fn(f, r,
+ * arg) prints run r into a memory stream on worker threads (runs taken in
+ * increasing order), while the calling thread writes the finished runs to
+ * out in order.  0 on success. */
+int gac_par_output(FILE *out, int64_t nr, void (*fn)(FILE *f, int64_t r, void *arg), void *arg);
 
 /* ---- host view of a resident sequence (kept after gac_genome_finalize) ----
  * packed: 2 bits/base MSB-first (T=0 C=1 A=2 G=3); N runs merged and sorted. */

@@ -22,6 +22,7 @@
 #include "gac_host.h"
 
 #include <stdatomic.h>
+#include <math.h>
 #include <stdio.h>
 #include <time.h>
 #include <stdlib.h>
@@ -828,75 +829,124 @@ static int full_size(const gac_net *n, int64_t c) {
 
 /* visibility of each fill: reached by rOutputFill and passing its filters
  * given the score rule; for the T side with rescore the score filter always
- * passes (partial scores are >= 1, netted chains >= minScore = 0). */
+ * passes (partial scores are >= 1, netted chains >= minScore = 0).
+ * Fills in parallel (contiguous index runs), then the visibility DFS in
+ * parallel over chromosomes. */
+typedef struct gf_job {
+    const gac_net *n;
+    int side;
+    int32_t *chain, *start, *end, *ali;
+    uint8_t *flags;
+    int64_t per;
+    _Atomic int64_t next;
+} gf_job;
+
+static void *fills_thread(void *arg) {
+    gf_job *J = arg;
+    const gac_net *n = J->n;
+    const gac_net_input *in = &n->in;
+    const int side = J->side;
+    for (;;) {
+        const int64_t a = atomic_fetch_add(&J->next, 1) * J->per;
+        if (a >= n->n_order[side])
+            break;
+        const int64_t b = a + J->per < n->n_order[side] ? a + J->per : n->n_order[side];
+        for (int64_t i = a; i < b; ++i) {
+            const nfill *f = n->order[side][i];
+            int64_t c = f->chain;
+            int s = f->start, e = f->end;
+            int full, sz;
+            if (side == GAC_Q) {
+                if (in->q_strand[c]) {
+                    int qsize = in->q_sizes[in->q_seq[c]];
+                    int t = s;
+                    s = qsize - e;
+                    e = qsize - t;
+                }
+                full = (s <= in->q_start[c] && e >= in->q_end[c]);
+            } else {
+                full = (s <= in->t_start[c] && e >= in->t_end[c]);
+            }
+            sz = full ? full_size(n, c) : sub_size(n, c, s, e, side == GAC_Q);
+            if (J->chain)
+                J->chain[i] = (int32_t)c;
+            if (J->start)
+                J->start[i] = f->start;
+            if (J->end)
+                J->end[i] = f->end;
+            if (J->ali)
+                J->ali[i] = sz;
+            if (J->flags)
+                J->flags[i] = (uint8_t)(full ? 0 : 1);
+        }
+    }
+    return NULL;
+}
+
+static void *visible_thread(void *arg) {
+    gf_job *J = arg;
+    const gac_net *n = J->n;
+    const int side = J->side;
+    int64_t cap = 1024;
+    typedef struct {
+        const nfill *f;
+        int vis;
+    } item;
+    item *st = malloc(cap * sizeof(item));
+    for (;;) {
+        const int64_t k = atomic_fetch_add(&J->next, 1);
+        if (k >= n->n_chroms[side])
+            break;
+        /* iterative DFS */
+        const nchrom *c = &n->chroms[side][k];
+        if (!c->root->fill_head)
+            continue;
+        int64_t top = 0;
+        for (int i = c->root->n_fills - 1; i >= 0; --i) {
+            if (top == cap) {
+                cap *= 2;
+                st = realloc(st, cap * sizeof(item));
+            }
+            st[top++] = (item){c->root->fills[i], 1};
+        }
+        while (top) {
+            item it = st[--top];
+            const nfill *f = it.f;
+            int sz = J->ali ? J->ali[f->ord] : 0;
+            int vis = it.vis && sz >= n->opt.min_fill;
+            if (vis)
+                J->flags[f->ord] |= 2;
+            for (int g = f->n_gaps - 1; g >= 0; --g) {
+                const ngap *gp = f->gaps[g];
+                for (int j = gp->n_fills - 1; j >= 0; --j) {
+                    if (top == cap) {
+                        cap *= 2;
+                        st = realloc(st, cap * sizeof(item));
+                    }
+                    st[top++] = (item){gp->fills[j], vis};
+                }
+            }
+        }
+    }
+    free(st);
+    return NULL;
+}
+
 int gac_net_get_fills(const gac_net *n, int side, int32_t *chain, int32_t *start, int32_t *end,
                       int32_t *ali, uint8_t *flags) {
     if (!n || (side != GAC_T && side != GAC_Q))
         return gac_fail(GAC_E_ARG, "gac_net_get_fills: bad argument");
-    const gac_net_input *in = &n->in;
-    for (int64_t i = 0; i < n->n_order[side]; ++i) {
-        const nfill *f = n->order[side][i];
-        int64_t c = f->chain;
-        int s = f->start, e = f->end;
-        int full, sz;
-        if (side == GAC_Q) {
-            if (in->q_strand[c]) {
-                int qsize = in->q_sizes[in->q_seq[c]];
-                int t = s;
-                s = qsize - e;
-                e = qsize - t;
-            }
-            full = (s <= in->q_start[c] && e >= in->q_end[c]);
-        } else {
-            full = (s <= in->t_start[c] && e >= in->t_end[c]);
-        }
-        sz = full ? full_size(n, c) : sub_size(n, c, s, e, side == GAC_Q);
-        if (chain)
-            chain[i] = (int32_t)c;
-        if (start)
-            start[i] = f->start;
-        if (end)
-            end[i] = f->end;
-        if (ali)
-            ali[i] = sz;
-        if (flags)
-            flags[i] = (uint8_t)(full ? 0 : 1);
-    }
+    const int nt = gac_host_threads();
+    const int64_t nf = n->n_order[side];
+    gf_job J = {n, side, chain, start, end, ali, flags, nf / (8 * (int64_t)nt) + 1, 0};
+    atomic_init(&J.next, 0);
+    const int64_t nrun = (nf + J.per - 1) / J.per;
+    gac_run_threads(nt < nrun ? nt : (int)(nrun ? nrun : 1), fills_thread, &J);
     /* visibility pass (pre-order: parents precede children) */
     if (flags) {
-        for (int32_t k = 0; k < n->n_chroms[side]; ++k) {
-            /* iterative DFS */
-            const nchrom *c = &n->chroms[side][k];
-            if (!c->root->fill_head)
-                continue;
-            typedef struct {
-                const nfill *f;
-                int vis;
-            } item;
-            int64_t cap = 1024, top = 0;
-            item *st = malloc(cap * sizeof(item));
-            for (int i = c->root->n_fills - 1; i >= 0; --i)
-                st[top++] = (item){c->root->fills[i], 1};
-            while (top) {
-                item it = st[--top];
-                const nfill *f = it.f;
-                int sz = ali ? ali[f->ord] : 0;
-                int vis = it.vis && sz >= n->opt.min_fill;
-                if (vis)
-                    flags[f->ord] |= 2;
-                for (int g = f->n_gaps - 1; g >= 0; --g) {
-                    const ngap *gp = f->gaps[g];
-                    for (int j = gp->n_fills - 1; j >= 0; --j) {
-                        if (top == cap) {
-                            cap *= 2;
-                            st = realloc(st, cap * sizeof(item));
-                        }
-                        st[top++] = (item){gp->fills[j], vis};
-                    }
-                }
-            }
-            free(st);
-        }
+        atomic_store(&J.next, 0);
+        const int nc = n->n_chroms[side];
+        gac_run_threads(nt < nc ? nt : (nc ? nc : 1), visible_thread, &J);
     }
     return GAC_OK;
 }
@@ -911,9 +961,41 @@ typedef struct wctx {
     char *buf;
 } wctx;
 
-static void spaces(FILE *f, int k) {
+/* line formatting without stdio's format parsing (the .net files hold
+ * millions of lines) */
+static char *put_int(char *p, int64_t v) {
+    char tmp[24];
+    int k = 0;
+    uint64_t u = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
+    do {
+        tmp[k++] = (char)('0' + u % 10);
+        u /= 10;
+    } while (u);
+    if (v < 0)
+        *p++ = '-';
+    while (k)
+        *p++ = tmp[--k];
+    return p;
+}
+
+static char *put_str(char *p, const char *s) {
+    while (*s)
+        *p++ = *s++;
+    return p;
+}
+
+/* "%1.0f": integral values (all but the Q net's scaled scores) directly,
+ * the rest through printf (round-half-even) */
+static char *put_score(char *p, double v) {
+    if (v == (double)(int64_t)v && v > -1e15 && v < 1e15 && !(v == 0 && signbit(v)))
+        return put_int(p, (int64_t)v);
+    return p + sprintf(p, "%1.0f", v);
+}
+
+static char *put_spaces(char *p, int k) {
     while (k-- > 0)
-        fputc(' ', f);
+        *p++ = ' ';
+    return p;
 }
 
 static void out_fill(wctx *w, const nfill *f);
@@ -923,9 +1005,30 @@ static void out_gap(wctx *w, const nfill *parent, const ngap *g) {
     const int64_t c = parent->chain;
     const char *ochrom = w->side == GAC_Q ? in->t_names[in->t_seq[c]] : in->q_names[in->q_seq[c]];
     ++w->depth;
-    spaces(w->f, w->depth);
-    fprintf(w->f, "gap %d %d %s %c %d %d\n", g->start, g->end - g->start, ochrom,
-            in->q_strand[c] ? '-' : '+', g->o_start, g->o_end - g->o_start);
+    {
+        char buf[512 + 400], *p = buf;
+        if (strlen(ochrom) > 400 || w->depth > 400) {
+            fprintf(w->f, "%*sgap %d %d %s %c %d %d\n", w->depth, "", g->start,
+                    g->end - g->start, ochrom, in->q_strand[c] ? '-' : '+', g->o_start,
+                    g->o_end - g->o_start);
+        } else {
+            p = put_spaces(p, w->depth);
+            p = put_str(p, "gap ");
+            p = put_int(p, g->start);
+            *p++ = ' ';
+            p = put_int(p, g->end - g->start);
+            *p++ = ' ';
+            p = put_str(p, ochrom);
+            *p++ = ' ';
+            *p++ = in->q_strand[c] ? '-' : '+';
+            *p++ = ' ';
+            p = put_int(p, g->o_start);
+            *p++ = ' ';
+            p = put_int(p, g->o_end - g->o_start);
+            *p++ = '\n';
+            fwrite(buf, 1, (size_t)(p - buf), w->f);
+        }
+    }
     for (int i = 0; i < g->n_fills; ++i)
         out_fill(w, g->fills[i]);
     --w->depth;
@@ -970,11 +1073,35 @@ static void out_fill(wctx *w, const nfill *f) {
     }
     if (score >= n->opt.min_score && sub >= n->opt.min_fill) {
         ++w->depth;
-        spaces(w->f, w->depth);
         const char *ochrom = w->side == GAC_Q ? in->t_names[in->t_seq[c]] : in->q_names[in->q_seq[c]];
-        fprintf(w->f, "fill %d %d %s %c %d %d id %d score %1.0f ali %d\n", f->start,
-                f->end - f->start, ochrom, in->q_strand[c] ? '-' : '+', f->o_start,
-                f->o_end - f->o_start, in->id[c], score, sub);
+        if (strlen(ochrom) > 400 || w->depth > 400 || !(score > -1e300 && score < 1e300)) {
+            fprintf(w->f, "%*sfill %d %d %s %c %d %d id %d score %1.0f ali %d\n", w->depth, "",
+                    f->start, f->end - f->start, ochrom, in->q_strand[c] ? '-' : '+', f->o_start,
+                    f->o_end - f->o_start, in->id[c], score, sub);
+        } else {
+            char buf[512 + 400 + 400], *p = buf;
+            p = put_spaces(p, w->depth);
+            p = put_str(p, "fill ");
+            p = put_int(p, f->start);
+            *p++ = ' ';
+            p = put_int(p, f->end - f->start);
+            *p++ = ' ';
+            p = put_str(p, ochrom);
+            *p++ = ' ';
+            *p++ = in->q_strand[c] ? '-' : '+';
+            *p++ = ' ';
+            p = put_int(p, f->o_start);
+            *p++ = ' ';
+            p = put_int(p, f->o_end - f->o_start);
+            p = put_str(p, " id ");
+            p = put_int(p, in->id[c]);
+            p = put_str(p, " score ");
+            p = put_score(p, score);
+            p = put_str(p, " ali ");
+            p = put_int(p, sub);
+            *p++ = '\n';
+            fwrite(buf, 1, (size_t)(p - buf), w->f);
+        }
         for (int i = 0; i < f->n_gaps; ++i)
             out_gap(w, f, f->gaps[i]);
         --w->depth;
@@ -995,31 +1122,20 @@ typedef struct wjob {
     const int64_t *tscore;
     const witem *items;
     int64_t n_items, per;
-    _Atomic int64_t next;
-    char **buf;
-    size_t *len;
 } wjob;
 
-static void *write_thread(void *arg) {
+static void write_run(FILE *f, int64_t r, void *arg) {
     wjob *J = arg;
-    for (;;) {
-        const int64_t r = atomic_fetch_add(&J->next, 1);
-        const int64_t a = r * J->per;
-        if (a >= J->n_items)
-            break;
-        const int64_t b = a + J->per < J->n_items ? a + J->per : J->n_items;
-        FILE *f = open_memstream(&J->buf[r], &J->len[r]);
-        wctx w = {J->n, f, J->side, J->tscore, 0, NULL};
-        for (int64_t i = a; i < b; ++i) {
-            const nchrom *c = &J->n->chroms[J->side][J->items[i].chrom];
-            if (J->items[i].fill == 0)
-                fprintf(f, "net %s %d\n", c->name, c->size);
-            w.depth = 0;
-            out_fill(&w, c->root->fills[J->items[i].fill]);
-        }
-        fclose(f);
+    const int64_t a = r * J->per;
+    const int64_t b = a + J->per < J->n_items ? a + J->per : J->n_items;
+    wctx w = {J->n, f, J->side, J->tscore, 0, NULL};
+    for (int64_t i = a; i < b; ++i) {
+        const nchrom *c = &J->n->chroms[J->side][J->items[i].chrom];
+        if (J->items[i].fill == 0)
+            fprintf(f, "net %s %d\n", c->name, c->size);
+        w.depth = 0;
+        out_fill(&w, c->root->fills[J->items[i].fill]);
     }
-    return NULL;
 }
 
 int gac_net_write(const gac_net *n, int side, const int64_t *tscores, const char *path,
@@ -1053,22 +1169,12 @@ int gac_net_write(const gac_net *n, int side, const int64_t *tscores, const char
                 items[ni++] = (witem){k, i};
     }
     const int nt = gac_host_threads();
-    int64_t per = ni / (8 * (int64_t)nt) + 1;
+    int64_t per = ni / (64 * (int64_t)nt) + 1;
     const int64_t nr = (ni + per - 1) / per;
-    wjob J = {n, side, side == GAC_T ? tscores : NULL, items, ni, per, 0, NULL, NULL};
-    atomic_init(&J.next, 0);
-    J.buf = calloc((size_t)(nr ? nr : 1), sizeof(char *));
-    J.len = calloc((size_t)(nr ? nr : 1), sizeof(size_t));
-    gac_run_threads(nt < nr ? nt : (int)(nr ? nr : 1), write_thread, &J);
-    for (int64_t r = 0; r < nr; ++r) {
-        if (J.len[r])
-            fwrite(J.buf[r], 1, J.len[r], f);
-        free(J.buf[r]);
-    }
-    free(J.buf);
-    free(J.len);
+    wjob J = {n, side, side == GAC_T ? tscores : NULL, items, ni, per};
+    int wbad = gac_par_output(f, nr, write_run, &J);
     free(items);
-    int bad = ferror(f);
+    int bad = ferror(f) || wbad;
     if (close_it) {
         if (fclose(f) != 0)
             bad = 1;

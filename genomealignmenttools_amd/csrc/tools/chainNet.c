@@ -8,6 +8,7 @@
  * replacing the per-fill chainSubsetOnT + chainCalcScore of subchainInfo
  * (:795-843). */
 #include <math.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -48,6 +49,25 @@ static void usage(int min_space, double min_score) {
         "   -scoreScheme=fileName       Read the scoring matrix from a blastz-format file\n"
         "   -linearGap=<medium|loose|filename> Specify type of linearGap to use.\n",
         min_space, min_score);
+}
+
+typedef struct net_out {
+    const gac_net *net;
+    int side;
+    const int64_t *tscores;
+    const char *path;
+    const gt_chains *c;
+    int threaded, rc;
+    char err[1024];
+} net_out;
+
+static void *write_net(void *arg) {
+    net_out *w = arg;
+    w->rc = gac_net_write(w->net, w->side, w->tscores, w->path, (const char *const *)w->c->meta,
+                          w->c->n_meta);
+    if (w->rc != GAC_OK) /* thread-local error text */
+        snprintf(w->err, sizeof(w->err), "%s", gac_last_error());
+    return NULL;
 }
 
 int main(int argc, char *argv[]) {
@@ -132,6 +152,7 @@ int main(int argc, char *argv[]) {
             gt_abort("%s is %d in %s but %d in %s", tn, c.tsize[i], chain_file, ts.size[tix[i]],
                      tsizes_file);
     }
+    gt_stage("chain checks");
     gac_net_input in;
     memset(&in, 0, sizeof(in));
     in.n_chains = c.n;
@@ -180,7 +201,7 @@ int main(int argc, char *argv[]) {
             }
         tscores = calloc(nf ? nf : 1, 8);
         if (nr) {
-            gt_stage(NULL);
+            gt_stage("fill list");
             gac_ctx *ctx = gt_device_join(&dev);
             gt_stage("device open + 2bit genomes (rest)");
             /* upload only the chains owning a rescored fill (their sequences
@@ -204,13 +225,14 @@ int main(int argc, char *argv[]) {
                 if (remap[i] >= 0)
                     src[remap[i]] = i;
             goff[0] = 0;
+            int32_t *tmap = gt_seq_map(ctx, GAC_T, &c.tnames), *qmap = gt_seq_map(ctx, GAC_Q, &c.qnames);
             for (int64_t j = 0; j < nsub; ++j) {
                 const int64_t i = src[j];
                 const char *tn = c.tnames.names[c.tname[i]], *qn = c.qnames.names[c.qname[i]];
-                gts[j] = gac_genome_seq_index(ctx, GAC_T, tn);
+                gts[j] = tmap[c.tname[i]];
                 if (gts[j] < 0)
                     gt_abort("%s is not in %s", tn, tnib);
-                gqs[j] = gac_genome_seq_index(ctx, GAC_Q, qn);
+                gqs[j] = qmap[c.qname[i]];
                 if (gqs[j] < 0)
                     gt_abort("%s is not in %s", qn, qnib);
                 gst[j] = c.qstrand[i];
@@ -220,6 +242,8 @@ int main(int argc, char *argv[]) {
                 memcpy(gbs + goff[j], c.bs + b0, nb * 4);
                 goff[j + 1] = goff[j] + nb;
             }
+            free(tmap);
+            free(qmap);
             for (int64_t k = 0; k < nr; ++k)
                 r[k].chain = remap[r[k].chain];
             gac_chainset_desc d = {nsub, gts, gqs, gst, goff, nbsub, gbt, gbq, gbs};
@@ -245,6 +269,7 @@ int main(int argc, char *argv[]) {
             free(remap);
             gac_chains_free(cs);
             gac_close(ctx);
+            gt_stage("device close");
         }
         if (dev.started) { /* nothing to rescore: the genomes were never needed */
             gac_ctx *ctx = gt_device_wait(&dev);
@@ -259,18 +284,24 @@ int main(int argc, char *argv[]) {
         free(r);
         free(rix);
     }
+    /* the two nets are independent files: written concurrently */
     gt_verbose(1, "writing %s\n", tnet);
-    gt_check(gac_net_write(net, GAC_T, tscores, tnet, (const char *const *)c.meta, c.n_meta));
     gt_verbose(1, "writing %s\n", qnet);
-    gt_check(gac_net_write(net, GAC_Q, NULL, qnet, (const char *const *)c.meta, c.n_meta));
+    net_out wo[2] = {{net, GAC_T, tscores, tnet, &c, 0, {0}}, {net, GAC_Q, NULL, qnet, &c, 0, {0}}};
+    pthread_t qth;
+    if (pthread_create(&qth, NULL, write_net, &wo[1]) != 0)
+        write_net(&wo[1]);
+    else
+        wo[1].threaded = 1;
+    write_net(&wo[0]);
+    if (wo[1].threaded)
+        pthread_join(qth, NULL);
+    for (int k = 0; k < 2; ++k)
+        if (wo[k].rc != GAC_OK)
+            gt_abort("%s\n", wo[k].err);
     gt_stage("write nets");
-    free(tscores);
-    gac_net_free(net);
+    /* the net, chains and sizes are left to process exit (freeing millions
+     * of arena blocks and arrays only costs time) */
     gac_gapcalc_free(gap);
-    gt_chains_free(&c);
-    gt_sizes_free(&qs);
-    gt_sizes_free(&ts);
-    free(tix);
-    free(qix);
     return 0;
 }

@@ -928,19 +928,52 @@ void gt_chains_free(gt_chains *c) {
 
 int gt_next_chain_id(void) { return g_next_id++; }
 
+/* decimal text of v at p, returns the end */
+static char *put_int(char *p, int64_t v) {
+    char tmp[24];
+    int k = 0;
+    uint64_t u = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
+    do {
+        tmp[k++] = (char)('0' + u % 10);
+        u /= 10;
+    } while (u);
+    if (v < 0)
+        *p++ = '-';
+    while (k)
+        *p++ = tmp[--k];
+    return p;
+}
+
+/* block lines "size\tdt\tdq" and the last "size", then the blank line
+ * (chainWrite, chain.c:214-226), formatted without stdio */
+static void write_blocks(FILE *f, const int32_t *bt, const int32_t *bq, const int32_t *bs,
+                         int64_t nb) {
+    char buf[1 << 14];
+    char *p = buf;
+    for (int64_t b = 0; b < nb; ++b) {
+        if (p - buf > (int)sizeof(buf) - 64) {
+            fwrite(buf, 1, (size_t)(p - buf), f);
+            p = buf;
+        }
+        p = put_int(p, bs[b]);
+        if (b + 1 < nb) {
+            *p++ = '\t';
+            p = put_int(p, (int64_t)bt[b + 1] - (bt[b] + bs[b]));
+            *p++ = '\t';
+            p = put_int(p, (int64_t)bq[b + 1] - (bq[b] + bs[b]));
+        }
+        *p++ = '\n';
+    }
+    *p++ = '\n';
+    fwrite(buf, 1, (size_t)(p - buf), f);
+}
+
 void gt_write_chain(FILE *f, const gt_chains *c, int64_t i, double score, int32_t id) {
     fprintf(f, "chain %1.0f %s %d + %d %d %s %d %c %d %d %d\n", score, c->tnames.names[c->tname[i]],
             c->tsize[i], c->tstart[i], c->tend[i], c->qnames.names[c->qname[i]], c->qsize[i],
             c->qstrand[i] ? '-' : '+', c->qstart[i], c->qend[i], id);
-    const int64_t b0 = c->blk_off[i], b1 = c->blk_off[i + 1];
-    for (int64_t b = b0; b < b1; ++b) {
-        if (b + 1 < b1)
-            fprintf(f, "%d\t%d\t%d\n", c->bs[b], c->bt[b + 1] - (c->bt[b] + c->bs[b]),
-                    c->bq[b + 1] - (c->bq[b] + c->bs[b]));
-        else
-            fprintf(f, "%d\n", c->bs[b]);
-    }
-    fputc('\n', f);
+    const int64_t b0 = c->blk_off[i];
+    write_blocks(f, c->bt + b0, c->bq + b0, c->bs + b0, c->blk_off[i + 1] - b0);
 }
 
 void gt_write_chain_raw(FILE *f, double score, const char *tname, int32_t tsize, int32_t tstart,
@@ -949,62 +982,37 @@ void gt_write_chain_raw(FILE *f, double score, const char *tname, int32_t tsize,
                         const int32_t *bq, const int32_t *bs, int64_t nb) {
     fprintf(f, "chain %1.0f %s %d + %d %d %s %d %c %d %d %d\n", score, tname, tsize, tstart, tend,
             qname, qsize, qminus ? '-' : '+', qstart, qend, id);
-    for (int64_t b = 0; b < nb; ++b) {
-        if (b + 1 < nb)
-            fprintf(f, "%d\t%d\t%d\n", bs[b], bt[b + 1] - (bt[b] + bs[b]),
-                    bq[b + 1] - (bq[b] + bs[b]));
-        else
-            fprintf(f, "%d\n", bs[b]);
-    }
-    fputc('\n', f);
+    write_blocks(f, bt, bq, bs, nb);
+}
+
+int32_t *gt_seq_map(gac_ctx *ctx, int side, const gt_names *names) {
+    int32_t *m = malloc((size_t)(names->n ? names->n : 1) * 4);
+    for (int32_t k = 0; k < names->n; ++k)
+        m[k] = gac_genome_seq_index(ctx, side, names->names[k]);
+    return m;
 }
 
 typedef struct pw_job {
     int64_t n, per;
     void (*fn)(FILE *, int64_t, void *);
     void *arg;
-    int64_t next; /* atomic */
-    char **buf;
-    size_t *len;
 } pw_job;
 
-static void *pw_thread(void *p) {
-    pw_job *J = *(pw_job **)p;
-    for (;;) {
-        const int64_t r = __atomic_fetch_add(&J->next, 1, __ATOMIC_RELAXED);
-        const int64_t a = r * J->per;
-        if (a >= J->n)
-            break;
-        const int64_t b = a + J->per < J->n ? a + J->per : J->n;
-        FILE *f = open_memstream(&J->buf[r], &J->len[r]);
-        if (!f)
-            gt_abort("out of memory formatting output\n");
-        for (int64_t i = a; i < b; ++i)
-            J->fn(f, i, J->arg);
-        fclose(f);
-    }
-    return NULL;
+static void pw_run(FILE *f, int64_t r, void *p) {
+    pw_job *J = p;
+    const int64_t a = r * J->per, b = a + J->per < J->n ? a + J->per : J->n;
+    for (int64_t i = a; i < b; ++i)
+        J->fn(f, i, J->arg);
 }
 
 void gt_par_write(FILE *out, int64_t n, void (*fn)(FILE *f, int64_t i, void *arg), void *arg) {
     if (n <= 0)
         return;
-    const int nt = gt_threads();
-    const int64_t per = n / (8 * (int64_t)nt) + 1, nr = (n + per - 1) / per;
-    pw_job J = {n, per, fn, arg, 0, calloc((size_t)nr, sizeof(char *)),
-                calloc((size_t)nr, sizeof(size_t))};
-    pw_job **args = malloc((size_t)nt * sizeof(pw_job *));
-    for (int t = 0; t < nt; ++t)
-        args[t] = &J;
-    gt_parallel(nt < nr ? nt : (int)nr, pw_thread, args, sizeof(pw_job *));
-    for (int64_t r = 0; r < nr; ++r) {
-        if (J.len[r])
-            fwrite(J.buf[r], 1, J.len[r], out);
-        free(J.buf[r]);
-    }
-    free(args);
-    free(J.buf);
-    free(J.len);
+    /* runs of ~256 KB of text: small enough to overlap formatting with writing */
+    const int64_t per = n / (64 * (int64_t)gt_threads()) + 1;
+    pw_job J = {n, per, fn, arg};
+    if (gac_par_output(out, (n + per - 1) / per, pw_run, &J) != 0)
+        gt_abort("write error\n");
 }
 
 /* ------------------------------------------------------------ sizes */

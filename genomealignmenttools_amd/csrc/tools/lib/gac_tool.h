@@ -130,6 +130,10 @@ void gt_write_chain_raw(FILE *f, double score, const char *tname, int32_t tsize,
                         int32_t qstart, int32_t qend, int32_t id, const int32_t *bt,
                         const int32_t *bq, const int32_t *bs, int64_t nb);
 
+/* sequence index (gac_genome_seq_index) of every name of a chain file's
+ * name table, -1 where absent (malloc'ed) */
+int32_t *gt_seq_map(gac_ctx *ctx, int side, const gt_names *names);
+
 /* Ordered parallel output: items [0, n) are cut into contiguous runs, each
  * printed by fn(f, i, arg) into a per-run memory stream on gt_threads()
  * threads, and the runs are written to out in order (the bytes equal a

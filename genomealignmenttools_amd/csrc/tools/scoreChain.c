@@ -115,14 +115,17 @@ int main(int argc, char *argv[]) {
 
     /* resolve sequence names (twoBitReadSeqFrag aborts on unknown names) */
     int32_t *tseq = malloc((c.n ? c.n : 1) * 4), *qseq = malloc((c.n ? c.n : 1) * 4);
+    int32_t *tmap = gt_seq_map(ctx, GAC_T, &c.tnames), *qmap = gt_seq_map(ctx, GAC_Q, &c.qnames);
     for (int64_t i = 0; i < c.n; ++i) {
-        tseq[i] = gac_genome_seq_index(ctx, GAC_T, c.tnames.names[c.tname[i]]);
+        tseq[i] = tmap[c.tname[i]];
         if (tseq[i] < 0)
             gt_abort("%s is not in %s", c.tnames.names[c.tname[i]], t2bit);
-        qseq[i] = gac_genome_seq_index(ctx, GAC_Q, c.qnames.names[c.qname[i]]);
+        qseq[i] = qmap[c.qname[i]];
         if (qseq[i] < 0)
             gt_abort("%s is not in %s", c.qnames.names[c.qname[i]], q2bit);
     }
+    free(tmap);
+    free(qmap);
     gac_chainset_desc d = {c.n, tseq, qseq, c.qstrand, c.blk_off, c.nb, c.bt, c.bq, c.bs};
     gac_chainset *cs = NULL;
     gt_check(gac_chains_upload(ctx, &d, &cs));
@@ -148,15 +151,9 @@ int main(int argc, char *argv[]) {
     free(ids);
     gt_careful_close(out, argv[4]);
     gt_stage("write output");
-    free(r);
-    free(glob);
-    free(loc);
-    free(ali);
-    free(tseq);
-    free(qseq);
+    /* host arrays are left to process exit; the device context is closed */
     gac_chains_free(cs);
-    gac_gapcalc_free(gap);
-    gt_chains_free(&c);
     gac_close(ctx);
+    gt_stage("device close");
     return 0;
 }

@@ -344,6 +344,43 @@ def c2_case(seed: int = 42, n_chains: int = 200_000, sizes_dir: Optional[str] = 
     return tg, qg, ca
 
 
+def concat_chains(parts: List[ChainArrays]) -> ChainArrays:
+    """Chain sets one after another (block offsets rebased)."""
+    offs, base = [np.zeros(1, np.int64)], 0
+    for p in parts:
+        offs.append(p.blk_off[1:] + base)
+        base += int(p.blk_off[-1])
+    cat = lambda k: np.concatenate([getattr(p, k) for p in parts])
+    return ChainArrays(
+        score=cat("score"), tname=[x for p in parts for x in p.tname], tsize=cat("tsize"),
+        tstart=cat("tstart"), tend=cat("tend"), qname=[x for p in parts for x in p.qname],
+        qsize=cat("qsize"), qstrand=cat("qstrand"), qstart=cat("qstart"), qend=cat("qend"),
+        id=cat("id"), blk_off=np.concatenate(offs), blk_t=cat("blk_t"), blk_q=cat("blk_q"),
+        blk_size=cat("blk_size"))
+
+
+def c5_case(seed: int = 1234, n_chains: int = 1_000_000, sizes_dir: Optional[str] = None):
+    """SURVEY §8(d) C5 at a stated chain count: every hg38 sequence (455) as
+    target x every mm10 sequence (66) as query, chains per target sequence in
+    proportion to its length, C2's chain model on each; one score-sorted set
+    (ids 1..n)."""
+    here = sizes_dir or os.path.join(os.path.dirname(__file__), "data")
+    hg = read_sizes(os.path.join(here, "hg38.chrom.sizes"))
+    mm = read_sizes(os.path.join(here, "mm10.chrom.sizes"))
+    tg = random_genome(hg, seed, n_frac=0.005, n_mean=20_000)
+    qg = random_genome(mm, seed + 1, n_frac=0.005, n_mean=20_000)
+    total = float(sum(hg.values()))
+    parts = []
+    for k, (name, size) in enumerate(hg.items()):
+        nc = int(round(n_chains * size / total))
+        if nc > 0:
+            parts.append(make_chains(tg, name, qg, SynthConfig(n_chains=nc, seed=seed + 7 * (k + 1))))
+    ca = concat_chains(parts)
+    ca = ca.subset(np.argsort(-ca.score, kind="stable"))
+    ca.id = np.arange(1, ca.n + 1, dtype=np.int64)
+    return tg, qg, ca
+
+
 # ---------------------------------------------------------------- chainCleaner loci
 def _mutate(rng, codes: np.ndarray, div: float) -> np.ndarray:
     r = rng.random(len(codes))

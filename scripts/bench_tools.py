@@ -195,9 +195,80 @@ def chainnet(a):
     print(json.dumps(res), flush=True)
 
 
+def host_info():
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"host_cpu": model, "host_nproc": os.cpu_count(),
+            "threads": int(os.environ.get("GAC_THREADS") or os.environ.get("OMP_NUM_THREADS") or 0)
+            or os.cpu_count()}
+
+
+def c5(a):
+    """Whole-genome C5 (every hg38 x every mm10 sequence) at --chains chains:
+    scoreChain and chainNet -rescore end to end, ours vs the reference
+    binaries on this host, outputs compared byte for byte."""
+    d = os.path.join(a.tmp, f"c5_{a.chains}_{a.seed}")
+    os.makedirs(d, exist_ok=True)
+    p = lambda x: os.path.join(d, x)
+    gen_s = 0.0
+    if not os.path.exists(p("in.chain")):
+        t = time.time()
+        tg, qg, ca = synth.c5_case(a.seed, a.chains)
+        synth.write_2bit(tg, p("t.2bit"))
+        synth.write_2bit(qg, p("q.2bit"))
+        synth.write_sizes(tg.sizes, p("t.sizes"))
+        synth.write_sizes(qg.sizes, p("q.sizes"))
+        chainfile.write_chains(ca, p("in.chain.tmp"))
+        os.rename(p("in.chain.tmp"), p("in.chain"))
+        info = {"chains": ca.n, "blocks": int(len(ca.blk_size)), "aligned_bases": ca.aligned_bases(),
+                "t_seqs": len(tg.names), "q_seqs": len(qg.names),
+                "t_seqs_with_chains": len(set(ca.tname))}
+        with open(p("info.json"), "w") as f:
+            json.dump(info, f)
+        del tg, qg, ca
+        gen_s = time.time() - t
+        log(f"C5: {info} generated in {gen_s:.1f}s")
+    with open(p("info.json")) as f:
+        info = json.load(f)
+    res = {"tool": "C5 scoreChain + chainNet -rescore", "seed": a.seed, **info, **host_info(),
+           "gen_s": round(gen_s, 1)}
+    sc_args = [p("in.chain"), p("t.2bit"), p("q.2bit")]
+    t1, r1 = timed([os.path.join(BIN, "scoreChain")] + sc_args + [p("ours.sc.chain"),
+                                                                   "-linearGap=loose", "-verbose=2"])
+    cn_args = [p("in.chain"), p("t.sizes"), p("q.sizes")]
+    opts = ["-rescore", f"-tNibDir={p('t.2bit')}", f"-qNibDir={p('q.2bit')}", "-linearGap=loose"]
+    t2, r2 = timed([os.path.join(BIN, "chainNet")] + cn_args + [p("ours.t.net"), p("ours.q.net")] +
+                   opts + ["-verbose=2"])
+    res.update(ours_scorechain_s=round(t1, 3), ours_chainnet_s=round(t2, 3),
+               ours_s=round(t1 + t2, 3),
+               ours_stages=[l for l in (r1.stderr + r2.stderr).splitlines() if "[stage]" in l],
+               ours_gbases_per_s=round(2 * info["aligned_bases"] / (t1 + t2) / 1e9, 3))
+    log(f"ours: scoreChain {t1:.2f}s chainNet {t2:.2f}s")
+    if os.path.exists(os.path.join(REF, "chainNet")) and not a.no_ref:
+        t3, _ = timed([os.path.join(REF, "scoreChain")] + sc_args + [p("ref.sc.chain"),
+                                                                      "-linearGap=loose"])
+        log(f"ref scoreChain {t3:.2f}s")
+        t4, _ = timed([os.path.join(REF, "chainNet")] + cn_args + [p("ref.t.net"), p("ref.q.net")] +
+                      opts)
+        log(f"ref chainNet {t4:.2f}s")
+        res.update(ref_scorechain_s=round(t3, 3), ref_chainnet_s=round(t4, 3),
+                   ref_s=round(t3 + t4, 3), ref_cores=1, speedup=round((t3 + t4) / (t1 + t2), 2),
+                   identical={"scoreChain": filecmp.cmp(p("ours.sc.chain"), p("ref.sc.chain"), False),
+                              "t.net": filecmp.cmp(p("ours.t.net"), p("ref.t.net"), False),
+                              "q.net": filecmp.cmp(p("ours.q.net"), p("ref.q.net"), False)})
+    print(json.dumps(res), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("tool", choices=["axtchain", "cleaner", "scorechain", "chainnet"])
+    ap.add_argument("tool", choices=["axtchain", "cleaner", "scorechain", "chainnet", "c5"])
     ap.add_argument("--chains", type=int, default=200_000)
     ap.add_argument("--blocks", type=int, default=2_000_000)
     ap.add_argument("--tsize", type=int, default=60_000_000)
@@ -208,9 +279,9 @@ def main():
     ap.add_argument("--tmp", default=os.environ.get("TMPDIR", "/tmp"))
     a = ap.parse_args()
     if a.seed is None:
-        a.seed = 42 if a.tool in ("scorechain", "chainnet") else 7
+        a.seed = {"scorechain": 42, "chainnet": 42, "c5": 1234}.get(a.tool, 7)
     {"axtchain": axtchain, "cleaner": cleaner, "scorechain": scorechain,
-     "chainnet": chainnet}[a.tool](a)
+     "chainnet": chainnet, "c5": c5}[a.tool](a)
 
 
 if __name__ == "__main__":
