@@ -3,7 +3,8 @@
  * Same fill/gap trees, same .net text as the reference's
  * src/chainNet/chainNet.c, without its O(fills x blocks) list rescans:
  *   makeChroms / addSpaceForGap / findSpaces   :328-354, :289-300, :527-544
- *       -> per-chromosome treap of disjoint spaces, in-order range query
+ *       -> per-chromosome B+tree of disjoint spaces, in-order range query;
+ *          a filled space is replaced by its remnants and inner gaps at once
  *   addChainT / addChainQ / fillSpace / innerBounds / strictlyInside
  *       :557-679, :487-523, :356-391, :321-325
  *       -> identical decisions; the gap scan stops at the first gap that
@@ -51,18 +52,12 @@ struct nfill {
     int64_t ord; /* pre-order index on its side */
 };
 
-typedef struct tnode {
-    int start, end;
-    ngap *gap;
-    uint32_t prio;
-    int32_t l, r;
-} tnode;
-
 typedef struct nchrom {
     const char *name;
     int size;
     ngap *root;
-    int32_t troot;
+    int32_t sroot; /* space index root (a leaf when height == 0) */
+    int32_t height;
 } nchrom;
 
 /* ------------------------------------------------------------ arena */
@@ -101,12 +96,14 @@ static void arena_free(arena *a) {
  * each in score order, and nothing else is shared). */
 typedef struct nwork {
     arena ar;
-    tnode *tn;
-    int32_t tn_n, tn_cap, tn_free;
-    uint32_t rng;
-    /* scratch for findSpaces */
-    int32_t *fs;
-    int64_t fs_n, fs_cap;
+    /* space index pools (shared by the chromosomes this worker nets) */
+    struct sleaf *lf;
+    int32_t lf_n, lf_cap, lf_free;
+    struct snode *in;
+    int32_t in_n, in_cap, in_free;
+    /* scratch: findSpaces result, a fill's new spaces, leaf split runs */
+    struct sitem *q, *it, *cmb;
+    int64_t q_n, q_cap, it_n, it_cap, cmb_cap;
     /* scratch for reversed blocks */
     int32_t *rs, *re, *ros, *roe;
     int64_t r_cap;
@@ -127,112 +124,318 @@ struct gac_net {
     int64_t n_order[2];
 };
 
-/* ------------------------------------------------------------ treap */
-static uint32_t net_rand(nwork *n) {
-    n->rng ^= n->rng << 13;
-    n->rng ^= n->rng >> 17;
-    n->rng ^= n->rng << 5;
-    return n->rng;
-}
+/* ------------------------------------------------------------ space index */
+/* The open spaces of one chromosome side (chainNet.c's per-chrom rbTree of
+ * spaces, :289-300): disjoint [start, end) intervals, each pointing at the
+ * gap it lies in.  A B+tree over start with wide nodes, so a chain's range
+ * query and the replacement of a filled space by its remnants and inner gaps
+ * touch a few cache lines instead of a treap's ~30 dependent nodes.  Leaves
+ * are linked in order; inner separators are kept exact (key[i] = smallest
+ * start under child i, i >= 1); empty leaves are unlinked. */
+#define SP_LF 32    /* spaces per leaf */
+#define SP_IF 32    /* children per inner node */
+#define SP_FILL 24  /* entries per node after a split */
+#define SP_MAXH 24
 
-static int32_t tn_new(nwork *n, int start, int end, ngap *gap) {
+typedef struct sleaf {
+    int32_t n, next, prev, pad;
+    int32_t start[SP_LF], end[SP_LF];
+    ngap *gap[SP_LF];
+} sleaf;
+
+typedef struct snode {
+    int32_t n;
+    int32_t child[SP_IF];
+    int64_t key[SP_IF]; /* spkey of the smallest space under child i (i >= 1) */
+} snode;
+
+/* spaces ordered by (start, end): only zero-length spaces (-minSpace=0) share
+ * a start */
+static inline int64_t spkey(int32_t s, int32_t e) { return ((int64_t)s << 32) | (uint32_t)e; }
+
+typedef struct sitem {
+    int32_t start, end;
+    ngap *gap;
+} sitem;
+
+static int32_t sp_new_leaf(nwork *w) {
     int32_t i;
-    if (n->tn_free >= 0) {
-        i = n->tn_free;
-        n->tn_free = n->tn[i].l;
+    if (w->lf_free >= 0) {
+        i = w->lf_free;
+        w->lf_free = w->lf[i].next;
     } else {
-        if (n->tn_n == n->tn_cap) {
-            n->tn_cap = n->tn_cap ? n->tn_cap * 2 : 1 << 16;
-            n->tn = realloc(n->tn, (size_t)n->tn_cap * sizeof(tnode));
+        if (w->lf_n == w->lf_cap) {
+            w->lf_cap = w->lf_cap ? w->lf_cap * 2 : 1 << 12;
+            w->lf = realloc(w->lf, (size_t)w->lf_cap * sizeof(sleaf));
         }
-        i = n->tn_n++;
+        i = w->lf_n++;
     }
-    tnode *t = &n->tn[i];
-    t->start = start;
-    t->end = end;
-    t->gap = gap;
-    t->prio = net_rand(n);
-    t->l = t->r = -1;
+    w->lf[i].n = 0;
+    w->lf[i].next = w->lf[i].prev = -1;
     return i;
 }
 
-static void tn_release(nwork *n, int32_t i) {
-    n->tn[i].l = n->tn_free;
-    n->tn_free = i;
-}
-
-/* split by start: l gets starts < key, r gets starts >= key */
-static void tn_split(nwork *n, int32_t t, int key, int32_t *l, int32_t *r) {
-    if (t < 0) {
-        *l = *r = -1;
-        return;
-    }
-    if (n->tn[t].start < key) {
-        tn_split(n, n->tn[t].r, key, &n->tn[t].r, r);
-        *l = t;
+static int32_t sp_new_inner(nwork *w) {
+    int32_t i;
+    if (w->in_free >= 0) {
+        i = w->in_free;
+        w->in_free = w->in[i].child[0];
     } else {
-        tn_split(n, n->tn[t].l, key, l, &n->tn[t].l);
-        *r = t;
+        if (w->in_n == w->in_cap) {
+            w->in_cap = w->in_cap ? w->in_cap * 2 : 1 << 10;
+            w->in = realloc(w->in, (size_t)w->in_cap * sizeof(snode));
+        }
+        i = w->in_n++;
+    }
+    w->in[i].n = 0;
+    return i;
+}
+
+static void sp_init(nwork *w, nchrom *c, int start, int end, ngap *gap) {
+    const int32_t l = sp_new_leaf(w);
+    w->lf[l].n = 1;
+    w->lf[l].start[0] = start;
+    w->lf[l].end[0] = end;
+    w->lf[l].gap[0] = gap;
+    c->sroot = l;
+    c->height = 0;
+}
+
+/* descend to the leaf holding the last space with start <= key; pn/pi = the
+ * inner node and child index taken at each depth (root = depth 0) */
+static int32_t sp_descend(const nwork *w, const nchrom *c, int64_t key, int32_t *pn, int *pi) {
+    int32_t x = c->sroot;
+    for (int d = 0; d < c->height; ++d) {
+        const snode *s = &w->in[x];
+        int i = s->n - 1;
+        while (i > 0 && s->key[i] > key)
+            --i;
+        if (pn) {
+            pn[d] = x;
+            pi[d] = i;
+        }
+        x = s->child[i];
+    }
+    return x;
+}
+
+static int sp_leaf_pos(const sleaf *L, int64_t key) {
+    int i = L->n - 1;
+    while (i >= 0 && spkey(L->start[i], L->end[i]) > key)
+        --i;
+    return i;
+}
+
+static void sq_push(nwork *w, int32_t s, int32_t e, ngap *g) {
+    if (w->q_n == w->q_cap) {
+        w->q_cap = w->q_cap ? w->q_cap * 2 : 1024;
+        w->q = realloc(w->q, (size_t)w->q_cap * sizeof(sitem));
+    }
+    w->q[w->q_n++] = (sitem){s, e, g};
+}
+
+/* spaces overlapping [qs, qe) in order (spaceCmp == 0, chainNet.c:277-287)
+ * into w->q */
+static void sp_query(nwork *w, const nchrom *c, int qs, int qe) {
+    w->q_n = 0;
+    const int64_t k = spkey(qs, 0x7fffffff);
+    int32_t l = sp_descend(w, c, k, NULL, NULL);
+    int i = sp_leaf_pos(&w->lf[l], k);
+    if (i < 0)
+        i = 0;
+    while (l >= 0) {
+        const sleaf *L = &w->lf[l];
+        for (; i < L->n; ++i) {
+            if (L->start[i] >= qe)
+                return;
+            if (L->end[i] > qs)
+                sq_push(w, L->start[i], L->end[i], L->gap[i]);
+        }
+        l = L->next;
+        i = 0;
     }
 }
 
-static int32_t tn_merge(nwork *n, int32_t a, int32_t b) {
-    if (a < 0)
-        return b;
-    if (b < 0)
-        return a;
-    if (n->tn[a].prio > n->tn[b].prio) {
-        n->tn[a].r = tn_merge(n, n->tn[a].r, b);
-        return a;
-    }
-    n->tn[b].l = tn_merge(n, a, n->tn[b].l);
-    return b;
-}
-
-static void tn_insert(nwork *n, int32_t *root, int32_t node) {
-    int32_t l, r;
-    tn_split(n, *root, n->tn[node].start, &l, &r);
-    *root = tn_merge(n, tn_merge(n, l, node), r);
-}
-
-static void tn_erase(nwork *n, int32_t *root, int key) {
-    /* spaces are disjoint: start is a unique key */
-    int32_t *p = root;
-    while (*p >= 0) {
-        tnode *t = &n->tn[*p];
-        if (t->start == key) {
-            *p = tn_merge(n, t->l, t->r);
+/* the smallest start under the child at depth d changed to v: fix the one
+ * separator that holds it */
+static void sp_fix_sep(nwork *w, const int32_t *pn, const int *pi, int d, int64_t v) {
+    for (int k = d - 1; k >= 0; --k)
+        if (pi[k] > 0) {
+            w->in[pn[k]].key[pi[k]] = v;
             return;
         }
-        p = (key < t->start) ? &t->l : &t->r;
+}
+
+/* remove child pi[d] of inner node pn[d] (its subtree is already gone) */
+static void sp_inner_remove(nwork *w, nchrom *c, const int32_t *pn, const int *pi, int d) {
+    const int32_t x = pn[d];
+    snode *s = &w->in[x];
+    const int i = pi[d];
+    const int64_t first_key = s->n > 1 ? s->key[1] : 0;
+    memmove(s->key + i, s->key + i + 1, (size_t)(s->n - i - 1) * 8);
+    memmove(s->child + i, s->child + i + 1, (size_t)(s->n - i - 1) * 4);
+    --s->n;
+    if (s->n == 0) {
+        if (d == 0) { /* the whole tree is empty: one empty leaf */
+            s->child[0] = w->in_free;
+            w->in_free = x;
+            c->sroot = sp_new_leaf(w);
+            c->height = 0;
+            return;
+        }
+        s->child[0] = w->in_free;
+        w->in_free = x;
+        sp_inner_remove(w, c, pn, pi, d - 1);
+    } else if (i == 0) {
+        sp_fix_sep(w, pn, pi, d, first_key); /* old key[1] is the new minimum */
     }
 }
 
-static void fs_push(nwork *n, int32_t v) {
-    if (n->fs_n == n->fs_cap) {
-        n->fs_cap = n->fs_cap ? n->fs_cap * 2 : 1024;
-        n->fs = realloc(n->fs, n->fs_cap * sizeof(int32_t));
+/* insert (key, child) pairs after child pi[d] of node pn[d], splitting as
+ * needed (a new root when the root splits) */
+static void sp_inner_insert(nwork *w, nchrom *c, const int32_t *pn, const int *pi, int d,
+                            const int64_t *keys, const int32_t *childs, int cnt) {
+    if (d < 0) { /* above the root: a new root over the old one and the new nodes */
+        int32_t r = sp_new_inner(w);
+        snode *s = &w->in[r];
+        s->key[0] = 0;
+        s->child[0] = c->sroot;
+        s->n = 1;
+        int32_t pn2[1] = {r};
+        int pi2[1] = {0};
+        c->sroot = r;
+        c->height += 1;
+        sp_inner_insert(w, c, pn2, pi2, 0, keys, childs, cnt);
+        return;
     }
-    n->fs[n->fs_n++] = v;
+    const int32_t x = pn[d];
+    const int at = pi[d] + 1, n0 = w->in[x].n, tot = n0 + cnt;
+    if (tot <= SP_IF) {
+        snode *s = &w->in[x];
+        memmove(s->key + at + cnt, s->key + at, (size_t)(n0 - at) * 8);
+        memmove(s->child + at + cnt, s->child + at, (size_t)(n0 - at) * 4);
+        memcpy(s->key + at, keys, (size_t)cnt * 8);
+        memcpy(s->child + at, childs, (size_t)cnt * 4);
+        s->n = tot;
+        return;
+    }
+    /* combined sequence, cut into nodes of SP_FILL */
+    int64_t *ck = malloc((size_t)tot * 8);
+    int32_t *cc = malloc((size_t)tot * 4);
+    {
+        const snode *s = &w->in[x];
+        memcpy(ck, s->key, (size_t)at * 8);
+        memcpy(cc, s->child, (size_t)at * 4);
+        memcpy(ck + at, keys, (size_t)cnt * 8);
+        memcpy(cc + at, childs, (size_t)cnt * 4);
+        memcpy(ck + at + cnt, s->key + at, (size_t)(n0 - at) * 8);
+        memcpy(cc + at + cnt, s->child + at, (size_t)(n0 - at) * 4);
+    }
+    const int parts = (tot + SP_FILL - 1) / SP_FILL;
+    int64_t *nk = malloc((size_t)parts * 8);
+    int32_t *nc = malloc((size_t)parts * 4);
+    for (int p = 0; p < parts; ++p) {
+        const int lo = (int)((int64_t)tot * p / parts), hi = (int)((int64_t)tot * (p + 1) / parts);
+        const int32_t y = p == 0 ? x : sp_new_inner(w);
+        snode *s = &w->in[y];
+        memcpy(s->key, ck + lo, (size_t)(hi - lo) * 8);
+        memcpy(s->child, cc + lo, (size_t)(hi - lo) * 4);
+        s->n = hi - lo;
+        nk[p] = ck[lo];
+        nc[p] = y;
+    }
+    free(ck);
+    free(cc);
+    sp_inner_insert(w, c, pn, pi, d - 1, nk + 1, nc + 1, parts - 1);
+    free(nk);
+    free(nc);
 }
 
-/* in-order spaces overlapping [qs, qe) (spaceCmp == 0, chainNet.c:277-287) */
-static void tn_range(nwork *n, int32_t t, int qs, int qe) {
-    while (t >= 0) {
-        tnode *x = &n->tn[t];
-        if (x->end > qs)
-            tn_range(n, x->l, qs, qe);
-        if (x->end > qs && x->start < qe)
-            fs_push(n, t);
-        if (x->start < qe)
-            t = x->r;
-        else
-            break;
+/* replace the space [sstart, send) by items[0..m) (sorted, inside it) */
+static void sp_replace(nwork *w, nchrom *c, int sstart, int send, const sitem *it, int m) {
+    int32_t pn[SP_MAXH];
+    int pi[SP_MAXH];
+    const int32_t l = sp_descend(w, c, spkey(sstart, send), pn, pi);
+    const int idx = sp_leaf_pos(&w->lf[l], spkey(sstart, send));
+    if (idx < 0 || w->lf[l].start[idx] != sstart || w->lf[l].end[idx] != send) {
+        fprintf(stderr, "gac_net: internal error: space %d-%d not indexed\n", sstart, send);
+        abort();
     }
-}
-
-static void add_space_for_gap(nwork *n, nchrom *c, ngap *g) {
-    tn_insert(n, &c->troot, tn_new(n, g->start, g->end, g));
+    const int n0 = w->lf[l].n, tot = n0 - 1 + m, H = c->height;
+    if (tot == 0) {
+        if (H == 0) {
+            w->lf[l].n = 0;
+            return;
+        }
+        sleaf *L = &w->lf[l];
+        if (L->prev >= 0)
+            w->lf[L->prev].next = L->next;
+        if (L->next >= 0)
+            w->lf[L->next].prev = L->prev;
+        L->next = w->lf_free;
+        w->lf_free = l;
+        sp_inner_remove(w, c, pn, pi, H - 1);
+        return;
+    }
+    if (idx == 0)
+        sp_fix_sep(w, pn, pi, H, m > 0 ? spkey(it[0].start, it[0].end)
+                                       : spkey(w->lf[l].start[1], w->lf[l].end[1]));
+    if (tot <= SP_LF) {
+        sleaf *L = &w->lf[l];
+        memmove(L->start + idx + m, L->start + idx + 1, (size_t)(n0 - idx - 1) * 4);
+        memmove(L->end + idx + m, L->end + idx + 1, (size_t)(n0 - idx - 1) * 4);
+        memmove(L->gap + idx + m, L->gap + idx + 1, (size_t)(n0 - idx - 1) * sizeof(ngap *));
+        for (int k = 0; k < m; ++k) {
+            L->start[idx + k] = it[k].start;
+            L->end[idx + k] = it[k].end;
+            L->gap[idx + k] = it[k].gap;
+        }
+        L->n = tot;
+        return;
+    }
+    /* combined run, cut into leaves of SP_FILL linked after l */
+    if (w->cmb_cap < tot) {
+        w->cmb_cap = tot * 2;
+        w->cmb = realloc(w->cmb, (size_t)w->cmb_cap * sizeof(sitem));
+    }
+    sitem *cb = w->cmb;
+    {
+        const sleaf *L = &w->lf[l];
+        for (int k = 0; k < idx; ++k)
+            cb[k] = (sitem){L->start[k], L->end[k], L->gap[k]};
+        memcpy(cb + idx, it, (size_t)m * sizeof(sitem));
+        for (int k = idx + 1; k < n0; ++k)
+            cb[k - 1 + m] = (sitem){L->start[k], L->end[k], L->gap[k]};
+    }
+    const int parts = (tot + SP_FILL - 1) / SP_FILL;
+    int64_t *nk = malloc((size_t)parts * 8);
+    int32_t *nc = malloc((size_t)parts * 4);
+    int32_t prev = -1;
+    const int32_t after = w->lf[l].next;
+    for (int p = 0; p < parts; ++p) {
+        const int lo = (int)((int64_t)tot * p / parts), hi = (int)((int64_t)tot * (p + 1) / parts);
+        const int32_t y = p == 0 ? l : sp_new_leaf(w);
+        sleaf *L = &w->lf[y];
+        for (int k = lo; k < hi; ++k) {
+            L->start[k - lo] = cb[k].start;
+            L->end[k - lo] = cb[k].end;
+            L->gap[k - lo] = cb[k].gap;
+        }
+        L->n = hi - lo;
+        if (p > 0) {
+            L->prev = prev;
+            w->lf[prev].next = y;
+        }
+        prev = y;
+        nk[p] = spkey(cb[lo].start, cb[lo].end);
+        nc[p] = y;
+    }
+    w->lf[prev].next = after;
+    if (after >= 0)
+        w->lf[after].prev = prev;
+    sp_inner_insert(w, c, pn, pi, H - 1, nk + 1, nc + 1, parts - 1);
+    free(nk);
+    free(nc);
 }
 
 static ngap *gap_new(nwork *n, int s, int e, int os, int oe) {
@@ -249,24 +452,28 @@ static int strictly_inside(const gac_net *n, int min_start, int max_end, int sta
     return min_start < start && start + n->opt.min_space <= end && end < max_end;
 }
 
+static void it_push(nwork *w, int32_t s, int32_t e, ngap *g) {
+    if (w->it_n == w->it_cap) {
+        w->it_cap = w->it_cap ? w->it_cap * 2 : 1024;
+        w->it = realloc(w->it, (size_t)w->it_cap * sizeof(sitem));
+    }
+    w->it[w->it_n++] = (sitem){s, e, g};
+}
+
 /* Generic addChainT/addChainQ on one side.  s[],e[] = this side's block
  * coordinates in list order (+ strand coords), os_gap/oe_gap = other-side
- * gap bounds per block (gap between block b and b+1). */
+ * gap bounds per block (gap between block b and b+1).  Each filled space is
+ * replaced in the index by its remnants and the chain's gaps strictly inside
+ * it, in one leaf update (fillSpace + addSpaceForGap, chainNet.c:487-523). */
 static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int32_t chain, int nb,
                            const int32_t *s, const int32_t *e, const int32_t *gos,
                            const int32_t *goe, int cstart, int cend) {
-    n->fs_n = 0;
-    tn_range(n, c->troot, cstart, cend);
-    int64_t nsp = n->fs_n;
-    if (nsp == 0)
-        return;
-    int32_t *sp = malloc(nsp * sizeof(int32_t));
-    memcpy(sp, n->fs, nsp * sizeof(int32_t));
+    sp_query(n, c, cstart, cend);
+    const int64_t nsp = n->q_n;
     int k = 0;
     for (int64_t si = 0; si < nsp; ++si) {
-        int32_t ti = sp[si];
-        const int sstart = n->tn[ti].start, send = n->tn[ti].end;
-        ngap *sgap = n->tn[ti].gap;
+        const int sstart = n->q[si].start, send = n->q[si].end;
+        ngap *sgap = n->q[si].gap;
         while (k + 1 < nb && s[k + 1] <= sstart)
             ++k;
         /* innerBounds (chainNet.c:356-391) */
@@ -293,28 +500,27 @@ static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int32_t chai
         f->start = start;
         f->end = end;
         f->chain = chain;
-        tn_erase(n, &c->troot, sstart);
-        if (start - sstart >= net->opt.min_space)
-            tn_insert(n, &c->troot, tn_new(n, sstart, start, sgap));
-        if (send - end >= net->opt.min_space)
-            tn_insert(n, &c->troot, tn_new(n, end, send, sgap));
         f->next = sgap->fill_head;
         sgap->fill_head = f;
-        /* gaps strictly inside the space */
+        n->it_n = 0;
+        if (start - sstart >= net->opt.min_space)
+            it_push(n, sstart, start, sgap);
+        /* gaps strictly inside the space (all inside [start, end]) */
         for (int b = k; b + 1 < nb; ++b) {
             int gs = e[b], ge = s[b + 1];
             if (ge >= send)
                 break;
             if (strictly_inside(net, sstart, send, gs, ge)) {
                 ngap *g = gap_new(n, gs, ge, gos[b], goe[b]);
-                add_space_for_gap(n, c, g);
+                it_push(n, gs, ge, g);
                 g->next = f->gap_head;
                 f->gap_head = g;
             }
         }
-        tn_release(n, ti);
+        if (send - end >= net->opt.min_space)
+            it_push(n, end, send, sgap);
+        sp_replace(n, c, sstart, send, n->it, (int)n->it_n);
     }
-    free(sp);
 }
 
 static void ensure_rev(nwork *n, int64_t nb) {
@@ -550,8 +756,11 @@ void gac_net_free(gac_net *n) {
     for (int i = 0; i < n->n_w; ++i) {
         nwork *w = &n->w[i];
         arena_free(&w->ar);
-        free(w->tn);
-        free(w->fs);
+        free(w->lf);
+        free(w->in);
+        free(w->q);
+        free(w->it);
+        free(w->cmb);
         free(w->rs);
         free(w->re);
         free(w->ros);
@@ -630,7 +839,7 @@ static void *net_thread(void *arg) {
         /* makeChroms (chainNet.c:328-354): one gap = one space over the
          * whole sequence */
         c->root = gap_new(w, 0, c->size, 0, 0);
-        add_space_for_gap(w, c, c->root);
+        sp_init(w, c, 0, c->size, c->root);
         for (int64_t i = 0; i < t->n; ++i) {
             if (t->side == GAC_T)
                 add_chain_t(J->n, w, t->chains[i]);
@@ -652,10 +861,8 @@ int gac_net_build(const gac_net_input *in, const gac_net_opts *opt, gac_net **ou
     n->n_w = gac_host_threads();
     n->w = calloc((size_t)n->n_w, sizeof(nwork));
     for (int k = 0; k < n->n_w; ++k) {
-        n->w[k].tn_free = -1;
-        /* xorshift seeds must be non-zero (a zero seed stays zero and
-         * degenerates the treap into a list) */
-        n->w[k].rng = (0x9E3779B9u ^ (0x85EBCA6Bu * (uint32_t)(k + 1))) | 1u;
+        n->w[k].lf_free = -1;
+        n->w[k].in_free = -1;
     }
     /* chains to net: in order until the first below minScore (must be
      * sorted), haplotype queries skipped unless incl_hap */
@@ -710,7 +917,7 @@ int gac_net_build(const gac_net_input *in, const gac_net_opts *opt, gac_net **ou
             nchrom *c = &n->chroms[side][k];
             c->name = names[k];
             c->size = sizes[k];
-            c->troot = -1;
+            c->sroot = -1;
         }
     }
     /* tasks, largest first; every task nets one chromosome of one side */

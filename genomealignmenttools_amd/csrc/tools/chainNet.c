@@ -287,7 +287,7 @@ int main(int argc, char *argv[]) {
     /* the two nets are independent files: written concurrently */
     gt_verbose(1, "writing %s\n", tnet);
     gt_verbose(1, "writing %s\n", qnet);
-    net_out wo[2] = {{net, GAC_T, tscores, tnet, &c, 0, {0}}, {net, GAC_Q, NULL, qnet, &c, 0, {0}}};
+    net_out wo[2] = {{net, GAC_T, tscores, tnet, &c, 0, 0}, {net, GAC_Q, NULL, qnet, &c, 0, 0}};
     pthread_t qth;
     if (pthread_create(&qth, NULL, write_net, &wo[1]) != 0)
         write_net(&wo[1]);
