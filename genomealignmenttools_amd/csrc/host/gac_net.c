@@ -45,8 +45,7 @@ struct ngap {
 struct nfill {
     int start, end, o_start, o_end;
     int32_t chain;
-    ngap *gap_head;
-    ngap **gaps;
+    ngap **gaps; /* ascending (created in block order at fill time) */
     int n_gaps;
     nfill *next;
     int64_t ord; /* pre-order index on its side */
@@ -207,9 +206,15 @@ static int32_t sp_descend(const nwork *w, const nchrom *c, int64_t key, int32_t 
     int32_t x = c->sroot;
     for (int d = 0; d < c->height; ++d) {
         const snode *s = &w->in[x];
-        int i = s->n - 1;
-        while (i > 0 && s->key[i] > key)
-            --i;
+        int lo = 1, hi = s->n; /* first i >= 1 with key[i] > key, minus one */
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s->key[mid] > key)
+                hi = mid;
+            else
+                lo = mid + 1;
+        }
+        const int i = lo - 1;
         if (pn) {
             pn[d] = x;
             pi[d] = i;
@@ -220,10 +225,15 @@ static int32_t sp_descend(const nwork *w, const nchrom *c, int64_t key, int32_t 
 }
 
 static int sp_leaf_pos(const sleaf *L, int64_t key) {
-    int i = L->n - 1;
-    while (i >= 0 && spkey(L->start[i], L->end[i]) > key)
-        --i;
-    return i;
+    int lo = 0, hi = L->n; /* first i with spkey > key, minus one */
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (spkey(L->start[mid], L->end[mid]) > key)
+            hi = mid;
+        else
+            lo = mid + 1;
+    }
+    return lo - 1;
 }
 
 static void sq_push(nwork *w, int32_t s, int32_t e, ngap *g) {
@@ -235,24 +245,54 @@ static void sq_push(nwork *w, int32_t s, int32_t e, ngap *g) {
 }
 
 /* spaces overlapping [qs, qe) in order (spaceCmp == 0, chainNet.c:277-287)
- * into w->q */
-static void sp_query(nwork *w, const nchrom *c, int qs, int qe) {
+ * into w->q, leaving out those that overlap none of the chain's blocks
+ * s[k], e[k] (sorted, disjoint): innerBounds finds nothing in them, so
+ * addChain skips them anyway.  Runs of spaces inside one chain gap are
+ * jumped over by a descent instead of a scan. */
+static void sp_query(nwork *w, const nchrom *c, int qs, int qe, const int32_t *bs,
+                     const int32_t *be, int nb) {
     w->q_n = 0;
-    const int64_t k = spkey(qs, 0x7fffffff);
-    int32_t l = sp_descend(w, c, k, NULL, NULL);
-    int i = sp_leaf_pos(&w->lf[l], k);
-    if (i < 0)
-        i = 0;
-    while (l >= 0) {
-        const sleaf *L = &w->lf[l];
-        for (; i < L->n; ++i) {
-            if (L->start[i] >= qe)
-                return;
-            if (L->end[i] > qs)
-                sq_push(w, L->start[i], L->end[i], L->gap[i]);
+    int k = 0; /* first block with end > the current space's start */
+    int64_t key = spkey(qs, 0x7fffffff);
+    for (;;) {
+        int32_t l = sp_descend(w, c, key, NULL, NULL);
+        int i = sp_leaf_pos(&w->lf[l], key);
+        if (i < 0)
+            i = 0;
+        int jump = 0;
+        while (l >= 0 && !jump) {
+            const sleaf *L = &w->lf[l];
+            for (; i < L->n; ++i) {
+                const int ss = L->start[i], se = L->end[i];
+                if (ss >= qe)
+                    return;
+                if (se <= qs)
+                    continue;
+                while (k < nb && be[k] <= ss)
+                    ++k;
+                if (k == nb)
+                    return; /* past the last block */
+                if (bs[k] < se) {
+                    sq_push(w, ss, se, L->gap[i]);
+                } else if (L->end[L->n - 1] <= bs[k] && L->next >= 0) {
+                    /* the rest of this leaf lies in the gap before block k:
+                     * on to the next leaf, or, when that one starts inside
+                     * the gap too, a descent to the space holding bs[k]
+                     * (which is then past this leaf: progress) */
+                    if (w->lf[L->next].start[0] <= bs[k]) {
+                        key = spkey(bs[k], 0x7fffffff);
+                        jump = 1;
+                    }
+                    break;
+                }
+            }
+            if (!jump) {
+                l = L->next;
+                i = 0;
+            }
         }
-        l = L->next;
-        i = 0;
+        if (!jump)
+            return;
     }
 }
 
@@ -468,7 +508,7 @@ static void it_push(nwork *w, int32_t s, int32_t e, ngap *g) {
 static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int32_t chain, int nb,
                            const int32_t *s, const int32_t *e, const int32_t *gos,
                            const int32_t *goe, int cstart, int cend) {
-    sp_query(n, c, cstart, cend);
+    sp_query(n, c, cstart, cend, s, e, nb);
     const int64_t nsp = n->q_n;
     int k = 0;
     for (int64_t si = 0; si < nsp; ++si) {
@@ -506,17 +546,18 @@ static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int32_t chai
         if (start - sstart >= net->opt.min_space)
             it_push(n, sstart, start, sgap);
         /* gaps strictly inside the space (all inside [start, end]) */
+        const int64_t g0 = n->it_n;
         for (int b = k; b + 1 < nb; ++b) {
             int gs = e[b], ge = s[b + 1];
             if (ge >= send)
                 break;
-            if (strictly_inside(net, sstart, send, gs, ge)) {
-                ngap *g = gap_new(n, gs, ge, gos[b], goe[b]);
-                it_push(n, gs, ge, g);
-                g->next = f->gap_head;
-                f->gap_head = g;
-            }
+            if (strictly_inside(net, sstart, send, gs, ge))
+                it_push(n, gs, ge, gap_new(n, gs, ge, gos[b], goe[b]));
         }
+        f->n_gaps = (int)(n->it_n - g0);
+        f->gaps = f->n_gaps ? arena_alloc(&n->ar, f->n_gaps * sizeof(ngap *)) : NULL;
+        for (int i = 0; i < f->n_gaps; ++i)
+            f->gaps[i] = n->it[g0 + i].gap;
         if (send - end >= net->opt.min_space)
             it_push(n, end, send, sgap);
         sp_replace(n, c, sstart, send, n->it, (int)n->it_n);
@@ -605,11 +646,6 @@ static void add_chain_t(const gac_net *net, nwork *n, int64_t c) {
 /* ------------------------------------------------------------ finish */
 static int cmp_fill(const void *a, const void *b) {
     const nfill *x = *(nfill *const *)a, *y = *(nfill *const *)b;
-    return (x->start > y->start) - (x->start < y->start);
-}
-
-static int cmp_gap(const void *a, const void *b) {
-    const ngap *x = *(ngap *const *)a, *y = *(ngap *const *)b;
     return (x->start > y->start) - (x->start < y->start);
 }
 
@@ -716,35 +752,46 @@ typedef struct fin_ctx {
 static void finish_gap(fin_ctx *x, ngap *g);
 
 static void finish_fill(fin_ctx *x, nfill *f) {
-    fill_other_range(x->n, f, x->side == GAC_Q);
     if (x->n_ord == x->cap) {
         x->cap = x->cap ? x->cap * 2 : 256;
         x->ord = realloc(x->ord, (size_t)x->cap * sizeof(nfill *));
     }
     x->ord[x->n_ord++] = f;
-    int cnt = 0;
-    for (ngap *g = f->gap_head; g; g = g->next)
-        ++cnt;
-    f->n_gaps = cnt;
-    f->gaps = cnt ? arena_alloc(&x->w->ar, cnt * sizeof(ngap *)) : NULL;
-    cnt = 0;
-    for (ngap *g = f->gap_head; g; g = g->next)
-        f->gaps[cnt++] = g;
-    qsort(f->gaps, f->n_gaps, sizeof(ngap *), cmp_gap);
     for (int i = 0; i < f->n_gaps; ++i)
         finish_gap(x, f->gaps[i]);
 }
 
-static void finish_gap(fin_ctx *x, ngap *g) {
+static void sort_gap_fills(nwork *w, ngap *g) {
+    if (!g->fill_head) {
+        g->n_fills = 0;
+        g->fills = NULL;
+        return;
+    }
     int cnt = 0;
     for (nfill *f = g->fill_head; f; f = f->next)
         ++cnt;
     g->n_fills = cnt;
-    g->fills = cnt ? arena_alloc(&x->w->ar, cnt * sizeof(nfill *)) : NULL;
+    g->fills = arena_alloc(&w->ar, cnt * sizeof(nfill *));
     cnt = 0;
     for (nfill *f = g->fill_head; f; f = f->next)
         g->fills[cnt++] = f;
-    qsort(g->fills, g->n_fills, sizeof(nfill *), cmp_fill);
+    if (cnt <= 16) { /* fills of one gap are disjoint: starts are distinct */
+        for (int i = 1; i < cnt; ++i) {
+            nfill *v = g->fills[i];
+            int j = i - 1;
+            while (j >= 0 && g->fills[j]->start > v->start) {
+                g->fills[j + 1] = g->fills[j];
+                --j;
+            }
+            g->fills[j + 1] = v;
+        }
+    } else {
+        qsort(g->fills, g->n_fills, sizeof(nfill *), cmp_fill);
+    }
+}
+
+static void finish_gap(fin_ctx *x, ngap *g) {
+    sort_gap_fills(x->w, g);
     for (int i = 0; i < g->n_fills; ++i)
         finish_fill(x, g->fills[i]);
 }
@@ -775,30 +822,71 @@ void gac_net_free(gac_net *n) {
     free(n);
 }
 
+/* finishNet in three parallel phases: (A) per chromosome side, the root
+ * gap's fills sorted; (B) per run of consecutive top-level fills (their
+ * subtrees are independent), the subtrees sorted into the run's own
+ * pre-order list (the runs are concatenated in order afterwards); (C) the
+ * other-side ranges of every fill, in balanced chunks. */
+typedef struct fin_task {
+    int side;
+    int32_t chrom, f0, f1; /* top-level fills [f0, f1) of the chromosome's root gap */
+} fin_task;
+
 typedef struct fin_job {
     gac_net *n;
-    fin_ctx *x; /* [T chromosomes..., Q chromosomes...] */
-    int64_t nc;
+    int phase;
+    fin_task *task; /* phase B */
+    fin_ctx *x;     /* [ntask] */
+    int64_t ntask;
     _Atomic int64_t next;
     _Atomic int wid;
 } fin_job;
 
 static void *fin_thread(void *arg) {
     fin_job *F = arg;
-    nwork *w = &F->n->w[atomic_fetch_add(&F->wid, 1)];
+    gac_net *n = F->n;
+    nwork *w = &n->w[atomic_fetch_add(&F->wid, 1)];
+    if (F->phase == 2) {
+        const int64_t nt = n->n_order[GAC_T], tot = nt + n->n_order[GAC_Q], chunk = 4096;
+        for (;;) {
+            const int64_t a = atomic_fetch_add(&F->next, chunk);
+            if (a >= tot)
+                break;
+            const int64_t b = a + chunk < tot ? a + chunk : tot;
+            for (int64_t i = a; i < b; ++i) {
+                if (i < nt)
+                    fill_other_range(n, n->order[GAC_T][i], 0);
+                else
+                    fill_other_range(n, n->order[GAC_Q][i - nt], 1);
+            }
+        }
+        return NULL;
+    }
+    if (F->phase == 0) {
+        const int64_t nc = n->n_chroms[GAC_T] + (int64_t)n->n_chroms[GAC_Q];
+        for (;;) {
+            const int64_t k = atomic_fetch_add(&F->next, 1);
+            if (k >= nc)
+                break;
+            const int side = k < n->n_chroms[GAC_T] ? GAC_T : GAC_Q;
+            nchrom *c = &n->chroms[side][side == GAC_T ? k : k - n->n_chroms[GAC_T]];
+            if (c->root)
+                sort_gap_fills(w, c->root);
+        }
+        return NULL;
+    }
     for (;;) {
         const int64_t k = atomic_fetch_add(&F->next, 1);
-        if (k >= F->nc)
+        if (k >= F->ntask)
             break;
-        const int side = k < F->n->n_chroms[GAC_T] ? GAC_T : GAC_Q;
-        const int32_t ci = (int32_t)(side == GAC_T ? k : k - F->n->n_chroms[GAC_T]);
-        nchrom *c = &F->n->chroms[side][ci];
+        const fin_task *t = &F->task[k];
+        const ngap *root = n->chroms[t->side][t->chrom].root;
         fin_ctx *x = &F->x[k];
-        x->n = F->n;
+        x->n = n;
         x->w = w;
-        x->side = side;
-        if (c->root->fill_head)
-            finish_gap(x, c->root);
+        x->side = t->side;
+        for (int32_t i = t->f0; i < t->f1; ++i)
+            finish_fill(x, root->fills[i]);
     }
     return NULL;
 }
@@ -933,7 +1021,14 @@ int gac_net_build(const gac_net_input *in, const gac_net_opts *opt, gac_net **ou
     qsort(J.task, (size_t)J.ntask, sizeof(net_task), net_task_cmp);
     atomic_init(&J.next, 0);
     atomic_init(&J.wid, 0);
+    struct timespec t_add0, t_add1;
+    clock_gettime(CLOCK_MONOTONIC, &t_add0);
     gac_run_threads(n->n_w < J.ntask ? n->n_w : (J.ntask ? J.ntask : 1), net_thread, &J);
+    clock_gettime(CLOCK_MONOTONIC, &t_add1);
+    if (getenv("GAC_TIMING"))
+        fprintf(stderr, "[gac_net_build] addChainT/Q %.3f s (%d threads, largest task %lld chains)\n",
+                (t_add1.tv_sec - t_add0.tv_sec) + 1e-9 * (t_add1.tv_nsec - t_add0.tv_nsec),
+                n->n_w, J.ntask ? (long long)J.task[0].n : 0LL);
     free(J.task);
     free(toff);
     free(qoff);
@@ -950,28 +1045,65 @@ int gac_net_build(const gac_net_input *in, const gac_net_opts *opt, gac_net **ou
         fin_job F;
         memset(&F, 0, sizeof(F));
         F.n = n;
-        F.nc = n->n_chroms[0] + n->n_chroms[1];
-        F.x = calloc((size_t)(F.nc ? F.nc : 1), sizeof(fin_ctx));
+        const int64_t nc = n->n_chroms[GAC_T] + (int64_t)n->n_chroms[GAC_Q];
         atomic_init(&F.next, 0);
         atomic_init(&F.wid, 0);
-        gac_run_threads(n->n_w < F.nc ? n->n_w : (F.nc ? (int)F.nc : 1), fin_thread, &F);
-        for (int side = 0; side < 2; ++side) {
-            int64_t tot = 0;
-            const int64_t base = side == GAC_T ? 0 : n->n_chroms[GAC_T];
+        gac_run_threads(n->n_w < nc ? n->n_w : (nc ? (int)nc : 1), fin_thread, &F);
+        /* phase B tasks, in output order: side, chromosome, fill run */
+        int64_t ntop = 0;
+        for (int side = 0; side < 2; ++side)
             for (int32_t k = 0; k < n->n_chroms[side]; ++k)
-                tot += F.x[base + k].n_ord;
-            n->order[side] = malloc((size_t)(tot ? tot : 1) * sizeof(nfill *));
-            int64_t o = 0;
+                if (n->chroms[side][k].root)
+                    ntop += n->chroms[side][k].root->n_fills;
+        const int64_t per = ntop / (16 * (int64_t)n->n_w) + 1;
+        int64_t cap = ntop / per + n->n_chroms[GAC_T] + n->n_chroms[GAC_Q] + 1;
+        F.task = malloc((size_t)cap * sizeof(fin_task));
+        F.ntask = 0;
+        for (int side = 0; side < 2; ++side)
             for (int32_t k = 0; k < n->n_chroms[side]; ++k) {
-                fin_ctx *x = &F.x[base + k];
-                for (int64_t j = 0; j < x->n_ord; ++j) {
-                    x->ord[j]->ord = o;
-                    n->order[side][o++] = x->ord[j];
-                }
-                free(x->ord);
+                const ngap *root = n->chroms[side][k].root;
+                const int32_t nf = root ? root->n_fills : 0;
+                for (int32_t f0 = 0; f0 < nf; f0 += (int32_t)per)
+                    F.task[F.ntask++] = (fin_task){side, k, f0,
+                                                   (int32_t)(f0 + per < nf ? f0 + per : nf)};
             }
-            n->n_order[side] = o;
+        F.x = calloc((size_t)(F.ntask ? F.ntask : 1), sizeof(fin_ctx));
+        struct timespec t_a;
+        clock_gettime(CLOCK_MONOTONIC, &t_a);
+        F.phase = 1;
+        atomic_init(&F.next, 0);
+        atomic_init(&F.wid, 0);
+        gac_run_threads(n->n_w < F.ntask ? n->n_w : (F.ntask ? (int)F.ntask : 1), fin_thread, &F);
+        int64_t tot[2] = {0, 0};
+        for (int64_t k = 0; k < F.ntask; ++k)
+            tot[F.task[k].side] += F.x[k].n_ord;
+        for (int side = 0; side < 2; ++side) {
+            n->order[side] = malloc((size_t)(tot[side] ? tot[side] : 1) * sizeof(nfill *));
+            n->n_order[side] = 0;
         }
+        for (int64_t k = 0; k < F.ntask; ++k) {
+            const int side = F.task[k].side;
+            fin_ctx *x = &F.x[k];
+            for (int64_t j = 0; j < x->n_ord; ++j) {
+                x->ord[j]->ord = n->n_order[side];
+                n->order[side][n->n_order[side]++] = x->ord[j];
+            }
+            free(x->ord);
+        }
+        free(F.task);
+        /* phase C: rCalcOtherFill over the flat pre-order lists (the sorts
+         * above key on the fills' own-side bounds, which it recomputes
+         * unchanged, so it can run last) */
+        struct timespec t_b;
+        clock_gettime(CLOCK_MONOTONIC, &t_b);
+        if (getenv("GAC_TIMING"))
+            fprintf(stderr, "[gac_net_build] finishNet sort roots %.3f s, subtrees %.3f s (%lld runs)\n",
+                    (t_a.tv_sec - t_fin0.tv_sec) + 1e-9 * (t_a.tv_nsec - t_fin0.tv_nsec),
+                    (t_b.tv_sec - t_a.tv_sec) + 1e-9 * (t_b.tv_nsec - t_a.tv_nsec), (long long)F.ntask);
+        F.phase = 2;
+        atomic_init(&F.next, 0);
+        atomic_init(&F.wid, 0);
+        gac_run_threads(n->n_w, fin_thread, &F);
         free(F.x);
     }
     clock_gettime(CLOCK_MONOTONIC, &t_fin1);
