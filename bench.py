@@ -148,7 +148,7 @@ def main():
     e.synchronize()
     e.prof_enable(False)
     kern_ms = {name: e.prof_read(k)[0] / max(e.prof_read(k)[1], 1)
-               for name, k in (("plan+mark", GAC_K_PLAN), ("tile", GAC_K_TILE),
+               for name, k in (("plan+tilemap", GAC_K_PLAN), ("tile", GAC_K_TILE),
                                ("combine", GAC_K_COMBINE))}
     if args.prof == "none":  # roofline from the breakdown pass
         tile_ms, tile_n = kern_ms["tile"], 1

@@ -23,8 +23,7 @@ namespace gac {
 int plan_grid(int64_t n);
 int persistent_blocks_per_cu(int which);
 hipError_t launch_plan(const ScoreArgs &a, hipStream_t s);
-int mark_chunks_bound(int64_t flat, int64_t n);
-hipError_t launch_mark(const ScoreArgs &a, int grid, hipStream_t s);
+hipError_t launch_tilemap(const ScoreArgs &a, hipStream_t s);
 hipError_t launch_tile(const ScoreArgs &a, int grid, hipStream_t s);
 hipError_t launch_combine(const ScoreArgs &a, int grid, hipStream_t s);
 struct SeqDev {
@@ -121,13 +120,11 @@ struct gac_ctx {
     int32_t *nblk = nullptr, *goff = nullptr;
     int32_t *pb0 = nullptr;                  // [ws_n]
     int32_t *agg = nullptr;                  // [plan workgroups]
-    int32_t *plan_off = nullptr, *chunk_off = nullptr;  // [plan workgroups]
-    int32_t *chunk_wg = nullptr;             // [ws_chunks]
-    int64_t ws_chunks = 0;
+    int32_t *plan_off = nullptr;             // [plan workgroups]
+    int32_t *gflat = nullptr;                // [ws_n]
     int32_t *status = nullptr;               // [8]
     int64_t ws_tiles = 0;
-    int32_t *ridx = nullptr, *bidx = nullptr;
-    int64_t ws_flat = 0;
+    int32_t *tile_r0 = nullptr;              // [ws_tiles]
     SegSum *sum_head = nullptr, *sum_tail = nullptr;
     // staging for the host API
     int64_t io_n = 0;
@@ -137,7 +134,6 @@ struct gac_ctx {
     int32_t *h_stat = nullptr;   // pinned, coherent host words written by k_scan_agg [8]
     int32_t *d_h_stat = nullptr; // its device address
     int32_t call_seq = 0;
-    int tile_grid = 2048;       // k_mark grid (resident workgroups)
     int tile_grid_g = 2048;     // k_tile<false> grid (resident workgroups)
     int tile_grid_l = 2048;     // k_tile<true> grid
     int combine_grid = 512;
@@ -189,7 +185,6 @@ extern "C" int gac_open(int device, gac_ctx **out) {
         return gac_fail(GAC_E_HIP, "hipStreamCreate failed");
     }
     // persistent tile grid: 8 workgroups (32 waves) per CU
-    c->tile_grid = prop.multiProcessorCount * persistent_blocks_per_cu(2);  // k_mark
     c->combine_grid = prop.multiProcessorCount * 8;  // one 64-range group per wave
     c->tile_grid_g = prop.multiProcessorCount * persistent_blocks_per_cu(0);
     c->tile_grid_l = prop.multiProcessorCount * persistent_blocks_per_cu(1);
@@ -218,8 +213,8 @@ extern "C" void gac_close(gac_ctx *c) {
     hipStreamSynchronize(c->stream);
     free_genome(c->g[0]);
     free_genome(c->g[1]);
-    void *bufs[] = {c->d_small,  c->d_gap_tab, c->rdesc,    c->nblk,     c->goff, c->pb0, c->agg, c->plan_off, c->chunk_off, c->chunk_wg,
-                    c->status,   c->ridx,     c->bidx,     c->sum_head, c->sum_tail,
+    void *bufs[] = {c->d_small,  c->d_gap_tab, c->rdesc,    c->nblk,     c->goff, c->pb0, c->agg, c->plan_off, c->gflat,
+                    c->status,   c->tile_r0,  c->sum_head, c->sum_tail,
                     c->d_ranges, c->d_g,      c->d_l,      c->d_ali};
     for (void *p : bufs)
         if (p) hipFree(p);
@@ -920,56 +915,41 @@ extern "C" void gac_chains_free(gac_chainset *cs) {
 extern "C" int64_t gac_chains_block_count(const gac_chainset *cs) { return cs ? cs->n_blocks : -1; }
 
 // ----------------------------------------------------------------- launch
-static int ensure_ws(gac_ctx *c, int64_t n, int64_t max_tiles, int64_t flat, hipStream_t s) {
+static int ensure_ws(gac_ctx *c, int64_t n, int64_t max_tiles, hipStream_t s) {
     // buffers may still be in use by calls in flight on the stream
-    if (n > c->ws_n || flat > c->ws_flat || max_tiles > c->ws_tiles || !c->status)
-        HIPCHK(hipStreamSynchronize(s));
+    if (n > c->ws_n || max_tiles > c->ws_tiles || !c->status) HIPCHK(hipStreamSynchronize(s));
     if (n > c->ws_n) {
         int64_t cap = n + n / 2 + 1024;
-        void *bufs[] = {c->rdesc, c->nblk, c->goff, c->pb0, c->agg, c->plan_off, c->chunk_off};
+        void *bufs[] = {c->rdesc, c->nblk, c->goff, c->pb0, c->agg, c->plan_off, c->gflat};
         for (void *p : bufs)
             if (p) hipFree(p);
         c->rdesc = nullptr;
-        c->nblk = c->goff = c->pb0 = c->plan_off = c->chunk_off = nullptr;
+        c->nblk = c->goff = c->pb0 = c->plan_off = c->gflat = nullptr;
         c->agg = nullptr;
         const int64_t G = plan_grid(cap) + 2;
         HIPCHK(hipMalloc(&c->rdesc, cap * sizeof(RangeDesc)));
         HIPCHK(hipMalloc(&c->nblk, cap * 4));
         HIPCHK(hipMalloc(&c->goff, cap * 4));
         HIPCHK(hipMalloc(&c->pb0, cap * 4));
+        HIPCHK(hipMalloc(&c->gflat, cap * 4));
         HIPCHK(hipMalloc(&c->agg, G * 4));
         HIPCHK(hipMalloc(&c->plan_off, G * 4));
-        HIPCHK(hipMalloc(&c->chunk_off, G * 4));
         c->ws_n = cap;
     }
     if (!c->status) {
         HIPCHK(hipMalloc(&c->status, kStatusBytes));
         HIPCHK(hipMemsetAsync(c->status, 0, kStatusBytes, s));
     }
-    if (flat > c->ws_flat) {
-        int64_t cap = flat + flat / 4 + 4096;
-        if (cap > INT32_MAX) cap = INT32_MAX;
-        if (c->ridx) hipFree(c->ridx);
-        if (c->bidx) hipFree(c->bidx);
-        c->ridx = c->bidx = nullptr;
-        HIPCHK(hipMalloc(&c->ridx, cap * 4));
-        HIPCHK(hipMalloc(&c->bidx, cap * 4));
-        c->ws_flat = cap;
-    }
-    const int64_t nq = mark_chunks_bound(c->ws_flat, c->ws_n);
-    if (nq > c->ws_chunks) {
-        if (c->chunk_wg) hipFree(c->chunk_wg);
-        c->chunk_wg = nullptr;
-        HIPCHK(hipMalloc(&c->chunk_wg, nq * 4));
-        c->ws_chunks = nq;
-    }
     if (max_tiles > c->ws_tiles) {
         int64_t cap = max_tiles + max_tiles / 4 + 1024;
         if (c->sum_head) hipFree(c->sum_head);
         if (c->sum_tail) hipFree(c->sum_tail);
+        if (c->tile_r0) hipFree(c->tile_r0);
         c->sum_head = c->sum_tail = nullptr;
+        c->tile_r0 = nullptr;
         HIPCHK(hipMalloc(&c->sum_head, cap * sizeof(SegSum)));
         HIPCHK(hipMalloc(&c->sum_tail, cap * sizeof(SegSum)));
+        HIPCHK(hipMalloc(&c->tile_r0, cap * 4));
         c->ws_tiles = cap;
     }
     return GAC_OK;
@@ -1020,7 +1000,7 @@ static int wait_status(gac_ctx *c, hipStream_t s, int32_t tag, int32_t st[4]) {
     }
 }
 
-// One call = 5 launches (k_plan, k_scan_agg, k_mark, k_tile, k_combine); the
+// One call = 5 launches (k_plan, k_scan_agg, k_tilemap, k_tile, k_combine); the
 // host waits only for k_scan_agg's status words (pinned memory), not for the
 // scoring itself.  The flat block count W is only known on the
 // device (ranges may overlap), so the kernels check the workspace capacity
@@ -1041,8 +1021,8 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
         const_cast<gac_chainset *>(cs)->gap_version = c->gap_version;
     }
     // first guess for an empty workspace: 8 window blocks per range
-    const int64_t guess = c->ws_flat ? 0 : 8 * n;
-    int rc = ensure_ws(c, n, guess / kTileBlocks + 1, guess, s);
+    const int64_t guess = c->ws_tiles ? 0 : 8 * n;
+    int rc = ensure_ws(c, n, guess / kTileBlocks + 1, s);
     if (rc != GAC_OK) return rc;
     ScoreArgs a;
     memset(&a, 0, sizeof(a));
@@ -1077,23 +1057,19 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
         a.pb0 = c->pb0;
         a.agg = c->agg;
         a.plan_off = c->plan_off;
-        a.chunk_off = c->chunk_off;
-        a.chunk_wg = c->chunk_wg;
-        a.cap_chunks = (int32_t)(c->ws_chunks < INT32_MAX ? c->ws_chunks : INT32_MAX);
+        a.gflat = c->gflat;
         a.status = c->status;
-        a.ridx = c->ridx;
-        a.bidx = c->bidx;
+        a.tile_r0 = c->tile_r0;
         a.sum_head = c->sum_head;
         a.sum_tail = c->sum_tail;
         a.host_status = c->d_h_stat;
         a.call_tag = ++c->call_seq;
         if (a.call_tag <= 0) a.call_tag = c->call_seq = 1;
-        a.cap_flat = (int32_t)c->ws_flat;
         a.cap_tiles = (int32_t)(c->ws_tiles < INT32_MAX ? c->ws_tiles : INT32_MAX);
         {
             PROF_BEGIN(GAC_K_PLAN);
             HIPCHK(launch_plan(a, s));
-            HIPCHK(launch_mark(a, c->tile_grid, s));
+            HIPCHK(launch_tilemap(a, s));
             PROF_END(GAC_K_PLAN);
         }
         {
@@ -1115,7 +1091,7 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
             return gac_fail(GAC_E_ARG, "window block total overflows int32");
         }
         if (!st[2]) return GAC_OK;
-        rc = ensure_ws(c, n, st[1], st[0], s);  // (synchronises before growing)
+        rc = ensure_ws(c, n, st[1], s);  // (synchronises before growing)
         if (rc != GAC_OK) return rc;
     }
     return gac_fail(GAC_E_STATE, "scoring workspace still too small after growing it");

@@ -106,21 +106,17 @@ struct ScoreArgs {
     int32_t *nblk;       // [n]   window blocks per range
     int32_t *goff;       // [n]   exclusive scan of nblk inside the plan workgroup
     int32_t *pb0;        // [n]   first window block (compact copy of rdesc.b0)
-    int32_t *ridx;       // [W]   range owning each flat block
-    int32_t *bidx;       // [W]   global block index of each flat block
+    int32_t *gflat;      // [n]   flat offset of each range's first window block
+    int32_t *tile_r0;    // [T]   range owning each tile's first flat block
     SegSum *sum_head;    // [T]   partial segment containing the tile's first block
     SegSum *sum_tail;    // [T]   partial segment containing the tile's last block
     int32_t *agg;        // [G]   window blocks of each plan workgroup (k_plan; saturated)
     int32_t *plan_off;   // [G+1] flat offset of plan workgroup w
-    int32_t *chunk_off;  // [G+1] first mark chunk of plan workgroup w (large batches)
-    int32_t *chunk_wg;   // [cap_chunks] plan workgroup of each mark chunk (large batches)
     int32_t *status;     // [8]   W (flat blocks, saturated), T (tiles), 1 = workspace too
-                         //       small, mark chunks
+                         //       small
     int32_t *host_status;  // pinned host words: status[0..4) + call_tag (k_scan_agg)
     int32_t call_tag;
-    int32_t cap_chunks;
-    int32_t cap_flat;    // ridx/bidx capacity
-    int32_t cap_tiles;   // sum_head/sum_tail capacity
+    int32_t cap_tiles;   // tile_r0 / sum_head / sum_tail capacity
     // outputs
     long long *out_g;
     long long *out_l;

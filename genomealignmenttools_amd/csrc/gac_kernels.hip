@@ -10,8 +10,9 @@
 //   k_plan    one lane per range: binary-search the block window (replaces
 //             the O(blocks) list walks of chainSubsetOnT / chainBaseCountSubT),
 //             write a 32-byte range descriptor; workgroup scan of window
-//             blocks, the last workgroup scans the workgroup totals
-//   k_mark    flat block -> (range, block) map, in balanced chunks
+//             blocks
+//   k_scan_agg one workgroup: scan of the plan workgroup totals
+//   k_tilemap one lane per range: flat offset, first range of each tile
 //   k_tile    one wave per tile of 64 consecutive flat blocks (ranges packed
 //             densely, many ranges per tile): lanes score 32-base chunks of
 //             2-bit packed T and Q straight from HBM (bit-plane popcounts, the
@@ -401,7 +402,6 @@ __device__ __forceinline__ RangeDesc plan_range(const ScoreArgs &a, const Range 
 // a last-arriver scan -- cost more than the separate one-workgroup
 // k_scan_agg launch).
 constexpr int kPlanWG = 256;
-constexpr int kMarkChunk = 1024;  // flat blocks per k_mark work item
 
 __device__ __forceinline__ long long wg_exclusive_scan(long long v, long long *s_wsum,
                                                       long long &total) {
@@ -442,8 +442,8 @@ __global__ void __launch_bounds__(kPlanWG, 8) k_plan(ScoreArgs a) {
             if (a.want_local) a.out_l[i] = 0;
         }
     }
-    // 64-bit: 256 windows of a huge chain may exceed int32 (saturated in
-    // k_mark; the host reports it)
+    // 64-bit: 256 windows of a huge chain may exceed int32 (saturated; the
+    // host reports it)
     long long agg;
     const long long excl = wg_exclusive_scan(nb, s_wsum, agg);
     if (i < a.n) a.goff[i] = (int32_t)(excl < 0x7fffffffLL ? excl : 0x7fffffffLL);
@@ -451,18 +451,12 @@ __global__ void __launch_bounds__(kPlanWG, 8) k_plan(ScoreArgs a) {
 }
 
 // Scan of the plan workgroups' totals by one workgroup (k_scan_agg): flat
-// offsets (plan_off), mark-chunk offsets (chunk_off) and, when it fits, the
-// chunk table (chunk_wg).  Thread t owns workgroups [8t, 8t + 8) of each
-// batch of 2048, loaded all at once.  Returns {W, chunks} (W saturated at
-// INT32_MAX).
-struct AggScan {
-    long long W, NQ;
-};
-
-__device__ AggScan scan_totals(const ScoreArgs &a, int G, long long *s_wsum) {
+// offsets (plan_off).  Thread t owns workgroups [8t, 8t + 8) of each batch of
+// 2048, loaded all at once.  Returns W (saturated at INT32_MAX).
+__device__ long long scan_totals(const ScoreArgs &a, int G, long long *s_wsum) {
     constexpr int kPer = 8, kBatch = kPer * kPlanWG;
     const int tid = threadIdx.x;
-    AggScan t = {0, 0};
+    long long W = 0;
     for (int b0 = 0; b0 < G; b0 += kBatch) {
         int32_t v[kPer];
 #pragma unroll
@@ -470,46 +464,30 @@ __device__ AggScan scan_totals(const ScoreArgs &a, int G, long long *s_wsum) {
             const int w = b0 + tid * kPer + k;
             v[k] = w < G ? a.agg[w] : 0;
         }
-        long long mine = 0, mch = 0;
+        long long mine = 0;
 #pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            mine += v[k];
-            mch += ((long long)v[k] + kMarkChunk - 1) / kMarkChunk;
-        }
-        long long bw, bq;
-        long long run = t.W + wg_exclusive_scan(mine, s_wsum, bw);
-        long long crun = t.NQ + wg_exclusive_scan(mch, s_wsum, bq);
-        t.W += bw;
-        t.NQ += bq;
-        const bool fits = t.NQ <= a.cap_chunks;
+        for (int k = 0; k < kPer; ++k) mine += v[k];
+        long long bw;
+        long long run = W + wg_exclusive_scan(mine, s_wsum, bw);
+        W += bw;
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
             const int w = b0 + tid * kPer + k;
-            const long long ch = ((long long)v[k] + kMarkChunk - 1) / kMarkChunk;
-            if (w < G) {
-                a.plan_off[w] = (int32_t)(run < 0x7fffffffLL ? run : 0x7fffffffLL);
-                a.chunk_off[w] = (int32_t)(crun < 0x7fffffffLL ? crun : 0x7fffffffLL);
-                if (fits)
-                    for (long long c = 0; c < ch; ++c) a.chunk_wg[crun + c] = w;
-            }
+            if (w < G) a.plan_off[w] = (int32_t)(run < 0x7fffffffLL ? run : 0x7fffffffLL);
             run += v[k];
-            crun += ch;
         }
     }
-    if (t.W > 0x7fffffffLL) t.W = 0x7fffffffLL;
-    return t;
+    return W > 0x7fffffffLL ? 0x7fffffffLL : W;
 }
 
-// {W, T, overflow, chunks} for the later kernels, and the same, tagged with
-// the call's sequence number, straight into the host's pinned status words:
-// the host learns whether the workspace sufficed as soon as this kernel ends,
-// while k_mark / k_tile / k_combine still run.
-__device__ __forceinline__ void publish_status(const ScoreArgs &a, AggScan t) {
-    const long long T = (t.W + kTileBlocks - 1) / kTileBlocks;
-    const bool over = t.W >= 0x7fffffffLL || t.W > a.cap_flat || T > a.cap_tiles ||
-                      t.NQ > a.cap_chunks;
-    const int32_t st[4] = {(int32_t)t.W, (int32_t)T, over ? 1 : 0,
-                           (int32_t)(t.NQ < 0x7fffffffLL ? t.NQ : 0x7fffffffLL)};
+// {W, T, overflow} for the later kernels, and the same, tagged with the
+// call's sequence number, straight into the host's pinned status words: the
+// host learns whether the workspace sufficed as soon as this kernel ends,
+// while k_tilemap / k_tile / k_combine still run.
+__device__ __forceinline__ void publish_status(const ScoreArgs &a, long long W) {
+    const long long T = (W + kTileBlocks - 1) / kTileBlocks;
+    const bool over = W >= 0x7fffffffLL || T > a.cap_tiles;
+    const int32_t st[4] = {(int32_t)W, (int32_t)T, over ? 1 : 0, 0};
     for (int k = 0; k < 4; ++k) {
         a.status[k] = st[k];
         __hip_atomic_store(&a.host_status[k], st[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -521,42 +499,26 @@ __device__ __forceinline__ void publish_status(const ScoreArgs &a, AggScan t) {
 __global__ void __launch_bounds__(kPlanWG) k_scan_agg(ScoreArgs a) {
     __shared__ long long s_wsum[kPlanWG / kWave];
     const int G = (int)((a.n + kPlanWG - 1) / kPlanWG);
-    const AggScan t = scan_totals(a, G, s_wsum);
-    if (threadIdx.x == 0) publish_status(a, t);
+    const long long W = scan_totals(a, G, s_wsum);
+    if (threadIdx.x == 0) publish_status(a, W);
 }
 
-// ------------------------------------------------------------ k_mark -----
-// Flat block -> (range, block) map.  Work item = one chunk of <= 1024 flat
-// blocks of one plan workgroup (balanced however long the windows are; the
-// chunk table comes from k_scan_agg); persistent grid.  The plan workgroup's
-// 256 local offsets go to LDS; each flat block finds its owner by an 8-step
-// LDS search; the ridx/bidx stores are coalesced.
-__global__ void __launch_bounds__(kPlanWG, 8) k_mark(ScoreArgs a) {
-    __shared__ int s_excl[kPlanWG];
-    __shared__ int s_b0[kPlanWG];
+// ------------------------------------------------------------ k_tilemap --
+// One lane per range: its flat offset (gflat), and, for every tile whose
+// first flat block falls in its window, tile_r0[tile] = the range.  k_tile
+// finds the owner of each of a tile's blocks from there with an LDS search
+// over the next 64 ranges' offsets (no per-block map in HBM).
+__global__ void __launch_bounds__(kPlanWG) k_tilemap(ScoreArgs a) {
     if (a.status[2]) return;  // workspace overflow: the host grows it and reruns
-    const int NQ = a.status[3], W = a.status[0];
-    const int G = (int)((a.n + kPlanWG - 1) / kPlanWG);
-    const int tid = threadIdx.x;
-    for (int q = blockIdx.x; q < NQ; q += gridDim.x) {
-        const int w = a.chunk_wg[q];
-        const int c = q - a.chunk_off[w];
-        const int base = a.plan_off[w];
-        const int tot = (w + 1 < G ? a.plan_off[w + 1] : W) - base;
-        const int64_t i = (int64_t)w * kPlanWG + tid;
-        s_excl[tid] = i < a.n ? a.goff[i] : 0x7fffffff;
-        s_b0[tid] = i < a.n ? a.pb0[i] : 0;
-        __syncthreads();
-        const int f1 = min(tot, (c + 1) * kMarkChunk);
-        for (int f = c * kMarkChunk + tid; f < f1; f += kPlanWG) {
-            int r = 0;
-#pragma unroll
-            for (int step = kPlanWG / 2; step > 0; step >>= 1)
-                if (s_excl[r + step] <= f) r += step;
-            a.ridx[base + f] = w * kPlanWG + r;
-            a.bidx[base + f] = s_b0[r] + (f - s_excl[r]);
-        }
-        __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * kPlanWG + threadIdx.x;
+    if (i >= a.n) return;
+    const int nb = a.nblk[i];
+    const int g = a.plan_off[i / kPlanWG] + a.goff[i];
+    a.gflat[i] = g;
+    if (nb > 0) {
+        const int64_t end = (int64_t)g + nb;
+        for (int64_t t = ((int64_t)g + kTileBlocks - 1) / kTileBlocks; t * kTileBlocks < end; ++t)
+            a.tile_r0[t] = (int32_t)i;
     }
 }
 
@@ -567,6 +529,8 @@ __global__ void __launch_bounds__(kPlanWG, 8) k_mark(ScoreArgs a) {
 // tile), one for the 2-bit windows (16-byte loads; N masks only for blocks
 // flagged at upload), then segmented per-range scans.
 struct WaveLds {
+    int cg[kTileBlocks];          // flat offsets of the tile's candidate ranges r0 + k
+    int cb[kTileBlocks];          // their first window blocks
     int coff[kTileBlocks];        // exclusive chunk prefix per lane-block
     long long tpos[kTileBlocks];  // global base index of the clipped target start
     long long qpos[kTileBlocks];  // '+': global base index of the clipped query start
@@ -721,27 +685,56 @@ __global__ void __launch_bounds__(256, 6) k_tile(ScoreArgs a) {
     const int L8 = (G % 8 == 0) ? ((b % 8) * (G / 8) + b / 8) : b;
     const int stride = G * kWavesPerWG;
 
+    // The tile's blocks belong to the ranges r0, r0 + 1, ... (r0 = tile_r0):
+    // their flat offsets / first blocks are loaded one tile ahead (r0 itself
+    // two ahead), staged in LDS, and each lane finds its owner by a 6-step
+    // search.
     int tile = L8 * kWavesPerWG + wave;
-    int ri_next = 0, bi_next = 0;
-    {
-        const int j = tile * kTileBlocks + lane;
-        if (tile < T && j < W) {
-            ri_next = a.ridx[j];
-            bi_next = a.bidx[j];
-        }
+    const int n = (int)a.n;
+    int r0 = tile < T ? a.tile_r0[tile] : 0;
+    int r0_next = tile + stride < T ? a.tile_r0[tile + stride] : 0;
+    int gv = 0x7fffffff, bv = 0;
+    if (tile < T && r0 + lane < n) {
+        gv = a.gflat[r0 + lane];
+        bv = a.pb0[r0 + lane];
     }
     for (; tile < T; tile += stride) {
         const int j = tile * kTileBlocks + lane;
         const bool active = j < W;
-        const int ri = ri_next, bi = bi_next;
+        L.cg[lane] = gv;
+        L.cb[lane] = bv;
+        const int rc = r0;
         {
-            const int jn = j + stride * kTileBlocks;
-            ri_next = bi_next = 0;
-            if (jn < W) {
-                ri_next = a.ridx[jn];
-                bi_next = a.bidx[jn];
+            r0 = r0_next;
+            const int tn = tile + stride;
+            gv = 0x7fffffff;
+            bv = 0;
+            if (tn < T && r0 + lane < n) {
+                gv = a.gflat[r0 + lane];
+                bv = a.pb0[r0 + lane];
             }
+            r0_next = tn + stride < T ? a.tile_r0[tn + stride] : 0;
         }
+        wave_sync();
+        int k = 0;  // largest k with cg[k] <= j (cg[0] <= the tile's first block)
+#pragma unroll
+        for (int step = kTileBlocks / 2; step > 0; step >>= 1)
+            if (L.cg[k + step] <= j) k += step;
+        int ri = rc + k, gr = L.cg[k], b0r = L.cb[k];
+        if (k == kTileBlocks - 1 && active && ri + 1 < n) {
+            // more than 63 range starts in this tile (ranges of one block or
+            // empty ones): binary search the flat offsets beyond
+            int lo = ri, hi = n - 1;  // gflat[lo] <= j
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (a.gflat[mid] <= j) lo = mid;
+                else hi = mid - 1;
+            }
+            ri = lo;
+            gr = a.gflat[lo];
+            b0r = a.pb0[lo];
+        }
+        const int bi = b0r + (j - gr);
 
         // ---- per-lane block: clip to [s, e), gap to the next block
         int len = 0, g = 0, lenq = 0;
@@ -1003,25 +996,22 @@ hipError_t launch_plan(const ScoreArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
-int mark_chunks_bound(int64_t flat, int64_t n) { return (int)(flat / kMarkChunk + plan_grid(n) + 2); }
-
-hipError_t launch_mark(const ScoreArgs &a, int grid, hipStream_t s) {
+hipError_t launch_tilemap(const ScoreArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(k_scan_agg, dim3(1), dim3(kPlanWG), 0, s, a);
-    hipLaunchKernelGGL(k_mark, dim3(grid), dim3(kPlanWG), 0, s, a);
+    hipLaunchKernelGGL(k_tilemap, dim3((unsigned)plan_grid(a.n)), dim3(kPlanWG), 0, s, a);
     return hipGetLastError();
 }
 
 // Resident workgroups per CU of the persistent kernels (a grid must not
 // exceed what fits at once, or the last workgroups run as a second wave):
-// 0 = k_tile<false>, 1 = k_tile<true>, 2 = k_mark.
+// 0 = k_tile<false>, 1 = k_tile<true>.
 int persistent_blocks_per_cu(int which) {
     int nb = 0;
     // (the symmetric and general variants differ by a few registers; size
     // for the general one)
     hipError_t e =
         which == 0   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<false, false>, 256, 0)
-        : which == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<true, false>, 256, 0)
-                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_mark, 256, 0);
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<true, false>, 256, 0);
     return (e == hipSuccess && nb > 0) ? nb : 4;
 }
 
