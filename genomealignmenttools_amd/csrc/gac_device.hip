@@ -3,6 +3,7 @@
 // There is deliberately no host fallback: every scoring entry point runs the
 // HIP kernels of gac_kernels.hip on a gfx950 device or returns an error.
 #include <hip/hip_runtime.h>
+#include <time.h>
 
 #include <stdint.h>
 #include <stdio.h>
@@ -164,8 +165,22 @@ extern "C" int gac_open(int device, gac_ctx **out) {
     gac_clear_error();
     if (!out) return gac_fail(GAC_E_ARG, "gac_open: NULL out");
     *out = nullptr;
+    const bool timing = getenv("GAC_TIMING") != nullptr;
+    auto t_now = [] {
+        struct timespec ts;
+        clock_gettime(CLOCK_MONOTONIC, &ts);
+        return ts.tv_sec + 1e-9 * ts.tv_nsec;
+    };
+    double t_mark = t_now();
+    auto lap = [&](const char *what) {
+        if (!timing) return;
+        const double t = t_now();
+        fprintf(stderr, "[gac_open] %-28s %.3f s\n", what, t - t_mark);
+        t_mark = t;
+    };
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
+    lap("hipGetDeviceCount (HIP init)");
     if (e != hipSuccess || n == 0)
         return gac_fail(GAC_E_HIP, "no HIP device available (%s); libgachain has no CPU fallback",
                         hipGetErrorString(e));
@@ -173,10 +188,12 @@ extern "C" int gac_open(int device, gac_ctx **out) {
         return gac_fail(GAC_E_ARG, "device %d out of range (%d devices)", device, n);
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
+    lap("hipGetDeviceProperties");
     if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         return gac_fail(GAC_E_HIP, "device %d is %s; libgachain is built for gfx950 only", device,
                         prop.gcnArchName);
     HIPCHK(hipSetDevice(device));
+    lap("hipSetDevice");
     gac_ctx *c = new gac_ctx();
     c->device = device;
     snprintf(c->arch, sizeof(c->arch), "%s", prop.gcnArchName);
@@ -184,10 +201,11 @@ extern "C" int gac_open(int device, gac_ctx **out) {
         delete c;
         return gac_fail(GAC_E_HIP, "hipStreamCreate failed");
     }
-    // persistent tile grid: 8 workgroups (32 waves) per CU
+    lap("hipStreamCreate");
     c->combine_grid = prop.multiProcessorCount * 8;  // one 64-range group per wave
     c->tile_grid_g = prop.multiProcessorCount * persistent_blocks_per_cu(0);
     c->tile_grid_l = prop.multiProcessorCount * persistent_blocks_per_cu(1);
+    lap("occupancy (code object)");
     if (hipHostMalloc((void **)&c->h_stat, 64, hipHostMallocMapped | hipHostMallocCoherent) !=
             hipSuccess ||
         hipHostGetDevicePointer((void **)&c->d_h_stat, c->h_stat, 0) != hipSuccess) {
@@ -195,6 +213,7 @@ extern "C" int gac_open(int device, gac_ctx **out) {
         delete c;
         return gac_fail(GAC_E_HIP, "hipHostMalloc failed");
     }
+    lap("hipHostMalloc");
     *out = c;
     return GAC_OK;
 }

@@ -638,6 +638,40 @@ typedef struct chunk {
     double stop_below;
 } chunk;
 
+/* Fast path for the common block line "size[\tdt\tdq]\n" (decimal fields of
+ * at most 9 digits, one tab apart): 1 = parsed into v[0..*bw), 0 = anything
+ * else (blank or '#' lines, spaces, CR, long numbers, a missing newline,
+ * errors), which the general lineFileChopNext + lineFileNeedNum path then
+ * reads from the same position. */
+static int fast_block_line(lf *f, int *v, int *bw) {
+    const char *p = f->cur, *end = f->end;
+    int k = 0;
+    for (;;) {
+        const int neg = p < end && *p == '-';
+        p += neg;
+        const char *d0 = p;
+        int x = 0;
+        while (p < end && (unsigned)(*p - '0') < 10u && p - d0 < 9) {
+            x = x * 10 + (*p - '0');
+            ++p;
+        }
+        if (p == d0 || p >= end || (unsigned)(*p - '0') < 10u)
+            return 0;
+        v[k++] = neg ? -x : x;
+        if (*p == '\n')
+            break;
+        if (*p != '\t' || k == 3)
+            return 0;
+        ++p;
+    }
+    if (k == 2)
+        return 0;
+    f->cur = (char *)p + 1;
+    ++f->line;
+    *bw = k;
+    return 1;
+}
+
 /* parse one record; 0 = ok, 1 = end of chunk, -1 = error (f->msg) */
 static int parse_chain(chunk *k) {
     lf *f = &k->f;
@@ -682,13 +716,18 @@ static int parse_chain(chunk *k) {
     /* chainReadBlocks (chain.c:301-335) */
     int q = c->qstart[i], t = c->tstart[i];
     for (;;) {
-        char *brow[3];
-        int bw = lf_chop(f, brow, 3);
-        if (bw == 0)
-            LF_FAIL(f, "Unexpected end of file in \002");
-        int size;
-        if (need_num(f, brow, 0, &size))
-            return -1;
+        int v[3], bw;
+        if (!fast_block_line(f, v, &bw)) {
+            char *brow[3];
+            bw = lf_chop(f, brow, 3);
+            if (bw == 0)
+                LF_FAIL(f, "Unexpected end of file in \002");
+            if (need_num(f, brow, 0, &v[0]))
+                return -1;
+            if (bw >= 3 && (need_num(f, brow, 1, &v[1]) || need_num(f, brow, 2, &v[2])))
+                return -1;
+        }
+        const int size = v[0];
         if (c->nb + 1 >= c->bcap) {
             c->bcap = c->bcap ? c->bcap * 2 : 1 << 16;
             c->bt = realloc(c->bt, c->bcap * 4);
@@ -705,11 +744,8 @@ static int parse_chain(chunk *k) {
             break;
         if (bw < 3)
             LF_FAIL(f, "Expecting 1 or 3 words line \001 of \002\n");
-        int dt, dq;
-        if (need_num(f, brow, 1, &dt) || need_num(f, brow, 2, &dq))
-            return -1;
-        t += dt;
-        q += dq;
+        t += v[1];
+        q += v[2];
     }
     if (q != c->qend[i])
         LF_FAIL(f, "q end mismatch %d vs %d line \001 of \002\n", q, c->qend[i]);
@@ -781,8 +817,19 @@ void gt_parallel(int n, void *(*fn)(void *), void *args, size_t stride) {
 
 void gt_read_chains(const char *path, gt_chains *c, double stop_below, int keep_meta) {
     memset(c, 0, sizeof(*c));
+    const int timing = getenv("GAC_TIMING") != NULL;
+    double t_mark = now_s();
+#define RC_LAP(what)                                                               \
+    do {                                                                           \
+        if (timing) {                                                              \
+            const double t_ = now_s();                                             \
+            fprintf(stderr, "[gt_read_chains] %-16s %.3f s\n", what, t_ - t_mark); \
+            t_mark = t_;                                                           \
+        }                                                                          \
+    } while (0)
     size_t len;
     char *buf = gt_slurp(path, &len);
+    RC_LAP("read file");
     /* chunk boundaries at "\nchain" */
     int nt = len < (8u << 20) ? 1 : gt_threads();
     char **cut = malloc((size_t)(nt + 1) * sizeof(char *));
@@ -815,8 +862,11 @@ void gt_read_chains(const char *path, gt_chains *c, double stop_below, int keep_
         K[k].stop_below = stop_below;
         NL[k] = (nl_job){cut[k], cut[k + 1], 0};
     }
+    RC_LAP("cut");
     gt_parallel(nk, count_newlines, NL, sizeof(nl_job)); /* before parsing cuts lines */
+    RC_LAP("count lines");
     gt_parallel(nk, parse_chunk, K, sizeof(chunk));
+    RC_LAP("parse");
     /* stitch in file order up to the first error or stop */
     c->blk_off = malloc(8);
     c->blk_off[0] = 0;
@@ -894,12 +944,15 @@ void gt_read_chains(const char *path, gt_chains *c, double stop_below, int keep_
         if (ch->stop >= 0)
             break;
     }
+    RC_LAP("stitch");
     for (int k = 0; k < nk; ++k)
         gt_chains_free(&K[k].c);
     free(K);
     free(NL);
     free(cut);
     free(buf);
+    RC_LAP("free");
+#undef RC_LAP
 }
 
 void gt_chains_free(gt_chains *c) {
