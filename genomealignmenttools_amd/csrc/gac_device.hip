@@ -1026,24 +1026,20 @@ static int wait_status(gac_ctx *c, hipStream_t s, int32_t tag, int32_t st[4]) {
 // themselves; on overflow k_tile / k_combine do nothing and the call grows the
 // workspace to the reported {W, T} and runs once more (first call or a larger
 // batch only).
-static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_ranges, int64_t n,
-                        uint32_t flags, long long *d_g, long long *d_l, int32_t *d_ali,
-                        hipStream_t s) {
+// Checks shared by both scoring paths, the per-setup block gaps, and the
+// kernel arguments that do not depend on the workspace.
+static int prepare_args(gac_ctx *c, const gac_chainset *cs, int64_t n, uint32_t flags,
+                        const void *d_l, hipStream_t s, ScoreArgs &a) {
     if (!c->scoring) return gac_fail(GAC_E_STATE, "gac_set_scoring() not called");
     if (!cs || cs->ctx != c) return gac_fail(GAC_E_ARG, "chainset does not belong to this context");
     if (n < 0 || n > INT32_MAX / 2) return gac_fail(GAC_E_ARG, "bad range count %lld", (long long)n);
-    if (n == 0) return GAC_OK;
     if ((flags & GAC_WANT_LOCAL) && !d_l) return gac_fail(GAC_E_ARG, "GAC_WANT_LOCAL needs local output");
+    if (n == 0) return GAC_OK;
     if (cs->gap_version != c->gap_version) {  // blk[].w for this scoring setup
         HIPCHK(launch_block_gaps(cs->chains, cs->n_chains, cs->blk, c->gap, c->d_small,
                                  c->d_gap_tab, c->gap_len, s));
         const_cast<gac_chainset *>(cs)->gap_version = c->gap_version;
     }
-    // first guess for an empty workspace: 8 window blocks per range
-    const int64_t guess = c->ws_tiles ? 0 : 8 * n;
-    int rc = ensure_ws(c, n, guess / kTileBlocks + 1, s);
-    if (rc != GAC_OK) return rc;
-    ScoreArgs a;
     memset(&a, 0, sizeof(a));
     const Genome &T = c->g[0], &Q = c->g[1];
     a.t_planes = T.planes;
@@ -1057,11 +1053,7 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
     a.blk = cs->blk;
     a.tspan = cs->tspan;
     a.bucket = cs->bucket;
-    a.ranges = d_ranges;
     a.n = n;
-    a.out_g = d_g;
-    a.out_l = d_l;
-    a.out_ali = d_ali;
     a.want_local = (flags & GAC_WANT_LOCAL) ? 1 : 0;
     a.gap_len = c->gap_len;
     a.gap_tab = c->d_gap_tab;
@@ -1069,6 +1061,24 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
     memcpy(a.coef, c->coef, sizeof(a.coef));
     a.sym = c->sym;
     a.gap = c->gap;
+    return GAC_OK;
+}
+
+static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_ranges, int64_t n,
+                        uint32_t flags, long long *d_g, long long *d_l, int32_t *d_ali,
+                        hipStream_t s) {
+    ScoreArgs a_base;
+    int rc = prepare_args(c, cs, n, flags, d_l, s, a_base);
+    if (rc != GAC_OK || n == 0) return rc;
+    // first guess for an empty workspace: 8 window blocks per range
+    const int64_t guess = c->ws_tiles ? 0 : 8 * n;
+    rc = ensure_ws(c, n, guess / kTileBlocks + 1, s);
+    if (rc != GAC_OK) return rc;
+    ScoreArgs a = a_base;
+    a.ranges = d_ranges;
+    a.out_g = d_g;
+    a.out_l = d_l;
+    a.out_ali = d_ali;
     for (int pass = 0; pass < 2; ++pass) {
         a.rdesc = c->rdesc;
         a.nblk = c->nblk;

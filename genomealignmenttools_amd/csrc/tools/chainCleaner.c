@@ -28,6 +28,7 @@
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <time.h>
 #include <string.h>
 #include <unistd.h>
 
@@ -564,6 +565,13 @@ static sres *g_cv = NULL;
 static uint8_t *g_cused = NULL;
 static int64_t g_cslots = 0, g_cn = 0;
 static int64_t g_gpu_calls = 0, g_gpu_ranges = 0, g_uploads = 0;
+static double g_gpu_s = 0; /* wall time inside the scoring calls */
+
+static double wall_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
 
 static uint64_t key_hash(qkey k) {
     uint64_t h = (uint64_t)(uint32_t)k.ich * 0x9E3779B97F4A7C15ull;
@@ -675,6 +683,7 @@ static void score_keys(state *S, const qkey *in, int64_t n) {
         rb[n0] = (gac_range){q[n0].ich, q[n0].s, q[n0].e};
         ++n0;
     }
+    const double t0 = wall_s();
     if (n0) {
         gt_check(gac_score_ranges(S->ctx, S->cs_base, rb, n0, GAC_WANT_LOCAL, g, l, a));
         ++g_gpu_calls;
@@ -727,6 +736,7 @@ static void score_keys(state *S, const qkey *in, int64_t n) {
         free(bq);
         free(bs);
     }
+    g_gpu_s += wall_s() - t0;
     for (int64_t i = 0; i < m; ++i)
         cache_put(q[i], (sres){g[i], l[i], a[i]});
     free(rb);
@@ -1530,8 +1540,8 @@ int main(int argc, char *argv[]) {
         free(k);
     }
     gt_verbose(1, "DONE\n\n");
-    gt_verbose(1, "GPU: %lld scoring calls, %lld sub-chains, %lld re-uploads\n",
-               (long long)g_gpu_calls, (long long)g_gpu_ranges, (long long)g_uploads);
+    gt_verbose(1, "GPU: %lld scoring calls, %lld sub-chains, %lld re-uploads, %.3f s in scoring calls\n",
+               (long long)g_gpu_calls, (long long)g_gpu_ranges, (long long)g_uploads, g_gpu_s);
     gt_verbose(1, "\nALL DONE. New chains are in %s. Deleted suspects in %s\n", out_chain, out_bed);
     gac_chains_free(S.cs_base);
     gac_close(S.ctx);

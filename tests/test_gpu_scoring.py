@@ -204,6 +204,8 @@ def test_edge_ranges():
     g, l, a = e.score_ranges(cs, R, want_local=True)
     og, ol, oa = _oracle(tg, qg).score_ranges(ca, R)
     assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
+    g, l, a = _score_chunked(e, cs, R, True)  # small batches
+    assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
 
 
 @pytest.mark.parametrize("gap,table_max", [("loose", None), ("medium", None),
@@ -256,3 +258,47 @@ def test_genome_roundtrip():
     e.add_sequences(GAC_T, tg.seq_records())
     for i, n in enumerate(tg.names):
         assert e.decode(GAC_T, e.seq_index(GAC_T, n), 0, len(tg.codes[i])) == tg.text(i)
+
+
+def _score_chunked(e, cs, R, want_local):
+    """Score R in batches of at most 256 ranges (chainCleaner's on-demand
+    calls), batch sizes cycling through edge values."""
+    sizes, out, i, k = (1, 7, 64, 255, 256, 100), [], 0, 0
+    while i < len(R):
+        m = sizes[k % len(sizes)]
+        out.append(e.score_ranges(cs, R[i:i + m], want_local=want_local))
+        i += m
+        k += 1
+    cat = lambda j: np.concatenate([o[j] for o in out])
+    return cat(0), (cat(1) if want_local else None), cat(2)
+
+
+@pytest.mark.parametrize("case", ["sym", "asym", "long"])
+def test_small_batches_vs_oracle(case):
+    """Small batches (<= 256 ranges: chainCleaner's on-demand sub-chains, a
+    first call's workspace guess) are bit-exact vs the oracle with and
+    without the local score, symmetric and asymmetric matrices, windows of
+    thousands of blocks."""
+    from genomealignmenttools_amd import synth
+    rng = np.random.default_rng(17)
+    mat = BLASTZ
+    if case == "long":
+        tg = synth.random_genome({"chrT1": 3_000_000}, 11, n_frac=0.01, n_mean=300)
+        qg = synth.random_genome({"q1": 2_000_000, "q2": 1_500_000}, 12, n_frac=0.01, n_mean=300)
+        cfg = synth.SynthConfig(n_chains=40, alpha=1.1, max_blocks=20_000, seed=5,
+                                gap_p_small=0.97, gap_p_med=0.03)
+        ca = synth.make_chains(tg, "chrT1", qg, cfg)
+    else:
+        tg, qg, ca = synth.small_case(seed=21, n_chains=150, max_blocks=500)
+        if case == "asym":
+            mat = rng.integers(-300, 301, 16).astype(np.int32)
+    e, cs = _setup(None, tg, qg, ca, mat=mat)
+    R = _ranges(ca, rng, per_chain=4)
+    og, ol, oa = _oracle(tg, qg, mat=mat).score_ranges(ca, R)
+    g, l, a = _score_chunked(e, cs, R, True)
+    assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
+    g2, _, a2 = _score_chunked(e, cs, R, False)
+    assert np.array_equal(g2, og) and np.array_equal(a2, oa)
+    # the same ranges in one large batch (tile pipeline) agree too
+    g3, l3, a3 = e.score_ranges(cs, R, want_local=True)
+    assert np.array_equal(g3, og) and np.array_equal(l3, ol) and np.array_equal(a3, oa)
