@@ -1303,18 +1303,28 @@ typedef struct wctx {
 /* line formatting without stdio's format parsing (the .net files hold
  * millions of lines) */
 static char *put_int(char *p, int64_t v) {
-    char tmp[24];
-    int k = 0;
+    static const char dig2[201] = "00010203040506070809101112131415161718192021222324"
+                                  "25262728293031323334353637383940414243444546474849"
+                                  "50515253545556575859606162636465666768697071727374"
+                                  "75767778798081828384858687888990919293949596979899";
+    char tmp[24], *e = tmp + sizeof(tmp), *q = e;
     uint64_t u = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
-    do {
-        tmp[k++] = (char)('0' + u % 10);
-        u /= 10;
-    } while (u);
+    while (u >= 100) { /* two digits per step */
+        const unsigned r = (unsigned)(u % 100);
+        u /= 100;
+        q -= 2;
+        memcpy(q, dig2 + 2 * r, 2);
+    }
+    if (u >= 10) {
+        q -= 2;
+        memcpy(q, dig2 + 2 * u, 2);
+    } else {
+        *--q = (char)('0' + u);
+    }
     if (v < 0)
         *p++ = '-';
-    while (k)
-        *p++ = tmp[--k];
-    return p;
+    memcpy(p, q, (size_t)(e - q));
+    return p + (e - q);
 }
 
 static char *put_str(char *p, const char *s) {

@@ -13,6 +13,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 #include <pthread.h>
+#include <stdatomic.h>
 #include <time.h>
 #include <zlib.h>
 
@@ -468,7 +469,36 @@ int gt_file_exists(const char *path) {
     return strcmp(path, "stdin") == 0 || stat(path, &st) == 0;
 }
 
-/* whole file into a NUL-terminated heap buffer (.gz decompressed) */
+/* parallel pread of [a, b) of a regular file */
+typedef struct pr_job {
+    int fd;
+    char *buf;
+    size_t size, per;
+    _Atomic size_t next;
+    _Atomic int bad;
+} pr_job;
+
+static void *pr_thread(void *p) {
+    pr_job *J = p;
+    for (;;) {
+        const size_t a = atomic_fetch_add(&J->next, J->per);
+        if (a >= J->size)
+            break;
+        const size_t b = a + J->per < J->size ? a + J->per : J->size;
+        for (size_t o = a; o < b;) {
+            const ssize_t r = pread(J->fd, J->buf + o, b - o, (off_t)o);
+            if (r <= 0) {
+                atomic_store(&J->bad, 1);
+                break;
+            }
+            o += (size_t)r;
+        }
+    }
+    return NULL;
+}
+
+/* whole file into a NUL-terminated heap buffer (.gz decompressed); regular
+ * files of more than 32 MB are read by several threads at once */
 char *gt_slurp(const char *path, size_t *len) {
     size_t n = strlen(path);
     int gz = n > 3 && strcmp(path + n - 3, ".gz") == 0;
@@ -498,8 +528,26 @@ char *gt_slurp(const char *path, size_t *len) {
         if (fd < 0)
             gt_abort("Couldn't open %s , %s", path, strerror(errno));
         struct stat st;
-        if (fd != 0 && fstat(fd, &st) == 0 && S_ISREG(st.st_mode))
+        if (fd != 0 && fstat(fd, &st) == 0 && S_ISREG(st.st_mode)) {
             cap = (size_t)st.st_size + 1;
+            if (st.st_size > (32 << 20)) {
+                const size_t size = (size_t)st.st_size;
+                buf = malloc(size + 1);
+                pr_job J = {fd, buf, size, 8u << 20, 0, 0};
+                atomic_init(&J.next, 0);
+                atomic_init(&J.bad, 0);
+                int nt = gt_threads();
+                if ((size_t)nt > size / J.per + 1)
+                    nt = (int)(size / J.per + 1);
+                gac_run_threads(nt, pr_thread, &J);
+                if (atomic_load(&J.bad))
+                    gt_abort("read error on %s", path);
+                close(fd);
+                buf[size] = 0;
+                *len = size;
+                return buf;
+            }
+        }
         buf = malloc(cap + 1);
         for (;;) {
             if (l == cap) {
@@ -983,18 +1031,28 @@ int gt_next_chain_id(void) { return g_next_id++; }
 
 /* decimal text of v at p, returns the end */
 static char *put_int(char *p, int64_t v) {
-    char tmp[24];
-    int k = 0;
+    static const char dig2[201] = "00010203040506070809101112131415161718192021222324"
+                                  "25262728293031323334353637383940414243444546474849"
+                                  "50515253545556575859606162636465666768697071727374"
+                                  "75767778798081828384858687888990919293949596979899";
+    char tmp[24], *e = tmp + sizeof(tmp), *q = e;
     uint64_t u = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
-    do {
-        tmp[k++] = (char)('0' + u % 10);
-        u /= 10;
-    } while (u);
+    while (u >= 100) { /* two digits per step */
+        const unsigned r = (unsigned)(u % 100);
+        u /= 100;
+        q -= 2;
+        memcpy(q, dig2 + 2 * r, 2);
+    }
+    if (u >= 10) {
+        q -= 2;
+        memcpy(q, dig2 + 2 * u, 2);
+    } else {
+        *--q = (char)('0' + u);
+    }
     if (v < 0)
         *p++ = '-';
-    while (k)
-        *p++ = tmp[--k];
-    return p;
+    memcpy(p, q, (size_t)(e - q));
+    return p + (e - q);
 }
 
 /* block lines "size\tdt\tdq" and the last "size", then the blank line
