@@ -735,93 +735,9 @@ static void *po_thread(void *p) {
     return NULL;
 }
 
-/* parallel pwrite of the formatted runs at their offsets */
-typedef struct pw_job {
-    int fd;
-    int64_t nr;
-    char **buf;
-    size_t *len;
-    off_t *off;
-    _Atomic int64_t next;
-    _Atomic int bad;
-} pw_job;
-
-static void *pw_thread(void *p) {
-    pw_job *J = p;
-    for (;;) {
-        const int64_t r = atomic_fetch_add(&J->next, 1);
-        if (r >= J->nr)
-            break;
-        for (size_t o = 0; o < J->len[r];) {
-            const ssize_t w = pwrite(J->fd, J->buf[r] + o, J->len[r] - o, J->off[r] + (off_t)o);
-            if (w <= 0) {
-                atomic_store(&J->bad, 1);
-                break;
-            }
-            o += (size_t)w;
-        }
-        free(J->buf[r]);
-        J->buf[r] = NULL;
-    }
-    return NULL;
-}
-
-/* Regular files: every run formatted in parallel, then written in parallel
- * at its offset (the runs' sizes are only known once they are formatted). */
-static int par_output_file(FILE *out, int fd, int64_t nr,
-                           void (*fn)(FILE *f, int64_t r, void *arg), void *arg) {
-    const off_t base = ftello(out);
-    if (base < 0)
-        return -1;
-    po_job J;
-    J.nr = nr;
-    J.fn = fn;
-    J.arg = arg;
-    J.buf = calloc((size_t)nr, sizeof(char *));
-    J.len = calloc((size_t)nr, sizeof(size_t));
-    J.ready = calloc((size_t)nr, sizeof(_Atomic int));
-    atomic_init(&J.next, 0);
-    atomic_init(&J.oom, 0);
-    int nt = gac_host_threads();
-    if (nt > nr)
-        nt = (int)nr;
-    gac_run_threads(nt, po_thread, &J);
-    off_t *off = malloc((size_t)(nr + 1) * sizeof(off_t));
-    off[0] = base;
-    for (int64_t r = 0; r < nr; ++r)
-        off[r + 1] = off[r] + (off_t)J.len[r];
-    pw_job W;
-    W.fd = fd;
-    W.nr = nr;
-    W.buf = J.buf;
-    W.len = J.len;
-    W.off = off;
-    atomic_init(&W.next, 0);
-    atomic_init(&W.bad, 0);
-    gac_run_threads(nt, pw_thread, &W);
-    const int bad = atomic_load(&W.bad) || atomic_load(&J.oom);
-    const off_t end = off[nr];
-    for (int64_t r = 0; r < nr; ++r)
-        free(J.buf[r]);
-    free(J.buf);
-    free(J.len);
-    free((void *)J.ready);
-    free(off);
-    if (fseeko(out, end, SEEK_SET) != 0)
-        return -1;
-    return bad ? -1 : 0;
-}
-
 int gac_par_output(FILE *out, int64_t nr, void (*fn)(FILE *f, int64_t r, void *arg), void *arg) {
     if (nr <= 0)
         return 0;
-    {
-        struct stat st;
-        const int fd = fileno(out);
-        if (fd >= 0 && fflush(out) == 0 && fstat(fd, &st) == 0 && S_ISREG(st.st_mode) &&
-            !(fcntl(fd, F_GETFL) & O_APPEND))
-            return par_output_file(out, fd, nr, fn, arg);
-    }
     po_job J;
     J.nr = nr;
     J.fn = fn;
