@@ -9,6 +9,7 @@
  * (:795-843). */
 #include <math.h>
 #include <pthread.h>
+#include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -67,6 +68,32 @@ static void *write_net(void *arg) {
                           w->c->n_meta);
     if (w->rc != GAC_OK) /* thread-local error text */
         snprintf(w->err, sizeof(w->err), "%s", gac_last_error());
+    return NULL;
+}
+
+/* block lists of the chains owning a rescored fill, copied in parallel */
+typedef struct subset_copy {
+    const gt_chains *c;
+    const int64_t *src, *goff;
+    int32_t *bt, *bq, *bs;
+    int64_t n;
+    _Atomic int64_t next;
+} subset_copy;
+
+static void *subset_copy_thread(void *arg) {
+    subset_copy *J = arg;
+    for (;;) {
+        const int64_t a = atomic_fetch_add(&J->next, 4096);
+        if (a >= J->n)
+            break;
+        const int64_t b = a + 4096 < J->n ? a + 4096 : J->n;
+        for (int64_t j = a; j < b; ++j) {
+            const int64_t i = J->src[j], b0 = J->c->blk_off[i], nb = J->c->blk_off[i + 1] - b0;
+            memcpy(J->bt + J->goff[j], J->c->bt + b0, nb * 4);
+            memcpy(J->bq + J->goff[j], J->c->bq + b0, nb * 4);
+            memcpy(J->bs + J->goff[j], J->c->bs + b0, nb * 4);
+        }
+    }
     return NULL;
 }
 
@@ -236,14 +263,13 @@ int main(int argc, char *argv[]) {
                 if (gqs[j] < 0)
                     gt_abort("%s is not in %s", qn, qnib);
                 gst[j] = c.qstrand[i];
-                const int64_t b0 = c.blk_off[i], nb = c.blk_off[i + 1] - b0;
-                memcpy(gbt + goff[j], c.bt + b0, nb * 4);
-                memcpy(gbq + goff[j], c.bq + b0, nb * 4);
-                memcpy(gbs + goff[j], c.bs + b0, nb * 4);
-                goff[j + 1] = goff[j] + nb;
+                goff[j + 1] = goff[j] + (c.blk_off[i + 1] - c.blk_off[i]);
             }
             free(tmap);
             free(qmap);
+            subset_copy sj = {&c, src, goff, gbt, gbq, gbs, nsub, 0};
+            atomic_init(&sj.next, 0);
+            gac_run_threads(gt_threads(), subset_copy_thread, &sj);
             for (int64_t k = 0; k < nr; ++k)
                 r[k].chain = remap[r[k].chain];
             gac_chainset_desc d = {nsub, gts, gqs, gst, goff, nbsub, gbt, gbq, gbs};
@@ -267,9 +293,7 @@ int main(int argc, char *argv[]) {
             free(gbs);
             free(src);
             free(remap);
-            gac_chains_free(cs);
-            gac_close(ctx);
-            gt_stage("device close");
+            gt_device_close_async(&dev, ctx, cs); /* overlaps writing the nets */
         }
         if (dev.started) { /* nothing to rescore: the genomes were never needed */
             gac_ctx *ctx = gt_device_wait(&dev);
@@ -300,6 +324,8 @@ int main(int argc, char *argv[]) {
         if (wo[k].rc != GAC_OK)
             gt_abort("%s\n", wo[k].err);
     gt_stage("write nets");
+    gt_device_close_join(&dev);
+    gt_stage("device close (rest)");
     /* the net, chains and sizes are left to process exit (freeing millions
      * of arena blocks and arrays only costs time) */
     gac_gapcalc_free(gap);

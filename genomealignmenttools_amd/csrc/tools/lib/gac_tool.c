@@ -96,6 +96,10 @@ void gt_device_start(gt_device *d, const char *t2bit, const char *q2bit, const i
 
 static void join_live_device(void) {
     gt_device *d = g_live_dev;
+    if (d && d->closing && !pthread_equal(pthread_self(), (pthread_t)d->close_th)) {
+        pthread_join((pthread_t)d->close_th, NULL);
+        d->closing = 0;
+    }
     if (d && d->started && !pthread_equal(pthread_self(), (pthread_t)d->th)) {
         pthread_join((pthread_t)d->th, NULL);
         d->started = 0;
@@ -122,6 +126,42 @@ gac_ctx *gt_device_join(gt_device *d) {
     gt_verbose(2, "[stage] (overlapped) device open %.3f s, 2bit genomes to HBM %.3f s\n",
                d->open_s, d->load_s);
     return d->ctx;
+}
+
+typedef struct close_job {
+    gac_ctx *ctx;
+    gac_chainset *cs;
+} close_job;
+
+static void *close_thread(void *arg) {
+    close_job *j = arg;
+    gac_chains_free(j->cs);
+    gac_close(j->ctx);
+    free(j);
+    return NULL;
+}
+
+void gt_device_close_async(gt_device *d, gac_ctx *ctx, gac_chainset *cs) {
+    close_job *j = malloc(sizeof(*j));
+    j->ctx = ctx;
+    j->cs = cs;
+    pthread_t th;
+    if (pthread_create(&th, NULL, close_thread, j) != 0) {
+        close_thread(j);
+        return;
+    }
+    d->close_th = (unsigned long)th;
+    d->closing = 1;
+    g_live_dev = d; /* gt_abort joins it before exiting */
+}
+
+void gt_device_close_join(gt_device *d) {
+    if (d->closing) {
+        pthread_join((pthread_t)d->close_th, NULL);
+        d->closing = 0;
+    }
+    if (g_live_dev == d)
+        g_live_dev = NULL;
 }
 
 void gt_check(int rc) {

@@ -41,12 +41,18 @@ typedef struct gt_device {
     double open_s, load_s;
     char err[1024];
     unsigned long th; /* pthread_t */
+    unsigned long close_th;
+    int closing;
 } gt_device;
 void gt_device_start(gt_device *d, const char *t2bit, const char *q2bit, const int32_t mat[16],
                      const gac_gapcalc *gap);
 gac_ctx *gt_device_join(gt_device *d);
 /* the same wait without the abort: NULL if the bring-up failed */
 gac_ctx *gt_device_wait(gt_device *d);
+/* Release a chain set and close the context on a helper thread (the host
+ * writes its output meanwhile); gt_device_close_join waits for it. */
+void gt_device_close_async(gt_device *d, gac_ctx *ctx, gac_chainset *cs);
+void gt_device_close_join(gt_device *d);
 
 /* ---- options ---- */
 enum { GT_BOOL, GT_INT, GT_DOUBLE, GT_STRING };

@@ -140,6 +140,7 @@ int main(int argc, char *argv[]) {
     int32_t *ali = malloc((c.n ? c.n : 1) * 4);
     gt_check(gac_score_ranges(ctx, cs, r, c.n, GAC_WANT_LOCAL, glob, loc, ali));
     gt_stage("GPU scoring");
+    gt_device_close_async(&dev, ctx, cs); /* overlaps writing the output */
 
     /* chainWriteHead assigns ids to id-less chains in output order
      * (chain.c:203-204): fix them before the parallel formatting */
@@ -151,9 +152,8 @@ int main(int argc, char *argv[]) {
     free(ids);
     gt_careful_close(out, argv[4]);
     gt_stage("write output");
-    /* host arrays are left to process exit; the device context is closed */
-    gac_chains_free(cs);
-    gac_close(ctx);
-    gt_stage("device close");
+    /* host arrays are left to process exit */
+    gt_device_close_join(&dev);
+    gt_stage("device close (rest)");
     return 0;
 }
