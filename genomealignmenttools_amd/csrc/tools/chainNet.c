@@ -329,5 +329,5 @@ int main(int argc, char *argv[]) {
     /* the net, chains and sizes are left to process exit (freeing millions
      * of arena blocks and arrays only costs time) */
     gac_gapcalc_free(gap);
-    return 0;
+    gt_exit_ok();
 }

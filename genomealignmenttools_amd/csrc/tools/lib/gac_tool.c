@@ -164,6 +164,13 @@ void gt_device_close_join(gt_device *d) {
         g_live_dev = NULL;
 }
 
+void gt_exit_ok(void) {
+    join_live_device();
+    if (fflush(NULL) != 0)
+        gt_abort("write error\n");
+    _exit(0);
+}
+
 void gt_check(int rc) {
     if (rc != GAC_OK)
         gt_abort("%s", gac_last_error());

@@ -53,6 +53,11 @@ gac_ctx *gt_device_wait(gt_device *d);
  * writes its output meanwhile); gt_device_close_join waits for it. */
 void gt_device_close_async(gt_device *d, gac_ctx *ctx, gac_chainset *cs);
 void gt_device_close_join(gt_device *d);
+/* Successful end of a tool once its outputs are closed and the device context
+ * is released: flush stdio and leave without running exit-time destructors
+ * (the HIP runtime's teardown of an already closed context, freeing of the
+ * host arrays); the kernel reclaims both. */
+void gt_exit_ok(void) __attribute__((noreturn));
 
 /* ---- options ---- */
 enum { GT_BOOL, GT_INT, GT_DOUBLE, GT_STRING };

@@ -155,5 +155,5 @@ int main(int argc, char *argv[]) {
     /* host arrays are left to process exit */
     gt_device_close_join(&dev);
     gt_stage("device close (rest)");
-    return 0;
+    gt_exit_ok();
 }
