@@ -98,6 +98,7 @@ static void *subset_copy_thread(void *arg) {
 }
 
 int main(int argc, char *argv[]) {
+    gt_stage("");
     int min_space = 25;
     double min_score = 2000;
     gt_options(&argc, argv, k_opts);
@@ -143,7 +144,7 @@ int main(int argc, char *argv[]) {
         gt_device_start(&dev, tnib, qnib, mat, gap);
 
     gt_sizes qs, ts;
-    gt_stage(NULL);
+    gt_stage("options + setup");
     gt_read_sizes(qsizes_file, &qs);
     gt_read_sizes(tsizes_file, &ts);
     gt_verbose(1, "Got %d chroms in %s, %d in %s\n", ts.names.n, tsizes_file, qs.names.n,

@@ -46,11 +46,41 @@ void gt_verbose(int level, const char *fmt, ...) {
 
 int gt_verbosity(void) { return g_verbose; }
 
+/* seconds since this process started (/proc/self/stat starttime, clock
+ * ticks since boot, against CLOCK_BOOTTIME); -1 if unavailable */
+static double since_process_start(void) {
+    FILE *f = fopen("/proc/self/stat", "r");
+    if (!f)
+        return -1;
+    char buf[1024];
+    const size_t n = fread(buf, 1, sizeof(buf) - 1, f);
+    fclose(f);
+    buf[n] = 0;
+    const char *p = strrchr(buf, ')'); /* the command name may hold spaces */
+    if (!p)
+        return -1;
+    unsigned long long start = 0;
+    /* fields after ")": state is field 3, starttime is field 22 */
+    if (sscanf(p + 2, "%*c %*d %*d %*d %*d %*d %*u %*u %*u %*u %*u %*u %*u %*d %*d %*d %*d %*d %*d %llu",
+               &start) != 1)
+        return -1;
+    struct timespec ts;
+    clock_gettime(CLOCK_BOOTTIME, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec - (double)start / (double)sysconf(_SC_CLK_TCK);
+}
+
 void gt_stage(const char *what) {
     static double last = -1;
     struct timespec ts;
     clock_gettime(CLOCK_MONOTONIC, &ts);
     const double now = ts.tv_sec + 1e-9 * ts.tv_nsec;
+    static double startup = -2; /* process start -> first call (main's entry) */
+    if (startup == -2)
+        startup = since_process_start();
+    if (last >= 0 && what && g_verbose >= 2 && startup > -2) {
+        fprintf(stderr, "[stage] %-32s %8.3f s\n", "exec + libraries (approx.)", startup);
+        startup = -3;
+    }
     if (last >= 0 && what && g_verbose >= 2)
         fprintf(stderr, "[stage] %-32s %8.3f s\n", what, now - last);
     last = now;

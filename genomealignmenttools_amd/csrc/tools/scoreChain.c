@@ -72,6 +72,7 @@ static void write_one(FILE *out, int64_t i, void *arg) {
 }
 
 int main(int argc, char *argv[]) {
+    gt_stage("");
     gt_options(&argc, argv, k_opts);
     const char *gap_name = gt_opt_str("linearGap", NULL);
     const char *scheme_name = gt_opt_str("scoreScheme", NULL);
@@ -103,7 +104,7 @@ int main(int argc, char *argv[]) {
 
     /* device open + genome upload run on a helper thread beside the parse */
     gt_device dev;
-    gt_stage(NULL);
+    gt_stage("options + setup");
     gt_device_start(&dev, t2bit, q2bit, mat, gap);
 
     FILE *out = gt_must_open(argv[4], "w");

@@ -167,7 +167,7 @@ def scorechain(a):
     t_ours, r = timed([os.path.join(BIN, "scoreChain")] + args + [p("ours.chain"), "-linearGap=loose",
                                                                   "-verbose=2"])
     res = {"tool": "scoreChain", "chains": a.chains, "seed": a.seed, "ours_s": round(t_ours, 3),
-           "stages": [l for l in r.stderr.splitlines() if " s" in l][-8:]}
+           "stages": [l for l in r.stderr.splitlines() if "[stage]" in l]}
     if os.path.exists(os.path.join(REF, "scoreChain")) and not a.no_ref:
         t_ref, _ = timed([os.path.join(REF, "scoreChain")] + args + [p("ref.chain"),
                                                                      "-linearGap=loose"])
@@ -185,7 +185,7 @@ def chainnet(a):
                       opts + ["-verbose=2"])
     res = {"tool": "chainNet -rescore", "chains": a.chains, "seed": a.seed,
            "ours_s": round(t_ours, 3),
-           "stages": [l for l in r.stderr.splitlines() if " s" in l][-8:]}
+           "stages": [l for l in r.stderr.splitlines() if "[stage]" in l]}
     if os.path.exists(os.path.join(REF, "chainNet")) and not a.no_ref:
         t_ref, _ = timed([os.path.join(REF, "chainNet")] + args + [p("ref.t.net"), p("ref.q.net")] +
                          opts)
