@@ -565,7 +565,6 @@ int main(int argc, char *argv[]) {
     gt_verbose(2, "chaining + writing in %.3f s\n", wall() - t0);
     gt_verbose(2, "%lld pairs, %lld blocks, %lld chains\n", (long long)np, (long long)nb,
                (long long)ch->n_chains);
-    gac_axt_chains_free(ch);
-    gac_close(ctx);
-    return 0;
+    gac_close(ctx); /* host arrays are left to process exit */
+    gt_exit_ok();
 }

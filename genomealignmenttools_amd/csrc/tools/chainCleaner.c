@@ -1190,6 +1190,7 @@ static void net_in_process(const char *in_chain, const char *tsizes, const char 
 
 /* ================================================================ main */
 int main(int argc, char *argv[]) {
+    gt_stage("");
     gt_options(&argc, argv, k_opts);
     if (argc != 6)
         usage();
@@ -1243,6 +1244,7 @@ int main(int argc, char *argv[]) {
     /* device + genomes come up on a helper thread during steps 0-2 */
     gt_device dev;
     gt_device_start(&dev, tnib, qnib, mat, gap);
+    gt_stage("options + setup");
 
     /* ---- 0. net the chains if no net is given */
     gt_lines net_lines;
@@ -1260,6 +1262,7 @@ int main(int argc, char *argv[]) {
         gt_lines_read(in_net, &net_lines);
     }
 
+    gt_stage("0. netting + filter");
     /* ---- 1. fills/gaps and valid breaks (getFillGapAndValidBreaks) */
     gt_verbose(1, "1. parsing fills/gaps from %s and getting valid breaks ...\n", net_what);
     gt_net_parse(&net_lines, net_what, &g_net.ns);
@@ -1344,6 +1347,7 @@ int main(int argc, char *argv[]) {
     }
     gt_lines_free(&net_lines);
     gt_verbose(1, "DONE (parsing fills/gaps and getting valid breaks)\n\n");
+    gt_stage("1. net parse + valid breaks");
 
     /* ---- 2. read the chains; the others go straight to the output */
     gt_verbose(1, "2. reading breaking and broken chains from %s ...\n", in_chain);
@@ -1390,6 +1394,7 @@ int main(int argc, char *argv[]) {
     gt_verbose(1, "DONE\n\n");
 
     /* ---- 3. genomes and the chains of interest to the GPU */
+    gt_stage("2. read chains");
     gt_verbose(1, "3. reading target and query DNA sequences for breaking and broken chains ...\n");
     {
         int32_t *order = malloc((size_t)(interest.n ? interest.n : 1) * 4);
@@ -1437,6 +1442,7 @@ int main(int argc, char *argv[]) {
     }
     gt_verbose(1, "DONE\n\n");
 
+    gt_stage("3. device + chains of interest");
     /* ---- 4. loopOverBreaks */
     gt_verbose(1, "4. loop over all breaks. Remove suspects if they pass our filters and write out deleted suspects to %s ...\n",
                out_bed);
@@ -1484,6 +1490,7 @@ int main(int argc, char *argv[]) {
     }
     gt_verbose(1, "DONE\n\n");
 
+    gt_stage("4. loop over breaks");
     /* ---- 5. the breaking and broken chains (writeAndFreeChainsOfInterest),
      * modified ones rescored -- one batch */
     gt_verbose(1, "5. write the (new) breaking and the broken chains ...\n");
@@ -1514,6 +1521,7 @@ int main(int argc, char *argv[]) {
     gt_verbose(1, "DONE\n\n");
 
     /* ---- 6. chainSort */
+    gt_stage("5. write chains of interest");
     gt_verbose(1, "6. chainSort %s ...\n", out_chain);
     {
         FILE *f = gt_must_open(out_chain, "w");
@@ -1540,10 +1548,11 @@ int main(int argc, char *argv[]) {
         free(k);
     }
     gt_verbose(1, "DONE\n\n");
+    gt_stage("6. chainSort");
     gt_verbose(1, "GPU: %lld scoring calls, %lld sub-chains, %lld re-uploads, %.3f s in scoring calls\n",
                (long long)g_gpu_calls, (long long)g_gpu_ranges, (long long)g_uploads, g_gpu_s);
     gt_verbose(1, "\nALL DONE. New chains are in %s. Deleted suspects in %s\n", out_chain, out_bed);
     gac_chains_free(S.cs_base);
     gac_close(S.ctx);
-    return 0;
+    gt_exit_ok(); /* host state is left to process exit */
 }

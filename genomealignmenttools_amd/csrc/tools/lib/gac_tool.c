@@ -71,17 +71,21 @@ static double since_process_start(void) {
 
 void gt_stage(const char *what) {
     static double last = -1;
+    static int env = -1; /* GAC_TIMING prints the stages at any verbosity */
+    if (env < 0)
+        env = getenv("GAC_TIMING") != NULL;
+    const int show = g_verbose >= 2 || env;
     struct timespec ts;
     clock_gettime(CLOCK_MONOTONIC, &ts);
     const double now = ts.tv_sec + 1e-9 * ts.tv_nsec;
     static double startup = -2; /* process start -> first call (main's entry) */
     if (startup == -2)
         startup = since_process_start();
-    if (last >= 0 && what && g_verbose >= 2 && startup > -2) {
+    if (last >= 0 && what && show && startup > -2) {
         fprintf(stderr, "[stage] %-32s %8.3f s\n", "exec + libraries (approx.)", startup);
         startup = -3;
     }
-    if (last >= 0 && what && g_verbose >= 2)
+    if (last >= 0 && what && show)
         fprintf(stderr, "[stage] %-32s %8.3f s\n", what, now - last);
     last = now;
 }

@@ -109,10 +109,12 @@ def cleaner(a):
     p = lambda x: os.path.join(d, x)
     t_ours, r = timed([os.path.join(BIN, "chainCleaner"), inc, p("t.2bit"), p("q.2bit"),
                        p("ours.chain"), p("ours.bed"), f"-tSizes={p('t.sizes')}",
-                       f"-qSizes={p('q.sizes')}", "-linearGap=loose", "-verbose=1"], cwd=d)
+                       f"-qSizes={p('q.sizes')}", "-linearGap=loose", "-verbose=1"], cwd=d,
+                      env=dict(os.environ, GAC_TIMING="1"))
     res = {"tool": "chainCleaner", "loci": a.loci, "seed": a.seed, "ours_s": round(t_ours, 3),
            "removed": sum(1 for _ in open(p("ours.bed"))),
-           "gpu": [l for l in r.stderr.splitlines() if l.startswith("GPU:")]}
+           "gpu": [l for l in r.stderr.splitlines() if l.startswith("GPU:")],
+           "stages": [l for l in r.stderr.splitlines() if "[stage]" in l]}
     if os.path.exists(os.path.join(REF, "chainCleaner")) and not a.no_ref:
         env = dict(os.environ, PATH=REF + os.pathsep + os.environ.get("PATH", ""))
         t_net, rn = timed([os.path.join(REF, "chainNet"), "-minScore=0", inc, p("t.sizes"),
