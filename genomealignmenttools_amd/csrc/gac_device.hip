@@ -27,6 +27,7 @@ hipError_t launch_plan(const ScoreArgs &a, hipStream_t s);
 hipError_t launch_tilemap(const ScoreArgs &a, hipStream_t s);
 hipError_t launch_tile(const ScoreArgs &a, int grid, hipStream_t s);
 hipError_t launch_combine(const ScoreArgs &a, int grid, hipStream_t s);
+hipError_t launch_small(const ScoreArgs &a, const Range *rin, SmallOut *out, hipStream_t s);
 struct SeqDev {
     int64_t byte_off;
     int64_t word_off;
@@ -132,6 +133,11 @@ struct gac_ctx {
     Range *d_ranges = nullptr;
     long long *d_g = nullptr, *d_l = nullptr;
     int32_t *d_ali = nullptr;
+    Range *h_small_in = nullptr;     // pinned, mapped: ranges of a small batch [kSmallMax]
+    SmallOut *h_small_out = nullptr; // pinned, mapped, coherent: its results
+    Range *d_small_in = nullptr;     // their device addresses
+    SmallOut *d_small_out = nullptr;
+    int small_max = kSmallMax;       // batches up to this size take k_small (GAC_SMALL_MAX)
     int32_t *h_stat = nullptr;   // pinned, coherent host words written by k_scan_agg [8]
     int32_t *d_h_stat = nullptr; // its device address
     int32_t call_seq = 0;
@@ -213,6 +219,19 @@ extern "C" int gac_open(int device, gac_ctx **out) {
         delete c;
         return gac_fail(GAC_E_HIP, "hipHostMalloc failed");
     }
+    if (hipHostMalloc((void **)&c->h_small_in, kSmallMax * sizeof(Range), hipHostMallocMapped) !=
+            hipSuccess ||
+        hipHostMalloc((void **)&c->h_small_out, kSmallMax * sizeof(SmallOut),
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&c->d_small_in, c->h_small_in, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&c->d_small_out, c->h_small_out, 0) != hipSuccess) {
+        gac_close(c);
+        return gac_fail(GAC_E_HIP, "hipHostMalloc failed");
+    }
+    if (const char *v = getenv("GAC_SMALL_MAX")) {
+        const int m = atoi(v);
+        c->small_max = m < 0 ? 0 : (m > kSmallMax ? kSmallMax : m);
+    }
     lap("hipHostMalloc");
     *out = c;
     return GAC_OK;
@@ -243,6 +262,8 @@ extern "C" void gac_close(gac_ctx *c) {
     }
     for (auto ev : c->prof_free) hipEventDestroy(ev);
     if (c->h_stat) hipHostFree(c->h_stat);
+    if (c->h_small_in) hipHostFree(c->h_small_in);
+    if (c->h_small_out) hipHostFree(c->h_small_out);
     for (int k = 0; k < 2; ++k) {
         if (c->pin[k]) hipHostFree(c->pin[k]);
         if (c->pin_ev[k]) hipEventDestroy(c->pin_ev[k]);
@@ -1153,6 +1174,23 @@ extern "C" int gac_score_ranges(gac_ctx *c, const gac_chainset *cs, const gac_ra
             return gac_fail(GAC_E_ARG, "range %lld: chain %d out of range", (long long)i,
                             ranges[i].chain);
     HIPCHK(hipSetDevice(c->device));
+    if (n <= c->small_max) {
+        // one launch; ranges in and results out through pinned host memory
+        hipStream_t s = c->stream;
+        ScoreArgs a;
+        int rc = prepare_args(c, cs, n, flags, local, s, a);
+        if (rc != GAC_OK) return rc;
+        memcpy(c->h_small_in, ranges, (size_t)n * sizeof(Range));
+        HIPCHK(launch_small(a, c->d_small_in, c->d_small_out, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (int64_t i = 0; i < n; ++i) {
+            const SmallOut o = c->h_small_out[i];
+            global[i] = o.g;
+            ali[i] = o.ali;
+            if (flags & GAC_WANT_LOCAL) local[i] = o.l;
+        }
+        return GAC_OK;
+    }
     if (n > c->io_n) {
         int64_t cap = n + n / 2 + 1024;
         if (c->d_ranges) hipFree(c->d_ranges);

@@ -132,6 +132,14 @@ struct ScoreArgs {
     GapDev gap;
 };
 
+// Result of one range of a small batch (k_small writes it straight to pinned
+// host memory).
+struct SmallOut {
+    long long g, l;
+    int32_t ali, pad;
+};
+constexpr int kSmallMax = 256;  // ranges per small-batch call
+
 // One ungapped block for k_blocks (axtScoreUngapped): global plane positions
 // of its first target base and, for the query, of its first base ('+') or
 // one past its last base on the forward strand ('-').

@@ -923,6 +923,73 @@ __global__ void __launch_bounds__(256) k_combine(ScoreArgs a) {
     }
 }
 
+// ------------------------------------------------------------ k_small ----
+// Small batches (chainCleaner's on-demand sub-chains): one launch, one wave
+// per range, ranges read from and results written to pinned host memory.
+// The wave plans the range like k_plan, then walks its window 64 blocks at a
+// time (lane = block, the block's 32-base chunks in turn) and folds global,
+// aligned bases and the local-score element in block order.  No workspace,
+// no scans across workgroups: a call costs one launch.
+template <bool LOCAL, bool SYM>
+__global__ void __launch_bounds__(256) k_small(ScoreArgs a, const Range *rin, SmallOut *out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (w >= a.n) return;
+    const RangeDesc d = plan_range(a, rin[w]);
+    const bool minus = d.qbase < 0;
+    long long gsum = 0, asum = 0;
+    Elem acc = {0, kNeg, kNeg, kNeg};
+    for (int base = 0; base < d.nblk; base += kWave) {
+        const int k = base + lane;
+        long long vg = 0;
+        int va = 0;
+        Elem e = {0, kNeg, kNeg, kNeg};
+        if (k < d.nblk) {
+            const int4 bk = a.blk[d.b0 + k];  // {tStart, qStart, size | N flags, gap to next}
+            const bool last = (k == d.nblk - 1);
+            const int z = bk.z & kSizeMask;
+            int cts = bk.x, cqs = bk.y, cte = bk.x + z;
+            if (cts < d.s) {
+                cqs += d.s - cts;
+                cts = d.s;
+            }
+            if (cte > d.e) cte = d.e;
+            const int len = cte - cts;
+            const int64_t tpos = d.tbase + cts;
+            const int64_t qpos = minus ? ~d.qbase - cqs : d.qbase + cqs;
+            ChunkRef c;
+            c.k = 0;
+            c.lq = len | (minus ? (int)0x80000000 : 0) | (bk.z & (kTHasN | kQHasN));
+            long long bsc = 0;
+            for (int off = 0; off < len; off += 32) {
+                c.n = min(32, len - off);
+                c.tp = tpos + off;
+                c.qp = minus ? qpos - off - c.n : qpos + off;
+                bsc += chunk_eval<SYM>(a, c, chunk_load(a, c));
+            }
+            const int g = last ? 0 : bk.w;
+            vg = bsc - g;
+            va = len;
+            if (LOCAL) {
+                e.A = last ? bsc : bsc - g;
+                e.B = last ? kNeg : 0;
+                e.C = bsc;
+            }
+        }
+        gsum += wave_sum(vg);
+        asum += wave_sum(va);
+        if (LOCAL) acc = compose(acc, wave_fold(e, lane));  // lane 0 holds the fold
+    }
+    if (lane == 0) {
+        SmallOut o;
+        o.g = gsum;
+        o.l = LOCAL ? max2(0, max2(acc.C, acc.D)) : 0;
+        o.ali = (int32_t)asum;
+        o.pad = 0;
+        out[w] = o;
+    }
+}
+
 // ------------------------------------------------------------ genome -----
 // Raw .2bit payload (2 bits/base, MSB first in each byte) -> bit planes.
 struct SeqDev {
@@ -1022,6 +1089,18 @@ hipError_t launch_tile(const ScoreArgs &a, int grid, hipStream_t s) {
     } else {
         if (a.sym) hipLaunchKernelGGL((k_tile<false, true>), dim3(grid), dim3(256), 0, s, a);
         else hipLaunchKernelGGL((k_tile<false, false>), dim3(grid), dim3(256), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_small(const ScoreArgs &a, const Range *rin, SmallOut *out, hipStream_t s) {
+    const dim3 g((unsigned)((a.n + kWavesPerWG - 1) / kWavesPerWG)), b(256);
+    if (a.want_local) {
+        if (a.sym) hipLaunchKernelGGL((k_small<true, true>), g, b, 0, s, a, rin, out);
+        else hipLaunchKernelGGL((k_small<true, false>), g, b, 0, s, a, rin, out);
+    } else {
+        if (a.sym) hipLaunchKernelGGL((k_small<false, true>), g, b, 0, s, a, rin, out);
+        else hipLaunchKernelGGL((k_small<false, false>), g, b, 0, s, a, rin, out);
     }
     return hipGetLastError();
 }
