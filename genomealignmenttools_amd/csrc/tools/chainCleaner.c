@@ -1189,6 +1189,24 @@ static void net_in_process(const char *in_chain, const char *tsizes, const char 
 }
 
 /* ================================================================ main */
+/* chainSort's output, formatted in parallel (gt_par_write keeps the order) */
+typedef struct sorted_out {
+    const gt_chains *c;
+    const sortkey *k;
+} sorted_out;
+
+static void write_sorted(FILE *f, int64_t j, void *arg) {
+    const sorted_out *so = arg;
+    const gt_chains *c = so->c;
+    const outchain *o = &g_out[g_nout - 1 - so->k[j].rank];
+    if (o->from >= 0)
+        gt_write_chain(f, c, o->from, o->score, c->id[o->from]);
+    else
+        gt_write_chain_raw(f, o->score, c->tnames.names[o->tname], o->tsize, o->tstart, o->tend,
+                           c->qnames.names[o->qname], o->qsize, o->qminus, o->qstart, o->qend,
+                           o->id, o->bt, o->bq, o->bs, o->nb);
+}
+
 int main(int argc, char *argv[]) {
     gt_stage("");
     gt_options(&argc, argv, k_opts);
@@ -1535,15 +1553,8 @@ int main(int argc, char *argv[]) {
             k[i].rank = g_nout - 1 - i;
         }
         qsort(k, (size_t)g_nout, sizeof(sortkey), sortkey_cmp);
-        for (int64_t j = 0; j < g_nout; ++j) {
-            const outchain *o = &g_out[g_nout - 1 - k[j].rank];
-            if (o->from >= 0)
-                gt_write_chain(f, &S.c, o->from, o->score, S.c.id[o->from]);
-            else
-                gt_write_chain_raw(f, o->score, S.c.tnames.names[o->tname], o->tsize, o->tstart,
-                                   o->tend, S.c.qnames.names[o->qname], o->qsize, o->qminus,
-                                   o->qstart, o->qend, o->id, o->bt, o->bq, o->bs, o->nb);
-        }
+        sorted_out so = {&S.c, k};
+        gt_par_write(f, g_nout, write_sorted, &so);
         gt_careful_close(f, out_chain);
         free(k);
     }
