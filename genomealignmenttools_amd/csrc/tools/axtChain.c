@@ -22,6 +22,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <stdatomic.h>
 #include <time.h>
 
 #include "gac_tool.h"
@@ -105,53 +106,9 @@ static char *rd_next(rd *r) {
     return line;
 }
 
-/* lineFileNextReal: not blank, not starting (after spaces) with '#' */
-static char *rd_next_real(rd *r) {
-    char *line;
-    while ((line = rd_next(r)) != NULL) {
-        const char *s = line;
-        while (isspace((unsigned char)*s))
-            ++s;
-        if (*s != 0 && *s != '#')
-            return line;
-    }
-    return NULL;
-}
-
 /* kent chopByWhite into at most max words (modifies s) */
 static int chop(char *s, char **w, int max) {
     return gac_chop_white(s, w, max);
-}
-
-static unsigned sql_unsigned(const char *s) {
-    char *end;
-    if (!isdigit((unsigned char)*s))
-        gt_abort("invalid unsigned integer: \"%s\"", s);
-    unsigned long v = strtoul(s, &end, 10);
-    if (*end != 0)
-        gt_abort("invalid unsigned integer: \"%s\"", s);
-    return (unsigned)v;
-}
-
-/* sqlUnsignedDynamicArray: comma-separated, optional trailing comma */
-static int32_t *sql_uarray(char *s, int *count) {
-    int n = 0, cap = 16;
-    int32_t *a = malloc(cap * sizeof(int32_t));
-    while (*s) {
-        char *c = strchr(s, ',');
-        if (c)
-            *c = 0;
-        if (n == cap) {
-            cap *= 2;
-            a = realloc(a, cap * sizeof(int32_t));
-        }
-        a[n++] = (int32_t)sql_unsigned(s);
-        if (!c)
-            break;
-        s = c + 1;
-    }
-    *count = n;
-    return a;
 }
 
 /* ------------------------------------------------------------ seqPairs */
@@ -200,6 +157,219 @@ static void pair_add(pair *p, int32_t t, int32_t q, int32_t size) {
     ++p->nb;
 }
 
+/* sqlUnsigned without aborting: 0 = ok */
+static int sql_unsigned_ok(const char *s, unsigned *v, char *err) {
+    char *end;
+    if (!isdigit((unsigned char)*s)) {
+        snprintf(err, 600, "invalid unsigned integer: \"%.400s\"", s);
+        return -1;
+    }
+    const unsigned long x = strtoul(s, &end, 10);
+    if (*end != 0) {
+        snprintf(err, 600, "invalid unsigned integer: \"%.400s\"", s);
+        return -1;
+    }
+    *v = (unsigned)x;
+    return 0;
+}
+
+/* sqlUnsignedDynamicArray into a reusable buffer: 0 = ok */
+static int sql_uarray_ok(char *s, int32_t **a, int *cap, int *count, char *err) {
+    int n = 0;
+    while (*s) {
+        char *c = strchr(s, ',');
+        if (c)
+            *c = 0;
+        if (n == *cap) {
+            *cap = *cap ? *cap * 2 : 64;
+            *a = realloc(*a, (size_t)*cap * sizeof(int32_t));
+        }
+        unsigned v;
+        if (sql_unsigned_ok(s, &v, err) != 0)
+            return -1;
+        (*a)[n++] = (int32_t)v;
+        if (!c)
+            break;
+        s = c + 1;
+    }
+    *count = n;
+    return 0;
+}
+
+/* One pslLoad line (psl.c pslLoad + readPslBlocks :345-377) into P.
+ * 0 = ok; else the reference's error: PSL_E_WORDS (word count in *wc_out),
+ * PSL_E_COUNT (block count mismatch) -- both name the file line, which the
+ * caller knows -- or PSL_E_MSG with the whole message in err. */
+enum { PSL_E_WORDS = 1, PSL_E_COUNT = 2, PSL_E_MSG = 3 };
+
+static void psl_error(int kind, int wc, const char *msg, int64_t lineno, const char *path) {
+    if (kind == PSL_E_WORDS)
+        gt_abort("Bad line %lld of %s wordCount is %d instead of 21 or 23\n", (long long)lineno,
+                 path, wc);
+    if (kind == PSL_E_COUNT)
+        gt_abort("Assertion `sizeOne == ret->blockCount' failed (line %lld of %s)",
+                 (long long)lineno, path);
+    gt_abort("%s", msg);
+}
+
+static int psl_line(char *line, pairs *P, char *err, int *wc_out) {
+    static __thread int32_t *sz, *qs, *ts;
+    static __thread int csz, cqs, cts;
+    char *w[32];
+    const int wc = chop(line, w, 32);
+    if (wc != 21 && wc != 23) {
+        *wc_out = wc;
+        return PSL_E_WORDS;
+    }
+    unsigned block_count, v;
+    if (sql_unsigned_ok(w[17], &block_count, err) != 0)
+        return PSL_E_MSG;
+    for (int i = 0; i < 8; ++i)
+        if (sql_unsigned_ok(w[i][0] == '-' ? w[i] + 1 : w[i], &v, err) != 0)
+            return PSL_E_MSG;
+    const char *strand = w[8];
+    if (sql_unsigned_ok(w[10], &v, err) != 0 || sql_unsigned_ok(w[14], &v, err) != 0)
+        return PSL_E_MSG;
+    int n1, n2, n3;
+    if (sql_uarray_ok(w[18], &sz, &csz, &n1, err) != 0 || sql_uarray_ok(w[19], &qs, &cqs, &n2, err) != 0 ||
+        sql_uarray_ok(w[20], &ts, &cts, &n3, err) != 0)
+        return PSL_E_MSG;
+    if ((unsigned)n1 != block_count || (unsigned)n2 != block_count || (unsigned)n3 != block_count)
+        return PSL_E_COUNT;
+    if (strand[1] != '\0') {
+        snprintf(err, 600, "requires PSLs to have implicit positive strand, found `%.400s'", strand);
+        return PSL_E_MSG;
+    }
+    pair *p = pair_get(P, w[9], strand, w[13]);
+    for (unsigned i = 0; i < block_count; ++i)
+        pair_add(p, ts[i], qs[i], sz[i]);
+    return 0;
+}
+
+/* A line-aligned piece of the PSL body, parsed on its own thread into local
+ * seqPairs (first-seen order, blocks in file order), its '#' lines and its
+ * first error; the pieces are merged in file order, so pair order, block
+ * order, metadata output and the reported error match a sequential read. */
+typedef struct psl_chunk {
+    char *a, *b;
+    const char *path;
+    int64_t lines; /* newlines parsed (up to the error) */
+    pairs P;
+    char **meta;
+    int32_t n_meta, meta_cap;
+    int err, err_wc;  /* PSL_E_* of the first bad line, its word count */
+    int64_t err_line; /* within the chunk, 1-based */
+    char msg[600];
+} psl_chunk;
+
+typedef struct psl_job {
+    psl_chunk *k;
+    int nk;
+    _Atomic int next;
+} psl_job;
+
+static void *psl_chunk_thread(void *arg) {
+    psl_job *J = arg;
+    for (;;) {
+        const int i = atomic_fetch_add(&J->next, 1);
+        if (i >= J->nk)
+            break;
+        psl_chunk *k = &J->k[i];
+        for (char *p = k->a; p < k->b;) {
+            char *nl = memchr(p, '\n', (size_t)(k->b - p));
+            char *line = p;
+            if (nl) {
+                *nl = 0;
+                p = nl + 1;
+            } else {
+                p = k->b;
+            }
+            ++k->lines;
+            if (line[0] == '#') { /* lineFileSetUniqueMetaData: in order, de-duplicated later */
+                if (k->n_meta == k->meta_cap) {
+                    k->meta_cap = k->meta_cap ? 2 * k->meta_cap : 16;
+                    k->meta = realloc(k->meta, (size_t)k->meta_cap * sizeof(char *));
+                }
+                k->meta[k->n_meta++] = line;
+            }
+            const char *s = line; /* lineFileNextReal */
+            while (isspace((unsigned char)*s))
+                ++s;
+            if (*s == 0 || *s == '#')
+                continue;
+            const int e = psl_line(line, &k->P, k->msg, &k->err_wc);
+            if (e) {
+                k->err = e;
+                k->err_line = k->lines;
+                break;
+            }
+        }
+    }
+    return NULL;
+}
+
+static void read_psl_chunks(rd *r, pairs *P) {
+    char *a = r->cur, *end = r->end;
+    const size_t len = (size_t)(end - a);
+    int nk = len < (4u << 20) ? 1 : gt_threads() * 4;
+    psl_chunk *K = calloc((size_t)nk, sizeof(psl_chunk));
+    int n = 0;
+    char *prev = a;
+    for (int i = 1; i <= nk && prev < end; ++i) {
+        char *cut = i == nk ? end : a + len / nk * i;
+        if (cut < prev)
+            cut = prev;
+        if (cut < end) {
+            char *nl = memchr(cut, '\n', (size_t)(end - cut));
+            cut = nl ? nl + 1 : end;
+        }
+        if (cut > prev) {
+            K[n].a = prev;
+            K[n].b = cut;
+            K[n].path = r->path;
+            ++n;
+            prev = cut;
+        }
+    }
+    psl_job J = {K, n, 0};
+    atomic_init(&J.next, 0);
+    gac_run_threads(gt_threads() < n ? gt_threads() : (n ? n : 1), psl_chunk_thread, &J);
+    int64_t line0 = r->line;
+    for (int i = 0; i < n; ++i) {
+        psl_chunk *k = &K[i];
+        for (int32_t m = 0; m < k->n_meta; ++m)
+            rd_meta(r, k->meta[m]);
+        if (k->err)
+            psl_error(k->err, k->err_wc, k->msg, line0 + k->err_line, r->path);
+        for (int32_t j = 0; j < k->P.n; ++j) {
+            pair *lp = &k->P.p[j];
+            const char strand[2] = {lp->strand, 0};
+            pair *gp = pair_get(P, lp->qname, strand, lp->tname);
+            if (gp->nb + lp->nb > gp->cap) {
+                gp->cap = gp->nb + lp->nb + gp->cap;
+                gp->bt = realloc(gp->bt, (size_t)gp->cap * 4);
+                gp->bq = realloc(gp->bq, (size_t)gp->cap * 4);
+                gp->bs = realloc(gp->bs, (size_t)gp->cap * 4);
+            }
+            memcpy(gp->bt + gp->nb, lp->bt, (size_t)lp->nb * 4);
+            memcpy(gp->bq + gp->nb, lp->bq, (size_t)lp->nb * 4);
+            memcpy(gp->bs + gp->nb, lp->bs, (size_t)lp->nb * 4);
+            gp->nb += lp->nb;
+            free(lp->bt);
+            free(lp->bq);
+            free(lp->bs);
+            free(lp->qname);
+            free(lp->tname);
+        }
+        free(k->P.p);
+        gt_names_free(&k->P.keys);
+        free(k->meta);
+        line0 += k->lines;
+    }
+    r->line = (int)line0;
+    free(K);
+}
+
 /* readPslBlocks (:345-377) with pslxFileOpenWithUniqueMeta (psl.c:547-612) */
 static void read_psl(const char *path, pairs *P, FILE *out) {
     rd r;
@@ -236,33 +406,17 @@ static void read_psl(const char *path, pairs *P, FILE *out) {
             r.reuse = 1;
         free(copy);
     }
-    while ((line = rd_next_real(&r)) != NULL) {
-        char *w[32];
-        const int wc = chop(line, w, 32);
-        if (wc != 21 && wc != 23)
-            gt_abort("Bad line %d of %s wordCount is %d instead of 21 or 23\n", r.line, path, wc);
-        const unsigned block_count = sql_unsigned(w[17]);
-        for (int i = 0; i < 8; ++i)
-            (void)sql_unsigned(w[i][0] == '-' ? w[i] + 1 : w[i]);
-        const char *strand = w[8];
-        (void)sql_unsigned(w[10]);
-        (void)sql_unsigned(w[14]);
-        int n1, n2, n3;
-        int32_t *sizes = sql_uarray(w[18], &n1);
-        int32_t *qstarts = sql_uarray(w[19], &n2);
-        int32_t *tstarts = sql_uarray(w[20], &n3);
-        if ((unsigned)n1 != block_count || (unsigned)n2 != block_count ||
-            (unsigned)n3 != block_count)
-            gt_abort("Assertion `sizeOne == ret->blockCount' failed (line %d of %s)", r.line, path);
-        if (strand[1] != '\0')
-            gt_abort("requires PSLs to have implicit positive strand, found `%s'", strand);
-        pair *p = pair_get(P, w[9], strand, w[13]);
-        for (unsigned i = 0; i < block_count; ++i)
-            pair_add(p, tstarts[i], qstarts[i], sizes[i]);
-        free(sizes);
-        free(qstarts);
-        free(tstarts);
+    /* the first data line was read for the format check: parse it here,
+     * then the rest of the file in parallel chunks */
+    char err[600];
+    int wc = 0;
+    if (r.reuse) {
+        r.reuse = 0;
+        const int e = psl_line(r.last, P, err, &wc);
+        if (e)
+            psl_error(e, wc, err, r.line, path);
     }
+    read_psl_chunks(&r, P);
     gt_names_free(&r.seen);
     free(r.buf);
 }
