@@ -39,7 +39,9 @@ struct ngap {
     nfill *fill_head; /* slAddHead order until sorted */
     nfill **fills;
     int n_fills;
-    ngap *next; /* in parent fill's list */
+    ngap *next;   /* in parent fill's list */
+    nfill *pfill; /* parent fill (NULL: a chromosome's root gap) */
+    int32_t pidx; /* index in pfill->gaps; for a root gap, the chromosome */
 };
 
 struct nfill {
@@ -48,7 +50,9 @@ struct nfill {
     ngap **gaps; /* ascending (created in block order at fill time) */
     int n_gaps;
     nfill *next;
-    int64_t ord; /* pre-order index on its side */
+    int64_t ord;  /* pre-order index on its side */
+    ngap *pgap;   /* parent gap; index in pgap->fills; fills above this one */
+    int32_t pidx, level;
 };
 
 typedef struct nchrom {
@@ -757,6 +761,10 @@ static void finish_fill(fin_ctx *x, nfill *f) {
         x->ord = realloc(x->ord, (size_t)x->cap * sizeof(nfill *));
     }
     x->ord[x->n_ord++] = f;
+    for (int i = 0; i < f->n_gaps; ++i) {
+        f->gaps[i]->pfill = f;
+        f->gaps[i]->pidx = i;
+    }
     for (int i = 0; i < f->n_gaps; ++i)
         finish_gap(x, f->gaps[i]);
 }
@@ -775,6 +783,7 @@ static void sort_gap_fills(nwork *w, ngap *g) {
     cnt = 0;
     for (nfill *f = g->fill_head; f; f = f->next)
         g->fills[cnt++] = f;
+    const int32_t level = g->pfill ? g->pfill->level + 1 : 0;
     if (cnt <= 16) { /* fills of one gap are disjoint: starts are distinct */
         for (int i = 1; i < cnt; ++i) {
             nfill *v = g->fills[i];
@@ -787,6 +796,11 @@ static void sort_gap_fills(nwork *w, ngap *g) {
         }
     } else {
         qsort(g->fills, g->n_fills, sizeof(nfill *), cmp_fill);
+    }
+    for (int i = 0; i < cnt; ++i) {
+        g->fills[i]->pgap = g;
+        g->fills[i]->pidx = i;
+        g->fills[i]->level = level;
     }
 }
 
@@ -927,6 +941,7 @@ static void *net_thread(void *arg) {
         /* makeChroms (chainNet.c:328-354): one gap = one space over the
          * whole sequence */
         c->root = gap_new(w, 0, c->size, 0, 0);
+        c->root->pidx = t->chrom;
         sp_init(w, c, 0, c->size, c->root);
         for (int64_t i = 0; i < t->n; ++i) {
             if (t->side == GAC_T)
@@ -1347,52 +1362,46 @@ static char *put_spaces(char *p, int k) {
     return p;
 }
 
-static void out_fill(wctx *w, const nfill *f);
-
-static void out_gap(wctx *w, const nfill *parent, const ngap *g) {
+/* gap line at the given indentation (rOutputGap, chainNet.c:747-761) */
+static void put_gap_line(const wctx *w, const nfill *parent, const ngap *g, int depth) {
     const gac_net_input *in = &w->n->in;
     const int64_t c = parent->chain;
     const char *ochrom = w->side == GAC_Q ? in->t_names[in->t_seq[c]] : in->q_names[in->q_seq[c]];
-    ++w->depth;
-    {
-        char buf[512 + 400], *p = buf;
-        if (strlen(ochrom) > 400 || w->depth > 400) {
-            fprintf(w->f, "%*sgap %d %d %s %c %d %d\n", w->depth, "", g->start,
-                    g->end - g->start, ochrom, in->q_strand[c] ? '-' : '+', g->o_start,
-                    g->o_end - g->o_start);
-        } else {
-            p = put_spaces(p, w->depth);
-            p = put_str(p, "gap ");
-            p = put_int(p, g->start);
-            *p++ = ' ';
-            p = put_int(p, g->end - g->start);
-            *p++ = ' ';
-            p = put_str(p, ochrom);
-            *p++ = ' ';
-            *p++ = in->q_strand[c] ? '-' : '+';
-            *p++ = ' ';
-            p = put_int(p, g->o_start);
-            *p++ = ' ';
-            p = put_int(p, g->o_end - g->o_start);
-            *p++ = '\n';
-            fwrite(buf, 1, (size_t)(p - buf), w->f);
-        }
+    if (strlen(ochrom) > 400 || depth > 400) {
+        fprintf(w->f, "%*sgap %d %d %s %c %d %d\n", depth, "", g->start, g->end - g->start, ochrom,
+                in->q_strand[c] ? '-' : '+', g->o_start, g->o_end - g->o_start);
+        return;
     }
-    for (int i = 0; i < g->n_fills; ++i)
-        out_fill(w, g->fills[i]);
-    --w->depth;
+    char buf[512 + 400], *p = buf;
+    p = put_spaces(p, depth);
+    p = put_str(p, "gap ");
+    p = put_int(p, g->start);
+    *p++ = ' ';
+    p = put_int(p, g->end - g->start);
+    *p++ = ' ';
+    p = put_str(p, ochrom);
+    *p++ = ' ';
+    *p++ = in->q_strand[c] ? '-' : '+';
+    *p++ = ' ';
+    p = put_int(p, g->o_start);
+    *p++ = ' ';
+    p = put_int(p, g->o_end - g->o_start);
+    *p++ = '\n';
+    fwrite(buf, 1, (size_t)(p - buf), w->f);
 }
 
-static void out_fill(wctx *w, const nfill *f) {
-    const gac_net *n = w->n;
+/* subchainInfo (chainNet.c:795-843) and rOutputFill's filter (:763-775):
+ * the fill's score and aligned bases; 1 = the fill is printed (given that
+ * its parent is) */
+static int fill_info(const gac_net *n, int side, const int64_t *tscore, const nfill *f,
+                     double *score_out, int *sub_out) {
     const gac_net_input *in = &n->in;
     const int64_t c = f->chain;
     int s = f->start, e = f->end;
     int sub;
     double score;
-    /* subchainInfo (chainNet.c:795-843) */
     const int fullsz = full_size(n, c);
-    if (w->side == GAC_Q) {
+    if (side == GAC_Q) {
         if (in->q_strand[c]) {
             int qsize = in->q_sizes[in->q_seq[c]];
             int t = s;
@@ -1412,79 +1421,162 @@ static void out_fill(wctx *w, const nfill *f) {
             sub = fullsz;
         } else {
             sub = sub_size(n, c, s, e, 0);
-            if (w->tscore) {
-                double r = (double)w->tscore[f->ord];
+            if (tscore) {
+                double r = (double)tscore[f->ord];
                 score = r <= 0 ? 1 : r; /* chainNet.c:244-245 */
             } else {
                 score = in->score[c] * sub / fullsz;
             }
         }
     }
-    if (score >= n->opt.min_score && sub >= n->opt.min_fill) {
-        ++w->depth;
-        const char *ochrom = w->side == GAC_Q ? in->t_names[in->t_seq[c]] : in->q_names[in->q_seq[c]];
-        if (strlen(ochrom) > 400 || w->depth > 400 || !(score > -1e300 && score < 1e300)) {
-            fprintf(w->f, "%*sfill %d %d %s %c %d %d id %d score %1.0f ali %d\n", w->depth, "",
-                    f->start, f->end - f->start, ochrom, in->q_strand[c] ? '-' : '+', f->o_start,
-                    f->o_end - f->o_start, in->id[c], score, sub);
-        } else {
-            char buf[512 + 400 + 400], *p = buf;
-            p = put_spaces(p, w->depth);
-            p = put_str(p, "fill ");
-            p = put_int(p, f->start);
-            *p++ = ' ';
-            p = put_int(p, f->end - f->start);
-            *p++ = ' ';
-            p = put_str(p, ochrom);
-            *p++ = ' ';
-            *p++ = in->q_strand[c] ? '-' : '+';
-            *p++ = ' ';
-            p = put_int(p, f->o_start);
-            *p++ = ' ';
-            p = put_int(p, f->o_end - f->o_start);
-            p = put_str(p, " id ");
-            p = put_int(p, in->id[c]);
-            p = put_str(p, " score ");
-            p = put_score(p, score);
-            p = put_str(p, " ali ");
-            p = put_int(p, sub);
-            *p++ = '\n';
-            fwrite(buf, 1, (size_t)(p - buf), w->f);
-        }
-        for (int i = 0; i < f->n_gaps; ++i)
-            out_gap(w, f, f->gaps[i]);
-        --w->depth;
-    }
+    *score_out = score;
+    *sub_out = sub;
+    return score >= n->opt.min_score && sub >= n->opt.min_fill;
 }
 
-/* Parallel output: the top-level fills of every chromosome (in output
- * order) are cut into contiguous ranges; each thread prints its range into
- * its own memory stream (a range that starts a chromosome also prints the
- * "net" line), and the buffers are written in order. */
-typedef struct witem {
-    int32_t chrom, fill;
-} witem;
+/* fill line (fillOut, chainNet.c:847-856) */
+static void put_fill_line(const wctx *w, const nfill *f, int depth, double score, int sub) {
+    const gac_net_input *in = &w->n->in;
+    const int64_t c = f->chain;
+    const char *ochrom = w->side == GAC_Q ? in->t_names[in->t_seq[c]] : in->q_names[in->q_seq[c]];
+    if (strlen(ochrom) > 400 || depth > 400 || !(score > -1e300 && score < 1e300)) {
+        fprintf(w->f, "%*sfill %d %d %s %c %d %d id %d score %1.0f ali %d\n", depth, "", f->start,
+                f->end - f->start, ochrom, in->q_strand[c] ? '-' : '+', f->o_start,
+                f->o_end - f->o_start, in->id[c], score, sub);
+        return;
+    }
+    char buf[512 + 400 + 400], *p = buf;
+    p = put_spaces(p, depth);
+    p = put_str(p, "fill ");
+    p = put_int(p, f->start);
+    *p++ = ' ';
+    p = put_int(p, f->end - f->start);
+    *p++ = ' ';
+    p = put_str(p, ochrom);
+    *p++ = ' ';
+    *p++ = in->q_strand[c] ? '-' : '+';
+    *p++ = ' ';
+    p = put_int(p, f->o_start);
+    *p++ = ' ';
+    p = put_int(p, f->o_end - f->o_start);
+    p = put_str(p, " id ");
+    p = put_int(p, in->id[c]);
+    p = put_str(p, " score ");
+    p = put_score(p, score);
+    p = put_str(p, " ali ");
+    p = put_int(p, sub);
+    *p++ = '\n';
+    fwrite(buf, 1, (size_t)(p - buf), w->f);
+}
 
+/* Parallel output.  The .net text of a side is rOutputFill's depth-first
+ * walk (chainNet.c:747-776, 858-896).  Cut it at fill lines: the segment of
+ * the fill at pre-order index i is its "net" header (a chromosome's first
+ * top-level fill), its fill line, and every gap line printed before the next
+ * fill line -- its own gaps up to the first one with a printed fill, and,
+ * once its subtree is done, the remaining gaps of its ancestors up to the
+ * next printed fill.  Segments are independent given the per-fill print
+ * flags, so runs of consecutive pre-order fills are formatted on worker
+ * threads (balanced by fill count, whatever the nesting) and written in
+ * order. */
 typedef struct wjob {
     const gac_net *n;
     int side;
     const int64_t *tscore;
-    const witem *items;
-    int64_t n_items, per;
+    const nfill *const *ord;
+    int64_t nf, per;
+    double *score;   /* per fill (pre-order) */
+    int32_t *sub;
+    uint8_t *show;   /* passes its own filter */
+    uint8_t *more;   /* a later sibling in its gap passes its filter */
+    uint8_t *reached;/* printed: passes and every ancestor fill is printed */
+    _Atomic int64_t next;
 } wjob;
+
+static int gap_prints_fill(const wjob *J, const ngap *g) {
+    if (g->n_fills == 0)
+        return 0;
+    const int64_t o = g->fills[0]->ord;
+    return J->show[o] || J->more[o];
+}
+
+static void write_segment(const wjob *J, wctx *w, int64_t i) {
+    const nfill *f = J->ord[i];
+    if (!f->pgap->pfill && f->pidx == 0) { /* first top-level fill: the chromosome header */
+        const nchrom *c = &J->n->chroms[J->side][f->pgap->pidx];
+        fprintf(w->f, "net %s %d\n", c->name, c->size);
+    }
+    if (!J->reached[i])
+        return;
+    put_fill_line(w, f, 2 * f->level + 1, J->score[i], J->sub[i]);
+    const nfill *cur = f;
+    int g0 = 0;
+    for (;;) {
+        for (int gi = g0; gi < cur->n_gaps; ++gi) {
+            const ngap *g = cur->gaps[gi];
+            put_gap_line(w, cur, g, 2 * cur->level + 2);
+            if (gap_prints_fill(J, g))
+                return; /* the next line is that fill's */
+        }
+        /* cur's subtree is done: its next printed sibling, or up */
+        if (J->more[cur->ord])
+            return;
+        const ngap *pg = cur->pgap;
+        if (!pg->pfill)
+            return; /* end of the chromosome */
+        g0 = pg->pidx + 1;
+        cur = pg->pfill;
+    }
+}
 
 static void write_run(FILE *f, int64_t r, void *arg) {
     wjob *J = arg;
     const int64_t a = r * J->per;
-    const int64_t b = a + J->per < J->n_items ? a + J->per : J->n_items;
+    const int64_t b = a + J->per < J->nf ? a + J->per : J->nf;
     wctx w = {J->n, f, J->side, J->tscore, 0, NULL};
-    for (int64_t i = a; i < b; ++i) {
-        const nchrom *c = &J->n->chroms[J->side][J->items[i].chrom];
-        if (J->items[i].fill == 0)
-            fprintf(f, "net %s %d\n", c->name, c->size);
-        w.depth = 0;
-        out_fill(&w, c->root->fills[J->items[i].fill]);
+    for (int64_t i = a; i < b; ++i)
+        write_segment(J, &w, i);
+}
+
+/* per-fill score / print flags (parallel over the pre-order list) */
+static void *winfo_thread(void *arg) {
+    wjob *J = arg;
+    for (;;) {
+        const int64_t a = atomic_fetch_add(&J->next, 4096);
+        if (a >= J->nf)
+            break;
+        const int64_t b = a + 4096 < J->nf ? a + 4096 : J->nf;
+        for (int64_t i = a; i < b; ++i)
+            J->show[i] = (uint8_t)fill_info(J->n, J->side, J->tscore, J->ord[i], &J->score[i],
+                                            &J->sub[i]);
     }
+    return NULL;
+}
+
+/* "more" flags: every gap's fills, last to first */
+static void mark_more(wjob *J, const ngap *g) {
+    uint8_t any = 0;
+    for (int k = g->n_fills - 1; k >= 0; --k) {
+        const int64_t o = g->fills[k]->ord;
+        J->more[o] = any;
+        any |= J->show[o];
+    }
+}
+
+static void *wmore_thread(void *arg) {
+    wjob *J = arg;
+    for (;;) {
+        const int64_t a = atomic_fetch_add(&J->next, 4096);
+        if (a >= J->nf)
+            break;
+        const int64_t b = a + 4096 < J->nf ? a + 4096 : J->nf;
+        for (int64_t i = a; i < b; ++i) {
+            const nfill *f = J->ord[i];
+            for (int k = 0; k < f->n_gaps; ++k)
+                mark_more(J, f->gaps[k]);
+        }
+    }
+    return NULL;
 }
 
 int gac_net_write(const gac_net *n, int side, const int64_t *tscores, const char *path,
@@ -1503,26 +1595,42 @@ int gac_net_write(const gac_net *n, int side, const int64_t *tscores, const char
     }
     for (int32_t i = 0; i < n_meta; ++i)
         fprintf(f, "%s\n", meta[i]);
-    int64_t ni = 0;
-    for (int32_t k = 0; k < n->n_chroms[side]; ++k) {
-        const nchrom *c = &n->chroms[side][k];
-        if (c->root->fill_head)
-            ni += c->root->n_fills;
-    }
-    witem *items = malloc((size_t)(ni ? ni : 1) * sizeof(witem));
-    ni = 0;
-    for (int32_t k = 0; k < n->n_chroms[side]; ++k) {
-        const nchrom *c = &n->chroms[side][k];
-        if (c->root->fill_head)
-            for (int i = 0; i < c->root->n_fills; ++i)
-                items[ni++] = (witem){k, i};
-    }
+    const int64_t nf = n->n_order[side];
+    wjob J;
+    memset(&J, 0, sizeof(J));
+    J.n = n;
+    J.side = side;
+    J.tscore = side == GAC_T ? tscores : NULL;
+    J.ord = (const nfill *const *)n->order[side];
+    J.nf = nf;
+    const size_t m = (size_t)(nf ? nf : 1);
+    J.score = malloc(m * sizeof(double));
+    J.sub = malloc(m * sizeof(int32_t));
+    J.show = malloc(m);
+    J.more = malloc(m);
+    J.reached = malloc(m);
     const int nt = gac_host_threads();
-    int64_t per = ni / (64 * (int64_t)nt) + 1;
-    const int64_t nr = (ni + per - 1) / per;
-    wjob J = {n, side, side == GAC_T ? tscores : NULL, items, ni, per};
+    atomic_init(&J.next, 0);
+    gac_run_threads(nt, winfo_thread, &J);
+    atomic_store(&J.next, 0);
+    gac_run_threads(nt, wmore_thread, &J);
+    for (int32_t k = 0; k < n->n_chroms[side]; ++k) {
+        const nchrom *c = &n->chroms[side][k];
+        if (c->root && c->root->fill_head)
+            mark_more(&J, c->root);
+    }
+    for (int64_t i = 0; i < nf; ++i) { /* parents precede children */
+        const nfill *f = J.ord[i];
+        J.reached[i] = J.show[i] && (!f->pgap->pfill || J.reached[f->pgap->pfill->ord]);
+    }
+    J.per = nf / (64 * (int64_t)nt) + 1;
+    const int64_t nr = (nf + J.per - 1) / J.per;
     int wbad = gac_par_output(f, nr, write_run, &J);
-    free(items);
+    free(J.score);
+    free(J.sub);
+    free(J.show);
+    free(J.more);
+    free(J.reached);
     int bad = ferror(f) || wbad;
     if (close_it) {
         if (fclose(f) != 0)
