@@ -944,6 +944,49 @@ void gt_parallel(int n, void *(*fn)(void *), void *args, size_t stride) {
     free(th);
 }
 
+/* copy of the chunks' arrays into the stitched set (disjoint ranges) */
+typedef struct stitch_job {
+    gt_chains *c;
+    chunk *K;
+    const int64_t *c0, *b0;
+    int32_t **tmaps, **qmaps;
+    int nk;
+    _Atomic int next;
+} stitch_job;
+
+static void *stitch_thread(void *arg) {
+    stitch_job *J = arg;
+    gt_chains *c = J->c;
+    for (;;) {
+        const int k = atomic_fetch_add(&J->next, 1);
+        if (k >= J->nk)
+            break;
+        const gt_chains *s = &J->K[k].c;
+        const int64_t take = s->n, o = J->c0[k], bo = J->b0[k];
+        const int32_t *tmap = J->tmaps[k], *qmap = J->qmaps[k];
+        for (int64_t i = 0; i < take; ++i) {
+            const int64_t j = o + i;
+            c->score[j] = s->score[i];
+            c->tname[j] = tmap[s->tname[i]];
+            c->tsize[j] = s->tsize[i];
+            c->tstart[j] = s->tstart[i];
+            c->tend[j] = s->tend[i];
+            c->qname[j] = qmap[s->qname[i]];
+            c->qsize[j] = s->qsize[i];
+            c->qstart[j] = s->qstart[i];
+            c->qend[j] = s->qend[i];
+            c->qstrand[j] = s->qstrand[i];
+            c->id[j] = s->id[i];
+            c->blk_off[j + 1] = bo + s->blk_off[i + 1];
+        }
+        const int64_t nb = J->b0[k + 1] - bo;
+        memcpy(c->bt + bo, s->bt, (size_t)nb * 4);
+        memcpy(c->bq + bo, s->bq, (size_t)nb * 4);
+        memcpy(c->bs + bo, s->bs, (size_t)nb * 4);
+    }
+    return NULL;
+}
+
 void gt_read_chains(const char *path, gt_chains *c, double stop_below, int keep_meta) {
     memset(c, 0, sizeof(*c));
     const int timing = getenv("GAC_TIMING") != NULL;
@@ -996,10 +1039,13 @@ void gt_read_chains(const char *path, gt_chains *c, double stop_below, int keep_
     RC_LAP("count lines");
     gt_parallel(nk, parse_chunk, K, sizeof(chunk));
     RC_LAP("parse");
-    /* stitch in file order up to the first error or stop */
-    c->blk_off = malloc(8);
-    c->blk_off[0] = 0;
+    /* stitch in file order up to the first error or stop: a serial pass for
+     * everything order-dependent (names, ids, metadata, errors, offsets),
+     * then the chunks' arrays are copied in parallel */
+    int64_t *c0 = calloc((size_t)nk + 1, 8), *b0 = calloc((size_t)nk + 1, 8);
+    int32_t **tmaps = calloc((size_t)nk, sizeof(int32_t *)), **qmaps = calloc((size_t)nk, sizeof(int32_t *));
     int64_t line0 = 0;
+    int nuse = 0;
     for (int k = 0; k < nk; ++k) {
         chunk *ch = &K[k];
         const int64_t take = ch->stop >= 0 ? ch->stop : ch->c.n; /* the stop chain is dropped */
@@ -1013,43 +1059,17 @@ void gt_read_chains(const char *path, gt_chains *c, double stop_below, int keep_
             tmap[i] = gt_names_add(&c->tnames, ch->c.tnames.names[i], strlen(ch->c.tnames.names[i]));
         for (int32_t i = 0; i < ch->c.qnames.n; ++i)
             qmap[i] = gt_names_add(&c->qnames, ch->c.qnames.names[i], strlen(ch->c.qnames.names[i]));
+        tmaps[k] = tmap;
+        qmaps[k] = qmap;
         /* ids: every header read so far consumes chainIdNext, kept or not */
         const int64_t nread = ch->c.n;
         for (int64_t i = 0; i < nread; ++i)
             if (ch->c.id[i] == INT32_MIN)
                 ch->c.id[i] = g_next_id++;
-        if (take > 0) {
-            const int64_t nb = ch->c.blk_off[take];
-            chains_reserve_n(c, c->n + take + 1);
-            for (int64_t i = 0; i < take; ++i) {
-                const int64_t j = c->n + i;
-                c->score[j] = ch->c.score[i];
-                c->tname[j] = tmap[ch->c.tname[i]];
-                c->tsize[j] = ch->c.tsize[i];
-                c->tstart[j] = ch->c.tstart[i];
-                c->tend[j] = ch->c.tend[i];
-                c->qname[j] = qmap[ch->c.qname[i]];
-                c->qsize[j] = ch->c.qsize[i];
-                c->qstart[j] = ch->c.qstart[i];
-                c->qend[j] = ch->c.qend[i];
-                c->qstrand[j] = ch->c.qstrand[i];
-                c->id[j] = ch->c.id[i];
-                c->blk_off[j + 1] = c->nb + ch->c.blk_off[i + 1];
-            }
-            c->n += take;
-            if (c->nb + nb + 1 > c->bcap) {
-                c->bcap = c->nb + nb + 1;
-                c->bt = realloc(c->bt, c->bcap * 4);
-                c->bq = realloc(c->bq, c->bcap * 4);
-                c->bs = realloc(c->bs, c->bcap * 4);
-            }
-            memcpy(c->bt + c->nb, ch->c.bt, (size_t)nb * 4);
-            memcpy(c->bq + c->nb, ch->c.bq, (size_t)nb * 4);
-            memcpy(c->bs + c->nb, ch->c.bs, (size_t)nb * 4);
-            c->nb += nb;
-        }
-        free(tmap);
-        free(qmap);
+        ch->c.n = take; /* chains to copy */
+        c0[k + 1] = c0[k] + take;
+        b0[k + 1] = b0[k] + (take > 0 ? ch->c.blk_off[take] : 0);
+        nuse = k + 1;
         const int err = ch->f.err && ch->stop < 0;
         if (err) {
             char msg[2048];
@@ -1073,6 +1093,25 @@ void gt_read_chains(const char *path, gt_chains *c, double stop_below, int keep_
         if (ch->stop >= 0)
             break;
     }
+    chains_reserve_n(c, c0[nuse] + 1);
+    c->blk_off[0] = 0;
+    c->bcap = b0[nuse] + 1;
+    c->bt = malloc((size_t)c->bcap * 4);
+    c->bq = malloc((size_t)c->bcap * 4);
+    c->bs = malloc((size_t)c->bcap * 4);
+    stitch_job SJ = {c, K, c0, b0, tmaps, qmaps, nuse, 0};
+    atomic_init(&SJ.next, 0);
+    gac_run_threads(nuse < gt_threads() ? nuse : gt_threads(), stitch_thread, &SJ);
+    c->n = c0[nuse];
+    c->nb = b0[nuse];
+    for (int k = 0; k < nuse; ++k) {
+        free(tmaps[k]);
+        free(qmaps[k]);
+    }
+    free(tmaps);
+    free(qmaps);
+    free(c0);
+    free(b0);
     RC_LAP("stitch");
     for (int k = 0; k < nk; ++k)
         gt_chains_free(&K[k].c);
