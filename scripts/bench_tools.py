@@ -36,7 +36,13 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def timed(cmd, cwd=None, env=None, timeout=3000):
+def timed(cmd, cwd=None, env=None, timeout=3000, outputs=()):
+    # outputs are removed first: overwriting a file truncates it, and some
+    # filesystems (ext4 auto_da_alloc) flush a truncated-and-rewritten file
+    # on close, which would time the disk instead of the tool
+    for o in outputs:
+        if os.path.exists(o):
+            os.remove(o)
     t = time.time()
     r = subprocess.run(cmd, capture_output=True, text=True, cwd=cwd, env=env, timeout=timeout)
     dt = time.time() - t
@@ -68,14 +74,14 @@ def axtchain(a):
     args = ["-psl", psl, os.path.join(d, "t.2bit"), os.path.join(d, "q.2bit")]
     ours = os.path.join(d, "ours.chain")
     t_ours, r = timed([os.path.join(BIN, "axtChain"), "-linearGap=loose", "-verbose=0"] + args +
-                      [ours], env=env)
+                      [ours], env=env, outputs=[ours])
     log(r.stderr)
     res = {"tool": "axtChain", "blocks": a.blocks, "seed": a.seed, "ours_s": round(t_ours, 3),
            "ours_sha": sha(ours), "timing": [l for l in r.stderr.splitlines() if "gac_axt" in l]}
     refbin = os.path.join(REF, "axtChain")
     if os.path.exists(refbin) and not a.no_ref:
         ref = os.path.join(d, "ref.chain")
-        t_ref, _ = timed([refbin, "-linearGap=loose", "-verbose=0"] + args + [ref])
+        t_ref, _ = timed([refbin, "-linearGap=loose", "-verbose=0"] + args + [ref], outputs=[ref])
         res.update(ref_s=round(t_ref, 3), ref_cores=1, identical=filecmp.cmp(ours, ref, False),
                    speedup=round(t_ref / t_ours, 2))
     res["chains"] = sum(1 for line in open(ours) if line.startswith("chain"))
@@ -110,7 +116,7 @@ def cleaner(a):
     t_ours, r = timed([os.path.join(BIN, "chainCleaner"), inc, p("t.2bit"), p("q.2bit"),
                        p("ours.chain"), p("ours.bed"), f"-tSizes={p('t.sizes')}",
                        f"-qSizes={p('q.sizes')}", "-linearGap=loose", "-verbose=1"], cwd=d,
-                      env=dict(os.environ, GAC_TIMING="1"))
+                      env=dict(os.environ, GAC_TIMING="1"), outputs=[p("ours.chain"), p("ours.bed")])
     res = {"tool": "chainCleaner", "loci": a.loci, "seed": a.seed, "ours_s": round(t_ours, 3),
            "removed": sum(1 for _ in open(p("ours.bed"))),
            "gpu": [l for l in r.stderr.splitlines() if l.startswith("GPU:")],
@@ -134,7 +140,8 @@ def cleaner(a):
                 f.write(net.stdout)
             t_ref, _ = timed([os.path.join(REF, "chainCleaner"), inc, p("t.2bit"), p("q.2bit"),
                               p("ref.chain"), p("ref.bed"), f"-net={p('ref.net')}",
-                              "-linearGap=loose", "-verbose=0"], cwd=d, env=env)
+                              "-linearGap=loose", "-verbose=0"], cwd=d, env=env,
+                             outputs=[p("ref.chain"), p("ref.bed")])
             res.update(ref_s=round(t_net + t_filter + t_ref, 3), ref_net_s=round(t_net, 3),
                        ref_filter_s=round(t_filter, 3), ref_clean_s=round(t_ref, 3), ref_cores=1,
                        identical=filecmp.cmp(p("ours.chain"), p("ref.chain"), False)
@@ -167,12 +174,14 @@ def scorechain(a):
     p = lambda x: os.path.join(d, x)
     args = [p("in.chain"), p("t.2bit"), p("q.2bit")]
     t_ours, r = timed([os.path.join(BIN, "scoreChain")] + args + [p("ours.chain"), "-linearGap=loose",
-                                                                  "-verbose=2"])
+                                                                  "-verbose=2"],
+                      outputs=[p("ours.chain")])
     res = {"tool": "scoreChain", "chains": a.chains, "seed": a.seed, "ours_s": round(t_ours, 3),
            "stages": [l for l in r.stderr.splitlines() if "[stage]" in l]}
     if os.path.exists(os.path.join(REF, "scoreChain")) and not a.no_ref:
         t_ref, _ = timed([os.path.join(REF, "scoreChain")] + args + [p("ref.chain"),
-                                                                     "-linearGap=loose"])
+                                                                     "-linearGap=loose"],
+                         outputs=[p("ref.chain")])
         res.update(ref_s=round(t_ref, 3), ref_cores=1, speedup=round(t_ref / t_ours, 2),
                    identical=filecmp.cmp(p("ours.chain"), p("ref.chain"), False))
     print(json.dumps(res), flush=True)
@@ -184,13 +193,13 @@ def chainnet(a):
     args = [p("in.chain"), p("t.sizes"), p("q.sizes")]
     opts = ["-rescore", f"-tNibDir={p('t.2bit')}", f"-qNibDir={p('q.2bit')}", "-linearGap=loose"]
     t_ours, r = timed([os.path.join(BIN, "chainNet")] + args + [p("ours.t.net"), p("ours.q.net")] +
-                      opts + ["-verbose=2"])
+                      opts + ["-verbose=2"], outputs=[p("ours.t.net"), p("ours.q.net")])
     res = {"tool": "chainNet -rescore", "chains": a.chains, "seed": a.seed,
            "ours_s": round(t_ours, 3),
            "stages": [l for l in r.stderr.splitlines() if "[stage]" in l]}
     if os.path.exists(os.path.join(REF, "chainNet")) and not a.no_ref:
         t_ref, _ = timed([os.path.join(REF, "chainNet")] + args + [p("ref.t.net"), p("ref.q.net")] +
-                         opts)
+                         opts, outputs=[p("ref.t.net"), p("ref.q.net")])
         res.update(ref_s=round(t_ref, 3), ref_cores=1, speedup=round(t_ref / t_ours, 2),
                    identical=filecmp.cmp(p("ours.t.net"), p("ref.t.net"), False)
                    and filecmp.cmp(p("ours.q.net"), p("ref.q.net"), False))
@@ -243,11 +252,12 @@ def c5(a):
            "gen_s": round(gen_s, 1)}
     sc_args = [p("in.chain"), p("t.2bit"), p("q.2bit")]
     t1, r1 = timed([os.path.join(BIN, "scoreChain")] + sc_args + [p("ours.sc.chain"),
-                                                                   "-linearGap=loose", "-verbose=2"])
+                                                                   "-linearGap=loose", "-verbose=2"],
+                   outputs=[p("ours.sc.chain")])
     cn_args = [p("in.chain"), p("t.sizes"), p("q.sizes")]
     opts = ["-rescore", f"-tNibDir={p('t.2bit')}", f"-qNibDir={p('q.2bit')}", "-linearGap=loose"]
     t2, r2 = timed([os.path.join(BIN, "chainNet")] + cn_args + [p("ours.t.net"), p("ours.q.net")] +
-                   opts + ["-verbose=2"])
+                   opts + ["-verbose=2"], outputs=[p("ours.t.net"), p("ours.q.net")])
     res.update(ours_scorechain_s=round(t1, 3), ours_chainnet_s=round(t2, 3),
                ours_s=round(t1 + t2, 3),
                ours_stages=[l for l in (r1.stderr + r2.stderr).splitlines() if "[stage]" in l],
@@ -255,10 +265,11 @@ def c5(a):
     log(f"ours: scoreChain {t1:.2f}s chainNet {t2:.2f}s")
     if os.path.exists(os.path.join(REF, "chainNet")) and not a.no_ref:
         t3, _ = timed([os.path.join(REF, "scoreChain")] + sc_args + [p("ref.sc.chain"),
-                                                                      "-linearGap=loose"])
+                                                                      "-linearGap=loose"],
+                      outputs=[p("ref.sc.chain")])
         log(f"ref scoreChain {t3:.2f}s")
         t4, _ = timed([os.path.join(REF, "chainNet")] + cn_args + [p("ref.t.net"), p("ref.q.net")] +
-                      opts)
+                      opts, outputs=[p("ref.t.net"), p("ref.q.net")])
         log(f"ref chainNet {t4:.2f}s")
         res.update(ref_scorechain_s=round(t3, 3), ref_chainnet_s=round(t4, 3),
                    ref_s=round(t3 + t4, 3), ref_cores=1, speedup=round((t3 + t4) / (t1 + t2), 2),
