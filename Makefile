@@ -25,7 +25,14 @@ HIP_SRC  := $(CSRC)/gac_kernels.hip $(CSRC)/gac_device.hip
 HIP_OBJ  := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRC))
 HDRS     := include/gachain.h $(CSRC)/gac_kernels.h $(wildcard $(CSRC)/host/*.h)
 
-TOOLS    := $(patsubst $(CSRC)/tools/%.c,$(BINDIR)/%,$(wildcard $(CSRC)/tools/*.c))
+EXECDIR  := $(PKG)/libexec
+# GPU tools: the binary lives in libexec/, bin/<tool> is a 2-line sh launcher
+# that turns on transparent huge pages for malloc (glibc.malloc.hugetlb=1:
+# fewer page faults on the GB-scale chain/net arrays) and execs it -- before
+# anything touches the GPU.  NetFilterNonNested.perl is host-only: in bin/.
+GPU_TOOLS := scoreChain chainNet chainCleaner axtChain
+TOOLS    := $(addprefix $(EXECDIR)/,$(GPU_TOOLS)) $(addprefix $(BINDIR)/,$(GPU_TOOLS)) \
+            $(BINDIR)/NetFilterNonNested.perl
 TOOL_LIB_SRC := $(wildcard $(CSRC)/tools/lib/*.c)
 TOOL_LIB_OBJ := $(patsubst $(CSRC)/tools/lib/%.c,$(OBJDIR)/tools/lib/%.o,$(TOOL_LIB_SRC))
 
@@ -47,10 +54,20 @@ $(OBJDIR)/tools/lib/%.o: $(CSRC)/tools/lib/%.c $(HDRS) $(wildcard $(CSRC)/tools/
 	@mkdir -p $(dir $@)
 	$(CC) $(CFLAGS) -I$(CSRC)/tools/lib -c $< -o $@
 
-$(BINDIR)/%: $(CSRC)/tools/%.c $(TOOL_LIB_OBJ) $(LIBDIR)/libgachain.so $(HDRS)
+$(EXECDIR)/%: $(CSRC)/tools/%.c $(TOOL_LIB_OBJ) $(LIBDIR)/libgachain.so $(HDRS)
+	@mkdir -p $(EXECDIR)
+	$(CC) $(CFLAGS) -I$(CSRC)/tools/lib $< $(TOOL_LIB_OBJ) -o $@ -L$(LIBDIR) -lgachain \
+	    -Wl,-rpath,'$$ORIGIN/../lib' -lz -lm -lpthread
+
+$(BINDIR)/NetFilterNonNested.perl: $(CSRC)/tools/NetFilterNonNested.perl.c $(TOOL_LIB_OBJ) $(LIBDIR)/libgachain.so $(HDRS)
 	@mkdir -p $(BINDIR)
 	$(CC) $(CFLAGS) -I$(CSRC)/tools/lib $< $(TOOL_LIB_OBJ) -o $@ -L$(LIBDIR) -lgachain \
 	    -Wl,-rpath,'$$ORIGIN/../lib' -lz -lm -lpthread
+
+$(BINDIR)/%: $(EXECDIR)/%
+	@mkdir -p $(BINDIR)
+	printf '#!/bin/sh\np=$$(readlink -f "$$0")\nGLIBC_TUNABLES="glibc.malloc.hugetlb=1$${GLIBC_TUNABLES:+:$$GLIBC_TUNABLES}" exec "$${p%%/*}/../libexec/%s" "$$@"\n' $* > $@
+	chmod +x $@
 
 oracle: oracle/_build/libgacoracle.so
 
@@ -62,7 +79,7 @@ ref:
 	$(MAKE) -f oracle/ref.mk -j8
 
 clean:
-	rm -rf build $(LIBDIR) $(BINDIR) oracle/_build
+	rm -rf build $(LIBDIR) $(BINDIR) $(EXECDIR) oracle/_build
 
 .PHONY: all oracle ref clean
 
