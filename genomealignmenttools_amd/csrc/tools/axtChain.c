@@ -49,7 +49,9 @@ static void usage(int min_score) {
         "              loose is chicken/human linear gap costs.\n"
         "              medium is mouse/human linear gap costs.\n"
         "              Or specify a piecewise linearGap tab delimited file.\n"
-        "   (this build reads .2bit genomes, or fasta with -faQ/-faT; not nib directories)\n",
+        "   (this build reads .2bit genomes, or fasta with -faQ/-faT; not nib directories)\n"
+        "batch (this build): axtChain -jobs=FILE runs every line of FILE as one axtChain\n"
+        "   command line (arguments only) in one process and one GPU context\n",
         min_score);
 }
 
@@ -585,7 +587,50 @@ static double wall(void) {
 }
 
 /* ------------------------------------------------------------ main */
-int main(int argc, char *argv[]) {
+/* -jobs=FILE: many chaining jobs in one process (SURVEY §8(f) item 4:
+ * RepeatFiller's thousands of small axtChain runs) -- one device context,
+ * genomes kept loaded while consecutive jobs name the same files */
+typedef struct ax_batch {
+    int on;
+    gac_ctx *ctx;
+    char *tpath, *qpath; /* genomes loaded in ctx */
+    int tfa, qfa;
+} ax_batch;
+
+static void batch_genomes(ax_batch *B, const char *tnib, const char *qnib, int fa_t, int fa_q) {
+    if (B->ctx && B->tpath && B->qpath && strcmp(B->tpath, tnib) == 0 && strcmp(B->qpath, qnib) == 0 &&
+        B->tfa == fa_t && B->qfa == fa_q)
+        return;
+    if (B->ctx) /* other genomes: a fresh context (the runtime stays initialised) */
+        gac_close(B->ctx);
+    B->ctx = NULL;
+    free(B->tpath);
+    free(B->qpath);
+    B->tpath = B->qpath = NULL;
+    gt_check(gac_open(0, &B->ctx));
+    if (fa_t) {
+        load_fasta(B->ctx, GAC_T, tnib);
+    } else {
+        if (!gac_is_twobit_file(tnib))
+            gt_abort("given tNibDir argument: '%s' is not a 2bit file (nib directories are not supported)\n",
+                     tnib);
+        gt_check(gac_genome_load_2bit(B->ctx, GAC_T, tnib));
+    }
+    if (fa_q) {
+        load_fasta(B->ctx, GAC_Q, qnib);
+    } else {
+        if (!gac_is_twobit_file(qnib))
+            gt_abort("given qNibDir argument: '%s' is not a 2bit file (nib directories are not supported)\n",
+                     qnib);
+        gt_check(gac_genome_load_2bit(B->ctx, GAC_Q, qnib));
+    }
+    B->tpath = strdup(tnib);
+    B->qpath = strdup(qnib);
+    B->tfa = fa_t;
+    B->qfa = fa_q;
+}
+
+static void run_job(int argc, char *argv[], ax_batch *B) {
     gt_options_hash(&argc, argv);
     int min_score = gt_opt_int("minScore", 1000);
     const char *details = gt_opt_str("details", NULL);
@@ -627,7 +672,8 @@ int main(int argc, char *argv[]) {
      * alignments are read (scoring is set later, by gac_axt_chain) */
     gt_device dev;
     memset(&dev, 0, sizeof(dev));
-    const int early_dev = !fa_t && !fa_q && gac_is_twobit_file(tnib) && gac_is_twobit_file(qnib);
+    const int early_dev =
+        !B->on && !fa_t && !fa_q && gac_is_twobit_file(tnib) && gac_is_twobit_file(qnib);
     if (early_dev)
         gt_device_start(&dev, tnib, qnib, NULL, NULL);
     double t0 = wall();
@@ -648,7 +694,10 @@ int main(int argc, char *argv[]) {
     gt_verbose(2, "read %d pairs from %s in %.3f s\n", P.n, in, wall() - t0);
     t0 = wall();
     gac_ctx *ctx = NULL;
-    if (early_dev) {
+    if (B->on) {
+        batch_genomes(B, tnib, qnib, fa_t, fa_q);
+        ctx = B->ctx;
+    } else if (early_dev) {
         ctx = gt_device_join(&dev);
     } else {
         gt_check(gac_open(0, &ctx));
@@ -719,6 +768,73 @@ int main(int argc, char *argv[]) {
     gt_verbose(2, "chaining + writing in %.3f s\n", wall() - t0);
     gt_verbose(2, "%lld pairs, %lld blocks, %lld chains\n", (long long)np, (long long)nb,
                (long long)ch->n_chains);
-    gac_close(ctx); /* host arrays are left to process exit */
+    if (!B->on) {
+        gac_close(ctx); /* host arrays are left to process exit */
+        gt_exit_ok();
+    }
+    /* batch: this job's arrays go now */
+    gac_axt_chains_free(ch);
+    for (int32_t i = 0; i < P.n; ++i) {
+        free(P.p[i].bt);
+        free(P.p[i].bq);
+        free(P.p[i].bs);
+        free(P.p[i].qname);
+        free(P.p[i].tname);
+    }
+    free(P.p);
+    gt_names_free(&P.keys);
+    free(ord);
+    free(tseq);
+    free(qseq);
+    free(strand);
+    free(boff);
+    free(bt);
+    free(bq);
+    free(bs);
+    gac_gapcalc_free(gap);
+    free(extra);
+}
+
+int main(int argc, char *argv[]) {
+    const char *jobs = NULL;
+    for (int i = 1; i < argc; ++i)
+        if (strncmp(argv[i], "-jobs=", 6) == 0)
+            jobs = argv[i] + 6;
+    ax_batch B;
+    memset(&B, 0, sizeof(B));
+    if (!jobs) {
+        run_job(argc, argv, &B); /* exits */
+        return 0;
+    }
+    /* one job per line: the arguments of one axtChain run (whitespace
+     * separated, no quoting); blank and '#' lines are skipped; the first
+     * failing job stops the batch with that job's error and exit status */
+    gt_options_hash(&argc, argv);
+    if (argc != 1)
+        gt_abort("axtChain -jobs=FILE takes no other arguments (put them in FILE, one run per line)\n");
+    B.on = 1;
+    size_t len;
+    char *text = gt_slurp(jobs, &len);
+    int64_t njobs = 0;
+    for (char *line = text, *nl; line && *line; line = nl ? nl + 1 : NULL) {
+        nl = strchr(line, '\n');
+        if (nl)
+            *nl = 0;
+        char *w[256];
+        const int wc = gac_chop_white(line, w, 255);
+        if (wc == 0 || w[0][0] == '#')
+            continue;
+        char *jargv[257];
+        jargv[0] = argv[0];
+        for (int i = 0; i < wc; ++i)
+            jargv[i + 1] = w[i];
+        jargv[wc + 1] = NULL;
+        gt_options_reset();
+        run_job(wc + 1, jargv, &B);
+        ++njobs;
+    }
+    gt_verbose(2, "%lld jobs in one device context\n", (long long)njobs);
+    if (B.ctx)
+        gac_close(B.ctx);
     gt_exit_ok();
 }

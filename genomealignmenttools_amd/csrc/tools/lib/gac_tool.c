@@ -318,6 +318,14 @@ void gt_options(int *argc, char **argv, const gt_spec *spec) {
     g_verbose = gt_opt_int("verbose", 1);
 }
 
+void gt_options_reset(void) {
+    for (int i = 0; i < g_nopts; ++i) {
+        free(g_opts[i].name);
+        free(g_opts[i].val);
+    }
+    g_nopts = 0;
+}
+
 void gt_options_hash(int *argc, char **argv) {
     g_any_option = 1;
     gt_options(argc, argv, NULL);

@@ -71,6 +71,8 @@ void gt_options(int *argc, char **argv, const gt_spec *spec);
 /* optionHash (kent/src/lib/options.c:200-214): the same parsing, but any
  * option name is accepted (axtChain) */
 void gt_options_hash(int *argc, char **argv);
+/* forget the parsed options (a batch parses one command line per job) */
+void gt_options_reset(void);
 const char *gt_opt_str(const char *name, const char *def);
 int gt_opt_exists(const char *name);
 int gt_opt_int(const char *name, int def);

@@ -279,9 +279,51 @@ def c5(a):
     print(json.dumps(res), flush=True)
 
 
+def microjobs(a):
+    """RepeatFiller-style micro-jobs: --jobs small
+    axtChain runs (the reference's chrM known-answer alignment, each to its
+    own output), as separate processes of the reference, separate processes
+    of ours, and one `axtChain -jobs=FILE` batch; all outputs compared."""
+    g = os.path.join(REPO, "tests", "golden", "chrM")
+    d = os.path.join(a.tmp, "microjobs")
+    os.makedirs(d, exist_ok=True)
+    args = lambda out: ["-psl", os.path.join(g, "newStyleLastz.psl"), "-minScore=3000",
+                        "-linearGap=loose", os.path.join(g, "hg19.chrM.2bit"),
+                        "-scoreScheme=" + os.path.join(g, "newStyleLastz.Q.txt"),
+                        os.path.join(g, "susScr3.chrM.2bit"), out]
+    outs = lambda tag: [os.path.join(d, f"{tag}{i}.chain") for i in range(a.jobs)]
+    res = {"tool": "axtChain micro-jobs", "jobs": a.jobs, "blocks_per_job": 0}
+    t = time.time()
+    for o in outs("sep"):
+        timed([os.path.join(BIN, "axtChain")] + args(o), outputs=[o])
+    res["ours_separate_s"] = round(time.time() - t, 3)
+    jobs = os.path.join(d, "jobs.txt")
+    with open(jobs, "w") as f:
+        for o in outs("bat"):
+            f.write(" ".join(args(o)) + "\n")
+    t_b, _ = timed([os.path.join(BIN, "axtChain"), f"-jobs={jobs}"], outputs=outs("bat"))
+    res["ours_batch_s"] = round(t_b, 3)
+    want = os.path.join(g, "newStyleLastz.chain")
+    same = all(filecmp.cmp(o, want, False) for o in outs("sep") + outs("bat"))
+    refbin = os.path.join(REF, "axtChain")
+    if os.path.exists(refbin) and not a.no_ref:
+        t = time.time()
+        for o in outs("ref"):
+            timed([refbin] + args(o), outputs=[o])
+        res["ref_separate_s"] = round(time.time() - t, 3)
+        same = same and all(filecmp.cmp(o, want, False) for o in outs("ref"))
+        res["speedup_batch_vs_ref"] = round(res["ref_separate_s"] / t_b, 2)
+    res["identical"] = same
+    with open(os.path.join(g, "newStyleLastz.psl")) as f:
+        res["blocks_per_job"] = sum(int(l.split()[17]) for l in f if l[:1].isdigit())
+    print(json.dumps(res), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("tool", choices=["axtchain", "cleaner", "scorechain", "chainnet", "c5"])
+    ap.add_argument("tool", choices=["axtchain", "cleaner", "scorechain", "chainnet", "c5",
+                                     "microjobs"])
+    ap.add_argument("--jobs", type=int, default=200)
     ap.add_argument("--chains", type=int, default=200_000)
     ap.add_argument("--blocks", type=int, default=2_000_000)
     ap.add_argument("--tsize", type=int, default=60_000_000)
@@ -294,7 +336,7 @@ def main():
     if a.seed is None:
         a.seed = {"scorechain": 42, "chainnet": 42, "c5": 1234}.get(a.tool, 7)
     {"axtchain": axtchain, "cleaner": cleaner, "scorechain": scorechain,
-     "chainnet": chainnet, "c5": c5}[a.tool](a)
+     "chainnet": chainnet, "c5": c5, "microjobs": microjobs}[a.tool](a)
 
 
 if __name__ == "__main__":

@@ -201,3 +201,45 @@ def test_axtchain_synth(seed, case, tmp_path):
         if o.startswith("-details="):
             fn = o.split("=", 1)[1]
             assert filecmp.cmp(tmp_path / fn, os.path.join(d, fn), shallow=False)
+
+
+def test_axtchain_jobs_batch(tmp_path):
+    """axtChain -jobs=FILE: the two reference KATs and
+    the 8 synthetic cases as one batch -- genomes switch between jobs, one
+    device context -- every output identical to its golden file."""
+    g = GOLDEN
+    lines, expect = [], []
+    for c in ["newStyleLastz", "oldStyleBlastz"]:
+        out = tmp_path / f"kat_{c}.chain"
+        lines.append(f"-psl {g}/chrM/{c}.psl -minScore=3000 -linearGap=loose {g}/chrM/hg19.chrM.2bit "
+                     f"-scoreScheme={g}/chrM/{c}.Q.txt {g}/chrM/susScr3.chrM.2bit {out}")
+        expect.append((out, os.path.join(g, "chrM", f"{c}.chain")))
+    with open(os.path.join(g, "axtchain", "cases.json")) as f:
+        cases = json.load(f)
+    for seed in (5, 6):
+        d = os.path.join(g, "axtchain", f"s{seed}")
+        for case, opts in cases.items():
+            opts = [o.replace("../../chrM", os.path.join(g, "chrM")) for o in opts]
+            opts = [f"-details={tmp_path}/s{seed}.details" if o.startswith("-details=") else o
+                    for o in opts]
+            if any(o.startswith("-details=") for o in opts):
+                expect.append((tmp_path / f"s{seed}.details", os.path.join(d, "hoxd.details")))
+            inp = "in.psl" if "-psl" in opts else "in.axt.gz"
+            out = tmp_path / f"s{seed}_{case}.chain"
+            lines.append(" ".join(opts + [os.path.join(d, inp), os.path.join(d, "t.2bit"),
+                                          os.path.join(d, "q.2bit"), str(out)]))
+            expect.append((out, os.path.join(d, f"{case}.chain")))
+    jobs = tmp_path / "jobs.txt"
+    jobs.write_text("# one axtChain run per line\n\n" + "\n".join(lines) + "\n")
+    r = subprocess.run([_bin("axtChain"), f"-jobs={jobs}"], capture_output=True, text=True,
+                       timeout=600, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr
+    for got, want in expect:
+        assert filecmp.cmp(got, want, shallow=False), got
+    # a failing job stops the batch with the reference's error and status
+    bad = tmp_path / "bad.txt"
+    bad.write_text(lines[0] + "\n" + f"-linearGap=loose {tmp_path}/missing.axt "
+                   f"{g}/chrM/hg19.chrM.2bit {g}/chrM/susScr3.chrM.2bit {tmp_path}/x.chain\n")
+    r = subprocess.run([_bin("axtChain"), f"-jobs={bad}"], capture_output=True, text=True,
+                       timeout=600, cwd=tmp_path)
+    assert r.returncode == 255 and "missing.axt" in r.stderr
