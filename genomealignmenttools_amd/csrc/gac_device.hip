@@ -138,6 +138,8 @@ struct gac_ctx {
     Range *d_small_in = nullptr;     // their device addresses
     SmallOut *d_small_out = nullptr;
     int small_max = kSmallMax;       // batches up to this size take k_small (GAC_SMALL_MAX)
+    int32_t mat[16] = {0};           // the current scoring setup (gac_set_scoring)
+    gac_gapcalc *gap_src = nullptr;
     int32_t *h_stat = nullptr;   // pinned, coherent host words written by k_scan_agg [8]
     int32_t *d_h_stat = nullptr; // its device address
     int32_t call_seq = 0;
@@ -262,6 +264,7 @@ extern "C" void gac_close(gac_ctx *c) {
     }
     for (auto ev : c->prof_free) hipEventDestroy(ev);
     if (c->h_stat) hipHostFree(c->h_stat);
+    gac_gapcalc_free(c->gap_src);
     if (c->h_small_in) hipHostFree(c->h_small_in);
     if (c->h_small_out) hipHostFree(c->h_small_out);
     for (int k = 0; k < 2; ++k) {
@@ -289,6 +292,10 @@ extern "C" int gac_set_scoring(gac_ctx *c, const int32_t mat[16], const gac_gapc
     if (g->small_size < 1 || g->small_size != g->long_pos[0])
         return gac_fail(GAC_E_ARG, "inconsistent gap table (smallSize %d)", g->small_size);
     HIPCHK(hipSetDevice(c->device));
+    // the same setup again (a batch of jobs): tables, gap version and the
+    // chain sets' per-block gaps stay valid
+    if (c->scoring && memcmp(c->mat, mat, sizeof(c->mat)) == 0 && gac_gapcalc_same(c->gap_src, g))
+        return GAC_OK;
     // the kernel multiplies basis coefficients (|c| <= 16 max|s|) by counts
     // <= 32 in 24 bits (v_mad_i32_i24) and sums 16 terms in int32
     for (int i = 0; i < 16; ++i)
@@ -351,6 +358,9 @@ extern "C" int gac_set_scoring(gac_ctx *c, const int32_t mat[16], const gac_gapc
     HIPCHK(hipStreamSynchronize(c->stream));
     c->gap_len = (int)len;
     ++c->gap_version;
+    memcpy(c->mat, mat, sizeof(c->mat));
+    gac_gapcalc_free(c->gap_src);
+    c->gap_src = gac_gapcalc_clone(g);
     c->scoring = true;
     return GAC_OK;
 }

@@ -840,6 +840,11 @@ void gac_axt_chains_free(gac_axt_chains *c) {
     free(c);
 }
 
+/* host gap-cost table of the last gap setup (gac_axt_chain) */
+static pthread_mutex_t g_gtab_mu = PTHREAD_MUTEX_INITIALIZER;
+static gac_gapcalc *cached_g = NULL;
+static int32_t *cached_tab = NULL;
+
 int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
                   const gac_axt_input *in, double min_score, int n_threads,
                   const char *details_path, gac_axt_chains **out) {
@@ -927,14 +932,24 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
             for (int tc = 0; tc < 5; ++tc)
                 env.m5[qc * 5 + tc] =
                     (qc == 4 || tc == 4) ? 0 : mat[acgt_of_code[qc] * 4 + acgt_of_code[tc]];
-        int len = 1 << 15;
-        env.gtab_len = len;
-        env.gtab = malloc((size_t)3 * len * sizeof(int32_t));
-        for (int d = 0; d < len; ++d) {
-            env.gtab[d] = gac_gap_cost(g, d, 0);
-            env.gtab[len + d] = gac_gap_cost(g, 0, d);
-            env.gtab[2 * len + d] = d >= 2 ? gac_gap_cost(g, 1, d - 1) : gac_gap_cost(g, 0, 0);
+        /* kept across calls while the gap table is the same (-jobs
+         * batches); held locked until the DP that reads it is done */
+        const int len = 1 << 15;
+        pthread_mutex_lock(&g_gtab_mu);
+        if (!cached_g || !gac_gapcalc_same(cached_g, g)) {
+            int32_t *tab = malloc((size_t)3 * len * sizeof(int32_t));
+            for (int d = 0; d < len; ++d) {
+                tab[d] = gac_gap_cost(g, d, 0);
+                tab[len + d] = gac_gap_cost(g, 0, d);
+                tab[2 * len + d] = d >= 2 ? gac_gap_cost(g, 1, d - 1) : gac_gap_cost(g, 0, 0);
+            }
+            gac_gapcalc_free(cached_g);
+            free(cached_tab);
+            cached_g = gac_gapcalc_clone(g);
+            cached_tab = tab;
         }
+        env.gtab_len = len;
+        env.gtab = cached_tab;
     }
     stage("host gap table", &tclock);
     /* ---- chainBlocks + overlap removal per pair on host threads */
@@ -982,7 +997,7 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
                         "pair %lld (%lld blocks) %.3f s\n", nt, (long long)np, (long long)nb, sum,
                 (long long)imx, (long long)(poff[imx + 1] - poff[imx]), mx);
     }
-    free(env.gtab);
+    pthread_mutex_unlock(&g_gtab_mu);
     free(score);
     free(order);
     free(psize);

@@ -278,6 +278,45 @@ void gac_gapcalc_free(gac_gapcalc *g) {
     free(g);
 }
 
+int gac_gapcalc_same(const gac_gapcalc *a, const gac_gapcalc *b) {
+    if (a == b)
+        return 1;
+    if (!a || !b || a->small_size != b->small_size || a->long_count != b->long_count ||
+        a->q_last_pos != b->q_last_pos || a->t_last_pos != b->t_last_pos ||
+        a->b_last_pos != b->b_last_pos || a->q_last_val != b->q_last_val ||
+        a->t_last_val != b->t_last_val || a->b_last_val != b->b_last_val ||
+        a->q_last_slope != b->q_last_slope || a->t_last_slope != b->t_last_slope ||
+        a->b_last_slope != b->b_last_slope)
+        return 0;
+    const size_t ns = (size_t)a->small_size * 4, nl = (size_t)a->long_count;
+    return memcmp(a->q_small, b->q_small, ns) == 0 && memcmp(a->t_small, b->t_small, ns) == 0 &&
+           memcmp(a->b_small, b->b_small, ns) == 0 &&
+           memcmp(a->long_pos, b->long_pos, nl * 4) == 0 &&
+           memcmp(a->q_long, b->q_long, nl * 8) == 0 && memcmp(a->t_long, b->t_long, nl * 8) == 0 &&
+           memcmp(a->b_long, b->b_long, nl * 8) == 0;
+}
+
+static void *dup_mem(const void *p, size_t n) {
+    void *q = malloc(n ? n : 1);
+    if (n)
+        memcpy(q, p, n);
+    return q;
+}
+
+gac_gapcalc *gac_gapcalc_clone(const gac_gapcalc *g) {
+    gac_gapcalc *c = malloc(sizeof(*c));
+    *c = *g;
+    const size_t ns = (size_t)g->small_size * 4, nl = (size_t)g->long_count;
+    c->q_small = dup_mem(g->q_small, ns);
+    c->t_small = dup_mem(g->t_small, ns);
+    c->b_small = dup_mem(g->b_small, ns);
+    c->long_pos = dup_mem(g->long_pos, nl * 4);
+    c->q_long = dup_mem(g->q_long, nl * 8);
+    c->t_long = dup_mem(g->t_long, nl * 8);
+    c->b_long = dup_mem(g->b_long, nl * 8);
+    return c;
+}
+
 static int gc_parse(char *text, const char *name, gac_gapcalc **out) {
     gc_text t = {text, text, name, 0};
     int table_size = 0, small_size = 0, rc;

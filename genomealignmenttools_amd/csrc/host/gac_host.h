@@ -61,6 +61,10 @@ int gac_is_twobit_file(const char *path);
 
 /* ---- host threads: GAC_THREADS, else OMP_NUM_THREADS, else all cores (<= 64) */
 int gac_host_threads(void);
+/* gap tables with the same content (as gapCalcCost sees them) */
+int gac_gapcalc_same(const gac_gapcalc *a, const gac_gapcalc *b);
+/* deep copy, freed with gac_gapcalc_free */
+gac_gapcalc *gac_gapcalc_clone(const gac_gapcalc *g);
 /* fn(arg) on n threads (one of them the caller); fn pulls work itself */
 void gac_run_threads(int n, void *(*fn)(void *), void *arg);
 /* Ordered parallel output with formatting and writing overlapped: fn(f, r,
