@@ -23,7 +23,8 @@ class Net:
     """A built net (both sides).  Keeps the borrowed input arrays alive."""
 
     def __init__(self, ca, tsizes: Dict[str, int], qsizes: Dict[str, int], min_score: float,
-                 min_space: int = 25, min_fill: Optional[int] = None, incl_hap: bool = False):
+                 min_space: int = 25, min_fill: Optional[int] = None, incl_hap: bool = False,
+                 sides: int = (1 << GAC_T) | (1 << GAC_Q)):
         tnames = list(tsizes)
         qnames = list(qsizes)
         tix = {n: i for i, n in enumerate(tnames)}
@@ -63,7 +64,7 @@ class Net:
                       float(min_score), 1 if incl_hap else 0)
         self.opts = opt
         h = C.c_void_p()
-        check(lib().gac_net_build(C.byref(inp), C.byref(opt), C.byref(h)))
+        check(lib().gac_net_build_sides(C.byref(inp), C.byref(opt), sides, C.byref(h)))
         self.h = h
 
     @property

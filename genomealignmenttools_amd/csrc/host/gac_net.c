@@ -125,6 +125,7 @@ struct gac_net {
     /* pre-order fill index per side */
     nfill **order[2];
     int64_t n_order[2];
+    int sides; /* bit 1 << side: side netted */
 };
 
 /* ------------------------------------------------------------ space index */
@@ -954,13 +955,21 @@ static void *net_thread(void *arg) {
 }
 
 int gac_net_build(const gac_net_input *in, const gac_net_opts *opt, gac_net **out) {
+    return gac_net_build_sides(in, opt, (1 << GAC_T) | (1 << GAC_Q), out);
+}
+
+int gac_net_build_sides(const gac_net_input *in, const gac_net_opts *opt, int sides,
+                        gac_net **out) {
     gac_clear_error();
     if (!in || !opt || !out)
         return gac_fail(GAC_E_ARG, "gac_net_build: NULL argument");
+    if (sides <= 0 || (sides & ~((1 << GAC_T) | (1 << GAC_Q))))
+        return gac_fail(GAC_E_ARG, "gac_net_build_sides: bad side mask %d", sides);
     *out = NULL;
     gac_net *n = calloc(1, sizeof(*n));
     n->in = *in;
     n->opt = *opt;
+    n->sides = sides;
     n->n_w = gac_host_threads();
     n->w = calloc((size_t)n->n_w, sizeof(nwork));
     for (int k = 0; k < n->n_w; ++k) {
@@ -1027,12 +1036,14 @@ int gac_net_build(const gac_net_input *in, const gac_net_opts *opt, gac_net **ou
     net_job J;
     memset(&J, 0, sizeof(J));
     J.n = n;
-    J.ntask = nt + nq;
-    J.task = malloc((size_t)(J.ntask ? J.ntask : 1) * sizeof(net_task));
-    for (int32_t k = 0; k < nt; ++k)
-        J.task[k] = (net_task){GAC_T, k, tl + toff[k], toff[k + 1] - toff[k]};
-    for (int32_t k = 0; k < nq; ++k)
-        J.task[nt + k] = (net_task){GAC_Q, k, ql + qoff[k], qoff[k + 1] - qoff[k]};
+    J.task = malloc((size_t)(nt + nq ? nt + nq : 1) * sizeof(net_task));
+    J.ntask = 0;
+    if (sides & (1 << GAC_T))
+        for (int32_t k = 0; k < nt; ++k)
+            J.task[J.ntask++] = (net_task){GAC_T, k, tl + toff[k], toff[k + 1] - toff[k]};
+    if (sides & (1 << GAC_Q))
+        for (int32_t k = 0; k < nq; ++k)
+            J.task[J.ntask++] = (net_task){GAC_Q, k, ql + qoff[k], qoff[k + 1] - qoff[k]};
     qsort(J.task, (size_t)J.ntask, sizeof(net_task), net_task_cmp);
     atomic_init(&J.next, 0);
     atomic_init(&J.wid, 0);
@@ -1253,7 +1264,7 @@ static void *visible_thread(void *arg) {
             break;
         /* iterative DFS */
         const nchrom *c = &n->chroms[side][k];
-        if (!c->root->fill_head)
+        if (!c->root || !c->root->fill_head)
             continue;
         int64_t top = 0;
         for (int i = c->root->n_fills - 1; i >= 0; --i) {
@@ -1290,6 +1301,8 @@ int gac_net_get_fills(const gac_net *n, int side, int32_t *chain, int32_t *start
                       int32_t *ali, uint8_t *flags) {
     if (!n || (side != GAC_T && side != GAC_Q))
         return gac_fail(GAC_E_ARG, "gac_net_get_fills: bad argument");
+    if (!(n->sides & (1 << side)))
+        return gac_fail(GAC_E_STATE, "gac_net_get_fills: side %d was not netted", side);
     const int nt = gac_host_threads();
     const int64_t nf = n->n_order[side];
     gf_job J = {n, side, chain, start, end, ali, flags, nf / (8 * (int64_t)nt) + 1, 0};
@@ -1583,6 +1596,8 @@ int gac_net_write(const gac_net *n, int side, const int64_t *tscores, const char
                   const char *const *meta, int32_t n_meta) {
     if (!n || !path || (side != GAC_T && side != GAC_Q))
         return gac_fail(GAC_E_ARG, "gac_net_write: bad argument");
+    if (!(n->sides & (1 << side)))
+        return gac_fail(GAC_E_STATE, "gac_net_write: side %d was not netted", side);
     FILE *f;
     int close_it = 1;
     if (strcmp(path, "stdout") == 0) {

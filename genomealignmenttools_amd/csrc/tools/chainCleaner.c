@@ -1173,7 +1173,8 @@ static void net_in_process(const char *in_chain, const char *tsizes, const char 
     in.q_sizes = qs.size;
     const gac_net_opts opt = {25, 12, 0.0, 0}; /* chainNet defaults, -minScore=0 */
     gac_net *net = NULL;
-    gt_check(gac_net_build(&in, &opt, &net));
+    /* only the target net is used (the query net goes to /dev/null) */
+    gt_check(gac_net_build_sides(&in, &opt, 1 << GAC_T, &net));
     gt_check(gac_net_write(net, GAC_T, NULL, tmp, (const char *const *)c.meta, c.n_meta));
     gac_net_free(net);
     gt_lines raw;

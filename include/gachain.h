@@ -265,6 +265,13 @@ typedef struct gac_net_opts {
  * scores increase).  Chains on *_hap* / *_alt* queries are skipped unless
  * incl_hap. */
 int gac_net_build(const gac_net_input *in, const gac_net_opts *opts, gac_net **out);
+/* The same for the sides in `sides` only (bit 1 << GAC_T, bit 1 << GAC_Q):
+ * the two sides' trees are independent, so a caller that writes only the
+ * target net (chainCleaner's `chainNet ... stdout /dev/null`,
+ * src/chainCleaner/chainCleaner.c:1660) skips the query side.  Fill queries
+ * and writes of a side not built fail with GAC_E_STATE. */
+int gac_net_build_sides(const gac_net_input *in, const gac_net_opts *opts, int sides,
+                        gac_net **out);
 void gac_net_free(gac_net *net);
 /* number of input chains consumed (netted or skipped) before stopping */
 int64_t gac_net_netted(const gac_net *net);

@@ -103,6 +103,23 @@ def test_netting_engine_vs_reference(seed, tmp_path):
     assert filecmp.cmp(tmp_path / "q2.net", os.path.join(d, "plain.q.net"), shallow=False)
 
 
+def test_netting_target_side_only(tmp_path):
+    """gac_net_build_sides with the target side only (chainCleaner's
+    self-netting): the same target net; the query side refuses to write."""
+    from genomealignmenttools_amd._lib import GAC_Q, GAC_T, GacError
+    from genomealignmenttools_amd.chainfile import read_chains
+    from genomealignmenttools_amd.chainnet import Net
+    from genomealignmenttools_amd.synth import read_sizes
+    d = os.path.join(GOLDEN, "synth12")
+    ca = read_chains(os.path.join(d, "in.chain"))
+    net = Net(ca, read_sizes(os.path.join(d, "t.sizes")), read_sizes(os.path.join(d, "q.sizes")),
+              2000, sides=1 << GAC_T)
+    net.write(GAC_T, str(tmp_path / "t.net"), meta=ca.meta)
+    assert filecmp.cmp(tmp_path / "t.net", os.path.join(d, "plain.t.net"), shallow=False)
+    with pytest.raises(GacError):
+        net.write(GAC_Q, str(tmp_path / "q.net"), meta=ca.meta)
+
+
 @pytest.mark.parametrize("seed", [11, 12])
 @pytest.mark.parametrize("tag,opts", [("ms1", ["-minSpace=1", "-minScore=0"]),
                                       ("ms100", ["-minSpace=100", "-minFill=10"])])
