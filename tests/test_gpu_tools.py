@@ -66,6 +66,21 @@ def test_chainnet_rescore_synth(seed, tmp_path):
 
 
 @pytest.mark.parametrize("seed", [11, 12])
+@pytest.mark.parametrize("tag,opts", [("ms1", ["-minSpace=1", "-minScore=0"]),
+                                      ("ms100", ["-minSpace=100", "-minFill=10"])])
+def test_chainnet_rescore_options(seed, tag, opts, tmp_path):
+    """-rescore with the medium gap table and space/fill/score thresholds
+    (tests/golden/make_golden.py::net_variants, reference chainNet)."""
+    d = os.path.join(GOLDEN, f"synth{seed}")
+    p = lambda x: os.path.join(d, x)
+    _run([_bin("chainNet"), p("in.chain"), p("t.sizes"), p("q.sizes"), str(tmp_path / "t.net"),
+          str(tmp_path / "q.net"), "-rescore", f"-tNibDir={p('t.2bit')}",
+          f"-qNibDir={p('q.2bit')}", "-linearGap=medium"] + opts)
+    assert filecmp.cmp(tmp_path / "t.net", p(f"rescore_{tag}.t.net"), shallow=False)
+    assert filecmp.cmp(tmp_path / "q.net", p(f"rescore_{tag}.q.net"), shallow=False)
+
+
+@pytest.mark.parametrize("seed", [11, 12])
 def test_api_subchains_vs_reference(seed):
     """The C ABI's batched sub-chain scores == reference chainSubsetOnT +
     chainCalcScore (+ scoreChain local loop) on 3000 random ranges."""
