@@ -50,6 +50,9 @@ def parse():
     p.add_argument("--prof", choices=["tile", "all", "none"], default="tile",
                    help="kernels bracketed by HIP events inside the timed region "
                         "(the roofline needs k_tile's)")
+    p.add_argument("--layout", choices=["tool", "full"], default="full",
+                   help="chain set on the GPU: as bin/chainNet uploads it (chains owning a "
+                        "rescored fill, in first-use order) or the whole input set")
     p.add_argument("--order", choices=["net", "chain", "t"], default="net",
                    help="range order handed to the GPU: .net output order, (chain, tStart), or tStart")
     p.add_argument("--tmp", default=os.environ.get("TMPDIR", "/tmp"))
@@ -78,7 +81,22 @@ def make_workload(args, rank):
         ranges = ranges[np.lexsort((ranges[:, 1], ranges[:, 0]))]
     elif args.order == "t":
         ranges = ranges[np.argsort(ranges[:, 1], kind="stable")]
-    return tg, qg, ca, np.ascontiguousarray(ranges, np.int32), info
+    if args.workload == "rescore" and args.layout == "tool":
+        # as bin/chainNet -rescore uploads them (chainNet.c's rescoring
+        # branch there): only the chains owning a rescored fill, in the order
+        # they first appear in the fill list
+        uniq, first = np.unique(ranges[:, 0], return_index=True)
+        keep = uniq[np.argsort(first, kind="stable")]
+        remap = np.full(ca.n, -1, np.int64)
+        remap[keep] = np.arange(len(keep))
+        ca_up = ca.subset(keep)
+        ranges = ranges.copy()
+        ranges[:, 0] = remap[ranges[:, 0]]
+        info["uploaded_chains"] = int(len(keep))
+        info["uploaded_blocks"] = int(len(ca_up.blk_size))
+    else:
+        ca_up = ca
+    return tg, qg, ca, ca_up, np.ascontiguousarray(ranges, np.int32), info
 
 
 def main():
@@ -98,13 +116,13 @@ def main():
     from genomealignmenttools_amd._lib import GAC_K_COMBINE, GAC_K_PLAN, GAC_K_TILE
     from genomealignmenttools_amd.gachain import GAC_Q, GAC_T, Engine, GapCosts
 
-    tg, qg, ca, ranges, info = make_workload(args, rank)
+    tg, qg, ca, ca_up, ranges, info = make_workload(args, rank)
     e = Engine(local)
     t0 = time.time()
     e.add_sequences(GAC_T, tg.seq_records())
     e.add_sequences(GAC_Q, qg.seq_records())
     e.set_scoring(BLASTZ, GapCosts("loose"))
-    cs = e.upload_chains(ca)
+    cs = e.upload_chains(ca_up)
     n = len(ranges)
     d_r = e.dev_alloc(ranges.nbytes)
     e.h2d(d_r, ranges)
@@ -118,7 +136,7 @@ def main():
     e.synchronize()
     e.d2h(ali, d_a)
     bases = int(ali.sum(dtype=np.int64))
-    nblk = _window_blocks(ca, ranges)
+    nblk = _window_blocks(ca_up, ranges)
 
     def barrier():
         if dist is not None:
@@ -183,7 +201,7 @@ def main():
             "chains": ca.n, "blocks": int(len(ca.blk_size)),
             "chain_aligned_bases": ca.aligned_bases(),
             "ranges_per_gpu": n, "scored_bases_per_gpu": bases, "scored_blocks_per_gpu": nblk,
-            "parallelism": f"chain-set shard x{world}", **info,
+            "parallelism": f"chain-set shard x{world}", "chain_layout": args.layout, **info,
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -196,7 +214,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(args, tg, qg, ca, ranges, ali)
+            out["cpu_baseline"] = cpu_baseline(args, tg, qg, ca_up, ranges, ali)
         except Exception as ex:  # reported, never fatal
             out["cpu_baseline"] = {"error": str(ex)[:300]}
     if rank == 0:
@@ -219,7 +237,8 @@ def _pmc_traffic(args, n, nblk):
     except (OSError, ValueError):
         return None
     if (t.get("workload") != args.workload or t.get("ranges") != n or t.get("blocks") != nblk
-            or t.get("chains") != args.chains or t.get("seed") != args.seed):
+            or t.get("chains") != args.chains or t.get("seed") != args.seed
+            or t.get("layout", "full") != args.layout):
         return None
     return t.get("hbm_bytes_per_launch")
 
