@@ -224,6 +224,31 @@ def test_axtchain_errors(tmp_path):
     assert r.returncode == 255 and "requires PSLs to have implicit positive strand" in r.stderr
 
 
+def test_axtchain_psl_errors_in_parallel_chunks(tmp_path):
+    """A PSL big enough to be parsed in parallel chunks: the first bad line in
+    file order is reported, with its file line number, whichever chunk a
+    thread finishes first (lineFile semantics of a sequential read)."""
+    from genomealignmenttools_amd._lib import BIN_DIR
+    ax = os.path.join(BIN_DIR, "axtChain")
+    d = os.path.join(GOLDEN, "chrM")
+    lines = open(os.path.join(d, "newStyleLastz.psl")).read().split("\n")
+    head = [l for l in lines if l.startswith("#")]
+    body = [l for l in lines if l and not l.startswith("#")]
+    rows = body * (6_000_000 // sum(len(b) + 1 for b in body) + 1)  # > 4 MB: many chunks
+    n0 = len(head)
+    bad_at, later = len(rows) // 3, 2 * len(rows) // 3
+    w = rows[later].split("\t")
+    rows[later] = "\t".join(w[:5])  # a later error of another kind
+    rows[bad_at] = "\t".join(rows[bad_at].split("\t")[:20])  # 20 words
+    psl = tmp_path / "big.psl"
+    psl.write_text("\n".join(head + rows) + "\n")
+    r = subprocess.run([ax, "-psl", "-linearGap=loose", str(psl), os.path.join(d, "hg19.chrM.2bit"),
+                        os.path.join(d, "susScr3.chrM.2bit"), str(tmp_path / "o.chain")],
+                       capture_output=True, text=True)
+    assert r.returncode == 255
+    assert f"Bad line {n0 + bad_at + 1} of {psl} wordCount is 20 instead of 21 or 23" in r.stderr
+
+
 def test_no_cpu_fallback_without_gpu():
     """On a box without a usable gfx950 device every scoring entry point must
     fail loudly (there is no CPU path to fall back to)."""
