@@ -25,6 +25,7 @@
 // an integer, so integer arithmetic is exact and bit-identical.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "gac_kernels.h"
 
@@ -514,6 +515,53 @@ __global__ void __launch_bounds__(kPlanWG) k_tilemap(ScoreArgs a) {
     if (i >= a.n) return;
     const int nb = a.nblk[i];
     const int g = a.plan_off[i / kPlanWG] + a.goff[i];
+    a.gflat[i] = g;
+    if (nb > 0) {
+        const int64_t end = (int64_t)g + nb;
+        for (int64_t t = ((int64_t)g + kTileBlocks - 1) / kTileBlocks; t * kTileBlocks < end; ++t)
+            a.tile_r0[t] = (int32_t)i;
+    }
+}
+
+// k_tilemap with k_scan_agg folded in, for up to kFusedMapWG plan
+// workgroups (1 M ranges): every workgroup sums the plan-workgroup totals
+// itself -- all of them for W, those before it for its own offset -- so the
+// one-workgroup scan launch disappears.  Workgroup 0 publishes the status
+// words; on overflow every workgroup stops before writing the map.
+constexpr int kFusedMapWG = 4096;
+
+__global__ void __launch_bounds__(kPlanWG) k_tilemap_fused(ScoreArgs a) {
+    __shared__ long long s_part[2][kPlanWG / kWave];
+    const int G = (int)((a.n + kPlanWG - 1) / kPlanWG);
+    const int w = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    long long tot = 0, pre = 0;
+    for (int k = tid; k < G; k += kPlanWG) {
+        const long long v = a.agg[k];
+        tot += v;
+        if (k < w) pre += v;
+    }
+    tot = wave_sum(tot);
+    pre = wave_sum(pre);
+    if (lane == 0) {
+        s_part[0][wave] = tot;
+        s_part[1][wave] = pre;
+    }
+    __syncthreads();
+    tot = pre = 0;
+#pragma unroll
+    for (int k = 0; k < kPlanWG / kWave; ++k) {
+        tot += s_part[0][k];
+        pre += s_part[1][k];
+    }
+    const long long W = tot > 0x7fffffffLL ? 0x7fffffffLL : tot;
+    if (w == 0 && tid == 0) publish_status(a, W);
+    const long long T = (W + kTileBlocks - 1) / kTileBlocks;
+    if (W >= 0x7fffffffLL || T > a.cap_tiles) return;  // the host grows the workspace, reruns
+    if (tid == 0) a.plan_off[w] = (int32_t)pre;
+    const int64_t i = (int64_t)w * kPlanWG + tid;
+    if (i >= a.n) return;
+    const int nb = a.nblk[i];
+    const int g = (int)pre + a.goff[i];
     a.gflat[i] = g;
     if (nb > 0) {
         const int64_t end = (int64_t)g + nb;
@@ -1064,8 +1112,13 @@ hipError_t launch_plan(const ScoreArgs &a, hipStream_t s) {
 }
 
 hipError_t launch_tilemap(const ScoreArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(k_scan_agg, dim3(1), dim3(kPlanWG), 0, s, a);
-    hipLaunchKernelGGL(k_tilemap, dim3((unsigned)plan_grid(a.n)), dim3(kPlanWG), 0, s, a);
+    const int G = plan_grid(a.n);
+    if (G <= kFusedMapWG && !getenv("GAC_UNFUSED_MAP")) {
+        hipLaunchKernelGGL(k_tilemap_fused, dim3((unsigned)G), dim3(kPlanWG), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(k_scan_agg, dim3(1), dim3(kPlanWG), 0, s, a);
+        hipLaunchKernelGGL(k_tilemap, dim3((unsigned)G), dim3(kPlanWG), 0, s, a);
+    }
     return hipGetLastError();
 }
 

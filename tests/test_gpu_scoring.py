@@ -302,3 +302,20 @@ def test_small_batches_vs_oracle(case):
     # the same ranges in one large batch (tile pipeline) agree too
     g3, l3, a3 = e.score_ranges(cs, R, want_local=True)
     assert np.array_equal(g3, og) and np.array_equal(l3, ol) and np.array_equal(a3, oa)
+
+
+def test_unfused_tile_map_path(monkeypatch):
+    """Batches of more than 1 M ranges scan the plan-workgroup totals in a
+    separate one-workgroup launch (k_scan_agg + k_tilemap); smaller ones fold
+    that scan into k_tilemap_fused.  Both give the oracle's scores
+    (GAC_UNFUSED_MAP forces the large-batch path on a small batch)."""
+    from genomealignmenttools_amd import synth
+    tg, qg, ca = synth.small_case(seed=31, n_chains=300, max_blocks=500)
+    e, cs = _setup(None, tg, qg, ca)
+    R = _ranges(ca, np.random.default_rng(31), per_chain=6)
+    og, ol, oa = _oracle(tg, qg).score_ranges(ca, R)
+    g, l, a = e.score_ranges(cs, R, want_local=True)
+    assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
+    monkeypatch.setenv("GAC_UNFUSED_MAP", "1")
+    g, l, a = e.score_ranges(cs, R, want_local=True)
+    assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
