@@ -299,7 +299,7 @@ int gac_memcpy_d2h(gac_ctx *ctx, void *dst, const void *src, size_t bytes);
 int gac_synchronize(gac_ctx *ctx);
 
 /* ---- kernel timing (HIP events on the launch stream) -------------------- */
-#define GAC_K_PLAN 0     /* block-window search + scans + tile map (k_plan, k_scan_agg, k_tilemap) */
+#define GAC_K_PLAN 0     /* block-window search + scans + tile map (k_plan, k_tilemap_fused or k_scan_agg + k_tilemap) */
 #define GAC_K_TILE 1     /* tile scoring: bases, gaps, per-tile scan (dominant) */
 #define GAC_K_COMBINE 2  /* multi-tile range combine */
 #define GAC_K_COUNT 3
