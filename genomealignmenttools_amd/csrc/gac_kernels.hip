@@ -11,8 +11,12 @@
 //             the O(blocks) list walks of chainSubsetOnT / chainBaseCountSubT),
 //             write a 32-byte range descriptor; workgroup scan of window
 //             blocks
-//   k_scan_agg one workgroup: scan of the plan workgroup totals
-//   k_tilemap one lane per range: flat offset, first range of each tile
+//   k_tilemap_fused  one lane per range: each workgroup sums the plan
+//             workgroup totals itself (its flat offset, W), then the range's
+//             flat offset and the first range of each tile; for > 1 M
+//             ranges the same in two launches, k_scan_agg (one-workgroup
+//             scan) + k_tilemap
+//   k_small   batches of <= 256 ranges: one wave per range, one launch
 //   k_tile    one wave per tile of 64 consecutive flat blocks (ranges packed
 //             densely, many ranges per tile): lanes score 32-base chunks of
 //             2-bit packed T and Q straight from HBM (bit-plane popcounts, the
