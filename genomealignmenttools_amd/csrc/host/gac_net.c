@@ -1195,8 +1195,8 @@ static int full_size(const gac_net *n, int64_t c) {
 /* visibility of each fill: reached by rOutputFill and passing its filters
  * given the score rule; for the T side with rescore the score filter always
  * passes (partial scores are >= 1, netted chains >= minScore = 0).
- * Fills in parallel (contiguous index runs), then the visibility DFS in
- * parallel over chromosomes. */
+ * Fills in parallel (contiguous index runs), then one visibility pass in
+ * pre-order over the parent links. */
 typedef struct gf_job {
     const gac_net *n;
     int side;
@@ -1248,55 +1248,6 @@ static void *fills_thread(void *arg) {
     return NULL;
 }
 
-static void *visible_thread(void *arg) {
-    gf_job *J = arg;
-    const gac_net *n = J->n;
-    const int side = J->side;
-    int64_t cap = 1024;
-    typedef struct {
-        const nfill *f;
-        int vis;
-    } item;
-    item *st = malloc(cap * sizeof(item));
-    for (;;) {
-        const int64_t k = atomic_fetch_add(&J->next, 1);
-        if (k >= n->n_chroms[side])
-            break;
-        /* iterative DFS */
-        const nchrom *c = &n->chroms[side][k];
-        if (!c->root || !c->root->fill_head)
-            continue;
-        int64_t top = 0;
-        for (int i = c->root->n_fills - 1; i >= 0; --i) {
-            if (top == cap) {
-                cap *= 2;
-                st = realloc(st, cap * sizeof(item));
-            }
-            st[top++] = (item){c->root->fills[i], 1};
-        }
-        while (top) {
-            item it = st[--top];
-            const nfill *f = it.f;
-            int sz = J->ali ? J->ali[f->ord] : 0;
-            int vis = it.vis && sz >= n->opt.min_fill;
-            if (vis)
-                J->flags[f->ord] |= 2;
-            for (int g = f->n_gaps - 1; g >= 0; --g) {
-                const ngap *gp = f->gaps[g];
-                for (int j = gp->n_fills - 1; j >= 0; --j) {
-                    if (top == cap) {
-                        cap *= 2;
-                        st = realloc(st, cap * sizeof(item));
-                    }
-                    st[top++] = (item){gp->fills[j], vis};
-                }
-            }
-        }
-    }
-    free(st);
-    return NULL;
-}
-
 int gac_net_get_fills(const gac_net *n, int side, int32_t *chain, int32_t *start, int32_t *end,
                       int32_t *ali, uint8_t *flags) {
     if (!n || (side != GAC_T && side != GAC_Q))
@@ -1309,11 +1260,16 @@ int gac_net_get_fills(const gac_net *n, int side, int32_t *chain, int32_t *start
     atomic_init(&J.next, 0);
     const int64_t nrun = (nf + J.per - 1) / J.per;
     gac_run_threads(nt < nrun ? nt : (int)(nrun ? nrun : 1), fills_thread, &J);
-    /* visibility pass (pre-order: parents precede children) */
+    /* visibility: one pass in pre-order (parents precede children), a fill
+     * is printed when its parent fill is and its own ali >= min_fill */
     if (flags) {
-        atomic_store(&J.next, 0);
-        const int nc = n->n_chroms[side];
-        gac_run_threads(nt < nc ? nt : (nc ? nc : 1), visible_thread, &J);
+        for (int64_t i = 0; i < nf; ++i) {
+            const nfill *f = n->order[side][i];
+            const nfill *pf = f->pgap->pfill;
+            const int sz = ali ? ali[i] : 0;
+            if ((!pf || (flags[pf->ord] & 2)) && sz >= n->opt.min_fill)
+                flags[i] |= 2;
+        }
     }
     return GAC_OK;
 }
