@@ -1248,6 +1248,33 @@ static void *fills_thread(void *arg) {
     return NULL;
 }
 
+static int64_t next_top_level(const gac_net *n, int side, int64_t i) {
+    while (i < n->n_order[side] && n->order[side][i]->pgap->pfill)
+        ++i;
+    return i;
+}
+
+static void *visible_thread(void *arg) {
+    gf_job *J = arg;
+    const gac_net *n = J->n;
+    const int side = J->side;
+    const int64_t nf = n->n_order[side];
+    for (;;) {
+        const int64_t r = atomic_fetch_add(&J->next, 1);
+        if (r * J->per >= nf)
+            break;
+        const int64_t a = next_top_level(n, side, r * J->per);
+        const int64_t b = next_top_level(n, side, (r + 1) * J->per < nf ? (r + 1) * J->per : nf);
+        for (int64_t i = a; i < b; ++i) {
+            const nfill *pf = n->order[side][i]->pgap->pfill;
+            const int sz = J->ali ? J->ali[i] : 0;
+            if ((!pf || (J->flags[pf->ord] & 2)) && sz >= n->opt.min_fill)
+                J->flags[i] |= 2;
+        }
+    }
+    return NULL;
+}
+
 int gac_net_get_fills(const gac_net *n, int side, int32_t *chain, int32_t *start, int32_t *end,
                       int32_t *ali, uint8_t *flags) {
     if (!n || (side != GAC_T && side != GAC_Q))
@@ -1260,16 +1287,12 @@ int gac_net_get_fills(const gac_net *n, int side, int32_t *chain, int32_t *start
     atomic_init(&J.next, 0);
     const int64_t nrun = (nf + J.per - 1) / J.per;
     gac_run_threads(nt < nrun ? nt : (int)(nrun ? nrun : 1), fills_thread, &J);
-    /* visibility: one pass in pre-order (parents precede children), a fill
-     * is printed when its parent fill is and its own ali >= min_fill */
+    /* visibility: a fill is printed when its parent fill is and its own ali
+     * >= min_fill -- one pass in pre-order (parents precede children), in
+     * parallel over runs that start at top-level fills (whole subtrees) */
     if (flags) {
-        for (int64_t i = 0; i < nf; ++i) {
-            const nfill *f = n->order[side][i];
-            const nfill *pf = f->pgap->pfill;
-            const int sz = ali ? ali[i] : 0;
-            if ((!pf || (flags[pf->ord] & 2)) && sz >= n->opt.min_fill)
-                flags[i] |= 2;
-        }
+        atomic_store(&J.next, 0);
+        gac_run_threads(nt < nrun ? nt : (int)(nrun ? nrun : 1), visible_thread, &J);
     }
     return GAC_OK;
 }
