@@ -97,6 +97,48 @@ static void *subset_copy_thread(void *arg) {
     return NULL;
 }
 
+/* With -rescore: the whole chain set goes to HBM on a helper thread while
+ * the chains are netted (the usual case: every chain's sequences are in the
+ * 2bit files).  If a sequence is missing -- the reference only looks up the
+ * chains of rescored fills -- or the upload fails, the main thread uploads
+ * just the chains owning a rescored fill, as before. */
+typedef struct pre_upload {
+    gt_device *dev;
+    const gt_chains *c;
+    gac_chainset *cs; /* NULL: use the subset path */
+    pthread_t th;
+    int started;
+} pre_upload;
+
+static void *pre_upload_thread(void *arg) {
+    pre_upload *u = arg;
+    gac_ctx *ctx = gt_device_wait(u->dev);
+    if (!ctx)
+        return NULL;
+    const gt_chains *c = u->c;
+    int32_t *tmap = gt_seq_map(ctx, GAC_T, &c->tnames), *qmap = gt_seq_map(ctx, GAC_Q, &c->qnames);
+    int ok = 1;
+    for (int32_t k = 0; k < c->tnames.n && ok; ++k)
+        ok = tmap[k] >= 0;
+    for (int32_t k = 0; k < c->qnames.n && ok; ++k)
+        ok = qmap[k] >= 0;
+    if (ok) {
+        int32_t *ts = malloc((size_t)(c->n ? c->n : 1) * 4), *qs = malloc((size_t)(c->n ? c->n : 1) * 4);
+        for (int64_t i = 0; i < c->n; ++i) {
+            ts[i] = tmap[c->tname[i]];
+            qs[i] = qmap[c->qname[i]];
+        }
+        gac_chainset_desc d = {c->n, ts, qs, c->qstrand, c->blk_off, c->nb, c->bt, c->bq, c->bs};
+        if (gac_chains_upload(ctx, &d, &u->cs) != GAC_OK)
+            u->cs = NULL;
+        free(ts);
+        free(qs);
+    }
+    free(tmap);
+    free(qmap);
+    return NULL;
+}
+
 int main(int argc, char *argv[]) {
     gt_stage("");
     int min_space = 25;
@@ -181,6 +223,13 @@ int main(int argc, char *argv[]) {
                      tsizes_file);
     }
     gt_stage("chain checks");
+    pre_upload pu;
+    memset(&pu, 0, sizeof(pu));
+    if (rescore) {
+        pu.dev = &dev;
+        pu.c = &c;
+        pu.started = pthread_create(&pu.th, NULL, pre_upload_thread, &pu) == 0;
+    }
     gac_net_input in;
     memset(&in, 0, sizeof(in));
     in.n_chains = c.n;
@@ -228,7 +277,27 @@ int main(int argc, char *argv[]) {
                 rix[nr++] = i;
             }
         tscores = calloc(nf ? nf : 1, 8);
-        if (nr) {
+        if (pu.started)
+            pthread_join(pu.th, NULL);
+        if (nr && pu.cs) { /* the whole set is on the device: original chain indices */
+            gt_stage("fill list");
+            gac_ctx *ctx = gt_device_join(&dev);
+            gt_stage("device open + 2bit genomes + chains to HBM (rest)");
+            int64_t *g = malloc(nr * 8);
+            int32_t *ali = malloc(nr * 4);
+            gt_check(gac_score_ranges(ctx, pu.cs, r, nr, 0, g, NULL, ali));
+            gt_stage("GPU fill rescoring");
+            for (int64_t k = 0; k < nr; ++k)
+                tscores[rix[k]] = g[k];
+            free(g);
+            free(ali);
+            gt_device_close_async(&dev, ctx, pu.cs); /* overlaps writing the nets */
+            pu.cs = NULL;
+        } else if (nr) {
+            if (pu.cs) {
+                gac_chains_free(pu.cs);
+                pu.cs = NULL;
+            }
             gt_stage("fill list");
             gac_ctx *ctx = gt_device_join(&dev);
             gt_stage("device open + 2bit genomes (rest)");
@@ -296,7 +365,9 @@ int main(int argc, char *argv[]) {
             free(remap);
             gt_device_close_async(&dev, ctx, cs); /* overlaps writing the nets */
         }
-        if (dev.started) { /* nothing to rescore: the genomes were never needed */
+        if (!nr) { /* nothing to rescore: the genomes were never needed */
+            if (pu.cs)
+                gac_chains_free(pu.cs);
             gac_ctx *ctx = gt_device_wait(&dev);
             if (ctx)
                 gac_close(ctx);

@@ -152,9 +152,9 @@ gac_ctx *gt_device_wait(gt_device *d) {
 }
 
 gac_ctx *gt_device_join(gt_device *d) {
-    if (!d->started)
-        gt_abort("gt_device_join: not started\n");
-    gt_device_wait(d);
+    gt_device_wait(d); /* (another thread may have waited already) */
+    if (d->rc == GAC_OK && !d->ctx)
+        gt_abort("gt_device_join: device never started\n");
     if (d->rc != GAC_OK)
         gt_abort("%s\n", d->err);
     gt_verbose(2, "[stage] (overlapped) device open %.3f s, 2bit genomes to HBM %.3f s\n",
