@@ -1,24 +1,42 @@
 #!/usr/bin/env python3
-"""bench.py -- aligned Gbases scored/sec, chainNet -rescore (BASELINE.json).
+"""bench.py -- aligned Gbases scored/sec, chainNet -rescore hg38-mm10 (BASELINE.json).
 
-Workload (SURVEY.md §8(d) C2, synthetic, seeded): target = hg38 chr1
-(248,956,422 bp), query = all 66 mm10 sequences (2.73 Gb), ~2e5 planted
+Workload (SURVEY.md §8(d) config C2, synthetic, seeded): target = hg38 chr1
+(248,956,422 bp), query = all 66 mm10 sequences (2.73 Gb), 2e5 planted
 chains (power-law blocks/chain, geometric 40-bp blocks, 12% substitutions,
-50% '-' strand, 20% short spurious chains), netted on the host by the
-product's chainNet engine.  One step = the GPU rescoring of every partial
-T-net fill (chainNet -rescore's subchainInfo -> chainSubsetOnT +
-chainCalcScore, src/chainNet/chainNet.c:795-843) with genomes, chains and
-the fill list already resident in HBM.  value = aligned bases of the
-rescored fills (all ranks) / max-over-ranks wall time.
+50% '-' strand, 20% short spurious chains), written as .2bit genomes,
+chrom.sizes files and a score-sorted .chain file.
 
-N>1: one process per GPU; every rank nets and rescores its own independent
-C2 set (seed + rank): chains shard by independent chain set, there is no
-data-path collective (scaling "weak").  torch.distributed (RCCL) is used for
-the barrier and the max-over-ranks timing only.
+Headline (`value`, SURVEY §8(d) primary metric): ONE STEP = one end-to-end
+`bin/chainNet in.chain t.sizes q.sizes t.net q.net -rescore -tNibDir=t.2bit
+-qNibDir=q.2bit -linearGap=loose` invocation (the drop-in tool: process
+start, chain parse, host netting, 2bit genomes + chains to HBM, GPU
+rescoring of every partial target fill, both nets written).  value = the
+aligned bases of the netted input chains (score >= 0) / wall time per step.
+
+N > 1 (torchrun, one process per GPU): every step runs the tool on every rank
+over the SAME input with -nranks=N -rank=r: rank r nets the chromosome sides
+it owns (LPT by aligned bases), rescores its target fills on its own GPU and
+writes its part; rank 0 assembles both nets.  Strong scaling on one chain
+set, no data-path collective (the netting partitions by chromosome side);
+torch.distributed (RCCL) carries the barriers and the max-over-ranks clock.
+
+Also reported:
+  kernel   -- the GPU rescoring call alone (gac_score_ranges_device over the
+              C2 partial fills, inputs resident in HBM), HIP-event timed;
+  roofline -- its dominant kernel k_tile: algorithmic bytes per launch
+               / k_tile's average launch time, vs 8 TB/s;
+  cpu_baseline -- the reference chainNet compiled from /root/reference
+              (oracle/_ref/chainNet, test infrastructure) on the same files on
+              this host: one process (the reference is single-threaded) and a
+              per-chromosome-side split over all cores; nets compared byte
+              for byte with ours.
 """
 import argparse
+import filecmp
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -30,6 +48,9 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BLASTZ = np.array([[91, -114, -31, -123], [-114, 100, -125, -31], [-31, -125, 100, -114],
                    [-123, -31, -114, 91]], np.int32)
+METRIC = "aligned Gbases scored/sec, chainNet -rescore hg38-mm10, 1/2/4/8 MI355X"
+TOOL = os.path.join(REPO, "genomealignmenttools_amd", "bin", "chainNet")
+REF_TOOL = os.path.join(REPO, "oracle", "_ref", "chainNet")
 
 
 def log(*a):
@@ -39,66 +60,310 @@ def log(*a):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--chains", type=int, default=200_000)
     p.add_argument("--seed", type=int, default=42)
-    p.add_argument("--workload", choices=["rescore", "scorechain"], default="rescore")
-    p.add_argument("--cpu-seconds", type=float, default=15.0,
-                   help="target CPU seconds for the cpu_baseline sample")
+    p.add_argument("--workload", choices=["chainnet", "rescore", "scorechain"], default="chainnet",
+                   help="chainnet: end-to-end bin/chainNet -rescore (headline); rescore / "
+                        "scorechain: the GPU scoring call alone as the step")
+    p.add_argument("--kernel-steps", type=int, default=20)
+    p.add_argument("--no-kernel", action="store_true", help="skip the kernel/roofline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-all-cores", action="store_true",
+                   help="skip the reference's per-chromosome-side all-cores run")
     p.add_argument("--prof", choices=["tile", "all", "none"], default="tile",
-                   help="kernels bracketed by HIP events inside the timed region "
-                        "(the roofline needs k_tile's)")
-    p.add_argument("--layout", choices=["tool", "full"], default="full",
-                   help="chain set on the GPU: as bin/chainNet uploads it (chains owning a "
-                        "rescored fill, in first-use order) or the whole input set")
-    p.add_argument("--order", choices=["net", "chain", "t"], default="net",
-                   help="range order handed to the GPU: .net output order, (chain, tStart), or tStart")
+                   help="kernels bracketed by HIP events in the kernel leg (the roofline "
+                        "needs k_tile's)")
     p.add_argument("--tmp", default=os.environ.get("TMPDIR", "/tmp"))
     return p.parse_args()
 
 
-def make_workload(args, rank):
-    from genomealignmenttools_amd import synth
+def host_threads():
+    v = os.environ.get("GAC_THREADS") or os.environ.get("OMP_NUM_THREADS")
+    return int(v) if v else len(os.sched_getaffinity(0))
+
+
+# ---------------------------------------------------------------- input files
+def c2_files(args):
+    """C2 written once per box under --tmp: t.2bit, q.2bit, *.sizes, in.chain."""
+    from genomealignmenttools_amd import chainfile, synth
+    d = os.path.join(args.tmp, f"gac_bench_c2_{args.chains}_{args.seed}")
+    p = lambda x: os.path.join(d, x)
+    if not os.path.exists(p("info.json")):
+        os.makedirs(d, exist_ok=True)
+        t0 = time.time()
+        tg, qg, ca = synth.c2_case(seed=args.seed, n_chains=args.chains)
+        synth.write_2bit(tg, p("t.2bit"))
+        synth.write_2bit(qg, p("q.2bit"))
+        synth.write_sizes(tg.sizes, p("t.sizes"))
+        synth.write_sizes(qg.sizes, p("q.sizes"))
+        chainfile.write_chains(ca, p("in.chain"))
+        # the netting loop stops at the first chain below minScore (0 with
+        # -rescore, chainNet.c:949-952,1022): those chains' aligned bases
+        # are the metric's numerator
+        neg = np.nonzero(ca.score < 0)[0]
+        stop = int(neg[0]) if len(neg) else ca.n
+        info = {"chains": ca.n, "blocks": int(len(ca.blk_size)),
+                "input_aligned_bases": ca.aligned_bases(),
+                "netted_chains": stop,
+                "netted_aligned_bases": int(ca.blk_size[:ca.blk_off[stop]].sum(dtype=np.int64))}
+        with open(p("info.json.tmp"), "w") as f:
+            json.dump(info, f)
+        os.rename(p("info.json.tmp"), p("info.json"))
+        log(f"C2: {info} written in {time.time() - t0:.1f}s")
+    with open(p("info.json")) as f:
+        return d, json.load(f)
+
+
+def tool_cmd(d, out, world, rank, extra=()):
+    p = lambda x: os.path.join(d, x)
+    cmd = [TOOL, p("in.chain"), p("t.sizes"), p("q.sizes"), out + ".t.net", out + ".q.net",
+           "-rescore", f"-tNibDir={p('t.2bit')}", f"-qNibDir={p('q.2bit')}", "-linearGap=loose"]
+    if world > 1:
+        cmd += [f"-nranks={world}", f"-rank={rank}", f"-gpu={int(os.environ.get('LOCAL_RANK', rank))}"]
+    return cmd + list(extra)
+
+
+def run_tool(cmd, outs, env=None):
+    for o in outs:  # (a truncated-and-rewritten file may be flushed on close)
+        if os.path.exists(o):
+            os.remove(o)
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=900)
+    if r.returncode != 0:
+        raise RuntimeError(f"{cmd[0]} rc={r.returncode}: {r.stderr[-3000:]}")
+    return r
+
+
+# ---------------------------------------------------------------- kernel leg
+def kernel_leg(args, d, steps):
+    """The GPU rescoring call alone (inputs resident in HBM), HIP-event timed:
+    the roofline of k_tile and a per-kernel breakdown."""
+    from genomealignmenttools_amd import chainfile
+    from genomealignmenttools_amd._lib import GAC_K_COMBINE, GAC_K_PLAN, GAC_K_TILE
+    from genomealignmenttools_amd.chainnet import net_fills
+    from genomealignmenttools_amd.gachain import GAC_Q, GAC_T, Engine, GapCosts
+    from genomealignmenttools_amd.synth import read_sizes
+    p = lambda x: os.path.join(d, x)
     t0 = time.time()
-    tg, qg, ca = synth.c2_case(seed=args.seed + rank, n_chains=args.chains)
-    log(f"[rank {rank}] synthetic C2: {ca.n} chains, {len(ca.blk_size)} blocks, "
-        f"{ca.aligned_bases() / 1e6:.1f} M aligned bases ({time.time() - t0:.1f}s)")
+    ca = chainfile.read_chains(p("in.chain"))
     if args.workload == "scorechain":
         ranges = np.stack([np.arange(ca.n, dtype=np.int32), ca.tstart, ca.tend], 1)
-        info = {"netted_chains": ca.n}
     else:
-        from genomealignmenttools_amd.chainnet import net_fills
-        t1 = time.time()
-        fills = net_fills(ca, tg.sizes, qg.sizes, min_score=0.0)
+        fills = net_fills(ca, read_sizes(p("t.sizes")), read_sizes(p("q.sizes")), min_score=0.0)
         part = fills["partial"]
         ranges = np.stack([fills["chain"][part], fills["start"][part], fills["end"][part]], 1)
-        info = {"netted_chains": int(fills["netted_chains"]), "tnet_fills": int(len(part)),
-                "partial_fills": int(part.sum())}
-        log(f"[rank {rank}] host netting: {info} ({time.time() - t1:.1f}s)")
-    if args.order == "chain":
-        ranges = ranges[np.lexsort((ranges[:, 1], ranges[:, 0]))]
-    elif args.order == "t":
-        ranges = ranges[np.argsort(ranges[:, 1], kind="stable")]
-    if args.workload == "rescore" and args.layout == "tool":
-        # as bin/chainNet -rescore uploads them (chainNet.c's rescoring
-        # branch there): only the chains owning a rescored fill, in the order
-        # they first appear in the fill list
-        uniq, first = np.unique(ranges[:, 0], return_index=True)
-        keep = uniq[np.argsort(first, kind="stable")]
-        remap = np.full(ca.n, -1, np.int64)
-        remap[keep] = np.arange(len(keep))
-        ca_up = ca.subset(keep)
-        ranges = ranges.copy()
-        ranges[:, 0] = remap[ranges[:, 0]]
-        info["uploaded_chains"] = int(len(keep))
-        info["uploaded_blocks"] = int(len(ca_up.blk_size))
-    else:
-        ca_up = ca
-    return tg, qg, ca, ca_up, np.ascontiguousarray(ranges, np.int32), info
+    ranges = np.ascontiguousarray(ranges, np.int32)
+    e = Engine(int(os.environ.get("LOCAL_RANK", "0")))
+    e.load_2bit(GAC_T, p("t.2bit"))
+    e.load_2bit(GAC_Q, p("q.2bit"))
+    e.set_scoring(BLASTZ, GapCosts("loose"))
+    cs = e.upload_chains(ca)
+    n = len(ranges)
+    d_r = e.dev_alloc(ranges.nbytes)
+    e.h2d(d_r, ranges)
+    d_g = e.dev_alloc(8 * n)
+    d_a = e.dev_alloc(4 * n)
+    ali = np.zeros(n, np.int32)
+    e.score_ranges_device(cs, d_r, n, d_g, d_a)
+    e.synchronize()
+    e.d2h(ali, d_a)
+    bases = int(ali.sum(dtype=np.int64))
+    nblk = _window_blocks(ca, ranges)
+    log(f"kernel leg: {n} ranges, {bases} bases, {nblk} window blocks ({time.time() - t0:.1f}s setup)")
+    for _ in range(3):
+        e.score_ranges_device(cs, d_r, n, d_g, d_a)
+    e.synchronize()
+    e.prof_reset()
+    if args.prof != "none":
+        e.prof_enable(True, None if args.prof == "all" else [GAC_K_TILE])
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        e.score_ranges_device(cs, d_r, n, d_g, d_a)
+    e.synchronize()
+    dt = time.perf_counter() - t0
+    e.prof_enable(False)
+    tile_ms, tile_n = e.prof_read(GAC_K_TILE)
+    e.prof_reset()
+    e.prof_enable(True)
+    for _ in range(min(steps, 5)):
+        e.score_ranges_device(cs, d_r, n, d_g, d_a)
+    e.synchronize()
+    e.prof_enable(False)
+    kern_ms = {name: e.prof_read(k)[0] / max(e.prof_read(k)[1], 1)
+               for name, k in (("plan+tilemap", GAC_K_PLAN), ("tile", GAC_K_TILE),
+                               ("combine", GAC_K_COMBINE))}
+    if args.prof == "none":
+        tile_ms, tile_n = kern_ms["tile"], 1
+    cs.close()
+    e.close()
+    # algorithmic bytes per k_tile launch: 0.75 B/base (t+q 2-bit + t+q
+    # N-mask bits) + 12 B/window block + 44 B/range (DESIGN.md §4)
+    algo = 0.75 * bases + 12.0 * nblk + 44.0 * n
+    tile_s = (tile_ms / 1e3) / max(tile_n, 1)
+    achieved = algo / tile_s / 1e9
+    kernel = {"workload": ("chainNet -rescore partial target fills" if args.workload != "scorechain"
+                           else "scoreChain whole chains, global + local"),
+              "value": bases * steps / dt / 1e9, "unit": "Gbases/s", "ms_per_step": dt / steps * 1e3,
+              "steps": steps, "ranges": n, "scored_bases": bases, "window_blocks": nblk,
+              "kernel_ms": kern_ms}
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc_traffic(args, n, nblk),
+            "kernel": "k_tile", "kernel_avg_ms": tile_s * 1e3, "algo_bytes_per_launch": algo}
+    return kernel, roof
 
 
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "k_tile_traffic.json")
+
+
+def _pmc_traffic(args, n, nblk):
+    """HBM bytes per k_tile launch from the committed PMC profile of this same
+    kernel-leg workload (scripts/gpu_counters.sh + scripts/pmc_summary.py),
+    or None when no profile matches it."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    wl = "scorechain" if args.workload == "scorechain" else "rescore"
+    if (t.get("workload") != wl or t.get("ranges") != n or t.get("blocks") != nblk
+            or t.get("chains") != args.chains or t.get("seed") != args.seed):
+        return None
+    return t.get("hbm_bytes_per_launch")
+
+
+def _window_blocks(ca, ranges):
+    """Blocks selected by each range (host binary search, for the byte model)."""
+    tot = 0
+    for c, s, e in ranges:
+        bt, _, bs = ca.blocks(int(c))
+        if s <= bt[0] and e >= bt[-1] + bs[-1]:
+            tot += len(bt)
+            continue
+        lo = np.searchsorted(bt + bs, s, side="right")
+        hi = np.searchsorted(bt, e, side="left")
+        tot += max(0, int(hi - lo))
+    return tot
+
+
+# ---------------------------------------------------------------- CPU baseline
+def cpu_baseline(args, d, info, ours):
+    """The reference chainNet (oracle/_ref, compiled from /root/reference) on
+    the same files: one process, then split per chromosome side over all
+    host cores; nets compared with ours."""
+    p = lambda x: os.path.join(d, x)
+    if not os.path.exists(REF_TOOL):
+        return {"error": f"{REF_TOOL} not built (make ref)"}
+    opts = ["-rescore", f"-tNibDir={p('t.2bit')}", f"-qNibDir={p('q.2bit')}", "-linearGap=loose"]
+    ref = p("ref")
+    t0 = time.time()
+    run_tool([REF_TOOL, p("in.chain"), p("t.sizes"), p("q.sizes"), ref + ".t.net", ref + ".q.net"]
+             + opts, [ref + ".t.net", ref + ".q.net"])
+    t1 = time.time() - t0
+    same = (filecmp.cmp(ours + ".t.net", ref + ".t.net", False)
+            and filecmp.cmp(ours + ".q.net", ref + ".q.net", False))
+    log(f"cpu baseline: reference chainNet -rescore {t1:.2f}s, nets identical: {same}")
+    out = {"value": info["netted_aligned_bases"] / t1 / 1e9, "unit": "Gbases/s", "cores": 1,
+           "kind": "reference", "seconds": t1, "identical_nets": same,
+           "sample": f"the whole workload: reference chainNet -rescore (oracle/_ref) on the same "
+                     f"C2 files, one process ({t1:.2f}s)"}
+    if not args.no_all_cores:
+        try:
+            out["all_cores"] = ref_all_cores(d, opts, ref)
+        except Exception as ex:  # reported, never fatal
+            out["all_cores"] = {"error": str(ex)[:300]}
+    return out
+
+
+def ref_all_cores(d, opts, ref):
+    """The reference run per chromosome side over all host cores: a target
+    sequence's net depends only on the chains on it (a query sequence's
+    likewise), so the chains are split by target sequence (target nets) and
+    by query sequence (query nets) and the reference runs on every group
+    concurrently; the groups' nets are reassembled and compared."""
+    from concurrent.futures import ThreadPoolExecutor
+    p = lambda x: os.path.join(d, x)
+    gd = p("ref_groups")
+    os.makedirs(gd, exist_ok=True)
+    groups = _split_chain_file(p("in.chain"), gd)
+    cores = host_threads()
+    jobs = []
+    for side, name, path in groups:
+        o = os.path.join(gd, f"{side}.{len(jobs)}")
+        jobs.append((side, name, [REF_TOOL, path, p("t.sizes"), p("q.sizes"), o + ".t.net",
+                                  o + ".q.net"] + opts, o))
+    t0 = time.time()
+    with ThreadPoolExecutor(max_workers=cores) as ex:
+        list(ex.map(lambda j: run_tool(j[2], [j[3] + ".t.net", j[3] + ".q.net"]), jobs))
+    wall = time.time() - t0
+    same = True
+    for side in ("t", "q"):
+        parts = {}
+        for s, name, _, o in jobs:
+            if s == side:
+                with open(o + f".{side}.net") as f:
+                    parts[name] = _net_sections(f.read())[1].get(name, "")
+        with open(ref + f".{side}.net") as f:
+            whole = f.read()
+        meta, _, order = _net_sections(whole)
+        same = same and meta + "".join(parts.get(k, "") for k in order) == whole
+    import shutil
+    shutil.rmtree(gd, ignore_errors=True)
+    log(f"cpu baseline (all cores): {len(jobs)} reference runs on {cores} cores, {wall:.2f}s, "
+        f"reassembled nets identical: {same}")
+    return {"seconds": wall, "cores": cores, "processes": len(jobs), "identical_nets": same}
+
+
+def _split_chain_file(path, gd):
+    """Chain text split by target and by query sequence (file order kept,
+    leading '#' lines copied to every group) -> [(side, sequence, file)]."""
+    meta, tg, qg = [], {}, {}
+    cur, cur_t, cur_q = [], None, None
+
+    def flush():
+        if cur_t is not None:
+            rec = "\n".join(cur) + "\n"
+            tg.setdefault(cur_t, []).append(rec)
+            qg.setdefault(cur_q, []).append(rec)
+    with open(path) as f:
+        for line in f.read().split("\n"):
+            if cur_t is None and line.startswith("#"):
+                meta.append(line + "\n")
+            elif line.startswith("chain "):
+                flush()
+                w = line.split()
+                cur, cur_t, cur_q = [line], w[2], w[7]
+            elif cur_t is not None:
+                cur.append(line)
+    flush()
+    out = []
+    for side, g in (("t", tg), ("q", qg)):
+        for k, (name, recs) in enumerate(g.items()):
+            fn = os.path.join(gd, f"in.{side}{k}.chain")
+            with open(fn, "w") as f:
+                f.write("".join(meta) + "".join(recs))
+            out.append((side, name, fn))
+    return out
+
+
+def _net_sections(text):
+    """('#' header, {sequence: its 'net' section}, sequence order) of .net text."""
+    meta_end = 0
+    while text.startswith("#", meta_end):
+        meta_end = text.index("\n", meta_end) + 1
+    secs, order = {}, []
+    pos = meta_end
+    while pos < len(text):
+        nxt = text.find("\nnet ", pos)
+        end = len(text) if nxt < 0 else nxt + 1
+        name = text[pos:text.index("\n", pos)].split()[1]
+        secs[name] = text[pos:end]
+        order.append(name)
+        pos = end
+    return text[:meta_end], secs, order
+
+
+# ---------------------------------------------------------------- main
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -113,185 +378,69 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world,
                                 device_id=torch.device(f"cuda:{local}"))
 
-    from genomealignmenttools_amd._lib import GAC_K_COMBINE, GAC_K_PLAN, GAC_K_TILE
-    from genomealignmenttools_amd.gachain import GAC_Q, GAC_T, Engine, GapCosts
-
-    tg, qg, ca, ca_up, ranges, info = make_workload(args, rank)
-    e = Engine(local)
-    t0 = time.time()
-    e.add_sequences(GAC_T, tg.seq_records())
-    e.add_sequences(GAC_Q, qg.seq_records())
-    e.set_scoring(BLASTZ, GapCosts("loose"))
-    cs = e.upload_chains(ca_up)
-    n = len(ranges)
-    d_r = e.dev_alloc(ranges.nbytes)
-    e.h2d(d_r, ranges)
-    d_g = e.dev_alloc(8 * n)
-    d_a = e.dev_alloc(4 * n)
-    log(f"[rank {rank}] upload {time.time() - t0:.1f}s; {n} ranges")
-
-    # bytes/blocks of the scored windows (for the roofline) from one host pass
-    ali = np.zeros(n, np.int32)
-    e.score_ranges_device(cs, d_r, n, d_g, d_a)
-    e.synchronize()
-    e.d2h(ali, d_a)
-    bases = int(ali.sum(dtype=np.int64))
-    nblk = _window_blocks(ca_up, ranges)
-
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        e.score_ranges_device(cs, d_r, n, d_g, d_a)
-    e.synchronize()
-    e.prof_reset()
-    if args.prof != "none":
-        e.prof_enable(True, None if args.prof == "all" else [GAC_K_TILE])
+    if rank == 0:
+        d, info = c2_files(args)
     barrier()
-    e.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        e.score_ranges_device(cs, d_r, n, d_g, d_a)
-    e.synchronize()
-    barrier()
-    dt = time.perf_counter() - t0
-    e.prof_enable(False)
-    tile_ms, tile_n = e.prof_read(GAC_K_TILE)
-    # per-kernel breakdown: a separate, untimed pass with every kernel bracketed
-    e.prof_reset()
-    e.prof_enable(True)
-    for _ in range(min(args.steps, 5)):
-        e.score_ranges_device(cs, d_r, n, d_g, d_a)
-    e.synchronize()
-    e.prof_enable(False)
-    kern_ms = {name: e.prof_read(k)[0] / max(e.prof_read(k)[1], 1)
-               for name, k in (("plan+tilemap", GAC_K_PLAN), ("tile", GAC_K_TILE),
-                               ("combine", GAC_K_COMBINE))}
-    if args.prof == "none":  # roofline from the breakdown pass
-        tile_ms, tile_n = kern_ms["tile"], 1
-    step_s = dt / args.steps
-    if dist is not None:
-        from genomealignmenttools_amd.shard import reduce_time_and_work
-        dt_max, total_bases = reduce_time_and_work(dist, dt, float(bases), device=f"cuda:{local}")
-    else:
-        dt_max, total_bases = dt, float(bases)
+    if rank != 0:
+        d, info = c2_files(args)  # written by rank 0 (same node)
+    out_base = os.path.join(d, f"ours.r{world}")
+    outs = [out_base + ".t.net", out_base + ".q.net"]
+    cmd = tool_cmd(d, out_base, world, rank)
 
-    # roofline of the dominant kernel (k_tile): algorithmic bytes per launch
-    # = 0.75 B/base (t+q 2-bit + t+q N-mask bits) + 12 B/block + 44 B/range
-    algo_bytes = 0.75 * bases + 12.0 * nblk + 44.0 * n
-    tile_avg_s = (tile_ms / 1e3) / max(tile_n, 1)
-    achieved = algo_bytes / tile_avg_s / 1e9
-    out = {
-        "metric": "aligned Gbases scored/sec, chainNet -rescore hg38-mm10, 1/2/4/8 MI355X",
-        "value": total_bases * args.steps / dt_max / 1e9,
-        "unit": "Gbases/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": dt_max / args.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "int64",
-        "data": "synthetic (seeded C2: hg38 chr1 x mm10 sizes, planted chains; no real genomes)",
-        "config": {
-            "workload": ("chainNet -rescore T-net partial-fill rescoring" if args.workload == "rescore"
-                         else "scoreChain full-chain global+local"),
-            "chains": ca.n, "blocks": int(len(ca.blk_size)),
-            "chain_aligned_bases": ca.aligned_bases(),
-            "ranges_per_gpu": n, "scored_bases_per_gpu": bases, "scored_blocks_per_gpu": nblk,
-            "parallelism": f"chain-set shard x{world}", "chain_layout": args.layout, **info,
-        },
-        "roofline": {
-            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc_traffic(args, n, nblk),
-            "kernel": "k_tile", "kernel_avg_ms": tile_avg_s * 1e3,
-            "algo_bytes_per_launch": algo_bytes,
-        },
-        "kernel_ms_per_step": kern_ms,
-        "cpu_baseline": None,
-    }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if args.workload == "chainnet":
+        for _ in range(args.warmup):
+            barrier()
+            run_tool(cmd, outs if rank == 0 else [])
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            run_tool(cmd, outs if rank == 0 else [])
+            barrier()  # rank 0 finishes last (it assembles the nets)
+        dt = time.perf_counter() - t0
+        if dist is not None:
+            from genomealignmenttools_amd.shard import reduce_time_and_work
+            dt, _ = reduce_time_and_work(dist, dt, 0.0, device=f"cuda:{local}")
+        step_s = dt / args.steps
+        stages = None
+        if rank == 0:  # one more, untimed run for the per-stage breakdown
+            r = run_tool(cmd + ["-verbose=2"], outs)
+            stages = [line.strip() for line in r.stderr.splitlines() if "[stage]" in line]
+        out = {
+            "metric": METRIC,
+            "value": info["netted_aligned_bases"] / step_s / 1e9,
+            "unit": "Gbases/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": step_s * 1e3, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "int64",
+            "data": "synthetic (seeded C2: hg38 chr1 x mm10 sizes, planted chains; no real genomes)",
+            "config": {"workload": "chainNet -rescore end to end (bin/chainNet, C2)",
+                       **info, "parallelism": f"chromosome-side shards x{world}",
+                       "host_threads_per_rank": host_threads(), "tool_stages": stages},
+        }
+    else:
+        out = {"metric": METRIC, "n_gpus": world, "unit": "Gbases/s", "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+               "data": "synthetic (seeded C2)", "config": {"workload": args.workload, **info}}
+    if rank == 0 and not args.no_kernel:
+        kernel, roof = kernel_leg(args, d, args.kernel_steps)
+        out["kernel"] = kernel
+        out["roofline"] = roof
+        if args.workload != "chainnet":  # the kernel call itself is the step
+            out.update(value=kernel["value"], steps=args.kernel_steps, warmup=3,
+                       ms_per_step=kernel["ms_per_step"])
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "chainnet":
         try:
-            out["cpu_baseline"] = cpu_baseline(args, tg, qg, ca_up, ranges, ali)
+            out["cpu_baseline"] = cpu_baseline(args, d, info, out_base)
         except Exception as ex:  # reported, never fatal
             out["cpu_baseline"] = {"error": str(ex)[:300]}
     if rank == 0:
         print(json.dumps(out), flush=True)
+    barrier()
     if dist is not None:
         dist.destroy_process_group()
-
-
-TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
-                            "k_tile_traffic.json")
-
-
-def _pmc_traffic(args, n, nblk):
-    """HBM bytes per k_tile launch from the committed PMC profile of this same
-    workload (scripts/gpu_counters.sh + scripts/pmc_summary.py: request
-    counters by size), or None when no profile matches the workload."""
-    try:
-        with open(TRAFFIC_FILE) as f:
-            t = json.load(f)
-    except (OSError, ValueError):
-        return None
-    if (t.get("workload") != args.workload or t.get("ranges") != n or t.get("blocks") != nblk
-            or t.get("chains") != args.chains or t.get("seed") != args.seed
-            or t.get("layout", "full") != args.layout):
-        return None
-    return t.get("hbm_bytes_per_launch")
-
-
-def _window_blocks(ca, ranges):
-    """Blocks selected by each range (host binary search, for the byte model)."""
-    tot = 0
-    for c, s, e in ranges:
-        bt, _, bs = ca.blocks(int(c))
-        lo = np.searchsorted(bt + bs, s, side="right")
-        hi = np.searchsorted(bt, e, side="left")
-        tot += max(0, int(hi - lo))
-    return tot
-
-
-def cpu_baseline(args, tg, qg, ca, ranges, ali):
-    """Reference CPU timing: oracle/_ref/kentref (the reference's own kent
-    chainSubsetOnT + chainCalcScore, as chainNet -rescore runs them per fill)
-    on a bounded random sample of the same fills, one core."""
-    from genomealignmenttools_amd import chainfile, synth
-    from oracle.oracle import KentRef, have_ref
-    if not have_ref():
-        return {"error": "oracle/_ref/kentref not built"}
-    import tempfile
-    d = tempfile.mkdtemp(dir=args.tmp)
-    t0 = time.time()
-    rng = np.random.default_rng(0)
-    order = rng.permutation(len(ranges))
-    frac0 = min(1.0, 4000 / max(len(ranges), 1))
-    def run(frac):
-        sel = np.sort(order[: max(1, int(len(ranges) * frac))])
-        chains = np.unique(ranges[sel, 0])
-        sub = ca.subset(chains)
-        remap = {int(c): i for i, c in enumerate(chains)}
-        r = np.array([(remap[int(c)], s, e) for c, s, e in ranges[sel]], np.int32)
-        cf = os.path.join(d, "s.chain")
-        chainfile.write_chains(sub, cf)
-        kr = KentRef(cf, os.path.join(d, "t.2bit"), os.path.join(d, "q.2bit"), None, "loose")
-        kr.rescore_fills(r)
-        return kr.last_seconds, int(ali[sel].sum(dtype=np.int64)), len(sel)
-    synth.write_2bit(tg, os.path.join(d, "t.2bit"))
-    synth.write_2bit(qg, os.path.join(d, "q.2bit"))
-    sec, b, k = run(frac0)
-    frac = frac0
-    if sec < args.cpu_seconds * 0.5 and frac0 < 1.0:
-        frac = min(1.0, frac0 * args.cpu_seconds / max(sec, 1e-3))
-        sec, b, k = run(frac)
-    import shutil
-    shutil.rmtree(d, ignore_errors=True)
-    log(f"cpu baseline: {k} fills, {b} bases, {sec:.2f}s ({time.time() - t0:.0f}s wall)")
-    return {"value": b / sec / 1e9, "unit": "Gbases/s", "cores": 1, "kind": "reference",
-            "sample": f"{k} of {len(ranges)} partial T-net fills (random, seed 0), {b} aligned "
-                      f"bases, {sec:.2f}s in kent chainSubsetOnT+chainCalcScore+base counts"}
 
 
 if __name__ == "__main__":

@@ -346,6 +346,13 @@ __device__ __forceinline__ RangeDesc plan_range(const ScoreArgs &a, const Range 
     if (n == 0) return d;
     const int2 *sp = a.tspan + c.blk_off;
     const int s = r.t_start, e = r.t_end;
+    if (s <= c.tstart && e >= c.tend) {
+        // chainFastSubsetOnT's easy case (chain.c:499-505): the whole chain,
+        // zero-size end blocks included (no clipping inside [s, e) either)
+        d.nblk = n;
+        d.b0 = (int32_t)c.blk_off;
+        return d;
+    }
     int lo, hi;  // the first block with tEnd > s is in [lo, hi]
     if (s < c.tstart) {
         lo = hi = 0;

@@ -229,6 +229,8 @@ int main(int argc, char *argv[]) {
         pu.dev = &dev;
         pu.c = &c;
         pu.started = pthread_create(&pu.th, NULL, pre_upload_thread, &pu) == 0;
+        if (pu.started) /* gt_abort joins it before exiting */
+            gt_helper_add(pu.th);
     }
     gac_net_input in;
     memset(&in, 0, sizeof(in));
@@ -278,7 +280,7 @@ int main(int argc, char *argv[]) {
             }
         tscores = calloc(nf ? nf : 1, 8);
         if (pu.started)
-            pthread_join(pu.th, NULL);
+            gt_helper_join(pu.th);
         if (nr && pu.cs) { /* the whole set is on the device: original chain indices */
             gt_stage("fill list");
             gac_ctx *ctx = gt_device_join(&dev);

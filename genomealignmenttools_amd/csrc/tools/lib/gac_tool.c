@@ -99,17 +99,22 @@ static double now_s(void) {
 static void *device_thread(void *arg) {
     gt_device *d = arg;
     const double t0 = now_s();
-    d->rc = gac_open(0, &d->ctx);
+    int rc = gac_open(0, &d->ctx);
     d->open_s = now_s() - t0;
-    if (d->rc == GAC_OK && d->mat)
-        d->rc = gac_set_scoring(d->ctx, d->mat, d->gap);
-    if (d->rc == GAC_OK)
-        d->rc = gac_genome_load_2bit(d->ctx, GAC_T, d->t2bit);
-    if (d->rc == GAC_OK)
-        d->rc = gac_genome_load_2bit(d->ctx, GAC_Q, d->q2bit);
+    if (rc == GAC_OK && d->mat)
+        rc = gac_set_scoring(d->ctx, d->mat, d->gap);
+    if (rc == GAC_OK)
+        rc = gac_genome_load_2bit(d->ctx, GAC_T, d->t2bit);
+    if (rc == GAC_OK)
+        rc = gac_genome_load_2bit(d->ctx, GAC_Q, d->q2bit);
     d->load_s = now_s() - t0 - d->open_s;
-    if (d->rc != GAC_OK) /* the error text is thread-local */
+    if (rc != GAC_OK) /* the error text is thread-local */
         snprintf(d->err, sizeof(d->err), "%s", gac_last_error());
+    pthread_mutex_lock(&d->mu);
+    d->rc = rc;
+    d->done = 1;
+    pthread_cond_broadcast(&d->cv);
+    pthread_mutex_unlock(&d->mu);
     return NULL;
 }
 
@@ -120,41 +125,74 @@ void gt_device_start(gt_device *d, const char *t2bit, const char *q2bit, const i
     d->q2bit = q2bit;
     d->mat = mat;
     d->gap = gap;
+    pthread_mutex_init(&d->mu, NULL);
+    pthread_cond_init(&d->cv, NULL);
+    pthread_attr_t at;
+    pthread_attr_init(&at);
+    pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
     pthread_t th;
-    if (pthread_create(&th, NULL, device_thread, d) != 0)
+    if (pthread_create(&th, &at, device_thread, d) != 0)
         gt_abort("can't start the device thread\n");
-    d->th = (unsigned long)th;
+    pthread_attr_destroy(&at);
     d->started = 1;
     g_live_dev = d;
 }
 
+/* wait until the bring-up thread has left the HIP runtime */
+static void device_wait_done(gt_device *d) {
+    pthread_mutex_lock(&d->mu);
+    while (!d->done)
+        pthread_cond_wait(&d->cv, &d->mu);
+    pthread_mutex_unlock(&d->mu);
+}
+
+/* registered helper threads (gt_helper_add); touched by the main thread only */
+#define GT_MAX_HELPERS 8
+static pthread_t g_helpers[GT_MAX_HELPERS];
+static int g_n_helpers;
+
+void gt_helper_add(pthread_t th) {
+    if (g_n_helpers == GT_MAX_HELPERS)
+        gt_abort("gt_helper_add: too many helper threads\n");
+    g_helpers[g_n_helpers++] = th;
+}
+
+void gt_helper_join(pthread_t th) {
+    for (int i = 0; i < g_n_helpers; ++i)
+        if (pthread_equal(g_helpers[i], th)) {
+            g_helpers[i] = g_helpers[--g_n_helpers];
+            break;
+        }
+    pthread_join(th, NULL);
+}
+
 static void join_live_device(void) {
+    /* helpers first: they may be waiting for the device themselves */
+    for (int i = 0; i < g_n_helpers; ++i)
+        if (!pthread_equal(pthread_self(), g_helpers[i]))
+            pthread_join(g_helpers[i], NULL);
+    g_n_helpers = 0;
     gt_device *d = g_live_dev;
     if (d && d->closing && !pthread_equal(pthread_self(), (pthread_t)d->close_th)) {
         pthread_join((pthread_t)d->close_th, NULL);
         d->closing = 0;
     }
-    if (d && d->started && !pthread_equal(pthread_self(), (pthread_t)d->th)) {
-        pthread_join((pthread_t)d->th, NULL);
-        d->started = 0;
-    }
+    if (d && d->started)
+        device_wait_done(d);
     g_live_dev = NULL;
 }
 
 gac_ctx *gt_device_wait(gt_device *d) {
-    if (d->started) {
-        pthread_join((pthread_t)d->th, NULL);
-        d->started = 0;
-    }
-    if (g_live_dev == d)
-        g_live_dev = NULL;
+    if (!d->started)
+        return NULL;
+    device_wait_done(d);
     return d->rc == GAC_OK ? d->ctx : NULL;
 }
 
 gac_ctx *gt_device_join(gt_device *d) {
-    gt_device_wait(d); /* (another thread may have waited already) */
-    if (d->rc == GAC_OK && !d->ctx)
+    if (!d->started)
         gt_abort("gt_device_join: device never started\n");
+    device_wait_done(d);
     if (d->rc != GAC_OK)
         gt_abort("%s\n", d->err);
     gt_verbose(2, "[stage] (overlapped) device open %.3f s, 2bit genomes to HBM %.3f s\n",

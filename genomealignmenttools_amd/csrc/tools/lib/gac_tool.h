@@ -5,6 +5,7 @@
 #ifndef GAC_TOOL_H
 #define GAC_TOOL_H
 
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 
@@ -40,15 +41,26 @@ typedef struct gt_device {
     int rc, started;
     double open_s, load_s;
     char err[1024];
-    unsigned long th; /* pthread_t */
+    /* bring-up completion: the (detached) device thread sets done under mu
+     * and broadcasts cv; any number of threads may wait for it */
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    int done;
     unsigned long close_th;
     int closing;
 } gt_device;
 void gt_device_start(gt_device *d, const char *t2bit, const char *q2bit, const int32_t mat[16],
                      const gac_gapcalc *gap);
+/* main thread only */
 gac_ctx *gt_device_join(gt_device *d);
-/* the same wait without the abort: NULL if the bring-up failed */
+/* the same wait without the abort: NULL if the bring-up failed.  Safe from
+ * any thread and any number of times (it only waits for completion). */
 gac_ctx *gt_device_wait(gt_device *d);
+/* Helper threads that may be inside the HIP runtime: gt_abort/gt_exit_ok
+ * join every registered thread (other than the caller) before the process
+ * exits.  gt_helper_join joins one and unregisters it (main thread). */
+void gt_helper_add(pthread_t th);
+void gt_helper_join(pthread_t th);
 /* Release a chain set and close the context on a helper thread (the host
  * writes its output meanwhile); gt_device_close_join waits for it. */
 void gt_device_close_async(gt_device *d, gac_ctx *ctx, gac_chainset *cs);

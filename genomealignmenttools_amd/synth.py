@@ -359,14 +359,19 @@ def concat_chains(parts: List[ChainArrays]) -> ChainArrays:
         blk_size=cat("blk_size"))
 
 
-def c5_case(seed: int = 1234, n_chains: int = 1_000_000, sizes_dir: Optional[str] = None):
+def c5_case(seed: int = 1234, n_chains: int = 1_000_000, sizes_dir: Optional[str] = None,
+            scale: float = 1.0, min_size: int = 20_000):
     """SURVEY §8(d) C5 at a stated chain count: every hg38 sequence (455) as
     target x every mm10 sequence (66) as query, chains per target sequence in
     proportion to its length, C2's chain model on each; one score-sorted set
-    (ids 1..n)."""
+    (ids 1..n).  scale < 1 shrinks every sequence (not below min_size) for
+    C5-shaped parity tests: same names, same sequence count."""
     here = sizes_dir or os.path.join(os.path.dirname(__file__), "data")
     hg = read_sizes(os.path.join(here, "hg38.chrom.sizes"))
     mm = read_sizes(os.path.join(here, "mm10.chrom.sizes"))
+    if scale != 1.0:
+        hg = {k: max(min_size, int(v * scale)) for k, v in hg.items()}
+        mm = {k: max(min_size, int(v * scale)) for k, v in mm.items()}
     tg = random_genome(hg, seed, n_frac=0.005, n_mean=20_000)
     qg = random_genome(mm, seed + 1, n_frac=0.005, n_mean=20_000)
     total = float(sum(hg.values()))

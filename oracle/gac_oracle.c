@@ -253,6 +253,12 @@ int or_subchain(const char *tseq, const char *qseq, const int *bt, const int *bq
                 long long *glob, long long *loc, int *ali) {
     const or_matrix *m = vm;
     int k, first = -1;
+    /* easy case (chain.c:499-505): a range covering the chain's extent is
+     * the whole chain -- every block, zero-size end blocks included */
+    if (nb > 0 && s <= bt[0] && e >= bt[nb - 1] + bs[nb - 1]) {
+        s = bt[0];
+        e = 0x7fffffff;
+    }
     for (k = 0; k < nb; ++k)
         if (bt[k] + bs[k] > s) {
             first = k;

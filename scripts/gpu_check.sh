@@ -8,7 +8,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 make -j16 all oracle > "$OUT/build.log" 2>&1 || { echo "build failed"; exit 1; }
-timeout -k 10 900 python -m pytest tests -x -q -m gpu > "$OUT/tests.log" 2>&1
+timeout -k 10 1000 python -u -m pytest tests -x -v -m gpu --timeout 900 --timeout-method thread > "$OUT/tests.log" 2>&1
 rc=$?
 echo "pytest rc=$rc" >> "$OUT/tests.log"
 tail -3 "$OUT/tests.log"
