@@ -160,6 +160,8 @@ _PROTOS = {
     "gac_net_build": (C.c_int, [C.POINTER(NetInput), C.POINTER(NetOpts), C.POINTER(C.c_void_p)]),
     "gac_net_build_sides": (C.c_int, [C.POINTER(NetInput), C.POINTER(NetOpts), C.c_int,
                                       C.POINTER(C.c_void_p)]),
+    "gac_net_build_subset": (C.c_int, [C.POINTER(NetInput), C.POINTER(NetOpts), C.c_void_p,
+                                       C.c_void_p, C.POINTER(C.c_void_p)]),
     "gac_net_free": (None, [C.c_void_p]),
     "gac_net_netted": (C.c_int64, [C.c_void_p]),
     "gac_net_fill_count": (C.c_int64, [C.c_void_p, C.c_int]),

@@ -958,6 +958,9 @@ int gac_net_build(const gac_net_input *in, const gac_net_opts *opt, gac_net **ou
     return gac_net_build_sides(in, opt, (1 << GAC_T) | (1 << GAC_Q), out);
 }
 
+static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides,
+                     const uint8_t *t_keep, const uint8_t *q_keep, gac_net **out);
+
 int gac_net_build_sides(const gac_net_input *in, const gac_net_opts *opt, int sides,
                         gac_net **out) {
     gac_clear_error();
@@ -965,6 +968,19 @@ int gac_net_build_sides(const gac_net_input *in, const gac_net_opts *opt, int si
         return gac_fail(GAC_E_ARG, "gac_net_build: NULL argument");
     if (sides <= 0 || (sides & ~((1 << GAC_T) | (1 << GAC_Q))))
         return gac_fail(GAC_E_ARG, "gac_net_build_sides: bad side mask %d", sides);
+    return net_build(in, opt, sides, NULL, NULL, out);
+}
+
+int gac_net_build_subset(const gac_net_input *in, const gac_net_opts *opt, const uint8_t *t_keep,
+                         const uint8_t *q_keep, gac_net **out) {
+    gac_clear_error();
+    if (!in || !opt || !out || !t_keep || !q_keep)
+        return gac_fail(GAC_E_ARG, "gac_net_build_subset: NULL argument");
+    return net_build(in, opt, (1 << GAC_T) | (1 << GAC_Q), t_keep, q_keep, out);
+}
+
+static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides,
+                     const uint8_t *t_keep, const uint8_t *q_keep, gac_net **out) {
     *out = NULL;
     gac_net *n = calloc(1, sizeof(*n));
     n->in = *in;
@@ -1040,10 +1056,12 @@ int gac_net_build_sides(const gac_net_input *in, const gac_net_opts *opt, int si
     J.ntask = 0;
     if (sides & (1 << GAC_T))
         for (int32_t k = 0; k < nt; ++k)
-            J.task[J.ntask++] = (net_task){GAC_T, k, tl + toff[k], toff[k + 1] - toff[k]};
+            if (!t_keep || t_keep[k])
+                J.task[J.ntask++] = (net_task){GAC_T, k, tl + toff[k], toff[k + 1] - toff[k]};
     if (sides & (1 << GAC_Q))
         for (int32_t k = 0; k < nq; ++k)
-            J.task[J.ntask++] = (net_task){GAC_Q, k, ql + qoff[k], qoff[k + 1] - qoff[k]};
+            if (!q_keep || q_keep[k])
+                J.task[J.ntask++] = (net_task){GAC_Q, k, ql + qoff[k], qoff[k + 1] - qoff[k]};
     qsort(J.task, (size_t)J.ntask, sizeof(net_task), net_task_cmp);
     atomic_init(&J.next, 0);
     atomic_init(&J.wid, 0);

@@ -7,8 +7,15 @@
  * target-side fill is rescored in ONE batched GPU call (gac_score_ranges),
  * replacing the per-fill chainSubsetOnT + chainCalcScore of subchainInfo
  * (:795-843). */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <fcntl.h>
 #include <math.h>
 #include <pthread.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
 #include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -22,6 +29,7 @@ static const gt_spec k_opts[] = {
     {"minSpace", GT_INT},      {"minFill", GT_INT},      {"minScore", GT_DOUBLE},
     {"inclHap", GT_BOOL},      {"rescore", GT_BOOL},     {"tNibDir", GT_STRING},
     {"qNibDir", GT_STRING},    {"scoreScheme", GT_STRING}, {"linearGap", GT_STRING},
+    {"nranks", GT_INT},        {"rank", GT_INT},         {"gpu", GT_INT},
     {NULL, 0},
 };
 
@@ -48,7 +56,11 @@ static void usage(int min_space, double min_score) {
         "   -tNibDir=fileName           target genome file (2bit)\n"
         "   -qNibDir=fileName           query genome file (2bit)\n"
         "   -scoreScheme=fileName       Read the scoring matrix from a blastz-format file\n"
-        "   -linearGap=<medium|loose|filename> Specify type of linearGap to use.\n",
+        "   -linearGap=<medium|loose|filename> Specify type of linearGap to use.\n"
+        "   -nranks=N -rank=R           multi-GPU run (one process per GPU, same node): rank R\n"
+        "                               nets its share of the chromosome sides; rank 0 writes\n"
+        "                               both nets once every rank's part is done\n"
+        "   -gpu=D                      device index (default: R with -nranks, else 0)\n",
         min_space, min_score);
 }
 
@@ -139,6 +151,217 @@ static void *pre_upload_thread(void *arg) {
     return NULL;
 }
 
+
+/* ---------------------------------------------------------------- ranks
+ * -nranks=N -rank=R: N processes (one per GPU of one node) run the same
+ * command.  A chromosome side's net depends only on the chains on that
+ * sequence (chainNet.c:557-679 add each chain to its own target and query
+ * trees), so the sides are dealt out to the ranks (LPT on aligned bases);
+ * rank R nets and rescores its sides and writes them to <net>.gacpart<R>;
+ * rank 0 waits for every part and assembles each net in sequence order. */
+typedef struct ranks {
+    int n, me;
+    const char *tnet, *qnet;
+} ranks;
+static ranks g_rk;
+
+static void part_name(char *buf, size_t cap, const char *net, int r, const char *suffix) {
+    snprintf(buf, cap, "%s.gacpart%d%s", net, r, suffix);
+}
+
+static void rank_abort_hook(void) { /* tell rank 0 this rank has failed */
+    char b[4096];
+    part_name(b, sizeof(b), g_rk.tnet, g_rk.me, ".failed");
+    const int fd = open(b, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd >= 0)
+        close(fd);
+}
+
+typedef struct side_job {
+    int side;
+    int32_t seq;
+    int64_t w;
+} side_job;
+
+static int side_job_cmp(const void *a, const void *b) {
+    const side_job *x = a, *y = b;
+    if (x->w != y->w)
+        return x->w > y->w ? -1 : 1;
+    if (x->side != y->side)
+        return x->side - y->side;
+    return (x->seq > y->seq) - (x->seq < y->seq);
+}
+
+/* keep[side][seq] for this rank; returns whether it owns a target side with
+ * chains */
+static int assign_sides(const gt_chains *c, int64_t n_net, const int32_t *tix, const int32_t *qix,
+                        int32_t nt, int32_t nq, uint8_t *tkeep, uint8_t *qkeep) {
+    int64_t *wt = calloc((size_t)nt + 1, 8), *wq = calloc((size_t)nq + 1, 8);
+    for (int64_t i = 0; i < n_net; ++i) {
+        int64_t a = 0;
+        for (int64_t b = c->blk_off[i]; b < c->blk_off[i + 1]; ++b)
+            a += c->bs[b];
+        wt[tix[i]] += a + 1;
+        wq[qix[i]] += a + 1;
+    }
+    side_job *J = malloc((size_t)(nt + nq + 1) * sizeof(side_job));
+    int64_t nj = 0;
+    for (int32_t k = 0; k < nt; ++k)
+        if (wt[k])
+            J[nj++] = (side_job){GAC_T, k, wt[k]};
+    for (int32_t k = 0; k < nq; ++k)
+        if (wq[k])
+            J[nj++] = (side_job){GAC_Q, k, wq[k]};
+    qsort(J, (size_t)nj, sizeof(side_job), side_job_cmp);
+    int64_t *load = calloc((size_t)g_rk.n, 8);
+    memset(tkeep, 0, (size_t)nt);
+    memset(qkeep, 0, (size_t)nq);
+    int own_t = 0;
+    for (int64_t j = 0; j < nj; ++j) {
+        int best = 0;
+        for (int r = 1; r < g_rk.n; ++r)
+            if (load[r] < load[best])
+                best = r;
+        load[best] += J[j].w;
+        if (best == g_rk.me) {
+            if (J[j].side == GAC_T) {
+                tkeep[J[j].seq] = 1;
+                own_t = 1;
+            } else {
+                qkeep[J[j].seq] = 1;
+            }
+        }
+    }
+    free(load);
+    free(J);
+    free(wt);
+    free(wq);
+    return own_t;
+}
+
+/* map a part file; sections[k] = "net" section of sequence k or empty */
+typedef struct part_map {
+    char *p;
+    size_t n;
+} part_map;
+
+static void map_part(const char *path, part_map *m) {
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0)
+        gt_abort("Can't open %s to read: %s", path, strerror(errno));
+    struct stat st;
+    fstat(fd, &st);
+    m->n = (size_t)st.st_size;
+    m->p = m->n ? mmap(NULL, m->n, PROT_READ, MAP_PRIVATE, fd, 0) : NULL;
+    if (m->n && m->p == MAP_FAILED)
+        gt_abort("mmap %s failed", path);
+    close(fd);
+}
+
+static void wait_parts(const char *net) {
+    const char *lim = getenv("GAC_RANK_TIMEOUT");
+    const double limit = lim ? atof(lim) : 3600.0;
+    struct timespec t0, t1, nap = {0, 500000};
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    char b[4096];
+    for (int r = 1; r < g_rk.n; ++r) {
+        part_name(b, sizeof(b), net, r, "");
+        for (;;) {
+            if (access(b, F_OK) == 0)
+                break;
+            char f[4096];
+            part_name(f, sizeof(f), g_rk.tnet, r, ".failed");
+            if (access(f, F_OK) == 0) {
+                unlink(f);
+                gt_abort("chainNet: rank %d failed", r);
+            }
+            clock_gettime(CLOCK_MONOTONIC, &t1);
+            if ((t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec) > limit)
+                gt_abort("chainNet: timed out waiting for rank %d's part %s", r, b);
+            nanosleep(&nap, NULL);
+        }
+    }
+}
+
+/* rank 0: <net> = rank 0's '#' lines + every sequence's section, sequence
+ * order, from the part of the rank that netted it */
+static void assemble_net(const char *net, const gt_names *names) {
+    part_map *pm = calloc((size_t)g_rk.n, sizeof(part_map));
+    char b[4096];
+    for (int r = 0; r < g_rk.n; ++r) {
+        part_name(b, sizeof(b), net, r, "");
+        map_part(b, &pm[r]);
+    }
+    /* section index: (start, end) per sequence */
+    const int32_t ns = names->n;
+    int64_t *sec = malloc((size_t)(ns ? ns : 1) * 2 * 8);
+    int32_t *own = malloc((size_t)(ns ? ns : 1) * 4);
+    for (int32_t k = 0; k < ns; ++k)
+        own[k] = -1;
+    size_t meta_end = 0;
+    for (int r = 0; r < g_rk.n; ++r) {
+        const char *p = pm[r].p;
+        const size_t n = pm[r].n;
+        size_t pos = 0;
+        while (pos < n && p[pos] == '#') { /* '#' lines (rank 0's are kept) */
+            const char *nl = memchr(p + pos, '\n', n - pos);
+            pos = nl ? (size_t)(nl - p) + 1 : n;
+        }
+        if (r == 0)
+            meta_end = pos;
+        int32_t cur = -1;
+        size_t cur0 = 0;
+        while (pos < n) {
+            const char *nl = memchr(p + pos, '\n', n - pos);
+            const size_t eol = nl ? (size_t)(nl - p) + 1 : n;
+            if (eol - pos > 4 && memcmp(p + pos, "net ", 4) == 0) {
+                if (cur >= 0) {
+                    sec[2 * cur] = (int64_t)cur0;
+                    sec[2 * cur + 1] = (int64_t)pos;
+                }
+                const char *nm = p + pos + 4;
+                const char *sp = memchr(nm, ' ', eol - pos - 4);
+                char name[1024];
+                const size_t len = sp ? (size_t)(sp - nm) : 0;
+                if (!len || len >= sizeof(name))
+                    gt_abort("chainNet: bad net line in part %d of %s", r, net);
+                memcpy(name, nm, len);
+                name[len] = 0;
+                cur = gt_names_find(names, name);
+                if (cur < 0 || own[cur] >= 0)
+                    gt_abort("chainNet: unexpected sequence %s in part %d of %s", name, r, net);
+                own[cur] = r;
+                cur0 = pos;
+            }
+            pos = eol;
+        }
+        if (cur >= 0) {
+            sec[2 * cur] = (int64_t)cur0;
+            sec[2 * cur + 1] = (int64_t)n;
+        }
+    }
+    FILE *f = gt_must_open(net, "w");
+    if (meta_end && fwrite(pm[0].p, 1, meta_end, f) != meta_end)
+        gt_abort("write error on %s", net);
+    for (int32_t k = 0; k < ns; ++k)
+        if (own[k] >= 0) {
+            const size_t len = (size_t)(sec[2 * k + 1] - sec[2 * k]);
+            if (fwrite(pm[own[k]].p + sec[2 * k], 1, len, f) != len)
+                gt_abort("write error on %s", net);
+        }
+    if (fclose(f) != 0)
+        gt_abort("close failed on %s", net);
+    for (int r = 0; r < g_rk.n; ++r) {
+        if (pm[r].n)
+            munmap(pm[r].p, pm[r].n);
+        part_name(b, sizeof(b), net, r, "");
+        unlink(b);
+    }
+    free(pm);
+    free(sec);
+    free(own);
+}
+
 int main(int argc, char *argv[]) {
     gt_stage("");
     int min_space = 25;
@@ -177,12 +400,35 @@ int main(int argc, char *argv[]) {
     }
     const char *chain_file = argv[1], *tsizes_file = argv[2], *qsizes_file = argv[3];
     const char *tnet = argv[4], *qnet = argv[5];
+    g_rk.n = gt_opt_int("nranks", 1);
+    g_rk.me = gt_opt_int("rank", 0);
+    g_rk.tnet = tnet;
+    g_rk.qnet = qnet;
+    if (g_rk.n < 1 || g_rk.me < 0 || g_rk.me >= g_rk.n)
+        gt_abort("-rank=%d is not in 0..%d (-nranks=%d)", g_rk.me, g_rk.n - 1, g_rk.n);
+    const int multi = g_rk.n > 1;
+    gt_set_gpu(gt_opt_int("gpu", multi ? g_rk.me : 0));
+    if (multi) {
+        if (!strcmp(tnet, "stdout") || !strcmp(qnet, "stdout"))
+            gt_abort("-nranks needs file names for both nets (not stdout)");
+        char b[4096];
+        const char *nets[2] = {tnet, qnet};
+        for (int k = 0; k < 2; ++k) { /* stale parts of an earlier run */
+            part_name(b, sizeof(b), nets[k], g_rk.me, "");
+            unlink(b);
+        }
+        part_name(b, sizeof(b), tnet, g_rk.me, ".failed");
+        unlink(b);
+        if (g_rk.me > 0)
+            gt_on_abort(rank_abort_hook);
+    }
 
     /* with -rescore the device and both genomes come up on a helper thread
-     * while the chains are read and netted */
+     * while the chains are read and netted (with -nranks once this rank knows
+     * it rescores target fills) */
     gt_device dev;
     memset(&dev, 0, sizeof(dev));
-    if (rescore)
+    if (rescore && !multi)
         gt_device_start(&dev, tnib, qnib, mat, gap);
 
     gt_sizes qs, ts;
@@ -223,9 +469,21 @@ int main(int argc, char *argv[]) {
                      tsizes_file);
     }
     gt_stage("chain checks");
+    uint8_t *tkeep = NULL, *qkeep = NULL;
+    if (multi) {
+        int64_t n_net = 0; /* the netting loop stops at the first chain below minScore */
+        while (n_net < c.n && c.score[n_net] >= min_score)
+            ++n_net;
+        tkeep = malloc((size_t)ts.names.n + 1);
+        qkeep = malloc((size_t)qs.names.n + 1);
+        const int own_t = assign_sides(&c, n_net, tix, qix, ts.names.n, qs.names.n, tkeep, qkeep);
+        if (rescore && own_t)
+            gt_device_start(&dev, tnib, qnib, mat, gap);
+        gt_stage("rank sides");
+    }
     pre_upload pu;
     memset(&pu, 0, sizeof(pu));
-    if (rescore) {
+    if (rescore && dev.started) {
         pu.dev = &dev;
         pu.c = &c;
         pu.started = pthread_create(&pu.th, NULL, pre_upload_thread, &pu) == 0;
@@ -256,7 +514,10 @@ int main(int argc, char *argv[]) {
     in.q_sizes = qs.size;
     gac_net_opts opt = {min_space, min_fill, min_score, incl_hap};
     gac_net *net = NULL;
-    gt_check(gac_net_build(&in, &opt, &net));
+    if (multi)
+        gt_check(gac_net_build_subset(&in, &opt, tkeep, qkeep, &net));
+    else
+        gt_check(gac_net_build(&in, &opt, &net));
     gt_stage("netting");
     gt_verbose(1, "Finishing nets\n");
 
@@ -382,10 +643,19 @@ int main(int argc, char *argv[]) {
         free(r);
         free(rix);
     }
-    /* the two nets are independent files: written concurrently */
+    /* the two nets are independent files: written concurrently (with
+     * -nranks: this rank's parts, renamed into place when complete) */
     gt_verbose(1, "writing %s\n", tnet);
     gt_verbose(1, "writing %s\n", qnet);
-    net_out wo[2] = {{net, GAC_T, tscores, tnet, &c, 0, 0}, {net, GAC_Q, NULL, qnet, &c, 0, 0}};
+    char tpart[4096], qpart[4096], tpart_tmp[4096], qpart_tmp[4096];
+    if (multi) {
+        part_name(tpart, sizeof(tpart), tnet, g_rk.me, "");
+        part_name(qpart, sizeof(qpart), qnet, g_rk.me, "");
+        part_name(tpart_tmp, sizeof(tpart_tmp), tnet, g_rk.me, ".tmp");
+        part_name(qpart_tmp, sizeof(qpart_tmp), qnet, g_rk.me, ".tmp");
+    }
+    net_out wo[2] = {{net, GAC_T, tscores, multi ? tpart_tmp : tnet, &c, 0, 0},
+                     {net, GAC_Q, NULL, multi ? qpart_tmp : qnet, &c, 0, 0}};
     pthread_t qth;
     if (pthread_create(&qth, NULL, write_net, &wo[1]) != 0)
         write_net(&wo[1]);
@@ -398,6 +668,18 @@ int main(int argc, char *argv[]) {
         if (wo[k].rc != GAC_OK)
             gt_abort("%s\n", wo[k].err);
     gt_stage("write nets");
+    if (multi) {
+        if (rename(qpart_tmp, qpart) != 0 || rename(tpart_tmp, tpart) != 0)
+            gt_abort("can't rename %s: %s", tpart_tmp, strerror(errno));
+        if (g_rk.me == 0) {
+            wait_parts(tnet);
+            wait_parts(qnet);
+            gt_stage("wait for ranks");
+            assemble_net(tnet, &ts.names);
+            assemble_net(qnet, &qs.names);
+            gt_stage("assemble nets");
+        }
+    }
     gt_device_close_join(&dev);
     gt_stage("device close (rest)");
     /* the net, chains and sizes are left to process exit (freeing millions

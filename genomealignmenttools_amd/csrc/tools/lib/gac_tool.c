@@ -22,8 +22,18 @@ static int g_verbose = 1;
 static void *g_live_dev; /* gt_device whose helper thread may still run HIP calls */
 static void join_live_device(void);
 
+static void (*g_abort_hook)(void);
+void gt_on_abort(void (*fn)(void)) { g_abort_hook = fn; }
+
+static int g_gpu; /* device index for gt_device_start */
+void gt_set_gpu(int gpu) { g_gpu = gpu; }
+
 void gt_abort(const char *fmt, ...) {
     va_list ap;
+    void (*hook)(void) = g_abort_hook;
+    g_abort_hook = NULL; /* (a failing hook must not recurse) */
+    if (hook)
+        hook();
     join_live_device(); /* never exit under a thread that is inside the HIP runtime */
     fflush(stdout);
     va_start(ap, fmt);
@@ -99,7 +109,7 @@ static double now_s(void) {
 static void *device_thread(void *arg) {
     gt_device *d = arg;
     const double t0 = now_s();
-    int rc = gac_open(0, &d->ctx);
+    int rc = gac_open(g_gpu, &d->ctx);
     d->open_s = now_s() - t0;
     if (rc == GAC_OK && d->mat)
         rc = gac_set_scoring(d->ctx, d->mat, d->gap);

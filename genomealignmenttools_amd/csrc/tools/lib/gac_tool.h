@@ -26,6 +26,10 @@ void gt_parallel(int n, void *(*fn)(void *), void *args, size_t stride);
 /* -verbose>=2: wall time since the previous gt_stage call, labelled */
 void gt_stage(const char *what);
 void gt_check(int rc); /* abort with gac_last_error() unless GAC_OK */
+/* fn runs once at the start of gt_abort (e.g. to tell other ranks) */
+void gt_on_abort(void (*fn)(void));
+/* device index gt_device_start opens (default 0) */
+void gt_set_gpu(int gpu);
 
 /* ---- device bring-up off the critical path ----
  * gt_device_start opens device 0, sets the scoring scheme and uploads both

@@ -386,6 +386,33 @@ def c5_case(seed: int = 1234, n_chains: int = 1_000_000, sizes_dir: Optional[str
     return tg, qg, ca
 
 
+def zero_end_blocks(ca: ChainArrays, every: int = 3) -> ChainArrays:
+    """Every `every`-th chain gets a zero-size block 3/2 bases before its
+    first block and 4/1 bases after its last (header span widened)."""
+    bt, bq, bs, off = [], [], [], [0]
+    tstart, tend = ca.tstart.copy(), ca.tend.copy()
+    qstart, qend = ca.qstart.copy(), ca.qend.copy()
+    for i in range(ca.n):
+        t, q, z = (x.astype(np.int64) for x in ca.blocks(i))
+        if i % every == 0 and t[0] >= 3 and q[0] >= 2 and \
+                t[-1] + z[-1] + 4 <= ca.tsize[i] and q[-1] + z[-1] + 1 <= ca.qsize[i]:
+            t = np.r_[t[0] - 3, t, t[-1] + z[-1] + 4]
+            q = np.r_[q[0] - 2, q, q[-1] + z[-1] + 1]
+            z = np.r_[0, z, 0]
+            tstart[i], qstart[i] = t[0], q[0]
+            tend[i], qend[i] = t[-1], q[-1]
+        bt.append(t)
+        bq.append(q)
+        bs.append(z)
+        off.append(off[-1] + len(t))
+    return ChainArrays(score=ca.score, tname=ca.tname, tsize=ca.tsize, tstart=tstart, tend=tend,
+                       qname=ca.qname, qsize=ca.qsize, qstrand=ca.qstrand, qstart=qstart,
+                       qend=qend, id=ca.id, blk_off=np.asarray(off, np.int64),
+                       blk_t=np.concatenate(bt).astype(np.int32),
+                       blk_q=np.concatenate(bq).astype(np.int32),
+                       blk_size=np.concatenate(bs).astype(np.int32))
+
+
 # ---------------------------------------------------------------- chainCleaner loci
 def _mutate(rng, codes: np.ndarray, div: float) -> np.ndarray:
     r = rng.random(len(codes))

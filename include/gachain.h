@@ -272,6 +272,12 @@ int gac_net_build(const gac_net_input *in, const gac_net_opts *opts, gac_net **o
  * and writes of a side not built fail with GAC_E_STATE. */
 int gac_net_build_sides(const gac_net_input *in, const gac_net_opts *opts, int sides,
                         gac_net **out);
+/* The same for a subset of chromosome sides: t_keep[k] / q_keep[k] != 0 =
+ * net target / query sequence k (a sequence's side depends only on the
+ * chains on it, so ranks of a multi-GPU run each net their own sequences;
+ * the unselected ones are written as if they held no chains). */
+int gac_net_build_subset(const gac_net_input *in, const gac_net_opts *opts, const uint8_t *t_keep,
+                         const uint8_t *q_keep, gac_net **out);
 void gac_net_free(gac_net *net);
 /* number of input chains consumed (netted or skipped) before stopping */
 int64_t gac_net_netted(const gac_net *net);

@@ -256,14 +256,16 @@ int or_subchain(const char *tseq, const char *qseq, const int *bt, const int *bq
     /* easy case (chain.c:499-505): a range covering the chain's extent is
      * the whole chain -- every block, zero-size end blocks included */
     if (nb > 0 && s <= bt[0] && e >= bt[nb - 1] + bs[nb - 1]) {
-        s = bt[0];
+        s = -0x7fffffff; /* nothing clipped, nothing left out */
         e = 0x7fffffff;
+        first = 0;
+    } else {
+        for (k = 0; k < nb; ++k)
+            if (bt[k] + bs[k] > s) {
+                first = k;
+                break;
+            }
     }
-    for (k = 0; k < nb; ++k)
-        if (bt[k] + bs[k] > s) {
-            first = k;
-            break;
-        }
     double score = 0, lscore = 0, lmax = 0;
     int aliBases = 0, kept = 0;
     int prevTe = 0, prevQe = 0;

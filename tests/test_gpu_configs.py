@@ -101,9 +101,46 @@ def test_c5_shaped_scorechain(c5_dir, mode):
     _same(p(f"sc.{mode}.ours"), p(f"sc.{mode}.ref"))
 
 
+@pytest.fixture(scope="module")
+def c5_ref_nets(c5_dir):
+    """The reference chainNet -rescore nets of the C5-shaped set (run once)."""
+    p = lambda x: os.path.join(c5_dir, x)
+    _run([_ref("chainNet"), p("in.chain"), p("t.sizes"), p("q.sizes"), p("ref.t.net"),
+          p("ref.q.net"), "-rescore", f"-tNibDir={p('t.2bit')}", f"-qNibDir={p('q.2bit')}",
+          "-linearGap=loose"])
+    return p("ref.t.net"), p("ref.q.net")
+
+
 @pytest.mark.timeout(900)
-def test_c5_shaped_chainnet_rescore(c5_dir):
-    _rescore_pair(c5_dir, "c5")
+def test_c5_shaped_chainnet_rescore(c5_dir, c5_ref_nets):
+    p = lambda x: os.path.join(c5_dir, x)
+    _run([_bin("chainNet"), p("in.chain"), p("t.sizes"), p("q.sizes"), p("c5.t.net"),
+          p("c5.q.net"), "-rescore", f"-tNibDir={p('t.2bit')}", f"-qNibDir={p('q.2bit')}",
+          "-linearGap=loose"])
+    _same(p("c5.t.net"), c5_ref_nets[0])
+    _same(p("c5.q.net"), c5_ref_nets[1])
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_c5_shaped_chainnet_rescore_ranks(c5_dir, c5_ref_nets, nranks):
+    """The multi-GPU mode (-nranks=N -rank=R, one process per rank): each
+    rank nets and rescores its share of the chromosome sides, rank 0
+    assembles both nets -- identical to the reference's single run.  (All
+    ranks on device 0 here: the box has one GPU.)"""
+    p = lambda x: os.path.join(c5_dir, x)
+    tag = f"mr{nranks}"
+    procs = [subprocess.Popen(
+        [_bin("chainNet"), p("in.chain"), p("t.sizes"), p("q.sizes"), p(f"{tag}.t.net"),
+         p(f"{tag}.q.net"), "-rescore", f"-tNibDir={p('t.2bit')}", f"-qNibDir={p('q.2bit')}",
+         "-linearGap=loose", f"-nranks={nranks}", f"-rank={r}", "-gpu=0"],
+        stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(nranks)]
+    for r, pr in enumerate(procs):
+        _, err = pr.communicate(timeout=600)
+        assert pr.returncode == 0, (r, err[-2000:])
+    _same(p(f"{tag}.t.net"), c5_ref_nets[0])
+    _same(p(f"{tag}.q.net"), c5_ref_nets[1])
+    assert not [f for f in os.listdir(c5_dir) if ".gacpart" in f]
 
 
 # ---------------------------------------------------------------- C2
@@ -158,42 +195,14 @@ def test_linear_gap_file(tool, tmp_path):
         _rescore_pair(str(tmp_path), "lg", [gap])
 
 
-def _zero_end_blocks(ca, every=3):
-    """Every `every`-th chain gets a zero-size block 3/2 bases before its
-    first block and 4/1 bases after its last (header span widened)."""
-    from genomealignmenttools_amd.chainfile import ChainArrays
-    bt, bq, bs, off = [], [], [], [0]
-    tstart, tend = ca.tstart.copy(), ca.tend.copy()
-    qstart, qend = ca.qstart.copy(), ca.qend.copy()
-    for i in range(ca.n):
-        t, q, z = (x.astype(np.int64) for x in ca.blocks(i))
-        if i % every == 0 and t[0] >= 3 and q[0] >= 2 and \
-                t[-1] + z[-1] + 4 <= ca.tsize[i] and q[-1] + z[-1] + 1 <= ca.qsize[i]:
-            t = np.r_[t[0] - 3, t, t[-1] + z[-1] + 4]
-            q = np.r_[q[0] - 2, q, q[-1] + z[-1] + 1]
-            z = np.r_[0, z, 0]
-            tstart[i], qstart[i] = t[0], q[0]
-            tend[i], qend[i] = t[-1], q[-1]
-        bt.append(t)
-        bq.append(q)
-        bs.append(z)
-        off.append(off[-1] + len(t))
-    return ChainArrays(score=ca.score, tname=ca.tname, tsize=ca.tsize, tstart=tstart, tend=tend,
-                       qname=ca.qname, qsize=ca.qsize, qstrand=ca.qstrand, qstart=qstart,
-                       qend=qend, id=ca.id, blk_off=np.asarray(off, np.int64),
-                       blk_t=np.concatenate(bt).astype(np.int32),
-                       blk_q=np.concatenate(bq).astype(np.int32),
-                       blk_size=np.concatenate(bs).astype(np.int32))
-
-
 def test_zero_size_end_blocks(tmp_path):
     """Chains whose first/last block has size 0: a full-chain query is
     chainFastSubsetOnT's easy case (kent/src/lib/chain.c:499-505), so those
     blocks and their gaps count in scoreChain's global and local scores."""
-    from genomealignmenttools_amd import chainfile
+    from genomealignmenttools_amd import chainfile, synth
     d = _synth(12)
     p = lambda x: os.path.join(d, x)
-    ca = _zero_end_blocks(chainfile.read_chains(p("in.chain")))
+    ca = synth.zero_end_blocks(chainfile.read_chains(p("in.chain")))
     chainfile.write_chains(ca, str(tmp_path / "in.chain"))
     for flag in (["-returnOnlyScoreAndCoords"], ["-forceLocalScore"], []):
         args = [tmp_path / "in.chain", p("t.2bit"), p("q.2bit")]
@@ -239,7 +248,7 @@ def test_chainnet_rescore_missing_sequence(tmp_path):
 def test_chainnet_rescore_no_partial_fills(tmp_path):
     """-rescore where every printed fill covers its whole chain: nothing is
     rescored, the genomes are never read."""
-    from genomealignmenttools_amd import chainfile
+    from genomealignmenttools_amd import chainfile, synth
     d = _synth(12)
     p = lambda x: os.path.join(d, x)
     ca = chainfile.read_chains(p("in.chain"))

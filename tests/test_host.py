@@ -275,3 +275,70 @@ def test_netfilter_nonnested_vs_reference(net, case):
                         os.path.join(d, f"{net}.net")] + opts, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     assert r.stdout == open(os.path.join(d, f"{net}.{case}.out")).read()
+
+
+def _c5_small(tmp_path):
+    from genomealignmenttools_amd import chainfile, synth
+    tg, qg, ca = synth.c5_case(seed=77, n_chains=6000, scale=0.002, min_size=5000)
+    d = str(tmp_path)
+    synth.write_sizes(tg.sizes, os.path.join(d, "t.sizes"))
+    synth.write_sizes(qg.sizes, os.path.join(d, "q.sizes"))
+    with open(os.path.join(d, "in.chain"), "w") as f:
+        f.write("# C5-shaped, seed 77\n")
+        chainfile.write_chains(ca, f)
+    return d
+
+
+@pytest.mark.parametrize("nranks", [2, 5])
+def test_chainnet_ranks_vs_reference(nranks, tmp_path):
+    """chainNet -nranks=N -rank=R (one process per rank; here without
+    -rescore, so no device): every rank nets its share of the 455 + 66
+    chromosome sides, rank 0 assembles the nets -- identical to the
+    reference's single-process nets, '#' lines included."""
+    from genomealignmenttools_amd._lib import BIN_DIR
+    from oracle.oracle import have_ref, ref_tool
+    d = _c5_small(tmp_path)
+    p = lambda x: os.path.join(d, x)
+    args = [p("in.chain"), p("t.sizes"), p("q.sizes")]
+    procs = [subprocess.Popen([os.path.join(BIN_DIR, "chainNet")] + args +
+                              [p("m.t.net"), p("m.q.net"), "-minScore=0", f"-nranks={nranks}",
+                               f"-rank={r}"], stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+             for r in range(nranks)]
+    for pr in procs:
+        _, err = pr.communicate(timeout=120)
+        assert pr.returncode == 0, err
+    assert not [f for f in os.listdir(d) if ".gacpart" in f]
+    r = subprocess.run([os.path.join(BIN_DIR, "chainNet")] + args +
+                       [p("one.t.net"), p("one.q.net"), "-minScore=0"], capture_output=True)
+    assert r.returncode == 0
+    assert filecmp.cmp(p("m.t.net"), p("one.t.net"), shallow=False)
+    assert filecmp.cmp(p("m.q.net"), p("one.q.net"), shallow=False)
+    assert open(p("m.t.net")).readline() == "# C5-shaped, seed 77\n"
+    if have_ref():
+        r = subprocess.run([ref_tool("chainNet")] + args + [p("ref.t.net"), p("ref.q.net"),
+                                                           "-minScore=0"], capture_output=True)
+        assert r.returncode == 0
+        assert filecmp.cmp(p("m.t.net"), p("ref.t.net"), shallow=False)
+        assert filecmp.cmp(p("m.q.net"), p("ref.q.net"), shallow=False)
+
+
+def test_chainnet_ranks_failure(tmp_path):
+    """A rank that fails makes rank 0 fail too (errAbort status 255), no hang
+    and no half-assembled output; bad -rank values are rejected."""
+    from genomealignmenttools_amd._lib import BIN_DIR
+    d = _c5_small(tmp_path)
+    p = lambda x: os.path.join(d, x)
+    with open(p("bad.chain"), "w") as f:
+        f.write("chain 10 chr1 5 + 0 1\n")
+    tool = os.path.join(BIN_DIR, "chainNet")
+    procs = [subprocess.Popen([tool, p("in.chain" if r == 0 else "bad.chain"), p("t.sizes"),
+                               p("q.sizes"), p("m.t.net"), p("m.q.net"), "-nranks=2",
+                               f"-rank={r}"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                              text=True, env=dict(os.environ, GAC_RANK_TIMEOUT="60"))
+             for r in range(2)]
+    outs = [pr.communicate(timeout=120) for pr in procs]
+    assert procs[1].returncode == 255
+    assert procs[0].returncode == 255 and "rank 1 failed" in outs[0][1]
+    r = subprocess.run([tool, p("in.chain"), p("t.sizes"), p("q.sizes"), "a", "b", "-nranks=2",
+                        "-rank=2"], capture_output=True, text=True)
+    assert r.returncode == 255 and "-rank=2" in r.stderr
