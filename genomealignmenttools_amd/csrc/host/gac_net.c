@@ -22,6 +22,7 @@
 #define _GNU_SOURCE
 #include "gac_host.h"
 
+#include <sched.h>
 #include <stdatomic.h>
 #include <math.h>
 #include <stdio.h>
@@ -545,8 +546,14 @@ static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int32_t chai
         f->start = start;
         f->end = end;
         f->chain = chain;
-        f->next = sgap->fill_head;
-        sgap->fill_head = f;
+        /* slAddHead onto the space's gap; region workers of one chromosome
+         * side (net_regions) may share the gap, so the push is atomic.  The
+         * order does not matter: finishNet sorts a gap's fills by start. */
+        nfill *h = __atomic_load_n(&sgap->fill_head, __ATOMIC_RELAXED);
+        do
+            f->next = h;
+        while (!__atomic_compare_exchange_n(&sgap->fill_head, &h, f, 1, __ATOMIC_RELEASE,
+                                            __ATOMIC_RELAXED));
         n->it_n = 0;
         if (start - sstart >= net->opt.min_space)
             it_push(n, sstart, start, sgap);
@@ -583,56 +590,99 @@ static int is_haplotype(const char *name) {
     return strstr(name, "_hap") != NULL || strstr(name, "_alt") != NULL;
 }
 
+/* Blocks of a chain that can touch spaces inside [A, B) (the whole chain
+ * when A/B are INT32_MIN/MAX): those ending after A and starting before B,
+ * plus one neighbour on each side, as an index range [*lo, *hi) over the
+ * side's + strand block order, whose starts st(i) / ends en(i) ascend.  Every
+ * space of a region lies inside [A, B), so innerBounds, the gaps strictly
+ * inside a space and findSpaces' skips over chain gaps only ever look at
+ * these blocks: a region worker builds just this slice of a long chain. */
+#define SLICE(st, en)                                                                      \
+    do {                                                                                   \
+        int l = 0, h = nb;                                                                 \
+        while (l < h) { /* first block ending after A */                                   \
+            const int m = (l + h) >> 1;                                                    \
+            if ((en(m)) > A) h = m;                                                        \
+            else l = m + 1;                                                                \
+        }                                                                                  \
+        *lo = l > 0 ? l - 1 : 0;                                                           \
+        h = nb;                                                                            \
+        while (l < h) { /* first block starting at or after B */                           \
+            const int m = (l + h) >> 1;                                                    \
+            if ((st(m)) >= B) h = m;                                                       \
+            else l = m + 1;                                                                \
+        }                                                                                  \
+        *hi = l < nb ? l + 1 : nb;                                                         \
+    } while (0)
+
 /* addChainQ (chainNet.c:610-679) */
-static void add_chain_q(const gac_net *net, nwork *n, int64_t c) {
+static void add_chain_q(const gac_net *net, nwork *n, int64_t c, nchrom *qc, int A, int B) {
     const gac_net_input *in = &net->in;
     const int64_t b0 = in->blk_off[c];
     const int nb = (int)(in->blk_off[c + 1] - b0);
     const int32_t *bt = in->blk_t + b0, *bq = in->blk_q + b0, *bs = in->blk_size + b0;
     const int minus = in->q_strand[c] != 0;
     const int qsize = in->q_sizes[in->q_seq[c]];
-    ensure_rev(n, nb);
-    nchrom *qc = &net->chroms[GAC_Q][in->q_seq[c]];
     int qs = in->q_start[c], qe = in->q_end[c];
+    int l0 = 0, l1 = nb, *lo = &l0, *hi = &l1;
+    if (A != INT32_MIN || B != INT32_MAX) {
+        if (!minus) {
+#define QST(i) bq[i]
+#define QEN(i) (bq[i] + bs[i])
+            SLICE(QST, QEN);
+        } else { /* reversed order: block i of the list is j = nb-1-i */
+#define RST(i) (qsize - (bq[nb - 1 - (i)] + bs[nb - 1 - (i)]))
+#define REN(i) (qsize - bq[nb - 1 - (i)])
+            SLICE(RST, REN);
+        }
+    }
+    const int m = l1 - l0;
+    ensure_rev(n, m);
     if (!minus) {
-        for (int b = 0; b < nb; ++b) {
-            n->rs[b] = bq[b];
-            n->re[b] = bq[b] + bs[b];
+        for (int b = l0; b < l1; ++b) {
+            n->rs[b - l0] = bq[b];
+            n->re[b - l0] = bq[b] + bs[b];
             if (b + 1 < nb) {
-                n->ros[b] = bt[b] + bs[b];
-                n->roe[b] = bt[b + 1];
+                n->ros[b - l0] = bt[b] + bs[b];
+                n->roe[b - l0] = bt[b + 1];
             }
         }
     } else {
         int t = qs;
         qs = qsize - qe;
         qe = qsize - t;
-        for (int i = 0; i < nb; ++i) {
+        for (int i = l0; i < l1; ++i) {
             int j = nb - 1 - i; /* original index */
-            n->rs[i] = qsize - (bq[j] + bs[j]);
-            n->re[i] = qsize - bq[j];
+            n->rs[i - l0] = qsize - (bq[j] + bs[j]);
+            n->re[i - l0] = qsize - bq[j];
             if (i + 1 < nb) { /* block = j, next = j-1 */
-                n->ros[i] = bt[j - 1];
-                n->roe[i] = bt[j] + bs[j];
+                n->ros[i - l0] = bt[j - 1];
+                n->roe[i - l0] = bt[j] + bs[j];
             }
         }
     }
-    add_chain_side(net, n, qc, (int32_t)c, nb, n->rs, n->re, n->ros, n->roe, qs, qe);
+    add_chain_side(net, n, qc, (int32_t)c, m, n->rs, n->re, n->ros, n->roe, qs, qe);
 }
 
 /* addChainT (chainNet.c:557-608) */
-static void add_chain_t(const gac_net *net, nwork *n, int64_t c) {
+static void add_chain_t(const gac_net *net, nwork *n, int64_t c, nchrom *tc, int A, int B) {
     const gac_net_input *in = &net->in;
     const int64_t b0 = in->blk_off[c];
     const int nb = (int)(in->blk_off[c + 1] - b0);
     const int32_t *bt = in->blk_t + b0, *bq = in->blk_q + b0, *bs = in->blk_size + b0;
     const int minus = in->q_strand[c] != 0;
     const int qsize = in->q_sizes[in->q_seq[c]];
-    ensure_rev(n, nb);
-    nchrom *tc = &net->chroms[GAC_T][in->t_seq[c]];
-    for (int b = 0; b < nb; ++b) {
-        n->rs[b] = bt[b];
-        n->re[b] = bt[b] + bs[b];
+    int l0 = 0, l1 = nb, *lo = &l0, *hi = &l1;
+    if (A != INT32_MIN || B != INT32_MAX) {
+#define TST(i) bt[i]
+#define TEN(i) (bt[i] + bs[i])
+        SLICE(TST, TEN);
+    }
+    const int m = l1 - l0;
+    ensure_rev(n, m);
+    for (int b = l0; b < l1; ++b) {
+        n->rs[b - l0] = bt[b];
+        n->re[b - l0] = bt[b] + bs[b];
         if (b + 1 < nb) {
             int qs = bq[b] + bs[b], qe = bq[b + 1];
             if (minus) {
@@ -640,11 +690,11 @@ static void add_chain_t(const gac_net *net, nwork *n, int64_t c) {
                 qs = qsize - qe;
                 qe = qsize - t;
             }
-            n->ros[b] = qs;
-            n->roe[b] = qe;
+            n->ros[b - l0] = qs;
+            n->roe[b - l0] = qe;
         }
     }
-    add_chain_side(net, n, tc, (int32_t)c, nb, n->rs, n->re, n->ros, n->roe, in->t_start[c],
+    add_chain_side(net, n, tc, (int32_t)c, m, n->rs, n->re, n->ros, n->roe, in->t_start[c],
                    in->t_end[c]);
 }
 
@@ -837,21 +887,66 @@ void gac_net_free(gac_net *n) {
     free(n);
 }
 
-/* finishNet in three parallel phases: (A) per chromosome side, the root
- * gap's fills sorted; (B) per run of consecutive top-level fills (their
- * subtrees are independent), the subtrees sorted into the run's own
- * pre-order list (the runs are concatenated in order afterwards); (C) the
- * other-side ranges of every fill, in balanced chunks. */
-typedef struct fin_task {
-    int side;
-    int32_t chrom, f0, f1; /* top-level fills [f0, f1) of the chromosome's root gap */
-} fin_task;
+/* finishNet in three parallel phases:
+ * (A) per chromosome side: the root gap's fills sorted, then the top of the
+ *     fill tree (fills of levels 0 and 1, their gaps' fills sorted) walked in
+ *     pre-order into a skeleton: FILL items, and GAP items standing for the
+ *     whole subtree under a gap of a level-1 fill;
+ * (B) the GAP subtrees (independent), in chunks over all threads: sorted
+ *     into per-chunk pre-order lists (one long chain's fill can hold most of
+ *     a chromosome, so its subtrees are the unit, not the top-level fills);
+ * the pre-order index is the skeletons with the subtree lists spliced in;
+ * (C) the other-side ranges of every fill, in balanced chunks. */
+#define SKEL_DEPTH 0 /* fills of levels 0..SKEL_DEPTH are skeleton FILL items */
+
+typedef struct sk_item {
+    nfill *f;    /* a fill in the skeleton, or */
+    ngap *g;     /* a gap whose subtree a phase-B chunk orders */
+    int64_t cnt; /* (GAP) fills in that subtree */
+} sk_item;
+
+typedef struct skel {
+    sk_item *it;
+    int64_t n, cap;
+} skel;
+
+static void sk_push(skel *k, nfill *f, ngap *g) {
+    if (k->n == k->cap) {
+        k->cap = k->cap ? k->cap * 2 : 256;
+        k->it = realloc(k->it, (size_t)k->cap * sizeof(sk_item));
+    }
+    k->it[k->n++] = (sk_item){f, g, 0};
+}
+
+/* finish_fill's pre-order walk down to SKEL_DEPTH */
+static void skel_fill(nwork *w, skel *k, nfill *f) {
+    sk_push(k, f, NULL);
+    for (int i = 0; i < f->n_gaps; ++i) {
+        f->gaps[i]->pfill = f;
+        f->gaps[i]->pidx = i;
+    }
+    for (int i = 0; i < f->n_gaps; ++i) {
+        ngap *g = f->gaps[i];
+        if (f->level < SKEL_DEPTH) {
+            sort_gap_fills(w, g);
+            for (int j = 0; j < g->n_fills; ++j)
+                skel_fill(w, k, g->fills[j]);
+        } else if (g->fill_head) {
+            sk_push(k, NULL, g);
+        } else {
+            g->n_fills = 0;
+            g->fills = NULL;
+        }
+    }
+}
 
 typedef struct fin_job {
     gac_net *n;
     int phase;
-    fin_task *task; /* phase B */
-    fin_ctx *x;     /* [ntask] */
+    skel *sk;          /* [n_chroms[T] + n_chroms[Q]]: T chromosomes, then Q */
+    sk_item **gi;      /* every GAP item, output order */
+    int64_t n_gi, per; /* phase B chunk = per consecutive GAP items */
+    fin_ctx *x;        /* [chunks] */
     int64_t ntask;
     _Atomic int64_t next;
     _Atomic int wid;
@@ -885,8 +980,11 @@ static void *fin_thread(void *arg) {
                 break;
             const int side = k < n->n_chroms[GAC_T] ? GAC_T : GAC_Q;
             nchrom *c = &n->chroms[side][side == GAC_T ? k : k - n->n_chroms[GAC_T]];
-            if (c->root)
-                sort_gap_fills(w, c->root);
+            if (!c->root)
+                continue;
+            sort_gap_fills(w, c->root);
+            for (int j = 0; j < c->root->n_fills; ++j)
+                skel_fill(w, &F->sk[k], c->root->fills[j]);
         }
         return NULL;
     }
@@ -894,14 +992,15 @@ static void *fin_thread(void *arg) {
         const int64_t k = atomic_fetch_add(&F->next, 1);
         if (k >= F->ntask)
             break;
-        const fin_task *t = &F->task[k];
-        const ngap *root = n->chroms[t->side][t->chrom].root;
         fin_ctx *x = &F->x[k];
         x->n = n;
         x->w = w;
-        x->side = t->side;
-        for (int32_t i = t->f0; i < t->f1; ++i)
-            finish_fill(x, root->fills[i]);
+        const int64_t a = k * F->per, b = a + F->per < F->n_gi ? a + F->per : F->n_gi;
+        for (int64_t i = a; i < b; ++i) {
+            const int64_t before = x->n_ord;
+            finish_gap(x, F->gi[i]->g);
+            F->gi[i]->cnt = x->n_ord - before;
+        }
     }
     return NULL;
 }
@@ -922,34 +1021,388 @@ static int net_task_cmp(const void *a, const void *b) {
     return (x->chrom > y->chrom) - (x->chrom < y->chrom);
 }
 
+/* add chain c to side `side` of its sequence, whose space index is ch;
+ * [A, B): the region ch covers (INT32_MIN/MAX: the whole sequence) */
+static void add_chain(const gac_net *net, nwork *w, int side, int64_t c, nchrom *ch, int A, int B) {
+    if (side == GAC_T)
+        add_chain_t(net, w, c, ch, A, B);
+    else
+        add_chain_q(net, w, c, ch, A, B);
+}
+
+/* a chain's range on one side (+ strand coordinates) */
+static void chain_span(const gac_net *net, int side, int64_t c, int *s, int *e) {
+    const gac_net_input *in = &net->in;
+    if (side == GAC_T) {
+        *s = in->t_start[c];
+        *e = in->t_end[c];
+    } else if (in->q_strand[c]) {
+        const int qsize = in->q_sizes[in->q_seq[c]];
+        *s = qsize - in->q_end[c];
+        *e = qsize - in->q_start[c];
+    } else {
+        *s = in->q_start[c];
+        *e = in->q_end[c];
+    }
+}
+
+/* ---- one chromosome side netted by many threads ----
+ * The open spaces of a side are disjoint, and every later space lies inside
+ * a current one (a filled space is replaced by its remnants and the chain's
+ * gaps inside it).  So once no current space contains a point P strictly
+ * inside it, no future space will: the chromosome splits at such points into
+ * regions whose space sets evolve independently.  A chain only acts on the
+ * spaces its range overlaps, space by space (innerBounds, fillSpace and the
+ * remnant/gap tests see one space and the chain's own blocks), so netting
+ * every region's spaces with the chains overlapping that region, each region
+ * in score order, makes exactly the fills and spaces of the sequential
+ * chainNet loop (chainNet.c:557-679); fills only meet again in their parent
+ * gaps' lists, which finishNet sorts by start.
+ *
+ * net_regions: the first chains go through sequentially (they are the long,
+ * high-scoring ones that cut the chromosome up), the region cuts are then
+ * placed at space ends near evenly spaced quantiles of the remaining chains'
+ * work, and the regions become tasks for every thread. */
+typedef struct region {
+    nchrom ch;          /* its own space index (built by the worker that nets it) */
+    const sitem *sp;    /* its spaces, in order */
+    int64_t n_sp;
+    int64_t *chains;    /* remaining chains overlapping it, in order */
+    int64_t n_chains;
+    int64_t work;
+    int side;
+    int a, b;           /* [a, b): its part of the sequence */
+} region;
+
+typedef struct big_net {
+    net_task *t;
+    int64_t m;          /* chains netted sequentially first */
+    sitem *spaces;      /* all spaces after the prefix */
+    int64_t *lists;     /* region chain lists, back to back */
+    region *reg;
+    int32_t n_reg;
+} big_net;
+
+/* bulk-load sorted spaces into an empty index of c in w's pools */
+static void sp_bulk(nwork *w, nchrom *c, const sitem *it, int64_t n) {
+    if (n == 0) {
+        c->sroot = sp_new_leaf(w);
+        c->height = 0;
+        return;
+    }
+    const int64_t nl = (n + SP_FILL - 1) / SP_FILL;
+    int32_t *lvl = malloc((size_t)nl * 4);
+    int64_t *key = malloc((size_t)nl * 8);
+    int32_t prev = -1;
+    for (int64_t j = 0; j < nl; ++j) {
+        const int64_t lo = n * j / nl, hi = n * (j + 1) / nl;
+        const int32_t l = sp_new_leaf(w);
+        sleaf *L = &w->lf[l];
+        for (int64_t k = lo; k < hi; ++k) {
+            L->start[k - lo] = it[k].start;
+            L->end[k - lo] = it[k].end;
+            L->gap[k - lo] = it[k].gap;
+        }
+        L->n = (int32_t)(hi - lo);
+        L->prev = prev;
+        if (prev >= 0)
+            w->lf[prev].next = l;
+        prev = l;
+        lvl[j] = l;
+        key[j] = spkey(it[lo].start, it[lo].end);
+    }
+    int64_t cnt = nl;
+    int h = 0;
+    while (cnt > 1) {
+        const int64_t np = (cnt + SP_FILL - 1) / SP_FILL;
+        for (int64_t j = 0; j < np; ++j) {
+            const int64_t lo = cnt * j / np, hi = cnt * (j + 1) / np;
+            const int32_t x = sp_new_inner(w);
+            snode *s = &w->in[x];
+            for (int64_t k = lo; k < hi; ++k) {
+                s->child[k - lo] = lvl[k];
+                s->key[k - lo] = k == lo ? 0 : key[k];
+            }
+            s->n = (int32_t)(hi - lo);
+            lvl[j] = x;
+            key[j] = key[lo];
+        }
+        cnt = np;
+        ++h;
+    }
+    c->sroot = lvl[0];
+    c->height = h;
+    free(lvl);
+    free(key);
+}
+
+/* every space of c in order (leaf chain from the leftmost leaf) */
+static sitem *sp_all(const nwork *w, const nchrom *c, int64_t *pn) {
+    int32_t l = sp_descend(w, c, INT64_MIN, NULL, NULL);
+    int64_t n = 0, cap = 1024;
+    sitem *out = malloc((size_t)cap * sizeof(sitem));
+    for (; l >= 0; l = w->lf[l].next) {
+        const sleaf *L = &w->lf[l];
+        for (int i = 0; i < L->n; ++i) {
+            if (n == cap) {
+                cap *= 2;
+                out = realloc(out, (size_t)cap * sizeof(sitem));
+            }
+            out[n++] = (sitem){L->start[i], L->end[i], L->gap[i]};
+        }
+    }
+    *pn = n;
+    return out;
+}
+
+static int64_t upper_bound32(const int32_t *a, int64_t n, int32_t v) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a[mid] <= v)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+/* work of chain c inside [a, b): a region builds the block slice there and
+ * scans the spaces its blocks reach */
+static int64_t chain_work_in(const gac_net *net, int side, int64_t c, int a, int b) {
+    int cs, ce;
+    chain_span(net, side, c, &cs, &ce);
+    const int64_t nb = net->in.blk_off[c + 1] - net->in.blk_off[c];
+    const int64_t lo = cs > a ? cs : a, hi = ce < b ? ce : b;
+    if (hi <= lo || ce <= cs)
+        return 8;
+    return 8 + nb * (hi - lo) / (ce - cs);
+}
+
+/* Region cuts for the chains after the first B->m: up to want-1 cut points
+ * near equal quantiles of their work along the sequence, each moved to the
+ * nearer end of the space holding it (no space may straddle a cut).  Returns
+ * the region count; *pmax / *ptot = the largest region's / all work. */
+static int32_t place_cuts(const gac_net *net, const big_net *B, const sitem *sp, int64_t nsp,
+                          int32_t want, int size, int32_t *cuts, int64_t *pmax, int64_t *ptot) {
+    const net_task *t = B->t;
+    const int64_t rest = t->n - B->m;
+    /* work density: each chain's blocks spread evenly over its span, on a
+     * grid of 4096 bins */
+    enum { NB = 4096 };
+    int64_t *bin = calloc(NB, 8), tot = 0;
+    const double scale = (double)NB / (size > 0 ? size : 1);
+    for (int64_t i = 0; i < rest; ++i) {
+        const int64_t c = t->chains[B->m + i];
+        int cs, ce;
+        chain_span(net, t->side, c, &cs, &ce);
+        const int64_t w = 8 + (net->in.blk_off[c + 1] - net->in.blk_off[c]);
+        int b0 = (int)(cs * scale), b1 = (int)((ce > cs ? ce - 1 : cs) * scale);
+        b0 = b0 < 0 ? 0 : (b0 >= NB ? NB - 1 : b0);
+        b1 = b1 < b0 ? b0 : (b1 >= NB ? NB - 1 : b1);
+        const int64_t per = w / (b1 - b0 + 1);
+        for (int k = b0; k <= b1; ++k)
+            bin[k] += per;
+        bin[b0] += w - per * (b1 - b0 + 1);
+        tot += w;
+    }
+    int32_t nc = 0;
+    int64_t acc = 0;
+    int k = 0;
+    for (int32_t j = 1; j < want && tot > 0; ++j) {
+        const int64_t target = tot * j / want;
+        while (k < NB && acc + bin[k] <= target)
+            acc += bin[k++];
+        if (k >= NB)
+            break;
+        int32_t x = (int32_t)((double)k / scale);
+        int64_t lo = 0, hi = nsp; /* last space with start <= x */
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (sp[mid].start <= x)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        if (lo > 0) {
+            const sitem *S = &sp[lo - 1];
+            if (S->start < x && x < S->end)
+                x = (x - S->start <= S->end - x) ? S->start : S->end;
+        }
+        if (x <= 0 || x >= size || (nc && x <= cuts[nc - 1]))
+            continue;
+        cuts[nc++] = x;
+    }
+    free(bin);
+    /* region work */
+    int64_t *rw = calloc((size_t)nc + 1, 8), mx = 0;
+    for (int64_t i = 0; i < rest; ++i) {
+        const int64_t c = t->chains[B->m + i];
+        int cs, ce;
+        chain_span(net, t->side, c, &cs, &ce);
+        const int64_t a = upper_bound32(cuts, nc, cs), b = upper_bound32(cuts, nc, ce > cs ? ce - 1 : cs);
+        for (int64_t r = a; r <= b; ++r)
+            rw[r] += chain_work_in(net, t->side, c, r ? cuts[r - 1] : 0, r < nc ? cuts[r] : size);
+    }
+    for (int32_t r = 0; r <= nc; ++r)
+        mx = rw[r] > mx ? rw[r] : mx;
+    free(rw);
+    *pmax = mx;
+    *ptot = tot;
+    return nc + 1;
+}
+
+/* thread 0: the sequential prefix of a big side and its regions */
+static void big_prefix(gac_net *n, nwork *w, big_net *B, int nthreads) {
+    net_task *t = B->t;
+    nchrom *c = &n->chroms[t->side][t->chrom];
+    c->root = gap_new(w, 0, c->size, 0, 0);
+    c->root->pidx = t->chrom;
+    sp_init(w, c, 0, c->size, c->root);
+    const int32_t want = 4 * nthreads;
+    int32_t *cuts = malloc((size_t)want * 4);
+    /* the prefix doubles from 8 chains until the regions balance: the
+     * first chains leave one space over everything they did not reach */
+    int64_t m = t->n < 8 ? t->n : 8, done = 0;
+    sitem *sp = NULL;
+    int64_t nsp = 0;
+    int32_t nreg = 1;
+    for (;;) {
+        for (; done < m; ++done)
+            add_chain(n, w, t->side, t->chains[done], c, INT32_MIN, INT32_MAX);
+        B->m = m;
+        free(sp);
+        sp = sp_all(w, c, &nsp);
+        int64_t mx, tot;
+        nreg = place_cuts(n, B, sp, nsp, want, c->size, cuts, &mx, &tot);
+        /* good enough: the largest region at most ~1/threads of the rest */
+        if (m >= t->n || mx * nthreads <= tot * 5 / 4 || m >= t->n / 4)
+            break;
+        m = m * 2 < t->n ? m * 2 : t->n;
+    }
+    /* regions: spaces and chain lists */
+    B->n_reg = nreg;
+    B->reg = calloc((size_t)nreg, sizeof(region));
+    B->spaces = sp;
+    int64_t k = 0;
+    for (int32_t r = 0; r < nreg; ++r) {
+        region *R = &B->reg[r];
+        R->side = t->side;
+        R->ch = *c;
+        R->a = r ? cuts[r - 1] : INT32_MIN;
+        R->b = r < nreg - 1 ? cuts[r] : INT32_MAX;
+        R->sp = sp + k;
+        while (k < nsp && (r == nreg - 1 || sp[k].start < cuts[r]))
+            ++k;
+        R->n_sp = sp + k - R->sp;
+    }
+    const int64_t rest = t->n - m;
+    int64_t *cnt = calloc((size_t)nreg + 1, 8);
+    int32_t *ra = malloc((size_t)(rest ? rest : 1) * 4), *rb = malloc((size_t)(rest ? rest : 1) * 4);
+    for (int64_t i = 0; i < rest; ++i) {
+        int cs, ce;
+        chain_span(n, t->side, t->chains[m + i], &cs, &ce);
+        ra[i] = (int32_t)upper_bound32(cuts, nreg - 1, cs);
+        rb[i] = (int32_t)upper_bound32(cuts, nreg - 1, ce > cs ? ce - 1 : cs);
+        for (int32_t r = ra[i]; r <= rb[i]; ++r) {
+            ++cnt[r];
+            B->reg[r].work += chain_work_in(n, t->side, t->chains[m + i], r ? cuts[r - 1] : 0,
+                                            r < nreg - 1 ? cuts[r] : c->size);
+        }
+    }
+    int64_t tot = 0;
+    for (int32_t r = 0; r < nreg; ++r)
+        tot += cnt[r];
+    B->lists = malloc((size_t)(tot ? tot : 1) * 8);
+    tot = 0;
+    for (int32_t r = 0; r < nreg; ++r) {
+        B->reg[r].chains = B->lists + tot;
+        tot += cnt[r];
+    }
+    for (int64_t i = 0; i < rest; ++i)
+        for (int32_t r = ra[i]; r <= rb[i]; ++r)
+            B->reg[r].chains[B->reg[r].n_chains++] = t->chains[m + i];
+    free(cnt);
+    free(ra);
+    free(rb);
+    free(cuts);
+}
+
+static void net_region(gac_net *n, nwork *w, region *R) {
+    sp_bulk(w, &R->ch, R->sp, R->n_sp);
+    for (int64_t i = 0; i < R->n_chains; ++i)
+        add_chain(n, w, R->side, R->chains[i], &R->ch, R->a, R->b);
+}
+
 typedef struct net_job {
     gac_net *n;
-    net_task *task;
+    net_task *task;     /* small sides, largest first */
     int64_t ntask;
-    _Atomic int64_t next;
+    big_net *big;       /* big sides (split into regions) */
+    int32_t nbig;
+    region **rq;        /* all regions, largest work first (after the prefixes) */
+    int64_t nrq;
+    _Atomic int64_t next, rnext;
+    _Atomic int ready;  /* the prefixes are done and rq is published */
     _Atomic int wid;
+    int nthreads;
+    double prefix_s;    /* thread 0's time in the sequential prefixes */
 } net_job;
+
+static int region_cmp(const void *a, const void *b) {
+    const region *x = *(region *const *)a, *y = *(region *const *)b;
+    return (x->work < y->work) - (x->work > y->work);
+}
+
+static void net_small(gac_net *n, nwork *w, const net_task *t) {
+    nchrom *c = &n->chroms[t->side][t->chrom];
+    /* makeChroms (chainNet.c:328-354): one gap = one space over the whole
+     * sequence */
+    c->root = gap_new(w, 0, c->size, 0, 0);
+    c->root->pidx = t->chrom;
+    sp_init(w, c, 0, c->size, c->root);
+    for (int64_t i = 0; i < t->n; ++i)
+        add_chain(n, w, t->side, t->chains[i], c, INT32_MIN, INT32_MAX);
+}
 
 static void *net_thread(void *arg) {
     net_job *J = arg;
-    nwork *w = &J->n->w[atomic_fetch_add(&J->wid, 1)];
-    for (;;) {
-        const int64_t k = atomic_fetch_add(&J->next, 1);
-        if (k >= J->ntask)
-            break;
-        const net_task *t = &J->task[k];
-        nchrom *c = &J->n->chroms[t->side][t->chrom];
-        /* makeChroms (chainNet.c:328-354): one gap = one space over the
-         * whole sequence */
-        c->root = gap_new(w, 0, c->size, 0, 0);
-        c->root->pidx = t->chrom;
-        sp_init(w, c, 0, c->size, c->root);
-        for (int64_t i = 0; i < t->n; ++i) {
-            if (t->side == GAC_T)
-                add_chain_t(J->n, w, t->chains[i]);
-            else
-                add_chain_q(J->n, w, t->chains[i]);
+    const int id = atomic_fetch_add(&J->wid, 1);
+    nwork *w = &J->n->w[id];
+    if (id == 0) {
+        int64_t nr = 0;
+        struct timespec t0, t1;
+        clock_gettime(CLOCK_MONOTONIC, &t0);
+        for (int32_t b = 0; b < J->nbig; ++b) {
+            big_prefix(J->n, w, &J->big[b], J->nthreads);
+            nr += J->big[b].n_reg;
         }
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        J->prefix_s = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+        J->rq = malloc((size_t)(nr ? nr : 1) * sizeof(region *));
+        for (int32_t b = 0; b < J->nbig; ++b)
+            for (int32_t r = 0; r < J->big[b].n_reg; ++r)
+                J->rq[J->nrq++] = &J->big[b].reg[r];
+        qsort(J->rq, (size_t)J->nrq, sizeof(region *), region_cmp);
+        atomic_store_explicit(&J->ready, 1, memory_order_release);
+    }
+    for (;;) {
+        if (atomic_load_explicit(&J->ready, memory_order_acquire)) {
+            const int64_t k = atomic_fetch_add(&J->rnext, 1);
+            if (k < J->nrq) {
+                net_region(J->n, w, J->rq[k]);
+                continue;
+            }
+        }
+        const int64_t k = atomic_fetch_add(&J->next, 1);
+        if (k < J->ntask) {
+            net_small(J->n, w, &J->task[k]);
+            continue;
+        }
+        if (atomic_load_explicit(&J->ready, memory_order_acquire) &&
+            atomic_load(&J->rnext) >= J->nrq)
+            break;
+        sched_yield();
     }
     return NULL;
 }
@@ -1048,12 +1501,14 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
             c->sroot = -1;
         }
     }
-    /* tasks, largest first; every task nets one chromosome of one side */
+    /* tasks, largest first; every task nets one chromosome of one side, the
+     * big ones are split into regions (net_regions) */
     net_job J;
     memset(&J, 0, sizeof(J));
     J.n = n;
     J.task = malloc((size_t)(nt + nq ? nt + nq : 1) * sizeof(net_task));
     J.ntask = 0;
+    J.nthreads = n->n_w;
     if (sides & (1 << GAC_T))
         for (int32_t k = 0; k < nt; ++k)
             if (!t_keep || t_keep[k])
@@ -1063,16 +1518,55 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
             if (!q_keep || q_keep[k])
                 J.task[J.ntask++] = (net_task){GAC_Q, k, ql + qoff[k], qoff[k + 1] - qoff[k]};
     qsort(J.task, (size_t)J.ntask, sizeof(net_task), net_task_cmp);
-    atomic_init(&J.next, 0);
-    atomic_init(&J.wid, 0);
+    /* big sides: more than a thread's share of all chains (and enough
+     * chains to be worth the split); the rest stay whole tasks */
+    int64_t all = 0;
+    for (int64_t k = 0; k < J.ntask; ++k)
+        all += J.task[k].n;
+    J.big = calloc((size_t)(J.ntask ? J.ntask : 1), sizeof(big_net));
+    const char *split_env = getenv("GAC_NET_SPLIT");
+    const int split = n->n_w > 1 && !(split_env && split_env[0] == '0');
+    while (split && J.nbig < J.ntask && J.task[J.nbig].n >= 8192 &&
+           J.task[J.nbig].n * 2 * n->n_w >= all) {
+        J.big[J.nbig].t = &J.task[J.nbig];
+        ++J.nbig;
+    }
+    net_task *small = J.task + J.nbig;
+    const int64_t nsmall = J.ntask - J.nbig;
+    net_job J2 = J; /* (the small-task view) */
+    J2.task = small;
+    J2.ntask = nsmall;
+    atomic_init(&J2.next, 0);
+    atomic_init(&J2.rnext, 0);
+    atomic_init(&J2.ready, J.nbig == 0);
+    atomic_init(&J2.wid, 0);
+    J2.rq = NULL;
+    J2.nrq = 0;
     struct timespec t_add0, t_add1;
     clock_gettime(CLOCK_MONOTONIC, &t_add0);
-    gac_run_threads(n->n_w < J.ntask ? n->n_w : (J.ntask ? J.ntask : 1), net_thread, &J);
+    const int64_t units = nsmall + (J.nbig ? n->n_w : 0);
+    gac_run_threads(n->n_w < units ? n->n_w : (units ? (int)units : 1), net_thread, &J2);
     clock_gettime(CLOCK_MONOTONIC, &t_add1);
-    if (getenv("GAC_TIMING"))
-        fprintf(stderr, "[gac_net_build] addChainT/Q %.3f s (%d threads, largest task %lld chains)\n",
+    if (getenv("GAC_TIMING")) {
+        fprintf(stderr, "[gac_net_build] addChainT/Q %.3f s (%d threads, largest task %lld chains; sequential prefixes %.3f s)\n",
                 (t_add1.tv_sec - t_add0.tv_sec) + 1e-9 * (t_add1.tv_nsec - t_add0.tv_nsec),
-                n->n_w, J.ntask ? (long long)J.task[0].n : 0LL);
+                n->n_w, J.ntask ? (long long)J.task[0].n : 0LL, J2.prefix_s);
+        for (int32_t b = 0; b < J.nbig; ++b) {
+            int64_t mx = 0;
+            for (int32_t r = 0; r < J.big[b].n_reg; ++r)
+                mx = J.big[b].reg[r].work > mx ? J.big[b].reg[r].work : mx;
+            fprintf(stderr, "[gac_net_build] side %d seq %d: %lld chains, %lld sequential, %d regions (largest work %lld)\n",
+                    J.big[b].t->side, J.big[b].t->chrom, (long long)J.big[b].t->n,
+                    (long long)J.big[b].m, J.big[b].n_reg, (long long)mx);
+        }
+    }
+    for (int32_t b = 0; b < J.nbig; ++b) {
+        free(J.big[b].spaces);
+        free(J.big[b].lists);
+        free(J.big[b].reg);
+    }
+    free(J.big);
+    free(J2.rq);
     free(J.task);
     free(toff);
     free(qoff);
@@ -1090,27 +1584,22 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
         memset(&F, 0, sizeof(F));
         F.n = n;
         const int64_t nc = n->n_chroms[GAC_T] + (int64_t)n->n_chroms[GAC_Q];
+        F.sk = calloc((size_t)(nc ? nc : 1), sizeof(skel));
         atomic_init(&F.next, 0);
         atomic_init(&F.wid, 0);
         gac_run_threads(n->n_w < nc ? n->n_w : (nc ? (int)nc : 1), fin_thread, &F);
-        /* phase B tasks, in output order: side, chromosome, fill run */
-        int64_t ntop = 0;
-        for (int side = 0; side < 2; ++side)
-            for (int32_t k = 0; k < n->n_chroms[side]; ++k)
-                if (n->chroms[side][k].root)
-                    ntop += n->chroms[side][k].root->n_fills;
-        const int64_t per = ntop / (16 * (int64_t)n->n_w) + 1;
-        int64_t cap = ntop / per + n->n_chroms[GAC_T] + n->n_chroms[GAC_Q] + 1;
-        F.task = malloc((size_t)cap * sizeof(fin_task));
-        F.ntask = 0;
-        for (int side = 0; side < 2; ++side)
-            for (int32_t k = 0; k < n->n_chroms[side]; ++k) {
-                const ngap *root = n->chroms[side][k].root;
-                const int32_t nf = root ? root->n_fills : 0;
-                for (int32_t f0 = 0; f0 < nf; f0 += (int32_t)per)
-                    F.task[F.ntask++] = (fin_task){side, k, f0,
-                                                   (int32_t)(f0 + per < nf ? f0 + per : nf)};
-            }
+        /* phase B: chunks of GAP items, in output order */
+        for (int64_t k = 0; k < nc; ++k)
+            for (int64_t i = 0; i < F.sk[k].n; ++i)
+                F.n_gi += F.sk[k].it[i].g != NULL;
+        F.gi = malloc((size_t)(F.n_gi ? F.n_gi : 1) * sizeof(sk_item *));
+        F.n_gi = 0;
+        for (int64_t k = 0; k < nc; ++k)
+            for (int64_t i = 0; i < F.sk[k].n; ++i)
+                if (F.sk[k].it[i].g)
+                    F.gi[F.n_gi++] = &F.sk[k].it[i];
+        F.per = F.n_gi / (16 * (int64_t)n->n_w) + 1;
+        F.ntask = (F.n_gi + F.per - 1) / F.per;
         F.x = calloc((size_t)(F.ntask ? F.ntask : 1), sizeof(fin_ctx));
         struct timespec t_a;
         clock_gettime(CLOCK_MONOTONIC, &t_a);
@@ -1118,32 +1607,56 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
         atomic_init(&F.next, 0);
         atomic_init(&F.wid, 0);
         gac_run_threads(n->n_w < F.ntask ? n->n_w : (F.ntask ? (int)F.ntask : 1), fin_thread, &F);
+        /* the pre-order index: skeletons with the subtree lists spliced in */
         int64_t tot[2] = {0, 0};
-        for (int64_t k = 0; k < F.ntask; ++k)
-            tot[F.task[k].side] += F.x[k].n_ord;
+        for (int64_t k = 0; k < nc; ++k) {
+            const int side = k < n->n_chroms[GAC_T] ? GAC_T : GAC_Q;
+            for (int64_t i = 0; i < F.sk[k].n; ++i)
+                tot[side] += F.sk[k].it[i].g ? F.sk[k].it[i].cnt : 1;
+        }
         for (int side = 0; side < 2; ++side) {
             n->order[side] = malloc((size_t)(tot[side] ? tot[side] : 1) * sizeof(nfill *));
             n->n_order[side] = 0;
         }
-        for (int64_t k = 0; k < F.ntask; ++k) {
-            const int side = F.task[k].side;
-            fin_ctx *x = &F.x[k];
-            for (int64_t j = 0; j < x->n_ord; ++j) {
-                x->ord[j]->ord = n->n_order[side];
-                n->order[side][n->n_order[side]++] = x->ord[j];
+        int64_t gidx = 0, used = 0; /* GAP item; fills taken from its chunk's list */
+        for (int64_t k = 0; k < nc; ++k) {
+            const int side = k < n->n_chroms[GAC_T] ? GAC_T : GAC_Q;
+            nfill **out = n->order[side];
+            int64_t no = n->n_order[side];
+            for (int64_t i = 0; i < F.sk[k].n; ++i) {
+                const sk_item *it = &F.sk[k].it[i];
+                if (!it->g) {
+                    it->f->ord = no;
+                    out[no++] = it->f;
+                    continue;
+                }
+                const fin_ctx *x = &F.x[gidx / F.per];
+                if (gidx % F.per == 0)
+                    used = 0;
+                for (int64_t j = 0; j < it->cnt; ++j) {
+                    x->ord[used + j]->ord = no;
+                    out[no++] = x->ord[used + j];
+                }
+                used += it->cnt;
+                ++gidx;
             }
-            free(x->ord);
+            n->n_order[side] = no;
+            free(F.sk[k].it);
         }
-        free(F.task);
+        for (int64_t k = 0; k < F.ntask; ++k)
+            free(F.x[k].ord);
+        free(F.sk);
+        free(F.gi);
         /* phase C: rCalcOtherFill over the flat pre-order lists (the sorts
          * above key on the fills' own-side bounds, which it recomputes
          * unchanged, so it can run last) */
         struct timespec t_b;
         clock_gettime(CLOCK_MONOTONIC, &t_b);
         if (getenv("GAC_TIMING"))
-            fprintf(stderr, "[gac_net_build] finishNet sort roots %.3f s, subtrees %.3f s (%lld runs)\n",
+            fprintf(stderr, "[gac_net_build] finishNet skeletons %.3f s, subtrees + index %.3f s (%lld gap subtrees in %lld chunks)\n",
                     (t_a.tv_sec - t_fin0.tv_sec) + 1e-9 * (t_a.tv_nsec - t_fin0.tv_nsec),
-                    (t_b.tv_sec - t_a.tv_sec) + 1e-9 * (t_b.tv_nsec - t_a.tv_nsec), (long long)F.ntask);
+                    (t_b.tv_sec - t_a.tv_sec) + 1e-9 * (t_b.tv_nsec - t_a.tv_nsec), (long long)F.n_gi,
+                    (long long)F.ntask);
         F.phase = 2;
         atomic_init(&F.next, 0);
         atomic_init(&F.wid, 0);

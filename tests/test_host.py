@@ -342,3 +342,40 @@ def test_chainnet_ranks_failure(tmp_path):
     r = subprocess.run([tool, p("in.chain"), p("t.sizes"), p("q.sizes"), "a", "b", "-nranks=2",
                         "-rank=2"], capture_output=True, text=True)
     assert r.returncode == 255 and "-rank=2" in r.stderr
+
+
+@pytest.mark.parametrize("opts", [["-minScore=0"], ["-minSpace=1", "-minScore=0"],
+                                  ["-minSpace=300", "-minFill=40"]])
+def test_netting_split_side_vs_reference(opts, tmp_path):
+    """One big chromosome side netted by many threads (gac_net.c net_regions:
+    a short sequential prefix, then regions between space boundaries):
+    identical to the sequential engine (GAC_NET_SPLIT=0) and to the
+    reference chainNet."""
+    from genomealignmenttools_amd import chainfile, synth
+    from genomealignmenttools_amd._lib import BIN_DIR
+    from oracle.oracle import have_ref, ref_tool
+    tg, qg, ca = synth.small_case(seed=21, n_chains=30000, tsize=6_000_000,
+                                  qsizes=(3_000_000, 2_000_000, 1_000_000), max_blocks=3000)
+    d = str(tmp_path)
+    p = lambda x: os.path.join(d, x)
+    synth.write_sizes(tg.sizes, p("t.sizes"))
+    synth.write_sizes(qg.sizes, p("q.sizes"))
+    chainfile.write_chains(ca, p("in.chain"))
+    args = [p("in.chain"), p("t.sizes"), p("q.sizes")]
+    outs = {}
+    for tag, env in (("split", {"GAC_THREADS": "8", "GAC_TIMING": "1"}),
+                     ("seq", {"GAC_THREADS": "8", "GAC_NET_SPLIT": "0"})):
+        r = subprocess.run([os.path.join(BIN_DIR, "chainNet")] + args +
+                           [p(f"{tag}.t.net"), p(f"{tag}.q.net")] + opts,
+                           capture_output=True, text=True, env=dict(os.environ, **env))
+        assert r.returncode == 0, r.stderr
+        outs[tag] = r.stderr
+    assert "regions" in outs["split"]  # the target side was split
+    for side in "tq":
+        assert filecmp.cmp(p(f"split.{side}.net"), p(f"seq.{side}.net"), shallow=False)
+    if have_ref():
+        r = subprocess.run([ref_tool("chainNet")] + args + [p("ref.t.net"), p("ref.q.net")] + opts,
+                           capture_output=True)
+        assert r.returncode == 0
+        for side in "tq":
+            assert filecmp.cmp(p(f"split.{side}.net"), p(f"ref.{side}.net"), shallow=False)
