@@ -75,6 +75,9 @@ def parse():
     p.add_argument("--prof", choices=["tile", "all", "none"], default="tile",
                    help="kernels bracketed by HIP events in the kernel leg (the roofline "
                         "needs k_tile's)")
+    p.add_argument("--order", choices=["chain", "net"], default="chain",
+                   help="kernel leg: ranges in (chain, tStart) order as bin/chainNet submits "
+                        "them, or in .net output order")
     p.add_argument("--tmp", default=os.environ.get("TMPDIR", "/tmp"))
     return p.parse_args()
 
@@ -153,6 +156,8 @@ def kernel_leg(args, d, steps):
         fills = net_fills(ca, read_sizes(p("t.sizes")), read_sizes(p("q.sizes")), min_score=0.0)
         part = fills["partial"]
         ranges = np.stack([fills["chain"][part], fills["start"][part], fills["end"][part]], 1)
+    if args.order == "chain":  # as bin/chainNet hands them over (chainNet.c chain_order)
+        ranges = ranges[np.lexsort((ranges[:, 1], ranges[:, 0]))]
     ranges = np.ascontiguousarray(ranges, np.int32)
     e = Engine(int(os.environ.get("LOCAL_RANK", "0")))
     e.load_2bit(GAC_T, p("t.2bit"))
@@ -205,7 +210,8 @@ def kernel_leg(args, d, steps):
     kernel = {"workload": ("chainNet -rescore partial target fills" if args.workload != "scorechain"
                            else "scoreChain whole chains, global + local"),
               "value": bases * steps / dt / 1e9, "unit": "Gbases/s", "ms_per_step": dt / steps * 1e3,
-              "steps": steps, "ranges": n, "scored_bases": bases, "window_blocks": nblk,
+              "steps": steps, "ranges": n, "order": args.order, "scored_bases": bases,
+              "window_blocks": nblk,
               "kernel_ms": kern_ms}
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc_traffic(args, n, nblk),
@@ -227,7 +233,8 @@ def _pmc_traffic(args, n, nblk):
         return None
     wl = "scorechain" if args.workload == "scorechain" else "rescore"
     if (t.get("workload") != wl or t.get("ranges") != n or t.get("blocks") != nblk
-            or t.get("chains") != args.chains or t.get("seed") != args.seed):
+            or t.get("chains") != args.chains or t.get("seed") != args.seed
+            or t.get("order", "net") != args.order):
         return None
     return t.get("hbm_bytes_per_launch")
 

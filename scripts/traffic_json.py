@@ -15,18 +15,19 @@ def main(summary_path, bench_path):
     if not k:
         sys.exit("no k_tile entry with hbm_bytes in " + summary_path)
     d = s[k[0]]
-    cfg = b["config"]
+    kern = b["kernel"]
     out = {
         "kernel": k[0],
         "hbm_bytes_per_launch": d["hbm_bytes"],
         "hbm_read_bytes_per_launch": d["hbm_read_bytes"],
         "hbm_write_bytes_per_launch": d["hbm_write_bytes"],
         "algo_bytes_per_launch": b["roofline"]["algo_bytes_per_launch"],
-        "workload": "rescore" if cfg["workload"].startswith("chainNet") else "scorechain",
-        "chains": cfg["chains"],
+        "workload": "rescore" if kern["workload"].startswith("chainNet") else "scorechain",
+        "chains": b["config"]["chains"],
         "seed": 42,
-        "ranges": cfg["ranges_per_gpu"],
-        "blocks": cfg["scored_blocks_per_gpu"],
+        "ranges": kern["ranges"],
+        "blocks": kern["window_blocks"],
+        "order": kern.get("order", "net"),
         "source": "rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_{32,64,128}B_sum / "
                   "TCC_EA0_WRREQ(_64B)_sum passes (scripts/gpu_counters.sh), "
                   "mean per dispatch (scripts/pmc_summary.py)",
