@@ -742,13 +742,18 @@ static char *lf_next(lf *f) {
     return line;
 }
 
-static void add_meta(gt_chains *c, const char *line) {
+static void add_meta_at(gt_chains *c, const char *line, int64_t at) {
     if (c->n_meta == c->meta_cap) {
         c->meta_cap = c->meta_cap ? c->meta_cap * 2 : 16;
         c->meta = realloc(c->meta, c->meta_cap * sizeof(char *));
+        c->meta_at = realloc(c->meta_at, c->meta_cap * sizeof(int64_t));
     }
+    c->meta_at[c->n_meta] = at;
     c->meta[c->n_meta++] = strdup(line);
 }
+
+/* a '#' line consumed while reading chain c->n (the next one) */
+static void add_meta(gt_chains *c, const char *line) { add_meta_at(c, line, c->n); }
 
 /* lineFileChopNext: next non-blank, non-'#' line chopped into <= max words */
 static int lf_chop(lf *f, char **row, int max) {
@@ -1108,7 +1113,7 @@ void gt_read_chains(const char *path, gt_chains *c, double stop_below, int keep_
         const int64_t take = ch->stop >= 0 ? ch->stop : ch->c.n; /* the stop chain is dropped */
         /* metadata: all '#' lines the chunk consumed (a stop drops the rest) */
         for (int32_t m = 0; m < ch->c.n_meta; ++m) {
-            add_meta(c, ch->c.meta[m]);
+            add_meta_at(c, ch->c.meta[m], c0[k] + ch->c.meta_at[m]);
         }
         int32_t *tmap = malloc((size_t)(ch->c.tnames.n ? ch->c.tnames.n : 1) * 4);
         int32_t *qmap = malloc((size_t)(ch->c.qnames.n ? ch->c.qnames.n : 1) * 4);
@@ -1201,6 +1206,7 @@ void gt_chains_free(gt_chains *c) {
     for (int32_t i = 0; i < c->n_meta; ++i)
         free(c->meta[i]);
     free(c->meta);
+    free(c->meta_at);
     memset(c, 0, sizeof(*c));
 }
 

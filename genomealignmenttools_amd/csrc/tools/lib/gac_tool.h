@@ -141,6 +141,7 @@ typedef struct gt_chains {
     int32_t *bt, *bq, *bs;
     gt_names tnames, qnames;
     char **meta; /* '#' lines in order */
+    int64_t *meta_at; /* the chain whose read consumed meta[k] (n: the read that hit EOF) */
     int32_t n_meta, meta_cap;
 } gt_chains;
 
