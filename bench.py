@@ -75,9 +75,9 @@ def parse():
     p.add_argument("--prof", choices=["tile", "all", "none"], default="tile",
                    help="kernels bracketed by HIP events in the kernel leg (the roofline "
                         "needs k_tile's)")
-    p.add_argument("--order", choices=["chain", "net"], default="chain",
-                   help="kernel leg: ranges in (chain, tStart) order as bin/chainNet submits "
-                        "them, or in .net output order")
+    p.add_argument("--order", choices=["chain", "net"], default="net",
+                   help="kernel leg: ranges in .net output order (as bin/chainNet submits "
+                        "them) or in (chain, tStart) order (measured slower for k_tile)")
     p.add_argument("--tmp", default=os.environ.get("TMPDIR", "/tmp"))
     return p.parse_args()
 
@@ -156,7 +156,7 @@ def kernel_leg(args, d, steps):
         fills = net_fills(ca, read_sizes(p("t.sizes")), read_sizes(p("q.sizes")), min_score=0.0)
         part = fills["partial"]
         ranges = np.stack([fills["chain"][part], fills["start"][part], fills["end"][part]], 1)
-    if args.order == "chain":  # as bin/chainNet hands them over (chainNet.c chain_order)
+    if args.order == "chain":
         ranges = ranges[np.lexsort((ranges[:, 1], ranges[:, 0]))]
     ranges = np.ascontiguousarray(ranges, np.int32)
     e = Engine(int(os.environ.get("LOCAL_RANK", "0")))

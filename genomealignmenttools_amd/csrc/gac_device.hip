@@ -588,6 +588,17 @@ extern "C" int gac_genome_load_2bit(gac_ctx *c, int side, const char *path) {
     gac_twobit tb;
     int rc = gac_twobit_open(path, &tb);
     if (rc != GAC_OK) return rc;
+    return gac_genome_load_twobit(c, side, &tb);
+}
+
+extern "C" int gac_genome_load_twobit(gac_ctx *c, int side, gac_twobit *tbp) {
+    gac_clear_error();
+    if (!side_of(c, side) || !tbp) {
+        if (tbp) gac_twobit_close(tbp);
+        return gac_fail(GAC_E_ARG, "gac_genome_load_twobit: bad argument");
+    }
+    gac_twobit tb = *tbp;
+    int rc = GAC_OK;
     std::vector<int32_t> ns, nz;
     for (uint32_t i = 0; i < tb.seq_count && rc == GAC_OK; ++i) {
         const gac_twobit_seq &s = tb.seqs[i];

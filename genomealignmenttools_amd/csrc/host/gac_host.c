@@ -45,7 +45,10 @@ const char *gac_last_error(void) { return g_err; }
 int gac_abi_version(void) { return GAC_ABI_VERSION; }
 
 /* ------------------------------------------------------------- file mapping */
-int gac_map_file(const char *path, gac_map *m) {
+static int map_file(const char *path, gac_map *m, int populate);
+int gac_map_file(const char *path, gac_map *m) { return map_file(path, m, 0); }
+
+static int map_file(const char *path, gac_map *m, int populate) {
     memset(m, 0, sizeof(*m));
     m->fd = -1;
     int fd = (strcmp(path, "stdin") == 0) ? 0 : open(path, O_RDONLY);
@@ -62,7 +65,7 @@ int gac_map_file(const char *path, gac_map *m) {
             m->fd = -1;
             return GAC_OK;
         }
-        void *p = mmap(NULL, m->size, PROT_READ, MAP_PRIVATE, fd, 0);
+        void *p = mmap(NULL, m->size, PROT_READ, MAP_PRIVATE | (populate ? MAP_POPULATE : 0), fd, 0);
         if (p == MAP_FAILED) {
             close(fd);
             return gac_fail(GAC_E_IO, "can't mmap %s: %s", path, strerror(errno));
@@ -646,9 +649,11 @@ void gac_twobit_close(gac_twobit *tb) {
     memset(tb, 0, sizeof(*tb));
 }
 
-int gac_twobit_open(const char *path, gac_twobit *tb) {
+int gac_twobit_open(const char *path, gac_twobit *tb) { return gac_twobit_open_ex(path, tb, 0); }
+
+int gac_twobit_open_ex(const char *path, gac_twobit *tb, int populate) {
     memset(tb, 0, sizeof(*tb));
-    int rc = gac_map_file(path, &tb->map);
+    int rc = map_file(path, &tb->map, populate);
     if (rc != GAC_OK)
         return rc;
     const uint8_t *d = tb->map.data;

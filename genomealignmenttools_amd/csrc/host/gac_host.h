@@ -55,6 +55,13 @@ typedef struct gac_twobit {
 } gac_twobit;
 
 int gac_twobit_open(const char *path, gac_twobit *tb);
+/* the same; populate != 0 maps the file with MAP_POPULATE (page tables
+ * filled up front: the tools open the .2bit files this way on a helper
+ * thread while the HIP runtime starts) */
+int gac_twobit_open_ex(const char *path, gac_twobit *tb, int populate);
+/* gac_genome_load_2bit of an already opened file; the genome side takes
+ * over tb (closed on error as well) */
+int gac_genome_load_twobit(gac_ctx *c, int side, gac_twobit *tb);
 void gac_twobit_close(gac_twobit *tb);
 uint32_t gac_twobit_u32(const gac_twobit *tb, const uint8_t *p);
 int gac_is_twobit_file(const char *path);

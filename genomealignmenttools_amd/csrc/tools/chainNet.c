@@ -152,58 +152,6 @@ static void *pre_upload_thread(void *arg) {
 }
 
 
-/* Fills handed to the GPU in (chain, tStart) order, not .net order: a
- * chain's fills then sit next to each other, so consecutive ranges share the
- * chain record, its bucket index and block lines in k_plan / k_tile.  The
- * scores go back by rix.  Counting sort by chain, then by start inside each
- * chain (stable, O(n) + the per-chain sorts). */
-static int range_start_cmp(const void *a, const void *b) {
-    const int64_t *x = a, *y = b; /* {t_start << 32 | pos} */
-    return (*x > *y) - (*x < *y);
-}
-
-static void chain_order(gac_range *r, int64_t *rix, int64_t nr, int64_t n_chains) {
-    if (nr < 2)
-        return;
-    int64_t *cnt = calloc((size_t)n_chains + 1, 8);
-    for (int64_t k = 0; k < nr; ++k)
-        ++cnt[r[k].chain + 1];
-    for (int64_t c = 0; c < n_chains; ++c)
-        cnt[c + 1] += cnt[c];
-    gac_range *r2 = malloc((size_t)nr * sizeof(gac_range));
-    int64_t *x2 = malloc((size_t)nr * 8), *key = malloc((size_t)nr * 8);
-    int64_t *pos = malloc((size_t)(n_chains + 1) * 8);
-    memcpy(pos, cnt, (size_t)(n_chains + 1) * 8);
-    for (int64_t k = 0; k < nr; ++k) {
-        const int64_t d = pos[r[k].chain]++;
-        r2[d] = r[k];
-        x2[d] = rix[k];
-    }
-    for (int64_t c = 0; c < n_chains; ++c) {
-        const int64_t a = cnt[c], b = cnt[c + 1];
-        if (b - a < 2)
-            continue;
-        for (int64_t k = a; k < b; ++k)
-            key[k] = ((int64_t)r2[k].t_start << 32) | (uint32_t)(k - a);
-        qsort(key + a, (size_t)(b - a), 8, range_start_cmp);
-        for (int64_t k = a; k < b; ++k) {
-            const int64_t src = a + (uint32_t)key[k];
-            r[k] = r2[src];
-            rix[k] = x2[src];
-        }
-    }
-    for (int64_t c = 0; c < n_chains; ++c) /* single-fill chains */
-        if (cnt[c + 1] - cnt[c] == 1) {
-            r[cnt[c]] = r2[cnt[c]];
-            rix[cnt[c]] = x2[cnt[c]];
-        }
-    free(cnt);
-    free(pos);
-    free(r2);
-    free(x2);
-    free(key);
-}
-
 /* ---------------------------------------------------------------- ranks
  * -nranks=N -rank=R: N processes (one per GPU of one node) run the same
  * command.  A chromosome side's net depends only on the chains on that
@@ -573,6 +521,29 @@ int main(int argc, char *argv[]) {
     gt_stage("netting");
     gt_verbose(1, "Finishing nets\n");
 
+    /* the two nets are independent files, written concurrently; the query
+     * net needs no rescoring, so it is written while the target fills are
+     * rescored (with -nranks: this rank's parts, renamed into place when
+     * complete) */
+    gt_verbose(1, "writing %s\n", tnet);
+    gt_verbose(1, "writing %s\n", qnet);
+    char tpart[4096], qpart[4096], tpart_tmp[4096], qpart_tmp[4096];
+    if (multi) {
+        part_name(tpart, sizeof(tpart), tnet, g_rk.me, "");
+        part_name(qpart, sizeof(qpart), qnet, g_rk.me, "");
+        part_name(tpart_tmp, sizeof(tpart_tmp), tnet, g_rk.me, ".tmp");
+        part_name(qpart_tmp, sizeof(qpart_tmp), qnet, g_rk.me, ".tmp");
+    }
+    net_out wo[2] = {{net, GAC_T, NULL, multi ? tpart_tmp : tnet, &c, 0, 0},
+                     {net, GAC_Q, NULL, multi ? qpart_tmp : qnet, &c, 0, 0}};
+    pthread_t qth;
+    if (pthread_create(&qth, NULL, write_net, &wo[1]) != 0) {
+        write_net(&wo[1]);
+    } else {
+        wo[1].threaded = 1;
+        gt_helper_add(qth); /* gt_abort joins it before exiting */
+    }
+
     int64_t *tscores = NULL;
     if (rescore) {
         const int64_t nf = gac_net_fill_count(net, GAC_T);
@@ -591,7 +562,6 @@ int main(int argc, char *argv[]) {
                 r[nr].t_end = fe[i];
                 rix[nr++] = i;
             }
-        chain_order(r, rix, nr, c.n);
         tscores = calloc(nf ? nf : 1, 8);
         if (pu.started)
             gt_helper_join(pu.th);
@@ -696,27 +666,10 @@ int main(int argc, char *argv[]) {
         free(r);
         free(rix);
     }
-    /* the two nets are independent files: written concurrently (with
-     * -nranks: this rank's parts, renamed into place when complete) */
-    gt_verbose(1, "writing %s\n", tnet);
-    gt_verbose(1, "writing %s\n", qnet);
-    char tpart[4096], qpart[4096], tpart_tmp[4096], qpart_tmp[4096];
-    if (multi) {
-        part_name(tpart, sizeof(tpart), tnet, g_rk.me, "");
-        part_name(qpart, sizeof(qpart), qnet, g_rk.me, "");
-        part_name(tpart_tmp, sizeof(tpart_tmp), tnet, g_rk.me, ".tmp");
-        part_name(qpart_tmp, sizeof(qpart_tmp), qnet, g_rk.me, ".tmp");
-    }
-    net_out wo[2] = {{net, GAC_T, tscores, multi ? tpart_tmp : tnet, &c, 0, 0},
-                     {net, GAC_Q, NULL, multi ? qpart_tmp : qnet, &c, 0, 0}};
-    pthread_t qth;
-    if (pthread_create(&qth, NULL, write_net, &wo[1]) != 0)
-        write_net(&wo[1]);
-    else
-        wo[1].threaded = 1;
+    wo[0].tscores = tscores;
     write_net(&wo[0]);
     if (wo[1].threaded)
-        pthread_join(qth, NULL);
+        gt_helper_join(qth);
     for (int k = 0; k < 2; ++k)
         if (wo[k].rc != GAC_OK)
             gt_abort("%s\n", wo[k].err);

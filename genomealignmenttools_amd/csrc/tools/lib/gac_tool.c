@@ -106,19 +106,55 @@ static double now_s(void) {
     return ts.tv_sec + 1e-9 * ts.tv_nsec;
 }
 
+/* the two .2bit files mapped (page tables populated) while the HIP
+ * runtime starts on the device thread */
+typedef struct twobit_pre {
+    const char *path[2];
+    gac_twobit tb[2];
+    int rc[2];
+    char err[2][512];
+} twobit_pre;
+
+static void *twobit_pre_thread(void *arg) {
+    twobit_pre *P = arg;
+    for (int k = 0; k < 2; ++k) {
+        P->rc[k] = gac_twobit_open_ex(P->path[k], &P->tb[k], 1);
+        if (P->rc[k] != GAC_OK)
+            snprintf(P->err[k], sizeof(P->err[k]), "%s", gac_last_error());
+    }
+    return NULL;
+}
+
 static void *device_thread(void *arg) {
     gt_device *d = arg;
     const double t0 = now_s();
+    twobit_pre P;
+    memset(&P, 0, sizeof(P));
+    P.path[0] = d->t2bit;
+    P.path[1] = d->q2bit;
+    pthread_t pre;
+    const int pre_ok = pthread_create(&pre, NULL, twobit_pre_thread, &P) == 0;
+    if (!pre_ok)
+        twobit_pre_thread(&P);
     int rc = gac_open(g_gpu, &d->ctx);
     d->open_s = now_s() - t0;
     if (rc == GAC_OK && d->mat)
         rc = gac_set_scoring(d->ctx, d->mat, d->gap);
-    if (rc == GAC_OK)
-        rc = gac_genome_load_2bit(d->ctx, GAC_T, d->t2bit);
-    if (rc == GAC_OK)
-        rc = gac_genome_load_2bit(d->ctx, GAC_Q, d->q2bit);
+    if (pre_ok)
+        pthread_join(pre, NULL);
+    for (int k = 0; k < 2; ++k) {
+        if (rc == GAC_OK && P.rc[k] != GAC_OK) {
+            rc = P.rc[k];
+            snprintf(d->err, sizeof(d->err), "%s", P.err[k]);
+            d->rc_err_set = 1;
+        }
+        if (rc == GAC_OK)
+            rc = gac_genome_load_twobit(d->ctx, k == 0 ? GAC_T : GAC_Q, &P.tb[k]);
+        else if (P.rc[k] == GAC_OK)
+            gac_twobit_close(&P.tb[k]);
+    }
     d->load_s = now_s() - t0 - d->open_s;
-    if (rc != GAC_OK) /* the error text is thread-local */
+    if (rc != GAC_OK && !d->rc_err_set) /* the error text is thread-local */
         snprintf(d->err, sizeof(d->err), "%s", gac_last_error());
     pthread_mutex_lock(&d->mu);
     d->rc = rc;

@@ -42,7 +42,7 @@ typedef struct gt_device {
     const int32_t *mat;
     const gac_gapcalc *gap;
     gac_ctx *ctx;
-    int rc, started;
+    int rc, started, rc_err_set;
     double open_s, load_s;
     char err[1024];
     /* bring-up completion: the (detached) device thread sets done under mu
