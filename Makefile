@@ -31,8 +31,9 @@ EXECDIR  := $(PKG)/libexec
 # fewer page faults on the GB-scale chain/net arrays) and execs it -- before
 # anything touches the GPU.  NetFilterNonNested.perl is host-only: in bin/.
 GPU_TOOLS := scoreChain chainNet chainCleaner axtChain
+HOST_TOOLS := NetFilterNonNested.perl chainSort chainMergeSort
 TOOLS    := $(addprefix $(EXECDIR)/,$(GPU_TOOLS)) $(addprefix $(BINDIR)/,$(GPU_TOOLS)) \
-            $(BINDIR)/NetFilterNonNested.perl
+            $(addprefix $(BINDIR)/,$(HOST_TOOLS))
 TOOL_LIB_SRC := $(wildcard $(CSRC)/tools/lib/*.c)
 TOOL_LIB_OBJ := $(patsubst $(CSRC)/tools/lib/%.c,$(OBJDIR)/tools/lib/%.o,$(TOOL_LIB_SRC))
 
@@ -59,7 +60,13 @@ $(EXECDIR)/%: $(CSRC)/tools/%.c $(TOOL_LIB_OBJ) $(LIBDIR)/libgachain.so $(HDRS)
 	$(CC) $(CFLAGS) -I$(CSRC)/tools/lib $< $(TOOL_LIB_OBJ) -o $@ -L$(LIBDIR) -lgachain \
 	    -Wl,-rpath,'$$ORIGIN/../lib' -lz -lm -lpthread
 
+# host-only tools (no device): built straight into bin/
 $(BINDIR)/NetFilterNonNested.perl: $(CSRC)/tools/NetFilterNonNested.perl.c $(TOOL_LIB_OBJ) $(LIBDIR)/libgachain.so $(HDRS)
+	@mkdir -p $(BINDIR)
+	$(CC) $(CFLAGS) -I$(CSRC)/tools/lib $< $(TOOL_LIB_OBJ) -o $@ -L$(LIBDIR) -lgachain \
+	    -Wl,-rpath,'$$ORIGIN/../lib' -lz -lm -lpthread
+
+$(BINDIR)/chainSort $(BINDIR)/chainMergeSort: $(BINDIR)/%: $(CSRC)/tools/%.c $(TOOL_LIB_OBJ) $(LIBDIR)/libgachain.so $(HDRS)
 	@mkdir -p $(BINDIR)
 	$(CC) $(CFLAGS) -I$(CSRC)/tools/lib $< $(TOOL_LIB_OBJ) -o $@ -L$(LIBDIR) -lgachain \
 	    -Wl,-rpath,'$$ORIGIN/../lib' -lz -lm -lpthread

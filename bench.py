@@ -79,6 +79,7 @@ def parse():
                    help="kernel leg: ranges in .net output order (as bin/chainNet submits "
                         "them) or in (chain, tStart) order (measured slower for k_tile)")
     p.add_argument("--tmp", default=os.environ.get("TMPDIR", "/tmp"))
+    p.add_argument("--gen-only", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
 
@@ -132,7 +133,9 @@ def run_tool(cmd, outs, env=None):
     for o in outs:  # (a truncated-and-rewritten file may be flushed on close)
         if os.path.exists(o):
             os.remove(o)
-    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=900)
+    # close_fds=False lets subprocess use posix_spawn (vfork): the launch
+    # costs the same whatever this process's size
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=900, close_fds=False)
     if r.returncode != 0:
         raise RuntimeError(f"{cmd[0]} rc={r.returncode}: {r.stderr[-3000:]}")
     return r
@@ -373,6 +376,9 @@ def _net_sections(text):
 # ---------------------------------------------------------------- main
 def main():
     args = parse()
+    if args.gen_only:
+        c2_files(args)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -389,7 +395,9 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    if rank == 0:
+    if rank == 0:  # generated in a child process: this one stays small
+        subprocess.run([sys.executable, os.path.abspath(__file__), "--gen-only", "--chains",
+                        str(args.chains), "--seed", str(args.seed), "--tmp", args.tmp], check=True)
         d, info = c2_files(args)
     barrier()
     if rank != 0:

@@ -39,7 +39,7 @@ LIBOBJ   := $(patsubst $(K)/lib/%.c,$(OBJ)/lib/%.o,$(LIBSRC))
 HGOBJ    := $(OBJ)/hg/chainNet.o
 
 TOOLS    := $(OUT)/scoreChain $(OUT)/chainNet $(OUT)/chainCleaner \
-            $(OUT)/axtChain $(OUT)/chainSort
+            $(OUT)/axtChain $(OUT)/chainSort $(OUT)/chainMergeSort $(OUT)/netSyntenic
 
 all: $(TOOLS) $(OUT)/kentref
 
@@ -68,6 +68,14 @@ $(OUT)/axtChain: $(K)/hg/mouseStuff/axtChain/axtChain.c $(OUT)/jkweb.a
 
 $(OUT)/chainSort: $(K)/hg/mouseStuff/chainSort/chainSort.c $(OUT)/jkweb.a
 	$(CC) $(TCFLAGS) $< -o $@ $(OUT)/jkweb.a $(LIBS) 2>/dev/null
+
+$(OUT)/chainMergeSort: $(K)/hg/mouseStuff/chainMergeSort/chainMergeSort.c $(OUT)/jkweb.a
+	$(CC) $(TCFLAGS) $< -o $@ $(OUT)/jkweb.a $(LIBS) 2>/dev/null
+
+# netSyntenic: adds the type/qFar/qDup fields NetFilterNonNested's synteny
+# modes read (goldens for those modes; not on the hot path)
+$(OUT)/netSyntenic: $(K)/hg/mouseStuff/netSyntenic/netSyntenic.c $(HGOBJ) $(OUT)/jkweb.a
+	$(CC) $(TCFLAGS) $< -o $@ $(HGOBJ) $(OUT)/jkweb.a $(LIBS) 2>/dev/null
 
 # The reference's kent objects driven by our harness (the reference's own
 # chainSubsetOnT + chainCalcScore, scoreChain's local-score loop restated) --
