@@ -10,10 +10,13 @@
  *   "12"    -minScore1 -minSizeT1 -minSizeQ1 [-minScore2 -minSizeT2 -minSizeQ2]
  *           (:93-109; an unset set is INT_MAX)
  *   batch   -minScore a,b,.. -minSizeT .. -minSizeQ .. (:110-120)
- * The UCSC-synteny / score+type modes (-doUCSCSynFilter, -doScoreFilter,
- * -keepSynNetsWithScore, -keepInvNetsWithScore) and -v are not implemented
- * here and are rejected with an error.  Options follow Getopt::Long:
- * "-opt value", "-opt=value" or "--opt", names case-insensitive. */
+ *   UCSC    -doUCSCSynFilter [-keepSynNetsWithScore n -keepInvNetsWithScore n]
+ *           (UCSCsynFilter_nonRecursive, :268-302)
+ *   score   -doScoreFilter -minScore1 n [-keepSyn.. -keepInv..] (:305-327)
+ * plus -keepSynNetsWithScore / -keepInvNetsWithScore in the other modes
+ * (:368-374); the type, ali and qFar fields come from netSyntenic.  -v (the
+ * script's debug trace, printed into its output) is rejected.  Options
+ * follow Getopt::Long: "-opt value", "-opt=value" or "--opt". */
 #define _GNU_SOURCE
 #include <ctype.h>
 #include <limits.h>
@@ -34,10 +37,11 @@ static void usage(void) {
             "Output goes to stdout\n"
             "\n"
             "NetFilterNonNested.perl input.net[.gz] [other parameters depending on filter mode]\n"
-            "\t   [-minScore comma-separated-string -minSizeT comma-separated-string -minSizeQ comma-separated-string]\n"
-            "\tOR [-minScore1 int -minSizeT1 int -minSizeQ1 int  -minScore2 int -minSizeT2 int -minSizeQ2 int]\n"
-            "(this native build implements these two modes; -doUCSCSynFilter, -doScoreFilter,\n"
-            " -keepSynNetsWithScore, -keepInvNetsWithScore and -v are not supported)\n\n");
+            "\tEITHER [-doUCSCSynFilter -keepSynNetsWithScore int -keepInvNetsWithScore int]\n"
+            "\t    OR [-doScoreFilter -minScore1 int -keepSynNetsWithScore int -keepInvNetsWithScore int]\n"
+            "\t    OR [-minScore comma-separated-string -minSizeT comma-separated-string -minSizeQ comma-separated-string]\n"
+            "\t    OR [-minScore1 int -minSizeT1 int -minSizeQ1 int  -minScore2 int -minSizeT2 int -minSizeQ2 int]\n"
+            "(this native build does not implement -v)\n\n");
     exit(255);
 }
 
@@ -78,10 +82,10 @@ static int split_nums(const char *s, double **out) {
 
 int main(int argc, char *argv[]) {
     int s1 = 0, t1 = 0, q1 = 0, s2 = 0, t2 = 0, q2 = 0;
+    int ucsc = 0, score_filter = 0, keep_syn = INT_MAX, keep_inv = INT_MAX;
     const char *ms = "", *mt = "", *mq = "";
     const char *input = NULL;
-    static const char *unsupported[] = {"v", "verbose", "doUCSCSynFilter", "doScoreFilter",
-                                        "keepSynNetsWithScore", "keepInvNetsWithScore", NULL};
+    static const char *unsupported[] = {"v", "verbose", NULL};
     for (int i = 1; i < argc; ++i) {
         const char *a = argv[i];
         if (a[0] != '-' || a[1] == 0) {
@@ -99,8 +103,20 @@ int main(int argc, char *argv[]) {
         for (int k = 0; unsupported[k]; ++k)
             if (strcasecmp(key, unsupported[k]) == 0)
                 gt_abort("NetFilterNonNested: option -%s is not supported by this native build", key);
+        if (strcasecmp(key, "doUCSCSynFilter") == 0 || strcasecmp(key, "doScoreFilter") == 0) {
+            if (eq) { /* a boolean takes no value */
+                fprintf(stderr, "Option %s does not take an argument\n", key);
+                usage();
+            }
+            *(strcasecmp(key, "doUCSCSynFilter") == 0 ? &ucsc : &score_filter) = 1;
+            continue;
+        }
         const char *val = eq ? eq + 1 : (i + 1 < argc ? argv[++i] : NULL);
-        if (strcasecmp(key, "minScore1") == 0)
+        if (strcasecmp(key, "keepSynNetsWithScore") == 0)
+            keep_syn = parse_int(key, val);
+        else if (strcasecmp(key, "keepInvNetsWithScore") == 0)
+            keep_inv = parse_int(key, val);
+        else if (strcasecmp(key, "minScore1") == 0)
             s1 = parse_int(key, val);
         else if (strcasecmp(key, "minSizeT1") == 0)
             t1 = parse_int(key, val);
@@ -125,29 +141,38 @@ int main(int argc, char *argv[]) {
     }
     if (!input)
         usage();
+    if (score_filter && s1 == 0)
+        gt_abort("ERROR: you have to set -minScore1 with -doScoreFilter");
     int mode12 = s1 || t1 || q1 || s2 || t2 || q2;
     int batch = *ms || *mt || *mq;
     if (batch && mode12)
         gt_abort("ERROR: you have used BOTH batch filtering (minScore/minSizeT/minSizeQ) AND individual filtering (minScore1/minSizeT1/minSizeQ1 etc)\n\n"
                  "\t\t     USE Either batch or individual");
-    if (!batch && !mode12)
-        gt_abort("ERROR: unknown value for filterMode ");
     gt_lines in, out;
     gt_lines_read(input, &in);
-    if (mode12) {
-        gt_netfilter_nonnested(&in, input, s1, t1, q1, s2, t2, q2, &out);
-    } else {
-        double *a, *b, *c;
+    gt_netfilter_opts o = {0, NULL, NULL, NULL, ucsc, score_filter, s1, keep_syn, keep_inv};
+    double sc[2], ts[2], qs[2], *a = NULL, *b = NULL, *c = NULL;
+    if (mode12) { /* an unset set is INT_MAX (:96-108) */
+        if (s2 == 0 && t2 == 0 && q2 == 0)
+            s2 = t2 = q2 = INT_MAX;
+        if (s1 == 0 && t1 == 0 && q1 == 0)
+            s1 = t1 = q1 = INT_MAX;
+        sc[0] = s1, ts[0] = t1, qs[0] = q1, sc[1] = s2, ts[1] = t2, qs[1] = q2;
+        o.nsets = 2;
+        o.set_score = sc, o.set_t = ts, o.set_q = qs;
+    } else if (batch) {
         const int na = split_nums(ms, &a), nb = split_nums(mt, &b), nc = split_nums(mq, &c);
         if (na != nb)
             gt_abort("ERROR: number of minScores differ from minTsizes");
         if (na != nc)
             gt_abort("ERROR: number of minScores differ from minQsizes");
-        gt_netfilter_sets(&in, input, na, a, b, c, &out);
-        free(a);
-        free(b);
-        free(c);
+        o.nsets = na;
+        o.set_score = a, o.set_t = b, o.set_q = c;
     }
+    gt_netfilter(&in, input, &o, &out);
+    free(a);
+    free(b);
+    free(c);
     for (int64_t i = 0; i < out.n; ++i) {
         fputs(out.line[i], stdout);
         fputc('\n', stdout);

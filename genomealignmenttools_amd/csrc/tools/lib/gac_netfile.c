@@ -223,10 +223,106 @@ void gt_netfilter_nonnested(const gt_lines *in, const char *what, double s1, dou
 
 void gt_netfilter_sets(const gt_lines *in, const char *what, int nsets, const double *set_score,
                        const double *set_t, const double *set_q, gt_lines *out) {
+    gt_netfilter_opts o = {nsets, set_score, set_t, set_q, 0, 0, 0, INT_MAX, INT_MAX};
+    gt_netfilter(in, what, &o, out);
+}
+
+/* first match of /<key>(X+) / in s (X: \w or \d) -- or, with at_end, of
+ * /<key>(X+)$/; the value as a string in buf */
+static int find_field(const char *s, const char *key, int word, int at_end, char *buf,
+                      size_t cap) {
+    const size_t kl = strlen(key);
+    for (const char *p = strstr(s, key); p; p = strstr(p + 1, key)) {
+        const char *v = p + kl, *q = v;
+        while (*q && (word ? (isalnum((unsigned char)*q) || *q == '_') : isdigit((unsigned char)*q)))
+            ++q;
+        if (q == v || (at_end ? *q != 0 : *q != ' '))
+            continue;
+        snprintf(buf, cap, "%.*s", (int)(q - v), v);
+        return 1;
+    }
+    return 0;
+}
+
+/* Level2IsSkipped (a perl hash: absent = 0) */
+typedef struct lvmap {
+    char *v;
+    int n;
+} lvmap;
+
+static int lv_get(const lvmap *m, int k) { return k >= 0 && k < m->n ? m->v[k] : 0; }
+
+static void lv_set(lvmap *m, int k, int x) {
+    if (k < 0)
+        return;
+    if (k >= m->n) {
+        const int n2 = k + 64;
+        m->v = realloc(m->v, (size_t)n2);
+        memset(m->v + m->n, 0, (size_t)(n2 - m->n));
+        m->n = n2;
+    }
+    m->v[k] = (char)x;
+}
+
+/* testInvSynNet (:330-361) */
+static int inv_syn_ok(const gt_netfilter_opts *o, const lvmap *skipped, double score,
+                      const char *type, int level) {
+    if (lv_get(skipped, level - 2) != 0)
+        return 0;
+    if (strcmp(type, "inv") == 0)
+        return score >= o->keep_inv;
+    if (strcmp(type, "syn") == 0)
+        return score >= o->keep_syn;
+    return 0;
+}
+
+/* passesFilter (:365-396) with UCSCsynFilter_nonRecursive (:268-302) and
+ * scoreFilter_nonRecursive (:305-327) */
+static int passes(const gt_netfilter_opts *o, const lvmap *skipped, double score, double tsz,
+                  double qsz, const char *type, double ali, double qfar, int level) {
+    if (o->ucsc) {
+        if (!*type)
+            gt_abort("No type field, please run input net through netSyntenic");
+        if (score >= 200000 && tsz >= 20000 && ali >= 10000) /* minSynScore/Size/Ali */
+            return 1;
+        if (strcmp(type, "top") == 0)
+            return score >= 300000; /* minTopScore */
+        if (strcmp(type, "nonSyn") == 0)
+            return 0;
+        if (qfar > 200000) /* maxFar */
+            return 0;
+        return inv_syn_ok(o, skipped, score, type, level);
+    }
+    if (o->score_filter) {
+        if (!*type)
+            gt_abort("No type field, please run input net through netSyntenic");
+        if (score >= o->min_score1)
+            return 1;
+        if (strcmp(type, "top") == 0 || strcmp(type, "nonSyn") == 0)
+            return 0;
+        return inv_syn_ok(o, skipped, score, type, level);
+    }
+    if (strcmp(type, "syn") == 0 && score >= o->keep_syn)
+        return 1;
+    if (strcmp(type, "inv") == 0 && score >= o->keep_inv)
+        return 1;
+    if (o->nsets == 0)
+        gt_abort("ERROR: unknown value for filterMode \n");
+    for (int k = 0; k < o->nsets; ++k)
+        if (score >= o->set_score[k] && tsz >= o->set_t[k] && qsz >= o->set_q[k])
+            return 1;
+    return 0;
+}
+
+void gt_netfilter(const gt_lines *in, const char *what, const gt_netfilter_opts *o,
+                  gt_lines *out) {
     memset(out, 0, sizeof(*out));
     const int64_t n = in->n;
     char *skip = calloc(n ? n : 1, 1);
     int *minus = calloc(n ? n : 1, sizeof(int));
+    const int want_type = o->keep_syn < INT_MAX || o->keep_inv < INT_MAX || o->ucsc;
+    lvmap skipped = {NULL, 0};
+    int max_level = 1;
     /* the script keys its per-net counter by the net line's text */
     gt_names netkey;
     memset(&netkey, 0, sizeof(netkey));
@@ -292,12 +388,32 @@ void gt_netfilter_sets(const gt_lines *in, const char *what, int nsets, const do
         }
         const double tsz = nf > 2 ? field_num(f[2]) : 0, qsz = nf > 6 ? field_num(f[6]) : 0;
         free(copy);
-        int pass = 0;
-        for (int k = 0; k < nsets && !pass; ++k)
-            pass = score >= set_score[k] && tsz >= set_t[k] && qsz >= set_q[k];
-        if (pass) {
+        char type[64] = "", num[64];
+        if (want_type && !find_field(rest, "type ", 1, 0, type, sizeof(type)) &&
+            !find_field(rest, "type ", 1, 1, type, sizeof(type)))
+            gt_abort("ERROR: parameter -keepSynNetsWithScore/-keepInvNetsWithScore-doUCSCSynFilter is given, but I cannot parse the net type from this fill line: %s\n",
+                     rest);
+        double ali = 0, qfar = 0;
+        if (o->ucsc) {
+            if (!find_field(rest, "ali ", 0, 0, num, sizeof(num)))
+                gt_abort("ERROR: parameter -doUCSCSynFilter is given, but I cannot parse the ali filed from this fill line: %s\n",
+                         rest);
+            ali = atof(num);
+            if (strcmp(type, "inv") == 0 || strcmp(type, "syn") == 0) {
+                if (!find_field(rest, "qFar ", 0, 0, num, sizeof(num)))
+                    gt_abort("ERROR: parameter -doUCSCSynFilter is given, but I cannot parse the qFar filed from this syn/inv fill line: %s\n",
+                             rest);
+                qfar = atof(num);
+            }
+        }
+        if (max_level < level)
+            max_level = level;
+        if (passes(o, &skipped, score, tsz, qsz, type, ali, qfar, level)) {
             kept[cur]++;
+            for (int l = level; l <= max_level; ++l) /* resetLevel2IsSkipped */
+                lv_set(&skipped, l, 0);
         } else {
+            lv_set(&skipped, level, 1);
             skip[k] = 1;
             /* eraseGapsMarkSkip(k + 1, level) */
             for (int64_t j = k + 1; j < n; ++j) {
@@ -344,5 +460,6 @@ void gt_netfilter_sets(const gt_lines *in, const char *what, int nsets, const do
     free(skip);
     free(minus);
     free(kept);
+    free(skipped.v);
     gt_names_free(&netkey);
 }

@@ -64,6 +64,21 @@ void gt_netfilter_nonnested(const gt_lines *in, const char *what, double s1, dou
 void gt_netfilter_sets(const gt_lines *in, const char *what, int nsets, const double *set_score,
                        const double *set_t, const double *set_q, gt_lines *out);
 
+/* All of NetFilterNonNested.perl's filter modes (:87-120, :268-396):
+ *   ucsc          -doUCSCSynFilter: UCSC netFilter -syn thresholds, non-nested
+ *   score_filter  -doScoreFilter: keep score >= min_score1, plus syn/inv nets
+ *   keep_syn/inv  -keepSynNetsWithScore / -keepInvNetsWithScore (INT_MAX: off)
+ *   sets          the "12" / batch (score, tSize, qSize) sets (nsets 0: none;
+ *                 a fill then reaching that test is an error, as in the script)
+ * The type / ali / qFar fields come from netSyntenic's fill lines. */
+typedef struct gt_netfilter_opts {
+    int nsets;
+    const double *set_score, *set_t, *set_q;
+    int ucsc, score_filter;
+    double min_score1, keep_syn, keep_inv;
+} gt_netfilter_opts;
+void gt_netfilter(const gt_lines *in, const char *what, const gt_netfilter_opts *o, gt_lines *out);
+
 #ifdef __cplusplus
 }
 #endif

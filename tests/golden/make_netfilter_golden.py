@@ -10,7 +10,10 @@ tests/golden/netfilter/
                       synth11/synth12 and its -minScore=0 net of the cleaner
                       set (chainCleaner's own self-netting input)
   <net>.<case>.out    the perl script's output
-  cases.json          option lists
+  <net>.syn.net       the reference netSyntenic's typed version of a net (and
+                      of a C5-shaped set's -minScore=0 target net, "big")
+  <net>.syn.<case>.out  the perl script's synteny / score / keep-type modes
+  cases.json, typed_cases.json  option lists
 """
 import json
 import os
@@ -23,6 +26,20 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 PERL = "/root/reference/src/NetFilterNonNested.perl"
 REF_BIN = os.path.join(REPO, "oracle", "_ref")
 OUT = os.path.join(HERE, "netfilter")
+
+# the synteny modes read netSyntenic's type/qFar fields: typed nets come from
+# the reference netSyntenic (oracle/_ref/netSyntenic) on the nets above plus
+# a C5-shaped set with large scores (UCSC thresholds: 200k / 300k)
+TYPED_CASES = {
+    "ucsc": ["-doUCSCSynFilter"],
+    "ucsc_keep": ["-doUCSCSynFilter", "-keepSynNetsWithScore", "5000", "-keepInvNetsWithScore",
+                  "5000"],
+    "scoref": ["-doScoreFilter", "-minScore1", "10000", "-keepSynNetsWithScore", "3000",
+               "-keepInvNetsWithScore", "3000"],
+    "keep12": ["-minScore1", "20000", "-keepSynNetsWithScore", "2000"],
+    "keepbatch": ["-minScore", "50000,10000", "-minSizeT", "0,5000", "-minSizeQ", "0,5000",
+                  "-keepInvNetsWithScore", "1000"],
+}
 
 CASES = {
     "s3000": ["-minScore1", "3000"],
@@ -51,8 +68,44 @@ def main():
             with open(os.path.join(OUT, f"{name}.{case}.out"), "w") as f:
                 f.write(r.stdout)
             print(name, case, r.stdout.count("fill"), "fills kept", file=sys.stderr)
+    # typed nets
+    sys.path.insert(0, REPO)
+    from genomealignmenttools_amd import chainfile, synth
+    import tempfile
+    with tempfile.TemporaryDirectory() as tmp:
+        tg, qg, ca = synth.c5_case(seed=99, n_chains=2500, scale=0.004, min_size=20000)
+        synth.write_sizes(tg.sizes, os.path.join(tmp, "t.sizes"))
+        synth.write_sizes(qg.sizes, os.path.join(tmp, "q.sizes"))
+        chainfile.write_chains(ca, os.path.join(tmp, "in.chain"))
+        subprocess.run([os.path.join(REF_BIN, "chainNet"), "-minScore=0",
+                        os.path.join(tmp, "in.chain"), os.path.join(tmp, "t.sizes"),
+                        os.path.join(tmp, "q.sizes"), os.path.join(tmp, "big.net"), "/dev/null"],
+                       check=True, capture_output=True)
+        # netSyntenic rejects a "net" line without fills (chainNet prints one
+        # when every fill of a sequence is below -minFill): drop those
+        with open(os.path.join(tmp, "big.net")) as f:
+            lines = f.read().split("\n")
+        keep = [l for i, l in enumerate(lines) if not (l.startswith("net ") and (
+            i + 1 >= len(lines) or not lines[i + 1].startswith(" ")))]
+        with open(os.path.join(tmp, "big.net"), "w") as f:
+            f.write("\n".join(keep))
+        for name, src in [("synth11", os.path.join(OUT, "synth11.net")),
+                          ("cleaner", os.path.join(OUT, "cleaner.net")),
+                          ("big", os.path.join(tmp, "big.net"))]:
+            dst = os.path.join(OUT, f"{name}.syn.net")
+            subprocess.run([os.path.join(REF_BIN, "netSyntenic"), src, dst], check=True,
+                           capture_output=True)
+            for case, opts in TYPED_CASES.items():
+                r = subprocess.run(["perl", PERL, dst] + opts, capture_output=True, text=True)
+                assert r.returncode == 0, r.stderr
+                with open(os.path.join(OUT, f"{name}.syn.{case}.out"), "w") as f:
+                    f.write(r.stdout)
+                print(name, case, r.stdout.count("fill"), "fills kept of",
+                      open(dst).read().count("fill"), file=sys.stderr)
     with open(os.path.join(OUT, "cases.json"), "w") as f:
         json.dump(CASES, f, indent=1)
+    with open(os.path.join(OUT, "typed_cases.json"), "w") as f:
+        json.dump(TYPED_CASES, f, indent=1)
 
 
 if __name__ == "__main__":

@@ -277,6 +277,44 @@ def test_netfilter_nonnested_vs_reference(net, case):
     assert r.stdout == open(os.path.join(d, f"{net}.{case}.out")).read()
 
 
+@pytest.mark.parametrize("net", ["synth11", "cleaner", "big"])
+@pytest.mark.parametrize("case", ["ucsc", "ucsc_keep", "scoref", "keep12", "keepbatch"])
+def test_netfilter_typed_modes_vs_reference(net, case):
+    """The synteny / score / keep-type modes (-doUCSCSynFilter,
+    -doScoreFilter, -keepSyn/InvNetsWithScore; src/NetFilterNonNested.perl:
+    268-396) on nets typed by the reference netSyntenic: byte-identical to
+    the reference perl script (tests/golden/make_netfilter_golden.py)."""
+    import json
+    from genomealignmenttools_amd._lib import BIN_DIR
+    d = os.path.join(GOLDEN, "netfilter")
+    with open(os.path.join(d, "typed_cases.json")) as f:
+        opts = json.load(f)[case]
+    r = subprocess.run([os.path.join(BIN_DIR, "NetFilterNonNested.perl"),
+                        os.path.join(d, f"{net}.syn.net")] + opts, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout == open(os.path.join(d, f"{net}.syn.{case}.out")).read()
+
+
+def test_netfilter_mode_errors():
+    """The script's checks: -doScoreFilter needs -minScore1; the synteny modes
+    need netSyntenic's type field; batch and "12" sets do not mix."""
+    from genomealignmenttools_amd._lib import BIN_DIR
+    tool = os.path.join(BIN_DIR, "NetFilterNonNested.perl")
+    d = os.path.join(GOLDEN, "netfilter")
+    r = subprocess.run([tool, os.path.join(d, "synth11.syn.net"), "-doScoreFilter"],
+                       capture_output=True, text=True)
+    assert r.returncode == 255 and "-minScore1 with -doScoreFilter" in r.stderr
+    r = subprocess.run([tool, os.path.join(d, "synth11.net"), "-doUCSCSynFilter"],
+                       capture_output=True, text=True)
+    assert r.returncode == 255 and "cannot parse the net type" in r.stderr
+    r = subprocess.run([tool, os.path.join(d, "synth11.syn.net"), "-doScoreFilter",
+                        "-minScore1=40000"], capture_output=True, text=True)
+    assert r.returncode == 255 and "No type field" in r.stderr  # the script's own quirk
+    r = subprocess.run([tool, os.path.join(d, "synth11.net"), "-minScore1", "5", "-minScore", "3"],
+                       capture_output=True, text=True)
+    assert r.returncode == 255 and "BOTH batch filtering" in r.stderr
+
+
 def _c5_small(tmp_path):
     from genomealignmenttools_amd import chainfile, synth
     tg, qg, ca = synth.c5_case(seed=77, n_chains=6000, scale=0.002, min_size=5000)
