@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -103,7 +104,19 @@ struct Prof {
 
 constexpr size_t kStatusBytes = 128;  // status[0..8)
 
+// held by every entry point that uses a context (see gac_ctx::mu)
+#define CTX_LOCK(c) std::lock_guard<std::recursive_mutex> ctx_lock_((c)->mu)
+
 struct gac_ctx {
+    // every entry point that touches the context's state holds this (the
+    // ABI is thread-safe per context; calls are serialised)
+    std::recursive_mutex mu;
+    // the scoring workspace is stream-ordered: ws_ev is recorded on the
+    // stream of the last call that used it (ws_last); a call on another
+    // stream waits for it on the device, and growing the workspace waits
+    // for it on the host
+    hipEvent_t ws_ev = nullptr;
+    hipStream_t ws_last = nullptr;
     int device = 0;
     char arch[64] = {0};
     hipStream_t stream = nullptr;
@@ -209,6 +222,11 @@ extern "C" int gac_open(int device, gac_ctx **out) {
         delete c;
         return gac_fail(GAC_E_HIP, "hipStreamCreate failed");
     }
+    if (hipEventCreateWithFlags(&c->ws_ev, hipEventDisableTiming) != hipSuccess) {
+        hipStreamDestroy(c->stream);
+        delete c;
+        return gac_fail(GAC_E_HIP, "hipEventCreate failed");
+    }
     lap("hipStreamCreate");
     c->combine_grid = prop.multiProcessorCount * 8;  // one 64-range group per wave
     c->tile_grid_g = prop.multiProcessorCount * persistent_blocks_per_cu(0);
@@ -271,6 +289,7 @@ extern "C" void gac_close(gac_ctx *c) {
         if (c->pin[k]) hipHostFree(c->pin[k]);
         if (c->pin_ev[k]) hipEventDestroy(c->pin_ev[k]);
     }
+    if (c->ws_ev) hipEventDestroy(c->ws_ev);
     hipStreamDestroy(c->stream);
     delete c;
 }
@@ -286,6 +305,7 @@ static int acgt_of_code(int code) {  // 2bit code T=0 C=1 A=2 G=3 -> A,C,G,T ind
 extern "C" int gac_set_scoring(gac_ctx *c, const int32_t mat[16], const gac_gapcalc *g) {
     gac_clear_error();
     if (!c || !mat || !g) return gac_fail(GAC_E_ARG, "gac_set_scoring: NULL argument");
+    CTX_LOCK(c);
     if (g->long_count < 2 || g->long_count > kMaxLong)
         return gac_fail(GAC_E_ARG, "gap table has %d long positions (2..%d supported)",
                         g->long_count, kMaxLong);
@@ -432,6 +452,8 @@ static int add_seq(gac_ctx *c, int side, const char *name, int32_t size, const u
 extern "C" int gac_genome_add_seq(gac_ctx *c, int side, const char *name, int32_t size,
                                   const uint8_t *packed, int32_t n_nblocks,
                                   const int32_t *n_starts, const int32_t *n_sizes) {
+    if (!c) return gac_fail(GAC_E_ARG, "NULL context");
+    CTX_LOCK(c);
     return add_seq(c, side, name, size, packed, true, n_nblocks, n_starts, n_sizes);
 }
 
@@ -524,6 +546,7 @@ extern "C" int gac_genome_finalize(gac_ctx *c, int side) {
     gac_clear_error();
     Genome *g = side_of(c, side);
     if (!g) return gac_fail(GAC_E_ARG, "gac_genome_finalize: bad side");
+    CTX_LOCK(c);
     if (g->final) return gac_fail(GAC_E_STATE, "genome side %d already finalized", side);
     HIPCHK(hipSetDevice(c->device));
     const int nseq = (int)g->names.size();
@@ -597,6 +620,7 @@ extern "C" int gac_genome_load_twobit(gac_ctx *c, int side, gac_twobit *tbp) {
         if (tbp) gac_twobit_close(tbp);
         return gac_fail(GAC_E_ARG, "gac_genome_load_twobit: bad argument");
     }
+    CTX_LOCK(c);
     gac_twobit tb = *tbp;
     int rc = GAC_OK;
     std::vector<int32_t> ns, nz;
@@ -695,6 +719,7 @@ extern "C" int gac_score_blocks(gac_ctx *c, int64_t n_pairs, const int32_t *t_se
     if (!c || n_pairs < 0 || (n_pairs && (!t_seq || !q_seq || !q_strand || !blk_off)))
         return gac_fail(GAC_E_ARG, "gac_score_blocks: bad argument");
     if (!c->scoring) return gac_fail(GAC_E_STATE, "gac_score_blocks before gac_set_scoring");
+    CTX_LOCK(c);
     if (!c->g[0].final || !c->g[1].final)
         return gac_fail(GAC_E_STATE, "load both genomes before scoring blocks");
     const int64_t n = n_pairs ? blk_off[n_pairs] : 0;
@@ -860,6 +885,7 @@ static int upload_staged(gac_ctx *c, void *d_dst, const void *h_src, size_t byte
 extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_chainset **out) {
     gac_clear_error();
     if (!c || !d || !out) return gac_fail(GAC_E_ARG, "gac_chains_upload: NULL argument");
+    CTX_LOCK(c);
     *out = nullptr;
     if (!c->g[0].final || !c->g[1].final)
         return gac_fail(GAC_E_STATE, "load both genomes before uploading chains");
@@ -965,7 +991,8 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
 
 extern "C" void gac_chains_free(gac_chainset *cs) {
     if (!cs) return;
-    hipSetDevice(cs->ctx->device);
+    CTX_LOCK(cs->ctx);
+    hipSetDevice(cs->ctx->device);  // (hipFree waits for work still using them)
     if (cs->chains) hipFree(cs->chains);
     if (cs->blk) hipFree(cs->blk);
     if (cs->tspan) hipFree(cs->tspan);
@@ -977,8 +1004,12 @@ extern "C" int64_t gac_chains_block_count(const gac_chainset *cs) { return cs ? 
 
 // ----------------------------------------------------------------- launch
 static int ensure_ws(gac_ctx *c, int64_t n, int64_t max_tiles, hipStream_t s) {
-    // buffers may still be in use by calls in flight on the stream
-    if (n > c->ws_n || max_tiles > c->ws_tiles || !c->status) HIPCHK(hipStreamSynchronize(s));
+    // buffers may still be in use by calls in flight (on this stream or, for
+    // the device-pointer API, on the stream of the previous call)
+    if (n > c->ws_n || max_tiles > c->ws_tiles || !c->status) {
+        HIPCHK(hipStreamSynchronize(s));
+        if (c->ws_last && c->ws_last != s) HIPCHK(hipEventSynchronize(c->ws_ev));
+    }
     if (n > c->ws_n) {
         int64_t cap = n + n / 2 + 1024;
         void *bufs[] = {c->rdesc, c->nblk, c->goff, c->pb0, c->agg, c->plan_off, c->gflat};
@@ -1106,12 +1137,28 @@ static int prepare_args(gac_ctx *c, const gac_chainset *cs, int64_t n, uint32_t 
     return GAC_OK;
 }
 
+static int score_device_split(gac_ctx *c, const ScoreArgs &a_base, const Range *d_ranges,
+                              int64_t n, long long *d_g, long long *d_l, int32_t *d_ali,
+                              hipStream_t s);
+
 static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_ranges, int64_t n,
                         uint32_t flags, long long *d_g, long long *d_l, int32_t *d_ali,
                         hipStream_t s) {
     ScoreArgs a_base;
+    if (c->ws_last && c->ws_last != s) HIPCHK(hipStreamWaitEvent(s, c->ws_ev, 0));
     int rc = prepare_args(c, cs, n, flags, d_l, s, a_base);
     if (rc != GAC_OK || n == 0) return rc;
+    rc = score_device_split(c, a_base, d_ranges, n, d_g, d_l, d_ali, s);
+    if (hipEventRecord(c->ws_ev, s) == hipSuccess) c->ws_last = s;
+    return rc;
+}
+
+// One batch through the pipeline; a batch whose window blocks overflow int32
+// (kernels index flat blocks with 32 bits) is split in halves, recursively.
+static int score_device_split(gac_ctx *c, const ScoreArgs &a_base, const Range *d_ranges,
+                              int64_t n, long long *d_g, long long *d_l, int32_t *d_ali,
+                              hipStream_t s) {
+    int rc;
     // first guess for an empty workspace: 8 window blocks per range
     const int64_t guess = c->ws_tiles ? 0 : 8 * n;
     rc = ensure_ws(c, n, guess / kTileBlocks + 1, s);
@@ -1157,9 +1204,17 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
         int32_t st[4];
         rc = wait_status(c, s, a.call_tag, st);
         if (rc != GAC_OK) return rc;
-        if (st[0] == INT32_MAX) {
+        if (st[0] == INT32_MAX) {  // W >= 2^31: two halves
             HIPCHK(hipStreamSynchronize(s));
-            return gac_fail(GAC_E_ARG, "window block total overflows int32");
+            if (n < 2) return gac_fail(GAC_E_ARG, "one range's window exceeds 2^31 blocks");
+            const int64_t h = n / 2;
+            ScoreArgs b = a_base;
+            b.n = h;
+            rc = score_device_split(c, b, d_ranges, h, d_g, d_l, d_ali, s);
+            if (rc != GAC_OK) return rc;
+            b.n = n - h;
+            return score_device_split(c, b, d_ranges + h, n - h, d_g + h, d_l ? d_l + h : nullptr,
+                                      d_ali + h, s);
         }
         if (!st[2]) return GAC_OK;
         rc = ensure_ws(c, n, st[1], s);  // (synchronises before growing)
@@ -1173,6 +1228,7 @@ extern "C" int gac_score_ranges_device(gac_ctx *c, const gac_chainset *cs, const
                                        int32_t *d_ali, void *stream) {
     gac_clear_error();
     if (!c) return gac_fail(GAC_E_ARG, "NULL context");
+    CTX_LOCK(c);
     if (n > 0 && (!d_ranges || !d_g || !d_ali)) return gac_fail(GAC_E_ARG, "NULL buffer");
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
@@ -1185,6 +1241,7 @@ extern "C" int gac_score_ranges(gac_ctx *c, const gac_chainset *cs, const gac_ra
                                 int32_t *ali) {
     gac_clear_error();
     if (!c) return gac_fail(GAC_E_ARG, "NULL context");
+    CTX_LOCK(c);
     if (n < 0) return gac_fail(GAC_E_ARG, "negative range count");
     if (n == 0) return GAC_OK;
     if (!ranges || !global || !ali || ((flags & GAC_WANT_LOCAL) && !local))
@@ -1253,18 +1310,21 @@ extern "C" int gac_dev_free(gac_ctx *c, void *p) {
 }
 extern "C" int gac_memcpy_h2d(gac_ctx *c, void *dst, const void *src, size_t n) {
     if (!c) return gac_fail(GAC_E_ARG, "NULL context");
+    CTX_LOCK(c);
     HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return GAC_OK;
 }
 extern "C" int gac_memcpy_d2h(gac_ctx *c, void *dst, const void *src, size_t n) {
     if (!c) return gac_fail(GAC_E_ARG, "NULL context");
+    CTX_LOCK(c);
     HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return GAC_OK;
 }
 extern "C" int gac_synchronize(gac_ctx *c) {
     if (!c) return gac_fail(GAC_E_ARG, "NULL context");
+    CTX_LOCK(c);
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipDeviceSynchronize());
     return GAC_OK;
@@ -1273,6 +1333,7 @@ extern "C" int gac_synchronize(gac_ctx *c) {
 // ----------------------------------------------------------------- profiling
 extern "C" int gac_prof_enable(gac_ctx *c, int on) {
     if (!c) return gac_fail(GAC_E_ARG, "NULL context");
+    CTX_LOCK(c);
     c->prof = on & GAC_PROF_ALL;
     return GAC_OK;
 }
@@ -1293,6 +1354,7 @@ static int prof_fold(gac_ctx *c) {
 
 extern "C" int gac_prof_read(gac_ctx *c, int k, double *ms, int64_t *n) {
     if (!c || k < 0 || k >= GAC_K_COUNT) return gac_fail(GAC_E_ARG, "bad argument");
+    CTX_LOCK(c);
     int rc = prof_fold(c);
     if (rc != GAC_OK) return rc;
     if (ms) *ms = c->prof_ms[k];
@@ -1302,6 +1364,7 @@ extern "C" int gac_prof_read(gac_ctx *c, int k, double *ms, int64_t *n) {
 
 extern "C" int gac_prof_reset(gac_ctx *c) {
     if (!c) return gac_fail(GAC_E_ARG, "NULL context");
+    CTX_LOCK(c);
     int rc = prof_fold(c);
     if (rc != GAC_OK) return rc;
     for (int k = 0; k < GAC_K_COUNT; ++k) {

@@ -319,3 +319,95 @@ def test_unfused_tile_map_path(monkeypatch):
     monkeypatch.setenv("GAC_UNFUSED_MAP", "1")
     g, l, a = e.score_ranges(cs, R, want_local=True)
     assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
+
+
+def _hip():
+    import ctypes as C
+    h = C.CDLL("libamdhip64.so")
+    h.hipStreamCreate.argtypes = [C.POINTER(C.c_void_p)]
+    h.hipStreamSynchronize.argtypes = [C.c_void_p]
+    h.hipStreamDestroy.argtypes = [C.c_void_p]
+    return h
+
+
+def test_two_streams_and_threads_one_context():
+    """The device-pointer call on two foreign streams of one context (the
+    shared workspace is stream-ordered; a batch that grows it waits for the
+    other stream), and the host call from two threads at once (calls on a
+    context are serialised): every result equals the oracle's."""
+    import ctypes as C
+    import threading
+
+    from genomealignmenttools_amd import synth
+    tg, qg, ca = synth.small_case(seed=31, n_chains=300)
+    e, cs = _setup(None, tg, qg, ca)
+    rng = np.random.default_rng(4)
+    Ra = _ranges(ca, rng, per_chain=3)
+    Rb = np.concatenate([_ranges(ca, rng, per_chain=12)] * 4)  # larger: grows the workspace
+    og_a, _, oa_a = _oracle(tg, qg).score_ranges(ca, Ra)
+    og_b, _, oa_b = _oracle(tg, qg).score_ranges(ca, Rb)
+    hip = _hip()
+    streams = [C.c_void_p(), C.c_void_p()]
+    for st in streams:
+        assert hip.hipStreamCreate(C.byref(st)) == 0
+    bufs = []
+    for R in (Ra, Rb):
+        R32 = np.ascontiguousarray(R, np.int32)
+        d_r = e.dev_alloc(R32.nbytes)
+        e.h2d(d_r, R32)
+        bufs.append((d_r, e.dev_alloc(8 * len(R)), e.dev_alloc(4 * len(R)), len(R)))
+    for _ in range(3):
+        for (d_r, d_g, d_a, n), st in zip(bufs, streams):
+            e.score_ranges_device(cs, d_r, n, d_g, d_a, stream=st.value)
+    for st in streams:
+        assert hip.hipStreamSynchronize(st) == 0
+    for (d_r, d_g, d_a, n), og, oa in zip(bufs, (og_a, og_b), (oa_a, oa_b)):
+        g = np.zeros(n, np.int64)
+        a = np.zeros(n, np.int32)
+        e.d2h(g, d_g)
+        e.d2h(a, d_a)
+        assert np.array_equal(g, og) and np.array_equal(a, oa)
+    for st in streams:
+        hip.hipStreamDestroy(st)
+    out = {}
+
+    def work(k, R):
+        for _ in range(5):
+            out[k] = e.score_ranges(cs, R)
+    th = [threading.Thread(target=work, args=(k, R)) for k, R in enumerate((Ra, Rb, Ra[:100]))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert np.array_equal(out[0][0], og_a) and np.array_equal(out[1][0], og_b)
+    assert np.array_equal(out[2][0], og_a[:100])
+
+
+@pytest.mark.timeout(600)
+def test_window_blocks_over_int32_are_split():
+    """A batch whose windows hold more than 2^31 blocks in total (1800 full
+    ranges of a 1.2 M-block chain: 2.16e9): split in halves instead of
+    failing; every range scores like the single one, which equals the
+    oracle's."""
+    from genomealignmenttools_amd import synth
+    from genomealignmenttools_amd.chainfile import ChainArrays
+    nb = 1_200_000
+    tg = synth.random_genome({"t": 2 * nb + 1000}, 41, n_frac=0.0)
+    qg = synth.random_genome({"q": 3 * nb + 1000}, 42, n_frac=0.0)
+    bt = (10 + 2 * np.arange(nb)).astype(np.int32)
+    bq = (20 + 3 * np.arange(nb)).astype(np.int32)
+    bs = np.ones(nb, np.int32)
+    ca = ChainArrays(score=np.zeros(1), tname=["t"], tsize=np.array([2 * nb + 1000], np.int32),
+                     tstart=bt[:1].copy(), tend=np.array([bt[-1] + 1], np.int32), qname=["q"],
+                     qsize=np.array([3 * nb + 1000], np.int32), qstrand=np.zeros(1, np.uint8),
+                     qstart=bq[:1].copy(), qend=np.array([bq[-1] + 1], np.int32),
+                     id=np.array([1], np.int64), blk_off=np.array([0, nb], np.int64),
+                     blk_t=bt, blk_q=bq, blk_size=bs)
+    e, cs = _setup(None, tg, qg, ca)
+    one = np.array([[0, int(bt[0]), int(bt[-1]) + 1]], np.int64)
+    g1, l1, a1 = e.score_ranges(cs, one, want_local=True)
+    og, ol, oa = _oracle(tg, qg).score_ranges(ca, one)
+    assert g1[0] == og[0] and l1[0] == ol[0] and a1[0] == oa[0] == nb
+    R = np.repeat(one, 1800, axis=0)
+    g, l, a = e.score_ranges(cs, R, want_local=True)
+    assert (g == g1[0]).all() and (l == l1[0]).all() and (a == nb).all()
