@@ -37,7 +37,7 @@ TOOLS    := $(addprefix $(EXECDIR)/,$(GPU_TOOLS)) $(addprefix $(BINDIR)/,$(GPU_T
 TOOL_LIB_SRC := $(wildcard $(CSRC)/tools/lib/*.c)
 TOOL_LIB_OBJ := $(patsubst $(CSRC)/tools/lib/%.c,$(OBJDIR)/tools/lib/%.o,$(TOOL_LIB_SRC))
 
-all: $(LIBDIR)/libgachain.so $(TOOLS)
+all: $(LIBDIR)/libgachain.so $(LIBDIR)/libgachain_kent.so $(TOOLS)
 
 $(OBJDIR)/host/%.o: $(CSRC)/host/%.c $(HDRS)
 	@mkdir -p $(dir $@)
@@ -50,6 +50,11 @@ $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 $(LIBDIR)/libgachain.so: $(HIP_OBJ) $(HOST_OBJ)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,libgachain.so
+
+# kent-signature shims over the batch ABI (include/gachain_kent.h)
+$(LIBDIR)/libgachain_kent.so: $(CSRC)/kent/gac_kent.c include/gachain_kent.h $(LIBDIR)/libgachain.so
+	$(CC) $(CFLAGS) -shared $< -o $@ -L$(LIBDIR) -lgachain -Wl,-rpath,'$$ORIGIN' \
+	    -Wl,-soname,libgachain_kent.so
 
 $(OBJDIR)/tools/lib/%.o: $(CSRC)/tools/lib/%.c $(HDRS) $(wildcard $(CSRC)/tools/lib/*.h)
 	@mkdir -p $(dir $@)

@@ -13,7 +13,8 @@ import threading
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libgachain.so")
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libgachain.so")
 BIN_DIR = os.path.join(PKG_DIR, "bin")
 
 GAC_OK = 0

@@ -1,0 +1,114 @@
+/* Test infrastructure: a kent-style caller of the libgachain_kent shims
+ * (include/gachain_kent.h).  It reads a .chain file into kent struct chain
+ * lists itself, binds a context with both .2bit genomes, and for every
+ * "chain_index start end" line of the ranges file prints
+ *   chainCalcScore(chainSubsetOnT(chain, start, end))   (0 if empty)
+ * exactly as src/chainNet/chainNet.c:230-248 / subchainInfo compose them.
+ * usage: kent_shim_driver in.chain t.2bit q.2bit ranges.txt gap [batch] */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "gachain_kent.h"
+
+static struct chain **read_chains(const char *path, int *pn) {
+    FILE *f = fopen(path, "r");
+    if (!f) {
+        perror(path);
+        exit(1);
+    }
+    char line[1 << 16];
+    int n = 0, cap = 1024;
+    struct chain **v = malloc(cap * sizeof(*v));
+    struct chain *c = NULL;
+    struct cBlock **tail = NULL;
+    int t = 0, q = 0;
+    while (fgets(line, sizeof(line), f)) {
+        if (line[0] == '#' || line[0] == '\n')
+            continue;
+        if (!strncmp(line, "chain ", 6)) {
+            c = calloc(1, sizeof(*c));
+            char tn[256], qn[256], qs;
+            sscanf(line, "chain %lf %255s %d + %d %d %255s %d %c %d %d %d", &c->score, tn, &c->tSize,
+                   &c->tStart, &c->tEnd, qn, &c->qSize, &qs, &c->qStart, &c->qEnd, &c->id);
+            c->tName = strdup(tn);
+            c->qName = strdup(qn);
+            c->qStrand = qs;
+            tail = &c->blockList;
+            t = c->tStart;
+            q = c->qStart;
+            if (n == cap)
+                v = realloc(v, (cap *= 2) * sizeof(*v));
+            v[n++] = c;
+            continue;
+        }
+        int size, dt = 0, dq = 0;
+        const int k = sscanf(line, "%d %d %d", &size, &dt, &dq);
+        struct cBlock *b = calloc(1, sizeof(*b));
+        b->tStart = t;
+        b->qStart = q;
+        b->tEnd = t + size;
+        b->qEnd = q + size;
+        *tail = b;
+        tail = &b->next;
+        t += size + (k == 3 ? dt : 0);
+        q += size + (k == 3 ? dq : 0);
+    }
+    fclose(f);
+    *pn = n;
+    return v;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 6)
+        return 2;
+    int n;
+    struct chain **ch = read_chains(argv[1], &n);
+    gac_ctx *ctx;
+    if (gac_open(0, &ctx) != GAC_OK || gac_genome_load_2bit(ctx, GAC_T, argv[2]) != GAC_OK ||
+        gac_genome_load_2bit(ctx, GAC_Q, argv[3]) != GAC_OK) {
+        fprintf(stderr, "%s\n", gac_last_error());
+        return 1;
+    }
+    gac_kent_bind(ctx);
+    struct axtScoreScheme *ss = calloc(1, sizeof(*ss)); /* blastz default */
+    const char *b = "ACGT";
+    const int m[4][4] = {{91, -114, -31, -123}, {-114, 100, -125, -31},
+                         {-31, -125, 100, -114}, {-123, -31, -114, 91}};
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+            for (int ci = 0; ci < 2; ++ci)
+                for (int cj = 0; cj < 2; ++cj)
+                    ss->matrix[(unsigned char)(ci ? b[i] + 32 : b[i])]
+                              [(unsigned char)(cj ? b[j] + 32 : b[j])] = m[i][j];
+    struct gapCalc *gc = gapCalcFromFile(argv[5]);
+    FILE *rf = fopen(argv[4], "r");
+    int ci, s, e, cnt = 0;
+    struct chain **sub = malloc(sizeof(*sub) * 100000), **fr = malloc(sizeof(*fr) * 100000);
+    while (fscanf(rf, "%d %d %d", &ci, &s, &e) == 3 && cnt < 100000) {
+        chainSubsetOnT(ch[ci], s, e, &sub[cnt], &fr[cnt]);
+        ++cnt;
+    }
+    fclose(rf);
+    if (argc > 6) { /* one batched call for every non-empty subset */
+        struct chain **list = malloc(sizeof(*list) * cnt);
+        double *g = malloc(sizeof(double) * cnt);
+        int k = 0;
+        for (int i = 0; i < cnt; ++i)
+            if (sub[i])
+                list[k++] = sub[i];
+        gac_kent_score_chains(list, k, ss, gc, g);
+        k = 0;
+        for (int i = 0; i < cnt; ++i)
+            printf("%.0f\n", sub[i] ? g[k++] : 0.0);
+    } else {
+        for (int i = 0; i < cnt; ++i)
+            printf("%.0f\n", sub[i] ? chainCalcScore(sub[i], ss, gc, NULL, NULL) : 0.0);
+    }
+    for (int i = 0; i < cnt; ++i)
+        gac_kent_chain_free(&fr[i]);
+    printf("gapCalcCost(110,0)=%d\n", gapCalcCost(gc, 110, 0));
+    gapCalcFree(&gc);
+    gac_close(ctx);
+    return 0;
+}
