@@ -159,23 +159,7 @@ static void *pre_upload_thread(void *arg) {
  * trees), so the sides are dealt out to the ranks (LPT on aligned bases);
  * rank R nets and rescores its sides and writes them to <net>.gacpart<R>;
  * rank 0 waits for every part and assembles each net in sequence order. */
-typedef struct ranks {
-    int n, me;
-    const char *tnet, *qnet;
-} ranks;
-static ranks g_rk;
-
-static void part_name(char *buf, size_t cap, const char *net, int r, const char *suffix) {
-    snprintf(buf, cap, "%s.gacpart%d%s", net, r, suffix);
-}
-
-static void rank_abort_hook(void) { /* tell rank 0 this rank has failed */
-    char b[4096];
-    part_name(b, sizeof(b), g_rk.tnet, g_rk.me, ".failed");
-    const int fd = open(b, O_WRONLY | O_CREAT | O_TRUNC, 0644);
-    if (fd >= 0)
-        close(fd);
-}
+static gt_ranks g_rk;
 
 typedef struct side_job {
     int side;
@@ -258,38 +242,13 @@ static void map_part(const char *path, part_map *m) {
     close(fd);
 }
 
-static void wait_parts(const char *net) {
-    const char *lim = getenv("GAC_RANK_TIMEOUT");
-    const double limit = lim ? atof(lim) : 3600.0;
-    struct timespec t0, t1, nap = {0, 500000};
-    clock_gettime(CLOCK_MONOTONIC, &t0);
-    char b[4096];
-    for (int r = 1; r < g_rk.n; ++r) {
-        part_name(b, sizeof(b), net, r, "");
-        for (;;) {
-            if (access(b, F_OK) == 0)
-                break;
-            char f[4096];
-            part_name(f, sizeof(f), g_rk.tnet, r, ".failed");
-            if (access(f, F_OK) == 0) {
-                unlink(f);
-                gt_abort("chainNet: rank %d failed", r);
-            }
-            clock_gettime(CLOCK_MONOTONIC, &t1);
-            if ((t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec) > limit)
-                gt_abort("chainNet: timed out waiting for rank %d's part %s", r, b);
-            nanosleep(&nap, NULL);
-        }
-    }
-}
-
 /* rank 0: <net> = rank 0's '#' lines + every sequence's section, sequence
  * order, from the part of the rank that netted it */
 static void assemble_net(const char *net, const gt_names *names) {
     part_map *pm = calloc((size_t)g_rk.n, sizeof(part_map));
     char b[4096];
     for (int r = 0; r < g_rk.n; ++r) {
-        part_name(b, sizeof(b), net, r, "");
+        gt_part_name(b, sizeof(b), net, r, "");
         map_part(b, &pm[r]);
     }
     /* section index: (start, end) per sequence */
@@ -354,7 +313,7 @@ static void assemble_net(const char *net, const gt_names *names) {
     for (int r = 0; r < g_rk.n; ++r) {
         if (pm[r].n)
             munmap(pm[r].p, pm[r].n);
-        part_name(b, sizeof(b), net, r, "");
+        gt_part_name(b, sizeof(b), net, r, "");
         unlink(b);
     }
     free(pm);
@@ -400,27 +359,13 @@ int main(int argc, char *argv[]) {
     }
     const char *chain_file = argv[1], *tsizes_file = argv[2], *qsizes_file = argv[3];
     const char *tnet = argv[4], *qnet = argv[5];
-    g_rk.n = gt_opt_int("nranks", 1);
-    g_rk.me = gt_opt_int("rank", 0);
-    g_rk.tnet = tnet;
-    g_rk.qnet = qnet;
-    if (g_rk.n < 1 || g_rk.me < 0 || g_rk.me >= g_rk.n)
-        gt_abort("-rank=%d is not in 0..%d (-nranks=%d)", g_rk.me, g_rk.n - 1, g_rk.n);
+    gt_ranks_init(&g_rk, gt_opt_int("nranks", 1), gt_opt_int("rank", 0), tnet);
     const int multi = g_rk.n > 1;
     gt_set_gpu(gt_opt_int("gpu", multi ? g_rk.me : 0));
     if (multi) {
         if (!strcmp(tnet, "stdout") || !strcmp(qnet, "stdout"))
             gt_abort("-nranks needs file names for both nets (not stdout)");
-        char b[4096];
-        const char *nets[2] = {tnet, qnet};
-        for (int k = 0; k < 2; ++k) { /* stale parts of an earlier run */
-            part_name(b, sizeof(b), nets[k], g_rk.me, "");
-            unlink(b);
-        }
-        part_name(b, sizeof(b), tnet, g_rk.me, ".failed");
-        unlink(b);
-        if (g_rk.me > 0)
-            gt_on_abort(rank_abort_hook);
+        gt_ranks_clear(&g_rk, qnet);
     }
 
     /* with -rescore the device and both genomes come up on a helper thread
@@ -529,10 +474,10 @@ int main(int argc, char *argv[]) {
     gt_verbose(1, "writing %s\n", qnet);
     char tpart[4096], qpart[4096], tpart_tmp[4096], qpart_tmp[4096];
     if (multi) {
-        part_name(tpart, sizeof(tpart), tnet, g_rk.me, "");
-        part_name(qpart, sizeof(qpart), qnet, g_rk.me, "");
-        part_name(tpart_tmp, sizeof(tpart_tmp), tnet, g_rk.me, ".tmp");
-        part_name(qpart_tmp, sizeof(qpart_tmp), qnet, g_rk.me, ".tmp");
+        gt_part_name(tpart, sizeof(tpart), tnet, g_rk.me, "");
+        gt_part_name(qpart, sizeof(qpart), qnet, g_rk.me, "");
+        gt_part_name(tpart_tmp, sizeof(tpart_tmp), tnet, g_rk.me, ".tmp");
+        gt_part_name(qpart_tmp, sizeof(qpart_tmp), qnet, g_rk.me, ".tmp");
     }
     net_out wo[2] = {{net, GAC_T, NULL, multi ? tpart_tmp : tnet, &c, 0, 0},
                      {net, GAC_Q, NULL, multi ? qpart_tmp : qnet, &c, 0, 0}};
@@ -678,8 +623,8 @@ int main(int argc, char *argv[]) {
         if (rename(qpart_tmp, qpart) != 0 || rename(tpart_tmp, tpart) != 0)
             gt_abort("can't rename %s: %s", tpart_tmp, strerror(errno));
         if (g_rk.me == 0) {
-            wait_parts(tnet);
-            wait_parts(qnet);
+            gt_ranks_wait(&g_rk, tnet);
+            gt_ranks_wait(&g_rk, qnet);
             gt_stage("wait for ranks");
             assemble_net(tnet, &ts.names);
             assemble_net(qnet, &qs.names);

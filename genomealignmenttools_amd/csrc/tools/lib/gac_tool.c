@@ -295,6 +295,84 @@ void gt_check(int rc) {
         gt_abort("%s", gac_last_error());
 }
 
+/* ------------------------------------------------------------ ranks */
+void gt_part_name(char *buf, size_t cap, const char *path, int r, const char *suffix) {
+    snprintf(buf, cap, "%s.gacpart%d%s", path, r, suffix);
+}
+
+static const gt_ranks *g_ranks;
+
+static void rank_failed_hook(void) { /* tell rank 0 this rank has failed */
+    char b[4096];
+    gt_part_name(b, sizeof(b), g_ranks->key, g_ranks->me, ".failed");
+    const int fd = open(b, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd >= 0)
+        close(fd);
+}
+
+void gt_ranks_init(gt_ranks *rk, int n, int me, const char *key) {
+    rk->n = n;
+    rk->me = me;
+    rk->key = key;
+    if (n < 1 || me < 0 || me >= n)
+        gt_abort("-rank=%d is not in 0..%d (-nranks=%d)", me, n - 1, n);
+    if (n == 1)
+        return;
+    gt_ranks_clear(rk, key);
+    char b[4096];
+    gt_part_name(b, sizeof(b), key, me, ".failed");
+    unlink(b);
+    g_ranks = rk;
+    if (me > 0)
+        gt_on_abort(rank_failed_hook);
+}
+
+void gt_ranks_clear(const gt_ranks *rk, const char *path) {
+    char b[4096];
+    gt_part_name(b, sizeof(b), path, rk->me, "");
+    unlink(b);
+    gt_part_name(b, sizeof(b), path, rk->me, ".tmp");
+    unlink(b);
+}
+
+void gt_ranks_wait(const gt_ranks *rk, const char *path) {
+    const char *lim = getenv("GAC_RANK_TIMEOUT");
+    const double limit = lim ? atof(lim) : 3600.0, t0 = now_s();
+    struct timespec nap = {0, 500000};
+    char b[4096], f[4096];
+    for (int r = 1; r < rk->n; ++r) {
+        gt_part_name(b, sizeof(b), path, r, "");
+        gt_part_name(f, sizeof(f), rk->key, r, ".failed");
+        while (access(b, F_OK) != 0) {
+            if (access(f, F_OK) == 0) {
+                unlink(f);
+                gt_abort("%s: rank %d failed", path, r);
+            }
+            if (now_s() - t0 > limit)
+                gt_abort("%s: timed out waiting for rank %d's part %s", path, r, b);
+            nanosleep(&nap, NULL);
+        }
+    }
+}
+
+void gt_ranks_append_parts(const gt_ranks *rk, const char *path, FILE *f) {
+    char b[4096];
+    char *buf = malloc(1 << 22);
+    for (int r = 1; r < rk->n; ++r) {
+        gt_part_name(b, sizeof(b), path, r, "");
+        FILE *p = fopen(b, "r");
+        if (!p)
+            gt_abort("Can't open %s to read: %s", b, strerror(errno));
+        size_t k;
+        while ((k = fread(buf, 1, 1 << 22, p)) > 0)
+            if (fwrite(buf, 1, k, f) != k)
+                gt_abort("write error on %s", path);
+        fclose(p);
+        unlink(b);
+    }
+    free(buf);
+}
+
 /* ------------------------------------------------------------ options */
 typedef struct gt_optval {
     char *name, *val;

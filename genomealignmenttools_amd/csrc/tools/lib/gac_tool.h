@@ -75,6 +75,27 @@ void gt_device_close_join(gt_device *d);
  * host arrays); the kernel reclaims both. */
 void gt_exit_ok(void) __attribute__((noreturn));
 
+/* ---- multi-GPU runs: -nranks=N -rank=R (one process per GPU, one node) ----
+ * Every rank writes its share of an output to <path>.gacpart<R> (renamed
+ * into place when complete); rank 0 waits for the other ranks' parts and
+ * assembles the output.  A rank that fails leaves <key>.gacpart<R>.failed,
+ * so rank 0 fails too instead of waiting (GAC_RANK_TIMEOUT seconds at most,
+ * default 3600).  key = the first output file. */
+typedef struct gt_ranks {
+    int n, me;
+    const char *key;
+} gt_ranks;
+/* checks n / me, removes this rank's stale parts of `key` and its failure
+ * marker, installs the failure marker hook (me > 0) */
+void gt_ranks_init(gt_ranks *rk, int n, int me, const char *key);
+/* removes this rank's stale part of another output */
+void gt_ranks_clear(const gt_ranks *rk, const char *path);
+void gt_part_name(char *buf, size_t cap, const char *path, int r, const char *suffix);
+/* rank 0: wait until <path>.gacpart<r> exists for every r > 0 */
+void gt_ranks_wait(const gt_ranks *rk, const char *path);
+/* rank 0: append <path>.gacpart<r>, r = 1..n-1, to f, then remove them */
+void gt_ranks_append_parts(const gt_ranks *rk, const char *path, FILE *f);
+
 /* ---- options ---- */
 enum { GT_BOOL, GT_INT, GT_DOUBLE, GT_STRING };
 typedef struct gt_spec {

@@ -91,6 +91,29 @@ def c5_dir(tmp_path_factory):
 
 
 @pytest.mark.timeout(900)
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_c5_shaped_scorechain_ranks(c5_dir, nranks):
+    """scoreChain -nranks=N -rank=R (one process per rank; all on device 0
+    here): each rank scores a contiguous share of the chains, rank 0 writes
+    the file -- identical to the reference's single run."""
+    p = lambda x: os.path.join(c5_dir, x)
+    args = [p("in.chain"), p("t.2bit"), p("q.2bit")]
+    if not os.path.exists(p("sc.chain.ref")):
+        _run([_ref("scoreChain")] + args + [p("sc.chain.ref"), "-linearGap=loose"])
+    out = p(f"sc.ranks{nranks}")
+    procs = [subprocess.Popen([_bin("scoreChain")] + args + [out, "-linearGap=loose",
+                                                            f"-nranks={nranks}", f"-rank={r}",
+                                                            "-gpu=0"],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for r in range(nranks)]
+    for r, pr in enumerate(procs):
+        _, err = pr.communicate(timeout=600)
+        assert pr.returncode == 0, (r, err[-2000:])
+    _same(out, p("sc.chain.ref"))
+    assert not [f for f in os.listdir(c5_dir) if ".gacpart" in f]
+
+
+@pytest.mark.timeout(900)
 @pytest.mark.parametrize("mode", ["chain", "coords"])
 def test_c5_shaped_scorechain(c5_dir, mode):
     p = lambda x: os.path.join(c5_dir, x)
