@@ -4,7 +4,15 @@ Chains / fills are independent, so a batch is split into contiguous shards
 balanced by window blocks, each rank scores its shard on its own GPU, and a
 single all-gather (RCCL over xGMI with backend "nccl"; gloo on CPU for tests)
 reassembles the per-range results in input order -- the only collective on
-the path.  One process per GPU (torch.distributed); rank r uses cuda:LOCAL_RANK.
+the path.  One process per GPU (torch.distributed); rank r uses
+cuda:LOCAL_RANK.  On GPUs everything stays in HBM: the shard's ranges, the
+libgachain outputs (written straight into torch tensors by
+gac_score_ranges_device on torch's current stream) and the gathered result.
+
+The command-line tools split differently (no collective at all): chainNet
+-nranks deals out chromosome sides, scoreChain -nranks contiguous chain runs
+(their outputs are the exchange).  This module is for callers that hold one
+range batch -- e.g. a rescoring service -- across the GPUs of a node.
 """
 from __future__ import annotations
 
@@ -29,39 +37,69 @@ def shard_bounds(weights: np.ndarray, world: int) -> List[Tuple[int, int]]:
     return [(cuts[i], cuts[i + 1]) for i in range(world)]
 
 
-def gather_sharded(dist, rank: int, world: int, n: int, bounds, local_cols: np.ndarray,
-                   device=None) -> np.ndarray:
-    """All-gather per-shard result rows (int64 [rows, k]) into [n, k] in order.
+def gather_sharded(dist, world: int, n: int, bounds, local):
+    """All-gather per-shard result rows (int64 tensor [rows, k], on the
+    process group's device) into [n, k] in input order, on that device.
     Shards are padded to the largest one so one all_gather_into_tensor call
-    (a single ring all-gather) moves everything."""
+    (a single ring all-gather) moves everything; the padding is dropped by a
+    gather on the same device (no host round trip)."""
     import torch
-    k = local_cols.shape[1]
+    k = local.shape[1]
+    dev = local.device
     maxrows = max(hi - lo for lo, hi in bounds)
-    buf = torch.zeros((maxrows, k), dtype=torch.int64, device=device)
-    if local_cols.shape[0]:
-        buf[: local_cols.shape[0]] = torch.from_numpy(np.ascontiguousarray(local_cols)).to(device)
-    out = torch.empty((world * maxrows, k), dtype=torch.int64, device=device)
+    buf = torch.zeros((maxrows, k), dtype=torch.int64, device=dev)
+    if local.shape[0]:
+        buf[: local.shape[0]] = local
+    out = torch.empty((world * maxrows, k), dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(out, buf)
-    out = out.cpu().numpy()
-    res = np.empty((n, k), np.int64)
-    for r, (lo, hi) in enumerate(bounds):
-        res[lo:hi] = out[r * maxrows: r * maxrows + (hi - lo)]
-    return res
+    idx = torch.cat([torch.arange(r * maxrows, r * maxrows + (hi - lo), device=dev)
+                     for r, (lo, hi) in enumerate(bounds)])
+    return out.index_select(0, idx) if n else out[:0]
 
 
 def score_sharded(dist, rank: int, world: int, ranges: np.ndarray, weights: np.ndarray,
-                  scorer: Callable[[np.ndarray], Tuple[np.ndarray, np.ndarray, np.ndarray]],
-                  device=None):
+                  scorer: Callable, device=None):
     """Score `ranges` across all ranks.  scorer(shard_ranges) -> (global,
-    local, ali) for this rank's shard (on its GPU).  Returns the full
-    (global, local, ali) on every rank."""
+    local, ali) for this rank's shard (numpy, e.g. a CPU scorer in tests).
+    Returns the full (global, local, ali) as numpy on every rank."""
+    import torch
     bounds = shard_bounds(weights, world)
     lo, hi = bounds[rank]
     g, l, a = scorer(ranges[lo:hi])
-    cols = np.stack([np.asarray(g, np.int64), np.asarray(l, np.int64),
-                     np.asarray(a, np.int64)], 1) if hi > lo else np.zeros((0, 3), np.int64)
-    full = gather_sharded(dist, rank, world, len(ranges), bounds, cols, device)
+    cols = (np.stack([np.asarray(g, np.int64), np.asarray(l, np.int64),
+                      np.asarray(a, np.int64)], 1) if hi > lo else np.zeros((0, 3), np.int64))
+    full = gather_sharded(dist, world, len(ranges), bounds,
+                          torch.from_numpy(cols).to(device if device is not None else "cpu"))
+    full = full.cpu().numpy()
     return full[:, 0], full[:, 1], full[:, 2].astype(np.int32)
+
+
+def score_sharded_gpu(dist, rank: int, world: int, engine, chainset, ranges, weights,
+                      want_local: bool = True):
+    """The GPU path: `ranges` is an int32 [n, 3] torch tensor (or array) of
+    (chain, tStart, tEnd) over a chain set every rank holds (`chainset`,
+    uploaded to this rank's GPU by `engine`).  This rank's shard is scored by
+    libgachain (gac_score_ranges_device) into device tensors on torch's
+    current stream, then one all-gather over RCCL.  Returns an int64 [n, 3]
+    device tensor (global, local, ali) on every rank."""
+    import torch
+    dev = torch.device("cuda", torch.cuda.current_device())
+    r = torch.as_tensor(ranges, dtype=torch.int32)
+    bounds = shard_bounds(np.asarray(weights), world)
+    lo, hi = bounds[rank]
+    m = hi - lo
+    shard = r[lo:hi].to(dev).contiguous()
+    g = torch.empty(m, dtype=torch.int64, device=dev)
+    l = torch.empty(m, dtype=torch.int64, device=dev)
+    a = torch.empty(m, dtype=torch.int32, device=dev)
+    if m:
+        engine.score_ranges_device(chainset, shard.data_ptr(), m, g.data_ptr(), a.data_ptr(),
+                                   d_l=l.data_ptr() if want_local else 0, want_local=want_local,
+                                   stream=torch.cuda.current_stream().cuda_stream)
+    if not want_local:
+        l.zero_()
+    local = torch.stack([g, l, a.to(torch.int64)], 1)
+    return gather_sharded(dist, world, r.shape[0], bounds, local)
 
 
 def reduce_time_and_work(dist, seconds: float, work: float, device=None) -> Tuple[float, float]:

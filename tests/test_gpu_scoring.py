@@ -441,3 +441,45 @@ def test_kent_shims_vs_reference(batch, tmp_path):
     got = np.array([int(x) for x in lines[:len(R)]], np.int64)
     assert np.array_equal(got, z["glob"][:len(R)])
     assert lines[len(R)] == "gapCalcCost(110,0)=598"
+
+
+@pytest.mark.timeout(300)
+def test_sharded_scoring_rccl_world1():
+    """shard.score_sharded_gpu on the GPU: libgachain scores this rank's shard
+    into torch device tensors on torch's current stream, one RCCL
+    all_gather_into_tensor (backend "nccl", world size 1 on the box's one
+    GPU; the N-rank split is covered by the gloo world-2 test) reassembles
+    them on the device -- equal to the reference's scores (subchain.npz)."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from genomealignmenttools_amd.chainfile import read_chains
+    from genomealignmenttools_amd.gachain import GAC_Q, GAC_T, Engine, GapCosts
+    from genomealignmenttools_amd.shard import score_sharded_gpu
+    d = os.path.join(GOLDEN, "synth12")
+    z = np.load(os.path.join(d, "subchain.npz"))
+    ca = read_chains(os.path.join(d, "in.chain"))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        e = Engine(0)
+        e.load_2bit(GAC_T, os.path.join(d, "t.2bit"))
+        e.load_2bit(GAC_Q, os.path.join(d, "q.2bit"))
+        e.set_scoring(np.asarray(BLASTZ, np.int32), GapCosts("loose"))
+        cs = e.upload_chains(ca)
+        R = z["ranges"]
+        w = np.diff(ca.blk_off)[R[:, 0]].astype(float)
+        out = score_sharded_gpu(dist, 0, 1, e, cs, R, w)
+        assert out.is_cuda
+        res = out.cpu().numpy()
+        assert np.array_equal(res[:, 0], z["glob"]) and np.array_equal(res[:, 1], z["loc"])
+        assert np.array_equal(res[:, 2], z["ali"])
+    finally:
+        dist.destroy_process_group()
