@@ -1,10 +1,12 @@
 """GPU parity: libgachain (HIP, gfx950) vs the CPU oracle on the same seeded
 inputs.  Integer scores must be bit-exact (the reference accumulates integer
 addends in double; see include/gachain.h)."""
+import os
+
 import numpy as np
 import pytest
 
-from conftest import BLASTZ
+from conftest import BLASTZ, GOLDEN
 
 pytestmark = pytest.mark.gpu
 
