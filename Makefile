@@ -21,9 +21,9 @@ CFLAGS   := -O2 -std=gnu11 -fPIC -Wall -Iinclude -I$(CSRC)
 
 HOST_SRC := $(wildcard $(CSRC)/host/*.c)
 HOST_OBJ := $(patsubst $(CSRC)/host/%.c,$(OBJDIR)/host/%.o,$(HOST_SRC))
-HIP_SRC  := $(CSRC)/gac_kernels.hip $(CSRC)/gac_device.hip
+HIP_SRC  := $(CSRC)/gac_kernels.hip $(CSRC)/gac_dp.hip $(CSRC)/gac_device.hip
 HIP_OBJ  := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRC))
-HDRS     := include/gachain.h $(CSRC)/gac_kernels.h $(wildcard $(CSRC)/host/*.h)
+HDRS     := include/gachain.h $(CSRC)/gac_kernels.h $(CSRC)/gac_dp.h $(wildcard $(CSRC)/host/*.h)
 
 EXECDIR  := $(PKG)/libexec
 # GPU tools: the binary lives in libexec/, bin/<tool> is a 2-line sh launcher

@@ -75,9 +75,10 @@ def parse():
     p.add_argument("--prof", choices=["tile", "all", "none"], default="tile",
                    help="kernels bracketed by HIP events in the kernel leg (the roofline "
                         "needs k_tile's)")
-    p.add_argument("--order", choices=["chain", "net"], default="net",
+    p.add_argument("--order", choices=["chain", "net", "t", "q"], default="net",
                    help="kernel leg: ranges in .net output order (as bin/chainNet submits "
-                        "them) or in (chain, tStart) order (measured slower for k_tile)")
+                        "them), (chain, tStart), target start, or (query sequence, forward "
+                        "query position) order")
     p.add_argument("--tmp", default=os.environ.get("TMPDIR", "/tmp"))
     p.add_argument("--gen-only", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
@@ -161,6 +162,10 @@ def kernel_leg(args, d, steps):
         ranges = np.stack([fills["chain"][part], fills["start"][part], fills["end"][part]], 1)
     if args.order == "chain":
         ranges = ranges[np.lexsort((ranges[:, 1], ranges[:, 0]))]
+    elif args.order == "t":
+        ranges = ranges[np.argsort(ranges[:, 1], kind="stable")]
+    elif args.order == "q":
+        ranges = ranges[np.lexsort(_query_key(ca, ranges)[::-1])]
     ranges = np.ascontiguousarray(ranges, np.int32)
     e = Engine(int(os.environ.get("LOCAL_RANK", "0")))
     e.load_2bit(GAC_T, p("t.2bit"))
@@ -240,6 +245,21 @@ def _pmc_traffic(args, n, nblk):
             or t.get("order", "net") != args.order):
         return None
     return t.get("hbm_bytes_per_launch")
+
+
+def _query_key(ca, ranges):
+    """(query sequence id, forward-strand query position of the first window
+    block) per range: the query-plane order of the fills."""
+    names = {n: i for i, n in enumerate(dict.fromkeys(ca.qname))}
+    qid = np.array([names[n] for n in ca.qname], np.int64)[ranges[:, 0]]
+    pos = np.zeros(len(ranges), np.int64)
+    for i, (c, s, _) in enumerate(ranges):
+        a, b = int(ca.blk_off[c]), int(ca.blk_off[c + 1])
+        k = a + int(np.searchsorted(ca.blk_t[a:b] + ca.blk_size[a:b], s, side="right"))
+        k = min(k, b - 1)
+        q = int(ca.blk_q[k])
+        pos[i] = int(ca.qsize[c]) - q if ca.qstrand[c] else q
+    return qid, pos
 
 
 def _window_blocks(ca, ranges):

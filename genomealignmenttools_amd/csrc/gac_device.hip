@@ -17,6 +17,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "gac_dp.h"
 #include "gac_kernels.h"
 #include "gachain.h"
 #include "host/gac_host.h"
@@ -768,6 +769,216 @@ extern "C" int gac_score_blocks(gac_ctx *c, int64_t n_pairs, const int32_t *t_se
     hipFree(d_jobs);
     hipFree(d_out);
     return GAC_OK;
+}
+
+// ----------------------------------------------------------------- chaining DP
+// DpArgs common part: genomes, matrix by code, gap setup
+static void dp_base_args(gac_ctx *c, DpArgs &a) {
+    memset(&a, 0, sizeof(a));
+    a.t_planes = c->g[0].planes;
+    a.t_nmask = c->g[0].nmask;
+    a.q_planes = c->g[1].planes;
+    a.q_nmask = c->g[1].nmask;
+    a.gap = c->gap;
+    a.small_tab = c->d_small;
+    a.gap_tab = c->d_gap_tab;
+    a.gap_len = c->gap_len;
+    for (int q = 0; q < 4; ++q)
+        for (int t = 0; t < 4; ++t) a.m16[q * 4 + t] = c->mat[acgt_of_code(q) * 4 + acgt_of_code(t)];
+}
+
+// global base index of a pair's target start / query start ('-': ~(start + qSize))
+static int pair_bases(gac_ctx *c, int32_t ts, int32_t qs, uint8_t minus, int64_t &tb,
+                      int64_t &qb) {
+    const Genome &T = c->g[0], &Q = c->g[1];
+    if (ts < 0 || ts >= (int32_t)T.sizes.size() || qs < 0 || qs >= (int32_t)Q.sizes.size())
+        return gac_fail(GAC_E_ARG, "bad sequence index (%d, %d)", ts, qs);
+    tb = T.woff[ts] * 32;
+    qb = minus ? ~(Q.woff[qs] * 32 + Q.sizes[qs]) : Q.woff[qs] * 32;
+    return GAC_OK;
+}
+
+template <class T>
+static int dev_upload(gac_ctx *c, T **d, const void *h, size_t n) {
+    *d = nullptr;
+    if (n == 0) return GAC_OK;
+    HIPCHK(hipMalloc((void **)d, n * sizeof(T)));
+    if (h) HIPCHK(hipMemcpyAsync(*d, h, n * sizeof(T), hipMemcpyHostToDevice, c->stream));
+    return GAC_OK;
+}
+
+extern "C" int gac_chain_dp(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq, const int32_t *q_seq,
+                            const uint8_t *q_strand, const int64_t *node_off,
+                            const int32_t *node_a, const int32_t *node_b, const int64_t *leaf_off,
+                            const int32_t *leaf, const int32_t *leaf_score,
+                            const int32_t *leaf_node, const int64_t *path_off,
+                            const int32_t *path, int64_t *total, int32_t *pred) {
+    gac_clear_error();
+    if (!c || n_pairs < 0 ||
+        (n_pairs && (!t_seq || !q_seq || !q_strand || !node_off || !leaf_off || !path_off)))
+        return gac_fail(GAC_E_ARG, "gac_chain_dp: bad argument");
+    if (!c->scoring) return gac_fail(GAC_E_STATE, "gac_chain_dp before gac_set_scoring");
+    CTX_LOCK(c);
+    if (!c->g[0].final || !c->g[1].final)
+        return gac_fail(GAC_E_STATE, "load both genomes before gac_chain_dp");
+    if (n_pairs == 0) return GAC_OK;
+    const int64_t nn = node_off[n_pairs], nl = leaf_off[n_pairs], np_ = path_off[nl];
+    if (nl == 0) return GAC_OK;
+    if (!node_a || !node_b || !leaf || !leaf_score || !leaf_node || !path || !total || !pred)
+        return gac_fail(GAC_E_ARG, "gac_chain_dp: NULL array");
+    std::vector<DpPair> pairs(n_pairs);
+    std::vector<long long> tot0(nn, 0);
+    for (int64_t p = 0; p < n_pairs; ++p) {
+        DpPair &P = pairs[p];
+        int rc = pair_bases(c, t_seq[p], q_seq[p], q_strand[p], P.tbase, P.qbase);
+        if (rc != GAC_OK) return rc;
+        const int64_t n_nodes = node_off[p + 1] - node_off[p], n_leaves = leaf_off[p + 1] - leaf_off[p];
+        if (n_nodes < 0 || n_nodes > 0x7fffffff || n_leaves < 0 || (n_leaves > 0 && n_nodes < 1))
+            return gac_fail(GAC_E_ARG, "gac_chain_dp: pair %lld: bad tree size", (long long)p);
+        P.node_off = node_off[p];
+        P.leaf_off = leaf_off[p];
+        P.n_nodes = (int32_t)n_nodes;
+        P.n_leaves = (int32_t)n_leaves;
+        for (int64_t i = leaf_off[p]; i < leaf_off[p + 1]; ++i) {
+            const int32_t v = leaf_node[i];
+            if (v < 0 || v >= n_nodes || node_b[2 * (node_off[p] + v) + 1] != ~(int32_t)(i - leaf_off[p]))
+                return gac_fail(GAC_E_ARG, "gac_chain_dp: leaf %lld: bad node", (long long)i);
+            tot0[node_off[p] + v] = leaf_score[i];
+        }
+    }
+    // a kernel reading past its pair would fault: check the structure first
+    for (int64_t p = 0; p < n_pairs; ++p) {
+        const int64_t o = node_off[p];
+        const int32_t n = pairs[p].n_nodes;
+        for (int32_t v = 0; v < n; ++v) {
+            const int32_t end = node_b[2 * (o + v)], info = node_b[2 * (o + v) + 1];
+            const int32_t lo = node_a[4 * (o + v) + 3];
+            if (end <= v || end > n || (info >= 0 && (info > 1 || lo <= v + 1 || lo >= end)))
+                return gac_fail(GAC_E_ARG, "gac_chain_dp: pair %lld node %d: bad links", (long long)p, v);
+        }
+    }
+    for (int64_t p = 0; p < n_pairs; ++p)
+        for (int64_t i = leaf_off[p]; i < leaf_off[p + 1]; ++i)
+            for (int64_t k = path_off[i]; k < path_off[i + 1]; ++k)
+                if (path[k] < 0 || path[k] >= pairs[p].n_nodes)
+                    return gac_fail(GAC_E_ARG, "gac_chain_dp: leaf %lld: bad path node", (long long)i);
+    HIPCHK(hipSetDevice(c->device));
+    DpArgs a;
+    dp_base_args(c, a);
+    a.n_pairs = n_pairs;
+    DpPair *d_pairs = nullptr;
+    int4 *d_na = nullptr, *d_lf = nullptr;
+    int2 *d_nb = nullptr;
+    long long *d_ms = nullptr, *d_tot = nullptr, *d_total = nullptr;
+    int32_t *d_score = nullptr, *d_node = nullptr, *d_path = nullptr, *d_pred = nullptr;
+    int64_t *d_poff = nullptr;
+    int rc = GAC_OK;
+    if ((rc = dev_upload(c, &d_pairs, pairs.data(), n_pairs)) == GAC_OK &&
+        (rc = dev_upload(c, &d_na, node_a, nn)) == GAC_OK &&
+        (rc = dev_upload(c, &d_nb, node_b, nn)) == GAC_OK &&
+        (rc = dev_upload(c, &d_ms, nullptr, nn)) == GAC_OK &&
+        (rc = dev_upload(c, &d_tot, tot0.data(), nn)) == GAC_OK &&
+        (rc = dev_upload(c, &d_lf, leaf, nl)) == GAC_OK &&
+        (rc = dev_upload(c, &d_score, leaf_score, nl)) == GAC_OK &&
+        (rc = dev_upload(c, &d_node, leaf_node, nl)) == GAC_OK &&
+        (rc = dev_upload(c, &d_poff, path_off, nl + 1)) == GAC_OK &&
+        (rc = dev_upload(c, &d_path, path, np_ ? np_ : 1)) == GAC_OK &&
+        (rc = dev_upload(c, &d_total, nullptr, nl)) == GAC_OK &&
+        (rc = dev_upload(c, &d_pred, nullptr, nl)) == GAC_OK) {
+        hipError_t e = hipMemsetAsync(d_ms, 0, nn * sizeof(long long), c->stream);
+        a.pairs = d_pairs;
+        a.nd_ms = d_ms;
+        a.nd_tot = d_tot;
+        a.nd_a = d_na;
+        a.nd_b = d_nb;
+        a.lf = d_lf;
+        a.lf_score = d_score;
+        a.lf_node = d_node;
+        a.path_off = d_poff;
+        a.path = d_path;
+        a.lf_total = d_total;
+        a.lf_pred = d_pred;
+        // one wave per pair, every pair resident at once (largest first is
+        // the caller's order; the grid covers them all)
+        const int grid = (int)std::min<int64_t>(n_pairs, 1 << 20);
+        if (e == hipSuccess) e = launch_dp(a, grid, c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(total, d_total, nl * sizeof(long long), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(pred, d_pred, nl * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) rc = gac_fail(GAC_E_HIP, "gac_chain_dp: %s", hipGetErrorString(e));
+    }
+    hipStreamSynchronize(c->stream);
+    hipFree(d_pairs);
+    hipFree(d_na);
+    hipFree(d_nb);
+    hipFree(d_ms);
+    hipFree(d_tot);
+    hipFree(d_lf);
+    hipFree(d_score);
+    hipFree(d_node);
+    hipFree(d_poff);
+    hipFree(d_path);
+    hipFree(d_total);
+    hipFree(d_pred);
+    return rc;
+}
+
+extern "C" int gac_crossovers(gac_ctx *c, int64_t n, const int32_t *t_seq, const int32_t *q_seq,
+                              const uint8_t *q_strand, const int32_t *lqe, const int32_t *lte,
+                              const int32_t *rqs, const int32_t *rts, const int32_t *overlap,
+                              int32_t *pos, int32_t *adj) {
+    gac_clear_error();
+    if (!c || n < 0 || (n && (!t_seq || !q_seq || !q_strand || !lqe || !lte || !rqs || !rts ||
+                              !overlap || !pos || !adj)))
+        return gac_fail(GAC_E_ARG, "gac_crossovers: bad argument");
+    if (!c->scoring) return gac_fail(GAC_E_STATE, "gac_crossovers before gac_set_scoring");
+    CTX_LOCK(c);
+    if (!c->g[0].final || !c->g[1].final)
+        return gac_fail(GAC_E_STATE, "load both genomes before gac_crossovers");
+    if (n == 0) return GAC_OK;
+    std::vector<XoverJob> jobs(n);
+    const Genome &T = c->g[0], &Q = c->g[1];
+    for (int64_t j = 0; j < n; ++j) {
+        XoverJob &J = jobs[j];
+        int rc = pair_bases(c, t_seq[j], q_seq[j], q_strand[j], J.tbase, J.qbase);
+        if (rc != GAC_OK) return rc;
+        const int32_t ov = overlap[j];
+        if (ov < 0 || lqe[j] - ov < 0 || lte[j] - ov < 0 || rqs[j] < 0 || rts[j] < 0 ||
+            lqe[j] > Q.sizes[q_seq[j]] || (int64_t)rqs[j] + ov > Q.sizes[q_seq[j]] ||
+            lte[j] > T.sizes[t_seq[j]] || (int64_t)rts[j] + ov > T.sizes[t_seq[j]])
+            return gac_fail(GAC_E_ARG, "gac_crossovers: overlap %lld outside its sequences",
+                            (long long)j);
+        J.lqe = lqe[j];
+        J.lte = lte[j];
+        J.rqs = rqs[j];
+        J.rts = rts[j];
+        J.ov = ov;
+        J.pad = 0;
+    }
+    HIPCHK(hipSetDevice(c->device));
+    DpArgs a;
+    dp_base_args(c, a);
+    XoverJob *d_jobs = nullptr;
+    int32_t *d_pos = nullptr, *d_adj = nullptr;
+    int rc = GAC_OK;
+    if ((rc = dev_upload(c, &d_jobs, jobs.data(), n)) == GAC_OK &&
+        (rc = dev_upload(c, &d_pos, nullptr, n)) == GAC_OK &&
+        (rc = dev_upload(c, &d_adj, nullptr, n)) == GAC_OK) {
+        hipError_t e = launch_xover(a, d_jobs, n, d_pos, d_adj, c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(pos, d_pos, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(adj, d_adj, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) rc = gac_fail(GAC_E_HIP, "gac_crossovers: %s", hipGetErrorString(e));
+    }
+    hipStreamSynchronize(c->stream);
+    hipFree(d_jobs);
+    hipFree(d_pos);
+    hipFree(d_adj);
+    return rc;
 }
 
 // ----------------------------------------------------------------- chains

@@ -192,8 +192,13 @@ static void crossover(ax_work *w, int32_t lqs, int32_t lqe, int32_t lts, int32_t
     *ret_adj = (int)(r_score + l_score - best);
 }
 
-/* chainConnectCost (chainConnect.c:114-149) of block a then block b */
-static int connect_cost(ax_work *w, int32_t a, int32_t b) {
+/* chainConnectCost (chainConnect.c:114-149) of block a then block b; pre:
+ * the crossover adjustment of this overlap computed on the device, or NULL */
+static int connect_cost_pre(ax_work *w, int32_t a, int32_t b, const int32_t *pre);
+
+static int connect_cost(ax_work *w, int32_t a, int32_t b) { return connect_cost_pre(w, a, b, NULL); }
+
+static int connect_cost_pre(ax_work *w, int32_t a, int32_t b, const int32_t *pre) {
     int dq = w->qs[b] - w->qe[a];
     int dt = w->ts[b] - w->te[a];
     int adj = 0;
@@ -210,8 +215,11 @@ static int connect_cost(ax_work *w, int32_t a, int32_t b) {
             adj = 100000000;
         } else {
             int cross;
-            crossover(w, w->qs[a], w->qe[a], w->ts[a], w->te[a], w->qs[b], w->qe[b], w->ts[b],
-                      w->te[b], overlap, &cross, &adj);
+            if (pre)
+                adj = *pre;
+            else
+                crossover(w, w->qs[a], w->qe[a], w->ts[a], w->te[a], w->qs[b], w->qe[b], w->ts[b],
+                          w->te[b], overlap, &cross, &adj);
             dq += overlap;
             dt += overlap;
         }
@@ -386,13 +394,31 @@ typedef struct ax_cb {
     int32_t next;
 } ax_cb;
 
-static void xover_cb(ax_work *w, const ax_cb *a, const ax_cb *b, int overlap, int *pos, int *adj) {
+/* crossovers of the chains' adjacent overlapping blocks computed on the
+ * device (GAC_AXT_DP=gpu): by chain-block position j (the pair j-1, j), with
+ * the inputs they were computed from */
+typedef struct ax_xres {
+    const int32_t *job;  /* [blocks] job index or -1 */
+    const int32_t *pos, *adj;
+    const int32_t *lqe, *lte, *rqs, *rts, *ov;
+} ax_xres;
+
+static void xover_cb(ax_work *w, const ax_cb *a, const ax_cb *b, int overlap, int *pos, int *adj,
+                     const ax_xres *x, int32_t jb) {
+    const int32_t k = x ? x->job[jb] : -1;
+    if (k >= 0 && x->lqe[k] == a->qe && x->lte[k] == a->te && x->rqs[k] == b->qs &&
+        x->rts[k] == b->ts && x->ov[k] == overlap && overlap <= a->te - a->ts &&
+        overlap <= b->te - b->ts) {
+        *pos = x->pos[k];
+        *adj = x->adj[k];
+        return;
+    }
     crossover(w, a->qs, a->qe, a->ts, a->te, b->qs, b->qe, b->ts, b->te, overlap, pos, adj);
 }
 
 /* chainRemovePartialOverlaps (chainConnect.c:255-344) + chainMergeAbutting
  * (:346-368); returns the new head (blocks in cb[], list by next) */
-static int32_t remove_partial_overlaps(ax_work *w, ax_cb *cb, int32_t head) {
+static int32_t remove_partial_overlaps(ax_work *w, ax_cb *cb, int32_t head, const ax_xres *x) {
     for (int32_t a = head, b = cb[a].next; b >= 0; a = b, b = cb[b].next)
         if (cb[a].qs >= cb[b].qs || cb[a].ts >= cb[b].ts) {
             w_fail(w, "a (%d %d) not before b (%d %d) before removePartialOverlaps", cb[a].qs,
@@ -413,7 +439,7 @@ static int32_t remove_partial_overlaps(ax_work *w, ax_cb *cb, int32_t head) {
                     trim_b = 1;
                 } else {
                     int cross, adj;
-                    xover_cb(w, &cb[a], &cb[b], overlap, &cross, &adj);
+                    xover_cb(w, &cb[a], &cb[b], overlap, &cross, &adj, b == a + 1 ? x : NULL, b);
                     cb[b].qs += cross;
                     cb[b].ts += cross;
                     const int inv = overlap - cross;
@@ -491,11 +517,11 @@ typedef struct ax_pairinfo {
     char strand;
 } ax_pairinfo;
 
-static void chain_pair(ax_work *w, const ax_pairinfo *pi, FILE *details, ax_out *out) {
+/* leaves: slAddHead over the block list (reversed), zero-length blocks
+ * skipped, then slSort by tStart (stable); and the query-ordered copy
+ * (dlSort by qStart of the target-ordered list).  Returns the leaf count. */
+static int32_t pair_leaves(ax_work *w) {
     const int32_t nb = w->n;
-    memset(out, 0, sizeof(*out));
-    /* leaves: slAddHead over the block list (reversed), zero-length blocks
-     * skipped, then slSort by tStart (stable) */
     ikey *k = malloc((size_t)(nb ? nb : 1) * sizeof(ikey));
     int32_t nl = 0;
     for (int32_t i = nb - 1; i >= 0; --i) {
@@ -507,13 +533,11 @@ static void chain_pair(ax_work *w, const ax_pairinfo *pi, FILE *details, ax_out 
     w->nl = nl;
     if (nl == 0) {
         free(k);
-        out->coff = calloc(1, sizeof(int32_t));
-        return;
+        return 0;
     }
     qsort(k, (size_t)nl, sizeof(ikey), ikey_cmp);
     for (int32_t i = 0; i < nl; ++i)
         w->tord[i] = k[i].v;
-    /* query-ordered copy: dlSort by qStart of the target-ordered list */
     for (int32_t i = 0; i < nl; ++i)
         k[i] = (ikey){w->qs[w->tord[i]], i, w->tord[i]};
     qsort(k, (size_t)nl, sizeof(ikey), ikey_cmp);
@@ -524,7 +548,13 @@ static void chain_pair(ax_work *w, const ax_pairinfo *pi, FILE *details, ax_out 
         w->total[i] = w->score[i];
         w->pred[i] = -1;
     }
-    /* the tree is built from copies: kd_build permutes its lists */
+    return nl;
+}
+
+/* kdTreeMake (chainBlock.c:166-205); the tree is built from copies: kd_build
+ * permutes its lists */
+static void pair_tree(ax_work *w) {
+    const int32_t nl = w->nl;
     int32_t *Q = malloc((size_t)nl * sizeof(int32_t)), *T = malloc((size_t)nl * sizeof(int32_t));
     memcpy(Q, w->qord, (size_t)nl * sizeof(int32_t));
     memcpy(T, w->tord, (size_t)nl * sizeof(int32_t));
@@ -532,8 +562,11 @@ static void chain_pair(ax_work *w, const ax_pairinfo *pi, FILE *details, ax_out 
     kd_build(w, Q, T, nl, 0);
     free(Q);
     free(T);
-    /* findBestPredecessors (chainBlock.c:281-300) */
-    for (int32_t i = 0; i < nl && !w->err; ++i) {
+}
+
+/* findBestPredecessors (chainBlock.c:281-300) on this thread */
+static void pair_dp_host(ax_work *w) {
+    for (int32_t i = 0; i < w->nl && !w->err; ++i) {
         const int32_t l = w->tord[i];
         double s;
         int32_t p;
@@ -544,16 +577,25 @@ static void chain_pair(ax_work *w, const ax_pairinfo *pi, FILE *details, ax_out 
         }
         update_scores(w, l);
     }
-    if (w->err)
-        return;
-    /* peelChains (chainBlock.c:311-373) in totalScore order */
+}
+
+/* the chains peelChains (chainBlock.c:311-373) takes off the tree: blocks of
+ * chain c are cblk[cstart[c] .. cstart[c+1]), ascending */
+typedef struct ax_chains {
+    int32_t *cblk, *cstart;
+    int32_t nc, nbk;
+} ax_chains;
+
+static void pair_peel(ax_work *w, const ax_pairinfo *pi, FILE *details, ax_chains *pc) {
+    const int32_t nb = w->n, nl = w->nl;
+    /* in totalScore order */
     dkey *dk = malloc((size_t)nl * sizeof(dkey));
     for (int32_t i = 0; i < nl; ++i)
         dk[i] = (dkey){w->total[w->tord[i]], i, w->tord[i]};
     qsort(dk, (size_t)nl, sizeof(dkey), dkey_cmp_desc);
     for (int32_t i = 0; i < nb; ++i)
         w->hit[i] = 0;
-    int32_t *cblk = malloc((size_t)nl * sizeof(int32_t)); /* chain blocks, chain by chain */
+    int32_t *cblk = malloc((size_t)nl * sizeof(int32_t));
     int32_t *cstart = malloc((size_t)(nl + 1) * sizeof(int32_t));
     int32_t nc = 0, nbk = 0;
     for (int32_t i = 0; i < nl; ++i) {
@@ -591,19 +633,31 @@ static void chain_pair(ax_work *w, const ax_pairinfo *pi, FILE *details, ax_out 
     }
     cstart[nc] = nbk;
     free(dk);
-    /* scoreBlocks (chainBlock.c:296-309), then slSort(chainCmpScore) */
+    pc->cblk = cblk;
+    pc->cstart = cstart;
+    pc->nc = nc;
+    pc->nbk = nbk;
+}
+
+/* scoreBlocks (chainBlock.c:296-309), slSort(chainCmpScore), then
+ * chainRemovePartialOverlaps + chainMergeAbutting per chain, in that order.
+ * x: the device's crossovers of the chains' adjacent overlaps, or NULL */
+static void pair_finish(ax_work *w, ax_chains *pc, const ax_xres *x, ax_out *out) {
+    const int32_t nc = pc->nc, nbk = pc->nbk;
+    const int32_t *cblk = pc->cblk, *cstart = pc->cstart;
     dkey *ck = malloc((size_t)(nc ? nc : 1) * sizeof(dkey));
     for (int32_t c = 0; c < nc && !w->err; ++c) {
         double s = 0;
         for (int32_t j = cstart[c]; j < cstart[c + 1]; ++j) {
             s += w->score[cblk[j]];
-            if (j > cstart[c])
-                s -= connect_cost(w, cblk[j - 1], cblk[j]);
+            if (j > cstart[c]) {
+                const int32_t k = x ? x->job[j] : -1;
+                s -= connect_cost_pre(w, cblk[j - 1], cblk[j], k >= 0 ? &x->adj[k] : NULL);
+            }
         }
         ck[c] = (dkey){s, c, c};
     }
     qsort(ck, (size_t)nc, sizeof(dkey), dkey_cmp_desc);
-    /* removePartialOverlaps + mergeAbutting per chain, in that order */
     ax_cb *cb = malloc((size_t)(nbk ? nbk : 1) * sizeof(ax_cb));
     out->coff = malloc((size_t)(nc + 1) * sizeof(int32_t));
     out->bt = malloc((size_t)(nbk ? nbk : 1) * sizeof(int32_t));
@@ -613,15 +667,15 @@ static void chain_pair(ax_work *w, const ax_pairinfo *pi, FILE *details, ax_out 
     for (int32_t r = 0; r < nc && !w->err; ++r) {
         const int32_t c = ck[r].v, b0 = cstart[c], b1 = cstart[c + 1];
         for (int32_t j = b0; j < b1; ++j) {
-            const int32_t x = cblk[j];
-            cb[j] = (ax_cb){w->qs[x], w->qe[x], w->ts[x], w->te[x], j + 1 < b1 ? j + 1 : -1};
+            const int32_t b = cblk[j];
+            cb[j] = (ax_cb){w->qs[b], w->qe[b], w->ts[b], w->te[b], j + 1 < b1 ? j + 1 : -1};
         }
-        const int32_t head = remove_partial_overlaps(w, cb, b0);
+        const int32_t head = remove_partial_overlaps(w, cb, b0, x);
         out->coff[no] = nob;
-        for (int32_t x = head; x >= 0; x = cb[x].next) {
-            out->bt[nob] = cb[x].ts;
-            out->bq[nob] = cb[x].qs;
-            out->bs[nob] = cb[x].qe - cb[x].qs;
+        for (int32_t b = head; b >= 0; b = cb[b].next) {
+            out->bt[nob] = cb[b].ts;
+            out->bq[nob] = cb[b].qs;
+            out->bs[nob] = cb[b].qe - cb[b].qs;
             ++nob;
         }
         if (nob > out->coff[no])
@@ -631,8 +685,24 @@ static void chain_pair(ax_work *w, const ax_pairinfo *pi, FILE *details, ax_out 
     out->n_chains = no;
     free(ck);
     free(cb);
-    free(cblk);
-    free(cstart);
+    free(pc->cblk);
+    free(pc->cstart);
+    pc->cblk = pc->cstart = NULL;
+}
+
+static void chain_pair(ax_work *w, const ax_pairinfo *pi, FILE *details, ax_out *out) {
+    memset(out, 0, sizeof(*out));
+    if (pair_leaves(w) == 0) {
+        out->coff = calloc(1, sizeof(int32_t));
+        return;
+    }
+    pair_tree(w);
+    pair_dp_host(w);
+    if (w->err)
+        return;
+    ax_chains pc;
+    pair_peel(w, pi, details, &pc);
+    pair_finish(w, &pc, NULL, out);
 }
 
 /* ------------------------------------------------------------------ threads */
@@ -723,6 +793,409 @@ static void *ax_thread(void *arg) {
     free(w.nodes);
     free(w.xs);
     return NULL;
+}
+
+/* ------------------------------------------------------------------ device DP
+ * GAC_AXT_DP=gpu: the kd-tree DP of every pair in one gac_chain_dp launch
+ * (one wave per pair), and the crossovers of the peeled chains' adjacent
+ * overlaps (scoreBlocks, chainRemovePartialOverlaps) in one gac_crossovers
+ * batch; tree building, peeling and list surgery stay on host threads.
+ * Phases (threads over pairs, largest first): 1 leaves + tree + export,
+ * [device DP], 2 import + peel + crossover jobs, [device crossovers],
+ * 3 scoreBlocks + sort + overlap removal. */
+typedef struct ax_gpair {
+    ax_work w;          /* this pair's own buffers (they live across phases) */
+    int ok;             /* genome views resolved */
+    /* export: tree and leaves */
+    int32_t *na, *nb;   /* [nn][4], [nn][2] */
+    int32_t *lf, *lsc, *lnode; /* [nl][4], [nl], [nl] */
+    int64_t *poff;      /* [nl + 1], local */
+    int32_t *path;
+    /* peel */
+    ax_chains pc;
+    int32_t *xjob;      /* [nbk] global crossover job or -1 */
+    int32_t nx;         /* this pair's jobs */
+    int32_t *xl;        /* [nx][5] lqe, lte, rqs, rts, ov */
+    double t0;
+} ax_gpair;
+
+typedef struct ax_gjob {
+    ax_job *J;
+    ax_gpair *G;
+    int phase;
+    _Atomic int64_t next;
+    /* device results */
+    const int64_t *leaf_off, *xoff;
+    const int64_t *total;
+    const int32_t *pred;
+    const int32_t *xpos, *xadj, *xlqe, *xlte, *xrqs, *xrts, *xov;
+} ax_gjob;
+
+static double gnow(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+
+/* the nodes updateScoresOnWay's descent reaches for leaf block l */
+static int64_t leaf_path(const ax_work *w, int32_t l, int32_t **path, int64_t *len, int64_t *cap) {
+    const int32_t lq = w->qs[l], lt = w->ts[l];
+    int32_t st_node[kStack];
+    uint8_t st_dim[kStack];
+    int sp = 0;
+    int64_t n0 = *len;
+    st_node[sp] = 0;
+    st_dim[sp++] = 0;
+    while (sp > 0) {
+        --sp;
+        const int32_t b = st_node[sp];
+        const int dim = st_dim[sp];
+        if (*len == *cap) {
+            *cap = *cap * 2 + 64;
+            *path = realloc(*path, (size_t)*cap * sizeof(int32_t));
+        }
+        (*path)[(*len)++] = b;
+        const ax_node *nd = &w->nodes[b];
+        if (nd->leaf < 0) {
+            if (sp + 2 > kStack)
+                return -1;
+            const int32_t coord = dim == 0 ? lq : lt;
+            if (coord <= nd->cut) {
+                st_node[sp] = nd->lo;
+                st_dim[sp++] = (uint8_t)(1 - dim);
+            }
+            if (coord >= nd->cut) {
+                st_node[sp] = nd->hi;
+                st_dim[sp++] = (uint8_t)(1 - dim);
+            }
+        }
+    }
+    return *len - n0;
+}
+
+static void gpair_export(ax_gpair *G) {
+    ax_work *w = &G->w;
+    const int32_t nn = w->nn, nl = w->nl;
+    G->na = malloc((size_t)nn * 4 * sizeof(int32_t));
+    G->nb = malloc((size_t)nn * 2 * sizeof(int32_t));
+    G->lf = malloc((size_t)nl * 4 * sizeof(int32_t));
+    G->lsc = malloc((size_t)nl * sizeof(int32_t));
+    G->lnode = malloc((size_t)nl * sizeof(int32_t));
+    G->poff = malloc((size_t)(nl + 1) * sizeof(int64_t));
+    int32_t *end = malloc((size_t)nn * sizeof(int32_t));
+    uint8_t *dim = malloc((size_t)nn);
+    int32_t *pos = w->tmp; /* leaf position of each block */
+    for (int32_t i = 0; i < nl; ++i)
+        pos[w->tord[i]] = i;
+    for (int32_t v = nn - 1; v >= 0; --v)
+        end[v] = w->nodes[v].leaf >= 0 ? v + 1 : end[w->nodes[v].lo];
+    dim[0] = 0;
+    for (int32_t v = 0; v < nn; ++v) {
+        const ax_node *nd = &w->nodes[v];
+        if (nd->leaf >= 0) {
+            const int32_t l = nd->leaf;
+            G->na[4 * v] = nd->max_q;
+            G->na[4 * v + 1] = nd->max_t;
+            G->na[4 * v + 2] = w->qs[l];
+            G->na[4 * v + 3] = w->ts[l];
+            G->nb[2 * v] = v + 1;
+            G->nb[2 * v + 1] = ~pos[l];
+            G->lnode[pos[l]] = v;
+        } else {
+            dim[nd->hi] = dim[nd->lo] = (uint8_t)(1 - dim[v]);
+            G->na[4 * v] = nd->max_q;
+            G->na[4 * v + 1] = nd->max_t;
+            G->na[4 * v + 2] = nd->cut;
+            G->na[4 * v + 3] = nd->lo;
+            G->nb[2 * v] = end[v];
+            G->nb[2 * v + 1] = dim[v];
+        }
+    }
+    int64_t len = 0, cap = (int64_t)nl * 24 + 64;
+    G->path = malloc((size_t)cap * sizeof(int32_t));
+    G->poff[0] = 0;
+    for (int32_t i = 0; i < nl && !w->err; ++i) {
+        const int32_t l = w->tord[i];
+        G->lf[4 * i] = w->qs[l];
+        G->lf[4 * i + 1] = w->qe[l];
+        G->lf[4 * i + 2] = w->ts[l];
+        G->lf[4 * i + 3] = w->te[l];
+        G->lsc[i] = w->score[l];
+        if (leaf_path(w, l, &G->path, &len, &cap) < 0)
+            w_fail(w, "kd-tree deeper than %d", kStack / 2);
+        G->poff[i + 1] = len;
+    }
+    free(end);
+    free(dim);
+}
+
+static void gpair_free_export(ax_gpair *G) {
+    free(G->na);
+    free(G->nb);
+    free(G->lf);
+    free(G->lsc);
+    free(G->lnode);
+    free(G->poff);
+    free(G->path);
+    G->na = G->nb = G->lf = G->lsc = G->lnode = G->path = NULL;
+    G->poff = NULL;
+}
+
+static void *gdp_thread(void *arg) {
+    ax_gjob *X = arg;
+    ax_job *J = X->J;
+    for (;;) {
+        const int64_t k = atomic_fetch_add(&X->next, 1);
+        if (k >= J->n_pairs)
+            break;
+        const int32_t p = J->order[k];
+        ax_gpair *G = &X->G[p];
+        ax_work *w = &G->w;
+        ax_out *o = &J->out[p];
+        const double t0 = gnow();
+        if (X->phase == 1) {
+            memset(o, 0, sizeof(*o));
+            w->e = J->e;
+            if (gac_genome_view(J->ctx, GAC_Q, J->in->q_seq[p], &w->q.v) != GAC_OK ||
+                gac_genome_view(J->ctx, GAC_T, J->in->t_seq[p], &w->t.v) != GAC_OK) {
+                o->err = 1;
+                snprintf(o->msg, sizeof(o->msg), "pair %d: no host sequence", p);
+                continue;
+            }
+            G->ok = 1;
+            w->q.minus = J->in->q_strand[p] ? 1 : 0;
+            w->t.minus = 0;
+            const int64_t b0 = J->poff[p];
+            w->n = (int32_t)(J->poff[p + 1] - b0);
+            w->qs = J->qs + b0;
+            w->qe = J->qe + b0;
+            w->ts = J->ts + b0;
+            w->te = J->te + b0;
+            w->score = J->score + b0;
+            work_reserve(w, w->n);
+            if (pair_leaves(w) > 0) {
+                pair_tree(w);
+                gpair_export(G);
+            }
+        } else if (X->phase == 2) {
+            if (!G->ok || w->err)
+                continue;
+            if (w->nl == 0) {
+                o->coff = calloc(1, sizeof(int32_t));
+                continue;
+            }
+            const int64_t lo = X->leaf_off[p];
+            for (int32_t i = 0; i < w->nl; ++i) {
+                const int32_t l = w->tord[i];
+                w->total[l] = (double)X->total[lo + i];
+                w->pred[l] = X->pred[lo + i];
+            }
+            gpair_free_export(G);
+            char *dbuf = NULL;
+            size_t dlen = 0;
+            FILE *df = J->want_details ? open_memstream(&dbuf, &dlen) : NULL;
+            pair_peel(w, &J->info[p], df, &G->pc);
+            if (df) {
+                fclose(df);
+                o->details = dbuf;
+                o->details_len = dlen;
+            }
+            /* the chains' adjacent overlapping blocks that take a crossover */
+            G->xjob = malloc((size_t)(G->pc.nbk ? G->pc.nbk : 1) * sizeof(int32_t));
+            G->xl = NULL;
+            G->nx = 0;
+            int32_t cap = 0;
+            for (int32_t c = 0; c < G->pc.nc; ++c)
+                for (int32_t j = G->pc.cstart[c]; j < G->pc.cstart[c + 1]; ++j) {
+                    G->xjob[j] = -1;
+                    if (j == G->pc.cstart[c])
+                        continue;
+                    const int32_t a = G->pc.cblk[j - 1], b = G->pc.cblk[j];
+                    const int dq = w->qs[b] - w->qe[a], dt = w->ts[b] - w->te[a];
+                    if (dq >= 0 && dt >= 0)
+                        continue;
+                    const int ov = -(dq < dt ? dq : dt);
+                    if (ov >= w->qe[b] - w->qs[b] || ov >= w->qe[a] - w->qs[a])
+                        continue;
+                    if (G->nx == cap) {
+                        cap = cap * 2 + 16;
+                        G->xl = realloc(G->xl, (size_t)cap * 5 * sizeof(int32_t));
+                    }
+                    int32_t *x = G->xl + 5 * G->nx;
+                    x[0] = w->qe[a];
+                    x[1] = w->te[a];
+                    x[2] = w->qs[b];
+                    x[3] = w->ts[b];
+                    x[4] = ov;
+                    G->xjob[j] = G->nx++; /* local: made global in phase 3 */
+                }
+        } else {
+            if (!G->ok || w->err || w->nl == 0)
+                continue;
+            const int64_t x0 = X->xoff[p];
+            for (int32_t j = 0; j < G->pc.nbk; ++j)
+                if (G->xjob[j] >= 0)
+                    G->xjob[j] += (int32_t)x0;
+            ax_xres xr = {G->xjob, X->xpos, X->xadj, X->xlqe, X->xlte, X->xrqs, X->xrts, X->xov};
+            pair_finish(w, &G->pc, &xr, o);
+            free(G->xjob);
+            free(G->xl);
+            G->xjob = G->xl = NULL;
+        }
+        G->t0 += gnow() - t0;
+        o->secs = G->t0;
+        if (w->err) {
+            o->err = 1;
+            memcpy(o->msg, w->msg, sizeof(o->msg));
+        }
+    }
+    return NULL;
+}
+
+static void gdp_phase(ax_gjob *X, int phase, int nt) {
+    X->phase = phase;
+    atomic_store(&X->next, 0);
+    gac_run_threads(nt, gdp_thread, X);
+}
+
+static int axt_dp_gpu(ax_job *J, int nt) {
+    const int64_t np = J->n_pairs;
+    ax_gpair *G = calloc((size_t)(np ? np : 1), sizeof(ax_gpair));
+    ax_gjob X;
+    memset(&X, 0, sizeof(X));
+    X.J = J;
+    X.G = G;
+    atomic_init(&X.next, 0);
+    int rc = GAC_OK;
+    double t = gnow();
+    gdp_phase(&X, 1, nt);
+    double t1 = gnow();
+    /* gather the pairs' trees */
+    int64_t *node_off = malloc((size_t)(np + 1) * sizeof(int64_t));
+    int64_t *leaf_off = malloc((size_t)(np + 1) * sizeof(int64_t));
+    node_off[0] = leaf_off[0] = 0;
+    int64_t npath = 0;
+    for (int64_t p = 0; p < np; ++p) {
+        const int live = G[p].ok && !G[p].w.err && G[p].w.nl > 0;
+        node_off[p + 1] = node_off[p] + (live ? G[p].w.nn : 0);
+        leaf_off[p + 1] = leaf_off[p] + (live ? G[p].w.nl : 0);
+        npath += live ? G[p].poff[G[p].w.nl] : 0;
+    }
+    const int64_t nn = node_off[np], nl = leaf_off[np];
+    int32_t *na = malloc((size_t)(nn ? nn : 1) * 16), *nb = malloc((size_t)(nn ? nn : 1) * 8);
+    int32_t *lf = malloc((size_t)(nl ? nl : 1) * 16), *lsc = malloc((size_t)(nl ? nl : 1) * 4);
+    int32_t *lnode = malloc((size_t)(nl ? nl : 1) * 4);
+    int64_t *poff = malloc((size_t)(nl + 1) * 8);
+    int32_t *path = malloc((size_t)(npath ? npath : 1) * 4);
+    int64_t *total = malloc((size_t)(nl ? nl : 1) * 8);
+    int32_t *pred = malloc((size_t)(nl ? nl : 1) * 4);
+    poff[0] = 0;
+    for (int64_t p = 0; p < np; ++p) {
+        const int64_t n0 = node_off[p], l0 = leaf_off[p], cn = node_off[p + 1] - n0,
+                      cl = leaf_off[p + 1] - l0;
+        if (!cl)
+            continue;
+        memcpy(na + 4 * n0, G[p].na, (size_t)cn * 16);
+        memcpy(nb + 2 * n0, G[p].nb, (size_t)cn * 8);
+        memcpy(lf + 4 * l0, G[p].lf, (size_t)cl * 16);
+        memcpy(lsc + l0, G[p].lsc, (size_t)cl * 4);
+        memcpy(lnode + l0, G[p].lnode, (size_t)cl * 4);
+        const int64_t pb = poff[l0];
+        memcpy(path + pb, G[p].path, (size_t)G[p].poff[cl] * 4);
+        for (int64_t i = 0; i < cl; ++i)
+            poff[l0 + i + 1] = pb + G[p].poff[i + 1];
+    }
+    for (int64_t p = 0; p < np; ++p)
+        if (leaf_off[p + 1] == leaf_off[p])
+            for (int64_t i = leaf_off[p]; i < leaf_off[p + 1]; ++i)
+                poff[i + 1] = poff[i];
+    double t2 = gnow();
+    rc = gac_chain_dp(J->ctx, np, J->in->t_seq, J->in->q_seq, J->in->q_strand, node_off, na, nb,
+                      leaf_off, lf, lsc, lnode, poff, path, total, pred);
+    double t3 = gnow();
+    free(na);
+    free(nb);
+    free(lf);
+    free(lsc);
+    free(lnode);
+    free(poff);
+    free(path);
+    free(node_off);
+    int64_t *xoff = NULL;
+    double t4 = t3, t5 = t3, t6 = t3;
+    if (rc == GAC_OK) {
+        X.leaf_off = leaf_off;
+        X.total = total;
+        X.pred = pred;
+        gdp_phase(&X, 2, nt);
+        t4 = gnow();
+        xoff = malloc((size_t)(np + 1) * sizeof(int64_t));
+        xoff[0] = 0;
+        for (int64_t p = 0; p < np; ++p)
+            xoff[p + 1] = xoff[p] + G[p].nx;
+        const int64_t nx = xoff[np];
+        int32_t *xt = malloc((size_t)(nx ? nx : 1) * 4), *xq = malloc((size_t)(nx ? nx : 1) * 4);
+        uint8_t *xs = malloc((size_t)(nx ? nx : 1));
+        int32_t *xv[5], *xpos = malloc((size_t)(nx ? nx : 1) * 4), *xadj = malloc((size_t)(nx ? nx : 1) * 4);
+        for (int f = 0; f < 5; ++f)
+            xv[f] = malloc((size_t)(nx ? nx : 1) * 4);
+        for (int64_t p = 0; p < np; ++p)
+            for (int32_t k = 0; k < G[p].nx; ++k) {
+                const int64_t g = xoff[p] + k;
+                xt[g] = J->in->t_seq[p];
+                xq[g] = J->in->q_seq[p];
+                xs[g] = J->in->q_strand[p] ? 1 : 0;
+                for (int f = 0; f < 5; ++f)
+                    xv[f][g] = G[p].xl[5 * k + f];
+            }
+        rc = gac_crossovers(J->ctx, nx, xt, xq, xs, xv[0], xv[1], xv[2], xv[3], xv[4], xpos, xadj);
+        t5 = gnow();
+        if (rc == GAC_OK) {
+            X.xoff = xoff;
+            X.xpos = xpos;
+            X.xadj = xadj;
+            X.xlqe = xv[0];
+            X.xlte = xv[1];
+            X.xrqs = xv[2];
+            X.xrts = xv[3];
+            X.xov = xv[4];
+            gdp_phase(&X, 3, nt);
+        }
+        t6 = gnow();
+        if (getenv("GAC_TIMING"))
+            fprintf(stderr, "[gac_axt_chain] device DP: trees %.3f s, gather %.3f s, gac_chain_dp "
+                            "%.3f s, peel %.3f s, %lld crossovers %.3f s, finish %.3f s\n",
+                    t1 - t, t2 - t1, t3 - t2, t4 - t3, (long long)nx, t5 - t4, t6 - t5);
+        free(xt);
+        free(xq);
+        free(xs);
+        free(xpos);
+        free(xadj);
+        for (int f = 0; f < 5; ++f)
+            free(xv[f]);
+    }
+    free(xoff);
+    free(leaf_off);
+    free(total);
+    free(pred);
+    for (int64_t p = 0; p < np; ++p) {
+        ax_work *w = &G[p].w;
+        gpair_free_export(&G[p]);
+        free(G[p].pc.cblk);
+        free(G[p].pc.cstart);
+        free(G[p].xjob);
+        free(G[p].xl);
+        free(w->total);
+        free(w->pred);
+        free(w->hit);
+        free(w->tord);
+        free(w->qord);
+        free(w->tmp);
+        free(w->nodes);
+        free(w->xs);
+    }
+    free(G);
+    return rc;
 }
 
 static int thread_count(int req) {
@@ -981,8 +1454,14 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
     int nt = nthreads;
     if (nt > np)
         nt = np > 0 ? (int)np : 1;
-    run_threads(nt, ax_thread, &J);
-    stage("kd-tree DP (threads)", &tclock);
+    const char *dpm = getenv("GAC_AXT_DP");
+    if (dpm && strcmp(dpm, "gpu") == 0) {
+        rc = axt_dp_gpu(&J, nt);
+        stage("kd-tree DP (device)", &tclock);
+    } else {
+        run_threads(nt, ax_thread, &J);
+        stage("kd-tree DP (threads)", &tclock);
+    }
     if (getenv("GAC_TIMING")) {
         double sum = 0, mx = 0;
         int64_t imx = 0;

@@ -184,6 +184,41 @@ int gac_score_blocks(gac_ctx *ctx, int64_t n_pairs, const int32_t *t_seq, const 
                      const uint8_t *q_strand, const int64_t *blk_off, const int32_t *blk_t,
                      const int32_t *blk_q, const int32_t *blk_size, int32_t *score);
 
+/* The kd-tree DP of chainBlocks on the device: findBestPredecessors
+ * (kent/src/lib/chainBlock.c:281-300) -- bestPredecessor (:207-263) with
+ * chainConnectCost / cBlockFindCrossover (chainConnect.c:61-149) as its
+ * connect cost, updateScoresOnWay (:265-279) -- for n_pairs seqPairs in one
+ * launch, one wave per pair.  The caller builds each pair's tree (kdBuild,
+ * :124-164) in pre-order with the hi child first:
+ *   node_a[4v..] = {maxQ, maxT, cut, lo child}         internal node
+ *                  {qEnd, tEnd, qStart, tStart}        leaf node
+ *   node_b[2v..] = {end of v's subtree, dim (0 q, 1 t)} internal node
+ *                  {end = v + 1, ~(leaf position)}     leaf node
+ * node indices are relative to the pair (nodes [node_off[p], node_off[p+1])).
+ * Leaves are in findBestPredecessors' target order, [leaf_off[p],
+ * leaf_off[p+1]): leaf[4i..] = {qStart, qEnd, tStart, tEnd}, leaf_score[i]
+ * (axtScoreUngapped), leaf_node[i] (its node), and path[path_off[i] ..
+ * path_off[i+1]) = the nodes updateScoresOnWay's descent reaches for it
+ * (global leaf index i; path_off has total leaves + 1 entries).  Out, per
+ * leaf: total[i] = totalScore, pred[i] = best predecessor node or -1.
+ * Uses the context's scoring setup (gac_set_scoring) and genomes. */
+int gac_chain_dp(gac_ctx *ctx, int64_t n_pairs, const int32_t *t_seq, const int32_t *q_seq,
+                 const uint8_t *q_strand, const int64_t *node_off, const int32_t *node_a,
+                 const int32_t *node_b, const int64_t *leaf_off, const int32_t *leaf,
+                 const int32_t *leaf_score, const int32_t *leaf_node, const int64_t *path_off,
+                 const int32_t *path, int64_t *total, int32_t *pred);
+
+/* cBlockFindCrossover (kent/src/lib/chainConnect.c:61-105) of n overlapping
+ * block pairs on the device (one wave per pair, a prefix-sum / first-maximum
+ * scan): left block ending at (lqe, lte), right block starting at (rqs, rts),
+ * `overlap` bases, on seqPair (t_seq, q_seq, q_strand) -- strand coordinates.
+ * Out: pos (crossover offset from the right block's start) and adj (the
+ * score adjustment).  Uses the context's score matrix. */
+int gac_crossovers(gac_ctx *ctx, int64_t n, const int32_t *t_seq, const int32_t *q_seq,
+                   const uint8_t *q_strand, const int32_t *lqe, const int32_t *lte,
+                   const int32_t *rqs, const int32_t *rts, const int32_t *overlap, int32_t *pos,
+                   int32_t *adj);
+
 /* axtChain's chaining of every seqPair (axtChain.c:250-309 chainPair and
  * :452-470 the final sort), replacing
  *   removeExactOverlaps          axtChain.c:173-197
@@ -200,7 +235,10 @@ int gac_score_blocks(gac_ctx *ctx, int64_t n_pairs, const int32_t *t_seq, const 
  * them before removeExactOverlaps (input order: the PSL/axt records and their
  * blocks as read).  Pairs are processed in the given order (spList order);
  * the kd-tree DP runs on host threads (n_threads, 0 = all cores), one pair at
- * a time per thread.  Output chains are in chainWrite order; ids are 1..n.
+ * a time per thread -- or, with GAC_AXT_DP=gpu in the environment, on the
+ * device (gac_chain_dp, then the crossovers of scoreBlocks and
+ * chainRemovePartialOverlaps through gac_crossovers); the output is the same.
+ * Output chains are in chainWrite order; ids are 1..n.
  * details_path (may be NULL): axtChain -details text.  Installs mat/g on
  * the context (gac_set_scoring). */
 typedef struct gac_axt_input {

@@ -56,11 +56,20 @@ int gac_set_scoring(gac_ctx *c, const int32_t mat[16], const gac_gapcalc *g) {
     return GAC_OK;
 }
 
+int gac_genome_load_twobit(gac_ctx *c, int which, gac_twobit *tb);
+
 int gac_genome_load_2bit(gac_ctx *c, int which, const char *path) {
-    side *s = &c->s[which];
-    int rc = gac_twobit_open(path, &s->tb);
+    gac_twobit tb;
+    int rc = gac_twobit_open(path, &tb);
     if (rc != GAC_OK)
         return rc;
+    return gac_genome_load_twobit(c, which, &tb);
+}
+
+/* the file is already open (the tools map it while the device starts) */
+int gac_genome_load_twobit(gac_ctx *c, int which, gac_twobit *tb) {
+    side *s = &c->s[which];
+    s->tb = *tb;
     s->n = (int32_t)s->tb.seq_count;
     s->names = calloc(s->n, sizeof(char *));
     s->sizes = calloc(s->n, 4);
@@ -136,9 +145,16 @@ int gac_genome_view(gac_ctx *c, int which, int32_t i, gac_seq_view *v) {
 static int base(const side *s, int32_t i, int minus, int32_t j) {
     const int32_t size = s->sizes[i];
     const int32_t f = minus ? size - 1 - j : j;
-    for (int32_t k = 0; k < s->nn[i]; ++k)
-        if (f >= s->ns[i][k] && f < s->ns[i][k] + s->nz[i][k])
-            return 4;
+    int32_t lo = 0, hi = s->nn[i]; /* first N run ending past f (runs sorted, disjoint) */
+    while (lo < hi) {
+        const int32_t mid = (lo + hi) / 2;
+        if (s->ns[i][mid] + s->nz[i][mid] > f)
+            hi = mid;
+        else
+            lo = mid + 1;
+    }
+    if (lo < s->nn[i] && s->ns[i][lo] <= f)
+        return 4;
     const int c = (s->packed[i][f >> 2] >> (6 - 2 * (f & 3))) & 3;
     return minus ? c ^ 2 : c;
 }
@@ -218,5 +234,180 @@ int gac_score_ranges(gac_ctx *c, const gac_chainset *s, const gac_range *r, int6
         g[i] = sc;
         ali[i] = a;
     }
+    return GAC_OK;
+}
+
+/* ---- gac_chain_dp / gac_crossovers: a lane-by-lane CPU emulation of the
+ * device algorithm of k_dp / k_xover (csrc/gac_dp.hip) -- windows of 64
+ * pre-order nodes resolved by prefix-max rounds, crossovers by prefix sum
+ * and first maximum -- so that the algorithm and the host's GAC_AXT_DP=gpu
+ * phases can be checked against the reference here. */
+static int emu_gap(gac_ctx *c, int dq, int dt) {
+    if (dq < 0)
+        dq = 0;
+    if (dt < 0)
+        dt = 0;
+    return gac_gap_cost(c->g, dq, dt);
+}
+
+static int emu_msc(gac_ctx *c, int q, int t) {
+    static const int acgt[4] = {3, 1, 0, 2};
+    return (q == 4 || t == 4) ? 0 : c->mat[acgt[q] * 4 + acgt[t]];
+}
+
+static void emu_xover(gac_ctx *c, int32_t ts, int32_t qs, int minus, int lqe, int lte, int rqs,
+                      int rts, int ov, int *pos, int *adj) {
+    long long carry = 0, lsum = 0, bestv = 0;
+    int bestpos = 0;
+    for (int base0 = 0; base0 < ov; base0 += 64) {
+        long long incl[64], l[64];
+        long long run = 0;
+        for (int lane = 0; lane < 64; ++lane) {
+            const int k = base0 + lane;
+            long long d = 0;
+            l[lane] = 0;
+            if (k < ov) {
+                l[lane] = emu_msc(c, base(&c->s[1], qs, minus, lqe - ov + k), base(&c->s[0], ts, 0, lte - ov + k));
+                d = l[lane] - emu_msc(c, base(&c->s[1], qs, minus, rqs + k), base(&c->s[0], ts, 0, rts + k));
+            }
+            run += d;
+            incl[lane] = run;
+        }
+        long long mv = INT64_MIN;
+        int mk = 0;
+        for (int lane = 0; lane < 64; ++lane)
+            if (base0 + lane < ov && carry + incl[lane] > mv) {
+                mv = carry + incl[lane];
+                mk = base0 + lane;
+            }
+        if (mv > bestv) {
+            bestv = mv;
+            bestpos = mk + 1;
+        }
+        carry += incl[63];
+        for (int lane = 0; lane < 64; ++lane)
+            lsum += l[lane];
+    }
+    *pos = bestpos;
+    *adj = (int)(lsum - bestv);
+}
+
+int gac_crossovers(gac_ctx *c, int64_t n, const int32_t *t_seq, const int32_t *q_seq,
+                   const uint8_t *q_strand, const int32_t *lqe, const int32_t *lte,
+                   const int32_t *rqs, const int32_t *rts, const int32_t *overlap, int32_t *pos,
+                   int32_t *adj) {
+    for (int64_t j = 0; j < n; ++j)
+        emu_xover(c, t_seq[j], q_seq[j], q_strand[j], lqe[j], lte[j], rqs[j], rts[j], overlap[j],
+                  &pos[j], &adj[j]);
+    return GAC_OK;
+}
+
+static int emu_connect(gac_ctx *c, int32_t ts, int32_t qs, int minus, int aqs, int aqe, int ate,
+                       int bqs, int bqe, int bts) {
+    int dq = bqs - aqe, dt = bts - ate, adj = 0;
+    if (dq < 0 || dt < 0) {
+        const int bsz = bqe - bqs, asz = aqe - aqs, ov = -(dq < dt ? dq : dt);
+        if (ov >= bsz || ov >= asz) {
+            adj = 100000000;
+        } else {
+            int p;
+            emu_xover(c, ts, qs, minus, aqe, ate, bqs, bts, ov, &p, &adj);
+            dq += ov;
+            dt += ov;
+        }
+    }
+    return adj + emu_gap(c, dq, dt);
+}
+
+int gac_chain_dp(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq, const int32_t *q_seq,
+                 const uint8_t *q_strand, const int64_t *node_off, const int32_t *node_a,
+                 const int32_t *node_b, const int64_t *leaf_off, const int32_t *leaf,
+                 const int32_t *leaf_score, const int32_t *leaf_node, const int64_t *path_off,
+                 const int32_t *path, int64_t *total, int32_t *pred) {
+    const int64_t NN = node_off[n_pairs];
+    long long *ms = calloc((size_t)(NN ? NN : 1), 8), *tot = calloc((size_t)(NN ? NN : 1), 8);
+    for (int64_t p = 0; p < n_pairs; ++p)
+        for (int64_t i = leaf_off[p]; i < leaf_off[p + 1]; ++i)
+            tot[node_off[p] + leaf_node[i]] = leaf_score[i];
+    for (int64_t p = 0; p < n_pairs; ++p) {
+        const int64_t o = node_off[p];
+        const int nn = (int)(node_off[p + 1] - o);
+        const int32_t *na = node_a + 4 * o, *nb = node_b + 2 * o;
+        for (int64_t li = leaf_off[p]; li < leaf_off[p + 1]; ++li) {
+            const int lq = leaf[4 * li], lqe = leaf[4 * li + 1], lt = leaf[4 * li + 2];
+            const long long ls = leaf_score[li];
+            long long best = 0;
+            int best_node = -1, p0 = 0;
+            while (p0 < nn) {
+                long long key[64], sc[64];
+                int cand[64], se[64], nxt[64], in[64], lf[64], end[64];
+                for (int lane = 0; lane < 64; ++lane) {
+                    const int v = p0 + lane;
+                    in[lane] = v < nn;
+                    se[lane] = v + 1;
+                    cand[lane] = 0;
+                    lf[lane] = 0;
+                    key[lane] = 0;
+                    nxt[lane] = v + 1;
+                    end[lane] = v + 1;
+                    if (!in[lane])
+                        continue;
+                    const int32_t *A = na + 4 * v, *B = nb + 2 * v;
+                    const long long m1 = ms[o + v] + ls;
+                    const long long m2 = m1 - emu_gap(c, lq - A[0], lt - A[1]);
+                    key[lane] = m1 < m2 ? m1 : m2;
+                    lf[lane] = B[1] < 0;
+                    end[lane] = B[0];
+                    if (lf[lane] && A[2] < lq && A[3] < lt) {
+                        cand[lane] = 1;
+                        sc[lane] = tot[o + v] + ls -
+                                   emu_connect(c, t_seq[p], q_seq[p], q_strand[p], A[2], A[0], A[1],
+                                               lq, lqe, lt);
+                    }
+                    if (!lf[lane])
+                        nxt[lane] = (B[1] == 0 ? lq : lt) > A[2] ? v + 1 : A[3];
+                }
+                int cur = 0;
+                for (;;) {
+                    for (int lane = cur; lane < 64; ++lane)
+                        if (in[lane])
+                            se[lane] = key[lane] < best ? end[lane] : (lf[lane] ? p0 + lane + 1 : nxt[lane]);
+                    int u = -1, pm = 0;
+                    for (int lane = 0; lane < 64; ++lane) {
+                        const int visited = in[lane] && pm <= p0 + lane;
+                        if (u < 0 && visited && lane >= cur && cand[lane] && !(key[lane] < best) &&
+                            sc[lane] > best)
+                            u = lane;
+                        if (se[lane] > pm)
+                            pm = se[lane];
+                    }
+                    if (u < 0)
+                        break;
+                    best = sc[u];
+                    best_node = p0 + u;
+                    cur = u + 1;
+                }
+                int mx = 0;
+                for (int lane = 0; lane < 64; ++lane)
+                    if (in[lane] && se[lane] > mx)
+                        mx = se[lane];
+                p0 = p0 + 64 > mx ? p0 + 64 : mx;
+            }
+            long long t = ls;
+            int pr = -1;
+            if (best > ls) {
+                t = best;
+                pr = best_node;
+            }
+            total[li] = t;
+            pred[li] = pr;
+            tot[o + leaf_node[li]] = t;
+            for (int64_t k = path_off[li]; k < path_off[li + 1]; ++k)
+                if (ms[o + path[k]] < t)
+                    ms[o + path[k]] = t;
+        }
+    }
+    free(ms);
+    free(tot);
     return GAC_OK;
 }

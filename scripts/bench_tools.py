@@ -70,13 +70,13 @@ def axtchain(a):
         synth.write_2bit(qg, os.path.join(d, "q.2bit"))
         nrec = synth.write_psl_c4(tg, qg, pairs, b, psl, a.seed)
         log(f"generated {len(b['t'])} blocks, {nrec} records in {time.time() - t:.1f}s")
-    env = dict(os.environ, GAC_TIMING="1")
+    env = dict(os.environ, GAC_TIMING="1", GAC_AXT_DP=a.dp)
     args = ["-psl", psl, os.path.join(d, "t.2bit"), os.path.join(d, "q.2bit")]
     ours = os.path.join(d, "ours.chain")
     t_ours, r = timed([os.path.join(BIN, "axtChain"), "-linearGap=loose", "-verbose=0"] + args +
                       [ours], env=env, outputs=[ours])
     log(r.stderr)
-    res = {"tool": "axtChain", "blocks": a.blocks, "seed": a.seed, "ours_s": round(t_ours, 3),
+    res = {"tool": "axtChain", "blocks": a.blocks, "seed": a.seed, "dp": a.dp, "ours_s": round(t_ours, 3),
            "ours_sha": sha(ours), "timing": [l for l in r.stderr.splitlines() if "gac_axt" in l]}
     refbin = os.path.join(REF, "axtChain")
     if os.path.exists(refbin) and not a.no_ref:
@@ -326,6 +326,8 @@ def main():
     ap.add_argument("tool", choices=["axtchain", "cleaner", "scorechain", "chainnet", "c5",
                                      "microjobs"])
     ap.add_argument("--jobs", type=int, default=200)
+    ap.add_argument("--dp", choices=["host", "gpu"], default="host",
+                    help="axtchain: kd-tree DP on host threads or on the device (GAC_AXT_DP)")
     ap.add_argument("--no-separate", action="store_true")
     ap.add_argument("--chains", type=int, default=200_000)
     ap.add_argument("--blocks", type=int, default=2_000_000)

@@ -192,6 +192,12 @@ def test_c4_shaped_axtchain(tmp_path):
     _run([_bin("axtChain")] + args + ["ours.chain"], cwd=d)
     _run([_ref("axtChain")] + args + ["ref.chain"], cwd=d)
     _same(os.path.join(d, "ours.chain"), os.path.join(d, "ref.chain"))
+    # the kd-tree DP and the crossovers on the device (rows A13/A14)
+    env = dict(os.environ, GAC_AXT_DP="gpu")
+    r = subprocess.run([_bin("axtChain")] + args + ["gpu.chain"], cwd=d, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    _same(os.path.join(d, "gpu.chain"), os.path.join(d, "ref.chain"))
 
 
 # ---------------------------------------------------------------- edge cases

@@ -218,10 +218,14 @@ def test_axtchain_synth(seed, case, tmp_path):
             assert filecmp.cmp(tmp_path / fn, os.path.join(d, fn), shallow=False)
 
 
-def test_axtchain_jobs_batch(tmp_path):
+@pytest.mark.parametrize("dp", ["host", "gpu"])
+def test_axtchain_jobs_batch(dp, tmp_path):
     """axtChain -jobs=FILE: the two reference KATs and
     the 8 synthetic cases as one batch -- genomes switch between jobs, one
-    device context -- every output identical to its golden file."""
+    device context -- every output identical to its golden file.  dp=gpu:
+    the kd-tree DP and the chains' crossovers on the device (GAC_AXT_DP=gpu:
+    k_dp, k_xover), rows A13/A14."""
+    env = dict(os.environ, GAC_AXT_DP=dp)
     g = GOLDEN
     lines, expect = [], []
     for c in ["newStyleLastz", "oldStyleBlastz"]:
@@ -247,7 +251,7 @@ def test_axtchain_jobs_batch(tmp_path):
     jobs = tmp_path / "jobs.txt"
     jobs.write_text("# one axtChain run per line\n\n" + "\n".join(lines) + "\n")
     r = subprocess.run([_bin("axtChain"), f"-jobs={jobs}"], capture_output=True, text=True,
-                       timeout=600, cwd=tmp_path)
+                       timeout=600, cwd=tmp_path, env=env)
     assert r.returncode == 0, r.stderr
     for got, want in expect:
         assert filecmp.cmp(got, want, shallow=False), got
@@ -256,5 +260,5 @@ def test_axtchain_jobs_batch(tmp_path):
     bad.write_text(lines[0] + "\n" + f"-linearGap=loose {tmp_path}/missing.axt "
                    f"{g}/chrM/hg19.chrM.2bit {g}/chrM/susScr3.chrM.2bit {tmp_path}/x.chain\n")
     r = subprocess.run([_bin("axtChain"), f"-jobs={bad}"], capture_output=True, text=True,
-                       timeout=600, cwd=tmp_path)
+                       timeout=600, cwd=tmp_path, env=env)
     assert r.returncode == 255 and "missing.axt" in r.stderr
