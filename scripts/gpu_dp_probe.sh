@@ -21,6 +21,6 @@ cat "$OUT/gpu.json"
 D=/tmp/c4_$BLOCKS
 cmp "$D/ours.chain" "$D/ref.chain" && echo "device DP output identical to the reference"
 cd /tmp
-GAC_AXT_DP=gpu timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- "$GRAFT_REPO_ROOT/genomealignmenttools_amd/libexec/axtChain" -linearGap=loose -verbose=0 -psl $D/in.psl $D/t.2bit $D/q.2bit /tmp/prof.chain > "$GRAFT_REPO_ROOT/$OUT/prof.log" 2>&1
+GAC_PROFILE_EXIT=1 GAC_AXT_DP=gpu timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- "$GRAFT_REPO_ROOT/genomealignmenttools_amd/libexec/axtChain" -linearGap=loose -verbose=0 -psl $D/in.psl $D/t.2bit $D/q.2bit /tmp/prof.chain > "$GRAFT_REPO_ROOT/$OUT/prof.log" 2>&1
 echo "prof rc=$?"
 cmp /tmp/prof.chain $D/ref.chain && echo "profiled run identical"
