@@ -16,7 +16,7 @@ OBJDIR   := build/obj
 
 ARCH     := gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
-            -Iinclude -I$(CSRC) -Wall -Wno-unused-result -Wno-unused-value
+            -Iinclude -I$(CSRC) -Wall -Wno-unused-result -Wno-unused-value $(HIPEXTRA)
 CFLAGS   := -O2 -std=gnu11 -fPIC -Wall -Iinclude -I$(CSRC)
 
 HOST_SRC := $(wildcard $(CSRC)/host/*.c)
