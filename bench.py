@@ -14,12 +14,19 @@ start, chain parse, host netting, 2bit genomes + chains to HBM, GPU
 rescoring of every partial target fill, both nets written).  value = the
 aligned bases of the netted input chains (score >= 0) / wall time per step.
 
-N > 1 (torchrun, one process per GPU): every step runs the tool on every rank
-over the SAME input with -nranks=N -rank=r: rank r nets the chromosome sides
-it owns (LPT by aligned bases), rescores its target fills on its own GPU and
-writes its part; rank 0 assembles both nets.  Strong scaling on one chain
-set, no data-path collective (the netting partitions by chromosome side);
-torch.distributed (RCCL) carries the barriers and the max-over-ranks clock.
+N > 1 (torchrun, one process per GPU): weak scaling, C2 per GPU.  The input
+is ONE chain set over N target chromosomes: N replicas of C2's target
+chromosome (chr1, chr1_r1, ..., same sequence) and of its chains (renamed,
+ids renumbered, interleaved in score order), against the same mm10 query.
+Every step runs the tool on every rank over that input with -nranks=N
+-rank=r: rank r nets the chromosome sides it owns (contiguous runs of each
+sizes file, balanced by length: one target chromosome per rank, 1/N of the
+query chromosomes), parses only the chains on its sides, loads only its
+target sequence, rescores its target fills on its own GPU and writes its
+part; rank 0 assembles both nets.  No data-path collective (the netting
+partitions by chromosome side); torch.distributed (RCCL) carries the
+barriers and the max-over-ranks clock.  value = netted aligned bases of the
+whole set / wall time.
 
 Also reported:
   kernel   -- the GPU rescoring call alone (gac_score_ranges_device over the
@@ -81,6 +88,7 @@ def parse():
                         "query position) order")
     p.add_argument("--tmp", default=os.environ.get("TMPDIR", "/tmp"))
     p.add_argument("--gen-only", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--replicas", type=int, default=1, help=argparse.SUPPRESS)
     return p.parse_args()
 
 
@@ -117,6 +125,76 @@ def c2_files(args):
             json.dump(info, f)
         os.rename(p("info.json.tmp"), p("info.json"))
         log(f"C2: {info} written in {time.time() - t0:.1f}s")
+    with open(p("info.json")) as f:
+        return d, json.load(f)
+
+
+def _replicate_2bit(src, dst, names):
+    """A version-0 .2bit holding the one sequence of `src` under every name
+    (its record bytes copied, the index rebuilt)."""
+    import struct
+    with open(src, "rb") as f:
+        data = f.read()
+    magic, _, cnt, _ = struct.unpack_from("<IIII", data, 0)
+    assert cnt == 1, src
+    nl = data[16]
+    rec = data[struct.unpack_from("<I", data, 17 + nl)[0]:]
+    off = 16 + sum(1 + len(n) + 4 for n in names)
+    with open(dst + ".tmp", "wb") as f:
+        f.write(struct.pack("<IIII", magic, 0, len(names), 0))
+        for k, n in enumerate(names):
+            f.write(struct.pack("<B", len(n)) + n.encode() + struct.pack("<I", off + k * len(rec)))
+        for _ in names:
+            f.write(rec)
+    os.rename(dst + ".tmp", dst)
+
+
+def _replicate_chains(src, dst, names):
+    """Every chain of `src` once per target name (tName replaced), copies
+    adjacent (the file stays sorted by score), ids 1..n in file order."""
+    with open(src, "rb") as f:
+        data = f.read()
+    head, sep, body = data.partition(b"chain ")
+    out, nid = [head], 0
+    enc = [n.encode() for n in names]
+    for rec in (sep + body).split(b"\n\n"):
+        if not rec.strip():
+            continue
+        hdr, _, blocks = rec.partition(b"\n")
+        w = hdr.split(b" ")
+        for nm in enc:
+            nid += 1
+            w[2] = nm
+            w[12:] = [str(nid).encode()]
+            out.append(b" ".join(w) + b"\n" + blocks + b"\n\n")
+    with open(dst + ".tmp", "wb") as f:
+        f.write(b"".join(out))
+    os.rename(dst + ".tmp", dst)
+
+
+def c2n_files(args, n):
+    """The N>1 input: C2 replicated per rank (see the module docstring)."""
+    d1, info1 = c2_files(args)
+    d = d1 + f"_x{n}"
+    p = lambda x: os.path.join(d, x)
+    if not os.path.exists(p("info.json")):
+        os.makedirs(d, exist_ok=True)
+        t0 = time.time()
+        names = ["chr1"] + [f"chr1_r{k}" for k in range(1, n)]
+        tsize = open(os.path.join(d1, "t.sizes")).read().split()[1]
+        with open(p("t.sizes"), "w") as f:
+            f.write("".join(f"{nm}\t{tsize}\n" for nm in names))
+        _replicate_2bit(os.path.join(d1, "t.2bit"), p("t.2bit"), names)
+        _replicate_chains(os.path.join(d1, "in.chain"), p("in.chain"), names)
+        for x in ("q.2bit", "q.sizes"):
+            if not os.path.exists(p(x)):
+                os.symlink(os.path.join(d1, x), p(x))
+        info = {k: v * n for k, v in info1.items()}
+        info["replicas"] = n
+        with open(p("info.json.tmp"), "w") as f:
+            json.dump(info, f)
+        os.rename(p("info.json.tmp"), p("info.json"))
+        log(f"C2 x{n}: written in {time.time() - t0:.1f}s")
     with open(p("info.json")) as f:
         return d, json.load(f)
 
@@ -398,6 +476,8 @@ def main():
     args = parse()
     if args.gen_only:
         c2_files(args)
+        if args.replicas > 1:
+            c2n_files(args, args.replicas)
         return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -415,13 +495,15 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    files = (lambda: c2_files(args)) if world == 1 else (lambda: c2n_files(args, world))
     if rank == 0:  # generated in a child process: this one stays small
         subprocess.run([sys.executable, os.path.abspath(__file__), "--gen-only", "--chains",
-                        str(args.chains), "--seed", str(args.seed), "--tmp", args.tmp], check=True)
-        d, info = c2_files(args)
+                        str(args.chains), "--seed", str(args.seed), "--tmp", args.tmp,
+                        "--replicas", str(world)], check=True)
+        d, info = files()
     barrier()
     if rank != 0:
-        d, info = c2_files(args)  # written by rank 0 (same node)
+        d, info = files()  # written by rank 0 (same node)
     out_base = os.path.join(d, f"ours.r{world}")
     outs = [out_base + ".t.net", out_base + ".q.net"]
     cmd = tool_cmd(d, out_base, world, rank)
@@ -449,9 +531,13 @@ def main():
             "value": info["netted_aligned_bases"] / step_s / 1e9,
             "unit": "Gbases/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": step_s * 1e3, "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "int64",
-            "data": "synthetic (seeded C2: hg38 chr1 x mm10 sizes, planted chains; no real genomes)",
-            "config": {"workload": "chainNet -rescore end to end (bin/chainNet, C2)",
+            "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+            "data": "synthetic (seeded C2: hg38 chr1 x mm10 sizes, planted chains; no real genomes)"
+                    + ("" if world == 1 else f"; C2 replicated x{world}: {world} target "
+                       "chromosomes (copies of C2's chr1) in one chain set"),
+            "config": {"workload": "chainNet -rescore end to end (bin/chainNet, C2"
+                                   + (")" if world == 1 else f" per GPU, one set over {world} "
+                                      "target chromosomes, chromosome sides split across ranks)"),
                        **info, "parallelism": f"chromosome-side shards x{world}",
                        "host_threads_per_rank": host_threads(), "tool_stages": stages},
         }

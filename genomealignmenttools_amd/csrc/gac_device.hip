@@ -616,6 +616,11 @@ extern "C" int gac_genome_load_2bit(gac_ctx *c, int side, const char *path) {
 }
 
 extern "C" int gac_genome_load_twobit(gac_ctx *c, int side, gac_twobit *tbp) {
+    return gac_genome_load_twobit_keep(c, side, tbp, nullptr);
+}
+
+extern "C" int gac_genome_load_twobit_keep(gac_ctx *c, int side, gac_twobit *tbp,
+                                           const uint8_t *keep) {
     gac_clear_error();
     if (!side_of(c, side) || !tbp) {
         if (tbp) gac_twobit_close(tbp);
@@ -626,6 +631,7 @@ extern "C" int gac_genome_load_twobit(gac_ctx *c, int side, gac_twobit *tbp) {
     int rc = GAC_OK;
     std::vector<int32_t> ns, nz;
     for (uint32_t i = 0; i < tb.seq_count && rc == GAC_OK; ++i) {
+        if (keep && !keep[i]) continue;  // a sequence this process never scores
         const gac_twobit_seq &s = tb.seqs[i];
         ns.resize(s.n_count);
         nz.resize(s.n_count);

@@ -62,6 +62,9 @@ int gac_twobit_open_ex(const char *path, gac_twobit *tb, int populate);
 /* gac_genome_load_2bit of an already opened file; the genome side takes
  * over tb (closed on error as well) */
 int gac_genome_load_twobit(gac_ctx *c, int side, gac_twobit *tb);
+/* the same with only the sequences i of the file where keep[i] != 0 (keep
+ * may be NULL: all) */
+int gac_genome_load_twobit_keep(gac_ctx *c, int side, gac_twobit *tb, const uint8_t *keep);
 void gac_twobit_close(gac_twobit *tb);
 uint32_t gac_twobit_u32(const gac_twobit *tb, const uint8_t *p);
 int gac_is_twobit_file(const char *path);

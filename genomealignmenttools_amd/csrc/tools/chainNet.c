@@ -117,7 +117,10 @@ static void *subset_copy_thread(void *arg) {
 typedef struct pre_upload {
     gt_device *dev;
     const gt_chains *c;
-    gac_chainset *cs; /* NULL: use the subset path */
+    const uint8_t *tkeep; /* -nranks: this rank's target sides (NULL: all) */
+    const int32_t *tix;   /* chain -> target sizes index */
+    gac_chainset *cs;     /* NULL: use the subset path */
+    int32_t *remap;       /* chain -> uploaded index (-1: not uploaded); NULL: identity */
     pthread_t th;
     int started;
 } pre_upload;
@@ -130,11 +133,12 @@ static void *pre_upload_thread(void *arg) {
     const gt_chains *c = u->c;
     int32_t *tmap = gt_seq_map(ctx, GAC_T, &c->tnames), *qmap = gt_seq_map(ctx, GAC_Q, &c->qnames);
     int ok = 1;
-    for (int32_t k = 0; k < c->tnames.n && ok; ++k)
-        ok = tmap[k] >= 0;
     for (int32_t k = 0; k < c->qnames.n && ok; ++k)
         ok = qmap[k] >= 0;
-    if (ok) {
+    if (!u->tkeep)
+        for (int32_t k = 0; k < c->tnames.n && ok; ++k)
+            ok = tmap[k] >= 0;
+    if (ok && !u->tkeep) { /* the whole set */
         int32_t *ts = malloc((size_t)(c->n ? c->n : 1) * 4), *qs = malloc((size_t)(c->n ? c->n : 1) * 4);
         for (int64_t i = 0; i < c->n; ++i) {
             ts[i] = tmap[c->tname[i]];
@@ -145,6 +149,49 @@ static void *pre_upload_thread(void *arg) {
             u->cs = NULL;
         free(ts);
         free(qs);
+    } else if (ok) { /* -nranks: the chains on this rank's target sides */
+        int32_t *remap = malloc((size_t)(c->n ? c->n : 1) * 4);
+        int64_t m = 0, mb = 0;
+        for (int64_t i = 0; i < c->n; ++i) {
+            remap[i] = -1;
+            if (u->tkeep[u->tix[i]] && tmap[c->tname[i]] >= 0) {
+                remap[i] = (int32_t)m++;
+                mb += c->blk_off[i + 1] - c->blk_off[i];
+            }
+        }
+        int32_t *ts = malloc((size_t)(m ? m : 1) * 4), *qs = malloc((size_t)(m ? m : 1) * 4);
+        uint8_t *st = malloc((size_t)(m ? m : 1));
+        int64_t *off = malloc((size_t)(m + 1) * 8), *src = malloc((size_t)(m ? m : 1) * 8);
+        int32_t *bt = malloc((size_t)(mb ? mb : 1) * 4), *bq = malloc((size_t)(mb ? mb : 1) * 4),
+                *bs = malloc((size_t)(mb ? mb : 1) * 4);
+        off[0] = 0;
+        for (int64_t i = 0; i < c->n; ++i)
+            if (remap[i] >= 0) {
+                const int64_t j = remap[i];
+                src[j] = i;
+                ts[j] = tmap[c->tname[i]];
+                qs[j] = qmap[c->qname[i]];
+                st[j] = c->qstrand[i];
+                off[j + 1] = off[j] + (c->blk_off[i + 1] - c->blk_off[i]);
+            }
+        subset_copy sj = {c, src, off, bt, bq, bs, m, 0};
+        atomic_init(&sj.next, 0);
+        gac_run_threads(gt_threads(), subset_copy_thread, &sj);
+        gac_chainset_desc d = {m, ts, qs, st, off, mb, bt, bq, bs};
+        if (gac_chains_upload(ctx, &d, &u->cs) != GAC_OK) {
+            u->cs = NULL;
+            free(remap);
+        } else {
+            u->remap = remap;
+        }
+        free(ts);
+        free(qs);
+        free(st);
+        free(off);
+        free(src);
+        free(bt);
+        free(bq);
+        free(bs);
     }
     free(tmap);
     free(qmap);
@@ -161,164 +208,114 @@ static void *pre_upload_thread(void *arg) {
  * rank 0 waits for every part and assembles each net in sequence order. */
 static gt_ranks g_rk;
 
-typedef struct side_job {
-    int side;
-    int32_t seq;
-    int64_t w;
-} side_job;
-
-static int side_job_cmp(const void *a, const void *b) {
-    const side_job *x = a, *y = b;
-    if (x->w != y->w)
-        return x->w > y->w ? -1 : 1;
-    if (x->side != y->side)
-        return x->side - y->side;
-    return (x->seq > y->seq) - (x->seq < y->seq);
-}
-
-/* keep[side][seq] for this rank; returns whether it owns a target side with
- * chains */
-static int assign_sides(const gt_chains *c, int64_t n_net, const int32_t *tix, const int32_t *qix,
-                        int32_t nt, int32_t nq, uint8_t *tkeep, uint8_t *qkeep) {
-    int64_t *wt = calloc((size_t)nt + 1, 8), *wq = calloc((size_t)nq + 1, 8);
-    for (int64_t i = 0; i < n_net; ++i) {
-        int64_t a = 0;
-        for (int64_t b = c->blk_off[i]; b < c->blk_off[i + 1]; ++b)
-            a += c->bs[b];
-        wt[tix[i]] += a + 1;
-        wq[qix[i]] += a + 1;
-    }
-    side_job *J = malloc((size_t)(nt + nq + 1) * sizeof(side_job));
-    int64_t nj = 0;
-    for (int32_t k = 0; k < nt; ++k)
-        if (wt[k])
-            J[nj++] = (side_job){GAC_T, k, wt[k]};
-    for (int32_t k = 0; k < nq; ++k)
-        if (wq[k])
-            J[nj++] = (side_job){GAC_Q, k, wq[k]};
-    qsort(J, (size_t)nj, sizeof(side_job), side_job_cmp);
-    int64_t *load = calloc((size_t)g_rk.n, 8);
-    memset(tkeep, 0, (size_t)nt);
-    memset(qkeep, 0, (size_t)nq);
-    int own_t = 0;
-    for (int64_t j = 0; j < nj; ++j) {
-        int best = 0;
-        for (int r = 1; r < g_rk.n; ++r)
-            if (load[r] < load[best])
-                best = r;
-        load[best] += J[j].w;
-        if (best == g_rk.me) {
-            if (J[j].side == GAC_T) {
-                tkeep[J[j].seq] = 1;
-                own_t = 1;
-            } else {
-                qkeep[J[j].seq] = 1;
-            }
+/* keep[k] for this rank: a contiguous run of the sizes file's sequences,
+ * runs balanced by sequence length (the same on every rank and known before
+ * the chains are read); kept names go to `kept` */
+static int assign_range(const gt_sizes *sz, uint8_t *keep, gt_names *kept) {
+    const int32_t n = sz->names.n;
+    int64_t total = 0, before = 0;
+    for (int32_t k = 0; k < n; ++k)
+        total += sz->size[k];
+    int any = 0;
+    memset(kept, 0, sizeof(*kept));
+    for (int32_t k = 0; k < n; ++k) {
+        /* the rank whose share of the length holds this sequence's middle */
+        int r = total > 0 ? (int)(((2 * before + sz->size[k]) * (int64_t)g_rk.n) / (2 * total)) : 0;
+        if (r >= g_rk.n)
+            r = g_rk.n - 1;
+        keep[k] = r == g_rk.me;
+        if (keep[k]) {
+            gt_names_add(kept, sz->names.names[k], strlen(sz->names.names[k]));
+            any = 1;
         }
+        before += sz->size[k];
     }
-    free(load);
-    free(J);
-    free(wt);
-    free(wq);
-    return own_t;
+    return any;
 }
 
-/* map a part file; sections[k] = "net" section of sequence k or empty */
-typedef struct part_map {
-    char *p;
-    size_t n;
-} part_map;
+/* rank 0: <net> = rank 0's '#' lines + every rank's part without its '#'
+ * lines, in rank order (the ranks hold contiguous runs of the sequences, and
+ * a part lists its sequences in order), copied in the kernel on one thread
+ * per part at precomputed offsets */
+typedef struct part_copy {
+    int in, out;
+    off_t from, to;
+    size_t len;
+    int err;
+} part_copy;
 
-static void map_part(const char *path, part_map *m) {
-    const int fd = open(path, O_RDONLY);
-    if (fd < 0)
-        gt_abort("Can't open %s to read: %s", path, strerror(errno));
-    struct stat st;
-    fstat(fd, &st);
-    m->n = (size_t)st.st_size;
-    m->p = m->n ? mmap(NULL, m->n, PROT_READ, MAP_PRIVATE, fd, 0) : NULL;
-    if (m->n && m->p == MAP_FAILED)
-        gt_abort("mmap %s failed", path);
-    close(fd);
+static void *part_copy_thread(void *arg) {
+    part_copy *p = arg;
+    off_t a = p->from, b = p->to;
+    size_t left = p->len;
+    while (left > 0) {
+        const ssize_t k = copy_file_range(p->in, &a, p->out, &b, left, 0);
+        if (k <= 0) {
+            p->err = k < 0 ? errno : EIO;
+            return NULL;
+        }
+        left -= (size_t)k;
+    }
+    return NULL;
 }
 
-/* rank 0: <net> = rank 0's '#' lines + every sequence's section, sequence
- * order, from the part of the rank that netted it */
-static void assemble_net(const char *net, const gt_names *names) {
-    part_map *pm = calloc((size_t)g_rk.n, sizeof(part_map));
+/* bytes of the leading '#' lines of a file */
+static size_t meta_len(int fd) {
+    char b[65536];
+    const ssize_t n = pread(fd, b, sizeof(b), 0);
+    size_t pos = 0;
+    while (n > 0 && pos < (size_t)n && b[pos] == '#') {
+        const char *nl = memchr(b + pos, '\n', (size_t)n - pos);
+        if (!nl)
+            gt_abort("chainNet: '#' line longer than %zu bytes in a part", sizeof(b));
+        pos = (size_t)(nl - b) + 1;
+    }
+    return pos;
+}
+
+static void assemble_net(const char *net) {
+    const int n = g_rk.n;
+    part_copy *pc = calloc((size_t)n, sizeof(part_copy));
+    pthread_t *th = calloc((size_t)n, sizeof(pthread_t));
     char b[4096];
-    for (int r = 0; r < g_rk.n; ++r) {
+    const int out = open(net, O_WRONLY | O_CREAT | O_TRUNC, 0666);
+    if (out < 0)
+        gt_abort("Can't open %s to write: %s", net, strerror(errno));
+    off_t pos = 0;
+    for (int r = 0; r < n; ++r) {
         gt_part_name(b, sizeof(b), net, r, "");
-        map_part(b, &pm[r]);
+        pc[r].in = open(b, O_RDONLY);
+        if (pc[r].in < 0)
+            gt_abort("Can't open %s to read: %s", b, strerror(errno));
+        struct stat st;
+        fstat(pc[r].in, &st);
+        const size_t m = meta_len(pc[r].in);
+        pc[r].from = r == 0 ? 0 : (off_t)m; /* rank 0's '#' lines head the net */
+        pc[r].len = (size_t)st.st_size - (size_t)pc[r].from;
+        pc[r].to = pos;
+        pc[r].out = out;
+        pos += (off_t)pc[r].len;
     }
-    /* section index: (start, end) per sequence */
-    const int32_t ns = names->n;
-    int64_t *sec = malloc((size_t)(ns ? ns : 1) * 2 * 8);
-    int32_t *own = malloc((size_t)(ns ? ns : 1) * 4);
-    for (int32_t k = 0; k < ns; ++k)
-        own[k] = -1;
-    size_t meta_end = 0;
-    for (int r = 0; r < g_rk.n; ++r) {
-        const char *p = pm[r].p;
-        const size_t n = pm[r].n;
-        size_t pos = 0;
-        while (pos < n && p[pos] == '#') { /* '#' lines (rank 0's are kept) */
-            const char *nl = memchr(p + pos, '\n', n - pos);
-            pos = nl ? (size_t)(nl - p) + 1 : n;
-        }
-        if (r == 0)
-            meta_end = pos;
-        int32_t cur = -1;
-        size_t cur0 = 0;
-        while (pos < n) {
-            const char *nl = memchr(p + pos, '\n', n - pos);
-            const size_t eol = nl ? (size_t)(nl - p) + 1 : n;
-            if (eol - pos > 4 && memcmp(p + pos, "net ", 4) == 0) {
-                if (cur >= 0) {
-                    sec[2 * cur] = (int64_t)cur0;
-                    sec[2 * cur + 1] = (int64_t)pos;
-                }
-                const char *nm = p + pos + 4;
-                const char *sp = memchr(nm, ' ', eol - pos - 4);
-                char name[1024];
-                const size_t len = sp ? (size_t)(sp - nm) : 0;
-                if (!len || len >= sizeof(name))
-                    gt_abort("chainNet: bad net line in part %d of %s", r, net);
-                memcpy(name, nm, len);
-                name[len] = 0;
-                cur = gt_names_find(names, name);
-                if (cur < 0 || own[cur] >= 0)
-                    gt_abort("chainNet: unexpected sequence %s in part %d of %s", name, r, net);
-                own[cur] = r;
-                cur0 = pos;
-            }
-            pos = eol;
-        }
-        if (cur >= 0) {
-            sec[2 * cur] = (int64_t)cur0;
-            sec[2 * cur + 1] = (int64_t)n;
-        }
-    }
-    FILE *f = gt_must_open(net, "w");
-    if (meta_end && fwrite(pm[0].p, 1, meta_end, f) != meta_end)
-        gt_abort("write error on %s", net);
-    for (int32_t k = 0; k < ns; ++k)
-        if (own[k] >= 0) {
-            const size_t len = (size_t)(sec[2 * k + 1] - sec[2 * k]);
-            if (fwrite(pm[own[k]].p + sec[2 * k], 1, len, f) != len)
-                gt_abort("write error on %s", net);
-        }
-    if (fclose(f) != 0)
-        gt_abort("close failed on %s", net);
-    for (int r = 0; r < g_rk.n; ++r) {
-        if (pm[r].n)
-            munmap(pm[r].p, pm[r].n);
+    if (ftruncate(out, pos) != 0)
+        gt_abort("can't size %s: %s", net, strerror(errno));
+    for (int r = 1; r < n; ++r)
+        if (pthread_create(&th[r], NULL, part_copy_thread, &pc[r]) != 0)
+            part_copy_thread(&pc[r]), th[r] = 0;
+    part_copy_thread(&pc[0]);
+    for (int r = 1; r < n; ++r)
+        if (th[r])
+            pthread_join(th[r], NULL);
+    for (int r = 0; r < n; ++r) {
+        if (pc[r].err)
+            gt_abort("write error on %s: %s", net, strerror(pc[r].err));
+        close(pc[r].in);
         gt_part_name(b, sizeof(b), net, r, "");
         unlink(b);
     }
-    free(pm);
-    free(sec);
-    free(own);
+    if (close(out) != 0)
+        gt_abort("close failed on %s", net);
+    free(pc);
+    free(th);
 }
 
 int main(int argc, char *argv[]) {
@@ -390,8 +387,25 @@ int main(int argc, char *argv[]) {
     if (qf != stdout)
         fclose(qf);
 
+    /* -nranks: this rank's chromosome sides (from the sizes files), the
+     * device with just its target sequences, and only the chains on its
+     * sides parsed in full */
+    uint8_t *tkeep = NULL, *qkeep = NULL;
+    gt_names tkept, qkept;
+    if (multi) {
+        tkeep = malloc((size_t)ts.names.n + 1);
+        qkeep = malloc((size_t)qs.names.n + 1);
+        const int own_t = assign_range(&ts, tkeep, &tkept);
+        assign_range(&qs, qkeep, &qkept);
+        if (rescore && own_t)
+            gt_device_start_keep(&dev, tnib, qnib, mat, gap, &tkept);
+        gt_stage("rank sides");
+    }
     gt_chains c;
-    gt_read_chains(chain_file, &c, min_score, 1);
+    if (multi)
+        gt_read_chains_keep(chain_file, &c, min_score, 1, &tkept, &qkept);
+    else
+        gt_read_chains(chain_file, &c, min_score, 1);
     gt_stage("read chains");
     int32_t *tix = malloc((c.n ? c.n : 1) * 4), *qix = malloc((c.n ? c.n : 1) * 4);
     double last = -1;
@@ -414,23 +428,13 @@ int main(int argc, char *argv[]) {
                      tsizes_file);
     }
     gt_stage("chain checks");
-    uint8_t *tkeep = NULL, *qkeep = NULL;
-    if (multi) {
-        int64_t n_net = 0; /* the netting loop stops at the first chain below minScore */
-        while (n_net < c.n && c.score[n_net] >= min_score)
-            ++n_net;
-        tkeep = malloc((size_t)ts.names.n + 1);
-        qkeep = malloc((size_t)qs.names.n + 1);
-        const int own_t = assign_sides(&c, n_net, tix, qix, ts.names.n, qs.names.n, tkeep, qkeep);
-        if (rescore && own_t)
-            gt_device_start(&dev, tnib, qnib, mat, gap);
-        gt_stage("rank sides");
-    }
     pre_upload pu;
     memset(&pu, 0, sizeof(pu));
     if (rescore && dev.started) {
         pu.dev = &dev;
         pu.c = &c;
+        pu.tkeep = tkeep;
+        pu.tix = tix;
         pu.started = pthread_create(&pu.th, NULL, pre_upload_thread, &pu) == 0;
         if (pu.started) /* gt_abort joins it before exiting */
             gt_helper_add(pu.th);
@@ -510,7 +514,19 @@ int main(int argc, char *argv[]) {
         tscores = calloc(nf ? nf : 1, 8);
         if (pu.started)
             gt_helper_join(pu.th);
-        if (nr && pu.cs) { /* the whole set is on the device: original chain indices */
+        if (pu.cs && pu.remap) { /* -nranks: the uploaded subset's indices */
+            int ok = 1;
+            for (int64_t k = 0; k < nr && ok; ++k)
+                ok = pu.remap[r[k].chain] >= 0;
+            if (ok) {
+                for (int64_t k = 0; k < nr; ++k)
+                    r[k].chain = pu.remap[r[k].chain];
+            } else { /* (cannot happen: every fill's chain is on a kept side) */
+                gac_chains_free(pu.cs);
+                pu.cs = NULL;
+            }
+        }
+        if (nr && pu.cs) { /* the chain set is on the device */
             gt_stage("fill list");
             gac_ctx *ctx = gt_device_join(&dev);
             gt_stage("device open + 2bit genomes + chains to HBM (rest)");
@@ -626,8 +642,8 @@ int main(int argc, char *argv[]) {
             gt_ranks_wait(&g_rk, tnet);
             gt_ranks_wait(&g_rk, qnet);
             gt_stage("wait for ranks");
-            assemble_net(tnet, &ts.names);
-            assemble_net(qnet, &qs.names);
+            assemble_net(tnet);
+            assemble_net(qnet);
             gt_stage("assemble nets");
         }
     }

@@ -148,10 +148,17 @@ static void *device_thread(void *arg) {
             snprintf(d->err, sizeof(d->err), "%s", P.err[k]);
             d->rc_err_set = 1;
         }
+        uint8_t *keep = NULL;
+        if (rc == GAC_OK && k == 0 && d->tkeep) {
+            keep = malloc(P.tb[k].seq_count + 1);
+            for (uint32_t i = 0; i < P.tb[k].seq_count; ++i)
+                keep[i] = gt_names_find(d->tkeep, P.tb[k].seqs[i].name) >= 0;
+        }
         if (rc == GAC_OK)
-            rc = gac_genome_load_twobit(d->ctx, k == 0 ? GAC_T : GAC_Q, &P.tb[k]);
+            rc = gac_genome_load_twobit_keep(d->ctx, k == 0 ? GAC_T : GAC_Q, &P.tb[k], keep);
         else if (P.rc[k] == GAC_OK)
             gac_twobit_close(&P.tb[k]);
+        free(keep);
     }
     d->load_s = now_s() - t0 - d->open_s;
     if (rc != GAC_OK && !d->rc_err_set) /* the error text is thread-local */
@@ -166,7 +173,13 @@ static void *device_thread(void *arg) {
 
 void gt_device_start(gt_device *d, const char *t2bit, const char *q2bit, const int32_t mat[16],
                      const gac_gapcalc *gap) {
+    gt_device_start_keep(d, t2bit, q2bit, mat, gap, NULL);
+}
+
+void gt_device_start_keep(gt_device *d, const char *t2bit, const char *q2bit,
+                          const int32_t mat[16], const gac_gapcalc *gap, const gt_names *tkeep) {
     memset(d, 0, sizeof(*d));
+    d->tkeep = tkeep;
     d->t2bit = t2bit;
     d->q2bit = q2bit;
     d->mat = mat;
@@ -941,7 +954,32 @@ typedef struct chunk {
     int64_t lines;     /* newlines in the chunk */
     int64_t err_line;  /* local line of the error */
     double stop_below;
+    const gt_names *tkeep, *qkeep; /* gt_read_chains_keep: NULL = keep all */
 } chunk;
+
+/* gt_read_chains_keep: the blocks of a chain on neither kept side are
+ * skipped to the next "chain" header line of the chunk when only block lines
+ * lie between (no '#' line, which is metadata, and a header follows); 1 =
+ * skipped, 0 = parse them normally */
+static int skip_blocks(lf *f) {
+    const char *s = f->cur, *end = f->end;
+    int64_t lines = 0;
+    while (s < end) {
+        if (*s == '#')
+            return 0;
+        const char *nl = memchr(s, '\n', (size_t)(end - s));
+        if (!nl)
+            return 0;
+        ++lines;
+        s = nl + 1;
+        if (end - s >= 6 && memcmp(s, "chain", 5) == 0 && (s[5] == ' ' || s[5] == '\t')) {
+            f->cur = (char *)s;
+            f->line += lines;
+            return 1;
+        }
+    }
+    return 0;
+}
 
 /* Fast path for the common block line "size[\tdt\tdq]\n" (decimal fields of
  * at most 9 digits, one tab apart): 1 = parsed into v[0..*bw), 0 = anything
@@ -1018,6 +1056,17 @@ static int parse_chain(chunk *k) {
         LF_FAIL(f, "Start before zero line \001 of \002");
     if (c->qend[i] > c->qsize[i] || c->tend[i] > c->tsize[i])
         LF_FAIL(f, "Past end of sequence line \001 of \002");
+    if (k->tkeep && gt_names_find(k->tkeep, c->tnames.names[c->tname[i]]) < 0 &&
+        gt_names_find(k->qkeep, c->qnames.names[c->qname[i]]) < 0 && skip_blocks(f)) {
+        /* on no side this process nets: header only, no blocks */
+        c->n++;
+        c->blk_off[c->n] = c->nb;
+        if (c->score[i] < k->stop_below) {
+            k->stop = i;
+            return 1;
+        }
+        return 0;
+    }
     /* chainReadBlocks (chain.c:301-335) */
     int q = c->qstart[i], t = c->tstart[i];
     for (;;) {
@@ -1163,7 +1212,20 @@ static void *stitch_thread(void *arg) {
     return NULL;
 }
 
+static void read_chains(const char *path, gt_chains *c, double stop_below, int keep_meta,
+                        const gt_names *tkeep, const gt_names *qkeep);
+
 void gt_read_chains(const char *path, gt_chains *c, double stop_below, int keep_meta) {
+    read_chains(path, c, stop_below, keep_meta, NULL, NULL);
+}
+
+void gt_read_chains_keep(const char *path, gt_chains *c, double stop_below, int keep_meta,
+                         const gt_names *tkeep, const gt_names *qkeep) {
+    read_chains(path, c, stop_below, keep_meta, tkeep, qkeep);
+}
+
+static void read_chains(const char *path, gt_chains *c, double stop_below, int keep_meta,
+                        const gt_names *tkeep, const gt_names *qkeep) {
     memset(c, 0, sizeof(*c));
     const int timing = getenv("GAC_TIMING") != NULL;
     double t_mark = now_s();
@@ -1208,6 +1270,8 @@ void gt_read_chains(const char *path, gt_chains *c, double stop_below, int keep_
         K[k].f = (lf){cut[k], cut[k + 1], path, 0, keep_meta ? &K[k].c : NULL, 0, {0}};
         K[k].stop = -1;
         K[k].stop_below = stop_below;
+        K[k].tkeep = tkeep;
+        K[k].qkeep = qkeep;
         NL[k] = (nl_job){cut[k], cut[k + 1], 0};
     }
     RC_LAP("cut");

@@ -52,9 +52,14 @@ typedef struct gt_device {
     int done;
     unsigned long close_th;
     int closing;
+    const struct gt_names *tkeep; /* target sequences to load (NULL: all); -nranks */
 } gt_device;
 void gt_device_start(gt_device *d, const char *t2bit, const char *q2bit, const int32_t mat[16],
                      const gac_gapcalc *gap);
+/* the same, loading only the target sequences named in tkeep */
+void gt_device_start_keep(gt_device *d, const char *t2bit, const char *q2bit,
+                          const int32_t mat[16], const gac_gapcalc *gap,
+                          const struct gt_names *tkeep);
 /* main thread only */
 gac_ctx *gt_device_join(gt_device *d);
 /* the same wait without the abort: NULL if the bring-up failed.  Safe from
@@ -170,6 +175,12 @@ typedef struct gt_chains {
  * (that chain is read, like chainNet's loop, but not kept); pass -HUGE_VAL
  * to read everything.  Reads .gz transparently, "stdin" allowed. */
 void gt_read_chains(const char *path, gt_chains *c, double stop_below, int keep_meta);
+/* Same, but a chain whose target name is not in tkeep and whose query name is
+ * not in qkeep keeps its header only (no blocks; its block lines are not
+ * parsed): chainNet -nranks, where a rank nets some chromosome sides.  Ids,
+ * the minScore stop, '#' lines and header errors are as for every chain. */
+void gt_read_chains_keep(const char *path, gt_chains *c, double stop_below, int keep_meta,
+                         const gt_names *tkeep, const gt_names *qkeep);
 void gt_chains_free(gt_chains *c);
 /* chainIdNext (chain.c:180-198): the shared "next id" counter */
 int gt_next_chain_id(void);

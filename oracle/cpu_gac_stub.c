@@ -66,6 +66,11 @@ int gac_genome_load_2bit(gac_ctx *c, int which, const char *path) {
     return gac_genome_load_twobit(c, which, &tb);
 }
 
+int gac_genome_load_twobit_keep(gac_ctx *c, int which, gac_twobit *tb, const uint8_t *keep) {
+    (void)keep; /* the axtChain front end loads whole files */
+    return gac_genome_load_twobit(c, which, tb);
+}
+
 /* the file is already open (the tools map it while the device starts) */
 int gac_genome_load_twobit(gac_ctx *c, int which, gac_twobit *tb) {
     side *s = &c->s[which];
