@@ -483,13 +483,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    if os.environ.get("GAC_BENCH_ONE_GPU"):  # rehearsal on a one-GPU box: every rank on device 0
+        local = 0
+        os.environ["LOCAL_RANK"] = "0"
     if world > 1:
         import torch
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world,
-                                device_id=torch.device(f"cuda:{local}"))
+        if os.environ.get("GAC_BENCH_ONE_GPU"):  # (RCCL wants one device per rank)
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world,
+                                    device_id=torch.device(f"cuda:{local}"))
 
     def barrier():
         if dist is not None:
@@ -508,22 +514,32 @@ def main():
     outs = [out_base + ".t.net", out_base + ".q.net"]
     cmd = tool_cmd(d, out_base, world, rank)
 
+    # every rank of one step shares a marker token (tells this step's part
+    # markers from an earlier, failed one's; see gt_ranks_place)
+    run_id = f"{os.environ.get('TORCHELASTIC_RUN_ID', 'x')}-{os.environ.get('MASTER_PORT', '0')}"
+    step_no = [0]
+
+    def step_env():
+        step_no[0] += 1
+        return dict(os.environ, GAC_RANK_TOKEN=f"{run_id}-{step_no[0]}")
+
     if args.workload == "chainnet":
         for _ in range(args.warmup):
             barrier()
-            run_tool(cmd, outs if rank == 0 else [])
+            run_tool(cmd, outs if rank == 0 else [], env=step_env())
         barrier()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            run_tool(cmd, outs if rank == 0 else [])
-            barrier()  # rank 0 finishes last (it assembles the nets)
+            run_tool(cmd, outs if rank == 0 else [], env=step_env())
+            barrier()  # rank 0 finishes last (it waits for every part)
         dt = time.perf_counter() - t0
         if dist is not None:
             from genomealignmenttools_amd.shard import reduce_time_and_work
-            dt, _ = reduce_time_and_work(dist, dt, 0.0, device=f"cuda:{local}")
+            dev = "cpu" if os.environ.get("GAC_BENCH_ONE_GPU") else f"cuda:{local}"
+            dt, _ = reduce_time_and_work(dist, dt, 0.0, device=dev)
         step_s = dt / args.steps
         stages = None
-        if rank == 0:  # one more, untimed run for the per-stage breakdown
+        if world == 1:  # one more, untimed run for the per-stage breakdown
             r = run_tool(cmd + ["-verbose=2"], outs)
             stages = [line.strip() for line in r.stderr.splitlines() if "[stage]" in line]
         out = {

@@ -2102,6 +2102,9 @@ static void *wmore_thread(void *arg) {
     return NULL;
 }
 
+static int net_write_f(const gac_net *n, int side, const int64_t *tscores, FILE *f,
+                       const char *const *meta, int32_t n_meta);
+
 int gac_net_write(const gac_net *n, int side, const int64_t *tscores, const char *path,
                   const char *const *meta, int32_t n_meta) {
     if (!n || !path || (side != GAC_T && side != GAC_Q))
@@ -2118,6 +2121,31 @@ int gac_net_write(const gac_net *n, int side, const int64_t *tscores, const char
         if (!f)
             return gac_fail(GAC_E_IO, "Can't open %s to write", path);
     }
+    int bad = net_write_f(n, side, tscores, f, meta, n_meta) != GAC_OK;
+    if (close_it) {
+        if (fclose(f) != 0)
+            bad = 1;
+    } else {
+        fflush(f);
+    }
+    if (bad)
+        return gac_fail(GAC_E_IO, "write error on %s", path);
+    return GAC_OK;
+}
+
+int gac_net_write_file(const gac_net *n, int side, const int64_t *tscores, FILE *f,
+                       const char *const *meta, int32_t n_meta) {
+    if (!n || !f || (side != GAC_T && side != GAC_Q))
+        return gac_fail(GAC_E_ARG, "gac_net_write_file: bad argument");
+    if (!(n->sides & (1 << side)))
+        return gac_fail(GAC_E_STATE, "gac_net_write_file: side %d was not netted", side);
+    if (net_write_f(n, side, tscores, f, meta, n_meta) != GAC_OK || fflush(f) != 0)
+        return gac_fail(GAC_E_IO, "write error");
+    return GAC_OK;
+}
+
+static int net_write_f(const gac_net *n, int side, const int64_t *tscores, FILE *f,
+                       const char *const *meta, int32_t n_meta) {
     for (int32_t i = 0; i < n_meta; ++i)
         fprintf(f, "%s\n", meta[i]);
     const int64_t nf = n->n_order[side];
@@ -2156,14 +2184,5 @@ int gac_net_write(const gac_net *n, int side, const int64_t *tscores, const char
     free(J.show);
     free(J.more);
     free(J.reached);
-    int bad = ferror(f) || wbad;
-    if (close_it) {
-        if (fclose(f) != 0)
-            bad = 1;
-    } else {
-        fflush(f);
-    }
-    if (bad)
-        return gac_fail(GAC_E_IO, "write error on %s", path);
-    return GAC_OK;
+    return (ferror(f) || wbad) ? GAC_E_IO : GAC_OK;
 }

@@ -58,8 +58,8 @@ static void usage(int min_space, double min_score) {
         "   -scoreScheme=fileName       Read the scoring matrix from a blastz-format file\n"
         "   -linearGap=<medium|loose|filename> Specify type of linearGap to use.\n"
         "   -nranks=N -rank=R           multi-GPU run (one process per GPU, same node): rank R\n"
-        "                               nets its share of the chromosome sides; rank 0 writes\n"
-        "                               both nets once every rank's part is done\n"
+        "                               nets its share of the chromosome sides and writes its\n"
+        "                               part of both nets in place; rank 0 waits for all parts\n"
         "   -gpu=D                      device index (default: R with -nranks, else 0)\n",
         min_space, min_score);
 }
@@ -74,8 +74,30 @@ typedef struct net_out {
     char err[1024];
 } net_out;
 
+static gt_ranks g_rk;
+
 static void *write_net(void *arg) {
     net_out *w = arg;
+    if (g_rk.n > 1) {
+        /* -nranks: this rank's part formatted in memory and written in place
+         * (rank 0's part carries the '#' lines) */
+        char *buf = NULL;
+        size_t len = 0;
+        FILE *mf = open_memstream(&buf, &len);
+        const int m = g_rk.me == 0;
+        w->rc = mf ? gac_net_write_file(w->net, w->side, w->tscores, mf,
+                                        m ? (const char *const *)w->c->meta : NULL,
+                                        m ? w->c->n_meta : 0)
+                   : GAC_E_IO;
+        if (mf && fclose(mf) != 0 && w->rc == GAC_OK)
+            w->rc = GAC_E_IO;
+        if (w->rc == GAC_OK)
+            gt_ranks_place(&g_rk, w->path, buf, len);
+        else
+            snprintf(w->err, sizeof(w->err), "write error on %s", w->path);
+        free(buf);
+        return NULL;
+    }
     w->rc = gac_net_write(w->net, w->side, w->tscores, w->path, (const char *const *)w->c->meta,
                           w->c->n_meta);
     if (w->rc != GAC_OK) /* thread-local error text */
@@ -203,11 +225,11 @@ static void *pre_upload_thread(void *arg) {
  * -nranks=N -rank=R: N processes (one per GPU of one node) run the same
  * command.  A chromosome side's net depends only on the chains on that
  * sequence (chainNet.c:557-679 add each chain to its own target and query
- * trees), so the sides are dealt out to the ranks (LPT on aligned bases);
- * rank R nets and rescores its sides and writes them to <net>.gacpart<R>;
- * rank 0 waits for every part and assembles each net in sequence order. */
-static gt_ranks g_rk;
-
+ * trees), so each rank takes a contiguous run of the target and of the
+ * query sequences (assign_range); the sequences' sections of a net are in
+ * sizes-file order, so rank R's part of each net is one contiguous piece of
+ * it: rank R formats it in memory and writes it in place once the lower
+ * ranks' sizes are known (gt_ranks_place); rank 0 waits for all parts. */
 /* keep[k] for this rank: a contiguous run of the sizes file's sequences,
  * runs balanced by sequence length (the same on every rank and known before
  * the chains are read); kept names go to `kept` */
@@ -231,91 +253,6 @@ static int assign_range(const gt_sizes *sz, uint8_t *keep, gt_names *kept) {
         before += sz->size[k];
     }
     return any;
-}
-
-/* rank 0: <net> = rank 0's '#' lines + every rank's part without its '#'
- * lines, in rank order (the ranks hold contiguous runs of the sequences, and
- * a part lists its sequences in order), copied in the kernel on one thread
- * per part at precomputed offsets */
-typedef struct part_copy {
-    int in, out;
-    off_t from, to;
-    size_t len;
-    int err;
-} part_copy;
-
-static void *part_copy_thread(void *arg) {
-    part_copy *p = arg;
-    off_t a = p->from, b = p->to;
-    size_t left = p->len;
-    while (left > 0) {
-        const ssize_t k = copy_file_range(p->in, &a, p->out, &b, left, 0);
-        if (k <= 0) {
-            p->err = k < 0 ? errno : EIO;
-            return NULL;
-        }
-        left -= (size_t)k;
-    }
-    return NULL;
-}
-
-/* bytes of the leading '#' lines of a file */
-static size_t meta_len(int fd) {
-    char b[65536];
-    const ssize_t n = pread(fd, b, sizeof(b), 0);
-    size_t pos = 0;
-    while (n > 0 && pos < (size_t)n && b[pos] == '#') {
-        const char *nl = memchr(b + pos, '\n', (size_t)n - pos);
-        if (!nl)
-            gt_abort("chainNet: '#' line longer than %zu bytes in a part", sizeof(b));
-        pos = (size_t)(nl - b) + 1;
-    }
-    return pos;
-}
-
-static void assemble_net(const char *net) {
-    const int n = g_rk.n;
-    part_copy *pc = calloc((size_t)n, sizeof(part_copy));
-    pthread_t *th = calloc((size_t)n, sizeof(pthread_t));
-    char b[4096];
-    const int out = open(net, O_WRONLY | O_CREAT | O_TRUNC, 0666);
-    if (out < 0)
-        gt_abort("Can't open %s to write: %s", net, strerror(errno));
-    off_t pos = 0;
-    for (int r = 0; r < n; ++r) {
-        gt_part_name(b, sizeof(b), net, r, "");
-        pc[r].in = open(b, O_RDONLY);
-        if (pc[r].in < 0)
-            gt_abort("Can't open %s to read: %s", b, strerror(errno));
-        struct stat st;
-        fstat(pc[r].in, &st);
-        const size_t m = meta_len(pc[r].in);
-        pc[r].from = r == 0 ? 0 : (off_t)m; /* rank 0's '#' lines head the net */
-        pc[r].len = (size_t)st.st_size - (size_t)pc[r].from;
-        pc[r].to = pos;
-        pc[r].out = out;
-        pos += (off_t)pc[r].len;
-    }
-    if (ftruncate(out, pos) != 0)
-        gt_abort("can't size %s: %s", net, strerror(errno));
-    for (int r = 1; r < n; ++r)
-        if (pthread_create(&th[r], NULL, part_copy_thread, &pc[r]) != 0)
-            part_copy_thread(&pc[r]), th[r] = 0;
-    part_copy_thread(&pc[0]);
-    for (int r = 1; r < n; ++r)
-        if (th[r])
-            pthread_join(th[r], NULL);
-    for (int r = 0; r < n; ++r) {
-        if (pc[r].err)
-            gt_abort("write error on %s: %s", net, strerror(pc[r].err));
-        close(pc[r].in);
-        gt_part_name(b, sizeof(b), net, r, "");
-        unlink(b);
-    }
-    if (close(out) != 0)
-        gt_abort("close failed on %s", net);
-    free(pc);
-    free(th);
 }
 
 int main(int argc, char *argv[]) {
@@ -362,7 +299,8 @@ int main(int argc, char *argv[]) {
     if (multi) {
         if (!strcmp(tnet, "stdout") || !strcmp(qnet, "stdout"))
             gt_abort("-nranks needs file names for both nets (not stdout)");
-        gt_ranks_clear(&g_rk, qnet);
+        gt_ranks_clear_markers(&g_rk, tnet);
+        gt_ranks_clear_markers(&g_rk, qnet);
     }
 
     /* with -rescore the device and both genomes come up on a helper thread
@@ -379,13 +317,24 @@ int main(int argc, char *argv[]) {
     gt_read_sizes(tsizes_file, &ts);
     gt_verbose(1, "Got %d chroms in %s, %d in %s\n", ts.names.n, tsizes_file, qs.names.n,
                qsizes_file);
-    /* open outputs like mustOpen before reading */
-    FILE *tf = gt_must_open(tnet, "w");
-    FILE *qf = gt_must_open(qnet, "w");
-    if (tf != stdout)
-        fclose(tf);
-    if (qf != stdout)
-        fclose(qf);
+    /* open outputs like mustOpen before reading (with -nranks only rank 0
+     * truncates them: the other ranks write their parts in place later) */
+    if (!multi || g_rk.me == 0) {
+        FILE *tf = gt_must_open(tnet, "w");
+        FILE *qf = gt_must_open(qnet, "w");
+        if (tf != stdout)
+            fclose(tf);
+        if (qf != stdout)
+            fclose(qf);
+    } else {
+        for (int k = 0; k < 2; ++k) {
+            const char *o = k ? qnet : tnet;
+            const int fd = open(o, O_WRONLY | O_CREAT, 0666);
+            if (fd < 0)
+                gt_abort("Can't open %s to write: %s", o, strerror(errno));
+            close(fd);
+        }
+    }
 
     /* -nranks: this rank's chromosome sides (from the sizes files), the
      * device with just its target sequences, and only the chains on its
@@ -476,15 +425,7 @@ int main(int argc, char *argv[]) {
      * complete) */
     gt_verbose(1, "writing %s\n", tnet);
     gt_verbose(1, "writing %s\n", qnet);
-    char tpart[4096], qpart[4096], tpart_tmp[4096], qpart_tmp[4096];
-    if (multi) {
-        gt_part_name(tpart, sizeof(tpart), tnet, g_rk.me, "");
-        gt_part_name(qpart, sizeof(qpart), qnet, g_rk.me, "");
-        gt_part_name(tpart_tmp, sizeof(tpart_tmp), tnet, g_rk.me, ".tmp");
-        gt_part_name(qpart_tmp, sizeof(qpart_tmp), qnet, g_rk.me, ".tmp");
-    }
-    net_out wo[2] = {{net, GAC_T, NULL, multi ? tpart_tmp : tnet, &c, 0, 0},
-                     {net, GAC_Q, NULL, multi ? qpart_tmp : qnet, &c, 0, 0}};
+    net_out wo[2] = {{net, GAC_T, NULL, tnet, &c, 0, 0}, {net, GAC_Q, NULL, qnet, &c, 0, 0}};
     pthread_t qth;
     if (pthread_create(&qth, NULL, write_net, &wo[1]) != 0) {
         write_net(&wo[1]);
@@ -635,17 +576,10 @@ int main(int argc, char *argv[]) {
         if (wo[k].rc != GAC_OK)
             gt_abort("%s\n", wo[k].err);
     gt_stage("write nets");
-    if (multi) {
-        if (rename(qpart_tmp, qpart) != 0 || rename(tpart_tmp, tpart) != 0)
-            gt_abort("can't rename %s: %s", tpart_tmp, strerror(errno));
-        if (g_rk.me == 0) {
-            gt_ranks_wait(&g_rk, tnet);
-            gt_ranks_wait(&g_rk, qnet);
-            gt_stage("wait for ranks");
-            assemble_net(tnet);
-            assemble_net(qnet);
-            gt_stage("assemble nets");
-        }
+    if (multi && g_rk.me == 0) {
+        gt_ranks_finish(&g_rk, tnet);
+        gt_ranks_finish(&g_rk, qnet);
+        gt_stage("wait for ranks");
     }
     gt_device_close_join(&dev);
     gt_stage("device close (rest)");

@@ -368,6 +368,103 @@ void gt_ranks_wait(const gt_ranks *rk, const char *path) {
     }
 }
 
+/* ---- positioned parts (chainNet -nranks): every rank writes its part of
+ * an output straight into the final file.  Markers next to the output:
+ * "<path>.gacsize<r>" = "<token> <bytes>", published once rank r's part is
+ * formatted (rank 0 publishes only after truncating the file at startup),
+ * and "<path>.gacdone<r>" once written.  Rank r writes at the sum of the
+ * sizes of ranks < r; rank 0 waits for every done marker and removes the
+ * markers.  The token (GAC_RANK_TOKEN, default "0") tells this run's
+ * markers from a failed earlier run's. */
+static const char *rank_token(void) {
+    const char *t = getenv("GAC_RANK_TOKEN");
+    return t && *t ? t : "0";
+}
+
+static void marker_name(char *b, size_t cap, const char *path, const char *what, int r) {
+    snprintf(b, cap, "%s.gac%s%d", path, what, r);
+}
+
+static void put_marker(const char *path, const char *what, int r, long long v) {
+    char b[4096], t[4200];
+    marker_name(b, sizeof(b), path, what, r);
+    snprintf(t, sizeof(t), "%s.tmp", b);
+    FILE *f = fopen(t, "w");
+    if (!f || fprintf(f, "%s %lld\n", rank_token(), v) < 0 || fclose(f) != 0 || rename(t, b) != 0)
+        gt_abort("can't write %s: %s", b, strerror(errno));
+}
+
+/* the value of rank r's marker of this run, waiting for it */
+static long long get_marker(const gt_ranks *rk, const char *path, const char *what, int r) {
+    const char *lim = getenv("GAC_RANK_TIMEOUT");
+    const double limit = lim ? atof(lim) : 3600.0, t0 = now_s();
+    struct timespec nap = {0, 200000};
+    char b[4096], fl[4096], tok[256];
+    marker_name(b, sizeof(b), path, what, r);
+    gt_part_name(fl, sizeof(fl), rk->key, r, ".failed");
+    for (;;) {
+        FILE *f = fopen(b, "r");
+        if (f) {
+            long long v;
+            const int ok = fscanf(f, "%255s %lld", tok, &v) == 2 && strcmp(tok, rank_token()) == 0;
+            fclose(f);
+            if (ok)
+                return v;
+        }
+        if (access(fl, F_OK) == 0) {
+            unlink(fl);
+            gt_abort("%s: rank %d failed", path, r);
+        }
+        if (now_s() - t0 > limit)
+            gt_abort("%s: timed out waiting for rank %d", path, r);
+        nanosleep(&nap, NULL);
+    }
+}
+
+void gt_ranks_clear_markers(const gt_ranks *rk, const char *path) {
+    char b[4096];
+    marker_name(b, sizeof(b), path, "size", rk->me);
+    unlink(b);
+    marker_name(b, sizeof(b), path, "done", rk->me);
+    unlink(b);
+}
+
+void gt_ranks_place(const gt_ranks *rk, const char *path, const char *buf, size_t len) {
+    put_marker(path, "size", rk->me, (long long)len);
+    off_t off = 0;
+    for (int r = 0; r < rk->me; ++r)
+        off += (off_t)get_marker(rk, path, "size", r);
+    const int fd = open(path, O_WRONLY | O_CREAT, 0666);
+    if (fd < 0)
+        gt_abort("Can't open %s to write: %s", path, strerror(errno));
+    for (size_t done = 0; done < len;) {
+        const ssize_t k = pwrite(fd, buf + done, len - done, off + (off_t)done);
+        if (k <= 0)
+            gt_abort("write error on %s: %s", path, strerror(errno));
+        done += (size_t)k;
+    }
+    if (close(fd) != 0)
+        gt_abort("close failed on %s", path);
+    put_marker(path, "done", rk->me, 1);
+}
+
+void gt_ranks_finish(const gt_ranks *rk, const char *path) {
+    off_t total = 0;
+    for (int r = 0; r < rk->n; ++r) {
+        total += (off_t)get_marker(rk, path, "size", r);
+        get_marker(rk, path, "done", r);
+    }
+    if (truncate(path, total) != 0)
+        gt_abort("can't size %s: %s", path, strerror(errno));
+    char b[4096];
+    for (int r = 0; r < rk->n; ++r) {
+        marker_name(b, sizeof(b), path, "size", r);
+        unlink(b);
+        marker_name(b, sizeof(b), path, "done", r);
+        unlink(b);
+    }
+}
+
 void gt_ranks_append_parts(const gt_ranks *rk, const char *path, FILE *f) {
     char b[4096];
     char *buf = malloc(1 << 22);

@@ -100,6 +100,13 @@ void gt_part_name(char *buf, size_t cap, const char *path, int r, const char *su
 void gt_ranks_wait(const gt_ranks *rk, const char *path);
 /* rank 0: append <path>.gacpart<r>, r = 1..n-1, to f, then remove them */
 void gt_ranks_append_parts(const gt_ranks *rk, const char *path, FILE *f);
+/* positioned parts: this rank's part of `path` (len bytes) written in place
+ * at the sum of the lower ranks' sizes (rank 0 must have truncated `path`
+ * before it calls this); rank 0 then waits for all parts (gt_ranks_finish).
+ * gt_ranks_clear_markers removes this rank's stale markers at startup. */
+void gt_ranks_clear_markers(const gt_ranks *rk, const char *path);
+void gt_ranks_place(const gt_ranks *rk, const char *path, const char *buf, size_t len);
+void gt_ranks_finish(const gt_ranks *rk, const char *path);
 
 /* ---- options ---- */
 enum { GT_BOOL, GT_INT, GT_DOUBLE, GT_STRING };

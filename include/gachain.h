@@ -36,6 +36,7 @@
 
 #include <stddef.h>
 #include <stdint.h>
+#include <stdio.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -333,6 +334,10 @@ int gac_net_get_fills(const gac_net *net, int side, int32_t *chain, int32_t *sta
  * (<= 0 prints as 1); NULL = reference's proportional approximation. */
 int gac_net_write(const gac_net *net, int side, const int64_t *t_scores, const char *path,
                   const char *const *meta, int32_t n_meta);
+/* The same text written to an open stream (e.g. an open_memstream buffer:
+ * chainNet -nranks formats a rank's part in memory, then writes it in place). */
+int gac_net_write_file(const gac_net *net, int side, const int64_t *t_scores, FILE *f,
+                       const char *const *meta, int32_t n_meta);
 
 /* ---- device memory helpers (for callers without their own allocator) ---- */
 int gac_dev_alloc(gac_ctx *ctx, size_t bytes, void **dptr);

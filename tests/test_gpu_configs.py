@@ -163,7 +163,7 @@ def test_c5_shaped_chainnet_rescore_ranks(c5_dir, c5_ref_nets, nranks):
         assert pr.returncode == 0, (r, err[-2000:])
     _same(p(f"{tag}.t.net"), c5_ref_nets[0])
     _same(p(f"{tag}.q.net"), c5_ref_nets[1])
-    assert not [f for f in os.listdir(c5_dir) if ".gacpart" in f]
+    assert not [f for f in os.listdir(c5_dir) if ".gacsize" in f or ".gacdone" in f]
 
 
 # ---------------------------------------------------------------- C2

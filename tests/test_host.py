@@ -345,7 +345,7 @@ def test_chainnet_ranks_vs_reference(nranks, tmp_path):
     for pr in procs:
         _, err = pr.communicate(timeout=120)
         assert pr.returncode == 0, err
-    assert not [f for f in os.listdir(d) if ".gacpart" in f]
+    assert not [f for f in os.listdir(d) if ".gac" in f]  # no part or marker files left
     r = subprocess.run([os.path.join(BIN_DIR, "chainNet")] + args +
                        [p("one.t.net"), p("one.q.net"), "-minScore=0"], capture_output=True)
     assert r.returncode == 0
