@@ -28,8 +28,10 @@ HDRS     := include/gachain.h $(CSRC)/gac_kernels.h $(CSRC)/gac_dp.h $(wildcard 
 EXECDIR  := $(PKG)/libexec
 # GPU tools: the binary lives in libexec/, bin/<tool> is a 2-line sh launcher
 # that turns on transparent huge pages for malloc (glibc.malloc.hugetlb=1:
-# fewer page faults on the GB-scale chain/net arrays) and execs it -- before
-# anything touches the GPU.  NetFilterNonNested.perl is host-only: in bin/.
+# fewer page faults on the GB-scale chain/net arrays) and host->device copies
+# by blit kernels instead of the SDMA engines (HSA_ENABLE_SDMA=0: 20 vs 13
+# GB/s for the genome uploads on the box, profiles/r02f_*), and execs it --
+# before anything touches the GPU.  Either can be overridden from outside.  NetFilterNonNested.perl is host-only: in bin/.
 GPU_TOOLS := scoreChain chainNet chainCleaner axtChain
 HOST_TOOLS := NetFilterNonNested.perl chainSort chainMergeSort
 TOOLS    := $(addprefix $(EXECDIR)/,$(GPU_TOOLS)) $(addprefix $(BINDIR)/,$(GPU_TOOLS)) \
@@ -78,7 +80,7 @@ $(BINDIR)/chainSort $(BINDIR)/chainMergeSort: $(BINDIR)/%: $(CSRC)/tools/%.c $(T
 
 $(BINDIR)/%: $(EXECDIR)/%
 	@mkdir -p $(BINDIR)
-	printf '#!/bin/sh\np=$$(readlink -f "$$0")\nGLIBC_TUNABLES="glibc.malloc.hugetlb=1$${GLIBC_TUNABLES:+:$$GLIBC_TUNABLES}" exec "$${p%%/*}/../libexec/%s" "$$@"\n' $* > $@
+	printf '#!/bin/sh\np=$$(readlink -f "$$0")\nHSA_ENABLE_SDMA=$${HSA_ENABLE_SDMA:-0} GLIBC_TUNABLES="glibc.malloc.hugetlb=1$${GLIBC_TUNABLES:+:$$GLIBC_TUNABLES}" exec "$${p%%/*}/../libexec/%s" "$$@"\n' $* > $@
 	chmod +x $@
 
 oracle: oracle/_build/libgacoracle.so

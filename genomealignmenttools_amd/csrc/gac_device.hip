@@ -461,7 +461,12 @@ extern "C" int gac_genome_add_seq(gac_ctx *c, int side, const char *name, int32_
 // Staged upload of the packed payloads to d_raw (layout: seqs[i].byte_off,
 // 8-byte aligned): host threads copy 32 MB windows into two alternating
 // pinned buffers while the previous window's DMA runs.
-constexpr size_t kPinBytes = 32u << 20;
+// (GAC_PIN_MB overrides the window size: measurement knob)
+static size_t pin_bytes() {
+    static const size_t b = getenv("GAC_PIN_MB") ? (size_t)std::max(1, atoi(getenv("GAC_PIN_MB"))) << 20
+                                                  : (size_t)32 << 20;
+    return b;
+}
 
 struct StageJob {
     const Genome *g;
@@ -517,7 +522,7 @@ static void *stage_thread(void *p) {
 
 static int ensure_pinned(gac_ctx *c) {
     for (int k = 0; k < 2; ++k) {
-        if (!c->pin[k]) HIPCHK(hipHostMalloc((void **)&c->pin[k], kPinBytes, hipHostMallocDefault));
+        if (!c->pin[k]) HIPCHK(hipHostMalloc((void **)&c->pin[k], pin_bytes(), hipHostMallocDefault));
         if (!c->pin_ev[k]) HIPCHK(hipEventCreateWithFlags(&c->pin_ev[k], hipEventDisableTiming));
     }
     return GAC_OK;
@@ -529,8 +534,8 @@ static int upload_payloads(gac_ctx *c, const Genome *g, const SeqDev *seqs, int 
     if (rc != GAC_OK) return rc;
     const int nt = std::max(1, std::min(16, gac_host_threads()));
     int k = 0;
-    for (size_t lo = 0; lo < raw_bytes; lo += kPinBytes, k ^= 1) {
-        const size_t hi = std::min(raw_bytes, lo + kPinBytes);
+    for (size_t lo = 0; lo < raw_bytes; lo += pin_bytes(), k ^= 1) {
+        const size_t hi = std::min(raw_bytes, lo + pin_bytes());
         HIPCHK(hipEventSynchronize(c->pin_ev[k]));  // its previous DMA is done
         StageJob J = {g, seqs, nseq, lo, hi, c->pin[k], nt};
         StageArg A;
@@ -543,12 +548,33 @@ static int upload_payloads(gac_ctx *c, const Genome *g, const SeqDev *seqs, int 
     return GAC_OK;
 }
 
+static double wall_s() {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+// GAC_TIMING laps of a genome upload
+struct FinLaps {
+    bool on = getenv("GAC_TIMING") != nullptr;
+    int side;
+    double t = wall_s();
+    void operator()(const char *what) {
+        if (!on) return;
+        const double n = wall_s();
+        fprintf(stderr, "[gac_genome_finalize %c] %-22s %.3f s\n", side ? 'Q' : 'T', what, n - t);
+        t = n;
+    }
+};
+
 extern "C" int gac_genome_finalize(gac_ctx *c, int side) {
     gac_clear_error();
     Genome *g = side_of(c, side);
     if (!g) return gac_fail(GAC_E_ARG, "gac_genome_finalize: bad side");
     CTX_LOCK(c);
     if (g->final) return gac_fail(GAC_E_STATE, "genome side %d already finalized", side);
+    FinLaps lap;
+    lap.side = side;
     HIPCHK(hipSetDevice(c->device));
     const int nseq = (int)g->names.size();
     std::vector<SeqDev> seqs(nseq);
@@ -579,8 +605,10 @@ extern "C" int gac_genome_finalize(gac_ctx *c, int side) {
         NPiece *d_np = nullptr;
         HIPCHK(hipMalloc(&d_raw, raw_bytes + 16));
         HIPCHK(hipMalloc(&d_seqs, nseq * sizeof(SeqDev)));
+        lap("allocations");
         int rc = upload_payloads(c, g, seqs.data(), nseq, d_raw, raw_bytes);
         if (rc != GAC_OK) return rc;
+        lap("payload copies queued");
         HIPCHK(hipMemcpyAsync(d_seqs, seqs.data(), nseq * sizeof(SeqDev), hipMemcpyHostToDevice,
                               c->stream));
         HIPCHK(launch_relayout(d_raw, d_seqs, nseq, w, g->planes, g->nmask, c->stream));
@@ -594,6 +622,7 @@ extern "C" int gac_genome_finalize(gac_ctx *c, int side) {
             HIPCHK(launch_nruns(d_np, np, g->nmask, c->stream));
         }
         HIPCHK(hipStreamSynchronize(c->stream));
+        lap("relayout + N runs done");
         hipFree(d_raw);
         hipFree(d_seqs);
         if (d_np) hipFree(d_np);
@@ -1082,8 +1111,8 @@ static int upload_staged(gac_ctx *c, void *d_dst, const void *h_src, size_t byte
     if (rc != GAC_OK) return rc;
     const int nt = std::max(1, std::min(16, gac_host_threads()));
     int k = 0;
-    for (size_t lo = 0; lo < bytes; lo += kPinBytes, k ^= 1) {
-        const size_t hi = std::min(bytes, lo + kPinBytes);
+    for (size_t lo = 0; lo < bytes; lo += pin_bytes(), k ^= 1) {
+        const size_t hi = std::min(bytes, lo + pin_bytes());
         HIPCHK(hipEventSynchronize(c->pin_ev[k]));
         CopyJob J;
         J.src = (const uint8_t *)h_src + lo;
