@@ -31,7 +31,8 @@ EXECDIR  := $(PKG)/libexec
 # fewer page faults on the GB-scale chain/net arrays) and host->device copies
 # by blit kernels instead of the SDMA engines (HSA_ENABLE_SDMA=0: 20 vs 13
 # GB/s for the genome uploads on the box, profiles/r02f_*), and execs it --
-# before anything touches the GPU.  Either can be overridden from outside.  NetFilterNonNested.perl is host-only: in bin/.
+# before anything touches the GPU.  Either can be overridden from outside.
+# NetFilterNonNested.perl, chainSort and chainMergeSort are host-only: in bin/.
 GPU_TOOLS := scoreChain chainNet chainCleaner axtChain
 HOST_TOOLS := NetFilterNonNested.perl chainSort chainMergeSort
 TOOLS    := $(addprefix $(EXECDIR)/,$(GPU_TOOLS)) $(addprefix $(BINDIR)/,$(GPU_TOOLS)) \
