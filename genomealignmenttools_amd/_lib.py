@@ -170,6 +170,16 @@ _PROTOS = {
         C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "gac_net_write": (
         C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_char_p, C.c_void_p, C.c_int32]),
+    "gac_net_write_file": (
+        C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32]),
+    "gac_net_write_begin": (
+        C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]),
+    "gac_net_write_end": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "gac_net_write_free": (None, [C.c_void_p]),
+    "gac_chain_dp": (
+        C.c_int, [C.c_void_p, C.c_int64] + [C.c_void_p] * 14),
+    "gac_crossovers": (
+        C.c_int, [C.c_void_p, C.c_int64] + [C.c_void_p] * 10),
     "gac_dev_alloc": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
     "gac_dev_free": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gac_memcpy_h2d": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),

@@ -779,6 +779,29 @@ static void *po_thread(void *p) {
     return NULL;
 }
 
+/* the same runs formatted in parallel but kept: bufs[r] / lens[r] (malloc'd) */
+int gac_par_format(int64_t nr, void (*fn)(FILE *f, int64_t r, void *arg), void *arg, char ***bufs,
+                   size_t **lens) {
+    po_job J;
+    J.nr = nr;
+    J.fn = fn;
+    J.arg = arg;
+    J.buf = calloc((size_t)(nr > 0 ? nr : 1), sizeof(char *));
+    J.len = calloc((size_t)(nr > 0 ? nr : 1), sizeof(size_t));
+    J.ready = calloc((size_t)(nr > 0 ? nr : 1), sizeof(_Atomic int));
+    atomic_init(&J.next, 0);
+    atomic_init(&J.oom, 0);
+    int nt = gac_host_threads();
+    if (nt > nr)
+        nt = (int)(nr > 0 ? nr : 1);
+    if (nr > 0)
+        gac_run_threads(nt, po_thread, &J);
+    free((void *)J.ready);
+    *bufs = J.buf;
+    *lens = J.len;
+    return atomic_load(&J.oom) ? -1 : 0;
+}
+
 int gac_par_output(FILE *out, int64_t nr, void (*fn)(FILE *f, int64_t r, void *arg), void *arg) {
     if (nr <= 0)
         return 0;

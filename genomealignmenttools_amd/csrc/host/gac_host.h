@@ -82,6 +82,9 @@ void gac_run_threads(int n, void *(*fn)(void *), void *arg);
  * increasing order), while the calling thread writes the finished runs to
  * out in order.  0 on success. */
 int gac_par_output(FILE *out, int64_t nr, void (*fn)(FILE *f, int64_t r, void *arg), void *arg);
+/* the same runs formatted on worker threads and returned, not written */
+int gac_par_format(int64_t nr, void (*fn)(FILE *f, int64_t r, void *arg), void *arg, char ***bufs,
+                   size_t **lens);
 
 /* ---- host view of a resident sequence (kept after gac_genome_finalize) ----
  * packed: 2 bits/base MSB-first (T=0 C=1 A=2 G=3); N runs merged and sorted. */

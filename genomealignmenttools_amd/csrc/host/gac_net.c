@@ -1829,6 +1829,16 @@ int gac_net_get_fills(const gac_net *n, int side, int32_t *chain, int32_t *start
 }
 
 /* ------------------------------------------------------------ output */
+/* deferred scores (gac_net_write_begin): where each rescored fill's score
+ * goes in a run's text */
+typedef struct wmark {
+    int64_t pos, ord;
+} wmark;
+typedef struct wmarks {
+    wmark *m;
+    int64_t n, cap;
+} wmarks;
+
 typedef struct wctx {
     const gac_net *n;
     FILE *f;
@@ -1836,7 +1846,13 @@ typedef struct wctx {
     const int64_t *tscore; /* per T fill (pre-order), GPU-rescored partial scores */
     int depth;
     char *buf;
+    wmarks *marks; /* deferred: the run's score positions (else NULL) */
 } wctx;
+
+/* fill_info's stand-in for the rescored target-fill scores while they are
+ * being computed: a rescored score is >= 1 (chainNet.c:244-245), so with
+ * minScore <= 1 the fills that print do not depend on it */
+static const int64_t k_deferred[1] = {1};
 
 /* line formatting without stdio's format parsing (the .net files hold
  * millions of lines) */
@@ -1944,7 +1960,9 @@ static int fill_info(const gac_net *n, int side, const int64_t *tscore, const nf
             sub = fullsz;
         } else {
             sub = sub_size(n, c, s, e, 0);
-            if (tscore) {
+            if (tscore == k_deferred) {
+                score = 1; /* placeholder: the fill's text gets the score later */
+            } else if (tscore) {
                 double r = (double)tscore[f->ord];
                 score = r <= 0 ? 1 : r; /* chainNet.c:244-245 */
             } else {
@@ -1962,10 +1980,23 @@ static void put_fill_line(const wctx *w, const nfill *f, int depth, double score
     const gac_net_input *in = &w->n->in;
     const int64_t c = f->chain;
     const char *ochrom = w->side == GAC_Q ? in->t_names[in->t_seq[c]] : in->q_names[in->q_seq[c]];
+    const int deferred =
+        w->marks && w->side == GAC_T && !(f->start <= in->t_start[c] && f->end >= in->t_end[c]);
     if (strlen(ochrom) > 400 || depth > 400 || !(score > -1e300 && score < 1e300)) {
-        fprintf(w->f, "%*sfill %d %d %s %c %d %d id %d score %1.0f ali %d\n", depth, "", f->start,
+        fprintf(w->f, "%*sfill %d %d %s %c %d %d id %d score ", depth, "", f->start,
                 f->end - f->start, ochrom, in->q_strand[c] ? '-' : '+', f->o_start,
-                f->o_end - f->o_start, in->id[c], score, sub);
+                f->o_end - f->o_start, in->id[c]);
+        if (deferred) {
+            wmarks *m = w->marks;
+            if (m->n == m->cap) {
+                m->cap = m->cap ? 2 * m->cap : 256;
+                m->m = realloc(m->m, (size_t)m->cap * sizeof(wmark));
+            }
+            m->m[m->n++] = (wmark){(int64_t)ftell(w->f), f->ord};
+        } else {
+            fprintf(w->f, "%1.0f", score);
+        }
+        fprintf(w->f, " ali %d\n", sub);
         return;
     }
     char buf[512 + 400 + 400], *p = buf;
@@ -1985,7 +2016,16 @@ static void put_fill_line(const wctx *w, const nfill *f, int depth, double score
     p = put_str(p, " id ");
     p = put_int(p, in->id[c]);
     p = put_str(p, " score ");
-    p = put_score(p, score);
+    if (deferred) {
+        wmarks *m = w->marks; /* a rescored fill: its score is inserted here later */
+        if (m->n == m->cap) {
+            m->cap = m->cap ? 2 * m->cap : 256;
+            m->m = realloc(m->m, (size_t)m->cap * sizeof(wmark));
+        }
+        m->m[m->n++] = (wmark){(int64_t)ftell(w->f) + (p - buf), f->ord};
+    } else {
+        p = put_score(p, score);
+    }
     p = put_str(p, " ali ");
     p = put_int(p, sub);
     *p++ = '\n';
@@ -2006,6 +2046,7 @@ typedef struct wjob {
     const gac_net *n;
     int side;
     const int64_t *tscore;
+    wmarks *marks; /* deferred: per run */
     const nfill *const *ord;
     int64_t nf, per;
     double *score;   /* per fill (pre-order) */
@@ -2056,7 +2097,7 @@ static void write_run(FILE *f, int64_t r, void *arg) {
     wjob *J = arg;
     const int64_t a = r * J->per;
     const int64_t b = a + J->per < J->nf ? a + J->per : J->nf;
-    wctx w = {J->n, f, J->side, J->tscore, 0, NULL};
+    wctx w = {J->n, f, J->side, J->tscore, 0, NULL, J->marks ? &J->marks[r] : NULL};
     for (int64_t i = a; i < b; ++i)
         write_segment(J, &w, i);
 }
@@ -2144,45 +2185,140 @@ int gac_net_write_file(const gac_net *n, int side, const int64_t *tscores, FILE 
     return GAC_OK;
 }
 
+/* per-fill score / print flags of a side and the run split (wjob) */
+static void wjob_flags(wjob *J, const gac_net *n, int side, const int64_t *tscore) {
+    const int64_t nf = n->n_order[side];
+    memset(J, 0, sizeof(*J));
+    J->n = n;
+    J->side = side;
+    J->tscore = side == GAC_T ? tscore : NULL;
+    J->ord = (const nfill *const *)n->order[side];
+    J->nf = nf;
+    const size_t m = (size_t)(nf ? nf : 1);
+    J->score = malloc(m * sizeof(double));
+    J->sub = malloc(m * sizeof(int32_t));
+    J->show = malloc(m);
+    J->more = malloc(m);
+    J->reached = malloc(m);
+    const int nt = gac_host_threads();
+    atomic_init(&J->next, 0);
+    gac_run_threads(nt, winfo_thread, J);
+    atomic_store(&J->next, 0);
+    gac_run_threads(nt, wmore_thread, J);
+    for (int32_t k = 0; k < n->n_chroms[side]; ++k) {
+        const nchrom *c = &n->chroms[side][k];
+        if (c->root && c->root->fill_head)
+            mark_more(J, c->root);
+    }
+    for (int64_t i = 0; i < nf; ++i) { /* parents precede children */
+        const nfill *f = J->ord[i];
+        J->reached[i] = J->show[i] && (!f->pgap->pfill || J->reached[f->pgap->pfill->ord]);
+    }
+    J->per = nf / (64 * (int64_t)nt) + 1;
+}
+
+static void wjob_free_flags(wjob *J) {
+    free(J->score);
+    free(J->sub);
+    free(J->show);
+    free(J->more);
+    free(J->reached);
+    J->score = NULL;
+    J->sub = NULL;
+    J->show = J->more = J->reached = NULL;
+}
+
 static int net_write_f(const gac_net *n, int side, const int64_t *tscores, FILE *f,
                        const char *const *meta, int32_t n_meta) {
     for (int32_t i = 0; i < n_meta; ++i)
         fprintf(f, "%s\n", meta[i]);
-    const int64_t nf = n->n_order[side];
     wjob J;
-    memset(&J, 0, sizeof(J));
-    J.n = n;
-    J.side = side;
-    J.tscore = side == GAC_T ? tscores : NULL;
-    J.ord = (const nfill *const *)n->order[side];
-    J.nf = nf;
-    const size_t m = (size_t)(nf ? nf : 1);
-    J.score = malloc(m * sizeof(double));
-    J.sub = malloc(m * sizeof(int32_t));
-    J.show = malloc(m);
-    J.more = malloc(m);
-    J.reached = malloc(m);
-    const int nt = gac_host_threads();
-    atomic_init(&J.next, 0);
-    gac_run_threads(nt, winfo_thread, &J);
-    atomic_store(&J.next, 0);
-    gac_run_threads(nt, wmore_thread, &J);
-    for (int32_t k = 0; k < n->n_chroms[side]; ++k) {
-        const nchrom *c = &n->chroms[side][k];
-        if (c->root && c->root->fill_head)
-            mark_more(&J, c->root);
-    }
-    for (int64_t i = 0; i < nf; ++i) { /* parents precede children */
-        const nfill *f = J.ord[i];
-        J.reached[i] = J.show[i] && (!f->pgap->pfill || J.reached[f->pgap->pfill->ord]);
-    }
-    J.per = nf / (64 * (int64_t)nt) + 1;
-    const int64_t nr = (nf + J.per - 1) / J.per;
+    wjob_flags(&J, n, side, tscores);
+    const int64_t nr = (J.nf + J.per - 1) / J.per;
     int wbad = gac_par_output(f, nr, write_run, &J);
-    free(J.score);
-    free(J.sub);
-    free(J.show);
-    free(J.more);
-    free(J.reached);
+    wjob_free_flags(&J);
     return (ferror(f) || wbad) ? GAC_E_IO : GAC_OK;
+}
+
+/* ---- two-phase target net for -rescore (gac_net_write_begin/_end) */
+struct gac_net_wpre {
+    wjob J;
+    int64_t nr;
+    char **bufs;
+    size_t *lens;
+    char **meta;
+    int32_t n_meta;
+    const int64_t *tscores;
+};
+
+int gac_net_write_begin(const gac_net *n, int side, const char *const *meta, int32_t n_meta,
+                        gac_net_wpre **out) {
+    if (!n || !out || side != GAC_T)
+        return gac_fail(GAC_E_ARG, "gac_net_write_begin: bad argument");
+    if (!(n->sides & (1 << side)))
+        return gac_fail(GAC_E_STATE, "gac_net_write_begin: side %d was not netted", side);
+    if (n->opt.min_score > 1)
+        return gac_fail(GAC_E_STATE, "gac_net_write_begin: minScore > 1 (which fills print "
+                                     "depends on the rescored scores)");
+    gac_net_wpre *P = calloc(1, sizeof(*P));
+    P->meta = malloc((size_t)(n_meta > 0 ? n_meta : 1) * sizeof(char *));
+    for (int32_t i = 0; i < n_meta; ++i)
+        P->meta[i] = strdup(meta[i]);
+    P->n_meta = n_meta;
+    wjob_flags(&P->J, n, side, k_deferred);
+    P->nr = (P->J.nf + P->J.per - 1) / P->J.per;
+    P->J.marks = calloc((size_t)(P->nr > 0 ? P->nr : 1), sizeof(wmarks));
+    const int bad = gac_par_format(P->nr, write_run, &P->J, &P->bufs, &P->lens);
+    wjob_free_flags(&P->J);
+    if (bad) {
+        gac_net_write_free(P);
+        return gac_fail(GAC_E_IO, "gac_net_write_begin: out of memory");
+    }
+    *out = P;
+    return GAC_OK;
+}
+
+/* run r of a prepared net with the scores inserted (gac_par_output item) */
+static void wpre_run(FILE *f, int64_t r, void *arg) {
+    gac_net_wpre *P = arg;
+    const char *buf = P->bufs[r];
+    const wmarks *m = &P->J.marks[r];
+    int64_t last = 0;
+    char tmp[64];
+    for (int64_t k = 0; k < m->n; ++k) {
+        fwrite(buf + last, 1, (size_t)(m->m[k].pos - last), f);
+        const double v = (double)P->tscores[m->m[k].ord];
+        const char *e = put_score(tmp, v <= 0 ? 1 : v); /* chainNet.c:244-245 */
+        fwrite(tmp, 1, (size_t)(e - tmp), f);
+        last = m->m[k].pos;
+    }
+    fwrite(buf + last, 1, P->lens[r] - (size_t)last, f);
+}
+
+int gac_net_write_end(gac_net_wpre *P, const int64_t *tscores, FILE *f) {
+    if (!P || !tscores || !f)
+        return gac_fail(GAC_E_ARG, "gac_net_write_end: bad argument");
+    for (int32_t i = 0; i < P->n_meta; ++i)
+        fprintf(f, "%s\n", P->meta[i]);
+    P->tscores = tscores;
+    const int wbad = gac_par_output(f, P->nr, wpre_run, P);
+    const int bad = ferror(f) || wbad || fflush(f) != 0;
+    gac_net_write_free(P);
+    return bad ? gac_fail(GAC_E_IO, "write error") : GAC_OK;
+}
+
+void gac_net_write_free(gac_net_wpre *P) {
+    if (!P)
+        return;
+    for (int64_t r = 0; r < P->nr; ++r) {
+        free(P->bufs ? P->bufs[r] : NULL);
+        free(P->J.marks ? P->J.marks[r].m : NULL);
+    }
+    free(P->bufs);
+    free(P->lens);
+    free(P->J.marks);
+    for (int32_t i = 0; i < P->n_meta; ++i)
+        free(P->meta[i]);
+    free(P->meta);
+    free(P);
 }

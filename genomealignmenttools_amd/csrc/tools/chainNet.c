@@ -72,12 +72,48 @@ typedef struct net_out {
     const gt_chains *c;
     int threaded, rc;
     char err[1024];
+    /* -rescore: the target net formatted ahead of its scores (pre_net) */
+    gac_net_wpre *pre;
+    pthread_t pre_th;
+    int pre_started, pre_rc;
 } net_out;
 
 static gt_ranks g_rk;
 
+static void *pre_net(void *arg) {
+    net_out *w = arg;
+    const int m = g_rk.n <= 1 || g_rk.me == 0;
+    w->pre_rc = gac_net_write_begin(w->net, w->side, m ? (const char *const *)w->c->meta : NULL,
+                                    m ? w->c->n_meta : 0, &w->pre);
+    return NULL;
+}
+
+/* the prepared target net with its scores */
+static int write_pre(net_out *w, FILE *f) {
+    const int rc = gac_net_write_end(w->pre, w->tscores, f);
+    w->pre = NULL;
+    return rc;
+}
+
 static void *write_net(void *arg) {
     net_out *w = arg;
+    if (w->pre_started) {
+        gt_helper_join(w->pre_th);
+        w->pre_started = 0;
+        if (w->pre_rc != GAC_OK) {
+            gac_net_write_free(w->pre);
+            w->pre = NULL;
+        }
+    }
+    if (w->pre && g_rk.n <= 1) {
+        FILE *f = strcmp(w->path, "stdout") ? fopen(w->path, "w") : stdout;
+        w->rc = f ? write_pre(w, f) : GAC_E_IO;
+        if (f && f != stdout && fclose(f) != 0 && w->rc == GAC_OK)
+            w->rc = GAC_E_IO;
+        if (w->rc != GAC_OK)
+            snprintf(w->err, sizeof(w->err), "write error on %s", w->path);
+        return NULL;
+    }
     if (g_rk.n > 1) {
         /* -nranks: this rank's part formatted in memory and written in place
          * (rank 0's part carries the '#' lines) */
@@ -85,10 +121,13 @@ static void *write_net(void *arg) {
         size_t len = 0;
         FILE *mf = open_memstream(&buf, &len);
         const int m = g_rk.me == 0;
-        w->rc = mf ? gac_net_write_file(w->net, w->side, w->tscores, mf,
-                                        m ? (const char *const *)w->c->meta : NULL,
-                                        m ? w->c->n_meta : 0)
-                   : GAC_E_IO;
+        if (w->pre)
+            w->rc = mf ? write_pre(w, mf) : GAC_E_IO;
+        else
+            w->rc = mf ? gac_net_write_file(w->net, w->side, w->tscores, mf,
+                                            m ? (const char *const *)w->c->meta : NULL,
+                                            m ? w->c->n_meta : 0)
+                       : GAC_E_IO;
         if (mf && fclose(mf) != 0 && w->rc == GAC_OK)
             w->rc = GAC_E_IO;
         if (w->rc == GAC_OK)
@@ -426,6 +465,12 @@ int main(int argc, char *argv[]) {
     gt_verbose(1, "writing %s\n", tnet);
     gt_verbose(1, "writing %s\n", qnet);
     net_out wo[2] = {{net, GAC_T, NULL, tnet, &c, 0, 0}, {net, GAC_Q, NULL, qnet, &c, 0, 0}};
+    const char *pf = getenv("GAC_NET_PREFORMAT"); /* 0: off (measurement knob) */
+    if (rescore && !(pf && *pf == '0')) { /* the target net's text is formatted while the GPU rescores */
+        wo[0].pre_started = pthread_create(&wo[0].pre_th, NULL, pre_net, &wo[0]) == 0;
+        if (wo[0].pre_started)
+            gt_helper_add(wo[0].pre_th);
+    }
     pthread_t qth;
     if (pthread_create(&qth, NULL, write_net, &wo[1]) != 0) {
         write_net(&wo[1]);

@@ -338,6 +338,17 @@ int gac_net_write(const gac_net *net, int side, const int64_t *t_scores, const c
  * chainNet -nranks formats a rank's part in memory, then writes it in place). */
 int gac_net_write_file(const gac_net *net, int side, const int64_t *t_scores, FILE *f,
                        const char *const *meta, int32_t n_meta);
+/* The target net in two phases, for -rescore: _begin formats everything but
+ * the rescored partial fills' scores (which fills print does not depend on
+ * them when minScore <= 1: a rescored score is >= 1, chainNet.c:244-245),
+ * e.g. while the GPU computes them; _end inserts the scores and writes the
+ * same text as gac_net_write(..., t_scores, ...).  _free drops a prepared
+ * net that is not written. */
+typedef struct gac_net_wpre gac_net_wpre;
+int gac_net_write_begin(const gac_net *net, int side, const char *const *meta, int32_t n_meta,
+                        gac_net_wpre **out);
+int gac_net_write_end(gac_net_wpre *w, const int64_t *t_scores, FILE *f);
+void gac_net_write_free(gac_net_wpre *w);
 
 /* ---- device memory helpers (for callers without their own allocator) ---- */
 int gac_dev_alloc(gac_ctx *ctx, size_t bytes, void **dptr);

@@ -445,3 +445,42 @@ def test_kent_shim_library_exports_and_gapcalc():
         gc = lib.gapCalcFromFile(src)
         got = [lib.gapCalcCost(gc, int(dq), int(dt)) for dq, dt in pairs]
         assert got == gj[name][:2000], name
+
+
+def test_net_write_two_phase(tmp_path):
+    """gac_net_write_begin/_end (chainNet -rescore formats the target net
+    while the GPU rescores): the same bytes as gac_net_write with the same
+    scores, rescored scores <= 0 printed as 1; with minScore > 1 the two-phase
+    writer refuses (which fills print would depend on the scores)."""
+    import ctypes as C
+    from genomealignmenttools_amd import chainfile
+    from genomealignmenttools_amd._lib import lib
+    from genomealignmenttools_amd.chainnet import Net as NetBuilder
+    from genomealignmenttools_amd.synth import read_sizes
+    d = os.path.join(GOLDEN, "synth11")
+    ca = chainfile.read_chains(os.path.join(d, "in.chain"))
+    ts, qs = read_sizes(os.path.join(d, "t.sizes")), read_sizes(os.path.join(d, "q.sizes"))
+    libc = C.CDLL(None)
+    libc.fopen.restype = C.c_void_p
+    libc.fopen.argtypes = [C.c_char_p, C.c_char_p]
+    libc.fclose.argtypes = [C.c_void_p]
+    for min_score in (0.0, 1.0):
+        nb = NetBuilder(ca, ts, qs, min_score=min_score)
+        nf = lib().gac_net_fill_count(nb.h, 0)
+        rng = np.random.default_rng(5)
+        scores = rng.integers(-50, 10 ** 7, nf).astype(np.int64)
+        scores[::7] = 0
+        meta = ["# two-phase test"]
+        nb.write(0, str(tmp_path / "a.net"), scores, meta)
+        marr = (C.c_char_p * 1)(meta[0].encode())
+        h = C.c_void_p()
+        assert lib().gac_net_write_begin(nb.h, 0, C.cast(marr, C.c_void_p), 1, C.byref(h)) == 0
+        f = libc.fopen(str(tmp_path / "b.net").encode(), b"w")
+        assert lib().gac_net_write_end(h, scores.ctypes.data, f) == 0
+        assert libc.fclose(f) == 0
+        assert filecmp.cmp(tmp_path / "a.net", tmp_path / "b.net", shallow=False)
+        nb.close()
+    nb = NetBuilder(ca, ts, qs, min_score=2000.0)
+    h = C.c_void_p()
+    assert lib().gac_net_write_begin(nb.h, 0, None, 0, C.byref(h)) != 0
+    nb.close()
