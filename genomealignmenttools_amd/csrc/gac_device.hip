@@ -1208,7 +1208,7 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
     int32_t *d_bt = nullptr;  // caller's block arrays, staged; blocks / spans / buckets are
                               // built from them on the device (k_build_*)
     hipError_t e = hipMalloc(&cs->chains, ch.size() * sizeof(DChain));
-    if (e == hipSuccess) e = hipMalloc(&cs->blk, (nb + 1) * sizeof(int4));
+    if (e == hipSuccess) e = hipMalloc(&cs->blk, (nb + 8) * sizeof(int4));
     if (e == hipSuccess) e = hipMalloc(&cs->bucket, (size_t)std::max<int64_t>(idx_n, 1) * 4);
     if (e == hipSuccess) e = hipMalloc(&cs->tspan, (nb + 8) * sizeof(int2));
     if (e == hipSuccess) e = hipMalloc(&d_bt, std::max<size_t>(3 * nb, 1) * 4);

@@ -96,7 +96,7 @@ struct ScoreArgs {
     const int64_t *q_woff;
     const DChain *chains;
     int64_t n_chains;
-    const int4 *blk;     // [n_blocks + 1] {tStart, qStart, size | N flags, gap to next}
+    const int4 *blk;     // [n_blocks + 8] {tStart, qStart, size | N flags, gap to next}
     const int2 *tspan;   // [n_blocks + 8] {tStart, tEnd} (window searches; padded)
     const uint32_t *bucket;  // chain bucket indexes (see DChain)
     const Range *ranges;

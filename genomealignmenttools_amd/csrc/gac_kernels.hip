@@ -224,9 +224,9 @@ __global__ void __launch_bounds__(256) k_build_blocks(const int32_t *bt, const i
         const int t = bt[b], z = bs[b];
         blk[b] = make_int4(t, bq[b], z, 0);
         tspan[b] = make_int2(t, t + z);
-    } else if (b < nb + 8) {
+    } else if (b < nb + 8) {  // padding: a window search may read 8 past a chain
         tspan[b] = make_int2(0x7fffffff, 0x7fffffff);
-        if (b == nb) blk[b] = make_int4(0, 0, 0, 0);
+        blk[b] = make_int4(0x7fffffff, 0, 0, 0);
     }
 }
 
