@@ -109,4 +109,14 @@ oracle/_build/axtChain_cpu: $(CSRC)/tools/axtChain.c $(CSRC)/host/gac_axtchain.c
 	$(CC) -O2 -g -std=gnu11 -Wall -Iinclude -I$(CSRC) -I$(CSRC)/host -I$(CSRC)/tools/lib $^ \
 	    -o $@ -lz -lm -lpthread $(CPU_EXTRA)
 
-.PHONY: cpu-axtchain
+# chainNet -rescore on the same stand-in: the sparse genome upload's word
+# runs are checked on CPU (the stand-in poisons every word outside them)
+cpu-chainnet: oracle/_build/chainNet_cpu
+
+oracle/_build/chainNet_cpu: $(CSRC)/tools/chainNet.c $(CSRC)/host/gac_net.c \
+		$(CSRC)/host/gac_host.c oracle/cpu_gac_stub.c $(TOOL_LIB_SRC)
+	@mkdir -p oracle/_build
+	$(CC) -O2 -g -std=gnu11 -Wall -Iinclude -I$(CSRC) -I$(CSRC)/host -I$(CSRC)/tools/lib $^ \
+	    -o $@ -lz -lm -lpthread $(CPU_EXTRA)
+
+.PHONY: cpu-axtchain cpu-chainnet

@@ -54,6 +54,8 @@ hipError_t launch_build(const int32_t *bt, const int32_t *bq, const int32_t *bs,
                         const DChain *chains, int64_t n_chains, int4 *blk, int2 *tspan,
                         uint32_t *bucket, hipStream_t s);
 hipError_t launch_nruns(const NPiece *p, int64_t n, uint32_t *nmask, hipStream_t s);
+hipError_t launch_scatter(const SparseRun *runs, int64_t n, const uint64_t *compact,
+                          uint64_t *raw, hipStream_t s);
 hipError_t launch_blocks(const ScoreArgs &a, const BlockJob *jobs, int64_t n, int32_t *out,
                          hipStream_t s);
 }  // namespace gac
@@ -80,6 +82,10 @@ struct Genome {
     std::vector<const uint8_t *> ext;  // per seq: payload inside the mapped .2bit file
     gac_twobit tb{};                // mapping kept open for ext (gac_genome_load_2bit)
     bool tb_open = false;
+    // sparse upload (gac_genome_load_twobit_runs): only these word runs of
+    // registered sequence run_seq[k], [run_lo, run_hi) in 32-base words
+    bool sparse = false;
+    std::vector<int32_t> run_seq, run_lo, run_hi;
     std::vector<NPiece> npieces;    // bit0 relative to the seq start until finalize
     std::vector<int32_t> npiece_seq;
     // host copy kept after finalize (raw stays): merged, sorted N runs per
@@ -528,6 +534,83 @@ static int ensure_pinned(gac_ctx *c) {
     return GAC_OK;
 }
 
+// Sparse: the runs' bytes packed (compact layout, SparseRun::src), staged the
+// same way through the pinned windows.
+struct StageRunsJob {
+    const Genome *g;
+    const SparseRun *runs;
+    const int32_t *seq;  // registered sequence of each run
+    const SeqDev *seqs;
+    int64_t nruns;
+    size_t lo, hi;
+    uint8_t *dst;
+    int nt;
+};
+
+static void stage_runs_body(StageRunsJob *J, int t) {
+    const size_t len = J->hi - J->lo, per = (len + J->nt - 1) / J->nt;
+    const size_t a = J->lo + std::min(len, per * t), b = J->lo + std::min(len, per * (t + 1));
+    if (a >= b) return;
+    int64_t lo = 0, hi = J->nruns;  // first run ending after a
+    while (lo < hi) {
+        const int64_t m = (lo + hi) / 2;
+        if ((size_t)(J->runs[m].src + ((J->runs[m].len + 7) & ~7LL)) <= a) lo = m + 1;
+        else hi = m;
+    }
+    size_t pos = a;
+    for (int64_t r = lo; r < J->nruns && pos < b; ++r) {
+        const SparseRun &R = J->runs[r];
+        const size_t s0 = (size_t)R.src, s1 = s0 + (size_t)R.len;
+        const size_t e0 = s0 + (((size_t)R.len + 7) & ~(size_t)7);  // padded end
+        const int k = J->seq[r];
+        const uint8_t *from = J->g->packed(k) + (R.dst - J->seqs[k].byte_off);
+        if (s1 > pos) {
+            const size_t e = std::min(s1, b);
+            memcpy(J->dst + (pos - J->lo), from + (pos - s0), e - pos);
+            pos = e;
+        }
+        if (pos < b && e0 > pos) {
+            const size_t e = std::min(e0, b);
+            memset(J->dst + (pos - J->lo), 0, e - pos);
+            pos = e;
+        }
+    }
+    if (pos < b) memset(J->dst + (pos - J->lo), 0, b - pos);
+}
+
+struct StageRunsArg {
+    StageRunsJob *J;
+    std::atomic<int> next;
+};
+
+static void *stage_runs_thread(void *p) {
+    StageRunsArg *A = (StageRunsArg *)p;
+    for (int t; (t = A->next.fetch_add(1)) < A->J->nt;) stage_runs_body(A->J, t);
+    return nullptr;
+}
+
+static int ensure_pinned(gac_ctx *c);
+
+static int upload_runs(gac_ctx *c, const Genome *g, const SeqDev *seqs, const SparseRun *runs,
+                       const int32_t *seq, int64_t nruns, uint8_t *d_compact, size_t bytes) {
+    int rc = ensure_pinned(c);
+    if (rc != GAC_OK) return rc;
+    const int nt = std::max(1, std::min(16, gac_host_threads()));
+    int k = 0;
+    for (size_t lo = 0; lo < bytes; lo += pin_bytes(), k ^= 1) {
+        const size_t hi = std::min(bytes, lo + pin_bytes());
+        HIPCHK(hipEventSynchronize(c->pin_ev[k]));
+        StageRunsJob J = {g, runs, seq, seqs, nruns, lo, hi, c->pin[k], nt};
+        StageRunsArg A;
+        A.J = &J;
+        A.next = 0;
+        gac_run_threads(nt, stage_runs_thread, &A);
+        HIPCHK(hipMemcpyAsync(d_compact + lo, c->pin[k], hi - lo, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipEventRecord(c->pin_ev[k], c->stream));
+    }
+    return GAC_OK;
+}
+
 static int upload_payloads(gac_ctx *c, const Genome *g, const SeqDev *seqs, int nseq,
                            uint8_t *d_raw, size_t raw_bytes) {
     int rc = ensure_pinned(c);
@@ -606,9 +689,36 @@ extern "C" int gac_genome_finalize(gac_ctx *c, int side) {
         HIPCHK(hipMalloc(&d_raw, raw_bytes + 16));
         HIPCHK(hipMalloc(&d_seqs, nseq * sizeof(SeqDev)));
         lap("allocations");
-        int rc = upload_payloads(c, g, seqs.data(), nseq, d_raw, raw_bytes);
-        if (rc != GAC_OK) return rc;
-        lap("payload copies queued");
+        uint8_t *d_compact = nullptr;
+        SparseRun *d_runs = nullptr;
+        if (g->sparse) {  // only the listed word runs
+            std::vector<SparseRun> runs;
+            std::vector<int32_t> rseq;
+            int64_t compact = 0;
+            for (size_t r = 0; r < g->run_seq.size(); ++r) {
+                const int k = g->run_seq[r];
+                const int64_t pay = ((int64_t)g->sizes[k] + 3) / 4;
+                const int64_t b0 = (int64_t)g->run_lo[r] * 8, b1 = std::min<int64_t>((int64_t)g->run_hi[r] * 8, pay);
+                if (b1 <= b0) continue;
+                runs.push_back(SparseRun{seqs[k].byte_off + b0, compact, b1 - b0});
+                rseq.push_back(k);
+                compact += ((b1 - b0) + 7) & ~7LL;
+            }
+            HIPCHK(hipMalloc(&d_compact, (size_t)compact + 16));
+            HIPCHK(hipMalloc(&d_runs, std::max<size_t>(runs.size(), 1) * sizeof(SparseRun)));
+            int rc = upload_runs(c, g, seqs.data(), runs.data(), rseq.data(), (int64_t)runs.size(),
+                                 d_compact, (size_t)compact);
+            if (rc != GAC_OK) return rc;
+            HIPCHK(hipMemcpyAsync(d_runs, runs.data(), runs.size() * sizeof(SparseRun),
+                                  hipMemcpyHostToDevice, c->stream));
+            HIPCHK(launch_scatter(d_runs, (int64_t)runs.size(), (const uint64_t *)d_compact,
+                                  (uint64_t *)d_raw, c->stream));
+            lap("sparse runs queued");
+        } else {
+            int rc = upload_payloads(c, g, seqs.data(), nseq, d_raw, raw_bytes);
+            if (rc != GAC_OK) return rc;
+            lap("payload copies queued");
+        }
         HIPCHK(hipMemcpyAsync(d_seqs, seqs.data(), nseq * sizeof(SeqDev), hipMemcpyHostToDevice,
                               c->stream));
         HIPCHK(launch_relayout(d_raw, d_seqs, nseq, w, g->planes, g->nmask, c->stream));
@@ -623,6 +733,8 @@ extern "C" int gac_genome_finalize(gac_ctx *c, int side) {
         }
         HIPCHK(hipStreamSynchronize(c->stream));
         lap("relayout + N runs done");
+        if (d_compact) hipFree(d_compact);
+        if (d_runs) hipFree(d_runs);
         hipFree(d_raw);
         hipFree(d_seqs);
         if (d_np) hipFree(d_np);
@@ -645,11 +757,17 @@ extern "C" int gac_genome_load_2bit(gac_ctx *c, int side, const char *path) {
 }
 
 extern "C" int gac_genome_load_twobit(gac_ctx *c, int side, gac_twobit *tbp) {
-    return gac_genome_load_twobit_keep(c, side, tbp, nullptr);
+    return gac_genome_load_twobit_runs(c, side, tbp, nullptr, nullptr, nullptr, nullptr);
 }
 
 extern "C" int gac_genome_load_twobit_keep(gac_ctx *c, int side, gac_twobit *tbp,
                                            const uint8_t *keep) {
+    return gac_genome_load_twobit_runs(c, side, tbp, keep, nullptr, nullptr, nullptr);
+}
+
+extern "C" int gac_genome_load_twobit_runs(gac_ctx *c, int side, gac_twobit *tbp,
+                                           const uint8_t *keep, const int64_t *run_off,
+                                           const int32_t *run_lo, const int32_t *run_hi) {
     gac_clear_error();
     if (!side_of(c, side) || !tbp) {
         if (tbp) gac_twobit_close(tbp);
@@ -670,6 +788,20 @@ extern "C" int gac_genome_load_twobit_keep(gac_ctx *c, int side, gac_twobit *tbp
         }
         rc = add_seq(c, side, s.name, (int32_t)s.size, s.packed, false, (int32_t)s.n_count,
                      ns.data(), nz.data());
+        if (rc == GAC_OK && run_off) {  // this sequence's word runs
+            Genome *g = side_of(c, side);
+            g->sparse = true;
+            const int32_t k = (int32_t)g->names.size() - 1;
+            const int64_t nw = ((int64_t)s.size + 31) / 32;
+            for (int64_t r = run_off[i]; r < run_off[i + 1]; ++r) {
+                const int32_t lo = std::max<int32_t>(0, run_lo[r]);
+                const int32_t hi = (int32_t)std::min<int64_t>(nw, run_hi[r]);
+                if (hi <= lo) continue;
+                g->run_seq.push_back(k);
+                g->run_lo.push_back(lo);
+                g->run_hi.push_back(hi);
+            }
+        }
     }
     if (rc != GAC_OK) {  // the side holds pointers into tb: drop it whole
         free_genome(*side_of(c, side));

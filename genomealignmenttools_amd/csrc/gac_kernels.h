@@ -140,6 +140,12 @@ struct SmallOut {
 };
 constexpr int kSmallMax = 256;  // ranges per small-batch call
 
+// One run of a sparse genome upload (bytes): its place in the staging layout
+// (8-byte aligned), its offset in the packed upload (8-byte aligned), length.
+struct SparseRun {
+    int64_t dst, src, len;
+};
+
 // One ungapped block for k_blocks (axtScoreUngapped): global plane positions
 // of its first target base and, for the query, of its first base ('+') or
 // one past its last base on the forward strand ('-').

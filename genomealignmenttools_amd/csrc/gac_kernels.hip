@@ -1268,6 +1268,33 @@ hipError_t launch_blocks(const ScoreArgs &a, const BlockJob *jobs, int64_t n, in
     return hipGetLastError();
 }
 
+// Sparse genome upload: the payload bytes of the uploaded runs arrive packed
+// one after another (8-byte aligned); one wave per run copies them to their
+// place in the staging layout (the rest of it is never read: no scored range
+// reaches outside the runs).
+__global__ void __launch_bounds__(256) k_scatter(const SparseRun *runs, int64_t n,
+                                                 const uint64_t *compact, uint64_t *raw) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave_id = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t r = wave_id; r < n; r += nwaves) {
+        const SparseRun R = runs[r];
+        const int64_t words = (R.len + 7) >> 3;
+        const uint64_t *src = compact + (R.src >> 3);
+        uint64_t *dst = raw + (R.dst >> 3);
+        for (int64_t u = lane; u < words; u += kWave) dst[u] = src[u];
+    }
+}
+
+hipError_t launch_scatter(const SparseRun *runs, int64_t n, const uint64_t *compact,
+                          uint64_t *raw, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    int64_t nb = (n + 3) / 4;
+    if (nb > 16384) nb = 16384;
+    hipLaunchKernelGGL(k_scatter, dim3((unsigned)nb), dim3(256), 0, s, runs, n, compact, raw);
+    return hipGetLastError();
+}
+
 hipError_t launch_nruns(const NPiece *p, int64_t n, uint32_t *nmask, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const int64_t nb = (n + 255) / 256;

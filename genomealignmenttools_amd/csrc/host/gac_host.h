@@ -65,6 +65,14 @@ int gac_genome_load_twobit(gac_ctx *c, int side, gac_twobit *tb);
 /* the same with only the sequences i of the file where keep[i] != 0 (keep
  * may be NULL: all) */
 int gac_genome_load_twobit_keep(gac_ctx *c, int side, gac_twobit *tb, const uint8_t *keep);
+/* the same uploading only word runs (32-base words) of each sequence i of
+ * the file: [run_lo[r], run_hi[r]) for r in [run_off[i], run_off[i+1]);
+ * bases outside them are undefined on the device -- the caller scores no
+ * range that reaches outside them (chainNet: the words under its chains'
+ * blocks, plus one).  run_off NULL: every base. */
+int gac_genome_load_twobit_runs(gac_ctx *c, int side, gac_twobit *tb, const uint8_t *keep,
+                                const int64_t *run_off, const int32_t *run_lo,
+                                const int32_t *run_hi);
 void gac_twobit_close(gac_twobit *tb);
 uint32_t gac_twobit_u32(const gac_twobit *tb, const uint8_t *p);
 int gac_is_twobit_file(const char *path);

@@ -170,6 +170,20 @@ static void *subset_copy_thread(void *arg) {
     return NULL;
 }
 
+/* -rescore: the genome word runs under the chains' blocks, computed while
+ * the chains are netted (the device thread uploads just these) */
+typedef struct runs_job {
+    gt_runs *R;
+    const gt_chains *c;
+    const char *t2bit, *q2bit;
+} runs_job;
+
+static void *runs_thread(void *arg) {
+    runs_job *j = arg;
+    gt_runs_build(j->R, j->c, j->t2bit, j->q2bit);
+    return NULL;
+}
+
 /* With -rescore: the whole chain set goes to HBM on a helper thread while
  * the chains are netted (the usual case: every chain's sequences are in the
  * 2bit files).  If a sequence is missing -- the reference only looks up the
@@ -347,8 +361,16 @@ int main(int argc, char *argv[]) {
      * it rescores target fills) */
     gt_device dev;
     memset(&dev, 0, sizeof(dev));
+    /* -rescore uploads only the genome words under the chains' blocks (about
+     * a tenth of a whole-genome query): the device thread opens the context
+     * and maps the .2bit files while the chains are read, then waits for the
+     * word runs (GAC_NET_SPARSE=0: upload both genomes whole) */
+    const char *sp = getenv("GAC_NET_SPARSE");
+    const int sparse = rescore && !(sp && *sp == '0');
+    gt_runs runs;
+    gt_runs_init(&runs);
     if (rescore && !multi)
-        gt_device_start(&dev, tnib, qnib, mat, gap);
+        gt_device_start_ex(&dev, tnib, qnib, mat, gap, NULL, sparse ? &runs : NULL);
 
     gt_sizes qs, ts;
     gt_stage("options + setup");
@@ -386,7 +408,7 @@ int main(int argc, char *argv[]) {
         const int own_t = assign_range(&ts, tkeep, &tkept);
         assign_range(&qs, qkeep, &qkept);
         if (rescore && own_t)
-            gt_device_start_keep(&dev, tnib, qnib, mat, gap, &tkept);
+            gt_device_start_ex(&dev, tnib, qnib, mat, gap, &tkept, sparse ? &runs : NULL);
         gt_stage("rank sides");
     }
     gt_chains c;
@@ -416,6 +438,14 @@ int main(int argc, char *argv[]) {
                      tsizes_file);
     }
     gt_stage("chain checks");
+    runs_job rj = {&runs, &c, tnib, qnib};
+    if (dev.started && dev.runs) {
+        pthread_t rth;
+        if (pthread_create(&rth, NULL, runs_thread, &rj) == 0)
+            gt_helper_add(rth); /* gt_abort joins it before exiting */
+        else
+            runs_thread(&rj);
+    }
     pre_upload pu;
     memset(&pu, 0, sizeof(pu));
     if (rescore && dev.started) {

@@ -154,8 +154,24 @@ static void *device_thread(void *arg) {
             for (uint32_t i = 0; i < P.tb[k].seq_count; ++i)
                 keep[i] = gt_names_find(d->tkeep, P.tb[k].seqs[i].name) >= 0;
         }
+        const gt_runs *R = NULL;
+        if (rc == GAC_OK && d->runs) { /* the word runs the chains need */
+            pthread_mutex_lock(&d->runs->mu);
+            while (!d->runs->ready)
+                pthread_cond_wait(&d->runs->cv, &d->runs->mu);
+            pthread_mutex_unlock(&d->runs->mu);
+            if (d->runs->ok < 0) { /* the tool is aborting: skip the upload */
+                gac_twobit_close(&P.tb[k]);
+                free(keep);
+                continue;
+            }
+            if (d->runs->ok)
+                R = d->runs;
+        }
         if (rc == GAC_OK)
-            rc = gac_genome_load_twobit_keep(d->ctx, k == 0 ? GAC_T : GAC_Q, &P.tb[k], keep);
+            rc = gac_genome_load_twobit_runs(d->ctx, k == 0 ? GAC_T : GAC_Q, &P.tb[k], keep,
+                                             R ? R->off[k] : NULL, R ? R->lo[k] : NULL,
+                                             R ? R->hi[k] : NULL);
         else if (P.rc[k] == GAC_OK)
             gac_twobit_close(&P.tb[k]);
         free(keep);
@@ -171,15 +187,164 @@ static void *device_thread(void *arg) {
     return NULL;
 }
 
+/* ---- genome word runs under the chains' blocks (gt_runs) */
+void gt_runs_init(gt_runs *R) {
+    memset(R, 0, sizeof(*R));
+    pthread_mutex_init(&R->mu, NULL);
+    pthread_cond_init(&R->cv, NULL);
+}
+
+typedef struct runs_mark {
+    const gt_chains *c;
+    const int32_t *tmap, *qmap;     /* chain name index -> .2bit sequence */
+    const int64_t *twoff, *qwoff;   /* first word of each .2bit sequence (bitmap space) */
+    const int32_t *tsize, *qsize;
+    _Atomic uint64_t *tbits, *qbits;
+    _Atomic int64_t next;
+} runs_mark;
+
+static void mark_words(_Atomic uint64_t *bits, int64_t w0, int64_t w1) {
+    for (int64_t w = w0; w < w1; ++w)
+        atomic_fetch_or_explicit(&bits[w >> 6], 1ull << (w & 63), memory_order_relaxed);
+}
+
+static void *runs_mark_thread(void *arg) {
+    runs_mark *M = arg;
+    const gt_chains *c = M->c;
+    for (;;) {
+        const int64_t a = atomic_fetch_add(&M->next, 1024);
+        if (a >= c->n)
+            break;
+        const int64_t b = a + 1024 < c->n ? a + 1024 : c->n;
+        for (int64_t i = a; i < b; ++i) {
+            const int32_t ts = M->tmap[c->tname[i]], qs = M->qmap[c->qname[i]];
+            for (int64_t k = c->blk_off[i]; k < c->blk_off[i + 1]; ++k) {
+                const int64_t z = c->bs[k];
+                if (z <= 0)
+                    continue;
+                if (ts >= 0) {
+                    const int64_t t = c->bt[k];
+                    const int64_t nw = ((int64_t)M->tsize[ts] + 31) / 32;
+                    const int64_t w1 = ((t + z - 1) >> 5) + 2;
+                    mark_words(M->tbits, M->twoff[ts] + (t >> 5), M->twoff[ts] + (w1 < nw ? w1 : nw));
+                }
+                if (qs >= 0) {
+                    const int64_t q = c->bq[k], qz = M->qsize[qs];
+                    const int64_t f0 = c->qstrand[i] ? qz - (q + z) : q, f1 = f0 + z;
+                    const int64_t nw = (qz + 31) / 32;
+                    const int64_t w1 = ((f1 - 1) >> 5) + 2;
+                    mark_words(M->qbits, M->qwoff[qs] + (f0 >> 5), M->qwoff[qs] + (w1 < nw ? w1 : nw));
+                }
+            }
+        }
+    }
+    return NULL;
+}
+
+/* runs of set bits of each sequence, CSR by sequence */
+static void bits_to_runs(const _Atomic uint64_t *bits, const int64_t *woff, int32_t nseq,
+                         int64_t **off_out, int32_t **lo_out, int32_t **hi_out, int64_t *words) {
+    int64_t *off = malloc((size_t)(nseq + 1) * 8), cap = 1024, n = 0;
+    int32_t *lo = malloc((size_t)cap * 4), *hi = malloc((size_t)cap * 4);
+    *words = 0;
+    for (int32_t s = 0; s < nseq; ++s) {
+        off[s] = n;
+        int64_t w = woff[s];
+        const int64_t end = woff[s + 1];
+        while (w < end) {
+            const uint64_t x = atomic_load_explicit(&bits[w >> 6], memory_order_relaxed) >> (w & 63);
+            if (!x) { /* skip the rest of this 64-bit word */
+                w = (w | 63) + 1;
+                continue;
+            }
+            w += __builtin_ctzll(x);
+            if (w >= end)
+                break;
+            const int64_t r0 = w;
+            while (w < end && ((atomic_load_explicit(&bits[w >> 6], memory_order_relaxed) >> (w & 63)) & 1))
+                ++w;
+            if (n == cap) {
+                cap *= 2;
+                lo = realloc(lo, (size_t)cap * 4);
+                hi = realloc(hi, (size_t)cap * 4);
+            }
+            lo[n] = (int32_t)(r0 - woff[s]);
+            hi[n] = (int32_t)(w - woff[s]);
+            *words += w - r0;
+            ++n;
+        }
+    }
+    off[nseq] = n;
+    *off_out = off;
+    *lo_out = lo;
+    *hi_out = hi;
+}
+
+void gt_runs_build(gt_runs *R, const gt_chains *c, const char *t2bit, const char *q2bit) {
+    gac_twobit tb[2];
+    int ok = gac_twobit_open_ex(t2bit, &tb[0], 0) == GAC_OK;
+    if (ok && gac_twobit_open_ex(q2bit, &tb[1], 0) != GAC_OK) {
+        gac_twobit_close(&tb[0]);
+        ok = 0;
+    }
+    if (ok) {
+        int64_t *woff[2];
+        int32_t *size[2], *map[2];
+        _Atomic uint64_t *bits[2];
+        const gt_names *cn[2] = {&c->tnames, &c->qnames};
+        for (int k = 0; k < 2; ++k) {
+            const int32_t ns = (int32_t)tb[k].seq_count;
+            gt_names fn;
+            memset(&fn, 0, sizeof(fn));
+            woff[k] = malloc((size_t)(ns + 1) * 8);
+            size[k] = malloc((size_t)(ns ? ns : 1) * 4);
+            woff[k][0] = 0;
+            for (int32_t i = 0; i < ns; ++i) {
+                gt_names_add(&fn, tb[k].seqs[i].name, strlen(tb[k].seqs[i].name));
+                size[k][i] = (int32_t)tb[k].seqs[i].size;
+                woff[k][i + 1] = woff[k][i] + ((int64_t)tb[k].seqs[i].size + 31) / 32;
+            }
+            map[k] = malloc((size_t)(cn[k]->n ? cn[k]->n : 1) * 4);
+            for (int32_t j = 0; j < cn[k]->n; ++j)
+                map[k][j] = gt_names_find(&fn, cn[k]->names[j]);
+            gt_names_free(&fn);
+            bits[k] = calloc((size_t)(woff[k][ns] / 64 + 2), 8);
+        }
+        runs_mark M = {c, map[0], map[1], woff[0], woff[1], size[0], size[1], bits[0], bits[1], 0};
+        atomic_init(&M.next, 0);
+        gac_run_threads(gt_threads(), runs_mark_thread, &M);
+        for (int k = 0; k < 2; ++k) {
+            bits_to_runs(bits[k], woff[k], (int32_t)tb[k].seq_count, &R->off[k], &R->lo[k],
+                         &R->hi[k], &R->words[k]);
+            free(bits[k]);
+            free(woff[k]);
+            free(size[k]);
+            free(map[k]);
+            gac_twobit_close(&tb[k]);
+        }
+    }
+    pthread_mutex_lock(&R->mu);
+    R->ok = ok;
+    R->ready = 1;
+    pthread_cond_broadcast(&R->cv);
+    pthread_mutex_unlock(&R->mu);
+}
+
 void gt_device_start(gt_device *d, const char *t2bit, const char *q2bit, const int32_t mat[16],
                      const gac_gapcalc *gap) {
-    gt_device_start_keep(d, t2bit, q2bit, mat, gap, NULL);
+    gt_device_start_ex(d, t2bit, q2bit, mat, gap, NULL, NULL);
 }
 
 void gt_device_start_keep(gt_device *d, const char *t2bit, const char *q2bit,
                           const int32_t mat[16], const gac_gapcalc *gap, const gt_names *tkeep) {
+    gt_device_start_ex(d, t2bit, q2bit, mat, gap, tkeep, NULL);
+}
+
+void gt_device_start_ex(gt_device *d, const char *t2bit, const char *q2bit, const int32_t mat[16],
+                        const gac_gapcalc *gap, const gt_names *tkeep, gt_runs *runs) {
     memset(d, 0, sizeof(*d));
     d->tkeep = tkeep;
+    d->runs = runs;
     d->t2bit = t2bit;
     d->q2bit = q2bit;
     d->mat = mat;
@@ -235,6 +400,15 @@ static void join_live_device(void) {
     if (d && d->closing && !pthread_equal(pthread_self(), (pthread_t)d->close_th)) {
         pthread_join((pthread_t)d->close_th, NULL);
         d->closing = 0;
+    }
+    if (d && d->started && d->runs) { /* never built (an early abort): let it go */
+        pthread_mutex_lock(&d->runs->mu);
+        if (!d->runs->ready) {
+            d->runs->ready = 1;
+            d->runs->ok = -1;
+            pthread_cond_broadcast(&d->runs->cv);
+        }
+        pthread_mutex_unlock(&d->runs->mu);
     }
     if (d && d->started)
         device_wait_done(d);

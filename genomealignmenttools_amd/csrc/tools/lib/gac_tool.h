@@ -37,6 +37,21 @@ void gt_set_gpu(int gpu);
  * genome upload overlap the host's chain parsing / netting; gt_device_join
  * waits for it and returns the context (aborting with its error, like
  * gt_check).  mat and gap must stay valid until the join. */
+struct gt_chains;
+struct gt_names;
+
+/* The genome word runs a tool's chains need (chainNet -rescore): the device
+ * thread uploads only these (gac_genome_load_twobit_runs) once they are
+ * ready.  Per side, CSR by sequence of the .2bit file. */
+typedef struct gt_runs {
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    int ready, ok;
+    int64_t *off[2];
+    int32_t *lo[2], *hi[2];
+    int64_t words[2]; /* words uploaded (diagnostics) */
+} gt_runs;
+
 typedef struct gt_device {
     const char *t2bit, *q2bit;
     const int32_t *mat;
@@ -53,13 +68,24 @@ typedef struct gt_device {
     unsigned long close_th;
     int closing;
     const struct gt_names *tkeep; /* target sequences to load (NULL: all); -nranks */
+    gt_runs *runs;                /* upload only these word runs (NULL: everything) */
 } gt_device;
 void gt_device_start(gt_device *d, const char *t2bit, const char *q2bit, const int32_t mat[16],
                      const gac_gapcalc *gap);
+/* chainNet -rescore: compute the word runs under the blocks of c's chains
+ * for the two .2bit files (on a helper thread) and publish them to R; the
+ * device thread of a gt_device whose runs == R waits for them */
+void gt_runs_init(gt_runs *R);
+void gt_runs_build(gt_runs *R, const struct gt_chains *c, const char *t2bit, const char *q2bit);
 /* the same, loading only the target sequences named in tkeep */
 void gt_device_start_keep(gt_device *d, const char *t2bit, const char *q2bit,
                           const int32_t mat[16], const gac_gapcalc *gap,
                           const struct gt_names *tkeep);
+/* the same with the genome uploads restricted to runs (NULL: all): the
+ * device thread waits for gt_runs_build to publish them (ok == 0: upload
+ * everything; an abort before they are built releases it) */
+void gt_device_start_ex(gt_device *d, const char *t2bit, const char *q2bit, const int32_t mat[16],
+                        const gac_gapcalc *gap, const struct gt_names *tkeep, gt_runs *runs);
 /* main thread only */
 gac_ctx *gt_device_join(gt_device *d);
 /* the same wait without the abort: NULL if the bring-up failed.  Safe from

@@ -66,6 +66,29 @@ int gac_genome_load_2bit(gac_ctx *c, int which, const char *path) {
     return gac_genome_load_twobit(c, which, &tb);
 }
 
+int gac_genome_load_twobit_runs(gac_ctx *c, int which, gac_twobit *tb, const uint8_t *keep,
+                                const int64_t *run_off, const int32_t *run_lo, const int32_t *run_hi) {
+    (void)keep; /* the host stand-in keeps every sequence */
+    int rc = gac_genome_load_twobit(c, which, tb);
+    if (rc != GAC_OK || !run_off)
+        return rc;
+    /* words outside the runs are poisoned (a different base pattern), so a
+     * run set that misses a word the scoring reads changes the scores */
+    side *s = &c->s[which];
+    const int all = getenv("GAC_STUB_POISON_ALL") != NULL; /* tests the check itself */
+    for (int32_t i = 0; i < s->n; ++i) {
+        const size_t nb = ((size_t)s->sizes[i] + 3) / 4;
+        uint8_t *p = malloc(nb + 8);
+        memset(p, 0x9c, nb + 8);
+        for (int64_t r = run_off[i]; r < run_off[i + 1] && !all; ++r) {
+            const size_t b0 = (size_t)run_lo[r] * 8, b1 = (size_t)run_hi[r] * 8;
+            memcpy(p + b0, s->packed[i] + b0, (b1 < nb ? b1 : nb) - b0);
+        }
+        s->packed[i] = p;
+    }
+    return GAC_OK;
+}
+
 int gac_genome_load_twobit_keep(gac_ctx *c, int which, gac_twobit *tb, const uint8_t *keep) {
     (void)keep; /* the axtChain front end loads whole files */
     return gac_genome_load_twobit(c, which, tb);
@@ -220,21 +243,30 @@ void gac_chains_free(gac_chainset *s) {
     free(s);
 }
 
-/* whole-chain ranges only (what gac_axt_chain asks for) */
+/* the chain's blocks clipped to [t_start, t_end) on the target, scored with
+ * the linear gap costs between consecutive clipped blocks (whole chains for
+ * gac_axt_chain; chainNet's partial fills) */
 int gac_score_ranges(gac_ctx *c, const gac_chainset *s, const gac_range *r, int64_t n,
                      uint32_t flags, int64_t *g, int64_t *l, int32_t *ali) {
     (void)flags;
     (void)l;
     for (int64_t i = 0; i < n; ++i) {
-        const int32_t k = r[i].chain;
+        const int32_t k = r[i].chain, lo = r[i].t_start, hi = r[i].t_end;
         int64_t sc = 0;
-        int32_t a = 0;
+        int32_t a = 0, have = 0, pq = 0, pt = 0;
         for (int64_t b = s->off[k]; b < s->off[k + 1]; ++b) {
-            sc += block_score(c, s->tseq[k], s->qseq[k], s->strand[k], s->bt[b], s->bq[b], s->bs[b]);
-            a += s->bs[b];
-            if (b + 1 < s->off[k + 1])
-                sc -= gac_gap_cost(c->g, s->bq[b + 1] - (s->bq[b] + s->bs[b]),
-                                   s->bt[b + 1] - (s->bt[b] + s->bs[b]));
+            const int32_t t0 = s->bt[b] > lo ? s->bt[b] : lo;
+            const int32_t t1 = s->bt[b] + s->bs[b] < hi ? s->bt[b] + s->bs[b] : hi;
+            if (t1 <= t0)
+                continue;
+            const int32_t q0 = s->bq[b] + (t0 - s->bt[b]);
+            if (have)
+                sc -= gac_gap_cost(c->g, q0 - pq, t0 - pt);
+            sc += block_score(c, s->tseq[k], s->qseq[k], s->strand[k], t0, q0, t1 - t0);
+            a += t1 - t0;
+            pq = q0 + (t1 - t0);
+            pt = t1;
+            have = 1;
         }
         g[i] = sc;
         ali[i] = a;
