@@ -802,6 +802,7 @@ int main(int argc, char *argv[]) {
             jobs = argv[i] + 6;
     ax_batch B;
     memset(&B, 0, sizeof(B));
+    gt_one_device(); /* device 0 only (before any thread or HIP call) */
     if (!jobs) {
         run_job(argc, argv, &B); /* exits */
         return 0;

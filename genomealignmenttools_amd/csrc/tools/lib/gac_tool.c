@@ -156,10 +156,12 @@ static void *device_thread(void *arg) {
         }
         const gt_runs *R = NULL;
         if (rc == GAC_OK && d->runs) { /* the word runs the chains need */
+            const double w0 = now_s();
             pthread_mutex_lock(&d->runs->mu);
             while (!d->runs->ready)
                 pthread_cond_wait(&d->runs->cv, &d->runs->mu);
             pthread_mutex_unlock(&d->runs->mu);
+            d->runs_wait_s += now_s() - w0;
             if (d->runs->ok < 0) { /* the tool is aborting: skip the upload */
                 gac_twobit_close(&P.tb[k]);
                 free(keep);
@@ -203,9 +205,35 @@ typedef struct runs_mark {
     _Atomic int64_t next;
 } runs_mark;
 
+/* set bits [w0, w1): one atomic OR per 64-bit bitmap word, skipped when its
+ * bits are set already (dense regions are marked by many chains) */
 static void mark_words(_Atomic uint64_t *bits, int64_t w0, int64_t w1) {
-    for (int64_t w = w0; w < w1; ++w)
-        atomic_fetch_or_explicit(&bits[w >> 6], 1ull << (w & 63), memory_order_relaxed);
+    for (int64_t i = w0 >> 6; w0 < w1; ++i) {
+        const int64_t hi = (i + 1) << 6 < w1 ? (i + 1) << 6 : w1;
+        const int lo_b = (int)(w0 & 63), n = (int)(hi - w0);
+        const uint64_t m = (n == 64 ? ~0ull : ((1ull << n) - 1ull)) << lo_b;
+        if ((atomic_load_explicit(&bits[i], memory_order_relaxed) & m) != m)
+            atomic_fetch_or_explicit(&bits[i], m, memory_order_relaxed);
+        w0 = hi;
+    }
+}
+
+/* a chain's word intervals on one side, merged while they touch (the blocks
+ * of a chain are co-linear: mostly one interval per run of close blocks) */
+typedef struct word_span {
+    int64_t a, b; /* pending [a, b), a == b: none */
+} word_span;
+
+static void span_add(word_span *p, _Atomic uint64_t *bits, int64_t a, int64_t b) {
+    if (p->a < p->b && a <= p->b && b >= p->a) {
+        p->a = a < p->a ? a : p->a;
+        p->b = b > p->b ? b : p->b;
+        return;
+    }
+    if (p->a < p->b)
+        mark_words(bits, p->a, p->b);
+    p->a = a;
+    p->b = b;
 }
 
 static void *runs_mark_thread(void *arg) {
@@ -218,24 +246,29 @@ static void *runs_mark_thread(void *arg) {
         const int64_t b = a + 1024 < c->n ? a + 1024 : c->n;
         for (int64_t i = a; i < b; ++i) {
             const int32_t ts = M->tmap[c->tname[i]], qs = M->qmap[c->qname[i]];
+            word_span pt = {0, 0}, pq = {0, 0};
             for (int64_t k = c->blk_off[i]; k < c->blk_off[i + 1]; ++k) {
                 const int64_t z = c->bs[k];
                 if (z <= 0)
                     continue;
-                if (ts >= 0) {
+                if (ts >= 0) { /* the kernel reads the block's words and the next one */
                     const int64_t t = c->bt[k];
                     const int64_t nw = ((int64_t)M->tsize[ts] + 31) / 32;
                     const int64_t w1 = ((t + z - 1) >> 5) + 2;
-                    mark_words(M->tbits, M->twoff[ts] + (t >> 5), M->twoff[ts] + (w1 < nw ? w1 : nw));
+                    span_add(&pt, M->tbits, M->twoff[ts] + (t >> 5), M->twoff[ts] + (w1 < nw ? w1 : nw));
                 }
-                if (qs >= 0) {
+                if (qs >= 0) { /* '-': the forward coordinates of the block */
                     const int64_t q = c->bq[k], qz = M->qsize[qs];
                     const int64_t f0 = c->qstrand[i] ? qz - (q + z) : q, f1 = f0 + z;
                     const int64_t nw = (qz + 31) / 32;
                     const int64_t w1 = ((f1 - 1) >> 5) + 2;
-                    mark_words(M->qbits, M->qwoff[qs] + (f0 >> 5), M->qwoff[qs] + (w1 < nw ? w1 : nw));
+                    span_add(&pq, M->qbits, M->qwoff[qs] + (f0 >> 5), M->qwoff[qs] + (w1 < nw ? w1 : nw));
                 }
             }
+            if (pt.a < pt.b)
+                mark_words(M->tbits, pt.a, pt.b);
+            if (pq.a < pq.b)
+                mark_words(M->qbits, pq.a, pq.b);
         }
     }
     return NULL;
@@ -261,8 +294,18 @@ static void bits_to_runs(const _Atomic uint64_t *bits, const int64_t *woff, int3
             if (w >= end)
                 break;
             const int64_t r0 = w;
-            while (w < end && ((atomic_load_explicit(&bits[w >> 6], memory_order_relaxed) >> (w & 63)) & 1))
-                ++w;
+            for (;;) { /* to the next clear bit (or the sequence's end) */
+                const uint64_t y = ~atomic_load_explicit(&bits[w >> 6], memory_order_relaxed) >> (w & 63);
+                if (y) {
+                    w += __builtin_ctzll(y);
+                    break;
+                }
+                w = (w | 63) + 1;
+                if (w >= end)
+                    break;
+            }
+            if (w > end)
+                w = end;
             if (n == cap) {
                 cap *= 2;
                 lo = realloc(lo, (size_t)cap * 4);
@@ -281,6 +324,7 @@ static void bits_to_runs(const _Atomic uint64_t *bits, const int64_t *woff, int3
 }
 
 void gt_runs_build(gt_runs *R, const gt_chains *c, const char *t2bit, const char *q2bit) {
+    const double t0 = now_s();
     gac_twobit tb[2];
     int ok = gac_twobit_open_ex(t2bit, &tb[0], 0) == GAC_OK;
     if (ok && gac_twobit_open_ex(q2bit, &tb[1], 0) != GAC_OK) {
@@ -324,10 +368,26 @@ void gt_runs_build(gt_runs *R, const gt_chains *c, const char *t2bit, const char
         }
     }
     pthread_mutex_lock(&R->mu);
+    R->build_s = now_s() - t0;
     R->ok = ok;
     R->ready = 1;
     pthread_cond_broadcast(&R->cv);
     pthread_mutex_unlock(&R->mu);
+}
+
+/* A tool drives one device: unless the caller chose the visible devices,
+ * show the runtime only that one, so that its start-up initialises one GPU
+ * rather than every GPU of the node.  Before any HIP call and before other
+ * threads run (setenv); idempotent. */
+void gt_one_device(void) {
+    if (getenv("ROCR_VISIBLE_DEVICES") || getenv("HIP_VISIBLE_DEVICES") ||
+        getenv("CUDA_VISIBLE_DEVICES") || getenv("GPU_DEVICE_ORDINAL") ||
+        getenv("GAC_ALL_DEVICES") || g_gpu < 0)
+        return;
+    char b[16];
+    snprintf(b, sizeof(b), "%d", g_gpu);
+    setenv("ROCR_VISIBLE_DEVICES", b, 1);
+    g_gpu = 0;
 }
 
 void gt_device_start(gt_device *d, const char *t2bit, const char *q2bit, const int32_t mat[16],
@@ -342,6 +402,7 @@ void gt_device_start_keep(gt_device *d, const char *t2bit, const char *q2bit,
 
 void gt_device_start_ex(gt_device *d, const char *t2bit, const char *q2bit, const int32_t mat[16],
                         const gac_gapcalc *gap, const gt_names *tkeep, gt_runs *runs) {
+    gt_one_device();
     memset(d, 0, sizeof(*d));
     d->tkeep = tkeep;
     d->runs = runs;
@@ -428,8 +489,14 @@ gac_ctx *gt_device_join(gt_device *d) {
     device_wait_done(d);
     if (d->rc != GAC_OK)
         gt_abort("%s\n", d->err);
-    gt_verbose(2, "[stage] (overlapped) device open %.3f s, 2bit genomes to HBM %.3f s\n",
-               d->open_s, d->load_s);
+    if (d->runs)
+        gt_verbose(2, "[stage] (overlapped) device open %.3f s, 2bit genomes to HBM %.3f s "
+                      "(of which waiting for the word runs %.3f s; runs built in %.3f s, %lld + %lld words)\n",
+                   d->open_s, d->load_s, d->runs_wait_s, d->runs->build_s,
+                   (long long)d->runs->words[0], (long long)d->runs->words[1]);
+    else
+        gt_verbose(2, "[stage] (overlapped) device open %.3f s, 2bit genomes to HBM %.3f s\n",
+                   d->open_s, d->load_s);
     return d->ctx;
 }
 

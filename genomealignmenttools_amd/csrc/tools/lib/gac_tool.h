@@ -30,6 +30,10 @@ void gt_check(int rc); /* abort with gac_last_error() unless GAC_OK */
 void gt_on_abort(void (*fn)(void));
 /* device index gt_device_start opens (default 0) */
 void gt_set_gpu(int gpu);
+/* expose only that device to the runtime (ROCR_VISIBLE_DEVICES) unless a
+ * visibility list is already set; main thread, before any HIP call (the
+ * device start calls it) */
+void gt_one_device(void);
 
 /* ---- device bring-up off the critical path ----
  * gt_device_start opens device 0, sets the scoring scheme and uploads both
@@ -50,6 +54,7 @@ typedef struct gt_runs {
     int64_t *off[2];
     int32_t *lo[2], *hi[2];
     int64_t words[2]; /* words uploaded (diagnostics) */
+    double build_s;
 } gt_runs;
 
 typedef struct gt_device {
@@ -58,7 +63,7 @@ typedef struct gt_device {
     const gac_gapcalc *gap;
     gac_ctx *ctx;
     int rc, started, rc_err_set;
-    double open_s, load_s;
+    double open_s, load_s, runs_wait_s;
     char err[1024];
     /* bring-up completion: the (detached) device thread sets done under mu
      * and broadcasts cv; any number of threads may wait for it */
