@@ -361,12 +361,15 @@ int main(int argc, char *argv[]) {
      * it rescores target fills) */
     gt_device dev;
     memset(&dev, 0, sizeof(dev));
-    /* -rescore uploads only the genome words under the chains' blocks (about
-     * a tenth of a whole-genome query): the device thread opens the context
-     * and maps the .2bit files while the chains are read, then waits for the
-     * word runs (GAC_NET_SPARSE=0: upload both genomes whole) */
+    /* GAC_NET_SPARSE=1: upload only the genome words under the chains'
+     * blocks (a tenth of a whole-genome query; for genomes that crowd HBM):
+     * the device thread opens the context and maps the .2bit files while the
+     * chains are read, then waits for the word runs.  Off by default: the
+     * whole upload overlaps HIP start-up anyway, and building the runs costs
+     * host time (C2: 274 vs 288 ms median single-GPU, 860-879 vs 871-927 ms
+     * with 4 ranks on one GPU; profiles/r02h_sparse) */
     const char *sp = getenv("GAC_NET_SPARSE");
-    const int sparse = rescore && !(sp && *sp == '0');
+    const int sparse = rescore && sp && *sp == '1';
     gt_runs runs;
     gt_runs_init(&runs);
     if (rescore && !multi)

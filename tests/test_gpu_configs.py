@@ -45,9 +45,9 @@ def _ref(name):
     return p
 
 
-def _run(cmd, cwd=None, rc=0, timeout=900):
+def _run(cmd, cwd=None, rc=0, timeout=900, env=None):
     r = subprocess.run([str(c) for c in cmd], capture_output=True, text=True, timeout=timeout,
-                       cwd=cwd)
+                       cwd=cwd, env=dict(os.environ, **env) if env else None)
     assert r.returncode == rc, (cmd[0], r.returncode, r.stderr[-2000:])
     return r
 
@@ -142,6 +142,18 @@ def test_c5_shaped_chainnet_rescore(c5_dir, c5_ref_nets):
           "-linearGap=loose"])
     _same(p("c5.t.net"), c5_ref_nets[0])
     _same(p("c5.q.net"), c5_ref_nets[1])
+
+
+@pytest.mark.timeout(900)
+def test_c5_shaped_chainnet_rescore_sparse(c5_dir, c5_ref_nets):
+    """GAC_NET_SPARSE=1: only the genome words under the chains' blocks go
+    to HBM (word runs from the host, k_scatter into the plane layout)."""
+    p = lambda x: os.path.join(c5_dir, x)
+    _run([_bin("chainNet"), p("in.chain"), p("t.sizes"), p("q.sizes"), p("sp.t.net"),
+          p("sp.q.net"), "-rescore", f"-tNibDir={p('t.2bit')}", f"-qNibDir={p('q.2bit')}",
+          "-linearGap=loose"], env={"GAC_NET_SPARSE": "1"})
+    _same(p("sp.t.net"), c5_ref_nets[0])
+    _same(p("sp.q.net"), c5_ref_nets[1])
 
 
 @pytest.mark.timeout(900)

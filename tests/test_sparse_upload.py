@@ -5,7 +5,8 @@ The tool uploads only the 32-base words under its chains' blocks
 real tool linked against the CPU stand-in of the device ABI
 (oracle/cpu_gac_stub.c), which poisons every word outside the runs: a run set
 that misses a word the fill rescoring reads changes a score.  The nets must
-equal the whole-genome run (GAC_NET_SPARSE=0) and, when it is built, the
+equal the whole-genome run (the default; GAC_NET_SPARSE=1 turns the sparse
+upload on) and, when it is built, the
 reference chainNet (oracle/_ref).  TEST INFRASTRUCTURE only.
 """
 import filecmp
@@ -58,7 +59,7 @@ def _net(exe, d, tag, env=None, extra=()):
 def test_sparse_runs_cover_rescoring(tool, tmp_path, kind, seed):
     d = str(tmp_path)
     _case(d, kind, seed)
-    sparse = _net(tool, d, "sparse")
+    sparse = _net(tool, d, "sparse", env={"GAC_NET_SPARSE": "1"})
     whole = _net(tool, d, "whole", env={"GAC_NET_SPARSE": "0"})
     for a, b in zip(sparse, whole):
         assert filecmp.cmp(a, b, shallow=False), f"{a} differs from {b}"
@@ -79,5 +80,5 @@ def test_poisoned_words_change_scores(tool, tmp_path):
     d = str(tmp_path)
     _case(d, "small", 3)
     whole = _net(tool, d, "whole", env={"GAC_NET_SPARSE": "0"})
-    poisoned = _net(tool, d, "poison", env={"GAC_STUB_POISON_ALL": "1"})
+    poisoned = _net(tool, d, "poison", env={"GAC_NET_SPARSE": "1", "GAC_STUB_POISON_ALL": "1"})
     assert not filecmp.cmp(whole[0], poisoned[0], shallow=False)
