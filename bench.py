@@ -87,6 +87,10 @@ def parse():
                         "them), (chain, tStart), target start, or (query sequence, forward "
                         "query position) order")
     p.add_argument("--tmp", default=os.environ.get("TMPDIR", "/tmp"))
+    p.add_argument("--no-pmc", action="store_true",
+                   help="roofline.traffic from the committed profile instead of this run's "
+                        "rocprofv3 counter passes")
+    p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--gen-only", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--replicas", type=int, default=1, help=argparse.SUPPRESS)
     return p.parse_args()
@@ -221,17 +225,18 @@ def run_tool(cmd, outs, env=None):
 
 
 # ---------------------------------------------------------------- kernel leg
-def kernel_leg(args, d, steps):
-    """The GPU rescoring call alone (inputs resident in HBM), HIP-event timed:
-    the roofline of k_tile and a per-kernel breakdown."""
+def kernel_ranges(args, d):
+    """The kernel leg's chain set and ranges (host only, no device): the C2
+    partial target fills (or whole chains), in the --order order; cached as
+    .npy beside the input for the counter passes' child processes."""
     from genomealignmenttools_amd import chainfile
-    from genomealignmenttools_amd._lib import GAC_K_COMBINE, GAC_K_PLAN, GAC_K_TILE
     from genomealignmenttools_amd.chainnet import net_fills
-    from genomealignmenttools_amd.gachain import GAC_Q, GAC_T, Engine, GapCosts
     from genomealignmenttools_amd.synth import read_sizes
     p = lambda x: os.path.join(d, x)
-    t0 = time.time()
     ca = chainfile.read_chains(p("in.chain"))
+    cache = p(f"ranges.{args.workload}.{args.order}.npy")
+    if os.path.exists(cache):
+        return ca, np.load(cache)
     if args.workload == "scorechain":
         ranges = np.stack([np.arange(ca.n, dtype=np.int32), ca.tstart, ca.tend], 1)
     else:
@@ -245,6 +250,19 @@ def kernel_leg(args, d, steps):
     elif args.order == "q":
         ranges = ranges[np.lexsort(_query_key(ca, ranges)[::-1])]
     ranges = np.ascontiguousarray(ranges, np.int32)
+    np.save(cache + ".tmp.npy", ranges)
+    os.rename(cache + ".tmp.npy", cache)
+    return ca, ranges
+
+
+def kernel_leg(args, d, steps, ca, ranges, pmc=None):
+    """The GPU rescoring call alone (inputs resident in HBM), HIP-event timed:
+    the roofline of k_tile and a per-kernel breakdown.  pmc: this run's
+    counter-pass traffic (pmc_traffic) or None."""
+    from genomealignmenttools_amd._lib import GAC_K_COMBINE, GAC_K_PLAN, GAC_K_TILE
+    from genomealignmenttools_amd.gachain import GAC_Q, GAC_T, Engine, GapCosts
+    p = lambda x: os.path.join(d, x)
+    t0 = time.time()
     e = Engine(int(os.environ.get("LOCAL_RANK", "0")))
     e.load_2bit(GAC_T, p("t.2bit"))
     e.load_2bit(GAC_Q, p("q.2bit"))
@@ -300,9 +318,92 @@ def kernel_leg(args, d, steps):
               "window_blocks": nblk,
               "kernel_ms": kern_ms}
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": _pmc_traffic(args, n, nblk),
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
             "kernel": "k_tile", "kernel_avg_ms": tile_s * 1e3, "algo_bytes_per_launch": algo}
+    if pmc and pmc.get("hbm_bytes"):
+        roof["traffic"] = pmc["hbm_bytes"]
+        roof["traffic_source"] = pmc["source"]
+        roof["traffic_over_algo"] = pmc["hbm_bytes"] / algo
+        roof["traffic_kernel_avg_ms"] = pmc.get("avg_ms")
+    else:
+        roof["traffic"] = _pmc_traffic(args, n, nblk)
+        if roof["traffic"]:
+            roof["traffic_source"] = "committed profile " + os.path.relpath(TRAFFIC_FILE, REPO)
     return kernel, roof
+
+
+PMC_PASSES = ("TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum",
+              "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum")
+
+
+def pmc_traffic(args):
+    """HBM-side bytes per k_tile launch, measured in this run: two rocprofv3
+    --kernel-trace --pmc passes (no other trace domains; 3 and 2 TCC counters)
+    over a child process that runs the kernel leg's call.  Bytes by request
+    size, as MI355X_MICROARCH.md's HBM section prescribes for gfx950 (not
+    FETCH_SIZE, which tallies every request at 64 B): reads = 32 n32 + 64 n64
+    + 128 n128, writes = 64 n64 + 32 (n - n64).  Run before this process
+    touches the GPU.  Returns None on any failure (reported, never fatal)."""
+    import csv
+    import glob
+    import shutil
+    import tempfile
+    if not shutil.which("rocprofv3"):
+        return None
+    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--chains", str(args.chains),
+             "--seed", str(args.seed), "--workload", args.workload, "--order", args.order,
+             "--tmp", args.tmp]
+    vals, durs = {}, []
+    root = tempfile.mkdtemp(prefix="gac_pmc_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    for i, counters in enumerate(PMC_PASSES):
+        out = os.path.join(root, f"pass{i}")
+        cmd = ["timeout", "-s", "KILL", "180", "rocprofv3", "--kernel-trace", "--pmc",
+               *counters.split(), "--output-format", "csv", "-d", out, "-o", "run", "--", *child]
+        r = subprocess.run(cmd, capture_output=True, text=True, cwd="/tmp", env=env, timeout=240)
+        if r.returncode != 0:
+            log(f"pmc pass {i} rc={r.returncode}: {r.stderr[-800:]}")
+            return None
+        per = {}
+        for path in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+            with open(path) as f:
+                for row in csv.DictReader(f):
+                    if "k_tile<" not in row["Kernel_Name"]:  # (not k_tilemap*)
+                        continue
+                    key = (row["Dispatch_Id"], row["Counter_Name"])
+                    per[key] = per.get(key, 0.0) + float(row["Counter_Value"])
+        by = {}
+        for (_, c), v in per.items():
+            by.setdefault(c, []).append(v)
+        if not by:
+            log(f"pmc pass {i}: no k_tile rows")
+            return None
+        vals.update({c: sum(v) / len(v) for c, v in by.items()})
+        for path in glob.glob(os.path.join(out, "**", "*kernel_trace.csv"), recursive=True):
+            with open(path) as f:
+                for row in csv.DictReader(f):
+                    if "k_tile<" in row["Kernel_Name"]:
+                        durs.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    shutil.rmtree(root, ignore_errors=True)
+    try:
+        rd = (32.0 * vals["TCC_EA0_RDREQ_32B_sum"] + 64.0 * vals["TCC_EA0_RDREQ_64B_sum"]
+              + 128.0 * vals["TCC_EA0_RDREQ_128B_sum"])
+        w64 = vals["TCC_EA0_WRREQ_64B_sum"]
+        wr = 64.0 * w64 + 32.0 * (vals["TCC_EA0_WRREQ_sum"] - w64)
+    except KeyError as ex:
+        log(f"pmc: missing counter {ex}")
+        return None
+    return {"hbm_bytes": rd + wr, "hbm_read_bytes": rd, "hbm_write_bytes": wr,
+            "avg_ms": (sum(durs) / len(durs) / 1e6) if durs else None,
+            "source": "this run: rocprofv3 --kernel-trace --pmc " + " | ".join(PMC_PASSES)
+                      + " (k_tile dispatches, mean)"}
+
+
+def pmc_child(args):
+    """The counter passes' workload: the kernel leg's call, a few times."""
+    d, _ = c2_files(args)
+    ca, ranges = kernel_ranges(args, d)
+    kernel_leg(args, d, 3, ca, ranges)
 
 
 TRAFFIC_FILE = os.path.join(REPO, "profiles", "k_tile_traffic.json")
@@ -479,6 +580,9 @@ def main():
         if args.replicas > 1:
             c2n_files(args, args.replicas)
         return
+    if args.pmc_child:
+        pmc_child(args)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -562,7 +666,10 @@ def main():
                "scaling": "weak", "vs_baseline": None, "dtype": "int64",
                "data": "synthetic (seeded C2)", "config": {"workload": args.workload, **info}}
     if rank == 0 and not args.no_kernel:
-        kernel, roof = kernel_leg(args, d, args.kernel_steps)
+        ca, ranges = kernel_ranges(args, d)
+        # counter passes in child processes before this one opens the device
+        pmc = None if (args.no_pmc or world > 1) else pmc_traffic(args)
+        kernel, roof = kernel_leg(args, d, args.kernel_steps, ca, ranges, pmc)
         out["kernel"] = kernel
         out["roofline"] = roof
         if args.workload != "chainnet":  # the kernel call itself is the step
