@@ -65,6 +65,39 @@ def test_chainnet_rescore_synth(seed, tmp_path):
     assert filecmp.cmp(tmp_path / "q.net", p("rescore.q.net"), shallow=False)
 
 
+@pytest.mark.parametrize("mode", ["gz", "stdin"])
+def test_stream_inputs_and_stdout(mode, tmp_path):
+    """kent file-name conventions on the GPU tools: a .gz chain file (read
+    through gzip, lineFileOpen) or `stdin` as the input, `stdout` as
+    scoreChain's output; same bytes as the reference's goldens."""
+    import gzip
+    import shutil
+    d = os.path.join(GOLDEN, "synth11")
+    p = lambda x: os.path.join(d, x)
+    src = p("in.chain")
+    if mode == "gz":
+        with open(src, "rb") as f, gzip.open(tmp_path / "in.chain.gz", "wb") as g:
+            shutil.copyfileobj(f, g)
+        src = str(tmp_path / "in.chain.gz")
+
+    def run(cmd):
+        with open(p("in.chain"), "rb") as fin:
+            r = subprocess.run([c if c != "IN" else ("stdin" if mode == "stdin" else src)
+                                for c in cmd], stdin=fin if mode == "stdin" else None,
+                               capture_output=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return r.stdout
+
+    out = run([_bin("scoreChain"), "IN", p("t.2bit"), p("q.2bit"), "stdout", "-linearGap=loose",
+               "-returnOnlyScoreAndCoords"])
+    assert out == open(p("score.out"), "rb").read()
+    run([_bin("chainNet"), "IN", p("t.sizes"), p("q.sizes"), str(tmp_path / "t.net"),
+         str(tmp_path / "q.net"), "-rescore", f"-tNibDir={p('t.2bit')}", f"-qNibDir={p('q.2bit')}",
+         "-linearGap=loose"])
+    assert filecmp.cmp(tmp_path / "t.net", p("rescore.t.net"), shallow=False)
+    assert filecmp.cmp(tmp_path / "q.net", p("rescore.q.net"), shallow=False)
+
+
 @pytest.mark.parametrize("seed", [11, 12])
 @pytest.mark.parametrize("tag,opts", [("ms1", ["-minSpace=1", "-minScore=0"]),
                                       ("ms100", ["-minSpace=100", "-minFill=10"])])

@@ -484,3 +484,54 @@ def test_net_write_two_phase(tmp_path):
     h = C.c_void_p()
     assert lib().gac_net_write_begin(nb.h, 0, None, 0, C.byref(h)) != 0
     nb.close()
+
+
+def _hap_case(d):
+    """A small set whose query names include haplotype/alt sequences."""
+    from genomealignmenttools_amd import chainfile, synth
+    tg, qg, ca = synth.small_case(seed=21, n_chains=300)
+    ren = {"chrQ2": "chrQ2_hap1", "chrQ3": "chrQ3_alt"}
+    qsizes = {ren.get(k, k): v for k, v in qg.sizes.items()}
+    ca.qname = [ren.get(n, n) for n in ca.qname]
+    synth.write_sizes(tg.sizes, os.path.join(d, "t.sizes"))
+    synth.write_sizes(qsizes, os.path.join(d, "q.sizes"))
+    chainfile.write_chains(ca, os.path.join(d, "in.chain"))
+
+
+@pytest.mark.parametrize("mode", ["plain", "inclHap", "gz", "stdin"])
+def test_chainnet_input_modes_vs_reference(mode, tmp_path):
+    """chainNet's haplotype filter (`_hap`/`_alt` query names skipped unless
+    -inclHap, chainNet.c:253-257), a .gz chain file (read through gzip like
+    lineFileOpen) and `stdin` as the chain file name, against the reference
+    chainNet (oracle/_ref) on the same input.  Plain netting: no device."""
+    import gzip
+    import shutil
+    from genomealignmenttools_amd._lib import BIN_DIR
+    from oracle.oracle import ref_tool
+    ref = ref_tool("chainNet")
+    if not os.path.exists(ref):
+        pytest.skip("oracle/_ref/chainNet not built (make ref)")
+    d = str(tmp_path)
+    _hap_case(d)
+    p = lambda x: os.path.join(d, x)
+    chain = p("in.chain")
+    opts = ["-inclHap"] if mode == "inclHap" else []
+    if mode == "gz":
+        with open(chain, "rb") as f, gzip.open(p("in.chain.gz"), "wb") as g:
+            shutil.copyfileobj(f, g)
+        chain = p("in.chain.gz")
+    outs = {}
+    for tag, exe in (("ours", os.path.join(BIN_DIR, "chainNet")), ("ref", ref)):
+        src = "stdin" if mode == "stdin" else chain
+        with open(p("in.chain"), "rb") as fin:
+            r = subprocess.run([exe, src, p("t.sizes"), p("q.sizes"), p(f"{tag}.t.net"),
+                                p(f"{tag}.q.net")] + opts,
+                               stdin=fin if mode == "stdin" else None, capture_output=True)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs[tag] = [open(p(f"{tag}.{s}.net"), "rb").read() for s in "tq"]
+    assert outs["ours"] == outs["ref"]
+    qnet = outs["ours"][1].decode()
+    if mode == "inclHap":
+        assert "chrQ2_hap1" in qnet
+    else:  # the haplotype query sides are netted only with -inclHap
+        assert "net chrQ2_hap1" not in qnet
