@@ -274,9 +274,12 @@ static void *runs_mark_thread(void *arg) {
     return NULL;
 }
 
-/* runs of set bits of each sequence, CSR by sequence */
+/* runs of set bits of each sequence, CSR by sequence; runs less than `gap`
+ * words apart are merged (fewer, longer copies: the upload's cost per run
+ * outweighs a few KB of extra bases) */
 static void bits_to_runs(const _Atomic uint64_t *bits, const int64_t *woff, int32_t nseq,
-                         int64_t **off_out, int32_t **lo_out, int32_t **hi_out, int64_t *words) {
+                         int64_t gap, int64_t **off_out, int32_t **lo_out, int32_t **hi_out,
+                         int64_t *words) {
     int64_t *off = malloc((size_t)(nseq + 1) * 8), cap = 1024, n = 0;
     int32_t *lo = malloc((size_t)cap * 4), *hi = malloc((size_t)cap * 4);
     *words = 0;
@@ -306,6 +309,11 @@ static void bits_to_runs(const _Atomic uint64_t *bits, const int64_t *woff, int3
             }
             if (w > end)
                 w = end;
+            if (n > off[s] && r0 - (woff[s] + hi[n - 1]) < gap) { /* close to the last run */
+                *words += w - (woff[s] + hi[n - 1]);
+                hi[n - 1] = (int32_t)(w - woff[s]);
+                continue;
+            }
             if (n == cap) {
                 cap *= 2;
                 lo = realloc(lo, (size_t)cap * 4);
@@ -356,9 +364,12 @@ void gt_runs_build(gt_runs *R, const gt_chains *c, const char *t2bit, const char
         }
         runs_mark M = {c, map[0], map[1], woff[0], woff[1], size[0], size[1], bits[0], bits[1], 0};
         atomic_init(&M.next, 0);
-        gac_run_threads(gt_threads(), runs_mark_thread, &M);
+        /* a few threads: this runs beside the netting, off the critical path */
+        gac_run_threads(gt_threads() < 4 ? gt_threads() : 4, runs_mark_thread, &M);
+        const char *gs = getenv("GAC_RUN_GAP"); /* words (32 bases); default 64 */
+        const int64_t gap = gs && *gs ? atoll(gs) : 64;
         for (int k = 0; k < 2; ++k) {
-            bits_to_runs(bits[k], woff[k], (int32_t)tb[k].seq_count, &R->off[k], &R->lo[k],
+            bits_to_runs(bits[k], woff[k], (int32_t)tb[k].seq_count, gap, &R->off[k], &R->lo[k],
                          &R->hi[k], &R->words[k]);
             free(bits[k]);
             free(woff[k]);
