@@ -25,6 +25,7 @@
 #include <string.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <time.h>
 #include <unistd.h>
 
 /* ------------------------------------------------------------------ errors */
@@ -802,6 +803,95 @@ int gac_par_format(int64_t nr, void (*fn)(FILE *f, int64_t r, void *arg), void *
     return atomic_load(&J.oom) ? -1 : 0;
 }
 
+/* Large outputs into a regular file: every run formatted first, then copied
+ * into a shared mapping of the reserved file range by all threads.  Buffered
+ * write() calls into one file serialise on its inode lock (≈1.4 GB/s for a
+ * GB-scale .chain/.net on the GPU box); page faults on a mapping do not.
+ * GAC_OUTPUT_MMAP_MIN = the size from which it is used (bytes, default
+ * 64 MB; 0 = always, -1 = never). */
+static long long output_mmap_min(void) {
+    const char *s = getenv("GAC_OUTPUT_MMAP_MIN");
+    return s && *s ? atoll(s) : (64ll << 20);
+}
+
+typedef struct mcopy_job {
+    char *dst;
+    char **buf;
+    const size_t *len, *pre;
+    int64_t nr;
+    size_t total, chunk;
+    _Atomic size_t next;
+} mcopy_job;
+
+static void *mcopy_thread(void *p) {
+    mcopy_job *M = p;
+    for (;;) {
+        size_t a = atomic_fetch_add(&M->next, M->chunk);
+        if (a >= M->total)
+            break;
+        const size_t b = a + M->chunk < M->total ? a + M->chunk : M->total;
+        int64_t lo = 0, hi = M->nr - 1; /* last run starting at or before a */
+        while (lo < hi) {
+            const int64_t mid = (lo + hi + 1) / 2;
+            if (M->pre[mid] <= a)
+                lo = mid;
+            else
+                hi = mid - 1;
+        }
+        for (int64_t r = lo; a < b && r < M->nr; ++r) {
+            const size_t s0 = M->pre[r], s1 = s0 + M->len[r];
+            if (s1 <= a)
+                continue;
+            const size_t e = s1 < b ? s1 : b;
+            memcpy(M->dst + a, M->buf[r] + (a - s0), e - a);
+            a = e;
+        }
+    }
+    return NULL;
+}
+
+/* 1: written; 0: not possible here (the caller writes with fwrite); -1: error */
+static int par_output_mapped(FILE *out, char **buf, const size_t *len, int64_t nr, size_t total) {
+    const int fd = fileno(out);
+    if (fflush(out) != 0)
+        return -1;
+    const off_t off0 = ftello(out);
+    if (off0 < 0 || posix_fallocate(fd, off0, (off_t)total) != 0)
+        return 0; /* (no space: the fwrite path reports it) */
+    char path[64];
+    snprintf(path, sizeof(path), "/proc/self/fd/%d", fd);
+    const int rw = open(path, O_RDWR); /* a shared writable mapping needs read access too */
+    if (rw < 0)
+        return 0;
+    const long pg = sysconf(_SC_PAGESIZE);
+    const off_t pa = off0 & ~(off_t)(pg - 1);
+    const size_t mlen = (size_t)(off0 - pa) + total;
+    char *m = mmap(NULL, mlen, PROT_READ | PROT_WRITE, MAP_SHARED, rw, pa);
+    close(rw);
+    if (m == MAP_FAILED)
+        return 0;
+    size_t *pre = malloc((size_t)nr * sizeof(size_t));
+    size_t acc = 0;
+    for (int64_t r = 0; r < nr; ++r) {
+        pre[r] = acc;
+        acc += len[r];
+    }
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    mcopy_job M = {m + (off0 - pa), buf, len, pre, nr, total, 4u << 20, 0};
+    atomic_init(&M.next, 0);
+    gac_run_threads(gac_host_threads(), mcopy_thread, &M);
+    free(pre);
+    const int bad = munmap(m, mlen) != 0;
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (getenv("GAC_TIMING"))
+        fprintf(stderr, "[gac_par_output] %zu bytes copied through a mapping in %.3f s\n", total,
+                (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec));
+    if (fseeko(out, off0 + (off_t)total, SEEK_SET) != 0 || bad)
+        return -1;
+    return 1;
+}
+
 int gac_par_output(FILE *out, int64_t nr, void (*fn)(FILE *f, int64_t r, void *arg), void *arg) {
     if (nr <= 0)
         return 0;
@@ -823,7 +913,39 @@ int gac_par_output(FILE *out, int64_t nr, void (*fn)(FILE *f, int64_t r, void *a
     for (int i = 0; i < nt; ++i)
         pthread_create(&th[i], NULL, po_thread, &J);
     int bad = 0;
-    for (int64_t r = 0; r < nr; ++r) {
+    int64_t r = 0;
+    /* a regular file and a large output (estimated from the first runs):
+     * format everything, then copy through a mapping */
+    const long long mmin = output_mmap_min();
+    struct stat st;
+    if (mmin >= 0 && fstat(fileno(out), &st) == 0 && S_ISREG(st.st_mode)) {
+        const int64_t probe = nr < 2 * (int64_t)nt ? nr : 2 * (int64_t)nt;
+        size_t got = 0;
+        for (int64_t k = 0; k < probe; ++k) {
+            while (!atomic_load_explicit(&J.ready[k], memory_order_acquire))
+                usleep(20);
+            got += J.len[k];
+        }
+        if ((double)got / (double)probe * (double)nr >= (double)mmin) {
+            size_t total = got;
+            for (int64_t k = probe; k < nr; ++k) {
+                while (!atomic_load_explicit(&J.ready[k], memory_order_acquire))
+                    usleep(20);
+                total += J.len[k];
+            }
+            for (int i = 0; i < nt; ++i)
+                pthread_join(th[i], NULL);
+            nt = 0;
+            const int rc = atomic_load(&J.oom) ? 0 : par_output_mapped(out, J.buf, J.len, nr, total);
+            if (rc != 0) {
+                bad = rc < 0;
+                for (int64_t k = 0; k < nr; ++k)
+                    free(J.buf[k]);
+                r = nr;
+            }
+        }
+    }
+    for (; r < nr; ++r) {
         while (!atomic_load_explicit(&J.ready[r], memory_order_acquire))
             usleep(20);
         if (J.len[r] && fwrite(J.buf[r], 1, J.len[r], out) != J.len[r])

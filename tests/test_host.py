@@ -535,3 +535,31 @@ def test_chainnet_input_modes_vs_reference(mode, tmp_path):
         assert "chrQ2_hap1" in qnet
     else:  # the haplotype query sides are netted only with -inclHap
         assert "net chrQ2_hap1" not in qnet
+
+
+@pytest.mark.parametrize("tool", ["chainNet", "chainSort"])
+def test_mapped_output_path(tool, tmp_path):
+    """The large-output path of gac_par_output (every run formatted, then
+    copied into a shared mapping of the reserved file range by all threads),
+    forced on small files with GAC_OUTPUT_MMAP_MIN=0: same bytes as the
+    reference's goldens, header lines before the mapped range included."""
+    from genomealignmenttools_amd._lib import BIN_DIR
+    d = os.path.join(GOLDEN, "synth11")
+    env = dict(os.environ, GAC_OUTPUT_MMAP_MIN="0")
+    if tool == "chainNet":
+        r = subprocess.run([os.path.join(BIN_DIR, "chainNet"), os.path.join(d, "in.chain"),
+                            os.path.join(d, "t.sizes"), os.path.join(d, "q.sizes"),
+                            str(tmp_path / "t.net"), str(tmp_path / "q.net")],
+                           capture_output=True, text=True, env=env)
+        assert r.returncode == 0, r.stderr
+        assert filecmp.cmp(tmp_path / "t.net", os.path.join(d, "plain.t.net"), shallow=False)
+        assert filecmp.cmp(tmp_path / "q.net", os.path.join(d, "plain.q.net"), shallow=False)
+    else:
+        outs = {}
+        for tag, e in (("mapped", env), ("plain", dict(os.environ, GAC_OUTPUT_MMAP_MIN="-1"))):
+            r = subprocess.run([os.path.join(BIN_DIR, "chainSort"), os.path.join(d, "in.chain"),
+                                str(tmp_path / f"{tag}.chain")], capture_output=True, text=True,
+                               env=e)
+            assert r.returncode == 0, r.stderr
+            outs[tag] = open(tmp_path / f"{tag}.chain", "rb").read()
+        assert outs["mapped"] == outs["plain"] and len(outs["plain"]) > 0
