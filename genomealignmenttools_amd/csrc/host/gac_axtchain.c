@@ -40,6 +40,11 @@ typedef struct ax_env {
     int32_t m5[25];    /* [q code * 5 + t code], codes T C A G = 0..3, N = 4 */
     int32_t *gtab;     /* [3][gtab_len] gapCalcCost by kind and distance */
     int gtab_len;
+    /* gapCalcCost's linear tail past the last long position, by kind: where
+     * most kd-tree bounds of a large pair land (a call into the general
+     * function cost the largest C4 pair 10 %) */
+    int32_t last_pos[3];
+    double last_val[3], last_slope[3];
 } ax_env;
 
 /* chainConnectGapCost = gapCalcCost (chainConnect.c:108-112) */
@@ -61,6 +66,10 @@ static inline int gap_cost(const ax_env *e, int dq, int dt) {
     }
     if (d >= 0 && d < e->gtab_len)
         return e->gtab[kind * e->gtab_len + d];
+    if (d >= e->last_pos[kind]) { /* gapCalc.c:307,316,326, same operations (-ffp-contract=off) */
+        const double prod = e->last_slope[kind] * (double)(d - e->last_pos[kind]);
+        return (int)(e->last_val[kind] + prod);
+    }
     return gac_gap_cost(e->g, dq, dt);
 }
 
@@ -1317,6 +1326,7 @@ void gac_axt_chains_free(gac_axt_chains *c) {
 static pthread_mutex_t g_gtab_mu = PTHREAD_MUTEX_INITIALIZER;
 static gac_gapcalc *cached_g = NULL;
 static int32_t *cached_tab = NULL;
+static int cached_len = 0;
 
 int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
                   const gac_axt_input *in, double min_score, int n_threads,
@@ -1407,9 +1417,16 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
                     (qc == 4 || tc == 4) ? 0 : mat[acgt_of_code[qc] * 4 + acgt_of_code[tc]];
         /* kept across calls while the gap table is the same (-jobs
          * batches); held locked until the DP that reads it is done */
-        const int len = 1 << 15;
+        /* 2^15 distances; 2^18 (past the built-in tables' last long
+         * position) when a pair is large enough for its DP to pay back the
+         * few ms: the interpolation range then never reaches the function */
+        int64_t big = 0;
+        for (int64_t p = 0; p < np; ++p)
+            if (in->blk_off[p + 1] - in->blk_off[p] > big)
+                big = in->blk_off[p + 1] - in->blk_off[p];
+        const int len = big > 200000 ? 1 << 18 : 1 << 15;
         pthread_mutex_lock(&g_gtab_mu);
-        if (!cached_g || !gac_gapcalc_same(cached_g, g)) {
+        if (!cached_g || !gac_gapcalc_same(cached_g, g) || cached_len < len) {
             int32_t *tab = malloc((size_t)3 * len * sizeof(int32_t));
             for (int d = 0; d < len; ++d) {
                 tab[d] = gac_gap_cost(g, d, 0);
@@ -1420,9 +1437,19 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
             free(cached_tab);
             cached_g = gac_gapcalc_clone(g);
             cached_tab = tab;
+            cached_len = len;
         }
-        env.gtab_len = len;
+        env.gtab_len = cached_len;
         env.gtab = cached_tab;
+        env.last_pos[0] = g->q_last_pos;
+        env.last_pos[1] = g->t_last_pos;
+        env.last_pos[2] = g->b_last_pos;
+        env.last_val[0] = g->q_last_val;
+        env.last_val[1] = g->t_last_val;
+        env.last_val[2] = g->b_last_val;
+        env.last_slope[0] = g->q_last_slope;
+        env.last_slope[1] = g->t_last_slope;
+        env.last_slope[2] = g->b_last_slope;
     }
     stage("host gap table", &tclock);
     /* ---- chainBlocks + overlap removal per pair on host threads */
