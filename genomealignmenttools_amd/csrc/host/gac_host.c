@@ -803,15 +803,18 @@ int gac_par_format(int64_t nr, void (*fn)(FILE *f, int64_t r, void *arg), void *
     return atomic_load(&J.oom) ? -1 : 0;
 }
 
-/* Large outputs into a regular file: every run formatted first, then copied
- * into a shared mapping of the reserved file range by all threads.  Buffered
- * write() calls into one file serialise on its inode lock (≈1.4 GB/s for a
- * GB-scale .chain/.net on the GPU box); page faults on a mapping do not.
- * GAC_OUTPUT_MMAP_MIN = the size from which it is used (bytes, default
- * 64 MB; 0 = always, -1 = never). */
+/* Large outputs into a regular file, opt-in: every run formatted first,
+ * then copied into a shared mapping of the reserved file range by all
+ * threads (buffered write() calls into one file serialise on its inode lock;
+ * page faults on a mapping do not).  GAC_OUTPUT_MMAP_MIN = the size from
+ * which it is used (bytes; 0 = always; unset or negative = never).  Off by
+ * default: on the GPU box's overlay filesystem the copy itself is fast (330
+ * MB in 0.14-0.18 s) but losing the overlap of formatting and writing made
+ * chainNet's two nets slower (write stage 0.40 vs 0.22 s on C5 at 1 M
+ * chains) and scoreChain no faster (0.26 vs 0.29 s); scripts/gpu_output_ab.sh. */
 static long long output_mmap_min(void) {
     const char *s = getenv("GAC_OUTPUT_MMAP_MIN");
-    return s && *s ? atoll(s) : (64ll << 20);
+    return s && *s ? atoll(s) : -1;
 }
 
 typedef struct mcopy_job {
