@@ -327,7 +327,7 @@ def _c5_small(tmp_path):
     return d
 
 
-@pytest.mark.parametrize("nranks", [2, 5])
+@pytest.mark.parametrize("nranks", [2, 5, 8])
 def test_chainnet_ranks_vs_reference(nranks, tmp_path):
     """chainNet -nranks=N -rank=R (one process per rank; here without
     -rescore, so no device): every rank nets its share of the 455 + 66
