@@ -1272,6 +1272,11 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
         return gac_fail(GAC_E_ARG, "gac_chains_upload: bad descriptor");
     if (d->n_chains && d->blk_off[d->n_chains] != d->n_blocks)
         return gac_fail(GAC_E_ARG, "blk_off[n_chains] != n_blocks");
+    // the kernels index blocks of one chain set with int32 (RangeDesc::b0,
+    // flat windows): a larger set must be uploaded in parts
+    if (d->n_blocks > (int64_t)INT32_MAX - 16)
+        return gac_fail(GAC_E_ARG, "chain set of %lld blocks: at most %d per gac_chains_upload "
+                        "(upload it in parts)", (long long)d->n_blocks, INT32_MAX - 16);
     const int64_t n = d->n_chains;
     std::vector<DChain> ch(n ? n : 1);
     // tasks: contiguous chain ranges of about equal blocks + chains
