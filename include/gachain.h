@@ -149,6 +149,7 @@ int gac_genome_decode(gac_ctx *ctx, int side, int32_t index, int32_t start,
                       int32_t end, char *out);
 
 /* ---- chains ------------------------------------------------------------- */
+/* At most 2^31 - 17 blocks per chain set (GAC_E_ARG beyond: upload in parts). */
 int gac_chains_upload(gac_ctx *ctx, const gac_chainset_desc *d, gac_chainset **out);
 void gac_chains_free(gac_chainset *cs);
 int64_t gac_chains_block_count(const gac_chainset *cs);
