@@ -157,19 +157,20 @@ def test_c5_shaped_chainnet_rescore_sparse(c5_dir, c5_ref_nets):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("nranks", [2, 3])
-def test_c5_shaped_chainnet_rescore_ranks(c5_dir, c5_ref_nets, nranks):
+@pytest.mark.parametrize("nranks,env", [(2, {}), (3, {}), (2, {"GAC_NET_SPARSE": "1"})])
+def test_c5_shaped_chainnet_rescore_ranks(c5_dir, c5_ref_nets, nranks, env):
     """The multi-GPU mode (-nranks=N -rank=R, one process per rank): each
     rank nets and rescores its share of the chromosome sides, rank 0
     assembles both nets -- identical to the reference's single run.  (All
     ranks on device 0 here: the box has one GPU.)"""
     p = lambda x: os.path.join(c5_dir, x)
-    tag = f"mr{nranks}"
+    tag = f"mr{nranks}{'s' if env else ''}"
     procs = [subprocess.Popen(
         [_bin("chainNet"), p("in.chain"), p("t.sizes"), p("q.sizes"), p(f"{tag}.t.net"),
          p(f"{tag}.q.net"), "-rescore", f"-tNibDir={p('t.2bit')}", f"-qNibDir={p('q.2bit')}",
          "-linearGap=loose", f"-nranks={nranks}", f"-rank={r}", "-gpu=0"],
-        stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(nranks)]
+        stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+        env=dict(os.environ, **env)) for r in range(nranks)]
     for r, pr in enumerate(procs):
         _, err = pr.communicate(timeout=600)
         assert pr.returncode == 0, (r, err[-2000:])
