@@ -2214,7 +2214,12 @@ static void wjob_flags(wjob *J, const gac_net *n, int side, const int64_t *tscor
         const nfill *f = J->ord[i];
         J->reached[i] = J->show[i] && (!f->pgap->pfill || J->reached[f->pgap->pfill->ord]);
     }
+    /* runs of at most 128 fills (≈15 KB of net text): small reused
+     * formatting buffers, batched into one writev per 256 runs
+     * (gac_par_output) */
     J->per = nf / (64 * (int64_t)nt) + 1;
+    if (J->per > 128)
+        J->per = 128;
 }
 
 static void wjob_free_flags(wjob *J) {
