@@ -2214,12 +2214,10 @@ static void wjob_flags(wjob *J, const gac_net *n, int side, const int64_t *tscor
         const nfill *f = J->ord[i];
         J->reached[i] = J->show[i] && (!f->pgap->pfill || J->reached[f->pgap->pfill->ord]);
     }
-    /* runs of at most 128 fills (≈15 KB of net text): small reused
-     * formatting buffers, batched into one writev per 256 runs
-     * (gac_par_output) */
+    /* (runs of 1/64 of a thread's share: capping them at 128 or 1024 fills
+     * as for chains made the C5 nets slower, 1.79-1.86 / 1.36 vs 1.31-1.34
+     * s; scripts/gpu_net_runs_ab.sh) */
     J->per = nf / (64 * (int64_t)nt) + 1;
-    if (J->per > 128)
-        J->per = 128;
 }
 
 static void wjob_free_flags(wjob *J) {
