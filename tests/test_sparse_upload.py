@@ -21,8 +21,13 @@ TOOL = os.path.join(ROOT, "oracle", "_build", "chainNet_cpu")
 
 @pytest.fixture(scope="module")
 def tool():
-    r = subprocess.run(["make", "-s", "cpu-chainnet"], cwd=ROOT, capture_output=True, text=True,
-                       timeout=300)
+    # one build at a time: pytest-xdist workers may reach this together
+    import fcntl
+    os.makedirs(os.path.join(ROOT, "oracle", "_build"), exist_ok=True)
+    with open(os.path.join(ROOT, "oracle", "_build", ".cpu-chainnet.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        r = subprocess.run(["make", "-s", "cpu-chainnet"], cwd=ROOT, capture_output=True,
+                           text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     return TOOL
 
