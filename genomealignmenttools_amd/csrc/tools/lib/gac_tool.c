@@ -1573,6 +1573,25 @@ void gt_read_chains_keep(const char *path, gt_chains *c, double stop_below, int 
     read_chains(path, c, stop_below, keep_meta, tkeep, qkeep);
 }
 
+typedef struct rc_free_job {
+    chunk *K;
+    int nk;
+    void *NL, *cut;
+    char *buf;
+} rc_free_job;
+
+static void *rc_free_thread(void *arg) {
+    rc_free_job *F = arg;
+    for (int k = 0; k < F->nk; ++k)
+        gt_chains_free(&F->K[k].c);
+    free(F->K);
+    free(F->NL);
+    free(F->cut);
+    free(F->buf);
+    free(F);
+    return NULL;
+}
+
 static void read_chains(const char *path, gt_chains *c, double stop_below, int keep_meta,
                         const gt_names *tkeep, const gt_names *qkeep) {
     memset(c, 0, sizeof(*c));
@@ -1702,12 +1721,18 @@ static void read_chains(const char *path, gt_chains *c, double stop_below, int k
     free(c0);
     free(b0);
     RC_LAP("stitch");
-    for (int k = 0; k < nk; ++k)
-        gt_chains_free(&K[k].c);
-    free(K);
-    free(NL);
-    free(cut);
-    free(buf);
+    /* the file text and the per-chunk arrays (GBs at whole-genome size:
+     * 0.2 s of page freeing on C5 at 5 M chains) are released off the
+     * caller's path */
+    rc_free_job *F = malloc(sizeof(*F));
+    *F = (rc_free_job){K, nk, NL, cut, buf};
+    pthread_attr_t at;
+    pthread_attr_init(&at);
+    pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
+    pthread_t th;
+    if (pthread_create(&th, &at, rc_free_thread, F) != 0)
+        rc_free_thread(F);
+    pthread_attr_destroy(&at);
     RC_LAP("free");
 #undef RC_LAP
 }
