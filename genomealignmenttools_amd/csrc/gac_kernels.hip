@@ -725,8 +725,11 @@ __device__ __forceinline__ void seg_store(const ScoreArgs &a, int ri, long long 
     if (LOCAL) a.out_l[ri] = max2(0, max2(e.C, e.D));
 }
 
+#ifndef GAC_TILE_MINB
+#define GAC_TILE_MINB 6  // waves per SIMD the register budget is sized for
+#endif
 template <bool LOCAL, bool SYM>
-__global__ void __launch_bounds__(256, 6) k_tile(ScoreArgs a) {
+__global__ void __launch_bounds__(256, GAC_TILE_MINB) k_tile(ScoreArgs a) {
     __shared__ WaveLds s_w[kWavesPerWG];
 
     const int wave = threadIdx.x >> 6;
