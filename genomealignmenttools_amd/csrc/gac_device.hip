@@ -1278,6 +1278,14 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
         return gac_fail(GAC_E_ARG, "chain set of %lld blocks: at most %d per gac_chains_upload "
                         "(upload it in parts)", (long long)d->n_blocks, INT32_MAX - 16);
     const int64_t n = d->n_chains;
+    const bool timing = getenv("GAC_TIMING") != nullptr;
+    double t_lap = wall_s();
+    auto lap = [&](const char *what) {
+        if (!timing) return;
+        const double t = wall_s();
+        fprintf(stderr, "[gac_chains_upload] %-22s %.3f s\n", what, t - t_lap);
+        t_lap = t;
+    };
     std::vector<DChain> ch(n ? n : 1);
     // tasks: contiguous chain ranges of about equal blocks + chains
     const int nt = std::max(1, std::min(64, gac_host_threads()));
@@ -1330,6 +1338,7 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
         }
         return gac_fail(GAC_E_FORMAT, "chain %lld: invalid", (long long)i);
     }
+    lap("chain records + checks");
     int64_t idx_n = 0;
     for (int64_t i = 0; i < n; ++i) {
         const int64_t k = ch[i].idx_off;
@@ -1350,10 +1359,12 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
     if (e == hipSuccess) e = hipMalloc(&cs->tspan, (nb + 8) * sizeof(int2));
     if (e == hipSuccess) e = hipMalloc(&d_bt, std::max<size_t>(3 * nb, 1) * 4);
     int rc = GAC_OK;
+    lap("allocations");
     if (e == hipSuccess) rc = upload_staged(c, cs->chains, ch.data(), ch.size() * sizeof(DChain));
     if (e == hipSuccess && rc == GAC_OK && nb) rc = upload_staged(c, d_bt, d->blk_t, nb * 4);
     if (e == hipSuccess && rc == GAC_OK && nb) rc = upload_staged(c, d_bt + nb, d->blk_q, nb * 4);
     if (e == hipSuccess && rc == GAC_OK && nb) rc = upload_staged(c, d_bt + 2 * nb, d->blk_size, nb * 4);
+    lap("staged copies");
     if (e == hipSuccess && rc == GAC_OK)
         e = launch_build(d_bt, d_bt + nb, d_bt + 2 * nb, (int64_t)nb, cs->chains, cs->n_chains,
                          cs->blk, cs->tspan, cs->bucket, c->stream);
@@ -1362,6 +1373,7 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
         e = launch_nflags(cs->chains, cs->n_chains, cs->blk, c->g[0].nmask, c->g[0].d_woff,
                           c->g[1].nmask, c->g[1].d_woff, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    lap("device build + sync");
     if (d_bt) hipFree(d_bt);
     if (e != hipSuccess || rc != GAC_OK) {
         gac_chains_free(cs);

@@ -260,7 +260,8 @@ def c5(a):
                    opts + ["-verbose=2"], outputs=[p("ours.t.net"), p("ours.q.net")])
     res.update(ours_scorechain_s=round(t1, 3), ours_chainnet_s=round(t2, 3),
                ours_s=round(t1 + t2, 3),
-               ours_stages=[l for l in (r1.stderr + r2.stderr).splitlines() if "[stage]" in l],
+               ours_stages=[l for l in (r1.stderr + r2.stderr).splitlines()
+                            if "[stage]" in l or "[gac_chains_upload]" in l],
                ours_gbases_per_s=round(2 * info["aligned_bases"] / (t1 + t2) / 1e9, 3))
     log(f"ours: scoreChain {t1:.2f}s chainNet {t2:.2f}s")
     print(json.dumps(res), flush=True)  # ours alone, in case the reference run is cut off
