@@ -86,6 +86,13 @@ $(BINDIR)/%: $(EXECDIR)/%
 
 oracle: oracle/_build/libgacoracle.so
 
+# bench/test infrastructure: the whole-genome synthetic set generator (C5)
+synth: $(EXECDIR)/gac_synth
+
+$(EXECDIR)/gac_synth: $(CSRC)/synth/gac_synth.c
+	@mkdir -p $(EXECDIR)
+	$(CC) -O2 -std=gnu11 -Wall $< -o $@ -lm -lpthread
+
 oracle/_build/libgacoracle.so: oracle/gac_oracle.c
 	@mkdir -p oracle/_build
 	$(CC) -O2 -std=gnu11 -fPIC -shared -Wall $< -o $@ -lm
@@ -96,7 +103,7 @@ ref:
 clean:
 	rm -rf build $(LIBDIR) $(BINDIR) $(EXECDIR) oracle/_build
 
-.PHONY: all oracle ref clean
+.PHONY: all oracle synth ref clean
 
 # TEST INFRASTRUCTURE: axtChain's host half (front end + kd-tree DP) on a CPU
 # stand-in of the device ABI, for profiling in GPU-less containers.  Not part

@@ -1,43 +1,51 @@
 #!/usr/bin/env python3
-"""bench.py -- aligned Gbases scored/sec, chainNet -rescore hg38-mm10 (BASELINE.json).
+"""bench.py -- aligned Gbases scored/sec, chainNet -rescore hg38-mm10, 1/2/4/8 MI355X
+(BASELINE.json).
 
-Workload (synthetic, seeded): target = hg38 chr1
-(248,956,422 bp), query = all 66 mm10 sequences (2.73 Gb), 2e5 planted
-chains (power-law blocks/chain, geometric 40-bp blocks, 12% substitutions,
-50% '-' strand, 20% short spurious chains), written as .2bit genomes,
-chrom.sizes files and a score-sorted .chain file.
+Headline workload (synthetic, seeded): the whole
+genome -- all 455 hg38 sequences as target x all 66 mm10 sequences as query,
+5e6 chains (C2's chain model: power-law blocks/chain, geometric 40-bp
+blocks, 70/28/2 % gap mixture, 12 % substitutions, 50 % '-' strand, 20 %
+short spurious chains; chains per target sequence in proportion to its
+length), written as .2bit genomes, chrom.sizes files and a score-sorted
+.chain file by the C generator gac_synth (bench infrastructure,
+csrc/synth/gac_synth.c).
 
-Headline (`value`, SURVEY §8(d) primary metric): ONE STEP = one end-to-end
-`bin/chainNet in.chain t.sizes q.sizes t.net q.net -rescore -tNibDir=t.2bit
--qNibDir=q.2bit -linearGap=loose` invocation (the drop-in tool: process
-start, chain parse, host netting, 2bit genomes + chains to HBM, GPU
-rescoring of every partial target fill, both nets written).  value = the
-aligned bases of the netted input chains (score >= 0) / wall time per step.
+ONE STEP = one end-to-end `bin/chainNet in.chain t.sizes q.sizes t.net q.net
+-rescore -tNibDir=t.2bit -qNibDir=q.2bit -linearGap=loose` over that input:
+process start, chain parse, host netting, 2bit genomes + chains to HBM, GPU
+rescoring of every partial target fill, both nets written, process exit.
+value = the aligned bases of the netted input chains (score >= 0) / wall time
+per step (SURVEY §8(d) primary metric).
 
-N > 1 (torchrun, one process per GPU): weak scaling, C2 per GPU.  The input
-is ONE chain set over N target chromosomes: N replicas of C2's target
-chromosome (chr1, chr1_r1, ..., same sequence) and of its chains (renamed,
-ids renumbered, interleaved in score order), against the same mm10 query.
-Every step runs the tool on every rank over that input with -nranks=N
--rank=r: rank r nets the chromosome sides it owns (contiguous runs of each
-sizes file, balanced by length: one target chromosome per rank, 1/N of the
-query chromosomes), parses only the chains on its sides, loads only its
-target sequence, rescores its target fills on its own GPU and writes its
-part; rank 0 assembles both nets.  No data-path collective (the netting
-partitions by chromosome side); torch.distributed (RCCL) carries the
-barriers and the max-over-ranks clock.  value = netted aligned bases of the
-whole set / wall time.
+N > 1 (torchrun, one process per GPU): STRONG scaling on the same fixed input.
+Every rank runs the tool with -nranks=N -rank=r -gpu=LOCAL_RANK each step:
+rank r nets the chromosome sides it owns (contiguous runs of each sizes file,
+balanced by length), parses only the chains on its sides, loads only its
+target sequences, rescores its target fills on its GPU and writes its part of
+both nets in place.  The netting partitions by chromosome side, so there is no
+data-path collective; torch.distributed (RCCL) carries the barriers and the
+max-over-ranks clock.  value = the set's netted aligned bases / step time.
 
-Also reported:
-  kernel   -- the GPU rescoring call alone (gac_score_ranges_device over the
-              C2 partial fills, inputs resident in HBM), HIP-event timed;
-  roofline -- its dominant kernel k_tile: algorithmic bytes per launch
-               / k_tile's average launch time, vs 8 TB/s;
+Also reported (rank 0):
+  c2          -- configs[1]: the same tool on C2 (hg38 chr1 x mm10, 2e5
+                 chains), N = 1 only, with its reference time;
+  kernel      -- the GPU rescoring call alone (gac_score_ranges_device over
+                 exactly the partial fills the tool rescored in the headline,
+                 dumped by GAC_DUMP_RANGES), inputs resident in HBM, HIP-event
+                 timed on the launch stream;
+  roofline    -- its dominant kernel k_tile against the SURVEY §8(d) RANGE
+                 model: 32 B/range + 8 B/window block + 0.75 B/scored base;
+                 traffic = HBM-side bytes from rocprofv3 counter passes in this
+                 run (N = 1);
+  scorechain  -- the whole-chain scoring call (global + local, the scoreChain
+                 path) over every C5 chain, with its own roofline on the
+                 §8(d) full-chain model: 0.75 B/base + 12 B/block + 44 B/chain;
   cpu_baseline -- the reference chainNet compiled from /root/reference
-              (oracle/_ref/chainNet, test infrastructure) on the same files on
-              this host: one process (the reference is single-threaded) and a
-              per-chromosome-side split over all cores; nets compared byte
-              for byte with ours.
+                 (oracle/_ref/chainNet, test infrastructure) timed on this
+                 host, one process (it is single-threaded), on a bounded
+                 sample of the same workload: the C5 chains on chr21 + chr22
+                 (their target nets are compared with ours byte for byte).
 """
 import argparse
 import filecmp
@@ -56,8 +64,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BLASTZ = np.array([[91, -114, -31, -123], [-114, 100, -125, -31], [-31, -125, 100, -114],
                    [-123, -31, -114, 91]], np.int32)
 METRIC = "aligned Gbases scored/sec, chainNet -rescore hg38-mm10, 1/2/4/8 MI355X"
-TOOL = os.path.join(REPO, "genomealignmenttools_amd", "bin", "chainNet")
+PKG = os.path.join(REPO, "genomealignmenttools_amd")
+TOOL = os.path.join(PKG, "bin", "chainNet")
+SYNTH = os.path.join(PKG, "libexec", "gac_synth")
 REF_TOOL = os.path.join(REPO, "oracle", "_ref", "chainNet")
+SAMPLE_TARGETS = ("chr21", "chr22")
 
 
 def log(*a):
@@ -67,32 +78,21 @@ def log(*a):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--chains", type=int, default=200_000)
-    p.add_argument("--seed", type=int, default=42)
-    p.add_argument("--workload", choices=["chainnet", "rescore", "scorechain"], default="chainnet",
-                   help="chainnet: end-to-end bin/chainNet -rescore (headline); rescore / "
-                        "scorechain: the GPU scoring call alone as the step")
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--chains", type=int, default=5_000_000, help="C5 chain count")
+    p.add_argument("--seed", type=int, default=1234)
+    p.add_argument("--c2-chains", type=int, default=200_000)
+    p.add_argument("--c2-steps", type=int, default=10)
     p.add_argument("--kernel-steps", type=int, default=20)
-    p.add_argument("--no-kernel", action="store_true", help="skip the kernel/roofline leg")
+    p.add_argument("--no-c2", action="store_true")
+    p.add_argument("--no-kernel", action="store_true", help="skip the kernel/roofline legs")
+    p.add_argument("--no-scorechain", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-all-cores", action="store_true",
-                   help="skip the reference's per-chromosome-side all-cores run")
-    p.add_argument("--prof", choices=["tile", "all", "none"], default="tile",
-                   help="kernels bracketed by HIP events in the kernel leg (the roofline "
-                        "needs k_tile's)")
-    p.add_argument("--order", choices=["chain", "net", "t", "q"], default="net",
-                   help="kernel leg: ranges in .net output order (as bin/chainNet submits "
-                        "them), (chain, tStart), target start, or (query sequence, forward "
-                        "query position) order")
+    p.add_argument("--no-pmc", action="store_true")
     p.add_argument("--tmp", default=os.environ.get("TMPDIR", "/tmp"))
-    p.add_argument("--no-pmc", action="store_true",
-                   help="roofline.traffic from the committed profile instead of this run's "
-                        "rocprofv3 counter passes")
-    p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--pmc-child", choices=["fills", "scorechain"], help=argparse.SUPPRESS)
     p.add_argument("--gen-only", action="store_true", help=argparse.SUPPRESS)
-    p.add_argument("--replicas", type=int, default=1, help=argparse.SUPPRESS)
     return p.parse_args()
 
 
@@ -102,28 +102,39 @@ def host_threads():
 
 
 # ---------------------------------------------------------------- input files
+def c5_files(args):
+    """C5 written once per box under --tmp by gac_synth (~15 s on 16 threads)."""
+    d = os.path.join(args.tmp, f"gac_bench_c5_{args.chains}_{args.seed}")
+    if not os.path.exists(os.path.join(d, "info.json")):
+        if not os.path.exists(SYNTH):
+            raise SystemExit(f"{SYNTH} missing: run `make synth` (or __graft_entry__.build())")
+        t0 = time.time()
+        subprocess.run([SYNTH, "c5", d, f"-seed={args.seed}", f"-chains={args.chains}",
+                        f"-sizesDir={os.path.join(PKG, 'data')}",
+                        f"-threads={min(host_threads(), 32)}"], check=True)
+        log(f"C5: written in {time.time() - t0:.1f}s")
+    with open(os.path.join(d, "info.json")) as f:
+        return d, json.load(f)
+
+
 def c2_files(args):
     """C2 written once per box under --tmp: t.2bit, q.2bit, *.sizes, in.chain."""
     from genomealignmenttools_amd import chainfile, synth
-    d = os.path.join(args.tmp, f"gac_bench_c2_{args.chains}_{args.seed}")
+    d = os.path.join(args.tmp, f"gac_bench_c2_{args.c2_chains}_42")
     p = lambda x: os.path.join(d, x)
     if not os.path.exists(p("info.json")):
         os.makedirs(d, exist_ok=True)
         t0 = time.time()
-        tg, qg, ca = synth.c2_case(seed=args.seed, n_chains=args.chains)
+        tg, qg, ca = synth.c2_case(seed=42, n_chains=args.c2_chains)
         synth.write_2bit(tg, p("t.2bit"))
         synth.write_2bit(qg, p("q.2bit"))
         synth.write_sizes(tg.sizes, p("t.sizes"))
         synth.write_sizes(qg.sizes, p("q.sizes"))
-        chainfile.write_chains(ca, p("in.chain"))
-        # the netting loop stops at the first chain below minScore (0 with
-        # -rescore, chainNet.c:949-952,1022): those chains' aligned bases
-        # are the metric's numerator
+        chainfile.write_chains_fast(ca, p("in.chain"))
         neg = np.nonzero(ca.score < 0)[0]
         stop = int(neg[0]) if len(neg) else ca.n
         info = {"chains": ca.n, "blocks": int(len(ca.blk_size)),
-                "input_aligned_bases": ca.aligned_bases(),
-                "netted_chains": stop,
+                "input_aligned_bases": ca.aligned_bases(), "netted_chains": stop,
                 "netted_aligned_bases": int(ca.blk_size[:ca.blk_off[stop]].sum(dtype=np.int64))}
         with open(p("info.json.tmp"), "w") as f:
             json.dump(info, f)
@@ -133,74 +144,20 @@ def c2_files(args):
         return d, json.load(f)
 
 
-def _replicate_2bit(src, dst, names):
-    """A version-0 .2bit holding the one sequence of `src` under every name
-    (its record bytes copied, the index rebuilt)."""
-    import struct
-    with open(src, "rb") as f:
-        data = f.read()
-    magic, _, cnt, _ = struct.unpack_from("<IIII", data, 0)
-    assert cnt == 1, src
-    nl = data[16]
-    rec = data[struct.unpack_from("<I", data, 17 + nl)[0]:]
-    off = 16 + sum(1 + len(n) + 4 for n in names)
-    with open(dst + ".tmp", "wb") as f:
-        f.write(struct.pack("<IIII", magic, 0, len(names), 0))
-        for k, n in enumerate(names):
-            f.write(struct.pack("<B", len(n)) + n.encode() + struct.pack("<I", off + k * len(rec)))
-        for _ in names:
-            f.write(rec)
-    os.rename(dst + ".tmp", dst)
-
-
-def _replicate_chains(src, dst, names):
-    """Every chain of `src` once per target name (tName replaced), copies
-    adjacent (the file stays sorted by score), ids 1..n in file order."""
-    with open(src, "rb") as f:
-        data = f.read()
-    head, sep, body = data.partition(b"chain ")
-    out, nid = [head], 0
-    enc = [n.encode() for n in names]
-    for rec in (sep + body).split(b"\n\n"):
-        if not rec.strip():
-            continue
-        hdr, _, blocks = rec.partition(b"\n")
-        w = hdr.split(b" ")
-        for nm in enc:
-            nid += 1
-            w[2] = nm
-            w[12:] = [str(nid).encode()]
-            out.append(b" ".join(w) + b"\n" + blocks + b"\n\n")
-    with open(dst + ".tmp", "wb") as f:
-        f.write(b"".join(out))
-    os.rename(dst + ".tmp", dst)
-
-
-def c2n_files(args, n):
-    """The N>1 input: C2 replicated per rank (see the module docstring)."""
-    d1, info1 = c2_files(args)
-    d = d1 + f"_x{n}"
-    p = lambda x: os.path.join(d, x)
-    if not os.path.exists(p("info.json")):
-        os.makedirs(d, exist_ok=True)
-        t0 = time.time()
-        names = ["chr1"] + [f"chr1_r{k}" for k in range(1, n)]
-        tsize = open(os.path.join(d1, "t.sizes")).read().split()[1]
-        with open(p("t.sizes"), "w") as f:
-            f.write("".join(f"{nm}\t{tsize}\n" for nm in names))
-        _replicate_2bit(os.path.join(d1, "t.2bit"), p("t.2bit"), names)
-        _replicate_chains(os.path.join(d1, "in.chain"), p("in.chain"), names)
-        for x in ("q.2bit", "q.sizes"):
-            if not os.path.exists(p(x)):
-                os.symlink(os.path.join(d1, x), p(x))
-        info = {k: v * n for k, v in info1.items()}
-        info["replicas"] = n
-        with open(p("info.json.tmp"), "w") as f:
-            json.dump(info, f)
-        os.rename(p("info.json.tmp"), p("info.json"))
-        log(f"C2 x{n}: written in {time.time() - t0:.1f}s")
-    with open(p("info.json")) as f:
-        return d, json.load(f)
+def load_chains_bin(d):
+    """chains.bin of gac_synth (layout in csrc/synth/gac_synth.c) -> arrays."""
+    path = os.path.join(d, "chains.bin")
+    with open(path, "rb") as f:
+        assert f.read(8) == b"GACSYN01", path
+        n, nb = (int(x) for x in np.fromfile(f, np.int64, 2))
+        out = {"n": n, "nb": nb, "score": np.fromfile(f, np.float64, n)}
+        for k in ("tseq", "qseq", "tstart", "tend", "qstart", "qend"):
+            out[k] = np.fromfile(f, np.int32, n)
+        out["strand"] = np.fromfile(f, np.uint8, (n + 7) // 8 * 8)[:n]
+        out["off"] = np.fromfile(f, np.int64, n + 1)
+        for k in ("bt", "bq", "bs"):
+            out[k] = np.fromfile(f, np.int32, nb)
+    return out
 
 
 def tool_cmd(d, out, world, rank, extra=()):
@@ -224,145 +181,181 @@ def run_tool(cmd, outs, env=None):
     return r
 
 
-# ---------------------------------------------------------------- kernel leg
-def kernel_ranges(args, d):
-    """The kernel leg's chain set and ranges (host only, no device): the C2
-    partial target fills (or whole chains), in the --order order; cached as
-    .npy beside the input for the counter passes' child processes."""
-    from genomealignmenttools_amd import chainfile
-    from genomealignmenttools_amd.chainnet import net_fills
-    from genomealignmenttools_amd.synth import read_sizes
-    p = lambda x: os.path.join(d, x)
-    ca = chainfile.read_chains(p("in.chain"))
-    cache = p(f"ranges.{args.workload}.{args.order}.npy")
-    if os.path.exists(cache):
-        return ca, np.load(cache)
-    if args.workload == "scorechain":
-        ranges = np.stack([np.arange(ca.n, dtype=np.int32), ca.tstart, ca.tend], 1)
-    else:
-        fills = net_fills(ca, read_sizes(p("t.sizes")), read_sizes(p("q.sizes")), min_score=0.0)
-        part = fills["partial"]
-        ranges = np.stack([fills["chain"][part], fills["start"][part], fills["end"][part]], 1)
-    if args.order == "chain":
-        ranges = ranges[np.lexsort((ranges[:, 1], ranges[:, 0]))]
-    elif args.order == "t":
-        ranges = ranges[np.argsort(ranges[:, 1], kind="stable")]
-    elif args.order == "q":
-        ranges = ranges[np.lexsort(_query_key(ca, ranges)[::-1])]
-    ranges = np.ascontiguousarray(ranges, np.int32)
-    np.save(cache + ".tmp.npy", ranges)
-    os.rename(cache + ".tmp.npy", cache)
-    return ca, ranges
+def staged_run(d, out):
+    """One untimed single-process run with the stage laps (-verbose=2) and
+    the rescored fills dumped for the kernel leg; returns the stage lines."""
+    env = dict(os.environ, GAC_DUMP_RANGES=os.path.join(d, "fills.bin"))
+    r = run_tool(tool_cmd(d, out, 1, 0, ["-verbose=2"]), [out + ".t.net", out + ".q.net"], env=env)
+    return [line.strip() for line in r.stderr.splitlines() if "[stage]" in line]
 
 
-def kernel_leg(args, d, steps, ca, ranges, pmc=None):
-    """The GPU rescoring call alone (inputs resident in HBM), HIP-event timed:
-    the roofline of k_tile and a per-kernel breakdown.  pmc: this run's
-    counter-pass traffic (pmc_traffic) or None."""
-    from genomealignmenttools_amd._lib import GAC_K_COMBINE, GAC_K_PLAN, GAC_K_TILE
-    from genomealignmenttools_amd.gachain import GAC_Q, GAC_T, Engine, GapCosts
-    p = lambda x: os.path.join(d, x)
-    t0 = time.time()
-    e = Engine(int(os.environ.get("LOCAL_RANK", "0")))
-    e.load_2bit(GAC_T, p("t.2bit"))
-    e.load_2bit(GAC_Q, p("q.2bit"))
-    e.set_scoring(BLASTZ, GapCosts("loose"))
-    cs = e.upload_chains(ca)
-    n = len(ranges)
-    d_r = e.dev_alloc(ranges.nbytes)
-    e.h2d(d_r, ranges)
-    d_g = e.dev_alloc(8 * n)
-    d_a = e.dev_alloc(4 * n)
-    ali = np.zeros(n, np.int32)
-    e.score_ranges_device(cs, d_r, n, d_g, d_a)
-    e.synchronize()
-    e.d2h(ali, d_a)
-    bases = int(ali.sum(dtype=np.int64))
-    nblk = _window_blocks(ca, ranges)
-    log(f"kernel leg: {n} ranges, {bases} bases, {nblk} window blocks ({time.time() - t0:.1f}s setup)")
-    for _ in range(3):
-        e.score_ranges_device(cs, d_r, n, d_g, d_a)
-    e.synchronize()
-    e.prof_reset()
-    if args.prof != "none":
-        e.prof_enable(True, None if args.prof == "all" else [GAC_K_TILE])
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        e.score_ranges_device(cs, d_r, n, d_g, d_a)
-    e.synchronize()
-    dt = time.perf_counter() - t0
-    e.prof_enable(False)
-    tile_ms, tile_n = e.prof_read(GAC_K_TILE)
-    e.prof_reset()
-    e.prof_enable(True)
-    for _ in range(min(steps, 5)):
-        e.score_ranges_device(cs, d_r, n, d_g, d_a)
-    e.synchronize()
-    e.prof_enable(False)
-    kern_ms = {name: e.prof_read(k)[0] / max(e.prof_read(k)[1], 1)
-               for name, k in (("plan+tilemap", GAC_K_PLAN), ("tile", GAC_K_TILE),
-                               ("combine", GAC_K_COMBINE))}
-    if args.prof == "none":
-        tile_ms, tile_n = kern_ms["tile"], 1
-    cs.close()
-    e.close()
-    # algorithmic bytes per k_tile launch: 0.75 B/base (t+q 2-bit + t+q
-    # N-mask bits) + 12 B/window block + 44 B/range (DESIGN.md §4)
-    algo = 0.75 * bases + 12.0 * nblk + 44.0 * n
-    tile_s = (tile_ms / 1e3) / max(tile_n, 1)
-    achieved = algo / tile_s / 1e9
-    kernel = {"workload": ("chainNet -rescore partial target fills" if args.workload != "scorechain"
-                           else "scoreChain whole chains, global + local"),
-              "value": bases * steps / dt / 1e9, "unit": "Gbases/s", "ms_per_step": dt / steps * 1e3,
-              "steps": steps, "ranges": n, "order": args.order, "scored_bases": bases,
-              "window_blocks": nblk,
-              "kernel_ms": kern_ms}
-    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-            "kernel": "k_tile", "kernel_avg_ms": tile_s * 1e3, "algo_bytes_per_launch": algo}
+# ---------------------------------------------------------------- kernel legs
+def _window_blocks(ch, ranges):
+    """Blocks each range selects (tEnd > s and tStart < e; the whole chain
+    when the range covers it), vectorised with a (chain, t) key that is
+    monotone over the concatenated block arrays."""
+    c = ranges[:, 0].astype(np.int64)
+    s, e = ranges[:, 1].astype(np.int64), ranges[:, 2].astype(np.int64)
+    nbk = np.diff(ch["off"])
+    cid = np.repeat(np.arange(ch["n"], dtype=np.int64), nbk) << 32
+    bt = ch["bt"].astype(np.int64)
+    lo = np.searchsorted(cid + bt + ch["bs"], (c << 32) + s, side="right")
+    hi = np.searchsorted(cid + bt, (c << 32) + e, side="left")
+    w = np.maximum(0, hi - lo)
+    full = (s <= ch["tstart"][c]) & (e >= ch["tend"][c])
+    w[full] = nbk[c[full]]
+    return int(w.sum())
+
+
+class Legs:
+    """One device context with C5's genomes and chain set resident in HBM."""
+
+    def __init__(self, d, ch):
+        from genomealignmenttools_amd.gachain import GAC_Q, GAC_T, Engine, GapCosts
+        t0 = time.time()
+        self.e = e = Engine(int(os.environ.get("LOCAL_RANK", "0")))
+        e.load_2bit(GAC_T, os.path.join(d, "t.2bit"))
+        e.load_2bit(GAC_Q, os.path.join(d, "q.2bit"))
+        e.set_scoring(BLASTZ, GapCosts("loose"))
+        names = lambda side, path: [ln.split()[0] for ln in open(path) if ln.strip()]
+        tmap = np.array([e.seq_index(GAC_T, x) for x in names(GAC_T, os.path.join(d, "t.sizes"))],
+                        np.int32)
+        qmap = np.array([e.seq_index(GAC_Q, x) for x in names(GAC_Q, os.path.join(d, "q.sizes"))],
+                        np.int32)
+        self.cs = e.upload_chain_arrays(tmap[ch["tseq"]], qmap[ch["qseq"]], ch["strand"], ch["off"],
+                                        ch["bt"], ch["bq"], ch["bs"])
+        log(f"legs: genomes + {ch['n']} chains in HBM ({time.time() - t0:.1f}s)")
+
+    def run(self, ranges, want_local, steps):
+        """HIP-event timed calls over `ranges` (device-resident): the call's
+        wall time per step, k_tile's average launch, a per-kernel breakdown
+        and the scored bases."""
+        from genomealignmenttools_amd._lib import GAC_K_COMBINE, GAC_K_PLAN, GAC_K_TILE
+        e, cs = self.e, self.cs
+        n = len(ranges)
+        d_r = e.dev_alloc(max(ranges.nbytes, 16))
+        e.h2d(d_r, np.ascontiguousarray(ranges, np.int32))
+        d_g = e.dev_alloc(8 * n + 8)
+        d_l = e.dev_alloc(8 * n + 8) if want_local else 0
+        d_a = e.dev_alloc(4 * n + 8)
+        call = lambda: e.score_ranges_device(cs, d_r, n, d_g, d_a, d_l, want_local)
+        for _ in range(3):
+            call()
+        e.synchronize()
+        ali = np.zeros(n, np.int32)
+        e.d2h(ali, d_a)
+        e.prof_reset()
+        e.prof_enable(True, [GAC_K_TILE])
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            call()
+        e.synchronize()
+        dt = time.perf_counter() - t0
+        e.prof_enable(False)
+        tile_ms, tile_n = e.prof_read(GAC_K_TILE)
+        e.prof_reset()
+        e.prof_enable(True)
+        for _ in range(min(steps, 5)):
+            call()
+        e.synchronize()
+        e.prof_enable(False)
+        kern = {}
+        for name, k in (("plan+tilemap", GAC_K_PLAN), ("tile", GAC_K_TILE), ("combine", GAC_K_COMBINE)):
+            ms, cnt = e.prof_read(k)
+            kern[name] = ms / max(cnt, 1)
+        for p in (d_r, d_g, d_a) + ((d_l,) if d_l else ()):
+            e.dev_free(p)
+        return {"step_ms": dt / steps * 1e3, "tile_ms": tile_ms / max(tile_n, 1), "kernel_ms": kern,
+                "bases": int(ali.sum(dtype=np.int64)), "steps": steps}
+
+    def close(self):
+        self.cs.close()
+        self.e.close()
+
+
+def fills_ranges(d):
+    r = np.fromfile(os.path.join(d, "fills.bin"), np.int32).reshape(-1, 3)
+    return np.ascontiguousarray(r)
+
+
+def chain_ranges(ch):
+    return np.ascontiguousarray(np.stack([np.arange(ch["n"], dtype=np.int32), ch["tstart"],
+                                          ch["tend"]], 1), np.int32)
+
+
+def roofline(algo, t_ms, pmc, kernel):
+    roof = {"bound": "hbm", "achieved": algo / (t_ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "traffic": None, "kernel": kernel, "kernel_avg_ms": t_ms,
+            "algo_bytes_per_launch": algo}
+    roof["frac"] = roof["achieved"] / HBM_PEAK_GBS
     if pmc and pmc.get("hbm_bytes"):
-        roof["traffic"] = pmc["hbm_bytes"]
-        roof["traffic_source"] = pmc["source"]
-        roof["traffic_over_algo"] = pmc["hbm_bytes"] / algo
-        roof["traffic_kernel_avg_ms"] = pmc.get("avg_ms")
-    else:
-        roof["traffic"] = _pmc_traffic(args, n, nblk)
-        if roof["traffic"]:
-            roof["traffic_source"] = "committed profile " + os.path.relpath(TRAFFIC_FILE, REPO)
-    return kernel, roof
+        roof.update(traffic=pmc["hbm_bytes"], traffic_source=pmc["source"],
+                    traffic_over_algo=pmc["hbm_bytes"] / algo, traffic_kernel_avg_ms=pmc.get("avg_ms"))
+    return roof
+
+
+def fills_leg(legs, d, ch, steps, pmc):
+    ranges = fills_ranges(d)
+    res = legs.run(ranges, False, steps)
+    nblk = _window_blocks(ch, ranges)
+    n = len(ranges)
+    # SURVEY §8(d) range model: 32 B/range (16 in, 16 out) + 8 B/window block
+    # + 0.75 B/scored base (t+q 2-bit + t+q N-mask bits)
+    algo = 32.0 * n + 8.0 * nblk + 0.75 * res["bases"]
+    kernel = {"workload": "chainNet -rescore: the C5 partial target fills the headline rescored",
+              "value": res["bases"] / (res["step_ms"] / 1e3) / 1e9, "unit": "Gbases/s",
+              "ms_per_step": res["step_ms"], "steps": steps, "ranges": n, "order": "net",
+              "scored_bases": res["bases"], "window_blocks": nblk, "kernel_ms": res["kernel_ms"],
+              "model": "range: 32 B/range + 8 B/window block + 0.75 B/scored base"}
+    return kernel, roofline(algo, res["tile_ms"], pmc, "k_tile")
+
+
+def scorechain_leg(legs, ch, steps, pmc):
+    ranges = chain_ranges(ch)
+    res = legs.run(ranges, True, steps)
+    n, nb = ch["n"], ch["nb"]
+    # SURVEY §8(d) full-chain model: 0.75 B/base + 12 B/block + 44 B/chain
+    algo = 0.75 * res["bases"] + 12.0 * nb + 44.0 * n
+    step = roofline(algo, res["step_ms"], None, "whole call (plan + tile map + k_tile + combine)")
+    tile = roofline(algo, res["tile_ms"], pmc, "k_tile")
+    return {"workload": "scoreChain: every C5 chain, global + local + aligned bases",
+            "value": res["bases"] / (res["step_ms"] / 1e3) / 1e9, "unit": "Gbases/s",
+            "ms_per_step": res["step_ms"], "steps": steps, "chains": n, "blocks": nb,
+            "scored_bases": res["bases"], "kernel_ms": res["kernel_ms"],
+            "model": "full chain: 0.75 B/base + 12 B/block + 44 B/chain",
+            "roofline_step": step, "roofline": tile}
 
 
 PMC_PASSES = ("TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum",
               "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum")
 
 
-def pmc_traffic(args):
-    """HBM-side bytes per k_tile launch, measured in this run: two rocprofv3
-    --kernel-trace --pmc passes (no other trace domains; 3 and 2 TCC counters)
-    over a child process that runs the kernel leg's call.  Bytes by request
-    size, as MI355X_MICROARCH.md's HBM section prescribes for gfx950 (not
-    FETCH_SIZE, which tallies every request at 64 B): reads = 32 n32 + 64 n64
-    + 128 n128, writes = 64 n64 + 32 (n - n64).  Run before this process
-    touches the GPU.  Returns None on any failure (reported, never fatal)."""
+def pmc_traffic(args, which):
+    """HBM-side bytes per k_tile launch of one leg, measured in this run: two
+    rocprofv3 --kernel-trace --pmc passes (no other trace domains; 3 and 2
+    TCC counters) over a child process that makes the leg's call.  Bytes by
+    request size, as MI355X_MICROARCH.md's HBM section prescribes for gfx950
+    (not FETCH_SIZE): reads = 32 n32 + 64 n64 + 128 n128, writes = 64 n64 +
+    32 (n - n64).  Run before this process touches the GPU.  Returns None on
+    any failure (reported, never fatal)."""
     import csv
     import glob
     import shutil
     import tempfile
     if not shutil.which("rocprofv3"):
         return None
-    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--chains", str(args.chains),
-             "--seed", str(args.seed), "--workload", args.workload, "--order", args.order,
-             "--tmp", args.tmp]
+    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", which, "--chains",
+             str(args.chains), "--seed", str(args.seed), "--tmp", args.tmp]
     vals, durs = {}, []
     root = tempfile.mkdtemp(prefix="gac_pmc_", dir="/tmp")
     env = dict(os.environ, TMPDIR="/tmp")
     for i, counters in enumerate(PMC_PASSES):
         out = os.path.join(root, f"pass{i}")
-        cmd = ["timeout", "-s", "KILL", "180", "rocprofv3", "--kernel-trace", "--pmc",
+        cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--kernel-trace", "--pmc",
                *counters.split(), "--output-format", "csv", "-d", out, "-o", "run", "--", *child]
-        r = subprocess.run(cmd, capture_output=True, text=True, cwd="/tmp", env=env, timeout=240)
+        r = subprocess.run(cmd, capture_output=True, text=True, cwd="/tmp", env=env, timeout=300)
         if r.returncode != 0:
-            log(f"pmc pass {i} rc={r.returncode}: {r.stderr[-800:]}")
+            log(f"pmc {which} pass {i} rc={r.returncode}: {r.stderr[-800:]}")
             return None
         per = {}
         for path in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
@@ -376,7 +369,7 @@ def pmc_traffic(args):
         for (_, c), v in per.items():
             by.setdefault(c, []).append(v)
         if not by:
-            log(f"pmc pass {i}: no k_tile rows")
+            log(f"pmc {which} pass {i}: no k_tile rows")
             return None
         vals.update({c: sum(v) / len(v) for c, v in by.items()})
         for path in glob.glob(os.path.join(out, "**", "*kernel_trace.csv"), recursive=True):
@@ -400,161 +393,16 @@ def pmc_traffic(args):
 
 
 def pmc_child(args):
-    """The counter passes' workload: the kernel leg's call, a few times."""
-    d, _ = c2_files(args)
-    ca, ranges = kernel_ranges(args, d)
-    kernel_leg(args, d, 3, ca, ranges)
-
-
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "k_tile_traffic.json")
-
-
-def _pmc_traffic(args, n, nblk):
-    """HBM bytes per k_tile launch from the committed PMC profile of this same
-    kernel-leg workload (scripts/gpu_counters.sh + scripts/pmc_summary.py),
-    or None when no profile matches it."""
-    try:
-        with open(TRAFFIC_FILE) as f:
-            t = json.load(f)
-    except (OSError, ValueError):
-        return None
-    wl = "scorechain" if args.workload == "scorechain" else "rescore"
-    if (t.get("workload") != wl or t.get("ranges") != n or t.get("blocks") != nblk
-            or t.get("chains") != args.chains or t.get("seed") != args.seed
-            or t.get("order", "net") != args.order):
-        return None
-    return t.get("hbm_bytes_per_launch")
-
-
-def _query_key(ca, ranges):
-    """(query sequence id, forward-strand query position of the first window
-    block) per range: the query-plane order of the fills."""
-    names = {n: i for i, n in enumerate(dict.fromkeys(ca.qname))}
-    qid = np.array([names[n] for n in ca.qname], np.int64)[ranges[:, 0]]
-    pos = np.zeros(len(ranges), np.int64)
-    for i, (c, s, _) in enumerate(ranges):
-        a, b = int(ca.blk_off[c]), int(ca.blk_off[c + 1])
-        k = a + int(np.searchsorted(ca.blk_t[a:b] + ca.blk_size[a:b], s, side="right"))
-        k = min(k, b - 1)
-        q = int(ca.blk_q[k])
-        pos[i] = int(ca.qsize[c]) - q if ca.qstrand[c] else q
-    return qid, pos
-
-
-def _window_blocks(ca, ranges):
-    """Blocks selected by each range (host binary search, for the byte model)."""
-    tot = 0
-    for c, s, e in ranges:
-        bt, _, bs = ca.blocks(int(c))
-        if s <= bt[0] and e >= bt[-1] + bs[-1]:
-            tot += len(bt)
-            continue
-        lo = np.searchsorted(bt + bs, s, side="right")
-        hi = np.searchsorted(bt, e, side="left")
-        tot += max(0, int(hi - lo))
-    return tot
+    """The counter passes' workload: one leg's call, a few times."""
+    d, _ = c5_files(args)
+    ch = load_chains_bin(d)
+    legs = Legs(d, ch)
+    ranges = fills_ranges(d) if args.pmc_child == "fills" else chain_ranges(ch)
+    legs.run(ranges, args.pmc_child == "scorechain", 3)
+    legs.close()
 
 
 # ---------------------------------------------------------------- CPU baseline
-def cpu_baseline(args, d, info, ours):
-    """The reference chainNet (oracle/_ref, compiled from /root/reference) on
-    the same files: one process, then split per chromosome side over all
-    host cores; nets compared with ours."""
-    p = lambda x: os.path.join(d, x)
-    if not os.path.exists(REF_TOOL):
-        return {"error": f"{REF_TOOL} not built (make ref)"}
-    opts = ["-rescore", f"-tNibDir={p('t.2bit')}", f"-qNibDir={p('q.2bit')}", "-linearGap=loose"]
-    ref = p("ref")
-    t0 = time.time()
-    run_tool([REF_TOOL, p("in.chain"), p("t.sizes"), p("q.sizes"), ref + ".t.net", ref + ".q.net"]
-             + opts, [ref + ".t.net", ref + ".q.net"])
-    t1 = time.time() - t0
-    same = (filecmp.cmp(ours + ".t.net", ref + ".t.net", False)
-            and filecmp.cmp(ours + ".q.net", ref + ".q.net", False))
-    log(f"cpu baseline: reference chainNet -rescore {t1:.2f}s, nets identical: {same}")
-    out = {"value": info["netted_aligned_bases"] / t1 / 1e9, "unit": "Gbases/s", "cores": 1,
-           "kind": "reference", "seconds": t1, "identical_nets": same,
-           "sample": f"the whole workload: reference chainNet -rescore (oracle/_ref) on the same "
-                     f"C2 files, one process ({t1:.2f}s)"}
-    if not args.no_all_cores:
-        try:
-            out["all_cores"] = ref_all_cores(d, opts, ref)
-        except Exception as ex:  # reported, never fatal
-            out["all_cores"] = {"error": str(ex)[:300]}
-    return out
-
-
-def ref_all_cores(d, opts, ref):
-    """The reference run per chromosome side over all host cores: a target
-    sequence's net depends only on the chains on it (a query sequence's
-    likewise), so the chains are split by target sequence (target nets) and
-    by query sequence (query nets) and the reference runs on every group
-    concurrently; the groups' nets are reassembled and compared."""
-    from concurrent.futures import ThreadPoolExecutor
-    p = lambda x: os.path.join(d, x)
-    gd = p("ref_groups")
-    os.makedirs(gd, exist_ok=True)
-    groups = _split_chain_file(p("in.chain"), gd)
-    cores = host_threads()
-    jobs = []
-    for side, name, path in groups:
-        o = os.path.join(gd, f"{side}.{len(jobs)}")
-        jobs.append((side, name, [REF_TOOL, path, p("t.sizes"), p("q.sizes"), o + ".t.net",
-                                  o + ".q.net"] + opts, o))
-    t0 = time.time()
-    with ThreadPoolExecutor(max_workers=cores) as ex:
-        list(ex.map(lambda j: run_tool(j[2], [j[3] + ".t.net", j[3] + ".q.net"]), jobs))
-    wall = time.time() - t0
-    same = True
-    for side in ("t", "q"):
-        parts = {}
-        for s, name, _, o in jobs:
-            if s == side:
-                with open(o + f".{side}.net") as f:
-                    parts[name] = _net_sections(f.read())[1].get(name, "")
-        with open(ref + f".{side}.net") as f:
-            whole = f.read()
-        meta, _, order = _net_sections(whole)
-        same = same and meta + "".join(parts.get(k, "") for k in order) == whole
-    import shutil
-    shutil.rmtree(gd, ignore_errors=True)
-    log(f"cpu baseline (all cores): {len(jobs)} reference runs on {cores} cores, {wall:.2f}s, "
-        f"reassembled nets identical: {same}")
-    return {"seconds": wall, "cores": cores, "processes": len(jobs), "identical_nets": same}
-
-
-def _split_chain_file(path, gd):
-    """Chain text split by target and by query sequence (file order kept,
-    leading '#' lines copied to every group) -> [(side, sequence, file)]."""
-    meta, tg, qg = [], {}, {}
-    cur, cur_t, cur_q = [], None, None
-
-    def flush():
-        if cur_t is not None:
-            rec = "\n".join(cur) + "\n"
-            tg.setdefault(cur_t, []).append(rec)
-            qg.setdefault(cur_q, []).append(rec)
-    with open(path) as f:
-        for line in f.read().split("\n"):
-            if cur_t is None and line.startswith("#"):
-                meta.append(line + "\n")
-            elif line.startswith("chain "):
-                flush()
-                w = line.split()
-                cur, cur_t, cur_q = [line], w[2], w[7]
-            elif cur_t is not None:
-                cur.append(line)
-    flush()
-    out = []
-    for side, g in (("t", tg), ("q", qg)):
-        for k, (name, recs) in enumerate(g.items()):
-            fn = os.path.join(gd, f"in.{side}{k}.chain")
-            with open(fn, "w") as f:
-                f.write("".join(meta) + "".join(recs))
-            out.append((side, name, fn))
-    return out
-
-
 def _net_sections(text):
     """('#' header, {sequence: its 'net' section}, sequence order) of .net text."""
     meta_end = 0
@@ -572,13 +420,91 @@ def _net_sections(text):
     return text[:meta_end], secs, order
 
 
+def _sample_chains(path, targets, dst):
+    """The chains of `path` whose target is in `targets` (file order kept):
+    their aligned bases up to the netting stop."""
+    keep = set(targets)
+    out, bases, stopped, cur = [], 0, False, None
+    with open(path) as f:
+        for line in f:
+            if line.startswith("chain "):
+                w = line.split()
+                cur = w[2] in keep
+                if cur:
+                    out.append(line)
+                    stopped = stopped or float(w[1]) < 0
+            elif cur:
+                out.append(line)
+                if not stopped and line.strip():
+                    bases += int(line.split()[0])
+    with open(dst, "w") as f:
+        f.writelines(out)
+    return bases
+
+
+def cpu_baseline_c5(d, ours):
+    """The reference chainNet -rescore on a bounded sample of C5 (the chains on
+    SAMPLE_TARGETS), one process; its target nets vs ours for those sequences."""
+    p = lambda x: os.path.join(d, x)
+    if not os.path.exists(REF_TOOL):
+        return {"error": f"{REF_TOOL} not built (make ref)"}
+    sample = p("sample.chain")
+    bases = _sample_chains(p("in.chain"), SAMPLE_TARGETS, sample)
+    ref = p("ref.sample")
+    t0 = time.time()
+    run_tool([REF_TOOL, sample, p("t.sizes"), p("q.sizes"), ref + ".t.net", ref + ".q.net",
+              "-rescore", f"-tNibDir={p('t.2bit')}", f"-qNibDir={p('q.2bit')}", "-linearGap=loose"],
+             [ref + ".t.net", ref + ".q.net"])
+    t1 = time.time() - t0
+    with open(ref + ".t.net") as f:
+        rsec = _net_sections(f.read())[1]
+    with open(ours + ".t.net") as f:
+        osec = _net_sections(f.read())[1]
+    same = all(rsec.get(k) == osec.get(k) and k in osec for k in SAMPLE_TARGETS)
+    log(f"cpu baseline: reference chainNet -rescore on the {'+'.join(SAMPLE_TARGETS)} chains "
+        f"{t1:.2f}s, target nets identical to ours: {same}")
+    return {"value": bases / t1 / 1e9, "unit": "Gbases/s", "cores": 1, "kind": "reference",
+            "seconds": t1, "identical_target_nets": same, "sample_aligned_bases": bases,
+            "sample": f"reference chainNet -rescore (oracle/_ref, one process) on the C5 chains "
+                      f"whose target is {' or '.join(SAMPLE_TARGETS)} (their netted aligned bases / "
+                      f"wall time; their target-net sections compared with the headline's)"}
+
+
+def c2_leg(args, steps, warmup):
+    d, info = c2_files(args)
+    out = os.path.join(d, "ours")
+    outs = [out + ".t.net", out + ".q.net"]
+    cmd = tool_cmd(d, out, 1, 0)
+    for _ in range(warmup):
+        run_tool(cmd, outs)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run_tool(cmd, outs)
+    dt = (time.perf_counter() - t0) / steps
+    res = {"workload": "configs[1]: chainNet -rescore end to end on C2 (hg38 chr1 x mm10)",
+           "value": info["netted_aligned_bases"] / dt / 1e9, "unit": "Gbases/s",
+           "ms_per_step": dt * 1e3, "steps": steps, **info}
+    if not args.no_cpu_baseline and os.path.exists(REF_TOOL):
+        p = lambda x: os.path.join(d, x)
+        ref = p("ref")
+        t0 = time.time()
+        run_tool([REF_TOOL, p("in.chain"), p("t.sizes"), p("q.sizes"), ref + ".t.net",
+                  ref + ".q.net", "-rescore", f"-tNibDir={p('t.2bit')}", f"-qNibDir={p('q.2bit')}",
+                  "-linearGap=loose"], [ref + ".t.net", ref + ".q.net"])
+        t1 = time.time() - t0
+        same = (filecmp.cmp(out + ".t.net", ref + ".t.net", False)
+                and filecmp.cmp(out + ".q.net", ref + ".q.net", False))
+        res["cpu_reference"] = {"seconds": t1, "cores": 1, "identical_nets": same,
+                                "value": info["netted_aligned_bases"] / t1 / 1e9}
+        log(f"C2: ours {dt * 1e3:.1f} ms, reference {t1:.2f}s, nets identical: {same}")
+    return res
+
+
 # ---------------------------------------------------------------- main
 def main():
     args = parse()
     if args.gen_only:
-        c2_files(args)
-        if args.replicas > 1:
-            c2n_files(args, args.replicas)
+        c5_files(args)
         return
     if args.pmc_child:
         pmc_child(args)
@@ -586,18 +512,23 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if os.environ.get("GAC_BENCH_ONE_GPU"):  # rehearsal on a one-GPU box: every rank on device 0
+    one_gpu = bool(os.environ.get("GAC_BENCH_ONE_GPU"))  # rehearsal: every rank on device 0
+    if one_gpu:
         local = 0
         os.environ["LOCAL_RANK"] = "0"
+
+    d = info = None
+    if rank == 0:  # generated before any process opens a device
+        d, info = c5_files(args)
+    dist = None
     if world > 1:
         import torch
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        if os.environ.get("GAC_BENCH_ONE_GPU"):  # (RCCL wants one device per rank)
+        if one_gpu:  # (RCCL wants one device per rank)
             dist.init_process_group("gloo", rank=rank, world_size=world)
         else:
+            torch.cuda.set_device(local)
             dist.init_process_group("nccl", rank=rank, world_size=world,
                                     device_id=torch.device(f"cuda:{local}"))
 
@@ -605,19 +536,21 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    files = (lambda: c2_files(args)) if world == 1 else (lambda: c2n_files(args, world))
-    if rank == 0:  # generated in a child process: this one stays small
-        subprocess.run([sys.executable, os.path.abspath(__file__), "--gen-only", "--chains",
-                        str(args.chains), "--seed", str(args.seed), "--tmp", args.tmp,
-                        "--replicas", str(world)], check=True)
-        d, info = files()
     barrier()
     if rank != 0:
-        d, info = files()  # written by rank 0 (same node)
+        d, info = c5_files(args)  # written by rank 0 (same node)
     out_base = os.path.join(d, f"ours.r{world}")
     outs = [out_base + ".t.net", out_base + ".q.net"]
-    cmd = tool_cmd(d, out_base, world, rank)
+    ch = None
+    stages = pmc_f = pmc_s = None
+    if rank == 0 and world == 1:
+        stages = staged_run(d, out_base)  # also dumps the fills for the kernel leg
+        if not (args.no_pmc or args.no_kernel):
+            pmc_f = pmc_traffic(args, "fills")
+            if not args.no_scorechain:
+                pmc_s = pmc_traffic(args, "scorechain")
 
+    cmd = tool_cmd(d, out_base, world, rank)
     # every rank of one step shares a marker token (tells this step's part
     # markers from an earlier, failed one's; see gt_ranks_place)
     run_id = f"{os.environ.get('TORCHELASTIC_RUN_ID', 'x')}-{os.environ.get('MASTER_PORT', '0')}"
@@ -627,57 +560,50 @@ def main():
         step_no[0] += 1
         return dict(os.environ, GAC_RANK_TOKEN=f"{run_id}-{step_no[0]}")
 
-    if args.workload == "chainnet":
-        for _ in range(args.warmup):
-            barrier()
-            run_tool(cmd, outs if rank == 0 else [], env=step_env())
+    for _ in range(args.warmup):
         barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            run_tool(cmd, outs if rank == 0 else [], env=step_env())
-            barrier()  # rank 0 finishes last (it waits for every part)
-        dt = time.perf_counter() - t0
-        if dist is not None:
-            from genomealignmenttools_amd.shard import reduce_time_and_work
-            dev = "cpu" if os.environ.get("GAC_BENCH_ONE_GPU") else f"cuda:{local}"
-            dt, _ = reduce_time_and_work(dist, dt, 0.0, device=dev)
-        step_s = dt / args.steps
-        stages = None
-        if world == 1:  # one more, untimed run for the per-stage breakdown
-            r = run_tool(cmd + ["-verbose=2"], outs)
-            stages = [line.strip() for line in r.stderr.splitlines() if "[stage]" in line]
-        out = {
-            "metric": METRIC,
-            "value": info["netted_aligned_bases"] / step_s / 1e9,
-            "unit": "Gbases/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": step_s * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "int64",
-            "data": "synthetic (seeded C2: hg38 chr1 x mm10 sizes, planted chains; no real genomes)"
-                    + ("" if world == 1 else f"; C2 replicated x{world}: {world} target "
-                       "chromosomes (copies of C2's chr1) in one chain set"),
-            "config": {"workload": "chainNet -rescore end to end (bin/chainNet, C2"
-                                   + (")" if world == 1 else f" per GPU, one set over {world} "
-                                      "target chromosomes, chromosome sides split across ranks)"),
-                       **info, "parallelism": f"chromosome-side shards x{world}",
-                       "host_threads_per_rank": host_threads(), "tool_stages": stages},
-        }
-    else:
-        out = {"metric": METRIC, "n_gpus": world, "unit": "Gbases/s", "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "int64",
-               "data": "synthetic (seeded C2)", "config": {"workload": args.workload, **info}}
-    if rank == 0 and not args.no_kernel:
-        ca, ranges = kernel_ranges(args, d)
-        # counter passes in child processes before this one opens the device
-        pmc = None if (args.no_pmc or world > 1) else pmc_traffic(args)
-        kernel, roof = kernel_leg(args, d, args.kernel_steps, ca, ranges, pmc)
-        out["kernel"] = kernel
-        out["roofline"] = roof
-        if args.workload != "chainnet":  # the kernel call itself is the step
-            out.update(value=kernel["value"], steps=args.kernel_steps, warmup=3,
-                       ms_per_step=kernel["ms_per_step"])
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "chainnet":
+        run_tool(cmd, outs if rank == 0 else [], env=step_env())
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run_tool(cmd, outs if rank == 0 else [], env=step_env())
+        barrier()  # rank 0 finishes last (it waits for every part)
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        from genomealignmenttools_amd.shard import reduce_time_and_work
+        dev = "cpu" if one_gpu else f"cuda:{local}"
+        dt, _ = reduce_time_and_work(dist, dt, 0.0, device=dev)
+    step_s = dt / args.steps
+    out = {
+        "metric": METRIC,
+        "value": info["netted_aligned_bases"] / step_s / 1e9,
+        "unit": "Gbases/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": step_s * 1e3, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic (seeded C5 by gac_synth: all 455 hg38 x 66 mm10 sequences at their "
+                "real sizes, planted chains; no real genomes)",
+        "config": {"workload": "chainNet -rescore end to end (bin/chainNet), C5 whole genome"
+                               + ("" if world == 1 else f", chromosome sides split over {world} ranks"),
+                   **info, "parallelism": f"chromosome-side shards x{world}",
+                   "host_threads_per_rank": host_threads(), "tool_stages": stages},
+    }
+    if rank == 0 and world == 1 and not args.no_c2:
         try:
-            out["cpu_baseline"] = cpu_baseline(args, d, info, out_base)
+            out["c2"] = c2_leg(args, args.c2_steps, 1)
+        except Exception as ex:  # reported, never fatal
+            out["c2"] = {"error": str(ex)[:300]}
+    if rank == 0 and not args.no_kernel:
+        if world > 1 and not os.path.exists(os.path.join(d, "fills.bin")):
+            staged_run(d, os.path.join(d, "ours.fills"))  # untimed, after the timed region
+        ch = load_chains_bin(d)
+        legs = Legs(d, ch)
+        out["kernel"], out["roofline"] = fills_leg(legs, d, ch, args.kernel_steps, pmc_f)
+        if not args.no_scorechain:
+            out["scorechain"] = scorechain_leg(legs, ch, args.kernel_steps, pmc_s)
+        legs.close()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline_c5(d, out_base)
         except Exception as ex:  # reported, never fatal
             out["cpu_baseline"] = {"error": str(ex)[:300]}
     if rank == 0:

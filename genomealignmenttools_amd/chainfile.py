@@ -45,21 +45,18 @@ class ChainArrays:
 
     def subset(self, idx) -> "ChainArrays":
         idx = np.asarray(idx, dtype=np.int64)
-        offs = [0]
-        bt, bq, bs = [], [], []
-        for i in idx:
-            t, q, s = self.blocks(int(i))
-            bt.append(t)
-            bq.append(q)
-            bs.append(s)
-            offs.append(offs[-1] + len(s))
-        cat = (lambda xs: np.concatenate(xs).astype(np.int32) if xs else np.zeros(0, np.int32))
+        lens = self.blk_off[idx + 1] - self.blk_off[idx]
+        offs = np.zeros(len(idx) + 1, np.int64)
+        np.cumsum(lens, out=offs[1:])
+        src = np.repeat(self.blk_off[idx] - offs[:-1], lens) + np.arange(offs[-1], dtype=np.int64)
+        as32 = lambda x: np.ascontiguousarray(x[src], dtype=np.int32)
         return ChainArrays(
             score=self.score[idx], tname=[self.tname[i] for i in idx], tsize=self.tsize[idx],
             tstart=self.tstart[idx], tend=self.tend[idx], qname=[self.qname[i] for i in idx],
             qsize=self.qsize[idx], qstrand=self.qstrand[idx], qstart=self.qstart[idx],
-            qend=self.qend[idx], id=self.id[idx], blk_off=np.asarray(offs, np.int64),
-            blk_t=cat(bt), blk_q=cat(bq), blk_size=cat(bs), meta=list(self.meta))
+            qend=self.qend[idx], id=self.id[idx], blk_off=offs,
+            blk_t=as32(self.blk_t), blk_q=as32(self.blk_q), blk_size=as32(self.blk_size),
+            meta=list(self.meta))
 
 
 def _open_text(path: str) -> str:
@@ -180,3 +177,172 @@ def write_chains(ca: ChainArrays, path_or_file, scores: Optional[np.ndarray] = N
     finally:
         if own:
             f.close()
+
+
+# ---------------------------------------------------------------- fast writer
+def _ndig(v: np.ndarray) -> np.ndarray:
+    """Decimal digits of |v| (int64), sign excluded."""
+    a = np.abs(v)
+    nd = np.ones(len(a), np.int64)
+    p = 10
+    for _ in range(18):
+        m = a >= p
+        if not m.any():
+            break
+        nd += m
+        p *= 10
+    return nd
+
+
+def _put_int(out: np.ndarray, pos: np.ndarray, v: np.ndarray, neg: np.ndarray, nd: np.ndarray):
+    """Decimal text of v at pos ('-' first where neg); returns the end positions."""
+    if neg.any():
+        out[pos[neg]] = ord("-")
+    end = pos + neg + nd
+    a = np.abs(v)
+    k, p = 0, 1
+    while True:
+        m = nd > k
+        if not m.any():
+            break
+        out[end[m] - 1 - k] = 48 + (a[m] // p) % 10
+        k += 1
+        p *= 10
+    return end
+
+
+def _put_lit(out: np.ndarray, pos: np.ndarray, lit: bytes):
+    for k, ch in enumerate(lit):
+        out[pos + k] = ch
+    return pos + len(lit)
+
+
+def _put_str(out: np.ndarray, pos: np.ndarray, ids: np.ndarray, tab: np.ndarray, tlen: np.ndarray):
+    ln = tlen[ids]
+    for k in range(tab.shape[1]):
+        m = ln > k
+        if not m.any():
+            break
+        out[pos[m] + k] = tab[ids[m], k]
+    return pos + ln
+
+
+def _name_table(names: List[str]):
+    """(ids per entry, byte table [u, maxlen], lengths) of a name list."""
+    uniq, ids = np.unique(np.asarray(names, dtype=object).astype(str), return_inverse=True)
+    enc = [u.encode() for u in uniq]
+    tab = np.zeros((len(enc), max(1, max((len(e) for e in enc), default=1))), np.uint8)
+    for i, e in enumerate(enc):
+        tab[i, :len(e)] = np.frombuffer(e, np.uint8)
+    return ids.astype(np.int64), tab, np.array([len(e) for e in enc], np.int64)
+
+
+def write_chains_fast(ca: ChainArrays, path: str, chunk: int = 400_000) -> None:
+    """write_chains for large synthetic sets: the same bytes (chainWrite,
+    kent/src/lib/chain.c:200-227), formatted with numpy a chunk of chains at
+    a time.  Scores must be integer-valued (%1.0f of an integer double,
+    '-0' for negative zero); otherwise this falls back to write_chains."""
+    sc = np.asarray(ca.score, np.float64)
+    if ca.n and not np.array_equal(sc, np.round(sc)):
+        write_chains(ca, path)
+        return
+    tid, ttab, tlen = _name_table(ca.tname)
+    qid, qtab, qlen = _name_table(ca.qname)
+    with open(path, "wb") as f:
+        for c0 in range(0, ca.n, chunk):
+            c1 = min(ca.n, c0 + chunk)
+            s = sc[c0:c1]
+            sv = s.astype(np.int64)
+            sneg = np.signbit(s)
+            ints = {k: np.asarray(getattr(ca, k)[c0:c1], np.int64)
+                    for k in ("tsize", "tstart", "tend", "qsize", "qstart", "qend", "id")}
+            nd = {k: _ndig(v) for k, v in ints.items()}
+            ti, qi = tid[c0:c1], qid[c0:c1]
+            hlen = (6 + sneg + _ndig(sv) + 1 + tlen[ti] + 1 + nd["tsize"] + 3 + nd["tstart"] + 1
+                    + nd["tend"] + 1 + qlen[qi] + 1 + nd["qsize"] + 3 + nd["qstart"] + 1
+                    + nd["qend"] + 1 + nd["id"] + 1)
+            b0, b1 = int(ca.blk_off[c0]), int(ca.blk_off[c1])
+            nb = np.diff(ca.blk_off[c0:c1 + 1])
+            if (nb < 1).any():
+                raise ValueError("write_chains_fast: chain without blocks")
+            bt = ca.blk_t[b0:b1].astype(np.int64)
+            bq = ca.blk_q[b0:b1].astype(np.int64)
+            bs = ca.blk_size[b0:b1].astype(np.int64)
+            last = np.zeros(b1 - b0, bool)
+            last[np.cumsum(nb) - 1] = True
+            dt = np.zeros(b1 - b0, np.int64)
+            dq = np.zeros(b1 - b0, np.int64)
+            dt[:-1] = bt[1:] - (bt[:-1] + bs[:-1])
+            dq[:-1] = bq[1:] - (bq[:-1] + bs[:-1])
+            dt[last] = 0
+            dq[last] = 0
+            ndt, ndq, nds = _ndig(dt), _ndig(dq), _ndig(bs)
+            blen = np.where(last, nds + 2, nds + 3 + (dt < 0) + ndt + (dq < 0) + ndq)
+            bsum = np.add.reduceat(blen, np.r_[0, np.cumsum(nb)[:-1]])
+            tot = hlen + bsum
+            H = np.zeros(c1 - c0, np.int64)
+            np.cumsum(tot[:-1], out=H[1:])
+            out = np.empty(int(tot.sum()), np.uint8)
+            # headers
+            p = _put_lit(out, H, b"chain ")
+            p = _put_int(out, p, sv, sneg, _ndig(sv))
+            p = _put_lit(out, p, b" ")
+            p = _put_str(out, p, ti, ttab, tlen)
+            p = _put_lit(out, p, b" ")
+            p = _put_int(out, p, ints["tsize"], ints["tsize"] < 0, nd["tsize"])
+            p = _put_lit(out, p, b" + ")
+            p = _put_int(out, p, ints["tstart"], ints["tstart"] < 0, nd["tstart"])
+            p = _put_lit(out, p, b" ")
+            p = _put_int(out, p, ints["tend"], ints["tend"] < 0, nd["tend"])
+            p = _put_lit(out, p, b" ")
+            p = _put_str(out, p, qi, qtab, qlen)
+            p = _put_lit(out, p, b" ")
+            p = _put_int(out, p, ints["qsize"], ints["qsize"] < 0, nd["qsize"])
+            p = _put_lit(out, p, b" ")
+            out[p] = np.where(np.asarray(ca.qstrand[c0:c1]) != 0, ord("-"), ord("+"))
+            p = _put_lit(out, p + 1, b" ")
+            p = _put_int(out, p, ints["qstart"], ints["qstart"] < 0, nd["qstart"])
+            p = _put_lit(out, p, b" ")
+            p = _put_int(out, p, ints["qend"], ints["qend"] < 0, nd["qend"])
+            p = _put_lit(out, p, b" ")
+            p = _put_int(out, p, ints["id"], ints["id"] < 0, nd["id"])
+            _put_lit(out, p, b"\n")
+            # blocks
+            cb = np.cumsum(blen) - blen
+            ch = np.repeat(np.arange(c1 - c0), nb)
+            first = np.r_[0, np.cumsum(nb)[:-1]]
+            pos = H[ch] + hlen[ch] + cb - cb[first][ch]
+            del cb
+            e = _put_int(out, pos, bs, np.zeros(len(bs), bool), nds)
+            out[e[last]] = 10
+            out[e[last] + 1] = 10
+            nl = ~last
+            e2 = e[nl]
+            out[e2] = 9
+            e2 = _put_int(out, e2 + 1, dt[nl], dt[nl] < 0, ndt[nl])
+            out[e2] = 9
+            e2 = _put_int(out, e2 + 1, dq[nl], dq[nl] < 0, ndq[nl])
+            out[e2] = 10
+            f.write(out.tobytes())
+
+
+def save_npz(ca: ChainArrays, path: str) -> None:
+    """The arrays of a chain set (names as tables + ids), for fast reloads."""
+    tid, ttab, tlen = _name_table(ca.tname)
+    qid, qtab, qlen = _name_table(ca.qname)
+    np.savez(path, score=ca.score, tsize=ca.tsize, tstart=ca.tstart, tend=ca.tend,
+             qsize=ca.qsize, qstrand=ca.qstrand, qstart=ca.qstart, qend=ca.qend, id=ca.id,
+             blk_off=ca.blk_off, blk_t=ca.blk_t, blk_q=ca.blk_q, blk_size=ca.blk_size,
+             tid=tid.astype(np.int32), ttab=ttab, tlen=tlen, qid=qid.astype(np.int32), qtab=qtab,
+             qlen=qlen)
+
+
+def load_npz(path: str) -> ChainArrays:
+    z = np.load(path)
+    names = lambda tab, ln: [bytes(tab[i, :ln[i]]).decode() for i in range(len(ln))]
+    tn, qn = names(z["ttab"], z["tlen"]), names(z["qtab"], z["qlen"])
+    return ChainArrays(
+        score=z["score"], tname=[tn[i] for i in z["tid"]], tsize=z["tsize"], tstart=z["tstart"],
+        tend=z["tend"], qname=[qn[i] for i in z["qid"]], qsize=z["qsize"], qstrand=z["qstrand"],
+        qstart=z["qstart"], qend=z["qend"], id=z["id"], blk_off=z["blk_off"], blk_t=z["blk_t"],
+        blk_q=z["blk_q"], blk_size=z["blk_size"])

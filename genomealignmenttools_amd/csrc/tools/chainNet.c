@@ -531,6 +531,15 @@ int main(int argc, char *argv[]) {
                 rix[nr++] = i;
             }
         tscores = calloc(nf ? nf : 1, 8);
+        /* GAC_DUMP_RANGES=FILE (measurement hook, one process only): the
+         * rescored fills as int32 (chain index in file order, tStart, tEnd),
+         * in submission order -- bench.py replays them in its kernel leg */
+        const char *dump = multi ? NULL : getenv("GAC_DUMP_RANGES");
+        if (dump && *dump) {
+            FILE *df = fopen(dump, "wb");
+            if (!df || (nr && fwrite(r, sizeof(gac_range), nr, df) != (size_t)nr) || fclose(df) != 0)
+                gt_abort("can't write %s", dump);
+        }
         if (pu.started)
             gt_helper_join(pu.th);
         if (pu.cs && pu.remap) { /* -nranks: the uploaded subset's indices */
@@ -664,5 +673,6 @@ int main(int argc, char *argv[]) {
     /* the net, chains and sizes are left to process exit (freeing millions
      * of arena blocks and arrays only costs time) */
     gac_gapcalc_free(gap);
+    gt_ranks_done(&g_rk);
     gt_exit_ok();
 }

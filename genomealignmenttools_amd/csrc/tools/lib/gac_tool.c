@@ -10,6 +10,7 @@
 #include <stdarg.h>
 #include <stdlib.h>
 #include <string.h>
+#include <signal.h>
 #include <sys/stat.h>
 #include <unistd.h>
 #include <pthread.h>
@@ -561,19 +562,46 @@ void gt_check(int rc) {
 }
 
 /* ------------------------------------------------------------ ranks */
+/* The ranks of one run share a token (GAC_RANK_TOKEN, required with
+ * -nranks > 1): every part, marker and liveness file carries it in its name
+ * or content, so files a failed earlier run left behind are never read. */
+static char g_token[128];
+
+static const char *rank_token(void) { return g_token; }
+
 void gt_part_name(char *buf, size_t cap, const char *path, int r, const char *suffix) {
-    snprintf(buf, cap, "%s.gacpart%d%s", path, r, suffix);
+    snprintf(buf, cap, "%s.gacpart%d.%s%s", path, r, g_token, suffix);
 }
 
 static const gt_ranks *g_ranks;
 
-static void rank_failed_hook(void) { /* tell rank 0 this rank has failed */
+static void rank_failed_hook(void) { /* tell the waiting ranks this one has failed */
     char b[4096];
     gt_part_name(b, sizeof(b), g_ranks->key, g_ranks->me, ".failed");
     const int fd = open(b, O_WRONLY | O_CREAT | O_TRUNC, 0644);
     if (fd >= 0)
         close(fd);
 }
+
+/* "<boot id> <pid namespace> <pid>": a waiting rank on the same machine and
+ * in the same pid namespace can tell whether a peer process still exists */
+static void self_identity(char *b, size_t cap) {
+    char boot[64] = "?", ns[64] = "?";
+    FILE *f = fopen("/proc/sys/kernel/random/boot_id", "r");
+    if (f) {
+        if (fscanf(f, "%63s", boot) != 1)
+            strcpy(boot, "?");
+        fclose(f);
+    }
+    const ssize_t k = readlink("/proc/self/ns/pid", ns, sizeof(ns) - 1);
+    ns[k > 0 ? k : 1] = 0;
+    for (char *p = ns; *p; ++p)
+        if (*p == ' ')
+            *p = '_';
+    snprintf(b, cap, "%s %s %ld", boot, ns, (long)getpid());
+}
+
+static char g_ident[192];
 
 void gt_ranks_init(gt_ranks *rk, int n, int me, const char *key) {
     rk->n = n;
@@ -583,13 +611,25 @@ void gt_ranks_init(gt_ranks *rk, int n, int me, const char *key) {
         gt_abort("-rank=%d is not in 0..%d (-nranks=%d)", me, n - 1, n);
     if (n == 1)
         return;
-    gt_ranks_clear(rk, key);
-    char b[4096];
-    gt_part_name(b, sizeof(b), key, me, ".failed");
-    unlink(b);
+    const char *t = getenv("GAC_RANK_TOKEN");
+    if (!t || !*t)
+        gt_abort("-nranks=%d: set GAC_RANK_TOKEN to one per-run value, the same on every rank "
+                 "(it tells this run's part files from an earlier run's)", n);
+    size_t j = 0;
+    for (; t[j] && j + 1 < sizeof(g_token); ++j)
+        g_token[j] = (isalnum((unsigned char)t[j]) || t[j] == '-' || t[j] == '_' || t[j] == '.')
+                         ? t[j] : '_';
+    g_token[j] = 0;
     g_ranks = rk;
-    if (me > 0)
-        gt_on_abort(rank_failed_hook);
+    gt_on_abort(rank_failed_hook); /* every rank: the others may wait on any of them */
+    /* liveness: "<key>.gacpart<r>.<token>.alive" = this process's identity */
+    self_identity(g_ident, sizeof(g_ident));
+    char b[4096], tmp[4200];
+    gt_part_name(b, sizeof(b), key, me, ".alive");
+    snprintf(tmp, sizeof(tmp), "%s.tmp", b);
+    FILE *f = fopen(tmp, "w");
+    if (!f || fprintf(f, "%s\n", g_ident) < 0 || fclose(f) != 0 || rename(tmp, b) != 0)
+        gt_abort("can't write %s: %s", b, strerror(errno));
 }
 
 void gt_ranks_clear(const gt_ranks *rk, const char *path) {
@@ -600,21 +640,86 @@ void gt_ranks_clear(const gt_ranks *rk, const char *path) {
     unlink(b);
 }
 
+/* Waiting for rank r: abort if it has failed (its .failed file), if its
+ * process is gone (same machine: its .alive identity names a pid that no
+ * longer exists), if it has not started within GAC_RANK_START_TIMEOUT
+ * seconds (default 300), or after GAC_RANK_TIMEOUT seconds in all (default
+ * 3600, for a live but stuck rank). */
+typedef struct rank_wait {
+    int r;
+    double t0, next_check;
+    int seen_alive;
+} rank_wait;
+
+static void rank_wait_init(rank_wait *w, int r) {
+    w->r = r;
+    w->t0 = now_s();
+    w->next_check = 0;
+    w->seen_alive = 0;
+}
+
+static void rank_wait_check(rank_wait *w, const gt_ranks *rk, const char *what) {
+    const double now = now_s();
+    if (now < w->next_check)
+        return;
+    w->next_check = now + 0.05;
+    char b[4096];
+    gt_part_name(b, sizeof(b), rk->key, w->r, ".failed");
+    if (access(b, F_OK) == 0)
+        gt_abort("%s: rank %d failed", what, w->r);
+    if (!w->seen_alive) {
+        gt_part_name(b, sizeof(b), rk->key, w->r, ".alive");
+        w->seen_alive = access(b, F_OK) == 0;
+    }
+    const char *st = getenv("GAC_RANK_START_TIMEOUT"), *lim = getenv("GAC_RANK_TIMEOUT");
+    const double start_limit = st ? atof(st) : 300.0, limit = lim ? atof(lim) : 3600.0;
+    if (!w->seen_alive && now - w->t0 > start_limit)
+        gt_abort("%s: rank %d did not start within %.0f s", what, w->r, start_limit);
+    if (now - w->t0 > limit)
+        gt_abort("%s: timed out waiting for rank %d", what, w->r);
+}
+
+/* 1 if rank r's process is known to be gone (same machine) */
+static int rank_dead(const gt_ranks *rk, int r) {
+    char b[4096];
+    gt_part_name(b, sizeof(b), rk->key, r, ".alive");
+    FILE *f = fopen(b, "r");
+    if (!f)
+        return 0;
+    char boot[64], ns[64], mine_boot[64], mine_ns[64];
+    long pid = 0, mine = 0;
+    const int ok = fscanf(f, "%63s %63s %ld", boot, ns, &pid) == 3;
+    fclose(f);
+    if (!(ok && sscanf(g_ident, "%63s %63s %ld", mine_boot, mine_ns, &mine) == 3 &&
+          strcmp(boot, "?") != 0 && strcmp(boot, mine_boot) == 0 && strcmp(ns, mine_ns) == 0 &&
+          pid > 0))
+        return 0; /* another machine or pid namespace: only the timeouts apply */
+    if (kill((pid_t)pid, 0) != 0)
+        return errno == ESRCH;
+    /* a killed process stays a zombie until its parent reaps it */
+    char sp[64], st[512];
+    snprintf(sp, sizeof(sp), "/proc/%ld/stat", pid);
+    f = fopen(sp, "r");
+    if (!f)
+        return 0;
+    const size_t k = fread(st, 1, sizeof(st) - 1, f);
+    fclose(f);
+    st[k] = 0;
+    const char *q = strrchr(st, ')');
+    return q && (q[2] == 'Z' || q[2] == 'X');
+}
+
 void gt_ranks_wait(const gt_ranks *rk, const char *path) {
-    const char *lim = getenv("GAC_RANK_TIMEOUT");
-    const double limit = lim ? atof(lim) : 3600.0, t0 = now_s();
     struct timespec nap = {0, 500000};
-    char b[4096], f[4096];
+    char b[4096];
     for (int r = 1; r < rk->n; ++r) {
         gt_part_name(b, sizeof(b), path, r, "");
-        gt_part_name(f, sizeof(f), rk->key, r, ".failed");
+        rank_wait w;
+        rank_wait_init(&w, r);
         while (access(b, F_OK) != 0) {
-            if (access(f, F_OK) == 0) {
-                unlink(f);
-                gt_abort("%s: rank %d failed", path, r);
-            }
-            if (now_s() - t0 > limit)
-                gt_abort("%s: timed out waiting for rank %d's part %s", path, r, b);
+            rank_wait_check(&w, rk, path);
+            if (rank_dead(rk, r) && access(b, F_OK) != 0)
+                gt_abort("%s: rank %d died without its part", path, r);
             nanosleep(&nap, NULL);
         }
     }
@@ -626,13 +731,8 @@ void gt_ranks_wait(const gt_ranks *rk, const char *path) {
  * formatted (rank 0 publishes only after truncating the file at startup),
  * and "<path>.gacdone<r>" once written.  Rank r writes at the sum of the
  * sizes of ranks < r; rank 0 waits for every done marker and removes the
- * markers.  The token (GAC_RANK_TOKEN, default "0") tells this run's
- * markers from a failed earlier run's. */
-static const char *rank_token(void) {
-    const char *t = getenv("GAC_RANK_TOKEN");
-    return t && *t ? t : "0";
-}
-
+ * markers.  The token inside tells this run's markers from an earlier
+ * run's. */
 static void marker_name(char *b, size_t cap, const char *path, const char *what, int r) {
     snprintf(b, cap, "%s.gac%s%d", path, what, r);
 }
@@ -646,29 +746,30 @@ static void put_marker(const char *path, const char *what, int r, long long v) {
         gt_abort("can't write %s: %s", b, strerror(errno));
 }
 
+static int read_marker(const char *b, long long *v) {
+    char tok[256];
+    FILE *f = fopen(b, "r");
+    if (!f)
+        return 0;
+    const int ok = fscanf(f, "%255s %lld", tok, v) == 2 && strcmp(tok, rank_token()) == 0;
+    fclose(f);
+    return ok;
+}
+
 /* the value of rank r's marker of this run, waiting for it */
 static long long get_marker(const gt_ranks *rk, const char *path, const char *what, int r) {
-    const char *lim = getenv("GAC_RANK_TIMEOUT");
-    const double limit = lim ? atof(lim) : 3600.0, t0 = now_s();
     struct timespec nap = {0, 200000};
-    char b[4096], fl[4096], tok[256];
+    char b[4096];
     marker_name(b, sizeof(b), path, what, r);
-    gt_part_name(fl, sizeof(fl), rk->key, r, ".failed");
+    rank_wait w;
+    rank_wait_init(&w, r);
     for (;;) {
-        FILE *f = fopen(b, "r");
-        if (f) {
-            long long v;
-            const int ok = fscanf(f, "%255s %lld", tok, &v) == 2 && strcmp(tok, rank_token()) == 0;
-            fclose(f);
-            if (ok)
-                return v;
-        }
-        if (access(fl, F_OK) == 0) {
-            unlink(fl);
-            gt_abort("%s: rank %d failed", path, r);
-        }
-        if (now_s() - t0 > limit)
-            gt_abort("%s: timed out waiting for rank %d", path, r);
+        long long v;
+        if (read_marker(b, &v))
+            return v;
+        rank_wait_check(&w, rk, path);
+        if (rank_dead(rk, r) && !read_marker(b, &v))
+            gt_abort("%s: rank %d died before its %s marker", path, r, what);
         nanosleep(&nap, NULL);
     }
 }
@@ -715,6 +816,20 @@ void gt_ranks_finish(const gt_ranks *rk, const char *path) {
         marker_name(b, sizeof(b), path, "done", r);
         unlink(b);
     }
+}
+
+/* the last step of a successful multi-rank run: this rank's liveness file
+ * goes (rank 0, once every part is in, also removes the others') */
+void gt_ranks_done(const gt_ranks *rk) {
+    if (rk->n <= 1)
+        return;
+    char b[4096];
+    for (int r = 0; r < rk->n; ++r)
+        if (r == rk->me || rk->me == 0) {
+            gt_part_name(b, sizeof(b), rk->key, r, ".alive");
+            unlink(b);
+        }
+    gt_on_abort(NULL);
 }
 
 void gt_ranks_append_parts(const gt_ranks *rk, const char *path, FILE *f) {

@@ -112,21 +112,25 @@ void gt_device_close_join(gt_device *d);
 void gt_exit_ok(void) __attribute__((noreturn));
 
 /* ---- multi-GPU runs: -nranks=N -rank=R (one process per GPU, one node) ----
- * Every rank writes its share of an output to <path>.gacpart<R> (renamed
- * into place when complete); rank 0 waits for the other ranks' parts and
- * assembles the output.  A rank that fails leaves <key>.gacpart<R>.failed,
- * so rank 0 fails too instead of waiting (GAC_RANK_TIMEOUT seconds at most,
- * default 3600).  key = the first output file. */
+ * The ranks of a run share GAC_RANK_TOKEN (required with N > 1); every part
+ * and marker file carries it.  A rank that fails leaves
+ * <key>.gacpart<R>.<token>.failed; each rank also publishes
+ * <key>.gacpart<R>.<token>.alive (boot id, pid namespace, pid), so a rank
+ * waiting for a peer stops at once when the peer failed or its process is
+ * gone, after GAC_RANK_START_TIMEOUT s (300) if the peer never started, and
+ * after GAC_RANK_TIMEOUT s (3600) in all.  key = the first output file. */
 typedef struct gt_ranks {
     int n, me;
     const char *key;
 } gt_ranks;
-/* checks n / me, removes this rank's stale parts of `key` and its failure
- * marker, installs the failure marker hook (me > 0) */
+/* checks n / me and the token, publishes this rank's liveness file and
+ * installs the failure-marker hook (every rank) */
 void gt_ranks_init(gt_ranks *rk, int n, int me, const char *key);
 /* removes this rank's stale part of another output */
 void gt_ranks_clear(const gt_ranks *rk, const char *path);
 void gt_part_name(char *buf, size_t cap, const char *path, int r, const char *suffix);
+/* end of a successful run: liveness files removed, failure hook off */
+void gt_ranks_done(const gt_ranks *rk);
 /* rank 0: wait until <path>.gacpart<r> exists for every r > 0 */
 void gt_ranks_wait(const gt_ranks *rk, const char *path);
 /* rank 0: append <path>.gacpart<r>, r = 1..n-1, to f, then remove them */

@@ -224,5 +224,6 @@ int main(int argc, char *argv[]) {
     /* host arrays are left to process exit */
     gt_device_close_join(&dev);
     gt_stage("device close (rest)");
+    gt_ranks_done(&rk);
     gt_exit_ok();
 }

@@ -450,7 +450,8 @@ class _Chain:
                 return t, q
 
 
-def cleaner_case(seed: int = 7, n_loci: int = 24):
+def cleaner_case(seed: int = 7, n_loci: int = 24, genomes=None, tmap=None, qmap=None,
+                 t_origin=None, q_origin=None):
     """Planted chain-breaking alignments (chainCleaner).
 
     Per locus a high-scoring chain P (the would-be breaking chain) has two
@@ -465,6 +466,11 @@ def cleaner_case(seed: int = 7, n_loci: int = 24):
     unrelated noise chains (with exact score ties) fill the space between
     loci.  Header scores are left 0: the caller rescores the chains with the
     reference scoreChain, sorts them and assigns ids.
+    genomes=(tg, qg) plants the loci into existing genomes instead (the
+    chr1-scale C3 set): tmap/qmap map the logical names chrT1/chrT2 and
+    chrQ1..3 to sequences of those genomes, t_origin/q_origin give the first
+    target position of each logical target and the first query position of
+    each logical query (their regions must not overlap).
     Returns (target Genome, query Genome, list of _Chain)."""
     rng = np.random.default_rng(seed)
     span = 56_000
@@ -472,10 +478,23 @@ def cleaner_case(seed: int = 7, n_loci: int = 24):
               "chrT2": (n_loci - n_loci // 2 + 1) * span + 20_000}
     qsizes = {"chrQ1": sum(tsizes.values()) + 40_000, "chrQ2": n_loci * 36_000 + 20_000,
               "chrQ3": n_loci * 30_000 + 20_000}
-    tg = random_genome(tsizes, seed, n_frac=0.0)
-    qg = random_genome(qsizes, seed + 1, n_frac=0.0)
+    if genomes is None:
+        tg = random_genome(tsizes, seed, n_frac=0.0)
+        qg = random_genome(qsizes, seed + 1, n_frac=0.0)
+        tmap = {k: k for k in tsizes}
+        qmap = {k: k for k in qsizes}
+        t_origin = {"chrT1": 5_000, "chrT2": 5_000}
+        q_origin = {"chrQ1": 1000, "chrQ2": 1000, "chrQ3": 1000}
+    else:
+        tg, qg = genomes
+        full = qg.sizes
+        for k in qsizes:  # the logical query's region ends where its sequence does
+            qsizes[k] = full[qmap[k]]
+            assert q_origin[k] + {"chrQ1": sum(tsizes.values()) + 40_000,
+                                  "chrQ2": n_loci * 36_000 + 20_000,
+                                  "chrQ3": n_loci * 30_000 + 20_000}[k] < qsizes[k], k
     chains: List[_Chain] = []
-    qcur = {"chrQ1": 1000, "chrQ2": 1000, "chrQ3": 1000}  # forward allocation cursors
+    qcur = dict(q_origin)  # forward allocation cursors
 
     def q_alloc(qname: str, length: int, strand: int) -> int:
         """Allocate `length` forward bases; return the start in strand coords."""
@@ -484,7 +503,10 @@ def cleaner_case(seed: int = 7, n_loci: int = 24):
         assert qcur[qname] < qsizes[qname], qname
         return f if strand == 0 else qsizes[qname] - (f + length)
 
-    locus_t = {"chrT1": 5_000, "chrT2": 5_000}
+    def chain(tname: str, qname: str, strand: int) -> "_Chain":
+        return _Chain(tmap[tname], qmap[qname], strand)
+
+    locus_t = dict(t_origin)
     for li in range(n_loci):
         tname = "chrT1" if li % 2 == 0 else "chrT2"
         x = locus_t[tname]
@@ -499,7 +521,7 @@ def cleaner_case(seed: int = 7, n_loci: int = 24):
         susp = [int(rng.choice([150, 250] if pair_locus else [20, 40, 80, 150, 300, 700]))
                 for _ in range(k)]
         # ---- P on chrQ1 '+': anchors, gaps (two-sided), suspects
-        p = _Chain(tname, "chrQ1", 0)
+        p = chain(tname, "chrQ1", 0)
         total_t = a_l + sum(gaps) + sum(susp) + a_r
         q0 = q_alloc("chrQ1", total_t + 600 * (k + 1), 0)
         t, q = p.add_run(rng, x, q0, a_l, 0.04)
@@ -539,7 +561,7 @@ def cleaner_case(seed: int = 7, n_loci: int = 24):
         # suspect), the last at the left end of the last gap
         qlen = sum(b - a for a, b in pieces) + 400 * len(pieces) + 5000
         bq = q_alloc("chrQ2", qlen, strand)
-        b = _Chain(tname, "chrQ2", strand)
+        b = chain(tname, "chrQ2", strand)
         qb = bq
         for pi, (a0, a1) in enumerate(pieces):
             tiny = pair_locus and 0 < pi < len(pieces) - 1
@@ -553,7 +575,7 @@ def cleaner_case(seed: int = 7, n_loci: int = 24):
             a0, a1 = pieces[j]
             lo, hi = (g0 + 20, a0 - 20) if a0 - g0 > g1 - a1 else (a1 + 20, g1 - 20)
             if hi - lo > 200:
-                c = _Chain(tname, "chrQ3", int(rng.integers(0, 2)))
+                c = chain(tname, "chrQ3", int(rng.integers(0, 2)))
                 clen = int(rng.integers(150, hi - lo))
                 c0 = int(rng.integers(lo, hi - clen + 1))
                 cq = q_alloc("chrQ3", clen + 200, c.strand)
@@ -565,7 +587,7 @@ def cleaner_case(seed: int = 7, n_loci: int = 24):
         while t_sp + 900 < x + span - 200 and n_noise < 10:
             n_noise += 1
             n_len = int(rng.integers(60, 700))
-            c = _Chain(tname, "chrQ3", int(rng.integers(0, 2)))
+            c = chain(tname, "chrQ3", int(rng.integers(0, 2)))
             cq = q_alloc("chrQ3", n_len + 100, c.strand)
             c.add_run(rng, t_sp, cq, n_len, float(rng.choice([0.0, 0.1, 0.3])), bmin=30,
                       bmax=300)
@@ -584,7 +606,8 @@ def cleaner_case(seed: int = 7, n_loci: int = 24):
                 f0 = qsize - (q + size)
                 qcodes[f0:f0 + size] = (m ^ 2)[::-1]
     # ---- exact score ties: duplicate a few noise chains' target and query text
-    noise = [c for c in chains if c.qname == "chrQ3" and len(c.blocks) == 1 and c.blocks[0][3] == 0.0]
+    noise = [c for c in chains
+             if c.qname == qmap["chrQ3"] and len(c.blocks) == 1 and c.blocks[0][3] == 0.0]
     for a, b2 in zip(noise[0::2], noise[1::2]):
         (ta, qa, sa, _), (tb, qb, sb, _) = a.blocks[0], b2.blocks[0]
         s = min(sa, sb)
@@ -602,6 +625,27 @@ def cleaner_case(seed: int = 7, n_loci: int = 24):
                 f0 = len(qcodes) - (q + size)
                 qcodes[f0:f0 + size] = (m ^ 2)[::-1]
     return tg, qg, chains
+
+
+def c3_case(seed: int = 42, n_chains: int = 200_000, n_loci: int = 1000,
+            sizes_dir: Optional[str] = None):
+    """C2 (hg38 chr1 x all mm10, n_chains background chains)
+    plus n_loci planted chain-breaking-alignment loci (cleaner_case's loci:
+    a higher-scoring chain whose short suspect runs break a lower chain into
+    pieces) in chr1 30 Mb onwards, their query sides on mm10 chr1/chr2/chr3.
+    The loci's header scores are 0 and the background's approximate: the
+    caller rescores every chain (scoreChain), sorts by score and numbers
+    them, as the reference pipeline would have."""
+    tg, qg, bg = c2_case(seed, n_chains, sizes_dir)
+    span = 56_000
+    t1 = 30_000_000
+    t2 = t1 + (n_loci // 2 + 1) * span + 120_000
+    _, _, loci = cleaner_case(seed + 1, n_loci, genomes=(tg, qg),
+                              tmap={"chrT1": "chr1", "chrT2": "chr1"},
+                              qmap={"chrQ1": "chr1", "chrQ2": "chr2", "chrQ3": "chr3"},
+                              t_origin={"chrT1": t1, "chrT2": t2},
+                              q_origin={"chrQ1": 1_000_000, "chrQ2": 1_000_000, "chrQ3": 1_000_000})
+    return tg, qg, concat_chains([bg, chains_to_arrays(tg, qg, loci)])
 
 
 def chains_to_arrays(tg: Genome, qg: Genome, chains) -> ChainArrays:

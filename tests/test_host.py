@@ -340,7 +340,8 @@ def test_chainnet_ranks_vs_reference(nranks, tmp_path):
     args = [p("in.chain"), p("t.sizes"), p("q.sizes")]
     procs = [subprocess.Popen([os.path.join(BIN_DIR, "chainNet")] + args +
                               [p("m.t.net"), p("m.q.net"), "-minScore=0", f"-nranks={nranks}",
-                               f"-rank={r}"], stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+                               f"-rank={r}"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                              env=dict(os.environ, GAC_RANK_TOKEN=f"t{nranks}"))
              for r in range(nranks)]
     for pr in procs:
         _, err = pr.communicate(timeout=120)
@@ -360,26 +361,84 @@ def test_chainnet_ranks_vs_reference(nranks, tmp_path):
         assert filecmp.cmp(p("m.q.net"), p("ref.q.net"), shallow=False)
 
 
+def _ranks(tool, d, chain_of, n, token="tk", env=None, only=None):
+    p = lambda x: os.path.join(d, x)
+    e = dict(os.environ, GAC_RANK_TIMEOUT="600", **({"GAC_RANK_TOKEN": token} if token else {}),
+             **(env or {}))
+    return [subprocess.Popen([tool, p(chain_of(r)), p("t.sizes"), p("q.sizes"), p("m.t.net"),
+                              p("m.q.net"), f"-nranks={n}", f"-rank={r}"],
+                             stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=e)
+            for r in (range(n) if only is None else only)]
+
+
 def test_chainnet_ranks_failure(tmp_path):
-    """A rank that fails makes rank 0 fail too (errAbort status 255), no hang
-    and no half-assembled output; bad -rank values are rejected."""
+    """A rank that fails makes every rank waiting on it fail too (errAbort
+    status 255) within seconds -- not after GAC_RANK_TIMEOUT -- whichever rank
+    it is, with no half-assembled output; bad -rank values and a missing run
+    token are rejected."""
+    import time
     from genomealignmenttools_amd._lib import BIN_DIR
     d = _c5_small(tmp_path)
     p = lambda x: os.path.join(d, x)
     with open(p("bad.chain"), "w") as f:
         f.write("chain 10 chr1 5 + 0 1\n")
     tool = os.path.join(BIN_DIR, "chainNet")
-    procs = [subprocess.Popen([tool, p("in.chain" if r == 0 else "bad.chain"), p("t.sizes"),
-                               p("q.sizes"), p("m.t.net"), p("m.q.net"), "-nranks=2",
-                               f"-rank={r}"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                              text=True, env=dict(os.environ, GAC_RANK_TIMEOUT="60"))
-             for r in range(2)]
-    outs = [pr.communicate(timeout=120) for pr in procs]
-    assert procs[1].returncode == 255
-    assert procs[0].returncode == 255 and "rank 1 failed" in outs[0][1]
+    for n, bad in ((2, 1), (3, 1), (3, 0), (4, 2)):
+        t0 = time.time()
+        procs = _ranks(tool, d, lambda r: "bad.chain" if r == bad else "in.chain", n,
+                       token=f"f{n}{bad}")
+        outs = [pr.communicate(timeout=120) for pr in procs]
+        assert time.time() - t0 < 60, (n, bad)
+        # the failing rank, rank 0 and every rank placed after it fail; ranks
+        # between 0 and it need only rank 0's sizes and may finish
+        for r in range(n):
+            if r == 0 or r >= bad:
+                assert procs[r].returncode == 255, (n, bad, r, outs[r][1][-300:])
+            if r != bad and procs[r].returncode == 255:
+                assert "failed" in outs[r][1], outs[r][1]
     r = subprocess.run([tool, p("in.chain"), p("t.sizes"), p("q.sizes"), "a", "b", "-nranks=2",
-                        "-rank=2"], capture_output=True, text=True)
+                        "-rank=2"], capture_output=True, text=True,
+                       env=dict(os.environ, GAC_RANK_TOKEN="x"))
     assert r.returncode == 255 and "-rank=2" in r.stderr
+    env = {k: v for k, v in os.environ.items() if k != "GAC_RANK_TOKEN"}
+    r = subprocess.run([tool, p("in.chain"), p("t.sizes"), p("q.sizes"), "a", "b", "-nranks=2",
+                        "-rank=0"], capture_output=True, text=True, env=env)
+    assert r.returncode == 255 and "GAC_RANK_TOKEN" in r.stderr
+
+
+def test_chainnet_ranks_killed(tmp_path):
+    """A rank killed outright (SIGKILL: no failure marker) is noticed by the
+    ranks waiting on it through its liveness file: they exit 255 within
+    seconds instead of waiting GAC_RANK_TIMEOUT; a rank that never starts
+    ends the wait after GAC_RANK_START_TIMEOUT."""
+    import signal
+    import time
+    from genomealignmenttools_amd._lib import BIN_DIR
+    d = _c5_small(tmp_path)
+    p = lambda x: os.path.join(d, x)
+    os.mkfifo(p("stall.chain"))  # rank 1 blocks opening it, after publishing its liveness
+    tool = os.path.join(BIN_DIR, "chainNet")
+    procs = _ranks(tool, d, lambda r: "stall.chain" if r == 1 else "in.chain", 3, token="kill3")
+    alive = p("m.t.net.gacpart1.kill3.alive")
+    t0 = time.time()
+    while not os.path.exists(alive) and time.time() - t0 < 60:
+        time.sleep(0.05)
+    assert os.path.exists(alive)
+    time.sleep(0.5)
+    procs[1].send_signal(signal.SIGKILL)
+    t0 = time.time()
+    outs = [pr.communicate(timeout=120) for pr in procs]
+    assert time.time() - t0 < 30
+    assert procs[1].returncode == -signal.SIGKILL
+    for r in (0, 2):
+        assert procs[r].returncode == 255 and "rank 1 died" in outs[r][1], outs[r][1]
+    # rank 2 never launched: ranks 0 and 1 give up after the start timeout
+    t0 = time.time()
+    procs = _ranks(tool, d, lambda r: "in.chain", 3, token="nostart",
+                   env={"GAC_RANK_START_TIMEOUT": "3"}, only=(0, 1))
+    outs = [pr.communicate(timeout=120) for pr in procs]
+    assert time.time() - t0 < 60
+    assert procs[0].returncode == 255 and "did not start" in outs[0][1], outs[0][1]
 
 
 @pytest.mark.parametrize("opts", [["-minScore=0"], ["-minSpace=1", "-minScore=0"],
