@@ -183,10 +183,27 @@ def run_tool(cmd, outs, env=None):
 
 def staged_run(d, out):
     """One untimed single-process run with the stage laps (-verbose=2) and
-    the rescored fills dumped for the kernel leg; returns the stage lines."""
+    the rescored fills dumped for the kernel leg.  Returns the stage lines
+    plus the attribution of the parent's wall time: spawn -> the tool's
+    process start (fork + exec of the launcher), the tool's own laps (process
+    start -> main -> ... -> its exit call), and its exit call -> the parent's
+    wait returning (process teardown: HIP runtime / driver)."""
     env = dict(os.environ, GAC_DUMP_RANGES=os.path.join(d, "fills.bin"))
+    t0 = time.time()
     r = run_tool(tool_cmd(d, out, 1, 0, ["-verbose=2"]), [out + ".t.net", out + ".q.net"], env=env)
-    return [line.strip() for line in r.stderr.splitlines() if "[stage]" in line]
+    t1 = time.time()
+    lines = [line.strip() for line in r.stderr.splitlines() if "[stage]" in line]
+    clk = {}
+    for line in r.stderr.splitlines():
+        if line.startswith("[stage-clock]"):
+            w = line.split()
+            for k in range(1, len(w) - 1, 2):
+                clk[w[k]] = float(w[k + 1])
+    if {"main", "process-start", "exit"} <= clk.keys():
+        lines.append(f"[wall] spawn -> process start {clk['process-start'] - t0:.3f} s, process "
+                     f"start -> exit call {clk['exit'] - clk['process-start']:.3f} s, exit call -> "
+                     f"parent's wait returns {t1 - clk['exit']:.3f} s (total {t1 - t0:.3f} s)")
+    return lines
 
 
 # ---------------------------------------------------------------- kernel legs
@@ -227,18 +244,23 @@ class Legs:
         log(f"legs: genomes + {ch['n']} chains in HBM ({time.time() - t0:.1f}s)")
 
     def run(self, ranges, want_local, steps):
-        """HIP-event timed calls over `ranges` (device-resident): the call's
-        wall time per step, k_tile's average launch, a per-kernel breakdown
-        and the scored bases."""
+        """HIP-event timed calls over `ranges` (device-resident; None = every
+        chain whole, gac_score_chains_device): the call's wall time per step,
+        k_tile's average launch, a per-kernel breakdown and the scored
+        bases."""
         from genomealignmenttools_amd._lib import GAC_K_COMBINE, GAC_K_PLAN, GAC_K_TILE
         e, cs = self.e, self.cs
-        n = len(ranges)
-        d_r = e.dev_alloc(max(ranges.nbytes, 16))
-        e.h2d(d_r, np.ascontiguousarray(ranges, np.int32))
+        n = cs.n_chains if ranges is None else len(ranges)
+        d_r = e.dev_alloc(16 if ranges is None else max(ranges.nbytes, 16))
+        if ranges is not None:
+            e.h2d(d_r, np.ascontiguousarray(ranges, np.int32))
         d_g = e.dev_alloc(8 * n + 8)
         d_l = e.dev_alloc(8 * n + 8) if want_local else 0
         d_a = e.dev_alloc(4 * n + 8)
-        call = lambda: e.score_ranges_device(cs, d_r, n, d_g, d_a, d_l, want_local)
+        if ranges is None:
+            call = lambda: e.score_chains_device(cs, d_g, d_a, d_l, want_local)
+        else:
+            call = lambda: e.score_ranges_device(cs, d_r, n, d_g, d_a, d_l, want_local)
         for _ in range(3):
             call()
         e.synchronize()
@@ -278,11 +300,6 @@ def fills_ranges(d):
     return np.ascontiguousarray(r)
 
 
-def chain_ranges(ch):
-    return np.ascontiguousarray(np.stack([np.arange(ch["n"], dtype=np.int32), ch["tstart"],
-                                          ch["tend"]], 1), np.int32)
-
-
 def roofline(algo, t_ms, pmc, kernel):
     roof = {"bound": "hbm", "achieved": algo / (t_ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "traffic": None, "kernel": kernel, "kernel_avg_ms": t_ms,
@@ -311,14 +328,14 @@ def fills_leg(legs, d, ch, steps, pmc):
 
 
 def scorechain_leg(legs, ch, steps, pmc):
-    ranges = chain_ranges(ch)
-    res = legs.run(ranges, True, steps)
+    res = legs.run(None, True, steps)
     n, nb = ch["n"], ch["nb"]
     # SURVEY §8(d) full-chain model: 0.75 B/base + 12 B/block + 44 B/chain
     algo = 0.75 * res["bases"] + 12.0 * nb + 44.0 * n
-    step = roofline(algo, res["step_ms"], None, "whole call (plan + tile map + k_tile + combine)")
+    step = roofline(algo, res["step_ms"], None, "whole call (k_tile + cross-tile fold)")
     tile = roofline(algo, res["tile_ms"], pmc, "k_tile")
-    return {"workload": "scoreChain: every C5 chain, global + local + aligned bases",
+    return {"workload": "scoreChain: every C5 chain, global + local + aligned bases "
+                        "(gac_score_chains_device)",
             "value": res["bases"] / (res["step_ms"] / 1e3) / 1e9, "unit": "Gbases/s",
             "ms_per_step": res["step_ms"], "steps": steps, "chains": n, "blocks": nb,
             "scored_bases": res["bases"], "kernel_ms": res["kernel_ms"],
@@ -397,7 +414,7 @@ def pmc_child(args):
     d, _ = c5_files(args)
     ch = load_chains_bin(d)
     legs = Legs(d, ch)
-    ranges = fills_ranges(d) if args.pmc_child == "fills" else chain_ranges(ch)
+    ranges = fills_ranges(d) if args.pmc_child == "fills" else None
     legs.run(ranges, args.pmc_child == "scorechain", 3)
     legs.close()
 

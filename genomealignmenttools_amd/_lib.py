@@ -147,6 +147,11 @@ _PROTOS = {
         [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_uint32, C.c_void_p, C.c_void_p,
          C.c_void_p, C.c_void_p],
     ),
+    "gac_score_chains": (
+        C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "gac_score_chains_device": (
+        C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
+                  C.c_void_p]),
     "gac_score_blocks": (
         C.c_int,
         [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,

@@ -58,6 +58,10 @@ hipError_t launch_scatter(const SparseRun *runs, int64_t n, const uint64_t *comp
                           uint64_t *raw, hipStream_t s);
 hipError_t launch_blocks(const ScoreArgs &a, const BlockJob *jobs, int64_t n, int32_t *out,
                          hipStream_t s);
+hipError_t launch_whole_plan(const DChain *chains, int64_t n, RangeDesc *rdesc, int32_t *nblk,
+                             int32_t *gflat, int32_t *tile_r0, hipStream_t s);
+hipError_t launch_zero_list(const int32_t *list, int64_t n, long long *g, long long *l,
+                            int32_t *ali, hipStream_t s);
 }  // namespace gac
 
 using namespace gac;
@@ -148,6 +152,8 @@ struct gac_ctx {
     int64_t ws_tiles = 0;
     int32_t *tile_r0 = nullptr;              // [ws_tiles]
     SegSum *sum_head = nullptr, *sum_tail = nullptr;
+    SegSum *sup_head = nullptr, *sup_tail = nullptr;  // [ws_tiles / 64 + 2]
+    int32_t *sup_tail_r = nullptr;
     // staging for the host API
     int64_t io_n = 0;
     Range *d_ranges = nullptr;
@@ -186,6 +192,16 @@ struct gac_chainset {
     uint32_t gap_version = 0;  // scoring setup the blk[].w gaps were computed for
     int2 *tspan = nullptr;  // {tStart, tEnd}
     uint32_t *bucket = nullptr;  // per-chain bucket indexes
+    // whole-chain plan (gac_score_chains; built at its first call): the
+    // scoring workspace of the batch "range c = chain c", fixed per set
+    bool w_ready = false;
+    RangeDesc *w_rdesc = nullptr;  // [n_chains]
+    int32_t *w_nblk = nullptr;     // [n_chains]
+    int32_t *w_gflat = nullptr;    // [n_chains] first block (= flat offset)
+    int32_t *w_tile_r0 = nullptr;  // [tiles] chain owning each tile's first block
+    int32_t *w_status = nullptr;   // {W, T, 0, 0}
+    int32_t *w_empty = nullptr;    // chains without blocks (their results are 0)
+    int64_t w_nempty = 0;
 };
 
 // ----------------------------------------------------------------- context
@@ -235,7 +251,7 @@ extern "C" int gac_open(int device, gac_ctx **out) {
         return gac_fail(GAC_E_HIP, "hipEventCreate failed");
     }
     lap("hipStreamCreate");
-    c->combine_grid = prop.multiProcessorCount * 8;  // one 64-range group per wave
+    c->combine_grid = prop.multiProcessorCount * 8;  // k_fold_tiles: 32 waves per CU
     c->tile_grid_g = prop.multiProcessorCount * persistent_blocks_per_cu(0);
     c->tile_grid_l = prop.multiProcessorCount * persistent_blocks_per_cu(1);
     lap("occupancy (code object)");
@@ -280,6 +296,7 @@ extern "C" void gac_close(gac_ctx *c) {
     free_genome(c->g[1]);
     void *bufs[] = {c->d_small,  c->d_gap_tab, c->rdesc,    c->nblk,     c->goff, c->pb0, c->agg, c->plan_off, c->gflat,
                     c->status,   c->tile_r0,  c->sum_head, c->sum_tail,
+                    c->sup_head, c->sup_tail, c->sup_tail_r,
                     c->d_ranges, c->d_g,      c->d_l,      c->d_ali};
     for (void *p : bufs)
         if (p) hipFree(p);
@@ -1392,6 +1409,9 @@ extern "C" void gac_chains_free(gac_chainset *cs) {
     if (cs->blk) hipFree(cs->blk);
     if (cs->tspan) hipFree(cs->tspan);
     if (cs->bucket) hipFree(cs->bucket);
+    void *w[] = {cs->w_rdesc, cs->w_nblk, cs->w_gflat, cs->w_tile_r0, cs->w_status, cs->w_empty};
+    for (void *p : w)
+        if (p) hipFree(p);
     delete cs;
 }
 
@@ -1429,14 +1449,19 @@ static int ensure_ws(gac_ctx *c, int64_t n, int64_t max_tiles, hipStream_t s) {
     }
     if (max_tiles > c->ws_tiles) {
         int64_t cap = max_tiles + max_tiles / 4 + 1024;
-        if (c->sum_head) hipFree(c->sum_head);
-        if (c->sum_tail) hipFree(c->sum_tail);
-        if (c->tile_r0) hipFree(c->tile_r0);
-        c->sum_head = c->sum_tail = nullptr;
-        c->tile_r0 = nullptr;
+        void *old[] = {c->sum_head, c->sum_tail, c->tile_r0, c->sup_head, c->sup_tail,
+                       c->sup_tail_r};
+        for (void *p : old)
+            if (p) hipFree(p);
+        c->sum_head = c->sum_tail = c->sup_head = c->sup_tail = nullptr;
+        c->tile_r0 = c->sup_tail_r = nullptr;
+        const int64_t ucap = cap / kWave + 2;
         HIPCHK(hipMalloc(&c->sum_head, cap * sizeof(SegSum)));
         HIPCHK(hipMalloc(&c->sum_tail, cap * sizeof(SegSum)));
         HIPCHK(hipMalloc(&c->tile_r0, cap * 4));
+        HIPCHK(hipMalloc(&c->sup_head, ucap * sizeof(SegSum)));
+        HIPCHK(hipMalloc(&c->sup_tail, ucap * sizeof(SegSum)));
+        HIPCHK(hipMalloc(&c->sup_tail_r, ucap * 4));
         c->ws_tiles = cap;
     }
     return GAC_OK;
@@ -1575,6 +1600,9 @@ static int score_device_split(gac_ctx *c, const ScoreArgs &a_base, const Range *
         a.tile_r0 = c->tile_r0;
         a.sum_head = c->sum_head;
         a.sum_tail = c->sum_tail;
+        a.sup_head = c->sup_head;
+        a.sup_tail = c->sup_tail;
+        a.sup_tail_r = c->sup_tail_r;
         a.host_status = c->d_h_stat;
         a.call_tag = ++c->call_seq;
         if (a.call_tag <= 0) a.call_tag = c->call_seq = 1;
@@ -1616,6 +1644,129 @@ static int score_device_split(gac_ctx *c, const ScoreArgs &a_base, const Range *
         if (rc != GAC_OK) return rc;
     }
     return gac_fail(GAC_E_STATE, "scoring workspace still too small after growing it");
+}
+
+// ----------------------------------------------------------------- whole chains
+// scoreChain's batch: every chain of the set, in order (kent chainCalcScore +
+// chainCalcScoreLocal per chain).  The plan is the chain set's own, built
+// once; a call is the empty-chain zeroing (if any), k_tile and the fold.
+static int ensure_whole(gac_ctx *c, gac_chainset *cs, hipStream_t s) {
+    if (cs->w_ready) return GAC_OK;
+    const int64_t n = cs->n_chains, nb = cs->n_blocks;
+    const int64_t T = (nb + kTileBlocks - 1) / kTileBlocks;
+    HIPCHK(hipMalloc(&cs->w_rdesc, std::max<int64_t>(n, 1) * sizeof(RangeDesc)));
+    HIPCHK(hipMalloc(&cs->w_nblk, std::max<int64_t>(n, 1) * 4));
+    HIPCHK(hipMalloc(&cs->w_gflat, std::max<int64_t>(n, 1) * 4));
+    HIPCHK(hipMalloc(&cs->w_tile_r0, std::max<int64_t>(T, 1) * 4));
+    HIPCHK(hipMalloc(&cs->w_status, kStatusBytes));
+    HIPCHK(launch_whole_plan(cs->chains, n, cs->w_rdesc, cs->w_nblk, cs->w_gflat, cs->w_tile_r0, s));
+    const int32_t st[8] = {(int32_t)nb, (int32_t)T, 0, 0, 0, 0, 0, 0};
+    HIPCHK(hipMemcpyAsync(cs->w_status, st, sizeof(st), hipMemcpyHostToDevice, s));
+    // chains without blocks: their results are zeroed by every call
+    std::vector<int32_t> nblk(n);
+    HIPCHK(hipMemcpyAsync(nblk.data(), cs->w_nblk, n * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<int32_t> empty;
+    for (int64_t i = 0; i < n; ++i)
+        if (nblk[i] == 0) empty.push_back((int32_t)i);
+    cs->w_nempty = (int64_t)empty.size();
+    if (!empty.empty()) {
+        HIPCHK(hipMalloc(&cs->w_empty, empty.size() * 4));
+        HIPCHK(hipMemcpy(cs->w_empty, empty.data(), empty.size() * 4, hipMemcpyHostToDevice));
+    }
+    cs->w_ready = true;
+    return GAC_OK;
+}
+
+static int score_whole(gac_ctx *c, const gac_chainset *cs_in, uint32_t flags, long long *d_g,
+                       long long *d_l, int32_t *d_ali, hipStream_t s) {
+    gac_chainset *cs = const_cast<gac_chainset *>(cs_in);
+    ScoreArgs a;
+    if (c->ws_last && c->ws_last != s) HIPCHK(hipStreamWaitEvent(s, c->ws_ev, 0));
+    int rc = prepare_args(c, cs, cs ? cs->n_chains : 0, flags, d_l, s, a);
+    if (rc != GAC_OK || cs->n_chains == 0) return rc;
+    if (cs->n_chains > INT32_MAX / 2) return gac_fail(GAC_E_ARG, "too many chains");
+    rc = ensure_whole(c, cs, s);
+    if (rc != GAC_OK) return rc;
+    const int64_t T = (cs->n_blocks + kTileBlocks - 1) / kTileBlocks;
+    rc = ensure_ws(c, 0, T, s);
+    if (rc != GAC_OK) return rc;
+    a.ranges = nullptr;
+    a.out_g = d_g;
+    a.out_l = d_l;
+    a.out_ali = d_ali;
+    a.rdesc = cs->w_rdesc;
+    a.nblk = cs->w_nblk;
+    a.gflat = cs->w_gflat;
+    a.pb0 = cs->w_gflat;
+    a.tile_r0 = cs->w_tile_r0;
+    a.status = cs->w_status;
+    a.sum_head = c->sum_head;
+    a.sum_tail = c->sum_tail;
+    a.sup_head = c->sup_head;
+    a.sup_tail = c->sup_tail;
+    a.sup_tail_r = c->sup_tail_r;
+    a.cap_tiles = (int32_t)(c->ws_tiles < INT32_MAX ? c->ws_tiles : INT32_MAX);
+    HIPCHK(launch_zero_list(cs->w_empty, cs->w_nempty, d_g, a.want_local ? d_l : nullptr, d_ali, s));
+    {
+        PROF_BEGIN(GAC_K_TILE);
+        HIPCHK(launch_tile(a, a.want_local ? c->tile_grid_l : c->tile_grid_g, s));
+        PROF_END(GAC_K_TILE);
+    }
+    {
+        PROF_BEGIN(GAC_K_COMBINE);
+        HIPCHK(launch_combine(a, c->combine_grid, s));
+        PROF_END(GAC_K_COMBINE);
+    }
+    if (hipEventRecord(c->ws_ev, s) == hipSuccess) c->ws_last = s;
+    return GAC_OK;
+}
+
+extern "C" int gac_score_chains_device(gac_ctx *c, const gac_chainset *cs, uint32_t flags,
+                                       int64_t *d_g, int64_t *d_l, int32_t *d_ali, void *stream) {
+    gac_clear_error();
+    if (!c) return gac_fail(GAC_E_ARG, "NULL context");
+    CTX_LOCK(c);
+    if (!cs) return gac_fail(GAC_E_ARG, "NULL chainset");
+    if (cs->n_chains > 0 && (!d_g || !d_ali)) return gac_fail(GAC_E_ARG, "NULL buffer");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return score_whole(c, cs, flags, (long long *)d_g, (long long *)d_l, d_ali, s);
+}
+
+extern "C" int gac_score_chains(gac_ctx *c, const gac_chainset *cs, uint32_t flags, int64_t *global,
+                                int64_t *local, int32_t *ali) {
+    gac_clear_error();
+    if (!c) return gac_fail(GAC_E_ARG, "NULL context");
+    CTX_LOCK(c);
+    if (!cs) return gac_fail(GAC_E_ARG, "NULL chainset");
+    const int64_t n = cs->n_chains;
+    if (n == 0) return GAC_OK;
+    if (!global || !ali || ((flags & GAC_WANT_LOCAL) && !local)) return gac_fail(GAC_E_ARG, "NULL buffer");
+    HIPCHK(hipSetDevice(c->device));
+    if (n > c->io_n) {
+        int64_t cap = n + n / 2 + 1024;
+        if (c->d_ranges) hipFree(c->d_ranges);
+        if (c->d_g) hipFree(c->d_g);
+        if (c->d_l) hipFree(c->d_l);
+        if (c->d_ali) hipFree(c->d_ali);
+        c->d_ranges = nullptr;
+        c->d_g = c->d_l = nullptr;
+        c->d_ali = nullptr;
+        HIPCHK(hipMalloc(&c->d_ranges, cap * sizeof(Range)));
+        HIPCHK(hipMalloc(&c->d_g, cap * 8));
+        HIPCHK(hipMalloc(&c->d_l, cap * 8));
+        HIPCHK(hipMalloc(&c->d_ali, cap * 4));
+        c->io_n = cap;
+    }
+    hipStream_t s = c->stream;
+    int rc = score_whole(c, cs, flags, c->d_g, c->d_l, c->d_ali, s);
+    if (rc != GAC_OK) return rc;
+    HIPCHK(hipMemcpyAsync(global, c->d_g, n * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(ali, c->d_ali, n * 4, hipMemcpyDeviceToHost, s));
+    if (flags & GAC_WANT_LOCAL) HIPCHK(hipMemcpyAsync(local, c->d_l, n * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return GAC_OK;
 }
 
 extern "C" int gac_score_ranges_device(gac_ctx *c, const gac_chainset *cs, const gac_range *d_ranges,

@@ -110,6 +110,10 @@ struct ScoreArgs {
     int32_t *tile_r0;    // [T]   range owning each tile's first flat block
     SegSum *sum_head;    // [T]   partial segment containing the tile's first block
     SegSum *sum_tail;    // [T]   partial segment containing the tile's last block
+    // cross-tile fold (k_fold_tiles / k_fold_super), per super-tile of 64 tiles
+    SegSum *sup_head;    // [U]   fold of the heads, in super-tile u, of a range begun before it
+    SegSum *sup_tail;    // [U]   prefix of the range that continues past super-tile u
+    int32_t *sup_tail_r; // [U]   that range, or -1
     int32_t *agg;        // [G]   window blocks of each plan workgroup (k_plan; saturated)
     int32_t *plan_off;   // [G+1] flat offset of plan workgroup w
     int32_t *status;     // [8]   W (flat blocks, saturated), T (tiles), 1 = workspace too

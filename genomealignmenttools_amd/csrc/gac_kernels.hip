@@ -24,7 +24,9 @@
 //             evaluate gapCalcCost in exact f64, and segmented (by range)
 //             wave scans fold sums and the max-plus local-score element;
 //             ranges complete inside the tile are written directly
-//   k_combine ranges spanning > 1 tile: ordered fold of tile segments
+//   k_fold_tiles + k_fold_super  ranges spanning > 1 tile: ordered fold of
+//             tile segments, parallel over tiles (a segmented wave scan per
+//             64 tiles, then one lane per range spanning super-tiles)
 // All sums are int64: every addend of the reference's double accumulation is
 // an integer, so integer arithmetic is exact and bit-identical.
 #include <hip/hip_runtime.h>
@@ -581,6 +583,45 @@ __global__ void __launch_bounds__(kPlanWG) k_tilemap_fused(ScoreArgs a) {
     }
 }
 
+// ------------------------------------------------------------ k_whole_plan
+// Whole-chain calls (scoreChain: every chain of a set, in order) need no
+// window search: the plan of "range c = chain c" is fixed per chain set, so
+// it is built once (first gac_score_chains call) into the same workspace
+// shapes k_tile and the folds read -- rdesc, nblk, gflat (= pb0 = the chain's
+// first block), tile_r0 -- and a call is k_tile + the fold.  One lane per
+// chain.
+__global__ void __launch_bounds__(256) k_whole_plan(const DChain *chains, int64_t n,
+                                                    RangeDesc *rdesc, int32_t *nblk,
+                                                    int32_t *gflat, int32_t *tile_r0) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const DChain ch = chains[c];
+    RangeDesc d;
+    d.tbase = ch.tbase;
+    d.qbase = ch.qbase;
+    d.b0 = (int32_t)ch.blk_off;
+    d.nblk = ch.nblk;
+    d.s = ch.tstart;
+    d.e = ch.tend;
+    rdesc[c] = d;
+    nblk[c] = ch.nblk;
+    gflat[c] = (int32_t)ch.blk_off;
+    const int64_t g = ch.blk_off, end = g + ch.nblk;
+    for (int64_t t = (g + kTileBlocks - 1) / kTileBlocks; t * kTileBlocks < end; ++t)
+        tile_r0[t] = (int32_t)c;
+}
+
+// outputs of the ranges in `list` (chains without blocks) := 0
+__global__ void __launch_bounds__(256) k_zero_list(const int32_t *list, int64_t n, long long *g,
+                                                   long long *l, int32_t *ali) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int32_t r = list[i];
+    g[r] = 0;
+    ali[r] = 0;
+    if (l) l[r] = 0;
+}
+
 // ------------------------------------------------------------ k_tile -----
 // One wave per tile of 64 consecutive flat blocks (ranges packed densely,
 // many per tile).  Per tile: one round trip for the range descriptors and
@@ -912,76 +953,136 @@ __global__ void __launch_bounds__(256, GAC_TILE_MINB) k_tile(ScoreArgs a) {
     }
 }
 
-// ------------------------------------------------------------ k_combine --
-// Ranges spanning > 1 tile: tail segment of the first tile, then the head
-// segments of the following tiles, folded in order.  Short spans are folded
-// by one lane; long spans (> kLaneFold tiles) by the whole wave.
-constexpr int kLaneFold = 16;
+// ------------------------------------------------------------ cross-tile fold
+// Ranges spanning > 1 tile are folded in tile order: the tail segment of the
+// range's first tile (sum_tail), then the head segments of the following
+// tiles (sum_head).  The work is spread over tiles, not ranges, so that a
+// few very long ranges (score-sorted whole chains put them all at the start)
+// do not serialise a wave:
+//   k_fold_tiles  one wave per super-tile of 64 tiles, lane = tile: the tile's
+//                 head segment keyed by its range, a segmented (by range)
+//                 wave scan over the super-tile; the last lane of each run
+//                 finishes its range when the run holds all of the range's
+//                 heads (prefixed with the first tile's tail), else leaves
+//                 the run in sup_head (run starting at lane 0) or the range's
+//                 prefix in sup_tail (run reaching lane 63);
+//   k_fold_super  one lane per super-tile whose tail range continues: that
+//                 prefix, then sup_head of every later super-tile the range
+//                 reaches (a 1e5-block chain spans ~25).
+struct Seg {
+    long long g, ali;
+    Elem e;
+};
 
 template <bool LOCAL>
-__global__ void __launch_bounds__(256) k_combine(ScoreArgs a) {
-    if (a.status[2]) return;
+__device__ __forceinline__ Seg seg_compose(const Seg &x, const Seg &y) {
+    Seg r;
+    r.g = x.g + y.g;
+    r.ali = x.ali + y.ali;
+    if (LOCAL) r.e = compose(x.e, y.e);
+    return r;
+}
+
+__device__ __forceinline__ Seg seg_load(const SegSum &s) {
+    Seg r;
+    r.g = s.g;
+    r.ali = s.ali;
+    r.e.A = s.A;
+    r.e.B = s.B;
+    r.e.C = s.C;
+    r.e.D = s.D;
+    return r;
+}
+
+__device__ __forceinline__ SegSum seg_pack(const Seg &x) {
+    SegSum s;
+    s.g = x.g;
+    s.ali = x.ali;
+    s.A = x.e.A;
+    s.B = x.e.B;
+    s.C = x.e.C;
+    s.D = x.e.D;
+    return s;
+}
+
+template <bool LOCAL>
+__global__ void __launch_bounds__(256) k_fold_tiles(ScoreArgs a) {
+    if (a.status[2]) return;  // workspace overflow: the host grows it and reruns
+    const int T = a.status[1];
+    const int64_t U = ((int64_t)T + kWave - 1) / kWave;
     const int lane = threadIdx.x & 63;
+    const unsigned long long lanemask_le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
     const int64_t wave_id = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    for (int64_t base = wave_id * kWave; base < a.n; base += nwaves * kWave) {
-        const int64_t my = base + lane;
-        int tf = 0, tl = 0;
-        if (my < a.n) {
-            const int nb = a.nblk[my];
-            if (nb > 0) {
-                const int g0 = a.plan_off[my / kPlanWG] + a.goff[my];
-                tf = g0 / kTileBlocks;
-                tl = (g0 + nb - 1) / kTileBlocks;
-            }
+    for (int64_t u = wave_id; u < U; u += nwaves) {
+        const int t = (int)(u * kWave) + lane;
+        int key = -1, gr = 0;  // key: the range continuing into tile t (-1: none)
+        if (t < T) {
+            const int r = a.tile_r0[t];
+            gr = a.gflat[r];
+            if ((long long)gr < (long long)t * kTileBlocks) key = r;
         }
-        const int nt = tl - tf;
-        if (nt > 0 && nt <= kLaneFold) {
-            SegSum s0 = a.sum_tail[tf];
-            Elem e = {s0.A, s0.B, s0.C, s0.D};
-            long long g = s0.g, ali = s0.ali;
-            for (int t = tf + 1; t <= tl; ++t) {
-                const SegSum s = a.sum_head[t];
-                g += s.g;
-                ali += s.ali;
-                if (LOCAL) {
-                    const Elem y = {s.A, s.B, s.C, s.D};
-                    e = compose(e, y);
+        Seg v;
+        if (key >= 0) {
+            v = seg_load(a.sum_head[t]);
+        } else {
+            v.g = v.ali = 0;
+            v.e = {0, kNeg, kNeg, kNeg};
+        }
+        const int prev = __shfl_up(key, 1, kWave);
+        const bool head = lane == 0 || key < 0 || key != prev;
+        const unsigned long long heads = __ballot(head);
+        const int seg0 = 63 - __builtin_clzll(heads & lanemask_le);
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            Seg o;
+            o.g = __shfl_up(v.g, d, kWave);
+            o.ali = __shfl_up(v.ali, d, kWave);
+            if (LOCAL) {
+                o.e.A = __shfl_up(v.e.A, d, kWave);
+                o.e.B = __shfl_up(v.e.B, d, kWave);
+                o.e.C = __shfl_up(v.e.C, d, kWave);
+                o.e.D = __shfl_up(v.e.D, d, kWave);
+            }
+            if (lane - d >= seg0) v = seg_compose<LOCAL>(o, v);
+        }
+        const bool run_end = key >= 0 && (lane == 63 || ((heads >> (lane + 1)) & 1ull));
+        int tail_r = -1;
+        if (run_end) {
+            const int nb = a.nblk[key];
+            const int tf = gr / kTileBlocks;
+            const int tl = (int)(((long long)gr + nb - 1) / kTileBlocks);
+            const int ta = (int)(u * kWave) + seg0;
+            if (ta == tf + 1) {  // the run holds the range's first heads
+                const Seg full = seg_compose<LOCAL>(seg_load(a.sum_tail[tf]), v);
+                if (tl == t) {
+                    seg_store<LOCAL>(a, key, full.g, (int)full.ali, full.e);
+                } else {  // continues past this super-tile (so t is its last tile)
+                    a.sup_tail[u] = seg_pack(full);
+                    tail_r = key;
                 }
-            }
-            seg_store<LOCAL>(a, (int)my, g, (int)ali, e);
-        }
-        unsigned long long mask = __ballot(nt > kLaneFold);
-        while (mask) {
-            const int src = __builtin_ctzll(mask);
-            mask &= mask - 1;
-            const int64_t ri = base + src;
-            const int f0 = __shfl(tf, src, kWave);
-            const int f1 = __shfl(tl, src, kWave);
-            const int cnt = f1 - f0;  // head segments in tiles f0+1 .. f1
-            const int per = (cnt + kWave - 1) / kWave;
-            const int lo = min(cnt, lane * per), hi = min(cnt, lo + per);
-            long long g = 0, ali = 0;
-            Elem e = {0, kNeg, kNeg, kNeg};
-            for (int t = lo; t < hi; ++t) {
-                const SegSum s = a.sum_head[f0 + 1 + t];
-                g += s.g;
-                ali += s.ali;
-                if (LOCAL) {
-                    const Elem y = {s.A, s.B, s.C, s.D};
-                    e = compose(e, y);
-                }
-            }
-            g = wave_sum(g);
-            ali = wave_sum(ali);
-            if (LOCAL) e = wave_fold(e, lane);
-            if (lane == 0) {
-                const SegSum s0 = a.sum_tail[f0];
-                const Elem x = {s0.A, s0.B, s0.C, s0.D};
-                if (LOCAL) e = compose(x, e);
-                seg_store<LOCAL>(a, (int)ri, s0.g + g, (int)(s0.ali + ali), e);
+            } else {  // begun in an earlier super-tile: the run starts at lane 0
+                a.sup_head[u] = seg_pack(v);
             }
         }
+        if (lane == 63) a.sup_tail_r[u] = tail_r;
+    }
+}
+
+template <bool LOCAL>
+__global__ void __launch_bounds__(256) k_fold_super(ScoreArgs a) {
+    if (a.status[2]) return;
+    const int T = a.status[1];
+    const int64_t U = ((int64_t)T + kWave - 1) / kWave;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < U; u += stride) {
+        const int r = a.sup_tail_r[u];
+        if (r < 0) continue;
+        Seg acc = seg_load(a.sup_tail[u]);
+        const long long gr = a.gflat[r];
+        const int64_t ul = ((gr + a.nblk[r] - 1) / kTileBlocks) / kWave;
+        for (int64_t w = u + 1; w <= ul; ++w) acc = seg_compose<LOCAL>(acc, seg_load(a.sup_head[w]));
+        seg_store<LOCAL>(a, r, acc.g, (int)acc.ali, acc.e);
     }
 }
 
@@ -1173,10 +1274,29 @@ hipError_t launch_small(const ScoreArgs &a, const Range *rin, SmallOut *out, hip
 }
 
 hipError_t launch_combine(const ScoreArgs &a, int grid, hipStream_t s) {
-    if (a.want_local)
-        hipLaunchKernelGGL(k_combine<true>, dim3(grid), dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL(k_combine<false>, dim3(grid), dim3(256), 0, s, a);
+    if (a.want_local) {
+        hipLaunchKernelGGL(k_fold_tiles<true>, dim3(grid), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_fold_super<true>, dim3(grid / 8 + 1), dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(k_fold_tiles<false>, dim3(grid), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_fold_super<false>, dim3(grid / 8 + 1), dim3(256), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_whole_plan(const DChain *chains, int64_t n, RangeDesc *rdesc, int32_t *nblk,
+                             int32_t *gflat, int32_t *tile_r0, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_whole_plan, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, chains, n,
+                       rdesc, nblk, gflat, tile_r0);
+    return hipGetLastError();
+}
+
+hipError_t launch_zero_list(const int32_t *list, int64_t n, long long *g, long long *l,
+                            int32_t *ali, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_zero_list, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, list, n, g,
+                       l, ali);
     return hipGetLastError();
 }
 

@@ -90,9 +90,16 @@ void gt_stage(const char *what) {
     clock_gettime(CLOCK_MONOTONIC, &ts);
     const double now = ts.tv_sec + 1e-9 * ts.tv_nsec;
     static double startup = -2; /* process start -> first call (main's entry) */
-    if (startup == -2)
+    static double main_rt;      /* CLOCK_REALTIME at main's entry */
+    if (startup == -2) {
         startup = since_process_start();
+        struct timespec rt;
+        clock_gettime(CLOCK_REALTIME, &rt);
+        main_rt = rt.tv_sec + 1e-9 * rt.tv_nsec;
+    }
     if (last >= 0 && what && show && startup > -2) {
+        /* wall-clock anchors: a parent can attribute spawn and exit */
+        fprintf(stderr, "[stage-clock] main %.6f process-start %.6f\n", main_rt, main_rt - startup);
         fprintf(stderr, "[stage] %-32s %8.3f s\n", "exec + libraries (approx.)", startup);
         startup = -3;
     }
@@ -550,6 +557,11 @@ void gt_device_close_join(gt_device *d) {
 
 void gt_exit_ok(void) {
     join_live_device();
+    if (g_verbose >= 2 || getenv("GAC_TIMING")) { /* the last wall-clock anchor */
+        struct timespec rt;
+        clock_gettime(CLOCK_REALTIME, &rt);
+        fprintf(stderr, "[stage-clock] exit %.6f\n", rt.tv_sec + 1e-9 * rt.tv_nsec);
+    }
     if (fflush(NULL) != 0)
         gt_abort("write error\n");
     if (getenv("GAC_PROFILE_EXIT")) exit(0); /* gprof builds: write gmon.out */

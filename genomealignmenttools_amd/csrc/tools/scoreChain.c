@@ -5,7 +5,7 @@
  * -returnOnlyScoreAndCoords; :42-79, :301-331).  Genomes are loaded once,
  * resident 2-bit packed on the GPU; every chain's global score
  * (chainCalcScore), local score (chainCalcScoreLocal, :176-198) and aligned
- * bases are computed in one batched GPU call (gac_score_ranges).
+ * bases are computed in one batched GPU call (gac_score_chains).
  *
  * -nranks=N -rank=R: chains are independent, so N processes (one per GPU)
  * each parse the file, score a contiguous run of chains balanced by blocks
@@ -178,16 +178,11 @@ int main(int argc, char *argv[]) {
     gac_chainset *cs = NULL;
     gt_check(gac_chains_upload(ctx, &d, &cs));
     gt_stage("chains to HBM");
-    gac_range *r = malloc((nc ? nc : 1) * sizeof(gac_range));
-    for (int64_t i = 0; i < nc; ++i) {
-        r[i].chain = (int32_t)i;
-        r[i].t_start = c.tstart[c0 + i];
-        r[i].t_end = c.tend[c0 + i];
-    }
-    /* results indexed like the chains (this rank's run filled) */
+    /* results indexed like the chains (this rank's run filled): every chain
+     * of the uploaded set, whole (gac_score_chains) */
     int64_t *glob = malloc((c.n ? c.n : 1) * 8), *loc = malloc((c.n ? c.n : 1) * 8);
     int32_t *ali = malloc((c.n ? c.n : 1) * 4);
-    gt_check(gac_score_ranges(ctx, cs, r, nc, GAC_WANT_LOCAL, glob + c0, loc + c0, ali + c0));
+    gt_check(gac_score_chains(ctx, cs, GAC_WANT_LOCAL, glob + c0, loc + c0, ali + c0));
     gt_stage("GPU scoring");
     gt_device_close_async(&dev, ctx, cs); /* overlaps writing the output */
 

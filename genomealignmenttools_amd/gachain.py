@@ -8,7 +8,7 @@ axtScoreSchemeRead/Default (axt.c:423,692)   read_score_scheme(path | None)
 twoBitOpen + twoBitReadSeqFrag (twoBit.c)    Engine.load_2bit(side, path)
 chainRead loop (chain.c:337)                 chainfile.read_chains -> Engine.upload_chains
 chainSubsetOnT + chainCalcScore (+ local)    Engine.score_ranges(chainset, ranges)
-scoreChain getChainScore (scoreChain.c:207)  Engine.score_chains(chainset)
+scoreChain getChainScore (scoreChain.c:207)  Engine.score_chains(chainset) (gac_score_chains)
 
 Every scoring call runs on the GPU through libgachain; there is no CPU path.
 """
@@ -200,9 +200,23 @@ class Engine:
         return np.stack([np.arange(ca.n, dtype=np.int32), ca.tstart.astype(np.int32),
                          ca.tend.astype(np.int32)], axis=1)
 
-    def score_chains(self, cs: ChainSet, ca, want_local: bool = True):
-        """scoreChain: global, local and aligned bases of every chain."""
-        return self.score_ranges(cs, self.full_ranges(ca), want_local)
+    def score_chains(self, cs: ChainSet, ca=None, want_local: bool = True):
+        """scoreChain: global, local and aligned bases of every chain of the
+        set, in order (gac_score_chains: the set's own plan, no ranges)."""
+        n = cs.n_chains
+        g = np.zeros(n, np.int64)
+        ali = np.zeros(n, np.int32)
+        loc = np.zeros(n, np.int64) if want_local else None
+        check(lib().gac_score_chains(self.h, cs.handle, GAC_WANT_LOCAL if want_local else 0,
+                                     _p(g), _p(loc) if want_local else None, _p(ali)))
+        return g, loc, ali
+
+    def score_chains_device(self, cs: ChainSet, d_g: int, d_ali: int, d_l: int = 0,
+                            want_local: bool = False, stream: int = 0) -> None:
+        check(lib().gac_score_chains_device(
+            self.h, cs.handle, GAC_WANT_LOCAL if want_local else 0, C.c_void_p(d_g),
+            C.c_void_p(d_l) if d_l else None, C.c_void_p(d_ali),
+            C.c_void_p(stream) if stream else None))
 
     # ---- device buffers / timing (bench)
     def dev_alloc(self, nbytes: int) -> int:

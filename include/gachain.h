@@ -177,6 +177,19 @@ int gac_score_ranges_device(gac_ctx *ctx, const gac_chainset *cs,
                             int64_t *d_global, int64_t *d_local, int32_t *d_ali,
                             void *stream);
 
+/* Every chain of the set, in order -- scoreChain's batch (the per-chain
+ * chainCalcScore + chainCalcScoreLocal of src/scoreChain/scoreChain.c:207-220,
+ * 301-331): global[c], local[c] (GAC_WANT_LOCAL), ali[c] for c in
+ * 0..n_chains-1, equal to gac_score_ranges over ranges covering each whole
+ * chain.  The chain set's own scoring plan is built at the first call and
+ * kept with the set, so a call is just the scoring kernels. */
+int gac_score_chains(gac_ctx *ctx, const gac_chainset *cs, uint32_t flags, int64_t *global,
+                     int64_t *local, int32_t *ali);
+/* The same into device buffers on `stream` (NULL: the context's); returns once
+ * enqueued. */
+int gac_score_chains_device(gac_ctx *ctx, const gac_chainset *cs, uint32_t flags,
+                            int64_t *d_global, int64_t *d_local, int32_t *d_ali, void *stream);
+
 /* ---- axtChain ------------------------------------------------------------
  * Per-block scores: axtScoreUngapped (kent/src/lib/axt.c:186-194) of every
  * block, the scores chainPair gives the kd-tree (axtChain.c:276-282).  Pairs

@@ -159,6 +159,52 @@ def test_long_chains_multi_tile():
     assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
 
 
+@pytest.mark.parametrize("want_local", [True, False])
+def test_whole_chains_vs_ranges(want_local):
+    """gac_score_chains (scoreChain's batch: the chain set's own plan, then
+    k_tile and the two-level cross-tile fold) equals the oracle's whole-chain
+    scores, on chains of 1 to 20k blocks (ranges spanning many tiles and
+    several 64-tile super-tiles: the fold's second level), chains without
+    blocks interleaved, and repeated calls; the range path on the same set
+    agrees."""
+    from genomealignmenttools_amd import synth
+    from genomealignmenttools_amd.chainfile import ChainArrays
+    from genomealignmenttools_amd.gachain import GAC_Q, GAC_T
+    tg = synth.random_genome({"chrT1": 6_000_000}, 13, n_frac=0.01, n_mean=300)
+    qg = synth.random_genome({"q1": 4_000_000, "q2": 3_000_000}, 14, n_frac=0.01, n_mean=300)
+    cfg = synth.SynthConfig(n_chains=400, alpha=1.05, max_blocks=20_000, seed=7,
+                            gap_p_small=0.97, gap_p_med=0.03)
+    ca = synth.make_chains(tg, "chrT1", qg, cfg)
+    assert int(np.diff(ca.blk_off).max()) > 64 * 64 * 2  # > two super-tiles
+    e, cs = _setup(None, tg, qg, ca)
+    orc = _oracle(tg, qg)
+    full = np.stack([np.arange(ca.n), ca.tstart, ca.tend], 1).astype(np.int64)
+    og, ol, oa = orc.score_ranges(ca, full)
+    for _ in range(2):
+        g, l, a = e.score_chains(cs, want_local=want_local)
+        assert np.array_equal(g, og) and np.array_equal(a, oa)
+        if want_local:
+            assert np.array_equal(l, ol)
+    g2, l2, a2 = e.score_ranges(cs, full, want_local=want_local)
+    assert np.array_equal(g2, og) and np.array_equal(a2, oa)
+    # chains without blocks between them (results 0)
+    nb = np.diff(ca.blk_off)
+    off = np.zeros(2 * ca.n + 1, np.int64)  # chain 2k: empty, chain 2k+1: chain k
+    off[1::2] = ca.blk_off[:-1]
+    off[2::2] = ca.blk_off[1:]
+    tix = np.array([e.seq_index(GAC_T, x) for x in ca.tname], np.int32)
+    qix = np.array([e.seq_index(GAC_Q, x) for x in ca.qname], np.int32)
+    cs2 = e.upload_chain_arrays(np.repeat(tix, 2), np.repeat(qix, 2), np.repeat(ca.qstrand, 2),
+                                off, ca.blk_t, ca.blk_q, ca.blk_size)
+    g, l, a = e.score_chains(cs2, want_local=True)
+    assert not g[0::2].any() and not l[0::2].any() and not a[0::2].any()
+    assert np.array_equal(g[1::2], og) and np.array_equal(l[1::2], ol)
+    assert np.array_equal(a[1::2], oa)
+    cs2.close()
+    cs.close()
+    e.close()
+
+
 def test_edge_ranges():
     """Empty windows, single-base windows, ranges ending inside blocks,
     1-bp blocks, ranges beyond the chain."""
