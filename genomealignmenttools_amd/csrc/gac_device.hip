@@ -62,6 +62,10 @@ hipError_t launch_whole_plan(const DChain *chains, int64_t n, RangeDesc *rdesc, 
                              int32_t *gflat, int32_t *tile_r0, hipStream_t s);
 hipError_t launch_zero_list(const int32_t *list, int64_t n, long long *g, long long *l,
                             int32_t *ali, hipStream_t s);
+hipError_t launch_text_blocks(const uint8_t *text, const TextJob *jobs, int64_t n, const M25 &m,
+                              long long *out, hipStream_t s);
+hipError_t launch_text_xover(const uint8_t *text, const TextXJob *jobs, int64_t n, const M25 &m,
+                             int32_t *pos, int32_t *adj, hipStream_t s);
 }  // namespace gac
 
 using namespace gac;
@@ -1840,6 +1844,116 @@ extern "C" int gac_score_ranges(gac_ctx *c, const gac_chainset *cs, const gac_ra
         HIPCHK(hipMemcpyAsync(local, c->d_l, n * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     return GAC_OK;
+}
+
+// ----------------------------------------------------------------- text (kent API)
+// Caller-owned char text scored on the device (the kent in-process API's
+// chainScoreBlock / axtScoreUngapped / cBlockFindCrossover take raw text):
+// the batch's text is packed into one buffer, uploaded, scored, read back.
+static M25 text_matrix(const int32_t mat[16]) {
+    M25 m;
+    memset(&m, 0, sizeof(m));
+    for (int q = 0; q < 4; ++q)
+        for (int t = 0; t < 4; ++t) m.m[q * 5 + t] = mat[q * 4 + t];
+    return m;
+}
+
+template <class J>
+static int text_run(gac_ctx *c, const std::vector<uint8_t> &text, const std::vector<J> &jobs,
+                    size_t out_bytes, void **d_text, J **d_jobs, void **d_out) {
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMalloc(d_text, std::max<size_t>(text.size(), 1)));
+    HIPCHK(hipMalloc((void **)d_jobs, jobs.size() * sizeof(J)));
+    HIPCHK(hipMalloc(d_out, out_bytes));
+    HIPCHK(hipMemcpyAsync(*d_text, text.data(), text.size(), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(*d_jobs, jobs.data(), jobs.size() * sizeof(J), hipMemcpyHostToDevice,
+                          c->stream));
+    return GAC_OK;
+}
+
+extern "C" int gac_score_text_blocks(gac_ctx *c, int64_t n, const char *const *q,
+                                     const char *const *t, const int32_t *size,
+                                     const int32_t mat[16], int64_t *score) {
+    gac_clear_error();
+    if (!c || n < 0 || (n && (!q || !t || !size || !mat || !score)))
+        return gac_fail(GAC_E_ARG, "gac_score_text_blocks: bad argument");
+    if (n == 0) return GAC_OK;
+    CTX_LOCK(c);
+    std::vector<TextJob> jobs(n);
+    size_t tot = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (size[i] < 0) return gac_fail(GAC_E_ARG, "block %lld: negative size", (long long)i);
+        tot += 2 * (size_t)size[i];
+    }
+    std::vector<uint8_t> text(tot);
+    size_t o = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        jobs[i] = TextJob{(int64_t)o, (int64_t)(o + size[i]), size[i], 0};
+        memcpy(&text[o], q[i], size[i]);
+        memcpy(&text[o + size[i]], t[i], size[i]);
+        o += 2 * (size_t)size[i];
+    }
+    void *d_text = nullptr, *d_out = nullptr;
+    TextJob *d_jobs = nullptr;
+    int rc = text_run(c, text, jobs, n * 8, &d_text, &d_jobs, &d_out);
+    if (rc == GAC_OK) {
+        hipError_t e = launch_text_blocks((const uint8_t *)d_text, d_jobs, n, text_matrix(mat),
+                                          (long long *)d_out, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(score, d_out, n * 8, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) rc = gac_fail(GAC_E_HIP, "gac_score_text_blocks: %s", hipGetErrorString(e));
+    }
+    hipStreamSynchronize(c->stream);
+    hipFree(d_text);
+    hipFree(d_jobs);
+    hipFree(d_out);
+    return rc;
+}
+
+extern "C" int gac_text_crossovers(gac_ctx *c, int64_t n, const char *const *lq,
+                                   const char *const *lt, const char *const *rq,
+                                   const char *const *rt, const int32_t *overlap,
+                                   const int32_t mat[16], int32_t *pos, int32_t *adj) {
+    gac_clear_error();
+    if (!c || n < 0 || (n && (!lq || !lt || !rq || !rt || !overlap || !mat || !pos || !adj)))
+        return gac_fail(GAC_E_ARG, "gac_text_crossovers: bad argument");
+    if (n == 0) return GAC_OK;
+    CTX_LOCK(c);
+    std::vector<TextXJob> jobs(n);
+    size_t tot = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (overlap[i] < 0) return gac_fail(GAC_E_ARG, "overlap %lld: negative", (long long)i);
+        tot += 4 * (size_t)overlap[i];
+    }
+    std::vector<uint8_t> text(tot);
+    size_t o = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int32_t v = overlap[i];
+        jobs[i] = TextXJob{(int64_t)o, (int64_t)(o + v), (int64_t)(o + 2 * (size_t)v),
+                           (int64_t)(o + 3 * (size_t)v), v, 0};
+        memcpy(&text[o], lq[i], v);
+        memcpy(&text[o + v], lt[i], v);
+        memcpy(&text[o + 2 * (size_t)v], rq[i], v);
+        memcpy(&text[o + 3 * (size_t)v], rt[i], v);
+        o += 4 * (size_t)v;
+    }
+    void *d_text = nullptr, *d_out = nullptr;
+    TextXJob *d_jobs = nullptr;
+    int rc = text_run(c, text, jobs, n * 8, &d_text, &d_jobs, &d_out);
+    if (rc == GAC_OK) {
+        int32_t *d_pos = (int32_t *)d_out, *d_adj = d_pos + n;
+        hipError_t e = launch_text_xover((const uint8_t *)d_text, d_jobs, n, text_matrix(mat), d_pos,
+                                         d_adj, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(pos, d_pos, n * 4, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(adj, d_adj, n * 4, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) rc = gac_fail(GAC_E_HIP, "gac_text_crossovers: %s", hipGetErrorString(e));
+    }
+    hipStreamSynchronize(c->stream);
+    hipFree(d_text);
+    hipFree(d_jobs);
+    hipFree(d_out);
+    return rc;
 }
 
 // ----------------------------------------------------------------- memory

@@ -159,4 +159,22 @@ struct BlockJob {
     int32_t minus;
 };
 
+// Text jobs of the kent-API shims (k_text_blocks / k_text_xover): offsets
+// into one uploaded byte buffer of caller text.
+struct TextJob {
+    int64_t q, t;  // offsets of the query / target text
+    int32_t n;     // bases
+    int32_t pad;
+};
+
+struct TextXJob {
+    int64_t lq, lt, rq, rt;  // left block's last `ov` bases, right block's first
+    int32_t ov;
+    int32_t pad;
+};
+
+struct M25 {  // score by text code, [q * 5 + t]; code 4 (not acgt) scores 0
+    int32_t m[25];
+};
+
 }  // namespace gac

@@ -30,6 +30,7 @@
 // All sums are int64: every addend of the reference's double accumulation is
 // an integer, so integer arithmetic is exact and bit-identical.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -1214,6 +1215,78 @@ __global__ void __launch_bounds__(256) k_nruns(const NPiece *pieces, int64_t n, 
     }
 }
 
+// ------------------------------------------------------------ text blocks
+// The kent in-process API scores caller-owned char text (chainScoreBlock,
+// axtScoreUngapped, cBlockFindCrossover: kent/src/lib/chainConnect.c:14-22,
+// 61-105, axt.c:186-194).  Text codes: a/A 0, c/C 1, g/G 2, t/T 3, anything
+// else 4, scored 0 (the kent matrices are zero outside acgt/ACGT --
+// propagateCase, axt.c:402-421; gac_kent checks it).  m25[q * 5 + t].
+__device__ __forceinline__ int text_code(uint8_t ch) {
+    const int c = ch | 0x20;
+    return c == 'a' ? 0 : c == 'c' ? 1 : c == 'g' ? 2 : c == 't' ? 3 : 4;
+}
+
+__global__ void __launch_bounds__(256) k_text_blocks(const uint8_t *text, const TextJob *jobs,
+                                                     int64_t n, M25 m, long long *out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave_id = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t j = wave_id; j < n; j += nwaves) {
+        const TextJob J = jobs[j];
+        long long s = 0;
+        for (int k = lane; k < J.n; k += kWave)
+            s += m.m[text_code(text[J.q + k]) * 5 + text_code(text[J.t + k])];
+        s = wave_sum(s);
+        if (lane == 0) out[j] = s;
+    }
+}
+
+// cBlockFindCrossover on text: d_k = left_k - right_k; the crossover is the
+// first k where D_k = d_0 + .. + d_k reaches its maximum, if that maximum is
+// > 0 (strict improvements over the right block's score): pos = k + 1,
+// adj = lScore - max(0, max D).
+__global__ void __launch_bounds__(256) k_text_xover(const uint8_t *text, const TextXJob *jobs,
+                                                    int64_t n, M25 m, int32_t *out_pos,
+                                                    int32_t *out_adj) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave_id = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t j = wave_id; j < n; j += nwaves) {
+        const TextXJob J = jobs[j];
+        long long carry = 0, lsum = 0, bestv = 0;
+        int bestpos = 0;
+        for (int base = 0; base < J.ov; base += kWave) {
+            const int k = base + lane;
+            long long d = 0, l = 0;
+            if (k < J.ov) {
+                l = m.m[text_code(text[J.lq + k]) * 5 + text_code(text[J.lt + k])];
+                d = l - m.m[text_code(text[J.rq + k]) * 5 + text_code(text[J.rt + k])];
+            }
+            long long incl = d;
+#pragma unroll
+            for (int s = 1; s < kWave; s <<= 1) {
+                const long long o = __shfl_up(incl, s, kWave);
+                if (lane >= s) incl += o;
+            }
+            incl += carry;
+            long long mx = k < J.ov ? incl : kNeg;
+#pragma unroll
+            for (int s = 32; s > 0; s >>= 1) mx = max2(mx, __shfl_xor(mx, s, kWave));
+            if (mx > bestv) {
+                const unsigned long long hit = __ballot(k < J.ov && incl == mx);
+                bestv = mx;
+                bestpos = base + __builtin_ctzll(hit) + 1;
+            }
+            carry = __shfl(incl, kWave - 1, kWave);
+            lsum += wave_sum(l);
+        }
+        if (lane == 0) {
+            out_pos[j] = bestpos;
+            out_adj[j] = (int32_t)(lsum - bestv);
+        }
+    }
+}
+
 }  // namespace gac
 
 // ---------------------------------------------------------------- launch --
@@ -1297,6 +1370,23 @@ hipError_t launch_zero_list(const int32_t *list, int64_t n, long long *g, long l
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_zero_list, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, list, n, g,
                        l, ali);
+    return hipGetLastError();
+}
+
+hipError_t launch_text_blocks(const uint8_t *text, const TextJob *jobs, int64_t n, const M25 &m,
+                              long long *out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const int64_t nb = std::min<int64_t>((n + 3) / 4, 16384);
+    hipLaunchKernelGGL(k_text_blocks, dim3((unsigned)nb), dim3(256), 0, s, text, jobs, n, m, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_text_xover(const uint8_t *text, const TextXJob *jobs, int64_t n, const M25 &m,
+                             int32_t *pos, int32_t *adj, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const int64_t nb = std::min<int64_t>((n + 3) / 4, 16384);
+    hipLaunchKernelGGL(k_text_xover, dim3((unsigned)nb), dim3(256), 0, s, text, jobs, n, m, pos,
+                       adj);
     return hipGetLastError();
 }
 

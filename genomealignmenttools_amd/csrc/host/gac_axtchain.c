@@ -146,6 +146,10 @@ typedef struct ax_work {
     int err;
     char msg[512];
     size_t cap_n;
+    /* gac_chain_blocks: the caller's ConnectCost / GapCost (NULL: built in) */
+    gac_connect_fn cb_connect;
+    gac_gapcost_fn cb_gap;
+    void *cb_user;
 } ax_work;
 
 static void w_fail(ax_work *w, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
@@ -208,6 +212,8 @@ static int connect_cost_pre(ax_work *w, int32_t a, int32_t b, const int32_t *pre
 static int connect_cost(ax_work *w, int32_t a, int32_t b) { return connect_cost_pre(w, a, b, NULL); }
 
 static int connect_cost_pre(ax_work *w, int32_t a, int32_t b, const int32_t *pre) {
+    if (w->cb_connect)
+        return w->cb_connect(a, b, w->cb_user);
     int dq = w->qs[b] - w->qe[a];
     int dt = w->ts[b] - w->te[a];
     int adj = 0;
@@ -304,7 +310,8 @@ static void best_predecessor(ax_work *w, int32_t lonely, double *ret_score, int3
         double max_score = nd->max_score + lscore;
         if (max_score < best)
             continue;
-        max_score -= gap_cost(w->e, lq - nd->max_q, lt - nd->max_t);
+        max_score -= w->cb_gap ? w->cb_gap(lq - nd->max_q, lt - nd->max_t, w->cb_user)
+                               : gap_cost(w->e, lq - nd->max_q, lt - nd->max_t);
         if (max_score < best)
             continue;
         if (nd->leaf >= 0) {
@@ -712,6 +719,103 @@ static void chain_pair(ax_work *w, const ax_pairinfo *pi, FILE *details, ax_out 
     ax_chains pc;
     pair_peel(w, pi, details, &pc);
     pair_finish(w, &pc, NULL, out);
+}
+
+/* ------------------------------------------------------------------ chainBlocks */
+static void work_reserve(ax_work *w, int32_t n);
+
+/* kent's chainBlocks (kent/src/lib/chainBlock.c:392-452) with the caller's
+ * cost functions: leaves (zero-length blocks skipped), kdTreeMake,
+ * findBestPredecessors, peelChains, scoreBlocks with connect(), and the
+ * stable chainCmpScore sort -- on the calling thread. */
+int gac_chain_blocks(int32_t n, const int32_t *qs, const int32_t *qe, const int32_t *ts,
+                     const int32_t *te, const int32_t *score, gac_connect_fn connect,
+                     gac_gapcost_fn gap, void *user, const char *qname, int32_t qsize,
+                     char qstrand, const char *tname, int32_t tsize, FILE *details,
+                     gac_block_chains **out) {
+    gac_clear_error();
+    if (!out || n < 0 || !connect || !gap || (n && (!qs || !qe || !ts || !te || !score)))
+        return gac_fail(GAC_E_ARG, "gac_chain_blocks: bad argument");
+    *out = NULL;
+    ax_work w;
+    memset(&w, 0, sizeof(w));
+    w.cb_connect = connect;
+    w.cb_gap = gap;
+    w.cb_user = user;
+    w.n = n;
+    w.qs = qs;
+    w.qe = qe;
+    w.ts = ts;
+    w.te = te;
+    w.score = score;
+    work_reserve(&w, n);
+    gac_block_chains *r = calloc(1, sizeof(*r));
+    int rc = GAC_OK;
+    if (n > 0 && pair_leaves(&w) > 0) {
+        pair_tree(&w);
+        pair_dp_host(&w);
+        if (!w.err) {
+            const ax_pairinfo pi = {tname ? tname : "", qname ? qname : "", tsize, qsize, qstrand};
+            ax_chains pc;
+            pair_peel(&w, &pi, details, &pc);
+            dkey *ck = malloc((size_t)(pc.nc ? pc.nc : 1) * sizeof(dkey));
+            for (int32_t c = 0; c < pc.nc; ++c) { /* scoreBlocks (chainBlock.c:311-325) */
+                double sc = 0;
+                for (int32_t j = pc.cstart[c]; j < pc.cstart[c + 1]; ++j) {
+                    sc += score[pc.cblk[j]];
+                    if (j > pc.cstart[c])
+                        sc -= connect(pc.cblk[j - 1], pc.cblk[j], user);
+                }
+                ck[c] = (dkey){sc, c, c};
+            }
+            qsort(ck, (size_t)pc.nc, sizeof(dkey), dkey_cmp_desc);
+            r->n_chains = pc.nc;
+            r->score = malloc((size_t)(pc.nc ? pc.nc : 1) * sizeof(double));
+            r->off = malloc((size_t)(pc.nc + 1) * sizeof(int32_t));
+            r->blk = malloc((size_t)(pc.nbk ? pc.nbk : 1) * sizeof(int32_t));
+            int32_t k = 0;
+            for (int32_t i = 0; i < pc.nc; ++i) {
+                const int32_t c = ck[i].v;
+                r->score[i] = ck[i].k;
+                r->off[i] = k;
+                for (int32_t j = pc.cstart[c]; j < pc.cstart[c + 1]; ++j)
+                    r->blk[k++] = pc.cblk[j];
+            }
+            r->off[pc.nc] = k;
+            free(ck);
+            free(pc.cblk);
+            free(pc.cstart);
+        }
+    } else {
+        r->off = calloc(1, sizeof(int32_t));
+    }
+    if (w.err)
+        rc = gac_fail(GAC_E_ARG, "%s", w.msg);
+    free(w.total);
+    free(w.pred);
+    free(w.hit);
+    free(w.tord);
+    free(w.qord);
+    free(w.tmp);
+    free(w.nodes);
+    free(w.xs);
+    if (rc != GAC_OK) {
+        gac_block_chains_free(r);
+        return rc;
+    }
+    if (!r->off)
+        r->off = calloc(1, sizeof(int32_t));
+    *out = r;
+    return GAC_OK;
+}
+
+void gac_block_chains_free(gac_block_chains *c) {
+    if (!c)
+        return;
+    free(c->score);
+    free(c->off);
+    free(c->blk);
+    free(c);
 }
 
 /* ------------------------------------------------------------------ threads */

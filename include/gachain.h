@@ -190,6 +190,21 @@ int gac_score_chains(gac_ctx *ctx, const gac_chainset *cs, uint32_t flags, int64
 int gac_score_chains_device(gac_ctx *ctx, const gac_chainset *cs, uint32_t flags,
                             int64_t *d_global, int64_t *d_local, int32_t *d_ali, void *stream);
 
+/* ---- caller text (the kent in-process API's char* entry points) ---------
+ * chainScoreBlock / axtScoreUngapped (kent/src/lib/chainConnect.c:14-22,
+ * axt.c:186-194) of n blocks of caller-owned text: score[i] = sum over k <
+ * size[i] of mat[q][t] (A,C,G,T order as gac_scheme_read; any other
+ * character scores 0, either case).  On the device; synchronous. */
+int gac_score_text_blocks(gac_ctx *ctx, int64_t n, const char *const *q, const char *const *t,
+                          const int32_t *size, const int32_t mat[16], int64_t *score);
+/* cBlockFindCrossover (chainConnect.c:61-105) of n overlaps on caller text:
+ * lq/lt point at the left block's last overlap[i] bases (qEnd - overlap),
+ * rq/rt at the right block's first.  Out: pos (offset of the crossover from
+ * the right block's start) and adj (rScore + lScore - bestScore). */
+int gac_text_crossovers(gac_ctx *ctx, int64_t n, const char *const *lq, const char *const *lt,
+                        const char *const *rq, const char *const *rt, const int32_t *overlap,
+                        const int32_t mat[16], int32_t *pos, int32_t *adj);
+
 /* ---- axtChain ------------------------------------------------------------
  * Per-block scores: axtScoreUngapped (kent/src/lib/axt.c:186-194) of every
  * block, the scores chainPair gives the kd-tree (axtChain.c:276-282).  Pairs
@@ -279,6 +294,30 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
                   const gac_axt_input *in, double min_score, int n_threads,
                   const char *details_path, gac_axt_chains **out);
 void gac_axt_chains_free(gac_axt_chains *c);
+
+/* kent's chainBlocks (kent/src/lib/chainBlock.c:392-452) with the caller's
+ * cost functions -- the kd-tree DP behind axtChain, for callers that bring
+ * their own ConnectCost / GapCost (chainBlock.h:13-19): the DP runs on the
+ * calling thread (host: it is a sequential branch-and-bound search by the
+ * reference's definition), calling connect(a, b, user) /
+ * gap(dq, dt, user) with block indices.  Blocks i: q [qs, qe), t [ts, te),
+ * score[i]; zero-length blocks are skipped, as kent does.  Out: chains in
+ * chainCmpScore order (stable), chain c = blocks blk[off[c] .. off[c+1])
+ * ascending, score[c] = scoreBlocks (block scores minus connect costs).
+ * details (may be NULL): peelChains' -details text. */
+typedef int (*gac_connect_fn)(int32_t a, int32_t b, void *user);
+typedef int (*gac_gapcost_fn)(int dq, int dt, void *user);
+typedef struct gac_block_chains {
+    int32_t n_chains;
+    double *score;
+    int32_t *off; /* [n_chains + 1] */
+    int32_t *blk;
+} gac_block_chains;
+int gac_chain_blocks(int32_t n, const int32_t *qs, const int32_t *qe, const int32_t *ts,
+                     const int32_t *te, const int32_t *score, gac_connect_fn connect,
+                     gac_gapcost_fn gap, void *user, const char *qname, int32_t qsize, char qstrand,
+                     const char *tname, int32_t tsize, FILE *details, gac_block_chains **out);
+void gac_block_chains_free(gac_block_chains *c);
 
 /* ---- chainNet netting engine (host, no device needed) -------------------
  * Replaces chainNet's netting and output (src/chainNet/chainNet.c:328-896):

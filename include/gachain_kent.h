@@ -20,14 +20,31 @@
  *   gapCalcFromFile / gapCalcDefault /         gac_gapcalc_build ("loose",
  *     gapCalcOriginal / gapCalcFree /            "medium" or a file), gac_gap_cost
  *     gapCalcCost   kent/src/lib/gapCalc.c:233-331
- *   chainCalcScore  kent/src/lib/chainConnect.c:24-40   gac_score_ranges (full chain)
+ *   chainCalcScore  kent/src/lib/chainConnect.c:24-40   gac_score_chains on a chain set
+ *                                                        kept resident per chain list
+ *                                                        (gac_kent_score_chains)
  *   chainSubsetOnT / chainFastSubsetOnT        the same list surgery on the host
  *                   kent/src/lib/chain.c:471-558        (no scoring)
+ *   chainScoreBlock chainConnect.c:14-22       gac_score_text_blocks (device; the
+ *   axtScoreUngapped kent/src/lib/axt.c:186-194  caller's text; batch:
+ *                                               gac_kent_score_blocks)
+ *   cBlockFindCrossover chainConnect.c:61-105  gac_text_crossovers (device)
+ *   chainConnectCost / chainConnectGapCost     kent's case analysis on the host, the
+ *                   chainConnect.c:108-149      crossover on the device, gapCalcCost
+ *   chainRemovePartialOverlaps /               kent's list surgery on the host, each
+ *     chainMergeAbutting chainConnect.c:255-368  crossover on the device
+ *   chainBlocks     kent/src/lib/chainBlock.c:392-452  gac_chain_blocks (the kd-tree
+ *                                               DP with the caller's cost callbacks)
+ * The matrix of the text entry points must be a kent DNA scheme: nonzero
+ * only between a/c/g/t in either case, the same for both cases
+ * (propagateCase, axt.c:402-421); anything else ends the process, as an
+ * unsupported input.
  */
 #ifndef GACHAIN_KENT_H
 #define GACHAIN_KENT_H
 
 #include <stdint.h>
+#include <stdio.h>
 
 #include "gachain.h"
 
@@ -81,6 +98,20 @@ struct dnaSeq {
 
 struct gapCalc; /* opaque (wraps a gac_gapcalc) */
 
+#if !defined(CHAINCONNECT_H)
+struct chainConnect { /* kent/src/inc/chainConnect.h:8-15 */
+    struct dnaSeq *query;
+    struct dnaSeq *target;
+    struct axtScoreScheme *ss;
+    struct gapCalc *gapCalc;
+};
+#endif
+
+#if !defined(CHAINBLOCK_H)
+typedef int (*GapCost)(int dq, int dt, void *gapData);                         /* chainBlock.h:13 */
+typedef int (*ConnectCost)(struct cBlock *a, struct cBlock *b, void *gapData); /* chainBlock.h:17 */
+#endif
+
 /* The context the shims score on, for the calling thread (NULL: unbind). */
 void gac_kent_bind(gac_ctx *ctx);
 
@@ -101,9 +132,31 @@ void chainFastSubsetOnT(struct chain *chain, struct cBlock *firstBlock, int subS
  * memory handler) */
 void gac_kent_chain_free(struct chain **pChain);
 
-/* chainCalcScore of n chains in one GPU call: global[i] (kent's double) */
+/* chainCalcScore of n chains in one GPU call: global[i] (kent's double).
+ * The uploaded chain set stays resident while the same chains (same
+ * pointers, block lists unchanged) are scored again: a caller looping
+ * chainCalcScore over a list pays one upload, not one per call. */
 void gac_kent_score_chains(struct chain *const *chains, int64_t n, struct axtScoreScheme *ss,
                            struct gapCalc *gapCalc, double *global);
+/* drop the resident chain set (e.g. before freeing the chains) */
+void gac_kent_forget_chains(void);
+
+double chainScoreBlock(char *q, char *t, int size, int matrix[256][256]);
+int axtScoreUngapped(struct axtScoreScheme *ss, char *q, char *t, int size);
+/* chainScoreBlock of n blocks in one GPU call */
+void gac_kent_score_blocks(int64_t n, char *const *q, char *const *t, const int *size,
+                           int matrix[256][256], double *out);
+void cBlockFindCrossover(struct cBlock *left, struct cBlock *right, struct dnaSeq *qSeq,
+                         struct dnaSeq *tSeq, int overlap, int matrix[256][256], int *retPos,
+                         int *retScoreAdjustment);
+int chainConnectCost(struct cBlock *a, struct cBlock *b, struct chainConnect *cc);
+int chainConnectGapCost(int dq, int dt, struct chainConnect *cc);
+void chainRemovePartialOverlaps(struct chain *chain, struct dnaSeq *qSeq, struct dnaSeq *tSeq,
+                                int matrix[256][256]);
+void chainMergeAbutting(struct chain *chain);
+struct chain *chainBlocks(char *qName, int qSize, char qStrand, char *tName, int tSize,
+                          struct cBlock **pBlockList, ConnectCost connectCost, GapCost gapCost,
+                          void *gapData, FILE *details);
 
 #ifdef __cplusplus
 }

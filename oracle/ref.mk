@@ -80,8 +80,8 @@ $(OUT)/netSyntenic: $(K)/hg/mouseStuff/netSyntenic/netSyntenic.c $(HGOBJ) $(OUT)
 # The reference's kent objects driven by our harness (the reference's own
 # chainSubsetOnT + chainCalcScore, scoreChain's local-score loop restated) --
 # golden generation and the cpu_baseline "reference" leg.
-$(OUT)/kentref: oracle/ref_harness.c $(OUT)/jkweb.a
-	$(CC) $(TCFLAGS) -I$(K)/inc $< -o $@ $(OUT)/jkweb.a $(LIBS) 2>/dev/null
+$(OUT)/kentref: oracle/ref_harness.c oracle/kentapi_workload.inc $(OUT)/jkweb.a
+	$(CC) $(TCFLAGS) -std=gnu99 -I$(K)/inc -Ioracle $< -o $@ $(OUT)/jkweb.a $(LIBS)
 
 clean:
 	rm -rf $(OUT)

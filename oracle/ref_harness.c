@@ -26,7 +26,10 @@
 #include "axt.h"
 #include "gapCalc.h"
 #include "chainConnect.h"
+#include "chainBlock.h"
 #include <time.h>
+
+#include "kentapi_workload.inc"
 
 struct krHandle {
     struct chain **chains;
@@ -223,7 +226,21 @@ static double nowSec(void) {
     return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
+static struct dnaSeq *kaSeq(struct chain *c, int isT, void *u) {
+    return krSeq(u, isT ? c->tName : c->qName, isT ? '+' : c->qStrand, isT);
+}
+
 int main(int argc, char *argv[]) {
+    if (argc == 8 && sameString(argv[1], "kentapi")) {
+        /* kentref kentapi chain t.2bit q.2bit scheme|- gap max_chains */
+        struct krHandle *h = kr_open(argv[2], argv[3], argv[4],
+                                     sameString(argv[5], "-") ? NULL : argv[5], argv[6]);
+        int n = atoi(argv[7]);
+        if (n > h->nChains)
+            n = h->nChains;
+        kentapi_run(h->chains, n, kaSeq, h, h->ss, h->gc, stdout);
+        return 0;
+    }
     if (argc == 5 && sameString(argv[1], "gapcost")) {
         size_t nb;
         int *pairs = readAll(argv[3], &nb);

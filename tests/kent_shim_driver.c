@@ -4,12 +4,67 @@
  * "chain_index start end" line of the ranges file prints
  *   chainCalcScore(chainSubsetOnT(chain, start, end))   (0 if empty)
  * exactly as src/chainNet/chainNet.c:230-248 / subchainInfo compose them.
- * usage: kent_shim_driver in.chain t.2bit q.2bit ranges.txt gap [batch] */
+ * usage: kent_shim_driver in.chain t.2bit q.2bit ranges.txt gap [batch]
+ *        kent_shim_driver in.chain t.2bit q.2bit kentapi gap max_chains
+ * The second form runs oracle/kentapi_workload.inc (the rest of the kent
+ * chain API: chainScoreBlock, axtScoreUngapped, chainConnectCost,
+ * cBlockFindCrossover, chainBlocks, chainRemovePartialOverlaps,
+ * chainMergeAbutting, chainCalcScore) through the shims; oracle/_ref/kentref
+ * runs the same workload on the reference's objects. */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "gachain_kent.h"
+
+#include "kentapi_workload.inc"
+
+/* the text of a chain's sequence (decoded from the bound context's resident
+ * genome; the '-' query reverse-complemented, as axtChain loads it) */
+typedef struct seq_cache {
+    gac_ctx *ctx;
+    char *name[2][4096];
+    int strand[2][4096];
+    struct dnaSeq *seq[2][4096];
+    int n[2];
+} seq_cache;
+
+static struct dnaSeq *drv_seq(struct chain *c, int is_t, void *u) {
+    seq_cache *sc = u;
+    const int side = is_t ? 0 : 1;
+    const char *nm = is_t ? c->tName : c->qName;
+    const int minus = !is_t && c->qStrand == '-';
+    for (int i = 0; i < sc->n[side]; ++i)
+        if (!strcmp(sc->name[side][i], nm) && sc->strand[side][i] == minus)
+            return sc->seq[side][i];
+    const int32_t ix = gac_genome_seq_index(sc->ctx, side, nm);
+    const int32_t size = gac_genome_seq_size(sc->ctx, side, ix);
+    struct dnaSeq *d = calloc(1, sizeof(*d));
+    d->name = strdup(nm);
+    d->size = size;
+    d->dna = malloc(size + 1);
+    if (gac_genome_decode(sc->ctx, side, ix, 0, size, d->dna) != GAC_OK) {
+        fprintf(stderr, "%s\n", gac_last_error());
+        exit(1);
+    }
+    d->dna[size] = 0;
+    if (minus) { /* reverseComplement (kent/src/lib/dnautil.c:404-462) */
+        for (int i = 0, j = size - 1; i < j; ++i, --j) {
+            const char x = d->dna[i];
+            d->dna[i] = d->dna[j];
+            d->dna[j] = x;
+        }
+        for (int i = 0; i < size; ++i) {
+            const char x = d->dna[i];
+            d->dna[i] = x == 'a' ? 't' : x == 't' ? 'a' : x == 'c' ? 'g' : x == 'g' ? 'c' : x;
+        }
+    }
+    const int k = sc->n[side]++;
+    sc->name[side][k] = strdup(nm);
+    sc->strand[side][k] = minus;
+    sc->seq[side][k] = d;
+    return d;
+}
 
 static struct chain **read_chains(const char *path, int *pn) {
     FILE *f = fopen(path, "r");
@@ -82,6 +137,16 @@ int main(int argc, char **argv) {
                     ss->matrix[(unsigned char)(ci ? b[i] + 32 : b[i])]
                               [(unsigned char)(cj ? b[j] + 32 : b[j])] = m[i][j];
     struct gapCalc *gc = gapCalcFromFile(argv[5]);
+    if (!strcmp(argv[4], "kentapi")) {
+        seq_cache *sc = calloc(1, sizeof(*sc));
+        sc->ctx = ctx;
+        const int m = argc > 6 ? atoi(argv[6]) : n;
+        kentapi_run(ch, m < n ? m : n, drv_seq, sc, ss, gc, stdout);
+        fflush(stdout);
+        gac_kent_forget_chains();
+        gac_close(ctx);
+        return 0;
+    }
     FILE *rf = fopen(argv[4], "r");
     int ci, s, e, cnt = 0;
     struct chain **sub = malloc(sizeof(*sub) * 100000), **fr = malloc(sizeof(*fr) * 100000);

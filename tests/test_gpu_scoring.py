@@ -461,6 +461,49 @@ def test_window_blocks_over_int32_are_split():
     assert (g == g1[0]).all() and (l == l1[0]).all() and (a == nb).all()
 
 
+def _kent_driver(tmp_path):
+    """tests/kent_shim_driver.c compiled against include/gachain_kent.h +
+    libgachain_kent.so (and oracle/kentapi_workload.inc)."""
+    import subprocess
+    from genomealignmenttools_amd._lib import LIB_DIR
+    from conftest import REPO
+    exe = tmp_path / "drv"
+    r = subprocess.run(["gcc", "-O1", "-std=gnu11", "-I", os.path.join(REPO, "include"), "-I",
+                        os.path.join(REPO, "oracle"),
+                        os.path.join(REPO, "tests", "kent_shim_driver.c"), "-o", str(exe),
+                        "-L", LIB_DIR, "-lgachain_kent", "-lgachain", f"-Wl,-rpath,{LIB_DIR}"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return exe
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("seed", [11, 12])
+def test_kent_api_shims_vs_reference(seed, tmp_path):
+    """The rest of the kent chain API through the shims -- chainScoreBlock,
+    axtScoreUngapped (device text kernels), chainConnectCost and
+    cBlockFindCrossover on real and forced overlaps, chainBlocks (the kd-tree
+    DP with the caller's ConnectCost/GapCost callbacks) on block soups with
+    overlapping copies, chainRemovePartialOverlaps + chainMergeAbutting, and
+    chainCalcScore on the results -- prints exactly what the reference's own
+    kent objects print for the same workload (oracle/kentapi_workload.inc,
+    run by oracle/_ref/kentref in the same test)."""
+    import subprocess
+    from oracle.oracle import ref_tool
+    d = os.path.join(GOLDEN, f"synth{seed}")
+    exe = _kent_driver(tmp_path)
+    args = [os.path.join(d, "in.chain"), os.path.join(d, "t.2bit"), os.path.join(d, "q.2bit")]
+    ref = subprocess.run([ref_tool("kentref"), "kentapi"] + args + ["-", "loose", "150"],
+                         capture_output=True, text=True, timeout=300)
+    assert ref.returncode == 0, ref.stderr[-2000:]
+    ours = subprocess.run([str(exe)] + args + ["kentapi", "loose", "150"], capture_output=True,
+                          text=True, timeout=500)
+    assert ours.returncode == 0, ours.stderr[-2000:]
+    tags = {ln.split()[0] for ln in ref.stdout.splitlines()}
+    assert {"s", "c", "o", "k", "kb", "kr", "kx"} <= tags
+    assert ours.stdout == ref.stdout
+
+
 @pytest.mark.parametrize("batch", [False, True])
 def test_kent_shims_vs_reference(batch, tmp_path):
     """A kent-style C caller (tests/kent_shim_driver.c, compiled here against
@@ -473,12 +516,7 @@ def test_kent_shims_vs_reference(batch, tmp_path):
     from conftest import REPO
     d = os.path.join(GOLDEN, "synth11")
     z = np.load(os.path.join(d, "subchain.npz"))
-    exe = tmp_path / "drv"
-    r = subprocess.run(["gcc", "-O1", "-I", os.path.join(REPO, "include"),
-                        os.path.join(REPO, "tests", "kent_shim_driver.c"), "-o", str(exe),
-                        "-L", LIB_DIR, "-lgachain_kent", "-lgachain", f"-Wl,-rpath,{LIB_DIR}"],
-                       capture_output=True, text=True)
-    assert r.returncode == 0, r.stderr
+    exe = _kent_driver(tmp_path)
     R = z["ranges"][:600 if not batch else 3000]
     np.savetxt(tmp_path / "r.txt", R, fmt="%d")
     r = subprocess.run([str(exe), os.path.join(d, "in.chain"), os.path.join(d, "t.2bit"),
