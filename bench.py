@@ -91,6 +91,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pmc", action="store_true")
     p.add_argument("--tmp", default=os.environ.get("TMPDIR", "/tmp"))
+    p.add_argument("--sharded-scorechain", action="store_true",
+                   help="N = 1: also run the N > 1 scorechain leg (world-1 RCCL group)")
     p.add_argument("--pmc-child", choices=["fills", "scorechain"], help=argparse.SUPPRESS)
     p.add_argument("--gen-only", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
@@ -293,6 +295,11 @@ class Legs:
         return {"step_ms": dt / steps * 1e3, "tile_ms": tile_ms / max(tile_n, 1), "kernel_ms": kern,
                 "bases": int(ali.sum(dtype=np.int64)), "steps": steps}
 
+    def score_all(self):
+        """Every chain's (global, local, ali), one untimed call (the check of
+        the sharded N > 1 leg)."""
+        return self.e.score_chains(self.cs, want_local=True)
+
     def close(self):
         self.cs.close()
         self.e.close()
@@ -344,6 +351,66 @@ def scorechain_leg(legs, ch, steps, pmc):
             "scored_bases": res["bases"], "kernel_ms": res["kernel_ms"],
             "model": "full chain: 0.75 B/base + 12 B/block + 44 B/chain",
             "roofline_step": step, "roofline": tile}
+
+
+def scorechain_sharded_leg(d, ch, dist, rank, world, steps, expect=None):
+    """N > 1: scoreChain's batch in the north-star form: chain-ID
+    shards -- contiguous chain runs balanced by blocks, one per rank -- each
+    scored whole on its rank's GPU (gac_score_chains_device into torch
+    tensors), then ONE RCCL all-gather of {global, local, ali} over xGMI.  A
+    step = scoring + all-gather, between barriers, max over ranks.  Rank 0
+    checks the gathered set against the single-GPU scores (`expect`)."""
+    import torch
+    from genomealignmenttools_amd.gachain import GAC_Q, GAC_T, Engine, GapCosts
+    from genomealignmenttools_amd.shard import (reduce_time_and_work, score_chains_sharded_gpu,
+                                                shard_bounds)
+    e = Engine(int(os.environ.get("LOCAL_RANK", "0")))
+    e.load_2bit(GAC_T, os.path.join(d, "t.2bit"))
+    e.load_2bit(GAC_Q, os.path.join(d, "q.2bit"))
+    e.set_scoring(BLASTZ, GapCosts("loose"))
+    names = lambda path: [ln.split()[0] for ln in open(path) if ln.strip()]
+    tmap = np.array([e.seq_index(GAC_T, x) for x in names(os.path.join(d, "t.sizes"))], np.int32)
+    qmap = np.array([e.seq_index(GAC_Q, x) for x in names(os.path.join(d, "q.sizes"))], np.int32)
+    off = ch["off"]
+    bounds = shard_bounds(np.diff(off), world)
+    lo, hi = bounds[rank]
+    b0, b1 = int(off[lo]), int(off[hi])
+    cs = e.upload_chain_arrays(tmap[ch["tseq"][lo:hi]], qmap[ch["qseq"][lo:hi]],
+                               ch["strand"][lo:hi], off[lo:hi + 1] - b0, ch["bt"][b0:b1],
+                               ch["bq"][b0:b1], ch["bs"][b0:b1])
+    n = ch["n"]
+    for _ in range(3):
+        res = score_chains_sharded_gpu(dist, rank, world, e, cs, n, bounds)
+    torch.cuda.synchronize()
+    dt = 0.0
+    for _ in range(steps):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = score_chains_sharded_gpu(dist, rank, world, e, cs, n, bounds)
+        torch.cuda.synchronize()
+        dt += time.perf_counter() - t0
+    dt, _ = reduce_time_and_work(dist, dt, 0.0, device=f"cuda:{torch.cuda.current_device()}")
+    step = dt / steps
+    out = None
+    if rank == 0:
+        got = res.cpu().numpy()
+        same = None
+        if expect is not None:
+            g, l, a = expect
+            same = bool(np.array_equal(got[:, 0], g) and np.array_equal(got[:, 1], l)
+                        and np.array_equal(got[:, 2], a))
+        bases = int(ch["bs"].sum(dtype=np.int64))
+        out = {"workload": "scoreChain: every C5 chain, global + local + aligned bases; chain-ID "
+                           f"shards on {world} GPUs + one RCCL all-gather of (global, local, ali)",
+               "value": bases / step / 1e9, "unit": "Gbases/s", "ms_per_step": step * 1e3,
+               "steps": steps, "chains": n, "blocks": ch["nb"], "scored_bases": bases,
+               "shard_chains": [hi_ - lo_ for lo_, hi_ in bounds],
+               "allgather_bytes": 24 * max(hi_ - lo_ for lo_, hi_ in bounds) * world,
+               "identical_to_single_gpu": same}
+    cs.close()
+    e.close()
+    return out
 
 
 PMC_PASSES = ("TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum",
@@ -632,6 +699,7 @@ def main():
             out["c2"] = c2_leg(args, args.c2_steps, 1)
         except Exception as ex:  # reported, never fatal
             out["c2"] = {"error": str(ex)[:300]}
+    expect = None
     if rank == 0 and not args.no_kernel:
         if world > 1 and not os.path.exists(os.path.join(d, "fills.bin")):
             staged_run(d, os.path.join(d, "ours.fills"))  # untimed, after the timed region
@@ -639,8 +707,35 @@ def main():
         legs = Legs(d, ch)
         out["kernel"], out["roofline"] = fills_leg(legs, d, ch, args.kernel_steps, pmc_f)
         if not args.no_scorechain:
-            out["scorechain"] = scorechain_leg(legs, ch, args.kernel_steps, pmc_s)
+            if world == 1:
+                out["scorechain"] = scorechain_leg(legs, ch, args.kernel_steps, pmc_s)
+            else:
+                expect = legs.score_all()
         legs.close()
+    if world > 1 and not (args.no_kernel or args.no_scorechain or one_gpu):
+        barrier()
+        if ch is None:
+            ch = load_chains_bin(d)
+        sc = scorechain_sharded_leg(d, ch, dist, rank, world, args.kernel_steps, expect)
+        if rank == 0:
+            out["scorechain"] = sc
+    elif world == 1 and args.sharded_scorechain:  # rehearsal of the N > 1 leg on one GPU
+        import socket
+        import torch
+        import torch.distributed as tdist
+        s_ = socket.socket()
+        s_.bind(("127.0.0.1", 0))
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s_.getsockname()[1]))
+        s_.close()
+        torch.cuda.set_device(0)
+        tdist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+        legs = Legs(d, ch if ch is not None else load_chains_bin(d))
+        expect = legs.score_all()
+        legs.close()
+        out["scorechain_sharded"] = scorechain_sharded_leg(d, ch if ch is not None else
+                                                           load_chains_bin(d), tdist, 0, 1,
+                                                           args.kernel_steps, expect)
+        tdist.destroy_process_group()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline_c5(d, out_base)

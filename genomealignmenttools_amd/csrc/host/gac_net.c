@@ -23,6 +23,8 @@
 #include "gac_host.h"
 
 #include <sched.h>
+#include <stdint.h>
+#include <sys/mman.h>
 #include <stdatomic.h>
 #include <math.h>
 #include <stdio.h>
@@ -67,8 +69,33 @@ typedef struct nchrom {
 /* ------------------------------------------------------------ arena */
 typedef struct arena {
     char **blocks;
+    size_t *sizes;
     size_t n, cap, used, bsize;
 } arena;
+
+/* Arena blocks are 32 MB, 2 MB-aligned anonymous mappings advised for huge
+ * pages: a C5 net holds GBs of fills and gaps, and returning that many 4 KB
+ * pages to the kernel at exit cost more than writing the nets did. */
+#define ARENA_BLOCK ((size_t)32 << 20)
+#define ARENA_ALIGN ((size_t)2 << 20)
+
+static char *arena_map(size_t bs) {
+    size_t len = bs + ARENA_ALIGN;
+    char *m = mmap(NULL, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (m == MAP_FAILED) {
+        fprintf(stderr, "gac_net: out of memory mapping %zu bytes\n", bs);
+        abort();
+    }
+    char *p = (char *)(((uintptr_t)m + ARENA_ALIGN - 1) & ~(uintptr_t)(ARENA_ALIGN - 1));
+    if (p > m)
+        munmap(m, (size_t)(p - m));
+    if (p + bs < m + len)
+        munmap(p + bs, (size_t)(m + len - (p + bs)));
+#ifdef MADV_HUGEPAGE
+    madvise(p, bs, MADV_HUGEPAGE);
+#endif
+    return p;
+}
 
 static void *arena_alloc(arena *a, size_t sz) {
     sz = (sz + 15) & ~(size_t)15;
@@ -76,9 +103,11 @@ static void *arena_alloc(arena *a, size_t sz) {
         if (a->n == a->cap) {
             a->cap = a->cap ? a->cap * 2 : 64;
             a->blocks = realloc(a->blocks, a->cap * sizeof(char *));
+            a->sizes = realloc(a->sizes, a->cap * sizeof(size_t));
         }
-        size_t bs = sz > (1u << 22) ? sz : (1u << 22);
-        a->blocks[a->n++] = calloc(1, bs);
+        size_t bs = sz > ARENA_BLOCK ? (sz + ARENA_ALIGN - 1) & ~(ARENA_ALIGN - 1) : ARENA_BLOCK;
+        a->blocks[a->n] = arena_map(bs);
+        a->sizes[a->n++] = bs;
         a->bsize = bs;
         a->used = 0;
     }
@@ -89,8 +118,9 @@ static void *arena_alloc(arena *a, size_t sz) {
 
 static void arena_free(arena *a) {
     for (size_t i = 0; i < a->n; ++i)
-        free(a->blocks[i]);
+        munmap(a->blocks[i], a->sizes[i]);
     free(a->blocks);
+    free(a->sizes);
     memset(a, 0, sizeof(*a));
 }
 
@@ -127,6 +157,7 @@ struct gac_net {
     nfill **order[2];
     int64_t n_order[2];
     int sides; /* bit 1 << side: side netted */
+    atomic_int free_next; /* gac_net_free's worker cursor */
 };
 
 /* ------------------------------------------------------------ space index */
@@ -862,10 +893,14 @@ static void finish_gap(fin_ctx *x, ngap *g) {
 }
 
 /* ------------------------------------------------------------ API */
-void gac_net_free(gac_net *n) {
-    if (!n)
-        return;
-    for (int i = 0; i < n->n_w; ++i) {
+/* Workers' pools are released in parallel: unmapping a C5 net is ~0.2 s of
+ * page-table teardown on one core. */
+static void *free_worker(void *arg) {
+    gac_net *n = arg;
+    for (;;) {
+        int i = atomic_fetch_add(&n->free_next, 1);
+        if (i >= n->n_w)
+            return NULL;
         nwork *w = &n->w[i];
         arena_free(&w->ar);
         free(w->lf);
@@ -877,6 +912,15 @@ void gac_net_free(gac_net *n) {
         free(w->re);
         free(w->ros);
         free(w->roe);
+    }
+}
+
+void gac_net_free(gac_net *n) {
+    if (!n)
+        return;
+    if (n->w) {
+        atomic_store(&n->free_next, 0);
+        gac_run_threads(n->n_w < 8 ? n->n_w : 8, free_worker, n);
     }
     free(n->w);
     free(n->chroms[0]);

@@ -670,9 +670,10 @@ int main(int argc, char *argv[]) {
     }
     gt_device_close_join(&dev);
     gt_stage("device close (rest)");
-    /* the net, chains and sizes are left to process exit (freeing millions
-     * of arena blocks and arrays only costs time) */
     gac_gapcalc_free(gap);
     gt_ranks_done(&g_rk);
+    /* The net's pools are unmapped on 8 threads: left to process teardown
+     * they are freed on one core after the output is complete. */
+    gac_net_free(net);
     gt_exit_ok();
 }

@@ -1,4 +1,5 @@
-"""Multi-GPU sharding of one batch of sub-chain ranges.
+"""Multi-GPU sharding of one batch of sub-chain ranges or of a whole chain
+set.
 
 Chains / fills are independent, so a batch is split into contiguous shards
 balanced by window blocks, each rank scores its shard on its own GPU, and a
@@ -12,7 +13,9 @@ gac_score_ranges_device on torch's current stream) and the gathered result.
 The command-line tools split differently (no collective at all): chainNet
 -nranks deals out chromosome sides, scoreChain -nranks contiguous chain runs
 (their outputs are the exchange).  This module is for callers that hold one
-range batch -- e.g. a rescoring service -- across the GPUs of a node.
+range batch -- e.g. a rescoring service -- across the GPUs of a node, and
+for scoreChain's batch in the north-star form (chain-ID shards + one RCCL
+all-gather of {global, local, ali}), which bench.py measures at N > 1.
 """
 from __future__ import annotations
 
@@ -100,6 +103,47 @@ def score_sharded_gpu(dist, rank: int, world: int, engine, chainset, ranges, wei
         l.zero_()
     local = torch.stack([g, l, a.to(torch.int64)], 1)
     return gather_sharded(dist, world, r.shape[0], bounds, local)
+
+
+def score_chains_sharded(dist, rank: int, world: int, n: int, weights: np.ndarray,
+                         scorer: Callable, device=None):
+    """scoreChain's batch across ranks: chain-ID shards --
+    contiguous runs of chains balanced by `weights` (their block counts) --
+    scored by scorer(lo, hi) -> (global, local, ali) of chains [lo, hi) on
+    this rank, then ONE all-gather of {global, local, ali} reassembles the
+    set in chain order on every rank.  Returns numpy (global, local, ali)."""
+    import torch
+    bounds = shard_bounds(weights, world)
+    lo, hi = bounds[rank]
+    g, l, a = scorer(lo, hi) if hi > lo else (np.zeros(0),) * 3
+    cols = (np.stack([np.asarray(g, np.int64), np.asarray(l, np.int64),
+                      np.asarray(a, np.int64)], 1) if hi > lo else np.zeros((0, 3), np.int64))
+    full = gather_sharded(dist, world, n, bounds,
+                          torch.from_numpy(cols).to(device if device is not None else "cpu"))
+    full = full.cpu().numpy()
+    return full[:, 0], full[:, 1], full[:, 2].astype(np.int32)
+
+
+def score_chains_sharded_gpu(dist, rank: int, world: int, engine, shard_set, n: int, bounds,
+                             want_local: bool = True):
+    """The GPU path of score_chains_sharded: `shard_set` is this rank's chains
+    [bounds[rank]) uploaded to its GPU; libgachain scores them whole
+    (gac_score_chains_device) into device tensors on torch's current stream,
+    and one all-gather over RCCL (xGMI) reassembles the int64 [n, 3]
+    (global, local, ali) set on every rank's device."""
+    import torch
+    dev = torch.device("cuda", torch.cuda.current_device())
+    lo, hi = bounds[rank]
+    m = hi - lo
+    g = torch.empty(m, dtype=torch.int64, device=dev)
+    l = torch.zeros(m, dtype=torch.int64, device=dev)
+    a = torch.empty(m, dtype=torch.int32, device=dev)
+    if m:
+        engine.score_chains_device(shard_set, g.data_ptr(), a.data_ptr(),
+                                   d_l=l.data_ptr() if want_local else 0, want_local=want_local,
+                                   stream=torch.cuda.current_stream().cuda_stream)
+    local = torch.stack([g, l, a.to(torch.int64)], 1)
+    return gather_sharded(dist, world, n, bounds, local)
 
 
 def reduce_time_and_work(dist, seconds: float, work: float, device=None) -> Tuple[float, float]:

@@ -25,7 +25,8 @@ def _worker(rank, world, port, q):
     import torch.distributed as dist
 
     from genomealignmenttools_amd.chainfile import read_chains
-    from genomealignmenttools_amd.shard import reduce_time_and_work, score_sharded
+    from genomealignmenttools_amd.shard import (reduce_time_and_work, score_chains_sharded,
+                                                score_sharded)
     from oracle.oracle import OracleScorer, read_2bit_text
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -41,6 +42,12 @@ def _worker(rank, world, port, q):
         g, l, a = score_sharded(dist, rank, world, R, w, lambda r: sc.score_ranges(ca, r))
         ok = (np.array_equal(g, z["glob"]) and np.array_equal(l, z["loc"])
               and np.array_equal(a, z["ali"]))
+        # whole chains (scoreChain's batch): chain-ID shards + one all-gather
+        full = np.stack([np.arange(ca.n), ca.tstart, ca.tend], 1).astype(np.int64)
+        og, ol, oa = sc.score_ranges(ca, full)
+        g, l, a = score_chains_sharded(dist, rank, world, ca.n, np.diff(ca.blk_off).astype(float),
+                                       lambda lo, hi: sc.score_ranges(ca, full[lo:hi]))
+        ok = ok and np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
         mx, sm = reduce_time_and_work(dist, 1.0 + rank, 10.0 * (rank + 1))
         q.put((rank, ok, mx, sm))
     finally:

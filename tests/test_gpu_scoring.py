@@ -543,7 +543,8 @@ def test_sharded_scoring_rccl_world1():
 
     from genomealignmenttools_amd.chainfile import read_chains
     from genomealignmenttools_amd.gachain import GAC_Q, GAC_T, Engine, GapCosts
-    from genomealignmenttools_amd.shard import score_sharded_gpu
+    from genomealignmenttools_amd.shard import (score_chains_sharded_gpu, score_sharded_gpu,
+                                                shard_bounds)
     d = os.path.join(GOLDEN, "synth12")
     z = np.load(os.path.join(d, "subchain.npz"))
     ca = read_chains(os.path.join(d, "in.chain"))
@@ -567,5 +568,20 @@ def test_sharded_scoring_rccl_world1():
         res = out.cpu().numpy()
         assert np.array_equal(res[:, 0], z["glob"]) and np.array_equal(res[:, 1], z["loc"])
         assert np.array_equal(res[:, 2], z["ali"])
+        # scoreChain's batch in the north-star form: chain-ID shards (here the
+        # one rank's shard: all chains) + one RCCL all-gather of {g, l, ali}
+        bounds = shard_bounds(np.diff(ca.blk_off), 1)
+        out = score_chains_sharded_gpu(dist, 0, 1, e, cs, ca.n, bounds)
+        full = np.stack([np.arange(ca.n), ca.tstart, ca.tend], 1).astype(np.int64)
+        og, ol, oa = _oracle_text(d).score_ranges(ca, full)
+        res = out.cpu().numpy()
+        assert np.array_equal(res[:, 0], og) and np.array_equal(res[:, 1], ol)
+        assert np.array_equal(res[:, 2], oa)
     finally:
         dist.destroy_process_group()
+
+
+def _oracle_text(d):
+    from oracle.oracle import OracleScorer, read_2bit_text
+    return OracleScorer(read_2bit_text(os.path.join(d, "t.2bit")),
+                        read_2bit_text(os.path.join(d, "q.2bit")), BLASTZ, "loose")
