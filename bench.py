@@ -629,6 +629,20 @@ def main():
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", rank=rank, world_size=world,
                                     device_id=torch.device(f"cuda:{local}"))
+    rdist = None
+    if world == 1 and args.sharded_scorechain:
+        # rehearsal of the N > 1 scoreChain leg: a world-1 RCCL group, made
+        # before this process opens the device through libgachain (torch's
+        # HIP initialisation fails after it)
+        import socket
+        import torch
+        import torch.distributed as rdist
+        s_ = socket.socket()
+        s_.bind(("127.0.0.1", 0))
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s_.getsockname()[1]))
+        s_.close()
+        torch.cuda.set_device(0)
+        rdist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
 
     def barrier():
         if dist is not None:
@@ -719,23 +733,14 @@ def main():
         sc = scorechain_sharded_leg(d, ch, dist, rank, world, args.kernel_steps, expect)
         if rank == 0:
             out["scorechain"] = sc
-    elif world == 1 and args.sharded_scorechain:  # rehearsal of the N > 1 leg on one GPU
-        import socket
-        import torch
-        import torch.distributed as tdist
-        s_ = socket.socket()
-        s_.bind(("127.0.0.1", 0))
-        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s_.getsockname()[1]))
-        s_.close()
-        torch.cuda.set_device(0)
-        tdist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    elif rdist is not None:  # rehearsal of the N > 1 leg on one GPU
         legs = Legs(d, ch if ch is not None else load_chains_bin(d))
         expect = legs.score_all()
         legs.close()
         out["scorechain_sharded"] = scorechain_sharded_leg(d, ch if ch is not None else
-                                                           load_chains_bin(d), tdist, 0, 1,
+                                                           load_chains_bin(d), rdist, 0, 1,
                                                            args.kernel_steps, expect)
-        tdist.destroy_process_group()
+        rdist.destroy_process_group()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline_c5(d, out_base)

@@ -48,8 +48,9 @@ hipError_t launch_gap_table(const GapDev &g, const int32_t *small, int len, int3
 hipError_t launch_block_gaps(const DChain *chains, int64_t n_chains, int4 *blk, const GapDev &g,
                              const int32_t *small, const int32_t *tab, int len, hipStream_t s);
 hipError_t launch_nflags(const DChain *chains, int64_t n_chains, int4 *blk,
-                         const uint32_t *t_nmask, const int64_t *t_woff, const uint32_t *q_nmask,
-                         const int64_t *q_woff, hipStream_t s);
+                         const longlong2 *t_runs, int64_t n_trun, const uint32_t *t_nmask,
+                         const longlong2 *q_runs, int64_t n_qrun, const uint32_t *q_nmask,
+                         const int64_t *q_woff, int2 *list, int *count, hipStream_t s);
 hipError_t launch_build(const int32_t *bt, const int32_t *bq, const int32_t *bs, int64_t nb,
                         const DChain *chains, int64_t n_chains, int4 *blk, int2 *tspan,
                         uint32_t *bucket, hipStream_t s);
@@ -107,6 +108,8 @@ struct Genome {
     uint2 *planes = nullptr;
     uint32_t *nmask = nullptr;
     int64_t *d_woff = nullptr;
+    longlong2 *d_nrun = nullptr;    // the N runs as global {start, end} bases, sorted
+    int64_t n_nrun = 0;
     const uint8_t *packed(int i) const { return ext[i] ? ext[i] : raw.data() + raw_off[i]; }
 };
 
@@ -289,6 +292,7 @@ static void free_genome(Genome &g) {
     if (g.planes) hipFree(g.planes);
     if (g.nmask) hipFree(g.nmask);
     if (g.d_woff) hipFree(g.d_woff);
+    if (g.d_nrun) hipFree(g.d_nrun);
     g = Genome();
 }
 
@@ -764,6 +768,19 @@ extern "C" int gac_genome_finalize(gac_ctx *c, int side) {
     }
     std::vector<NPiece>().swap(g->npieces);
     std::vector<int32_t>().swap(g->npiece_seq);
+    {  // global N runs (chain-level N test at chain upload)
+        std::vector<longlong2> gr(g->nrun_start.size());
+        for (int i = 0; i < nseq; ++i)
+            for (int64_t k = g->nrun_off[i]; k < g->nrun_off[i + 1]; ++k) {
+                gr[k].x = g->woff[i] * 32 + g->nrun_start[k];
+                gr[k].y = gr[k].x + g->nrun_size[k];
+            }
+        g->n_nrun = (int64_t)gr.size();
+        HIPCHK(hipMalloc(&g->d_nrun, std::max<size_t>(gr.size(), 1) * sizeof(longlong2)));
+        if (!gr.empty())
+            HIPCHK(hipMemcpy(g->d_nrun, gr.data(), gr.size() * sizeof(longlong2),
+                             hipMemcpyHostToDevice));
+    }
     g->final = true;
     return GAC_OK;
 }
@@ -1390,12 +1407,18 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
         e = launch_build(d_bt, d_bt + nb, d_bt + 2 * nb, (int64_t)nb, cs->chains, cs->n_chains,
                          cs->blk, cs->tspan, cs->bucket, c->stream);
     // per-block N flags (scoring skips N-mask loads of N-free blocks)
-    if (e == hipSuccess && rc == GAC_OK)
-        e = launch_nflags(cs->chains, cs->n_chains, cs->blk, c->g[0].nmask, c->g[0].d_woff,
-                          c->g[1].nmask, c->g[1].d_woff, c->stream);
+    int2 *d_nlist = nullptr;  // chains whose span meets an N run (+ count)
+    if (e == hipSuccess && rc == GAC_OK && (c->g[0].n_nrun || c->g[1].n_nrun)) {
+        e = hipMalloc(&d_nlist, (size_t)(n + 1) * sizeof(int2));
+        if (e == hipSuccess)
+            e = launch_nflags(cs->chains, n, cs->blk, c->g[0].d_nrun, c->g[0].n_nrun,
+                              c->g[0].nmask, c->g[1].d_nrun, c->g[1].n_nrun, c->g[1].nmask,
+                              c->g[1].d_woff, d_nlist + 1, (int *)d_nlist, c->stream);
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     lap("device build + sync");
     if (d_bt) hipFree(d_bt);
+    if (d_nlist) hipFree(d_nlist);
     if (e != hipSuccess || rc != GAC_OK) {
         gac_chains_free(cs);
         if (rc != GAC_OK) return rc;

@@ -175,8 +175,12 @@ __device__ __forceinline__ long long wave_sum(long long v) {
 
 // ------------------------------------------------------------ k_nflags ---
 // At chain upload: flag blocks whose target / query bases contain an N, so
-// the scoring kernel can skip N-mask loads for all other blocks.  One wave
-// per chain, lanes over blocks.
+// the scoring kernel can skip N-mask loads for all other blocks.  Genomes
+// hold few N runs (assembly gaps), so a chain is first checked as a whole:
+// one lane per chain tests its target and query spans against the sorted
+// global N runs (k_nflags_chains); only chains whose span meets a run have
+// their blocks checked against the N mask (k_nflags_blocks, one wave per
+// listed chain, lanes over blocks).
 __device__ __forceinline__ bool range_has_n(const uint32_t *nmask, int64_t p, int len) {
     if (len <= 0) return false;
     int64_t w = p >> 5;
@@ -192,23 +196,59 @@ __device__ __forceinline__ bool range_has_n(const uint32_t *nmask, int64_t p, in
     return false;
 }
 
-__global__ void __launch_bounds__(256) k_nflags(const DChain *chains, int64_t n_chains, int4 *blk,
-                                                const uint32_t *t_nmask, const int64_t *t_woff,
-                                                const uint32_t *q_nmask, const int64_t *q_woff) {
+// does [lo, hi) meet one of the sorted, disjoint runs {start, end}?
+__device__ __forceinline__ bool span_meets(const longlong2 *runs, int64_t n, int64_t lo, int64_t hi) {
+    int64_t a = 0, b = n;  // first run ending past lo
+    while (a < b) {
+        const int64_t m = (a + b) >> 1;
+        if (runs[m].y > lo) b = m;
+        else a = m + 1;
+    }
+    return a < n && runs[a].x < hi;
+}
+
+__global__ void __launch_bounds__(256) k_nflags_chains(const DChain *chains, int64_t n_chains,
+                                                       const int4 *blk, const longlong2 *t_runs,
+                                                       int64_t n_trun, const longlong2 *q_runs,
+                                                       int64_t n_qrun, const int64_t *q_woff,
+                                                       int2 *list, int *count) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_chains) return;
+    const DChain ch = chains[c];
+    if (ch.nblk <= 0) return;
+    const bool t = n_trun && span_meets(t_runs, n_trun, ch.tbase + ch.tstart, ch.tbase + ch.tend);
+    bool q = false;
+    if (n_qrun) {
+        const int4 f = blk[ch.blk_off], l = blk[ch.blk_off + ch.nblk - 1];
+        const int64_t qs = f.y, qe = (int64_t)l.y + (l.z & kSizeMask);
+        const int64_t qsize = ch.qinfo & 0x7fffffff, qb = q_woff[ch.q_seq] * 32;
+        q = ch.qinfo < 0 ? span_meets(q_runs, n_qrun, qb + qsize - qe, qb + qsize - qs)
+                         : span_meets(q_runs, n_qrun, qb + qs, qb + qe);
+    }
+    if (t || q) list[atomicAdd(count, 1)] = make_int2((int)c, (t ? 1 : 0) | (q ? 2 : 0));
+}
+
+__global__ void __launch_bounds__(256) k_nflags_blocks(const DChain *chains, int4 *blk,
+                                                       const uint32_t *t_nmask,
+                                                       const uint32_t *q_nmask,
+                                                       const int64_t *q_woff, const int2 *list,
+                                                       const int *count) {
     const int lane = threadIdx.x & 63;
     const int64_t wave_id = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    for (int64_t c = wave_id; c < n_chains; c += nwaves) {
-        const DChain ch = chains[c];
-        const int64_t tb = t_woff[ch.t_seq] * 32, qb = q_woff[ch.q_seq] * 32;
+    const int cnt = *count;
+    for (int64_t i = wave_id; i < cnt; i += nwaves) {
+        const int2 e = list[i];
+        const DChain ch = chains[e.x];
+        const int64_t tb = ch.tbase, qb = q_woff[ch.q_seq] * 32;
         const bool minus = ch.qinfo < 0;
         const int qsize = ch.qinfo & 0x7fffffff;
         for (int k = lane; k < ch.nblk; k += kWave) {
             int4 b = blk[ch.blk_off + k];
             const int z = b.z & kSizeMask;
             const int64_t qf = minus ? (int64_t)qsize - b.y - z : b.y;
-            b.z = z | (range_has_n(t_nmask, tb + b.x, z) ? kTHasN : 0) |
-                  (range_has_n(q_nmask, qb + qf, z) ? kQHasN : 0);
+            b.z = z | ((e.y & 1) && range_has_n(t_nmask, tb + b.x, z) ? kTHasN : 0) |
+                  ((e.y & 2) && range_has_n(q_nmask, qb + qf, z) ? kQHasN : 0);
             blk[ch.blk_off + k] = b;
         }
     }
@@ -233,6 +273,10 @@ __global__ void __launch_bounds__(256) k_build_blocks(const int32_t *bt, const i
     }
 }
 
+// bucket k of a chain := the first block whose target end passes the
+// bucket's start tstart + k * 2^shift.  Block b is that block for the buckets
+// starting in [tEnd(b-1), tEnd(b)): one wave per chain, each lane writes the
+// buckets of its blocks (no search; at most 2 * nblk + 1 buckets per chain).
 __global__ void __launch_bounds__(256) k_build_buckets(const DChain *chains, int64_t n_chains,
                                                        const int2 *tspan, uint32_t *bucket) {
     const int lane = threadIdx.x & 63;
@@ -243,20 +287,14 @@ __global__ void __launch_bounds__(256) k_build_buckets(const DChain *chains, int
         const int2 *sp = tspan + ch.blk_off;
         const int64_t span = (int64_t)ch.tend - ch.tstart;
         const int64_t nbk = span > 0 ? ((span - 1) >> ch.shift) + 1 : 0;
+        const int64_t round = ((int64_t)1 << ch.shift) - 1;
         uint32_t *bk = bucket + ch.idx_off;
-        for (int64_t k = lane; k <= nbk; k += kWave) {
-            if (k == nbk) {
-                bk[k] = (uint32_t)ch.nblk;
-                continue;
-            }
-            const int64_t pos = ch.tstart + (k << ch.shift);
-            int lo = 0, hi = ch.nblk;  // first block with tEnd > pos
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if ((int64_t)sp[mid].y > pos) hi = mid;
-                else lo = mid + 1;
-            }
-            bk[k] = (uint32_t)lo;
+        if (lane == 0) bk[nbk] = (uint32_t)ch.nblk;
+        for (int b = lane; b < ch.nblk; b += kWave) {
+            const int64_t k0 = b ? ((int64_t)sp[b - 1].y - ch.tstart + round) >> ch.shift : 0;
+            int64_t k1 = ((int64_t)sp[b].y - ch.tstart + round) >> ch.shift;
+            if (k1 > nbk) k1 = nbk;
+            for (int64_t k = k0; k < k1; ++k) bk[k] = (uint32_t)b;
         }
     }
 }
@@ -659,10 +697,24 @@ struct ChunkRaw {
     u32x4a8 t, q;  // plane words w, w+1 ({p0, p1} each)
 };
 
+typedef int i32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ int4 ld_nt(const int4 *p) {
+    const i32x4v v = __builtin_nontemporal_load(reinterpret_cast<const i32x4v *>(p));
+    return make_int4(v.x, v.y, v.z, v.w);
+}
+
+template <bool NT>
 __device__ __forceinline__ ChunkRaw chunk_load(const ScoreArgs &a, const ChunkRef &c) {
     ChunkRaw r;
-    r.t = *reinterpret_cast<const u32x4a8 *>(a.t_planes + (c.tp >> 5));
-    r.q = *reinterpret_cast<const u32x4a8 *>(a.q_planes + (c.qp >> 5));
+    const u32x4a8 *pt = reinterpret_cast<const u32x4a8 *>(a.t_planes + (c.tp >> 5));
+    const u32x4a8 *pq = reinterpret_cast<const u32x4a8 *>(a.q_planes + (c.qp >> 5));
+    if (NT) {
+        r.t = __builtin_nontemporal_load(pt);
+        r.q = __builtin_nontemporal_load(pq);
+    } else {
+        r.t = *pt;
+        r.q = *pq;
+    }
     return r;
 }
 
@@ -770,7 +822,7 @@ __device__ __forceinline__ void seg_store(const ScoreArgs &a, int ri, long long 
 #ifndef GAC_TILE_MINB
 #define GAC_TILE_MINB 6  // waves per SIMD the register budget is sized for
 #endif
-template <bool LOCAL, bool SYM>
+template <bool LOCAL, bool SYM, bool NT>
 __global__ void __launch_bounds__(256, GAC_TILE_MINB) k_tile(ScoreArgs a) {
     __shared__ WaveLds s_w[kWavesPerWG];
 
@@ -846,7 +898,8 @@ __global__ void __launch_bounds__(256, GAC_TILE_MINB) k_tile(ScoreArgs a) {
         long long tpos = 0, qpos = 0;
         if (active) {
             const RangeDesc d = a.rdesc[ri];
-            const int4 bk = a.blk[bi];  // {tStart, qStart, size | N flags, gap to next}
+            // {tStart, qStart, size | N flags, gap to next}
+            const int4 bk = NT ? ld_nt(a.blk + bi) : a.blk[bi];
             first = (bi == d.b0);
             last = (bi == d.b0 + d.nblk - 1);
             const int z = bk.z & kSizeMask;
@@ -882,8 +935,8 @@ __global__ void __launch_bounds__(256, GAC_TILE_MINB) k_tile(ScoreArgs a) {
         for (int c0 = 0; c0 < C; c0 += 2 * kWave) {
             const ChunkRef ca = chunk_prep(L, c0 + lane);
             const ChunkRef cb = chunk_prep(L, c0 + kWave + lane);
-            const ChunkRaw ra = chunk_load(a, ca);
-            const ChunkRaw rb = chunk_load(a, cb);
+            const ChunkRaw ra = chunk_load<NT>(a, ca);
+            const ChunkRaw rb = chunk_load<NT>(a, cb);
             const int sa = chunk_eval<SYM>(a, ca, ra);
             const int sb = chunk_eval<SYM>(a, cb, rb);
             if (ca.n > 0) atomicAdd(&L.acc[ca.k], (unsigned long long)(long long)sa);
@@ -1129,7 +1182,7 @@ __global__ void __launch_bounds__(256) k_small(ScoreArgs a, const Range *rin, Sm
                 c.n = min(32, len - off);
                 c.tp = tpos + off;
                 c.qp = minus ? qpos - off - c.n : qpos + off;
-                bsc += chunk_eval<SYM>(a, c, chunk_load(a, c));
+                bsc += chunk_eval<SYM>(a, c, chunk_load<false>(a, c));
             }
             const int g = last ? 0 : bk.w;
             vg = bsc - g;
@@ -1318,19 +1371,30 @@ int persistent_blocks_per_cu(int which) {
     // (the symmetric and general variants differ by a few registers; size
     // for the general one)
     hipError_t e =
-        which == 0   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<false, false>, 256, 0)
-                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<true, false>, 256, 0);
+        which == 0   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<false, false, false>, 256, 0)
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<true, false, false>, 256, 0);
     return (e == hipSuccess && nb > 0) ? nb : 4;
 }
 
-hipError_t launch_tile(const ScoreArgs &a, int grid, hipStream_t s) {
+template <bool NT>
+static void launch_tile_t(const ScoreArgs &a, int grid, hipStream_t s) {
     if (a.want_local) {
-        if (a.sym) hipLaunchKernelGGL((k_tile<true, true>), dim3(grid), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((k_tile<true, false>), dim3(grid), dim3(256), 0, s, a);
+        if (a.sym) k_tile<true, true, NT><<<grid, 256, 0, s>>>(a);
+        else k_tile<true, false, NT><<<grid, 256, 0, s>>>(a);
     } else {
-        if (a.sym) hipLaunchKernelGGL((k_tile<false, true>), dim3(grid), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((k_tile<false, false>), dim3(grid), dim3(256), 0, s, a);
+        if (a.sym) k_tile<false, true, NT><<<grid, 256, 0, s>>>(a);
+        else k_tile<false, false, NT><<<grid, 256, 0, s>>>(a);
     }
+}
+
+hipError_t launch_tile(const ScoreArgs &a, int grid, hipStream_t s) {
+    // GAC_TILE_NT=1: non-temporal plane and block loads (tuning probe)
+    static const bool nt = [] {
+        const char *e = getenv("GAC_TILE_NT");
+        return e && e[0] == '1';
+    }();
+    if (nt) launch_tile_t<true>(a, grid, s);
+    else launch_tile_t<false>(a, grid, s);
     return hipGetLastError();
 }
 
@@ -1421,12 +1485,15 @@ hipError_t launch_build(const int32_t *bt, const int32_t *bq, const int32_t *bs,
 }
 
 hipError_t launch_nflags(const DChain *chains, int64_t n_chains, int4 *blk,
-                         const uint32_t *t_nmask, const int64_t *t_woff, const uint32_t *q_nmask,
-                         const int64_t *q_woff, hipStream_t s) {
-    if (n_chains == 0) return hipSuccess;
-    const int64_t waves = n_chains < 65536 ? n_chains : 65536;
-    hipLaunchKernelGGL(k_nflags, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, chains,
-                       n_chains, blk, t_nmask, t_woff, q_nmask, q_woff);
+                         const longlong2 *t_runs, int64_t n_trun, const uint32_t *t_nmask,
+                         const longlong2 *q_runs, int64_t n_qrun, const uint32_t *q_nmask,
+                         const int64_t *q_woff, int2 *list, int *count, hipStream_t s) {
+    if (n_chains == 0 || (n_trun == 0 && n_qrun == 0)) return hipSuccess;
+    hipMemsetAsync(count, 0, sizeof(int), s);
+    hipLaunchKernelGGL(k_nflags_chains, dim3((unsigned)((n_chains + 255) / 256)), dim3(256), 0, s,
+                       chains, n_chains, blk, t_runs, n_trun, q_runs, n_qrun, q_woff, list, count);
+    hipLaunchKernelGGL(k_nflags_blocks, dim3(1024), dim3(256), 0, s, chains, blk, t_nmask, q_nmask,
+                       q_woff, list, count);
     return hipGetLastError();
 }
 

@@ -524,6 +524,26 @@ void gac_kent_score_chains(struct chain *const *chains, int64_t n, struct axtSco
         global[i] = t_cache.score[cache_find(&t_cache, chains[i])];
 }
 
+/* the chain can go to the device: its sequences are loaded and its blocks
+ * ascend without overlap inside them (what gac_chains_upload accepts) */
+static int uploadable(gac_ctx *ctx, const struct chain *c) {
+    const int32_t ti = gac_genome_seq_index(ctx, GAC_T, c->tName);
+    const int32_t qi = gac_genome_seq_index(ctx, GAC_Q, c->qName);
+    if (ti < 0 || qi < 0)
+        return 0;
+    const int64_t tsize = gac_genome_seq_size(ctx, GAC_T, ti);
+    const int64_t qsize = gac_genome_seq_size(ctx, GAC_Q, qi);
+    int64_t pt = 0, pq = 0;
+    for (const struct cBlock *b = c->blockList; b; b = b->next) {
+        const int64_t z = (int64_t)b->tEnd - b->tStart;
+        if (z < 0 || b->tStart < pt || b->qStart < pq || b->tEnd > tsize || b->qStart + z > qsize)
+            return 0;
+        pt = b->tEnd;
+        pq = b->qStart + z;
+    }
+    return 1;
+}
+
 double chainCalcScore(struct chain *chain, struct axtScoreScheme *ss, struct gapCalc *gapCalc,
                       struct dnaSeq *query, struct dnaSeq *target) {
     (void)query, (void)target;
@@ -538,9 +558,12 @@ double chainCalcScore(struct chain *chain, struct axtScoreScheme *ss, struct gap
     struct chain **v = malloc((size_t)cap * sizeof(*v));
     gac_ctx *ctx = bound();
     for (struct chain *c = chain; c; c = c->next) {
-        if (!c->blockList || (c != chain && (gac_genome_seq_index(ctx, GAC_T, c->tName) < 0 ||
-                                             gac_genome_seq_index(ctx, GAC_Q, c->qName) < 0)))
-            continue; /* (only this chain's own sequences must be loaded) */
+        /* the rest of the list only where it can be scored as it stands (a
+         * list fresh from chainBlocks still holds overlapping blocks until
+         * chainRemovePartialOverlaps reaches each chain); this chain always,
+         * so that its problems are reported */
+        if (!c->blockList || (c != chain && !uploadable(ctx, c)))
+            continue;
         if (n == cap)
             v = realloc(v, (size_t)(cap *= 2) * sizeof(*v));
         v[n++] = c;
