@@ -524,6 +524,38 @@ void gac_kent_score_chains(struct chain *const *chains, int64_t n, struct axtSco
         global[i] = t_cache.score[cache_find(&t_cache, chains[i])];
 }
 
+/* chainConnect.c:42-59: the chain's blocks scored on caller text that
+ * starts at the chain's qStart / tStart (one batched device call), minus
+ * the gap costs */
+double chainCalcScoreSubChain(struct chain *chain, struct axtScoreScheme *ss,
+                              struct gapCalc *gapCalc, struct dnaSeq *query,
+                              struct dnaSeq *target) {
+    int64_t n = 0;
+    for (const struct cBlock *b = chain->blockList; b; b = b->next)
+        ++n;
+    if (!n)
+        return 0;
+    char **q = malloc((size_t)n * sizeof(char *)), **t = malloc((size_t)n * sizeof(char *));
+    int *z = malloc((size_t)n * sizeof(int));
+    double *sc = malloc((size_t)n * sizeof(double));
+    int64_t i = 0;
+    for (const struct cBlock *b = chain->blockList; b; b = b->next, ++i) {
+        q[i] = query->dna + (b->qStart - chain->qStart);
+        t[i] = target->dna + (b->tStart - chain->tStart);
+        z[i] = b->tEnd - b->tStart;
+    }
+    gac_kent_score_blocks(n, q, t, z, ss->matrix, sc);
+    double score = 0;
+    i = 0;
+    for (const struct cBlock *b = chain->blockList; b; b = b->next, ++i) {
+        score += sc[i];
+        if (b->next)
+            score -= gapCalcCost(gapCalc, b->next->qStart - b->qEnd, b->next->tStart - b->tEnd);
+    }
+    free(q), free(t), free(z), free(sc);
+    return score;
+}
+
 /* the chain can go to the device: its sequences are loaded and its blocks
  * ascend without overlap inside them (what gac_chains_upload accepts) */
 static int uploadable(gac_ctx *ctx, const struct chain *c) {

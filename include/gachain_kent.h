@@ -123,6 +123,10 @@ int gapCalcCost(struct gapCalc *gapCalc, int dq, int dt);
 
 double chainCalcScore(struct chain *chain, struct axtScoreScheme *ss, struct gapCalc *gapCalc,
                       struct dnaSeq *query, struct dnaSeq *target);
+/* chainConnect.h:41 -- query/target text starts at the chain's qStart/tStart */
+double chainCalcScoreSubChain(struct chain *chain, struct axtScoreScheme *ss,
+                              struct gapCalc *gapCalc, struct dnaSeq *query,
+                              struct dnaSeq *target);
 
 void chainSubsetOnT(struct chain *chain, int subStart, int subEnd, struct chain **retSubChain,
                     struct chain **retChainToFree);
