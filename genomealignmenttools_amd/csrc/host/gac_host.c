@@ -739,6 +739,23 @@ int gac_host_threads(void) {
     return n > 64 ? 64 : n;
 }
 
+void gac_mark(const char *what) {
+    static int on = -1;
+    static double t0;
+    if (on < 0) {
+        on = getenv("GAC_TIMING") != NULL;
+        struct timespec ts;
+        clock_gettime(CLOCK_MONOTONIC, &ts);
+        t0 = ts.tv_sec + 1e-9 * ts.tv_nsec;
+    }
+    if (!on)
+        return;
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    fprintf(stderr, "[mark] %8.3f %lx %s\n", ts.tv_sec + 1e-9 * ts.tv_nsec - t0,
+            (unsigned long)pthread_self() & 0xffff, what);
+}
+
 void gac_run_threads(int n, void *(*fn)(void *), void *arg) {
     if (n < 1)
         n = 1;

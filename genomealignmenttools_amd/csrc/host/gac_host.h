@@ -79,6 +79,9 @@ int gac_is_twobit_file(const char *path);
 
 /* ---- host threads: GAC_THREADS, else OMP_NUM_THREADS, else all cores (<= 64) */
 int gac_host_threads(void);
+/* GAC_TIMING: "[mark] <seconds since the first mark> <thread> <what>" on
+ * stderr (timelines of overlapped phases; no-op otherwise) */
+void gac_mark(const char *what);
 /* gap tables with the same content (as gapCalcCost sees them) */
 int gac_gapcalc_same(const gac_gapcalc *a, const gac_gapcalc *b);
 /* deep copy, freed with gac_gapcalc_free */

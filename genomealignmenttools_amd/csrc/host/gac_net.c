@@ -27,6 +27,7 @@
 #include <sys/mman.h>
 #include <stdatomic.h>
 #include <math.h>
+#include <stdarg.h>
 #include <stdio.h>
 #include <time.h>
 #include <stdlib.h>
@@ -50,8 +51,10 @@ struct ngap {
 struct nfill {
     int start, end, o_start, o_end;
     int32_t chain;
+    int32_t ali;  /* the chain's aligned bases inside [start, end) (chainBaseCountSub*) */
     ngap **gaps; /* ascending (created in block order at fill time) */
     int n_gaps;
+    int32_t full; /* the final [start, end) covers the chain's header span on this side */
     nfill *next;
     int64_t ord;  /* pre-order index on its side */
     ngap *pgap;   /* parent gap; index in pgap->fills; fills above this one */
@@ -152,7 +155,7 @@ struct gac_net {
     int32_t n_chroms[2];
     nwork *w;          /* [n_w]; w[0] also holds the finishNet arrays */
     int n_w;
-    int64_t *ali_prefix; /* per block prefix of sizes, per chain offset by blk_off */
+    int64_t *chain_ali; /* per chain: aligned bases (chainBaseCount) */
     /* pre-order fill index per side */
     nfill **order[2];
     int64_t n_order[2];
@@ -553,8 +556,11 @@ static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int32_t chai
         ngap *sgap = n->q[si].gap;
         while (k + 1 < nb && s[k + 1] <= sstart)
             ++k;
-        /* innerBounds (chainNet.c:356-391) */
+        /* innerBounds (chainNet.c:356-391), and the clipped blocks' bases:
+         * the fill's aligned bases, since no block of the chain lies in the
+         * space outside [start, end) */
         int start = BIGNUM, end = -BIGNUM;
+        int64_t ali = 0;
         for (int b = k; b < nb; ++b) {
             int bs = s[b], be = e[b];
             if (be <= sstart)
@@ -569,6 +575,7 @@ static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int32_t chai
                 start = bs;
             if (end < be)
                 end = be;
+            ali += be - bs;
         }
         if (end < 0 || end - start < net->opt.min_fill)
             continue;
@@ -577,6 +584,8 @@ static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int32_t chai
         f->start = start;
         f->end = end;
         f->chain = chain;
+        f->ali = (int32_t)ali;
+        f->full = 0; /* (set by fill_other_range, on the final bounds) */
         /* slAddHead onto the space's gap; region workers of one chromosome
          * side (net_regions) may share the gap, so the push is atomic.  The
          * order does not matter: finishNet sorts a gap's fills by start. */
@@ -783,6 +792,9 @@ static void fill_other_range(gac_net *n, nfill *f, int is_q) {
             if (tmin > ts) tmin = ts;
             if (tmax < te) tmax = te;
         }
+        /* the whole chain: subchainInfo's test (chainNet.c:802-823), in
+         * the chain's query coordinates */
+        f->full = qmin <= in->q_start[c] && qmax >= in->q_end[c];
         if (minus) {
             int t = qmin;
             qmin = qsize - qmax;
@@ -821,6 +833,7 @@ static void fill_other_range(gac_net *n, nfill *f, int is_q) {
         f->end = tmax;
         f->o_start = qmin;
         f->o_end = qmax;
+        f->full = tmin <= in->t_start[c] && tmax >= in->t_end[c];
     }
 }
 
@@ -927,7 +940,7 @@ void gac_net_free(gac_net *n) {
     free(n->chroms[1]);
     free(n->order[0]);
     free(n->order[1]);
-    free(n->ali_prefix);
+    free(n->chain_ali);
     free(n);
 }
 
@@ -1451,6 +1464,28 @@ static void *net_thread(void *arg) {
     return NULL;
 }
 
+typedef struct ca_job {
+    const gac_net_input *in;
+    int64_t *out;
+    _Atomic int64_t next;
+} ca_job;
+
+static void *chain_ali_thread(void *arg) {
+    ca_job *A = arg;
+    for (;;) {
+        const int64_t a = atomic_fetch_add(&A->next, 16384);
+        if (a >= A->in->n_chains)
+            return NULL;
+        const int64_t b = a + 16384 < A->in->n_chains ? a + 16384 : A->in->n_chains;
+        for (int64_t c = a; c < b; ++c) {
+            int64_t t = 0;
+            for (int64_t k = A->in->blk_off[c]; k < A->in->blk_off[c + 1]; ++k)
+                t += A->in->blk_size[k];
+            A->out[c] = t;
+        }
+    }
+}
+
 int gac_net_build(const gac_net_input *in, const gac_net_opts *opt, gac_net **out) {
     return gac_net_build_sides(in, opt, (1 << GAC_T) | (1 << GAC_Q), out);
 }
@@ -1711,14 +1746,13 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
     if (getenv("GAC_TIMING"))
         fprintf(stderr, "[gac_net_build] finishNet %.3f s\n",
                 (t_fin1.tv_sec - t_fin0.tv_sec) + 1e-9 * (t_fin1.tv_nsec - t_fin0.tv_nsec));
-    /* aligned-base prefix per block for chainBaseCount / SubT / SubQ */
-    n->ali_prefix = malloc((in->blk_off[in->n_chains] + 1) * sizeof(int64_t));
-    int64_t acc = 0;
-    for (int64_t b = 0; b < in->blk_off[in->n_chains]; ++b) {
-        n->ali_prefix[b] = acc;
-        acc += in->blk_size[b];
+    /* aligned bases per chain (chainBaseCount), in parallel over chains */
+    n->chain_ali = malloc((size_t)(in->n_chains ? in->n_chains : 1) * sizeof(int64_t));
+    {
+        ca_job A = {in, n->chain_ali, 0};
+        atomic_init(&A.next, 0);
+        gac_run_threads(gac_host_threads(), chain_ali_thread, &A);
     }
-    n->ali_prefix[in->blk_off[in->n_chains]] = acc;
     *out = n;
     return GAC_OK;
 }
@@ -1731,41 +1765,7 @@ int64_t gac_net_fill_count(const gac_net *n, int side) {
     return n->n_order[side];
 }
 
-/* aligned bases of chain c inside [s, e) on one side (chainBaseCountSubT/Q) */
-static int sub_size(const gac_net *n, int64_t c, int s, int e, int is_q) {
-    const gac_net_input *in = &n->in;
-    const int64_t b0 = in->blk_off[c];
-    const int nb = (int)(in->blk_off[c + 1] - b0);
-    const int32_t *st = (is_q ? in->blk_q : in->blk_t) + b0, *sz = in->blk_size + b0;
-    int lo = first_end_after(st, sz, nb, s);
-    /* first block with start >= e */
-    int a = lo, hi = nb;
-    while (a < hi) {
-        int mid = (a + hi) >> 1;
-        if (st[mid] >= e)
-            hi = mid;
-        else
-            a = mid + 1;
-    }
-    if (a <= lo)
-        return 0;
-    int64_t tot = n->ali_prefix[b0 + a] - n->ali_prefix[b0 + lo];
-    /* clip the first and last block */
-    int fs = st[lo], fe = st[lo] + sz[lo];
-    if (fs < s)
-        tot -= s - fs;
-    int ls = st[a - 1], le = st[a - 1] + sz[a - 1];
-    if (le > e)
-        tot -= le - e;
-    (void)fe;
-    (void)ls;
-    return (int)tot;
-}
-
-static int full_size(const gac_net *n, int64_t c) {
-    const gac_net_input *in = &n->in;
-    return (int)(n->ali_prefix[in->blk_off[c + 1]] - n->ali_prefix[in->blk_off[c]]);
-}
+static int full_size(const gac_net *n, int64_t c) { return (int)n->chain_ali[c]; }
 
 /* visibility of each fill: reached by rOutputFill and passing its filters
  * given the score rule; for the T side with rescore the score filter always
@@ -1784,7 +1784,6 @@ typedef struct gf_job {
 static void *fills_thread(void *arg) {
     gf_job *J = arg;
     const gac_net *n = J->n;
-    const gac_net_input *in = &n->in;
     const int side = J->side;
     for (;;) {
         const int64_t a = atomic_fetch_add(&J->next, 1) * J->per;
@@ -1793,21 +1792,9 @@ static void *fills_thread(void *arg) {
         const int64_t b = a + J->per < n->n_order[side] ? a + J->per : n->n_order[side];
         for (int64_t i = a; i < b; ++i) {
             const nfill *f = n->order[side][i];
-            int64_t c = f->chain;
-            int s = f->start, e = f->end;
-            int full, sz;
-            if (side == GAC_Q) {
-                if (in->q_strand[c]) {
-                    int qsize = in->q_sizes[in->q_seq[c]];
-                    int t = s;
-                    s = qsize - e;
-                    e = qsize - t;
-                }
-                full = (s <= in->q_start[c] && e >= in->q_end[c]);
-            } else {
-                full = (s <= in->t_start[c] && e >= in->t_end[c]);
-            }
-            sz = full ? full_size(n, c) : sub_size(n, c, s, e, side == GAC_Q);
+            const int64_t c = f->chain;
+            const int full = f->full;
+            const int sz = full ? full_size(n, c) : f->ali;
             if (J->chain)
                 J->chain[i] = (int32_t)c;
             if (J->start)
@@ -1861,7 +1848,9 @@ int gac_net_get_fills(const gac_net *n, int side, int32_t *chain, int32_t *start
     gf_job J = {n, side, chain, start, end, ali, flags, nf / (8 * (int64_t)nt) + 1, 0};
     atomic_init(&J.next, 0);
     const int64_t nrun = (nf + J.per - 1) / J.per;
+    gac_mark("get_fills: fills");
     gac_run_threads(nt < nrun ? nt : (int)(nrun ? nrun : 1), fills_thread, &J);
+    gac_mark("get_fills: visible");
     /* visibility: a fill is printed when its parent fill is and its own ali
      * >= min_fill -- one pass in pre-order (parents precede children), in
      * parallel over runs that start at top-level fills (whole subtrees) */
@@ -1869,6 +1858,7 @@ int gac_net_get_fills(const gac_net *n, int side, int32_t *chain, int32_t *start
         atomic_store(&J.next, 0);
         gac_run_threads(nt < nrun ? nt : (int)(nrun ? nrun : 1), visible_thread, &J);
     }
+    gac_mark("get_fills: done");
     return GAC_OK;
 }
 
@@ -1883,9 +1873,46 @@ typedef struct wmarks {
     int64_t n, cap;
 } wmarks;
 
+/* a run's text, formatted without stdio (one fwrite per run) */
+typedef struct obuf {
+    char *p;
+    size_t n, cap;
+} obuf;
+
+static char *ob_reserve(obuf *o, size_t k) {
+    if (o->n + k > o->cap) {
+        size_t c = o->cap ? 2 * o->cap : (size_t)1 << 16;
+        while (c < o->n + k)
+            c *= 2;
+        char *q = realloc(o->p, c);
+        if (!q) {
+            fprintf(stderr, "gac_net: out of memory formatting a net\n");
+            abort();
+        }
+        o->p = q;
+        o->cap = c;
+    }
+    return o->p + o->n;
+}
+
+static void ob_printf(obuf *o, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+static void ob_printf(obuf *o, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    const int k = vsnprintf(NULL, 0, fmt, ap);
+    va_end(ap);
+    if (k <= 0)
+        return;
+    char *p = ob_reserve(o, (size_t)k + 1);
+    va_start(ap, fmt);
+    vsnprintf(p, (size_t)k + 1, fmt, ap);
+    va_end(ap);
+    o->n += (size_t)k;
+}
+
 typedef struct wctx {
     const gac_net *n;
-    FILE *f;
+    obuf *o;
     int side;
     const int64_t *tscore; /* per T fill (pre-order), GPU-rescored partial scores */
     int depth;
@@ -1931,11 +1958,19 @@ static char *put_str(char *p, const char *s) {
     return p;
 }
 
-/* "%1.0f": integral values (all but the Q net's scaled scores) directly,
- * the rest through printf (round-half-even) */
+/* "%1.0f": printf rounds the double's exact value half to even, which is
+ * nearbyint in the default rounding mode (and "-0" for negatives that round
+ * to zero); beyond 1e15 through printf */
 static char *put_score(char *p, double v) {
-    if (v == (double)(int64_t)v && v > -1e15 && v < 1e15 && !(v == 0 && signbit(v)))
-        return put_int(p, (int64_t)v);
+    if (v > -1e15 && v < 1e15) {
+        const double r = nearbyint(v);
+        if (r == 0 && signbit(r)) {
+            *p++ = '-';
+            *p++ = '0';
+            return p;
+        }
+        return put_int(p, (int64_t)r);
+    }
     return p + sprintf(p, "%1.0f", v);
 }
 
@@ -1951,11 +1986,11 @@ static void put_gap_line(const wctx *w, const nfill *parent, const ngap *g, int 
     const int64_t c = parent->chain;
     const char *ochrom = w->side == GAC_Q ? in->t_names[in->t_seq[c]] : in->q_names[in->q_seq[c]];
     if (strlen(ochrom) > 400 || depth > 400) {
-        fprintf(w->f, "%*sgap %d %d %s %c %d %d\n", depth, "", g->start, g->end - g->start, ochrom,
-                in->q_strand[c] ? '-' : '+', g->o_start, g->o_end - g->o_start);
+        ob_printf(w->o, "%*sgap %d %d %s %c %d %d\n", depth, "", g->start, g->end - g->start,
+                  ochrom, in->q_strand[c] ? '-' : '+', g->o_start, g->o_end - g->o_start);
         return;
     }
-    char buf[512 + 400], *p = buf;
+    char *const buf = ob_reserve(w->o, 512 + 400), *p = buf;
     p = put_spaces(p, depth);
     p = put_str(p, "gap ");
     p = put_int(p, g->start);
@@ -1970,7 +2005,7 @@ static void put_gap_line(const wctx *w, const nfill *parent, const ngap *g, int 
     *p++ = ' ';
     p = put_int(p, g->o_end - g->o_start);
     *p++ = '\n';
-    fwrite(buf, 1, (size_t)(p - buf), w->f);
+    w->o->n += (size_t)(p - buf);
 }
 
 /* subchainInfo (chainNet.c:795-843) and rOutputFill's filter (:763-775):
@@ -1980,38 +2015,20 @@ static int fill_info(const gac_net *n, int side, const int64_t *tscore, const nf
                      double *score_out, int *sub_out) {
     const gac_net_input *in = &n->in;
     const int64_t c = f->chain;
-    int s = f->start, e = f->end;
     int sub;
     double score;
-    const int fullsz = full_size(n, c);
-    if (side == GAC_Q) {
-        if (in->q_strand[c]) {
-            int qsize = in->q_sizes[in->q_seq[c]];
-            int t = s;
-            s = qsize - e;
-            e = qsize - t;
-        }
-        if (s <= in->q_start[c] && e >= in->q_end[c]) {
-            score = in->score[c];
-            sub = fullsz;
-        } else {
-            sub = sub_size(n, c, s, e, 1);
-            score = in->score[c] * sub / fullsz;
-        }
+    if (f->full) { /* the whole chain */
+        score = in->score[c];
+        sub = full_size(n, c);
     } else {
-        if (s <= in->t_start[c] && e >= in->t_end[c]) {
-            score = in->score[c];
-            sub = fullsz;
+        sub = f->ali;
+        if (side == GAC_T && tscore == k_deferred) {
+            score = 1; /* placeholder: the fill's text gets the score later */
+        } else if (side == GAC_T && tscore) {
+            double r = (double)tscore[f->ord];
+            score = r <= 0 ? 1 : r; /* chainNet.c:244-245 */
         } else {
-            sub = sub_size(n, c, s, e, 0);
-            if (tscore == k_deferred) {
-                score = 1; /* placeholder: the fill's text gets the score later */
-            } else if (tscore) {
-                double r = (double)tscore[f->ord];
-                score = r <= 0 ? 1 : r; /* chainNet.c:244-245 */
-            } else {
-                score = in->score[c] * sub / fullsz;
-            }
+            score = in->score[c] * sub / full_size(n, c);
         }
     }
     *score_out = score;
@@ -2024,26 +2041,25 @@ static void put_fill_line(const wctx *w, const nfill *f, int depth, double score
     const gac_net_input *in = &w->n->in;
     const int64_t c = f->chain;
     const char *ochrom = w->side == GAC_Q ? in->t_names[in->t_seq[c]] : in->q_names[in->q_seq[c]];
-    const int deferred =
-        w->marks && w->side == GAC_T && !(f->start <= in->t_start[c] && f->end >= in->t_end[c]);
+    const int deferred = w->marks && w->side == GAC_T && !f->full;
     if (strlen(ochrom) > 400 || depth > 400 || !(score > -1e300 && score < 1e300)) {
-        fprintf(w->f, "%*sfill %d %d %s %c %d %d id %d score ", depth, "", f->start,
-                f->end - f->start, ochrom, in->q_strand[c] ? '-' : '+', f->o_start,
-                f->o_end - f->o_start, in->id[c]);
+        ob_printf(w->o, "%*sfill %d %d %s %c %d %d id %d score ", depth, "", f->start,
+                  f->end - f->start, ochrom, in->q_strand[c] ? '-' : '+', f->o_start,
+                  f->o_end - f->o_start, in->id[c]);
         if (deferred) {
             wmarks *m = w->marks;
             if (m->n == m->cap) {
                 m->cap = m->cap ? 2 * m->cap : 256;
                 m->m = realloc(m->m, (size_t)m->cap * sizeof(wmark));
             }
-            m->m[m->n++] = (wmark){(int64_t)ftell(w->f), f->ord};
+            m->m[m->n++] = (wmark){(int64_t)w->o->n, f->ord};
         } else {
-            fprintf(w->f, "%1.0f", score);
+            ob_printf(w->o, "%1.0f", score);
         }
-        fprintf(w->f, " ali %d\n", sub);
+        ob_printf(w->o, " ali %d\n", sub);
         return;
     }
-    char buf[512 + 400 + 400], *p = buf;
+    char *const buf = ob_reserve(w->o, 512 + 400 + 400), *p = buf;
     p = put_spaces(p, depth);
     p = put_str(p, "fill ");
     p = put_int(p, f->start);
@@ -2066,14 +2082,14 @@ static void put_fill_line(const wctx *w, const nfill *f, int depth, double score
             m->cap = m->cap ? 2 * m->cap : 256;
             m->m = realloc(m->m, (size_t)m->cap * sizeof(wmark));
         }
-        m->m[m->n++] = (wmark){(int64_t)ftell(w->f) + (p - buf), f->ord};
+        m->m[m->n++] = (wmark){(int64_t)w->o->n + (p - buf), f->ord};
     } else {
         p = put_score(p, score);
     }
     p = put_str(p, " ali ");
     p = put_int(p, sub);
     *p++ = '\n';
-    fwrite(buf, 1, (size_t)(p - buf), w->f);
+    w->o->n += (size_t)(p - buf);
 }
 
 /* Parallel output.  The .net text of a side is rOutputFill's depth-first
@@ -2112,7 +2128,7 @@ static void write_segment(const wjob *J, wctx *w, int64_t i) {
     const nfill *f = J->ord[i];
     if (!f->pgap->pfill && f->pidx == 0) { /* first top-level fill: the chromosome header */
         const nchrom *c = &J->n->chroms[J->side][f->pgap->pidx];
-        fprintf(w->f, "net %s %d\n", c->name, c->size);
+        ob_printf(w->o, "net %s %d\n", c->name, c->size);
     }
     if (!J->reached[i])
         return;
@@ -2141,9 +2157,31 @@ static void write_run(FILE *f, int64_t r, void *arg) {
     wjob *J = arg;
     const int64_t a = r * J->per;
     const int64_t b = a + J->per < J->nf ? a + J->per : J->nf;
-    wctx w = {J->n, f, J->side, J->tscore, 0, NULL, J->marks ? &J->marks[r] : NULL};
-    for (int64_t i = a; i < b; ++i)
+    obuf o = {NULL, 0, 0};
+    wctx w = {J->n, &o, J->side, J->tscore, 0, NULL, J->marks ? &J->marks[r] : NULL};
+    const gac_net_input *in = &J->n->in;
+    for (int64_t i = a; i < b; ++i) {
+        /* the fills are scattered over the netting arenas: fetch ahead */
+        if (i + 16 < b)
+            __builtin_prefetch(J->ord[i + 16]);
+        if (i + 8 < b) {
+            const nfill *f = J->ord[i + 8];
+            __builtin_prefetch(f->gaps);
+            __builtin_prefetch(&in->q_seq[f->chain]);
+            __builtin_prefetch(&in->q_strand[f->chain]);
+            __builtin_prefetch(&in->id[f->chain]);
+            __builtin_prefetch(&in->t_seq[f->chain]);
+        }
+        if (i + 4 < b) {
+            const nfill *f = J->ord[i + 4];
+            for (int k = 0; k < f->n_gaps && k < 4; ++k)
+                __builtin_prefetch(f->gaps[k]);
+        }
         write_segment(J, &w, i);
+    }
+    if (o.n)
+        fwrite_unlocked(o.p, 1, o.n, f);
+    free(o.p);
 }
 
 /* per-fill score / print flags (parallel over the pre-order list) */
@@ -2154,9 +2192,17 @@ static void *winfo_thread(void *arg) {
         if (a >= J->nf)
             break;
         const int64_t b = a + 4096 < J->nf ? a + 4096 : J->nf;
-        for (int64_t i = a; i < b; ++i)
+        for (int64_t i = a; i < b; ++i) {
+            if (i + 16 < b)
+                __builtin_prefetch(J->ord[i + 16]);
+            if (i + 8 < b) {
+                const int64_t c = J->ord[i + 8]->chain;
+                __builtin_prefetch(&J->n->in.score[c]);
+                __builtin_prefetch(&J->n->chain_ali[c]);
+            }
             J->show[i] = (uint8_t)fill_info(J->n, J->side, J->tscore, J->ord[i], &J->score[i],
                                             &J->sub[i]);
+        }
     }
     return NULL;
 }
@@ -2179,6 +2225,13 @@ static void *wmore_thread(void *arg) {
             break;
         const int64_t b = a + 4096 < J->nf ? a + 4096 : J->nf;
         for (int64_t i = a; i < b; ++i) {
+            if (i + 16 < b)
+                __builtin_prefetch(J->ord[i + 16]);
+            if (i + 8 < b) {
+                const nfill *p = J->ord[i + 8];
+                for (int k = 0; k < p->n_gaps && k < 4; ++k)
+                    __builtin_prefetch(p->gaps[k]);
+            }
             const nfill *f = J->ord[i];
             for (int k = 0; k < f->n_gaps; ++k)
                 mark_more(J, f->gaps[k]);
@@ -2189,6 +2242,25 @@ static void *wmore_thread(void *arg) {
 
 static int net_write_f(const gac_net *n, int side, const int64_t *tscores, FILE *f,
                        const char *const *meta, int32_t n_meta);
+
+/* "reached" flags: a fill prints when it passes and every ancestor fill
+ * prints; parents precede children in pre-order, so runs that start at
+ * top-level fills (whole subtrees) are independent */
+static void *wreached_thread(void *arg) {
+    wjob *J = arg;
+    const int64_t per = J->nf / (8 * (int64_t)gac_host_threads()) + 1;
+    for (;;) {
+        const int64_t r = atomic_fetch_add(&J->next, 1);
+        if (r * per >= J->nf)
+            return NULL;
+        const int64_t a = next_top_level(J->n, J->side, r * per);
+        const int64_t b = next_top_level(J->n, J->side, (r + 1) * per < J->nf ? (r + 1) * per : J->nf);
+        for (int64_t i = a; i < b; ++i) {
+            const nfill *pf = J->ord[i]->pgap->pfill;
+            J->reached[i] = J->show[i] && (!pf || J->reached[pf->ord]);
+        }
+    }
+}
 
 int gac_net_write(const gac_net *n, int side, const int64_t *tscores, const char *path,
                   const char *const *meta, int32_t n_meta) {
@@ -2247,17 +2319,19 @@ static void wjob_flags(wjob *J, const gac_net *n, int side, const int64_t *tscor
     const int nt = gac_host_threads();
     atomic_init(&J->next, 0);
     gac_run_threads(nt, winfo_thread, J);
+    gac_mark("flags: info done");
     atomic_store(&J->next, 0);
     gac_run_threads(nt, wmore_thread, J);
+    gac_mark("flags: more done");
     for (int32_t k = 0; k < n->n_chroms[side]; ++k) {
         const nchrom *c = &n->chroms[side][k];
         if (c->root && c->root->fill_head)
             mark_more(J, c->root);
     }
-    for (int64_t i = 0; i < nf; ++i) { /* parents precede children */
-        const nfill *f = J->ord[i];
-        J->reached[i] = J->show[i] && (!f->pgap->pfill || J->reached[f->pgap->pfill->ord]);
-    }
+    gac_mark("flags: roots done");
+    atomic_store(&J->next, 0);
+    gac_run_threads(nt, wreached_thread, J);
+    gac_mark("flags: reached done");
     /* (runs of 1/64 of a thread's share: capping them at 128 or 1024 fills
      * as for chains made the C5 nets slower, 1.79-1.86 / 1.36 vs 1.31-1.34
      * s; scripts/gpu_net_runs_ab.sh) */
@@ -2280,10 +2354,13 @@ static int net_write_f(const gac_net *n, int side, const int64_t *tscores, FILE 
     for (int32_t i = 0; i < n_meta; ++i)
         fprintf(f, "%s\n", meta[i]);
     wjob J;
+    gac_mark(side ? "net_write q: flags" : "net_write t: flags");
     wjob_flags(&J, n, side, tscores);
+    gac_mark(side ? "net_write q: format+write" : "net_write t: format+write");
     const int64_t nr = (J.nf + J.per - 1) / J.per;
     int wbad = gac_par_output(f, nr, write_run, &J);
     wjob_free_flags(&J);
+    gac_mark(side ? "net_write q: done" : "net_write t: done");
     return (ferror(f) || wbad) ? GAC_E_IO : GAC_OK;
 }
 
@@ -2312,11 +2389,14 @@ int gac_net_write_begin(const gac_net *n, int side, const char *const *meta, int
     for (int32_t i = 0; i < n_meta; ++i)
         P->meta[i] = strdup(meta[i]);
     P->n_meta = n_meta;
+    gac_mark("write_begin t: flags");
     wjob_flags(&P->J, n, side, k_deferred);
+    gac_mark("write_begin t: format");
     P->nr = (P->J.nf + P->J.per - 1) / P->J.per;
     P->J.marks = calloc((size_t)(P->nr > 0 ? P->nr : 1), sizeof(wmarks));
     const int bad = gac_par_format(P->nr, write_run, &P->J, &P->bufs, &P->lens);
     wjob_free_flags(&P->J);
+    gac_mark("write_begin t: done");
     if (bad) {
         gac_net_write_free(P);
         return gac_fail(GAC_E_IO, "gac_net_write_begin: out of memory");
@@ -2333,13 +2413,13 @@ static void wpre_run(FILE *f, int64_t r, void *arg) {
     int64_t last = 0;
     char tmp[64];
     for (int64_t k = 0; k < m->n; ++k) {
-        fwrite(buf + last, 1, (size_t)(m->m[k].pos - last), f);
+        fwrite_unlocked(buf + last, 1, (size_t)(m->m[k].pos - last), f);
         const double v = (double)P->tscores[m->m[k].ord];
         const char *e = put_score(tmp, v <= 0 ? 1 : v); /* chainNet.c:244-245 */
-        fwrite(tmp, 1, (size_t)(e - tmp), f);
+        fwrite_unlocked(tmp, 1, (size_t)(e - tmp), f);
         last = m->m[k].pos;
     }
-    fwrite(buf + last, 1, P->lens[r] - (size_t)last, f);
+    fwrite_unlocked(buf + last, 1, P->lens[r] - (size_t)last, f);
 }
 
 int gac_net_write_end(gac_net_wpre *P, const int64_t *tscores, FILE *f) {
@@ -2348,9 +2428,12 @@ int gac_net_write_end(gac_net_wpre *P, const int64_t *tscores, FILE *f) {
     for (int32_t i = 0; i < P->n_meta; ++i)
         fprintf(f, "%s\n", P->meta[i]);
     P->tscores = tscores;
+    gac_mark("write_end t: insert+write");
     const int wbad = gac_par_output(f, P->nr, wpre_run, P);
     const int bad = ferror(f) || wbad || fflush(f) != 0;
+    gac_mark("write_end t: free");
     gac_net_write_free(P);
+    gac_mark("write_end t: done");
     return bad ? gac_fail(GAC_E_IO, "write error") : GAC_OK;
 }
 

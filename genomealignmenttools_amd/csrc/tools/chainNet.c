@@ -523,6 +523,7 @@ int main(int argc, char *argv[]) {
         gac_range *r = malloc((nf ? nf : 1) * sizeof(gac_range));
         int64_t *rix = malloc((nf ? nf : 1) * 8);
         int64_t nr = 0;
+        gac_mark("fill list: ranges");
         for (int64_t i = 0; i < nf; ++i)
             if ((fl[i] & 3) == 3) { /* partial and printed */
                 r[nr].chain = fc[i];
@@ -540,8 +541,10 @@ int main(int argc, char *argv[]) {
             if (!df || (nr && fwrite(r, sizeof(gac_range), nr, df) != (size_t)nr) || fclose(df) != 0)
                 gt_abort("can't write %s", dump);
         }
+        gac_mark("fill list: join upload");
         if (pu.started)
             gt_helper_join(pu.th);
+        gac_mark("fill list: joined");
         if (pu.cs && pu.remap) { /* -nranks: the uploaded subset's indices */
             int ok = 1;
             for (int64_t k = 0; k < nr && ok; ++k)

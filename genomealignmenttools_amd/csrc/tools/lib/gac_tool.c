@@ -13,6 +13,7 @@
 #include <signal.h>
 #include <sys/stat.h>
 #include <unistd.h>
+#include <sys/syscall.h>
 #include <pthread.h>
 #include <stdatomic.h>
 #include <time.h>
@@ -29,7 +30,20 @@ void gt_on_abort(void (*fn)(void)) { g_abort_hook = fn; }
 static int g_gpu; /* device index for gt_device_start */
 void gt_set_gpu(int gpu) { g_gpu = gpu; }
 
+/* One thread aborts the process; a helper that aborts too ends itself (so
+ * that joins of it return), the main thread waits for the exit. */
+static atomic_int g_aborting;
+
+static void abort_second(void) {
+    if (syscall(SYS_gettid) == getpid())
+        for (;;)
+            pause();
+    pthread_exit(NULL);
+}
+
 void gt_abort(const char *fmt, ...) {
+    if (atomic_exchange(&g_aborting, 1))
+        abort_second();
     va_list ap;
     void (*hook)(void) = g_abort_hook;
     g_abort_hook = NULL; /* (a failing hook must not recurse) */
@@ -557,6 +571,8 @@ void gt_device_close_join(gt_device *d) {
 
 void gt_exit_ok(void) {
     join_live_device();
+    if (atomic_load(&g_aborting)) /* a helper is aborting: its exit status wins */
+        abort_second();
     if (g_verbose >= 2 || getenv("GAC_TIMING")) { /* the last wall-clock anchor */
         struct timespec rt;
         clock_gettime(CLOCK_REALTIME, &rt);
