@@ -308,6 +308,40 @@ static int assign_range(const gt_sizes *sz, uint8_t *keep, gt_names *kept) {
     return any;
 }
 
+/* chainNet's per-chain checks (score order, names in the sizes files, sizes
+ * agree): q/t sequence indices of every chain, the first failing chain */
+typedef struct check_job {
+    const gt_chains *c;
+    const gt_sizes *ts, *qs;
+    int32_t *tix, *qix;
+    int64_t n;
+    _Atomic int64_t next, first_bad;
+} check_job;
+
+static void *check_thread(void *arg) {
+    check_job *J = arg;
+    const gt_chains *c = J->c;
+    for (;;) {
+        const int64_t a = atomic_fetch_add(&J->next, 65536);
+        if (a >= J->n)
+            return NULL;
+        const int64_t b = a + 65536 < J->n ? a + 65536 : J->n;
+        for (int64_t i = a; i < b; ++i) {
+            int ok = i == 0 || c->score[i - 1] < 0 || c->score[i] <= c->score[i - 1];
+            J->qix[i] = gt_names_find(&J->qs->names, c->qnames.names[c->qname[i]]);
+            J->tix[i] = gt_names_find(&J->ts->names, c->tnames.names[c->tname[i]]);
+            ok = ok && J->qix[i] >= 0 && J->qs->size[J->qix[i]] == c->qsize[i] && J->tix[i] >= 0 &&
+                 J->ts->size[J->tix[i]] == c->tsize[i];
+            if (!ok) {
+                int64_t cur = atomic_load(&J->first_bad);
+                while (i < cur && !atomic_compare_exchange_weak(&J->first_bad, &cur, i)) {
+                }
+                break; /* later chains of this run cannot come first */
+            }
+        }
+    }
+}
+
 int main(int argc, char *argv[]) {
     gt_stage("");
     int min_space = 25;
@@ -421,24 +455,29 @@ int main(int argc, char *argv[]) {
         gt_read_chains(chain_file, &c, min_score, 1);
     gt_stage("read chains");
     int32_t *tix = malloc((c.n ? c.n : 1) * 4), *qix = malloc((c.n ? c.n : 1) * 4);
-    double last = -1;
-    for (int64_t i = 0; i < c.n; ++i) {
-        if (last >= 0 && c.score[i] > last)
-            gt_abort("%s must be sorted in order of score", chain_file);
-        last = c.score[i];
-        const char *qn = c.qnames.names[c.qname[i]], *tn = c.tnames.names[c.tname[i]];
-        qix[i] = gt_names_find(&qs.names, qn);
-        if (qix[i] < 0)
-            gt_abort("hashMustFindVal: '%s' not found", qn);
-        if (qs.size[qix[i]] != c.qsize[i])
-            gt_abort("%s is %d in %s but %d in %s", qn, c.qsize[i], chain_file, qs.size[qix[i]],
-                     qsizes_file);
-        tix[i] = gt_names_find(&ts.names, tn);
-        if (tix[i] < 0)
-            gt_abort("hashMustFindVal: '%s' not found", tn);
-        if (ts.size[tix[i]] != c.tsize[i])
+    {
+        /* in parallel; the first failing chain in file order is re-checked
+         * serially for its message */
+        check_job cj = {&c, &ts, &qs, tix, qix, c.n, 0};
+        atomic_init(&cj.next, 0);
+        atomic_init(&cj.first_bad, c.n);
+        gac_run_threads(gt_threads(), check_thread, &cj);
+        const int64_t bad = atomic_load(&cj.first_bad);
+        if (bad < c.n) {
+            const int64_t i = bad;
+            if (i > 0 && c.score[i - 1] >= 0 && c.score[i] > c.score[i - 1])
+                gt_abort("%s must be sorted in order of score", chain_file);
+            const char *qn = c.qnames.names[c.qname[i]], *tn = c.tnames.names[c.tname[i]];
+            if (qix[i] < 0)
+                gt_abort("hashMustFindVal: '%s' not found", qn);
+            if (qs.size[qix[i]] != c.qsize[i])
+                gt_abort("%s is %d in %s but %d in %s", qn, c.qsize[i], chain_file,
+                         qs.size[qix[i]], qsizes_file);
+            if (tix[i] < 0)
+                gt_abort("hashMustFindVal: '%s' not found", tn);
             gt_abort("%s is %d in %s but %d in %s", tn, c.tsize[i], chain_file, ts.size[tix[i]],
                      tsizes_file);
+        }
     }
     gt_stage("chain checks");
     runs_job rj = {&runs, &c, tnib, qnib};

@@ -162,6 +162,19 @@ def test_tool_errors(tmp_path):
     r = subprocess.run([cn, str(bad), os.path.join(d, "t.sizes"), os.path.join(d, "q.sizes"),
                         "/dev/null", "/dev/null"], capture_output=True, text=True)
     assert r.returncode == 255 and "must be sorted in order of score" in r.stderr
+    # sizes files that disagree with the chains (checked in parallel; the
+    # first failing chain in file order reports, as chainNet.c does)
+    qs = open(os.path.join(d, "q.sizes")).read()
+    for name, text, msg in (("qbad", qs.replace("150000", "150001"),
+                             "chrQ1 is 150000 in {c} but 150001 in {s}"),
+                            ("qmiss", "".join(x for x in qs.splitlines(True) if "chrQ2" not in x),
+                             "hashMustFindVal: 'chrQ2' not found")):
+        sz = tmp_path / f"{name}.sizes"
+        sz.write_text(text)
+        ch = os.path.join(d, "in.chain")
+        r = subprocess.run([cn, ch, os.path.join(d, "t.sizes"), str(sz), "/dev/null",
+                            "/dev/null"], capture_output=True, text=True)
+        assert r.returncode == 255 and msg.format(c=ch, s=sz) in r.stderr, r.stderr
     r = subprocess.run([cn, os.path.join(d, "in.chain"), os.path.join(d, "t.sizes"),
                         os.path.join(d, "q.sizes"), "/dev/null", "/dev/null", "-rescore"],
                        capture_output=True, text=True)
