@@ -769,9 +769,59 @@ void gac_run_threads(int n, void *(*fn)(void *), void *arg) {
 }
 
 /* ------------------------------------------------------------ output */
+FILE *gac_open_output(const char *path) {
+    const int fd = open(path, O_WRONLY | O_CREAT | O_CLOEXEC, 0666);
+    if (fd < 0)
+        return NULL;
+    FILE *f = fdopen(fd, "w");
+    if (!f)
+        close(fd);
+    return f;
+}
+
+int gac_close_output(FILE *f) {
+    int bad = fflush(f) != 0;
+    const off_t end = ftello(f);
+    struct stat st;
+    if (!bad && end >= 0 && fstat(fileno(f), &st) == 0 && S_ISREG(st.st_mode) && st.st_size > end)
+        bad = ftruncate(fileno(f), end) != 0;
+    return (fclose(f) != 0 || bad) ? EOF : 0;
+}
+
+char *gac_obuf_reserve(gac_obuf *o, size_t k) {
+    if (o->n + k > o->cap) {
+        size_t c = o->cap ? 2 * o->cap : (size_t)1 << 16;
+        while (c < o->n + k)
+            c *= 2;
+        char *q = realloc(o->p, c);
+        if (!q) {
+            fprintf(stderr, "out of memory formatting output\n");
+            abort();
+        }
+        o->p = q;
+        o->cap = c;
+    }
+    return o->p + o->n;
+}
+
+void gac_obuf_printf(gac_obuf *o, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    const int k = vsnprintf(NULL, 0, fmt, ap);
+    va_end(ap);
+    if (k <= 0)
+        return;
+    char *p = gac_obuf_reserve(o, (size_t)k + 1);
+    va_start(ap, fmt);
+    vsnprintf(p, (size_t)k + 1, fmt, ap);
+    va_end(ap);
+    o->n += (size_t)k;
+}
+
 typedef struct po_job {
     int64_t nr;
     void (*fn)(FILE *, int64_t, void *);
+    void (*fn_buf)(gac_obuf *, int64_t, void *);
     void *arg;
     char **buf;
     size_t *len;
@@ -786,6 +836,14 @@ static void *po_thread(void *p) {
         const int64_t r = atomic_fetch_add(&J->next, 1);
         if (r >= J->nr)
             break;
+        if (J->fn_buf) {
+            gac_obuf o = {NULL, 0, 0};
+            J->fn_buf(&o, r, J->arg);
+            J->buf[r] = o.p;
+            J->len[r] = o.n;
+            atomic_store_explicit(&J->ready[r], 1, memory_order_release);
+            continue;
+        }
         FILE *f = open_memstream(&J->buf[r], &J->len[r]);
         if (!f) {
             atomic_store(&J->oom, 1);
@@ -799,11 +857,13 @@ static void *po_thread(void *p) {
 }
 
 /* the same runs formatted in parallel but kept: bufs[r] / lens[r] (malloc'd) */
-int gac_par_format(int64_t nr, void (*fn)(FILE *f, int64_t r, void *arg), void *arg, char ***bufs,
-                   size_t **lens) {
+static int par_format(int64_t nr, void (*fn)(FILE *f, int64_t r, void *arg),
+                      void (*fn_buf)(gac_obuf *o, int64_t r, void *arg), void *arg, char ***bufs,
+                      size_t **lens) {
     po_job J;
     J.nr = nr;
     J.fn = fn;
+    J.fn_buf = fn_buf;
     J.arg = arg;
     J.buf = calloc((size_t)(nr > 0 ? nr : 1), sizeof(char *));
     J.len = calloc((size_t)(nr > 0 ? nr : 1), sizeof(size_t));
@@ -959,12 +1019,24 @@ static void wait_ready(_Atomic int *flag) {
         usleep(20);
 }
 
-int gac_par_output(FILE *out, int64_t nr, void (*fn)(FILE *f, int64_t r, void *arg), void *arg) {
+int gac_par_format(int64_t nr, void (*fn)(FILE *f, int64_t r, void *arg), void *arg, char ***bufs,
+                   size_t **lens) {
+    return par_format(nr, fn, NULL, arg, bufs, lens);
+}
+
+int gac_par_format_buf(int64_t nr, void (*fn)(gac_obuf *o, int64_t r, void *arg), void *arg,
+                       char ***bufs, size_t **lens) {
+    return par_format(nr, NULL, fn, arg, bufs, lens);
+}
+
+static int par_output(FILE *out, int64_t nr, void (*fn)(FILE *f, int64_t r, void *arg),
+                      void (*fn_buf)(gac_obuf *o, int64_t r, void *arg), void *arg) {
     if (nr <= 0)
         return 0;
     po_job J;
     J.nr = nr;
     J.fn = fn;
+    J.fn_buf = fn_buf;
     J.arg = arg;
     J.buf = calloc((size_t)nr, sizeof(char *));
     J.len = calloc((size_t)nr, sizeof(size_t));
@@ -1051,4 +1123,13 @@ int gac_par_output(FILE *out, int64_t nr, void (*fn)(FILE *f, int64_t r, void *a
     free(J.len);
     free((void *)J.ready);
     return (bad || atomic_load(&J.oom)) ? -1 : 0;
+}
+
+int gac_par_output(FILE *out, int64_t nr, void (*fn)(FILE *f, int64_t r, void *arg), void *arg) {
+    return par_output(out, nr, fn, NULL, arg);
+}
+
+int gac_par_output_buf(FILE *out, int64_t nr, void (*fn)(gac_obuf *o, int64_t r, void *arg),
+                       void *arg) {
+    return par_output(out, nr, NULL, fn, arg);
 }

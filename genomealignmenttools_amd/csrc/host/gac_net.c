@@ -1873,46 +1873,9 @@ typedef struct wmarks {
     int64_t n, cap;
 } wmarks;
 
-/* a run's text, formatted without stdio (one fwrite per run) */
-typedef struct obuf {
-    char *p;
-    size_t n, cap;
-} obuf;
-
-static char *ob_reserve(obuf *o, size_t k) {
-    if (o->n + k > o->cap) {
-        size_t c = o->cap ? 2 * o->cap : (size_t)1 << 16;
-        while (c < o->n + k)
-            c *= 2;
-        char *q = realloc(o->p, c);
-        if (!q) {
-            fprintf(stderr, "gac_net: out of memory formatting a net\n");
-            abort();
-        }
-        o->p = q;
-        o->cap = c;
-    }
-    return o->p + o->n;
-}
-
-static void ob_printf(obuf *o, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
-static void ob_printf(obuf *o, const char *fmt, ...) {
-    va_list ap;
-    va_start(ap, fmt);
-    const int k = vsnprintf(NULL, 0, fmt, ap);
-    va_end(ap);
-    if (k <= 0)
-        return;
-    char *p = ob_reserve(o, (size_t)k + 1);
-    va_start(ap, fmt);
-    vsnprintf(p, (size_t)k + 1, fmt, ap);
-    va_end(ap);
-    o->n += (size_t)k;
-}
-
 typedef struct wctx {
     const gac_net *n;
-    obuf *o;
+    gac_obuf *o;
     int side;
     const int64_t *tscore; /* per T fill (pre-order), GPU-rescored partial scores */
     int depth;
@@ -1986,11 +1949,11 @@ static void put_gap_line(const wctx *w, const nfill *parent, const ngap *g, int 
     const int64_t c = parent->chain;
     const char *ochrom = w->side == GAC_Q ? in->t_names[in->t_seq[c]] : in->q_names[in->q_seq[c]];
     if (strlen(ochrom) > 400 || depth > 400) {
-        ob_printf(w->o, "%*sgap %d %d %s %c %d %d\n", depth, "", g->start, g->end - g->start,
+        gac_obuf_printf(w->o, "%*sgap %d %d %s %c %d %d\n", depth, "", g->start, g->end - g->start,
                   ochrom, in->q_strand[c] ? '-' : '+', g->o_start, g->o_end - g->o_start);
         return;
     }
-    char *const buf = ob_reserve(w->o, 512 + 400), *p = buf;
+    char *const buf = gac_obuf_reserve(w->o, 512 + 400), *p = buf;
     p = put_spaces(p, depth);
     p = put_str(p, "gap ");
     p = put_int(p, g->start);
@@ -2043,7 +2006,7 @@ static void put_fill_line(const wctx *w, const nfill *f, int depth, double score
     const char *ochrom = w->side == GAC_Q ? in->t_names[in->t_seq[c]] : in->q_names[in->q_seq[c]];
     const int deferred = w->marks && w->side == GAC_T && !f->full;
     if (strlen(ochrom) > 400 || depth > 400 || !(score > -1e300 && score < 1e300)) {
-        ob_printf(w->o, "%*sfill %d %d %s %c %d %d id %d score ", depth, "", f->start,
+        gac_obuf_printf(w->o, "%*sfill %d %d %s %c %d %d id %d score ", depth, "", f->start,
                   f->end - f->start, ochrom, in->q_strand[c] ? '-' : '+', f->o_start,
                   f->o_end - f->o_start, in->id[c]);
         if (deferred) {
@@ -2054,12 +2017,12 @@ static void put_fill_line(const wctx *w, const nfill *f, int depth, double score
             }
             m->m[m->n++] = (wmark){(int64_t)w->o->n, f->ord};
         } else {
-            ob_printf(w->o, "%1.0f", score);
+            gac_obuf_printf(w->o, "%1.0f", score);
         }
-        ob_printf(w->o, " ali %d\n", sub);
+        gac_obuf_printf(w->o, " ali %d\n", sub);
         return;
     }
-    char *const buf = ob_reserve(w->o, 512 + 400 + 400), *p = buf;
+    char *const buf = gac_obuf_reserve(w->o, 512 + 400 + 400), *p = buf;
     p = put_spaces(p, depth);
     p = put_str(p, "fill ");
     p = put_int(p, f->start);
@@ -2128,7 +2091,7 @@ static void write_segment(const wjob *J, wctx *w, int64_t i) {
     const nfill *f = J->ord[i];
     if (!f->pgap->pfill && f->pidx == 0) { /* first top-level fill: the chromosome header */
         const nchrom *c = &J->n->chroms[J->side][f->pgap->pidx];
-        ob_printf(w->o, "net %s %d\n", c->name, c->size);
+        gac_obuf_printf(w->o, "net %s %d\n", c->name, c->size);
     }
     if (!J->reached[i])
         return;
@@ -2153,12 +2116,11 @@ static void write_segment(const wjob *J, wctx *w, int64_t i) {
     }
 }
 
-static void write_run(FILE *f, int64_t r, void *arg) {
+static void write_run(gac_obuf *o, int64_t r, void *arg) {
     wjob *J = arg;
     const int64_t a = r * J->per;
     const int64_t b = a + J->per < J->nf ? a + J->per : J->nf;
-    obuf o = {NULL, 0, 0};
-    wctx w = {J->n, &o, J->side, J->tscore, 0, NULL, J->marks ? &J->marks[r] : NULL};
+    wctx w = {J->n, o, J->side, J->tscore, 0, NULL, J->marks ? &J->marks[r] : NULL};
     const gac_net_input *in = &J->n->in;
     for (int64_t i = a; i < b; ++i) {
         /* the fills are scattered over the netting arenas: fetch ahead */
@@ -2179,9 +2141,6 @@ static void write_run(FILE *f, int64_t r, void *arg) {
         }
         write_segment(J, &w, i);
     }
-    if (o.n)
-        fwrite_unlocked(o.p, 1, o.n, f);
-    free(o.p);
 }
 
 /* per-fill score / print flags (parallel over the pre-order list) */
@@ -2274,14 +2233,15 @@ int gac_net_write(const gac_net *n, int side, const int64_t *tscores, const char
         f = stdout;
         close_it = 0;
     } else {
-        f = fopen(path, "w");
+        f = gac_open_output(path);
         if (!f)
             return gac_fail(GAC_E_IO, "Can't open %s to write", path);
     }
     int bad = net_write_f(n, side, tscores, f, meta, n_meta) != GAC_OK;
     if (close_it) {
-        if (fclose(f) != 0)
+        if (gac_close_output(f) != 0)
             bad = 1;
+        gac_mark(side ? "net_write q: closed" : "net_write t: closed");
     } else {
         fflush(f);
     }
@@ -2358,7 +2318,7 @@ static int net_write_f(const gac_net *n, int side, const int64_t *tscores, FILE 
     wjob_flags(&J, n, side, tscores);
     gac_mark(side ? "net_write q: format+write" : "net_write t: format+write");
     const int64_t nr = (J.nf + J.per - 1) / J.per;
-    int wbad = gac_par_output(f, nr, write_run, &J);
+    int wbad = gac_par_output_buf(f, nr, write_run, &J);
     wjob_free_flags(&J);
     gac_mark(side ? "net_write q: done" : "net_write t: done");
     return (ferror(f) || wbad) ? GAC_E_IO : GAC_OK;
@@ -2394,7 +2354,7 @@ int gac_net_write_begin(const gac_net *n, int side, const char *const *meta, int
     gac_mark("write_begin t: format");
     P->nr = (P->J.nf + P->J.per - 1) / P->J.per;
     P->J.marks = calloc((size_t)(P->nr > 0 ? P->nr : 1), sizeof(wmarks));
-    const int bad = gac_par_format(P->nr, write_run, &P->J, &P->bufs, &P->lens);
+    const int bad = gac_par_format_buf(P->nr, write_run, &P->J, &P->bufs, &P->lens);
     wjob_free_flags(&P->J);
     gac_mark("write_begin t: done");
     if (bad) {

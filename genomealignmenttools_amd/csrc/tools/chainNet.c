@@ -106,9 +106,9 @@ static void *write_net(void *arg) {
         }
     }
     if (w->pre && g_rk.n <= 1) {
-        FILE *f = strcmp(w->path, "stdout") ? fopen(w->path, "w") : stdout;
+        FILE *f = strcmp(w->path, "stdout") ? gac_open_output(w->path) : stdout;
         w->rc = f ? write_pre(w, f) : GAC_E_IO;
-        if (f && f != stdout && fclose(f) != 0 && w->rc == GAC_OK)
+        if (f && f != stdout && gac_close_output(f) != 0 && w->rc == GAC_OK)
             w->rc = GAC_E_IO;
         if (w->rc != GAC_OK)
             snprintf(w->err, sizeof(w->err), "write error on %s", w->path);
@@ -537,8 +537,13 @@ int main(int argc, char *argv[]) {
     gt_verbose(1, "writing %s\n", tnet);
     gt_verbose(1, "writing %s\n", qnet);
     net_out wo[2] = {{net, GAC_T, NULL, tnet, &c, 0, 0}, {net, GAC_Q, NULL, qnet, &c, 0, 0}};
-    const char *pf = getenv("GAC_NET_PREFORMAT"); /* 0: off (measurement knob) */
-    if (rescore && !(pf && *pf == '0')) { /* the target net's text is formatted while the GPU rescores */
+    /* GAC_NET_PREFORMAT=1 (measurement knob): the target net's text is
+     * formatted while the GPU rescores and the scores inserted afterwards.
+     * Off by default: the rescoring takes ~25 ms at C5, and holding the
+     * whole preformatted net to insert the scores cost more (1.16 s from the
+     * flags to the written net vs ~0.5 s streaming, r03e) */
+    const char *pf = getenv("GAC_NET_PREFORMAT");
+    if (rescore && pf && *pf == '1') {
         wo[0].pre_started = pthread_create(&wo[0].pre_th, NULL, pre_net, &wo[0]) == 0;
         if (wo[0].pre_started)
             gt_helper_add(wo[0].pre_th);
@@ -699,8 +704,10 @@ int main(int argc, char *argv[]) {
     }
     wo[0].tscores = tscores;
     write_net(&wo[0]);
+    gac_mark("target net written");
     if (wo[1].threaded)
         gt_helper_join(qth);
+    gac_mark("query net joined");
     for (int k = 0; k < 2; ++k)
         if (wo[k].rc != GAC_OK)
             gt_abort("%s\n", wo[k].err);
