@@ -48,9 +48,9 @@ hipError_t launch_gap_table(const GapDev &g, const int32_t *small, int len, int3
 hipError_t launch_block_gaps(const DChain *chains, int64_t n_chains, int4 *blk, const GapDev &g,
                              const int32_t *small, const int32_t *tab, int len, hipStream_t s);
 hipError_t launch_nflags(const DChain *chains, int64_t n_chains, int4 *blk,
-                         const longlong2 *t_runs, int64_t n_trun, const uint32_t *t_nmask,
-                         const longlong2 *q_runs, int64_t n_qrun, const uint32_t *q_nmask,
-                         const int64_t *q_woff, int2 *list, int *count, hipStream_t s);
+                         const longlong2 *t_runs, int64_t n_trun, const longlong2 *q_runs,
+                         int64_t n_qrun, const int64_t *q_woff, int2 *list, int *count,
+                         hipStream_t s);
 hipError_t launch_build(const int32_t *bt, const int32_t *bq, const int32_t *bs, int64_t nb,
                         const DChain *chains, int64_t n_chains, int4 *blk, int2 *tspan,
                         uint32_t *bucket, hipStream_t s);
@@ -1412,8 +1412,8 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
         e = hipMalloc(&d_nlist, (size_t)(n + 1) * sizeof(int2));
         if (e == hipSuccess)
             e = launch_nflags(cs->chains, n, cs->blk, c->g[0].d_nrun, c->g[0].n_nrun,
-                              c->g[0].nmask, c->g[1].d_nrun, c->g[1].n_nrun, c->g[1].nmask,
-                              c->g[1].d_woff, d_nlist + 1, (int *)d_nlist, c->stream);
+                              c->g[1].d_nrun, c->g[1].n_nrun, c->g[1].d_woff, d_nlist + 1,
+                              (int *)d_nlist, c->stream);
     }
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     lap("device build + sync");

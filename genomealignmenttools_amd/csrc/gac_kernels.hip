@@ -179,23 +179,8 @@ __device__ __forceinline__ long long wave_sum(long long v) {
 // hold few N runs (assembly gaps), so a chain is first checked as a whole:
 // one lane per chain tests its target and query spans against the sorted
 // global N runs (k_nflags_chains); only chains whose span meets a run have
-// their blocks checked against the N mask (k_nflags_blocks, one wave per
-// listed chain, lanes over blocks).
-__device__ __forceinline__ bool range_has_n(const uint32_t *nmask, int64_t p, int len) {
-    if (len <= 0) return false;
-    int64_t w = p >> 5;
-    const int64_t we = (p + len - 1) >> 5;
-    const int lo = (int)(p & 31);
-    const int hi = (int)((p + len - 1) & 31);
-    for (; w <= we; ++w) {
-        uint32_t m = nmask[w];
-        if (w == (p >> 5)) m &= ~((1u << lo) - 1u);
-        if (w == we) m &= (hi == 31) ? 0xffffffffu : ((2u << hi) - 1u);
-        if (m) return true;
-    }
-    return false;
-}
-
+// their blocks checked, against the same runs (k_nflags_blocks, one wave
+// per listed chain, lanes over blocks).
 // does [lo, hi) meet one of the sorted, disjoint runs {start, end}?
 __device__ __forceinline__ bool span_meets(const longlong2 *runs, int64_t n, int64_t lo, int64_t hi) {
     int64_t a = 0, b = n;  // first run ending past lo
@@ -229,10 +214,12 @@ __global__ void __launch_bounds__(256) k_nflags_chains(const DChain *chains, int
 }
 
 __global__ void __launch_bounds__(256) k_nflags_blocks(const DChain *chains, int4 *blk,
-                                                       const uint32_t *t_nmask,
-                                                       const uint32_t *q_nmask,
+                                                       const longlong2 *t_runs, int64_t n_trun,
+                                                       const longlong2 *q_runs, int64_t n_qrun,
                                                        const int64_t *q_woff, const int2 *list,
                                                        const int *count) {
+    // each block against the same sorted run lists (a few KB: cache
+    // resident), not the N mask (a random line per block and side)
     const int lane = threadIdx.x & 63;
     const int64_t wave_id = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -247,8 +234,9 @@ __global__ void __launch_bounds__(256) k_nflags_blocks(const DChain *chains, int
             int4 b = blk[ch.blk_off + k];
             const int z = b.z & kSizeMask;
             const int64_t qf = minus ? (int64_t)qsize - b.y - z : b.y;
-            b.z = z | ((e.y & 1) && range_has_n(t_nmask, tb + b.x, z) ? kTHasN : 0) |
-                  ((e.y & 2) && range_has_n(q_nmask, qb + qf, z) ? kQHasN : 0);
+            const bool tn = (e.y & 1) && z > 0 && span_meets(t_runs, n_trun, tb + b.x, tb + b.x + z);
+            const bool qn = (e.y & 2) && z > 0 && span_meets(q_runs, n_qrun, qb + qf, qb + qf + z);
+            b.z = z | (tn ? kTHasN : 0) | (qn ? kQHasN : 0);
             blk[ch.blk_off + k] = b;
         }
     }
@@ -257,8 +245,7 @@ __global__ void __launch_bounds__(256) k_nflags_blocks(const DChain *chains, int
 // ------------------------------------------------------------ k_build ----
 // Chain upload, device side: blocks {tStart, qStart, size, 0} and target
 // spans from the caller's plain block arrays (one lane per block), then every
-// chain's bucket index (one wave per chain, one lane per bucket: the first
-// block ending past the bucket's start, by binary search over the spans).
+// chain's bucket index (k_build_buckets).
 __global__ void __launch_bounds__(256) k_build_blocks(const int32_t *bt, const int32_t *bq,
                                                       const int32_t *bs, int64_t nb, int4 *blk,
                                                       int2 *tspan) {
@@ -1461,15 +1448,15 @@ hipError_t launch_build(const int32_t *bt, const int32_t *bq, const int32_t *bs,
 }
 
 hipError_t launch_nflags(const DChain *chains, int64_t n_chains, int4 *blk,
-                         const longlong2 *t_runs, int64_t n_trun, const uint32_t *t_nmask,
-                         const longlong2 *q_runs, int64_t n_qrun, const uint32_t *q_nmask,
-                         const int64_t *q_woff, int2 *list, int *count, hipStream_t s) {
+                         const longlong2 *t_runs, int64_t n_trun, const longlong2 *q_runs,
+                         int64_t n_qrun, const int64_t *q_woff, int2 *list, int *count,
+                         hipStream_t s) {
     if (n_chains == 0 || (n_trun == 0 && n_qrun == 0)) return hipSuccess;
     hipMemsetAsync(count, 0, sizeof(int), s);
     hipLaunchKernelGGL(k_nflags_chains, dim3((unsigned)((n_chains + 255) / 256)), dim3(256), 0, s,
                        chains, n_chains, blk, t_runs, n_trun, q_runs, n_qrun, q_woff, list, count);
-    hipLaunchKernelGGL(k_nflags_blocks, dim3(1024), dim3(256), 0, s, chains, blk, t_nmask, q_nmask,
-                       q_woff, list, count);
+    hipLaunchKernelGGL(k_nflags_blocks, dim3(1024), dim3(256), 0, s, chains, blk, t_runs, n_trun,
+                       q_runs, n_qrun, q_woff, list, count);
     return hipGetLastError();
 }
 
