@@ -545,7 +545,9 @@ static void it_push(nwork *w, int32_t s, int32_t e, ngap *g) {
  * gap bounds per block (gap between block b and b+1).  Each filled space is
  * replaced in the index by its remnants and the chain's gaps strictly inside
  * it, in one leaf update (fillSpace + addSpaceForGap, chainNet.c:487-523). */
-static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int32_t chain, int nb,
+static void fill_other_range(const gac_net *n, nfill *f, int is_q);
+
+static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int is_q, int32_t chain, int nb,
                            const int32_t *s, const int32_t *e, const int32_t *gos,
                            const int32_t *goe, int cstart, int cend) {
     sp_query(n, c, cstart, cend, s, e, nb);
@@ -585,7 +587,11 @@ static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int32_t chai
         f->end = end;
         f->chain = chain;
         f->ali = (int32_t)ali;
-        f->full = 0; /* (set by fill_other_range, on the final bounds) */
+        /* rCalcOtherFill (chainNet.c:393-484) now, while the chain's blocks
+         * are in cache: the final own-side bounds (zero-size blocks at the
+         * ends dropped; the order of a gap's fills is unchanged, their
+         * spaces being disjoint), the other-side range and f->full */
+        fill_other_range(net, f, is_q);
         /* slAddHead onto the space's gap; region workers of one chromosome
          * side (net_regions) may share the gap, so the push is atomic.  The
          * order does not matter: finishNet sorts a gap's fills by start. */
@@ -701,7 +707,7 @@ static void add_chain_q(const gac_net *net, nwork *n, int64_t c, nchrom *qc, int
             }
         }
     }
-    add_chain_side(net, n, qc, (int32_t)c, m, n->rs, n->re, n->ros, n->roe, qs, qe);
+    add_chain_side(net, n, qc, 1, (int32_t)c, m, n->rs, n->re, n->ros, n->roe, qs, qe);
 }
 
 /* addChainT (chainNet.c:557-608) */
@@ -734,7 +740,7 @@ static void add_chain_t(const gac_net *net, nwork *n, int64_t c, nchrom *tc, int
             n->roe[b - l0] = qe;
         }
     }
-    add_chain_side(net, n, tc, (int32_t)c, m, n->rs, n->re, n->ros, n->roe, in->t_start[c],
+    add_chain_side(net, n, tc, 0, (int32_t)c, m, n->rs, n->re, n->ros, n->roe, in->t_start[c],
                    in->t_end[c]);
 }
 
@@ -758,7 +764,7 @@ static int first_end_after(const int32_t *st, const int32_t *sz, int nb, int v) 
 }
 
 /* tFillOtherRange / qFillOtherRange (chainNet.c:393-484) */
-static void fill_other_range(gac_net *n, nfill *f, int is_q) {
+static void fill_other_range(const gac_net *n, nfill *f, int is_q) {
     const gac_net_input *in = &n->in;
     const int64_t c = f->chain, b0 = in->blk_off[c];
     const int nb = (int)(in->blk_off[c + 1] - b0);
@@ -1013,22 +1019,6 @@ static void *fin_thread(void *arg) {
     fin_job *F = arg;
     gac_net *n = F->n;
     nwork *w = &n->w[atomic_fetch_add(&F->wid, 1)];
-    if (F->phase == 2) {
-        const int64_t nt = n->n_order[GAC_T], tot = nt + n->n_order[GAC_Q], chunk = 4096;
-        for (;;) {
-            const int64_t a = atomic_fetch_add(&F->next, chunk);
-            if (a >= tot)
-                break;
-            const int64_t b = a + chunk < tot ? a + chunk : tot;
-            for (int64_t i = a; i < b; ++i) {
-                if (i < nt)
-                    fill_other_range(n, n->order[GAC_T][i], 0);
-                else
-                    fill_other_range(n, n->order[GAC_Q][i - nt], 1);
-            }
-        }
-        return NULL;
-    }
     if (F->phase == 0) {
         const int64_t nc = n->n_chroms[GAC_T] + (int64_t)n->n_chroms[GAC_Q];
         for (;;) {
@@ -1726,9 +1716,7 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
             free(F.x[k].ord);
         free(F.sk);
         free(F.gi);
-        /* phase C: rCalcOtherFill over the flat pre-order lists (the sorts
-         * above key on the fills' own-side bounds, which it recomputes
-         * unchanged, so it can run last) */
+        /* (rCalcOtherFill ran as each fill was made: fill_other_range) */
         struct timespec t_b;
         clock_gettime(CLOCK_MONOTONIC, &t_b);
         if (getenv("GAC_TIMING"))
@@ -1736,10 +1724,6 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
                     (t_a.tv_sec - t_fin0.tv_sec) + 1e-9 * (t_a.tv_nsec - t_fin0.tv_nsec),
                     (t_b.tv_sec - t_a.tv_sec) + 1e-9 * (t_b.tv_nsec - t_a.tv_nsec), (long long)F.n_gi,
                     (long long)F.ntask);
-        F.phase = 2;
-        atomic_init(&F.next, 0);
-        atomic_init(&F.wid, 0);
-        gac_run_threads(n->n_w, fin_thread, &F);
         free(F.x);
     }
     clock_gettime(CLOCK_MONOTONIC, &t_fin1);
