@@ -578,7 +578,8 @@ def c2_leg(args, steps, warmup):
     dt /= steps
     res = {"workload": "configs[1]: chainNet -rescore end to end on C2 (hg38 chr1 x mm10)",
            "value": info["netted_aligned_bases"] / dt / 1e9, "unit": "Gbases/s",
-           "ms_per_step": dt * 1e3, "steps": steps, **info}
+           "ms_per_step": dt * 1e3, "steps": steps, **info,
+           "tool_stages": staged_run(d, out)}  # (one more, untimed, with the stage laps)
     if not args.no_cpu_baseline and os.path.exists(REF_TOOL):
         p = lambda x: os.path.join(d, x)
         ref = p("ref")
