@@ -1392,8 +1392,10 @@ typedef struct net_job {
     _Atomic int64_t next, rnext;
     _Atomic int ready;  /* the prefixes are done and rq is published */
     _Atomic int wid;
+    _Atomic int32_t bnext, bdone; /* big sides whose prefix was taken / is done */
     int nthreads;
-    double prefix_s;    /* thread 0's time in the sequential prefixes */
+    double t0;          /* start of the threads */
+    double prefix_s;    /* from the start until every prefix was done */
 } net_job;
 
 static int region_cmp(const void *a, const void *b) {
@@ -1412,25 +1414,34 @@ static void net_small(gac_net *n, nwork *w, const net_task *t) {
         add_chain(n, w, t->side, t->chains[i], c, INT32_MIN, INT32_MAX);
 }
 
+static double mono_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+
 static void *net_thread(void *arg) {
     net_job *J = arg;
     const int id = atomic_fetch_add(&J->wid, 1);
     nwork *w = &J->n->w[id];
-    if (id == 0) {
+    /* the big sides' sequential prefixes, one side per thread; the thread
+     * finishing the last one publishes every region, largest work first */
+    for (;;) {
+        const int32_t b = atomic_fetch_add(&J->bnext, 1);
+        if (b >= J->nbig)
+            break;
+        big_prefix(J->n, w, &J->big[b], J->nthreads);
+        if (atomic_fetch_add(&J->bdone, 1) + 1 < J->nbig)
+            continue;
         int64_t nr = 0;
-        struct timespec t0, t1;
-        clock_gettime(CLOCK_MONOTONIC, &t0);
-        for (int32_t b = 0; b < J->nbig; ++b) {
-            big_prefix(J->n, w, &J->big[b], J->nthreads);
-            nr += J->big[b].n_reg;
-        }
-        clock_gettime(CLOCK_MONOTONIC, &t1);
-        J->prefix_s = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+        for (int32_t k = 0; k < J->nbig; ++k)
+            nr += J->big[k].n_reg;
         J->rq = malloc((size_t)(nr ? nr : 1) * sizeof(region *));
-        for (int32_t b = 0; b < J->nbig; ++b)
-            for (int32_t r = 0; r < J->big[b].n_reg; ++r)
-                J->rq[J->nrq++] = &J->big[b].reg[r];
+        for (int32_t k = 0; k < J->nbig; ++k)
+            for (int32_t r = 0; r < J->big[k].n_reg; ++r)
+                J->rq[J->nrq++] = &J->big[k].reg[r];
         qsort(J->rq, (size_t)J->nrq, sizeof(region *), region_cmp);
+        J->prefix_s = mono_s() - J->t0;
         atomic_store_explicit(&J->ready, 1, memory_order_release);
     }
     for (;;) {
@@ -1609,15 +1620,18 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
     atomic_init(&J2.rnext, 0);
     atomic_init(&J2.ready, J.nbig == 0);
     atomic_init(&J2.wid, 0);
+    atomic_init(&J2.bnext, 0);
+    atomic_init(&J2.bdone, 0);
     J2.rq = NULL;
     J2.nrq = 0;
     struct timespec t_add0, t_add1;
     clock_gettime(CLOCK_MONOTONIC, &t_add0);
+    J2.t0 = mono_s();
     const int64_t units = nsmall + (J.nbig ? n->n_w : 0);
     gac_run_threads(n->n_w < units ? n->n_w : (units ? (int)units : 1), net_thread, &J2);
     clock_gettime(CLOCK_MONOTONIC, &t_add1);
     if (getenv("GAC_TIMING")) {
-        fprintf(stderr, "[gac_net_build] addChainT/Q %.3f s (%d threads, largest task %lld chains; sequential prefixes %.3f s)\n",
+        fprintf(stderr, "[gac_net_build] addChainT/Q %.3f s (%d threads, largest task %lld chains; sequential prefixes done after %.3f s)\n",
                 (t_add1.tv_sec - t_add0.tv_sec) + 1e-9 * (t_add1.tv_nsec - t_add0.tv_nsec),
                 n->n_w, J.ntask ? (long long)J.task[0].n : 0LL, J2.prefix_s);
         for (int32_t b = 0; b < J.nbig; ++b) {
