@@ -68,6 +68,8 @@ PKG = os.path.join(REPO, "genomealignmenttools_amd")
 TOOL = os.path.join(PKG, "bin", "chainNet")
 SYNTH = os.path.join(PKG, "libexec", "gac_synth")
 REF_TOOL = os.path.join(REPO, "oracle", "_ref", "chainNet")
+SC_TOOL = os.path.join(PKG, "bin", "scoreChain")
+REF_SC_TOOL = os.path.join(REPO, "oracle", "_ref", "scoreChain")
 SAMPLE_TARGETS = ("chr21", "chr22")
 
 
@@ -560,6 +562,53 @@ def cpu_baseline_c5(d, ours):
                       f"wall time; their target-net sections compared with the headline's)"}
 
 
+def scorechain_e2e_leg(d, info, steps, ref_sample):
+    """bin/scoreChain end to end on C5 (every chain rescored: global score,
+    written as chain text), input aligned bases / wall time; with
+    ref_sample, the reference scoreChain on the cpu baseline's sample chains
+    (one process) against ours on the same file."""
+    p = lambda x: os.path.join(d, x)
+    out = p("ours.sc.chain")
+    cmd = [SC_TOOL, p("in.chain"), p("t.2bit"), p("q.2bit"), out, "-linearGap=loose"]
+    run_tool(cmd, [out])  # warmup
+    dt = 0.0
+    for _ in range(steps):
+        if os.path.exists(out):
+            os.remove(out)
+        t0 = time.perf_counter()
+        run_tool(cmd, [])
+        dt += time.perf_counter() - t0
+    dt /= steps
+    os.remove(out)
+    r = run_tool(cmd + ["-verbose=2"], [], env=dict(os.environ, GAC_TIMING="1"))
+    res = {"workload": "scoreChain end to end (bin/scoreChain), C5 whole genome: every chain's "
+                       "score rescored and the chain file rewritten",
+           "value": info["input_aligned_bases"] / dt / 1e9, "unit": "Gbases/s",
+           "ms_per_step": dt * 1e3, "steps": steps,
+           "tool_stages": [x.strip() for x in r.stderr.splitlines() if x.startswith("[stage]")]}
+    os.remove(out)
+    if ref_sample and os.path.exists(REF_SC_TOOL) and os.path.exists(p("sample.chain")):
+        sample, ro, oo = p("sample.chain"), p("ref.sample.sc.chain"), p("ours.sample.sc.chain")
+        t0 = time.time()
+        run_tool([REF_SC_TOOL, sample, p("t.2bit"), p("q.2bit"), ro, "-linearGap=loose"], [ro])
+        t1 = time.time() - t0
+        run_tool([SC_TOOL, sample, p("t.2bit"), p("q.2bit"), oo, "-linearGap=loose"], [oo])
+        bases = 0
+        with open(sample) as f:
+            for line in f:
+                w = line.split()
+                if len(w) in (1, 3) and w[0].isdigit():
+                    bases += int(w[0])
+        res["cpu_reference"] = {"seconds": t1, "cores": 1, "kind": "reference",
+                                "value": bases / t1 / 1e9, "sample_aligned_bases": bases,
+                                "identical_output": filecmp.cmp(ro, oo, False),
+                                "sample": "reference scoreChain (oracle/_ref) on the cpu "
+                                          "baseline's sample chains"}
+        log(f"scoreChain: ours {dt * 1e3:.0f} ms on C5; reference {t1:.2f}s on the sample "
+            f"({bases / 1e6:.0f} M bases), identical: {res['cpu_reference']['identical_output']}")
+    return res
+
+
 def c2_leg(args, steps, warmup):
     d, info = c2_files(args)
     out = os.path.join(d, "ours")
@@ -747,6 +796,11 @@ def main():
             out["cpu_baseline"] = cpu_baseline_c5(d, out_base)
         except Exception as ex:  # reported, never fatal
             out["cpu_baseline"] = {"error": str(ex)[:300]}
+    if rank == 0 and world == 1 and not args.no_scorechain:
+        try:
+            out["scorechain_e2e"] = scorechain_e2e_leg(d, info, 2, not args.no_cpu_baseline)
+        except Exception as ex:  # reported, never fatal
+            out["scorechain_e2e"] = {"error": str(ex)[:300]}
     if rank == 0:
         print(json.dumps(out), flush=True)
     barrier()
