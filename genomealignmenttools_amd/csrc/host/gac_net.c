@@ -552,6 +552,10 @@ static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int is_q, in
                            const int32_t *goe, int cstart, int cend) {
     sp_query(n, c, cstart, cend, s, e, nb);
     const int64_t nsp = n->q_n;
+    /* each filled space's gap gets the fill pushed: its line is a cache
+     * miss (the gap was made long before), so fetch them all now */
+    for (int64_t si = 0; si < nsp; ++si)
+        __builtin_prefetch(&n->q[si].gap->fill_head, 1);
     int k = 0;
     for (int64_t si = 0; si < nsp; ++si) {
         const int sstart = n->q[si].start, send = n->q[si].end;
