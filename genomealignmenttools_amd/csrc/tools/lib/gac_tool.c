@@ -1289,7 +1289,8 @@ char *gt_slurp(const char *path, size_t *len) {
             cap = (size_t)st.st_size + 1;
             if (st.st_size > (32 << 20)) {
                 const size_t size = (size_t)st.st_size;
-                buf = malloc(size + 1);
+                buf = malloc(size + 17);
+                memset(buf + size, 0, 17); /* (over-reads of the parsers) */
                 pr_job J = {fd, buf, size, 8u << 20, 0, 0};
                 atomic_init(&J.next, 0);
                 atomic_init(&J.bad, 0);
@@ -1321,7 +1322,8 @@ char *gt_slurp(const char *path, size_t *len) {
         if (fd != 0)
             close(fd);
     }
-    buf[l] = 0;
+    buf = realloc(buf, l + 17);
+    memset(buf + l, 0, 17); /* (over-reads of the parsers) */
     *len = l;
     return buf;
 }
@@ -1478,7 +1480,7 @@ static int skip_blocks(lf *f) {
  * else (blank or '#' lines, spaces, CR, long numbers, a missing newline,
  * errors), which the general lineFileChopNext + lineFileNeedNum path then
  * reads from the same position. */
-static int fast_block_line(lf *f, int *v, int *bw) {
+static int fast_block_line_scalar(lf *f, int *v, int *bw) {
     const char *p = f->cur, *end = f->end;
     int k = 0;
     for (;;) {
@@ -1497,6 +1499,52 @@ static int fast_block_line(lf *f, int *v, int *bw) {
             break;
         if (*p != '\t' || k == 3)
             return 0;
+        ++p;
+    }
+    if (k == 2)
+        return 0;
+    f->cur = (char *)p + 1;
+    ++f->line;
+    *bw = k;
+    return 1;
+}
+
+/* One decimal field of 1-7 digits starting at p, eight bytes at a time
+ * (gt_slurp pads the text, so the load may run past the chunk): the digit
+ * count from the first byte that is not '0'..'9', then the digits as one
+ * 8-digit number with leading zeros (three multiply-add steps).  0 = not
+ * such a field (8+ digits, a sign, the chunk's end): the scalar path. */
+static inline int swar_field(const char *p, const char *end, int *val) {
+    uint64_t w;
+    memcpy(&w, p, 8);
+    const uint64_t x = w - 0x3030303030303030ull;
+    const uint64_t nd = ((x + 0x7676767676767676ull) | x) & 0x8080808080808080ull;
+    if (!nd)
+        return 0;
+    const int n = __builtin_ctzll(nd) >> 3;
+    if (n == 0 || n == 8 || p + n >= end)
+        return 0;
+    uint64_t d = (x & ((1ull << (8 * n)) - 1)) << (8 * (8 - n));
+    d = (d * 10 + (d >> 8)) & 0x00FF00FF00FF00FFull;
+    d = (d * 100 + (d >> 16)) & 0x0000FFFF0000FFFFull;
+    d = (d * 10000 + (d >> 32)) & 0xFFFFFFFFull;
+    *val = (int)d;
+    return n;
+}
+
+static int fast_block_line(lf *f, int *v, int *bw) {
+    const char *p = f->cur, *end = f->end;
+    int k = 0;
+    for (;;) {
+        const int n = swar_field(p, end, &v[k]);
+        if (!n)
+            return fast_block_line_scalar(f, v, bw);
+        p += n;
+        ++k;
+        if (*p == '\n')
+            break;
+        if (*p != '\t' || k == 3)
+            return fast_block_line_scalar(f, v, bw);
         ++p;
     }
     if (k == 2)
@@ -1610,6 +1658,12 @@ static void *parse_chunk(void *arg) {
     chunk *k = arg;
     k->c.blk_off = malloc(8);
     k->c.blk_off[0] = 0;
+    if (k->lines > 0) { /* every block is a line: the arrays never grow */
+        k->c.bcap = k->lines + 1;
+        k->c.bt = malloc((size_t)k->c.bcap * 4);
+        k->c.bq = malloc((size_t)k->c.bcap * 4);
+        k->c.bs = malloc((size_t)k->c.bcap * 4);
+    }
     int r;
     while ((r = parse_chain(k)) == 0)
         ;
@@ -1787,6 +1841,8 @@ static void read_chains(const char *path, gt_chains *c, double stop_below, int k
     }
     RC_LAP("cut");
     gt_parallel(nk, count_newlines, NL, sizeof(nl_job)); /* before parsing cuts lines */
+    for (int k = 0; k < nk; ++k)
+        K[k].lines = NL[k].n;
     RC_LAP("count lines");
     gt_parallel(nk, parse_chunk, K, sizeof(chunk));
     RC_LAP("parse");
