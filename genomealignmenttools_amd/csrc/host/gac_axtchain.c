@@ -392,6 +392,7 @@ typedef struct dkey {
     double k;
     int32_t rank, v;
 } dkey;
+struct dkey;
 
 /* descending by k (kdLeafCmpTotal / chainCmpScore: sign of b - a) */
 static int dkey_cmp_desc(const void *a, const void *b) {
@@ -1338,8 +1339,98 @@ typedef struct fold_job {
     int32_t *qs, *qe, *ts, *te;
     int64_t *poff; /* poff[p + 1] = folded count of pair p */
     int64_t np;
+    int64_t big;   /* pairs above this many blocks were folded beforehand */
     _Atomic int64_t next;
 } fold_job;
+
+/* ---- parallel sort of one large pair's keys (ranks make every key unique,
+ * so any correct sort is the stable one): runs sorted on threads, then
+ * merged pairwise, the merges of a round on threads */
+typedef struct psort_job {
+    bkey *a, *tmp;
+    int64_t n;
+    int nrun;
+    int64_t *cut; /* [nrun + 1] */
+    int64_t width; /* runs merged per output run this round / 2 */
+    _Atomic int next;
+} psort_job;
+
+static void *psort_runs(void *arg) {
+    psort_job *J = arg;
+    for (;;) {
+        const int r = atomic_fetch_add(&J->next, 1);
+        if (r >= J->nrun)
+            return NULL;
+        qsort(J->a + J->cut[r], (size_t)(J->cut[r + 1] - J->cut[r]), sizeof(bkey), bkey_cmp);
+    }
+}
+
+static void *psort_merge(void *arg) {
+    psort_job *J = arg;
+    for (;;) {
+        const int m = atomic_fetch_add(&J->next, 1);
+        const int64_t r0 = (int64_t)m * 2 * J->width;
+        if (r0 >= J->nrun)
+            return NULL;
+        const int64_t r1 = r0 + J->width < J->nrun ? r0 + J->width : J->nrun;
+        const int64_t r2 = r0 + 2 * J->width < J->nrun ? r0 + 2 * J->width : J->nrun;
+        int64_t i = J->cut[r0], j = J->cut[r1], o = J->cut[r0];
+        const int64_t ie = J->cut[r1], je = J->cut[r2];
+        while (i < ie && j < je)
+            J->tmp[o++] = bkey_cmp(&J->a[j], &J->a[i]) < 0 ? J->a[j++] : J->a[i++];
+        while (i < ie)
+            J->tmp[o++] = J->a[i++];
+        while (j < je)
+            J->tmp[o++] = J->a[j++];
+    }
+}
+
+static void par_sort_bkey(bkey *a, int64_t n, int nt) {
+    psort_job J;
+    J.a = a;
+    J.n = n;
+    J.nrun = nt;
+    J.cut = malloc((size_t)(nt + 1) * sizeof(int64_t));
+    for (int r = 0; r <= nt; ++r)
+        J.cut[r] = n * r / nt;
+    atomic_init(&J.next, 0);
+    gac_run_threads(nt, psort_runs, &J);
+    J.tmp = malloc((size_t)n * sizeof(bkey));
+    for (J.width = 1; J.width < nt; J.width *= 2) {
+        atomic_store(&J.next, 0);
+        const int64_t merges = (nt + 2 * J.width - 1) / (2 * J.width);
+        gac_run_threads(merges < nt ? (int)merges : nt, psort_merge, &J);
+        bkey *t = J.a;
+        J.a = J.tmp;
+        J.tmp = t;
+    }
+    if (J.a != a) { /* an odd number of rounds: the result is in the scratch */
+        memcpy(a, J.a, (size_t)n * sizeof(bkey));
+        J.tmp = J.a;
+    }
+    free(J.tmp);
+    free(J.cut);
+}
+
+/* removeExactOverlaps' fold of one pair's sorted keys into its input slot */
+static int64_t fold_sorted(fold_job *F, const bkey *k, int64_t a, int64_t m) {
+    int64_t n = a;
+    for (int64_t i = 0; i < m; ++i) {
+        if (n > a && k[i].qs == F->qs[n - 1] && k[i].ts == F->ts[n - 1]) {
+            if (F->qe[n - 1] < k[i].qe)
+                F->qe[n - 1] = k[i].qe;
+            if (F->te[n - 1] < k[i].te)
+                F->te[n - 1] = k[i].te;
+            continue;
+        }
+        F->qs[n] = k[i].qs;
+        F->qe[n] = k[i].qe;
+        F->ts[n] = k[i].ts;
+        F->te[n] = k[i].te;
+        ++n;
+    }
+    return n - a;
+}
 
 /* removeExactOverlaps (axtChain.c:173-197): slSort by (qStart, tStart),
  * stable; blocks with both starts equal fold into the first (max ends) */
@@ -1353,6 +1444,8 @@ static void *fold_thread(void *arg) {
         if (p >= F->np)
             break;
         const int64_t a = in->blk_off[p], b = in->blk_off[p + 1];
+        if (b - a > F->big)
+            continue;
         if (b - a > kcap) {
             kcap = b - a;
             k = realloc(k, (size_t)kcap * sizeof(bkey));
@@ -1361,22 +1454,7 @@ static void *fold_thread(void *arg) {
             k[i - a] = (bkey){in->blk_q[i], in->blk_t[i], (int32_t)(i - a),
                               in->blk_q[i] + in->blk_size[i], in->blk_t[i] + in->blk_size[i]};
         qsort(k, (size_t)(b - a), sizeof(bkey), bkey_cmp);
-        int64_t n = a;
-        for (int64_t i = 0; i < b - a; ++i) {
-            if (n > a && k[i].qs == F->qs[n - 1] && k[i].ts == F->ts[n - 1]) {
-                if (F->qe[n - 1] < k[i].qe)
-                    F->qe[n - 1] = k[i].qe;
-                if (F->te[n - 1] < k[i].te)
-                    F->te[n - 1] = k[i].te;
-                continue;
-            }
-            F->qs[n] = k[i].qs;
-            F->qe[n] = k[i].qe;
-            F->ts[n] = k[i].ts;
-            F->te[n] = k[i].te;
-            ++n;
-        }
-        F->poff[p + 1] = n - a;
+        F->poff[p + 1] = fold_sorted(F, k, a, b - a);
     }
     free(k);
     return NULL;
@@ -1408,6 +1486,77 @@ static int cmp_i64_desc_pair(const void *a, const void *b, void *arg) {
     if (sz[x] != sz[y])
         return sz[x] > sz[y] ? -1 : 1;
     return (x > y) - (x < y);
+}
+
+/* the pairs' chains gathered into one chain set (parallel over pairs) */
+typedef struct gather_job {
+    const ax_out *po;
+    const gac_axt_input *in;
+    int32_t *ct, *cq;
+    uint8_t *cs;
+    int32_t *cpair;
+    int64_t *coff;
+    int32_t *bt, *bq, *bs;
+    int64_t *c0, *x0; /* per pair: first chain, first block */
+    int64_t np;
+    _Atomic int64_t next;
+} gather_job;
+
+static void *gather_thread(void *arg) {
+    gather_job *G = arg;
+    for (;;) {
+        const int64_t p = atomic_fetch_add(&G->next, 1);
+        if (p >= G->np)
+            return NULL;
+        const ax_out *o = &G->po[p];
+        int64_t c = G->c0[p], x = G->x0[p];
+        for (int32_t k = 0; k < o->n_chains; ++k, ++c) {
+            G->ct[c] = G->in->t_seq[p];
+            G->cq[c] = G->in->q_seq[p];
+            G->cs[c] = G->in->q_strand[p] ? 1 : 0;
+            G->cpair[c] = (int32_t)p;
+            const int32_t b0 = o->coff[k], b1 = o->coff[k + 1];
+            memcpy(G->bt + x, o->bt + b0, (size_t)(b1 - b0) * 4);
+            memcpy(G->bq + x, o->bq + b0, (size_t)(b1 - b0) * 4);
+            memcpy(G->bs + x, o->bs + b0, (size_t)(b1 - b0) * 4);
+            x += b1 - b0;
+            G->coff[c + 1] = x;
+        }
+    }
+}
+
+/* the kept chains in output order (parallel over chains) */
+typedef struct out_job {
+    gac_axt_chains *R;
+    const struct dkey *k;
+    const int64_t *coff, *gsc;
+    const int32_t *cpair, *bt, *bq, *bs;
+    int64_t nk;
+    _Atomic int64_t next;
+} out_job;
+
+static void *out_thread(void *arg) {
+    out_job *O = arg;
+    gac_axt_chains *R = O->R;
+    for (;;) {
+        const int64_t j0 = atomic_fetch_add(&O->next, 1024);
+        if (j0 >= O->nk)
+            return NULL;
+        const int64_t j1 = j0 + 1024 < O->nk ? j0 + 1024 : O->nk;
+        for (int64_t j = j0; j < j1; ++j) {
+            const int32_t i = O->k[j].v;
+            const int64_t b0 = O->coff[i], b1 = O->coff[i + 1], o = R->blk_off[j];
+            R->score[j] = (double)O->gsc[i];
+            R->pair[j] = O->cpair[i];
+            R->t_start[j] = O->bt[b0];
+            R->q_start[j] = O->bq[b0];
+            R->t_end[j] = O->bt[b1 - 1] + O->bs[b1 - 1];
+            R->q_end[j] = O->bq[b1 - 1] + O->bs[b1 - 1];
+            memcpy(R->blk_t + o, O->bt + b0, (size_t)(b1 - b0) * 4);
+            memcpy(R->blk_q + o, O->bq + b0, (size_t)(b1 - b0) * 4);
+            memcpy(R->blk_size + o, O->bs + b0, (size_t)(b1 - b0) * 4);
+        }
+    }
 }
 
 void gac_axt_chains_free(gac_axt_chains *c) {
@@ -1468,7 +1617,24 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
     {
         /* every pair folds in parallel into its own input slot, then the
          * slots are compacted in pair order */
-        fold_job F = {in, qs, qe, ts, te, poff, np, 0};
+        fold_job F = {in, qs, qe, ts, te, poff, np, INT64_MAX, 0};
+        /* pairs of more than 1 M blocks (one can hold a third of a
+         * whole-genome run) are sorted with every thread first */
+        if (nthreads > 1) {
+            F.big = 1 << 20;
+            for (int64_t p = 0; p < np; ++p) {
+                const int64_t a = in->blk_off[p], b = in->blk_off[p + 1];
+                if (b - a <= F.big)
+                    continue;
+                bkey *k = malloc((size_t)(b - a) * sizeof(bkey));
+                for (int64_t i = a; i < b; ++i)
+                    k[i - a] = (bkey){in->blk_q[i], in->blk_t[i], (int32_t)(i - a),
+                                      in->blk_q[i] + in->blk_size[i], in->blk_t[i] + in->blk_size[i]};
+                par_sort_bkey(k, b - a, nthreads);
+                poff[p + 1] = fold_sorted(&F, k, a, b - a);
+                free(k);
+            }
+        }
         atomic_init(&F.next, 0);
         run_threads(nthreads < np ? nthreads : (int)(np ? np : 1), fold_thread, &F);
     }
@@ -1642,33 +1808,29 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
         int64_t *coff = malloc((size_t)(nc + 1) * 8);
         int32_t *bt = malloc((size_t)(ncb ? ncb : 1) * 4), *bq = malloc((size_t)(ncb ? ncb : 1) * 4),
                 *bs = malloc((size_t)(ncb ? ncb : 1) * 4);
-        gac_range *rg = malloc((size_t)(nc ? nc : 1) * sizeof(gac_range));
         int64_t *gsc = malloc((size_t)(nc ? nc : 1) * 8);
         int32_t *gali = malloc((size_t)(nc ? nc : 1) * 4);
-        int64_t c = 0, x = 0;
-        coff[0] = 0;
+        /* every pair's chains into the set, pairs in parallel (disjoint
+         * slots from prefix sums over the pairs) */
+        gather_job G = {po, in, ct, cq, cs, cpair, coff, bt, bq, bs, NULL, NULL, np, 0};
+        G.c0 = malloc((size_t)(np + 1) * 8);
+        G.x0 = malloc((size_t)(np + 1) * 8);
+        G.c0[0] = G.x0[0] = 0;
         for (int64_t p = 0; p < np; ++p) {
-            const ax_out *o = &po[p];
-            for (int32_t k = 0; k < o->n_chains; ++k) {
-                ct[c] = in->t_seq[p];
-                cq[c] = in->q_seq[p];
-                cs[c] = in->q_strand[p] ? 1 : 0;
-                cpair[c] = (int32_t)p;
-                const int32_t b0 = o->coff[k], b1 = o->coff[k + 1];
-                memcpy(bt + x, o->bt + b0, (size_t)(b1 - b0) * 4);
-                memcpy(bq + x, o->bq + b0, (size_t)(b1 - b0) * 4);
-                memcpy(bs + x, o->bs + b0, (size_t)(b1 - b0) * 4);
-                rg[c] = (gac_range){(int32_t)c, o->bt[b0], o->bt[b1 - 1] + o->bs[b1 - 1]};
-                x += b1 - b0;
-                coff[++c] = x;
-            }
+            G.c0[p + 1] = G.c0[p] + po[p].n_chains;
+            G.x0[p + 1] = G.x0[p] + (po[p].coff ? po[p].coff[po[p].n_chains] : 0);
         }
+        coff[0] = 0;
+        atomic_init(&G.next, 0);
+        run_threads(nthreads < np ? nthreads : (int)(np ? np : 1), gather_thread, &G);
+        free(G.c0);
+        free(G.x0);
         gac_chainset_desc d = {nc, ct, cq, cs, coff, ncb, bt, bq, bs};
         gac_chainset *set = NULL;
-        if (nc > 0) {
+        if (nc > 0) { /* whole chains: chainCalcScore of each (axtChain.c:300-305) */
             rc = gac_chains_upload(ctx, &d, &set);
             if (rc == GAC_OK)
-                rc = gac_score_ranges(ctx, set, rg, nc, 0, gsc, NULL, gali);
+                rc = gac_score_chains(ctx, set, 0, gsc, NULL, gali);
             gac_chains_free(set);
         }
         stage("GPU chain scores", &tclock);
@@ -1700,20 +1862,11 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
             R->blk_q = malloc((size_t)(tb ? tb : 1) * 4);
             R->blk_size = malloc((size_t)(tb ? tb : 1) * 4);
             R->blk_off[0] = 0;
-            for (int64_t j = 0; j < nk; ++j) {
-                const int32_t i = k[j].v;
-                const int64_t b0 = coff[i], b1 = coff[i + 1], o = R->blk_off[j];
-                R->score[j] = (double)gsc[i];
-                R->pair[j] = cpair[i];
-                R->t_start[j] = bt[b0];
-                R->q_start[j] = bq[b0];
-                R->t_end[j] = bt[b1 - 1] + bs[b1 - 1];
-                R->q_end[j] = bq[b1 - 1] + bs[b1 - 1];
-                memcpy(R->blk_t + o, bt + b0, (size_t)(b1 - b0) * 4);
-                memcpy(R->blk_q + o, bq + b0, (size_t)(b1 - b0) * 4);
-                memcpy(R->blk_size + o, bs + b0, (size_t)(b1 - b0) * 4);
-                R->blk_off[j + 1] = o + (b1 - b0);
-            }
+            for (int64_t j = 0; j < nk; ++j)
+                R->blk_off[j + 1] = R->blk_off[j] + (coff[k[j].v + 1] - coff[k[j].v]);
+            out_job O = {R, k, coff, gsc, cpair, bt, bq, bs, nk, 0};
+            atomic_init(&O.next, 0);
+            run_threads(nthreads, out_thread, &O);
             free(k);
         }
         free(ct);
@@ -1724,7 +1877,6 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
         free(bt);
         free(bq);
         free(bs);
-        free(rg);
         free(gsc);
         free(gali);
     }

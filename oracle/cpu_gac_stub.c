@@ -329,6 +329,21 @@ static void emu_xover(gac_ctx *c, int32_t ts, int32_t qs, int minus, int lqe, in
     *adj = (int)(lsum - bestv);
 }
 
+/* whole chains: the ranges API over every chain's full target span */
+int gac_score_chains(gac_ctx *c, const gac_chainset *s, uint32_t flags, int64_t *g, int64_t *l,
+                     int32_t *ali) {
+    gac_range *r = malloc((size_t)(s->n ? s->n : 1) * sizeof(gac_range));
+    for (int64_t k = 0; k < s->n; ++k) {
+        const int64_t b0 = s->off[k], b1 = s->off[k + 1];
+        r[k].chain = (int32_t)k;
+        r[k].t_start = b1 > b0 ? s->bt[b0] : 0;
+        r[k].t_end = b1 > b0 ? s->bt[b1 - 1] + s->bs[b1 - 1] : 0;
+    }
+    const int rc = gac_score_ranges(c, s, r, s->n, flags, g, l, ali);
+    free(r);
+    return rc;
+}
+
 int gac_crossovers(gac_ctx *c, int64_t n, const int32_t *t_seq, const int32_t *q_seq,
                    const uint8_t *q_strand, const int32_t *lqe, const int32_t *lte,
                    const int32_t *rqs, const int32_t *rts, const int32_t *overlap, int32_t *pos,
