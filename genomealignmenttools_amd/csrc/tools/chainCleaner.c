@@ -1213,6 +1213,7 @@ int main(int argc, char *argv[]) {
     gt_options(&argc, argv, k_opts);
     if (argc != 6)
         usage();
+    gt_one_device(); /* before the chain reader's threads (setenv) */
     const char *in_chain = argv[1], *tnib = argv[2], *qnib = argv[3];
     const char *out_chain = argv[4], *out_bed = argv[5];
     const char *in_net = gt_opt_str("net", NULL);
