@@ -77,11 +77,15 @@ typedef struct cursor {
 static void cursor_read(cursor *c, stream *out) {
     c->chain = NULL;
     while (c->pos < c->s->n) {
-        const item *x = &c->s->it[c->pos++];
+        item *x = &c->s->it[c->pos++];
         if (x->meta) {
             push(out, *x); /* echoed to the merge's output as it is read */
             continue;
         }
+        /* a header without an id takes chainIdNext when chainRead reads it:
+         * files interleave in the merge's order (chainMergeSort.c:35-67) */
+        if (x->id == INT32_MIN)
+            x->id = gt_next_chain_id();
         c->chain = x;
         return;
     }
@@ -226,6 +230,7 @@ int main(int argc, char *argv[]) {
     /* every input parsed; its stream: chain k after the '#' lines read with it */
     gt_chains *files = calloc((size_t)(nf ? nf : 1), sizeof(gt_chains));
     stream *level = calloc((size_t)(nf ? nf : 1), sizeof(stream));
+    gt_defer_chain_ids(1); /* ids in read order: cursor_read */
     for (int i = 0; i < nf; ++i) {
         gt_read_chains(names[i], &files[i], -HUGE_VAL, 1);
         const gt_chains *c = &files[i];

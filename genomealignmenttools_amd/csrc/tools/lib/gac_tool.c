@@ -1440,6 +1440,7 @@ static void chains_reserve_n(gt_chains *c, int64_t need) {
 }
 
 static int g_next_id = 1; /* chainIdNext (chain.c:180-198) */
+static int g_defer_ids;   /* gt_defer_chain_ids: id-less headers keep INT32_MIN */
 
 typedef struct chunk {
     lf f;
@@ -1870,7 +1871,7 @@ static void read_chains(const char *path, gt_chains *c, double stop_below, int k
         qmaps[k] = qmap;
         /* ids: every header read so far consumes chainIdNext, kept or not */
         const int64_t nread = ch->c.n;
-        for (int64_t i = 0; i < nread; ++i)
+        for (int64_t i = 0; i < nread && !g_defer_ids; ++i)
             if (ch->c.id[i] == INT32_MIN)
                 ch->c.id[i] = g_next_id++;
         ch->c.n = take; /* chains to copy */
@@ -1962,6 +1963,8 @@ void gt_chains_free(gt_chains *c) {
 }
 
 int gt_next_chain_id(void) { return g_next_id++; }
+
+void gt_defer_chain_ids(int on) { g_defer_ids = on; }
 
 /* decimal text of v at p, returns the end */
 static char *put_int(char *p, int64_t v) {

@@ -226,6 +226,9 @@ void gt_read_chains_keep(const char *path, gt_chains *c, double stop_below, int 
 void gt_chains_free(gt_chains *c);
 /* chainIdNext (chain.c:180-198): the shared "next id" counter */
 int gt_next_chain_id(void);
+/* 1: gt_read_chains leaves header ids absent from the text as INT32_MIN, for
+ * a caller that consumes chainIdNext in its own read order (chainMergeSort) */
+void gt_defer_chain_ids(int on);
 /* chainWrite (chain.c:200-227) of chain i with the given score and id */
 void gt_write_chain(FILE *f, const gt_chains *c, int64_t i, double score, int32_t id);
 /* chainWrite of an explicit header and block list */

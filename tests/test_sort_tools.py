@@ -90,16 +90,23 @@ def check_chainsort(chains, tmp_path):
         assert filecmp.cmp(tmp_path / f"ours{k}.idx", tmp_path / f"ref{k}.idx", shallow=False)
 
 
-def check_chainmergesort(chains, tmp_path, nfiles=12, frac=False):
-    """nfiles score-sorted inputs (the reference chainSort makes them) merged."""
+def check_chainmergesort(chains, tmp_path, nfiles=12, frac=False, idless=False):
+    """nfiles score-sorted inputs (the reference chainSort makes them; with
+    idless, written sorted without header ids, so that chainIdNext numbers
+    them in the merge's read order -- visible with -saveId) merged."""
     rng = np.random.default_rng(nfiles)
     parts = np.array_split(rng.permutation(chains.n), nfiles)
     names = []
     for k, p in enumerate(parts):
+        srt = tmp_path / f"part{k}.chain"
+        if idless:
+            p = p[np.argsort(-np.round(chains.score[p] / 500.0), kind="stable")]
+            srt.write_text(_chain_text(chains, p, rng, idless=True))
+            names.append(str(srt))
+            continue
         raw = tmp_path / f"raw{k}.chain"
         body = _chain_text(chains, p, rng, frac=frac, meta_every=11 if k % 3 == 0 else 0)
         raw.write_text((f"# part {k}\n" if k % 2 == 0 else "") + body)
-        srt = tmp_path / f"part{k}.chain"
         _run([_ref("chainSort"), raw, srt])
         if k % 4 == 1:  # a '#' line after the last chain
             with open(srt, "a") as f:
@@ -124,6 +131,12 @@ def test_chainsort_vs_reference(chains, tmp_path):
 
 def test_chainmergesort_vs_reference(chains, tmp_path):
     check_chainmergesort(chains, tmp_path, nfiles=12)
+
+
+def test_chainmergesort_idless_saveid_vs_reference(chains, tmp_path):
+    """Inputs without header ids: -saveId shows the ids chainRead gave them,
+    in the order the merge reads the files (interleaved, not file by file)."""
+    check_chainmergesort(chains, tmp_path, nfiles=7, idless=True)
 
 
 def test_chainmergesort_hierarchical_vs_reference(chains, tmp_path):
