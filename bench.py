@@ -585,7 +585,8 @@ def scorechain_e2e_leg(d, info, steps, ref_sample):
                        "score rescored and the chain file rewritten",
            "value": info["input_aligned_bases"] / dt / 1e9, "unit": "Gbases/s",
            "ms_per_step": dt * 1e3, "steps": steps,
-           "tool_stages": [x.strip() for x in r.stderr.splitlines() if x.startswith("[stage]")]}
+           "tool_stages": [x.strip() for x in r.stderr.splitlines()
+                           if x.startswith(("[stage]", "[gac_chains_upload]", "[gt_read_chains]"))]}
     os.remove(out)
     if ref_sample and os.path.exists(REF_SC_TOOL) and os.path.exists(p("sample.chain")):
         sample, ro, oo = p("sample.chain"), p("ref.sample.sc.chain"), p("ours.sample.sc.chain")
