@@ -209,7 +209,23 @@ struct gac_chainset {
     int32_t *w_status = nullptr;   // {W, T, 0, 0}
     int32_t *w_empty = nullptr;    // chains without blocks (their results are 0)
     int64_t w_nempty = 0;
+    // capacities (gac_chains_reupload refills these buffers when they fit)
+    size_t cap_chains = 0, cap_blocks = 0, cap_tspan = 0, cap_idx = 0;
+    int32_t *d_stage = nullptr;  // the caller's block arrays, staged (3 x blocks)
+    size_t cap_stage = 0;
+    int2 *d_nlist = nullptr;     // chains meeting an N run (+ count)
+    size_t cap_nlist = 0;
 };
+
+static void free_whole_plan(gac_chainset *cs) {
+    void *w[] = {cs->w_rdesc, cs->w_nblk, cs->w_gflat, cs->w_tile_r0, cs->w_status, cs->w_empty};
+    for (void *p : w)
+        if (p) hipFree(p);
+    cs->w_rdesc = nullptr;
+    cs->w_nblk = cs->w_gflat = cs->w_tile_r0 = cs->w_status = cs->w_empty = nullptr;
+    cs->w_nempty = 0;
+    cs->w_ready = false;
+}
 
 // ----------------------------------------------------------------- context
 extern "C" int gac_open(int device, gac_ctx **out) {
@@ -1298,11 +1314,20 @@ static int upload_staged(gac_ctx *c, void *d_dst, const void *h_src, size_t byte
     return GAC_OK;
 }
 
-extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_chainset **out) {
-    gac_clear_error();
-    if (!c || !d || !out) return gac_fail(GAC_E_ARG, "gac_chains_upload: NULL argument");
-    CTX_LOCK(c);
-    *out = nullptr;
+// device buffer *p of capacity *cap holds at least want elements of sz bytes
+// (grown with headroom; the contents are not kept)
+static hipError_t ensure_buf(void **p, size_t *cap, size_t want, size_t sz) {
+    if (*p && *cap >= want) return hipSuccess;
+    if (*p) hipFree(*p);
+    *p = nullptr;
+    const size_t n = want + want / 4 + 64;
+    const hipError_t e = hipMalloc(p, n * sz);
+    *cap = e == hipSuccess ? n : 0;
+    return e;
+}
+
+// the chain set's contents := d (its device buffers reused where they fit)
+static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs) {
     if (!c->g[0].final || !c->g[1].final)
         return gac_fail(GAC_E_STATE, "load both genomes before uploading chains");
     if (d->n_chains < 0 || d->n_blocks < 0 || (d->n_chains && (!d->t_seq || !d->q_seq ||
@@ -1384,18 +1409,22 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
         idx_n += k;
     }
     HIPCHK(hipSetDevice(c->device));
-    gac_chainset *cs = new gac_chainset();
     cs->ctx = c;
     cs->n_chains = d->n_chains;
     cs->n_blocks = d->n_blocks;
+    cs->gap_version = 0;  // block gaps are computed at the next scoring call
+    free_whole_plan(cs);
     const size_t nb = (size_t)d->n_blocks;
-    int32_t *d_bt = nullptr;  // caller's block arrays, staged; blocks / spans / buckets are
-                              // built from them on the device (k_build_*)
-    hipError_t e = hipMalloc(&cs->chains, ch.size() * sizeof(DChain));
-    if (e == hipSuccess) e = hipMalloc(&cs->blk, (nb + 8) * sizeof(int4));
-    if (e == hipSuccess) e = hipMalloc(&cs->bucket, (size_t)std::max<int64_t>(idx_n, 1) * 4);
-    if (e == hipSuccess) e = hipMalloc(&cs->tspan, (nb + 8) * sizeof(int2));
-    if (e == hipSuccess) e = hipMalloc(&d_bt, std::max<size_t>(3 * nb, 1) * 4);
+    // the caller's block arrays, staged; blocks / spans / buckets are built
+    // from them on the device (k_build_*)
+    hipError_t e = ensure_buf((void **)&cs->chains, &cs->cap_chains, ch.size(), sizeof(DChain));
+    if (e == hipSuccess) e = ensure_buf((void **)&cs->blk, &cs->cap_blocks, nb + 8, sizeof(int4));
+    if (e == hipSuccess) e = ensure_buf((void **)&cs->tspan, &cs->cap_tspan, nb + 8, sizeof(int2));
+    if (e == hipSuccess)
+        e = ensure_buf((void **)&cs->bucket, &cs->cap_idx, (size_t)std::max<int64_t>(idx_n, 1), 4);
+    if (e == hipSuccess)
+        e = ensure_buf((void **)&cs->d_stage, &cs->cap_stage, std::max<size_t>(3 * nb, 1), 4);
+    int32_t *d_bt = cs->d_stage;
     int rc = GAC_OK;
     lap("allocations");
     if (e == hipSuccess) rc = upload_staged(c, cs->chains, ch.data(), ch.size() * sizeof(DChain));
@@ -1409,7 +1438,8 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
     // per-block N flags (scoring skips N-mask loads of N-free blocks)
     int2 *d_nlist = nullptr;  // chains whose span meets an N run (+ count)
     if (e == hipSuccess && rc == GAC_OK && (c->g[0].n_nrun || c->g[1].n_nrun)) {
-        e = hipMalloc(&d_nlist, (size_t)(n + 1) * sizeof(int2));
+        e = ensure_buf((void **)&cs->d_nlist, &cs->cap_nlist, (size_t)(n + 1), sizeof(int2));
+        d_nlist = cs->d_nlist;
         if (e == hipSuccess)
             e = launch_nflags(cs->chains, n, cs->blk, c->g[0].d_nrun, c->g[0].n_nrun,
                               c->g[1].d_nrun, c->g[1].n_nrun, c->g[1].d_woff, d_nlist + 1,
@@ -1417,15 +1447,35 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
     }
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     lap("device build + sync");
-    if (d_bt) hipFree(d_bt);
-    if (d_nlist) hipFree(d_nlist);
-    if (e != hipSuccess || rc != GAC_OK) {
+    if (rc != GAC_OK) return rc;
+    if (e != hipSuccess) return gac_fail(GAC_E_HIP, "chain upload failed: %s", hipGetErrorString(e));
+    return GAC_OK;
+}
+
+extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_chainset **out) {
+    gac_clear_error();
+    if (!c || !d || !out) return gac_fail(GAC_E_ARG, "gac_chains_upload: NULL argument");
+    CTX_LOCK(c);
+    *out = nullptr;
+    gac_chainset *cs = new gac_chainset();
+    cs->ctx = c;
+    const int rc = chains_fill(c, d, cs);
+    if (rc != GAC_OK) {
         gac_chains_free(cs);
-        if (rc != GAC_OK) return rc;
-        return gac_fail(GAC_E_HIP, "chain upload failed: %s", hipGetErrorString(e));
+        return rc;
     }
     *out = cs;
     return GAC_OK;
+}
+
+extern "C" int gac_chains_reupload(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs) {
+    gac_clear_error();
+    if (!c || !d || !cs) return gac_fail(GAC_E_ARG, "gac_chains_reupload: NULL argument");
+    if (cs->ctx != c) return gac_fail(GAC_E_ARG, "gac_chains_reupload: a set of another context");
+    CTX_LOCK(c);
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));  // (calls in flight may still read the set)
+    return chains_fill(c, d, cs);
 }
 
 extern "C" void gac_chains_free(gac_chainset *cs) {
@@ -1436,9 +1486,9 @@ extern "C" void gac_chains_free(gac_chainset *cs) {
     if (cs->blk) hipFree(cs->blk);
     if (cs->tspan) hipFree(cs->tspan);
     if (cs->bucket) hipFree(cs->bucket);
-    void *w[] = {cs->w_rdesc, cs->w_nblk, cs->w_gflat, cs->w_tile_r0, cs->w_status, cs->w_empty};
-    for (void *p : w)
-        if (p) hipFree(p);
+    if (cs->d_stage) hipFree(cs->d_stage);
+    if (cs->d_nlist) hipFree(cs->d_nlist);
+    free_whole_plan(cs);
     delete cs;
 }
 

@@ -1342,6 +1342,7 @@ typedef struct lf {
     char *cur, *end;
     const char *path;
     int64_t line;
+
     gt_chains *meta_to;
     /* first error of the chunk: message, byte position */
     int err;
@@ -1456,24 +1457,35 @@ typedef struct chunk {
  * skipped to the next "chain" header line of the chunk when only block lines
  * lie between (no '#' line, which is metadata, and a header follows); 1 =
  * skipped, 0 = parse them normally */
-static int skip_blocks(lf *f) {
-    const char *s = f->cur, *end = f->end;
-    int64_t lines = 0;
-    while (s < end) {
-        if (*s == '#')
-            return 0;
-        const char *nl = memchr(s, '\n', (size_t)(end - s));
-        if (!nl)
-            return 0;
-        ++lines;
-        s = nl + 1;
-        if (end - s >= 6 && memcmp(s, "chain", 5) == 0 && (s[5] == ' ' || s[5] == '\t')) {
-            f->cur = (char *)s;
-            f->line += lines;
-            return 1;
-        }
+/* newlines in [p, p + n), eight bytes at a time */
+static int64_t count_nl(const char *p, size_t n) {
+    int64_t k = 0;
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        memcpy(&w, p + i, 8);
+        const uint64_t x = w ^ 0x0a0a0a0a0a0a0a0aull; /* zero byte = newline */
+        k += __builtin_popcountll((x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull);
     }
-    return 0;
+    for (; i < n; ++i)
+        k += p[i] == '\n';
+    return k;
+}
+
+static int skip_blocks(lf *f) {
+    /* block lines hold only digits, tabs and newlines: the next 'c' is the
+     * next header (checked), and a '#' before it is a metadata line (then
+     * the lines are parsed normally); both found by memchr */
+    const char *s = f->cur, *end = f->end;
+    if (s >= end || *s == '#')
+        return 0;
+    const char *c = memchr(s, 'c', (size_t)(end - s));
+    if (!c || c == s || c[-1] != '\n' || end - c < 6 || memcmp(c, "chain", 5) != 0 ||
+        (c[5] != ' ' && c[5] != '\t') || memchr(s, '#', (size_t)(c - s)))
+        return 0;
+    f->line += count_nl(s, (size_t)(c - s));
+    f->cur = (char *)c;
+    return 1;
 }
 
 /* Fast path for the common block line "size[\tdt\tdq]\n" (decimal fields of
@@ -1670,26 +1682,7 @@ static void *parse_chunk(void *arg) {
         ;
     if (r < 0)
         k->err_line = k->f.line;
-    /* newlines of the whole chunk (for the next chunks' line numbers) */
-    return NULL;
-}
-
-typedef struct nl_job {
-    const char *a, *b;
-    int64_t n;
-} nl_job;
-
-static void *count_newlines(void *arg) {
-    nl_job *j = arg;
-    int64_t n = 0;
-    for (const char *p = j->a; p < j->b;) {
-        const char *q = memchr(p, '\n', (size_t)(j->b - p));
-        if (!q)
-            break;
-        ++n;
-        p = q + 1;
-    }
-    j->n = n;
+    /* (f.line now counts the chunk's lines up to where it stopped) */
     return NULL;
 }
 
@@ -1774,7 +1767,7 @@ void gt_read_chains_keep(const char *path, gt_chains *c, double stop_below, int 
 typedef struct rc_free_job {
     chunk *K;
     int nk;
-    void *NL, *cut;
+    void *cut;
     char *buf;
 } rc_free_job;
 
@@ -1783,7 +1776,6 @@ static void *rc_free_thread(void *arg) {
     for (int k = 0; k < F->nk; ++k)
         gt_chains_free(&F->K[k].c);
     free(F->K);
-    free(F->NL);
     free(F->cut);
     free(F->buf);
     free(F);
@@ -1831,20 +1823,16 @@ static void read_chains(const char *path, gt_chains *c, double stop_below, int k
     }
     cut[nk] = buf + len;
     chunk *K = calloc((size_t)nk, sizeof(chunk));
-    nl_job *NL = calloc((size_t)nk, sizeof(nl_job));
     for (int k = 0; k < nk; ++k) {
-        K[k].f = (lf){cut[k], cut[k + 1], path, 0, keep_meta ? &K[k].c : NULL, 0, {0}};
+        K[k].f = (lf){.cur = cut[k], .end = cut[k + 1], .path = path, .line = 0,
+                      .meta_to = keep_meta ? &K[k].c : NULL};
+        K[k].lines = (cut[k + 1] - cut[k]) / 8; /* (block-array size hint: a line is ~10 B) */
         K[k].stop = -1;
         K[k].stop_below = stop_below;
         K[k].tkeep = tkeep;
         K[k].qkeep = qkeep;
-        NL[k] = (nl_job){cut[k], cut[k + 1], 0};
     }
     RC_LAP("cut");
-    gt_parallel(nk, count_newlines, NL, sizeof(nl_job)); /* before parsing cuts lines */
-    for (int k = 0; k < nk; ++k)
-        K[k].lines = NL[k].n;
-    RC_LAP("count lines");
     gt_parallel(nk, parse_chunk, K, sizeof(chunk));
     RC_LAP("parse");
     /* stitch in file order up to the first error or stop: a serial pass for
@@ -1897,7 +1885,7 @@ static void read_chains(const char *path, gt_chains *c, double stop_below, int k
                 gt_chains_free(&K[j].c);
             gt_abort("%s", msg);
         }
-        line0 += NL[k].n;
+        line0 += ch->f.line; /* (a chunk that errs or stops is the last one used) */
         if (ch->stop >= 0)
             break;
     }
@@ -1925,7 +1913,7 @@ static void read_chains(const char *path, gt_chains *c, double stop_below, int k
      * 0.2 s of page freeing on C5 at 5 M chains) are released off the
      * caller's path */
     rc_free_job *F = malloc(sizeof(*F));
-    *F = (rc_free_job){K, nk, NL, cut, buf};
+    *F = (rc_free_job){K, nk, cut, buf};
     pthread_attr_t at;
     pthread_attr_init(&at);
     pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
@@ -2123,7 +2111,7 @@ void gt_read_sizes(const char *path, gt_sizes *s) {
     memset(s, 0, sizeof(*s));
     size_t len;
     char *buf = gt_slurp(path, &len);
-    lf f = {buf, buf + len, path, 0, NULL, 0, {0}};
+    lf f = {.cur = buf, .end = buf + len, .path = path, .line = 0};
     int32_t cap = 0;
     char *row[3];
     int wc;

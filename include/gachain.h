@@ -151,6 +151,11 @@ int gac_genome_decode(gac_ctx *ctx, int side, int32_t index, int32_t start,
 /* ---- chains ------------------------------------------------------------- */
 /* At most 2^31 - 17 blocks per chain set (GAC_E_ARG beyond: upload in parts). */
 int gac_chains_upload(gac_ctx *ctx, const gac_chainset_desc *d, gac_chainset **out);
+/* Replace the contents of an uploaded set with d, reusing its device memory
+ * when it is large enough (for callers that score a changing handful of
+ * chains many times, e.g. chainCleaner's modified chains: no allocation or
+ * free per call). Waits for calls still using the set. */
+int gac_chains_reupload(gac_ctx *ctx, const gac_chainset_desc *d, gac_chainset *cs);
 void gac_chains_free(gac_chainset *cs);
 int64_t gac_chains_block_count(const gac_chainset *cs);
 
