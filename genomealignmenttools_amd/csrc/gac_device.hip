@@ -30,6 +30,8 @@ hipError_t launch_tilemap(const ScoreArgs &a, hipStream_t s);
 hipError_t launch_tile(const ScoreArgs &a, int grid, hipStream_t s);
 hipError_t launch_combine(const ScoreArgs &a, int grid, hipStream_t s);
 hipError_t launch_small(const ScoreArgs &a, const Range *rin, SmallOut *out, hipStream_t s);
+hipError_t launch_small_host(const ScoreArgs &a, const RangeDesc *hin, const int4 *pool,
+                             SmallOut *out, hipStream_t s);
 struct SeqDev {
     int64_t byte_off;
     int64_t word_off;
@@ -171,6 +173,11 @@ struct gac_ctx {
     Range *d_small_in = nullptr;     // their device addresses
     SmallOut *d_small_out = nullptr;
     int small_max = kSmallMax;       // batches up to this size take k_small (GAC_SMALL_MAX)
+    // gac_score_ranges_host: planned ranges and their window records, pinned
+    // and mapped (the kernel reads them over the bus), grown on demand
+    RangeDesc *h_hq = nullptr, *d_hq = nullptr;  // [kSmallMax]
+    int4 *h_pool = nullptr, *d_pool = nullptr;
+    int64_t pool_cap = 0;
     int32_t mat[16] = {0};           // the current scoring setup (gac_set_scoring)
     gac_gapcalc *gap_src = nullptr;
     int32_t *h_stat = nullptr;   // pinned, coherent host words written by k_scan_agg [8]
@@ -333,6 +340,8 @@ extern "C" void gac_close(gac_ctx *c) {
     gac_gapcalc_free(c->gap_src);
     if (c->h_small_in) hipHostFree(c->h_small_in);
     if (c->h_small_out) hipHostFree(c->h_small_out);
+    if (c->h_hq) hipHostFree(c->h_hq);
+    if (c->h_pool) hipHostFree(c->h_pool);
     for (int k = 0; k < 2; ++k) {
         if (c->pin[k]) hipHostFree(c->pin[k]);
         if (c->pin_ev[k]) hipEventDestroy(c->pin_ev[k]);
@@ -1857,6 +1866,120 @@ extern "C" int gac_score_ranges_device(gac_ctx *c, const gac_chainset *cs, const
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     return score_device(c, cs, (const Range *)d_ranges, n, flags, (long long *)d_g,
                         (long long *)d_l, d_ali, s);
+}
+
+// ranges of chains given in host memory: planned here (window by binary
+// search over the chain's block starts/ends), scored by k_small<HOST> reading
+// the window records from pinned mapped memory, 256 ranges per launch
+extern "C" int gac_score_ranges_host(gac_ctx *c, const gac_chainset_desc *d, const gac_range *r,
+                                     int64_t n, uint32_t flags, int64_t *global, int64_t *local,
+                                     int32_t *ali) {
+    gac_clear_error();
+    if (!c || !d) return gac_fail(GAC_E_ARG, "gac_score_ranges_host: NULL argument");
+    CTX_LOCK(c);
+    if (n < 0) return gac_fail(GAC_E_ARG, "negative range count");
+    if (n == 0) return GAC_OK;
+    if (!r || !global || !ali || ((flags & GAC_WANT_LOCAL) && !local))
+        return gac_fail(GAC_E_ARG, "NULL buffer");
+    if (!c->scoring) return gac_fail(GAC_E_STATE, "gac_set_scoring() not called");
+    if (!c->g[0].final || !c->g[1].final)
+        return gac_fail(GAC_E_STATE, "load both genomes before scoring");
+    HIPCHK(hipSetDevice(c->device));
+    if (!c->h_hq) {
+        HIPCHK(hipHostMalloc((void **)&c->h_hq, kSmallMax * sizeof(RangeDesc), hipHostMallocMapped));
+        HIPCHK(hipHostGetDevicePointer((void **)&c->d_hq, c->h_hq, 0));
+    }
+    const Genome &T = c->g[0], &Q = c->g[1];
+    ScoreArgs a;
+    memset(&a, 0, sizeof(a));
+    a.t_planes = T.planes;
+    a.t_nmask = T.nmask;
+    a.t_woff = T.d_woff;
+    a.q_planes = Q.planes;
+    a.q_nmask = Q.nmask;
+    a.q_woff = Q.d_woff;
+    a.want_local = (flags & GAC_WANT_LOCAL) ? 1 : 0;
+    a.gap_len = c->gap_len;
+    a.gap_tab = c->d_gap_tab;
+    a.small_tab = c->d_small;
+    memcpy(a.coef, c->coef, sizeof(a.coef));
+    a.sym = c->sym;
+    a.gap = c->gap;
+    hipStream_t s = c->stream;
+    for (int64_t i0 = 0; i0 < n; i0 += kSmallMax) {
+        const int64_t m = std::min<int64_t>(kSmallMax, n - i0);
+        // windows (and their checks) first, to size the pool
+        int64_t lo[kSmallMax], hi[kSmallMax], tot = 0;
+        for (int64_t k = 0; k < m; ++k) {
+            const gac_range &q = r[i0 + k];
+            if (q.chain < 0 || q.chain >= d->n_chains)
+                return gac_fail(GAC_E_ARG, "range %lld: chain %d out of range",
+                                (long long)(i0 + k), q.chain);
+            const int64_t b0 = d->blk_off[q.chain], b1 = d->blk_off[q.chain + 1];
+            int64_t a0 = b0, a1 = b1;  // first block ending past s
+            while (a0 < a1) {
+                const int64_t mid = (a0 + a1) >> 1;
+                if ((int64_t)d->blk_t[mid] + d->blk_size[mid] > q.t_start) a1 = mid;
+                else a0 = mid + 1;
+            }
+            int64_t e0 = a0, e1 = b1;  // first block starting at or past e
+            while (e0 < e1) {
+                const int64_t mid = (e0 + e1) >> 1;
+                if (d->blk_t[mid] >= q.t_end) e1 = mid;
+                else e0 = mid + 1;
+            }
+            lo[k] = a0;
+            hi[k] = std::max(a0, e0);
+            tot += hi[k] - lo[k];
+        }
+        if (tot > c->pool_cap) {
+            if (c->h_pool) hipHostFree(c->h_pool);
+            c->h_pool = nullptr;
+            c->pool_cap = 0;
+            const int64_t cap = tot + tot / 2 + 1024;
+            HIPCHK(hipHostMalloc((void **)&c->h_pool, cap * sizeof(int4), hipHostMallocMapped));
+            HIPCHK(hipHostGetDevicePointer((void **)&c->d_pool, c->h_pool, 0));
+            c->pool_cap = cap;
+        }
+        int64_t j = 0;
+        for (int64_t k = 0; k < m; ++k) {
+            const gac_range &q = r[i0 + k];
+            const int32_t ts = d->t_seq[q.chain], qs = d->q_seq[q.chain];
+            if (ts < 0 || ts >= (int32_t)T.sizes.size() || qs < 0 || qs >= (int32_t)Q.sizes.size())
+                return gac_fail(GAC_E_ARG, "chain %d: sequence index out of range", q.chain);
+            const int64_t tsize = T.sizes[ts], qsize = Q.sizes[qs];
+            RangeDesc &h = c->h_hq[k];
+            h.tbase = T.woff[ts] * 32;
+            const int64_t qw = Q.woff[qs] * 32;
+            h.qbase = d->q_strand[q.chain] ? ~(qw + qsize) : qw;
+            h.b0 = (int32_t)j;
+            h.nblk = (int32_t)(hi[k] - lo[k]);
+            h.s = q.t_start;
+            h.e = q.t_end;
+            int64_t pt = 0, pq = 0;
+            for (int64_t b = lo[k]; b < hi[k]; ++b, ++j) {
+                const int64_t t = d->blk_t[b], qq = d->blk_q[b], z = d->blk_size[b];
+                if (z < 0 || z >= (1 << 29) || t < 0 || qq < 0 || t + z > tsize || qq + z > qsize ||
+                    (b > lo[k] && (t < pt || qq < pq)))
+                    return gac_fail(GAC_E_FORMAT, "chain %d: block [t %lld q %lld size %lld] "
+                                    "outside its sequences or not ascending", q.chain,
+                                    (long long)t, (long long)qq, (long long)z);
+                pt = t + z;
+                pq = qq + z;
+                c->h_pool[j] = make_int4((int)t, (int)qq, (int)z, 0);
+            }
+        }
+        a.n = m;
+        HIPCHK(launch_small_host(a, c->d_hq, c->d_pool, c->d_small_out, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (int64_t k = 0; k < m; ++k) {
+            const SmallOut o = c->h_small_out[k];
+            global[i0 + k] = o.g;
+            ali[i0 + k] = o.ali;
+            if (flags & GAC_WANT_LOCAL) local[i0 + k] = o.l;
+        }
+    }
+    return GAC_OK;
 }
 
 extern "C" int gac_score_ranges(gac_ctx *c, const gac_chainset *cs, const gac_range *ranges,

@@ -1121,12 +1121,17 @@ __global__ void __launch_bounds__(256) k_fold_super(ScoreArgs a) {
 // time (lane = block, the block's 32-base chunks in turn) and folds global,
 // aligned bases and the local-score element in block order.  No workspace,
 // no scans across workgroups: a call costs one launch.
-template <bool LOCAL, bool SYM>
-__global__ void __launch_bounds__(256) k_small(ScoreArgs a, const Range *rin, SmallOut *out) {
+// HOST: the ranges of chains held in (mapped, pinned) host memory --
+// descriptors already planned by the host (b0 = the window's first record in
+// `pool`, records {tStart, qStart, size, 0}); the gaps are computed here from
+// the next record and every chunk takes the N-mask path (no upload flags).
+template <bool LOCAL, bool SYM, bool HOST>
+__global__ void __launch_bounds__(256) k_small(ScoreArgs a, const Range *rin, const RangeDesc *hin,
+                                               const int4 *pool, SmallOut *out) {
     const int lane = threadIdx.x & 63;
     const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (w >= a.n) return;
-    const RangeDesc d = plan_range(a, rin[w]);
+    const RangeDesc d = HOST ? hin[w] : plan_range(a, rin[w]);
     const bool minus = d.qbase < 0;
     long long gsum = 0, asum = 0;
     Elem acc = {0, kNeg, kNeg, kNeg};
@@ -1136,9 +1141,21 @@ __global__ void __launch_bounds__(256) k_small(ScoreArgs a, const Range *rin, Sm
         int va = 0;
         Elem e = {0, kNeg, kNeg, kNeg};
         if (k < d.nblk) {
-            const int4 bk = a.blk[d.b0 + k];  // {tStart, qStart, size | N flags, gap to next}
+            // {tStart, qStart, size | N flags, gap to next}
+            int4 bk = HOST ? pool[d.b0 + k] : a.blk[d.b0 + k];
             const bool last = (k == d.nblk - 1);
             const int z = bk.z & kSizeMask;
+            if (HOST) {
+                bk.w = 0;
+                if (!last) {
+                    const int4 nx = pool[d.b0 + k + 1];
+                    int dd;
+                    const int which = gap_kind(nx.y - (bk.y + z), nx.x - (bk.x + z), dd);
+                    bk.w = dd < a.gap_len ? a.gap_tab[which * a.gap_len + dd]
+                                          : gap_cost_wd(a.gap, a.small_tab, which, dd);
+                }
+                bk.z = z | kTHasN | kQHasN;
+            }
             int cts = bk.x, cqs = bk.y, cte = bk.x + z;
             if (cts < d.s) {
                 cqs += d.s - cts;
@@ -1361,15 +1378,27 @@ hipError_t launch_tile(const ScoreArgs &a, int grid, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_small(const ScoreArgs &a, const Range *rin, SmallOut *out, hipStream_t s) {
+template <bool HOST>
+static void launch_small_t(const ScoreArgs &a, const Range *rin, const RangeDesc *hin,
+                           const int4 *pool, SmallOut *out, hipStream_t s) {
     const dim3 g((unsigned)((a.n + kWavesPerWG - 1) / kWavesPerWG)), b(256);
     if (a.want_local) {
-        if (a.sym) hipLaunchKernelGGL((k_small<true, true>), g, b, 0, s, a, rin, out);
-        else hipLaunchKernelGGL((k_small<true, false>), g, b, 0, s, a, rin, out);
+        if (a.sym) k_small<true, true, HOST><<<g, b, 0, s>>>(a, rin, hin, pool, out);
+        else k_small<true, false, HOST><<<g, b, 0, s>>>(a, rin, hin, pool, out);
     } else {
-        if (a.sym) hipLaunchKernelGGL((k_small<false, true>), g, b, 0, s, a, rin, out);
-        else hipLaunchKernelGGL((k_small<false, false>), g, b, 0, s, a, rin, out);
+        if (a.sym) k_small<false, true, HOST><<<g, b, 0, s>>>(a, rin, hin, pool, out);
+        else k_small<false, false, HOST><<<g, b, 0, s>>>(a, rin, hin, pool, out);
     }
+}
+
+hipError_t launch_small(const ScoreArgs &a, const Range *rin, SmallOut *out, hipStream_t s) {
+    launch_small_t<false>(a, rin, nullptr, nullptr, out, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_small_host(const ScoreArgs &a, const RangeDesc *hin, const int4 *pool,
+                             SmallOut *out, hipStream_t s) {
+    launch_small_t<true>(a, nullptr, hin, pool, out, s);
     return hipGetLastError();
 }
 

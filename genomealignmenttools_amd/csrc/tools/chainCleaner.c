@@ -437,7 +437,6 @@ typedef struct state {
     int32_t *id2ich_val;
     gac_ctx *ctx;
     gac_chainset *cs_base; /* every chain of interest as read (version 0) */
-    gac_chainset *cs_scratch; /* modified chains of one scoring call (refilled) */
     int32_t *t_seq, *q_seq;
     uint8_t *strand;
 } state;
@@ -720,14 +719,11 @@ static void score_keys(state *S, const qkey *in, int64_t n) {
             off[k + 1] = off[k] + x->nb;
         }
         gac_chainset_desc d = {ns, ts, qs, st, off, nbk, bt, bq, bs};
-        /* one scratch set for all modified chains, refilled in place */
-        if (S->cs_scratch)
-            gt_check(gac_chains_reupload(S->ctx, &d, S->cs_scratch));
-        else
-            gt_check(gac_chains_upload(S->ctx, &d, &S->cs_scratch));
+        /* the modified chains' current blocks stay on the host: their
+         * windows are read by the kernel over the bus (no upload) */
         ++g_uploads;
-        gt_check(gac_score_ranges(S->ctx, S->cs_scratch, rb + n0, m - n0, GAC_WANT_LOCAL, g + n0,
-                                  l + n0, a + n0));
+        gt_check(gac_score_ranges_host(S->ctx, &d, rb + n0, m - n0, GAC_WANT_LOCAL, g + n0,
+                                       l + n0, a + n0));
         ++g_gpu_calls;
         g_gpu_ranges += m - n0;
         free(sel);
@@ -1569,7 +1565,6 @@ int main(int argc, char *argv[]) {
                (long long)g_gpu_calls, (long long)g_gpu_ranges, (long long)g_uploads, g_gpu_s);
     gt_verbose(1, "\nALL DONE. New chains are in %s. Deleted suspects in %s\n", out_chain, out_bed);
     gac_chains_free(S.cs_base);
-    gac_chains_free(S.cs_scratch);
     gac_close(S.ctx);
     gt_exit_ok(); /* host state is left to process exit */
 }

@@ -168,7 +168,9 @@ class Engine:
         return self.upload_chain_arrays(tidx, qidx, ca.qstrand, ca.blk_off, ca.blk_t, ca.blk_q,
                                         ca.blk_size)
 
-    def upload_chain_arrays(self, t_seq, q_seq, q_strand, blk_off, blk_t, blk_q, blk_size) -> ChainSet:
+    @staticmethod
+    def _desc(t_seq, q_seq, q_strand, blk_off, blk_t, blk_q, blk_size):
+        """(gac_chainset_desc, the arrays it points into: keep them alive)"""
         arrs = [np.ascontiguousarray(t_seq, np.int32), np.ascontiguousarray(q_seq, np.int32),
                 np.ascontiguousarray(q_strand, np.uint8), np.ascontiguousarray(blk_off, np.int64),
                 np.ascontiguousarray(blk_t, np.int32), np.ascontiguousarray(blk_q, np.int32),
@@ -178,9 +180,35 @@ class Engine:
         d.t_seq, d.q_seq, d.q_strand, d.blk_off = (_p(a) for a in arrs[:4])
         d.n_blocks = len(arrs[4])
         d.blk_t, d.blk_q, d.blk_size = (_p(a) for a in arrs[4:])
+        return d, arrs
+
+    def upload_chain_arrays(self, t_seq, q_seq, q_strand, blk_off, blk_t, blk_q, blk_size) -> ChainSet:
+        d, arrs = self._desc(t_seq, q_seq, q_strand, blk_off, blk_t, blk_q, blk_size)
         h = C.c_void_p()
         check(lib().gac_chains_upload(self.h, C.byref(d), C.byref(h)))
         return ChainSet(self, h, d.n_chains, d.n_blocks, int(arrs[6].sum(dtype=np.int64)))
+
+    def reupload_chain_arrays(self, cs: ChainSet, t_seq, q_seq, q_strand, blk_off, blk_t, blk_q,
+                              blk_size) -> ChainSet:
+        """gac_chains_reupload: cs now holds these chains (its memory reused)."""
+        d, arrs = self._desc(t_seq, q_seq, q_strand, blk_off, blk_t, blk_q, blk_size)
+        check(lib().gac_chains_reupload(self.h, C.byref(d), cs.handle))
+        cs.n_chains, cs.n_blocks = d.n_chains, d.n_blocks
+        return cs
+
+    def score_ranges_host(self, t_seq, q_seq, q_strand, blk_off, blk_t, blk_q, blk_size,
+                          ranges: np.ndarray, want_local: bool = False):
+        """gac_score_ranges_host: ranges of chains held in host memory."""
+        d, arrs = self._desc(t_seq, q_seq, q_strand, blk_off, blk_t, blk_q, blk_size)
+        r = np.ascontiguousarray(np.asarray(ranges, dtype=np.int32).reshape(-1, 3))
+        n = r.shape[0]
+        g = np.zeros(n, np.int64)
+        ali = np.zeros(n, np.int32)
+        loc = np.zeros(n, np.int64) if want_local else None
+        check(lib().gac_score_ranges_host(self.h, C.byref(d), _p(r), n,
+                                          GAC_WANT_LOCAL if want_local else 0, _p(g),
+                                          _p(loc) if want_local else None, _p(ali)))
+        return g, loc, ali
 
     # ---- scoring
     def score_ranges(self, cs: ChainSet, ranges: np.ndarray, want_local: bool = False):

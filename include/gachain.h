@@ -157,6 +157,15 @@ int gac_chains_upload(gac_ctx *ctx, const gac_chainset_desc *d, gac_chainset **o
  * free per call). Waits for calls still using the set. */
 int gac_chains_reupload(gac_ctx *ctx, const gac_chainset_desc *d, gac_chainset *cs);
 void gac_chains_free(gac_chainset *cs);
+/* gac_score_ranges for chains held in host memory (no upload): each range is
+ * planned on the host (its window of blocks found by binary search) and the
+ * windows are scored by one kernel launch per 256 ranges reading them from
+ * pinned mapped memory, gap costs and N masks on the device.  For callers
+ * that score a few sub-chains of chains they keep changing (chainCleaner's
+ * modified chains).  Results as gac_score_ranges. */
+int gac_score_ranges_host(gac_ctx *ctx, const gac_chainset_desc *d, const gac_range *ranges,
+                          int64_t n, uint32_t flags, int64_t *global, int64_t *local,
+                          int32_t *ali);
 int64_t gac_chains_block_count(const gac_chainset *cs);
 
 /* ---- scoring ------------------------------------------------------------ */

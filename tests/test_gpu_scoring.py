@@ -205,6 +205,62 @@ def test_whole_chains_vs_ranges(want_local):
     e.close()
 
 
+@pytest.mark.parametrize("seed", [4, 5])
+def test_host_ranges_and_reupload(seed):
+    """gac_score_ranges_host (chains left in host memory: windows planned on
+    the host, read by the kernel over the bus, gaps and N masks on the
+    device) and gac_chains_reupload (a set refilled in place, smaller then
+    larger than its buffers) equal the oracle, on N-rich genomes, both
+    strands, more than 256 ranges (several launches), empty windows and
+    ranges beyond the chain -- and on chains with blocks removed, as
+    chainCleaner's modified chains are."""
+    from genomealignmenttools_amd import synth
+    from genomealignmenttools_amd.chainfile import ChainArrays
+    from genomealignmenttools_amd.gachain import GAC_Q, GAC_T
+    tg, qg, ca = synth.small_case(seed=seed, n_chains=300, max_blocks=400, n_frac=0.05)
+    e, cs = _setup(None, tg, qg, ca)
+    orc = _oracle(tg, qg)
+    R = _ranges(ca, np.random.default_rng(seed), per_chain=3)
+    tix = np.array([e.seq_index(GAC_T, x) for x in ca.tname], np.int32)
+    qix = np.array([e.seq_index(GAC_Q, x) for x in ca.qname], np.int32)
+    arrs = (tix, qix, ca.qstrand, ca.blk_off, ca.blk_t, ca.blk_q, ca.blk_size)
+    og, ol, oa = orc.score_ranges(ca, R)
+    g, l, a = e.score_ranges_host(*arrs, R, want_local=True)
+    assert len(R) > 256
+    assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
+    # every other inner block run removed (chainRemoveBlocks keeps the ends)
+    rng = np.random.default_rng(seed + 10)
+    keep = np.ones(ca.blk_off[-1], bool)
+    for c in range(ca.n):
+        b0, b1 = ca.blk_off[c], ca.blk_off[c + 1]
+        if b1 - b0 > 4 and rng.random() < 0.5:
+            x = int(rng.integers(b0 + 1, b1 - 2))
+            keep[x:x + int(rng.integers(1, min(4, b1 - 1 - x) + 1))] = False
+    nb = np.add.reduceat(keep.astype(np.int64), ca.blk_off[:-1]) if ca.n else np.zeros(0)
+    off2 = np.concatenate([[0], np.cumsum(nb)]).astype(np.int64)
+    ca2 = ChainArrays(score=ca.score, tname=ca.tname, tsize=ca.tsize, tstart=ca.tstart,
+                      tend=ca.tend, qname=ca.qname, qsize=ca.qsize, qstrand=ca.qstrand,
+                      qstart=ca.qstart, qend=ca.qend, id=ca.id, blk_off=off2,
+                      blk_t=ca.blk_t[keep], blk_q=ca.blk_q[keep], blk_size=ca.blk_size[keep])
+    arrs2 = (tix, qix, ca.qstrand, off2, ca2.blk_t, ca2.blk_q, ca2.blk_size)
+    og2, ol2, oa2 = orc.score_ranges(ca2, R)
+    g, l, a = e.score_ranges_host(*arrs2, R, want_local=True)
+    assert np.array_equal(g, og2) and np.array_equal(l, ol2) and np.array_equal(a, oa2)
+    # the same through a refilled set: the subset (smaller), then the full set again
+    e.reupload_chain_arrays(cs, *arrs2)
+    g, l, a = e.score_ranges(cs, R, want_local=True)
+    assert np.array_equal(g, og2) and np.array_equal(l, ol2) and np.array_equal(a, oa2)
+    g, l, a = e.score_chains(cs, want_local=True)
+    full = np.stack([np.arange(ca.n), ca2.tstart, ca2.tend], 1)
+    fg, fl, fa = orc.score_ranges(ca2, full)
+    assert np.array_equal(g, fg) and np.array_equal(l, fl) and np.array_equal(a, fa)
+    e.reupload_chain_arrays(cs, *arrs)
+    g, l, a = e.score_ranges(cs, R, want_local=True)
+    assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
+    cs.close()
+    e.close()
+
+
 def test_edge_ranges():
     """Empty windows, single-base windows, ranges ending inside blocks,
     1-bp blocks, ranges beyond the chain."""
