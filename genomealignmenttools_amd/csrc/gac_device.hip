@@ -65,6 +65,13 @@ hipError_t launch_whole_plan(const DChain *chains, int64_t n, RangeDesc *rdesc, 
                              int32_t *gflat, int32_t *tile_r0, hipStream_t s);
 hipError_t launch_zero_list(const int32_t *list, int64_t n, long long *g, long long *l,
                             int32_t *ali, hipStream_t s);
+hipError_t launch_whole_plan_sorted(const DChain *chains, int64_t n, int32_t *perm,
+                                    unsigned long long *keys, int32_t *vals, RangeDesc *rdesc,
+                                    int32_t *nblk, int32_t *gflat, int32_t *pb0,
+                                    int32_t *tile_r0, int32_t *inv, void *tmp,
+                                    size_t &tmp_bytes, hipStream_t s);
+hipError_t launch_unpermute(const int32_t *inv, const SmallOut *pack, int64_t n, long long *g,
+                            long long *l, int32_t *ali, hipStream_t s);
 hipError_t launch_text_blocks(const uint8_t *text, const TextJob *jobs, int64_t n, const M25 &m,
                               long long *out, hipStream_t s);
 hipError_t launch_text_xover(const uint8_t *text, const TextXJob *jobs, int64_t n, const M25 &m,
@@ -216,6 +223,13 @@ struct gac_chainset {
     int32_t *w_status = nullptr;   // {W, T, 0, 0}
     int32_t *w_empty = nullptr;    // chains without blocks (their results are 0)
     int64_t w_nempty = 0;
+    // target-ordered plan (k_whole_keys): positions p are chains in target
+    // order; w_pb0[p] their first blocks, results packed per position and
+    // scattered back through w_inv (chain -> position, -1 without blocks)
+    bool w_sorted = false;
+    int32_t *w_pb0 = nullptr;
+    int32_t *w_inv = nullptr;
+    SmallOut *w_pack = nullptr;
     // capacities (gac_chains_reupload refills these buffers when they fit)
     size_t cap_chains = 0, cap_blocks = 0, cap_tspan = 0, cap_idx = 0;
     int32_t *d_stage = nullptr;  // the caller's block arrays, staged (3 x blocks)
@@ -225,11 +239,15 @@ struct gac_chainset {
 };
 
 static void free_whole_plan(gac_chainset *cs) {
-    void *w[] = {cs->w_rdesc, cs->w_nblk, cs->w_gflat, cs->w_tile_r0, cs->w_status, cs->w_empty};
+    void *w[] = {cs->w_rdesc, cs->w_nblk,  cs->w_gflat, cs->w_tile_r0, cs->w_status,
+                 cs->w_empty, cs->w_pb0,   cs->w_inv,   cs->w_pack};
     for (void *p : w)
         if (p) hipFree(p);
     cs->w_rdesc = nullptr;
     cs->w_nblk = cs->w_gflat = cs->w_tile_r0 = cs->w_status = cs->w_empty = nullptr;
+    cs->w_pb0 = cs->w_inv = nullptr;
+    cs->w_pack = nullptr;
+    cs->w_sorted = false;
     cs->w_nempty = 0;
     cs->w_ready = false;
 }
@@ -1745,9 +1763,45 @@ static int ensure_whole(gac_ctx *c, gac_chainset *cs, hipStream_t s) {
     HIPCHK(hipMalloc(&cs->w_gflat, std::max<int64_t>(n, 1) * 4));
     HIPCHK(hipMalloc(&cs->w_tile_r0, std::max<int64_t>(T, 1) * 4));
     HIPCHK(hipMalloc(&cs->w_status, kStatusBytes));
-    HIPCHK(launch_whole_plan(cs->chains, n, cs->w_rdesc, cs->w_nblk, cs->w_gflat, cs->w_tile_r0, s));
     const int32_t st[8] = {(int32_t)nb, (int32_t)T, 0, 0, 0, 0, 0, 0};
     HIPCHK(hipMemcpyAsync(cs->w_status, st, sizeof(st), hipMemcpyHostToDevice, s));
+    // target order for sets of >= 4096 chains; GAC_WHOLE_ORDER=set / =target
+    // forces either (A/B, tests)
+    const char *ord = getenv("GAC_WHOLE_ORDER");
+    const bool sorted = ord && !strcmp(ord, "target") ? true
+                        : ord && !strcmp(ord, "set") ? false
+                                                     : n >= 4096;
+    if (sorted) {
+        HIPCHK(hipMalloc(&cs->w_pb0, n * 4));
+        HIPCHK(hipMalloc(&cs->w_inv, n * 4));
+        HIPCHK(hipMalloc(&cs->w_pack, n * sizeof(SmallOut)));
+        unsigned long long *keys = nullptr;
+        int32_t *vals = nullptr, *perm = nullptr;
+        void *tmp = nullptr;
+        size_t tmp_bytes = 0;
+        int rc = GAC_OK;
+        hipError_t e = launch_whole_plan_sorted(cs->chains, n, nullptr, nullptr, nullptr, nullptr,
+                                                cs->w_nblk, cs->w_gflat, nullptr, nullptr, nullptr,
+                                                nullptr, tmp_bytes, s);
+        if (e == hipSuccess) e = hipMalloc(&keys, 2 * n * sizeof(unsigned long long));
+        if (e == hipSuccess) e = hipMalloc(&vals, 2 * n * 4);
+        perm = vals ? vals + n : nullptr;
+        if (e == hipSuccess) e = hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 16));
+        if (e == hipSuccess)
+            e = launch_whole_plan_sorted(cs->chains, n, perm, keys, vals, cs->w_rdesc, cs->w_nblk,
+                                         cs->w_gflat, cs->w_pb0, cs->w_tile_r0, cs->w_inv, tmp,
+                                         tmp_bytes, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = gac_fail(GAC_E_HIP, "whole-chain plan: %s", hipGetErrorString(e));
+        if (keys) hipFree(keys);
+        if (vals) hipFree(vals);
+        if (tmp) hipFree(tmp);
+        if (rc != GAC_OK) return rc;
+        cs->w_sorted = true;
+        cs->w_ready = true;
+        return GAC_OK;
+    }
+    HIPCHK(launch_whole_plan(cs->chains, n, cs->w_rdesc, cs->w_nblk, cs->w_gflat, cs->w_tile_r0, s));
     // chains without blocks: their results are zeroed by every call
     std::vector<int32_t> nblk(n);
     HIPCHK(hipMemcpyAsync(nblk.data(), cs->w_nblk, n * 4, hipMemcpyDeviceToHost, s));
@@ -1784,7 +1838,8 @@ static int score_whole(gac_ctx *c, const gac_chainset *cs_in, uint32_t flags, lo
     a.rdesc = cs->w_rdesc;
     a.nblk = cs->w_nblk;
     a.gflat = cs->w_gflat;
-    a.pb0 = cs->w_gflat;
+    a.pb0 = cs->w_sorted ? cs->w_pb0 : cs->w_gflat;
+    a.out_pack = cs->w_sorted ? cs->w_pack : nullptr;
     a.tile_r0 = cs->w_tile_r0;
     a.status = cs->w_status;
     a.sum_head = c->sum_head;
@@ -1793,7 +1848,8 @@ static int score_whole(gac_ctx *c, const gac_chainset *cs_in, uint32_t flags, lo
     a.sup_tail = c->sup_tail;
     a.sup_tail_r = c->sup_tail_r;
     a.cap_tiles = (int32_t)(c->ws_tiles < INT32_MAX ? c->ws_tiles : INT32_MAX);
-    HIPCHK(launch_zero_list(cs->w_empty, cs->w_nempty, d_g, a.want_local ? d_l : nullptr, d_ali, s));
+    if (!cs->w_sorted)
+        HIPCHK(launch_zero_list(cs->w_empty, cs->w_nempty, d_g, a.want_local ? d_l : nullptr, d_ali, s));
     {
         PROF_BEGIN(GAC_K_TILE);
         HIPCHK(launch_tile(a, a.want_local ? c->tile_grid_l : c->tile_grid_g, s));
@@ -1802,6 +1858,9 @@ static int score_whole(gac_ctx *c, const gac_chainset *cs_in, uint32_t flags, lo
     {
         PROF_BEGIN(GAC_K_COMBINE);
         HIPCHK(launch_combine(a, c->combine_grid, s));
+        if (cs->w_sorted)
+            HIPCHK(launch_unpermute(cs->w_inv, cs->w_pack, cs->n_chains, d_g,
+                                    a.want_local ? d_l : nullptr, d_ali, s));
         PROF_END(GAC_K_COMBINE);
     }
     if (hipEventRecord(c->ws_ev, s) == hipSuccess) c->ws_last = s;

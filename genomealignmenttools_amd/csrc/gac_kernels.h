@@ -87,6 +87,14 @@ struct Range {
     int32_t chain, t_start, t_end;
 };
 
+// Result of one range of a small batch (k_small writes it straight to pinned
+// host memory); also the packed per-position result of a target-ordered
+// whole-chain plan (out_pack, scattered back to chain order by k_unpermute).
+struct SmallOut {
+    long long g, l;
+    int32_t ali, pad;
+};
+
 struct ScoreArgs {
     const uint2 *t_planes;
     const uint32_t *t_nmask;
@@ -134,14 +142,10 @@ struct ScoreArgs {
                                // t0<<2 | d1<<1 | d0 (set bits = factors)
     int32_t sym;               // matrix is strand-symmetric: coef[8..15] == 0
     GapDev gap;
+    SmallOut *out_pack;  // non-null: results go to out_pack[range] (the whole-chain
+                         // plan in target order; k_unpermute restores chain order)
 };
 
-// Result of one range of a small batch (k_small writes it straight to pinned
-// host memory).
-struct SmallOut {
-    long long g, l;
-    int32_t ali, pad;
-};
 constexpr int kSmallMax = 256;  // ranges per small-batch call
 
 // One run of a sparse genome upload (bytes): its place in the staging layout

@@ -30,6 +30,7 @@
 // All sums are int64: every addend of the reference's double accumulation is
 // an integer, so integer arithmetic is exact and bit-identical.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 #include <algorithm>
 #include <stdint.h>
 #include <stdlib.h>
@@ -637,6 +638,70 @@ __global__ void __launch_bounds__(256) k_whole_plan(const DChain *chains, int64_
         tile_r0[t] = (int32_t)c;
 }
 
+// The same plan with the chains in target order (position p = chain perm[p]):
+// chains that overlap on the target are scored by neighbouring tiles, so an
+// XCD's L2 (and the Infinity Cache) serves their shared target-plane lines
+// once instead of once per chain.  Flat offsets are the scan of the permuted
+// block counts; results go to out_pack[p] and k_unpermute scatters them back.
+constexpr int kOrderBits = 36;  // sort key bits: global target base of the chain start
+
+__global__ void __launch_bounds__(256) k_whole_keys(const DChain *chains, int64_t n,
+                                                    unsigned long long *key, int32_t *val) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const DChain ch = chains[c];
+    key[c] = ch.nblk > 0 ? (unsigned long long)(ch.tbase + ch.tstart)
+                         : (1ull << kOrderBits) - 1;  // empty chains last
+    val[c] = (int32_t)c;
+}
+
+__global__ void __launch_bounds__(256) k_whole_count(const DChain *chains, const int32_t *perm,
+                                                     int64_t n, int32_t *nblk) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    nblk[p] = chains[perm[p]].nblk;
+}
+
+__global__ void __launch_bounds__(256) k_whole_plan_sorted(const DChain *chains,
+                                                           const int32_t *perm, int64_t n,
+                                                           const int32_t *gflat, RangeDesc *rdesc,
+                                                           int32_t *pb0, int32_t *tile_r0,
+                                                           int32_t *inv) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const int32_t c = perm[p];
+    const DChain ch = chains[c];
+    RangeDesc d;
+    d.tbase = ch.tbase;
+    d.qbase = ch.qbase;
+    d.b0 = (int32_t)ch.blk_off;
+    d.nblk = ch.nblk;
+    d.s = ch.tstart;
+    d.e = ch.tend;
+    rdesc[p] = d;
+    pb0[p] = (int32_t)ch.blk_off;
+    inv[c] = ch.nblk > 0 ? (int32_t)p : -1;
+    const int64_t g = gflat[p], end = g + ch.nblk;
+    for (int64_t t = (g + kTileBlocks - 1) / kTileBlocks; t * kTileBlocks < end; ++t)
+        tile_r0[t] = (int32_t)p;
+}
+
+// out[c] = out_pack[inv[c]] (0 for chains without blocks): one random
+// 24-B record per chain, from a buffer just written (Infinity-Cache resident
+// at these sizes), coalesced stores
+__global__ void __launch_bounds__(256) k_unpermute(const int32_t *inv, const SmallOut *pack,
+                                                   int64_t n, long long *g, long long *l,
+                                                   int32_t *ali) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const int32_t p = inv[c];
+    SmallOut o = {0, 0, 0, 0};
+    if (p >= 0) o = pack[p];
+    g[c] = o.g;
+    ali[c] = o.ali;
+    if (l) l[c] = o.l;
+}
+
 // outputs of the ranges in `list` (chains without blocks) := 0
 __global__ void __launch_bounds__(256) k_zero_list(const int32_t *list, int64_t n, long long *g,
                                                    long long *l, int32_t *ali) {
@@ -789,6 +854,15 @@ __device__ __forceinline__ ChunkRef chunk_prep(const WaveLds &L, int j) {
 template <bool LOCAL>
 __device__ __forceinline__ void seg_store(const ScoreArgs &a, int ri, long long g, int ali,
                                           const Elem &e) {
+    if (a.out_pack) {
+        SmallOut o;
+        o.g = g;
+        o.l = LOCAL ? max2(0, max2(e.C, e.D)) : 0;
+        o.ali = ali;
+        o.pad = 0;
+        a.out_pack[ri] = o;
+        return;
+    }
     a.out_g[ri] = g;
     a.out_ali[ri] = ali;
     if (LOCAL) a.out_l[ri] = max2(0, max2(e.C, e.D));
@@ -1418,6 +1492,50 @@ hipError_t launch_whole_plan(const DChain *chains, int64_t n, RangeDesc *rdesc, 
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_whole_plan, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, chains, n,
                        rdesc, nblk, gflat, tile_r0);
+    return hipGetLastError();
+}
+
+// The target-ordered whole-chain plan (see k_whole_keys): radix sort of
+// the chains by target start, scan of the permuted block counts, then the
+// plan.  `tmp` / `tmp_bytes`: caller-owned scratch, sized by a first call
+// with tmp == nullptr (returns the bytes needed in tmp_bytes).
+hipError_t launch_whole_plan_sorted(const DChain *chains, int64_t n, int32_t *perm,
+                                    unsigned long long *keys, int32_t *vals, RangeDesc *rdesc,
+                                    int32_t *nblk, int32_t *gflat, int32_t *pb0,
+                                    int32_t *tile_r0, int32_t *inv, void *tmp,
+                                    size_t &tmp_bytes, hipStream_t s) {
+    unsigned long long *keys_out = keys + n;
+    size_t b_sort = 0, b_scan = 0;
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, b_sort, keys, keys_out, vals, perm,
+                                                      (int)n, 0, kOrderBits, s);
+    if (e != hipSuccess) return e;
+    e = hipcub::DeviceScan::ExclusiveSum(nullptr, b_scan, nblk, gflat, (int)n, s);
+    if (e != hipSuccess) return e;
+    const size_t need = std::max(b_sort, b_scan);
+    if (!tmp) {
+        tmp_bytes = need;
+        return hipSuccess;
+    }
+    if (tmp_bytes < need) return hipErrorInvalidValue;
+    if (n == 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + 255) / 256));
+    hipLaunchKernelGGL(k_whole_keys, grid, dim3(256), 0, s, chains, n, keys, vals);
+    e = hipcub::DeviceRadixSort::SortPairs(tmp, b_sort, keys, keys_out, vals, perm, (int)n, 0,
+                                           kOrderBits, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_whole_count, grid, dim3(256), 0, s, chains, perm, n, nblk);
+    e = hipcub::DeviceScan::ExclusiveSum(tmp, b_scan, nblk, gflat, (int)n, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_whole_plan_sorted, grid, dim3(256), 0, s, chains, perm, n, gflat, rdesc,
+                       pb0, tile_r0, inv);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpermute(const int32_t *inv, const SmallOut *pack, int64_t n, long long *g,
+                            long long *l, int32_t *ali, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_unpermute, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, inv, pack,
+                       n, g, l, ali);
     return hipGetLastError();
 }
 

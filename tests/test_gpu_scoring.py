@@ -159,14 +159,18 @@ def test_long_chains_multi_tile():
     assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
 
 
+@pytest.mark.parametrize("order", ["set", "target"])
 @pytest.mark.parametrize("want_local", [True, False])
-def test_whole_chains_vs_ranges(want_local):
+def test_whole_chains_vs_ranges(want_local, order, monkeypatch):
     """gac_score_chains (scoreChain's batch: the chain set's own plan, then
     k_tile and the two-level cross-tile fold) equals the oracle's whole-chain
     scores, on chains of 1 to 20k blocks (ranges spanning many tiles and
     several 64-tile super-tiles: the fold's second level), chains without
     blocks interleaved, and repeated calls; the range path on the same set
-    agrees."""
+    agrees.  Both plans: chains in set order, and in target order (sorted
+    plan, packed results scattered back by k_unpermute; the default from
+    4096 chains)."""
+    monkeypatch.setenv("GAC_WHOLE_ORDER", order)
     from genomealignmenttools_amd import synth
     from genomealignmenttools_amd.chainfile import ChainArrays
     from genomealignmenttools_amd.gachain import GAC_Q, GAC_T
