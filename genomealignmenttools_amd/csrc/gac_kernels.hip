@@ -174,6 +174,59 @@ __device__ __forceinline__ long long wave_sum(long long v) {
     return v;
 }
 
+// ---- wave scans on DPP (row_shr 1/2/4/8 inside each 16-lane row, then
+// row_bcast15 / row_bcast31 across rows: VALU moves, no LDS).  Step k of
+// kScanSteps moves lane src(lane) = the step's source to `lane`; the caller
+// combines when src_ok(k, lane) and the source lies in its segment.
+template <int CTRL, int RM>
+__device__ __forceinline__ int dpp32(int v) {
+    return __builtin_amdgcn_update_dpp(v, v, CTRL, RM, 0xf, false);
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ long long dpp64(long long v) {
+    const unsigned long long u = (unsigned long long)v;
+    const int lo = dpp32<CTRL, RM>((int)(uint32_t)u);
+    const int hi = dpp32<CTRL, RM>((int)(uint32_t)(u >> 32));
+    return (long long)(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+// source lane of step K for `lane` (meaningful only where scan_src_ok)
+template <int K>
+__device__ __forceinline__ int scan_src(int lane) {
+    if (K < 4) return lane - (1 << K);
+    if (K == 4) return (lane & ~15) - 1;
+    return 31;
+}
+template <int K>
+__device__ __forceinline__ bool scan_src_ok(int lane) {
+    if (K < 4) return (lane & 15) >= (1 << K);
+    if (K == 4) return (lane & 16) != 0;  // rows 1 and 3
+    return lane >= 32;                    // rows 2 and 3
+}
+template <int K>
+struct ScanCtl;  // dpp control and row mask of step K
+template <> struct ScanCtl<0> { static constexpr int c = 0x111, rm = 0xf; };
+template <> struct ScanCtl<1> { static constexpr int c = 0x112, rm = 0xf; };
+template <> struct ScanCtl<2> { static constexpr int c = 0x114, rm = 0xf; };
+template <> struct ScanCtl<3> { static constexpr int c = 0x118, rm = 0xf; };
+template <> struct ScanCtl<4> { static constexpr int c = 0x142, rm = 0xa; };
+template <> struct ScanCtl<5> { static constexpr int c = 0x143, rm = 0xc; };
+
+template <int K>
+__device__ __forceinline__ int scan_step_add(int v, int lane) {
+    const int o = dpp32<ScanCtl<K>::c, ScanCtl<K>::rm>(v);
+    return scan_src_ok<K>(lane) ? v + o : v;
+}
+// plain inclusive prefix sum over the wave (int)
+__device__ __forceinline__ int wave_incl_sum(int v, int lane) {
+    v = scan_step_add<0>(v, lane);
+    v = scan_step_add<1>(v, lane);
+    v = scan_step_add<2>(v, lane);
+    v = scan_step_add<3>(v, lane);
+    v = scan_step_add<4>(v, lane);
+    v = scan_step_add<5>(v, lane);
+    return v;
+}
+
 // ------------------------------------------------------------ k_nflags ---
 // At chain upload: flag blocks whose target / query bases contain an N, so
 // the scoring kernel can skip N-mask loads for all other blocks.  Genomes
@@ -868,6 +921,27 @@ __device__ __forceinline__ void seg_store(const ScoreArgs &a, int ri, long long 
     if (LOCAL) a.out_l[ri] = max2(0, max2(e.C, e.D));
 }
 
+// one step of k_tile's segmented (by range) inclusive scan: the source
+// lane's (g, ali, local element) folded in front when it lies in my segment
+template <int K, bool LOCAL>
+__device__ __forceinline__ void seg_scan_step(long long &vg, int &va, Elem &e, int lane, int seg0) {
+    constexpr int C = ScanCtl<K>::c, RM = ScanCtl<K>::rm;
+    const long long og = dpp64<C, RM>(vg);
+    const int oa = dpp32<C, RM>(va);
+    Elem o;
+    if (LOCAL) {
+        o.A = dpp64<C, RM>(e.A);
+        o.B = dpp64<C, RM>(e.B);
+        o.C = dpp64<C, RM>(e.C);
+        o.D = dpp64<C, RM>(e.D);
+    }
+    if (scan_src_ok<K>(lane) && scan_src<K>(lane) >= seg0) {
+        vg += og;
+        va += oa;
+        if (LOCAL) e = compose(o, e);
+    }
+}
+
 #ifndef GAC_TILE_MINB
 #define GAC_TILE_MINB 6  // waves per SIMD the register budget is sized for
 #endif
@@ -966,13 +1040,8 @@ __global__ void __launch_bounds__(256, GAC_TILE_MINB) k_tile(ScoreArgs a) {
         }
         // ---- chunk prefix (32 bases per chunk)
         const int nch = (len + 31) >> 5;
-        int incl = nch;
-#pragma unroll
-        for (int d = 1; d < kWave; d <<= 1) {
-            const int o = __shfl_up(incl, d, kWave);
-            if (lane >= d) incl += o;
-        }
-        const int C = __shfl(incl, kWave - 1, kWave);
+        const int incl = wave_incl_sum(nch, lane);
+        const int C = __builtin_amdgcn_readlane(incl, kWave - 1);
         L.coff[lane] = incl - nch;
         L.tpos[lane] = tpos;
         L.qpos[lane] = qpos;
@@ -1013,23 +1082,12 @@ __global__ void __launch_bounds__(256, GAC_TILE_MINB) k_tile(ScoreArgs a) {
         const bool head = !active || lane == 0 || first;
         const unsigned long long heads = __ballot(head);
         const int seg0 = 63 - __builtin_clzll(heads & lanemask_le);  // my segment's first lane
-#pragma unroll
-        for (int d = 1; d < kWave; d <<= 1) {
-            const long long og = __shfl_up(vg, d, kWave);
-            const int oa = __shfl_up(va, d, kWave);
-            Elem o;
-            if (LOCAL) {
-                o.A = __shfl_up(e.A, d, kWave);
-                o.B = __shfl_up(e.B, d, kWave);
-                o.C = __shfl_up(e.C, d, kWave);
-                o.D = __shfl_up(e.D, d, kWave);
-            }
-            if (lane - d >= seg0) {
-                vg += og;
-                va += oa;
-                if (LOCAL) e = compose(o, e);
-            }
-        }
+        seg_scan_step<0, LOCAL>(vg, va, e, lane, seg0);
+        seg_scan_step<1, LOCAL>(vg, va, e, lane, seg0);
+        seg_scan_step<2, LOCAL>(vg, va, e, lane, seg0);
+        seg_scan_step<3, LOCAL>(vg, va, e, lane, seg0);
+        seg_scan_step<4, LOCAL>(vg, va, e, lane, seg0);
+        seg_scan_step<5, LOCAL>(vg, va, e, lane, seg0);
         const bool seg_end = active && (lane == kWave - 1 || ((heads >> (lane + 1)) & 1ull));
         const bool first0 = __builtin_amdgcn_readfirstlane(first ? 1 : 0) != 0;
         if (seg_end) {
