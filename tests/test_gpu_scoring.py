@@ -168,8 +168,8 @@ def test_whole_chains_vs_ranges(want_local, order, monkeypatch):
     several 64-tile super-tiles: the fold's second level), chains without
     blocks interleaved, and repeated calls; the range path on the same set
     agrees.  Both plans: chains in set order, and in target order (sorted
-    plan, packed results scattered back by k_unpermute; the default from
-    4096 chains)."""
+    plan, packed results scattered back by k_unpermute; opt-in through
+    GAC_WHOLE_ORDER=target)."""
     monkeypatch.setenv("GAC_WHOLE_ORDER", order)
     from genomealignmenttools_amd import synth
     from genomealignmenttools_amd.chainfile import ChainArrays
