@@ -109,6 +109,16 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// The same for LDS handed between the lanes of ONE wave (a wave's LDS
+// operations execute in order): wavefront-scope fences order the compiler's
+// accesses without the vmcnt(0) a workgroup-scope release implies, so loads
+// in flight (the LDS-DMA of k_tile_pipe) stay in flight.
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, int sh) {
     return __builtin_amdgcn_alignbit(hi, lo, (uint32_t)sh);
 }
@@ -178,9 +188,11 @@ __device__ __forceinline__ long long wave_sum(long long v) {
 // row_bcast15 / row_bcast31 across rows: VALU moves, no LDS).  Step k of
 // kScanSteps moves lane src(lane) = the step's source to `lane`; the caller
 // combines when src_ok(k, lane) and the source lies in its segment.
+// (mov_dpp: lanes whose source is out of the row / rows outside RM get 0 or
+// keep garbage -- callers only use lanes where scan_src_ok)
 template <int CTRL, int RM>
 __device__ __forceinline__ int dpp32(int v) {
-    return __builtin_amdgcn_update_dpp(v, v, CTRL, RM, 0xf, false);
+    return __builtin_amdgcn_mov_dpp(v, CTRL, RM, 0xf, true);
 }
 template <int CTRL, int RM>
 __device__ __forceinline__ long long dpp64(long long v) {
@@ -926,25 +938,165 @@ __device__ __forceinline__ void seg_store(const ScoreArgs &a, int ri, long long 
 template <int K, bool LOCAL>
 __device__ __forceinline__ void seg_scan_step(long long &vg, int &va, Elem &e, int lane, int seg0) {
     constexpr int C = ScanCtl<K>::c, RM = ScanCtl<K>::rm;
+    // branch-free: outside my segment the source becomes the identity
+    const bool in = scan_src_ok<K>(lane) && scan_src<K>(lane) >= seg0;
     const long long og = dpp64<C, RM>(vg);
     const int oa = dpp32<C, RM>(va);
-    Elem o;
+    vg += in ? og : 0;
+    va += in ? oa : 0;
     if (LOCAL) {
+        Elem o;
         o.A = dpp64<C, RM>(e.A);
         o.B = dpp64<C, RM>(e.B);
         o.C = dpp64<C, RM>(e.C);
         o.D = dpp64<C, RM>(e.D);
-    }
-    if (scan_src_ok<K>(lane) && scan_src<K>(lane) >= seg0) {
-        vg += og;
-        va += oa;
-        if (LOCAL) e = compose(o, e);
+        if (!in) o = {0, kNeg, kNeg, kNeg};
+        e = compose(o, e);
     }
 }
 
 #ifndef GAC_TILE_MINB
 #define GAC_TILE_MINB 6  // waves per SIMD the register budget is sized for
 #endif
+// Owner of lane-block j of a tile whose candidate ranges rc + k (flat
+// offsets L.cg, first window blocks L.cb) are staged: the largest k with
+// cg[k] <= j (cg[0] <= the tile's first block), by a 6-step LDS search; past
+// 63 range starts in the tile (ranges of one block or empty ones), a binary
+// search of the flat offsets beyond.  Returns the range; bi = its block.
+__device__ __forceinline__ int tile_owner(const ScoreArgs &a, const WaveLds &L, int j, int rc,
+                                          bool active, int n, int &bi) {
+    int k = 0;
+#pragma unroll
+    for (int step = kTileBlocks / 2; step > 0; step >>= 1)
+        if (L.cg[k + step] <= j) k += step;
+    int ri = rc + k, gr = L.cg[k], b0r = L.cb[k];
+    // (keeps these LDS reads: merged with the fallback's global loads they
+    // become flat loads, whose vmcnt wait would drain the LDS-DMA in flight)
+    asm volatile("" : "+v"(gr), "+v"(b0r));
+    if (k == kTileBlocks - 1 && active && ri + 1 < n) {
+        int lo = ri, hi = n - 1;  // gflat[lo] <= j
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (a.gflat[mid] <= j) lo = mid;
+            else hi = mid - 1;
+        }
+        ri = lo;
+        gr = a.gflat[lo];
+        b0r = a.pb0[lo];
+    }
+    bi = b0r + (j - gr);
+    return ri;
+}
+
+// Per-lane block of the tile: clip to [s, e), gap to the next block, plane
+// positions (see WaveLds).
+struct LaneBlock {
+    int len, g, lenq;
+    bool first, last;
+    long long tpos, qpos;
+};
+
+__device__ __forceinline__ LaneBlock lane_block(const RangeDesc &d, const int4 bk, int bi) {
+    LaneBlock r;
+    r.first = (bi == d.b0);
+    r.last = (bi == d.b0 + d.nblk - 1);
+    const int z = bk.z & kSizeMask;
+    int cts = bk.x, cqs = bk.y, cte = bk.x + z;
+    if (cts < d.s) {
+        cqs += d.s - cts;
+        cts = d.s;
+    }
+    if (cte > d.e) cte = d.e;
+    r.len = cte - cts;
+    r.g = r.last ? 0 : bk.w;
+    r.tpos = d.tbase + cts;
+    const bool minus = d.qbase < 0;
+    r.qpos = minus ? ~d.qbase - cqs : d.qbase + cqs;
+    r.lenq = r.len | (minus ? (int)0x80000000 : 0) | (bk.z & (kTHasN | kQHasN));
+    return r;
+}
+
+// The tile once its lane-blocks are known: 32-base chunks spread over the
+// wave (both chunks of a lane loaded together), block sums in LDS, then the
+// segmented (by range) scans and the stores / boundary segments.
+template <bool LOCAL, bool SYM>
+__device__ __forceinline__ void tile_score(const ScoreArgs &a, WaveLds &L, int lane, int tile,
+                                           int j, bool active, int W, int ri, const LaneBlock &B,
+                                           unsigned long long lanemask_le) {
+    // ---- chunk prefix (32 bases per chunk)
+    const int nch = (B.len + 31) >> 5;
+    const int incl = wave_incl_sum(nch, lane);
+    const int C = __builtin_amdgcn_readlane(incl, kWave - 1);
+    L.coff[lane] = incl - nch;
+    L.tpos[lane] = B.tpos;
+    L.qpos[lane] = B.qpos;
+    L.lenq[lane] = B.lenq;
+    L.acc[lane] = 0ull;
+    wave_sync_lds();
+
+    for (int c0 = 0; c0 < C; c0 += 2 * kWave) {
+        const ChunkRef ca = chunk_prep(L, c0 + lane);
+        const ChunkRef cb = chunk_prep(L, c0 + kWave + lane);
+        const ChunkRaw ra = chunk_load(a, ca);
+        const ChunkRaw rb = chunk_load(a, cb);
+        const int sa = chunk_eval<SYM>(a, ca, ra);
+        const int sb = chunk_eval<SYM>(a, cb, rb);
+        if (ca.n > 0) atomicAdd(&L.acc[ca.k], (unsigned long long)(long long)sa);
+        if (cb.n > 0) atomicAdd(&L.acc[cb.k], (unsigned long long)(long long)sb);
+    }
+    wave_sync_lds();
+
+    // ---- segmented (by range) inclusive scans over the tile's lanes
+    const long long bsc = active ? (long long)L.acc[lane] : 0;
+    long long vg = active ? bsc - B.g : 0;
+    int va = active ? B.len : 0;
+    Elem e;
+    if (LOCAL) {
+        if (active) {
+            e.A = B.last ? bsc : bsc - B.g;
+            e.B = B.last ? kNeg : 0;
+            e.C = bsc;
+            e.D = kNeg;
+        } else {
+            e.A = 0;
+            e.B = kNeg;
+            e.C = kNeg;
+            e.D = kNeg;
+        }
+    }
+    const bool head = !active || lane == 0 || B.first;
+    const unsigned long long heads = __ballot(head);
+    const int seg0 = 63 - __builtin_clzll(heads & lanemask_le);  // my segment's first lane
+    seg_scan_step<0, LOCAL>(vg, va, e, lane, seg0);
+    seg_scan_step<1, LOCAL>(vg, va, e, lane, seg0);
+    seg_scan_step<2, LOCAL>(vg, va, e, lane, seg0);
+    seg_scan_step<3, LOCAL>(vg, va, e, lane, seg0);
+    seg_scan_step<4, LOCAL>(vg, va, e, lane, seg0);
+    seg_scan_step<5, LOCAL>(vg, va, e, lane, seg0);
+    const bool seg_end = active && (lane == kWave - 1 || ((heads >> (lane + 1)) & 1ull));
+    const bool first0 = __builtin_amdgcn_readfirstlane(B.first ? 1 : 0) != 0;
+    if (seg_end) {
+        const bool has0 = (seg0 == 0);
+        const bool starts = !has0 || first0;
+        if (starts && B.last) {
+            seg_store<LOCAL>(a, ri, vg, va, e);
+        } else {
+            SegSum ssum;
+            ssum.g = vg;
+            ssum.ali = va;
+            if (LOCAL) {
+                ssum.A = e.A;
+                ssum.B = e.B;
+                ssum.C = e.C;
+                ssum.D = e.D;
+            }
+            if (has0 && !starts) a.sum_head[tile] = ssum;
+            if (!B.last && (lane == kWave - 1 || j + 1 == W)) a.sum_tail[tile] = ssum;
+        }
+    }
+    wave_sync_lds();
+}
+
 template <bool LOCAL, bool SYM>
 __global__ void __launch_bounds__(256, GAC_TILE_MINB) k_tile(ScoreArgs a) {
     __shared__ WaveLds s_w[kWavesPerWG];
@@ -994,122 +1146,136 @@ __global__ void __launch_bounds__(256, GAC_TILE_MINB) k_tile(ScoreArgs a) {
             }
             r0_next = tn + stride < T ? a.tile_r0[tn + stride] : 0;
         }
-        wave_sync();
-        int k = 0;  // largest k with cg[k] <= j (cg[0] <= the tile's first block)
-#pragma unroll
-        for (int step = kTileBlocks / 2; step > 0; step >>= 1)
-            if (L.cg[k + step] <= j) k += step;
-        int ri = rc + k, gr = L.cg[k], b0r = L.cb[k];
-        if (k == kTileBlocks - 1 && active && ri + 1 < n) {
-            // more than 63 range starts in this tile (ranges of one block or
-            // empty ones): binary search the flat offsets beyond
-            int lo = ri, hi = n - 1;  // gflat[lo] <= j
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (a.gflat[mid] <= j) lo = mid;
-                else hi = mid - 1;
-            }
-            ri = lo;
-            gr = a.gflat[lo];
-            b0r = a.pb0[lo];
-        }
-        const int bi = b0r + (j - gr);
+        wave_sync_lds();
+        int bi;
+        const int ri = tile_owner(a, L, j, rc, active, n, bi);
+        LaneBlock B = {0, 0, 0, false, false, 0, 0};
+        if (active) B = lane_block(a.rdesc[ri], a.blk[bi], bi);
+        tile_score<LOCAL, SYM>(a, L, lane, tile, j, active, W, ri, B, lanemask_le);
+    }
+}
 
-        // ---- per-lane block: clip to [s, e), gap to the next block
-        int len = 0, g = 0, lenq = 0;
-        bool first = false, last = false;
-        long long tpos = 0, qpos = 0;
+// k_tile with the descriptor/block round trip of tile t + 1 overlapped with
+// the plane loads of tile t: the next tile's owners are found while tile t
+// is prepared, its RangeDesc halves and block records go to LDS by LDS-DMA
+// (global_load_lds, no registers held), issued before t's plane loads, so
+// the wave waits for one round trip per tile instead of two.  The candidate
+// ranges' offsets are loaded two tiles ahead, tile_r0 three.
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void gbl_void;
+
+struct WaveNext {
+    int4 rd_lo[kTileBlocks];  // RangeDesc {tbase, qbase} of each lane's owner, next tile
+    int4 rd_hi[kTileBlocks];  // RangeDesc {b0, nblk, s, e}
+    int4 bk[kTileBlocks];     // block record
+    int ri[kTileBlocks];      // owner range
+    int bi[kTileBlocks];      // block index
+    int r0;                   // tile_r0 of the tile after next (LDS-DMA, lane 0)
+    int pad[3];
+};
+
+__device__ __forceinline__ void tile_fetch(const ScoreArgs &a, WaveNext &N, int lane, int ri,
+                                           int bi, bool active) {
+    // inactive lanes fetch a valid record (range 0, block 0) and ignore it
+    const RangeDesc *rd = a.rdesc + (active ? ri : 0);
+    const int4 *bk = a.blk + (active ? bi : 0);
+    N.ri[lane] = ri;
+    N.bi[lane] = bi;
+    __builtin_amdgcn_global_load_lds((gbl_void *)rd, (lds_void *)N.rd_lo, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_void *)((const char *)rd + 16), (lds_void *)N.rd_hi, 16,
+                                     0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_void *)bk, (lds_void *)N.bk, 16, 0, 0);
+}
+
+template <bool LOCAL, bool SYM>
+__global__ void __launch_bounds__(256, GAC_TILE_MINB) k_tile_pipe(ScoreArgs a) {
+    __shared__ WaveLds s_w[kWavesPerWG];
+    __shared__ WaveNext s_n[kWavesPerWG];
+
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    WaveLds &L = s_w[wave];
+    WaveNext &N = s_n[wave];
+    if (a.status[2]) return;  // workspace overflow: the host grows it and reruns
+    const int T = a.status[1];
+    const int W = a.status[0];
+    const unsigned long long lanemask_le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
+    const int G = gridDim.x;
+    const int b = blockIdx.x;
+    const int L8 = (G % 8 == 0) ? ((b % 8) * (G / 8) + b / 8) : b;
+    const int stride = G * kWavesPerWG;
+    const int n = (int)a.n;
+
+    // wave-uniform tile index (scalar loads of tile_r0: their waits are on
+    // lgkmcnt, not on the vmcnt the LDS-DMA counts)
+    int tile = __builtin_amdgcn_readfirstlane(L8 * kWavesPerWG + wave);
+    if (tile >= T) return;
+    // prologue: owners of the first tile, its fetch; offsets of the second
+    {
+        const int r0 = a.tile_r0[tile];
+        L.cg[lane] = r0 + lane < n ? a.gflat[r0 + lane] : 0x7fffffff;
+        L.cb[lane] = r0 + lane < n ? a.pb0[r0 + lane] : 0;
+        wave_sync_lds();
+        const int j = tile * kTileBlocks + lane;
+        int bi;
+        const int ri = tile_owner(a, L, j, r0, j < W, n, bi);
+        tile_fetch(a, N, lane, ri, bi, j < W);
+    }
+    int r1 = tile + stride < T ? a.tile_r0[tile + stride] : 0;  // range r0 of the next tile
+    int gv = 0x7fffffff, bv = 0;  // its candidates' offsets
+    if (tile + stride < T && r1 + lane < n) {
+        gv = a.gflat[r1 + lane];
+        bv = a.pb0[r1 + lane];
+    }
+    // tile_r0 of the tile after next goes to LDS (N.r0) by LDS-DMA: a
+    // register copy of a loaded value would make the compiler wait for every
+    // load in flight, the LDS-DMA included
+    if (tile + 2 * stride < T && lane == 0)
+        __builtin_amdgcn_global_load_lds((gbl_void *)(a.tile_r0 + tile + 2 * stride),
+                                         (lds_void *)&N.r0, 4, 0, 0);
+    for (; tile < T; tile += stride) {
+        const int j = tile * kTileBlocks + lane;
+        const bool active = j < W;
+        // this tile's descriptors and blocks (fetched during the previous tile)
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the LDS-DMA has landed
+        wave_sync_lds();
+        const int ri = N.ri[lane];
+        LaneBlock B = {0, 0, 0, false, false, 0, 0};
         if (active) {
-            const RangeDesc d = a.rdesc[ri];
-            const int4 bk = a.blk[bi];  // {tStart, qStart, size | N flags, gap to next}
-            first = (bi == d.b0);
-            last = (bi == d.b0 + d.nblk - 1);
-            const int z = bk.z & kSizeMask;
-            int cts = bk.x, cqs = bk.y, cte = bk.x + z;
-            if (cts < d.s) {
-                cqs += d.s - cts;
-                cts = d.s;
+            const int4 lo = N.rd_lo[lane], hi = N.rd_hi[lane];
+            RangeDesc d;
+            d.tbase = (long long)(((unsigned long long)(uint32_t)lo.y << 32) | (uint32_t)lo.x);
+            d.qbase = (long long)(((unsigned long long)(uint32_t)lo.w << 32) | (uint32_t)lo.z);
+            d.b0 = hi.x;
+            d.nblk = hi.y;
+            d.s = hi.z;
+            d.e = hi.w;
+            B = lane_block(d, N.bk[lane], N.bi[lane]);
+        }
+        // owners of the next tile, and its fetch (lands while this tile's
+        // planes are read)
+        const int tn = tile + stride;
+        if (tn < T) {
+            L.cg[lane] = gv;
+            L.cb[lane] = bv;
+            wave_sync_lds();
+            const int jn = tn * kTileBlocks + lane;
+            int bin;
+            const int rin = tile_owner(a, L, jn, r1, jn < W, n, bin);
+            r1 = tn + stride < T ? N.r0 : 0;
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this tile's LDS reads are done
+            tile_fetch(a, N, lane, rin, bin, jn < W);
+            gv = 0x7fffffff;
+            bv = 0;
+            if (tn + stride < T && r1 + lane < n) {
+                gv = a.gflat[r1 + lane];
+                bv = a.pb0[r1 + lane];
             }
-            if (cte > d.e) cte = d.e;
-            len = cte - cts;
-            if (!last) g = bk.w;
-            tpos = d.tbase + cts;
-            const bool minus = d.qbase < 0;
-            qpos = minus ? ~d.qbase - cqs : d.qbase + cqs;
-            lenq = len | (minus ? (int)0x80000000 : 0) | (bk.z & (kTHasN | kQHasN));
+            if (tn + 2 * stride < T && lane == 0)
+                __builtin_amdgcn_global_load_lds((gbl_void *)(a.tile_r0 + tn + 2 * stride),
+                                                 (lds_void *)&N.r0, 4, 0, 0);
         }
-        // ---- chunk prefix (32 bases per chunk)
-        const int nch = (len + 31) >> 5;
-        const int incl = wave_incl_sum(nch, lane);
-        const int C = __builtin_amdgcn_readlane(incl, kWave - 1);
-        L.coff[lane] = incl - nch;
-        L.tpos[lane] = tpos;
-        L.qpos[lane] = qpos;
-        L.lenq[lane] = lenq;
-        L.acc[lane] = 0ull;
-        wave_sync();
-
-        for (int c0 = 0; c0 < C; c0 += 2 * kWave) {
-            const ChunkRef ca = chunk_prep(L, c0 + lane);
-            const ChunkRef cb = chunk_prep(L, c0 + kWave + lane);
-            const ChunkRaw ra = chunk_load(a, ca);
-            const ChunkRaw rb = chunk_load(a, cb);
-            const int sa = chunk_eval<SYM>(a, ca, ra);
-            const int sb = chunk_eval<SYM>(a, cb, rb);
-            if (ca.n > 0) atomicAdd(&L.acc[ca.k], (unsigned long long)(long long)sa);
-            if (cb.n > 0) atomicAdd(&L.acc[cb.k], (unsigned long long)(long long)sb);
-        }
-        wave_sync();
-
-        // ---- segmented (by range) inclusive scans over the tile's lanes
-        const long long bsc = active ? (long long)L.acc[lane] : 0;
-        long long vg = active ? bsc - g : 0;
-        int va = active ? len : 0;
-        Elem e;
-        if (LOCAL) {
-            if (active) {
-                e.A = last ? bsc : bsc - g;
-                e.B = last ? kNeg : 0;
-                e.C = bsc;
-                e.D = kNeg;
-            } else {
-                e.A = 0;
-                e.B = kNeg;
-                e.C = kNeg;
-                e.D = kNeg;
-            }
-        }
-        const bool head = !active || lane == 0 || first;
-        const unsigned long long heads = __ballot(head);
-        const int seg0 = 63 - __builtin_clzll(heads & lanemask_le);  // my segment's first lane
-        seg_scan_step<0, LOCAL>(vg, va, e, lane, seg0);
-        seg_scan_step<1, LOCAL>(vg, va, e, lane, seg0);
-        seg_scan_step<2, LOCAL>(vg, va, e, lane, seg0);
-        seg_scan_step<3, LOCAL>(vg, va, e, lane, seg0);
-        seg_scan_step<4, LOCAL>(vg, va, e, lane, seg0);
-        seg_scan_step<5, LOCAL>(vg, va, e, lane, seg0);
-        const bool seg_end = active && (lane == kWave - 1 || ((heads >> (lane + 1)) & 1ull));
-        const bool first0 = __builtin_amdgcn_readfirstlane(first ? 1 : 0) != 0;
-        if (seg_end) {
-            const bool has0 = (seg0 == 0);
-            const bool starts = !has0 || first0;
-            if (starts && last) {
-                seg_store<LOCAL>(a, ri, vg, va, e);
-            } else {
-                SegSum ssum;
-                ssum.g = vg;
-                ssum.ali = va;
-                if (LOCAL) {
-                    ssum.A = e.A;
-                    ssum.B = e.B;
-                    ssum.C = e.C;
-                    ssum.D = e.D;
-                }
-                if (has0 && !starts) a.sum_head[tile] = ssum;
-                if (!last && (lane == kWave - 1 || j + 1 == W)) a.sum_tail[tile] = ssum;
-            }
-        }
-        wave_sync();
+        tile_score<LOCAL, SYM>(a, L, lane, tile, j, active, W, ri, B, lanemask_le);
     }
 }
 
@@ -1486,21 +1652,26 @@ hipError_t launch_tilemap(const ScoreArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// Resident workgroups per CU of the persistent kernels (a grid must not
-// exceed what fits at once, or the last workgroups run as a second wave):
-// 0 = k_tile<false>, 1 = k_tile<true>.
-int persistent_blocks_per_cu(int which) {
-    int nb = 0;
-    // (the symmetric and general variants differ by a few registers; size
-    // for the general one)
-    hipError_t e =
-        which == 0   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<false, false>, 256, 0)
-                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<true, false>, 256, 0);
-    return (e == hipSuccess && nb > 0) ? nb : 4;
+
+// GAC_TILE_PIPE=0: k_tile (two round trips per tile) instead of k_tile_pipe
+static bool tile_pipe() {
+    static const bool on = [] {
+        const char *e = getenv("GAC_TILE_PIPE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 hipError_t launch_tile(const ScoreArgs &a, int grid, hipStream_t s) {
-    if (a.want_local) {
+    if (tile_pipe()) {
+        if (a.want_local) {
+            if (a.sym) k_tile_pipe<true, true><<<grid, 256, 0, s>>>(a);
+            else k_tile_pipe<true, false><<<grid, 256, 0, s>>>(a);
+        } else {
+            if (a.sym) k_tile_pipe<false, true><<<grid, 256, 0, s>>>(a);
+            else k_tile_pipe<false, false><<<grid, 256, 0, s>>>(a);
+        }
+    } else if (a.want_local) {
         if (a.sym) k_tile<true, true><<<grid, 256, 0, s>>>(a);
         else k_tile<true, false><<<grid, 256, 0, s>>>(a);
     } else {
@@ -1508,6 +1679,23 @@ hipError_t launch_tile(const ScoreArgs &a, int grid, hipStream_t s) {
         else k_tile<false, false><<<grid, 256, 0, s>>>(a);
     }
     return hipGetLastError();
+}
+
+// Resident workgroups per CU of the persistent kernels (a grid must not
+// exceed what fits at once, or the last workgroups run as a second wave):
+// 0 = k_tile<false>, 1 = k_tile<true> (whichever variant launch_tile runs).
+int persistent_blocks_per_cu(int which) {
+    int nb = 0;
+    // (the symmetric and general variants differ by a few registers; size
+    // for the general one)
+    const bool pipe = tile_pipe();
+    hipError_t e =
+        which == 0
+            ? (pipe ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_pipe<false, false>, 256, 0)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<false, false>, 256, 0))
+            : (pipe ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_pipe<true, false>, 256, 0)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<true, false>, 256, 0));
+    return (e == hipSuccess && nb > 0) ? nb : 4;
 }
 
 template <bool HOST>
