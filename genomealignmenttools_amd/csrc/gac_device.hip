@@ -1657,6 +1657,11 @@ static int prepare_args(gac_ctx *c, const gac_chainset *cs, int64_t n, uint32_t 
     a.small_tab = c->d_small;
     memcpy(a.coef, c->coef, sizeof(a.coef));
     a.sym = c->sym;
+    static const int scan64 = [] {
+        const char *e = getenv("GAC_TILE_SCAN64");
+        return e && e[0] == '1' ? 1 : 0;
+    }();
+    a.scan64 = scan64;
     a.gap = c->gap;
     return GAC_OK;
 }

@@ -141,6 +141,7 @@ struct ScoreArgs {
                                // (t1, t0, d1, d0), d = q ^ t: coef[S], S = t1<<3 |
                                // t0<<2 | d1<<1 | d0 (set bits = factors)
     int32_t sym;               // matrix is strand-symmetric: coef[8..15] == 0
+    int32_t scan64;            // A/B probe (GAC_TILE_SCAN64=1): k_tile's 64-bit scans only
     GapDev gap;
     SmallOut *out_pack;  // non-null: results go to out_pack[range] (the whole-chain
                          // plan in target order; k_unpermute restores chain order)

@@ -159,6 +159,40 @@ def test_long_chains_multi_tile():
     assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
 
 
+@pytest.mark.parametrize("want_local", [True, False])
+def test_wide_tiles_64bit_scans(want_local):
+    """Tiles holding a block score or gap of 2^20 or more take k_tile's
+    64-bit segmented scans, all others the 32-bit ones: chains of huge
+    near-identical blocks (scores of millions) and of megabase gaps mixed
+    with ordinary chains, ranges and whole chains, vs the oracle."""
+    from genomealignmenttools_amd import synth
+    tg = synth.random_genome({"chrT1": 8_000_000}, 21, n_frac=0.002, n_mean=300)
+    qg = synth.random_genome({"q1": 6_000_000, "q2": 5_000_000}, 22, n_frac=0.002, n_mean=300)
+    big = synth.make_chains(tg, "chrT1", qg, synth.SynthConfig(
+        n_chains=40, alpha=1.3, max_blocks=120, block_mean=20_000, sub_rate=0.01, seed=3,
+        gap_p_small=0.5, gap_p_med=0.2))
+    small = synth.make_chains(tg, "chrT1", qg, synth.SynthConfig(
+        n_chains=300, alpha=1.3, max_blocks=3_000, seed=4))
+    ca = synth.concat_chains([big, small])
+    e, cs = _setup(None, tg, qg, ca)
+    orc = _oracle(tg, qg)
+    full = np.stack([np.arange(ca.n), ca.tstart, ca.tend], 1).astype(np.int64)
+    og, ol, oa = orc.score_ranges(ca, full)
+    assert np.abs(og).max() >= 1 << 24  # some chains far beyond the 32-bit tile bound
+    g, l, a = e.score_chains(cs, want_local=want_local)
+    assert np.array_equal(g, og) and np.array_equal(a, oa)
+    if want_local:
+        assert np.array_equal(l, ol)
+    R = _ranges(ca, np.random.default_rng(8), per_chain=4)
+    og, ol, oa = orc.score_ranges(ca, R)
+    g, l, a = e.score_ranges(cs, R, want_local=want_local)
+    assert np.array_equal(g, og) and np.array_equal(a, oa)
+    if want_local:
+        assert np.array_equal(l, ol)
+    cs.close()
+    e.close()
+
+
 @pytest.mark.parametrize("order", ["set", "target"])
 @pytest.mark.parametrize("want_local", [True, False])
 def test_whole_chains_vs_ranges(want_local, order, monkeypatch):
