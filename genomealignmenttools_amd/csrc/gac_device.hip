@@ -47,8 +47,9 @@ hipError_t launch_relayout(const uint8_t *raw, const SeqDev *seqs, int nseq, int
                            uint2 *planes, uint32_t *nmask, hipStream_t s);
 hipError_t launch_gap_table(const GapDev &g, const int32_t *small, int len, int32_t *tab,
                             hipStream_t s);
-hipError_t launch_block_gaps(const DChain *chains, int64_t n_chains, int4 *blk, const GapDev &g,
-                             const int32_t *small, const int32_t *tab, int len, hipStream_t s);
+hipError_t launch_block_gaps(const DChain *chains, int64_t n_chains, int4 *blk, Blk12 *blk12,
+                             const GapDev &g, const int32_t *small, const int32_t *tab, int len,
+                             hipStream_t s);
 hipError_t launch_nflags(const DChain *chains, int64_t n_chains, int4 *blk,
                          const longlong2 *t_runs, int64_t n_trun, const longlong2 *q_runs,
                          int64_t n_qrun, const int64_t *q_woff, int2 *list, int *count,
@@ -210,6 +211,7 @@ struct gac_chainset {
     int64_t n_blocks;
     DChain *chains = nullptr;
     int4 *blk = nullptr;  // {tStart, qStart, size | N flags, gap}, padded by one entry
+    Blk12 *blk12 = nullptr;  // compact copy for k_tile (written with the gaps)
     uint32_t gap_version = 0;  // scoring setup the blk[].w gaps were computed for
     int2 *tspan = nullptr;  // {tStart, tEnd}
     uint32_t *bucket = nullptr;  // per-chain bucket indexes
@@ -231,7 +233,7 @@ struct gac_chainset {
     int32_t *w_inv = nullptr;
     SmallOut *w_pack = nullptr;
     // capacities (gac_chains_reupload refills these buffers when they fit)
-    size_t cap_chains = 0, cap_blocks = 0, cap_tspan = 0, cap_idx = 0;
+    size_t cap_chains = 0, cap_blocks = 0, cap_blk12 = 0, cap_tspan = 0, cap_idx = 0;
     int32_t *d_stage = nullptr;  // the caller's block arrays, staged (3 x blocks)
     size_t cap_stage = 0;
     int2 *d_nlist = nullptr;     // chains meeting an N run (+ count)
@@ -1446,6 +1448,7 @@ static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs)
     // from them on the device (k_build_*)
     hipError_t e = ensure_buf((void **)&cs->chains, &cs->cap_chains, ch.size(), sizeof(DChain));
     if (e == hipSuccess) e = ensure_buf((void **)&cs->blk, &cs->cap_blocks, nb + 8, sizeof(int4));
+    if (e == hipSuccess) e = ensure_buf((void **)&cs->blk12, &cs->cap_blk12, nb + 8, sizeof(Blk12));
     if (e == hipSuccess) e = ensure_buf((void **)&cs->tspan, &cs->cap_tspan, nb + 8, sizeof(int2));
     if (e == hipSuccess)
         e = ensure_buf((void **)&cs->bucket, &cs->cap_idx, (size_t)std::max<int64_t>(idx_n, 1), 4);
@@ -1511,6 +1514,7 @@ extern "C" void gac_chains_free(gac_chainset *cs) {
     hipSetDevice(cs->ctx->device);  // (hipFree waits for work still using them)
     if (cs->chains) hipFree(cs->chains);
     if (cs->blk) hipFree(cs->blk);
+    if (cs->blk12) hipFree(cs->blk12);
     if (cs->tspan) hipFree(cs->tspan);
     if (cs->bucket) hipFree(cs->bucket);
     if (cs->d_stage) hipFree(cs->d_stage);
@@ -1633,8 +1637,8 @@ static int prepare_args(gac_ctx *c, const gac_chainset *cs, int64_t n, uint32_t 
     if ((flags & GAC_WANT_LOCAL) && !d_l) return gac_fail(GAC_E_ARG, "GAC_WANT_LOCAL needs local output");
     if (n == 0) return GAC_OK;
     if (cs->gap_version != c->gap_version) {  // blk[].w for this scoring setup
-        HIPCHK(launch_block_gaps(cs->chains, cs->n_chains, cs->blk, c->gap, c->d_small,
-                                 c->d_gap_tab, c->gap_len, s));
+        HIPCHK(launch_block_gaps(cs->chains, cs->n_chains, cs->blk, cs->blk12, c->gap,
+                                 c->d_small, c->d_gap_tab, c->gap_len, s));
         const_cast<gac_chainset *>(cs)->gap_version = c->gap_version;
     }
     memset(&a, 0, sizeof(a));
@@ -1648,6 +1652,11 @@ static int prepare_args(gac_ctx *c, const gac_chainset *cs, int64_t n, uint32_t 
     a.chains = cs->chains;
     a.n_chains = cs->n_chains;
     a.blk = cs->blk;
+    static const bool blk16 = [] {
+        const char *e = getenv("GAC_TILE_BLK16");
+        return e && e[0] == '1';
+    }();
+    a.blk12 = blk16 ? nullptr : cs->blk12;
     a.tspan = cs->tspan;
     a.bucket = cs->bucket;
     a.n = n;

@@ -27,6 +27,19 @@ constexpr int kSizeMask = (1 << 29) - 1;  // block size field of blk[].z
 constexpr int kTHasN = 1 << 29;           // blk[].z: target bases contain an N
 constexpr int kQHasN = 1 << 30;           // blk[].z: query bases contain an N
 
+// Compact copy of the block records for k_tile (12 B instead of 16: fewer
+// 128-B lines per scored window), written with the gaps per scoring setup:
+// {tStart, qStart, w}, w = size (bits 0-11) | gap (bits 12-29) | tN << 30 |
+// qN << 31.  A block of kB12Wide or more bases, or a gap costing 2^18 - 1 or
+// more, has size field kB12Wide: k_tile reads its 16-B record instead.
+struct Blk12 {
+    int32_t t, q;
+    uint32_t w;
+};
+static_assert(sizeof(Blk12) == 12, "Blk12 layout");
+constexpr int kB12Wide = 0xFFF;
+constexpr int kB12GapMax = (1 << 18) - 1;
+
 struct DChain {
     int64_t blk_off;
     int32_t nblk;
@@ -105,6 +118,7 @@ struct ScoreArgs {
     const DChain *chains;
     int64_t n_chains;
     const int4 *blk;     // [n_blocks + 8] {tStart, qStart, size | N flags, gap to next}
+    const Blk12 *blk12;  // [n_blocks] the same, compact (k_tile)
     const int2 *tspan;   // [n_blocks + 8] {tStart, tEnd} (window searches; padded)
     const uint32_t *bucket;  // chain bucket indexes (see DChain)
     const Range *ranges;

@@ -359,8 +359,9 @@ __global__ void __launch_bounds__(256) k_build_buckets(const DChain *chains, int
 // (clipping only moves the first block's start and the last block's end), so
 // the tile kernel reads it with the block instead of evaluating it.
 __global__ void __launch_bounds__(256) k_block_gaps(const DChain *chains, int64_t n_chains,
-                                                    int4 *blk, GapDev g, const int32_t *small,
-                                                    const int32_t *tab, int len) {
+                                                    int4 *blk, Blk12 *blk12, GapDev g,
+                                                    const int32_t *small, const int32_t *tab,
+                                                    int len) {
     const int lane = threadIdx.x & 63;
     const int64_t wave_id = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -368,15 +369,23 @@ __global__ void __launch_bounds__(256) k_block_gaps(const DChain *chains, int64_
         const DChain ch = chains[c];
         for (int k = lane; k < ch.nblk; k += kWave) {
             int4 *b = blk + ch.blk_off + k;
+            const int4 x = b[0];
+            const int z = x.z & kSizeMask;
             int cost = 0;
             if (k + 1 < ch.nblk) {
-                const int4 x = b[0], y = b[1];
-                const int z = x.z & kSizeMask;
+                const int4 y = b[1];
                 int d;
                 const int which = gap_kind(y.y - (x.y + z), y.x - (x.x + z), d);
                 cost = d < len ? tab[which * len + d] : gap_cost_wd(g, small, which, d);
             }
             b->w = cost;
+            const bool wide = z >= kB12Wide || cost < 0 || cost >= kB12GapMax;
+            Blk12 r;
+            r.t = x.x;
+            r.q = x.y;
+            r.w = (wide ? (uint32_t)kB12Wide : ((uint32_t)z | ((uint32_t)cost << 12))) |
+                  ((uint32_t)(x.z & (kTHasN | kQHasN)) << 1);
+            blk12[ch.blk_off + k] = r;
         }
     }
 }
@@ -1031,6 +1040,17 @@ __device__ __forceinline__ int tile_owner(const ScoreArgs &a, const WaveLds &L, 
     return ri;
 }
 
+// Block record bi from the compact copy, as {tStart, qStart, size | N
+// flags, gap}; a wide block (rare) reads its 16-B record.
+__device__ __forceinline__ int4 load_blk12(const ScoreArgs &a, int bi) {
+    if (!a.blk12) return a.blk[bi];  // (A/B probe: GAC_TILE_BLK16=1)
+    const Blk12 r = a.blk12[bi];
+    const uint32_t sz = r.w & kB12Wide;
+    if (sz == (uint32_t)kB12Wide) return a.blk[bi];
+    return make_int4(r.t, r.q, (int)(sz | ((r.w >> 1) & (uint32_t)(kTHasN | kQHasN))),
+                     (int)((r.w >> 12) & (uint32_t)kB12GapMax));
+}
+
 // Per-lane block of the tile: clip to [s, e), gap to the next block, plane
 // positions (see WaveLds).
 struct LaneBlock {
@@ -1221,7 +1241,7 @@ __global__ void __launch_bounds__(256, GAC_TILE_MINB) k_tile(ScoreArgs a) {
         int bi;
         const int ri = tile_owner(a, L, j, rc, active, n, bi);
         LaneBlock B = {0, 0, 0, false, false, 0, 0};
-        if (active) B = lane_block(a.rdesc[ri], a.blk[bi], bi);
+        if (active) B = lane_block(a.rdesc[ri], load_blk12(a, bi), bi);
         tile_score<LOCAL, SYM>(a, L, lane, tile, j, active, W, ri, B, lanemask_le);
     }
 }
@@ -1889,12 +1909,13 @@ hipError_t launch_gap_table(const GapDev &g, const int32_t *small, int len, int3
     return hipGetLastError();
 }
 
-hipError_t launch_block_gaps(const DChain *chains, int64_t n_chains, int4 *blk, const GapDev &g,
-                             const int32_t *small, const int32_t *tab, int len, hipStream_t s) {
+hipError_t launch_block_gaps(const DChain *chains, int64_t n_chains, int4 *blk, Blk12 *blk12,
+                             const GapDev &g, const int32_t *small, const int32_t *tab, int len,
+                             hipStream_t s) {
     if (n_chains == 0) return hipSuccess;
     const int64_t waves = n_chains < 65536 ? n_chains : 65536;
     hipLaunchKernelGGL(k_block_gaps, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, chains,
-                       n_chains, blk, g, small, tab, len);
+                       n_chains, blk, blk12, g, small, tab, len);
     return hipGetLastError();
 }
 

@@ -1,19 +1,24 @@
 #!/bin/bash
-# A/B of the C5 kernel legs under two env settings, alternating on one box:
-#   gpu_ab_env.sh TAG "A_ENV" "B_ENV" [ROUNDS]   e.g. "GAC_TILE_SCAN64=1" ""
-# (the bench's kernel legs only: --no-c2 --no-cpu-baseline --no-pmc, one
-# headline step).  Each GPU step time-limited; stops at the first failure.
+# A/B of the C5 kernel legs under env settings, alternating on one box:
+#   gpu_ab_env.sh TAG ROUNDS NAME=ENV[,ENV...] ...
+#   e.g. gpu_ab_env.sh r03q 2 old=GAC_TILE_SCAN64=1,GAC_TILE_BLK16=1 new=
+# The scoring parity tests run first; then per round every setting runs the
+# bench's kernel legs (--no-c2 --no-cpu-baseline --no-pmc, one headline
+# step).  Each GPU step time-limited; stops at the first failure.
 set -o pipefail
-tag=$1; A=$2; B=$3; rounds=${4:-2}
+tag=$1; rounds=$2; shift 2
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_scoring.py -m gpu -x -v --timeout 240 \
+    --timeout-method thread > $out/gpu_tests.txt 2>&1 || exit $?
+tail -1 $out/gpu_tests.txt
 for r in $(seq $rounds); do
-    for v in A B; do
-        if [ $v = A ]; then e=$A; else e=$B; fi
-        env $e timeout -k 10 600 python -u bench.py --steps 1 --warmup 0 --no-c2 \
-            --no-cpu-baseline --kernel-steps 20 --no-pmc > $out/bench_${v}_$r.json \
-            2> $out/bench_${v}_$r.err || exit $?
+    for spec in "$@"; do
+        name=${spec%%=*}; envs=${spec#*=}
+        timeout -k 10 600 env ${envs//,/ } python -u bench.py --steps 1 --warmup 0 --no-c2 \
+            --no-cpu-baseline --kernel-steps 20 --no-pmc > $out/bench_${name}_$r.json \
+            2> $out/bench_${name}_$r.err || exit $?
     done
 done
 python - $out <<'P'
