@@ -127,3 +127,15 @@ oracle/_build/chainNet_cpu: $(CSRC)/tools/chainNet.c $(CSRC)/host/gac_net.c \
 	    -o $@ -lz -lm -lpthread $(CPU_EXTRA)
 
 .PHONY: cpu-axtchain cpu-chainnet
+
+# A/B probe builds of libgachain with extra compile flags (loaded by the
+# Python binding under GAC_LIB_VARIANT=NAME): make variant NAME=mb7 VFLAGS=-DGAC_TILE_MINB=7
+# (VSRC=DIR: the .hip sources and kernel headers from DIR instead, e.g. an
+# earlier commit's, extracted with git show)
+VSRC ?= $(CSRC)
+variant: $(HOST_OBJ)
+	@mkdir -p build/variants/$(NAME) $(LIBDIR)/variants/$(NAME)
+	for f in $(notdir $(HIP_SRC)); do $(HIPCC) -I$(VSRC) $(HIPFLAGS) $(VFLAGS) -c $(VSRC)/$$f -o build/variants/$(NAME)/$$(basename $$f .hip).o || exit 1; done
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/$(NAME)/libgachain.so \
+	    build/variants/$(NAME)/*.o $(HOST_OBJ) -Wl,-soname,libgachain.so
+.PHONY: variant

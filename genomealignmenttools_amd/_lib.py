@@ -15,6 +15,10 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_DIR = os.path.join(PKG_DIR, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libgachain.so")
+# A/B probes only: GAC_LIB_VARIANT=NAME loads lib/variants/NAME/libgachain.so
+# (built by `make variant NAME=... VFLAGS=...`; the tools keep lib/).
+if os.environ.get("GAC_LIB_VARIANT"):
+    LIB_PATH = os.path.join(LIB_DIR, "variants", os.environ["GAC_LIB_VARIANT"], "libgachain.so")
 BIN_DIR = os.path.join(PKG_DIR, "bin")
 
 GAC_OK = 0

@@ -24,7 +24,7 @@
 
 namespace gac {
 int plan_grid(int64_t n);
-int persistent_blocks_per_cu(int which);
+int persistent_blocks_per_cu(int which, int sym);
 hipError_t launch_plan(const ScoreArgs &a, hipStream_t s);
 hipError_t launch_tilemap(const ScoreArgs &a, hipStream_t s);
 hipError_t launch_tile(const ScoreArgs &a, int grid, hipStream_t s);
@@ -191,8 +191,8 @@ struct gac_ctx {
     int32_t *h_stat = nullptr;   // pinned, coherent host words written by k_scan_agg [8]
     int32_t *d_h_stat = nullptr; // its device address
     int32_t call_seq = 0;
-    int tile_grid_g = 2048;     // k_tile<false> grid (resident workgroups)
-    int tile_grid_l = 2048;     // k_tile<true> grid
+    // k_tile grids (resident workgroups) by [strand-symmetric matrix][local]
+    int tile_grid_sym[2][2] = {{2048, 2048}, {2048, 2048}};
     int combine_grid = 512;
     // pinned staging for genome uploads (two buffers, alternating)
     uint8_t *pin[2] = {nullptr, nullptr};
@@ -302,8 +302,9 @@ extern "C" int gac_open(int device, gac_ctx **out) {
     }
     lap("hipStreamCreate");
     c->combine_grid = prop.multiProcessorCount * 8;  // k_fold_tiles: 32 waves per CU
-    c->tile_grid_g = prop.multiProcessorCount * persistent_blocks_per_cu(0);
-    c->tile_grid_l = prop.multiProcessorCount * persistent_blocks_per_cu(1);
+    for (int sym = 0; sym < 2; ++sym)
+        for (int l = 0; l < 2; ++l)
+            c->tile_grid_sym[sym][l] = prop.multiProcessorCount * persistent_blocks_per_cu(l, sym);
     lap("occupancy (code object)");
     if (hipHostMalloc((void **)&c->h_stat, 64, hipHostMallocMapped | hipHostMallocCoherent) !=
             hipSuccess ||
@@ -744,6 +745,9 @@ extern "C" int gac_genome_finalize(gac_ctx *c, int side) {
         w += ((int64_t)g->sizes[i] + 31) / 32;
     }
     g->n_words = w;
+    // the scoring kernels index plane words in 32 bits (2^37 bases per side)
+    if (w + 4 > (int64_t)UINT32_MAX)
+        return gac_fail(GAC_E_ARG, "genome of %lld words: over the 2^32-word plane limit", (long long)w);
     const int64_t alloc_words = w + 4;  // padding: windows read word w+1
     HIPCHK(hipMalloc(&g->planes, alloc_words * sizeof(uint2)));
     HIPCHK(hipMalloc(&g->nmask, alloc_words * sizeof(uint32_t)));
@@ -1733,7 +1737,7 @@ static int score_device_split(gac_ctx *c, const ScoreArgs &a_base, const Range *
         }
         {
             PROF_BEGIN(GAC_K_TILE);
-            HIPCHK(launch_tile(a, a.want_local ? c->tile_grid_l : c->tile_grid_g, s));
+            HIPCHK(launch_tile(a, c->tile_grid_sym[a.sym ? 1 : 0][a.want_local ? 1 : 0], s));
             PROF_END(GAC_K_TILE);
         }
         {
@@ -1865,7 +1869,7 @@ static int score_whole(gac_ctx *c, const gac_chainset *cs_in, uint32_t flags, lo
         HIPCHK(launch_zero_list(cs->w_empty, cs->w_nempty, d_g, a.want_local ? d_l : nullptr, d_ali, s));
     {
         PROF_BEGIN(GAC_K_TILE);
-        HIPCHK(launch_tile(a, a.want_local ? c->tile_grid_l : c->tile_grid_g, s));
+        HIPCHK(launch_tile(a, c->tile_grid_sym[a.sym ? 1 : 0][a.want_local ? 1 : 0], s));
         PROF_END(GAC_K_TILE);
     }
     {

@@ -811,11 +811,24 @@ constexpr int kLenMask = kSizeMask;  // lenq: len | tN (bit 29) | qN (bit 30) | 
 // with no branch between them (a branch makes the compiler wait for every
 // load in flight).
 struct ChunkRef {
-    int64_t tp, qp;  // first word-aligned window of the target / query planes
-    int k;           // block (lane of the tile)
-    int n;           // bases in the chunk (<= 0: no chunk; loads stay in bounds)
-    int lq;          // the block's lenq
+    uint32_t tw, qw;  // first plane word of the target / query window
+    uint32_t m;       // n (bits 0-5, 0 = no chunk) | target shift (6-10) | query shift
+                      // (11-15) | block k (16-21) | minus (22) | tN (23) | qN (24)
 };
+
+// (packed: three registers per chunk instead of seven -- k_tile's register
+// peak is its two chunks in flight)
+__device__ __forceinline__ ChunkRef make_chunk(int64_t tp, int64_t qp, int n, int lq, int k) {
+    ChunkRef c;
+    c.tw = (uint32_t)(tp >> 5);
+    c.qw = (uint32_t)(qp >> 5);
+    c.m = (uint32_t)n | ((uint32_t)(tp & 31) << 6) | ((uint32_t)(qp & 31) << 11) |
+          ((uint32_t)k << 16) | ((uint32_t)lq >> 31 << 22) |
+          ((uint32_t)(lq & (kTHasN | kQHasN)) >> 29 << 23);
+    return c;
+}
+__device__ __forceinline__ int chunk_n(const ChunkRef &c) { return (int)(c.m & 63u); }
+__device__ __forceinline__ int chunk_k(const ChunkRef &c) { return (int)((c.m >> 16) & 63u); }
 
 __device__ __forceinline__ ChunkRef chunk_prep(const WaveLds &L, int j);
 
@@ -827,9 +840,14 @@ struct ChunkRaw {
 // C5 fills, r03d)
 __device__ __forceinline__ ChunkRaw chunk_load(const ScoreArgs &a, const ChunkRef &c) {
     ChunkRaw r;
-    r.t = *reinterpret_cast<const u32x4a8 *>(a.t_planes + (c.tp >> 5));
-    r.q = *reinterpret_cast<const u32x4a8 *>(a.q_planes + (c.qp >> 5));
+    r.t = *reinterpret_cast<const u32x4a8 *>(a.t_planes + c.tw);
+    r.q = *reinterpret_cast<const u32x4a8 *>(a.q_planes + c.qw);
     return r;
+}
+
+__device__ __forceinline__ uint32_t load_nmask_w(const uint32_t *nmask, uint32_t w, int sh) {
+    const u32x2a4 v = *reinterpret_cast<const u32x2a4 *>(nmask + w);
+    return funnel(v.y, v.x, sh);
 }
 
 // sum over the positions in v of the matrix score, in the multilinear basis
@@ -869,11 +887,11 @@ __device__ __forceinline__ int score_bits(const ScoreArgs &a, uint32_t v, uint32
 template <bool SYM>
 __device__ __forceinline__ int chunk_eval(const ScoreArgs &a, const ChunkRef &c,
                                           const ChunkRaw &r) {
-    const int n = c.n;
-    const int sht = (int)(c.tp & 31), shq = (int)(c.qp & 31);
+    const int n = chunk_n(c);
+    const int sht = (int)((c.m >> 6) & 31u), shq = (int)((c.m >> 11) & 31u);
     const uint32_t t0 = funnel(r.t.z, r.t.x, sht), t1 = funnel(r.t.w, r.t.y, sht);
     uint32_t q0 = funnel(r.q.z, r.q.x, shq), q1 = funnel(r.q.w, r.q.y, shq);
-    const bool minus = c.lq < 0;
+    const bool minus = (c.m >> 22) & 1u;
     const int sh = 32 - n;
     if (minus) {
         // '-' strand: rc base j = comp(fwd[qSize-1-(qp+j)]), comp = code ^ 2;
@@ -881,14 +899,14 @@ __device__ __forceinline__ int chunk_eval(const ScoreArgs &a, const ChunkRef &c,
         q0 = __builtin_bitreverse32(q0) >> sh;
         q1 = ~(__builtin_bitreverse32(q1) >> sh);
     }
-    const uint32_t v = n <= 0 ? 0u : n >= 32 ? 0xffffffffu : ((1u << n) - 1u);
+    const uint32_t v = n >= 32 ? 0xffffffffu : ((1u << n) - 1u);
     const uint32_t d0 = q0 ^ t0, d1 = q1 ^ t1;
     int sc = score_bits<SYM>(a, v, t0, t1, d0, d1);
-    if (c.lq & (kTHasN | kQHasN)) {
+    if (c.m & (3u << 23)) {
         uint32_t nm = 0;
-        if (c.lq & kTHasN) nm = load_nmask(a.t_nmask, c.tp);
-        if (c.lq & kQHasN) {
-            const uint32_t qn = load_nmask(a.q_nmask, c.qp);
+        if (c.m & (1u << 23)) nm = load_nmask_w(a.t_nmask, c.tw, sht);
+        if (c.m & (1u << 24)) {
+            const uint32_t qn = load_nmask_w(a.q_nmask, c.qw, shq);
             nm |= minus ? __builtin_bitreverse32(qn) >> sh : qn;
         }
         sc -= score_bits<SYM>(a, v & nm, t0, t1, d0, d1);
@@ -913,16 +931,17 @@ __device__ __forceinline__ int find_chunk_block(const WaveLds &L, int j) {
 // Chunk j of the tile: its block, base count and plane positions.  j past
 // the tile's chunks yields n <= 0 with in-bounds positions.
 __device__ __forceinline__ ChunkRef chunk_prep(const WaveLds &L, int j) {
-    ChunkRef c;
-    c.k = find_chunk_block(L, j);
-    c.lq = L.lenq[c.k];
-    int off = (j - L.coff[c.k]) << 5;
-    c.n = min(32, (c.lq & kLenMask) - off);
-    if (c.n <= 0) off = 0;
-    c.tp = L.tpos[c.k] + off;
+    const int k = find_chunk_block(L, j);
+    const int lq = L.lenq[k];
+    int off = (j - L.coff[k]) << 5;
+    int n = min(32, (lq & kLenMask) - off);
+    if (n <= 0) {
+        off = 0;
+        n = 0;
+    }
     // '-': read the forward window that ends where the chunk starts
-    c.qp = c.lq < 0 ? L.qpos[c.k] - off - max(c.n, 0) : L.qpos[c.k] + off;
-    return c;
+    const int64_t qp = lq < 0 ? L.qpos[k] - off - n : L.qpos[k] + off;
+    return make_chunk(L.tpos[k] + off, qp, n, lq, k);
 }
 
 template <bool LOCAL>
@@ -1008,7 +1027,7 @@ __device__ __forceinline__ void seg_scan_step32(int &vg, int &va, Elem32 &e, int
 }
 
 #ifndef GAC_TILE_MINB
-#define GAC_TILE_MINB 6  // waves per SIMD the register budget is sized for
+#define GAC_TILE_MINB 7  // waves per SIMD the register budget is sized for (r03u: 7 beats 6; 8 spills)
 #endif
 // Owner of lane-block j of a tile whose candidate ranges rc + k (flat
 // offsets L.cg, first window blocks L.cb) are staged: the largest k with
@@ -1085,7 +1104,7 @@ __device__ __forceinline__ LaneBlock lane_block(const RangeDesc &d, const int4 b
 template <bool LOCAL, bool SYM>
 __device__ __forceinline__ void tile_score(const ScoreArgs &a, WaveLds &L, int lane, int tile,
                                            int j, bool active, int W, int ri, const LaneBlock &B,
-                                           unsigned long long lanemask_le) {
+                                           int /*unused*/) {
     // ---- chunk prefix (32 bases per chunk)
     const int nch = (B.len + 31) >> 5;
     const int incl = wave_incl_sum(nch, lane);
@@ -1104,8 +1123,8 @@ __device__ __forceinline__ void tile_score(const ScoreArgs &a, WaveLds &L, int l
         const ChunkRaw rb = chunk_load(a, cb);
         const int sa = chunk_eval<SYM>(a, ca, ra);
         const int sb = chunk_eval<SYM>(a, cb, rb);
-        if (ca.n > 0) atomicAdd(&L.acc[ca.k], (unsigned long long)(long long)sa);
-        if (cb.n > 0) atomicAdd(&L.acc[cb.k], (unsigned long long)(long long)sb);
+        if (chunk_n(ca) > 0) atomicAdd(&L.acc[chunk_k(ca)], (unsigned long long)(long long)sa);
+        if (chunk_n(cb) > 0) atomicAdd(&L.acc[chunk_k(cb)], (unsigned long long)(long long)sb);
     }
     wave_sync_lds();
 
@@ -1113,7 +1132,8 @@ __device__ __forceinline__ void tile_score(const ScoreArgs &a, WaveLds &L, int l
     const long long bsc = active ? (long long)L.acc[lane] : 0;
     const bool head = !active || lane == 0 || B.first;
     const unsigned long long heads = __ballot(head);
-    const int seg0 = 63 - __builtin_clzll(heads & lanemask_le);  // my segment's first lane
+    // my segment's first lane (lanes <= me: computed here, not held across the tile)
+    const int seg0 = 63 - __builtin_clzll(heads & (~0ull >> (63 - lane)));
     int va = active ? B.len : 0;
     long long vg;
     Elem e;
@@ -1189,7 +1209,7 @@ __device__ __forceinline__ void tile_score(const ScoreArgs &a, WaveLds &L, int l
 }
 
 template <bool LOCAL, bool SYM>
-__global__ void __launch_bounds__(256, GAC_TILE_MINB) k_tile(ScoreArgs a) {
+__global__ void __launch_bounds__(256, SYM ? GAC_TILE_MINB : 6) k_tile(ScoreArgs a) {
     __shared__ WaveLds s_w[kWavesPerWG];
 
     const int wave = threadIdx.x >> 6;
@@ -1198,7 +1218,6 @@ __global__ void __launch_bounds__(256, GAC_TILE_MINB) k_tile(ScoreArgs a) {
     if (a.status[2]) return;  // workspace overflow: the host grows it and reruns
     const int T = a.status[1];
     const int W = a.status[0];
-    const unsigned long long lanemask_le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
 
     // XCD-aware logical id: workgroups b and b+8 share an XCD (round-robin
     // dispatch), so give them adjacent tiles (speed only).
@@ -1207,18 +1226,26 @@ __global__ void __launch_bounds__(256, GAC_TILE_MINB) k_tile(ScoreArgs a) {
     const int L8 = (G % 8 == 0) ? ((b % 8) * (G / 8) + b / 8) : b;
     const int stride = G * kWavesPerWG;
 
-    // The tile's blocks belong to the ranges r0, r0 + 1, ... (r0 = tile_r0):
-    // their flat offsets / first blocks are loaded one tile ahead (r0 itself
-    // two ahead), staged in LDS, and each lane finds its owner by a 6-step
-    // search.
+    // The tile's blocks belong to the ranges r0 .. r1 (r0 = tile_r0[t], r1 =
+    // tile_r0[t + 1], the owner of the next tile's first block).  During tile
+    // t the wave loads r0, r1 of its next tile t' (at the top; they land
+    // with t's descriptors and blocks) and then, once t's blocks are in,
+    // the flat offsets / first blocks of exactly t''s candidates r0 .. r1
+    // (their lines only, not those of 64 ranges), consumed at the top of t'
+    // from LDS by a 6-step owner search.  (Whole-chain plans in set order
+    // have pb0 == gflat: one load.)
     int tile = L8 * kWavesPerWG + wave;
     const int n = (int)a.n;
-    int r0 = tile < T ? a.tile_r0[tile] : 0;
-    int r0_next = tile + stride < T ? a.tile_r0[tile + stride] : 0;
-    int gv = 0x7fffffff, bv = 0;
-    if (tile < T && r0 + lane < n) {
-        gv = a.gflat[r0 + lane];
-        bv = a.pb0[r0 + lane];
+    const bool same_pb = a.pb0 == a.gflat;
+    const auto cand_end = [&](int t) { return t + 1 < T ? a.tile_r0[t + 1] : n - 1; };
+    int r0 = 0, gv = 0x7fffffff, bv = 0;
+    if (tile < T) {
+        r0 = a.tile_r0[tile];
+        const int r1 = cand_end(tile);
+        if (r0 + lane <= r1 && r0 + lane < n) {
+            gv = a.gflat[r0 + lane];
+            bv = same_pb ? gv : a.pb0[r0 + lane];
+        }
     }
     for (; tile < T; tile += stride) {
         const int j = tile * kTileBlocks + lane;
@@ -1226,23 +1253,25 @@ __global__ void __launch_bounds__(256, GAC_TILE_MINB) k_tile(ScoreArgs a) {
         L.cg[lane] = gv;
         L.cb[lane] = bv;
         const int rc = r0;
-        {
-            r0 = r0_next;
-            const int tn = tile + stride;
-            gv = 0x7fffffff;
-            bv = 0;
-            if (tn < T && r0 + lane < n) {
-                gv = a.gflat[r0 + lane];
-                bv = a.pb0[r0 + lane];
-            }
-            r0_next = tn + stride < T ? a.tile_r0[tn + stride] : 0;
+        const int tn = tile + stride;
+        int r0n = 0, r1n = 0;
+        if (tn < T) {
+            r0n = a.tile_r0[tn];
+            r1n = cand_end(tn);
         }
         wave_sync_lds();
         int bi;
         const int ri = tile_owner(a, L, j, rc, active, n, bi);
         LaneBlock B = {0, 0, 0, false, false, 0, 0};
         if (active) B = lane_block(a.rdesc[ri], load_blk12(a, bi), bi);
-        tile_score<LOCAL, SYM>(a, L, lane, tile, j, active, W, ri, B, lanemask_le);
+        gv = 0x7fffffff;
+        bv = 0;
+        if (tn < T && r0n + lane <= r1n && r0n + lane < n) {
+            gv = a.gflat[r0n + lane];
+            bv = same_pb ? gv : a.pb0[r0n + lane];
+        }
+        r0 = r0n;
+        tile_score<LOCAL, SYM>(a, L, lane, tile, j, active, W, ri, B, 0);
     }
 }
 
@@ -1290,7 +1319,6 @@ __global__ void __launch_bounds__(256, GAC_TILE_MINB) k_tile_pipe(ScoreArgs a) {
     if (a.status[2]) return;  // workspace overflow: the host grows it and reruns
     const int T = a.status[1];
     const int W = a.status[0];
-    const unsigned long long lanemask_le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
     const int G = gridDim.x;
     const int b = blockIdx.x;
     const int L8 = (G % 8 == 0) ? ((b % 8) * (G / 8) + b / 8) : b;
@@ -1366,7 +1394,7 @@ __global__ void __launch_bounds__(256, GAC_TILE_MINB) k_tile_pipe(ScoreArgs a) {
                 __builtin_amdgcn_global_load_lds((gbl_void *)(a.tile_r0 + tn + 2 * stride),
                                                  (lds_void *)&N.r0, 4, 0, 0);
         }
-        tile_score<LOCAL, SYM>(a, L, lane, tile, j, active, W, ri, B, lanemask_le);
+        tile_score<LOCAL, SYM>(a, L, lane, tile, j, active, W, ri, B, 0);
     }
 }
 
@@ -1554,14 +1582,12 @@ __global__ void __launch_bounds__(256) k_small(ScoreArgs a, const Range *rin, co
             const int len = cte - cts;
             const int64_t tpos = d.tbase + cts;
             const int64_t qpos = minus ? ~d.qbase - cqs : d.qbase + cqs;
-            ChunkRef c;
-            c.k = 0;
-            c.lq = len | (minus ? (int)0x80000000 : 0) | (bk.z & (kTHasN | kQHasN));
+            const int lq = len | (minus ? (int)0x80000000 : 0) | (bk.z & (kTHasN | kQHasN));
             long long bsc = 0;
             for (int off = 0; off < len; off += 32) {
-                c.n = min(32, len - off);
-                c.tp = tpos + off;
-                c.qp = minus ? qpos - off - c.n : qpos + off;
+                const int cn = min(32, len - off);
+                const ChunkRef c =
+                    make_chunk(tpos + off, minus ? qpos - off - cn : qpos + off, cn, lq, 0);
                 bsc += chunk_eval<SYM>(a, c, chunk_load(a, c));
             }
             const int g = last ? 0 : bk.w;
@@ -1775,18 +1801,21 @@ hipError_t launch_tile(const ScoreArgs &a, int grid, hipStream_t s) {
 
 // Resident workgroups per CU of the persistent kernels (a grid must not
 // exceed what fits at once, or the last workgroups run as a second wave):
-// 0 = k_tile<false>, 1 = k_tile<true> (whichever variant launch_tile runs).
-int persistent_blocks_per_cu(int which) {
+// which = 0 k_tile<false, *>, 1 = k_tile<true, *>; sym = the strand-symmetric
+// variant (register budgets differ: 7 vs 6 waves per SIMD).
+int persistent_blocks_per_cu(int which, int sym) {
     int nb = 0;
-    // (the symmetric and general variants differ by a few registers; size
-    // for the general one)
     const bool pipe = tile_pipe();
-    hipError_t e =
-        which == 0
-            ? (pipe ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_pipe<false, false>, 256, 0)
-                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<false, false>, 256, 0))
-            : (pipe ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_pipe<true, false>, 256, 0)
-                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<true, false>, 256, 0));
+    hipError_t e;
+    if (pipe)
+        e = which == 0 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_pipe<false, false>, 256, 0)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile_pipe<true, false>, 256, 0);
+    else if (sym)
+        e = which == 0 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<false, true>, 256, 0)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<true, true>, 256, 0);
+    else
+        e = which == 0 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<false, false>, 256, 0)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_tile<true, false>, 256, 0);
     return (e == hipSuccess && nb > 0) ? nb : 4;
 }
 

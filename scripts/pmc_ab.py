@@ -23,6 +23,20 @@ PASSES = (
     "SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES",
     "SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAVES",
 )
+# PMC_SET=mem: the memory pipeline (address translation, L1 -> L2 latency,
+# TA/TD/TCP stalls, DRAM credit stalls)
+MEM_PASSES = (
+    "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum "
+    "TCP_UTCL1_STALL_MULTI_MISS_sum",
+    "TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TOTAL_CACHE_ACCESSES_sum "
+    "TCP_PENDING_STALL_CYCLES_sum",
+    "TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TC_STALL_sum TD_TD_BUSY_sum "
+    "TCP_TCR_TCP_STALL_CYCLES_sum TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum "
+    "TCP_UTCL1_THRASHING_STALL_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum",
+    "TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_TAG_STALL_sum GRBM_GUI_ACTIVE",
+)
+if os.environ.get("PMC_SET") == "mem":
+    PASSES = MEM_PASSES
 
 
 def one(leg, env_extra, out):
