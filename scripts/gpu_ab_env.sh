@@ -10,7 +10,7 @@ tag=$1; rounds=$2; shift 2
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_scoring.py -m gpu -x -v --timeout 240 \
+timeout -s ABRT -k 10 300 python -X faulthandler -u -m pytest tests/test_gpu_scoring.py -m gpu -x -v --timeout 240 \
     --timeout-method thread > $out/gpu_tests.txt 2>&1 || exit $?
 tail -1 $out/gpu_tests.txt
 for r in $(seq $rounds); do
@@ -27,7 +27,8 @@ for f in sorted(glob.glob(sys.argv[1] + "/bench_*.json")):
     for l in open(f):
         if l.startswith("{"):
             d = json.loads(l); k = d["kernel"]; s = d["scorechain"]
-            print(f.split("/")[-1], "fills k_tile %.3f" % k["kernel_ms"]["tile"],
+            print(f.split("/")[-1], "fills call %.3f plan %.3f k_tile %.3f" % (
+                      k["ms_per_step"], k["kernel_ms"]["plan+tilemap"], k["kernel_ms"]["tile"]),
                   "frac %.3f" % d["roofline"]["frac"], "| whole k_tile %.3f" % s["kernel_ms"]["tile"],
                   "step %.3f" % s["ms_per_step"], "frac %.3f" % s["roofline_step"]["frac"])
 P

@@ -463,6 +463,47 @@ def test_unfused_tile_map_path(monkeypatch):
     assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
 
 
+@pytest.mark.parametrize("want_local", [False, True])
+def test_window_sizes_and_wide_blocks(want_local):
+    """k_plan's window search on windows of exactly 1..9 blocks starting at
+    every block of a chain (inside and past the 8 spans its one load reads),
+    clipped at both ends, whole short chains, wide blocks (>= 4095 bases:
+    k_tile reads their 16-B record) and empty ranges in between."""
+    from genomealignmenttools_amd import synth
+    tg, qg, ca = synth.small_case(seed=37, n_chains=200, max_blocks=40)
+    # widen a few blocks past the 12-bit size field (shift the rest of the chain)
+    rng = np.random.default_rng(37)
+    for c in rng.choice(ca.n, 20, replace=False):
+        b0, b1 = int(ca.blk_off[c]), int(ca.blk_off[c + 1])
+        k = b0 + int(rng.integers(0, b1 - b0))
+        grow = 5000
+        if ca.tend[c] + grow < ca.tsize[c] and ca.qend[c] + grow < ca.qsize[c]:
+            ca.blk_size[k] += grow
+            ca.blk_t[k + 1:b1] += grow
+            ca.blk_q[k + 1:b1] += grow
+            ca.tend[c] += grow
+            ca.qend[c] += grow
+    e, cs = _setup(None, tg, qg, ca)
+    R = []
+    for c in range(ca.n):
+        bt, _, bs = ca.blocks(c)
+        nb = len(bt)
+        ts, te = bt, bt + bs
+        R.append((c, ca.tstart[c], ca.tend[c]))
+        for i in range(nb):
+            for w in range(1, 10):
+                if i + w <= nb:
+                    R.append((c, ts[i], te[i + w - 1]))          # exactly w blocks
+                    R.append((c, ts[i] + 1, te[i + w - 1] - 1))  # clipped at both ends
+        R.append((c, ca.tend[c], ca.tend[c] + 10))               # empty
+    R = np.asarray(R, np.int64)
+    g, l, a = e.score_ranges(cs, R, want_local=want_local)
+    og, ol, oa = _oracle(tg, qg).score_ranges(ca, R)
+    assert np.array_equal(g, og) and np.array_equal(a, oa)
+    if want_local:
+        assert np.array_equal(l, ol)
+
+
 def _hip():
     import ctypes as C
     h = C.CDLL("libamdhip64.so")
