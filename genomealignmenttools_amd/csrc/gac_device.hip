@@ -71,8 +71,6 @@ hipError_t launch_whole_plan_sorted(const DChain *chains, int64_t n, int32_t *pe
                                     int32_t *nblk, int32_t *gflat, int32_t *pb0,
                                     int32_t *tile_r0, int32_t *inv, void *tmp,
                                     size_t &tmp_bytes, hipStream_t s);
-hipError_t launch_unpermute(const int32_t *inv, const SmallOut *pack, int64_t n, long long *g,
-                            long long *l, int32_t *ali, hipStream_t s);
 hipError_t launch_text_blocks(const uint8_t *text, const TextJob *jobs, int64_t n, const M25 &m,
                               long long *out, hipStream_t s);
 hipError_t launch_text_xover(const uint8_t *text, const TextXJob *jobs, int64_t n, const M25 &m,
@@ -226,12 +224,10 @@ struct gac_chainset {
     int32_t *w_empty = nullptr;    // chains without blocks (their results are 0)
     int64_t w_nempty = 0;
     // target-ordered plan (k_whole_keys): positions p are chains in target
-    // order; w_pb0[p] their first blocks, results packed per position and
-    // scattered back through w_inv (chain -> position, -1 without blocks)
+    // order; w_pb0[p] their first blocks, results stored to chain w_perm[p]
     bool w_sorted = false;
     int32_t *w_pb0 = nullptr;
-    int32_t *w_inv = nullptr;
-    SmallOut *w_pack = nullptr;
+    int32_t *w_perm = nullptr;
     // capacities (gac_chains_reupload refills these buffers when they fit)
     size_t cap_chains = 0, cap_blocks = 0, cap_blk12 = 0, cap_tspan = 0, cap_idx = 0;
     int32_t *d_stage = nullptr;  // the caller's block arrays, staged (3 x blocks)
@@ -242,13 +238,12 @@ struct gac_chainset {
 
 static void free_whole_plan(gac_chainset *cs) {
     void *w[] = {cs->w_rdesc, cs->w_nblk,  cs->w_gflat, cs->w_tile_r0, cs->w_status,
-                 cs->w_empty, cs->w_pb0,   cs->w_inv,   cs->w_pack};
+                 cs->w_empty, cs->w_pb0,   cs->w_perm};
     for (void *p : w)
         if (p) hipFree(p);
     cs->w_rdesc = nullptr;
     cs->w_nblk = cs->w_gflat = cs->w_tile_r0 = cs->w_status = cs->w_empty = nullptr;
-    cs->w_pb0 = cs->w_inv = nullptr;
-    cs->w_pack = nullptr;
+    cs->w_pb0 = cs->w_perm = nullptr;
     cs->w_sorted = false;
     cs->w_nempty = 0;
     cs->w_ready = false;
@@ -1785,15 +1780,15 @@ static int ensure_whole(gac_ctx *c, gac_chainset *cs, hipStream_t s) {
     HIPCHK(hipMemcpyAsync(cs->w_status, st, sizeof(st), hipMemcpyHostToDevice, s));
     // set order by default; GAC_WHOLE_ORDER=target plans the chains in
     // target order (r03k/r03m, C5: k_tile 2.29 vs 2.34 ms, but the scatter
-    // back to chain order costs 0.13 ms, so the call is slower)
+    // back to chain order cost 0.13 ms; r03zb, results stored straight to
+    // the chain: k_tile 2.34 vs 2.19 ms in set order, so set order stays)
     const char *ord = getenv("GAC_WHOLE_ORDER");
     const bool sorted = ord && !strcmp(ord, "target");
     if (sorted) {
         HIPCHK(hipMalloc(&cs->w_pb0, n * 4));
-        HIPCHK(hipMalloc(&cs->w_inv, n * 4));
-        HIPCHK(hipMalloc(&cs->w_pack, n * sizeof(SmallOut)));
+        HIPCHK(hipMalloc(&cs->w_perm, n * 4));
         unsigned long long *keys = nullptr;
-        int32_t *vals = nullptr, *perm = nullptr;
+        int32_t *vals = nullptr, *perm = nullptr, *inv = nullptr;
         void *tmp = nullptr;
         size_t tmp_bytes = 0;
         int rc = GAC_OK;
@@ -1801,14 +1796,27 @@ static int ensure_whole(gac_ctx *c, gac_chainset *cs, hipStream_t s) {
                                                 cs->w_nblk, cs->w_gflat, nullptr, nullptr, nullptr,
                                                 nullptr, tmp_bytes, s);
         if (e == hipSuccess) e = hipMalloc(&keys, 2 * n * sizeof(unsigned long long));
-        if (e == hipSuccess) e = hipMalloc(&vals, 2 * n * 4);
+        if (e == hipSuccess) e = hipMalloc(&vals, 3 * n * 4);
         perm = vals ? vals + n : nullptr;
+        inv = vals ? vals + 2 * n : nullptr;
         if (e == hipSuccess) e = hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 16));
         if (e == hipSuccess)
             e = launch_whole_plan_sorted(cs->chains, n, perm, keys, vals, cs->w_rdesc, cs->w_nblk,
-                                         cs->w_gflat, cs->w_pb0, cs->w_tile_r0, cs->w_inv, tmp,
+                                         cs->w_gflat, cs->w_pb0, cs->w_tile_r0, inv, tmp,
                                          tmp_bytes, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(cs->w_perm, perm, n * 4, hipMemcpyDeviceToDevice, s);
+        std::vector<int32_t> hinv(n);
+        if (e == hipSuccess) e = hipMemcpyAsync(hinv.data(), inv, n * 4, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
+        std::vector<int32_t> empty;  // chains without blocks (inv -1): zeroed by every call
+        for (int64_t i = 0; e == hipSuccess && i < n; ++i)
+            if (hinv[i] < 0) empty.push_back((int32_t)i);
+        cs->w_nempty = (int64_t)empty.size();
+        if (e == hipSuccess && !empty.empty()) {
+            e = hipMalloc(&cs->w_empty, empty.size() * 4);
+            if (e == hipSuccess)
+                e = hipMemcpy(cs->w_empty, empty.data(), empty.size() * 4, hipMemcpyHostToDevice);
+        }
         if (e != hipSuccess) rc = gac_fail(GAC_E_HIP, "whole-chain plan: %s", hipGetErrorString(e));
         if (keys) hipFree(keys);
         if (vals) hipFree(vals);
@@ -1856,7 +1864,7 @@ static int score_whole(gac_ctx *c, const gac_chainset *cs_in, uint32_t flags, lo
     a.nblk = cs->w_nblk;
     a.gflat = cs->w_gflat;
     a.pb0 = cs->w_sorted ? cs->w_pb0 : cs->w_gflat;
-    a.out_pack = cs->w_sorted ? cs->w_pack : nullptr;
+    a.out_perm = cs->w_sorted ? cs->w_perm : nullptr;
     a.tile_r0 = cs->w_tile_r0;
     a.status = cs->w_status;
     a.sum_head = c->sum_head;
@@ -1865,8 +1873,7 @@ static int score_whole(gac_ctx *c, const gac_chainset *cs_in, uint32_t flags, lo
     a.sup_tail = c->sup_tail;
     a.sup_tail_r = c->sup_tail_r;
     a.cap_tiles = (int32_t)(c->ws_tiles < INT32_MAX ? c->ws_tiles : INT32_MAX);
-    if (!cs->w_sorted)
-        HIPCHK(launch_zero_list(cs->w_empty, cs->w_nempty, d_g, a.want_local ? d_l : nullptr, d_ali, s));
+    HIPCHK(launch_zero_list(cs->w_empty, cs->w_nempty, d_g, a.want_local ? d_l : nullptr, d_ali, s));
     {
         PROF_BEGIN(GAC_K_TILE);
         HIPCHK(launch_tile(a, c->tile_grid_sym[a.sym ? 1 : 0][a.want_local ? 1 : 0], s));
@@ -1875,9 +1882,6 @@ static int score_whole(gac_ctx *c, const gac_chainset *cs_in, uint32_t flags, lo
     {
         PROF_BEGIN(GAC_K_COMBINE);
         HIPCHK(launch_combine(a, c->combine_grid, s));
-        if (cs->w_sorted)
-            HIPCHK(launch_unpermute(cs->w_inv, cs->w_pack, cs->n_chains, d_g,
-                                    a.want_local ? d_l : nullptr, d_ali, s));
         PROF_END(GAC_K_COMBINE);
     }
     if (hipEventRecord(c->ws_ev, s) == hipSuccess) c->ws_last = s;

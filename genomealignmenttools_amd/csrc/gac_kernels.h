@@ -101,8 +101,7 @@ struct Range {
 };
 
 // Result of one range of a small batch (k_small writes it straight to pinned
-// host memory); also the packed per-position result of a target-ordered
-// whole-chain plan (out_pack, scattered back to chain order by k_unpermute).
+// host memory).
 struct SmallOut {
     long long g, l;
     int32_t ali, pad;
@@ -157,8 +156,8 @@ struct ScoreArgs {
     int32_t sym;               // matrix is strand-symmetric: coef[8..15] == 0
     int32_t scan64;            // A/B probe (GAC_TILE_SCAN64=1): k_tile's 64-bit scans only
     GapDev gap;
-    SmallOut *out_pack;  // non-null: results go to out_pack[range] (the whole-chain
-                         // plan in target order; k_unpermute restores chain order)
+    const int32_t *out_perm;  // non-null: the results of range (position) p go to
+                              // chain out_perm[p] (the whole-chain plan in target order)
 };
 
 constexpr int kSmallMax = 256;  // ranges per small-batch call

@@ -716,7 +716,8 @@ __global__ void __launch_bounds__(256) k_whole_plan(const DChain *chains, int64_
 // chains that overlap on the target are scored by neighbouring tiles, so an
 // XCD's L2 (and the Infinity Cache) serves their shared target-plane lines
 // once instead of once per chain.  Flat offsets are the scan of the permuted
-// block counts; results go to out_pack[p] and k_unpermute scatters them back.
+// block counts; the results of position p are stored straight to chain
+// perm[p] (out_perm).
 constexpr int kOrderBits = 36;  // sort key bits: global target base of the chain start
 
 __global__ void __launch_bounds__(256) k_whole_keys(const DChain *chains, int64_t n,
@@ -758,22 +759,6 @@ __global__ void __launch_bounds__(256) k_whole_plan_sorted(const DChain *chains,
     const int64_t g = gflat[p], end = g + ch.nblk;
     for (int64_t t = (g + kTileBlocks - 1) / kTileBlocks; t * kTileBlocks < end; ++t)
         tile_r0[t] = (int32_t)p;
-}
-
-// out[c] = out_pack[inv[c]] (0 for chains without blocks): one random
-// 24-B record per chain, from a buffer just written (Infinity-Cache resident
-// at these sizes), coalesced stores
-__global__ void __launch_bounds__(256) k_unpermute(const int32_t *inv, const SmallOut *pack,
-                                                   int64_t n, long long *g, long long *l,
-                                                   int32_t *ali) {
-    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n) return;
-    const int32_t p = inv[c];
-    SmallOut o = {0, 0, 0, 0};
-    if (p >= 0) o = pack[p];
-    g[c] = o.g;
-    ali[c] = o.ali;
-    if (l) l[c] = o.l;
 }
 
 // outputs of the ranges in `list` (chains without blocks) := 0
@@ -947,18 +932,10 @@ __device__ __forceinline__ ChunkRef chunk_prep(const WaveLds &L, int j) {
 template <bool LOCAL>
 __device__ __forceinline__ void seg_store(const ScoreArgs &a, int ri, long long g, int ali,
                                           const Elem &e) {
-    if (a.out_pack) {
-        SmallOut o;
-        o.g = g;
-        o.l = LOCAL ? max2(0, max2(e.C, e.D)) : 0;
-        o.ali = ali;
-        o.pad = 0;
-        a.out_pack[ri] = o;
-        return;
-    }
-    a.out_g[ri] = g;
-    a.out_ali[ri] = ali;
-    if (LOCAL) a.out_l[ri] = max2(0, max2(e.C, e.D));
+    const int o = a.out_perm ? a.out_perm[ri] : ri;
+    a.out_g[o] = g;
+    a.out_ali[o] = ali;
+    if (LOCAL) a.out_l[o] = max2(0, max2(e.C, e.D));
 }
 
 // one step of k_tile's segmented (by range) inclusive scan: the source
@@ -1895,14 +1872,6 @@ hipError_t launch_whole_plan_sorted(const DChain *chains, int64_t n, int32_t *pe
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_whole_plan_sorted, grid, dim3(256), 0, s, chains, perm, n, gflat, rdesc,
                        pb0, tile_r0, inv);
-    return hipGetLastError();
-}
-
-hipError_t launch_unpermute(const int32_t *inv, const SmallOut *pack, int64_t n, long long *g,
-                            long long *l, int32_t *ali, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_unpermute, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, inv, pack,
-                       n, g, l, ali);
     return hipGetLastError();
 }
 
