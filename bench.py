@@ -71,6 +71,10 @@ REF_TOOL = os.path.join(REPO, "oracle", "_ref", "chainNet")
 SC_TOOL = os.path.join(PKG, "bin", "scoreChain")
 REF_SC_TOOL = os.path.join(REPO, "oracle", "_ref", "scoreChain")
 SAMPLE_TARGETS = ("chr21", "chr22")
+# all-cores baseline: the reference split by target chromosome, one process
+# per sequence, run side by side (how the reference is parallelised on a
+# cluster: chainNet per target chromosome)
+ALL_CORES_TARGETS = tuple(f"chr{i}" for i in range(7, 23))
 
 
 def log(*a):
@@ -562,6 +566,88 @@ def cpu_baseline_c5(d, ours):
                       f"wall time; their target-net sections compared with the headline's)"}
 
 
+def _split_by_target(path, targets, dst):
+    """One file per target in `targets` holding its chains (file order kept):
+    {target: path}."""
+    with open(path, "rb") as f:
+        data = f.read()
+    pieces = data.split(b"\nchain ")  # each piece: a chain without "chain " and its last newline
+    del data
+    if pieces[0].startswith(b"chain "):
+        pieces[0] = pieces[0][6:]
+    else:  # '#' lines before the first chain
+        pieces = pieces[1:]
+    last = len(pieces) - 1
+    keep = {t.encode(): [] for t in targets}
+    for k, p in enumerate(pieces):
+        i = p.find(b" ")
+        sel = keep.get(p[i + 1:p.find(b" ", i + 1)])
+        if sel is not None:
+            sel.append(b"chain " + p + (b"\n" if k < last else b""))
+    out = {}
+    for t, chunks in keep.items():
+        name = os.path.join(dst, f"allcores.{t.decode()}.chain")
+        with open(name, "wb") as f:
+            f.writelines(chunks)
+        out[t.decode()] = name
+    return out
+
+
+def _target_bases(d, targets):
+    """Aligned bases, up to the netting stop (the headline's measure), of the
+    chains whose target is in `targets`, from chains.bin."""
+    ch = load_chains_bin(d)
+    with open(os.path.join(d, "t.sizes")) as f:
+        names = [line.split()[0] for line in f if line.strip()]
+    ids = np.array([names.index(t) for t in targets if t in names], np.int32)
+    neg = np.flatnonzero(ch["score"] < 0)
+    stop = int(neg[0]) if len(neg) else ch["n"]
+    cs = np.concatenate([[0], np.cumsum(ch["bs"], dtype=np.int64)])
+    per = cs[ch["off"][1:stop + 1]] - cs[ch["off"][:stop]]
+    return int(per[np.isin(ch["tseq"][:stop], ids)].sum())
+
+
+def cpu_baseline_all_cores(d, cores):
+    """The reference chainNet -rescore on ALL_CORES_TARGETS' chains, one process
+    per target sequence, `cores` of them at a time: the chains' aligned bases up
+    to the netting stop / wall time."""
+    p = lambda x: os.path.join(d, x)
+    files = _split_by_target(p("in.chain"), ALL_CORES_TARGETS, d)
+    jobs = sorted(files.items(), key=lambda kv: -os.path.getsize(kv[1]))  # largest first
+    t0 = time.time()
+    running, done = [], []
+    while jobs or running:
+        while jobs and len(running) < cores:
+            t, f = jobs.pop(0)
+            o = p(f"allcores.{t}")
+            pr = subprocess.Popen([REF_TOOL, f, p("t.sizes"), p("q.sizes"), o + ".t.net",
+                                   o + ".q.net", "-rescore", f"-tNibDir={p('t.2bit')}",
+                                   f"-qNibDir={p('q.2bit')}", "-linearGap=loose"],
+                                  stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+            running.append((t, o, pr))
+        time.sleep(0.05)
+        for item in list(running):
+            if item[2].poll() is not None:
+                running.remove(item)
+                if item[2].returncode != 0:
+                    raise RuntimeError(f"reference chainNet on {item[0]}: "
+                                       f"{item[2].stderr.read()[-300:]!r}")
+                done.append(item)
+    wall = time.time() - t0
+    bases = _target_bases(d, [t for t, _, _ in done])
+    for _, o, _ in done:
+        for x in (o + ".t.net", o + ".q.net"):
+            os.remove(x)
+    for f in files.values():
+        os.remove(f)
+    return {"value": bases / wall / 1e9, "unit": "Gbases/s", "cores": cores, "kind": "reference",
+            "seconds": wall, "sample_aligned_bases": bases,
+            "sample": f"reference chainNet -rescore (oracle/_ref) on the C5 chains of "
+                      f"{len(done)} target sequences ({ALL_CORES_TARGETS[0]}..{ALL_CORES_TARGETS[-1]}), "
+                      f"one process per sequence, {cores} at a time; value = their chains' aligned bases "
+                      f"up to the netting stop (the headline's measure) / wall time"}
+
+
 def scorechain_e2e_leg(d, info, steps, ref_sample):
     """bin/scoreChain end to end on C5 (every chain rescored: global score,
     written as chain text), input aligned bases / wall time; with
@@ -797,6 +883,11 @@ def main():
             out["cpu_baseline"] = cpu_baseline_c5(d, out_base)
         except Exception as ex:  # reported, never fatal
             out["cpu_baseline"] = {"error": str(ex)[:300]}
+        try:
+            out["cpu_baseline"]["all_cores"] = cpu_baseline_all_cores(
+                d, min(16, host_threads(), len(ALL_CORES_TARGETS)))
+        except Exception as ex:  # reported, never fatal
+            out["cpu_baseline"]["all_cores"] = {"error": str(ex)[:300]}
     if rank == 0 and world == 1 and not args.no_scorechain:
         try:
             out["scorechain_e2e"] = scorechain_e2e_leg(d, info, 2, not args.no_cpu_baseline)
