@@ -805,9 +805,17 @@ def main():
     run_id = f"{os.environ.get('TORCHELASTIC_RUN_ID', 'x')}-{os.environ.get('MASTER_PORT', '0')}"
     step_no = [0]
 
+    # host threads per rank: the launcher's GAC_THREADS / OMP_NUM_THREADS, else
+    # this process's cores shared by the node's ranks (N ranks x all cores
+    # would oversubscribe the host)
+    tool_threads = {}
+    if world > 1 and not (os.environ.get("GAC_THREADS") or os.environ.get("OMP_NUM_THREADS")):
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        tool_threads["GAC_THREADS"] = str(max(1, len(os.sched_getaffinity(0)) // local_world))
+
     def step_env():
         step_no[0] += 1
-        return dict(os.environ, GAC_RANK_TOKEN=f"{run_id}-{step_no[0]}")
+        return dict(os.environ, GAC_RANK_TOKEN=f"{run_id}-{step_no[0]}", **tool_threads)
 
     for _ in range(args.warmup):
         barrier()
