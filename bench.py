@@ -851,7 +851,7 @@ def main():
         "config": {"workload": "chainNet -rescore end to end (bin/chainNet), C5 whole genome"
                                + ("" if world == 1 else f", chromosome sides split over {world} ranks"),
                    **info, "parallelism": f"chromosome-side shards x{world}",
-                   "host_threads_per_rank": host_threads(), "tool_stages": stages},
+                   "host_threads_per_rank": int(tool_threads.get("GAC_THREADS", host_threads())), "tool_stages": stages},
     }
     if rank == 0 and world == 1 and not args.no_c2:
         try:
