@@ -17,7 +17,8 @@ in about a minute on the GPU box's host.
   C3:        C2 + 1000 planted chain-breaking-alignment loci on chr1:
              chainCleaner -net= (about 12.5k suspects removed)
   C4-shaped: 24 x 21 chromosome pairs x 2 strands, power-law blocks per
-             pair, 1.2 M PSL blocks: axtChain -psl
+             pair, 1.2 M PSL blocks (host and device DP) and 5 M PSL blocks
+             (host DP): axtChain -psl
 plus the edge cases the round-1 review listed: a custom -linearGap file on
 the device, zero-size terminal blocks, chainNet -rescore's subset-upload
 branch (a sequence missing from the 2bit), no partial fills at all, and a
@@ -272,6 +273,26 @@ def test_c4_shaped_axtchain(tmp_path):
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr
     _same(os.path.join(d, "gpu.chain"), os.path.join(d, "ref.chain"))
+
+
+@pytest.mark.timeout(1200)
+def test_c4_shaped_axtchain_5m_blocks(tmp_path):
+    """The C4 shape at 5 M PSL blocks (a tenth of SURVEY §8(d)'s 50 M; the
+    reference takes about a minute here), the product's host DP, byte for
+    byte against the reference run in the same test."""
+    from genomealignmenttools_amd import synth
+    tg, qg, pairs, b = synth.psl_c4(7, 5_000_000, n_t=24, n_q=21, tsize=12_000_000,
+                                    qsize=10_000_000)
+    assert len(b["t"]) > 4_900_000
+    d = str(tmp_path)
+    synth.write_2bit(tg, os.path.join(d, "t.2bit"))
+    synth.write_2bit(qg, os.path.join(d, "q.2bit"))
+    synth.write_psl_c4(tg, qg, pairs, b, os.path.join(d, "in.psl"), 7)
+    del tg, qg, b
+    args = ["-linearGap=loose", "-psl", "in.psl", "t.2bit", "q.2bit"]
+    _run([_bin("axtChain")] + args + ["ours.chain"], cwd=d)
+    _run([_ref("axtChain")] + args + ["ref.chain"], cwd=d, timeout=900)
+    _same(os.path.join(d, "ours.chain"), os.path.join(d, "ref.chain"))
 
 
 # ---------------------------------------------------------------- edge cases
