@@ -1619,11 +1619,12 @@ static int wait_status(gac_ctx *c, hipStream_t s, int32_t tag, int32_t st[4]) {
     }
 }
 
-// One call = 5 launches (k_plan, k_scan_agg, k_tilemap, k_tile, k_combine); the
-// host waits only for k_scan_agg's status words (pinned memory), not for the
-// scoring itself.  The flat block count W is only known on the
+// One call = k_plan, the tile map (k_tilemap_fused, or k_scan_agg + k_tilemap
+// above 1 M ranges), k_tile and the cross-tile fold (k_fold_tiles +
+// k_fold_super); the host waits only for the status words (pinned memory),
+// not for the scoring itself.  The flat block count W is only known on the
 // device (ranges may overlap), so the kernels check the workspace capacity
-// themselves; on overflow k_tile / k_combine do nothing and the call grows the
+// themselves; on overflow k_tile and the folds do nothing and the call grows the
 // workspace to the reported {W, T} and runs once more (first call or a larger
 // batch only).
 // Checks shared by both scoring paths, the per-setup block gaps, and the

@@ -598,7 +598,7 @@ __device__ long long scan_totals(const ScoreArgs &a, int G, long long *s_wsum) {
 // {W, T, overflow} for the later kernels, and the same, tagged with the
 // call's sequence number, straight into the host's pinned status words: the
 // host learns whether the workspace sufficed as soon as this kernel ends,
-// while k_tilemap / k_tile / k_combine still run.
+// while k_tilemap / k_tile / the folds still run.
 __device__ __forceinline__ void publish_status(const ScoreArgs &a, long long W) {
     const long long T = (W + kTileBlocks - 1) / kTileBlocks;
     const bool over = W >= 0x7fffffffLL || T > a.cap_tiles;
