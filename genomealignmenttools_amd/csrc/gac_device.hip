@@ -15,6 +15,7 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <memory>
 #include <vector>
 
 #include "gac_dp.h"
@@ -1377,7 +1378,12 @@ static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs)
         fprintf(stderr, "[gac_chains_upload] %-22s %.3f s\n", what, t - t_lap);
         t_lap = t;
     };
-    std::vector<DChain> ch(n ? n : 1);
+    // (not value-initialised: upload_pass1 writes every field of every good
+    // chain on its own thread, so the 64 B/chain are first touched in
+    // parallel instead of zeroed on this thread -- 320 MB at C5)
+    const size_t n_rec = (size_t)(n ? n : 1);
+    std::unique_ptr<DChain[]> ch(new DChain[n_rec]);
+    if (!n) memset(ch.get(), 0, sizeof(DChain));
     // tasks: contiguous chain ranges of about equal blocks + chains
     const int nt = std::max(1, std::min(64, gac_host_threads()));
     const int ntask = (int)std::min<int64_t>(std::max<int64_t>(n, 1), 8 * nt);
@@ -1396,7 +1402,7 @@ static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs)
     UploadJob J;
     J.c = c;
     J.d = d;
-    J.ch = ch.data();
+    J.ch = ch.get();
     J.cut = cut.data();
     J.ntask = ntask;
     J.next = 0;
@@ -1445,7 +1451,7 @@ static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs)
     const size_t nb = (size_t)d->n_blocks;
     // the caller's block arrays, staged; blocks / spans / buckets are built
     // from them on the device (k_build_*)
-    hipError_t e = ensure_buf((void **)&cs->chains, &cs->cap_chains, ch.size(), sizeof(DChain));
+    hipError_t e = ensure_buf((void **)&cs->chains, &cs->cap_chains, n_rec, sizeof(DChain));
     if (e == hipSuccess) e = ensure_buf((void **)&cs->blk, &cs->cap_blocks, nb + 8, sizeof(int4));
     if (e == hipSuccess) e = ensure_buf((void **)&cs->blk12, &cs->cap_blk12, nb + 8, sizeof(Blk12));
     if (e == hipSuccess) e = ensure_buf((void **)&cs->tspan, &cs->cap_tspan, nb + 8, sizeof(int2));
@@ -1456,7 +1462,7 @@ static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs)
     int32_t *d_bt = cs->d_stage;
     int rc = GAC_OK;
     lap("allocations");
-    if (e == hipSuccess) rc = upload_staged(c, cs->chains, ch.data(), ch.size() * sizeof(DChain));
+    if (e == hipSuccess) rc = upload_staged(c, cs->chains, ch.get(), n_rec * sizeof(DChain));
     if (e == hipSuccess && rc == GAC_OK && nb) rc = upload_staged(c, d_bt, d->blk_t, nb * 4);
     if (e == hipSuccess && rc == GAC_OK && nb) rc = upload_staged(c, d_bt + nb, d->blk_q, nb * 4);
     if (e == hipSuccess && rc == GAC_OK && nb) rc = upload_staged(c, d_bt + 2 * nb, d->blk_size, nb * 4);
