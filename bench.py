@@ -18,7 +18,11 @@ rescoring of every partial target fill, both nets written, process exit.
 value = the aligned bases of the netted input chains (score >= 0) / wall time
 per step (SURVEY §8(d) primary metric).
 
-N > 1 (torchrun, one process per GPU): STRONG scaling on the same fixed input.
+N > 1 (one process per GPU): `python bench.py --gpus N` starts the N ranks
+itself (one torch.distributed.run child, before anything touches a GPU) unless
+it already runs under torchrun; every rank checks that the process group
+(backend nccl = RCCL) has --gpus ranks, and n_gpus is that group's size.
+STRONG scaling on the same fixed input.
 Every rank runs the tool with -nranks=N -rank=r -gpu=LOCAL_RANK each step:
 rank r nets the chromosome sides it owns (contiguous runs of each sizes file,
 balanced by length), parses only the chains on its sides, loads only its
@@ -101,12 +105,107 @@ def parse():
                    help="N = 1: also run the N > 1 scorechain leg (world-1 RCCL group)")
     p.add_argument("--pmc-child", choices=["fills", "scorechain"], help=argparse.SUPPRESS)
     p.add_argument("--gen-only", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--launch-check", action="store_true",
+                   help="start the ranks, report the process group each one sees, exit")
     return p.parse_args()
+
+
+# ---------------------------------------------------------------- launching
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_cmd(gpus, argv, port):
+    """The one child that runs N ranks when `bench.py --gpus N` is started
+    without a torchrun environment: torch.distributed.run, one process per
+    GPU on this node, rendezvous on 127.0.0.1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+            os.path.abspath(__file__), *argv]
+
+
+def maybe_self_launch(args):
+    """`python bench.py --gpus N`, N > 1, outside torchrun: start the N ranks
+    as a child process (before anything here touches a GPU) and leave with its
+    exit status.  Inside torchrun (WORLD_SIZE set) nothing happens here; the
+    ranks check WORLD_SIZE == --gpus themselves."""
+    if "WORLD_SIZE" in os.environ or args.gpus <= 1:
+        return
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL between processes)
+    log(f"bench: starting {args.gpus} ranks (torch.distributed.run)")
+    r = subprocess.run(launch_cmd(args.gpus, sys.argv[1:], free_port()), env=env)
+    sys.exit(r.returncode)
+
+
+def init_ranks(args):
+    """(dist or None, world, rank, local, one_gpu, group): this rank's place.
+    One process per GPU: backend nccl (RCCL over xGMI) on cuda:LOCAL_RANK;
+    GAC_BENCH_ONE_GPU=1 is the rehearsal with every rank on device 0 over
+    gloo.  Fails loudly when the group is not the --gpus the run asked for."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    one_gpu = bool(os.environ.get("GAC_BENCH_ONE_GPU"))
+    if one_gpu:
+        local = 0
+        os.environ["LOCAL_RANK"] = "0"
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if world == 1:
+        return None, 1, 0, 0, one_gpu, None
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if one_gpu:  # (RCCL wants one device per rank)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    else:
+        ndev = torch.cuda.device_count()
+        if ndev < int(os.environ.get("LOCAL_WORLD_SIZE", world)):
+            raise SystemExit(f"bench: {ndev} GPUs visible for {world} ranks on this node")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device(f"cuda:{local}"))
+    if dist.get_world_size() != args.gpus:
+        raise SystemExit(f"bench: process group has {dist.get_world_size()} ranks, "
+                         f"--gpus {args.gpus}")
+    me = {"rank": rank, "local_rank": local, "device": "cpu (rehearsal)" if one_gpu else
+          f"cuda:{local}", "pid": os.getpid()}
+    if not one_gpu:
+        pr = torch.cuda.get_device_properties(local)
+        me.update(name=pr.name, uuid=str(getattr(pr, "uuid", "")),
+                  pci_bus_id=getattr(pr, "pci_bus_id", None))
+    group = [None] * world
+    dist.all_gather_object(group, me)
+    return dist, world, rank, local, one_gpu, {"backend": dist.get_backend(),
+                                               "world_size": dist.get_world_size(),
+                                               "ranks": group}
 
 
 def host_threads():
     v = os.environ.get("GAC_THREADS") or os.environ.get("OMP_NUM_THREADS")
     return int(v) if v else len(os.sched_getaffinity(0))
+
+
+def host_cpu():
+    """The host the CPU baseline ran on: CPU model, the machine's logical
+    CPUs (nproc) and the CPUs this process may use (its share of the box)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "host_nproc": os.cpu_count(),
+            "affinity_cpus": len(os.sched_getaffinity(0))}
 
 
 # ---------------------------------------------------------------- input files
@@ -744,28 +843,22 @@ def main():
     if args.pmc_child:
         pmc_child(args)
         return
+    maybe_self_launch(args)
+    if args.launch_check:
+        dist, world, rank, local, one_gpu, group = init_ranks(args)
+        if rank == 0:
+            print(json.dumps({"launch_check": True, "n_gpus": world,
+                              "process_group": group}), flush=True)
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    one_gpu = bool(os.environ.get("GAC_BENCH_ONE_GPU"))  # rehearsal: every rank on device 0
-    if one_gpu:
-        local = 0
-        os.environ["LOCAL_RANK"] = "0"
-
     d = info = None
     if rank == 0:  # generated before any process opens a device
         d, info = c5_files(args)
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if one_gpu:  # (RCCL wants one device per rank)
-            dist.init_process_group("gloo", rank=rank, world_size=world)
-        else:
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", rank=rank, world_size=world,
-                                    device_id=torch.device(f"cuda:{local}"))
+    dist, world, rank, local, one_gpu, group = init_ranks(args)
     rdist = None
     if world == 1 and args.sharded_scorechain:
         # rehearsal of the N > 1 scoreChain leg: a world-1 RCCL group, made
@@ -851,8 +944,14 @@ def main():
         "config": {"workload": "chainNet -rescore end to end (bin/chainNet), C5 whole genome"
                                + ("" if world == 1 else f", chromosome sides split over {world} ranks"),
                    **info, "parallelism": f"chromosome-side shards x{world}",
-                   "host_threads_per_rank": int(tool_threads.get("GAC_THREADS", host_threads())), "tool_stages": stages},
+                   "host_threads_per_rank": int(tool_threads.get("GAC_THREADS", host_threads())),
+                   "tool_stages": stages},
+        # the group as torch.distributed (RCCL) saw it: n_gpus above is its size
+        "process_group": group or {"backend": None, "world_size": 1,
+                                   "ranks": [{"rank": 0, "local_rank": 0, "device": "cuda:0"}]},
     }
+    if one_gpu:
+        out["rehearsal"] = "GAC_BENCH_ONE_GPU: every rank on device 0 over gloo (not a GPU curve)"
     if rank == 0 and world == 1 and not args.no_c2:
         try:
             out["c2"] = c2_leg(args, args.c2_steps, 1)
@@ -891,6 +990,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline_c5(d, out_base)
         except Exception as ex:  # reported, never fatal
             out["cpu_baseline"] = {"error": str(ex)[:300]}
+        out["cpu_baseline"].update(host_cpu())
         try:
             out["cpu_baseline"]["all_cores"] = cpu_baseline_all_cores(
                 d, min(16, host_threads(), len(ALL_CORES_TARGETS)))

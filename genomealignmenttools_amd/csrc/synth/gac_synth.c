@@ -578,10 +578,406 @@ static char *path_in(const char *dir, const char *name) {
     return p;
 }
 
+/* ---------------------------------------------------------------- C4 (PSL) */
+/* n_blocks PSL blocks over nt x nq chromosome pairs x 2
+ * strands, blocks per pair by a power law (alpha 1.2 over a seeded
+ * permutation of the pairs, at least 50), 80 % of each pair's blocks on
+ * planted collinear paths of ~200 blocks (geometric sizes of mean 50 capped
+ * at 500; gaps 80 % 1-59 bp, 20 % 60-4999 bp on the target, the query or
+ * both, query gaps jittered by -20..19), the query bases under them := the
+ * target's with 12 % substitutions (reverse-complemented on '-'), and 20 %
+ * random blocks (20-299 bp anywhere).  Records: a path's blocks in runs of 5,
+ * one record per random block, all records in a seeded random order (as
+ * lastz job outputs are concatenated).  The same statistical model as
+ * synth.py's psl_c4, drawn from per-pair streams (any thread count gives the
+ * same bytes). */
+enum { P_C4PAIRS = 9, P_C4PAIR, P_C4MUT, P_C4ORDER };
+
+typedef struct {
+    int ti, qi, strand;
+    int64_t nb, ncol;      /* requested blocks, collinear share */
+    int64_t n;             /* blocks kept: collinear (after the bounds filter) + random */
+    int64_t nc;            /* collinear blocks kept (first nc of the arrays) */
+    int32_t *bt, *bq, *bs; /* n blocks; collinear first, in path order */
+    int32_t *path;         /* path of each collinear block */
+    int64_t nrec, rec0;    /* records of this pair, first global record */
+    int64_t *rec_first;    /* [nrec + 1]: first block of each record */
+} c4pair;
+
+typedef struct {
+    c4pair *P;
+    int np;
+    int64_t tsize, qsize;
+    _Atomic int next;
+    const int *qorder_pairs; /* pairs grouped by query sequence (mutation pass) */
+    const int *qoff;
+} c4job;
+
+static void *c4_pair_thread(void *arg) {
+    c4job *J = arg;
+    for (;;) {
+        const int w = atomic_fetch_add(&J->next, 1);
+        if (w >= J->np)
+            break;
+        c4pair *p = &J->P[w];
+        rng_t r;
+        rng_seed(&r, g_seed, P_C4PAIR, (uint64_t)w);
+        const int64_t ncol = p->ncol, nr = p->nb - ncol;
+        int64_t npath = ncol / 200;
+        if (npath < 1)
+            npath = 1;
+        p->bt = malloc((size_t)(p->nb + 1) * 4);
+        p->bq = malloc((size_t)(p->nb + 1) * 4);
+        p->bs = malloc((size_t)(p->nb + 1) * 4);
+        p->path = malloc((size_t)(ncol + 1) * 4);
+        int64_t *lt = malloc((size_t)(ncol + 1) * 8), *lq = malloc((size_t)(ncol + 1) * 8);
+        int32_t *sz = malloc((size_t)(ncol + 1) * 4);
+        /* path k holds blocks [k*ncol/npath, (k+1)*ncol/npath): local offsets */
+        int64_t k0 = 0;
+        for (int64_t k = 0; k < npath; ++k) {
+            const int64_t a = k0, b = (k + 1) * ncol / npath;
+            int64_t ct = 0, cq = 0, pdt = 0, pdq = 0;
+            for (int64_t i = a; i < b; ++i) {
+                int64_t s = geometric(&r, 1.0 / 50.0);
+                if (s > 500)
+                    s = 500;
+                const int mode = (int)uniform_int(&r, 0, 3);
+                const int64_t g = unif(&r) < 0.8 ? uniform_int(&r, 1, 60) : uniform_int(&r, 60, 5000);
+                int64_t dq = g + uniform_int(&r, -20, 20);
+                if (dq < 1)
+                    dq = 1;
+                if (i > a) {
+                    ct += pdt;
+                    cq += pdq;
+                }
+                lt[i] = ct;
+                lq[i] = cq;
+                sz[i] = (int32_t)s;
+                ct += s;
+                cq += s;
+                pdt = mode == 1 ? 0 : g;
+                pdq = mode == 0 ? 0 : dq;
+            }
+            /* origin: uniform where the path fits */
+            const int64_t rt = J->tsize - ct - 1 > 1 ? J->tsize - ct - 1 : 1;
+            const int64_t rq = J->qsize - cq - 1 > 1 ? J->qsize - cq - 1 : 1;
+            const int64_t t0 = (int64_t)(unif(&r) * (double)rt), q0 = (int64_t)(unif(&r) * (double)rq);
+            for (int64_t i = a; i < b; ++i) {
+                const int64_t bt = t0 + lt[i], bq = q0 + lq[i];
+                if (bt + sz[i] < J->tsize && bq + sz[i] < J->qsize) {
+                    p->bt[p->nc] = (int32_t)bt;
+                    p->bq[p->nc] = (int32_t)bq;
+                    p->bs[p->nc] = sz[i];
+                    p->path[p->nc++] = (int32_t)k;
+                }
+            }
+            k0 = b;
+        }
+        free(lt);
+        free(lq);
+        free(sz);
+        p->n = p->nc;
+        for (int64_t i = 0; i < nr; ++i, ++p->n) {
+            p->bs[p->n] = (int32_t)uniform_int(&r, 20, 300);
+            p->bt[p->n] = (int32_t)uniform_int(&r, 0, J->tsize - 400);
+            p->bq[p->n] = (int32_t)uniform_int(&r, 0, J->qsize - 400);
+        }
+        /* records: collinear runs of 5 (cut at path changes), random singles */
+        p->rec_first = malloc((size_t)(p->nc + nr + 2) * 8);
+        p->nrec = 0;
+        for (int64_t i = 0; i < p->nc; ++i)
+            if (i == 0 || i % 5 == 0 || p->path[i] != p->path[i - 1])
+                p->rec_first[p->nrec++] = i;
+        for (int64_t i = p->nc; i < p->n; ++i)
+            p->rec_first[p->nrec++] = i;
+        p->rec_first[p->nrec] = p->n;
+    }
+    return NULL;
+}
+
+static const genome_t *C4T, *C4Q;
+
+/* plant the collinear blocks' homology, one query sequence per work item
+ * (its pairs in pair order), from per-pair mutation streams */
+static void *c4_mut_thread(void *arg) {
+    c4job *J = arg;
+    for (;;) {
+        const int w = atomic_fetch_add(&J->next, 1);
+        if (w >= C4Q->n)
+            break;
+        uint8_t *qp = C4Q->packed[w];
+        for (int k = J->qoff[w]; k < J->qoff[w + 1]; ++k) {
+            const int pi = J->qorder_pairs[k];
+            const c4pair *p = &J->P[pi];
+            const uint8_t *tp = C4T->packed[p->ti];
+            rng_t r;
+            rng_seed(&r, g_seed, P_C4MUT, (uint64_t)pi);
+            uint64_t bits = 0;
+            int left = 0;
+            for (int64_t b = 0; b < p->nc; ++b)
+                for (int64_t j = 0; j < p->bs[b]; ++j) {
+                    if (!left) {
+                        bits = next64(&r);
+                        left = 8;
+                    }
+                    const int q = get_code(tp, p->bt[b] + j) ^ g_xor[bits & 255];
+                    bits >>= 8;
+                    --left;
+                    const int64_t rp = p->bq[b] + j;
+                    if (p->strand)
+                        set_code(qp, J->qsize - 1 - rp, q ^ 2);
+                    else
+                        set_code(qp, rp, q);
+                }
+        }
+    }
+    return NULL;
+}
+
+typedef struct {
+    const c4pair *P;
+    int np;
+    const int64_t *perm; /* output position -> global record */
+    int64_t nrec, per, nchunks;
+    int64_t tsize, qsize;
+    char **buf;
+    size_t *len;
+    _Atomic int64_t next;
+} c4fmt;
+
+static void *c4_fmt_thread(void *arg) {
+    c4fmt *J = arg;
+    for (;;) {
+        const int64_t k = atomic_fetch_add(&J->next, 1);
+        if (k >= J->nchunks)
+            break;
+        const int64_t a = k * J->per, b = a + J->per < J->nrec ? a + J->per : J->nrec;
+        size_t cap = 0;
+        int *pidx = malloc((size_t)(b - a + 1) * sizeof(int));
+        for (int64_t s = a; s < b; ++s) {
+            const int64_t g = J->perm[s];
+            int lo = 0, hi = J->np - 1; /* the pair owning global record g */
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) / 2;
+                if (J->P[mid].rec0 <= g) lo = mid;
+                else hi = mid - 1;
+            }
+            pidx[s - a] = lo;
+            const c4pair *p = &J->P[lo];
+            const int64_t r = g - p->rec0;
+            cap += 160 + 36 * (size_t)(p->rec_first[r + 1] - p->rec_first[r]);
+        }
+        char *buf = malloc(cap), *o = buf;
+        for (int64_t s = a; s < b; ++s) {
+            const c4pair *p = &J->P[pidx[s - a]];
+            const int64_t r = J->perm[s] - p->rec0, b0 = p->rec_first[r], b1 = p->rec_first[r + 1];
+            int64_t qs = INT64_MAX, qe = 0, te = 0;
+            for (int64_t i = b0; i < b1; ++i) {
+                if (p->bq[i] < qs) qs = p->bq[i];
+                if (p->bq[i] + p->bs[i] > qe) qe = p->bq[i] + p->bs[i];
+                if (p->bt[i] + p->bs[i] > te) te = p->bt[i] + p->bs[i];
+            }
+            if (p->strand) {
+                const int64_t x = J->qsize - qe;
+                qe = J->qsize - qs;
+                qs = x;
+            }
+            o += sprintf(o, "0\t0\t0\t0\t0\t0\t0\t0\t%c\t%s\t%lld\t%lld\t%lld\t%s\t%lld\t%d\t%lld\t%lld\t",
+                         p->strand ? '-' : '+', C4Q->names[p->qi], (long long)J->qsize,
+                         (long long)qs, (long long)qe, C4T->names[p->ti], (long long)J->tsize,
+                         p->bt[b0], (long long)te, (long long)(b1 - b0));
+            const int32_t *cols[3] = {p->bs, p->bq, p->bt};
+            for (int c = 0; c < 3; ++c) {
+                for (int64_t i = b0; i < b1; ++i) {
+                    o = put_i64(o, cols[c][i]);
+                    *o++ = ',';
+                }
+                *o++ = c < 2 ? '\t' : '\n';
+            }
+        }
+        free(pidx);
+        J->buf[k] = buf;
+        J->len[k] = (size_t)(o - buf);
+    }
+    return NULL;
+}
+
+static int c4_main(int argc, char **argv) {
+    const char *out = argv[2];
+    uint64_t seed = 7;
+    int64_t nblocks = 50000000, tsize = 60000000, qsize = 50000000;
+    int nt = 24, nq = 21;
+    double alpha = 1.2, collinear = 0.8;
+    for (int i = 3; i < argc; ++i) {
+        const char *a = argv[i];
+        if (!strncmp(a, "-seed=", 6)) seed = strtoull(a + 6, NULL, 10);
+        else if (!strncmp(a, "-blocks=", 8)) nblocks = atoll(a + 8);
+        else if (!strncmp(a, "-nt=", 4)) nt = atoi(a + 4);
+        else if (!strncmp(a, "-nq=", 4)) nq = atoi(a + 4);
+        else if (!strncmp(a, "-tsize=", 7)) tsize = atoll(a + 7);
+        else if (!strncmp(a, "-qsize=", 7)) qsize = atoll(a + 7);
+        else if (!strncmp(a, "-threads=", 9)) g_threads = atoi(a + 9);
+        else die("unknown option %s", a);
+    }
+    if (g_threads < 1)
+        g_threads = 1;
+    if (nt < 1 || nq < 1 || tsize < 1000 || qsize < 1000 || tsize >= (1ll << 31) ||
+        qsize >= (1ll << 31))
+        die("%s", "bad C4 shape");
+    mkdir(out, 0777);
+    g_seed = seed;
+    {
+        const int k = (int)lround(0.12 * 256), a = (int)lround(k * 2.0 / 3), b = (int)lround(k * 5.0 / 6);
+        for (int i = 0; i < 256; ++i)
+            g_xor[i] = i < a ? 1 : i < b ? 2 : i < k ? 3 : 0;
+    }
+    genome_t T, Q;
+    memset(&T, 0, sizeof(T));
+    memset(&Q, 0, sizeof(Q));
+    T.n = nt;
+    Q.n = nq;
+    T.names = malloc(nt * sizeof(char *));
+    T.size = malloc(nt * 8);
+    Q.names = malloc(nq * sizeof(char *));
+    Q.size = malloc(nq * 8);
+    char nm[64];
+    for (int i = 0; i < nt; ++i) {
+        snprintf(nm, sizeof(nm), "chr%d", i + 1);
+        T.names[i] = strdup(nm);
+        T.size[i] = tsize;
+    }
+    for (int i = 0; i < nq; ++i) {
+        snprintf(nm, sizeof(nm), "chrQ%d", i + 1);
+        Q.names[i] = strdup(nm);
+        Q.size[i] = qsize;
+    }
+    make_genome(&T, seed, 0);
+    make_genome(&Q, seed + 1, 1);
+    C4T = &T;
+    C4Q = &Q;
+
+    /* pairs (target, query, strand) and their block counts */
+    const int np = nt * nq * 2;
+    c4pair *P = calloc(np, sizeof(c4pair));
+    double *w = malloc(np * sizeof(double)), wsum = 0;
+    int *perm = malloc(np * sizeof(int));
+    rng_t r;
+    rng_seed(&r, seed, P_C4PAIRS, 0);
+    for (int i = 0; i < np; ++i)
+        perm[i] = i;
+    for (int i = np - 1; i > 0; --i) {
+        const int j = (int)uniform_int(&r, 0, i + 1), t = perm[i];
+        perm[i] = perm[j];
+        perm[j] = t;
+    }
+    for (int i = 0; i < np; ++i) {
+        w[i] = 1.0 / pow((double)(perm[i] + 1), alpha);
+        wsum += w[i];
+    }
+    int64_t total = 0;
+    for (int i = 0, k = 0; i < nt; ++i)
+        for (int j = 0; j < nq; ++j)
+            for (int s = 0; s < 2; ++s, ++k) {
+                P[k].ti = i;
+                P[k].qi = j;
+                P[k].strand = s;
+                P[k].nb = (int64_t)(w[k] / wsum * (double)nblocks);
+                if (P[k].nb < 50)
+                    P[k].nb = 50;
+                P[k].ncol = (int64_t)((double)P[k].nb * collinear);
+                total += P[k].nb;
+            }
+    c4job J = {P, np, tsize, qsize, 0, NULL, NULL};
+    atomic_init(&J.next, 0);
+    run_threads(c4_pair_thread, &J);
+    /* mutation pass: pairs grouped by query sequence, pair order inside */
+    int *qoff = calloc(nq + 1, sizeof(int)), *qp = malloc(np * sizeof(int));
+    for (int k = 0; k < np; ++k)
+        qoff[P[k].qi + 1]++;
+    for (int j = 0; j < nq; ++j)
+        qoff[j + 1] += qoff[j];
+    {
+        int *fill = malloc((nq + 1) * sizeof(int));
+        memcpy(fill, qoff, (nq + 1) * sizeof(int));
+        for (int k = 0; k < np; ++k)
+            qp[fill[P[k].qi]++] = k;
+        free(fill);
+    }
+    J.qorder_pairs = qp;
+    J.qoff = qoff;
+    atomic_store(&J.next, 0);
+    run_threads(c4_mut_thread, &J);
+
+    int64_t nrec = 0, nb = 0, largest = 0;
+    for (int k = 0; k < np; ++k) {
+        P[k].rec0 = nrec;
+        nrec += P[k].nrec;
+        nb += P[k].n;
+        if (P[k].n > largest)
+            largest = P[k].n;
+    }
+    int64_t *order = malloc((size_t)(nrec + 1) * 8);
+    for (int64_t i = 0; i < nrec; ++i)
+        order[i] = i;
+    rng_seed(&r, seed, P_C4ORDER, 0);
+    for (int64_t i = nrec - 1; i > 0; --i) {
+        const int64_t j = uniform_int(&r, 0, i + 1), t = order[i];
+        order[i] = order[j];
+        order[j] = t;
+    }
+    char *p;
+    write_2bit(&T, p = path_in(out, "t.2bit"));
+    write_2bit(&Q, p = path_in(out, "q.2bit"));
+    write_sizes(&T, p = path_in(out, "t.sizes"));
+    write_sizes(&Q, p = path_in(out, "q.sizes"));
+    c4fmt F;
+    memset(&F, 0, sizeof(F));
+    F.P = P;
+    F.np = np;
+    F.perm = order;
+    F.nrec = nrec;
+    F.per = 65536;
+    F.nchunks = (nrec + F.per - 1) / F.per;
+    F.tsize = tsize;
+    F.qsize = qsize;
+    F.buf = calloc(F.nchunks + 1, sizeof(char *));
+    F.len = calloc(F.nchunks + 1, sizeof(size_t));
+    atomic_init(&F.next, 0);
+    run_threads(c4_fmt_thread, &F);
+    char *tp = path_in(out, "in.psl.tmp");
+    FILE *f = fopen(tp, "wb");
+    if (!f)
+        die("can't write %s", tp);
+    for (int64_t k = 0; k < F.nchunks; ++k) {
+        fwrite_all(f, F.buf[k], F.len[k], tp);
+        free(F.buf[k]);
+    }
+    if (fclose(f) != 0)
+        die("write error on %s", tp);
+    if (rename(tp, p = path_in(out, "in.psl")) != 0)
+        die("can't rename %s", tp);
+    f = fopen(p = path_in(out, "info.json.tmp"), "w");
+    fprintf(f,
+            "{\"generator\": \"gac_synth c4\", \"seed\": %llu, \"t_seqs\": %d, \"q_seqs\": %d, "
+            "\"tsize\": %lld, \"qsize\": %lld, \"pairs\": %d, \"blocks\": %lld, \"records\": %lld, "
+            "\"largest_pair_blocks\": %lld}\n",
+            (unsigned long long)seed, nt, nq, (long long)tsize, (long long)qsize, np, (long long)nb,
+            (long long)nrec, (long long)largest);
+    fclose(f);
+    if (rename(p, path_in(out, "info.json")) != 0)
+        die("%s", "can't write info.json");
+    (void)total;
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc >= 3 && strcmp(argv[1], "c4") == 0)
+        return c4_main(argc, argv);
     if (argc < 3 || strcmp(argv[1], "c5") != 0) {
         fprintf(stderr, "usage: gac_synth c5 OUTDIR [-seed=S] [-chains=N] [-scale=X] "
-                        "[-minSize=M] [-sizesDir=D] [-threads=T]\n");
+                        "[-minSize=M] [-sizesDir=D] [-threads=T]\n"
+                        "       gac_synth c4 OUTDIR [-seed=S] [-blocks=N] [-nt=24] [-nq=21] "
+                        "[-tsize=60000000] [-qsize=50000000] [-threads=T]\n");
         return 1;
     }
     const char *out = argv[2];

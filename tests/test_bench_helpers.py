@@ -38,3 +38,43 @@ def test_split_by_target(tmp_path):
     for t in ("chr7", "chr21"):
         with open(out[t]) as f:
             assert f.read() == "".join(want[t])
+
+
+def _bench(args, env=None, timeout=300):
+    import json
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, capture_output=True,
+                       text=True, timeout=timeout, env=dict(os.environ, **(env or {})))
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, (json.loads(lines[-1]) if lines else None)
+
+
+def test_bench_self_launch_two_ranks():
+    """`python bench.py --gpus 2` outside torchrun starts the two ranks itself
+    (one torch.distributed.run child) and the line's n_gpus is the process
+    group's size; here the ranks are the gloo rehearsal (GAC_BENCH_ONE_GPU)."""
+    env = {"GAC_BENCH_ONE_GPU": "1"}
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    r, out = _bench(["--gpus", "2", "--launch-check"], env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert out["n_gpus"] == 2
+    g = out["process_group"]
+    assert g["world_size"] == 2 and g["backend"] == "gloo"
+    assert sorted(x["rank"] for x in g["ranks"]) == [0, 1]
+    assert len({x["pid"] for x in g["ranks"]}) == 2
+
+
+def test_bench_world_mismatch_fails():
+    """A torchrun world that is not --gpus is an error, not a 1-GPU number."""
+    r, out = _bench(["--gpus", "3", "--launch-check"], {"WORLD_SIZE": "2", "RANK": "0"})
+    assert r.returncode != 0 and out is None
+    assert "--gpus 3" in r.stderr
+
+
+def test_launch_cmd():
+    import bench
+    cmd = bench.launch_cmd(8, ["--gpus", "8", "--steps", "3"], 29500)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "3"]
