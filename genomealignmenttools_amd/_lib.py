@@ -141,6 +141,7 @@ _PROTOS = {
     "gac_chains_upload": (C.c_int, [C.c_void_p, C.POINTER(ChainsetDesc), C.POINTER(C.c_void_p)]),
     "gac_chains_reupload": (C.c_int, [C.c_void_p, C.POINTER(ChainsetDesc), C.c_void_p]),
     "gac_chains_free": (None, [C.c_void_p]),
+    "gac_chains_context": (C.c_void_p, [C.c_void_p]),
     "gac_score_ranges_host": (C.c_int, [C.c_void_p, C.POINTER(ChainsetDesc), C.c_void_p, C.c_int64,
                                         C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
     "gac_chains_block_count": (C.c_int64, [C.c_void_p]),

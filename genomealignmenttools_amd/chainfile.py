@@ -260,7 +260,8 @@ def write_chains_fast(ca: ChainArrays, path: str, chunk: int = 400_000) -> None:
             ti, qi = tid[c0:c1], qid[c0:c1]
             hlen = (6 + sneg + _ndig(sv) + 1 + tlen[ti] + 1 + nd["tsize"] + 3 + nd["tstart"] + 1
                     + nd["tend"] + 1 + qlen[qi] + 1 + nd["qsize"] + 3 + nd["qstart"] + 1
-                    + nd["qend"] + 1 + nd["id"] + 1)
+                    + nd["qend"] + 1 + nd["id"] + 1
+                    + sum((v < 0).astype(np.int64) for v in ints.values()))  # '-' signs
             b0, b1 = int(ca.blk_off[c0]), int(ca.blk_off[c1])
             nb = np.diff(ca.blk_off[c0:c1 + 1])
             if (nb < 1).any():

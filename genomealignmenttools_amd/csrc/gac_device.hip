@@ -202,6 +202,10 @@ struct gac_ctx {
     std::vector<hipEvent_t> prof_free;
     double prof_ms[GAC_K_COUNT] = {0};
     int64_t prof_n[GAC_K_COUNT] = {0};
+    // chain sets still open on this context: gac_close releases their
+    // device memory and orphans them (ctx = NULL), so a set freed after its
+    // context (a kent-shim cache, a garbage-collected binding) is only deleted
+    std::vector<gac_chainset *> sets;
 };
 
 struct gac_chainset {
@@ -336,10 +340,20 @@ static void free_genome(Genome &g) {
     g = Genome();
 }
 
+static void free_set_memory(gac_chainset *cs);
+
 extern "C" void gac_close(gac_ctx *c) {
     if (!c) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
+    {
+        CTX_LOCK(c);
+        for (gac_chainset *cs : c->sets) {
+            free_set_memory(cs);
+            cs->ctx = nullptr;
+        }
+        c->sets.clear();
+    }
     free_genome(c->g[0]);
     free_genome(c->g[1]);
     void *bufs[] = {c->d_small,  c->d_gap_tab, c->rdesc,    c->nblk,     c->goff, c->pb0, c->agg, c->plan_off, c->gflat,
@@ -1494,6 +1508,7 @@ extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_cha
     *out = nullptr;
     gac_chainset *cs = new gac_chainset();
     cs->ctx = c;
+    c->sets.push_back(cs);
     const int rc = chains_fill(c, d, cs);
     if (rc != GAC_OK) {
         gac_chains_free(cs);
@@ -1513,20 +1528,32 @@ extern "C" int gac_chains_reupload(gac_ctx *c, const gac_chainset_desc *d, gac_c
     return chains_fill(c, d, cs);
 }
 
+static void free_set_memory(gac_chainset *cs) {
+    hipSetDevice(cs->ctx->device);  // (hipFree waits for work still using them)
+    void *bufs[] = {cs->chains, cs->blk, cs->blk12, cs->tspan, cs->bucket, cs->d_stage, cs->d_nlist};
+    for (void *p : bufs)
+        if (p) hipFree(p);
+    cs->chains = nullptr;
+    cs->blk = nullptr;
+    cs->blk12 = nullptr;
+    cs->tspan = nullptr;
+    cs->bucket = nullptr;
+    cs->d_stage = nullptr;
+    cs->d_nlist = nullptr;
+    free_whole_plan(cs);
+}
+
 extern "C" void gac_chains_free(gac_chainset *cs) {
     if (!cs) return;
-    CTX_LOCK(cs->ctx);
-    hipSetDevice(cs->ctx->device);  // (hipFree waits for work still using them)
-    if (cs->chains) hipFree(cs->chains);
-    if (cs->blk) hipFree(cs->blk);
-    if (cs->blk12) hipFree(cs->blk12);
-    if (cs->tspan) hipFree(cs->tspan);
-    if (cs->bucket) hipFree(cs->bucket);
-    if (cs->d_stage) hipFree(cs->d_stage);
-    if (cs->d_nlist) hipFree(cs->d_nlist);
-    free_whole_plan(cs);
+    if (gac_ctx *c = cs->ctx) {  // (NULL: its context was closed, the memory went with it)
+        CTX_LOCK(c);
+        free_set_memory(cs);
+        c->sets.erase(std::remove(c->sets.begin(), c->sets.end(), cs), c->sets.end());
+    }
     delete cs;
 }
+
+extern "C" gac_ctx *gac_chains_context(const gac_chainset *cs) { return cs ? cs->ctx : nullptr; }
 
 extern "C" int64_t gac_chains_block_count(const gac_chainset *cs) { return cs ? cs->n_blocks : -1; }
 
@@ -1971,6 +1998,11 @@ extern "C" int gac_score_ranges_host(gac_ctx *c, const gac_chainset_desc *d, con
     if (!c->scoring) return gac_fail(GAC_E_STATE, "gac_set_scoring() not called");
     if (!c->g[0].final || !c->g[1].final)
         return gac_fail(GAC_E_STATE, "load both genomes before scoring");
+    if (d->n_chains < 0 || d->n_blocks < 0 || !d->blk_off || !d->t_seq || !d->q_seq ||
+        !d->q_strand || (d->n_blocks && (!d->blk_t || !d->blk_q || !d->blk_size)))
+        return gac_fail(GAC_E_ARG, "gac_score_ranges_host: incomplete chain set descriptor");
+    if (d->blk_off[0] != 0 || d->blk_off[d->n_chains] != d->n_blocks)
+        return gac_fail(GAC_E_ARG, "gac_score_ranges_host: blk_off must run from 0 to n_blocks");
     HIPCHK(hipSetDevice(c->device));
     if (!c->h_hq) {
         HIPCHK(hipHostMalloc((void **)&c->h_hq, kSmallMax * sizeof(RangeDesc), hipHostMallocMapped));
@@ -2003,6 +2035,10 @@ extern "C" int gac_score_ranges_host(gac_ctx *c, const gac_chainset_desc *d, con
                 return gac_fail(GAC_E_ARG, "range %lld: chain %d out of range",
                                 (long long)(i0 + k), q.chain);
             const int64_t b0 = d->blk_off[q.chain], b1 = d->blk_off[q.chain + 1];
+            if (b0 < 0 || b0 > b1 || b1 > d->n_blocks)
+                return gac_fail(GAC_E_ARG, "range %lld: chain %d has blocks [%lld, %lld) outside "
+                                "[0, %lld)", (long long)(i0 + k), q.chain, (long long)b0,
+                                (long long)b1, (long long)d->n_blocks);
             int64_t a0 = b0, a1 = b1;  // first block ending past s
             while (a0 < a1) {
                 const int64_t mid = (a0 + a1) >> 1;

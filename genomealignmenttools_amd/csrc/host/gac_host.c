@@ -769,22 +769,69 @@ void gac_run_threads(int n, void *(*fn)(void *), void *arg) {
 }
 
 /* ------------------------------------------------------------ output */
+/* outputs opened by gac_open_output and not yet closed: an abort cuts each
+ * to the bytes this run wrote (gac_outputs_cut), so no file is left holding
+ * new text followed by an earlier run's tail */
+#define GAC_MAX_OUTPUTS 32
+static pthread_mutex_t g_out_mu = PTHREAD_MUTEX_INITIALIZER;
+static int g_out_fd[GAC_MAX_OUTPUTS];
+static int g_out_n;
+
+static void out_register(int fd, int add) {
+    pthread_mutex_lock(&g_out_mu);
+    if (add) {
+        if (g_out_n < GAC_MAX_OUTPUTS)
+            g_out_fd[g_out_n++] = fd;
+    } else {
+        for (int i = 0; i < g_out_n; ++i)
+            if (g_out_fd[i] == fd) {
+                g_out_fd[i] = g_out_fd[--g_out_n];
+                break;
+            }
+    }
+    pthread_mutex_unlock(&g_out_mu);
+}
+
+/* cut a regular file to `end` bytes when it is longer */
+static int cut_to(int fd, off_t end) {
+    struct stat st;
+    if (end >= 0 && fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && st.st_size > end)
+        return ftruncate(fd, end);
+    return 0;
+}
+
+void gac_outputs_cut(void) {
+    /* (no lock: the abort path may run while another thread holds it; the
+     * table is only read, and a stale fd at worst fails the fstat) */
+    for (int i = 0; i < g_out_n; ++i)
+        (void)cut_to(g_out_fd[i], lseek(g_out_fd[i], 0, SEEK_CUR));
+}
+
 FILE *gac_open_output(const char *path) {
     const int fd = open(path, O_WRONLY | O_CREAT | O_CLOEXEC, 0666);
     if (fd < 0)
         return NULL;
     FILE *f = fdopen(fd, "w");
-    if (!f)
+    if (!f) {
         close(fd);
+        return NULL;
+    }
+    out_register(fd, 1);
     return f;
 }
 
+/* The file is opened without O_TRUNC (re-truncating a file the tool created
+ * at start makes ext4 flush it on close): it is cut to the bytes written
+ * here instead -- on a failed flush to the bytes that reached the file, so a
+ * failed write leaves a short file (as the reference's), never an earlier
+ * run's tail after the new text. */
 int gac_close_output(FILE *f) {
+    const int fd = fileno(f);
     int bad = fflush(f) != 0;
-    const off_t end = ftello(f);
-    struct stat st;
-    if (!bad && end >= 0 && fstat(fileno(f), &st) == 0 && S_ISREG(st.st_mode) && st.st_size > end)
-        bad = ftruncate(fileno(f), end) != 0;
+    const off_t end = bad ? lseek(fd, 0, SEEK_CUR) : ftello(f);
+    if (cut_to(fd, end) != 0)
+        bad = 1;
+    out_register(fd, 0);
     return (fclose(f) != 0 || bad) ? EOF : 0;
 }
 

@@ -100,6 +100,9 @@ int gac_par_output(FILE *out, int64_t nr, void (*fn)(FILE *f, int64_t r, void *a
  * net). */
 FILE *gac_open_output(const char *path);
 int gac_close_output(FILE *f); /* 0 or EOF, as fclose */
+/* Abort path: cut every output still open (gac_open_output) to the bytes
+ * written so far (the tools' gt_abort calls it before exiting). */
+void gac_outputs_cut(void);
 /* A growable text buffer (formatting without stdio): the *_buf variants hand
  * each run an empty one and take its bytes as the run's text (no copy). */
 typedef struct gac_obuf {

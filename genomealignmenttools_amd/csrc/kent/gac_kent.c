@@ -16,7 +16,16 @@ struct gapCalc {
 
 static __thread gac_ctx *t_ctx;
 
-void gac_kent_bind(gac_ctx *ctx) { t_ctx = ctx; }
+void gac_kent_forget_chains(void);
+
+/* a resident chain set (the chainCalcScore cache) belongs to the context it
+ * was scored on: rebinding drops it (gac_chains_free is safe even when that
+ * context was closed in between: the set is then only deleted) */
+void gac_kent_bind(gac_ctx *ctx) {
+    if (ctx != t_ctx)
+        gac_kent_forget_chains();
+    t_ctx = ctx;
+}
 
 static void die(const char *fmt, ...) { /* errAbort */
     va_list ap;
@@ -501,7 +510,8 @@ static void cache_fill(struct chain *const *chains, int64_t n, struct axtScoreSc
 /* the cached score of c, or NAN when c is not (or no longer) cached */
 static double cache_score(struct chain *c, struct axtScoreScheme *ss, struct gapCalc *gapCalc) {
     const kent_cache *k = &t_cache;
-    if (!k->cs || k->ss != ss || k->gap != gapCalc)
+    /* (a set orphaned by gac_close, or of another context, never answers) */
+    if (!k->cs || k->ss != ss || k->gap != gapCalc || !t_ctx || gac_chains_context(k->cs) != t_ctx)
         return NAN;
     const int64_t i = cache_find(k, c);
     if (i < 0 || k->fp[i] != fingerprint(c))

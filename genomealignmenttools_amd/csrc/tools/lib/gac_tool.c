@@ -49,6 +49,7 @@ void gt_abort(const char *fmt, ...) {
     g_abort_hook = NULL; /* (a failing hook must not recurse) */
     if (hook)
         hook();
+    gac_outputs_cut(); /* (no net left holding an earlier run's tail) */
     join_live_device(); /* never exit under a thread that is inside the HIP runtime */
     fflush(stdout);
     va_start(ap, fmt);

@@ -194,6 +194,7 @@ class Engine:
         d, arrs = self._desc(t_seq, q_seq, q_strand, blk_off, blk_t, blk_q, blk_size)
         check(lib().gac_chains_reupload(self.h, C.byref(d), cs.handle))
         cs.n_chains, cs.n_blocks = d.n_chains, d.n_blocks
+        cs.aligned_bases = int(arrs[6].sum(dtype=np.int64))
         return cs
 
     def score_ranges_host(self, t_seq, q_seq, q_strand, blk_off, blk_t, blk_q, blk_size,

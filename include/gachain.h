@@ -106,6 +106,9 @@ const char *gac_last_error(void);
 /* Open a context on HIP device `device`.  Fails (GAC_E_HIP) if there is no
  * usable gfx950 device: the library never falls back to the CPU. */
 int gac_open(int device, gac_ctx **out);
+/* Closing a context releases the device memory of every chain set still
+ * open on it; such a set is left orphaned (gac_chains_context() is NULL, every
+ * call on it fails with GAC_E_ARG) and gac_chains_free() only deletes it. */
 void gac_close(gac_ctx *ctx);
 /* Name of the device architecture the context runs on (e.g. "gfx950"). */
 const char *gac_device_arch(gac_ctx *ctx);
@@ -157,6 +160,8 @@ int gac_chains_upload(gac_ctx *ctx, const gac_chainset_desc *d, gac_chainset **o
  * free per call). Waits for calls still using the set. */
 int gac_chains_reupload(gac_ctx *ctx, const gac_chainset_desc *d, gac_chainset *cs);
 void gac_chains_free(gac_chainset *cs);
+/* The context a set belongs to; NULL once that context was closed. */
+gac_ctx *gac_chains_context(const gac_chainset *cs);
 /* gac_score_ranges for chains held in host memory (no upload): each range is
  * planned on the host (its window of blocks found by binary search) and the
  * windows are scored by one kernel launch per 256 ranges reading them from

@@ -142,7 +142,8 @@ void gac_kent_chain_free(struct chain **pChain);
  * chainCalcScore over a list pays one upload, not one per call. */
 void gac_kent_score_chains(struct chain *const *chains, int64_t n, struct axtScoreScheme *ss,
                            struct gapCalc *gapCalc, double *global);
-/* drop the resident chain set (e.g. before freeing the chains) */
+/* drop the resident chain set (e.g. before freeing the chains).  Binding
+ * another context drops it too; it stays safe after gac_close of its context. */
 void gac_kent_forget_chains(void);
 
 double chainScoreBlock(char *q, char *t, int size, int matrix[256][256]);

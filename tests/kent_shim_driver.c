@@ -4,7 +4,10 @@
  * "chain_index start end" line of the ranges file prints
  *   chainCalcScore(chainSubsetOnT(chain, start, end))   (0 if empty)
  * exactly as src/chainNet/chainNet.c:230-248 / subchainInfo compose them.
- * usage: kent_shim_driver in.chain t.2bit q.2bit ranges.txt gap [batch]
+ * usage: kent_shim_driver in.chain t.2bit q.2bit ranges.txt gap [batch|rebind]
+ * ("rebind": after the scores, close the context while its chainCalcScore
+ * cache is resident, open and bind a second one, score the same sub-chains
+ * again and print "rebind mismatches=K")
  *        kent_shim_driver in.chain t.2bit q.2bit kentapi gap max_chains
  * The second form runs oracle/kentapi_workload.inc (the rest of the kent
  * chain API: chainScoreBlock, axtScoreUngapped, chainConnectCost,
@@ -155,7 +158,9 @@ int main(int argc, char **argv) {
         ++cnt;
     }
     fclose(rf);
-    if (argc > 6) { /* one batched call for every non-empty subset */
+    const int rebind = argc > 6 && !strcmp(argv[6], "rebind");
+    double *first = malloc(sizeof(double) * (cnt + 1));
+    if (argc > 6 && !rebind) { /* one batched call for every non-empty subset */
         struct chain **list = malloc(sizeof(*list) * cnt);
         double *g = malloc(sizeof(double) * cnt);
         int k = 0;
@@ -168,7 +173,21 @@ int main(int argc, char **argv) {
             printf("%.0f\n", sub[i] ? g[k++] : 0.0);
     } else {
         for (int i = 0; i < cnt; ++i)
-            printf("%.0f\n", sub[i] ? chainCalcScore(sub[i], ss, gc, NULL, NULL) : 0.0);
+            printf("%.0f\n", first[i] = sub[i] ? chainCalcScore(sub[i], ss, gc, NULL, NULL) : 0.0);
+    }
+    if (rebind) { /* bind A, score, close A, bind B, score (the cache must not answer) */
+        gac_close(ctx);
+        if (gac_open(0, &ctx) != GAC_OK || gac_genome_load_2bit(ctx, GAC_T, argv[2]) != GAC_OK ||
+            gac_genome_load_2bit(ctx, GAC_Q, argv[3]) != GAC_OK) {
+            fprintf(stderr, "%s\n", gac_last_error());
+            return 1;
+        }
+        gac_kent_bind(ctx);
+        int bad = 0;
+        for (int i = 0; i < cnt; ++i)
+            bad += (sub[i] ? chainCalcScore(sub[i], ss, gc, NULL, NULL) : 0.0) != first[i];
+        printf("rebind mismatches=%d\n", bad);
+        gac_kent_forget_chains();
     }
     for (int i = 0; i < cnt; ++i)
         gac_kent_chain_free(&fr[i]);

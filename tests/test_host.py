@@ -638,3 +638,21 @@ def test_mapped_output_path(tool, tmp_path):
             assert r.returncode == 0, r.stderr
             outs[tag] = open(tmp_path / f"{tag}.chain", "rb").read()
         assert outs["mapped"] == outs["plain"] and len(outs["plain"]) > 0
+
+
+def test_write_chains_fast_negative_fields(tmp_path):
+    """write_chains_fast sizes '-' signs of header integers (a negative id is
+    legal input): the same bytes as write_chains."""
+    from genomealignmenttools_amd import chainfile
+    from genomealignmenttools_amd.chainfile import ChainArrays
+    ca = ChainArrays(score=np.array([5.0, -3.0]), tname=["chr1", "chr2"],
+                     tsize=np.array([1000, 900], np.int32), tstart=np.array([10, 20], np.int32),
+                     tend=np.array([60, 70], np.int32), qname=["q1", "q2"],
+                     qsize=np.array([800, 700], np.int32), qstrand=np.array([0, 1], np.uint8),
+                     qstart=np.array([5, 6], np.int32), qend=np.array([55, 56], np.int32),
+                     id=np.array([-7, 3], np.int64), blk_off=np.array([0, 2, 3], np.int64),
+                     blk_t=np.array([10, 40, 20], np.int32), blk_q=np.array([5, 35, 6], np.int32),
+                     blk_size=np.array([20, 20, 50], np.int32))
+    chainfile.write_chains(ca, str(tmp_path / "a"))
+    chainfile.write_chains_fast(ca, str(tmp_path / "b"))
+    assert (tmp_path / "a").read_bytes() == (tmp_path / "b").read_bytes()
