@@ -73,6 +73,7 @@ TOOL = os.path.join(PKG, "bin", "chainNet")
 SYNTH = os.path.join(PKG, "libexec", "gac_synth")
 REF_TOOL = os.path.join(REPO, "oracle", "_ref", "chainNet")
 SC_TOOL = os.path.join(PKG, "bin", "scoreChain")
+AXT_TOOL = os.path.join(PKG, "bin", "axtChain")
 REF_SC_TOOL = os.path.join(REPO, "oracle", "_ref", "scoreChain")
 SAMPLE_TARGETS = ("chr21", "chr22")
 # all-cores baseline: the reference split by target chromosome, one process
@@ -96,6 +97,9 @@ def parse():
     p.add_argument("--c2-steps", type=int, default=10)
     p.add_argument("--kernel-steps", type=int, default=20)
     p.add_argument("--no-c2", action="store_true")
+    p.add_argument("--no-c4", action="store_true", help="skip the axtChain C4 leg")
+    p.add_argument("--c4-blocks", type=int, default=50_000_000)
+    p.add_argument("--c4-steps", type=int, default=1)
     p.add_argument("--no-kernel", action="store_true", help="skip the kernel/roofline legs")
     p.add_argument("--no-scorechain", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -764,12 +768,13 @@ def scorechain_e2e_leg(d, info, steps, ref_sample):
         run_tool(cmd, [])
         dt += time.perf_counter() - t0
     dt /= steps
+    parity = full_parity("c5", {"in_chain_sha256": p("in.chain"), "scorechain.chain_sha256": out})
     os.remove(out)
     r = run_tool(cmd + ["-verbose=2"], [], env=dict(os.environ, GAC_TIMING="1"))
     res = {"workload": "scoreChain end to end (bin/scoreChain), C5 whole genome: every chain's "
                        "score rescored and the chain file rewritten",
            "value": info["input_aligned_bases"] / dt / 1e9, "unit": "Gbases/s",
-           "ms_per_step": dt * 1e3, "steps": steps,
+           "ms_per_step": dt * 1e3, "steps": steps, "parity_full": parity,
            "tool_stages": [x.strip() for x in r.stderr.splitlines()
                            if x.startswith(("[stage]", "[gac_chains_upload]", "[gt_read_chains]"))]}
     os.remove(out)
@@ -792,6 +797,113 @@ def scorechain_e2e_leg(d, info, steps, ref_sample):
                                           "baseline's sample chains"}
         log(f"scoreChain: ours {dt * 1e3:.0f} ms on C5; reference {t1:.2f}s on the sample "
             f"({bases / 1e6:.0f} M bases), identical: {res['cpu_reference']['identical_output']}")
+    return res
+
+
+# ---------------------------------------------------------------- full-scale parity
+GOLDEN_FULL = os.path.join(REPO, "tests", "golden", "fullscale")
+
+
+def sha256_files(paths):
+    """sha256 of several files at once (one thread each; hashlib drops the
+    GIL on large buffers): {path: hexdigest}."""
+    import hashlib
+    from concurrent.futures import ThreadPoolExecutor
+
+    def one(path):
+        h = hashlib.sha256()
+        with open(path, "rb") as f:
+            for b in iter(lambda: f.read(1 << 24), b""):
+                h.update(b)
+        return h.hexdigest()
+    with ThreadPoolExecutor(len(paths)) as ex:
+        return dict(zip(paths, ex.map(one, paths)))
+
+
+def full_parity(which, files):
+    """The outputs of a full-size run against the reference's sha256
+    (tests/golden/fullscale/<which>.json, made by the reference on the same
+    seeded input by tests/golden/make_fullscale_golden.py).  files: {golden
+    key ("a.b" = nested): path}.  Returns {"identical": all equal, per key
+    {"ours", "reference", "same"}} -- checked outside every timed region."""
+    with open(os.path.join(GOLDEN_FULL, f"{which}.json")) as f:
+        gold = json.load(f)
+    t0 = time.time()
+    got = sha256_files(list(files.values()))
+    res, same = {}, True
+    for key, path in files.items():
+        ref = gold
+        for k in key.split("."):
+            ref = ref[k]
+        ok = got[path] == ref
+        same = same and ok
+        res[key] = {"ours": got[path], "reference": ref, "same": ok}
+    res["identical"] = same
+    res["golden"] = f"tests/golden/fullscale/{which}.json ({gold['generator']}; reference run on "
+    res["golden"] += f"{gold['reference_host']})"
+    res["hash_seconds"] = round(time.time() - t0, 2)
+    return res
+
+
+def c4_files(args):
+    """C4: gac_synth c4, 50 M PSL blocks over 24 x 21 pairs x 2
+    strands, seed 7; written once per box under --tmp (~20 s)."""
+    d = os.path.join(args.tmp, f"gac_bench_c4_{args.c4_blocks}_7")
+    if not os.path.exists(os.path.join(d, "info.json")):
+        t0 = time.time()
+        subprocess.run([SYNTH, "c4", d, "-seed=7", f"-blocks={args.c4_blocks}",
+                        f"-threads={min(host_threads(), 32)}"], check=True)
+        log(f"C4: written in {time.time() - t0:.1f}s")
+    with open(os.path.join(d, "info.json")) as f:
+        return d, json.load(f)
+
+
+def c4_leg(args, dist, world, rank, local, barrier, step_env):
+    """configs[3]: axtChain -psl on C4 (50 M PSL blocks), 1 GPU, and at N > 1
+    chain-sharded: every rank runs axtChain -nranks=N -rank=r -gpu=LOCAL_RANK
+    (seqPairs dealt by block count, rank 0 merges and writes).  One warmup +
+    `steps` timed runs between barriers, max over ranks; the output's sha256
+    against the reference's (tests/golden/fullscale/c4.json)."""
+    d, info = c4_files(args) if rank == 0 else (None, None)
+    barrier()
+    if rank != 0:
+        d, info = c4_files(args)
+    p = lambda x: os.path.join(d, x)
+    out = p(f"ours.r{world}.chain")
+    cmd = [AXT_TOOL, "-linearGap=loose", "-verbose=0", "-psl", p("in.psl"), p("t.2bit"), p("q.2bit"),
+           out]
+    if world > 1:
+        cmd += [f"-nranks={world}", f"-rank={rank}", f"-gpu={local}"]
+    dt = 0.0
+    for k in range(1 + args.c4_steps):
+        if rank == 0 and os.path.exists(out):
+            os.remove(out)
+        barrier()
+        t0 = time.perf_counter()
+        run_tool(cmd, [], env=step_env())
+        barrier()
+        if k:
+            dt += time.perf_counter() - t0
+    if dist is not None:
+        from genomealignmenttools_amd.shard import reduce_time_and_work
+        dt, _ = reduce_time_and_work(dist, dt, 0.0, device="cpu" if os.environ.get(
+            "GAC_BENCH_ONE_GPU") else f"cuda:{local}")
+    if rank != 0:
+        return None
+    dt /= max(args.c4_steps, 1)
+    with open(os.path.join(GOLDEN_FULL, "c4.json")) as f:
+        gold = json.load(f)
+    res = {"workload": "configs[3]: axtChain -psl end to end (bin/axtChain) on C4, "
+                       + ("1 GPU" if world == 1 else f"{world} GPUs, seqPairs sharded (-nranks)"),
+           "blocks": info["blocks"], "pairs": info["pairs"],
+           "largest_pair_blocks": info["largest_pair_blocks"], "value": info["blocks"] / dt / 1e6,
+           "unit": "M PSL blocks chained/s", "ms_per_step": dt * 1e3, "steps": args.c4_steps,
+           "reference": {"seconds": gold["axtchain"]["reference_seconds"],
+                         "host": gold["reference_host"], "kind": "reference (oracle/_ref/axtChain)"}}
+    if args.c4_blocks == gold["info"]["blocks"] or args.c4_blocks == 50_000_000:
+        res["parity_full"] = full_parity("c4", {"in_psl_sha256": p("in.psl"),
+                                                "axtchain.chain_sha256": out})
+    os.remove(out)
     return res
 
 
@@ -933,6 +1045,12 @@ def main():
         dev = "cpu" if one_gpu else f"cuda:{local}"
         dt, _ = reduce_time_and_work(dist, dt, 0.0, device=dev)
     step_s = dt / args.steps
+    parity = None
+    if rank == 0:  # (outside the timed region)
+        parity = full_parity("c5", {"in_chain_sha256": os.path.join(d, "in.chain"),
+                                    "chainnet_rescore.t_net_sha256": outs[0],
+                                    "chainnet_rescore.q_net_sha256": outs[1]})
+        log(f"C5 nets identical to the reference's (sha256): {parity['identical']}")
     out = {
         "metric": METRIC,
         "value": info["netted_aligned_bases"] / step_s / 1e9,
@@ -949,6 +1067,9 @@ def main():
         # the group as torch.distributed (RCCL) saw it: n_gpus above is its size
         "process_group": group or {"backend": None, "world_size": 1,
                                    "ranks": [{"rank": 0, "local_rank": 0, "device": "cuda:0"}]},
+        # both nets of the last timed step vs the reference's on the whole C5
+        "parity_full": parity,
+        "identical_nets_full": parity["identical"] if parity else None,
     }
     if one_gpu:
         out["rehearsal"] = "GAC_BENCH_ONE_GPU: every rank on device 0 over gloo (not a GPU curve)"
@@ -957,6 +1078,13 @@ def main():
             out["c2"] = c2_leg(args, args.c2_steps, 1)
         except Exception as ex:  # reported, never fatal
             out["c2"] = {"error": str(ex)[:300]}
+    if not args.no_c4:
+        try:
+            c4 = c4_leg(args, dist, world, rank, local, barrier, step_env)
+        except Exception as ex:  # reported, never fatal
+            c4 = {"error": str(ex)[:300]}
+        if rank == 0:
+            out["c4"] = c4
     expect = None
     if rank == 0 and not args.no_kernel:
         if world > 1 and not os.path.exists(os.path.join(d, "fills.bin")):
@@ -991,6 +1119,21 @@ def main():
         except Exception as ex:  # reported, never fatal
             out["cpu_baseline"] = {"error": str(ex)[:300]}
         out["cpu_baseline"].update(host_cpu())
+        try:  # how the sample's rate relates to the whole genome's (same host, golden run)
+            with open(os.path.join(GOLDEN_FULL, "c5.json")) as f:
+                g = json.load(f)
+            whole = g["info"]["netted_aligned_bases"] / g["chainnet_rescore"]["reference_seconds"]
+            samp = g["reference_sample_chr21_chr22"]
+            srate = samp["netted_aligned_bases"] / samp["seconds"]
+            out["cpu_baseline"]["whole_c5_reference"] = {
+                "seconds": g["chainnet_rescore"]["reference_seconds"], "host": g["reference_host"],
+                "value": whole / 1e9, "sample_value_same_host": srate / 1e9,
+                "whole_over_sample_rate": whole / srate,
+                "note": "the reference chainNet -rescore on the whole C5 input (its nets are the "
+                        "full-scale parity golden); the sample rate above overstates the "
+                        "reference's whole-genome rate by 1/whole_over_sample_rate"}
+        except (OSError, KeyError, ValueError) as ex:
+            out["cpu_baseline"]["whole_c5_reference"] = {"error": str(ex)[:200]}
         try:
             out["cpu_baseline"]["all_cores"] = cpu_baseline_all_cores(
                 d, min(16, host_threads(), len(ALL_CORES_TARGETS)))

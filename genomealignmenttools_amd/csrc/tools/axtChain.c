@@ -24,6 +24,7 @@
 #include <string.h>
 #include <stdatomic.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "gac_tool.h"
 #include "gachain.h"
@@ -51,7 +52,10 @@ static void usage(int min_score) {
         "              Or specify a piecewise linearGap tab delimited file.\n"
         "   (this build reads .2bit genomes, or fasta with -faQ/-faT; not nib directories)\n"
         "batch (this build): axtChain -jobs=FILE runs every line of FILE as one axtChain\n"
-        "   command line (arguments only) in one process and one GPU context\n",
+        "   command line (arguments only) in one process and one GPU context\n"
+        "multi-GPU (this build): -nranks=N -rank=R [-gpu=D], one process per GPU on one node\n"
+        "   (GAC_RANK_TOKEN shared by the ranks): seqPairs dealt out by block count, rank 0\n"
+        "   merges every rank's chains and writes the file\n",
         min_score);
 }
 
@@ -630,6 +634,108 @@ static void batch_genomes(ax_batch *B, const char *tnib, const char *qnib, int f
     B->qfa = fa_q;
 }
 
+/* ------------------------------------------------------------ -nranks
+ * seqPairs are independent up to the final sort (axtChain.c:379-470:
+ * chainPair per pair, then one slSort(chainCmpScore) of the whole list), so
+ * rank R chains the pairs the LPT deal gives it -- largest block count first,
+ * each to the least loaded rank -- in spList order, and rank 0 merges.  The
+ * reference's list is built by slAddHead pair after pair, so its stable sort
+ * orders equal scores by pair index descending, then by the pair's own order;
+ * every rank's gac_axt_chain output is already sorted that way on its subset
+ * of pairs, so a merge by (score descending, global pair descending) that
+ * takes equal keys from one rank in that rank's order (one pair lives on one
+ * rank) is the reference's order, and ids 1..n follow it (chain.c:203-204). */
+typedef struct ax_part {
+    int64_t n, nb;
+    double *score;
+    int32_t *pair, *ts, *te, *qs, *qe;
+    int64_t *off;
+    int32_t *bt, *bq, *bs;
+} ax_part;
+
+static void lpt_deal(const int64_t *boff, int64_t np, int nranks, int32_t *owner) {
+    int64_t *ix = malloc((size_t)(np ? np : 1) * 8), *load = calloc((size_t)nranks, 8);
+    for (int64_t i = 0; i < np; ++i)
+        ix[i] = i;
+    /* by block count descending, then pair index (insertion into runs of a
+     * merge sort would do; pairs number in the thousands) */
+    for (int64_t w = 1; w < np; w *= 2) {
+        int64_t *tmp = malloc((size_t)np * 8);
+        for (int64_t lo = 0; lo < np; lo += 2 * w) {
+            int64_t a = lo, am = lo + w < np ? lo + w : np, b = am, bm = lo + 2 * w < np ? lo + 2 * w : np,
+                    k = lo;
+            while (a < am && b < bm) {
+                const int64_t na = boff[ix[a] + 1] - boff[ix[a]], nb = boff[ix[b] + 1] - boff[ix[b]];
+                tmp[k++] = (nb > na) ? ix[b++] : ix[a++];
+            }
+            while (a < am)
+                tmp[k++] = ix[a++];
+            while (b < bm)
+                tmp[k++] = ix[b++];
+        }
+        memcpy(ix, tmp, (size_t)np * 8);
+        free(tmp);
+    }
+    for (int64_t k = 0; k < np; ++k) {
+        int best = 0;
+        for (int r = 1; r < nranks; ++r)
+            if (load[r] < load[best])
+                best = r;
+        owner[ix[k]] = best;
+        load[best] += boff[ix[k] + 1] - boff[ix[k]];
+    }
+    free(ix);
+    free(load);
+}
+
+static void part_write(const char *path, const gac_axt_chains *ch, const int32_t *gpair) {
+    FILE *f = fopen(path, "wb");
+    if (!f)
+        gt_abort("Can't open %s to write: %s", path, strerror(errno));
+    const int64_t n = ch->n_chains, nb = ch->n_blocks;
+    int ok = fwrite("GACAXP01", 1, 8, f) == 8 && fwrite(&n, 8, 1, f) == 1 && fwrite(&nb, 8, 1, f) == 1;
+    int32_t *gp = malloc((size_t)(n ? n : 1) * 4);
+    for (int64_t c = 0; c < n; ++c)
+        gp[c] = gpair[ch->pair[c]];
+    ok = ok && fwrite(ch->score, 8, (size_t)n, f) == (size_t)n && fwrite(ch->blk_off, 8, (size_t)n + 1, f) == (size_t)n + 1;
+    const int32_t *cols[5] = {gp, ch->t_start, ch->t_end, ch->q_start, ch->q_end};
+    for (int k = 0; k < 5; ++k)
+        ok = ok && fwrite(cols[k], 4, (size_t)n, f) == (size_t)n;
+    const int32_t *bcols[3] = {ch->blk_t, ch->blk_q, ch->blk_size};
+    for (int k = 0; k < 3; ++k)
+        ok = ok && fwrite(bcols[k], 4, (size_t)nb, f) == (size_t)nb;
+    free(gp);
+    if (fclose(f) != 0 || !ok)
+        gt_abort("write error on %s", path);
+}
+
+static void part_read(const char *path, ax_part *P) {
+    FILE *f = fopen(path, "rb");
+    if (!f)
+        gt_abort("Can't open %s to read: %s", path, strerror(errno));
+    char mg[8];
+    if (fread(mg, 1, 8, f) != 8 || memcmp(mg, "GACAXP01", 8) != 0 || fread(&P->n, 8, 1, f) != 1 ||
+        fread(&P->nb, 8, 1, f) != 1 || P->n < 0 || P->nb < 0)
+        gt_abort("%s: not an axtChain rank part", path);
+    const size_t n = (size_t)P->n, nb = (size_t)P->nb;
+    P->score = malloc((n ? n : 1) * 8);
+    P->off = malloc((n + 1) * 8);
+    int32_t **cols[5] = {&P->pair, &P->ts, &P->te, &P->qs, &P->qe};
+    int ok = fread(P->score, 8, n, f) == n && fread(P->off, 8, n + 1, f) == n + 1;
+    for (int k = 0; k < 5; ++k) {
+        *cols[k] = malloc((n ? n : 1) * 4);
+        ok = ok && fread(*cols[k], 4, n, f) == n;
+    }
+    int32_t **bcols[3] = {&P->bt, &P->bq, &P->bs};
+    for (int k = 0; k < 3; ++k) {
+        *bcols[k] = malloc((nb ? nb : 1) * 4);
+        ok = ok && fread(*bcols[k], 4, nb, f) == nb;
+    }
+    fclose(f);
+    if (!ok || P->off[0] != 0 || P->off[n] != P->nb)
+        gt_abort("%s: truncated axtChain rank part", path);
+}
+
 static void run_job(int argc, char *argv[], ax_batch *B) {
     gt_options_hash(&argc, argv);
     int min_score = gt_opt_int("minScore", 1000);
@@ -650,7 +756,24 @@ static void run_job(int argc, char *argv[], ax_batch *B) {
     gt_check(gac_gapcalc_build(gap_name, &gap));
     const int fa_q = gt_opt_exists("faQ"), fa_t = gt_opt_exists("faT");
 
-    FILE *f = gt_must_open(out_path, "w");
+    gt_ranks rk;
+    memset(&rk, 0, sizeof(rk));
+    rk.n = 1;
+    if (gt_opt_int("nranks", 1) > 1) {
+        if (B->on)
+            gt_abort("-nranks does not go with -jobs\n");
+        if (details)
+            gt_abort("-details is not supported with -nranks\n");
+        if (!strcmp(out_path, "stdout"))
+            gt_abort("-nranks needs an output file name (not stdout)");
+        gt_ranks_init(&rk, gt_opt_int("nranks", 1), gt_opt_int("rank", 0), out_path);
+    }
+    const int multi = rk.n > 1;
+    /* ranks > 0 write a binary part; the text (headers, '#' lines, chains)
+     * is rank 0's */
+    FILE *f = multi && rk.me > 0 ? fopen("/dev/null", "w") : gt_must_open(out_path, "w");
+    if (!f)
+        gt_abort("Can't open /dev/null");
     /* axtScoreSchemeDnaWrite (axt.c:836-872): matrix in ACGT x ACGT order */
     fprintf(f, "##matrix=axtChain 16");
     for (int i = 0; i < 16; ++i)
@@ -741,30 +864,110 @@ static void run_job(int argc, char *argv[], ax_batch *B) {
         strand[i] = p->strand == '-' ? 1 : 0;
         boff[i + 1] = boff[i] + p->nb;
     }
-    const int64_t nb = boff[np];
+    /* this rank's pairs (all of them without -nranks), in spList order */
+    int32_t *mine = malloc((size_t)(np ? np : 1) * 4);
+    int64_t nm = 0;
+    if (multi) {
+        int32_t *owner = malloc((size_t)(np ? np : 1) * 4);
+        lpt_deal(boff, np, rk.n, owner);
+        for (int64_t i = 0; i < np; ++i)
+            if (owner[i] == rk.me)
+                mine[nm++] = (int32_t)i;
+        free(owner);
+    } else {
+        for (int64_t i = 0; i < np; ++i)
+            mine[nm++] = (int32_t)i;
+    }
+    int32_t *mt = malloc((size_t)(nm ? nm : 1) * 4), *mq = malloc((size_t)(nm ? nm : 1) * 4);
+    uint8_t *ms = malloc((size_t)(nm ? nm : 1));
+    int64_t *moff = malloc((size_t)(nm + 1) * 8);
+    moff[0] = 0;
+    for (int64_t k = 0; k < nm; ++k) {
+        mt[k] = tseq[mine[k]];
+        mq[k] = qseq[mine[k]];
+        ms[k] = strand[mine[k]];
+        moff[k + 1] = moff[k] + ord[mine[k]]->nb;
+    }
+    const int64_t nb = moff[nm];
     int32_t *bt = malloc((size_t)(nb ? nb : 1) * 4), *bq = malloc((size_t)(nb ? nb : 1) * 4),
             *bs = malloc((size_t)(nb ? nb : 1) * 4);
-    for (int64_t i = 0; i < np; ++i) {
-        const pair *p = ord[i];
-        memcpy(bt + boff[i], p->bt, (size_t)p->nb * 4);
-        memcpy(bq + boff[i], p->bq, (size_t)p->nb * 4);
-        memcpy(bs + boff[i], p->bs, (size_t)p->nb * 4);
+    for (int64_t k = 0; k < nm; ++k) {
+        const pair *p = ord[mine[k]];
+        memcpy(bt + moff[k], p->bt, (size_t)p->nb * 4);
+        memcpy(bq + moff[k], p->bq, (size_t)p->nb * 4);
+        memcpy(bs + moff[k], p->bs, (size_t)p->nb * 4);
     }
     gt_verbose(2, "device + genomes in %.3f s\n", wall() - t0);
     t0 = wall();
-    gac_axt_input ai = {np, tseq, qseq, strand, boff, bt, bq, bs};
+    gac_axt_input ai = {nm, mt, mq, ms, moff, bt, bq, bs};
     gac_axt_chains *ch = NULL;
     gt_check(gac_axt_chain(ctx, mat, gap, &ai, (double)min_score, 0, details, &ch));
-    for (int64_t c = 0; c < ch->n_chains; ++c) {
-        const int32_t p = ch->pair[c];
-        const int64_t b0 = ch->blk_off[c];
-        gt_write_chain_raw(f, ch->score[c], ord[p]->tname, gac_genome_seq_size(ctx, GAC_T, tseq[p]),
-                           ch->t_start[c], ch->t_end[c], ord[p]->qname,
-                           gac_genome_seq_size(ctx, GAC_Q, qseq[p]), strand[p], ch->q_start[c],
-                           ch->q_end[c], (int32_t)(c + 1), ch->blk_t + b0, ch->blk_q + b0,
-                           ch->blk_size + b0, ch->blk_off[c + 1] - b0);
+    if (multi && rk.me > 0) { /* this rank's chains, sorted, to rank 0 */
+        char part[4096], tmp[4096];
+        gt_part_name(part, sizeof(part), out_path, rk.me, "");
+        gt_part_name(tmp, sizeof(tmp), out_path, rk.me, ".tmp");
+        part_write(tmp, ch, mine);
+        if (rename(tmp, part) != 0)
+            gt_abort("can't rename %s", tmp);
+        fclose(f);
+        gt_verbose(2, "rank %d: %lld pairs, %lld blocks, %lld chains in %.3f s\n", rk.me,
+                   (long long)nm, (long long)nb, (long long)ch->n_chains, wall() - t0);
+        gac_close(ctx);
+        gt_ranks_done(&rk);
+        gt_exit_ok();
     }
+    /* rank 0 (or the only rank): its own chains as part 0, the others' read
+     * back, merged into chainWrite order */
+    ax_part *parts = calloc((size_t)rk.n, sizeof(ax_part));
+    {
+        ax_part *P0 = &parts[0];
+        P0->n = ch->n_chains;
+        P0->nb = ch->n_blocks;
+        P0->score = ch->score;
+        P0->pair = malloc((size_t)(P0->n ? P0->n : 1) * 4);
+        for (int64_t c = 0; c < P0->n; ++c)
+            P0->pair[c] = mine[ch->pair[c]];
+        P0->ts = ch->t_start, P0->te = ch->t_end, P0->qs = ch->q_start, P0->qe = ch->q_end;
+        P0->off = ch->blk_off;
+        P0->bt = ch->blk_t, P0->bq = ch->blk_q, P0->bs = ch->blk_size;
+    }
+    if (multi) {
+        gt_ranks_wait(&rk, out_path);
+        for (int r = 1; r < rk.n; ++r) {
+            char part[4096];
+            gt_part_name(part, sizeof(part), out_path, r, "");
+            part_read(part, &parts[r]);
+            unlink(part);
+        }
+    }
+    int64_t *head = calloc((size_t)rk.n, 8);
+    for (int32_t id = 1;; ++id) {
+        int best = -1;
+        for (int r = 0; r < rk.n; ++r) {
+            if (head[r] >= parts[r].n)
+                continue;
+            if (best < 0) {
+                best = r;
+                continue;
+            }
+            const double a = parts[r].score[head[r]], b = parts[best].score[head[best]];
+            if (a > b || (a == b && parts[r].pair[head[r]] > parts[best].pair[head[best]]))
+                best = r;
+        }
+        if (best < 0)
+            break;
+        const ax_part *P = &parts[best];
+        const int64_t c = head[best]++;
+        const int32_t p = P->pair[c];
+        const int64_t b0 = P->off[c];
+        gt_write_chain_raw(f, P->score[c], ord[p]->tname, gac_genome_seq_size(ctx, GAC_T, tseq[p]),
+                           P->ts[c], P->te[c], ord[p]->qname, gac_genome_seq_size(ctx, GAC_Q, qseq[p]),
+                           strand[p], P->qs[c], P->qe[c], id, P->bt + b0, P->bq + b0, P->bs + b0,
+                           P->off[c + 1] - b0);
+    }
+    free(head);
     gt_careful_close(f, out_path);
+    gt_ranks_done(&rk);
     gt_verbose(2, "chaining + writing in %.3f s\n", wall() - t0);
     gt_verbose(2, "%lld pairs, %lld blocks, %lld chains\n", (long long)np, (long long)nb,
                (long long)ch->n_chains);
@@ -788,6 +991,13 @@ static void run_job(int argc, char *argv[], ax_batch *B) {
     free(qseq);
     free(strand);
     free(boff);
+    free(mine);
+    free(mt);
+    free(mq);
+    free(ms);
+    free(moff);
+    free(parts[0].pair);
+    free(parts);
     free(bt);
     free(bq);
     free(bs);
@@ -802,7 +1012,19 @@ int main(int argc, char *argv[]) {
             jobs = argv[i] + 6;
     ax_batch B;
     memset(&B, 0, sizeof(B));
-    gt_one_device(); /* device 0 only (before any thread or HIP call) */
+    /* the device: -gpu=D, else the rank with -nranks, else 0 -- exposed alone
+     * to the runtime before any thread or HIP call */
+    int gpu = -1, rank = 0, nranks = 1;
+    for (int i = 1; i < argc; ++i) {
+        if (!strncmp(argv[i], "-gpu=", 5))
+            gpu = atoi(argv[i] + 5);
+        else if (!strncmp(argv[i], "-rank=", 6))
+            rank = atoi(argv[i] + 6);
+        else if (!strncmp(argv[i], "-nranks=", 8))
+            nranks = atoi(argv[i] + 8);
+    }
+    gt_set_gpu(gpu >= 0 ? gpu : (nranks > 1 ? rank : 0));
+    gt_one_device();
     if (!jobs) {
         run_job(argc, argv, &B); /* exits */
         return 0;

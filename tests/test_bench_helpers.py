@@ -78,3 +78,26 @@ def test_launch_cmd():
     assert cmd[1:3] == ["-m", "torch.distributed.run"]
     assert "--nproc-per-node=8" in cmd and "--master-addr=127.0.0.1" in cmd
     assert cmd[-4:] == ["--gpus", "8", "--steps", "3"]
+
+
+def test_full_parity_helper(tmp_path):
+    """bench.full_parity hashes the files against tests/golden/fullscale/*.json
+    (both goldens hold the keys bench and the GPU tests read)."""
+    import hashlib
+    import json
+    import bench
+    for which, keys in (("c5", ["in_chain_sha256", "chainnet_rescore.t_net_sha256",
+                                "chainnet_rescore.q_net_sha256", "scorechain.chain_sha256"]),
+                        ("c4", ["in_psl_sha256", "axtchain.chain_sha256"])):
+        files = {}
+        for k in keys:
+            f = tmp_path / f"{which}.{k}"
+            f.write_bytes(k.encode() * 1000)
+            files[k] = str(f)
+        res = bench.full_parity(which, files)
+        assert res["identical"] is False
+        for k in keys:
+            assert res[k]["ours"] == hashlib.sha256(k.encode() * 1000).hexdigest()
+            assert len(res[k]["reference"]) == 64 and res[k]["same"] is False
+        g = json.load(open(os.path.join(REPO, "tests", "golden", "fullscale", f"{which}.json")))
+        assert g["info"]["seed"] in (7, 1234)

@@ -402,3 +402,70 @@ def test_chainnet_rescore_failures_exit_cleanly(tmp_path):
         _run([_bin("chainNet")] + args + ["/dev/full", tmp_path / "q.net", "-rescore",
                                           f"-tNibDir={p('t.2bit')}", f"-qNibDir={p('q.2bit')}",
                                           "-linearGap=loose"], rc=255, timeout=300)
+
+
+# ---------------------------------------------------------------- full scale
+def _golden_full(which):
+    with open(os.path.join(GOLDEN, "fullscale", f"{which}.json")) as f:
+        return json.load(f)
+
+
+def _sha(*paths):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    got = bench.sha256_files(list(paths))
+    return [got[p] for p in paths]
+
+
+@pytest.mark.timeout(900)
+def test_c5_fullscale_vs_reference_sha(tmp_path):
+    """C5 at the bench's full size (5 M chains, 116 M blocks, all 455 x 66
+    sequences): bin/chainNet -rescore nets and bin/scoreChain's chains have
+    the sha256 of the reference's outputs on the same input
+    (tests/golden/fullscale/c5.json; the reference takes ~45 min for the
+    nets, so its outputs are pinned by hash)."""
+    from genomealignmenttools_amd._lib import PKG_DIR
+    g = _golden_full("c5")
+    d = str(tmp_path)
+    p = lambda x: os.path.join(d, x)
+    _run([os.path.join(PKG_DIR, "libexec", "gac_synth"), "c5", d, "-seed=1234", "-chains=5000000",
+          f"-sizesDir={os.path.join(PKG_DIR, 'data')}", "-threads=16"])
+    _run([_bin("chainNet"), p("in.chain"), p("t.sizes"), p("q.sizes"), p("o.t.net"), p("o.q.net"),
+          "-rescore", f"-tNibDir={p('t.2bit')}", f"-qNibDir={p('q.2bit')}", "-linearGap=loose"])
+    _run([_bin("scoreChain"), p("in.chain"), p("t.2bit"), p("q.2bit"), p("o.sc.chain"),
+          "-linearGap=loose"])
+    i, t, q, sc = _sha(p("in.chain"), p("o.t.net"), p("o.q.net"), p("o.sc.chain"))
+    assert i == g["in_chain_sha256"], "generated input differs from the golden run's"
+    assert t == g["chainnet_rescore"]["t_net_sha256"]
+    assert q == g["chainnet_rescore"]["q_net_sha256"]
+    assert sc == g["scorechain"]["chain_sha256"]
+
+
+@pytest.mark.timeout(900)
+def test_c4_fullscale_axtchain_vs_reference_sha(tmp_path):
+    """C4 at the SURVEY size (gac_synth c4: 50 M PSL blocks over 24 x 21 pairs
+    x 2 strands, largest pair 11.5 M blocks): bin/axtChain, one process and
+    -nranks=3 (seqPairs dealt out, rank 0 merges; all ranks on device 0
+    here), has the sha256 of the reference axtChain's output
+    (tests/golden/fullscale/c4.json: ~21 min for the reference)."""
+    from genomealignmenttools_amd._lib import PKG_DIR
+    g = _golden_full("c4")
+    d = str(tmp_path)
+    _run([os.path.join(PKG_DIR, "libexec", "gac_synth"), "c4", d, "-seed=7", "-blocks=50000000",
+          "-threads=16"])
+    args = ["-linearGap=loose", "-verbose=0", "-psl", "in.psl", "t.2bit", "q.2bit"]
+    _run([_bin("axtChain")] + args + ["one.chain"], cwd=d)
+    procs = [subprocess.Popen([_bin("axtChain")] + args + ["r3.chain", "-nranks=3", f"-rank={r}",
+                                                           "-gpu=0"], cwd=d,
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                              env=dict(os.environ, GAC_RANK_TOKEN="c4r3", GAC_THREADS="6"))
+             for r in range(3)]
+    for r, pr in enumerate(procs):
+        _, err = pr.communicate(timeout=600)
+        assert pr.returncode == 0, (r, err[-2000:])
+    i, one, r3 = _sha(os.path.join(d, "in.psl"), os.path.join(d, "one.chain"),
+                      os.path.join(d, "r3.chain"))
+    assert i == g["in_psl_sha256"], "generated input differs from the golden run's"
+    assert one == g["axtchain"]["chain_sha256"]
+    assert r3 == g["axtchain"]["chain_sha256"]

@@ -251,6 +251,29 @@ def test_axtchain_synth(seed, case, tmp_path):
             assert filecmp.cmp(tmp_path / fn, os.path.join(d, fn), shallow=False)
 
 
+@pytest.mark.parametrize("seed", [5, 6])
+@pytest.mark.parametrize("case", ["loose", "medium0", "axt"])
+def test_axtchain_synth_ranks(seed, case, tmp_path):
+    """axtChain -nranks=2/3 (one process per rank, all on device 0 here):
+    seqPairs dealt out by block count, rank 0 merges by (score, pair) --
+    byte-identical to the reference's single run (the golden files)."""
+    d = os.path.join(GOLDEN, "axtchain", f"s{seed}")
+    with open(os.path.join(GOLDEN, "axtchain", "cases.json")) as f:
+        opts = json.load(f)[case]
+    inp = "in.psl" if "-psl" in opts else "in.axt.gz"
+    args = opts + [os.path.join(d, inp), os.path.join(d, "t.2bit"), os.path.join(d, "q.2bit"),
+                   "out.chain"]
+    for n in (2, 3):
+        env = dict(os.environ, GAC_RANK_TOKEN=f"s{seed}{case}{n}")
+        procs = [subprocess.Popen([_bin("axtChain")] + args + [f"-nranks={n}", f"-rank={r}", "-gpu=0"],
+                                  cwd=tmp_path, env=env, stdout=subprocess.PIPE,
+                                  stderr=subprocess.PIPE, text=True) for r in range(n)]
+        for r, pr in enumerate(procs):
+            _, err = pr.communicate(timeout=300)
+            assert pr.returncode == 0, (r, err[-2000:])
+        assert filecmp.cmp(tmp_path / "out.chain", os.path.join(d, f"{case}.chain"), shallow=False)
+
+
 @pytest.mark.parametrize("dp", ["host", "gpu"])
 def test_axtchain_jobs_batch(dp, tmp_path):
     """axtChain -jobs=FILE: the two reference KATs and
