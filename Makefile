@@ -86,8 +86,13 @@ $(BINDIR)/%: $(EXECDIR)/%
 
 oracle: oracle/_build/libgacoracle.so
 
-# bench/test infrastructure: the whole-genome synthetic set generator (C5)
-synth: $(EXECDIR)/gac_synth
+# bench/test infrastructure: the whole-genome synthetic set generator (C5,
+# C4) and the random-line gather ceiling probe bench.py reports k_tile against
+synth: $(EXECDIR)/gac_synth $(EXECDIR)/gac_gather_ceiling
+
+$(EXECDIR)/gac_gather_ceiling: scripts/probes/gather_ceiling.hip
+	@mkdir -p $(EXECDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Wno-unused-result -Wno-unused-value $< -o $@
 
 $(EXECDIR)/gac_synth: $(CSRC)/synth/gac_synth.c
 	@mkdir -p $(EXECDIR)

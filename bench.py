@@ -430,6 +430,42 @@ def roofline(algo, t_ms, pmc, kernel):
     return roof
 
 
+GATHER = os.path.join(PKG, "libexec", "gac_gather_ceiling")
+
+
+def gather_ceiling():
+    """The random-128-B-line gather ceiling of this GPU
+    (scripts/probes/gather_ceiling.hip): the best line rate over isolated
+    16-B loads to random lines of a 2 GiB buffer (k_tile's access shape),
+    several loads in flight and occupancies.  None when unavailable."""
+    if not os.path.exists(GATHER):
+        return None
+    try:
+        r = subprocess.run(["timeout", "-k", "10", "120", GATHER, "2048"], capture_output=True,
+                           text=True, timeout=150)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        return json.loads(line[-1]) if r.returncode == 0 and line else None
+    except (OSError, ValueError, subprocess.SubprocessError):
+        return None
+
+
+def add_ceiling(roof, ceil):
+    """frac_of_gather_ceiling: k_tile's measured HBM bytes per second (the
+    in-run PMC traffic over its average launch) against the random-line
+    gather ceiling measured on the same GPU in the same run."""
+    if not roof or not ceil or not ceil.get("ceiling_isolated_GBps"):
+        return
+    c = ceil["ceiling_isolated_GBps"]
+    roof["gather_ceiling"] = {"GBps": c, "shape": ceil.get("ceiling_shape"),
+                              "source": "genomealignmenttools_amd/libexec/gac_gather_ceiling "
+                                        "(scripts/probes/gather_ceiling.hip), this run"}
+    if roof.get("traffic"):
+        ms = roof.get("traffic_kernel_avg_ms") or roof["kernel_avg_ms"]
+        rate = roof["traffic"] / (ms / 1e3) / 1e9
+        roof["traffic_GBps"] = rate
+        roof["frac_of_gather_ceiling"] = rate / c
+
+
 def fills_leg(legs, d, ch, steps, pmc):
     ranges = fills_ranges(d)
     res = legs.run(ranges, False, steps)
@@ -1113,6 +1149,11 @@ def main():
                                                            load_chains_bin(d), rdist, 0, 1,
                                                            args.kernel_steps, expect)
         rdist.destroy_process_group()
+    if rank == 0 and world == 1 and not args.no_kernel:
+        ceil = gather_ceiling()
+        out["gather_ceiling"] = ceil
+        add_ceiling(out.get("roofline"), ceil)
+        add_ceiling((out.get("scorechain") or {}).get("roofline"), ceil)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline_c5(d, out_base)

@@ -45,6 +45,14 @@ typedef struct ax_env {
      * function cost the largest C4 pair 10 %) */
     int32_t last_pos[3];
     double last_val[3], last_slope[3];
+    /* the exact fast DP (pair_dp_fast): gapCalcCost monotone in each
+     * distance (so a subtree's corner bounds every non-overlapping
+     * candidate), its linear minorant s*(dq+dt), s = lin_k/1024, and the
+     * smallest matrix entry (a lower bound on a crossover's adjustment per
+     * overlapping base) */
+    int fast;
+    int64_t lin_k;
+    int32_t min_entry;
 } ax_env;
 
 /* chainConnectGapCost = gapCalcCost (chainConnect.c:108-112) */
@@ -139,6 +147,13 @@ typedef struct ax_work {
     int32_t nl;
     ax_node *nodes;
     int32_t nn;
+    int32_t *lnode;  /* [block] the leaf's node */
+    int64_t *nw;     /* [node] pair_dp_fast's linear bound: max of 1024 total + k (qEnd + tEnd) */
+    int32_t *qpos;   /* [block] the leaf's place in qord */
+    int32_t *tpos;   /* [block] the leaf's place in tord */
+    int32_t cut_t;   /* fast searches see only leaves with tpos < cut_t */
+    long long fallbacks;
+    int team, team_batch; /* > 1: this pair's DP on that many threads (pair_dp_team) */
     /* crossover scratch */
     uint8_t *xs;
     int32_t xcap;
@@ -261,6 +276,7 @@ static int32_t kd_build(ax_work *w, int32_t *Q, int32_t *T, int32_t n, int dim) 
         const int32_t l = Q[0];
         /* leaf node: lo/hi carry the leaf's qStart/tStart */
         w->nodes[id] = (ax_node){w->qs[l], w->ts[l], l, 0, 0.0, w->qe[l], w->te[l]};
+        w->lnode[l] = id;
         return id;
     }
     const int32_t half = n / 2;
@@ -290,6 +306,17 @@ static int32_t kd_build(ax_work *w, int32_t *Q, int32_t *T, int32_t n, int dim) 
 
 enum { kStack = 512 };
 
+#ifdef GAC_DP_STATS /* profiling build only (make cpu-axtchain CPU_EXTRA=-DGAC_DP_STATS) */
+static __thread struct {
+    long long visits, prune1, prune2, leaves, cands, overlaps, xover_bases, updates, best_wins;
+} g_st;
+#define ST(x) (g_st.x++)
+#define STN(x, n) (g_st.x += (n))
+#else
+#define ST(x) ((void)0)
+#define STN(x, n) ((void)0)
+#endif
+
 /* bestPredecessor (chainBlock.c:207-263), iterative with the same order:
  * the hi subtree (only when the lonely leaf lies past the cut) before lo */
 static void best_predecessor(ax_work *w, int32_t lonely, double *ret_score, int32_t *ret_pred) {
@@ -307,18 +334,33 @@ static void best_predecessor(ax_work *w, int32_t lonely, double *ret_score, int3
         const int32_t b = st_node[sp];
         const int dim = st_dim[sp];
         const ax_node *nd = &w->nodes[b];
+        ST(visits);
         double max_score = nd->max_score + lscore;
-        if (max_score < best)
+        if (max_score < best) {
+            ST(prune1);
             continue;
+        }
         max_score -= w->cb_gap ? w->cb_gap(lq - nd->max_q, lt - nd->max_t, w->cb_user)
                                : gap_cost(w->e, lq - nd->max_q, lt - nd->max_t);
-        if (max_score < best)
+        if (max_score < best) {
+            ST(prune2);
             continue;
+        }
         if (nd->leaf >= 0) {
             const int32_t l = nd->leaf;
+            ST(leaves);
             if (nd->lo < lq && nd->hi < lt) {
+                ST(cands);
+#ifdef GAC_DP_STATS
+                if (w->qs[lonely] < w->qe[l] || w->ts[lonely] < w->te[l]) {
+                    ST(overlaps);
+                    const int dq = w->qs[lonely] - w->qe[l], dt = w->ts[lonely] - w->te[l];
+                    STN(xover_bases, -(dq < dt ? dq : dt));
+                }
+#endif
                 const double s = w->total[l] + lscore - connect_cost(w, l, lonely);
                 if (s > best) {
+                    ST(best_wins);
                     best = s;
                     best_node = b;
                 }
@@ -355,6 +397,7 @@ static void update_scores(ax_work *w, int32_t leaf) {
         const int32_t b = st_node[sp];
         const int dim = st_dim[sp];
         ax_node *nd = &w->nodes[b];
+        ST(updates);
         if (nd->max_score < total)
             nd->max_score = total;
         if (nd->leaf < 0) {
@@ -373,6 +416,139 @@ static void update_scores(ax_work *w, int32_t leaf) {
             }
         }
     }
+}
+
+/* ------------------------------------------------------------------ the exact fast DP
+ * bestPredecessor returns the first leaf, in its DFS order, of the best
+ * score among the candidates it does not prune, and it prunes a subtree when
+ * the subtree's bound (max total + the lonely leaf's score - gapCost to the
+ * subtree's top corner) is below the best so far.  For a non-overlapping
+ * candidate that bound is a true upper bound (gapCalcCost is monotone in
+ * each distance: checked per gap setup, ax_env.fast); for an overlapping one
+ * it is not when the crossover's adjustment is negative (chainConnect.c:
+ * 61-105).  Call a candidate anomalous if its score exceeds
+ * the bound at its own leaf node (every ancestor's bound is at least that).
+ * If every anomalous candidate scores below the best non-anomalous score M,
+ * the reference's search returns the first non-anomalous leaf scoring M:
+ * nothing on that leaf's path can be pruned (its bounds are >= M >= best),
+ * and nothing before it scores M.  The same holds for any search in the same
+ * DFS order that prunes by tighter TRUE bounds.  pair_dp_fast therefore
+ *   1. searches with a second bound per subtree, the linear minorant of the
+ *      gap cost: max over its leaves of total + s (qEnd + tEnd), minus
+ *      s (qStart + tStart) of the lonely leaf -- far high-scoring leaves no
+ *      longer keep whole subtrees open;
+ *   2. then looks at every overlapping candidate (blocks of earlier leaves
+ *      that reach past the lonely leaf's start in q or t, found by scanning
+ *      back over the t- and q-ordered leaves by the pair's longest block):
+ *      one that could score at least the best found (and > 0) and violates
+ *      either bound at its leaf node sends this leaf to the reference search
+ *      (best_predecessor), so the result is the reference's in every case. */
+static void best_predecessor_fast(ax_work *w, int32_t lonely, double *ret_score, int32_t *ret_pred) {
+    const int32_t lq = w->qs[lonely], lt = w->ts[lonely];
+    const double lscore = w->score[lonely];
+    const int64_t k = w->e->lin_k, kl = k * ((int64_t)lq + lt) - 1024 * (int64_t)lscore;
+    double best = 0.0;
+    int64_t best1024 = 0;
+    int32_t best_node = -1;
+    int32_t st_node[kStack];
+    uint8_t st_dim[kStack];
+    int sp = 0;
+    st_node[sp] = 0;
+    st_dim[sp++] = 0;
+    while (sp > 0) {
+        --sp;
+        const int32_t b = st_node[sp];
+        const int dim = st_dim[sp];
+        const ax_node *nd = &w->nodes[b];
+        ST(visits);
+        double max_score = nd->max_score + lscore;
+        if (max_score < best) {
+            ST(prune1);
+            continue;
+        }
+        if (w->nw[b] - kl < best1024) {
+            ST(prune1);
+            continue;
+        }
+        max_score -= gap_cost(w->e, lq - nd->max_q, lt - nd->max_t);
+        if (max_score < best) {
+            ST(prune2);
+            continue;
+        }
+        if (nd->leaf >= 0) {
+            const int32_t l = nd->leaf;
+            ST(leaves);
+            if (nd->lo < lq && nd->hi < lt && w->tpos[l] < w->cut_t) {
+                ST(cands);
+                const double s = w->total[l] + lscore - connect_cost(w, l, lonely);
+                if (s > best) {
+                    ST(best_wins);
+                    best = s;
+                    best1024 = 1024 * (int64_t)s;
+                    best_node = b;
+                }
+            }
+            continue;
+        }
+        if (sp + 2 > kStack) {
+            w_fail(w, "kd-tree deeper than %d", kStack / 2);
+            break;
+        }
+        const int32_t coord = dim == 0 ? lq : lt;
+        st_node[sp] = nd->lo;
+        st_dim[sp++] = (uint8_t)(1 - dim);
+        if (coord > nd->cut) {
+            st_node[sp] = nd->hi;
+            st_dim[sp++] = (uint8_t)(1 - dim);
+        }
+    }
+    *ret_score = best;
+    *ret_pred = best_node;
+}
+
+/* 1 when an overlapping candidate of `lonely` (the ti-th leaf in t order)
+ * could score >= best (and > 0) while violating a bound at its leaf node */
+static int dp_anomaly(ax_work *w, int32_t lonely, int32_t ti, double best, int32_t maxsz) {
+    const int32_t lq = w->qs[lonely], lt = w->ts[lonely];
+    const int32_t lsize = w->qe[lonely] - lq;
+    const double lscore = w->score[lonely];
+    const double need = best > 0 ? best : 1.0; /* (scores are integral) */
+    const int64_t k = w->e->lin_k;
+    for (int side = 0; side < 2; ++side) {
+        const int32_t *ord = side ? w->qord : w->tord;
+        const int32_t *st = side ? w->qs : w->ts;
+        const int32_t at = side ? w->qpos[lonely] : ti, lo = (side ? lq : lt) - maxsz;
+        for (int32_t j = at - 1; j >= 0 && st[ord[j]] > lo; --j) {
+            const int32_t c = ord[j];
+            if (w->ts[c] >= lt || w->qs[c] >= lq || w->tpos[c] >= w->cut_t)
+                continue; /* not a candidate (or not yet scored) */
+            int dq = lq - w->qe[c], dt = lt - w->te[c];
+            if (dq >= 0 && dt >= 0)
+                continue; /* no overlap: the bounds hold */
+            if (side == 1 && dt < 0)
+                continue; /* (the t scan saw it) */
+            const int ov = -(dq < dt ? dq : dt);
+            if (ov >= lsize || ov >= w->qe[c] - w->qs[c])
+                continue; /* connect cost 1e8 */
+            /* cheap upper bound first: adj >= ov * min_entry */
+            const double ub = w->total[c] + lscore - (double)gap_cost(w->e, dq + ov, dt + ov) -
+                              (double)ov * w->e->min_entry;
+            if (ub < need)
+                continue;
+            const double sc = w->total[c] + lscore - connect_cost(w, c, lonely);
+            if (sc < need)
+                continue;
+            /* the bounds at c's leaf node are at least those of c alone
+             * (its max is >= c's total, its corner is c's end): compared
+             * with these, the check holds whatever the node held when the
+             * search read it (pair_dp_team reads a tree being updated) */
+            const double bc = w->total[c] + lscore - gap_cost(w->e, dq, dt);
+            const int64_t bl = 1024 * (int64_t)w->total[c] - k * ((int64_t)dq + dt) + 1024 * (int64_t)lscore;
+            if (sc > bc || 1024 * (int64_t)sc > bl)
+                return 1;
+        }
+    }
+    return 0;
 }
 
 /* ---- sorts (glibc qsort is a stable merge sort here; ranks make it explicit) */
@@ -406,6 +582,85 @@ static int dkey_cmp_desc(const void *a, const void *b) {
 }
 
 /* ---- chain post-processing on a block list (linked by next[]) ---- */
+_Static_assert(sizeof(ikey) == 16 && sizeof(dkey) == 16, "par_sort16 keys");
+
+/* a stable parallel merge sort of 16-byte keys (ikey, dkey: their
+ * comparators end on a rank, so the order is total): runs sorted by qsort
+ * on every thread, then merged in rounds */
+typedef struct psort16 {
+    char *a, *tmp;
+    int64_t n;
+    int nrun;
+    int64_t *cut;
+    int64_t width;
+    int (*cmp)(const void *, const void *);
+    _Atomic int next;
+} psort16;
+
+static void *ps16_runs(void *arg) {
+    psort16 *J = arg;
+    for (;;) {
+        const int r = atomic_fetch_add(&J->next, 1);
+        if (r >= J->nrun)
+            return NULL;
+        qsort(J->a + 16 * J->cut[r], (size_t)(J->cut[r + 1] - J->cut[r]), 16, J->cmp);
+    }
+}
+
+static void *ps16_merge(void *arg) {
+    psort16 *J = arg;
+    for (;;) {
+        const int m = atomic_fetch_add(&J->next, 1);
+        const int64_t r0 = (int64_t)m * 2 * J->width;
+        if (r0 >= J->nrun)
+            return NULL;
+        const int64_t r1 = r0 + J->width < J->nrun ? r0 + J->width : J->nrun;
+        const int64_t r2 = r0 + 2 * J->width < J->nrun ? r0 + 2 * J->width : J->nrun;
+        int64_t i = J->cut[r0], j = J->cut[r1], o = J->cut[r0];
+        const int64_t ie = J->cut[r1], je = J->cut[r2];
+        while (i < ie && j < je) {
+            const int right = J->cmp(J->a + 16 * j, J->a + 16 * i) < 0;
+            memcpy(J->tmp + 16 * o++, J->a + 16 * (right ? j++ : i++), 16);
+        }
+        if (i < ie)
+            memcpy(J->tmp + 16 * o, J->a + 16 * i, (size_t)(ie - i) * 16), o += ie - i;
+        if (j < je)
+            memcpy(J->tmp + 16 * o, J->a + 16 * j, (size_t)(je - j) * 16);
+    }
+}
+
+static void par_sort16(void *a, int64_t n, int (*cmp)(const void *, const void *), int nt) {
+    if (nt <= 1 || n < (1 << 16)) {
+        qsort(a, (size_t)n, 16, cmp);
+        return;
+    }
+    psort16 J;
+    J.a = a;
+    J.n = n;
+    J.nrun = nt;
+    J.cmp = cmp;
+    J.cut = malloc((size_t)(nt + 1) * sizeof(int64_t));
+    for (int r = 0; r <= nt; ++r)
+        J.cut[r] = n * r / nt;
+    atomic_init(&J.next, 0);
+    gac_run_threads(nt, ps16_runs, &J);
+    J.tmp = malloc((size_t)n * 16);
+    for (J.width = 1; J.width < nt; J.width *= 2) {
+        atomic_store(&J.next, 0);
+        const int64_t merges = (nt + 2 * J.width - 1) / (2 * J.width);
+        gac_run_threads(merges < nt ? (int)merges : nt, ps16_merge, &J);
+        char *t = J.a;
+        J.a = J.tmp;
+        J.tmp = t;
+    }
+    if (J.a != (char *)a) {
+        memcpy(a, J.a, (size_t)n * 16);
+        J.tmp = J.a;
+    }
+    free(J.tmp);
+    free(J.cut);
+}
+
 typedef struct ax_cb {
     int32_t qs, qe, ts, te;
     int32_t next;
@@ -552,12 +807,13 @@ static int32_t pair_leaves(ax_work *w) {
         free(k);
         return 0;
     }
-    qsort(k, (size_t)nl, sizeof(ikey), ikey_cmp);
+    const int nt = w->team > 1 ? w->team : 1; /* (large pairs: every thread) */
+    par_sort16(k, nl, ikey_cmp, nt);
     for (int32_t i = 0; i < nl; ++i)
         w->tord[i] = k[i].v;
     for (int32_t i = 0; i < nl; ++i)
         k[i] = (ikey){w->qs[w->tord[i]], i, w->tord[i]};
-    qsort(k, (size_t)nl, sizeof(ikey), ikey_cmp);
+    par_sort16(k, nl, ikey_cmp, nt);
     for (int32_t i = 0; i < nl; ++i)
         w->qord[i] = k[i].v;
     free(k);
@@ -568,21 +824,567 @@ static int32_t pair_leaves(ax_work *w) {
     return nl;
 }
 
+/* kd_build of a subtree whose node ids are known in advance: a subtree of
+ * n leaves has 2n - 1 nodes, laid out hi-first in pre-order from `id`, so
+ * disjoint subtrees can be built by different threads (tmp: scratch the
+ * size of Q, the same offset as Q into the pair's list) */
+static void kd_build_at(ax_work *w, int32_t *Q, int32_t *T, int32_t n, int dim, int32_t id,
+                        int32_t *tmp) {
+    if (n == 1) {
+        const int32_t l = Q[0];
+        w->nodes[id] = (ax_node){w->qs[l], w->ts[l], l, 0, 0.0, w->qe[l], w->te[l]};
+        w->lnode[l] = id;
+        return;
+    }
+    const int32_t half = n / 2;
+    for (int32_t i = 0; i < n; ++i)
+        w->hit[Q[i]] = 0;
+    const int32_t *D = dim == 0 ? Q : T;
+    for (int32_t i = 0; i < half; ++i)
+        w->hit[D[i]] = 1;
+    const int32_t ml = D[half - 1];
+    const int32_t cut = dim == 0 ? w->qs[ml] : w->ts[ml];
+    partition(Q, n, w->hit, tmp);
+    partition(T, n, w->hit, tmp);
+    const int32_t hi = id + 1, lo = id + 2 * (n - half);
+    kd_build_at(w, Q + half, T + half, n - half, 1 - dim, hi, tmp + half);
+    kd_build_at(w, Q, T, half, 1 - dim, lo, tmp);
+    ax_node *nd = &w->nodes[id];
+    nd->lo = lo;
+    nd->hi = hi;
+    nd->leaf = -1;
+    nd->cut = cut;
+    nd->max_score = 0.0;
+    nd->max_q = w->nodes[lo].max_q > w->nodes[hi].max_q ? w->nodes[lo].max_q : w->nodes[hi].max_q;
+    nd->max_t = w->nodes[lo].max_t > w->nodes[hi].max_t ? w->nodes[lo].max_t : w->nodes[hi].max_t;
+}
+
+typedef struct kd_task {
+    int32_t *Q, *T, *tmp;
+    int32_t n, id;
+    int dim;
+} kd_task;
+
+typedef struct kd_job {
+    ax_work *w;
+    kd_task *t;
+    int32_t nt;
+    _Atomic int32_t next;
+} kd_job;
+
+static void *kd_thread(void *arg) {
+    kd_job *J = arg;
+    for (;;) {
+        const int32_t k = atomic_fetch_add(&J->next, 1);
+        if (k >= J->nt)
+            return NULL;
+        const kd_task *t = &J->t[k];
+        kd_build_at(J->w, t->Q, t->T, t->n, t->dim, t->id, t->tmp);
+    }
+}
+
+/* the top `depth` levels on this thread (cuts and partitions), the
+ * subtrees below them as tasks; *top collects the top nodes' ids */
+static void kd_top(ax_work *w, int32_t *Q, int32_t *T, int32_t n, int dim, int32_t id,
+                   int32_t *tmp, int depth, kd_task *tasks, int32_t *ntask, int32_t *top,
+                   int32_t *ntop) {
+    if (depth == 0 || n < 2) {
+        tasks[(*ntask)++] = (kd_task){Q, T, tmp, n, id, dim};
+        return;
+    }
+    const int32_t half = n / 2;
+    for (int32_t i = 0; i < n; ++i)
+        w->hit[Q[i]] = 0;
+    const int32_t *D = dim == 0 ? Q : T;
+    for (int32_t i = 0; i < half; ++i)
+        w->hit[D[i]] = 1;
+    const int32_t ml = D[half - 1];
+    const int32_t cut = dim == 0 ? w->qs[ml] : w->ts[ml];
+    partition(Q, n, w->hit, tmp);
+    partition(T, n, w->hit, tmp);
+    const int32_t hi = id + 1, lo = id + 2 * (n - half);
+    ax_node *nd = &w->nodes[id];
+    nd->lo = lo;
+    nd->hi = hi;
+    nd->leaf = -1;
+    nd->cut = cut;
+    nd->max_score = 0.0;
+    top[(*ntop)++] = id;
+    kd_top(w, Q + half, T + half, n - half, 1 - dim, hi, tmp + half, depth - 1, tasks, ntask, top,
+           ntop);
+    kd_top(w, Q, T, half, 1 - dim, lo, tmp, depth - 1, tasks, ntask, top, ntop);
+}
+
 /* kdTreeMake (chainBlock.c:166-205); the tree is built from copies: kd_build
- * permutes its lists */
+ * permutes its lists.  Large pairs (pair_dp_team's) build their subtrees
+ * below the top levels on every thread: the same tree, node for node. */
 static void pair_tree(ax_work *w) {
     const int32_t nl = w->nl;
     int32_t *Q = malloc((size_t)nl * sizeof(int32_t)), *T = malloc((size_t)nl * sizeof(int32_t));
     memcpy(Q, w->qord, (size_t)nl * sizeof(int32_t));
     memcpy(T, w->tord, (size_t)nl * sizeof(int32_t));
     w->nn = 0;
-    kd_build(w, Q, T, nl, 0);
+    if (w->team > 1 && nl > (1 << 16)) {
+        int depth = 0;
+        while ((1 << depth) < 4 * w->team && depth < 12)
+            ++depth;
+        kd_task *tasks = malloc(sizeof(kd_task) << depth);
+        int32_t *top = malloc(sizeof(int32_t) << depth), ntask = 0, ntop = 0;
+        kd_top(w, Q, T, nl, 0, 0, w->tmp, depth, tasks, &ntask, top, &ntop);
+        kd_job J = {w, tasks, ntask, 0};
+        gac_run_threads(w->team < ntask ? w->team : ntask, kd_thread, &J);
+        for (int32_t k = ntop - 1; k >= 0; --k) { /* children before parents */
+            ax_node *nd = &w->nodes[top[k]];
+            const ax_node *a = &w->nodes[nd->lo], *b = &w->nodes[nd->hi];
+            nd->max_q = a->max_q > b->max_q ? a->max_q : b->max_q;
+            nd->max_t = a->max_t > b->max_t ? a->max_t : b->max_t;
+        }
+        w->nn = 2 * nl - 1;
+        free(tasks);
+        free(top);
+    } else {
+        kd_build(w, Q, T, nl, 0);
+    }
     free(Q);
     free(T);
 }
 
 /* findBestPredecessors (chainBlock.c:281-300) on this thread */
+static int dp_fast_enabled(const ax_work *w) {
+    static int env = -1;
+    if (env < 0) {
+        const char *v = getenv("GAC_DP_FAST");
+        env = !(v && *v == '0');
+    }
+    return env && w->e && w->e->fast && !w->cb_gap && !w->cb_connect;
+}
+
+static void update_both(ax_work *w, int32_t leaf);
+
+static void pair_dp_fast(ax_work *w) {
+    int32_t maxsz = 0;
+    for (int32_t i = 0; i < w->nl; ++i) {
+        const int32_t l = w->tord[i];
+        if (w->te[l] - w->ts[l] > maxsz)
+            maxsz = w->te[l] - w->ts[l];
+        w->qpos[w->qord[i]] = i;
+        w->tpos[l] = i;
+    }
+    for (int32_t v = 0; v < w->nn; ++v)
+        w->nw[v] = INT64_MIN / 4;
+    w->fallbacks = 0;
+    for (int32_t i = 0; i < w->nl && !w->err; ++i) {
+        const int32_t l = w->tord[i];
+        double s;
+        int32_t p;
+        w->cut_t = i;
+        best_predecessor_fast(w, l, &s, &p);
+        if (dp_anomaly(w, l, i, s, maxsz)) {
+            best_predecessor(w, l, &s, &p);
+            ++w->fallbacks;
+        }
+        if (s > w->total[l]) {
+            w->total[l] = s;
+            w->pred[l] = p;
+        }
+        update_both(w, l);
+    }
+}
+
+/* ---- the fast DP of a large pair on several threads, exactly.
+ * Leaves go in batches of K consecutive leaves (target order).  Phase A, in
+ * parallel on the tree as the batch found it: every leaf's fast search and
+ * anomaly check.  Phase B, in order on one thread: a leaf keeps its result
+ * unless a leaf j before it in the batch -- not yet in the tree during phase
+ * A -- is its candidate and scores at least its best with j's final total
+ * (then j could be its true best predecessor, and the tree phase A searched
+ * lacked j), or its anomaly check failed; such a leaf is searched again
+ * there, on the tree with every earlier leaf in it.  A kept result is the
+ * reference's by pair_dp_fast's argument: every candidate phase A could not
+ * see correctly (the batch's earlier leaves) scores below the best it
+ * found.  Then the leaf's total and the subtree bounds are committed. */
+/* update_scores and update_nw in one walk (the same path) */
+static void update_both(ax_work *w, int32_t leaf) {
+    const double total = w->total[leaf];
+    const int64_t v = 1024 * (int64_t)total + w->e->lin_k * ((int64_t)w->qe[leaf] + w->te[leaf]);
+    const int32_t lq = w->qs[leaf], lt = w->ts[leaf];
+    int32_t st_node[kStack];
+    uint8_t st_dim[kStack];
+    int sp = 0;
+    st_node[sp] = 0;
+    st_dim[sp++] = 0;
+    while (sp > 0) {
+        --sp;
+        const int32_t b = st_node[sp];
+        const int dim = st_dim[sp];
+        ax_node *nd = &w->nodes[b];
+        if (nd->max_score < total)
+            __atomic_store(&nd->max_score, &total, __ATOMIC_RELAXED);
+        if (w->nw[b] < v)
+            __atomic_store_n(&w->nw[b], v, __ATOMIC_RELAXED);
+        if (nd->leaf < 0) {
+            if (sp + 2 > kStack) {
+                w_fail(w, "kd-tree deeper than %d", kStack / 2);
+                return;
+            }
+            const int32_t coord = dim == 0 ? lq : lt;
+            if (coord <= nd->cut) {
+                st_node[sp] = nd->lo;
+                st_dim[sp++] = (uint8_t)(1 - dim);
+            }
+            if (coord >= nd->cut) {
+                st_node[sp] = nd->hi;
+                st_dim[sp++] = (uint8_t)(1 - dim);
+            }
+        }
+    }
+}
+
+enum { kPath = 96 };
+
+/* the nodes update_both will touch for `leaf` (the path depends only on the
+ * coordinates and the cuts): *n = their count, or -1 past kPath */
+static void update_path(const ax_work *w, int32_t leaf, int32_t *out, int32_t *n) {
+    const int32_t lq = w->qs[leaf], lt = w->ts[leaf];
+    int32_t st_node[kStack];
+    uint8_t st_dim[kStack];
+    int sp = 0, m = 0;
+    st_node[sp] = 0;
+    st_dim[sp++] = 0;
+    while (sp > 0) {
+        --sp;
+        const int32_t b = st_node[sp];
+        const int dim = st_dim[sp];
+        if (m == kPath || sp + 2 > kStack) {
+            *n = -1;
+            return;
+        }
+        out[m++] = b;
+        const ax_node *nd = &w->nodes[b];
+        if (nd->leaf < 0) {
+            const int32_t coord = dim == 0 ? lq : lt;
+            if (coord <= nd->cut) {
+                st_node[sp] = nd->lo;
+                st_dim[sp++] = (uint8_t)(1 - dim);
+            }
+            if (coord >= nd->cut) {
+                st_node[sp] = nd->hi;
+                st_dim[sp++] = (uint8_t)(1 - dim);
+            }
+        }
+    }
+    *n = m;
+}
+
+static double mono_s(void);
+
+/* ---- the fast DP of a large pair on several threads, exactly.
+ * One thread commits leaves in target order; the others search ahead of it
+ * (best_predecessor_fast + dp_anomaly + the leaf's update path) on the tree
+ * as it stands -- every leaf committed before the search started is in it,
+ * later ones are still arriving (their bounds only grow, so the bounds the
+ * search reads stay true bounds for every leaf it may take).  A search sees
+ * only the leaves committed when it started (cut); the committer weighs the
+ * ones committed since (at most kLag) exactly: each that is a candidate is
+ * scored with its final total and compared with the search's best by score,
+ * then DFS (node) order, the first-in-order argmax rule of pair_dp_fast; if
+ * one of them scores at least the best while violating its own bounds (the
+ * reference's pruning could hide it), or the search flagged an anomaly, the
+ * leaf is searched again in place, on the tree with every earlier leaf in it
+ * (best_predecessor_fast, else the reference order).  Then its total and
+ * the bounds on its path are committed. */
+enum { kLagMax = 64, kRing = 256 }; /* kRing >= lag + searchers */
+
+typedef struct dp_slot {
+    double s, score;                 /* search result; the leaf's block score */
+    int32_t q, t, qe, te;            /* the leaf's block (read once, by its searcher) */
+    int32_t p, cut, plen;
+    uint8_t flag;
+    _Atomic int32_t ready; /* leaf index + 1 once the slot holds its search */
+    int32_t path[kPath];
+} dp_slot;
+
+typedef struct dp_team {
+    ax_work *w;
+    int32_t maxsz, lag;
+    _Atomic int32_t next;      /* next leaf to search */
+    _Atomic int32_t committed; /* leaves committed (target order) */
+    _Atomic int quit;
+    dp_slot *ring;
+    int32_t *cq, *ct, *cqe, *cte, *cnode; /* [kRing] committed leaves by tpos % kRing */
+    int64_t *cw;
+    double *ctot;
+    ax_work *tw;
+} dp_team;
+
+typedef struct dp_worker {
+    dp_team *T;
+    int id;
+} dp_worker;
+
+static void *team_thread(void *arg) {
+    dp_worker *me = arg;
+    dp_team *T = me->T;
+    ax_work *tw = &T->tw[me->id];
+    const int32_t nl = T->w->nl;
+    for (;;) {
+        const int32_t i = atomic_fetch_add(&T->next, 1);
+        if (i >= nl)
+            break;
+        int32_t cut;
+        while ((cut = atomic_load_explicit(&T->committed, memory_order_acquire)) + T->lag < i)
+            if (atomic_load_explicit(&T->quit, memory_order_relaxed))
+                return NULL;
+            else
+                __builtin_ia32_pause();
+        dp_slot *sl = &T->ring[i % kRing];
+        const int32_t l = T->w->tord[i];
+        tw->cut_t = cut;
+        best_predecessor_fast(tw, l, &sl->s, &sl->p);
+        sl->flag = (uint8_t)dp_anomaly(tw, l, i, sl->s, T->maxsz);
+        sl->cut = cut;
+        sl->q = T->w->qs[l];
+        sl->t = T->w->ts[l];
+        sl->qe = T->w->qe[l];
+        sl->te = T->w->te[l];
+        sl->score = T->w->score[l];
+        update_path(tw, l, sl->path, &sl->plen);
+        atomic_store_explicit(&sl->ready, i + 1, memory_order_release);
+    }
+    return NULL;
+}
+
+static void pair_dp_team(ax_work *w, int nt, int k) {
+    (void)k;
+    int32_t maxsz = 0;
+    for (int32_t i = 0; i < w->nl; ++i) {
+        const int32_t l = w->tord[i];
+        if (w->te[l] - w->ts[l] > maxsz)
+            maxsz = w->te[l] - w->ts[l];
+        w->qpos[w->qord[i]] = i;
+        w->tpos[l] = i;
+    }
+    for (int32_t v = 0; v < w->nn; ++v)
+        w->nw[v] = INT64_MIN / 4;
+    w->fallbacks = 0;
+    dp_team T;
+    memset(&T, 0, sizeof(T));
+    T.w = w;
+    T.maxsz = maxsz;
+    T.ring = calloc(kRing, sizeof(dp_slot));
+    T.cq = malloc(kRing * sizeof(int32_t));
+    T.ct = malloc(kRing * sizeof(int32_t));
+    T.cqe = malloc(kRing * sizeof(int32_t));
+    T.cte = malloc(kRing * sizeof(int32_t));
+    T.cw = malloc(kRing * sizeof(int64_t));
+    T.cnode = malloc(kRing * sizeof(int32_t));
+    T.ctot = malloc(kRing * sizeof(double));
+    const char *lv = getenv("GAC_DP_LAG");
+    T.lag = lv && atoi(lv) > 0 ? (atoi(lv) < kLagMax ? atoi(lv) : kLagMax) : 32; /* (<= 64: a mask) */
+    const int ns = nt - 1 > kRing - kLagMax ? kRing - kLagMax : nt - 1; /* searchers */
+    T.tw = calloc((size_t)(ns > 0 ? ns : 1), sizeof(ax_work));
+    for (int t = 0; t < ns; ++t) { /* shared tree, own crossover scratch and error */
+        T.tw[t] = *w;
+        T.tw[t].xs = NULL;
+        T.tw[t].xcap = 0;
+    }
+    pthread_t *th = malloc((size_t)(ns > 0 ? ns : 1) * sizeof(pthread_t));
+    dp_worker *wk = malloc((size_t)(ns > 0 ? ns : 1) * sizeof(dp_worker));
+    int started = 0;
+    for (int t = 0; t < ns; ++t) {
+        wk[t] = (dp_worker){&T, t};
+        if (pthread_create(&th[t], NULL, team_thread, &wk[t]) != 0)
+            break;
+        ++started;
+    }
+    long long redo = 0, lagsum = 0, nexact = 0, ncand = 0;
+    double twait = 0, tredo = 0;
+    uint64_t cyc_scan = 0, cyc_commit = 0;
+    for (int32_t i = 0; i < w->nl && !w->err; ++i) {
+        const int32_t l = w->tord[i];
+        dp_slot *sl = &T.ring[i % kRing];
+        double s;
+        int32_t p, cut, plen;
+        int again;
+        if (started) {
+            if (atomic_load_explicit(&sl->ready, memory_order_acquire) != i + 1) {
+                const double t0 = mono_s();
+                while (atomic_load_explicit(&sl->ready, memory_order_acquire) != i + 1)
+                    __builtin_ia32_pause();
+                twait += mono_s() - t0;
+            }
+            s = sl->s, p = sl->p, cut = sl->cut, plen = sl->plen, again = sl->flag;
+        } else { /* (no searcher thread could start: search here) */
+            w->cut_t = i;
+            best_predecessor_fast(w, l, &s, &p);
+            again = dp_anomaly(w, l, i, s, maxsz);
+            cut = i;
+            plen = -1;
+            sl->q = w->qs[l], sl->t = w->ts[l], sl->qe = w->qe[l], sl->te = w->te[l];
+            sl->score = w->score[l];
+        }
+        /* the update paths of the next searched leaves into this core's
+         * cache while this one is settled */
+        if (started && i + 16 < w->nl) { /* (a searcher wrote it: fetch it early) */
+            const char *sx = (const char *)&T.ring[(i + 16) % kRing];
+            for (size_t o = 0; o < sizeof(dp_slot); o += 64)
+                __builtin_prefetch(sx + o, 0);
+        }
+        if (started && i + 8 < w->nl) {
+            const dp_slot *nx = &T.ring[(i + 8) % kRing];
+            if (atomic_load_explicit(&nx->ready, memory_order_acquire) == i + 9)
+                for (int32_t m = 0; m < nx->plen; ++m) {
+                    __builtin_prefetch(&w->nodes[nx->path[m]], 1);
+                    __builtin_prefetch(&w->nw[nx->path[m]], 1);
+                }
+            const int32_t ln = w->tord[i + 8];
+            __builtin_prefetch(&w->total[ln], 1);
+            __builtin_prefetch(&w->pred[ln], 1);
+        }
+        const uint64_t k0 = __builtin_ia32_rdtsc();
+        /* the leaves committed since the search started: exact, here */
+        const int32_t ql = sl->q, tl = sl->t;
+        const double lsc = sl->score;
+        const int64_t kl = w->e->lin_k * ((int64_t)ql + tl) - 1024 * (int64_t)lsc;
+        const int64_t thr = 1024 * (int64_t)(s > 1.0 ? s : 1.0) + kl;
+        /* branch-free pre-filter: the candidates among them whose linear
+         * bound reaches max(best, 1), or that overlap the leaf */
+        uint64_t mask = 0;
+        for (int32_t j = cut; j < i; ++j) {
+            const int r = j % kRing;
+            const int cand = (T.cq[r] < ql) & (T.ct[r] < tl);
+            const int keep = (T.cw[r] >= thr) | (T.cqe[r] > ql) | (T.cte[r] > tl);
+            mask |= (uint64_t)(cand & keep) << (j - cut);
+        }
+        for (; mask && !again; mask &= mask - 1) {
+            const int32_t j = cut + __builtin_ctzll(mask);
+            const int r = j % kRing;
+            ++ncand;
+            const int32_t c = w->tord[j];
+            const double ctot = T.ctot[r];
+            const int dq = ql - T.cqe[r], dt = tl - T.cte[r];
+            if (dq < 0 || dt < 0) { /* overlap: its own bound */
+                const int ov = -(dq < dt ? dq : dt);
+                if (ov >= sl->qe - ql || ov >= T.cqe[r] - T.cq[r])
+                    continue;
+                const double ub = ctot + lsc - (double)gap_cost(w->e, dq + ov, dt + ov) -
+                                  (double)ov * w->e->min_entry;
+                if (ub < 1.0 || ub < s)
+                    continue;
+            }
+            ++nexact;
+            const double sc = ctot + lsc - connect_cost(w, c, l);
+            if (sc >= 1.0 && sc >= s) {
+                /* hidden by the reference's pruning?  (its bounds at c are
+                 * at least c's own) */
+                const double bc = ctot + lsc - gap_cost(w->e, dq, dt);
+                const int64_t bl = 1024 * (int64_t)ctot - w->e->lin_k * ((int64_t)dq + dt) +
+                                   1024 * (int64_t)lsc;
+                if (sc > bc || 1024 * (int64_t)sc > bl) {
+                    again = 1;
+                    break;
+                }
+            }
+            if (sc > 0 && (sc > s || (sc == s && T.cnode[r] < p))) {
+                s = sc;
+                p = T.cnode[r];
+            }
+        }
+        const uint64_t k1 = __builtin_ia32_rdtsc();
+        cyc_scan += k1 - k0;
+        lagsum += i - cut;
+        if (again) {
+            const double t0 = mono_s();
+            ++redo;
+            w->cut_t = i;
+            best_predecessor_fast(w, l, &s, &p);
+            if (dp_anomaly(w, l, i, s, maxsz)) {
+                best_predecessor(w, l, &s, &p);
+                ++w->fallbacks;
+            }
+            tredo += mono_s() - t0;
+        }
+        const uint64_t k2 = __builtin_ia32_rdtsc();
+        if (s > w->total[l]) {
+            w->total[l] = s;
+            w->pred[l] = p;
+        }
+        const double total = w->total[l];
+        const int64_t v = 1024 * (int64_t)total + w->e->lin_k * ((int64_t)sl->qe + sl->te);
+        if (plen < 0) {
+            update_both(w, l);
+        } else { /* the recorded path: the same nodes update_both visits */
+            for (int32_t m = 0; m < plen; ++m) {
+                const int32_t b = sl->path[m];
+                if (w->nodes[b].max_score < total)
+                    __atomic_store(&w->nodes[b].max_score, &total, __ATOMIC_RELAXED);
+                if (w->nw[b] < v)
+                    __atomic_store_n(&w->nw[b], v, __ATOMIC_RELAXED);
+            }
+        }
+        const int r = i % kRing;
+        T.cq[r] = ql;
+        T.ct[r] = tl;
+        T.cqe[r] = sl->qe;
+        T.cte[r] = sl->te;
+        T.cw[r] = v;
+        T.ctot[r] = total;
+        T.cnode[r] = w->lnode[l];
+        atomic_store_explicit(&T.committed, i + 1, memory_order_release);
+        cyc_commit += __builtin_ia32_rdtsc() - k2;
+    }
+    atomic_store_explicit(&T.quit, 1, memory_order_release);
+    atomic_store(&T.next, w->nl); /* (searchers still waiting leave) */
+    for (int t = 0; t < started; ++t)
+        pthread_join(th[t], NULL);
+    for (int t = 0; t < ns; ++t) {
+        if (T.tw[t].err && !w->err) {
+            w->err = 1;
+            memcpy(w->msg, T.tw[t].msg, sizeof(w->msg));
+        }
+        free(T.tw[t].xs);
+    }
+    if (getenv("GAC_TIMING"))
+        fprintf(stderr, "[gac_axt_chain] team DP: %d searchers + 1 committer, %lld of %d leaves "
+                "searched again in order (%lld by the reference order, %.3f s); the committer "
+                "waited %.3f s; mean lag %.1f, scan %.2f / commit %.2f Gcycles\n", started, redo, w->nl,
+                w->fallbacks, tredo, twait, (double)lagsum / (w->nl ? w->nl : 1), cyc_scan * 1e-9,
+                cyc_commit * 1e-9);
+    if (getenv("GAC_TIMING"))
+        fprintf(stderr, "[gac_axt_chain] team DP: %.2f candidates, %.3f exact scores per leaf\n",
+                (double)ncand / (w->nl ? w->nl : 1), (double)nexact / (w->nl ? w->nl : 1));
+    free(T.tw);
+    free(th);
+    free(wk);
+    free(T.ring);
+    free(T.cq);
+    free(T.ct);
+    free(T.cqe);
+    free(T.cte);
+    free(T.cw);
+    free(T.cnode);
+    free(T.ctot);
+}
+
 static void pair_dp_host(ax_work *w) {
+    w->fallbacks = 0;
+    if (dp_fast_enabled(w) && w->team > 1) {
+        pair_dp_team(w, w->team, w->team_batch);
+        return;
+    }
+    if (dp_fast_enabled(w)) {
+        pair_dp_fast(w);
+#ifdef GAC_DP_STATS
+        fprintf(stderr, "[dp stats] fast DP: %lld of %d leaves searched again by the reference "
+                "order\n", w->fallbacks, w->nl);
+        const double n = w->nl ? (double)w->nl : 1.0;
+        fprintf(stderr, "[dp stats] fast: per leaf visits %.1f prune1 %.1f prune2 %.1f leaves %.2f "
+                "cands %.2f wins %.2f\n", g_st.visits / n, g_st.prune1 / n, g_st.prune2 / n,
+                g_st.leaves / n, g_st.cands / n, g_st.best_wins / n);
+        memset(&g_st, 0, sizeof(g_st));
+#endif
+        return;
+    }
     for (int32_t i = 0; i < w->nl && !w->err; ++i) {
         const int32_t l = w->tord[i];
         double s;
@@ -594,6 +1396,73 @@ static void pair_dp_host(ax_work *w) {
         }
         update_scores(w, l);
     }
+#ifdef GAC_DP_STATS
+    {   /* overlapping candidates per leaf, and how many violate the corner
+         * bound of their own leaf node (anomalies: the reference's pruning
+         * can hide them) or a linear bound s*(dq+dt) */
+        long long ov = 0, neg = 0, big = 0, scans = 0, anom_c = 0, anom_l = 0, leaves_anom = 0;
+        int32_t maxsz = 0;
+        int32_t *qpos = malloc((size_t)w->n * 4);
+        for (int32_t i = 0; i < w->nl; ++i) {
+            const int32_t l = w->tord[i];
+            if (w->te[l] - w->ts[l] > maxsz) maxsz = w->te[l] - w->ts[l];
+            qpos[w->qord[i]] = i;
+        }
+        const double slope = 0.2;
+        for (int32_t i = 0; i < w->nl; ++i) {
+            const int32_t L = w->tord[i];
+            int any = 0;
+            for (int side = 0; side < 2; ++side) {
+                const int32_t *ord = side ? w->qord : w->tord;
+                const int32_t *st = side ? w->qs : w->ts;
+                const int32_t at = side ? qpos[L] : i;
+                for (int32_t j = at - 1; j >= 0 && st[ord[j]] > st[L] - maxsz; --j) {
+                    const int32_t c = ord[j];
+                    ++scans;
+                    if (w->ts[c] >= w->ts[L] || w->qs[c] >= w->qs[L])
+                        continue;
+                    const int dq = w->qs[L] - w->qe[c], dt = w->ts[L] - w->te[c];
+                    if (dq >= 0 && dt >= 0)
+                        continue;
+                    if (side == 1 && dt < 0)
+                        continue; /* (counted by the t scan) */
+                    ++ov;
+                    const int o = -(dq < dt ? dq : dt);
+                    if (o >= w->qe[L] - w->qs[L] || o >= w->qe[c] - w->qs[c]) {
+                        ++big;
+                        continue;
+                    }
+                    const double S = w->total[c] + w->score[L] - connect_cost(w, c, L);
+                    int pos, adj;
+                    crossover(w, w->qs[c], w->qe[c], w->ts[c], w->te[c], w->qs[L], w->qe[L],
+                              w->ts[L], w->te[L], o, &pos, &adj);
+                    neg += adj < 0;
+                    const double Bc = w->total[c] + w->score[L] -
+                                      gap_cost(w->e, dq < 0 ? 0 : dq, dt < 0 ? 0 : dt);
+                    const double Bl = w->total[c] + w->score[L] - slope * (dq + dt);
+                    if (S > Bc) { ++anom_c; any = 1; }
+                    if (S > Bl) { ++anom_l; any = 1; }
+                }
+            }
+            leaves_anom += any;
+        }
+        free(qpos);
+        fprintf(stderr, "[dp stats] scans %.1f/leaf, overlapping candidates %.2f (%.2f past a block "
+                "end), adj<0 %.4f, S > corner bound %.5f, S > linear bound %.5f per leaf; leaves "
+                "with an anomaly %.5f; max block %d\n",
+                (double)scans / w->nl, (double)ov / w->nl, (double)big / w->nl, (double)neg / w->nl,
+                (double)anom_c / w->nl, (double)anom_l / w->nl, (double)leaves_anom / w->nl, maxsz);
+    }
+    const double n = w->nl ? (double)w->nl : 1.0;
+    fprintf(stderr,
+            "[dp stats] leaves %d: per leaf visits %.1f prune1 %.1f prune2 %.1f leaves %.2f "
+            "cands %.2f overlaps %.2f (%.1f bases each) wins %.2f updates %.1f\n",
+            w->nl, g_st.visits / n, g_st.prune1 / n, g_st.prune2 / n, g_st.leaves / n,
+            g_st.cands / n, g_st.overlaps / n,
+            g_st.overlaps ? (double)g_st.xover_bases / g_st.overlaps : 0.0, g_st.best_wins / n,
+            g_st.updates / n);
+    memset(&g_st, 0, sizeof(g_st));
+#endif
 }
 
 /* the chains peelChains (chainBlock.c:311-373) takes off the tree: blocks of
@@ -609,7 +1478,7 @@ static void pair_peel(ax_work *w, const ax_pairinfo *pi, FILE *details, ax_chain
     dkey *dk = malloc((size_t)nl * sizeof(dkey));
     for (int32_t i = 0; i < nl; ++i)
         dk[i] = (dkey){w->total[w->tord[i]], i, w->tord[i]};
-    qsort(dk, (size_t)nl, sizeof(dkey), dkey_cmp_desc);
+    par_sort16(dk, nl, dkey_cmp_desc, w->team > 1 ? w->team : 1);
     for (int32_t i = 0; i < nb; ++i)
         w->hit[i] = 0;
     int32_t *cblk = malloc((size_t)nl * sizeof(int32_t));
@@ -707,19 +1576,180 @@ static void pair_finish(ax_work *w, ax_chains *pc, const ax_xres *x, ax_out *out
     pc->cblk = pc->cstart = NULL;
 }
 
+/* pair_finish of a large pair on every thread: scoreBlocks per chain,
+ * the sort, overlap removal per chain (each chain's blocks are its own
+ * slice of cb), then the surviving blocks gathered in sort order -- the
+ * same output; an error is the first failing chain's, as in pair_finish */
+typedef struct fin_job {
+    ax_work *w;
+    ax_work *tw;          /* per-thread copies (crossover scratch, errors) */
+    const ax_chains *pc;
+    dkey *ck;
+    ax_cb *cb;
+    int32_t *head, *cnt, *pos;
+    ax_out *out;
+    int32_t n;
+    int phase;
+    _Atomic int32_t next, wid;
+    pthread_mutex_t mu;
+    int32_t err_at;
+    char msg[512];
+} fin_job;
+
+static void *fin_thread(void *arg) {
+    fin_job *F = arg;
+    const int id = atomic_fetch_add(&F->wid, 1);
+    ax_work *w = &F->tw[id];
+    const int32_t *cblk = F->pc->cblk, *cstart = F->pc->cstart;
+    for (;;) {
+        const int32_t a = atomic_fetch_add(&F->next, 256);
+        if (a >= F->n)
+            break;
+        const int32_t b = a + 256 < F->n ? a + 256 : F->n;
+        for (int32_t r = a; r < b; ++r) {
+            if (F->phase == 0) { /* scoreBlocks of chain r */
+                double sc = 0;
+                for (int32_t j = cstart[r]; j < cstart[r + 1]; ++j) {
+                    sc += w->score[cblk[j]];
+                    if (j > cstart[r])
+                        sc -= connect_cost(w, cblk[j - 1], cblk[j]);
+                }
+                F->ck[r] = (dkey){sc, r, r};
+            } else if (F->phase == 1) { /* overlap removal of the r-th chain */
+                const int32_t c = F->ck[r].v, b0 = cstart[c], b1 = cstart[c + 1];
+                for (int32_t j = b0; j < b1; ++j) {
+                    const int32_t k = cblk[j];
+                    F->cb[j] = (ax_cb){w->qs[k], w->qe[k], w->ts[k], w->te[k], j + 1 < b1 ? j + 1 : -1};
+                }
+                const int32_t h = remove_partial_overlaps(w, F->cb, b0, NULL);
+                F->head[r] = h;
+                int32_t m = 0;
+                for (int32_t x = h; x >= 0; x = F->cb[x].next)
+                    ++m;
+                F->cnt[r] = m;
+            } else { /* copy the r-th chain's blocks out */
+                int32_t o = F->pos[r];
+                for (int32_t x = F->head[r]; x >= 0; x = F->cb[x].next, ++o) {
+                    F->out->bt[o] = F->cb[x].ts;
+                    F->out->bq[o] = F->cb[x].qs;
+                    F->out->bs[o] = F->cb[x].qe - F->cb[x].qs;
+                }
+            }
+            if (w->err) {
+                pthread_mutex_lock(&F->mu);
+                if (F->err_at < 0 || r < F->err_at) {
+                    F->err_at = r;
+                    memcpy(F->msg, w->msg, sizeof(F->msg));
+                }
+                pthread_mutex_unlock(&F->mu);
+                w->err = 0;
+            }
+        }
+    }
+    return NULL;
+}
+
+static void pair_finish_team(ax_work *w, ax_chains *pc, ax_out *out) {
+    const int32_t nc = pc->nc, nbk = pc->nbk, nt = w->team;
+    fin_job F;
+    memset(&F, 0, sizeof(F));
+    F.w = w;
+    F.pc = pc;
+    F.n = nc;
+    F.err_at = -1;
+    pthread_mutex_init(&F.mu, NULL);
+    F.tw = calloc((size_t)nt, sizeof(ax_work));
+    for (int t = 0; t < nt; ++t) {
+        F.tw[t] = *w;
+        F.tw[t].xs = NULL;
+        F.tw[t].xcap = 0;
+        F.tw[t].err = 0;
+    }
+    F.ck = malloc((size_t)(nc ? nc : 1) * sizeof(dkey));
+    F.phase = 0;
+    gac_run_threads(nt, fin_thread, &F);
+    if (F.err_at < 0) {
+        par_sort16(F.ck, nc, dkey_cmp_desc, nt);
+        F.cb = malloc((size_t)(nbk ? nbk : 1) * sizeof(ax_cb));
+        F.head = malloc((size_t)(nc ? nc : 1) * sizeof(int32_t));
+        F.cnt = malloc((size_t)(nc ? nc : 1) * sizeof(int32_t));
+        F.pos = malloc((size_t)(nc ? nc : 1) * sizeof(int32_t));
+        F.phase = 1;
+        atomic_store(&F.next, 0);
+        atomic_store(&F.wid, 0);
+        gac_run_threads(nt, fin_thread, &F);
+    }
+    if (F.err_at >= 0) {
+        w->err = 1;
+        memcpy(w->msg, F.msg, sizeof(w->msg));
+    } else {
+        out->coff = malloc((size_t)(nc + 1) * sizeof(int32_t));
+        int32_t no = 0, nob = 0;
+        for (int32_t r = 0; r < nc; ++r) {
+            F.pos[r] = nob;
+            if (F.cnt[r]) {
+                out->coff[no++] = nob;
+                nob += F.cnt[r];
+            }
+        }
+        out->coff[no] = nob;
+        out->n_chains = no;
+        out->bt = malloc((size_t)(nob ? nob : 1) * sizeof(int32_t));
+        out->bq = malloc((size_t)(nob ? nob : 1) * sizeof(int32_t));
+        out->bs = malloc((size_t)(nob ? nob : 1) * sizeof(int32_t));
+        F.out = out;
+        F.phase = 2;
+        atomic_store(&F.next, 0);
+        atomic_store(&F.wid, 0);
+        gac_run_threads(nt, fin_thread, &F);
+    }
+    for (int t = 0; t < nt; ++t)
+        free(F.tw[t].xs);
+    free(F.tw);
+    free(F.ck);
+    free(F.cb);
+    free(F.head);
+    free(F.cnt);
+    free(F.pos);
+    pthread_mutex_destroy(&F.mu);
+    free(pc->cblk);
+    free(pc->cstart);
+    pc->cblk = pc->cstart = NULL;
+}
+
+static double mono_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+
 static void chain_pair(ax_work *w, const ax_pairinfo *pi, FILE *details, ax_out *out) {
     memset(out, 0, sizeof(*out));
+    /* GAC_TIMING: the phases of pairs of over a million blocks */
+    const int tm = w->n > (1 << 20) && getenv("GAC_TIMING");
+    double t0 = tm ? mono_s() : 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
     if (pair_leaves(w) == 0) {
         out->coff = calloc(1, sizeof(int32_t));
         return;
     }
+    if (tm) t1 = mono_s();
     pair_tree(w);
+    if (tm) t2 = mono_s();
     pair_dp_host(w);
     if (w->err)
         return;
+    if (tm) t3 = mono_s();
     ax_chains pc;
     pair_peel(w, pi, details, &pc);
-    pair_finish(w, &pc, NULL, out);
+    if (tm) t4 = mono_s();
+    if (w->team > 1 && !details)
+        pair_finish_team(w, &pc, out);
+    else
+        pair_finish(w, &pc, NULL, out);
+    if (tm)
+        fprintf(stderr, "[gac_axt_chain] pair %s%c%s, %d leaves: leaves %.3f tree %.3f DP %.3f "
+                "(%lld reference-order searches) peel %.3f finish %.3f s\n", pi->qname, pi->strand,
+                pi->tname, w->nl, t1 - t0, t2 - t1, t3 - t2, w->fallbacks, t4 - t3, mono_s() - t4);
 }
 
 /* ------------------------------------------------------------------ chainBlocks */
@@ -799,6 +1829,10 @@ int gac_chain_blocks(int32_t n, const int32_t *qs, const int32_t *qe, const int3
     free(w.qord);
     free(w.tmp);
     free(w.nodes);
+    free(w.lnode);
+    free(w.qpos);
+    free(w.tpos);
+    free(w.nw);
     free(w.xs);
     if (rc != GAC_OK) {
         gac_block_chains_free(r);
@@ -846,7 +1880,68 @@ static void work_reserve(ax_work *w, int32_t n) {
     w->qord = realloc(w->qord, c * sizeof(int32_t));
     w->tmp = realloc(w->tmp, c * sizeof(int32_t));
     w->nodes = realloc(w->nodes, 2 * c * sizeof(ax_node));
+    w->lnode = realloc(w->lnode, c * sizeof(int32_t));
+    w->qpos = realloc(w->qpos, c * sizeof(int32_t));
+    w->tpos = realloc(w->tpos, c * sizeof(int32_t));
+    w->nw = realloc(w->nw, 2 * c * sizeof(int64_t));
     w->cap_n = c;
+}
+
+/* chain pair p with w (its buffers reused across pairs) */
+static void run_pair(ax_job *J, ax_work *w, int32_t p) {
+    const int64_t b0 = J->poff[p];
+    const int32_t n = (int32_t)(J->poff[p + 1] - b0);
+    ax_out *o = &J->out[p];
+    w->err = 0;
+    w->msg[0] = 0;
+    if (gac_genome_view(J->ctx, GAC_Q, J->in->q_seq[p], &w->q.v) != GAC_OK ||
+        gac_genome_view(J->ctx, GAC_T, J->in->t_seq[p], &w->t.v) != GAC_OK) {
+        memset(o, 0, sizeof(*o));
+        o->err = 1;
+        snprintf(o->msg, sizeof(o->msg), "pair %d: no host sequence", p);
+        return;
+    }
+    w->q.minus = J->in->q_strand[p] ? 1 : 0;
+    w->t.minus = 0;
+    w->n = n;
+    w->qs = J->qs + b0;
+    w->qe = J->qe + b0;
+    w->ts = J->ts + b0;
+    w->te = J->te + b0;
+    w->score = J->score + b0;
+    work_reserve(w, n);
+    char *dbuf = NULL;
+    size_t dlen = 0;
+    FILE *df = J->want_details ? open_memstream(&dbuf, &dlen) : NULL;
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    chain_pair(w, &J->info[p], df, o);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    o->secs = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+    if (df) {
+        fclose(df);
+        o->details = dbuf;
+        o->details_len = dlen;
+    }
+    if (w->err) {
+        o->err = 1;
+        memcpy(o->msg, w->msg, sizeof(o->msg));
+    }
+}
+
+static void work_free(ax_work *w) {
+    free(w->total);
+    free(w->pred);
+    free(w->hit);
+    free(w->tord);
+    free(w->qord);
+    free(w->tmp);
+    free(w->nodes);
+    free(w->lnode);
+    free(w->qpos);
+    free(w->tpos);
+    free(w->nw);
+    free(w->xs);
 }
 
 static void *ax_thread(void *arg) {
@@ -858,54 +1953,9 @@ static void *ax_thread(void *arg) {
         const int64_t k = atomic_fetch_add(&J->next, 1);
         if (k >= J->n_pairs)
             break;
-        const int32_t p = J->order[k];
-        const int64_t b0 = J->poff[p];
-        const int32_t n = (int32_t)(J->poff[p + 1] - b0);
-        ax_out *o = &J->out[p];
-        w.err = 0;
-        w.msg[0] = 0;
-        if (gac_genome_view(J->ctx, GAC_Q, J->in->q_seq[p], &w.q.v) != GAC_OK ||
-            gac_genome_view(J->ctx, GAC_T, J->in->t_seq[p], &w.t.v) != GAC_OK) {
-            memset(o, 0, sizeof(*o));
-            o->err = 1;
-            snprintf(o->msg, sizeof(o->msg), "pair %d: no host sequence", p);
-            continue;
-        }
-        w.q.minus = J->in->q_strand[p] ? 1 : 0;
-        w.t.minus = 0;
-        w.n = n;
-        w.qs = J->qs + b0;
-        w.qe = J->qe + b0;
-        w.ts = J->ts + b0;
-        w.te = J->te + b0;
-        w.score = J->score + b0;
-        work_reserve(&w, n);
-        char *dbuf = NULL;
-        size_t dlen = 0;
-        FILE *df = J->want_details ? open_memstream(&dbuf, &dlen) : NULL;
-        struct timespec t0, t1;
-        clock_gettime(CLOCK_MONOTONIC, &t0);
-        chain_pair(&w, &J->info[p], df, o);
-        clock_gettime(CLOCK_MONOTONIC, &t1);
-        o->secs = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
-        if (df) {
-            fclose(df);
-            o->details = dbuf;
-            o->details_len = dlen;
-        }
-        if (w.err) {
-            o->err = 1;
-            memcpy(o->msg, w.msg, sizeof(o->msg));
-        }
+        run_pair(J, &w, J->order[k]);
     }
-    free(w.total);
-    free(w.pred);
-    free(w.hit);
-    free(w.tord);
-    free(w.qord);
-    free(w.tmp);
-    free(w.nodes);
-    free(w.xs);
+    work_free(&w);
     return NULL;
 }
 
@@ -1306,6 +2356,9 @@ static int axt_dp_gpu(ax_job *J, int nt) {
         free(w->qord);
         free(w->tmp);
         free(w->nodes);
+        free(w->lnode);
+        free(w->qpos);
+        free(w->nw);
         free(w->xs);
     }
     free(G);
@@ -1575,6 +2628,64 @@ void gac_axt_chains_free(gac_axt_chains *c) {
     free(c);
 }
 
+/* pair_dp_fast's preconditions on the gap costs: with q(d) = cost(d, 0),
+ * t(d) = cost(0, d), b(d) = cost(dq, dt) for dq, dt > 0 and dq + dt = d
+ * (gapCalc.c:298-331), cost is monotone in each distance iff q, t and b are
+ * non-decreasing and b(d + 1) >= q(d), t(d).  Checked up to past the last
+ * long position (the linear tails beyond it: slopes >= 0, b's the steepest).
+ * lin_k/1024 = the largest s with s d <= every kind's cost at every d >= 1. */
+static void dp_fast_setup(ax_env *e) {
+    e->fast = 0;
+    e->lin_k = 0;
+    e->min_entry = 0;
+    for (int i = 0; i < 25; ++i)
+        if (e->m5[i] < e->min_entry)
+            e->min_entry = e->m5[i];
+    int32_t dmax = e->gtab_len;
+    for (int k = 0; k < 3; ++k)
+        if (e->last_pos[k] + 2 > dmax)
+            dmax = e->last_pos[k] + 2;
+    if (dmax > (1 << 22))
+        return;
+    for (int k = 0; k < 3; ++k)
+        if (!(e->last_slope[k] >= 0))
+            return;
+    if (e->last_slope[2] < e->last_slope[0] || e->last_slope[2] < e->last_slope[1])
+        return;
+    double smin = e->last_slope[0];
+    for (int k = 1; k < 3; ++k)
+        if (e->last_slope[k] < smin)
+            smin = e->last_slope[k];
+    int pq = gap_cost(e, 0, 0), pt = pq, pb = gap_cost(e, 1, 1);
+    if (pq != 0)
+        return;
+    for (int32_t d = 1; d <= dmax; ++d) {
+        const int q = gap_cost(e, d, 0), t = gap_cost(e, 0, d);
+        if (q < pq || t < pt)
+            return;
+        if (d >= 2) {
+            const int b = gap_cost(e, 1, d - 1);
+            if ((d > 2 && b < pb) || b < pq || b < pt) /* b(d) >= q(d - 1), t(d - 1) */
+                return;
+            pb = b;
+            if (b < smin * d)
+                smin = (double)b / d;
+        }
+        if (q < smin * d)
+            smin = (double)q / d;
+        if (t < smin * d)
+            smin = (double)t / d;
+        pq = q;
+        pt = t;
+    }
+    if (smin < 0)
+        return;
+    e->lin_k = (int64_t)(smin * 1024.0); /* (rounded down: s*d stays below the cost) */
+    if (e->lin_k > 0)
+        --e->lin_k;
+    e->fast = 1;
+}
+
 /* host gap-cost table of the last gap setup (gac_axt_chain) */
 static pthread_mutex_t g_gtab_mu = PTHREAD_MUTEX_INITIALIZER;
 static gac_gapcalc *cached_g = NULL;
@@ -1720,6 +2831,7 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
         env.last_slope[0] = g->q_last_slope;
         env.last_slope[1] = g->t_last_slope;
         env.last_slope[2] = g->b_last_slope;
+        dp_fast_setup(&env);
     }
     stage("host gap table", &tclock);
     /* ---- chainBlocks + overlap removal per pair on host threads */
@@ -1756,6 +2868,31 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
         rc = axt_dp_gpu(&J, nt);
         stage("kd-tree DP (device)", &tclock);
     } else {
+        /* pairs far above the even share (the critical path: one holds a
+         * quarter of a whole-genome C4 run) first, one at a time, each with
+         * its DP on every thread (pair_dp_team); then the rest, one pair
+         * per thread, largest first */
+        int64_t big = 0;
+        const char *tv = getenv("GAC_DP_TEAM");
+        const int team_on = !(tv && *tv == '0') && nthreads > 1;
+        const char *mv = getenv("GAC_DP_TEAM_MIN"); /* (tests: the size floor of a team pair) */
+        const int64_t floor_ = mv && atoll(mv) > 0 ? atoll(mv) : (1 << 20);
+        const int64_t share = nb / nthreads > floor_ ? nb / nthreads : floor_;
+        while (team_on && big < np && psize[order[big]] > share)
+            ++big;
+        if (big) {
+            ax_work w;
+            memset(&w, 0, sizeof(w));
+            w.e = &env;
+            w.team = nthreads;
+            const char *bv = getenv("GAC_DP_BATCH");
+            w.team_batch = bv && atoi(bv) > 0 ? atoi(bv) : 2 * nthreads;
+            for (int64_t k = 0; k < big; ++k)
+                run_pair(&J, &w, order[k]);
+            work_free(&w);
+            atomic_store(&J.next, big);
+            stage("kd-tree DP (largest pairs, every thread)", &tclock);
+        }
         run_threads(nt, ax_thread, &J);
         stage("kd-tree DP (threads)", &tclock);
     }

@@ -95,3 +95,56 @@ def test_axtchain_ranks_failing_rank(tool, tmp_path):
                         capture_output=True, text=True, timeout=120)
     _, err = p0.communicate(timeout=120)
     assert p1.returncode == 255 and p0.returncode == 255, (p0.returncode, err[-1000:])
+
+
+@pytest.mark.parametrize("mode", ["reference-order", "team", "team-lag1"])
+@pytest.mark.parametrize("seed", [5, 6])
+@pytest.mark.parametrize("case", ["loose", "medium0", "hoxd", "axt"])
+def test_axtchain_dp_modes_vs_golden(tool, seed, case, mode, tmp_path):
+    """The kd-tree DP's three exact forms write the reference's chains: the
+    reference-order search (GAC_DP_FAST=0), and the fast search (linear
+    bound, anomaly fallback) committed by one thread while others search
+    ahead (pair_dp_team, forced on these small pairs; lag 1 = every search
+    sees the tree of all earlier leaves)."""
+    d = os.path.join(GOLDEN, "axtchain", f"s{seed}")
+    with open(os.path.join(GOLDEN, "axtchain", "cases.json")) as f:
+        opts = json.load(f)[case]
+    inp = "in.psl" if "-psl" in opts else "in.axt.gz"
+    opts = [o.replace("../../chrM", os.path.join(GOLDEN, "chrM")) for o in opts]
+    env = dict(os.environ, GAC_THREADS="4")
+    env.update({"reference-order": {"GAC_DP_FAST": "0"},
+                "team": {"GAC_DP_TEAM_MIN": "20", "GAC_DP_LAG": "16"},
+                "team-lag1": {"GAC_DP_TEAM_MIN": "20", "GAC_DP_LAG": "1"}}[mode])
+    r = subprocess.run([tool] + opts + [os.path.join(d, inp), os.path.join(d, "t.2bit"),
+                                        os.path.join(d, "q.2bit"), "out.chain"],
+                       capture_output=True, text=True, timeout=600, cwd=tmp_path, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert filecmp.cmp(tmp_path / "out.chain", os.path.join(d, f"{case}.chain"), shallow=False)
+    for o in opts:
+        if o.startswith("-details="):
+            fn = o.split("=", 1)[1]
+            assert filecmp.cmp(tmp_path / fn, os.path.join(d, fn), shallow=False)
+
+
+def test_axtchain_team_dp_c4_shape(tool, tmp_path):
+    """A C4-shaped set dense enough for the anomaly fallback (overlapping
+    blocks with negative crossover adjustments), its largest pairs on the
+    team DP, against the reference's output when it is built (else the
+    reference-order DP's)."""
+    synth = os.path.join(ROOT, "genomealignmenttools_amd", "libexec", "gac_synth")
+    subprocess.run([synth, "c4", str(tmp_path), "-blocks=200000", "-nt=2", "-nq=2",
+                    "-tsize=3000000", "-qsize=2500000", "-threads=4"], check=True, timeout=300)
+    args = ["-linearGap=loose", "-psl", "in.psl", "t.2bit", "q.2bit"]
+    ref = os.path.join(ROOT, "oracle", "_ref", "axtChain")
+    if os.path.exists(ref):
+        subprocess.run([ref] + args + ["want.chain"], cwd=tmp_path, check=True, timeout=600,
+                       capture_output=True)
+    else:
+        subprocess.run([tool] + args + ["want.chain"], cwd=tmp_path, check=True, timeout=600,
+                       capture_output=True, env=dict(os.environ, GAC_DP_FAST="0"))
+    env = dict(os.environ, GAC_THREADS="4", GAC_DP_TEAM_MIN="1000", GAC_TIMING="1")
+    r = subprocess.run([tool] + args + ["team.chain"], cwd=tmp_path, capture_output=True, text=True,
+                       timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "team DP" in r.stderr and "reference order" in r.stderr
+    assert filecmp.cmp(tmp_path / "team.chain", tmp_path / "want.chain", shallow=False)
