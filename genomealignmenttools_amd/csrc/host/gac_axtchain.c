@@ -1225,8 +1225,8 @@ static void pair_dp_team(ax_work *w, int nt, int k) {
         }
         /* the update paths of the next searched leaves into this core's
          * cache while this one is settled */
-        if (started && i + 16 < w->nl) { /* (a searcher wrote it: fetch it early) */
-            const char *sx = (const char *)&T.ring[(i + 16) % kRing];
+        if (started && i + 4 < w->nl) { /* (a searcher wrote it: fetch it early) */
+            const char *sx = (const char *)&T.ring[(i + 4) % kRing];
             for (size_t o = 0; o < sizeof(dp_slot); o += 64)
                 __builtin_prefetch(sx + o, 0);
         }
@@ -2868,16 +2868,17 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
         rc = axt_dp_gpu(&J, nt);
         stage("kd-tree DP (device)", &tclock);
     } else {
-        /* pairs far above the even share (the critical path: one holds a
-         * quarter of a whole-genome C4 run) first, one at a time, each with
-         * its DP on every thread (pair_dp_team); then the rest, one pair
-         * per thread, largest first */
+        /* pairs of over 2^20 blocks (one holds a quarter of a whole-genome
+         * C4 run: on one thread it would be the critical path) first, one
+         * at a time, each on every thread (pair_dp_team and the parallel
+         * sorts / tree / finish); then the rest, one pair per thread,
+         * largest first */
         int64_t big = 0;
         const char *tv = getenv("GAC_DP_TEAM");
         const int team_on = !(tv && *tv == '0') && nthreads > 1;
         const char *mv = getenv("GAC_DP_TEAM_MIN"); /* (tests: the size floor of a team pair) */
         const int64_t floor_ = mv && atoll(mv) > 0 ? atoll(mv) : (1 << 20);
-        const int64_t share = nb / nthreads > floor_ ? nb / nthreads : floor_;
+        const int64_t share = floor_; /* (a pair past it would be the critical path) */
         while (team_on && big < np && psize[order[big]] > share)
             ++big;
         if (big) {
