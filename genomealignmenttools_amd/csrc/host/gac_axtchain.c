@@ -1199,7 +1199,7 @@ static void pair_dp_team(ax_work *w, int nt, int k) {
     }
     long long redo = 0, lagsum = 0, nexact = 0, ncand = 0;
     double twait = 0, tredo = 0;
-    uint64_t cyc_scan = 0, cyc_commit = 0;
+    uint64_t cyc_scan = 0, cyc_commit = 0, cyc_pref = 0, nwrites = 0;
     for (int32_t i = 0; i < w->nl && !w->err; ++i) {
         const int32_t l = w->tord[i];
         dp_slot *sl = &T.ring[i % kRing];
@@ -1225,8 +1225,9 @@ static void pair_dp_team(ax_work *w, int nt, int k) {
         }
         /* the update paths of the next searched leaves into this core's
          * cache while this one is settled */
-        if (started && i + 4 < w->nl) { /* (a searcher wrote it: fetch it early) */
-            const char *sx = (const char *)&T.ring[(i + 4) % kRing];
+        const uint64_t kp = __builtin_ia32_rdtsc();
+        if (started && i + 16 < w->nl) { /* (a searcher wrote it: fetch it early) */
+            const char *sx = (const char *)&T.ring[(i + 16) % kRing];
             for (size_t o = 0; o < sizeof(dp_slot); o += 64)
                 __builtin_prefetch(sx + o, 0);
         }
@@ -1242,6 +1243,7 @@ static void pair_dp_team(ax_work *w, int nt, int k) {
             __builtin_prefetch(&w->pred[ln], 1);
         }
         const uint64_t k0 = __builtin_ia32_rdtsc();
+        cyc_pref += k0 - kp;
         /* the leaves committed since the search started: exact, here */
         const int32_t ql = sl->q, tl = sl->t;
         const double lsc = sl->score;
@@ -1316,10 +1318,14 @@ static void pair_dp_team(ax_work *w, int nt, int k) {
         } else { /* the recorded path: the same nodes update_both visits */
             for (int32_t m = 0; m < plen; ++m) {
                 const int32_t b = sl->path[m];
-                if (w->nodes[b].max_score < total)
+                if (w->nodes[b].max_score < total) {
                     __atomic_store(&w->nodes[b].max_score, &total, __ATOMIC_RELAXED);
-                if (w->nw[b] < v)
+                    ++nwrites;
+                }
+                if (w->nw[b] < v) {
                     __atomic_store_n(&w->nw[b], v, __ATOMIC_RELAXED);
+                    ++nwrites;
+                }
             }
         }
         const int r = i % kRing;
@@ -1351,8 +1357,10 @@ static void pair_dp_team(ax_work *w, int nt, int k) {
                 w->fallbacks, tredo, twait, (double)lagsum / (w->nl ? w->nl : 1), cyc_scan * 1e-9,
                 cyc_commit * 1e-9);
     if (getenv("GAC_TIMING"))
-        fprintf(stderr, "[gac_axt_chain] team DP: %.2f candidates, %.3f exact scores per leaf\n",
-                (double)ncand / (w->nl ? w->nl : 1), (double)nexact / (w->nl ? w->nl : 1));
+        fprintf(stderr, "[gac_axt_chain] team DP: %.2f candidates, %.3f exact scores, %.2f node "
+                "writes per leaf; prefetch section %.2f Gcycles\n",
+                (double)ncand / (w->nl ? w->nl : 1), (double)nexact / (w->nl ? w->nl : 1),
+                (double)nwrites / (w->nl ? w->nl : 1), cyc_pref * 1e-9);
     free(T.tw);
     free(th);
     free(wk);
@@ -1942,6 +1950,26 @@ static void work_free(ax_work *w) {
     free(w->tpos);
     free(w->nw);
     free(w->xs);
+}
+
+typedef struct team_run {
+    ax_job *J;
+    const ax_env *env;
+    int32_t p;
+    int team, batch, started;
+    pthread_t th;
+} team_run;
+
+static void *team_runner(void *arg) {
+    team_run *R = arg;
+    ax_work w;
+    memset(&w, 0, sizeof(w));
+    w.e = R->env;
+    w.team = R->team;
+    w.team_batch = R->batch;
+    run_pair(R->J, &w, R->p);
+    work_free(&w);
+    return NULL;
 }
 
 static void *ax_thread(void *arg) {
@@ -2868,34 +2896,61 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
         rc = axt_dp_gpu(&J, nt);
         stage("kd-tree DP (device)", &tclock);
     } else {
-        /* pairs of over 2^20 blocks (one holds a quarter of a whole-genome
-         * C4 run: on one thread it would be the critical path) first, one
-         * at a time, each on every thread (pair_dp_team and the parallel
-         * sorts / tree / finish); then the rest, one pair per thread,
-         * largest first */
+        /* the pairs that would be the critical path on one thread -- over
+         * 2^20 blocks and over 1.5x an even share of all blocks (C4: the
+         * 11.5 M and 5 M block pairs of 50 M) -- each run as a team
+         * (pair_dp_team, parallel sorts / tree / finish) on its share of
+         * the threads, beside a pool that takes every other pair, largest
+         * first */
         int64_t big = 0;
         const char *tv = getenv("GAC_DP_TEAM");
-        const int team_on = !(tv && *tv == '0') && nthreads > 1;
+        const int team_on = !(tv && *tv == '0') && nthreads > 2;
         const char *mv = getenv("GAC_DP_TEAM_MIN"); /* (tests: the size floor of a team pair) */
         const int64_t floor_ = mv && atoll(mv) > 0 ? atoll(mv) : (1 << 20);
-        const int64_t share = floor_; /* (a pair past it would be the critical path) */
-        while (team_on && big < np && psize[order[big]] > share)
+        const int64_t even = (3 * (nb / nthreads)) / 2;
+        const int64_t share = mv ? floor_ : (even > floor_ ? even : floor_);
+        while (team_on && big < np && psize[order[big]] > share && big < nthreads / 2)
             ++big;
+        team_run *tr = big ? calloc((size_t)big, sizeof(team_run)) : NULL;
+        int pool = nt;
         if (big) {
-            ax_work w;
-            memset(&w, 0, sizeof(w));
-            w.e = &env;
-            w.team = nthreads;
-            const char *bv = getenv("GAC_DP_BATCH");
-            w.team_batch = bv && atoi(bv) > 0 ? atoi(bv) : 2 * nthreads;
+            int64_t sum = 0;
             for (int64_t k = 0; k < big; ++k)
-                run_pair(&J, &w, order[k]);
-            work_free(&w);
+                sum += psize[order[k]];
+            pool = nthreads / 3 > 1 ? nthreads / 3 : 1;
+            const int tt = nthreads - pool;
+            int used = 0;
+            for (int64_t k = 0; k < big; ++k) {
+                int t = (int)((double)tt * psize[order[k]] / (double)sum + 0.5);
+                t = t < 2 ? 2 : t;
+                if (k == big - 1 || used + t > tt)
+                    t = tt - used > 2 ? tt - used : 2;
+                used += t;
+                tr[k].J = &J;
+                tr[k].p = order[k];
+                tr[k].team = t;
+                const char *bv = getenv("GAC_DP_BATCH");
+                tr[k].batch = bv && atoi(bv) > 0 ? atoi(bv) : 2 * t;
+                tr[k].env = &env;
+                if (pthread_create(&tr[k].th, NULL, team_runner, &tr[k]) != 0)
+                    team_runner(&tr[k]); /* (no thread: here) */
+                else
+                    tr[k].started = 1;
+            }
             atomic_store(&J.next, big);
-            stage("kd-tree DP (largest pairs, every thread)", &tclock);
+            if (pool > np - big)
+                pool = np - big > 0 ? (int)(np - big) : 1;
         }
-        run_threads(nt, ax_thread, &J);
-        stage("kd-tree DP (threads)", &tclock);
+        if (big == 0 || np > big)
+            run_threads(pool, ax_thread, &J);
+        for (int64_t k = 0; k < big; ++k)
+            if (tr[k].started)
+                pthread_join(tr[k].th, NULL);
+        free(tr);
+        if (big)
+            stage("kd-tree DP (teams on the largest pairs, beside the pool)", &tclock);
+        else
+            stage("kd-tree DP (threads)", &tclock);
     }
     if (getenv("GAC_TIMING")) {
         double sum = 0, mx = 0;
