@@ -48,17 +48,16 @@ hipError_t launch_relayout(const uint8_t *raw, const SeqDev *seqs, int nseq, int
                            uint2 *planes, uint32_t *nmask, hipStream_t s);
 hipError_t launch_gap_table(const GapDev &g, const int32_t *small, int len, int32_t *tab,
                             hipStream_t s);
-hipError_t launch_block_gaps(const DChain *chains, int64_t n_chains, int4 *blk, Blk12 *blk12,
-                             const GapDev &g, const int32_t *small, const int32_t *tab, int len,
-                             hipStream_t s);
-hipError_t launch_nflags(const DChain *chains, int64_t n_chains, int4 *blk,
-                         const longlong2 *t_runs, int64_t n_trun, const longlong2 *q_runs,
-                         int64_t n_qrun, const int64_t *q_woff, int2 *list, int *count,
-                         hipStream_t s);
-hipError_t launch_build(const int32_t *bt, const int32_t *bq, const int32_t *bs, int64_t nb,
-                        const DChain *chains, int64_t n_chains, int4 *blk, int2 *tspan,
-                        uint32_t *bucket, hipStream_t s);
 hipError_t launch_nruns(const NPiece *p, int64_t n, uint32_t *nmask, hipStream_t s);
+hipError_t launch_build_flat(const int32_t *bt, const int32_t *bq, const int32_t *bs, int64_t nb,
+                             const DChain *chains, int64_t n_chains, int32_t *coff,
+                             int32_t *tile_c0, uint8_t *cflag, const longlong2 *t_runs,
+                             int64_t n_trun, const longlong2 *q_runs, int64_t n_qrun,
+                             const int64_t *q_woff, int4 *blk, int2 *tspan, uint32_t *bucket,
+                             hipStream_t s);
+hipError_t launch_block_gaps_flat(const int32_t *coff, const int32_t *tile_c0, int64_t nb,
+                                  int4 *blk, Blk12 *blk12, const GapDev &g, const int32_t *small,
+                                  const int32_t *tab, int len, hipStream_t s);
 hipError_t launch_scatter(const SparseRun *runs, int64_t n, const uint64_t *compact,
                           uint64_t *raw, hipStream_t s);
 hipError_t launch_blocks(const ScoreArgs &a, const BlockJob *jobs, int64_t n, int32_t *out,
@@ -237,8 +236,11 @@ struct gac_chainset {
     size_t cap_chains = 0, cap_blocks = 0, cap_blk12 = 0, cap_tspan = 0, cap_idx = 0;
     int32_t *d_stage = nullptr;  // the caller's block arrays, staged (3 x blocks)
     size_t cap_stage = 0;
-    int2 *d_nlist = nullptr;     // chains meeting an N run (+ count)
-    size_t cap_nlist = 0;
+    // flat (lane per block) kernels: compact chain offsets [n + 1], the chain
+    // of every 64-block tile's first block [tiles + 1], per-chain N flags
+    int32_t *d_coff = nullptr, *d_tile_c0 = nullptr;
+    uint8_t *d_cflag = nullptr;
+    size_t cap_coff = 0, cap_tile_c0 = 0, cap_cflag = 0;
 };
 
 static void free_whole_plan(gac_chainset *cs) {
@@ -762,8 +764,10 @@ extern "C" int gac_genome_finalize(gac_ctx *c, int side) {
     HIPCHK(hipMalloc(&g->planes, alloc_words * sizeof(uint2)));
     HIPCHK(hipMalloc(&g->nmask, alloc_words * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&g->d_woff, (nseq ? nseq : 1) * sizeof(int64_t)));
-    HIPCHK(hipMemsetAsync(g->planes, 0, alloc_words * sizeof(uint2), c->stream));
-    HIPCHK(hipMemsetAsync(g->nmask, 0xff, alloc_words * sizeof(uint32_t), c->stream));
+    // (k_relayout writes every word of the sequences: only the padding words
+    // past them are set here)
+    HIPCHK(hipMemsetAsync(g->planes + w, 0, (alloc_words - w) * sizeof(uint2), c->stream));
+    HIPCHK(hipMemsetAsync(g->nmask + w, 0xff, (alloc_words - w) * sizeof(uint32_t), c->stream));
     if (nseq) {
         HIPCHK(hipMemcpyAsync(g->d_woff, g->woff.data(), nseq * sizeof(int64_t),
                               hipMemcpyHostToDevice, c->stream));
@@ -1481,19 +1485,20 @@ static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs)
     if (e == hipSuccess && rc == GAC_OK && nb) rc = upload_staged(c, d_bt + nb, d->blk_q, nb * 4);
     if (e == hipSuccess && rc == GAC_OK && nb) rc = upload_staged(c, d_bt + 2 * nb, d->blk_size, nb * 4);
     lap("staged copies");
+    // blocks, spans, bucket indexes and per-block N flags (scoring skips the
+    // N-mask loads of N-free blocks), one lane per block
+    const int64_t ntiles = ((int64_t)nb + 63) >> 6;
+    if (e == hipSuccess)
+        e = ensure_buf((void **)&cs->d_coff, &cs->cap_coff, (size_t)(n + 1), sizeof(int32_t));
+    if (e == hipSuccess)
+        e = ensure_buf((void **)&cs->d_tile_c0, &cs->cap_tile_c0, (size_t)(ntiles + 1), sizeof(int32_t));
+    if (e == hipSuccess)
+        e = ensure_buf((void **)&cs->d_cflag, &cs->cap_cflag, (size_t)(n ? n : 1), 1);
     if (e == hipSuccess && rc == GAC_OK)
-        e = launch_build(d_bt, d_bt + nb, d_bt + 2 * nb, (int64_t)nb, cs->chains, cs->n_chains,
-                         cs->blk, cs->tspan, cs->bucket, c->stream);
-    // per-block N flags (scoring skips N-mask loads of N-free blocks)
-    int2 *d_nlist = nullptr;  // chains whose span meets an N run (+ count)
-    if (e == hipSuccess && rc == GAC_OK && (c->g[0].n_nrun || c->g[1].n_nrun)) {
-        e = ensure_buf((void **)&cs->d_nlist, &cs->cap_nlist, (size_t)(n + 1), sizeof(int2));
-        d_nlist = cs->d_nlist;
-        if (e == hipSuccess)
-            e = launch_nflags(cs->chains, n, cs->blk, c->g[0].d_nrun, c->g[0].n_nrun,
-                              c->g[1].d_nrun, c->g[1].n_nrun, c->g[1].d_woff, d_nlist + 1,
-                              (int *)d_nlist, c->stream);
-    }
+        e = launch_build_flat(d_bt, d_bt + nb, d_bt + 2 * nb, (int64_t)nb, cs->chains, n, cs->d_coff,
+                              cs->d_tile_c0, cs->d_cflag, c->g[0].d_nrun, c->g[0].n_nrun,
+                              c->g[1].d_nrun, c->g[1].n_nrun, c->g[1].d_woff, cs->blk, cs->tspan,
+                              cs->bucket, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     lap("device build + sync");
     if (rc != GAC_OK) return rc;
@@ -1530,7 +1535,8 @@ extern "C" int gac_chains_reupload(gac_ctx *c, const gac_chainset_desc *d, gac_c
 
 static void free_set_memory(gac_chainset *cs) {
     hipSetDevice(cs->ctx->device);  // (hipFree waits for work still using them)
-    void *bufs[] = {cs->chains, cs->blk, cs->blk12, cs->tspan, cs->bucket, cs->d_stage, cs->d_nlist};
+    void *bufs[] = {cs->chains, cs->blk,     cs->blk12,     cs->tspan,  cs->bucket,
+                    cs->d_stage, cs->d_coff, cs->d_tile_c0, cs->d_cflag};
     for (void *p : bufs)
         if (p) hipFree(p);
     cs->chains = nullptr;
@@ -1539,7 +1545,8 @@ static void free_set_memory(gac_chainset *cs) {
     cs->tspan = nullptr;
     cs->bucket = nullptr;
     cs->d_stage = nullptr;
-    cs->d_nlist = nullptr;
+    cs->d_coff = cs->d_tile_c0 = nullptr;
+    cs->d_cflag = nullptr;
     free_whole_plan(cs);
 }
 
@@ -1670,8 +1677,8 @@ static int prepare_args(gac_ctx *c, const gac_chainset *cs, int64_t n, uint32_t 
     if ((flags & GAC_WANT_LOCAL) && !d_l) return gac_fail(GAC_E_ARG, "GAC_WANT_LOCAL needs local output");
     if (n == 0) return GAC_OK;
     if (cs->gap_version != c->gap_version) {  // blk[].w for this scoring setup
-        HIPCHK(launch_block_gaps(cs->chains, cs->n_chains, cs->blk, cs->blk12, c->gap,
-                                 c->d_small, c->d_gap_tab, c->gap_len, s));
+        HIPCHK(launch_block_gaps_flat(cs->d_coff, cs->d_tile_c0, cs->n_blocks, cs->blk, cs->blk12,
+                                      c->gap, c->d_small, c->d_gap_tab, c->gap_len, s));
         const_cast<gac_chainset *>(cs)->gap_version = c->gap_version;
     }
     memset(&a, 0, sizeof(a));

@@ -33,7 +33,7 @@ namespace gac {
 
 // ------------------------------------------------------------ gap cost ---
 // gapCalcCost (kent/src/lib/gapCalc.c:298-331), the same operation order as
-// gac_kernels.hip (k_block_gaps) -- pinned there against the oracle
+// gac_kernels.hip (k_block_gaps_flat) -- pinned there against the oracle
 __device__ __forceinline__ int dp_interp(int x, const GapDev &g, int which) {
     const int n = g.long_count;
     const double *v = g.long_val[which];

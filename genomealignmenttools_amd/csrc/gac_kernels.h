@@ -11,7 +11,7 @@
 //   chains: DChain[c] + blocks blk[b] = int4 {tStart, qStart, size | flags, gap}
 //     flags (bits 29/30 of .z): the block's target/query bases contain an N
 //     (precomputed at upload; blocks without N skip the N-mask loads)
-//     gap: gapCalcCost to the chain's next block (k_block_gaps, per scoring
+//     gap: gapCalcCost to the chain's next block (k_block_gaps_flat, per scoring
 //     setup; 0 after the last block)
 #pragma once
 #include <stdint.h>

@@ -239,14 +239,13 @@ __device__ __forceinline__ int wave_incl_sum(int v, int lane) {
     return v;
 }
 
-// ------------------------------------------------------------ k_nflags ---
+// ------------------------------------------------------------ N flags ----
 // At chain upload: flag blocks whose target / query bases contain an N, so
 // the scoring kernel can skip N-mask loads for all other blocks.  Genomes
-// hold few N runs (assembly gaps), so a chain is first checked as a whole:
-// one lane per chain tests its target and query spans against the sorted
-// global N runs (k_nflags_chains); only chains whose span meets a run have
-// their blocks checked, against the same runs (k_nflags_blocks, one wave
-// per listed chain, lanes over blocks).
+// hold few N runs (assembly gaps), so a chain is first checked as a whole
+// (k_chain_prep: its target and query spans against the sorted global N
+// runs); only the blocks of chains whose span meets a run are checked,
+// against the same runs (k_build_flat).
 // does [lo, hi) meet one of the sorted, disjoint runs {start, end}?
 __device__ __forceinline__ bool span_meets(const longlong2 *runs, int64_t n, int64_t lo, int64_t hi) {
     int64_t a = 0, b = n;  // first run ending past lo
@@ -258,136 +257,150 @@ __device__ __forceinline__ bool span_meets(const longlong2 *runs, int64_t n, int
     return a < n && runs[a].x < hi;
 }
 
-__global__ void __launch_bounds__(256) k_nflags_chains(const DChain *chains, int64_t n_chains,
-                                                       const int4 *blk, const longlong2 *t_runs,
-                                                       int64_t n_trun, const longlong2 *q_runs,
-                                                       int64_t n_qrun, const int64_t *q_woff,
-                                                       int2 *list, int *count) {
+// ------------------------------------------------------------ flat upload
+// The chain-upload kernels one lane per BLOCK (a chain averages ~23 blocks:
+// a wave per chain left most lanes idle).  A lane finds its block's chain
+// from the chain of its 64-block tile (tile_c0, one binary search per tile)
+// and a short binary search of the compact chain offsets coff; empty chains
+// share their offset with the next chain, and "last chain starting at or
+// before b" picks the non-empty one.
+__device__ __forceinline__ int64_t owner_chain(const int32_t *coff, const int32_t *tile_c0,
+                                               int64_t ntiles, int64_t b) {
+    const int64_t t = b >> 6;
+    int64_t lo = tile_c0[t], hi = tile_c0[t + 1 < ntiles ? t + 1 : ntiles];
+    while (lo < hi) {  // last c in [lo, hi] with coff[c] <= b
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (coff[mid] <= b) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// one lane per chain: compact offsets, the bucket terminator, and whether the
+// chain's target / query span meets an N run (cflag bit 0 / 1)
+__global__ void __launch_bounds__(256) k_chain_prep(const DChain *chains, int64_t n_chains,
+                                                    int64_t nb, const int32_t *bq,
+                                                    const int32_t *bs, const longlong2 *t_runs,
+                                                    int64_t n_trun, const longlong2 *q_runs,
+                                                    int64_t n_qrun, const int64_t *q_woff,
+                                                    int32_t *coff, uint8_t *cflag,
+                                                    uint32_t *bucket) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_chains) return;
     const DChain ch = chains[c];
-    if (ch.nblk <= 0) return;
-    const bool t = n_trun && span_meets(t_runs, n_trun, ch.tbase + ch.tstart, ch.tbase + ch.tend);
-    bool q = false;
-    if (n_qrun) {
-        const int4 f = blk[ch.blk_off], l = blk[ch.blk_off + ch.nblk - 1];
-        const int64_t qs = f.y, qe = (int64_t)l.y + (l.z & kSizeMask);
-        const int64_t qsize = ch.qinfo & 0x7fffffff, qb = q_woff[ch.q_seq] * 32;
-        q = ch.qinfo < 0 ? span_meets(q_runs, n_qrun, qb + qsize - qe, qb + qsize - qs)
-                         : span_meets(q_runs, n_qrun, qb + qs, qb + qe);
-    }
-    if (t || q) list[atomicAdd(count, 1)] = make_int2((int)c, (t ? 1 : 0) | (q ? 2 : 0));
-}
-
-__global__ void __launch_bounds__(256) k_nflags_blocks(const DChain *chains, int4 *blk,
-                                                       const longlong2 *t_runs, int64_t n_trun,
-                                                       const longlong2 *q_runs, int64_t n_qrun,
-                                                       const int64_t *q_woff, const int2 *list,
-                                                       const int *count) {
-    // each block against the same sorted run lists (a few KB: cache
-    // resident), not the N mask (a random line per block and side)
-    const int lane = threadIdx.x & 63;
-    const int64_t wave_id = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    const int cnt = *count;
-    for (int64_t i = wave_id; i < cnt; i += nwaves) {
-        const int2 e = list[i];
-        const DChain ch = chains[e.x];
-        const int64_t tb = ch.tbase, qb = q_woff[ch.q_seq] * 32;
-        const bool minus = ch.qinfo < 0;
-        const int qsize = ch.qinfo & 0x7fffffff;
-        for (int k = lane; k < ch.nblk; k += kWave) {
-            int4 b = blk[ch.blk_off + k];
-            const int z = b.z & kSizeMask;
-            const int64_t qf = minus ? (int64_t)qsize - b.y - z : b.y;
-            const bool tn = (e.y & 1) && z > 0 && span_meets(t_runs, n_trun, tb + b.x, tb + b.x + z);
-            const bool qn = (e.y & 2) && z > 0 && span_meets(q_runs, n_qrun, qb + qf, qb + qf + z);
-            b.z = z | (tn ? kTHasN : 0) | (qn ? kQHasN : 0);
-            blk[ch.blk_off + k] = b;
+    coff[c] = (int32_t)ch.blk_off;
+    if (c == n_chains - 1) coff[n_chains] = (int32_t)nb;
+    const int64_t span = (int64_t)ch.tend - ch.tstart;
+    const int64_t nbk = span > 0 ? ((span - 1) >> ch.shift) + 1 : 0;
+    bucket[ch.idx_off + nbk] = (uint32_t)ch.nblk;
+    uint8_t f = 0;
+    if (ch.nblk > 0) {
+        if (n_trun && span_meets(t_runs, n_trun, ch.tbase + ch.tstart, ch.tbase + ch.tend)) f |= 1;
+        if (n_qrun) {
+            const int64_t l = ch.blk_off + ch.nblk - 1;
+            const int64_t qs = bq[ch.blk_off], qe = (int64_t)bq[l] + bs[l];
+            const int64_t qsize = ch.qinfo & 0x7fffffff, qb = q_woff[ch.q_seq] * 32;
+            const bool q = ch.qinfo < 0 ? span_meets(q_runs, n_qrun, qb + qsize - qe, qb + qsize - qs)
+                                        : span_meets(q_runs, n_qrun, qb + qs, qb + qe);
+            if (q) f |= 2;
         }
     }
+    cflag[c] = f;
 }
 
-// ------------------------------------------------------------ k_build ----
-// Chain upload, device side: blocks {tStart, qStart, size, 0} and target
-// spans from the caller's plain block arrays (one lane per block), then every
-// chain's bucket index (k_build_buckets).
-__global__ void __launch_bounds__(256) k_build_blocks(const int32_t *bt, const int32_t *bq,
-                                                      const int32_t *bs, int64_t nb, int4 *blk,
-                                                      int2 *tspan) {
+// one lane per 64-block tile: the chain holding its first block
+__global__ void __launch_bounds__(256) k_tile_chain(const int32_t *coff, int64_t n_chains,
+                                                    int64_t ntiles, int32_t *tile_c0) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > ntiles) return;
+    if (t == ntiles) {
+        tile_c0[t] = (int32_t)(n_chains - 1);
+        return;
+    }
+    const int64_t b = t << 6;
+    int64_t lo = 0, hi = n_chains - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (coff[mid] <= b) lo = mid;
+        else hi = mid - 1;
+    }
+    tile_c0[t] = (int32_t)lo;
+}
+
+// one lane per block: the block record {tStart, qStart, size | N flags, 0},
+// its target span, the N flags (blocks of chains whose span meets a run,
+// against the same sorted run lists), and the bucket entries it owns (block
+// k of a chain is bucket j's first block with tEnd past the bucket start
+// for the buckets starting in [tEnd(k-1), tEnd(k)))
+__global__ void __launch_bounds__(256) k_build_flat(const int32_t *bt, const int32_t *bq,
+                                                    const int32_t *bs, int64_t nb,
+                                                    const DChain *chains, const int32_t *coff,
+                                                    const int32_t *tile_c0, int64_t ntiles,
+                                                    const uint8_t *cflag, const longlong2 *t_runs,
+                                                    int64_t n_trun, const longlong2 *q_runs,
+                                                    int64_t n_qrun, const int64_t *q_woff,
+                                                    int4 *blk, int2 *tspan, uint32_t *bucket) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < nb) {
-        const int t = bt[b], z = bs[b];
-        blk[b] = make_int4(t, bq[b], z, 0);
-        tspan[b] = make_int2(t, t + z);
-    } else if (b < nb + 8) {  // padding: a window search may read 8 past a chain
-        tspan[b] = make_int2(0x7fffffff, 0x7fffffff);
-        blk[b] = make_int4(0x7fffffff, 0, 0, 0);
+    if (b >= nb) {
+        if (b < nb + 8) {  // padding: a window search may read 8 past a chain
+            tspan[b] = make_int2(0x7fffffff, 0x7fffffff);
+            blk[b] = make_int4(0x7fffffff, 0, 0, 0);
+        }
+        return;
     }
-}
-
-// bucket k of a chain := the first block whose target end passes the
-// bucket's start tstart + k * 2^shift.  Block b is that block for the buckets
-// starting in [tEnd(b-1), tEnd(b)): one wave per chain, each lane writes the
-// buckets of its blocks (no search; at most 2 * nblk + 1 buckets per chain).
-__global__ void __launch_bounds__(256) k_build_buckets(const DChain *chains, int64_t n_chains,
-                                                       const int2 *tspan, uint32_t *bucket) {
-    const int lane = threadIdx.x & 63;
-    const int64_t wave_id = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    for (int64_t c = wave_id; c < n_chains; c += nwaves) {
-        const DChain ch = chains[c];
-        const int2 *sp = tspan + ch.blk_off;
-        const int64_t span = (int64_t)ch.tend - ch.tstart;
-        const int64_t nbk = span > 0 ? ((span - 1) >> ch.shift) + 1 : 0;
-        const int64_t round = ((int64_t)1 << ch.shift) - 1;
-        uint32_t *bk = bucket + ch.idx_off;
-        if (lane == 0) bk[nbk] = (uint32_t)ch.nblk;
-        for (int b = lane; b < ch.nblk; b += kWave) {
-            const int64_t k0 = b ? ((int64_t)sp[b - 1].y - ch.tstart + round) >> ch.shift : 0;
-            int64_t k1 = ((int64_t)sp[b].y - ch.tstart + round) >> ch.shift;
-            if (k1 > nbk) k1 = nbk;
-            for (int64_t k = k0; k < k1; ++k) bk[k] = (uint32_t)b;
+    const int64_t c = owner_chain(coff, tile_c0, ntiles, b);
+    const DChain ch = chains[c];
+    const int t = bt[b], q = bq[b], z = bs[b];
+    int flags = 0;
+    const uint8_t f = cflag ? cflag[c] : 0;
+    if (f && z > 0) {
+        if ((f & 1) && span_meets(t_runs, n_trun, ch.tbase + t, ch.tbase + t + z)) flags |= kTHasN;
+        if (f & 2) {
+            const int64_t qb = q_woff[ch.q_seq] * 32;
+            const int64_t qf = ch.qinfo < 0 ? (int64_t)(ch.qinfo & 0x7fffffff) - q - z : q;
+            if (span_meets(q_runs, n_qrun, qb + qf, qb + qf + z)) flags |= kQHasN;
         }
     }
+    blk[b] = make_int4(t, q, z | flags, 0);
+    tspan[b] = make_int2(t, t + z);
+    const int64_t k = b - coff[c];
+    const int64_t span = (int64_t)ch.tend - ch.tstart;
+    const int64_t nbk = span > 0 ? ((span - 1) >> ch.shift) + 1 : 0;
+    const int64_t round = ((int64_t)1 << ch.shift) - 1;
+    const int64_t k0 = k ? ((int64_t)bt[b - 1] + bs[b - 1] - ch.tstart + round) >> ch.shift : 0;
+    int64_t k1 = ((int64_t)t + z - ch.tstart + round) >> ch.shift;
+    if (k1 > nbk) k1 = nbk;
+    uint32_t *bk = bucket + ch.idx_off;
+    for (int64_t j = k0; j < k1; ++j) bk[j] = (uint32_t)k;
 }
 
-// ------------------------------------------------------------ k_block_gaps
-// Per scoring setup and chain set: blk[b].w = gapCalcCost of the gap from
-// block b to block b+1 of the same chain (0 after a chain's last block).  A
-// gap inside a scored window is always between two unclipped block ends
-// (clipping only moves the first block's start and the last block's end), so
-// the tile kernel reads it with the block instead of evaluating it.
-__global__ void __launch_bounds__(256) k_block_gaps(const DChain *chains, int64_t n_chains,
-                                                    int4 *blk, Blk12 *blk12, GapDev g,
-                                                    const int32_t *small, const int32_t *tab,
-                                                    int len) {
-    const int lane = threadIdx.x & 63;
-    const int64_t wave_id = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    for (int64_t c = wave_id; c < n_chains; c += nwaves) {
-        const DChain ch = chains[c];
-        for (int k = lane; k < ch.nblk; k += kWave) {
-            int4 *b = blk + ch.blk_off + k;
-            const int4 x = b[0];
-            const int z = x.z & kSizeMask;
-            int cost = 0;
-            if (k + 1 < ch.nblk) {
-                const int4 y = b[1];
-                int d;
-                const int which = gap_kind(y.y - (x.y + z), y.x - (x.x + z), d);
-                cost = d < len ? tab[which * len + d] : gap_cost_wd(g, small, which, d);
-            }
-            b->w = cost;
-            const bool wide = z >= kB12Wide || cost < 0 || cost >= kB12GapMax;
-            Blk12 r;
-            r.t = x.x;
-            r.q = x.y;
-            r.w = (wide ? (uint32_t)kB12Wide : ((uint32_t)z | ((uint32_t)cost << 12))) |
-                  ((uint32_t)(x.z & (kTHasN | kQHasN)) << 1);
-            blk12[ch.blk_off + k] = r;
-        }
+// k_block_gaps one lane per block (the chain only says whether the block is
+// its last)
+__global__ void __launch_bounds__(256) k_block_gaps_flat(const int32_t *coff,
+                                                         const int32_t *tile_c0, int64_t ntiles,
+                                                         int64_t nb, int4 *blk, Blk12 *blk12,
+                                                         GapDev g, const int32_t *small,
+                                                         const int32_t *tab, int len) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    const int64_t c = owner_chain(coff, tile_c0, ntiles, b);
+    const int4 x = blk[b];
+    const int z = x.z & kSizeMask;
+    int cost = 0;
+    if (b + 1 < coff[c + 1]) {
+        const int4 y = blk[b + 1];
+        int d;
+        const int which = gap_kind(y.y - (x.y + z), y.x - (x.x + z), d);
+        cost = d < len ? tab[which * len + d] : gap_cost_wd(g, small, which, d);
     }
+    blk[b] = make_int4(x.x, x.y, x.z, cost);
+    const bool wide = z >= kB12Wide || cost < 0 || cost >= kB12GapMax;
+    Blk12 r;
+    r.t = x.x;
+    r.q = x.y;
+    r.w = (wide ? (uint32_t)kB12Wide : ((uint32_t)z | ((uint32_t)cost << 12))) |
+          ((uint32_t)(x.z & (kTHasN | kQHasN)) << 1);
+    blk12[b] = r;
 }
 
 // ------------------------------------------------------------ k_plan -----
@@ -1599,6 +1612,26 @@ struct SeqDev {
     int32_t pad;
 };
 
+// 32 codes of 2 bits, MSB first in each byte (8 payload bytes, loaded as one
+// little-endian u64: base 4j + k at bits 8j + 6 - 2k (low bit of the code)
+// and 8j + 7 - 2k (high bit)) -> the low-bit and high-bit planes, base i at
+// bit i: gather every other bit, then reverse each nibble
+__device__ __forceinline__ uint32_t even_bits(uint64_t x) {
+    x &= 0x5555555555555555ull;
+    x = (x | (x >> 1)) & 0x3333333333333333ull;
+    x = (x | (x >> 2)) & 0x0f0f0f0f0f0f0f0full;
+    x = (x | (x >> 4)) & 0x00ff00ff00ff00ffull;
+    x = (x | (x >> 8)) & 0x0000ffff0000ffffull;
+    x = (x | (x >> 16)) & 0x00000000ffffffffull;
+    return (uint32_t)x;
+}
+__device__ __forceinline__ uint32_t rev_nibbles(uint32_t v) {
+    v = ((v >> 1) & 0x55555555u) | ((v & 0x55555555u) << 1);
+    return ((v >> 2) & 0x33333333u) | ((v & 0x33333333u) << 2);
+}
+
+// one lane per plane word: one 8-byte load of the payload (every sequence
+// starts 8-byte aligned in the staging buffer, which is padded past its end)
 __global__ void __launch_bounds__(256) k_relayout(const uint8_t *raw, const SeqDev *seqs,
                                                   int nseq, int64_t nwords, uint2 *planes,
                                                   uint32_t *nmask) {
@@ -1612,18 +1645,11 @@ __global__ void __launch_bounds__(256) k_relayout(const uint8_t *raw, const SeqD
     }
     const SeqDev s = seqs[lo];
     const int64_t base0 = (w - s.word_off) * 32;
-    uint32_t p0 = 0, p1 = 0, pad = 0;
-    const uint8_t *src = raw + s.byte_off + (base0 >> 2);
-    for (int i = 0; i < 32; ++i) {
-        if (base0 + i >= s.size) {
-            pad |= 1u << i;  // padding scores 0 like an N
-            continue;
-        }
-        const uint32_t code = ((uint32_t)src[i >> 2] >> (6 - 2 * (i & 3))) & 3u;
-        p0 |= (code & 1u) << i;
-        p1 |= (code >> 1) << i;
-    }
-    planes[w] = make_uint2(p0, p1);
+    const uint64_t x = *reinterpret_cast<const uint64_t *>(raw + s.byte_off + (base0 >> 2));
+    const int64_t valid = s.size - base0;  // > 0
+    const uint32_t pad = valid >= 32 ? 0u : ~((1u << valid) - 1u);  // padding scores 0 like an N
+    const uint32_t p0 = rev_nibbles(even_bits(x)), p1 = rev_nibbles(even_bits(x >> 1));
+    planes[w] = make_uint2(p0 & ~pad, p1 & ~pad);
     nmask[w] = pad;
 }
 
@@ -1907,40 +1933,33 @@ hipError_t launch_gap_table(const GapDev &g, const int32_t *small, int len, int3
     return hipGetLastError();
 }
 
-hipError_t launch_block_gaps(const DChain *chains, int64_t n_chains, int4 *blk, Blk12 *blk12,
-                             const GapDev &g, const int32_t *small, const int32_t *tab, int len,
+hipError_t launch_build_flat(const int32_t *bt, const int32_t *bq, const int32_t *bs, int64_t nb,
+                             const DChain *chains, int64_t n_chains, int32_t *coff,
+                             int32_t *tile_c0, uint8_t *cflag, const longlong2 *t_runs,
+                             int64_t n_trun, const longlong2 *q_runs, int64_t n_qrun,
+                             const int64_t *q_woff, int4 *blk, int2 *tspan, uint32_t *bucket,
                              hipStream_t s) {
-    if (n_chains == 0) return hipSuccess;
-    const int64_t waves = n_chains < 65536 ? n_chains : 65536;
-    hipLaunchKernelGGL(k_block_gaps, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, chains,
-                       n_chains, blk, blk12, g, small, tab, len);
-    return hipGetLastError();
-}
-
-hipError_t launch_build(const int32_t *bt, const int32_t *bq, const int32_t *bs, int64_t nb,
-                        const DChain *chains, int64_t n_chains, int4 *blk, int2 *tspan,
-                        uint32_t *bucket, hipStream_t s) {
-    const int64_t g = (nb + 8 + 255) / 256;
-    hipLaunchKernelGGL(k_build_blocks, dim3((unsigned)g), dim3(256), 0, s, bt, bq, bs, nb, blk,
-                       tspan);
+    const int64_t ntiles = (nb + 63) >> 6;
     if (n_chains > 0) {
-        const int64_t waves = n_chains < 65536 ? n_chains : 65536;
-        hipLaunchKernelGGL(k_build_buckets, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s,
-                           chains, n_chains, tspan, bucket);
+        hipLaunchKernelGGL(k_chain_prep, dim3((unsigned)((n_chains + 255) / 256)), dim3(256), 0, s,
+                           chains, n_chains, nb, bq, bs, t_runs, n_trun, q_runs, n_qrun, q_woff,
+                           coff, cflag, bucket);
+        hipLaunchKernelGGL(k_tile_chain, dim3((unsigned)((ntiles + 1 + 255) / 256)), dim3(256), 0,
+                           s, coff, n_chains, ntiles, tile_c0);
     }
+    const int64_t g = (nb + 8 + 255) / 256;
+    hipLaunchKernelGGL(k_build_flat, dim3((unsigned)g), dim3(256), 0, s, bt, bq, bs, nb, chains,
+                       coff, tile_c0, ntiles, (n_trun || n_qrun) ? cflag : nullptr, t_runs, n_trun,
+                       q_runs, n_qrun, q_woff, blk, tspan, bucket);
     return hipGetLastError();
 }
 
-hipError_t launch_nflags(const DChain *chains, int64_t n_chains, int4 *blk,
-                         const longlong2 *t_runs, int64_t n_trun, const longlong2 *q_runs,
-                         int64_t n_qrun, const int64_t *q_woff, int2 *list, int *count,
-                         hipStream_t s) {
-    if (n_chains == 0 || (n_trun == 0 && n_qrun == 0)) return hipSuccess;
-    hipMemsetAsync(count, 0, sizeof(int), s);
-    hipLaunchKernelGGL(k_nflags_chains, dim3((unsigned)((n_chains + 255) / 256)), dim3(256), 0, s,
-                       chains, n_chains, blk, t_runs, n_trun, q_runs, n_qrun, q_woff, list, count);
-    hipLaunchKernelGGL(k_nflags_blocks, dim3(1024), dim3(256), 0, s, chains, blk, t_runs, n_trun,
-                       q_runs, n_qrun, q_woff, list, count);
+hipError_t launch_block_gaps_flat(const int32_t *coff, const int32_t *tile_c0, int64_t nb,
+                                  int4 *blk, Blk12 *blk12, const GapDev &g, const int32_t *small,
+                                  const int32_t *tab, int len, hipStream_t s) {
+    if (nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_block_gaps_flat, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, coff,
+                       tile_c0, (nb + 63) >> 6, nb, blk, blk12, g, small, tab, len);
     return hipGetLastError();
 }
 
