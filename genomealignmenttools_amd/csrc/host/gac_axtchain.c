@@ -1109,7 +1109,10 @@ typedef struct dp_team {
     int32_t maxsz, lag;
     _Atomic int32_t next;      /* next leaf to search */
     _Atomic int32_t committed; /* leaves committed (target order) */
+    _Atomic int32_t applied;   /* leaves whose path bounds are in the tree */
     _Atomic int quit;
+    int applier;               /* a thread of its own applies the path bounds */
+    uint64_t cyc_apply, napply_writes;
     dp_slot *ring;
     int32_t *cq, *ct, *cqe, *cte, *cnode; /* [kRing] committed leaves by tpos % kRing */
     int64_t *cw;
@@ -1132,7 +1135,8 @@ static void *team_thread(void *arg) {
         if (i >= nl)
             break;
         int32_t cut;
-        while ((cut = atomic_load_explicit(&T->committed, memory_order_acquire)) + T->lag < i)
+        _Atomic int32_t *const seen = T->applier ? &T->applied : &T->committed;
+        while ((cut = atomic_load_explicit(seen, memory_order_acquire)) + T->lag < i)
             if (atomic_load_explicit(&T->quit, memory_order_relaxed))
                 return NULL;
             else
@@ -1151,6 +1155,58 @@ static void *team_thread(void *arg) {
         update_path(tw, l, sl->path, &sl->plen);
         atomic_store_explicit(&sl->ready, i + 1, memory_order_release);
     }
+    return NULL;
+}
+
+/* the bounds of the committed leaves, in commit order, on a thread of its
+ * own: the node writes (lines the searchers share) leave the committer's
+ * critical path.  A search sees only leaves < applied, so its tree stays
+ * complete for every leaf it takes. */
+static void *apply_thread(void *arg) {
+    dp_team *T = arg;
+    ax_work *w = T->w;
+    const int64_t k = w->e->lin_k;
+    uint64_t cyc = 0, nwr = 0;
+    for (int32_t j = 0; j < w->nl; ++j) {
+        int32_t c;
+        while ((c = atomic_load_explicit(&T->committed, memory_order_acquire)) <= j)
+            if (atomic_load_explicit(&T->quit, memory_order_acquire))
+                goto done;
+            else
+                __builtin_ia32_pause();
+        const uint64_t k0 = __builtin_ia32_rdtsc();
+        if (j + 4 < c) { /* (committed, so its slot is final: fetch its path early) */
+            const dp_slot *nx = &T->ring[(j + 4) % kRing];
+            for (int32_t m = 0; m < nx->plen; ++m) {
+                __builtin_prefetch(&w->nodes[nx->path[m]], 1);
+                __builtin_prefetch(&w->nw[nx->path[m]], 1);
+            }
+        }
+        const dp_slot *sl = &T->ring[j % kRing];
+        const int32_t l = w->tord[j];
+        if (sl->plen < 0) {
+            update_both(w, l);
+        } else {
+            const double total = w->total[l];
+            const int64_t v = 1024 * (int64_t)total + k * ((int64_t)sl->qe + sl->te);
+            for (int32_t m = 0; m < sl->plen; ++m) {
+                const int32_t b = sl->path[m];
+                if (w->nodes[b].max_score < total) {
+                    __atomic_store(&w->nodes[b].max_score, &total, __ATOMIC_RELAXED);
+                    ++nwr;
+                }
+                if (w->nw[b] < v) {
+                    __atomic_store_n(&w->nw[b], v, __ATOMIC_RELAXED);
+                    ++nwr;
+                }
+            }
+        }
+        atomic_store_explicit(&T->applied, j + 1, memory_order_release);
+        cyc += __builtin_ia32_rdtsc() - k0;
+    }
+done:
+    T->cyc_apply = cyc;
+    T->napply_writes = nwr;
     return NULL;
 }
 
@@ -1181,7 +1237,10 @@ static void pair_dp_team(ax_work *w, int nt, int k) {
     T.ctot = malloc(kRing * sizeof(double));
     const char *lv = getenv("GAC_DP_LAG");
     T.lag = lv && atoi(lv) > 0 ? (atoi(lv) < kLagMax ? atoi(lv) : kLagMax) : 32; /* (<= 64: a mask) */
-    const int ns = nt - 1 > kRing - kLagMax ? kRing - kLagMax : nt - 1; /* searchers */
+    const char *av = getenv("GAC_DP_APPLY");
+    T.applier = nt >= 4 && !(av && *av == '0');
+    const int nsw = nt - 1 - T.applier;
+    const int ns = nsw > kRing - kLagMax ? kRing - kLagMax : nsw; /* searchers */
     T.tw = calloc((size_t)(ns > 0 ? ns : 1), sizeof(ax_work));
     for (int t = 0; t < ns; ++t) { /* shared tree, own crossover scratch and error */
         T.tw[t] = *w;
@@ -1191,6 +1250,9 @@ static void pair_dp_team(ax_work *w, int nt, int k) {
     pthread_t *th = malloc((size_t)(ns > 0 ? ns : 1) * sizeof(pthread_t));
     dp_worker *wk = malloc((size_t)(ns > 0 ? ns : 1) * sizeof(dp_worker));
     int started = 0;
+    pthread_t ath;
+    if (T.applier && pthread_create(&ath, NULL, apply_thread, &T) != 0)
+        T.applier = 0; /* (no thread: the committer applies) */
     for (int t = 0; t < ns; ++t) {
         wk[t] = (dp_worker){&T, t};
         if (pthread_create(&th[t], NULL, team_thread, &wk[t]) != 0)
@@ -1231,13 +1293,15 @@ static void pair_dp_team(ax_work *w, int nt, int k) {
             for (size_t o = 0; o < sizeof(dp_slot); o += 64)
                 __builtin_prefetch(sx + o, 0);
         }
-        if (started && i + 8 < w->nl) {
+        if (started && !T.applier && i + 8 < w->nl) {
             const dp_slot *nx = &T.ring[(i + 8) % kRing];
             if (atomic_load_explicit(&nx->ready, memory_order_acquire) == i + 9)
                 for (int32_t m = 0; m < nx->plen; ++m) {
                     __builtin_prefetch(&w->nodes[nx->path[m]], 1);
                     __builtin_prefetch(&w->nw[nx->path[m]], 1);
                 }
+        }
+        if (i + 8 < w->nl) {
             const int32_t ln = w->tord[i + 8];
             __builtin_prefetch(&w->total[ln], 1);
             __builtin_prefetch(&w->pred[ln], 1);
@@ -1298,6 +1362,9 @@ static void pair_dp_team(ax_work *w, int nt, int k) {
         if (again) {
             const double t0 = mono_s();
             ++redo;
+            if (T.applier) /* (the search needs every earlier leaf's bounds) */
+                while (atomic_load_explicit(&T.applied, memory_order_acquire) < i)
+                    __builtin_ia32_pause();
             w->cut_t = i;
             best_predecessor_fast(w, l, &s, &p);
             if (dp_anomaly(w, l, i, s, maxsz)) {
@@ -1313,7 +1380,9 @@ static void pair_dp_team(ax_work *w, int nt, int k) {
         }
         const double total = w->total[l];
         const int64_t v = 1024 * (int64_t)total + w->e->lin_k * ((int64_t)sl->qe + sl->te);
-        if (plen < 0) {
+        if (T.applier) {
+            /* (apply_thread writes the bounds) */
+        } else if (plen < 0) {
             update_both(w, l);
         } else { /* the recorded path: the same nodes update_both visits */
             for (int32_t m = 0; m < plen; ++m) {
@@ -1343,6 +1412,10 @@ static void pair_dp_team(ax_work *w, int nt, int k) {
     atomic_store(&T.next, w->nl); /* (searchers still waiting leave) */
     for (int t = 0; t < started; ++t)
         pthread_join(th[t], NULL);
+    if (T.applier) {
+        pthread_join(ath, NULL);
+        nwrites = T.napply_writes;
+    }
     for (int t = 0; t < ns; ++t) {
         if (T.tw[t].err && !w->err) {
             w->err = 1;
@@ -1358,9 +1431,10 @@ static void pair_dp_team(ax_work *w, int nt, int k) {
                 cyc_commit * 1e-9);
     if (getenv("GAC_TIMING"))
         fprintf(stderr, "[gac_axt_chain] team DP: %.2f candidates, %.3f exact scores, %.2f node "
-                "writes per leaf; prefetch section %.2f Gcycles\n",
+                "writes per leaf; prefetch section %.2f Gcycles; applier %s %.2f Gcycles\n",
                 (double)ncand / (w->nl ? w->nl : 1), (double)nexact / (w->nl ? w->nl : 1),
-                (double)nwrites / (w->nl ? w->nl : 1), cyc_pref * 1e-9);
+                (double)nwrites / (w->nl ? w->nl : 1), cyc_pref * 1e-9,
+                T.applier ? "thread" : "off", T.cyc_apply * 1e-9);
     free(T.tw);
     free(th);
     free(wk);

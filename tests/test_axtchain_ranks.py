@@ -97,7 +97,7 @@ def test_axtchain_ranks_failing_rank(tool, tmp_path):
     assert p1.returncode == 255 and p0.returncode == 255, (p0.returncode, err[-1000:])
 
 
-@pytest.mark.parametrize("mode", ["reference-order", "team", "team-lag1"])
+@pytest.mark.parametrize("mode", ["reference-order", "team", "team-lag1", "team-no-applier"])
 @pytest.mark.parametrize("seed", [5, 6])
 @pytest.mark.parametrize("case", ["loose", "medium0", "hoxd", "axt"])
 def test_axtchain_dp_modes_vs_golden(tool, seed, case, mode, tmp_path):
@@ -105,16 +105,18 @@ def test_axtchain_dp_modes_vs_golden(tool, seed, case, mode, tmp_path):
     reference-order search (GAC_DP_FAST=0), and the fast search (linear
     bound, anomaly fallback) committed by one thread while others search
     ahead (pair_dp_team, forced on these small pairs; lag 1 = every search
-    sees the tree of all earlier leaves)."""
+    sees the tree of all earlier leaves; the path bounds written by a thread
+    of their own, or by the committer)."""
     d = os.path.join(GOLDEN, "axtchain", f"s{seed}")
     with open(os.path.join(GOLDEN, "axtchain", "cases.json")) as f:
         opts = json.load(f)[case]
     inp = "in.psl" if "-psl" in opts else "in.axt.gz"
     opts = [o.replace("../../chrM", os.path.join(GOLDEN, "chrM")) for o in opts]
-    env = dict(os.environ, GAC_THREADS="4")
+    env = dict(os.environ, GAC_THREADS="6")
     env.update({"reference-order": {"GAC_DP_FAST": "0"},
                 "team": {"GAC_DP_TEAM_MIN": "20", "GAC_DP_LAG": "16"},
-                "team-lag1": {"GAC_DP_TEAM_MIN": "20", "GAC_DP_LAG": "1"}}[mode])
+                "team-lag1": {"GAC_DP_TEAM_MIN": "20", "GAC_DP_LAG": "1"},
+                "team-no-applier": {"GAC_DP_TEAM_MIN": "20", "GAC_DP_APPLY": "0"}}[mode])
     r = subprocess.run([tool] + opts + [os.path.join(d, inp), os.path.join(d, "t.2bit"),
                                         os.path.join(d, "q.2bit"), "out.chain"],
                        capture_output=True, text=True, timeout=600, cwd=tmp_path, env=env)
@@ -142,9 +144,10 @@ def test_axtchain_team_dp_c4_shape(tool, tmp_path):
     else:
         subprocess.run([tool] + args + ["want.chain"], cwd=tmp_path, check=True, timeout=600,
                        capture_output=True, env=dict(os.environ, GAC_DP_FAST="0"))
-    env = dict(os.environ, GAC_THREADS="4", GAC_DP_TEAM_MIN="1000", GAC_TIMING="1")
+    env = dict(os.environ, GAC_THREADS="8", GAC_DP_TEAM_MIN="30000", GAC_TIMING="1")
     r = subprocess.run([tool] + args + ["team.chain"], cwd=tmp_path, capture_output=True, text=True,
                        timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "team DP" in r.stderr and "reference order" in r.stderr
+    assert "applier thread" in r.stderr
     assert filecmp.cmp(tmp_path / "team.chain", tmp_path / "want.chain", shallow=False)
