@@ -116,11 +116,18 @@ static void seq_codes(const ax_seq *s, int32_t start, int32_t len, uint8_t *out)
 }
 
 /* ------------------------------------------------------------------ per-thread work */
-typedef struct ax_node { /* struct kdBranch (chainBlock.c:17-28) */
+typedef struct ax_node { /* struct kdBranch (chainBlock.c:17-28), the fixed part */
     int32_t lo, hi, leaf, cut;
-    double max_score;
     int32_t max_q, max_t;
 } ax_node;
+
+/* the part of a node the DP raises (kdBranch.maxScore, and the fast DP's
+ * linear bound), apart from the fixed part: a searcher's copy of a node's
+ * children and cuts is never invalidated by a bound update */
+typedef struct ax_bound {
+    double max_score;
+    int64_t nw; /* max of 1024 total + k (qEnd + tEnd) */
+} ax_bound;
 
 typedef struct ax_out { /* one pair's result */
     int32_t n_chains;
@@ -148,9 +155,12 @@ typedef struct ax_work {
     ax_node *nodes;
     int32_t nn;
     int32_t *lnode;  /* [block] the leaf's node */
-    int64_t *nw;     /* [node] pair_dp_fast's linear bound: max of 1024 total + k (qEnd + tEnd) */
+    ax_bound *bnd;   /* [node] the bounds the DP raises */
     int32_t *qpos;   /* [block] the leaf's place in qord */
     int32_t *tpos;   /* [block] the leaf's place in tord */
+    int32_t *tbox;   /* [4 leaves] by place in tord: {tStart, tEnd, qStart, qEnd} */
+    int32_t *qbox;   /* [4 leaves] by place in qord: {qStart, qEnd, tStart, tEnd} */
+    int32_t *qtp;    /* [leaf] by place in qord: its place in tord */
     int32_t cut_t;   /* fast searches see only leaves with tpos < cut_t */
     long long fallbacks;
     int team, team_batch; /* > 1: this pair's DP on that many threads (pair_dp_team) */
@@ -275,7 +285,8 @@ static int32_t kd_build(ax_work *w, int32_t *Q, int32_t *T, int32_t n, int dim) 
     if (n == 1) {
         const int32_t l = Q[0];
         /* leaf node: lo/hi carry the leaf's qStart/tStart */
-        w->nodes[id] = (ax_node){w->qs[l], w->ts[l], l, 0, 0.0, w->qe[l], w->te[l]};
+        w->nodes[id] = (ax_node){w->qs[l], w->ts[l], l, 0, w->qe[l], w->te[l]};
+        w->bnd[id] = (ax_bound){0.0, INT64_MIN / 4};
         w->lnode[l] = id;
         return id;
     }
@@ -298,7 +309,7 @@ static int32_t kd_build(ax_work *w, int32_t *Q, int32_t *T, int32_t n, int dim) 
     nd->hi = hi;
     nd->leaf = -1;
     nd->cut = cut;
-    nd->max_score = 0.0;
+    w->bnd[id] = (ax_bound){0.0, INT64_MIN / 4};
     nd->max_q = w->nodes[lo].max_q > w->nodes[hi].max_q ? w->nodes[lo].max_q : w->nodes[hi].max_q;
     nd->max_t = w->nodes[lo].max_t > w->nodes[hi].max_t ? w->nodes[lo].max_t : w->nodes[hi].max_t;
     return id;
@@ -335,7 +346,7 @@ static void best_predecessor(ax_work *w, int32_t lonely, double *ret_score, int3
         const int dim = st_dim[sp];
         const ax_node *nd = &w->nodes[b];
         ST(visits);
-        double max_score = nd->max_score + lscore;
+        double max_score = w->bnd[b].max_score + lscore;
         if (max_score < best) {
             ST(prune1);
             continue;
@@ -398,8 +409,8 @@ static void update_scores(ax_work *w, int32_t leaf) {
         const int dim = st_dim[sp];
         ax_node *nd = &w->nodes[b];
         ST(updates);
-        if (nd->max_score < total)
-            nd->max_score = total;
+        if (w->bnd[b].max_score < total)
+            w->bnd[b].max_score = total;
         if (nd->leaf < 0) {
             if (sp + 2 > kStack) {
                 w_fail(w, "kd-tree deeper than %d", kStack / 2);
@@ -461,26 +472,33 @@ static void best_predecessor_fast(ax_work *w, int32_t lonely, double *ret_score,
         const int dim = st_dim[sp];
         const ax_node *nd = &w->nodes[b];
         ST(visits);
-        double max_score = nd->max_score + lscore;
+        double max_score = w->bnd[b].max_score + lscore;
         if (max_score < best) {
             ST(prune1);
             continue;
         }
-        if (w->nw[b] - kl < best1024) {
+        if (w->bnd[b].nw - kl < best1024) {
             ST(prune1);
             continue;
         }
-        max_score -= gap_cost(w->e, lq - nd->max_q, lt - nd->max_t);
+        const int dq = lq - nd->max_q, dt = lt - nd->max_t;
+        const int gc = gap_cost(w->e, dq, dt);
+        max_score -= gc;
         if (max_score < best) {
             ST(prune2);
             continue;
         }
         if (nd->leaf >= 0) {
+            /* a leaf node holds its block (lo, hi = qStart, tStart; max_q,
+             * max_t = qEnd, tEnd) and its target position (cut, see
+             * dp_leaf_positions): a candidate that does not overlap costs
+             * the gap just computed, with no look-up of its block */
             const int32_t l = nd->leaf;
             ST(leaves);
-            if (nd->lo < lq && nd->hi < lt && w->tpos[l] < w->cut_t) {
+            if (nd->lo < lq && nd->hi < lt && nd->cut < w->cut_t) {
                 ST(cands);
-                const double s = w->total[l] + lscore - connect_cost(w, l, lonely);
+                const int cost = (dq >= 0 && dt >= 0) ? gc : connect_cost(w, l, lonely);
+                const double s = w->total[l] + lscore - cost;
                 if (s > best) {
                     ST(best_wins);
                     best = s;
@@ -497,6 +515,8 @@ static void best_predecessor_fast(ax_work *w, int32_t lonely, double *ret_score,
         const int32_t coord = dim == 0 ? lq : lt;
         st_node[sp] = nd->lo;
         st_dim[sp++] = (uint8_t)(1 - dim);
+        __builtin_prefetch(&w->nodes[nd->lo]); /* (visited after the hi side) */
+        __builtin_prefetch(&w->bnd[nd->lo]);
         if (coord > nd->cut) {
             st_node[sp] = nd->hi;
             st_dim[sp++] = (uint8_t)(1 - dim);
@@ -504,6 +524,29 @@ static void best_predecessor_fast(ax_work *w, int32_t lonely, double *ret_score,
     }
     *ret_score = best;
     *ret_pred = best_node;
+}
+
+/* the target position of every leaf, in w->tpos and in its leaf node's
+ * (otherwise unused) cut field, where the fast search reads it */
+static void dp_leaf_positions(ax_work *w, int32_t *maxsz) {
+    int32_t m = 0;
+    for (int32_t i = 0; i < w->nl; ++i) {
+        const int32_t l = w->tord[i];
+        if (w->te[l] - w->ts[l] > m)
+            m = w->te[l] - w->ts[l];
+        w->qpos[w->qord[i]] = i;
+        w->tpos[l] = i;
+        w->nodes[w->lnode[l]].cut = i;
+        int32_t *b = w->tbox + 4 * (size_t)i;
+        b[0] = w->ts[l], b[1] = w->te[l], b[2] = w->qs[l], b[3] = w->qe[l];
+    }
+    for (int32_t i = 0; i < w->nl; ++i) {
+        const int32_t l = w->qord[i];
+        int32_t *b = w->qbox + 4 * (size_t)i;
+        b[0] = w->qs[l], b[1] = w->qe[l], b[2] = w->ts[l], b[3] = w->te[l];
+        w->qtp[i] = w->tpos[l];
+    }
+    *maxsz = m;
 }
 
 /* 1 when an overlapping candidate of `lonely` (the ti-th leaf in t order)
@@ -515,21 +558,26 @@ static int dp_anomaly(ax_work *w, int32_t lonely, int32_t ti, double best, int32
     const double need = best > 0 ? best : 1.0; /* (scores are integral) */
     const int64_t k = w->e->lin_k;
     for (int side = 0; side < 2; ++side) {
-        const int32_t *ord = side ? w->qord : w->tord;
-        const int32_t *st = side ? w->qs : w->ts;
+        /* the leaves starting within the longest block before the lonely
+         * one on this side, read in order from the packed boxes */
+        const int32_t *box = side ? w->qbox : w->tbox;
         const int32_t at = side ? w->qpos[lonely] : ti, lo = (side ? lq : lt) - maxsz;
-        for (int32_t j = at - 1; j >= 0 && st[ord[j]] > lo; --j) {
-            const int32_t c = ord[j];
-            if (w->ts[c] >= lt || w->qs[c] >= lq || w->tpos[c] >= w->cut_t)
+        for (int32_t j = at - 1; j >= 0 && box[4 * (size_t)j] > lo; --j) {
+            const int32_t *b = box + 4 * (size_t)j;
+            const int32_t cqs = side ? b[0] : b[2], cqe = side ? b[1] : b[3];
+            const int32_t cts = side ? b[2] : b[0], cte = side ? b[3] : b[1];
+            const int32_t tp = side ? w->qtp[j] : j;
+            if (cts >= lt || cqs >= lq || tp >= w->cut_t)
                 continue; /* not a candidate (or not yet scored) */
-            int dq = lq - w->qe[c], dt = lt - w->te[c];
+            int dq = lq - cqe, dt = lt - cte;
             if (dq >= 0 && dt >= 0)
                 continue; /* no overlap: the bounds hold */
             if (side == 1 && dt < 0)
                 continue; /* (the t scan saw it) */
             const int ov = -(dq < dt ? dq : dt);
-            if (ov >= lsize || ov >= w->qe[c] - w->qs[c])
+            if (ov >= lsize || ov >= cqe - cqs)
                 continue; /* connect cost 1e8 */
+            const int32_t c = side ? w->qord[j] : w->tord[j];
             /* cheap upper bound first: adj >= ov * min_entry */
             const double ub = w->total[c] + lscore - (double)gap_cost(w->e, dq + ov, dt + ov) -
                               (double)ov * w->e->min_entry;
@@ -832,7 +880,8 @@ static void kd_build_at(ax_work *w, int32_t *Q, int32_t *T, int32_t n, int dim, 
                         int32_t *tmp) {
     if (n == 1) {
         const int32_t l = Q[0];
-        w->nodes[id] = (ax_node){w->qs[l], w->ts[l], l, 0, 0.0, w->qe[l], w->te[l]};
+        w->nodes[id] = (ax_node){w->qs[l], w->ts[l], l, 0, w->qe[l], w->te[l]};
+        w->bnd[id] = (ax_bound){0.0, INT64_MIN / 4};
         w->lnode[l] = id;
         return;
     }
@@ -854,7 +903,7 @@ static void kd_build_at(ax_work *w, int32_t *Q, int32_t *T, int32_t n, int dim, 
     nd->hi = hi;
     nd->leaf = -1;
     nd->cut = cut;
-    nd->max_score = 0.0;
+    w->bnd[id] = (ax_bound){0.0, INT64_MIN / 4};
     nd->max_q = w->nodes[lo].max_q > w->nodes[hi].max_q ? w->nodes[lo].max_q : w->nodes[hi].max_q;
     nd->max_t = w->nodes[lo].max_t > w->nodes[hi].max_t ? w->nodes[lo].max_t : w->nodes[hi].max_t;
 }
@@ -908,7 +957,7 @@ static void kd_top(ax_work *w, int32_t *Q, int32_t *T, int32_t n, int dim, int32
     nd->hi = hi;
     nd->leaf = -1;
     nd->cut = cut;
-    nd->max_score = 0.0;
+    w->bnd[id] = (ax_bound){0.0, INT64_MIN / 4};
     top[(*ntop)++] = id;
     kd_top(w, Q + half, T + half, n - half, 1 - dim, hi, tmp + half, depth - 1, tasks, ntask, top,
            ntop);
@@ -962,16 +1011,10 @@ static int dp_fast_enabled(const ax_work *w) {
 static void update_both(ax_work *w, int32_t leaf);
 
 static void pair_dp_fast(ax_work *w) {
-    int32_t maxsz = 0;
-    for (int32_t i = 0; i < w->nl; ++i) {
-        const int32_t l = w->tord[i];
-        if (w->te[l] - w->ts[l] > maxsz)
-            maxsz = w->te[l] - w->ts[l];
-        w->qpos[w->qord[i]] = i;
-        w->tpos[l] = i;
-    }
+    int32_t maxsz;
+    dp_leaf_positions(w, &maxsz);
     for (int32_t v = 0; v < w->nn; ++v)
-        w->nw[v] = INT64_MIN / 4;
+        w->bnd[v].nw = INT64_MIN / 4;
     w->fallbacks = 0;
     for (int32_t i = 0; i < w->nl && !w->err; ++i) {
         const int32_t l = w->tord[i];
@@ -1018,10 +1061,10 @@ static void update_both(ax_work *w, int32_t leaf) {
         const int32_t b = st_node[sp];
         const int dim = st_dim[sp];
         ax_node *nd = &w->nodes[b];
-        if (nd->max_score < total)
-            __atomic_store(&nd->max_score, &total, __ATOMIC_RELAXED);
-        if (w->nw[b] < v)
-            __atomic_store_n(&w->nw[b], v, __ATOMIC_RELAXED);
+        if (w->bnd[b].max_score < total)
+            __atomic_store(&w->bnd[b].max_score, &total, __ATOMIC_RELAXED);
+        if (w->bnd[b].nw < v)
+            __atomic_store_n(&w->bnd[b].nw, v, __ATOMIC_RELAXED);
         if (nd->leaf < 0) {
             if (sp + 2 > kStack) {
                 w_fail(w, "kd-tree deeper than %d", kStack / 2);
@@ -1096,13 +1139,17 @@ static double mono_s(void);
 enum { kLagMax = 64, kRing = 256 }; /* kRing >= lag + searchers */
 
 typedef struct dp_slot {
-    double s, score;                 /* search result; the leaf's block score */
+    /* the committer's line: one cache-to-cache transfer per leaf */
+    _Alignas(64) double s; /* search result */
+    double score;          /* the leaf's block score */
     int32_t q, t, qe, te;            /* the leaf's block (read once, by its searcher) */
     int32_t p, cut, plen;
     uint8_t flag;
     _Atomic int32_t ready; /* leaf index + 1 once the slot holds its search */
-    int32_t path[kPath];
+    /* the applier's lines */
+    _Alignas(64) int32_t path[kPath];
 } dp_slot;
+_Static_assert(offsetof(dp_slot, path) == 64, "dp_slot: the committer's fields fill one line");
 
 typedef struct dp_team {
     ax_work *w;
@@ -1178,8 +1225,7 @@ static void *apply_thread(void *arg) {
         if (j + 4 < c) { /* (committed, so its slot is final: fetch its path early) */
             const dp_slot *nx = &T->ring[(j + 4) % kRing];
             for (int32_t m = 0; m < nx->plen; ++m) {
-                __builtin_prefetch(&w->nodes[nx->path[m]], 1);
-                __builtin_prefetch(&w->nw[nx->path[m]], 1);
+                __builtin_prefetch(&w->bnd[nx->path[m]], 1);
             }
         }
         const dp_slot *sl = &T->ring[j % kRing];
@@ -1191,12 +1237,12 @@ static void *apply_thread(void *arg) {
             const int64_t v = 1024 * (int64_t)total + k * ((int64_t)sl->qe + sl->te);
             for (int32_t m = 0; m < sl->plen; ++m) {
                 const int32_t b = sl->path[m];
-                if (w->nodes[b].max_score < total) {
-                    __atomic_store(&w->nodes[b].max_score, &total, __ATOMIC_RELAXED);
+                if (w->bnd[b].max_score < total) {
+                    __atomic_store(&w->bnd[b].max_score, &total, __ATOMIC_RELAXED);
                     ++nwr;
                 }
-                if (w->nw[b] < v) {
-                    __atomic_store_n(&w->nw[b], v, __ATOMIC_RELAXED);
+                if (w->bnd[b].nw < v) {
+                    __atomic_store_n(&w->bnd[b].nw, v, __ATOMIC_RELAXED);
                     ++nwr;
                 }
             }
@@ -1212,22 +1258,19 @@ done:
 
 static void pair_dp_team(ax_work *w, int nt, int k) {
     (void)k;
-    int32_t maxsz = 0;
-    for (int32_t i = 0; i < w->nl; ++i) {
-        const int32_t l = w->tord[i];
-        if (w->te[l] - w->ts[l] > maxsz)
-            maxsz = w->te[l] - w->ts[l];
-        w->qpos[w->qord[i]] = i;
-        w->tpos[l] = i;
-    }
+    int32_t maxsz;
+    dp_leaf_positions(w, &maxsz);
     for (int32_t v = 0; v < w->nn; ++v)
-        w->nw[v] = INT64_MIN / 4;
+        w->bnd[v].nw = INT64_MIN / 4;
     w->fallbacks = 0;
     dp_team T;
     memset(&T, 0, sizeof(T));
     T.w = w;
     T.maxsz = maxsz;
-    T.ring = calloc(kRing, sizeof(dp_slot));
+    T.ring = aligned_alloc(64, kRing * sizeof(dp_slot));
+    memset(T.ring, 0, kRing * sizeof(dp_slot));
+    const char *pv = getenv("GAC_DP_PF"); /* (how far ahead the committer fetches slots) */
+    const int pf = pv && atoi(pv) > 0 && atoi(pv) < 64 ? atoi(pv) : 4;
     T.cq = malloc(kRing * sizeof(int32_t));
     T.ct = malloc(kRing * sizeof(int32_t));
     T.cqe = malloc(kRing * sizeof(int32_t));
@@ -1288,17 +1331,13 @@ static void pair_dp_team(ax_work *w, int nt, int k) {
         /* the update paths of the next searched leaves into this core's
          * cache while this one is settled */
         const uint64_t kp = __builtin_ia32_rdtsc();
-        if (started && i + 16 < w->nl) { /* (a searcher wrote it: fetch it early) */
-            const char *sx = (const char *)&T.ring[(i + 16) % kRing];
-            for (size_t o = 0; o < sizeof(dp_slot); o += 64)
-                __builtin_prefetch(sx + o, 0);
-        }
+        if (started && i + pf < w->nl) /* (a searcher wrote it: fetch it early) */
+            __builtin_prefetch(&T.ring[(i + pf) % kRing], 0);
         if (started && !T.applier && i + 8 < w->nl) {
             const dp_slot *nx = &T.ring[(i + 8) % kRing];
             if (atomic_load_explicit(&nx->ready, memory_order_acquire) == i + 9)
                 for (int32_t m = 0; m < nx->plen; ++m) {
-                    __builtin_prefetch(&w->nodes[nx->path[m]], 1);
-                    __builtin_prefetch(&w->nw[nx->path[m]], 1);
+                    __builtin_prefetch(&w->bnd[nx->path[m]], 1);
                 }
         }
         if (i + 8 < w->nl) {
@@ -1387,12 +1426,12 @@ static void pair_dp_team(ax_work *w, int nt, int k) {
         } else { /* the recorded path: the same nodes update_both visits */
             for (int32_t m = 0; m < plen; ++m) {
                 const int32_t b = sl->path[m];
-                if (w->nodes[b].max_score < total) {
-                    __atomic_store(&w->nodes[b].max_score, &total, __ATOMIC_RELAXED);
+                if (w->bnd[b].max_score < total) {
+                    __atomic_store(&w->bnd[b].max_score, &total, __ATOMIC_RELAXED);
                     ++nwrites;
                 }
-                if (w->nw[b] < v) {
-                    __atomic_store_n(&w->nw[b], v, __ATOMIC_RELAXED);
+                if (w->bnd[b].nw < v) {
+                    __atomic_store_n(&w->bnd[b].nw, v, __ATOMIC_RELAXED);
                     ++nwrites;
                 }
             }
@@ -1914,7 +1953,10 @@ int gac_chain_blocks(int32_t n, const int32_t *qs, const int32_t *qe, const int3
     free(w.lnode);
     free(w.qpos);
     free(w.tpos);
-    free(w.nw);
+    free(w.tbox);
+    free(w.qbox);
+    free(w.qtp);
+    free(w.bnd);
     free(w.xs);
     if (rc != GAC_OK) {
         gac_block_chains_free(r);
@@ -1965,7 +2007,10 @@ static void work_reserve(ax_work *w, int32_t n) {
     w->lnode = realloc(w->lnode, c * sizeof(int32_t));
     w->qpos = realloc(w->qpos, c * sizeof(int32_t));
     w->tpos = realloc(w->tpos, c * sizeof(int32_t));
-    w->nw = realloc(w->nw, 2 * c * sizeof(int64_t));
+    w->tbox = realloc(w->tbox, 4 * c * sizeof(int32_t));
+    w->qbox = realloc(w->qbox, 4 * c * sizeof(int32_t));
+    w->qtp = realloc(w->qtp, c * sizeof(int32_t));
+    w->bnd = realloc(w->bnd, 2 * c * sizeof(ax_bound));
     w->cap_n = c;
 }
 
@@ -2022,7 +2067,10 @@ static void work_free(ax_work *w) {
     free(w->lnode);
     free(w->qpos);
     free(w->tpos);
-    free(w->nw);
+    free(w->tbox);
+    free(w->qbox);
+    free(w->qtp);
+    free(w->bnd);
     free(w->xs);
 }
 
@@ -2460,7 +2508,11 @@ static int axt_dp_gpu(ax_job *J, int nt) {
         free(w->nodes);
         free(w->lnode);
         free(w->qpos);
-        free(w->nw);
+        free(w->tpos);
+        free(w->tbox);
+        free(w->qbox);
+        free(w->qtp);
+        free(w->bnd);
         free(w->xs);
     }
     free(G);
