@@ -22,6 +22,7 @@
  * chainBlock.c line by line (the sums are integral, so double is exact). */
 #define _GNU_SOURCE
 #include <pthread.h>
+#include <sched.h>
 #include <stdarg.h>
 #include <stdatomic.h>
 #include <stdint.h>
@@ -321,6 +322,7 @@ enum { kStack = 512 };
 static __thread struct {
     long long visits, prune1, prune2, leaves, cands, overlaps, xover_bases, updates, best_wins;
 } g_st;
+static __thread long long g_wr[8][2]; /* bound writes by depth / 4: max_score, linear */
 #define ST(x) (g_st.x++)
 #define STN(x, n) (g_st.x += (n))
 #else
@@ -1053,6 +1055,10 @@ static void update_both(ax_work *w, int32_t leaf) {
     const int32_t lq = w->qs[leaf], lt = w->ts[leaf];
     int32_t st_node[kStack];
     uint8_t st_dim[kStack];
+#ifdef GAC_DP_STATS
+    uint8_t st_dep[kStack];
+    st_dep[0] = 0;
+#endif
     int sp = 0;
     st_node[sp] = 0;
     st_dim[sp++] = 0;
@@ -1061,6 +1067,14 @@ static void update_both(ax_work *w, int32_t leaf) {
         const int32_t b = st_node[sp];
         const int dim = st_dim[sp];
         ax_node *nd = &w->nodes[b];
+#ifdef GAC_DP_STATS
+        const int dep = st_dep[sp];
+        if (w->bnd[b].max_score < total)
+            ++g_wr[dep / 4 < 7 ? dep / 4 : 7][0];
+        if (w->bnd[b].nw < v)
+            ++g_wr[dep / 4 < 7 ? dep / 4 : 7][1];
+        st_dep[sp] = st_dep[sp + 1] = (uint8_t)(dep + 1);
+#endif
         if (w->bnd[b].max_score < total)
             __atomic_store(&w->bnd[b].max_score, &total, __ATOMIC_RELAXED);
         if (w->bnd[b].nw < v)
@@ -1281,7 +1295,7 @@ static void pair_dp_team(ax_work *w, int nt, int k) {
     const char *lv = getenv("GAC_DP_LAG");
     T.lag = lv && atoi(lv) > 0 ? (atoi(lv) < kLagMax ? atoi(lv) : kLagMax) : 32; /* (<= 64: a mask) */
     const char *av = getenv("GAC_DP_APPLY");
-    T.applier = nt >= 4 && !(av && *av == '0');
+    T.applier = nt >= 4 && av && *av == '1'; /* (measured: in one L3 domain, slower) */
     const int nsw = nt - 1 - T.applier;
     const int ns = nsw > kRing - kLagMax ? kRing - kLagMax : nsw; /* searchers */
     T.tw = calloc((size_t)(ns > 0 ? ns : 1), sizeof(ax_work));
@@ -1503,6 +1517,10 @@ static void pair_dp_host(ax_work *w) {
                 "cands %.2f wins %.2f\n", g_st.visits / n, g_st.prune1 / n, g_st.prune2 / n,
                 g_st.leaves / n, g_st.cands / n, g_st.best_wins / n);
         memset(&g_st, 0, sizeof(g_st));
+        for (int d = 0; d < 8; ++d)
+            fprintf(stderr, "[dp stats] depth %2d-%2d: %.3f max-score writes, %.3f linear-bound "
+                    "writes per leaf\n", 4 * d, 4 * d + 3, g_wr[d][0] / n, g_wr[d][1] / n);
+        memset(g_wr, 0, sizeof(g_wr));
 #endif
         return;
     }
@@ -2078,12 +2096,69 @@ typedef struct team_run {
     ax_job *J;
     const ax_env *env;
     int32_t p;
-    int team, batch, started;
+    int team, batch, started, pin;
+    cpu_set_t cpus; /* (pin) the L3 domain the team runs in */
     pthread_t th;
 } team_run;
 
+/* the L3 domains (sysfs cache/index3/shared_cpu_list) of the CPUs this
+ * process may run on, in CPU order; 0 when sysfs does not say.  A team's
+ * threads pass every committed bound and search slot between them, so they
+ * share one L3 (an L3 line moves between cores in tens of ns, a line from
+ * another CCD or socket takes several times that) */
+typedef struct l3_dom {
+    cpu_set_t set;
+    int n;
+} l3_dom;
+
+static int l3_domains(l3_dom *d, int max) {
+    cpu_set_t ok;
+    if (sched_getaffinity(0, sizeof(ok), &ok) != 0)
+        return 0;
+    int nd = 0;
+    for (int c = 0; c < CPU_SETSIZE && nd < max; ++c) {
+        if (!CPU_ISSET(c, &ok))
+            continue;
+        int seen = 0;
+        for (int k = 0; k < nd && !seen; ++k)
+            seen = CPU_ISSET(c, &d[k].set);
+        if (seen)
+            continue;
+        char path[96], buf[1024];
+        snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", c);
+        FILE *f = fopen(path, "r");
+        if (!f)
+            return 0;
+        const int got = fgets(buf, sizeof(buf), f) != NULL;
+        fclose(f);
+        if (!got)
+            return 0;
+        CPU_ZERO(&d[nd].set);
+        for (char *q = buf; *q && *q != '\n';) { /* "a-b,c,..." */
+            char *e;
+            const long a = strtol(q, &e, 10);
+            long b = a;
+            if (e == q)
+                return 0;
+            if (*e == '-')
+                b = strtol(e + 1, &e, 10);
+            for (long x = a; x <= b && x < CPU_SETSIZE; ++x)
+                if (x >= 0 && CPU_ISSET((int)x, &ok))
+                    CPU_SET((int)x, &d[nd].set);
+            q = *e == ',' ? e + 1 : e;
+        }
+        if (!CPU_ISSET(c, &d[nd].set))
+            CPU_SET(c, &d[nd].set);
+        d[nd].n = CPU_COUNT(&d[nd].set);
+        ++nd;
+    }
+    return nd;
+}
+
 static void *team_runner(void *arg) {
     team_run *R = arg;
+    if (R->pin) /* (its searchers and applier inherit the mask) */
+        pthread_setaffinity_np(pthread_self(), sizeof(R->cpus), &R->cpus);
     ax_work w;
     memset(&w, 0, sizeof(w));
     w.e = R->env;
@@ -3033,7 +3108,9 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
         const int team_on = !(tv && *tv == '0') && nthreads > 2;
         const char *mv = getenv("GAC_DP_TEAM_MIN"); /* (tests: the size floor of a team pair) */
         const int64_t floor_ = mv && atoll(mv) > 0 ? atoll(mv) : (1 << 20);
-        const int64_t even = (3 * (nb / nthreads)) / 2;
+        const char *sv = getenv("GAC_DP_SHARE"); /* (a team pair: over this many even shares) */
+        const double mult = sv && atof(sv) > 0 ? atof(sv) : 1.5;
+        const int64_t even = (int64_t)(mult * (double)(nb / nthreads));
         const int64_t share = mv ? floor_ : (even > floor_ ? even : floor_);
         while (team_on && big < np && psize[order[big]] > share && big < nthreads / 2)
             ++big;
@@ -3043,9 +3120,21 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
             int64_t sum = 0;
             for (int64_t k = 0; k < big; ++k)
                 sum += psize[order[k]];
-            pool = nthreads / 3 > 1 ? nthreads / 3 : 1;
+            const char *pl = getenv("GAC_DP_POOL"); /* (threads beside the teams) */
+            pool = pl && atoi(pl) > 0 && atoi(pl) < nthreads ? atoi(pl)
+                                                             : (nthreads / 3 > 1 ? nthreads / 3 : 1);
             const int tt = nthreads - pool;
             int used = 0;
+            /* each team in an L3 domain of its own, from the one this
+             * thread runs in (GAC_DP_PIN=0: wherever the scheduler puts it) */
+            l3_dom dom[64];
+            const char *pv = getenv("GAC_DP_PIN");
+            const int nd = pv && *pv == '0' ? 0 : l3_domains(dom, 64);
+            int d0 = 0;
+            const int here = sched_getcpu();
+            for (int d = 0; d < nd; ++d)
+                if (here >= 0 && CPU_ISSET(here, &dom[d].set))
+                    d0 = d;
             for (int64_t k = 0; k < big; ++k) {
                 int t = (int)((double)tt * psize[order[k]] / (double)sum + 0.5);
                 t = t < 2 ? 2 : t;
@@ -3055,6 +3144,13 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
                 tr[k].J = &J;
                 tr[k].p = order[k];
                 tr[k].team = t;
+                if (nd >= 2 && k < nd && dom[(d0 + k) % nd].n >= t) {
+                    tr[k].pin = 1;
+                    tr[k].cpus = dom[(d0 + k) % nd].set;
+                }
+                if (getenv("GAC_TIMING"))
+                    fprintf(stderr, "[gac_axt_chain] team %lld: pair %d, %d threads, %s\n", (long long)k,
+                            order[k], t, tr[k].pin ? "in one L3 domain" : "unpinned");
                 const char *bv = getenv("GAC_DP_BATCH");
                 tr[k].batch = bv && atoi(bv) > 0 ? atoi(bv) : 2 * t;
                 tr[k].env = &env;

@@ -114,7 +114,7 @@ def test_axtchain_dp_modes_vs_golden(tool, seed, case, mode, tmp_path):
     opts = [o.replace("../../chrM", os.path.join(GOLDEN, "chrM")) for o in opts]
     env = dict(os.environ, GAC_THREADS="6")
     env.update({"reference-order": {"GAC_DP_FAST": "0"},
-                "team": {"GAC_DP_TEAM_MIN": "20", "GAC_DP_LAG": "16"},
+                "team": {"GAC_DP_TEAM_MIN": "20", "GAC_DP_LAG": "16", "GAC_DP_APPLY": "1"},
                 "team-lag1": {"GAC_DP_TEAM_MIN": "20", "GAC_DP_LAG": "1"},
                 "team-no-applier": {"GAC_DP_TEAM_MIN": "20", "GAC_DP_APPLY": "0"}}[mode])
     r = subprocess.run([tool] + opts + [os.path.join(d, inp), os.path.join(d, "t.2bit"),
@@ -144,7 +144,7 @@ def test_axtchain_team_dp_c4_shape(tool, tmp_path):
     else:
         subprocess.run([tool] + args + ["want.chain"], cwd=tmp_path, check=True, timeout=600,
                        capture_output=True, env=dict(os.environ, GAC_DP_FAST="0"))
-    env = dict(os.environ, GAC_THREADS="8", GAC_DP_TEAM_MIN="30000", GAC_TIMING="1")
+    env = dict(os.environ, GAC_THREADS="8", GAC_DP_TEAM_MIN="30000", GAC_TIMING="1", GAC_DP_APPLY="1")
     r = subprocess.run([tool] + args + ["team.chain"], cwd=tmp_path, capture_output=True, text=True,
                        timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
