@@ -280,6 +280,23 @@ static void partition(int32_t *a, int32_t n, const uint8_t *hit, int32_t *tmp) {
     memcpy(a, tmp, (size_t)n * sizeof(int32_t));
 }
 
+/* medianVal + splitList of one node (chainBlock.c:112-122, 92-110): the
+ * first half of the list in the cut dimension (D) is the lo side.  Hits are
+ * set on D directly (the same leaves as clearHits over Q), and only the other
+ * list is partitioned: D's own stable hit-first partition is the identity.
+ * Returns the cut. */
+static int32_t kd_split(ax_work *w, int32_t *Q, int32_t *T, int32_t n, int dim, int32_t *tmp) {
+    const int32_t half = n / 2;
+    const int32_t *D = dim == 0 ? Q : T;
+    for (int32_t i = 0; i < half; ++i)
+        w->hit[D[i]] = 1;
+    for (int32_t i = half; i < n; ++i)
+        w->hit[D[i]] = 0;
+    const int32_t ml = D[half - 1];
+    partition(dim == 0 ? T : Q, n, w->hit, tmp);
+    return dim == 0 ? w->qs[ml] : w->ts[ml];
+}
+
 /* kdBuild (chainBlock.c:124-164): Q in query order, T in target order */
 static int32_t kd_build(ax_work *w, int32_t *Q, int32_t *T, int32_t n, int dim) {
     const int32_t id = w->nn++;
@@ -292,15 +309,7 @@ static int32_t kd_build(ax_work *w, int32_t *Q, int32_t *T, int32_t n, int dim) 
         return id;
     }
     const int32_t half = n / 2;
-    for (int32_t i = 0; i < n; ++i) /* clearHits(lists[0]) */
-        w->hit[Q[i]] = 0;
-    const int32_t *D = dim == 0 ? Q : T; /* medianVal: first n/2 marked */
-    for (int32_t i = 0; i < half; ++i)
-        w->hit[D[i]] = 1;
-    const int32_t ml = D[half - 1];
-    const int32_t cut = dim == 0 ? w->qs[ml] : w->ts[ml];
-    partition(Q, n, w->hit, w->tmp);
-    partition(T, n, w->hit, w->tmp);
+    const int32_t cut = kd_split(w, Q, T, n, dim, w->tmp);
     /* hi first: nodes land in the DFS's usual visiting order (pre-order,
      * hi before lo), so a search walks memory forward */
     const int32_t hi = kd_build(w, Q + half, T + half, n - half, 1 - dim);
@@ -634,6 +643,93 @@ static int dkey_cmp_desc(const void *a, const void *b) {
 /* ---- chain post-processing on a block list (linked by next[]) ---- */
 _Static_assert(sizeof(ikey) == 16 && sizeof(dkey) == 16, "par_sort16 keys");
 
+/* ---- a stable parallel LSD radix sort of 16-byte records by their first 8
+ * bytes as an unsigned key.  Where the records go in input (rank) order,
+ * stable by key is the (key, rank) order of the comparator sorts.  Per pass
+ * every thread counts the digits of its own slice; one prefix over (digit,
+ * slice) makes the scatter stable; passes only over the key bits in use. */
+enum { kRadixBits = 10, kRadix = 1 << kRadixBits };
+
+typedef struct rsort {
+    uint8_t *src, *dst;
+    int64_t n;
+    int nt, shift;
+    int64_t *cnt; /* [nt][kRadix] */
+    _Atomic int next;
+} rsort;
+
+static inline uint64_t rs_key(const uint8_t *r) {
+    uint64_t k;
+    memcpy(&k, r, 8);
+    return k;
+}
+
+static void *rs_count(void *arg) {
+    rsort *R = arg;
+    for (int c; (c = atomic_fetch_add(&R->next, 1)) < R->nt;) {
+        const int64_t lo = R->n * c / R->nt, hi = R->n * (c + 1) / R->nt;
+        int64_t *h = R->cnt + (size_t)c * kRadix;
+        memset(h, 0, kRadix * sizeof(int64_t));
+        for (int64_t i = lo; i < hi; ++i)
+            ++h[(rs_key(R->src + 16 * i) >> R->shift) & (kRadix - 1)];
+    }
+    return NULL;
+}
+
+static void *rs_scatter(void *arg) {
+    rsort *R = arg;
+    for (int c; (c = atomic_fetch_add(&R->next, 1)) < R->nt;) {
+        const int64_t lo = R->n * c / R->nt, hi = R->n * (c + 1) / R->nt;
+        int64_t *h = R->cnt + (size_t)c * kRadix; /* (the slice's output offsets) */
+        for (int64_t i = lo; i < hi; ++i) {
+            const uint8_t *r = R->src + 16 * i;
+            memcpy(R->dst + 16 * h[(rs_key(r) >> R->shift) & (kRadix - 1)]++, r, 16);
+        }
+    }
+    return NULL;
+}
+
+static int radix_sort16(void *a, int64_t n, int nt) { /* -1, unsorted: a key < 0 as int64 */
+    uint64_t any = 0;
+    for (int64_t i = 0; i < n; ++i)
+        any |= rs_key((const uint8_t *)a + 16 * i);
+    if (any >> 63)
+        return -1;
+    if (n < 2 || any == 0)
+        return 0;
+    const int bits = 64 - __builtin_clzll(any);
+    if (nt < 1 || n < (1 << 16))
+        nt = 1;
+    rsort R;
+    R.src = a;
+    R.dst = malloc((size_t)n * 16);
+    R.n = n;
+    R.nt = nt;
+    R.cnt = malloc((size_t)nt * kRadix * sizeof(int64_t));
+    uint8_t *const tmp = R.dst;
+    for (R.shift = 0; R.shift < bits; R.shift += kRadixBits) {
+        atomic_init(&R.next, 0);
+        gac_run_threads(nt, rs_count, &R);
+        int64_t off = 0;
+        for (int d = 0; d < kRadix; ++d)
+            for (int c = 0; c < nt; ++c) {
+                const int64_t t = R.cnt[(size_t)c * kRadix + d];
+                R.cnt[(size_t)c * kRadix + d] = off;
+                off += t;
+            }
+        atomic_init(&R.next, 0);
+        gac_run_threads(nt, rs_scatter, &R);
+        uint8_t *t = R.src;
+        R.src = R.dst;
+        R.dst = t;
+    }
+    if (R.src != (uint8_t *)a)
+        memcpy(a, R.src, (size_t)n * 16);
+    free(tmp);
+    free(R.cnt);
+    return 0;
+}
+
 /* a stable parallel merge sort of 16-byte keys (ikey, dkey: their
  * comparators end on a rank, so the order is total): runs sorted by qsort
  * on every thread, then merged in rounds */
@@ -709,6 +805,34 @@ static void par_sort16(void *a, int64_t n, int (*cmp)(const void *, const void *
     }
     free(J.tmp);
     free(J.cut);
+}
+
+/* dkey_cmp_desc's order for keys whose ranks are their input positions:
+ * scores are integral (sums of integer block scores and gap costs), so
+ * (max - k) is an exact unsigned key for radix_sort16 (stable: ties stay in
+ * rank order); other keys take the comparator sort */
+static void sort_desc16(dkey *k, int64_t n, int nt) {
+    double mx = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const double x = k[i].k;
+        if (!(x > -4.0e15 && x < 4.0e15) || (double)(int64_t)x != x) {
+            par_sort16(k, n, dkey_cmp_desc, nt);
+            return;
+        }
+        if (i == 0 || x > mx)
+            mx = x;
+    }
+    const int64_t m = (int64_t)mx;
+    for (int64_t i = 0; i < n; ++i) {
+        const uint64_t u = (uint64_t)(m - (int64_t)k[i].k);
+        memcpy(&k[i].k, &u, 8);
+    }
+    radix_sort16(k, n, nt);
+    for (int64_t i = 0; i < n; ++i) {
+        uint64_t u;
+        memcpy(&u, &k[i].k, 8);
+        k[i].k = (double)(m - (int64_t)u);
+    }
 }
 
 typedef struct ax_cb {
@@ -858,12 +982,15 @@ static int32_t pair_leaves(ax_work *w) {
         return 0;
     }
     const int nt = w->team > 1 ? w->team : 1; /* (large pairs: every thread) */
-    par_sort16(k, nl, ikey_cmp, nt);
+    /* (ranks in input order: stable by key is the (k, rank) order) */
+    if (radix_sort16(k, nl, nt) != 0)
+        par_sort16(k, nl, ikey_cmp, nt);
     for (int32_t i = 0; i < nl; ++i)
         w->tord[i] = k[i].v;
     for (int32_t i = 0; i < nl; ++i)
         k[i] = (ikey){w->qs[w->tord[i]], i, w->tord[i]};
-    par_sort16(k, nl, ikey_cmp, nt);
+    if (radix_sort16(k, nl, nt) != 0)
+        par_sort16(k, nl, ikey_cmp, nt);
     for (int32_t i = 0; i < nl; ++i)
         w->qord[i] = k[i].v;
     free(k);
@@ -888,15 +1015,7 @@ static void kd_build_at(ax_work *w, int32_t *Q, int32_t *T, int32_t n, int dim, 
         return;
     }
     const int32_t half = n / 2;
-    for (int32_t i = 0; i < n; ++i)
-        w->hit[Q[i]] = 0;
-    const int32_t *D = dim == 0 ? Q : T;
-    for (int32_t i = 0; i < half; ++i)
-        w->hit[D[i]] = 1;
-    const int32_t ml = D[half - 1];
-    const int32_t cut = dim == 0 ? w->qs[ml] : w->ts[ml];
-    partition(Q, n, w->hit, tmp);
-    partition(T, n, w->hit, tmp);
+    const int32_t cut = kd_split(w, Q, T, n, dim, tmp);
     const int32_t hi = id + 1, lo = id + 2 * (n - half);
     kd_build_at(w, Q + half, T + half, n - half, 1 - dim, hi, tmp + half);
     kd_build_at(w, Q, T, half, 1 - dim, lo, tmp);
@@ -934,25 +1053,89 @@ static void *kd_thread(void *arg) {
     }
 }
 
+/* kd_split of a large node on nt threads: the hits set by slices of D, the
+ * other list's stable partition by slice counts (hits of earlier slices,
+ * then all hits, then the misses of earlier slices) */
+typedef struct ksplit {
+    ax_work *w;
+    const int32_t *D;
+    int32_t *O, *tmp;
+    int32_t n, half;
+    int nt, phase;
+    int32_t *nhit; /* [nt + 1]: hits per slice, then their exclusive prefix */
+    _Atomic int next;
+} ksplit;
+
+static void *ksplit_thread(void *arg) {
+    ksplit *K = arg;
+    for (int c; (c = atomic_fetch_add(&K->next, 1)) < K->nt;) {
+        const int32_t lo = (int32_t)((int64_t)K->n * c / K->nt);
+        const int32_t hi = (int32_t)((int64_t)K->n * (c + 1) / K->nt);
+        uint8_t *hit = K->w->hit;
+        if (K->phase == 0) {
+            for (int32_t i = lo; i < hi; ++i)
+                hit[K->D[i]] = i < K->half;
+        } else if (K->phase == 1) {
+            int32_t h = 0;
+            for (int32_t i = lo; i < hi; ++i)
+                h += hit[K->O[i]];
+            K->nhit[c] = h;
+        } else if (K->phase == 2) {
+            int32_t a = K->nhit[c], b = K->half + (lo - K->nhit[c]);
+            for (int32_t i = lo; i < hi; ++i) {
+                const int32_t x = K->O[i];
+                if (hit[x])
+                    K->tmp[a++] = x;
+                else
+                    K->tmp[b++] = x;
+            }
+        } else {
+            memcpy(K->O + lo, K->tmp + lo, (size_t)(hi - lo) * sizeof(int32_t));
+        }
+    }
+    return NULL;
+}
+
+static int32_t kd_split_par(ax_work *w, int32_t *Q, int32_t *T, int32_t n, int dim, int32_t *tmp,
+                            int nt) {
+    ksplit K;
+    K.w = w;
+    K.D = dim == 0 ? Q : T;
+    K.O = dim == 0 ? T : Q;
+    K.tmp = tmp;
+    K.n = n;
+    K.half = n / 2;
+    K.nt = nt;
+    K.nhit = malloc((size_t)(nt + 1) * sizeof(int32_t));
+    for (K.phase = 0; K.phase < 4; ++K.phase) {
+        if (K.phase == 2) { /* exclusive prefix of the hit counts (they sum to half) */
+            int32_t run = 0;
+            for (int c = 0; c < nt; ++c) {
+                const int32_t h = K.nhit[c];
+                K.nhit[c] = run;
+                run += h;
+            }
+        }
+        atomic_init(&K.next, 0);
+        gac_run_threads(nt, ksplit_thread, &K);
+    }
+    free(K.nhit);
+    const int32_t ml = K.D[K.half - 1];
+    return dim == 0 ? w->qs[ml] : w->ts[ml];
+}
+
 /* the top `depth` levels on this thread (cuts and partitions), the
  * subtrees below them as tasks; *top collects the top nodes' ids */
 static void kd_top(ax_work *w, int32_t *Q, int32_t *T, int32_t n, int dim, int32_t id,
                    int32_t *tmp, int depth, kd_task *tasks, int32_t *ntask, int32_t *top,
-                   int32_t *ntop) {
+                   int32_t *ntop, int nt) {
     if (depth == 0 || n < 2) {
         tasks[(*ntask)++] = (kd_task){Q, T, tmp, n, id, dim};
         return;
     }
     const int32_t half = n / 2;
-    for (int32_t i = 0; i < n; ++i)
-        w->hit[Q[i]] = 0;
-    const int32_t *D = dim == 0 ? Q : T;
-    for (int32_t i = 0; i < half; ++i)
-        w->hit[D[i]] = 1;
-    const int32_t ml = D[half - 1];
-    const int32_t cut = dim == 0 ? w->qs[ml] : w->ts[ml];
-    partition(Q, n, w->hit, tmp);
-    partition(T, n, w->hit, tmp);
+    const int32_t cut = n >= (1 << 18) && nt > 1 ? kd_split_par(w, Q, T, n, dim, tmp, nt)
+                                               : kd_split(w, Q, T, n, dim, tmp);
     const int32_t hi = id + 1, lo = id + 2 * (n - half);
     ax_node *nd = &w->nodes[id];
     nd->lo = lo;
@@ -962,8 +1145,8 @@ static void kd_top(ax_work *w, int32_t *Q, int32_t *T, int32_t n, int dim, int32
     w->bnd[id] = (ax_bound){0.0, INT64_MIN / 4};
     top[(*ntop)++] = id;
     kd_top(w, Q + half, T + half, n - half, 1 - dim, hi, tmp + half, depth - 1, tasks, ntask, top,
-           ntop);
-    kd_top(w, Q, T, half, 1 - dim, lo, tmp, depth - 1, tasks, ntask, top, ntop);
+           ntop, nt);
+    kd_top(w, Q, T, half, 1 - dim, lo, tmp, depth - 1, tasks, ntask, top, ntop, nt);
 }
 
 /* kdTreeMake (chainBlock.c:166-205); the tree is built from copies: kd_build
@@ -981,7 +1164,7 @@ static void pair_tree(ax_work *w) {
             ++depth;
         kd_task *tasks = malloc(sizeof(kd_task) << depth);
         int32_t *top = malloc(sizeof(int32_t) << depth), ntask = 0, ntop = 0;
-        kd_top(w, Q, T, nl, 0, 0, w->tmp, depth, tasks, &ntask, top, &ntop);
+        kd_top(w, Q, T, nl, 0, 0, w->tmp, depth, tasks, &ntask, top, &ntop, w->team);
         kd_job J = {w, tasks, ntask, 0};
         gac_run_threads(w->team < ntask ? w->team : ntask, kd_thread, &J);
         for (int32_t k = ntop - 1; k >= 0; --k) { /* children before parents */
@@ -1617,7 +1800,7 @@ static void pair_peel(ax_work *w, const ax_pairinfo *pi, FILE *details, ax_chain
     dkey *dk = malloc((size_t)nl * sizeof(dkey));
     for (int32_t i = 0; i < nl; ++i)
         dk[i] = (dkey){w->total[w->tord[i]], i, w->tord[i]};
-    par_sort16(dk, nl, dkey_cmp_desc, w->team > 1 ? w->team : 1);
+    sort_desc16(dk, nl, w->team > 1 ? w->team : 1);
     for (int32_t i = 0; i < nb; ++i)
         w->hit[i] = 0;
     int32_t *cblk = malloc((size_t)nl * sizeof(int32_t));
@@ -1808,7 +1991,7 @@ static void pair_finish_team(ax_work *w, ax_chains *pc, ax_out *out) {
     F.phase = 0;
     gac_run_threads(nt, fin_thread, &F);
     if (F.err_at < 0) {
-        par_sort16(F.ck, nc, dkey_cmp_desc, nt);
+        sort_desc16(F.ck, nc, nt);
         F.cb = malloc((size_t)(nbk ? nbk : 1) * sizeof(ax_cb));
         F.head = malloc((size_t)(nc ? nc : 1) * sizeof(int32_t));
         F.cnt = malloc((size_t)(nc ? nc : 1) * sizeof(int32_t));
@@ -2694,6 +2877,26 @@ static void par_sort_bkey(bkey *a, int64_t n, int nt) {
     free(J.cut);
 }
 
+/* removeExactOverlaps' 16-byte sort record: (qStart, tStart) as one key,
+ * the block's rank and size; NULL when a start is negative (the comparator
+ * sort then) */
+typedef struct fkey {
+    uint64_t k; /* qStart << 32 | tStart */
+    int32_t rank, size;
+} fkey;
+_Static_assert(sizeof(fkey) == 16, "radix_sort16 record");
+
+static fkey *fold_keys(const gac_axt_input *in, int64_t a, int64_t b, fkey *k, int nt) {
+    for (int64_t i = a; i < b; ++i) {
+        if (in->blk_q[i] < 0 || in->blk_t[i] < 0)
+            return NULL;
+        k[i - a] = (fkey){(uint64_t)in->blk_q[i] << 32 | (uint32_t)in->blk_t[i], (int32_t)(i - a),
+                          in->blk_size[i]};
+    }
+    radix_sort16(k, b - a, nt);
+    return k;
+}
+
 /* removeExactOverlaps' fold of one pair's sorted keys into its input slot */
 static int64_t fold_sorted(fold_job *F, const bkey *k, int64_t a, int64_t m) {
     int64_t n = a;
@@ -2709,6 +2912,27 @@ static int64_t fold_sorted(fold_job *F, const bkey *k, int64_t a, int64_t m) {
         F->qe[n] = k[i].qe;
         F->ts[n] = k[i].ts;
         F->te[n] = k[i].te;
+        ++n;
+    }
+    return n - a;
+}
+
+static int64_t fold_sorted_f(fold_job *F, const fkey *k, int64_t a, int64_t m) {
+    int64_t n = a;
+    for (int64_t i = 0; i < m; ++i) {
+        const int32_t q = (int32_t)(k[i].k >> 32), t = (int32_t)(uint32_t)k[i].k;
+        const int32_t qe = q + k[i].size, te = t + k[i].size;
+        if (n > a && q == F->qs[n - 1] && t == F->ts[n - 1]) {
+            if (F->qe[n - 1] < qe)
+                F->qe[n - 1] = qe;
+            if (F->te[n - 1] < te)
+                F->te[n - 1] = te;
+            continue;
+        }
+        F->qs[n] = q;
+        F->qe[n] = qe;
+        F->ts[n] = t;
+        F->te[n] = te;
         ++n;
     }
     return n - a;
@@ -2731,6 +2955,13 @@ static void *fold_thread(void *arg) {
         if (b - a > kcap) {
             kcap = b - a;
             k = realloc(k, (size_t)kcap * sizeof(bkey));
+        }
+        if (b - a >= 4096) { /* (radix: fkey fits in a bkey's room) */
+            const fkey *f = fold_keys(in, a, b, (fkey *)k, 1);
+            if (f) {
+                F->poff[p + 1] = fold_sorted_f(F, f, a, b - a);
+                continue;
+            }
         }
         for (int64_t i = a; i < b; ++i)
             k[i - a] = (bkey){in->blk_q[i], in->blk_t[i], (int32_t)(i - a),
@@ -2967,6 +3198,12 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
                 if (b - a <= F.big)
                     continue;
                 bkey *k = malloc((size_t)(b - a) * sizeof(bkey));
+                const fkey *f = fold_keys(in, a, b, (fkey *)k, nthreads);
+                if (f) {
+                    poff[p + 1] = fold_sorted_f(&F, f, a, b - a);
+                    free(k);
+                    continue;
+                }
                 for (int64_t i = a; i < b; ++i)
                     k[i - a] = (bkey){in->blk_q[i], in->blk_t[i], (int32_t)(i - a),
                                       in->blk_q[i] + in->blk_size[i], in->blk_t[i] + in->blk_size[i]};

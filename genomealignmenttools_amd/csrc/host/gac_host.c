@@ -760,10 +760,12 @@ void gac_run_threads(int n, void *(*fn)(void *), void *arg) {
     if (n < 1)
         n = 1;
     pthread_t *th = malloc((size_t)n * sizeof(pthread_t));
-    for (int i = 1; i < n; ++i)
-        pthread_create(&th[i], NULL, fn, arg);
+    int started = 1; /* (callers claim work from a shared counter, so fewer threads still finish it) */
+    for (int i = 1; i < n && th; ++i, ++started)
+        if (pthread_create(&th[i], NULL, fn, arg) != 0)
+            break;
     fn(arg);
-    for (int i = 1; i < n; ++i)
+    for (int i = 1; i < started; ++i)
         pthread_join(th[i], NULL);
     free(th);
 }
