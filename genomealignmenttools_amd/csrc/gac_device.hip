@@ -51,7 +51,7 @@ hipError_t launch_gap_table(const GapDev &g, const int32_t *small, int len, int3
 hipError_t launch_nruns(const NPiece *p, int64_t n, uint32_t *nmask, hipStream_t s);
 hipError_t launch_build_flat(const int32_t *bt, const int32_t *bq, const int32_t *bs, int64_t nb,
                              const DChain *chains, int64_t n_chains, int32_t *coff,
-                             int32_t *tile_c0, uint8_t *cflag, const longlong2 *t_runs,
+                             int32_t *tile_c0, int4 *crun, const longlong2 *t_runs,
                              int64_t n_trun, const longlong2 *q_runs, int64_t n_qrun,
                              const int64_t *q_woff, int4 *blk, int2 *tspan, uint32_t *bucket,
                              hipStream_t s);
@@ -237,10 +237,11 @@ struct gac_chainset {
     int32_t *d_stage = nullptr;  // the caller's block arrays, staged (3 x blocks)
     size_t cap_stage = 0;
     // flat (lane per block) kernels: compact chain offsets [n + 1], the chain
-    // of every 64-block tile's first block [tiles + 1], per-chain N flags
+    // of every 64-block tile's first block [tiles + 1], per-chain N-run
+    // ranges {t first, t end, q first, q end} (empty: no run in its span)
     int32_t *d_coff = nullptr, *d_tile_c0 = nullptr;
-    uint8_t *d_cflag = nullptr;
-    size_t cap_coff = 0, cap_tile_c0 = 0, cap_cflag = 0;
+    int4 *d_crun = nullptr;
+    size_t cap_coff = 0, cap_tile_c0 = 0, cap_crun = 0;
 };
 
 static void free_whole_plan(gac_chainset *cs) {
@@ -1493,10 +1494,10 @@ static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs)
     if (e == hipSuccess)
         e = ensure_buf((void **)&cs->d_tile_c0, &cs->cap_tile_c0, (size_t)(ntiles + 1), sizeof(int32_t));
     if (e == hipSuccess)
-        e = ensure_buf((void **)&cs->d_cflag, &cs->cap_cflag, (size_t)(n ? n : 1), 1);
+        e = ensure_buf((void **)&cs->d_crun, &cs->cap_crun, (size_t)(n ? n : 1), sizeof(int4));
     if (e == hipSuccess && rc == GAC_OK)
         e = launch_build_flat(d_bt, d_bt + nb, d_bt + 2 * nb, (int64_t)nb, cs->chains, n, cs->d_coff,
-                              cs->d_tile_c0, cs->d_cflag, c->g[0].d_nrun, c->g[0].n_nrun,
+                              cs->d_tile_c0, cs->d_crun, c->g[0].d_nrun, c->g[0].n_nrun,
                               c->g[1].d_nrun, c->g[1].n_nrun, c->g[1].d_woff, cs->blk, cs->tspan,
                               cs->bucket, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -1536,7 +1537,7 @@ extern "C" int gac_chains_reupload(gac_ctx *c, const gac_chainset_desc *d, gac_c
 static void free_set_memory(gac_chainset *cs) {
     hipSetDevice(cs->ctx->device);  // (hipFree waits for work still using them)
     void *bufs[] = {cs->chains, cs->blk,     cs->blk12,     cs->tspan,  cs->bucket,
-                    cs->d_stage, cs->d_coff, cs->d_tile_c0, cs->d_cflag};
+                    cs->d_stage, cs->d_coff, cs->d_tile_c0, cs->d_crun};
     for (void *p : bufs)
         if (p) hipFree(p);
     cs->chains = nullptr;
@@ -1546,7 +1547,7 @@ static void free_set_memory(gac_chainset *cs) {
     cs->bucket = nullptr;
     cs->d_stage = nullptr;
     cs->d_coff = cs->d_tile_c0 = nullptr;
-    cs->d_cflag = nullptr;
+    cs->d_crun = nullptr;
     free_whole_plan(cs);
 }
 

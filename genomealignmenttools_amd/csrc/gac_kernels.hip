@@ -246,15 +246,36 @@ __device__ __forceinline__ int wave_incl_sum(int v, int lane) {
 // (k_chain_prep: its target and query spans against the sorted global N
 // runs); only the blocks of chains whose span meets a run are checked,
 // against the same runs (k_build_flat).
-// does [lo, hi) meet one of the sorted, disjoint runs {start, end}?
-__device__ __forceinline__ bool span_meets(const longlong2 *runs, int64_t n, int64_t lo, int64_t hi) {
+// does [lo, hi) meet one of the sorted, disjoint runs [a, b) {start, end}?
+__device__ __forceinline__ bool span_meets(const longlong2 *runs, int64_t a, int64_t b, int64_t lo,
+                                           int64_t hi) {
+    const int64_t n = b;
+    while (a < b) {  // first run ending past lo
+        const int64_t m = (a + b) >> 1;
+        if (runs[m].y > lo) b = m;
+        else a = m + 1;
+    }
+    return a < n && runs[a].x < hi;
+}
+
+// the runs of the sorted, disjoint list that meet [lo, hi): [*a, *b), empty
+// when none does
+__device__ __forceinline__ void runs_in(const longlong2 *runs, int64_t n, int64_t lo, int64_t hi,
+                                        int32_t *ra, int32_t *rb) {
     int64_t a = 0, b = n;  // first run ending past lo
     while (a < b) {
         const int64_t m = (a + b) >> 1;
         if (runs[m].y > lo) b = m;
         else a = m + 1;
     }
-    return a < n && runs[a].x < hi;
+    int64_t e = a, f = n;  // first run starting at or after hi
+    while (e < f) {
+        const int64_t m = (e + f) >> 1;
+        if (runs[m].x >= hi) f = m;
+        else e = m + 1;
+    }
+    *ra = (int32_t)a;
+    *rb = (int32_t)(e > a ? e : a);
 }
 
 // ------------------------------------------------------------ flat upload
@@ -266,7 +287,8 @@ __device__ __forceinline__ bool span_meets(const longlong2 *runs, int64_t n, int
 // before b" picks the non-empty one.
 __device__ __forceinline__ int64_t owner_chain(const int32_t *coff, const int32_t *tile_c0,
                                                int64_t ntiles, int64_t b) {
-    const int64_t t = b >> 6;
+    // (a wave's 64 lanes are one tile: its bounds are wave-uniform loads)
+    const int64_t t = __builtin_amdgcn_readfirstlane((int)(b >> 6));
     int64_t lo = tile_c0[t], hi = tile_c0[t + 1 < ntiles ? t + 1 : ntiles];
     while (lo < hi) {  // last c in [lo, hi] with coff[c] <= b
         const int64_t mid = (lo + hi + 1) >> 1;
@@ -276,14 +298,51 @@ __device__ __forceinline__ int64_t owner_chain(const int32_t *coff, const int32_
     return lo;
 }
 
-// one lane per chain: compact offsets, the bucket terminator, and whether the
-// chain's target / query span meets an N run (cflag bit 0 / 1)
+// The chains of a workgroup's kUpPer x 256 blocks (4 kUpPer tiles), staged in LDS
+// with one coalesced load each: chains tile_c0[t0] .. tile_c0[t0 + 4 kUpPer],
+// their compact offsets (and the next chain's), so a lane finds its block's
+// chain by a search in LDS instead of dependent global loads.  A workgroup
+// over more than kStage chains (a run of empty chains) returns false: its
+// lanes take owner_chain's global search.  Each lane takes kUpPer blocks, so
+// the staging round trip is paid once per 4 kUpPer tiles.
+constexpr int kStage = 256, kUpPer = 2;
+struct ChainStage {
+    int32_t c0, m;  // (every lane's own copy: workgroup-uniform values)
+    int32_t *off;   // [m + 1] in LDS
+};
+
+__device__ __forceinline__ bool stage_offsets(const int32_t *coff, const int32_t *tile_c0,
+                                              int64_t ntiles, int64_t B0, int32_t *lds_off,
+                                              ChainStage &S) {
+    const int64_t t0 = B0 >> 6, t1 = t0 + 4 * kUpPer < ntiles ? t0 + 4 * kUpPer : ntiles;
+    S.c0 = tile_c0[t0];
+    S.m = tile_c0[t1] - S.c0 + 1;
+    S.off = lds_off;
+    if (S.m > kStage) return false;
+    for (int j = threadIdx.x; j <= S.m; j += blockDim.x) lds_off[j] = coff[S.c0 + j];  // (coff[c1 + 1] exists)
+    return true;
+}
+
+// the staged chain holding block b: last j with off[j] <= b (an empty chain
+// shares its offset with the next, which is then the one taken)
+__device__ __forceinline__ int staged_chain(const ChainStage &S, int64_t b) {
+    int lo = 0, hi = S.m - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (S.off[mid] <= b) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// one lane per chain: compact offsets, the bucket terminator, and the N runs
+// its target / query span meets (crun: {t first, t end, q first, q end})
 __global__ void __launch_bounds__(256) k_chain_prep(const DChain *chains, int64_t n_chains,
                                                     int64_t nb, const int32_t *bq,
                                                     const int32_t *bs, const longlong2 *t_runs,
                                                     int64_t n_trun, const longlong2 *q_runs,
                                                     int64_t n_qrun, const int64_t *q_woff,
-                                                    int32_t *coff, uint8_t *cflag,
+                                                    int32_t *coff, int4 *crun,
                                                     uint32_t *bucket) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_chains) return;
@@ -293,19 +352,18 @@ __global__ void __launch_bounds__(256) k_chain_prep(const DChain *chains, int64_
     const int64_t span = (int64_t)ch.tend - ch.tstart;
     const int64_t nbk = span > 0 ? ((span - 1) >> ch.shift) + 1 : 0;
     bucket[ch.idx_off + nbk] = (uint32_t)ch.nblk;
-    uint8_t f = 0;
+    int4 r = make_int4(0, 0, 0, 0);
     if (ch.nblk > 0) {
-        if (n_trun && span_meets(t_runs, n_trun, ch.tbase + ch.tstart, ch.tbase + ch.tend)) f |= 1;
+        if (n_trun) runs_in(t_runs, n_trun, ch.tbase + ch.tstart, ch.tbase + ch.tend, &r.x, &r.y);
         if (n_qrun) {
             const int64_t l = ch.blk_off + ch.nblk - 1;
             const int64_t qs = bq[ch.blk_off], qe = (int64_t)bq[l] + bs[l];
             const int64_t qsize = ch.qinfo & 0x7fffffff, qb = q_woff[ch.q_seq] * 32;
-            const bool q = ch.qinfo < 0 ? span_meets(q_runs, n_qrun, qb + qsize - qe, qb + qsize - qs)
-                                        : span_meets(q_runs, n_qrun, qb + qs, qb + qe);
-            if (q) f |= 2;
+            if (ch.qinfo < 0) runs_in(q_runs, n_qrun, qb + qsize - qe, qb + qsize - qs, &r.z, &r.w);
+            else runs_in(q_runs, n_qrun, qb + qs, qb + qe, &r.z, &r.w);
         }
     }
-    cflag[c] = f;
+    crun[c] = r;
 }
 
 // one lane per 64-block tile: the chain holding its first block
@@ -336,42 +394,86 @@ __global__ void __launch_bounds__(256) k_build_flat(const int32_t *bt, const int
                                                     const int32_t *bs, int64_t nb,
                                                     const DChain *chains, const int32_t *coff,
                                                     const int32_t *tile_c0, int64_t ntiles,
-                                                    const uint8_t *cflag, const longlong2 *t_runs,
+                                                    const int4 *crun, const longlong2 *t_runs,
                                                     int64_t n_trun, const longlong2 *q_runs,
                                                     int64_t n_qrun, const int64_t *q_woff,
                                                     int4 *blk, int2 *tspan, uint32_t *bucket) {
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= nb) {
-        if (b < nb + 8) {  // padding: a window search may read 8 past a chain
-            tspan[b] = make_int2(0x7fffffff, 0x7fffffff);
-            blk[b] = make_int4(0x7fffffff, 0, 0, 0);
-        }
-        return;
+    __shared__ int32_t s_off[kStage + 1];
+    __shared__ int64_t s_tbase[kStage], s_idx[kStage];
+    __shared__ int32_t s_ts[kStage], s_te[kStage], s_sh[kStage], s_qseq[kStage], s_qinfo[kStage];
+    __shared__ int4 s_run[kStage];
+    const int64_t B0 = (int64_t)blockIdx.x * blockDim.x * kUpPer;
+    int t[kUpPer], q[kUpPer], z[kUpPer];
+#pragma unroll
+    for (int i = 0; i < kUpPer; ++i) {  // (issued before the staging waits)
+        const int64_t b = B0 + i * (int64_t)blockDim.x + threadIdx.x;
+        t[i] = q[i] = z[i] = 0;
+        if (b < nb) t[i] = bt[b], q[i] = bq[b], z[i] = bs[b];
     }
-    const int64_t c = owner_chain(coff, tile_c0, ntiles, b);
-    const DChain ch = chains[c];
-    const int t = bt[b], q = bq[b], z = bs[b];
-    int flags = 0;
-    const uint8_t f = cflag ? cflag[c] : 0;
-    if (f && z > 0) {
-        if ((f & 1) && span_meets(t_runs, n_trun, ch.tbase + t, ch.tbase + t + z)) flags |= kTHasN;
-        if (f & 2) {
-            const int64_t qb = q_woff[ch.q_seq] * 32;
-            const int64_t qf = ch.qinfo < 0 ? (int64_t)(ch.qinfo & 0x7fffffff) - q - z : q;
-            if (span_meets(q_runs, n_qrun, qb + qf, qb + qf + z)) flags |= kQHasN;
+    ChainStage S;
+    const bool staged = B0 < nb && stage_offsets(coff, tile_c0, ntiles, B0, s_off, S);
+    if (staged) {  // the chain fields the blocks need, one chain per lane
+        const int c0 = S.c0;
+        for (int j = threadIdx.x; j < S.m; j += blockDim.x) {
+            const DChain ch = chains[c0 + j];
+            s_tbase[j] = ch.tbase;
+            s_idx[j] = ch.idx_off;
+            s_ts[j] = ch.tstart;
+            s_te[j] = ch.tend;
+            s_sh[j] = ch.shift;
+            s_qseq[j] = ch.q_seq;
+            s_qinfo[j] = ch.qinfo;
+            s_run[j] = crun ? crun[c0 + j] : make_int4(0, 0, 0, 0);
         }
     }
-    blk[b] = make_int4(t, q, z | flags, 0);
-    tspan[b] = make_int2(t, t + z);
-    const int64_t k = b - coff[c];
-    const int64_t span = (int64_t)ch.tend - ch.tstart;
-    const int64_t nbk = span > 0 ? ((span - 1) >> ch.shift) + 1 : 0;
-    const int64_t round = ((int64_t)1 << ch.shift) - 1;
-    const int64_t k0 = k ? ((int64_t)bt[b - 1] + bs[b - 1] - ch.tstart + round) >> ch.shift : 0;
-    int64_t k1 = ((int64_t)t + z - ch.tstart + round) >> ch.shift;
-    if (k1 > nbk) k1 = nbk;
-    uint32_t *bk = bucket + ch.idx_off;
-    for (int64_t j = k0; j < k1; ++j) bk[j] = (uint32_t)k;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kUpPer; ++i) {
+        const int64_t b = B0 + i * (int64_t)blockDim.x + threadIdx.x;
+        if (b >= nb) {
+            if (b < nb + 8) {  // padding: a window search may read 8 past a chain
+                tspan[b] = make_int2(0x7fffffff, 0x7fffffff);
+                blk[b] = make_int4(0x7fffffff, 0, 0, 0);
+            }
+            continue;
+        }
+        int64_t tbase, idx_off, coff_c;
+        int tstart, tend, shift, q_seq, qinfo;
+        int4 rr;
+        if (staged) {
+            const int j = staged_chain(S, b);
+            tbase = s_tbase[j], idx_off = s_idx[j], coff_c = S.off[j];
+            tstart = s_ts[j], tend = s_te[j], shift = s_sh[j], q_seq = s_qseq[j], qinfo = s_qinfo[j];
+            rr = s_run[j];
+        } else {
+            const int64_t c = owner_chain(coff, tile_c0, ntiles, b);
+            const DChain ch = chains[c];
+            tbase = ch.tbase, idx_off = ch.idx_off, coff_c = coff[c];
+            tstart = ch.tstart, tend = ch.tend, shift = ch.shift, q_seq = ch.q_seq, qinfo = ch.qinfo;
+            rr = crun ? crun[c] : make_int4(0, 0, 0, 0);
+        }
+        int flags = 0;  // (a block searches only the runs its chain's span meets)
+        if (z[i] > 0) {
+            if (rr.y > rr.x && span_meets(t_runs, rr.x, rr.y, tbase + t[i], tbase + t[i] + z[i]))
+                flags |= kTHasN;
+            if (rr.w > rr.z) {
+                const int64_t qb = q_woff[q_seq] * 32;
+                const int64_t qf = qinfo < 0 ? (int64_t)(qinfo & 0x7fffffff) - q[i] - z[i] : q[i];
+                if (span_meets(q_runs, rr.z, rr.w, qb + qf, qb + qf + z[i])) flags |= kQHasN;
+            }
+        }
+        blk[b] = make_int4(t[i], q[i], z[i] | flags, 0);
+        tspan[b] = make_int2(t[i], t[i] + z[i]);
+        const int64_t k = b - coff_c;
+        const int64_t span = (int64_t)tend - tstart;
+        const int64_t nbk = span > 0 ? ((span - 1) >> shift) + 1 : 0;
+        const int64_t round = ((int64_t)1 << shift) - 1;
+        const int64_t k0 = k ? ((int64_t)bt[b - 1] + bs[b - 1] - tstart + round) >> shift : 0;
+        int64_t k1 = ((int64_t)t[i] + z[i] - tstart + round) >> shift;
+        if (k1 > nbk) k1 = nbk;
+        uint32_t *bk = bucket + idx_off;
+        for (int64_t j = k0; j < k1; ++j) bk[j] = (uint32_t)k;
+    }
 }
 
 // k_block_gaps one lane per block (the chain only says whether the block is
@@ -381,26 +483,40 @@ __global__ void __launch_bounds__(256) k_block_gaps_flat(const int32_t *coff,
                                                          int64_t nb, int4 *blk, Blk12 *blk12,
                                                          GapDev g, const int32_t *small,
                                                          const int32_t *tab, int len) {
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= nb) return;
-    const int64_t c = owner_chain(coff, tile_c0, ntiles, b);
-    const int4 x = blk[b];
-    const int z = x.z & kSizeMask;
-    int cost = 0;
-    if (b + 1 < coff[c + 1]) {
-        const int4 y = blk[b + 1];
-        int d;
-        const int which = gap_kind(y.y - (x.y + z), y.x - (x.x + z), d);
-        cost = d < len ? tab[which * len + d] : gap_cost_wd(g, small, which, d);
+    __shared__ int32_t s_off[kStage + 1];
+    const int64_t B0 = (int64_t)blockIdx.x * blockDim.x * kUpPer;
+    int4 x[kUpPer];
+#pragma unroll
+    for (int i = 0; i < kUpPer; ++i) {  // (issued before the staging waits)
+        const int64_t b = B0 + i * (int64_t)blockDim.x + threadIdx.x;
+        x[i] = b < nb ? blk[b] : make_int4(0, 0, 0, 0);
     }
-    blk[b] = make_int4(x.x, x.y, x.z, cost);
-    const bool wide = z >= kB12Wide || cost < 0 || cost >= kB12GapMax;
-    Blk12 r;
-    r.t = x.x;
-    r.q = x.y;
-    r.w = (wide ? (uint32_t)kB12Wide : ((uint32_t)z | ((uint32_t)cost << 12))) |
-          ((uint32_t)(x.z & (kTHasN | kQHasN)) << 1);
-    blk12[b] = r;
+    ChainStage S;
+    const bool staged = stage_offsets(coff, tile_c0, ntiles, B0, s_off, S);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kUpPer; ++i) {
+        const int64_t b = B0 + i * (int64_t)blockDim.x + threadIdx.x;
+        if (b >= nb) break;
+        const int64_t next = staged ? S.off[staged_chain(S, b) + 1]
+                                    : coff[owner_chain(coff, tile_c0, ntiles, b) + 1];
+        const int z = x[i].z & kSizeMask;
+        int cost = 0;
+        if (b + 1 < next) {
+            const int4 y = blk[b + 1];
+            int d;
+            const int which = gap_kind(y.y - (x[i].y + z), y.x - (x[i].x + z), d);
+            cost = d < len ? tab[which * len + d] : gap_cost_wd(g, small, which, d);
+        }
+        blk[b] = make_int4(x[i].x, x[i].y, x[i].z, cost);
+        const bool wide = z >= kB12Wide || cost < 0 || cost >= kB12GapMax;
+        Blk12 r;
+        r.t = x[i].x;
+        r.q = x[i].y;
+        r.w = (wide ? (uint32_t)kB12Wide : ((uint32_t)z | ((uint32_t)cost << 12))) |
+              ((uint32_t)(x[i].z & (kTHasN | kQHasN)) << 1);
+        blk12[b] = r;
+    }
 }
 
 // ------------------------------------------------------------ k_plan -----
@@ -1635,14 +1751,19 @@ __device__ __forceinline__ uint32_t rev_nibbles(uint32_t v) {
 __global__ void __launch_bounds__(256) k_relayout(const uint8_t *raw, const SeqDev *seqs,
                                                   int nseq, int64_t nwords, uint2 *planes,
                                                   uint32_t *nmask) {
-    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= nwords) return;
+    const int64_t w0 = (int64_t)blockIdx.x * blockDim.x, w = w0 + threadIdx.x;
+    // the sequence of the workgroup's first word: a search on workgroup-uniform
+    // values (scalar loads), then the rare lanes past the next sequence start
+    // step forward (sequences are mostly far longer than 256 words)
     int lo = 0, hi = nseq - 1;
-    while (lo < hi) {  // last seq with word_off <= w
+    while (lo < hi) {  // last seq with word_off <= w0
         const int mid = (lo + hi + 1) >> 1;
-        if (seqs[mid].word_off <= w) lo = mid;
+        if (seqs[mid].word_off <= w0) lo = mid;
         else hi = mid - 1;
     }
+    if (lo + 1 < nseq && seqs[lo + 1].word_off < w0 + (int64_t)blockDim.x)
+        while (lo + 1 < nseq && seqs[lo + 1].word_off <= w) ++lo;
+    if (w >= nwords) return;
     const SeqDev s = seqs[lo];
     const int64_t base0 = (w - s.word_off) * 32;
     const uint64_t x = *reinterpret_cast<const uint64_t *>(raw + s.byte_off + (base0 >> 2));
@@ -1935,7 +2056,7 @@ hipError_t launch_gap_table(const GapDev &g, const int32_t *small, int len, int3
 
 hipError_t launch_build_flat(const int32_t *bt, const int32_t *bq, const int32_t *bs, int64_t nb,
                              const DChain *chains, int64_t n_chains, int32_t *coff,
-                             int32_t *tile_c0, uint8_t *cflag, const longlong2 *t_runs,
+                             int32_t *tile_c0, int4 *crun, const longlong2 *t_runs,
                              int64_t n_trun, const longlong2 *q_runs, int64_t n_qrun,
                              const int64_t *q_woff, int4 *blk, int2 *tspan, uint32_t *bucket,
                              hipStream_t s) {
@@ -1943,13 +2064,13 @@ hipError_t launch_build_flat(const int32_t *bt, const int32_t *bq, const int32_t
     if (n_chains > 0) {
         hipLaunchKernelGGL(k_chain_prep, dim3((unsigned)((n_chains + 255) / 256)), dim3(256), 0, s,
                            chains, n_chains, nb, bq, bs, t_runs, n_trun, q_runs, n_qrun, q_woff,
-                           coff, cflag, bucket);
+                           coff, crun, bucket);
         hipLaunchKernelGGL(k_tile_chain, dim3((unsigned)((ntiles + 1 + 255) / 256)), dim3(256), 0,
                            s, coff, n_chains, ntiles, tile_c0);
     }
-    const int64_t g = (nb + 8 + 255) / 256;
+    const int64_t g = (nb + 8 + 256 * kUpPer - 1) / (256 * kUpPer);
     hipLaunchKernelGGL(k_build_flat, dim3((unsigned)g), dim3(256), 0, s, bt, bq, bs, nb, chains,
-                       coff, tile_c0, ntiles, (n_trun || n_qrun) ? cflag : nullptr, t_runs, n_trun,
+                       coff, tile_c0, ntiles, (n_trun || n_qrun) ? crun : nullptr, t_runs, n_trun,
                        q_runs, n_qrun, q_woff, blk, tspan, bucket);
     return hipGetLastError();
 }
@@ -1958,7 +2079,8 @@ hipError_t launch_block_gaps_flat(const int32_t *coff, const int32_t *tile_c0, i
                                   int4 *blk, Blk12 *blk12, const GapDev &g, const int32_t *small,
                                   const int32_t *tab, int len, hipStream_t s) {
     if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_block_gaps_flat, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, coff,
+    hipLaunchKernelGGL(k_block_gaps_flat, dim3((unsigned)((nb + 256 * kUpPer - 1) / (256 * kUpPer))),
+                       dim3(256), 0, s, coff,
                        tile_c0, (nb + 63) >> 6, nb, blk, blk12, g, small, tab, len);
     return hipGetLastError();
 }

@@ -239,6 +239,22 @@ def test_whole_chains_vs_ranges(want_local, order, monkeypatch):
     assert np.array_equal(g[1::2], og) and np.array_equal(l[1::2], ol)
     assert np.array_equal(a[1::2], oa)
     cs2.close()
+    # runs of more empty chains than a 256-block upload workgroup stages
+    # (k_build_flat / k_block_gaps_flat take the global chain search there)
+    h = ca.n // 2
+    keep = np.concatenate([np.full(300, -1), np.arange(h), np.full(600, -1), np.arange(h, ca.n),
+                           np.full(5, -1)])
+    nbk = np.where(keep >= 0, nb[np.maximum(keep, 0)], 0)
+    off3 = np.concatenate([[0], np.cumsum(nbk)]).astype(np.int64)
+    src = np.maximum(keep, 0)
+    cs3 = e.upload_chain_arrays(tix[src], qix[src], ca.qstrand[src], off3, ca.blk_t, ca.blk_q,
+                                ca.blk_size)
+    g, l, a = e.score_chains(cs3, want_local=True)
+    real = keep >= 0
+    assert not g[~real].any() and not l[~real].any() and not a[~real].any()
+    assert np.array_equal(g[real], og) and np.array_equal(l[real], ol)
+    assert np.array_equal(a[real], oa)
+    cs3.close()
     cs.close()
     e.close()
 
