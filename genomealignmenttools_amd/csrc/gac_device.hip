@@ -1712,6 +1712,11 @@ static int prepare_args(gac_ctx *c, const gac_chainset *cs, int64_t n, uint32_t 
         return e && e[0] == '1' ? 1 : 0;
     }();
     a.scan64 = scan64;
+    static const int xcd_chunk = [] {
+        const char *e = getenv("GAC_TILE_XCD");
+        return e && e[0] == '1' ? 1 : 0;
+    }();
+    a.xcd_chunk = xcd_chunk;
     a.gap = c->gap;
     return GAC_OK;
 }

@@ -155,6 +155,8 @@ struct ScoreArgs {
                                // t0<<2 | d1<<1 | d0 (set bits = factors)
     int32_t sym;               // matrix is strand-symmetric: coef[8..15] == 0
     int32_t scan64;            // A/B probe (GAC_TILE_SCAN64=1): k_tile's 64-bit scans only
+    int32_t xcd_chunk;         // A/B probe (GAC_TILE_XCD=1): each XCD takes one contiguous
+                               // eighth of the tiles (default: per-round XCD blocks)
     GapDev gap;
     const int32_t *out_perm;  // non-null: the results of range (position) p go to
                               // chain out_perm[p] (the whole-chain plan in target order)

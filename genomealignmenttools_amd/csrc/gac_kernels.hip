@@ -1330,7 +1330,7 @@ __global__ void __launch_bounds__(256, SYM ? GAC_TILE_MINB : 6) k_tile(ScoreArgs
     const int G = gridDim.x;
     const int b = blockIdx.x;
     const int L8 = (G % 8 == 0) ? ((b % 8) * (G / 8) + b / 8) : b;
-    const int stride = G * kWavesPerWG;
+    int stride = G * kWavesPerWG, tend = T;
 
     // The tile's blocks belong to the ranges r0 .. r1 (r0 = tile_r0[t], r1 =
     // tile_r0[t + 1], the owner of the next tile's first block).  During tile
@@ -1341,11 +1341,17 @@ __global__ void __launch_bounds__(256, SYM ? GAC_TILE_MINB : 6) k_tile(ScoreArgs
     // from LDS by a 6-step owner search.  (Whole-chain plans in set order
     // have pb0 == gflat: one load.)
     int tile = L8 * kWavesPerWG + wave;
+    if (a.xcd_chunk && G % 8 == 0) {  // (probe) XCD x: tiles [x C, (x + 1) C)
+        const int C = (T + 7) / 8;
+        tile = (b % 8) * C + (b / 8) * kWavesPerWG + wave;
+        stride = (G / 8) * kWavesPerWG;
+        tend = T < (b % 8 + 1) * C ? T : (b % 8 + 1) * C;
+    }
     const int n = (int)a.n;
     const bool same_pb = a.pb0 == a.gflat;
     const auto cand_end = [&](int t) { return t + 1 < T ? a.tile_r0[t + 1] : n - 1; };
     int r0 = 0, gv = 0x7fffffff, bv = 0;
-    if (tile < T) {
+    if (tile < tend) {
         r0 = a.tile_r0[tile];
         const int r1 = cand_end(tile);
         if (r0 + lane <= r1 && r0 + lane < n) {
@@ -1353,7 +1359,7 @@ __global__ void __launch_bounds__(256, SYM ? GAC_TILE_MINB : 6) k_tile(ScoreArgs
             bv = same_pb ? gv : a.pb0[r0 + lane];
         }
     }
-    for (; tile < T; tile += stride) {
+    for (; tile < tend; tile += stride) {
         const int j = tile * kTileBlocks + lane;
         const bool active = j < W;
         L.cg[lane] = gv;
@@ -1361,7 +1367,7 @@ __global__ void __launch_bounds__(256, SYM ? GAC_TILE_MINB : 6) k_tile(ScoreArgs
         const int rc = r0;
         const int tn = tile + stride;
         int r0n = 0, r1n = 0;
-        if (tn < T) {
+        if (tn < tend) {
             r0n = a.tile_r0[tn];
             r1n = cand_end(tn);
         }
@@ -1372,7 +1378,7 @@ __global__ void __launch_bounds__(256, SYM ? GAC_TILE_MINB : 6) k_tile(ScoreArgs
         if (active) B = lane_block(a.rdesc[ri], load_blk12(a, bi), bi);
         gv = 0x7fffffff;
         bv = 0;
-        if (tn < T && r0n + lane <= r1n && r0n + lane < n) {
+        if (tn < tend && r0n + lane <= r1n && r0n + lane < n) {
             gv = a.gflat[r0n + lane];
             bv = same_pb ? gv : a.pb0[r0n + lane];
         }
