@@ -1007,6 +1007,39 @@ static void skel_fill(nwork *w, skel *k, nfill *f) {
     }
 }
 
+/* one span of the pre-order index: cnt fills from src, placed at pos */
+typedef struct ispan {
+    nfill **src;
+    int64_t pos, cnt;
+    int side;
+} ispan;
+
+typedef struct splice_job {
+    gac_net *n;
+    ispan *sp;
+    int64_t nspan;
+    _Atomic int64_t next;
+} splice_job;
+
+static void *splice_thread(void *arg) {
+    splice_job *J = arg;
+    for (;;) {
+        const int64_t a = atomic_fetch_add(&J->next, 4096);
+        if (a >= J->nspan)
+            return NULL;
+        const int64_t b = a + 4096 < J->nspan ? a + 4096 : J->nspan;
+        for (int64_t i = a; i < b; ++i) {
+            const ispan *s = &J->sp[i];
+            nfill **out = J->n->order[s->side] + s->pos;
+            for (int64_t j = 0; j < s->cnt; ++j) {
+                nfill *f = s->src[j];
+                f->ord = s->pos + j;
+                out[j] = f;
+            }
+        }
+    }
+}
+
 typedef struct fin_job {
     gac_net *n;
     int phase;
@@ -1694,6 +1727,8 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
         atomic_init(&F.next, 0);
         atomic_init(&F.wid, 0);
         gac_run_threads(n->n_w < F.ntask ? n->n_w : (F.ntask ? (int)F.ntask : 1), fin_thread, &F);
+        struct timespec t_sp;
+        clock_gettime(CLOCK_MONOTONIC, &t_sp);
         /* the pre-order index: skeletons with the subtree lists spliced in */
         int64_t tot[2] = {0, 0};
         for (int64_t k = 0; k < nc; ++k) {
@@ -1705,31 +1740,39 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
             n->order[side] = malloc((size_t)(tot[side] ? tot[side] : 1) * sizeof(nfill *));
             n->n_order[side] = 0;
         }
-        int64_t gidx = 0, used = 0; /* GAP item; fills taken from its chunk's list */
-        for (int64_t k = 0; k < nc; ++k) {
-            const int side = k < n->n_chroms[GAC_T] ? GAC_T : GAC_Q;
-            nfill **out = n->order[side];
-            int64_t no = n->n_order[side];
-            for (int64_t i = 0; i < F.sk[k].n; ++i) {
-                const sk_item *it = &F.sk[k].it[i];
-                if (!it->g) {
-                    it->f->ord = no;
-                    out[no++] = it->f;
-                    continue;
+        /* spans of the index in order (a FILL item: its fill; a GAP item:
+         * its run of its chunk's list), placed by a serial pass over the
+         * items, then copied -- and every fill's ord set -- on all threads */
+        int64_t nspan = 0;
+        for (int64_t k = 0; k < nc; ++k)
+            nspan += F.sk[k].n;
+        splice_job SJ = {n, malloc((size_t)(nspan ? nspan : 1) * sizeof(ispan)), nspan, 0};
+        {
+            int64_t gidx = 0, used = 0, m = 0; /* GAP item; fills taken from its chunk's list */
+            for (int64_t k = 0; k < nc; ++k) {
+                const int side = k < n->n_chroms[GAC_T] ? GAC_T : GAC_Q;
+                for (int64_t i = 0; i < F.sk[k].n; ++i) {
+                    sk_item *it = &F.sk[k].it[i];
+                    if (!it->g) {
+                        SJ.sp[m++] = (ispan){&it->f, n->n_order[side], 1, side};
+                        ++n->n_order[side];
+                        continue;
+                    }
+                    const fin_ctx *x = &F.x[gidx / F.per];
+                    if (gidx % F.per == 0)
+                        used = 0;
+                    SJ.sp[m++] = (ispan){x->ord + used, n->n_order[side], it->cnt, side};
+                    n->n_order[side] += it->cnt;
+                    used += it->cnt;
+                    ++gidx;
                 }
-                const fin_ctx *x = &F.x[gidx / F.per];
-                if (gidx % F.per == 0)
-                    used = 0;
-                for (int64_t j = 0; j < it->cnt; ++j) {
-                    x->ord[used + j]->ord = no;
-                    out[no++] = x->ord[used + j];
-                }
-                used += it->cnt;
-                ++gidx;
             }
-            n->n_order[side] = no;
-            free(F.sk[k].it);
         }
+        atomic_init(&SJ.next, 0);
+        gac_run_threads(n->n_w, splice_thread, &SJ);
+        free(SJ.sp);
+        for (int64_t k = 0; k < nc; ++k)
+            free(F.sk[k].it);
         for (int64_t k = 0; k < F.ntask; ++k)
             free(F.x[k].ord);
         free(F.sk);
@@ -1738,9 +1781,10 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
         struct timespec t_b;
         clock_gettime(CLOCK_MONOTONIC, &t_b);
         if (getenv("GAC_TIMING"))
-            fprintf(stderr, "[gac_net_build] finishNet skeletons %.3f s, subtrees + index %.3f s (%lld gap subtrees in %lld chunks)\n",
+            fprintf(stderr, "[gac_net_build] finishNet skeletons %.3f s, subtrees %.3f s, index %.3f s (%lld gap subtrees in %lld chunks)\n",
                     (t_a.tv_sec - t_fin0.tv_sec) + 1e-9 * (t_a.tv_nsec - t_fin0.tv_nsec),
-                    (t_b.tv_sec - t_a.tv_sec) + 1e-9 * (t_b.tv_nsec - t_a.tv_nsec), (long long)F.n_gi,
+                    (t_sp.tv_sec - t_a.tv_sec) + 1e-9 * (t_sp.tv_nsec - t_a.tv_nsec),
+                    (t_b.tv_sec - t_sp.tv_sec) + 1e-9 * (t_b.tv_nsec - t_sp.tv_nsec), (long long)F.n_gi,
                     (long long)F.ntask);
         free(F.x);
     }

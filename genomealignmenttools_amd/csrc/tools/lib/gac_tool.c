@@ -118,9 +118,17 @@ void gt_stage(const char *what) {
         fprintf(stderr, "[stage] %-32s %8.3f s\n", "exec + libraries (approx.)", startup);
         startup = -3;
     }
+    /* the process's CPU time over the stage: cpu / wall = the threads it kept
+     * busy on average (the headroom a stage leaves in the CPU quota) */
+    struct timespec cs;
+    clock_gettime(CLOCK_PROCESS_CPUTIME_ID, &cs);
+    const double cpu = cs.tv_sec + 1e-9 * cs.tv_nsec;
+    static double last_cpu = 0;
     if (last >= 0 && what && show)
-        fprintf(stderr, "[stage] %-32s %8.3f s\n", what, now - last);
+        fprintf(stderr, "[stage] %-32s %8.3f s  (cpu %.3f s, %.1f busy)\n", what, now - last,
+                cpu - last_cpu, now > last ? (cpu - last_cpu) / (now - last) : 0.0);
     last = now;
+    last_cpu = cpu;
 }
 
 static double now_s(void) {
@@ -1449,6 +1457,7 @@ typedef struct chunk {
     gt_chains c;       /* local: names local, id -1 = assign later */
     int64_t stop;      /* first chain (local index) scoring below stop_below, or -1 */
     int64_t lines;     /* newlines in the chunk */
+    double t0, t1;     /* (GAC_TIMING) when its parse started and ended */
     int64_t err_line;  /* local line of the error */
     double stop_below;
     const gt_names *tkeep, *qkeep; /* gt_read_chains_keep: NULL = keep all */
@@ -1670,6 +1679,7 @@ static int parse_chain(chunk *k) {
 
 static void *parse_chunk(void *arg) {
     chunk *k = arg;
+    k->t0 = now_s();
     k->c.blk_off = malloc(8);
     k->c.blk_off[0] = 0;
     if (k->lines > 0) { /* every block is a line: the arrays never grow */
@@ -1684,6 +1694,20 @@ static void *parse_chunk(void *arg) {
     if (r < 0)
         k->err_line = k->f.line;
     /* (f.line now counts the chunk's lines up to where it stopped) */
+    k->t1 = now_s();
+    return NULL;
+}
+
+typedef struct parse_pool {
+    chunk *K;
+    int nk;
+    _Atomic int next;
+} parse_pool;
+
+static void *parse_pool_thread(void *arg) {
+    parse_pool *P = arg;
+    for (int k; (k = atomic_fetch_add(&P->next, 1)) < P->nk;)
+        parse_chunk(&P->K[k]);
     return NULL;
 }
 
@@ -1799,8 +1823,11 @@ static void read_chains(const char *path, gt_chains *c, double stop_below, int k
     size_t len;
     char *buf = gt_slurp(path, &len);
     RC_LAP("read file");
-    /* chunk boundaries at "\nchain" */
-    int nt = len < (8u << 20) ? 1 : gt_threads();
+    /* chunk boundaries at "\nchain": 8 chunks per thread, taken in order by
+     * the threads as they finish (chain density varies along a file in score
+     * order: equal thirds of the bytes are not equal work) */
+    const int nthr = len < (8u << 20) ? 1 : gt_threads();
+    const int nt = nthr > 1 ? 8 * nthr : 1;
     char **cut = malloc((size_t)(nt + 1) * sizeof(char *));
     cut[0] = buf;
     int nk = 1;
@@ -1834,7 +1861,21 @@ static void read_chains(const char *path, gt_chains *c, double stop_below, int k
         K[k].qkeep = qkeep;
     }
     RC_LAP("cut");
-    gt_parallel(nk, parse_chunk, K, sizeof(chunk));
+    {
+        parse_pool P = {K, nk, 0};
+        atomic_init(&P.next, 0);
+        gac_run_threads(nthr < nk ? nthr : nk, parse_pool_thread, &P);
+    }
+    if (timing) {
+        double s0 = 1e30, e0 = 1e30, s1 = 0, e1 = 0, sum = 0;
+        for (int k = 0; k < nk; ++k) {
+            s0 = K[k].t0 < s0 ? K[k].t0 : s0, s1 = K[k].t0 > s1 ? K[k].t0 : s1;
+            e0 = K[k].t1 < e0 ? K[k].t1 : e0, e1 = K[k].t1 > e1 ? K[k].t1 : e1;
+            sum += K[k].t1 - K[k].t0;
+        }
+        fprintf(stderr, "[gt_read_chains] %d chunks: starts within %.3f s, ends within %.3f s, "
+                "mean %.3f s\n", nk, s1 - s0, e1 - e0, nk ? sum / nk : 0.0);
+    }
     RC_LAP("parse");
     /* stitch in file order up to the first error or stop: a serial pass for
      * everything order-dependent (names, ids, metadata, errors, offsets),
