@@ -119,7 +119,15 @@ static void *arena_alloc(arena *a, size_t sz) {
     return p;
 }
 
+/* The arenas' pages are dropped by madvise (under the mm's read lock, so the
+ * free workers run in parallel) before munmap (write lock: serial, and then
+ * cheap): C5 chainNet's nets freed in 0.055 s instead of 0.216 s, one core
+ * busy (`profiles/r04free/`).  GAC_FREE_MADV=0: munmap only. */
+static int g_free_madv = -1;
+
 static void arena_free(arena *a) {
+    for (size_t i = 0; i < a->n && g_free_madv == 1; ++i)
+        madvise(a->blocks[i], a->sizes[i], MADV_DONTNEED);
     for (size_t i = 0; i < a->n; ++i)
         munmap(a->blocks[i], a->sizes[i]);
     free(a->blocks);
@@ -942,8 +950,14 @@ void gac_net_free(gac_net *n) {
     if (!n)
         return;
     if (n->w) {
+        if (g_free_madv < 0) {
+            const char *e = getenv("GAC_FREE_MADV");
+            g_free_madv = !(e && *e == '0');
+        }
+        const char *ft = getenv("GAC_FREE_THREADS");
+        const int t = ft && atoi(ft) > 0 ? atoi(ft) : 16;
         atomic_store(&n->free_next, 0);
-        gac_run_threads(n->n_w < 8 ? n->n_w : 8, free_worker, n);
+        gac_run_threads(n->n_w < t ? n->n_w : t, free_worker, n);
     }
     free(n->w);
     free(n->chroms[0]);

@@ -724,5 +724,7 @@ int main(int argc, char *argv[]) {
     /* The net's pools are unmapped on 8 threads: left to process teardown
      * they are freed on one core after the output is complete. */
     gac_net_free(net);
+    gt_chains_drop_pages(&c);
+    gt_stage("free nets and chains");
     gt_exit_ok();
 }

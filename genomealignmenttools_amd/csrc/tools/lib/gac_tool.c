@@ -16,6 +16,7 @@
 #include <sys/syscall.h>
 #include <pthread.h>
 #include <stdatomic.h>
+#include <sys/mman.h>
 #include <time.h>
 #include <zlib.h>
 
@@ -576,6 +577,50 @@ void gt_device_close_join(gt_device *d) {
     }
     if (g_live_dev == d)
         g_live_dev = NULL;
+}
+
+typedef struct drop_job {
+    void *p[16];
+    size_t len[16];
+    int n;
+    _Atomic int next;
+} drop_job;
+
+static void *drop_thread(void *arg) {
+    drop_job *J = arg;
+    const uintptr_t pg = (uintptr_t)sysconf(_SC_PAGESIZE);
+    for (int k; (k = atomic_fetch_add(&J->next, 1)) < J->n;) {
+        const uintptr_t a = ((uintptr_t)J->p[k] + pg - 1) & ~(pg - 1);
+        const uintptr_t b = ((uintptr_t)J->p[k] + J->len[k]) & ~(pg - 1);
+        if (b > a)
+            madvise((void *)a, b - a, MADV_DONTNEED);
+    }
+    return NULL;
+}
+
+void gt_chains_drop_pages(gt_chains *c) {
+    const char *e = getenv("GAC_FREE_MADV");
+    if (e && *e == '0')
+        return;
+    drop_job J;
+    memset(&J, 0, sizeof(J));
+    const size_t n = (size_t)c->n, nb = (size_t)c->nb;
+#define DROP(ptr, bytes) \
+    if ((ptr) && J.n < 16) { J.p[J.n] = (void *)(ptr); J.len[J.n++] = (bytes); }
+    DROP(c->bt, nb * 4);
+    DROP(c->bq, nb * 4);
+    DROP(c->bs, nb * 4);
+    DROP(c->blk_off, (n + 1) * 8);
+    DROP(c->score, n * 8);
+    DROP(c->tstart, n * 4);
+    DROP(c->tend, n * 4);
+    DROP(c->qstart, n * 4);
+    DROP(c->qend, n * 4);
+    DROP(c->tname, n * 4);
+    DROP(c->qname, n * 4);
+#undef DROP
+    atomic_init(&J.next, 0);
+    gac_run_threads(J.n, drop_thread, &J);
 }
 
 void gt_exit_ok(void) {

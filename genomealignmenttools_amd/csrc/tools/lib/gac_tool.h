@@ -213,6 +213,11 @@ typedef struct gt_chains {
     int32_t n_meta, meta_cap;
 } gt_chains;
 
+/* Before exit: drop the pages of a chain set's arrays on several threads
+ * (madvise under the mm's read lock; the kernel's exit would free them on
+ * one core).  The set must not be used afterwards. */
+void gt_chains_drop_pages(gt_chains *c);
+
 /* stop_below: stop after reading the first chain whose score is < stop_below
  * (that chain is read, like chainNet's loop, but not kept); pass -HUGE_VAL
  * to read everything.  Reads .gz transparently, "stdin" allowed. */

@@ -216,7 +216,7 @@ int main(int argc, char *argv[]) {
         gt_careful_close(out, argv[4]);
     }
     gt_stage("write output");
-    /* host arrays are left to process exit */
+    gt_chains_drop_pages(&c); /* (the rest of the host arrays is left to process exit) */
     gt_device_close_join(&dev);
     gt_stage("device close (rest)");
     gt_ranks_done(&rk);
