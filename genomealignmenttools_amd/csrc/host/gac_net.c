@@ -1601,8 +1601,11 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
     int64_t *toff = calloc((size_t)nt + 1, 8), *qoff = calloc((size_t)nq + 1, 8);
     int64_t *tl = malloc((size_t)(nn ? nn : 1) * 8), *ql = malloc((size_t)(nn ? nn : 1) * 8);
     int64_t *tfill = malloc((size_t)(nt ? nt : 1) * 8), *qfill = malloc((size_t)(nq ? nq : 1) * 8);
+    uint8_t *skip = calloc((size_t)(nq ? nq : 1), 1); /* haplotype queries, by sequence */
+    for (int32_t k = 0; k < nq && !opt->incl_hap; ++k)
+        skip[k] = (uint8_t)is_haplotype(in->q_names[k]);
     for (int64_t c = 0; c < nn; ++c) {
-        if (!opt->incl_hap && is_haplotype(in->q_names[in->q_seq[c]]))
+        if (skip[in->q_seq[c]])
             continue;
         ++toff[in->t_seq[c] + 1];
         ++qoff[in->q_seq[c] + 1];
@@ -1614,11 +1617,12 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
     memcpy(tfill, toff, (size_t)nt * 8);
     memcpy(qfill, qoff, (size_t)nq * 8);
     for (int64_t c = 0; c < nn; ++c) {
-        if (!opt->incl_hap && is_haplotype(in->q_names[in->q_seq[c]]))
+        if (skip[in->q_seq[c]])
             continue;
         tl[tfill[in->t_seq[c]]++] = c;
         ql[qfill[in->q_seq[c]]++] = c;
     }
+    free(skip);
     for (int side = 0; side < 2; ++side) {
         int32_t cnt = side == GAC_T ? nt : nq;
         const char *const *names = side == GAC_T ? in->t_names : in->q_names;
