@@ -3372,6 +3372,9 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
             for (int d = 0; d < nd; ++d)
                 if (here >= 0 && CPU_ISSET(here, &dom[d].set))
                     d0 = d;
+            const char *db = getenv("GAC_DP_DOMAIN_BASE"); /* (axtChain -nranks: 2 x rank) */
+            if (db && nd > 0)
+                d0 = atoi(db) % nd;
             for (int64_t k = 0; k < big; ++k) {
                 int t = (int)((double)tt * psize[order[k]] / (double)sum + 0.5);
                 t = t < 2 ? 2 : t;

@@ -1025,6 +1025,11 @@ int main(int argc, char *argv[]) {
     }
     gt_set_gpu(gpu >= 0 ? gpu : (nranks > 1 ? rank : 0));
     gt_one_device();
+    if (nranks > 1 && !getenv("GAC_DP_DOMAIN_BASE")) { /* ranks' DP teams in L3 domains of their own */
+        char b[16];
+        snprintf(b, sizeof(b), "%d", 2 * rank);
+        setenv("GAC_DP_DOMAIN_BASE", b, 0);
+    }
     if (!jobs) {
         run_job(argc, argv, &B); /* exits */
         return 0;
