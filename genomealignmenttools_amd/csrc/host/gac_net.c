@@ -150,7 +150,7 @@ typedef struct nwork {
     struct sitem *q, *it, *cmb;
     int64_t q_n, q_cap, it_n, it_cap, cmb_cap;
     /* scratch for reversed blocks */
-    int32_t *rs, *re, *ros, *roe;
+    int32_t *rs, *re, *ros, *roe, *ro; /* ro: each block's other-side start */
     int64_t r_cap;
     char pad[64]; /* keep workers' hot fields on separate cache lines */
 } nwork;
@@ -553,11 +553,11 @@ static void it_push(nwork *w, int32_t s, int32_t e, ngap *g) {
  * gap bounds per block (gap between block b and b+1).  Each filled space is
  * replaced in the index by its remnants and the chain's gaps strictly inside
  * it, in one leaf update (fillSpace + addSpaceForGap, chainNet.c:487-523). */
-static void fill_other_range(const gac_net *n, nfill *f, int is_q);
 
-static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int is_q, int32_t chain, int nb,
+static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int32_t chain, int nb,
                            const int32_t *s, const int32_t *e, const int32_t *gos,
-                           const int32_t *goe, int cstart, int cend) {
+                           const int32_t *goe, const int32_t *os, int inv, int oflip, int cstart,
+                           int cend) {
     sp_query(n, c, cstart, cend, s, e, nb);
     const int64_t nsp = n->q_n;
     /* each filled space's gap gets the fill pushed: its line is a cache
@@ -599,11 +599,41 @@ static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int is_q, in
         f->end = end;
         f->chain = chain;
         f->ali = (int32_t)ali;
-        /* rCalcOtherFill (chainNet.c:393-484) now, while the chain's blocks
-         * are in cache: the final own-side bounds (zero-size blocks at the
-         * ends dropped; the order of a gap's fills is unchanged, their
-         * spaces being disjoint), the other-side range and f->full */
-        fill_other_range(net, f, is_q);
+        /* rCalcOtherFill (chainNet.c:393-484) now, on the same block slice:
+         * the blocks clipped to [start, end) give the final own-side bounds
+         * (zero-size blocks at the ends dropped; the order of a gap's fills
+         * is unchanged, their spaces being disjoint) and the other side's
+         * range (inv: the query side of a '-' chain, where the target runs
+         * backwards; oflip: the target side of a '-' chain, whose query
+         * range is flipped to + strand coordinates); f->full is subchainInfo's
+         * whole-chain test (chainNet.c:802-823) */
+        {
+            int fs = BIGNUM, fe = -BIGNUM, omin = BIGNUM, omax = -BIGNUM;
+            for (int b = k; b < nb; ++b) {
+                const int bs = s[b], be = e[b];
+                if (be <= start)
+                    continue;
+                if (bs >= end)
+                    break;
+                const int cs = bs < start ? start : bs, ce = be > end ? end : be;
+                const int o0 = inv ? os[b] + (be - ce) : os[b] + (cs - bs);
+                const int o1 = inv ? os[b] + (be - cs) : os[b] + (ce - bs);
+                if (fs > cs) fs = cs;
+                if (fe < ce) fe = ce;
+                if (omin > o0) omin = o0;
+                if (omax < o1) omax = o1;
+            }
+            if (oflip >= 0) {
+                const int t = omin;
+                omin = oflip - omax;
+                omax = oflip - t;
+            }
+            f->start = fs;
+            f->end = fe;
+            f->o_start = omin;
+            f->o_end = omax;
+            f->full = fs <= cstart && fe >= cend;
+        }
         /* slAddHead onto the space's gap; region workers of one chromosome
          * side (net_regions) may share the gap, so the push is atomic.  The
          * order does not matter: finishNet sorts a gap's fills by start. */
@@ -641,6 +671,7 @@ static void ensure_rev(nwork *n, int64_t nb) {
         n->re = realloc(n->re, n->r_cap * 4);
         n->ros = realloc(n->ros, n->r_cap * 4);
         n->roe = realloc(n->roe, n->r_cap * 4);
+        n->ro = realloc(n->ro, n->r_cap * 4);
     }
 }
 
@@ -700,6 +731,7 @@ static void add_chain_q(const gac_net *net, nwork *n, int64_t c, nchrom *qc, int
         for (int b = l0; b < l1; ++b) {
             n->rs[b - l0] = bq[b];
             n->re[b - l0] = bq[b] + bs[b];
+            n->ro[b - l0] = bt[b];
             if (b + 1 < nb) {
                 n->ros[b - l0] = bt[b] + bs[b];
                 n->roe[b - l0] = bt[b + 1];
@@ -713,13 +745,15 @@ static void add_chain_q(const gac_net *net, nwork *n, int64_t c, nchrom *qc, int
             int j = nb - 1 - i; /* original index */
             n->rs[i - l0] = qsize - (bq[j] + bs[j]);
             n->re[i - l0] = qsize - bq[j];
+            n->ro[i - l0] = bt[j];
             if (i + 1 < nb) { /* block = j, next = j-1 */
                 n->ros[i - l0] = bt[j - 1];
                 n->roe[i - l0] = bt[j] + bs[j];
             }
         }
     }
-    add_chain_side(net, n, qc, 1, (int32_t)c, m, n->rs, n->re, n->ros, n->roe, qs, qe);
+    add_chain_side(net, n, qc, (int32_t)c, m, n->rs, n->re, n->ros, n->roe, n->ro, minus, -1, qs,
+                   qe);
 }
 
 /* addChainT (chainNet.c:557-608) */
@@ -741,6 +775,7 @@ static void add_chain_t(const gac_net *net, nwork *n, int64_t c, nchrom *tc, int
     for (int b = l0; b < l1; ++b) {
         n->rs[b - l0] = bt[b];
         n->re[b - l0] = bt[b] + bs[b];
+        n->ro[b - l0] = bq[b];
         if (b + 1 < nb) {
             int qs = bq[b] + bs[b], qe = bq[b + 1];
             if (minus) {
@@ -752,107 +787,14 @@ static void add_chain_t(const gac_net *net, nwork *n, int64_t c, nchrom *tc, int
             n->roe[b - l0] = qe;
         }
     }
-    add_chain_side(net, n, tc, 0, (int32_t)c, m, n->rs, n->re, n->ros, n->roe, in->t_start[c],
-                   in->t_end[c]);
+    add_chain_side(net, n, tc, (int32_t)c, m, n->rs, n->re, n->ros, n->roe, n->ro, 0,
+                   minus ? qsize : -1, in->t_start[c], in->t_end[c]);
 }
 
 /* ------------------------------------------------------------ finish */
 static int cmp_fill(const void *a, const void *b) {
     const nfill *x = *(nfill *const *)a, *y = *(nfill *const *)b;
     return (x->start > y->start) - (x->start < y->start);
-}
-
-/* first block index with value[k] + size[k] > v (blocks monotone) */
-static int first_end_after(const int32_t *st, const int32_t *sz, int nb, int v) {
-    int lo = 0, hi = nb;
-    while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if (st[mid] + sz[mid] > v)
-            hi = mid;
-        else
-            lo = mid + 1;
-    }
-    return lo;
-}
-
-/* tFillOtherRange / qFillOtherRange (chainNet.c:393-484) */
-static void fill_other_range(const gac_net *n, nfill *f, int is_q) {
-    const gac_net_input *in = &n->in;
-    const int64_t c = f->chain, b0 = in->blk_off[c];
-    const int nb = (int)(in->blk_off[c + 1] - b0);
-    const int32_t *bt = in->blk_t + b0, *bq = in->blk_q + b0, *bs = in->blk_size + b0;
-    const int minus = in->q_strand[c] != 0;
-    const int qsize = in->q_sizes[in->q_seq[c]];
-    int clip_s = f->start, clip_e = f->end;
-    int tmin = BIGNUM, tmax = -BIGNUM, qmin = BIGNUM, qmax = -BIGNUM;
-    if (is_q) {
-        if (minus) {
-            int t = clip_s;
-            clip_s = qsize - clip_e;
-            clip_e = qsize - t;
-        }
-        for (int b = first_end_after(bq, bs, nb, clip_s); b < nb; ++b) {
-            int qs = bq[b], qe = bq[b] + bs[b], ts = bt[b], te = bt[b] + bs[b];
-            if (qe <= clip_s)
-                continue;
-            if (qs >= clip_e)
-                break;
-            if (qs < clip_s) {
-                ts += clip_s - qs;
-                qs = clip_s;
-            }
-            if (qe > clip_e) {
-                te -= qe - clip_e;
-                qe = clip_e;
-            }
-            if (qmin > qs) qmin = qs;
-            if (qmax < qe) qmax = qe;
-            if (tmin > ts) tmin = ts;
-            if (tmax < te) tmax = te;
-        }
-        /* the whole chain: subchainInfo's test (chainNet.c:802-823), in
-         * the chain's query coordinates */
-        f->full = qmin <= in->q_start[c] && qmax >= in->q_end[c];
-        if (minus) {
-            int t = qmin;
-            qmin = qsize - qmax;
-            qmax = qsize - t;
-        }
-        f->start = qmin;
-        f->end = qmax;
-        f->o_start = tmin;
-        f->o_end = tmax;
-    } else {
-        for (int b = first_end_after(bt, bs, nb, clip_s); b < nb; ++b) {
-            int ts = bt[b], te = bt[b] + bs[b], qs = bq[b], qe = bq[b] + bs[b];
-            if (te <= clip_s)
-                continue;
-            if (ts >= clip_e)
-                break;
-            if (ts < clip_s) {
-                qs += clip_s - ts;
-                ts = clip_s;
-            }
-            if (te > clip_e) {
-                qe -= te - clip_e;
-                te = clip_e;
-            }
-            if (qmin > qs) qmin = qs;
-            if (qmax < qe) qmax = qe;
-            if (tmin > ts) tmin = ts;
-            if (tmax < te) tmax = te;
-        }
-        if (minus) {
-            int t = qmin;
-            qmin = qsize - qmax;
-            qmax = qsize - t;
-        }
-        f->start = tmin;
-        f->end = tmax;
-        f->o_start = qmin;
-        f->o_end = qmax;
-        f->full = tmin <= in->t_start[c] && tmax >= in->t_end[c];
-    }
 }
 
 /* finishNet per chromosome (sortNet + rCalcOtherFill, chainNet.c:694-723):
@@ -943,6 +885,7 @@ static void *free_worker(void *arg) {
         free(w->re);
         free(w->ros);
         free(w->roe);
+        free(w->ro);
     }
 }
 
@@ -1795,7 +1738,7 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
             free(F.x[k].ord);
         free(F.sk);
         free(F.gi);
-        /* (rCalcOtherFill ran as each fill was made: fill_other_range) */
+        /* (rCalcOtherFill ran as each fill was made: add_chain_side) */
         struct timespec t_b;
         clock_gettime(CLOCK_MONOTONIC, &t_b);
         if (getenv("GAC_TIMING"))
