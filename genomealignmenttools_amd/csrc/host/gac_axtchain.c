@@ -3360,6 +3360,8 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
             const char *pl = getenv("GAC_DP_POOL"); /* (threads beside the teams) */
             pool = pl && atoi(pl) > 0 && atoi(pl) < nthreads ? atoi(pl)
                                                              : (nthreads / 3 > 1 ? nthreads / 3 : 1);
+            if (pool > np - big) /* (no pool pairs left, e.g. an -nranks rank holding one big pair) */
+                pool = (int)(np - big);
             const int tt = nthreads - pool;
             int used = 0;
             /* each team in an L3 domain of its own, from the one this
@@ -3400,8 +3402,6 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
                     tr[k].started = 1;
             }
             atomic_store(&J.next, big);
-            if (pool > np - big)
-                pool = np - big > 0 ? (int)(np - big) : 1;
         }
         if (big == 0 || np > big)
             run_threads(pool, ax_thread, &J);
