@@ -314,6 +314,36 @@ static void *psl_chunk_thread(void *arg) {
     return NULL;
 }
 
+typedef struct merge_task {
+    int32_t g;      /* the global pair */
+    pair *lp;       /* a chunk's pair */
+    int64_t off;    /* where its blocks go in the global pair's arrays */
+} merge_task;
+
+typedef struct merge_job {
+    pairs *P;
+    merge_task *t;
+    int64_t n;
+    _Atomic int64_t next;
+} merge_job;
+
+static void *merge_thread(void *arg) {
+    merge_job *M = arg;
+    for (int64_t i; (i = atomic_fetch_add(&M->next, 1)) < M->n;) {
+        const merge_task *t = &M->t[i];
+        pair *gp = &M->P->p[t->g], *lp = t->lp;
+        memcpy(gp->bt + t->off, lp->bt, (size_t)lp->nb * 4);
+        memcpy(gp->bq + t->off, lp->bq, (size_t)lp->nb * 4);
+        memcpy(gp->bs + t->off, lp->bs, (size_t)lp->nb * 4);
+        free(lp->bt);
+        free(lp->bq);
+        free(lp->bs);
+        free(lp->qname);
+        free(lp->tname);
+    }
+    return NULL;
+}
+
 static void read_psl_chunks(rd *r, pairs *P) {
     char *a = r->cur, *end = r->end;
     const size_t len = (size_t)(end - a);
@@ -340,39 +370,53 @@ static void read_psl_chunks(rd *r, pairs *P) {
     psl_job J = {K, n, 0};
     atomic_init(&J.next, 0);
     gac_run_threads(gt_threads() < n ? gt_threads() : (n ? n : 1), psl_chunk_thread, &J);
-    int64_t line0 = r->line;
+    /* merge in file order: the metadata and the first error as a sequential
+     * read meets them; every chunk's pairs placed at their offsets in the
+     * global pairs (serial: pair order is first-seen order), then the block
+     * runs copied on all threads */
+    int64_t line0 = r->line, ntask = 0;
     for (int i = 0; i < n; ++i) {
         psl_chunk *k = &K[i];
         for (int32_t m = 0; m < k->n_meta; ++m)
             rd_meta(r, k->meta[m]);
         if (k->err)
             psl_error(k->err, k->err_wc, k->msg, line0 + k->err_line, r->path);
+        line0 += k->lines;
+        ntask += k->P.n;
+    }
+    r->line = (int)line0;
+    merge_job M;
+    M.P = P;
+    M.t = malloc((size_t)(ntask ? ntask : 1) * sizeof(merge_task));
+    M.n = 0;
+    for (int i = 0; i < n; ++i) {
+        psl_chunk *k = &K[i];
         for (int32_t j = 0; j < k->P.n; ++j) {
             pair *lp = &k->P.p[j];
             const char strand[2] = {lp->strand, 0};
             pair *gp = pair_get(P, lp->qname, strand, lp->tname);
-            if (gp->nb + lp->nb > gp->cap) {
-                gp->cap = gp->nb + lp->nb + gp->cap;
-                gp->bt = realloc(gp->bt, (size_t)gp->cap * 4);
-                gp->bq = realloc(gp->bq, (size_t)gp->cap * 4);
-                gp->bs = realloc(gp->bs, (size_t)gp->cap * 4);
-            }
-            memcpy(gp->bt + gp->nb, lp->bt, (size_t)lp->nb * 4);
-            memcpy(gp->bq + gp->nb, lp->bq, (size_t)lp->nb * 4);
-            memcpy(gp->bs + gp->nb, lp->bs, (size_t)lp->nb * 4);
-            gp->nb += lp->nb;
-            free(lp->bt);
-            free(lp->bq);
-            free(lp->bs);
-            free(lp->qname);
-            free(lp->tname);
+            M.t[M.n++] = (merge_task){(int32_t)(gp - P->p), lp, gp->nb};
+            gp->nb += lp->nb; /* (reserved: the copy follows) */
         }
+    }
+    for (int32_t g = 0; g < P->n; ++g) {
+        pair *gp = &P->p[g];
+        if (gp->nb > gp->cap) {
+            gp->cap = gp->nb;
+            gp->bt = realloc(gp->bt, (size_t)gp->cap * 4);
+            gp->bq = realloc(gp->bq, (size_t)gp->cap * 4);
+            gp->bs = realloc(gp->bs, (size_t)gp->cap * 4);
+        }
+    }
+    atomic_init(&M.next, 0);
+    gac_run_threads(gt_threads() < M.n ? gt_threads() : (M.n ? (int)M.n : 1), merge_thread, &M);
+    free(M.t);
+    for (int i = 0; i < n; ++i) {
+        psl_chunk *k = &K[i];
         free(k->P.p);
         gt_names_free(&k->P.keys);
         free(k->meta);
-        line0 += k->lines;
     }
-    r->line = (int)line0;
     free(K);
 }
 
