@@ -342,6 +342,44 @@ static void *check_thread(void *arg) {
     }
 }
 
+
+/* chainNet -rescore's rescoring list: the target fills that are partial
+ * (flag 1) and printed (flag 2), in fill order */
+typedef struct range_job {
+    const int32_t *fc, *fs, *fe;
+    const uint8_t *fl;
+    gac_range *r;
+    int64_t *rix;
+    int64_t nf;
+    int nt;
+    int64_t *cnt; /* [nt + 1]: per slice, then where its ranges start */
+    int phase;
+    _Atomic int next;
+} range_job;
+
+static void *range_thread(void *arg) {
+    range_job *J = arg;
+    for (int k; (k = atomic_fetch_add(&J->next, 1)) < J->nt;) {
+        const int64_t a = J->nf * k / J->nt, b = J->nf * (k + 1) / J->nt;
+        if (J->phase == 0) {
+            int64_t c = 0;
+            for (int64_t i = a; i < b; ++i)
+                c += (J->fl[i] & 3) == 3;
+            J->cnt[k] = c;
+            continue;
+        }
+        int64_t o = J->cnt[k];
+        for (int64_t i = a; i < b; ++i)
+            if ((J->fl[i] & 3) == 3) {
+                J->r[o].chain = J->fc[i];
+                J->r[o].t_start = J->fs[i];
+                J->r[o].t_end = J->fe[i];
+                J->rix[o++] = i;
+            }
+    }
+    return NULL;
+}
+
 int main(int argc, char *argv[]) {
     gt_stage("");
     int min_space = 25;
@@ -566,15 +604,22 @@ int main(int argc, char *argv[]) {
         gt_check(gac_net_get_fills(net, GAC_T, fc, fs, fe, fa, fl));
         gac_range *r = malloc((nf ? nf : 1) * sizeof(gac_range));
         int64_t *rix = malloc((nf ? nf : 1) * 8);
-        int64_t nr = 0;
         gac_mark("fill list: ranges");
-        for (int64_t i = 0; i < nf; ++i)
-            if ((fl[i] & 3) == 3) { /* partial and printed */
-                r[nr].chain = fc[i];
-                r[nr].t_start = fs[i];
-                r[nr].t_end = fe[i];
-                rix[nr++] = i;
-            }
+        /* the partial, printed fills in order: counted per slice, then
+         * placed, on all threads */
+        range_job RJ = {fc, fs, fe, fl, r, rix, nf, gt_threads(), NULL, 0, 0};
+        RJ.cnt = calloc((size_t)RJ.nt + 1, 8);
+        atomic_init(&RJ.next, 0);
+        gac_run_threads(RJ.nt, range_thread, &RJ);
+        for (int k = 0; k < RJ.nt; ++k) /* (exclusive prefix) */
+            RJ.cnt[k + 1] += RJ.cnt[k];
+        memmove(RJ.cnt + 1, RJ.cnt, (size_t)RJ.nt * 8);
+        RJ.cnt[0] = 0;
+        RJ.phase = 1;
+        atomic_init(&RJ.next, 0);
+        gac_run_threads(RJ.nt, range_thread, &RJ);
+        const int64_t nr = RJ.cnt[RJ.nt];
+        free(RJ.cnt);
         tscores = calloc(nf ? nf : 1, 8);
         /* GAC_DUMP_RANGES=FILE (measurement hook, one process only): the
          * rescored fills as int32 (chain index in file order, tStart, tEnd),
