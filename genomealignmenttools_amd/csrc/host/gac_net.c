@@ -624,23 +624,31 @@ static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int32_t chai
         /* innerBounds (chainNet.c:356-391), and the clipped blocks' bases:
          * the fill's aligned bases, since no block of the chain lies in the
          * space outside [start, end) */
-        int start = BIGNUM, end = -BIGNUM;
+        int start = BIGNUM, end = -BIGNUM, zero = 0;
+        int fs = BIGNUM, fe = -BIGNUM, omin = BIGNUM, omax = -BIGNUM; /* (see below) */
         int64_t ali = 0;
         for (int b = k; b < nb; ++b) {
-            int bs = s[b], be = e[b];
-            if (be <= sstart)
+            const int b0 = s[b], b1 = e[b];
+            if (b1 <= sstart)
                 continue;
-            if (bs >= send)
+            if (b0 >= send)
                 break;
-            if (bs < sstart)
-                bs = sstart;
-            if (be > send)
-                be = send;
-            if (start > bs)
-                start = bs;
-            if (end < be)
-                end = be;
-            ali += be - bs;
+            const int cs = b0 < sstart ? sstart : b0, ce = b1 > send ? send : b1;
+            if (start > cs)
+                start = cs;
+            if (end < ce)
+                end = ce;
+            ali += ce - cs;
+            if (ce > cs) {
+                const int o0 = inv ? os[b] + (b1 - ce) : os[b] + (cs - b0);
+                const int o1 = inv ? os[b] + (b1 - cs) : os[b] + (ce - b0);
+                if (fs > cs) fs = cs;
+                if (fe < ce) fe = ce;
+                if (omin > o0) omin = o0;
+                if (omax < o1) omax = o1;
+            } else {
+                zero = 1;
+            }
         }
         if (end < 0 || end - start < net->opt.min_fill)
             continue;
@@ -658,8 +666,12 @@ static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int32_t chai
          * backwards; oflip: the target side of a '-' chain, whose query
          * range is flipped to + strand coordinates); f->full is subchainInfo's
          * whole-chain test (chainNet.c:802-823) */
-        {
-            int fs = BIGNUM, fe = -BIGNUM, omin = BIGNUM, omax = -BIGNUM;
+        /* Every block with bases in the space is inside [start, end), so
+         * the loop above already clipped it the same way and saw it; only a
+         * zero-size block is treated differently (kept only strictly inside
+         * the fill), and then the blocks are walked again */
+        if (zero) {
+            fs = BIGNUM, fe = -BIGNUM, omin = BIGNUM, omax = -BIGNUM;
             for (int b = k; b < nb; ++b) {
                 const int bs = s[b], be = e[b];
                 if (be <= start)
@@ -674,6 +686,8 @@ static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int32_t chai
                 if (omin > o0) omin = o0;
                 if (omax < o1) omax = o1;
             }
+        }
+        {
             if (oflip >= 0) {
                 const int t = omin;
                 omin = oflip - omax;

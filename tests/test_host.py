@@ -656,3 +656,53 @@ def test_write_chains_fast_negative_fields(tmp_path):
     chainfile.write_chains(ca, str(tmp_path / "a"))
     chainfile.write_chains_fast(ca, str(tmp_path / "b"))
     assert (tmp_path / "a").read_bytes() == (tmp_path / "b").read_bytes()
+
+
+@pytest.mark.parametrize("opts", [[], ["-minSpace=1", "-minFill=1"]])
+def test_chainnet_zero_size_blocks_vs_reference(opts, tmp_path):
+    """Zero-size blocks (inside a chain's gaps, and as a chain's first
+    block) against the reference chainNet: innerBounds counts them, the
+    fill's final bounds and other-side range (rCalcOtherFill) keep them only
+    strictly inside the fill -- the path add_chain_side takes a second walk
+    over the blocks for.  (With -minFill=0 the reference asserts on the
+    zero-size fills such blocks make, fillSpace's `s < e`: no case here.)"""
+    from genomealignmenttools_amd import chainfile, synth
+    from genomealignmenttools_amd._lib import BIN_DIR
+    from oracle.oracle import ref_tool
+    ref = ref_tool("chainNet")
+    if not os.path.exists(ref):
+        pytest.skip("oracle/_ref/chainNet not built (make ref)")
+    tg, qg, ca = synth.small_case(seed=23, n_chains=300)
+    bt, bq, bs, off = [], [], [], [0]
+    for i in range(ca.n):
+        t, q, z = (x.tolist() for x in ca.blocks(i))
+        nt, nq, nz = [], [], []
+        for k in range(len(t)):
+            if k == 0 and i % 3 == 0 and t[0] > 0 and q[0] > 0:  # a zero-size first block
+                nt.append(t[0] - 1), nq.append(q[0] - 1), nz.append(0)
+            nt.append(t[k]), nq.append(q[k]), nz.append(z[k])
+            if k + 1 < len(t) and i % 2 == 0:  # one inside the gap, when there is room
+                gt, gq = t[k + 1] - (t[k] + z[k]), q[k + 1] - (q[k] + z[k])
+                if gt >= 2 and gq >= 2:
+                    nt.append(t[k] + z[k] + gt // 2), nq.append(q[k] + z[k] + gq // 2), nz.append(0)
+        bt += nt
+        bq += nq
+        bs += nz
+        off.append(off[-1] + len(nt))
+        ca.tstart[i], ca.qstart[i] = nt[0], nq[0]
+    ca.blk_t = np.array(bt, np.int32)
+    ca.blk_q = np.array(bq, np.int32)
+    ca.blk_size = np.array(bs, np.int32)
+    ca.blk_off = np.array(off, np.int64)
+    d = str(tmp_path)
+    p = lambda x: os.path.join(d, x)
+    synth.write_sizes(tg.sizes, p("t.sizes"))
+    synth.write_sizes(qg.sizes, p("q.sizes"))
+    chainfile.write_chains(ca, p("in.chain"))
+    outs = {}
+    for tag, exe in (("ours", os.path.join(BIN_DIR, "chainNet")), ("ref", ref)):
+        r = subprocess.run([exe, p("in.chain"), p("t.sizes"), p("q.sizes"), p(f"{tag}.t.net"),
+                            p(f"{tag}.q.net")] + opts, capture_output=True)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs[tag] = [open(p(f"{tag}.{s}.net"), "rb").read() for s in "tq"]
+    assert outs["ours"] == outs["ref"]
