@@ -329,7 +329,7 @@ enum { kStack = 512 };
 
 #ifdef GAC_DP_STATS /* profiling build only (make cpu-axtchain CPU_EXTRA=-DGAC_DP_STATS) */
 static __thread struct {
-    long long visits, prune1, prune2, leaves, cands, overlaps, xover_bases, updates, best_wins;
+    long long visits, prune1, prune2, leaves, cands, overlaps, xover_bases, updates, best_wins, ref_visits;
 } g_st;
 static __thread long long g_wr[8][2]; /* bound writes by depth / 4: max_score, linear */
 #define ST(x) (g_st.x++)
@@ -340,23 +340,36 @@ static __thread long long g_wr[8][2]; /* bound writes by depth / 4: max_score, l
 #endif
 
 /* bestPredecessor (chainBlock.c:207-263), iterative with the same order:
- * the hi subtree (only when the lonely leaf lies past the cut) before lo */
-static void best_predecessor(ax_work *w, int32_t lonely, double *ret_score, int32_t *ret_pred) {
+ * the hi subtree (only when the lonely leaf lies past the cut) before lo.
+ * ov (the fast DP's fallback, where the nodes' linear bounds are kept): the
+ * leaf nodes of the lonely leaf's overlapping candidates, nov of them.  A
+ * subtree holding none of them holds only non-overlapping candidates, whose
+ * scores its linear bound caps; when that is below the best so far, the
+ * reference walks the subtree without taking anything (it takes a strictly
+ * greater score only), so skipping it leaves its answer as it was.  Node
+ * ranges come from the pre-order layout: node b's subtree is [b, end), its
+ * hi child's [b + 1, lo), its lo child's [lo, end). */
+static void best_predecessor_at(ax_work *w, int32_t lonely, double *ret_score, int32_t *ret_pred,
+                                const int32_t *ov, int nov) {
     const int32_t lq = w->qs[lonely], lt = w->ts[lonely];
     const double lscore = w->score[lonely];
+    const int sure = nov >= 0;
+    const int64_t kl = sure ? w->e->lin_k * ((int64_t)lq + lt) - 1024 * (int64_t)lscore : 0;
     double best = 0.0;
     int32_t best_node = -1;
-    int32_t st_node[kStack];
+    int32_t st_node[kStack], st_end[kStack];
     uint8_t st_dim[kStack];
     int sp = 0;
     st_node[sp] = 0;
+    st_end[sp] = w->nn;
     st_dim[sp++] = 0;
     while (sp > 0) {
         --sp;
-        const int32_t b = st_node[sp];
+        const int32_t b = st_node[sp], end = st_end[sp];
         const int dim = st_dim[sp];
         const ax_node *nd = &w->nodes[b];
         ST(visits);
+        ST(ref_visits);
         double max_score = w->bnd[b].max_score + lscore;
         if (max_score < best) {
             ST(prune1);
@@ -367,6 +380,13 @@ static void best_predecessor(ax_work *w, int32_t lonely, double *ret_score, int3
         if (max_score < best) {
             ST(prune2);
             continue;
+        }
+        if (sure && w->bnd[b].nw - kl < 1024 * (int64_t)best) {
+            int held = 0;
+            for (int k = 0; k < nov && !held; ++k)
+                held = ov[k] >= b && ov[k] < end;
+            if (!held)
+                continue;
         }
         if (nd->leaf >= 0) {
             const int32_t l = nd->leaf;
@@ -380,10 +400,10 @@ static void best_predecessor(ax_work *w, int32_t lonely, double *ret_score, int3
                     STN(xover_bases, -(dq < dt ? dq : dt));
                 }
 #endif
-                const double s = w->total[l] + lscore - connect_cost(w, l, lonely);
-                if (s > best) {
+                const double sc = w->total[l] + lscore - connect_cost(w, l, lonely);
+                if (sc > best) {
                     ST(best_wins);
-                    best = s;
+                    best = sc;
                     best_node = b;
                 }
             }
@@ -395,14 +415,20 @@ static void best_predecessor(ax_work *w, int32_t lonely, double *ret_score, int3
         }
         const int32_t coord = dim == 0 ? lq : lt;
         st_node[sp] = nd->lo;
+        st_end[sp] = end;
         st_dim[sp++] = (uint8_t)(1 - dim);
         if (coord > nd->cut) {
             st_node[sp] = nd->hi;
+            st_end[sp] = nd->lo;
             st_dim[sp++] = (uint8_t)(1 - dim);
         }
     }
     *ret_score = best;
     *ret_pred = best_node;
+}
+
+static void best_predecessor(ax_work *w, int32_t lonely, double *ret_score, int32_t *ret_pred) {
+    best_predecessor_at(w, lonely, ret_score, ret_pred, NULL, -1);
 }
 
 /* updateScoresOnWay (chainBlock.c:265-279): both sides on a tie with the cut */
@@ -608,6 +634,48 @@ static int dp_anomaly(ax_work *w, int32_t lonely, int32_t ti, double best, int32
         }
     }
     return 0;
+}
+
+/* the leaf nodes of every overlapping candidate of `lonely` (dp_anomaly's
+ * scan, all of them): their count, or -1 past cap */
+static int dp_overlaps(ax_work *w, int32_t lonely, int32_t ti, int32_t maxsz, int32_t *out,
+                       int cap) {
+    const int32_t lq = w->qs[lonely], lt = w->ts[lonely];
+    int n = 0;
+    for (int side = 0; side < 2; ++side) {
+        const int32_t *box = side ? w->qbox : w->tbox;
+        const int32_t at = side ? w->qpos[lonely] : ti, lo = (side ? lq : lt) - maxsz;
+        for (int32_t j = at - 1; j >= 0 && box[4 * (size_t)j] > lo; --j) {
+            const int32_t *b = box + 4 * (size_t)j;
+            const int32_t cqs = side ? b[0] : b[2], cqe = side ? b[1] : b[3];
+            const int32_t cts = side ? b[2] : b[0], cte = side ? b[3] : b[1];
+            const int32_t tp = side ? w->qtp[j] : j;
+            if (cts >= lt || cqs >= lq || tp >= w->cut_t)
+                continue;
+            const int dq = lq - cqe, dt = lt - cte;
+            if (dq >= 0 && dt >= 0)
+                continue;
+            if (side == 1 && dt < 0)
+                continue; /* (the t scan saw it) */
+            if (n == cap)
+                return -1;
+            out[n++] = w->lnode[side ? w->qord[j] : w->tord[j]];
+        }
+    }
+    return n;
+}
+
+/* the reference-order search, sped up where it provably changes nothing */
+static void best_predecessor_fallback(ax_work *w, int32_t lonely, int32_t ti, int32_t maxsz,
+                                      double *ret_score, int32_t *ret_pred) {
+    static int on = -1;
+    if (on < 0) {
+        const char *e = getenv("GAC_DP_FALLBACK_PRUNE");
+        on = !(e && *e == '0');
+    }
+    int32_t ov[64];
+    const int nov = on ? dp_overlaps(w, lonely, ti, maxsz, ov, 64) : -1;
+    best_predecessor_at(w, lonely, ret_score, ret_pred, ov, nov);
 }
 
 /* ---- sorts (glibc qsort is a stable merge sort here; ranks make it explicit) */
@@ -1208,7 +1276,7 @@ static void pair_dp_fast(ax_work *w) {
         w->cut_t = i;
         best_predecessor_fast(w, l, &s, &p);
         if (dp_anomaly(w, l, i, s, maxsz)) {
-            best_predecessor(w, l, &s, &p);
+            best_predecessor_fallback(w, l, i, maxsz, &s, &p);
             ++w->fallbacks;
         }
         if (s > w->total[l]) {
@@ -1604,7 +1672,7 @@ static void pair_dp_team(ax_work *w, int nt, int k) {
             w->cut_t = i;
             best_predecessor_fast(w, l, &s, &p);
             if (dp_anomaly(w, l, i, s, maxsz)) {
-                best_predecessor(w, l, &s, &p);
+                best_predecessor_fallback(w, l, i, maxsz, &s, &p);
                 ++w->fallbacks;
             }
             tredo += mono_s() - t0;
@@ -1694,7 +1762,8 @@ static void pair_dp_host(ax_work *w) {
         pair_dp_fast(w);
 #ifdef GAC_DP_STATS
         fprintf(stderr, "[dp stats] fast DP: %lld of %d leaves searched again by the reference "
-                "order\n", w->fallbacks, w->nl);
+                "order (%.1f nodes visited each)\n", w->fallbacks, w->nl,
+                (double)g_st.ref_visits / (w->fallbacks ? w->fallbacks : 1));
         const double n = w->nl ? (double)w->nl : 1.0;
         fprintf(stderr, "[dp stats] fast: per leaf visits %.1f prune1 %.1f prune2 %.1f leaves %.2f "
                 "cands %.2f wins %.2f\n", g_st.visits / n, g_st.prune1 / n, g_st.prune2 / n,
