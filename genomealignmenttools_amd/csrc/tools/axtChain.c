@@ -246,7 +246,19 @@ static int psl_line(char *line, pairs *P, char *err, int *wc_out) {
         snprintf(err, 600, "requires PSLs to have implicit positive strand, found `%.400s'", strand);
         return PSL_E_MSG;
     }
-    pair *p = pair_get(P, w[9], strand, w[13]);
+    /* (consecutive records mostly share their pair: the last one is kept,
+     * by index, and its names compared before any key is built) */
+    static __thread const pairs *last_P;
+    static __thread int32_t last_i = -1;
+    pair *p;
+    if (last_P == P && last_i >= 0 && last_i < P->n && P->p[last_i].strand == strand[0] &&
+        strcmp(P->p[last_i].qname, w[9]) == 0 && strcmp(P->p[last_i].tname, w[13]) == 0) {
+        p = &P->p[last_i];
+    } else {
+        p = pair_get(P, w[9], strand, w[13]);
+        last_P = P;
+        last_i = (int32_t)(p - P->p);
+    }
     for (unsigned i = 0; i < block_count; ++i)
         pair_add(p, ts[i], qs[i], sz[i]);
     return 0;
