@@ -326,6 +326,8 @@ static void *psl_chunk_thread(void *arg) {
     return NULL;
 }
 
+static double wall(void);
+
 typedef struct merge_task {
     int32_t g;      /* the global pair */
     pair *lp;       /* a chunk's pair */
@@ -381,7 +383,9 @@ static void read_psl_chunks(rd *r, pairs *P) {
     }
     psl_job J = {K, n, 0};
     atomic_init(&J.next, 0);
+    const double tp = wall();
     gac_run_threads(gt_threads() < n ? gt_threads() : (n ? n : 1), psl_chunk_thread, &J);
+    gt_verbose(2, "[read_psl] %d chunks parsed in %.3f s\n", n, wall() - tp);
     /* merge in file order: the metadata and the first error as a sequential
      * read meets them; every chunk's pairs placed at their offsets in the
      * global pairs (serial: pair order is first-seen order), then the block
@@ -435,7 +439,9 @@ static void read_psl_chunks(rd *r, pairs *P) {
 /* readPslBlocks (:345-377) with pslxFileOpenWithUniqueMeta (psl.c:547-612) */
 static void read_psl(const char *path, pairs *P, FILE *out) {
     rd r;
+    const double t0 = wall();
     rd_open(&r, path, out);
+    gt_verbose(2, "[read_psl] file in memory after %.3f s\n", wall() - t0);
     char *line = rd_next(&r);
     if (!line) {
         fprintf(stderr, "%s is empty\n", path);
