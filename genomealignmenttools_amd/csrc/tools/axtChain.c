@@ -164,39 +164,44 @@ static void pair_add(pair *p, int32_t t, int32_t q, int32_t size) {
 }
 
 /* sqlUnsigned without aborting: 0 = ok */
+/* sqlUnsignedOrError (kent/src/lib/sqlNum.c:14-46): digits to the end,
+ * accumulated in unsigned arithmetic (wrapping as the reference does) */
 static int sql_unsigned_ok(const char *s, unsigned *v, char *err) {
-    char *end;
-    if (!isdigit((unsigned char)*s)) {
+    unsigned res = 0;
+    const char *p = s;
+    while (*p >= '0' && *p <= '9')
+        res = res * 10u + (unsigned)(*p++ - '0');
+    if (*p != 0 || p == s) {
         snprintf(err, 600, "invalid unsigned integer: \"%.400s\"", s);
         return -1;
     }
-    const unsigned long x = strtoul(s, &end, 10);
-    if (*end != 0) {
-        snprintf(err, 600, "invalid unsigned integer: \"%.400s\"", s);
-        return -1;
-    }
-    *v = (unsigned)x;
+    *v = res;
     return 0;
 }
 
 /* sqlUnsignedDynamicArray into a reusable buffer: 0 = ok */
 static int sql_uarray_ok(char *s, int32_t **a, int *cap, int *count, char *err) {
     int n = 0;
-    while (*s) {
-        char *c = strchr(s, ',');
-        if (c)
-            *c = 0;
+    while (*s) { /* (sqlUnsignedInList per item, kent/src/lib/sqlNum.c:56-85) */
+        unsigned res = 0;
+        char *q = s;
+        while (*q >= '0' && *q <= '9')
+            res = res * 10u + (unsigned)(*q++ - '0');
+        if ((*q != ',' && *q != 0) || q == s) {
+            char *c = strchr(s, ',');
+            if (c)
+                *c = 0;
+            snprintf(err, 600, "invalid unsigned integer: \"%.400s\"", s);
+            return -1;
+        }
         if (n == *cap) {
             *cap = *cap ? *cap * 2 : 64;
             *a = realloc(*a, (size_t)*cap * sizeof(int32_t));
         }
-        unsigned v;
-        if (sql_unsigned_ok(s, &v, err) != 0)
-            return -1;
-        (*a)[n++] = (int32_t)v;
-        if (!c)
+        (*a)[n++] = (int32_t)res;
+        if (*q == 0)
             break;
-        s = c + 1;
+        s = q + 1;
     }
     *count = n;
     return 0;
