@@ -3448,6 +3448,9 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
                 d0 = atoi(db) % nd;
             for (int64_t k = 0; k < big; ++k) {
                 int t = (int)((double)tt * psize[order[k]] / (double)sum + 0.5);
+                const char *t0v = getenv("GAC_DP_TEAM0"); /* (probe: the largest team's threads) */
+                if (k == 0 && t0v && atoi(t0v) >= 2 && atoi(t0v) <= tt - 2 * (int)(big - 1))
+                    t = atoi(t0v);
                 t = t < 2 ? 2 : t;
                 if (k == big - 1 || used + t > tt)
                     t = tt - used > 2 ? tt - used : 2;
