@@ -390,7 +390,8 @@ static void read_psl_chunks(rd *r, pairs *P) {
     atomic_init(&J.next, 0);
     const double tp = wall();
     gac_run_threads(gt_threads() < n ? gt_threads() : (n ? n : 1), psl_chunk_thread, &J);
-    gt_verbose(2, "[read_psl] %d chunks parsed in %.3f s\n", n, wall() - tp);
+    const double tpe = wall();
+    gt_verbose(2, "[read_psl] %d chunks parsed in %.3f s\n", n, tpe - tp);
     /* merge in file order: the metadata and the first error as a sequential
      * read meets them; every chunk's pairs placed at their offsets in the
      * global pairs (serial: pair order is first-seen order), then the block
@@ -430,7 +431,10 @@ static void read_psl_chunks(rd *r, pairs *P) {
         }
     }
     atomic_init(&M.next, 0);
+    const double tm = wall();
     gac_run_threads(gt_threads() < M.n ? gt_threads() : (M.n ? (int)M.n : 1), merge_thread, &M);
+    gt_verbose(2, "[read_psl] %lld chunk pairs placed %.3f s after the parse, copied in %.3f s\n",
+               (long long)M.n, tm - tpe, wall() - tm);
     free(M.t);
     for (int i = 0; i < n; ++i) {
         psl_chunk *k = &K[i];
@@ -439,6 +443,11 @@ static void read_psl_chunks(rd *r, pairs *P) {
         free(k->meta);
     }
     free(K);
+}
+
+static void *free_text(void *p) {
+    free(p);
+    return NULL;
 }
 
 /* readPslBlocks (:345-377) with pslxFileOpenWithUniqueMeta (psl.c:547-612) */
@@ -491,7 +500,15 @@ static void read_psl(const char *path, pairs *P, FILE *out) {
     }
     read_psl_chunks(&r, P);
     gt_names_free(&r.seen);
-    free(r.buf);
+    /* the text (GBs at C4) is released off the caller's path: unmapping 2.6 GB
+     * takes a core ~0.3 s */
+    pthread_t th;
+    pthread_attr_t at;
+    pthread_attr_init(&at);
+    pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
+    if (pthread_create(&th, &at, free_text, r.buf) != 0)
+        free(r.buf);
+    pthread_attr_destroy(&at);
 }
 
 static int need_num(rd *r, char **w, int i) {
