@@ -3081,18 +3081,23 @@ typedef struct gather_job {
     int32_t *bt, *bq, *bs;
     int64_t *c0, *x0; /* per pair: first chain, first block */
     int64_t np;
+    int64_t *task, ntask; /* (pair, first chain, end chain) */
     _Atomic int64_t next;
 } gather_job;
 
 static void *gather_thread(void *arg) {
     gather_job *G = arg;
     for (;;) {
-        const int64_t p = atomic_fetch_add(&G->next, 1);
-        if (p >= G->np)
+        const int64_t t = atomic_fetch_add(&G->next, 1);
+        if (t >= G->ntask)
             return NULL;
+        /* task t: chains [k0, k1) of pair p (a large pair's chains are
+         * several tasks, so one pair does not hold up the copy) */
+        const int64_t p = G->task[3 * t];
+        const int32_t k0 = (int32_t)G->task[3 * t + 1], k1 = (int32_t)G->task[3 * t + 2];
         const ax_out *o = &G->po[p];
-        int64_t c = G->c0[p], x = G->x0[p];
-        for (int32_t k = 0; k < o->n_chains; ++k, ++c) {
+        int64_t c = G->c0[p] + k0, x = G->x0[p] + o->coff[k0];
+        for (int32_t k = k0; k < k1; ++k, ++c) {
             G->ct[c] = G->in->t_seq[p];
             G->cq[c] = G->in->q_seq[p];
             G->cs[c] = G->in->q_strand[p] ? 1 : 0;
@@ -3539,17 +3544,31 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
         int32_t *gali = malloc((size_t)(nc ? nc : 1) * 4);
         /* every pair's chains into the set, pairs in parallel (disjoint
          * slots from prefix sums over the pairs) */
-        gather_job G = {po, in, ct, cq, cs, cpair, coff, bt, bq, bs, NULL, NULL, np, 0};
+        gather_job G;
+        memset(&G, 0, sizeof(G));
+        G.po = po, G.in = in, G.ct = ct, G.cq = cq, G.cs = cs, G.cpair = cpair, G.coff = coff;
+        G.bt = bt, G.bq = bq, G.bs = bs, G.np = np;
         G.c0 = malloc((size_t)(np + 1) * 8);
         G.x0 = malloc((size_t)(np + 1) * 8);
         G.c0[0] = G.x0[0] = 0;
+        int64_t nt_ = 0;
         for (int64_t p = 0; p < np; ++p) {
             G.c0[p + 1] = G.c0[p] + po[p].n_chains;
             G.x0[p + 1] = G.x0[p] + (po[p].coff ? po[p].coff[po[p].n_chains] : 0);
+            nt_ += (po[p].n_chains + 4095) / 4096;
         }
+        G.task = malloc((size_t)(nt_ ? nt_ : 1) * 3 * sizeof(int64_t));
+        for (int64_t p = 0; p < np; ++p)
+            for (int32_t k = 0; k < po[p].n_chains; k += 4096) {
+                G.task[3 * G.ntask] = p;
+                G.task[3 * G.ntask + 1] = k;
+                G.task[3 * G.ntask + 2] = k + 4096 < po[p].n_chains ? k + 4096 : po[p].n_chains;
+                ++G.ntask;
+            }
         coff[0] = 0;
         atomic_init(&G.next, 0);
-        run_threads(nthreads < np ? nthreads : (int)(np ? np : 1), gather_thread, &G);
+        run_threads(nthreads < G.ntask ? nthreads : (int)(G.ntask ? G.ntask : 1), gather_thread, &G);
+        free(G.task);
         free(G.c0);
         free(G.x0);
         gac_chainset_desc d = {nc, ct, cq, cs, coff, ncb, bt, bq, bs};
@@ -3571,7 +3590,7 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
                     k[nk] = (dkey){(double)gsc[i], (int32_t)nk, (int32_t)i};
                     ++nk;
                 }
-            qsort(k, (size_t)nk, sizeof(dkey), dkey_cmp_desc);
+            sort_desc16(k, nk, nthreads); /* (ranks in list order: the stable sort) */
             R = calloc(1, sizeof(*R));
             R->n_chains = nk;
             R->score = malloc((size_t)(nk ? nk : 1) * sizeof(double));
