@@ -122,13 +122,25 @@ typedef struct pair {
     char *qname, *tname;
     char strand;
     int64_t nb, cap;
+    int64_t deferred; /* of nb, the blocks still in PSL chunk runs (pairs.defer) */
     int32_t *bt, *bq, *bs;
 } pair;
+
+typedef struct merge_task {
+    int32_t g;                 /* the global pair */
+    int64_t off, nb;           /* where a chunk's run goes among the pair's blocks */
+    int32_t *bt, *bq, *bs;     /* the run (the chunk's arrays) */
+    char *qname, *tname;       /* the chunk pair's names, freed with the run */
+} merge_task;
 
 typedef struct pairs {
     gt_names keys;   /* "qName<strand>tName" -> index (hashAddSaveName) */
     pair *p;
     int32_t n, cap;
+    /* PSL input: each pair's blocks past its own arrays stay as chunk runs
+     * until they are copied once, straight into the chaining input */
+    merge_task *defer;
+    int64_t ndefer;
 } pairs;
 
 static pair *pair_get(pairs *P, const char *qname, const char *strand, const char *tname) {
@@ -333,16 +345,15 @@ static void *psl_chunk_thread(void *arg) {
 
 static double wall(void);
 
-typedef struct merge_task {
-    int32_t g;      /* the global pair */
-    pair *lp;       /* a chunk's pair */
-    int64_t off;    /* where its blocks go in the global pair's arrays */
-} merge_task;
-
+/* the chaining input's block columns filled from the pairs: each deferred
+ * chunk run copied once, on all threads, to its pair's slice (pairs not on
+ * this rank only freed) */
 typedef struct merge_job {
-    pairs *P;
-    merge_task *t;
+    const merge_task *t;
     int64_t n;
+    const int32_t *pos;   /* global pair -> its index in the input, or -1 */
+    const int64_t *moff;  /* input index -> first block */
+    int32_t *bt, *bq, *bs;
     _Atomic int64_t next;
 } merge_job;
 
@@ -350,15 +361,18 @@ static void *merge_thread(void *arg) {
     merge_job *M = arg;
     for (int64_t i; (i = atomic_fetch_add(&M->next, 1)) < M->n;) {
         const merge_task *t = &M->t[i];
-        pair *gp = &M->P->p[t->g], *lp = t->lp;
-        memcpy(gp->bt + t->off, lp->bt, (size_t)lp->nb * 4);
-        memcpy(gp->bq + t->off, lp->bq, (size_t)lp->nb * 4);
-        memcpy(gp->bs + t->off, lp->bs, (size_t)lp->nb * 4);
-        free(lp->bt);
-        free(lp->bq);
-        free(lp->bs);
-        free(lp->qname);
-        free(lp->tname);
+        const int32_t k = M->pos[t->g];
+        if (k >= 0) {
+            const int64_t o = M->moff[k] + t->off;
+            memcpy(M->bt + o, t->bt, (size_t)t->nb * 4);
+            memcpy(M->bq + o, t->bq, (size_t)t->nb * 4);
+            memcpy(M->bs + o, t->bs, (size_t)t->nb * 4);
+        }
+        free(t->bt);
+        free(t->bq);
+        free(t->bs);
+        free(t->qname);
+        free(t->tname);
     }
     return NULL;
 }
@@ -394,8 +408,8 @@ static void read_psl_chunks(rd *r, pairs *P) {
     gt_verbose(2, "[read_psl] %d chunks parsed in %.3f s\n", n, tpe - tp);
     /* merge in file order: the metadata and the first error as a sequential
      * read meets them; every chunk's pairs placed at their offsets in the
-     * global pairs (serial: pair order is first-seen order), then the block
-     * runs copied on all threads */
+     * global pairs (serial: pair order is first-seen order); the block runs
+     * stay where the parse left them (copied once, into the chaining input) */
     int64_t line0 = r->line, ntask = 0;
     for (int i = 0; i < n; ++i) {
         psl_chunk *k = &K[i];
@@ -407,35 +421,24 @@ static void read_psl_chunks(rd *r, pairs *P) {
         ntask += k->P.n;
     }
     r->line = (int)line0;
-    merge_job M;
-    M.P = P;
-    M.t = malloc((size_t)(ntask ? ntask : 1) * sizeof(merge_task));
-    M.n = 0;
+    merge_task *T = realloc(P->defer, (size_t)(P->ndefer + ntask + 1) * sizeof(merge_task));
+    int64_t nt = P->ndefer;
     for (int i = 0; i < n; ++i) {
         psl_chunk *k = &K[i];
         for (int32_t j = 0; j < k->P.n; ++j) {
             pair *lp = &k->P.p[j];
             const char strand[2] = {lp->strand, 0};
             pair *gp = pair_get(P, lp->qname, strand, lp->tname);
-            M.t[M.n++] = (merge_task){(int32_t)(gp - P->p), lp, gp->nb};
-            gp->nb += lp->nb; /* (reserved: the copy follows) */
+            T[nt++] = (merge_task){(int32_t)(gp - P->p), gp->nb, lp->nb, lp->bt, lp->bq, lp->bs,
+                                   lp->qname, lp->tname};
+            gp->nb += lp->nb;
+            gp->deferred += lp->nb;
         }
     }
-    for (int32_t g = 0; g < P->n; ++g) {
-        pair *gp = &P->p[g];
-        if (gp->nb > gp->cap) {
-            gp->cap = gp->nb;
-            gp->bt = realloc(gp->bt, (size_t)gp->cap * 4);
-            gp->bq = realloc(gp->bq, (size_t)gp->cap * 4);
-            gp->bs = realloc(gp->bs, (size_t)gp->cap * 4);
-        }
-    }
-    atomic_init(&M.next, 0);
-    const double tm = wall();
-    gac_run_threads(gt_threads() < M.n ? gt_threads() : (M.n ? (int)M.n : 1), merge_thread, &M);
-    gt_verbose(2, "[read_psl] %lld chunk pairs placed %.3f s after the parse, copied in %.3f s\n",
-               (long long)M.n, tm - tpe, wall() - tm);
-    free(M.t);
+    P->defer = T;
+    P->ndefer = nt;
+    gt_verbose(2, "[read_psl] %lld chunk pairs placed %.3f s after the parse\n", (long long)ntask,
+               wall() - tpe);
     for (int i = 0; i < n; ++i) {
         psl_chunk *k = &K[i];
         free(k->P.p);
@@ -975,11 +978,31 @@ static void run_job(int argc, char *argv[], ax_batch *B) {
     const int64_t nb = moff[nm];
     int32_t *bt = malloc((size_t)(nb ? nb : 1) * 4), *bq = malloc((size_t)(nb ? nb : 1) * 4),
             *bs = malloc((size_t)(nb ? nb : 1) * 4);
-    for (int64_t k = 0; k < nm; ++k) {
-        const pair *p = ord[mine[k]];
-        memcpy(bt + moff[k], p->bt, (size_t)p->nb * 4);
-        memcpy(bq + moff[k], p->bq, (size_t)p->nb * 4);
-        memcpy(bs + moff[k], p->bs, (size_t)p->nb * 4);
+    {
+        /* each pair's own blocks first (all of them from an axt file, the
+         * first line's from a PSL), then the PSL chunk runs at their offsets */
+        int32_t *pos = malloc((size_t)(np ? np : 1) * 4);
+        for (int64_t i = 0; i < np; ++i)
+            pos[i] = -1;
+        for (int64_t k = 0; k < nm; ++k) {
+            const pair *p = ord[mine[k]];
+            const int64_t own = p->nb - p->deferred;
+            pos[p - P.p] = (int32_t)k;
+            memcpy(bt + moff[k], p->bt, (size_t)own * 4);
+            memcpy(bq + moff[k], p->bq, (size_t)own * 4);
+            memcpy(bs + moff[k], p->bs, (size_t)own * 4);
+        }
+        merge_job M = {P.defer, P.ndefer, pos, moff, bt, bq, bs};
+        atomic_init(&M.next, 0);
+        const double tm = wall();
+        const int nth = gt_threads() < M.n ? gt_threads() : (M.n ? (int)M.n : 1);
+        gac_run_threads(nth, merge_thread, &M);
+        gt_verbose(2, "[input] %lld blocks gathered from %lld chunk runs in %.3f s\n", (long long)nb,
+                   (long long)M.n, wall() - tm);
+        free(P.defer);
+        P.defer = NULL;
+        P.ndefer = 0;
+        free(pos);
     }
     gt_verbose(2, "device + genomes in %.3f s\n", wall() - t0);
     t0 = wall();
