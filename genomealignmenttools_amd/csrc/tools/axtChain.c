@@ -354,6 +354,8 @@ typedef struct merge_job {
     const int32_t *pos;   /* global pair -> its index in the input, or -1 */
     const int64_t *moff;  /* input index -> first block */
     int32_t *bt, *bq, *bs;
+    int release; /* free the runs as they are copied (batch jobs; a single
+                  * run leaves them to process exit, as its other arrays) */
     _Atomic int64_t next;
 } merge_job;
 
@@ -368,6 +370,8 @@ static void *merge_thread(void *arg) {
             memcpy(M->bq + o, t->bq, (size_t)t->nb * 4);
             memcpy(M->bs + o, t->bs, (size_t)t->nb * 4);
         }
+        if (!M->release)
+            continue;
         free(t->bt);
         free(t->bq);
         free(t->bs);
@@ -992,7 +996,7 @@ static void run_job(int argc, char *argv[], ax_batch *B) {
             memcpy(bq + moff[k], p->bq, (size_t)own * 4);
             memcpy(bs + moff[k], p->bs, (size_t)own * 4);
         }
-        merge_job M = {P.defer, P.ndefer, pos, moff, bt, bq, bs};
+        merge_job M = {P.defer, P.ndefer, pos, moff, bt, bq, bs, B->on};
         atomic_init(&M.next, 0);
         const double tm = wall();
         const int nth = gt_threads() < M.n ? gt_threads() : (M.n ? (int)M.n : 1);
