@@ -54,10 +54,9 @@ hipError_t launch_build_flat(const int32_t *bt, const int32_t *bq, const int32_t
                              int32_t *tile_c0, int4 *crun, const longlong2 *t_runs,
                              int64_t n_trun, const longlong2 *q_runs, int64_t n_qrun,
                              const int64_t *q_woff, int4 *blk, int2 *tspan, uint32_t *bucket,
-                             hipStream_t s);
+                             const UploadGaps &G, hipStream_t s);
 hipError_t launch_block_gaps_flat(const int32_t *coff, const int32_t *tile_c0, int64_t nb,
-                                  int4 *blk, Blk12 *blk12, const GapDev &g, const int32_t *small,
-                                  const int32_t *tab, int len, hipStream_t s);
+                                  int4 *blk, Blk12 *blk12, const UploadGaps &G, hipStream_t s);
 hipError_t launch_scatter(const SparseRun *runs, int64_t n, const uint64_t *compact,
                           uint64_t *raw, hipStream_t s);
 hipError_t launch_blocks(const ScoreArgs &a, const BlockJob *jobs, int64_t n, int32_t *out,
@@ -1375,6 +1374,17 @@ static hipError_t ensure_buf(void **p, size_t *cap, size_t want, size_t sz) {
 }
 
 // the chain set's contents := d (its device buffers reused where they fit)
+// the context's scoring setup, as the upload kernels take it
+static UploadGaps upload_gaps(const gac_ctx *c, Blk12 *blk12) {
+    UploadGaps G;
+    G.blk12 = blk12;
+    G.g = c->gap;
+    G.small = c->d_small;
+    G.tab = c->d_gap_tab;
+    G.len = c->gap_len;
+    return G;
+}
+
 static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs) {
     if (!c->g[0].final || !c->g[1].final)
         return gac_fail(GAC_E_STATE, "load both genomes before uploading chains");
@@ -1495,11 +1505,21 @@ static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs)
         e = ensure_buf((void **)&cs->d_tile_c0, &cs->cap_tile_c0, (size_t)(ntiles + 1), sizeof(int32_t));
     if (e == hipSuccess)
         e = ensure_buf((void **)&cs->d_crun, &cs->cap_crun, (size_t)(n ? n : 1), sizeof(int4));
+    // with the scoring already set, the block gaps and 12-byte records come
+    // out of the same pass (GAC_UP_FUSE=0: at the first scoring call, as
+    // when the scoring follows the chains)
+    static const bool fuse = [] {
+        const char *v = getenv("GAC_UP_FUSE");
+        return !(v && v[0] == '0');
+    }();
+    const bool gaps = fuse && c->scoring;
+    const UploadGaps G = gaps ? upload_gaps(c, cs->blk12) : UploadGaps{};
     if (e == hipSuccess && rc == GAC_OK)
         e = launch_build_flat(d_bt, d_bt + nb, d_bt + 2 * nb, (int64_t)nb, cs->chains, n, cs->d_coff,
                               cs->d_tile_c0, cs->d_crun, c->g[0].d_nrun, c->g[0].n_nrun,
                               c->g[1].d_nrun, c->g[1].n_nrun, c->g[1].d_woff, cs->blk, cs->tspan,
-                              cs->bucket, c->stream);
+                              cs->bucket, G, c->stream);
+    if (e == hipSuccess && rc == GAC_OK && gaps) cs->gap_version = c->gap_version;
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     lap("device build + sync");
     if (rc != GAC_OK) return rc;
@@ -1679,7 +1699,7 @@ static int prepare_args(gac_ctx *c, const gac_chainset *cs, int64_t n, uint32_t 
     if (n == 0) return GAC_OK;
     if (cs->gap_version != c->gap_version) {  // blk[].w for this scoring setup
         HIPCHK(launch_block_gaps_flat(cs->d_coff, cs->d_tile_c0, cs->n_blocks, cs->blk, cs->blk12,
-                                      c->gap, c->d_small, c->d_gap_tab, c->gap_len, s));
+                                      upload_gaps(c, cs->blk12), s));
         const_cast<gac_chainset *>(cs)->gap_version = c->gap_version;
     }
     memset(&a, 0, sizeof(a));

@@ -77,6 +77,15 @@ struct GapDev {
     double long_val[3][kMaxLong];
 };
 
+// A scoring setup's gap costs for the upload kernels (k_block_gaps_flat, and
+// k_build_flat when the setup precedes the chains): blk12 null = none.
+struct UploadGaps {
+    Blk12 *blk12;
+    GapDev g;
+    const int32_t *small, *tab;
+    int len;
+};
+
 // Per-range descriptor written by k_plan (two 16-B loads in k_tile).
 struct RangeDesc {
     int64_t tbase;   // global base index of the target sequence start (word_off * 32)

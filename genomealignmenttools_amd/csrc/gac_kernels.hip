@@ -305,7 +305,10 @@ __device__ __forceinline__ int64_t owner_chain(const int32_t *coff, const int32_
 // over more than kStage chains (a run of empty chains) returns false: its
 // lanes take owner_chain's global search.  Each lane takes kUpPer blocks, so
 // the staging round trip is paid once per 4 kUpPer tiles.
-constexpr int kStage = 256, kUpPer = 2;
+#ifndef GAC_UP_PER
+#define GAC_UP_PER 2  // (A/B probes: make variant VFLAGS=-DGAC_UP_PER=4)
+#endif
+constexpr int kStage = 256, kUpPer = GAC_UP_PER;
 struct ChainStage {
     int32_t c0, m;  // (every lane's own copy: workgroup-uniform values)
     int32_t *off;   // [m + 1] in LDS
@@ -385,11 +388,34 @@ __global__ void __launch_bounds__(256) k_tile_chain(const int32_t *coff, int64_t
     tile_c0[t] = (int32_t)lo;
 }
 
-// one lane per block: the block record {tStart, qStart, size | N flags, 0},
+// the 12-byte scoring record of a block {t, q, size | N flags} with the gap
+// cost to its successor (k_tile reads the 16-byte record of a wide one)
+__device__ __forceinline__ Blk12 blk12_of(int t, int q, int zf, int cost) {
+    const int z = zf & kSizeMask;
+    const bool wide = z >= kB12Wide || cost < 0 || cost >= kB12GapMax;
+    Blk12 r;
+    r.t = t;
+    r.q = q;
+    r.w = (wide ? (uint32_t)kB12Wide : ((uint32_t)z | ((uint32_t)cost << 12))) |
+          ((uint32_t)(zf & (kTHasN | kQHasN)) << 1);
+    return r;
+}
+
+// the gap cost between a block and its successor {nt, nq} in the chain
+__device__ __forceinline__ int block_gap(const UploadGaps &G, int t, int q, int z, int nt, int nq) {
+    int d;
+    const int which = gap_kind(nq - (q + z), nt - (t + z), d);
+    return d < G.len ? G.tab[which * G.len + d] : gap_cost_wd(G.g, G.small, which, d);
+}
+
+// one lane per block: the block record {tStart, qStart, size | N flags, gap},
 // its target span, the N flags (blocks of chains whose span meets a run,
 // against the same sorted run lists), and the bucket entries it owns (block
 // k of a chain is bucket j's first block with tEnd past the bucket start
-// for the buckets starting in [tEnd(k-1), tEnd(k)))
+// for the buckets starting in [tEnd(k-1), tEnd(k))).  GAPS (the scoring is
+// set when the chains arrive): the gap costs and the 12-byte records too,
+// k_block_gaps_flat's pass folded in; otherwise gap 0 until it runs.
+template <bool GAPS>
 __global__ void __launch_bounds__(256) k_build_flat(const int32_t *bt, const int32_t *bq,
                                                     const int32_t *bs, int64_t nb,
                                                     const DChain *chains, const int32_t *coff,
@@ -397,7 +423,8 @@ __global__ void __launch_bounds__(256) k_build_flat(const int32_t *bt, const int
                                                     const int4 *crun, const longlong2 *t_runs,
                                                     int64_t n_trun, const longlong2 *q_runs,
                                                     int64_t n_qrun, const int64_t *q_woff,
-                                                    int4 *blk, int2 *tspan, uint32_t *bucket) {
+                                                    int4 *blk, int2 *tspan, uint32_t *bucket,
+                                                    UploadGaps G) {
     __shared__ int32_t s_off[kStage + 1];
     __shared__ int64_t s_tbase[kStage], s_idx[kStage];
     __shared__ int32_t s_ts[kStage], s_te[kStage], s_sh[kStage], s_qseq[kStage], s_qinfo[kStage];
@@ -437,18 +464,18 @@ __global__ void __launch_bounds__(256) k_build_flat(const int32_t *bt, const int
             }
             continue;
         }
-        int64_t tbase, idx_off, coff_c;
+        int64_t tbase, idx_off, coff_c, coff_n;
         int tstart, tend, shift, q_seq, qinfo;
         int4 rr;
         if (staged) {
             const int j = staged_chain(S, b);
-            tbase = s_tbase[j], idx_off = s_idx[j], coff_c = S.off[j];
+            tbase = s_tbase[j], idx_off = s_idx[j], coff_c = S.off[j], coff_n = S.off[j + 1];
             tstart = s_ts[j], tend = s_te[j], shift = s_sh[j], q_seq = s_qseq[j], qinfo = s_qinfo[j];
             rr = s_run[j];
         } else {
             const int64_t c = owner_chain(coff, tile_c0, ntiles, b);
             const DChain ch = chains[c];
-            tbase = ch.tbase, idx_off = ch.idx_off, coff_c = coff[c];
+            tbase = ch.tbase, idx_off = ch.idx_off, coff_c = coff[c], coff_n = coff[c + 1];
             tstart = ch.tstart, tend = ch.tend, shift = ch.shift, q_seq = ch.q_seq, qinfo = ch.qinfo;
             rr = crun ? crun[c] : make_int4(0, 0, 0, 0);
         }
@@ -462,7 +489,12 @@ __global__ void __launch_bounds__(256) k_build_flat(const int32_t *bt, const int
                 if (span_meets(q_runs, rr.z, rr.w, qb + qf, qb + qf + z[i])) flags |= kQHasN;
             }
         }
-        blk[b] = make_int4(t[i], q[i], z[i] | flags, 0);
+        int cost = 0;
+        if (GAPS) {
+            if (b + 1 < coff_n) cost = block_gap(G, t[i], q[i], z[i], bt[b + 1], bq[b + 1]);
+            G.blk12[b] = blk12_of(t[i], q[i], z[i] | flags, cost);
+        }
+        blk[b] = make_int4(t[i], q[i], z[i] | flags, cost);
         tspan[b] = make_int2(t[i], t[i] + z[i]);
         const int64_t k = b - coff_c;
         const int64_t span = (int64_t)tend - tstart;
@@ -481,8 +513,7 @@ __global__ void __launch_bounds__(256) k_build_flat(const int32_t *bt, const int
 __global__ void __launch_bounds__(256) k_block_gaps_flat(const int32_t *coff,
                                                          const int32_t *tile_c0, int64_t ntiles,
                                                          int64_t nb, int4 *blk, Blk12 *blk12,
-                                                         GapDev g, const int32_t *small,
-                                                         const int32_t *tab, int len) {
+                                                         UploadGaps G) {
     __shared__ int32_t s_off[kStage + 1];
     const int64_t B0 = (int64_t)blockIdx.x * blockDim.x * kUpPer;
     int4 x[kUpPer];
@@ -504,18 +535,10 @@ __global__ void __launch_bounds__(256) k_block_gaps_flat(const int32_t *coff,
         int cost = 0;
         if (b + 1 < next) {
             const int4 y = blk[b + 1];
-            int d;
-            const int which = gap_kind(y.y - (x[i].y + z), y.x - (x[i].x + z), d);
-            cost = d < len ? tab[which * len + d] : gap_cost_wd(g, small, which, d);
+            cost = block_gap(G, x[i].x, x[i].y, z, y.x, y.y);
         }
         blk[b] = make_int4(x[i].x, x[i].y, x[i].z, cost);
-        const bool wide = z >= kB12Wide || cost < 0 || cost >= kB12GapMax;
-        Blk12 r;
-        r.t = x[i].x;
-        r.q = x[i].y;
-        r.w = (wide ? (uint32_t)kB12Wide : ((uint32_t)z | ((uint32_t)cost << 12))) |
-              ((uint32_t)(x[i].z & (kTHasN | kQHasN)) << 1);
-        blk12[b] = r;
+        blk12[b] = blk12_of(x[i].x, x[i].y, x[i].z, cost);
     }
 }
 
@@ -2065,7 +2088,7 @@ hipError_t launch_build_flat(const int32_t *bt, const int32_t *bq, const int32_t
                              int32_t *tile_c0, int4 *crun, const longlong2 *t_runs,
                              int64_t n_trun, const longlong2 *q_runs, int64_t n_qrun,
                              const int64_t *q_woff, int4 *blk, int2 *tspan, uint32_t *bucket,
-                             hipStream_t s) {
+                             const UploadGaps &G, hipStream_t s) {
     const int64_t ntiles = (nb + 63) >> 6;
     if (n_chains > 0) {
         hipLaunchKernelGGL(k_chain_prep, dim3((unsigned)((n_chains + 255) / 256)), dim3(256), 0, s,
@@ -2075,19 +2098,23 @@ hipError_t launch_build_flat(const int32_t *bt, const int32_t *bq, const int32_t
                            s, coff, n_chains, ntiles, tile_c0);
     }
     const int64_t g = (nb + 8 + 256 * kUpPer - 1) / (256 * kUpPer);
-    hipLaunchKernelGGL(k_build_flat, dim3((unsigned)g), dim3(256), 0, s, bt, bq, bs, nb, chains,
-                       coff, tile_c0, ntiles, (n_trun || n_qrun) ? crun : nullptr, t_runs, n_trun,
-                       q_runs, n_qrun, q_woff, blk, tspan, bucket);
+    if (G.blk12)
+        hipLaunchKernelGGL(k_build_flat<true>, dim3((unsigned)g), dim3(256), 0, s, bt, bq, bs, nb,
+                           chains, coff, tile_c0, ntiles, (n_trun || n_qrun) ? crun : nullptr,
+                           t_runs, n_trun, q_runs, n_qrun, q_woff, blk, tspan, bucket, G);
+    else
+        hipLaunchKernelGGL(k_build_flat<false>, dim3((unsigned)g), dim3(256), 0, s, bt, bq, bs, nb,
+                           chains, coff, tile_c0, ntiles, (n_trun || n_qrun) ? crun : nullptr,
+                           t_runs, n_trun, q_runs, n_qrun, q_woff, blk, tspan, bucket, G);
     return hipGetLastError();
 }
 
 hipError_t launch_block_gaps_flat(const int32_t *coff, const int32_t *tile_c0, int64_t nb,
-                                  int4 *blk, Blk12 *blk12, const GapDev &g, const int32_t *small,
-                                  const int32_t *tab, int len, hipStream_t s) {
+                                  int4 *blk, Blk12 *blk12, const UploadGaps &G, hipStream_t s) {
     if (nb == 0) return hipSuccess;
     hipLaunchKernelGGL(k_block_gaps_flat, dim3((unsigned)((nb + 256 * kUpPer - 1) / (256 * kUpPer))),
                        dim3(256), 0, s, coff,
-                       tile_c0, (nb + 63) >> 6, nb, blk, blk12, g, small, tab, len);
+                       tile_c0, (nb + 63) >> 6, nb, blk, blk12, G);
     return hipGetLastError();
 }
 
