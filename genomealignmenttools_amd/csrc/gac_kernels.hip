@@ -308,6 +308,9 @@ __device__ __forceinline__ int64_t owner_chain(const int32_t *coff, const int32_
 #ifndef GAC_UP_PER
 #define GAC_UP_PER 2  // (A/B probes: make variant VFLAGS=-DGAC_UP_PER=4)
 #endif
+#ifndef GAC_UP_PROBE
+#define GAC_UP_PROBE 0  // (timing probes only: 1 no bucket entries, 2 no N flags, 4 no 12-B records / spans)
+#endif
 constexpr int kStage = 256, kUpPer = GAC_UP_PER;
 struct ChainStage {
     int32_t c0, m;  // (every lane's own copy: workgroup-uniform values)
@@ -429,6 +432,8 @@ __global__ void __launch_bounds__(256) k_build_flat(const int32_t *bt, const int
     __shared__ int64_t s_tbase[kStage], s_idx[kStage];
     __shared__ int32_t s_ts[kStage], s_te[kStage], s_sh[kStage], s_qseq[kStage], s_qinfo[kStage];
     __shared__ int4 s_run[kStage];
+    __shared__ int64_t s_pre[256], s_dst[256];
+    __shared__ uint32_t s_val[256];
     const int64_t B0 = (int64_t)blockIdx.x * blockDim.x * kUpPer;
     int t[kUpPer], q[kUpPer], z[kUpPer];
 #pragma unroll
@@ -457,54 +462,79 @@ __global__ void __launch_bounds__(256) k_build_flat(const int32_t *bt, const int
 #pragma unroll
     for (int i = 0; i < kUpPer; ++i) {
         const int64_t b = B0 + i * (int64_t)blockDim.x + threadIdx.x;
+        int64_t cnt = 0, dst = 0;  // this block's bucket entries: cnt from bucket[dst]
+        uint32_t val = 0;
         if (b >= nb) {
             if (b < nb + 8) {  // padding: a window search may read 8 past a chain
                 tspan[b] = make_int2(0x7fffffff, 0x7fffffff);
                 blk[b] = make_int4(0x7fffffff, 0, 0, 0);
             }
-            continue;
-        }
-        int64_t tbase, idx_off, coff_c, coff_n;
-        int tstart, tend, shift, q_seq, qinfo;
-        int4 rr;
-        if (staged) {
-            const int j = staged_chain(S, b);
-            tbase = s_tbase[j], idx_off = s_idx[j], coff_c = S.off[j], coff_n = S.off[j + 1];
-            tstart = s_ts[j], tend = s_te[j], shift = s_sh[j], q_seq = s_qseq[j], qinfo = s_qinfo[j];
-            rr = s_run[j];
         } else {
-            const int64_t c = owner_chain(coff, tile_c0, ntiles, b);
-            const DChain ch = chains[c];
-            tbase = ch.tbase, idx_off = ch.idx_off, coff_c = coff[c], coff_n = coff[c + 1];
-            tstart = ch.tstart, tend = ch.tend, shift = ch.shift, q_seq = ch.q_seq, qinfo = ch.qinfo;
-            rr = crun ? crun[c] : make_int4(0, 0, 0, 0);
-        }
-        int flags = 0;  // (a block searches only the runs its chain's span meets)
-        if (z[i] > 0) {
-            if (rr.y > rr.x && span_meets(t_runs, rr.x, rr.y, tbase + t[i], tbase + t[i] + z[i]))
-                flags |= kTHasN;
-            if (rr.w > rr.z) {
-                const int64_t qb = q_woff[q_seq] * 32;
-                const int64_t qf = qinfo < 0 ? (int64_t)(qinfo & 0x7fffffff) - q[i] - z[i] : q[i];
-                if (span_meets(q_runs, rr.z, rr.w, qb + qf, qb + qf + z[i])) flags |= kQHasN;
+            int64_t tbase, idx_off, coff_c, coff_n;
+            int tstart, tend, shift, q_seq, qinfo;
+            int4 rr;
+            if (staged) {
+                const int j = staged_chain(S, b);
+                tbase = s_tbase[j], idx_off = s_idx[j], coff_c = S.off[j], coff_n = S.off[j + 1];
+                tstart = s_ts[j], tend = s_te[j], shift = s_sh[j], q_seq = s_qseq[j], qinfo = s_qinfo[j];
+                rr = s_run[j];
+            } else {
+                const int64_t c = owner_chain(coff, tile_c0, ntiles, b);
+                const DChain ch = chains[c];
+                tbase = ch.tbase, idx_off = ch.idx_off, coff_c = coff[c], coff_n = coff[c + 1];
+                tstart = ch.tstart, tend = ch.tend, shift = ch.shift, q_seq = ch.q_seq, qinfo = ch.qinfo;
+                rr = crun ? crun[c] : make_int4(0, 0, 0, 0);
             }
+            int flags = 0;  // (a block searches only the runs its chain's span meets)
+            if (!(GAC_UP_PROBE & 2) && z[i] > 0) {
+                if (rr.y > rr.x && span_meets(t_runs, rr.x, rr.y, tbase + t[i], tbase + t[i] + z[i]))
+                    flags |= kTHasN;
+                if (rr.w > rr.z) {
+                    const int64_t qb = q_woff[q_seq] * 32;
+                    const int64_t qf = qinfo < 0 ? (int64_t)(qinfo & 0x7fffffff) - q[i] - z[i] : q[i];
+                    if (span_meets(q_runs, rr.z, rr.w, qb + qf, qb + qf + z[i])) flags |= kQHasN;
+                }
+            }
+            int cost = 0;
+            if (GAPS) {
+                if (b + 1 < coff_n) cost = block_gap(G, t[i], q[i], z[i], bt[b + 1], bq[b + 1]);
+                if (!(GAC_UP_PROBE & 4)) G.blk12[b] = blk12_of(t[i], q[i], z[i] | flags, cost);
+            }
+            blk[b] = make_int4(t[i], q[i], z[i] | flags, cost);
+            if (!(GAC_UP_PROBE & 4)) tspan[b] = make_int2(t[i], t[i] + z[i]);
+            const int64_t k = b - coff_c;
+            const int64_t span = (int64_t)tend - tstart;
+            const int64_t nbk = span > 0 ? ((span - 1) >> shift) + 1 : 0;
+            const int64_t round = ((int64_t)1 << shift) - 1;
+            const int64_t k0 = k ? ((int64_t)bt[b - 1] + bs[b - 1] - tstart + round) >> shift : 0;
+            int64_t k1 = ((int64_t)t[i] + z[i] - tstart + round) >> shift;
+            if (k1 > nbk) k1 = nbk;
+            if (!(GAC_UP_PROBE & 1) && k1 > k0) cnt = k1 - k0, dst = idx_off + k0, val = (uint32_t)k;
         }
-        int cost = 0;
-        if (GAPS) {
-            if (b + 1 < coff_n) cost = block_gap(G, t[i], q[i], z[i], bt[b + 1], bq[b + 1]);
-            G.blk12[b] = blk12_of(t[i], q[i], z[i] | flags, cost);
+        // the wave's bucket entries, lane-strided: a block after a wide gap
+        // owns many, and a loop per block left the other lanes idle.  Entry e
+        // of the wave belongs to the last lane whose exclusive count is <= e.
+        const int lane = threadIdx.x & 63, wb = threadIdx.x & ~63;
+        int64_t pre = cnt;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t y = __shfl_up(pre, o, 64);
+            if (lane >= o) pre += y;
         }
-        blk[b] = make_int4(t[i], q[i], z[i] | flags, cost);
-        tspan[b] = make_int2(t[i], t[i] + z[i]);
-        const int64_t k = b - coff_c;
-        const int64_t span = (int64_t)tend - tstart;
-        const int64_t nbk = span > 0 ? ((span - 1) >> shift) + 1 : 0;
-        const int64_t round = ((int64_t)1 << shift) - 1;
-        const int64_t k0 = k ? ((int64_t)bt[b - 1] + bs[b - 1] - tstart + round) >> shift : 0;
-        int64_t k1 = ((int64_t)t[i] + z[i] - tstart + round) >> shift;
-        if (k1 > nbk) k1 = nbk;
-        uint32_t *bk = bucket + idx_off;
-        for (int64_t j = k0; j < k1; ++j) bk[j] = (uint32_t)k;
+        const int64_t tot = __shfl(pre, 63, 64);
+        s_pre[threadIdx.x] = pre - cnt;
+        s_dst[threadIdx.x] = dst;
+        s_val[threadIdx.x] = val;
+        __syncthreads();
+        for (int64_t e = lane; e < tot; e += 64) {
+            int lo = 0, hi = 63;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (s_pre[wb + mid] <= e) lo = mid;
+                else hi = mid - 1;
+            }
+            bucket[s_dst[wb + lo] + (e - s_pre[wb + lo])] = s_val[wb + lo];
+        }
+        __syncthreads();  // (the next round's entries reuse the arrays)
     }
 }
 

@@ -50,6 +50,34 @@ def test_ranges_vs_oracle(seed):
     assert np.array_equal(a, oa)
 
 
+@pytest.mark.parametrize("order", ["scoring-first", "chains-first"])
+def test_scoring_before_and_after_upload(order):
+    """The block gap costs come from the upload pass when the scoring is set
+    first (k_build_flat<true>), else from k_block_gaps_flat at the first
+    scoring call; a new scoring setup recomputes them.  Both orders, and a
+    switch of gap table and matrix between calls, agree with the oracle."""
+    from genomealignmenttools_amd import synth
+    from genomealignmenttools_amd.gachain import GAC_Q, GAC_T, Engine, GapCosts
+    tg, qg, ca = synth.small_case(seed=11, n_chains=300, max_blocks=800)
+    R = _ranges(ca, np.random.default_rng(11))
+    e = Engine(0)
+    e.add_sequences(GAC_T, tg.seq_records())
+    e.add_sequences(GAC_Q, qg.seq_records())
+    if order == "scoring-first":
+        e.set_scoring(np.asarray(BLASTZ, np.int32), GapCosts("loose"))
+    cs = e.upload_chains(ca)
+    if order == "chains-first":
+        e.set_scoring(np.asarray(BLASTZ, np.int32), GapCosts("loose"))
+    g, l, a = e.score_ranges(cs, R, want_local=True)
+    og, ol, oa = _oracle(tg, qg).score_ranges(ca, R)
+    assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
+    mat = np.random.default_rng(3).integers(-200, 201, 16).astype(np.int32)
+    e.set_scoring(mat, GapCosts("medium"))
+    g, l, a = e.score_ranges(cs, R, want_local=True)
+    og, ol, oa = _oracle(tg, qg, mat=mat, gap="medium").score_ranges(ca, R)
+    assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
+
+
 @pytest.mark.parametrize("lim", [300, (1 << 17) - 1])
 def test_asymmetric_matrix(lim):
     """A random, strand-asymmetric score matrix takes the 16-term scoring
