@@ -1806,31 +1806,41 @@ __device__ __forceinline__ uint32_t rev_nibbles(uint32_t v) {
 }
 
 // one lane per plane word: one 8-byte load of the payload (every sequence
-// starts 8-byte aligned in the staging buffer, which is padded past its end)
+// starts 8-byte aligned in the staging buffer, which is padded past its end).
+// A workgroup takes kRelPer runs of 256 words: the sequence search (a chain
+// of dependent scalar loads) is paid once per workgroup, not per 5 KB.
+constexpr int kRelPer = 8;
 __global__ void __launch_bounds__(256) k_relayout(const uint8_t *raw, const SeqDev *seqs,
                                                   int nseq, int64_t nwords, uint2 *planes,
                                                   uint32_t *nmask) {
-    const int64_t w0 = (int64_t)blockIdx.x * blockDim.x, w = w0 + threadIdx.x;
+    const int64_t W0 = (int64_t)blockIdx.x * blockDim.x * kRelPer;
     // the sequence of the workgroup's first word: a search on workgroup-uniform
-    // values (scalar loads), then the rare lanes past the next sequence start
-    // step forward (sequences are mostly far longer than 256 words)
+    // values (scalar loads); each run then steps it forward, and the rare lanes
+    // past the next sequence start step further (sequences are mostly far
+    // longer than 256 words)
     int lo = 0, hi = nseq - 1;
-    while (lo < hi) {  // last seq with word_off <= w0
+    while (lo < hi) {  // last seq with word_off <= W0
         const int mid = (lo + hi + 1) >> 1;
-        if (seqs[mid].word_off <= w0) lo = mid;
+        if (seqs[mid].word_off <= W0) lo = mid;
         else hi = mid - 1;
     }
-    if (lo + 1 < nseq && seqs[lo + 1].word_off < w0 + (int64_t)blockDim.x)
-        while (lo + 1 < nseq && seqs[lo + 1].word_off <= w) ++lo;
-    if (w >= nwords) return;
-    const SeqDev s = seqs[lo];
-    const int64_t base0 = (w - s.word_off) * 32;
-    const uint64_t x = *reinterpret_cast<const uint64_t *>(raw + s.byte_off + (base0 >> 2));
-    const int64_t valid = s.size - base0;  // > 0
-    const uint32_t pad = valid >= 32 ? 0u : ~((1u << valid) - 1u);  // padding scores 0 like an N
-    const uint32_t p0 = rev_nibbles(even_bits(x)), p1 = rev_nibbles(even_bits(x >> 1));
-    planes[w] = make_uint2(p0 & ~pad, p1 & ~pad);
-    nmask[w] = pad;
+    for (int r = 0; r < kRelPer; ++r) {
+        const int64_t w0 = W0 + r * (int64_t)blockDim.x, w = w0 + threadIdx.x;
+        if (w0 >= nwords) return;
+        while (lo + 1 < nseq && seqs[lo + 1].word_off <= w0) ++lo;  // (uniform)
+        int l = lo;
+        if (l + 1 < nseq && seqs[l + 1].word_off < w0 + (int64_t)blockDim.x)
+            while (l + 1 < nseq && seqs[l + 1].word_off <= w) ++l;
+        if (w >= nwords) return;
+        const SeqDev s = seqs[l];
+        const int64_t base0 = (w - s.word_off) * 32;
+        const uint64_t x = *reinterpret_cast<const uint64_t *>(raw + s.byte_off + (base0 >> 2));
+        const int64_t valid = s.size - base0;  // > 0
+        const uint32_t pad = valid >= 32 ? 0u : ~((1u << valid) - 1u);  // padding scores 0 like an N
+        const uint32_t p0 = rev_nibbles(even_bits(x)), p1 = rev_nibbles(even_bits(x >> 1));
+        planes[w] = make_uint2(p0 & ~pad, p1 & ~pad);
+        nmask[w] = pad;
+    }
 }
 
 // N runs, pre-split on the host into pieces of <= 1024 bases.
@@ -2150,7 +2160,7 @@ hipError_t launch_block_gaps_flat(const int32_t *coff, const int32_t *tile_c0, i
 
 hipError_t launch_relayout(const uint8_t *raw, const SeqDev *seqs, int nseq, int64_t nwords,
                            uint2 *planes, uint32_t *nmask, hipStream_t s) {
-    const int64_t nb = (nwords + 255) / 256;
+    const int64_t nb = (nwords + 256 * kRelPer - 1) / (256 * kRelPer);
     if (nb == 0) return hipSuccess;
     hipLaunchKernelGGL(k_relayout, dim3((unsigned)nb), dim3(256), 0, s, raw, seqs, nseq, nwords,
                        planes, nmask);
