@@ -174,3 +174,43 @@ def test_axtchain_team_dp_large_pair(tool, tmp_path):
     subprocess.run([tool] + args + ["ref.chain"], cwd=tmp_path, check=True, timeout=600,
                    capture_output=True, env=env)
     assert filecmp.cmp(tmp_path / "team.chain", tmp_path / "ref.chain", shallow=False)
+
+
+@pytest.mark.parametrize("side", ["target", "query", "both"])
+def test_axtchain_block_past_sequence_end(tool, side, tmp_path):
+    """checkBlockRange (axtChain.c:242-248) after the fold: the first block in
+    pair order that runs past its sequence's end is reported (query before
+    target within a block), exit 255 -- the reference's message when it is
+    built.  Two PSL lines of different pairs are made bad."""
+    d = os.path.join(GOLDEN, "axtchain", "s5")
+    lines = open(os.path.join(d, "in.psl")).read().split("\n")
+    body = [i for i, l in enumerate(lines) if l.split("\t")[0].isdigit()]
+    seen, picks = set(), []
+    for i in body:  # lines of two different pairs, blocks of size >= 2
+        w = lines[i].split("\t")
+        key = (w[8], w[9], w[13])
+        if key in seen or min(int(x) for x in w[18].rstrip(",").split(",")) < 2:
+            continue
+        seen.add(key)
+        picks.append(i)
+        if len(picks) == 2:
+            break
+    for k, i in enumerate(picks):
+        w = lines[i].split("\t")
+        col, size = (16, 14) if side == "target" or (side == "both" and k) else (15, 10)
+        starts = w[col + 4].rstrip(",").split(",")
+        starts[-1] = str(int(w[size]) - 1)
+        w[col + 4] = ",".join(starts) + ","
+        lines[i] = "\t".join(w)
+    psl = tmp_path / "bad.psl"
+    psl.write_text("\n".join(lines))
+    args = ["-linearGap=loose", "-psl", str(psl), os.path.join(d, "t.2bit"), os.path.join(d, "q.2bit")]
+    r = subprocess.run([tool] + args + [str(tmp_path / "o.chain")], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 255 and "exceeds sequence length" in r.stderr, r.stderr[-1000:]
+    ref = os.path.join(ROOT, "oracle", "_ref", "axtChain")
+    if os.path.exists(ref):
+        rr = subprocess.run([ref] + args + [str(tmp_path / "r.chain")], capture_output=True,
+                            text=True, timeout=300)
+        assert rr.returncode == 255
+        assert r.stderr.strip().splitlines()[-1] == rr.stderr.strip().splitlines()[-1]
