@@ -2868,41 +2868,6 @@ static int bkey_cmp(const void *a, const void *b) {
     return (x->rank > y->rank) - (x->rank < y->rank);
 }
 
-/* the folded pairs compacted into fresh arrays, pairs in parallel (each pair's
- * run lands at its prefix offset), with checkBlockRange's test (axtChain.c:
- * 242-248: query, then target, per block) and the block sizes on the way; the
- * first failing block in order is reported by the caller */
-typedef struct compact_job {
-    const gac_axt_input *in;
-    const ax_pairinfo *info;
-    const int32_t *qs, *qe, *ts, *te;        /* folded, at in->blk_off[p] */
-    int32_t *nqs, *nqe, *nts, *nte, *nbsz;   /* compacted */
-    const int64_t *cnt, *dst;                /* per pair: folded count, offset */
-    int64_t *bad;                            /* per pair: 2 i + (target) of its first bad block, or -1 */
-    int64_t np;
-    _Atomic int64_t next;
-} compact_job;
-
-static void *compact_thread(void *arg) {
-    compact_job *C = arg;
-    for (int64_t p; (p = atomic_fetch_add(&C->next, 1)) < C->np;) {
-        const int64_t a = C->in->blk_off[p], c = C->cnt[p], d = C->dst[p];
-        memcpy(C->nqs + d, C->qs + a, (size_t)c * 4);
-        memcpy(C->nqe + d, C->qe + a, (size_t)c * 4);
-        memcpy(C->nts + d, C->ts + a, (size_t)c * 4);
-        memcpy(C->nte + d, C->te + a, (size_t)c * 4);
-        const int32_t qsize = C->info[p].qsize, tsize = C->info[p].tsize;
-        int64_t bad = -1;
-        for (int64_t i = d; i < d + c; ++i) {
-            C->nbsz[i] = C->nqe[i] - C->nqs[i];
-            if (bad < 0 && (C->nqe[i] > qsize || C->nte[i] > tsize))
-                bad = 2 * i + (C->nqe[i] > qsize ? 0 : 1);
-        }
-        C->bad[p] = bad;
-    }
-    return NULL;
-}
-
 typedef struct fold_job {
     const gac_axt_input *in;
     int32_t *qs, *qe, *ts, *te;
@@ -3325,45 +3290,36 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
         run_threads(nthreads < np ? nthreads : (int)(np ? np : 1), fold_thread, &F);
     }
     int64_t nb = 0;
-    {
-        int64_t *cnt = malloc((size_t)(np ? np : 1) * 8), *dst = malloc((size_t)(np ? np : 1) * 8);
-        int64_t *bad = malloc((size_t)(np ? np : 1) * 8);
-        for (int64_t p = 0; p < np; ++p) {
-            cnt[p] = poff[p + 1]; /* the folded count of pair p */
-            dst[p] = nb;
-            nb += cnt[p];
-        }
-        const size_t sz = (size_t)(nb ? nb : 1) * 4;
-        compact_job C = {in, info, qs, qe, ts, te, malloc(sz), malloc(sz), malloc(sz), malloc(sz),
-                         bsz, cnt, dst, bad, np, 0};
-        atomic_init(&C.next, 0);
-        run_threads(nthreads < np ? nthreads : (int)(np ? np : 1), compact_thread, &C);
-        free(qs), free(qe), free(ts), free(te);
-        qs = C.nqs, qe = C.nqe, ts = C.nts, te = C.nte;
-        free(cnt);
-        free(dst);
-        for (int64_t p = 0; p < np && rc == GAC_OK; ++p) {
-            if (bad[p] < 0)
-                continue;
-            const int64_t i = bad[p] >> 1;
-            if (!(bad[p] & 1))
+    for (int64_t p = 0; p < np; ++p) {
+        const int64_t a = in->blk_off[p], c = poff[p + 1]; /* c: folded count of pair p */
+        memmove(qs + nb, qs + a, (size_t)c * 4);
+        memmove(qe + nb, qe + a, (size_t)c * 4);
+        memmove(ts + nb, ts + a, (size_t)c * 4);
+        memmove(te + nb, te + a, (size_t)c * 4);
+        const int64_t first = nb;
+        nb += c;
+        /* checkBlockRange (axtChain.c:242-248), query then target per block */
+        for (int64_t i = first; i < nb; ++i) {
+            if (qe[i] > info[p].qsize) {
                 rc = gac_fail(GAC_E_ARG, "query %s block %d-%d exceeds sequence length %d",
                               info[p].qname, qs[i], qe[i], info[p].qsize);
-            else
+                goto fail;
+            }
+            if (te[i] > info[p].tsize) {
                 rc = gac_fail(GAC_E_ARG, "target %s block %d-%d exceeds sequence length %d",
                               info[p].tname, ts[i], te[i], info[p].tsize);
+                goto fail;
+            }
         }
-        free(bad);
-        if (rc != GAC_OK)
-            goto fail;
     }
     poff[0] = 0;
     for (int64_t p = 0; p < np; ++p)
         poff[p + 1] += poff[p];
     stage("removeExactOverlaps", &tclock);
-    /* ---- axtScoreUngapped of every block: one GPU batch (the block sizes
-     * were written by the compaction) */
+    /* ---- axtScoreUngapped of every block: one GPU batch */
     int32_t *score = malloc((size_t)(nb ? nb : 1) * 4);
+    for (int64_t i = 0; i < nb; ++i)
+        bsz[i] = qe[i] - qs[i];
     rc = gac_score_blocks(ctx, np, in->t_seq, in->q_seq, in->q_strand, poff, ts, qs, bsz, score);
     if (rc != GAC_OK) {
         free(score);
