@@ -980,6 +980,51 @@ extern "C" int gac_genome_view(gac_ctx *c, int side, int32_t i, gac_seq_view *v)
     return GAC_OK;
 }
 
+// The block jobs of gac_score_blocks, 1 M-block chunks on all threads (one
+// pair can hold a quarter of a whole-genome run); the first bad block in
+// order is kept for the serial message.
+struct BlockFill {
+    const int64_t *blk_off;
+    int64_t np, n;
+    const int32_t *bt, *bq, *bs;
+    const int64_t *tw, *qw;  // per pair: global base of the target / query sequence
+    const int32_t *tsz, *qsz;
+    const uint8_t *minus;
+    BlockJob *jobs;
+    std::atomic<int64_t> next, err_b;
+};
+
+static void *block_fill_thread(void *arg) {
+    BlockFill *F = (BlockFill *)arg;
+    const int64_t chunk = 1 << 20;
+    for (int64_t a; (a = F->next.fetch_add(chunk)) < F->n;) {
+        const int64_t e = std::min(F->n, a + chunk);
+        int64_t p = std::upper_bound(F->blk_off, F->blk_off + F->np + 1, a) - F->blk_off - 1;
+        for (int64_t b = a; b < e; ++b) {
+            if (b < F->blk_off[0]) {  // (before the first pair: an empty job, as before)
+                F->jobs[b] = BlockJob{0, 0, 0, 0};
+                continue;
+            }
+            if (p < 0) p = 0;
+            while (b >= F->blk_off[p + 1]) ++p;  // (past empty pairs too)
+            const int32_t bt = F->bt[b], bq = F->bq[b], sz = F->bs[b];
+            if (bt < 0 || bq < 0 || sz < 0 || (int64_t)bt + sz > F->tsz[p] ||
+                (int64_t)bq + sz > F->qsz[p]) {
+                int64_t cur = F->err_b.load();
+                while ((cur < 0 || b < cur) && !F->err_b.compare_exchange_weak(cur, b)) {
+                }
+                break;
+            }
+            BlockJob &j = F->jobs[b];
+            j.tp = F->tw[p] + bt;
+            j.minus = F->minus[p];
+            j.qp = j.minus ? F->qw[p] + (F->qsz[p] - bq) : F->qw[p] + bq;
+            j.n = sz;
+        }
+    }
+    return nullptr;
+}
+
 extern "C" int gac_score_blocks(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq,
                                 const int32_t *q_seq, const uint8_t *q_strand,
                                 const int64_t *blk_off, const int32_t *blk_t,
@@ -995,33 +1040,46 @@ extern "C" int gac_score_blocks(gac_ctx *c, int64_t n_pairs, const int32_t *t_se
     if (n == 0) return GAC_OK;
     if (!blk_t || !blk_q || !blk_size || !score)
         return gac_fail(GAC_E_ARG, "gac_score_blocks: NULL block array");
-    std::vector<BlockJob> jobs(n);
     const Genome &T = c->g[0], &Q = c->g[1];
+    std::vector<int64_t> tw(n_pairs), qw(n_pairs);
+    std::vector<int32_t> tsz(n_pairs), qsz(n_pairs);
+    std::vector<uint8_t> minus(n_pairs);
     for (int64_t p = 0; p < n_pairs; ++p) {
         const int32_t ts = t_seq[p], qs = q_seq[p];
         if (ts < 0 || ts >= (int32_t)T.sizes.size() || qs < 0 || qs >= (int32_t)Q.sizes.size())
             return gac_fail(GAC_E_ARG, "gac_score_blocks: pair %lld: bad sequence index",
                             (long long)p);
-        const int64_t tw = T.woff[ts] * 32, qw = Q.woff[qs] * 32;
-        const int32_t tsize = T.sizes[ts], qsize = Q.sizes[qs];
-        for (int64_t b = blk_off[p]; b < blk_off[p + 1]; ++b) {
-            const int32_t bt = blk_t[b], bq = blk_q[b], sz = blk_size[b];
-            if (bt < 0 || bq < 0 || sz < 0 || (int64_t)bt + sz > tsize || (int64_t)bq + sz > qsize)
-                return gac_fail(GAC_E_ARG, "block %lld (%d %d %d) outside %s/%s", (long long)b,
-                                bt, bq, sz, T.names[ts].c_str(), Q.names[qs].c_str());
-            BlockJob &j = jobs[b];
-            j.tp = tw + bt;
-            j.minus = q_strand[p] ? 1 : 0;
-            j.qp = j.minus ? qw + (qsize - bq) : qw + bq;
-            j.n = sz;
-        }
+        if (blk_off[p + 1] < blk_off[p])
+            return gac_fail(GAC_E_ARG, "gac_score_blocks: pair %lld: block offsets descend",
+                            (long long)p);
+        tw[p] = T.woff[ts] * 32, qw[p] = Q.woff[qs] * 32;
+        tsz[p] = T.sizes[ts], qsz[p] = Q.sizes[qs];
+        minus[p] = q_strand[p] ? 1 : 0;
+    }
+    // (not value-initialised: every job is written by a fill thread)
+    std::unique_ptr<BlockJob[]> jobs(new BlockJob[n]);
+    BlockFill F;
+    F.blk_off = blk_off, F.np = n_pairs, F.n = n;
+    F.bt = blk_t, F.bq = blk_q, F.bs = blk_size;
+    F.tw = tw.data(), F.qw = qw.data(), F.tsz = tsz.data(), F.qsz = qsz.data();
+    F.minus = minus.data();
+    F.jobs = jobs.get();
+    F.next = 0;
+    F.err_b = -1;
+    const int nt = std::max(1, std::min(16, gac_host_threads()));
+    gac_run_threads((int)std::min<int64_t>(nt, (n + (1 << 20) - 1) >> 20), block_fill_thread, &F);
+    if (F.err_b.load() >= 0) {  // the first bad block in order, as the serial check reports it
+        const int64_t b = F.err_b.load();
+        const int64_t p = std::upper_bound(blk_off, blk_off + n_pairs + 1, b) - blk_off - 1;
+        return gac_fail(GAC_E_ARG, "block %lld (%d %d %d) outside %s/%s", (long long)b, blk_t[b],
+                        blk_q[b], blk_size[b], T.names[t_seq[p]].c_str(), Q.names[q_seq[p]].c_str());
     }
     HIPCHK(hipSetDevice(c->device));
     BlockJob *d_jobs = nullptr;
     int32_t *d_out = nullptr;
     HIPCHK(hipMalloc((void **)&d_jobs, n * sizeof(BlockJob)));
     HIPCHK(hipMalloc((void **)&d_out, n * sizeof(int32_t)));
-    HIPCHK(hipMemcpyAsync(d_jobs, jobs.data(), n * sizeof(BlockJob), hipMemcpyHostToDevice,
+    HIPCHK(hipMemcpyAsync(d_jobs, jobs.get(), n * sizeof(BlockJob), hipMemcpyHostToDevice,
                           c->stream));
     ScoreArgs a;
     memset(&a, 0, sizeof(a));
