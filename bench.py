@@ -875,6 +875,11 @@ def full_parity(which, files):
         same = same and ok
         res[key] = {"ours": got[path], "reference": ref, "same": ok}
     res["identical"] = same
+    ins = [k for k in files if k.startswith("in_")]
+    if ins and not all(res[k]["same"] for k in ins):
+        # another seed or size than the golden's: nothing to compare against
+        res["identical"] = None
+        res["unpinned"] = "input differs from the golden's (another --seed / size): parity unpinned"
     res["golden"] = f"tests/golden/fullscale/{which}.json ({gold['generator']}; reference run on "
     res["golden"] += f"{gold['reference_host']})"
     res["hash_seconds"] = round(time.time() - t0, 2)

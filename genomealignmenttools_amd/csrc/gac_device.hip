@@ -1451,6 +1451,13 @@ static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs)
         return gac_fail(GAC_E_ARG, "gac_chains_upload: bad descriptor");
     if (d->n_chains && d->blk_off[d->n_chains] != d->n_blocks)
         return gac_fail(GAC_E_ARG, "blk_off[n_chains] != n_blocks");
+    // every block belongs to a chain: the flat upload kernels find a block's
+    // chain by its offset, so blocks before chain 0 (or with no chain) would
+    // be written to negative positions
+    if (d->n_chains && d->blk_off[0] != 0)
+        return gac_fail(GAC_E_ARG, "blk_off[0] != 0");
+    if (!d->n_chains && d->n_blocks)
+        return gac_fail(GAC_E_ARG, "blocks without chains (n_chains == 0, n_blocks > 0)");
     // the kernels index blocks of one chain set with int32 (RangeDesc::b0,
     // flat windows): a larger set must be uploaded in parts
     if (d->n_blocks > (int64_t)INT32_MAX - 16)

@@ -3473,9 +3473,12 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
                 const char *bv = getenv("GAC_DP_BATCH");
                 tr[k].batch = bv && atoi(bv) > 0 ? atoi(bv) : 2 * t;
                 tr[k].env = &env;
-                if (pthread_create(&tr[k].th, NULL, team_runner, &tr[k]) != 0)
-                    team_runner(&tr[k]); /* (no thread: here) */
-                else
+                if (pthread_create(&tr[k].th, NULL, team_runner, &tr[k]) != 0) {
+                    /* (no thread: here, unpinned -- a pinned caller would
+                     * leave the pool and every later stage in one L3 domain) */
+                    tr[k].pin = 0;
+                    team_runner(&tr[k]);
+                } else
                     tr[k].started = 1;
             }
             atomic_store(&J.next, big);

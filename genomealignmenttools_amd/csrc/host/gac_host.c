@@ -14,6 +14,7 @@
 #include <stdatomic.h>
 
 #include <pthread.h>
+#include <sched.h>
 #include <unistd.h>
 
 #include <ctype.h>
@@ -727,15 +728,65 @@ trunc:
 }
 
 /* ------------------------------------------------------------------- threads */
+/* CPUs of a cgroup CPU quota, rounded up: cgroup v2 "cpu.max" ("max 100000"
+ * or "<quota> <period>") or v1 cpu.cfs_quota_us / cpu.cfs_period_us.  0 = no
+ * quota (or none readable). */
+static int cgroup_quota_cpus(const char *v2_path) {
+    long long q = -1, p = 0;
+    FILE *f = fopen(v2_path, "r");
+    if (f) {
+        char a[32] = {0};
+        if (fscanf(f, "%31s %lld", a, &p) == 2 && strcmp(a, "max") != 0)
+            q = atoll(a);
+        fclose(f);
+    } else if ((f = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r"))) {
+        if (fscanf(f, "%lld", &q) != 1)
+            q = -1;
+        fclose(f);
+        if ((f = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r"))) {
+            if (fscanf(f, "%lld", &p) != 1)
+                p = 0;
+            fclose(f);
+        }
+    }
+    if (q <= 0 || p <= 0)
+        return 0;
+    const long long n = (q + p - 1) / p;
+    return n > 0 && n < 1 << 20 ? (int)n : 0;
+}
+
+/* The CPUs this process may use: the online CPUs, narrowed by its affinity
+ * mask and by its cgroup's CPU quota (a container with a 16-CPU quota on a
+ * 256-CPU host gets 16 threads, not 64 time-sliced ones). */
+int gac_host_cpus(void) {
+    static _Atomic int cached;
+    const char *cg = getenv("GAC_CGROUP_CPU_MAX"); /* (tests: another cpu.max file) */
+    int n = cg ? 0 : atomic_load(&cached);
+    if (n > 0)
+        return n;
+    const long c = sysconf(_SC_NPROCESSORS_ONLN);
+    n = c > 0 ? (int)c : 1;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) {
+        const int a = CPU_COUNT(&set);
+        if (a > 0 && a < n)
+            n = a;
+    }
+    const int q = cgroup_quota_cpus(cg ? cg : "/sys/fs/cgroup/cpu.max");
+    if (q > 0 && q < n)
+        n = q;
+    if (!cg)
+        atomic_store(&cached, n);
+    return n;
+}
+
 int gac_host_threads(void) {
     const char *s = getenv("GAC_THREADS");
     if (!s || !*s)
         s = getenv("OMP_NUM_THREADS");
     int n = s && *s ? atoi(s) : 0;
-    if (n <= 0) {
-        const long c = sysconf(_SC_NPROCESSORS_ONLN);
-        n = c > 0 ? (int)c : 1;
-    }
+    if (n <= 0)
+        n = gac_host_cpus();
     return n > 64 ? 64 : n;
 }
 

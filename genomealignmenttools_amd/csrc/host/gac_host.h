@@ -77,7 +77,10 @@ void gac_twobit_close(gac_twobit *tb);
 uint32_t gac_twobit_u32(const gac_twobit *tb, const uint8_t *p);
 int gac_is_twobit_file(const char *path);
 
-/* ---- host threads: GAC_THREADS, else OMP_NUM_THREADS, else all cores (<= 64) */
+/* ---- host threads: GAC_THREADS, else OMP_NUM_THREADS, else gac_host_cpus() (<= 64) */
+/* CPUs usable by this process: online CPUs narrowed by the affinity mask and
+ * the cgroup CPU quota (cpu.max) */
+int gac_host_cpus(void);
 int gac_host_threads(void);
 /* GAC_TIMING: "[mark] <seconds since the first mark> <thread> <what>" on
  * stderr (timelines of overlapped phases; no-op otherwise) */

@@ -1761,10 +1761,8 @@ int gt_threads(void) {
     if (!s || !*s)
         s = getenv("OMP_NUM_THREADS");
     int n = s && *s ? atoi(s) : 0;
-    if (n <= 0) {
-        long c = sysconf(_SC_NPROCESSORS_ONLN);
-        n = c > 0 ? (int)c : 1;
-    }
+    if (n <= 0)
+        n = gac_host_cpus(); /* (affinity mask and cgroup quota) */
     return n > 64 ? 64 : n;
 }
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Bench under each event-timing mode (how much the HIP event markers cost).
-# usage: bash scripts/gpu_bench_modes.sh TAG [bench args...]
+# usage: bash scripts/archive/gpu_bench_modes.sh TAG [bench args...]
 set -o pipefail
 TAG=${1:-modes}; shift
 cd "$GRAFT_REPO_ROOT" || exit 1

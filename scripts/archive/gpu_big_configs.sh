@@ -3,7 +3,7 @@
 # -rescore) or C4 at 5e7 PSL blocks (axtChain), ours vs the reference
 # binaries on this host, outputs compared byte for byte.  A heartbeat file
 # marks progress while the single-threaded reference runs.
-# usage: bash scripts/gpu_big_configs.sh TAG c5|c4
+# usage: bash scripts/archive/gpu_big_configs.sh TAG c5|c4
 set -o pipefail
 TAG=${1:-big}; WHAT=${2:-c5}
 cd "$GRAFT_REPO_ROOT" || exit 1

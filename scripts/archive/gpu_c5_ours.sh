@@ -1,7 +1,7 @@
 #!/bin/bash
 # C5 at --chains (default 5e6): ours only (scoreChain + chainNet -rescore),
 # twice, with the per-stage times; the reference side is in
-# scripts/gpu_big_configs.sh (its outputs' checksums are compared here
+# scripts/archive/gpu_big_configs.sh (its outputs' checksums are compared here
 # against the committed reference-checked run when given).
 set -o pipefail
 TAG=${1:-c5ours}; CH=${2:-5000000}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Run the chainCleaner drop-in on every golden case (tests/golden/cleaner),
 # keep the outputs under gpurun_out/cc/<case>/ and diff them against the
-# reference's.  Usage (GPU box): bash scripts/gpu_cleaner_probe.sh
+# reference's.  Usage (GPU box): bash scripts/archive/gpu_cleaner_probe.sh
 set -u
 G=tests/golden/cleaner
 BIN=genomealignmenttools_amd/bin/chainCleaner

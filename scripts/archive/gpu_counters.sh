@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC counter passes for the bench's kernels (separate rocprofv3 runs, each
 # with --kernel-trace only; never combined with sys/runtime traces).
-# usage: bash scripts/gpu_counters.sh TAG [bench args...]
+# usage: bash scripts/archive/gpu_counters.sh TAG [bench args...]
 set -o pipefail
 TAG=${1:-ctr}; shift
 cd "$GRAFT_REPO_ROOT" || exit 1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # axtChain host-DP A/B on the C4-like set (GPU box host): environment
 # variants interleaved, 3 rounds; DP stage lines and outputs compared.
-# usage: bash scripts/gpu_dp_ab.sh TAG BLOCKS "NAME:ENV=V,ENV=V" ...
+# usage: bash scripts/archive/gpu_dp_ab.sh TAG BLOCKS "NAME:ENV=V,ENV=V" ...
 set -o pipefail
 TAG=${1:-dpab}; BLOCKS=${2:-2000000}; shift 2
 cd "$GRAFT_REPO_ROOT" || exit 1

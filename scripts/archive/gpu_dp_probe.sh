@@ -2,7 +2,7 @@
 # Device kd-tree DP (GAC_AXT_DP=gpu, rows A13/A14): parity tests, then the
 # C4-like axtChain timed with the DP on host threads and on the device, and a
 # rocprofv3 kernel trace of the device run.
-# usage: bash scripts/gpu_dp_probe.sh TAG BLOCKS
+# usage: bash scripts/archive/gpu_dp_probe.sh TAG BLOCKS
 set -o pipefail
 TAG=${1:-dp}; BLOCKS=${2:-2000000}
 cd "$GRAFT_REPO_ROOT" || exit 1

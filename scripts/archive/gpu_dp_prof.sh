@@ -2,7 +2,7 @@
 # The device kd-tree DP (GAC_AXT_DP=gpu) on the C4-like axtChain input:
 # one timed run checked against the reference's output, then a rocprofv3
 # kernel trace (k_dp / k_xover durations) of the same command.
-# usage: bash scripts/gpu_dp_prof.sh TAG BLOCKS
+# usage: bash scripts/archive/gpu_dp_prof.sh TAG BLOCKS
 set -o pipefail
 TAG=${1:-dpprof}; BLOCKS=${2:-2000000}
 cd "$GRAFT_REPO_ROOT" || exit 1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # bin/chainNet -rescore on C2 under several environments, interleaved (one
 # run of each per round, 6 rounds): wall time per run and the device laps.
-# usage: bash scripts/gpu_e2e_ab.sh TAG "NAME:ENV=V,ENV=V" ...
+# usage: bash scripts/archive/gpu_e2e_ab.sh TAG "NAME:ENV=V,ENV=V" ...
 set -o pipefail
 TAG=${1:-ab}; shift
 cd "$GRAFT_REPO_ROOT" || exit 1

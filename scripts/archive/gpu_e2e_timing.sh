@@ -1,7 +1,7 @@
 #!/bin/bash
 # bin/chainNet -rescore on C2 with every timing lap (GAC_TIMING=1), 3 runs,
 # wall clock per run; the last run's log is printed.
-# usage: bash scripts/gpu_e2e_timing.sh TAG [ENV=VAL ...]
+# usage: bash scripts/archive/gpu_e2e_timing.sh TAG [ENV=VAL ...]
 set -o pipefail
 TAG=${1:-e2e}; shift
 cd "$GRAFT_REPO_ROOT" || exit 1

@@ -2,7 +2,7 @@
 # Kernel leg (rescore fills) under several range orders: per-kernel times and
 # memory-side read requests / L2 hits of each kernel (one --pmc pass per
 # counter group, --kernel-trace only).
-# usage: bash scripts/gpu_order_pmc.sh TAG "order1 order2 ..." [bench args...]
+# usage: bash scripts/archive/gpu_order_pmc.sh TAG "order1 order2 ..." [bench args...]
 set -o pipefail
 TAG=${1:-ordpmc}; shift
 ORDERS=${1:-"net chain"}; shift

@@ -7,7 +7,7 @@ tag=${1:-r03f}
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
-bash scripts/gpu_r03_prof.sh $tag || exit $?
+bash scripts/archive/gpu_r03_prof.sh $tag || exit $?
 GAC_BENCH_ONE_GPU=1 GAC_THREADS=8 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 \
     --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 2 \
     --warmup 1 --no-kernel > $out/bench_n2.json 2> $out/bench_n2.err

@@ -2,7 +2,7 @@
 # chainNet -rescore -nranks=N on the replicated-C2 input (bench.py's N>1
 # workload), all ranks on this box's one GPU: wall time per step and the
 # per-rank stage times.  GAC_THREADS per rank = 16/N (the box's CPU share).
-# usage: bash scripts/gpu_ranks_probe.sh TAG "1 2 4"
+# usage: bash scripts/archive/gpu_ranks_probe.sh TAG "1 2 4"
 set -o pipefail
 TAG=${1:-ranks}; NS=${2:-"1 2 4"}
 cd "$GRAFT_REPO_ROOT" || exit 1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # chainNet -rescore with the sparse genome upload: the chainNet GPU parity
 # tests, then C2 end to end with sparse vs whole-genome uploads (A/B).
-# usage: bash scripts/gpu_sparse_check.sh TAG
+# usage: bash scripts/archive/gpu_sparse_check.sh TAG
 set -o pipefail
 TAG=${1:-sparse}
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -12,4 +12,4 @@ timeout -k 10 900 python -u -m pytest tests/test_gpu_tools.py tests/test_gpu_con
 rc=$?
 tail -3 "$OUT/tests.log"
 [ $rc -eq 0 ] || exit $rc
-bash scripts/gpu_e2e_ab.sh "$TAG/ab" "sparse:GAC_NET_SPARSE=1" "whole:GAC_NET_SPARSE=0"
+bash scripts/archive/gpu_e2e_ab.sh "$TAG/ab" "sparse:GAC_NET_SPARSE=1" "whole:GAC_NET_SPARSE=0"

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Per-stage timings of bin/chainNet -rescore on C2 (GAC_TIMING=1: device
 # open laps, genome upload, netting phases) under several environments.
-# usage: bash scripts/gpu_stage_probe.sh TAG
+# usage: bash scripts/archive/gpu_stage_probe.sh TAG
 set -o pipefail
 TAG=${1:-probe}; shift
 cd "$GRAFT_REPO_ROOT" || exit 1

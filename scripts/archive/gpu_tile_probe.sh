@@ -2,7 +2,7 @@
 # k_tile experiments on the kernel leg (rescore fills): each argument is
 # "NAME:ENV=VAL,ENV=VAL:MAKEVARS" -- rebuild with MAKEVARS (e.g.
 # HIPEXTRA=-DGAC_VARIANT=1) when given, then time the kernel leg with ENV set.
-# usage: bash scripts/gpu_tile_probe.sh TAG SPEC...
+# usage: bash scripts/archive/gpu_tile_probe.sh TAG SPEC...
 set -o pipefail
 TAG=${1:-tile}; shift
 cd "$GRAFT_REPO_ROOT" || exit 1

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round-5 A/B: the whole-chain k_tile leg (scoreChain) under chain order x
+# tile schedule: set (score) order vs target order (GAC_WHOLE_ORDER=target),
+# per-round XCD blocks vs one contiguous eighth of the tiles per XCD
+# (GAC_TILE_XCD=1).  bench kernel legs only (the headline step once), in-run
+# PMC traffic; the scoreChain e2e leg's full-scale sha checks each order.
+set -o pipefail
+tag=${1:-r05whole}
+out=gpurun_out/$tag
+mkdir -p $out
+export TMPDIR=/tmp
+(while sleep 50; do date +%T >> $out/heartbeat.txt; done) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+for i in 1 2; do
+  for v in set:0 target:1 target:0; do
+    o=${v%:*}; x=${v#*:}
+    GAC_WHOLE_ORDER=$o GAC_TILE_XCD=$x timeout -k 10 500 python -u bench.py --steps 1 --warmup 0 \
+        --kernel-steps 20 --no-c2 --no-cpu-baseline --no-c4 \
+        > $out/bench_${o}_x${x}_$i.json 2> $out/bench_${o}_x${x}_$i.err || exit $?
+  done
+done
+echo ok

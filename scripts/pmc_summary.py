@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 --pmc passes (scripts/gpu_counters.sh output) into one
+"""Summarise rocprofv3 --pmc passes (scripts/archive/gpu_counters.sh output) into one
 JSON: per kernel, the mean counter value per dispatch, plus derived figures
 (FETCH_SIZE/WRITE_SIZE in bytes, waves and wait fractions).
 

@@ -29,7 +29,7 @@ def main(summary_path, bench_path):
         "blocks": kern["window_blocks"],
         "order": kern.get("order", "net"),
         "source": "rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_{32,64,128}B_sum / "
-                  "TCC_EA0_WRREQ(_64B)_sum passes (scripts/gpu_counters.sh), "
+                  "TCC_EA0_WRREQ(_64B)_sum passes (scripts/archive/gpu_counters.sh), "
                   "mean per dispatch (scripts/pmc_summary.py)",
     }
     json.dump(out, sys.stdout, indent=1)

@@ -348,6 +348,15 @@ def test_host_ranges_and_reupload(seed):
         with pytest.raises(GacError):
             e.score_ranges_host(tix[:len(off) - 1], qix[:len(off) - 1], ca.qstrand[:len(off) - 1],
                                 off, ca.blk_t, ca.blk_q, ca.blk_size, R[R[:, 0] < len(off) - 1])
+    # the device upload: blocks in front of chain 0, blocks without chains
+    lead = ca.blk_off.copy()
+    lead[0] = 1
+    z = np.zeros(0, np.int32)
+    for arrs_bad in ((tix, qix, ca.qstrand, lead, ca.blk_t, ca.blk_q, ca.blk_size),
+                     (z, z, np.zeros(0, np.uint8), np.zeros(1, np.int64), ca.blk_t, ca.blk_q,
+                      ca.blk_size)):
+        with pytest.raises(GacError):
+            e.upload_chain_arrays(*arrs_bad)
     # a set closed with its context: orphaned, then freed without a fault
     cs2 = e.upload_chain_arrays(*arrs)
     e.close()

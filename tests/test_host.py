@@ -26,6 +26,31 @@ def test_lib_exports_every_header_symbol():
     assert set(_lib.EXPORTED) <= decl
 
 
+def test_host_threads_follow_cgroup_quota(tmp_path, monkeypatch):
+    """An un-configured tool sizes its thread pools from the CPUs the process
+    may use: the affinity mask, narrowed by the cgroup CPU quota (cpu.max,
+    rounded up) -- not the host's online CPU count."""
+    import ctypes
+    from genomealignmenttools_amd import _lib
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    affinity = len(os.sched_getaffinity(0))
+    monkeypatch.delenv("GAC_THREADS", raising=False)
+    monkeypatch.delenv("OMP_NUM_THREADS", raising=False)
+    f = tmp_path / "cpu.max"
+    for text, want in (("200000 100000\n", min(2, affinity)), ("150000 100000\n", min(2, affinity)),
+                       ("50000 100000\n", 1), ("max 100000\n", affinity)):
+        f.write_text(text)
+        monkeypatch.setenv("GAC_CGROUP_CPU_MAX", str(f))
+        assert L.gac_host_cpus() == want, text
+        assert L.gac_host_threads() == min(want, 64), text
+    monkeypatch.setenv("GAC_CGROUP_CPU_MAX", str(tmp_path / "absent"))
+    assert L.gac_host_cpus() >= 1
+    f.write_text("100000 100000\n")
+    monkeypatch.setenv("GAC_CGROUP_CPU_MAX", str(f))
+    monkeypatch.setenv("GAC_THREADS", "5")  # an explicit count wins
+    assert L.gac_host_threads() == 5
+
+
 def test_gapcalc_tables_match_oracle():
     from genomealignmenttools_amd.gachain import GapCosts
     from oracle.oracle import OracleGap
