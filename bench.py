@@ -365,6 +365,7 @@ class Legs:
         from genomealignmenttools_amd._lib import GAC_K_COMBINE, GAC_K_PLAN, GAC_K_TILE
         e, cs = self.e, self.cs
         n = cs.n_chains if ranges is None else len(ranges)
+        wins = ranges is not None and ranges.shape[1] == 5  # gac_window records
         d_r = e.dev_alloc(16 if ranges is None else max(ranges.nbytes, 16))
         if ranges is not None:
             e.h2d(d_r, np.ascontiguousarray(ranges, np.int32))
@@ -373,6 +374,8 @@ class Legs:
         d_a = e.dev_alloc(4 * n + 8)
         if ranges is None:
             call = lambda: e.score_chains_device(cs, d_g, d_a, d_l, want_local)
+        elif wins:
+            call = lambda: e.score_windows_device(cs, d_r, n, d_g, d_a, d_l, want_local)
         else:
             call = lambda: e.score_ranges_device(cs, d_r, n, d_g, d_a, d_l, want_local)
         for _ in range(3):
@@ -414,8 +417,11 @@ class Legs:
         self.e.close()
 
 
-def fills_ranges(d):
-    r = np.fromfile(os.path.join(d, "fills.bin"), np.int32).reshape(-1, 3)
+def fills_windows(d):
+    """The fills the headline rescored, as the tool dumped them
+    (GAC_DUMP_RANGES): gac_window records (chain, tStart, tEnd, first block,
+    block count)."""
+    r = np.fromfile(os.path.join(d, "fills.bin"), np.int32).reshape(-1, 5)
     return np.ascontiguousarray(r)
 
 
@@ -467,18 +473,31 @@ def add_ceiling(roof, ceil):
 
 
 def fills_leg(legs, d, ch, steps, pmc):
-    ranges = fills_ranges(d)
-    res = legs.run(ranges, False, steps)
-    nblk = _window_blocks(ch, ranges)
-    n = len(ranges)
+    """The headline's rescoring call on its own: gac_score_windows_device over
+    the fills with the windows the netting found (what bin/chainNet calls),
+    and, for comparison, gac_score_ranges_device over the same (chain, tStart,
+    tEnd) ranges (the device searches every window: k_plan)."""
+    wins = fills_windows(d)
+    res = legs.run(wins, False, steps)
+    res_r = legs.run(np.ascontiguousarray(wins[:, :3]), False, steps)
+    nblk = _window_blocks(ch, wins[:, :3])
+    n = len(wins)
     # SURVEY §8(d) range model: 32 B/range (16 in, 16 out) + 8 B/window block
     # + 0.75 B/scored base (t+q 2-bit + t+q N-mask bits)
     algo = 32.0 * n + 8.0 * nblk + 0.75 * res["bases"]
-    kernel = {"workload": "chainNet -rescore: the C5 partial target fills the headline rescored",
+    kernel = {"workload": "chainNet -rescore: the C5 partial target fills the headline rescored "
+                          "(gac_score_windows_device: windows from the netting)",
               "value": res["bases"] / (res["step_ms"] / 1e3) / 1e9, "unit": "Gbases/s",
               "ms_per_step": res["step_ms"], "steps": steps, "ranges": n, "order": "net",
-              "scored_bases": res["bases"], "window_blocks": nblk, "kernel_ms": res["kernel_ms"],
-              "model": "range: 32 B/range + 8 B/window block + 0.75 B/scored base"}
+              "scored_bases": res["bases"], "window_blocks": nblk,
+              "window_blocks_given": int(wins[:, 4].sum(dtype=np.int64)),
+              "kernel_ms": res["kernel_ms"],
+              "model": "range: 32 B/range + 8 B/window block + 0.75 B/scored base",
+              "ranges_call": {"api": "gac_score_ranges_device (windows searched on the device)",
+                              "ms_per_step": res_r["step_ms"], "kernel_ms": res_r["kernel_ms"],
+                              "same_bases": res_r["bases"] == res["bases"]},
+              "roofline_step": roofline(algo, res["step_ms"], None,
+                                        "whole call (plan + tile map + k_tile + fold)")}
     return kernel, roofline(algo, res["tile_ms"], pmc, "k_tile")
 
 
@@ -629,7 +648,7 @@ def pmc_child(args):
     d, _ = c5_files(args)
     ch = load_chains_bin(d)
     legs = Legs(d, ch)
-    ranges = fills_ranges(d) if args.pmc_child == "fills" else None
+    ranges = fills_windows(d) if args.pmc_child == "fills" else None
     legs.run(ranges, args.pmc_child == "scorechain", 3)
     legs.close()
 

@@ -155,6 +155,16 @@ _PROTOS = {
         [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_uint32, C.c_void_p, C.c_void_p,
          C.c_void_p, C.c_void_p],
     ),
+    "gac_score_windows": (
+        C.c_int,
+        [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_uint32, C.c_void_p, C.c_void_p,
+         C.c_void_p],
+    ),
+    "gac_score_windows_device": (
+        C.c_int,
+        [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_uint32, C.c_void_p, C.c_void_p,
+         C.c_void_p, C.c_void_p],
+    ),
     "gac_score_chains": (
         C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
     "gac_score_chains_device": (
@@ -181,6 +191,7 @@ _PROTOS = {
     "gac_net_fill_count": (C.c_int64, [C.c_void_p, C.c_int]),
     "gac_net_get_fills": (
         C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "gac_net_get_fill_windows": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
     "gac_net_write": (
         C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_char_p, C.c_void_p, C.c_int32]),
     "gac_net_write_file": (

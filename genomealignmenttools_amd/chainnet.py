@@ -78,6 +78,11 @@ class Net:
         check(lib().gac_net_get_fills(self.h, side, _p(out["chain"]), _p(out["start"]),
                                       _p(out["end"]), _p(out["ali"]), _p(flags)))
         out["flags"] = flags
+        if side == GAC_T:  # chainSubsetOnT's window of every target fill
+            out["first_block"] = np.zeros(n, np.int32)
+            out["n_blocks"] = np.zeros(n, np.int32)
+            check(lib().gac_net_get_fill_windows(self.h, side, _p(out["first_block"]),
+                                                 _p(out["n_blocks"])))
         return out
 
     def write(self, side: int, path: str, t_scores: Optional[np.ndarray] = None,

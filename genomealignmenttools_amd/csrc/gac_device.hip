@@ -65,6 +65,9 @@ hipError_t launch_whole_plan(const DChain *chains, int64_t n, RangeDesc *rdesc, 
                              int32_t *gflat, int32_t *tile_r0, hipStream_t s);
 hipError_t launch_zero_list(const int32_t *list, int64_t n, long long *g, long long *l,
                             int32_t *ali, hipStream_t s);
+hipError_t launch_tile_order(const DChain *chains, const int4 *blk, const int32_t *tile_r0,
+                             int64_t T, unsigned long long *keys, int32_t *vals, int32_t *perm,
+                             void *tmp, size_t &tmp_bytes, hipStream_t s);
 hipError_t launch_whole_plan_sorted(const DChain *chains, int64_t n, int32_t *perm,
                                     unsigned long long *keys, int32_t *vals, RangeDesc *rdesc,
                                     int32_t *nblk, int32_t *gflat, int32_t *pb0,
@@ -231,6 +234,9 @@ struct gac_chainset {
     bool w_sorted = false;
     int32_t *w_pb0 = nullptr;
     int32_t *w_perm = nullptr;
+    // set-order plan's tile schedule (k_tile's tile_perm): tiles in the
+    // target order of their first blocks
+    int32_t *w_tile_perm = nullptr;
     // capacities (gac_chains_reupload refills these buffers when they fit)
     size_t cap_chains = 0, cap_blocks = 0, cap_blk12 = 0, cap_tspan = 0, cap_idx = 0;
     int32_t *d_stage = nullptr;  // the caller's block arrays, staged (3 x blocks)
@@ -244,13 +250,13 @@ struct gac_chainset {
 };
 
 static void free_whole_plan(gac_chainset *cs) {
-    void *w[] = {cs->w_rdesc, cs->w_nblk,  cs->w_gflat, cs->w_tile_r0, cs->w_status,
-                 cs->w_empty, cs->w_pb0,   cs->w_perm};
+    void *w[] = {cs->w_rdesc, cs->w_nblk, cs->w_gflat, cs->w_tile_r0, cs->w_status,
+                 cs->w_empty, cs->w_pb0,  cs->w_perm,  cs->w_tile_perm};
     for (void *p : w)
         if (p) hipFree(p);
     cs->w_rdesc = nullptr;
     cs->w_nblk = cs->w_gflat = cs->w_tile_r0 = cs->w_status = cs->w_empty = nullptr;
-    cs->w_pb0 = cs->w_perm = nullptr;
+    cs->w_pb0 = cs->w_perm = cs->w_tile_perm = nullptr;
     cs->w_sorted = false;
     cs->w_nempty = 0;
     cs->w_ready = false;
@@ -1807,17 +1813,19 @@ static int prepare_args(gac_ctx *c, const gac_chainset *cs, int64_t n, uint32_t 
 }
 
 static int score_device_split(gac_ctx *c, const ScoreArgs &a_base, const Range *d_ranges,
-                              int64_t n, long long *d_g, long long *d_l, int32_t *d_ali,
-                              hipStream_t s);
+                              const Window *d_wins, int64_t n, long long *d_g, long long *d_l,
+                              int32_t *d_ali, hipStream_t s);
 
-static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_ranges, int64_t n,
-                        uint32_t flags, long long *d_g, long long *d_l, int32_t *d_ali,
-                        hipStream_t s) {
+// d_wins non-null: the ranges come with their windows (gac_score_windows*),
+// d_ranges is ignored
+static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_ranges,
+                        const Window *d_wins, int64_t n, uint32_t flags, long long *d_g,
+                        long long *d_l, int32_t *d_ali, hipStream_t s) {
     ScoreArgs a_base;
     if (c->ws_last && c->ws_last != s) HIPCHK(hipStreamWaitEvent(s, c->ws_ev, 0));
     int rc = prepare_args(c, cs, n, flags, d_l, s, a_base);
     if (rc != GAC_OK || n == 0) return rc;
-    rc = score_device_split(c, a_base, d_ranges, n, d_g, d_l, d_ali, s);
+    rc = score_device_split(c, a_base, d_ranges, d_wins, n, d_g, d_l, d_ali, s);
     if (hipEventRecord(c->ws_ev, s) == hipSuccess) c->ws_last = s;
     return rc;
 }
@@ -1825,15 +1833,16 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
 // One batch through the pipeline; a batch whose window blocks overflow int32
 // (kernels index flat blocks with 32 bits) is split in halves, recursively.
 static int score_device_split(gac_ctx *c, const ScoreArgs &a_base, const Range *d_ranges,
-                              int64_t n, long long *d_g, long long *d_l, int32_t *d_ali,
-                              hipStream_t s) {
+                              const Window *d_wins, int64_t n, long long *d_g, long long *d_l,
+                              int32_t *d_ali, hipStream_t s) {
     int rc;
     // first guess for an empty workspace: 8 window blocks per range
     const int64_t guess = c->ws_tiles ? 0 : 8 * n;
     rc = ensure_ws(c, n, guess / kTileBlocks + 1, s);
     if (rc != GAC_OK) return rc;
     ScoreArgs a = a_base;
-    a.ranges = d_ranges;
+    a.ranges = d_wins ? nullptr : d_ranges;
+    a.wins = d_wins;
     a.out_g = d_g;
     a.out_l = d_l;
     a.out_ali = d_ali;
@@ -1876,17 +1885,23 @@ static int score_device_split(gac_ctx *c, const ScoreArgs &a_base, const Range *
         int32_t st[4];
         rc = wait_status(c, s, a.call_tag, st);
         if (rc != GAC_OK) return rc;
+        if (st[3]) {  // k_plan<true>: a window outside its chain (it selected nothing)
+            HIPCHK(hipStreamSynchronize(s));
+            return gac_fail(GAC_E_ARG, "a window's blocks lie outside its chain (or its chain "
+                            "index is out of range)");
+        }
         if (st[0] == INT32_MAX) {  // W >= 2^31: two halves
             HIPCHK(hipStreamSynchronize(s));
             if (n < 2) return gac_fail(GAC_E_ARG, "one range's window exceeds 2^31 blocks");
             const int64_t h = n / 2;
             ScoreArgs b = a_base;
             b.n = h;
-            rc = score_device_split(c, b, d_ranges, h, d_g, d_l, d_ali, s);
+            rc = score_device_split(c, b, d_ranges, d_wins, h, d_g, d_l, d_ali, s);
             if (rc != GAC_OK) return rc;
             b.n = n - h;
-            return score_device_split(c, b, d_ranges + h, n - h, d_g + h, d_l ? d_l + h : nullptr,
-                                      d_ali + h, s);
+            return score_device_split(c, b, d_wins ? nullptr : d_ranges + h,
+                                      d_wins ? d_wins + h : nullptr, n - h, d_g + h,
+                                      d_l ? d_l + h : nullptr, d_ali + h, s);
         }
         if (!st[2]) return GAC_OK;
         rc = ensure_ws(c, n, st[1], s);  // (synchronises before growing)
@@ -1959,6 +1974,34 @@ static int ensure_whole(gac_ctx *c, gac_chainset *cs, hipStream_t s) {
         return GAC_OK;
     }
     HIPCHK(launch_whole_plan(cs->chains, n, cs->w_rdesc, cs->w_nblk, cs->w_gflat, cs->w_tile_r0, s));
+    // k_tile's schedule: the tiles in the target order of their first
+    // blocks (GAC_WHOLE_TILES=set: tile order), so that the tiles an XCD
+    // scores at once share target plane lines in its L2 (chains are in score
+    // order, so neighbouring tiles of the set are far apart on the target)
+    static const bool tiles_set = [] {
+        const char *e = getenv("GAC_WHOLE_TILES");
+        return e && !strcmp(e, "set");
+    }();
+    if (!tiles_set && T > 1) {
+        unsigned long long *keys = nullptr;
+        int32_t *vals = nullptr;
+        void *tmp = nullptr;
+        size_t tmp_bytes = 0;
+        hipError_t e = launch_tile_order(cs->chains, cs->blk, cs->w_tile_r0, T, nullptr, nullptr,
+                                         nullptr, nullptr, tmp_bytes, s);
+        if (e == hipSuccess) e = hipMalloc(&keys, 2 * T * sizeof(unsigned long long));
+        if (e == hipSuccess) e = hipMalloc(&vals, T * 4);
+        if (e == hipSuccess) e = hipMalloc(&cs->w_tile_perm, T * 4);
+        if (e == hipSuccess) e = hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 16));
+        if (e == hipSuccess)
+            e = launch_tile_order(cs->chains, cs->blk, cs->w_tile_r0, T, keys, vals,
+                                  cs->w_tile_perm, tmp, tmp_bytes, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (keys) hipFree(keys);
+        if (vals) hipFree(vals);
+        if (tmp) hipFree(tmp);
+        if (e != hipSuccess) return gac_fail(GAC_E_HIP, "whole-chain tile order: %s", hipGetErrorString(e));
+    }
     // chains without blocks: their results are zeroed by every call
     std::vector<int32_t> nblk(n);
     HIPCHK(hipMemcpyAsync(nblk.data(), cs->w_nblk, n * 4, hipMemcpyDeviceToHost, s));
@@ -1997,6 +2040,7 @@ static int score_whole(gac_ctx *c, const gac_chainset *cs_in, uint32_t flags, lo
     a.gflat = cs->w_gflat;
     a.pb0 = cs->w_sorted ? cs->w_pb0 : cs->w_gflat;
     a.out_perm = cs->w_sorted ? cs->w_perm : nullptr;
+    a.tile_perm = cs->w_sorted ? nullptr : cs->w_tile_perm;
     a.tile_r0 = cs->w_tile_r0;
     a.status = cs->w_status;
     a.sum_head = c->sum_head;
@@ -2076,7 +2120,20 @@ extern "C" int gac_score_ranges_device(gac_ctx *c, const gac_chainset *cs, const
     if (n > 0 && (!d_ranges || !d_g || !d_ali)) return gac_fail(GAC_E_ARG, "NULL buffer");
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    return score_device(c, cs, (const Range *)d_ranges, n, flags, (long long *)d_g,
+    return score_device(c, cs, (const Range *)d_ranges, nullptr, n, flags, (long long *)d_g,
+                        (long long *)d_l, d_ali, s);
+}
+
+extern "C" int gac_score_windows_device(gac_ctx *c, const gac_chainset *cs,
+                                        const gac_window *d_wins, int64_t n, uint32_t flags,
+                                        int64_t *d_g, int64_t *d_l, int32_t *d_ali, void *stream) {
+    gac_clear_error();
+    if (!c) return gac_fail(GAC_E_ARG, "NULL context");
+    CTX_LOCK(c);
+    if (n > 0 && (!d_wins || !d_g || !d_ali)) return gac_fail(GAC_E_ARG, "NULL buffer");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return score_device(c, cs, nullptr, (const Window *)d_wins, n, flags, (long long *)d_g,
                         (long long *)d_l, d_ali, s);
 }
 
@@ -2253,7 +2310,50 @@ extern "C" int gac_score_ranges(gac_ctx *c, const gac_chainset *cs, const gac_ra
     }
     hipStream_t s = c->stream;
     HIPCHK(hipMemcpyAsync(c->d_ranges, ranges, n * sizeof(Range), hipMemcpyHostToDevice, s));
-    int rc = score_device(c, cs, c->d_ranges, n, flags, c->d_g, c->d_l, c->d_ali, s);
+    int rc = score_device(c, cs, c->d_ranges, nullptr, n, flags, c->d_g, c->d_l, c->d_ali, s);
+    if (rc != GAC_OK) return rc;
+    HIPCHK(hipMemcpyAsync(global, c->d_g, n * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(ali, c->d_ali, n * 4, hipMemcpyDeviceToHost, s));
+    if (flags & GAC_WANT_LOCAL)
+        HIPCHK(hipMemcpyAsync(local, c->d_l, n * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return GAC_OK;
+}
+
+extern "C" int gac_score_windows(gac_ctx *c, const gac_chainset *cs, const gac_window *wins,
+                                 int64_t n, uint32_t flags, int64_t *global, int64_t *local,
+                                 int32_t *ali) {
+    gac_clear_error();
+    if (!c) return gac_fail(GAC_E_ARG, "NULL context");
+    CTX_LOCK(c);
+    if (n < 0) return gac_fail(GAC_E_ARG, "negative window count");
+    if (n == 0) return GAC_OK;
+    if (!wins || !global || !ali || ((flags & GAC_WANT_LOCAL) && !local))
+        return gac_fail(GAC_E_ARG, "NULL buffer");
+    if (!cs) return gac_fail(GAC_E_ARG, "NULL chainset");
+    HIPCHK(hipSetDevice(c->device));
+    // the window records in the range staging buffer (20 B each: sized by
+    // the 12-B ranges' capacity + one half)
+    const int64_t need = (n * (int64_t)sizeof(Window) + sizeof(Range) - 1) / sizeof(Range);
+    if (need > c->io_n) {
+        int64_t cap = need + need / 2 + 1024;
+        if (c->d_ranges) hipFree(c->d_ranges);
+        if (c->d_g) hipFree(c->d_g);
+        if (c->d_l) hipFree(c->d_l);
+        if (c->d_ali) hipFree(c->d_ali);
+        c->d_ranges = nullptr;
+        c->d_g = c->d_l = nullptr;
+        c->d_ali = nullptr;
+        HIPCHK(hipMalloc(&c->d_ranges, cap * sizeof(Range)));
+        HIPCHK(hipMalloc(&c->d_g, cap * 8));
+        HIPCHK(hipMalloc(&c->d_l, cap * 8));
+        HIPCHK(hipMalloc(&c->d_ali, cap * 4));
+        c->io_n = cap;
+    }
+    hipStream_t s = c->stream;
+    Window *d_w = reinterpret_cast<Window *>(c->d_ranges);
+    HIPCHK(hipMemcpyAsync(d_w, wins, n * sizeof(Window), hipMemcpyHostToDevice, s));
+    int rc = score_device(c, cs, nullptr, d_w, n, flags, c->d_g, c->d_l, c->d_ali, s);
     if (rc != GAC_OK) return rc;
     HIPCHK(hipMemcpyAsync(global, c->d_g, n * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(ali, c->d_ali, n * 4, hipMemcpyDeviceToHost, s));

@@ -109,6 +109,14 @@ struct Range {
     int32_t chain, t_start, t_end;
 };
 
+// A range with its window of blocks known to the caller (gac_window):
+// chain-local first block and count (chainSubsetOnT's window of
+// [t_start, t_end)).
+struct Window {
+    int32_t chain, t_start, t_end, first, nblk;
+};
+static_assert(sizeof(Window) == 20, "Window layout (gac_window)");
+
 // Result of one range of a small batch (k_small writes it straight to pinned
 // host memory).
 struct SmallOut {
@@ -130,6 +138,7 @@ struct ScoreArgs {
     const int2 *tspan;   // [n_blocks + 8] {tStart, tEnd} (window searches; padded)
     const uint32_t *bucket;  // chain bucket indexes (see DChain)
     const Range *ranges;
+    const Window *wins;  // non-null: the ranges come with their windows (k_plan<true>)
     int64_t n;
     // workspace
     RangeDesc *rdesc;    // [n]
@@ -147,7 +156,8 @@ struct ScoreArgs {
     int32_t *agg;        // [G]   window blocks of each plan workgroup (k_plan; saturated)
     int32_t *plan_off;   // [G+1] flat offset of plan workgroup w
     int32_t *status;     // [8]   W (flat blocks, saturated), T (tiles), 1 = workspace too
-                         //       small
+                         //       small; status[5]: a window lay outside its chain (k_plan<true>,
+                         //       published to host_status[3] and cleared)
     int32_t *host_status;  // pinned host words: status[0..4) + call_tag (k_scan_agg)
     int32_t call_tag;
     int32_t cap_tiles;   // tile_r0 / sum_head / sum_tail capacity
@@ -169,6 +179,8 @@ struct ScoreArgs {
     GapDev gap;
     const int32_t *out_perm;  // non-null: the results of range (position) p go to
                               // chain out_perm[p] (the whole-chain plan in target order)
+    const int32_t *tile_perm; // non-null: k_tile's schedule, tile_perm[k] = the k-th tile
+                              // scored (whole chains: target order of the tiles' first blocks)
 };
 
 constexpr int kSmallMax = 256;  // ranges per small-batch call

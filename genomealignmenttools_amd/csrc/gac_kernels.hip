@@ -691,6 +691,41 @@ __device__ __forceinline__ RangeDesc plan_range(const ScoreArgs &a, const Range 
     return d;
 }
 
+// A range whose window the caller knows (gac_score_windows: chainNet's
+// netting found each fill's blocks while making it, chainNet.c:557-608):
+// only the chain record is read.  A range covering the chain is the whole
+// chain, as in plan_range; a window outside its chain sets `bad` and selects
+// nothing.
+__device__ __forceinline__ RangeDesc plan_window(const ScoreArgs &a, const Window w, bool &bad) {
+    RangeDesc d;
+    d.tbase = 0;
+    d.qbase = 0;
+    d.b0 = 0;
+    d.nblk = 0;
+    d.s = w.t_start;
+    d.e = w.t_end;
+    if (w.chain < 0 || w.chain >= a.n_chains) {
+        bad = true;
+        return d;
+    }
+    const DChain c = a.chains[w.chain];
+    d.tbase = c.tbase;
+    d.qbase = c.qbase;
+    if (w.first < 0 || w.nblk < 0 || (int64_t)w.first + w.nblk > c.nblk) {
+        bad = true;
+        return d;
+    }
+    if (c.nblk == 0 || w.t_start >= w.t_end) return d;
+    if (w.t_start <= c.tstart && w.t_end >= c.tend) {  // chain.c:499-505
+        d.nblk = c.nblk;
+        d.b0 = (int32_t)c.blk_off;
+        return d;
+    }
+    d.nblk = w.nblk;
+    d.b0 = (int32_t)(c.blk_off + w.first);
+    return d;
+}
+
 // ------------------------------------------------------------ k_plan -----
 // One lane per range: plan, then the workgroup's scan of its window blocks:
 // goff[i] = exclusive prefix inside plan workgroup w = i / 256, pb0[i] =
@@ -723,13 +758,16 @@ __device__ __forceinline__ long long wg_exclusive_scan(long long v, long long *s
     return pre + incl - v;
 }
 
+template <bool WIN>
 __global__ void __launch_bounds__(kPlanWG, 8) k_plan(ScoreArgs a) {
     __shared__ long long s_wsum[kPlanWG / kWave];
     const int tid = threadIdx.x;
     const int64_t i = (int64_t)blockIdx.x * kPlanWG + tid;
     int nb = 0;
     if (i < a.n) {
-        const RangeDesc d = plan_range(a, a.ranges[i]);
+        bool bad = false;
+        const RangeDesc d = WIN ? plan_window(a, a.wins[i], bad) : plan_range(a, a.ranges[i]);
+        if (WIN && bad) atomicOr(&a.status[5], 1);
         a.rdesc[i] = d;
         a.nblk[i] = nb = d.nblk;
         a.pb0[i] = d.b0;
@@ -784,11 +822,13 @@ __device__ long long scan_totals(const ScoreArgs &a, int G, long long *s_wsum) {
 __device__ __forceinline__ void publish_status(const ScoreArgs &a, long long W) {
     const long long T = (W + kTileBlocks - 1) / kTileBlocks;
     const bool over = W >= 0x7fffffffLL || T > a.cap_tiles;
-    const int32_t st[4] = {(int32_t)W, (int32_t)T, over ? 1 : 0, 0};
+    const int32_t bad = a.status[5];  // (k_plan<true>; cleared for the next call)
+    const int32_t st[4] = {(int32_t)W, (int32_t)T, over ? 1 : 0, bad};
     for (int k = 0; k < 4; ++k) {
-        a.status[k] = st[k];
+        a.status[k] = k == 3 ? 0 : st[k];
         __hip_atomic_store(&a.host_status[k], st[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    if (bad) a.status[5] = 0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: values before the tag
     __hip_atomic_store(&a.host_status[4], a.call_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -941,6 +981,19 @@ __global__ void __launch_bounds__(256) k_whole_plan_sorted(const DChain *chains,
     const int64_t g = gflat[p], end = g + ch.nblk;
     for (int64_t t = (g + kTileBlocks - 1) / kTileBlocks; t * kTileBlocks < end; ++t)
         tile_r0[t] = (int32_t)p;
+}
+
+// Whole-chain tile schedule: key of tile t = global target base of its
+// first block (set order: flat block = block index, the tile's first chain
+// is tile_r0[t]).
+__global__ void __launch_bounds__(256) k_tile_keys(const DChain *chains, const int4 *blk,
+                                                   const int32_t *tile_r0, int64_t T,
+                                                   unsigned long long *key, int32_t *val) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const DChain c = chains[tile_r0[t]];
+    key[t] = (unsigned long long)(c.tbase + blk[t * kTileBlocks].x);
+    val[t] = (int32_t)t;
 }
 
 // outputs of the ranges in `list` (chains without blocks) := 0
@@ -1393,18 +1446,26 @@ __global__ void __launch_bounds__(256, SYM ? GAC_TILE_MINB : 6) k_tile(ScoreArgs
     // (their lines only, not those of 64 ranges), consumed at the top of t'
     // from LDS by a 6-step owner search.  (Whole-chain plans in set order
     // have pb0 == gflat: one load.)
-    int tile = L8 * kWavesPerWG + wave;
+    // lt: the wave's place in the schedule; the tile it scores is lt itself,
+    // or a.tile_perm[lt] (whole chains: tiles in the target order of their
+    // first blocks, so the tiles an XCD holds at once read neighbouring
+    // target lines -- each tile's partial sums still go to its own slot, and
+    // the fold combines them in tile order)
+    int lt = L8 * kWavesPerWG + wave;
     if (a.xcd_chunk && G % 8 == 0) {  // (probe) XCD x: tiles [x C, (x + 1) C)
         const int C = (T + 7) / 8;
-        tile = (b % 8) * C + (b / 8) * kWavesPerWG + wave;
+        lt = (b % 8) * C + (b / 8) * kWavesPerWG + wave;
         stride = (G / 8) * kWavesPerWG;
         tend = T < (b % 8 + 1) * C ? T : (b % 8 + 1) * C;
     }
+    const int32_t *perm = a.tile_perm;
+    const auto tile_at = [&](int x) { return perm ? perm[x] : x; };
     const int n = (int)a.n;
     const bool same_pb = a.pb0 == a.gflat;
     const auto cand_end = [&](int t) { return t + 1 < T ? a.tile_r0[t + 1] : n - 1; };
     int r0 = 0, gv = 0x7fffffff, bv = 0;
-    if (tile < tend) {
+    int tile = lt < tend ? tile_at(lt) : 0;
+    if (lt < tend) {
         r0 = a.tile_r0[tile];
         const int r1 = cand_end(tile);
         if (r0 + lane <= r1 && r0 + lane < n) {
@@ -1412,15 +1473,16 @@ __global__ void __launch_bounds__(256, SYM ? GAC_TILE_MINB : 6) k_tile(ScoreArgs
             bv = same_pb ? gv : a.pb0[r0 + lane];
         }
     }
-    for (; tile < tend; tile += stride) {
+    for (; lt < tend; lt += stride) {
         const int j = tile * kTileBlocks + lane;
         const bool active = j < W;
         L.cg[lane] = gv;
         L.cb[lane] = bv;
         const int rc = r0;
-        const int tn = tile + stride;
+        const int ltn = lt + stride;
+        const int tn = ltn < tend ? tile_at(ltn) : 0;
         int r0n = 0, r1n = 0;
-        if (tn < tend) {
+        if (ltn < tend) {
             r0n = a.tile_r0[tn];
             r1n = cand_end(tn);
         }
@@ -1431,12 +1493,13 @@ __global__ void __launch_bounds__(256, SYM ? GAC_TILE_MINB : 6) k_tile(ScoreArgs
         if (active) B = lane_block(a.rdesc[ri], load_blk12(a, bi), bi);
         gv = 0x7fffffff;
         bv = 0;
-        if (tn < tend && r0n + lane <= r1n && r0n + lane < n) {
+        if (ltn < tend && r0n + lane <= r1n && r0n + lane < n) {
             gv = a.gflat[r0n + lane];
             bv = same_pb ? gv : a.pb0[r0n + lane];
         }
         r0 = r0n;
         tile_score<LOCAL, SYM>(a, L, lane, tile, j, active, W, ri, B, 0);
+        tile = tn;
     }
 }
 
@@ -1947,7 +2010,10 @@ namespace gac {
 int plan_grid(int64_t n) { return (int)((n + kPlanWG - 1) / kPlanWG); }
 
 hipError_t launch_plan(const ScoreArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(k_plan, dim3((unsigned)plan_grid(a.n)), dim3(kPlanWG), 0, s, a);
+    if (a.wins)
+        hipLaunchKernelGGL(k_plan<true>, dim3((unsigned)plan_grid(a.n)), dim3(kPlanWG), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_plan<false>, dim3((unsigned)plan_grid(a.n)), dim3(kPlanWG), 0, s, a);
     return hipGetLastError();
 }
 
@@ -2089,6 +2155,27 @@ hipError_t launch_whole_plan_sorted(const DChain *chains, int64_t n, int32_t *pe
     hipLaunchKernelGGL(k_whole_plan_sorted, grid, dim3(256), 0, s, chains, perm, n, gflat, rdesc,
                        pb0, tile_r0, inv);
     return hipGetLastError();
+}
+
+// tiles of a whole-chain plan (set order) sorted by their first block's
+// global target base: perm[T]; tmp == nullptr: tmp_bytes := the scratch size
+hipError_t launch_tile_order(const DChain *chains, const int4 *blk, const int32_t *tile_r0,
+                             int64_t T, unsigned long long *keys, int32_t *vals, int32_t *perm,
+                             void *tmp, size_t &tmp_bytes, hipStream_t s) {
+    size_t b_sort = 0;
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, b_sort, keys, keys + T, vals, perm,
+                                                      (int)T, 0, kOrderBits, s);
+    if (e != hipSuccess) return e;
+    if (!tmp) {
+        tmp_bytes = b_sort;
+        return hipSuccess;
+    }
+    if (tmp_bytes < b_sort) return hipErrorInvalidValue;
+    if (T == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_tile_keys, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, s, chains,
+                       blk, tile_r0, T, keys, vals);
+    return hipcub::DeviceRadixSort::SortPairs(tmp, b_sort, keys, keys + T, vals, perm, (int)T, 0,
+                                              kOrderBits, s);
 }
 
 hipError_t launch_zero_list(const int32_t *list, int64_t n, long long *g, long long *l,

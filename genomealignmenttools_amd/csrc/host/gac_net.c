@@ -60,6 +60,10 @@ struct nfill {
     int64_t ord;  /* pre-order index on its side */
     ngap *pgap;   /* parent gap; index in pgap->fills; fills above this one */
     int32_t pidx, level;
+    /* T side: the blocks chainSubsetOnT(chain, start, end) selects
+     * (chain.c:481-500: from the first with tEnd > start while tStart < end),
+     * chain-local first block and count, known from the netting's own walk */
+    int32_t wb0, wn;
 };
 
 typedef struct nchrom {
@@ -608,7 +612,7 @@ static void it_push(nwork *w, int32_t s, int32_t e, ngap *g) {
 static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int32_t chain, int nb,
                            const int32_t *s, const int32_t *e, const int32_t *gos,
                            const int32_t *goe, const int32_t *os, int inv, int oflip, int cstart,
-                           int cend) {
+                           int cend, int boff) {
     sp_query(n, c, cstart, cend, s, e, nb);
     const int64_t nsp = n->q_n;
     /* each filled space's gap gets the fill pushed: its line is a cache
@@ -626,6 +630,7 @@ static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int32_t chai
          * space outside [start, end) */
         int start = BIGNUM, end = -BIGNUM, zero = 0;
         int fs = BIGNUM, fe = -BIGNUM, omin = BIGNUM, omax = -BIGNUM; /* (see below) */
+        int wfirst = -1, wlast = -2; /* the blocks seen (window when none is zero-size) */
         int64_t ali = 0;
         for (int b = k; b < nb; ++b) {
             const int b0 = s[b], b1 = e[b];
@@ -633,6 +638,9 @@ static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int32_t chai
                 continue;
             if (b0 >= send)
                 break;
+            if (wfirst < 0)
+                wfirst = b;
+            wlast = b;
             const int cs = b0 < sstart ? sstart : b0, ce = b1 > send ? send : b1;
             if (start > cs)
                 start = cs;
@@ -698,6 +706,22 @@ static void add_chain_side(const gac_net *net, nwork *n, nchrom *c, int32_t chai
             f->o_start = omin;
             f->o_end = omax;
             f->full = fs <= cstart && fe >= cend;
+        }
+        if (boff >= 0) {
+            /* chainSubsetOnT's window of [fs, fe): every block the walk saw
+             * ends after fs (fs is the first clipped start) and starts before
+             * fe -- unless a zero-size block sits at a bound, when the rule is
+             * applied as written */
+            if (zero) {
+                wfirst = k;
+                while (wfirst < nb && e[wfirst] <= fs)
+                    ++wfirst;
+                wlast = wfirst - 1;
+                while (wlast + 1 < nb && s[wlast + 1] < fe)
+                    ++wlast;
+            }
+            f->wb0 = boff + (wfirst < 0 ? 0 : wfirst);
+            f->wn = wfirst < 0 ? 0 : wlast - wfirst + 1;
         }
         /* slAddHead onto the space's gap; region workers of one chromosome
          * side (net_regions) may share the gap, so the push is atomic.  The
@@ -818,7 +842,7 @@ static void add_chain_q(const gac_net *net, nwork *n, int64_t c, nchrom *qc, int
         }
     }
     add_chain_side(net, n, qc, (int32_t)c, m, n->rs, n->re, n->ros, n->roe, n->ro, minus, -1, qs,
-                   qe);
+                   qe, -1);
 }
 
 /* addChainT (chainNet.c:557-608) */
@@ -853,7 +877,7 @@ static void add_chain_t(const gac_net *net, nwork *n, int64_t c, nchrom *tc, int
         }
     }
     add_chain_side(net, n, tc, (int32_t)c, m, n->rs, n->re, n->ros, n->roe, n->ro, 0,
-                   minus ? qsize : -1, in->t_start[c], in->t_end[c]);
+                   minus ? qsize : -1, in->t_start[c], in->t_end[c], l0);
 }
 
 /* ------------------------------------------------------------ finish */
@@ -1851,6 +1875,7 @@ typedef struct gf_job {
     uint8_t *flags;
     int64_t per;
     _Atomic int64_t next;
+    int32_t *wb0, *wn; /* gac_net_get_fill_windows */
 } gf_job;
 
 static void *fills_thread(void *arg) {
@@ -1877,6 +1902,10 @@ static void *fills_thread(void *arg) {
                 J->ali[i] = sz;
             if (J->flags)
                 J->flags[i] = (uint8_t)(full ? 0 : 1);
+            if (J->wb0)
+                J->wb0[i] = f->wb0;
+            if (J->wn)
+                J->wn[i] = f->wn;
         }
     }
     return NULL;
@@ -1917,7 +1946,7 @@ int gac_net_get_fills(const gac_net *n, int side, int32_t *chain, int32_t *start
         return gac_fail(GAC_E_STATE, "gac_net_get_fills: side %d was not netted", side);
     const int nt = gac_host_threads();
     const int64_t nf = n->n_order[side];
-    gf_job J = {n, side, chain, start, end, ali, flags, nf / (8 * (int64_t)nt) + 1, 0};
+    gf_job J = {n, side, chain, start, end, ali, flags, nf / (8 * (int64_t)nt) + 1, 0, NULL, NULL};
     atomic_init(&J.next, 0);
     const int64_t nrun = (nf + J.per - 1) / J.per;
     gac_mark("get_fills: fills");
@@ -1931,6 +1960,21 @@ int gac_net_get_fills(const gac_net *n, int side, int32_t *chain, int32_t *start
         gac_run_threads(nt < nrun ? nt : (int)(nrun ? nrun : 1), visible_thread, &J);
     }
     gac_mark("get_fills: done");
+    return GAC_OK;
+}
+
+int gac_net_get_fill_windows(const gac_net *n, int side, int32_t *first_block, int32_t *n_blocks) {
+    if (!n || side != GAC_T)
+        return gac_fail(GAC_E_ARG, "gac_net_get_fill_windows: target side only");
+    if (!(n->sides & (1 << side)))
+        return gac_fail(GAC_E_STATE, "gac_net_get_fill_windows: side %d was not netted", side);
+    const int nt = gac_host_threads();
+    const int64_t nf = n->n_order[side];
+    gf_job J = {n, side, NULL, NULL, NULL, NULL, NULL, nf / (8 * (int64_t)nt) + 1, 0, first_block,
+                n_blocks};
+    atomic_init(&J.next, 0);
+    const int64_t nrun = (nf + J.per - 1) / J.per;
+    gac_run_threads(nt < nrun ? nt : (int)(nrun ? nrun : 1), fills_thread, &J);
     return GAC_OK;
 }
 

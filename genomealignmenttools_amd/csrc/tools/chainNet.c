@@ -346,9 +346,9 @@ static void *check_thread(void *arg) {
 /* chainNet -rescore's rescoring list: the target fills that are partial
  * (flag 1) and printed (flag 2), in fill order */
 typedef struct range_job {
-    const int32_t *fc, *fs, *fe;
+    const int32_t *fc, *fs, *fe, *fw0, *fwn;
     const uint8_t *fl;
-    gac_range *r;
+    gac_window *r;
     int64_t *rix;
     int64_t nf;
     int nt;
@@ -374,6 +374,8 @@ static void *range_thread(void *arg) {
                 J->r[o].chain = J->fc[i];
                 J->r[o].t_start = J->fs[i];
                 J->r[o].t_end = J->fe[i];
+                J->r[o].first_block = J->fw0[i];
+                J->r[o].n_blocks = J->fwn[i];
                 J->rix[o++] = i;
             }
     }
@@ -601,13 +603,17 @@ int main(int argc, char *argv[]) {
                 *fe = malloc((nf ? nf : 1) * 4);
         uint8_t *fl = malloc(nf ? nf : 1);
         int32_t *fa = malloc((nf ? nf : 1) * 4);
+        int32_t *fw0 = malloc((nf ? nf : 1) * 4), *fwn = malloc((nf ? nf : 1) * 4);
         gt_check(gac_net_get_fills(net, GAC_T, fc, fs, fe, fa, fl));
-        gac_range *r = malloc((nf ? nf : 1) * sizeof(gac_range));
+        /* each fill's block window, found by the netting when it made the
+         * fill: the device reads it instead of searching the chain */
+        gt_check(gac_net_get_fill_windows(net, GAC_T, fw0, fwn));
+        gac_window *r = malloc((nf ? nf : 1) * sizeof(gac_window));
         int64_t *rix = malloc((nf ? nf : 1) * 8);
         gac_mark("fill list: ranges");
         /* the partial, printed fills in order: counted per slice, then
          * placed, on all threads */
-        range_job RJ = {fc, fs, fe, fl, r, rix, nf, gt_threads(), NULL, 0, 0};
+        range_job RJ = {fc, fs, fe, fw0, fwn, fl, r, rix, nf, gt_threads(), NULL, 0, 0};
         RJ.cnt = calloc((size_t)RJ.nt + 1, 8);
         atomic_init(&RJ.next, 0);
         gac_run_threads(RJ.nt, range_thread, &RJ);
@@ -622,12 +628,13 @@ int main(int argc, char *argv[]) {
         free(RJ.cnt);
         tscores = calloc(nf ? nf : 1, 8);
         /* GAC_DUMP_RANGES=FILE (measurement hook, one process only): the
-         * rescored fills as int32 (chain index in file order, tStart, tEnd),
-         * in submission order -- bench.py replays them in its kernel leg */
+         * rescored fills as gac_window records (int32 chain index in file
+         * order, tStart, tEnd, first block, block count), in submission order
+         * -- bench.py replays them in its kernel leg */
         const char *dump = multi ? NULL : getenv("GAC_DUMP_RANGES");
         if (dump && *dump) {
             FILE *df = fopen(dump, "wb");
-            if (!df || (nr && fwrite(r, sizeof(gac_range), nr, df) != (size_t)nr) || fclose(df) != 0)
+            if (!df || (nr && fwrite(r, sizeof(gac_window), nr, df) != (size_t)nr) || fclose(df) != 0)
                 gt_abort("can't write %s", dump);
         }
         gac_mark("fill list: join upload");
@@ -652,7 +659,7 @@ int main(int argc, char *argv[]) {
             gt_stage("device open + 2bit genomes + chains to HBM (rest)");
             int64_t *g = malloc(nr * 8);
             int32_t *ali = malloc(nr * 4);
-            gt_check(gac_score_ranges(ctx, pu.cs, r, nr, 0, g, NULL, ali));
+            gt_check(gac_score_windows(ctx, pu.cs, r, nr, 0, g, NULL, ali));
             gt_stage("GPU fill rescoring");
             for (int64_t k = 0; k < nr; ++k)
                 tscores[rix[k]] = g[k];
@@ -715,7 +722,7 @@ int main(int argc, char *argv[]) {
             gt_stage("chains to HBM");
             int64_t *g = malloc(nr * 8);
             int32_t *ali = malloc(nr * 4);
-            gt_check(gac_score_ranges(ctx, cs, r, nr, 0, g, NULL, ali));
+            gt_check(gac_score_windows(ctx, cs, r, nr, 0, g, NULL, ali));
             gt_stage("GPU fill rescoring");
             for (int64_t k = 0; k < nr; ++k)
                 tscores[rix[k]] = g[k];
@@ -744,6 +751,8 @@ int main(int argc, char *argv[]) {
         free(fe);
         free(fl);
         free(fa);
+        free(fw0);
+        free(fwn);
         free(r);
         free(rix);
     }

@@ -225,6 +225,19 @@ class Engine:
                                      _p(loc) if want_local else None, _p(ali)))
         return g, loc, ali
 
+    def score_windows(self, cs: ChainSet, windows: np.ndarray, want_local: bool = False):
+        """windows: int32 [n, 5] (chain, tStart, tEnd, first block, block count;
+        gac_window).  Returns as score_ranges."""
+        w = np.ascontiguousarray(np.asarray(windows, dtype=np.int32).reshape(-1, 5))
+        n = w.shape[0]
+        g = np.zeros(n, np.int64)
+        ali = np.zeros(n, np.int32)
+        loc = np.zeros(n, np.int64) if want_local else None
+        check(lib().gac_score_windows(self.h, cs.handle, _p(w), n,
+                                      GAC_WANT_LOCAL if want_local else 0, _p(g),
+                                      _p(loc) if want_local else None, _p(ali)))
+        return g, loc, ali
+
     def full_ranges(self, ca) -> np.ndarray:
         return np.stack([np.arange(ca.n, dtype=np.int32), ca.tstart.astype(np.int32),
                          ca.tend.astype(np.int32)], axis=1)
@@ -267,6 +280,13 @@ class Engine:
                             d_l: int = 0, want_local: bool = False, stream: int = 0) -> None:
         check(lib().gac_score_ranges_device(
             self.h, cs.handle, C.c_void_p(d_ranges), n, GAC_WANT_LOCAL if want_local else 0,
+            C.c_void_p(d_g), C.c_void_p(d_l) if d_l else None, C.c_void_p(d_ali),
+            C.c_void_p(stream) if stream else None))
+
+    def score_windows_device(self, cs: ChainSet, d_windows: int, n: int, d_g: int, d_ali: int,
+                             d_l: int = 0, want_local: bool = False, stream: int = 0) -> None:
+        check(lib().gac_score_windows_device(
+            self.h, cs.handle, C.c_void_p(d_windows), n, GAC_WANT_LOCAL if want_local else 0,
             C.c_void_p(d_g), C.c_void_p(d_l) if d_l else None, C.c_void_p(d_ali),
             C.c_void_p(stream) if stream else None))
 

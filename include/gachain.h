@@ -12,6 +12,7 @@
  *
  * Reference interfaces replaced (paths relative to the reference root):
  *   gac_score_ranges      <- chainSubsetOnT      kent/src/lib/chain.c:471-558
+ *   (gac_score_windows: the same, windows known -- chainFastSubsetOnT :489-558)
  *                          + chainCalcScore       kent/src/lib/chainConnect.c:24-40
  *                          + chainScoreBlock      kent/src/lib/chainConnect.c:14-22
  *                          + gapCalcCost          kent/src/lib/gapCalc.c:298-331
@@ -83,6 +84,23 @@ typedef struct gac_range {
     int32_t t_start;
     int32_t t_end;
 } gac_range;
+
+/* A sub-chain whose block window the caller already knows: chain, half-open
+ * target range, and the blocks chainSubsetOnT(chain, t_start, t_end) selects
+ * (kent/src/lib/chain.c:481-500: from the first block with tEnd > t_start,
+ * while tStart < t_end) as a chain-local first block and count.  chainNet's
+ * netting walks a fill's blocks when it creates the fill (innerBounds,
+ * src/chainNet/chainNet.c:356-391), so its fills come with their windows
+ * (gac_net_get_fill_windows) and scoring them needs no block search
+ * (subchainInfo's three rescans, chainNet.c:795-843).  A window covering the
+ * chain's span scores the whole chain, as a gac_range does. */
+typedef struct gac_window {
+    int32_t chain;
+    int32_t t_start;
+    int32_t t_end;
+    int32_t first_block; /* chain-local index of the window's first block */
+    int32_t n_blocks;    /* blocks in the window (0: scores 0) */
+} gac_window;
 
 /* Parsed chains, struct-of-arrays.  Blocks of chain c are
  * blk_*[blk_off[c] .. blk_off[c+1]), in chain order (ascending t and q;
@@ -195,6 +213,22 @@ int gac_score_ranges_device(gac_ctx *ctx, const gac_chainset *cs,
                             const gac_range *d_ranges, int64_t n, uint32_t flags,
                             int64_t *d_global, int64_t *d_local, int32_t *d_ali,
                             void *stream);
+
+/* gac_score_ranges for sub-chains given with their windows (gac_window): the
+ * same results as gac_score_ranges on (chain, t_start, t_end) when each window
+ * is chainSubsetOnT's; the device reads one chain record per window instead of
+ * searching the chain's blocks.  A window outside its chain (first_block < 0,
+ * n_blocks < 0, or past the chain's last block; chain out of range) is
+ * GAC_E_ARG.  Host buffers, synchronous. */
+int gac_score_windows(gac_ctx *ctx, const gac_chainset *cs, const gac_window *windows,
+                      int64_t n, uint32_t flags, int64_t *global, int64_t *local,
+                      int32_t *ali);
+/* The same on device-resident buffers, enqueued on `stream` (NULL: the
+ * context's); returns as gac_score_ranges_device does (a bad window is
+ * reported by this call, once the planning kernel has run). */
+int gac_score_windows_device(gac_ctx *ctx, const gac_chainset *cs, const gac_window *d_windows,
+                             int64_t n, uint32_t flags, int64_t *d_global, int64_t *d_local,
+                             int32_t *d_ali, void *stream);
 
 /* Every chain of the set, in order -- scoreChain's batch (the per-chain
  * chainCalcScore + chainCalcScoreLocal of src/scoreChain/scoreChain.c:207-220,
@@ -400,6 +434,11 @@ int64_t gac_net_fill_count(const gac_net *net, int side);
  * its ancestors have ali >= min_fill).  Any pointer may be NULL. */
 int gac_net_get_fills(const gac_net *net, int side, int32_t *chain, int32_t *start,
                       int32_t *end, int32_t *ali, uint8_t *flags);
+/* Per target fill, in gac_net_get_fills order: the window of the fill's chain
+ * that chainSubsetOnT(chain, start, end) selects (gac_window's first_block /
+ * n_blocks), recorded while netting.  side must be GAC_T. */
+int gac_net_get_fill_windows(const gac_net *net, int side, int32_t *first_block,
+                             int32_t *n_blocks);
 /* Write one side's .net (outputNetSide) to path ("stdout" allowed) after the
  * n_meta '#' metadata lines.  t_scores (T side only, may be NULL): per fill
  * in gac_net_get_fills order, the rescored global score of partial fills

@@ -274,6 +274,45 @@ int gac_score_ranges(gac_ctx *c, const gac_chainset *s, const gac_range *r, int6
     return GAC_OK;
 }
 
+/* windows: each one checked against chainSubsetOnT's walk (kent/src/lib/
+ * chain.c:481-500: first block with tEnd > tStart, then while tStart < tEnd)
+ * -- the netting's recorded windows must be exactly those -- then scored as
+ * its range */
+int gac_score_windows(gac_ctx *c, const gac_chainset *s, const gac_window *w, int64_t n,
+                      uint32_t flags, int64_t *g, int64_t *l, int32_t *ali) {
+    gac_range *r = malloc((size_t)(n ? n : 1) * sizeof(gac_range));
+    for (int64_t i = 0; i < n; ++i) {
+        const int32_t k = w[i].chain;
+        if (k < 0 || k >= s->n) {
+            free(r);
+            return gac_fail(GAC_E_ARG, "window %lld: chain %d out of range", (long long)i, k);
+        }
+        const int64_t b0 = s->off[k], b1 = s->off[k + 1];
+        const int32_t ts = b1 > b0 ? s->bt[b0] : 0, te = b1 > b0 ? s->bt[b1 - 1] + s->bs[b1 - 1] : 0;
+        if (!(w[i].t_start <= ts && w[i].t_end >= te) && w[i].t_start < w[i].t_end) {
+            int64_t f = b0, e;
+            while (f < b1 && s->bt[f] + s->bs[f] <= w[i].t_start)
+                ++f;
+            for (e = f; e < b1 && s->bt[e] < w[i].t_end; ++e)
+                ;
+            if (w[i].first_block != f - b0 || w[i].n_blocks != e - f) {
+                fprintf(stderr, "cpu stub: window %lld of chain %d [%d, %d): got blocks %d + %d, "
+                                "chainSubsetOnT selects %lld + %lld\n", (long long)i, k,
+                        w[i].t_start, w[i].t_end, w[i].first_block, w[i].n_blocks,
+                        (long long)(f - b0), (long long)(e - f));
+                free(r);
+                return gac_fail(GAC_E_ARG, "window mismatch");
+            }
+        }
+        r[i].chain = k;
+        r[i].t_start = w[i].t_start;
+        r[i].t_end = w[i].t_end;
+    }
+    const int rc = gac_score_ranges(c, s, r, n, flags, g, l, ali);
+    free(r);
+    return rc;
+}
+
 /* ---- gac_chain_dp / gac_crossovers: a lane-by-lane CPU emulation of the
  * device algorithm of k_dp / k_xover (csrc/gac_dp.hip) -- windows of 64
  * pre-order nodes resolved by prefix-max rounds, crossovers by prefix sum

@@ -50,6 +50,43 @@ def test_ranges_vs_oracle(seed):
     assert np.array_equal(a, oa)
 
 
+@pytest.mark.parametrize("seed", [1, 4])
+def test_windows_vs_oracle(seed):
+    """gac_score_windows (the range's window given, k_plan<true>) equals the
+    oracle on the same sub-chains: random and covering ranges, empty windows,
+    zero-size end blocks, both strands, a batch large enough for the
+    multi-kernel pipeline and a small one; a window outside its chain is
+    GAC_E_ARG and the context stays usable."""
+    from genomealignmenttools_amd import synth
+    from genomealignmenttools_amd._lib import GacError
+    from test_host import subset_windows
+    tg, qg, ca = synth.small_case(seed=seed, n_chains=400, max_blocks=600)
+    if seed == 4:
+        ca = synth.zero_end_blocks(ca, every=3)
+    e, cs = _setup(None, tg, qg, ca)
+    R = _ranges(ca, np.random.default_rng(seed), per_chain=4)
+    first, cnt = subset_windows(ca, R[:, 0], R[:, 1], R[:, 2])
+    W = np.concatenate([R, first[:, None], cnt[:, None]], 1).astype(np.int32)
+    og, ol, oa = _oracle(tg, qg).score_ranges(ca, R)
+    for sel in (slice(None), slice(0, 100)):
+        g, l, a = e.score_windows(cs, W[sel], want_local=True)
+        assert np.array_equal(g, og[sel]) and np.array_equal(l, ol[sel]) and np.array_equal(a, oa[sel])
+    # the same ranges searched on the device
+    g2, _, a2 = e.score_ranges(cs, R)
+    assert np.array_equal(g2, og) and np.array_equal(a2, oa)
+    nb = np.diff(ca.blk_off)
+    for bad in ((0, 1, 2, -1, 1), (0, 1, 2, 0, int(nb[0]) + 1), (1, 1, 2, int(nb[1]), 1),
+                (ca.n, 0, 5, 0, 0), (0, 1, 2, 0, -1)):
+        Wb = W.copy()
+        Wb[len(W) // 2] = bad
+        with pytest.raises(GacError):
+            e.score_windows(cs, Wb)
+    g, _, a = e.score_windows(cs, W)
+    assert np.array_equal(g, og) and np.array_equal(a, oa)
+    cs.close()
+    e.close()
+
+
 @pytest.mark.parametrize("order", ["scoring-first", "chains-first"])
 def test_scoring_before_and_after_upload(order):
     """The block gap costs come from the upload pass when the scoring is set

@@ -103,6 +103,60 @@ def test_chainfile_roundtrip(tmp_path):
     assert open(out).read() == "".join(body)
 
 
+def subset_windows(ca, chain, s, e):
+    """chainSubsetOnT's window (kent/src/lib/chain.c:481-500) of each (chain,
+    s, e): chain-local first block with tEnd > s, and the count of blocks from
+    there with tStart < e."""
+    first, cnt = np.zeros(len(chain), np.int64), np.zeros(len(chain), np.int64)
+    for i, (c, a, b) in enumerate(zip(chain, s, e)):
+        o0, o1 = ca.blk_off[c], ca.blk_off[c + 1]
+        bt, bs = ca.blk_t[o0:o1], ca.blk_size[o0:o1]
+        f = int(np.searchsorted(bt + bs, a, side="right"))
+        k = f
+        while k < len(bt) and bt[k] < b:
+            k += 1
+        first[i], cnt[i] = f, k - f
+    return first, cnt
+
+
+@pytest.mark.parametrize("case", ["synth11", "synth12", "zero_end", "c5", "split"])
+def test_net_fill_windows(case, monkeypatch):
+    """The window of every partial target fill, recorded by the netting while
+    it makes the fill (gac_net_get_fill_windows, what chainNet -rescore hands
+    gac_score_windows), is exactly chainSubsetOnT's window of the fill's final
+    range -- including chains with zero-size blocks at their ends."""
+    from genomealignmenttools_amd import synth
+    from genomealignmenttools_amd._lib import GAC_T
+    from genomealignmenttools_amd.chainfile import read_chains
+    from genomealignmenttools_amd.chainnet import Net
+    from genomealignmenttools_amd.synth import read_sizes
+    if case.startswith("synth"):
+        d = os.path.join(GOLDEN, case)
+        ca = read_chains(os.path.join(d, "in.chain"))
+        ts, qs = read_sizes(os.path.join(d, "t.sizes")), read_sizes(os.path.join(d, "q.sizes"))
+    else:
+        if case == "zero_end":
+            tg, qg, ca = synth.small_case(seed=5, n_chains=300)
+            ca = synth.zero_end_blocks(ca, every=2)
+        elif case == "split":  # one big side netted in regions (chain slices: block offsets)
+            monkeypatch.setenv("GAC_THREADS", "8")
+            monkeypatch.setenv("GAC_TIMING", "1")
+            tg, qg, ca = synth.small_case(seed=21, n_chains=30000, tsize=6_000_000,
+                                          qsizes=(3_000_000, 2_000_000, 1_000_000), max_blocks=3000)
+        else:
+            tg, qg, ca = synth.c5_case(seed=3, n_chains=3000, scale=0.002, min_size=20_000)
+        ts, qs = tg.sizes, qg.sizes
+    for opts in ({}, {"min_space": 1}):
+        net = Net(ca, ts, qs, 0.0, **opts)
+        f = net.fills(GAC_T)
+        part = (f["flags"] & 1) == 1
+        assert part.sum() > 10
+        first, cnt = subset_windows(ca, f["chain"][part], f["start"][part], f["end"][part])
+        assert np.array_equal(f["first_block"][part], first)
+        assert np.array_equal(f["n_blocks"][part], cnt)
+        net.close()
+
+
 @pytest.mark.parametrize("seed", [11, 12])
 def test_netting_engine_vs_reference(seed, tmp_path):
     """Plain chainNet (no -rescore: no GPU involved) through the Python
