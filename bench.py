@@ -97,6 +97,8 @@ def parse():
     p.add_argument("--c2-steps", type=int, default=10)
     p.add_argument("--kernel-steps", type=int, default=20)
     p.add_argument("--no-c2", action="store_true")
+    p.add_argument("--no-c3", action="store_true", help="skip the chainCleaner C3 leg")
+    p.add_argument("--c3-steps", type=int, default=3)
     p.add_argument("--no-c4", action="store_true", help="skip the axtChain C4 leg")
     p.add_argument("--c4-blocks", type=int, default=50_000_000)
     p.add_argument("--c4-steps", type=int, default=1)
@@ -1006,6 +1008,105 @@ def c2_leg(args, steps, warmup):
     return res
 
 
+CC_TOOL = os.path.join(PKG, "bin", "chainCleaner")
+REF_CC_TOOL = os.path.join(REPO, "oracle", "_ref", "chainCleaner")
+
+
+def c3_files(args):
+    """C3 (configs[2]): the C2 shape (hg38 chr1 x mm10, 200 k chains) plus
+    1000 planted chain-breaking loci (synth.c3_case, as
+    tests/test_gpu_configs.py::test_c3_chaincleaner), header scores from
+    bin/scoreChain, sorted and numbered, and the reference pipeline's net
+    (chainNet -minScore=0 | NetFilterNonNested.perl -minScore1 3000; the
+    reference chainNet when it is built, else ours -- byte-identical).
+    Written once per box under --tmp."""
+    d = os.path.join(args.tmp, "gac_bench_c3_42")
+    p = lambda x: os.path.join(d, x)
+    if os.path.exists(p("info.json")):
+        with open(p("info.json")) as f:
+            return d, json.load(f)
+    from genomealignmenttools_amd import chainfile, synth
+    os.makedirs(d, exist_ok=True)
+    t0 = time.time()
+    tg, qg, ca = synth.c3_case(seed=42, n_chains=200_000, n_loci=1000)
+    synth.write_2bit(tg, p("t.2bit"))
+    synth.write_2bit(qg, p("q.2bit"))
+    synth.write_sizes(tg.sizes, p("t.sizes"))
+    synth.write_sizes(qg.sizes, p("q.sizes"))
+    chainfile.write_chains_fast(ca, p("unscored.chain"))
+    del tg, qg, ca
+    run_tool([SC_TOOL, p("unscored.chain"), p("t.2bit"), p("q.2bit"), p("sc.chain"),
+              "-linearGap=loose"], [])
+    sc = chainfile.read_chains(p("sc.chain"))
+    sc = sc.subset(np.argsort(-sc.score, kind="stable"))
+    sc.id = np.arange(1, sc.n + 1, dtype=np.int64)
+    chainfile.write_chains_fast(sc, p("in.chain"))
+    info = {"chains": int(sc.n), "blocks": int(sc.blk_off[-1]), "planted_loci": 1000}
+    del sc
+    net_tool = REF_TOOL if os.path.exists(REF_TOOL) else os.path.join(PKG, "bin", "chainNet")
+    net = subprocess.run([net_tool, "-minScore=0", p("in.chain"), p("t.sizes"), p("q.sizes"),
+                          "stdout", "/dev/null"], capture_output=True, check=True)
+    filt = subprocess.run([os.path.join(PKG, "bin", "NetFilterNonNested.perl"), "/dev/stdin",
+                           "-minScore1", "3000"], input=net.stdout, capture_output=True, check=True)
+    with open(p("in.net"), "wb") as f:
+        f.write(filt.stdout)
+    info["net_from"] = "reference chainNet" if net_tool == REF_TOOL else "bin/chainNet"
+    for x in ("unscored.chain", "sc.chain"):
+        os.remove(p(x))
+    with open(p("info.json"), "w") as f:
+        json.dump(info, f)
+    log(f"C3: written in {time.time() - t0:.1f}s")
+    return d, info
+
+
+def c3_leg(args, steps):
+    """configs[2]: bin/chainCleaner -net= end to end on C3 (the suspect-block
+    rescoring on the GPU, the replay of the reference's decisions on the
+    host), `steps` timed runs (outputs removed outside the clock), then the
+    reference chainCleaner on the same files, timed, and the outputs
+    (chains, removedSuspects.bed) compared byte for byte outside every
+    clock."""
+    d, info = c3_files(args)
+    p = lambda x: os.path.join(d, x)
+    opts = [f"-net={p('in.net')}", "-linearGap=loose"]
+    outs = [p("ours.chain"), p("ours.bed")]
+    cmd = [CC_TOOL, p("in.chain"), p("t.2bit"), p("q.2bit")] + outs + opts
+    run_tool(cmd, outs)  # warmup
+    dt = 0.0
+    for _ in range(steps):
+        for o in outs:
+            if os.path.exists(o):
+                os.remove(o)
+        t0 = time.perf_counter()
+        run_tool(cmd, [])
+        dt += time.perf_counter() - t0
+    dt /= steps
+    r = run_tool(cmd + ["-verbose=2"], [], env=dict(os.environ, GAC_TIMING="1"))
+    with open(p("ours.bed")) as f:
+        removed = sum(1 for _ in f)
+    res = {"workload": "configs[2]: chainCleaner -net= end to end (bin/chainCleaner) on C3: the "
+                       "C2 chain set + 1000 planted chain-breaking loci",
+           "ms_per_step": dt * 1e3, "steps": steps, **info, "removed_suspects": removed,
+           "tool_stages": [x.strip() for x in r.stderr.splitlines() if x.startswith("[")][-20:]}
+    if os.path.exists(REF_CC_TOOL):
+        ro = [p("ref.chain"), p("ref.bed")]
+        for o in ro:
+            if os.path.exists(o):
+                os.remove(o)
+        env = dict(os.environ, PATH=os.path.dirname(REF_CC_TOOL) + os.pathsep + os.environ["PATH"])
+        t0 = time.time()
+        run_tool([REF_CC_TOOL, p("in.chain"), p("t.2bit"), p("q.2bit")] + ro + opts, [], env=env)
+        t1 = time.time() - t0
+        same = filecmp.cmp(outs[0], ro[0], False) and filecmp.cmp(outs[1], ro[1], False)
+        res["reference"] = {"seconds": t1, "cores": 1, "kind": "reference (oracle/_ref/chainCleaner)"}
+        res["identical"] = same
+        res["speedup_vs_reference"] = t1 / dt
+        log(f"C3: ours {dt * 1e3:.0f} ms, reference {t1:.2f}s, outputs identical: {same}")
+    else:
+        res["identical"] = None
+    return res
+
+
 # ---------------------------------------------------------------- main
 def main():
     args = parse()
@@ -1140,6 +1241,11 @@ def main():
             out["c2"] = c2_leg(args, args.c2_steps, 1)
         except Exception as ex:  # reported, never fatal
             out["c2"] = {"error": str(ex)[:300]}
+    if rank == 0 and world == 1 and not args.no_c3:
+        try:
+            out["c3"] = c3_leg(args, args.c3_steps)
+        except Exception as ex:  # (reported, never fatal to the headline)
+            out["c3"] = {"error": str(ex)[:300]}
     if not args.no_c4:
         try:
             c4 = c4_leg(args, dist, world, rank, local, barrier, step_env)

@@ -1145,6 +1145,22 @@ extern "C" int gac_chain_dp(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq, c
                             const int32_t *leaf, const int32_t *leaf_score,
                             const int32_t *leaf_node, const int64_t *path_off,
                             const int32_t *path, int64_t *total, int32_t *pred) {
+    return gac_chain_dp_ex(c, n_pairs, t_seq, q_seq, q_strand, node_off, node_a, node_b, leaf_off,
+                           leaf, leaf_score, leaf_node, path_off, path, nullptr, nullptr, 0, 0,
+                           total, pred);
+}
+
+// gac_chain_dp with the exact fast DP (k_dp_fast) when ov_off is given: the
+// linear gap-cost minorant lin_k / 1024, the smallest matrix entry, and each
+// leaf's overlapping candidates (leaf nodes; -1 = too many to list)
+extern "C" int gac_chain_dp_ex(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq,
+                               const int32_t *q_seq, const uint8_t *q_strand,
+                               const int64_t *node_off, const int32_t *node_a,
+                               const int32_t *node_b, const int64_t *leaf_off,
+                               const int32_t *leaf, const int32_t *leaf_score,
+                               const int32_t *leaf_node, const int64_t *path_off,
+                               const int32_t *path, const int64_t *ov_off, const int32_t *ov,
+                               int64_t lin_k, int32_t min_entry, int64_t *total, int32_t *pred) {
     gac_clear_error();
     if (!c || n_pairs < 0 ||
         (n_pairs && (!t_seq || !q_seq || !q_strand || !node_off || !leaf_off || !path_off)))
@@ -1194,6 +1210,24 @@ extern "C" int gac_chain_dp(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq, c
             for (int64_t k = path_off[i]; k < path_off[i + 1]; ++k)
                 if (path[k] < 0 || path[k] >= pairs[p].n_nodes)
                     return gac_fail(GAC_E_ARG, "gac_chain_dp: leaf %lld: bad path node", (long long)i);
+    const bool fast = ov_off != nullptr;
+    const int64_t nov = fast ? ov_off[nl] : 0;
+    if (fast) {
+        if (ov_off[0] != 0 || (nov && !ov) || lin_k < 0)
+            return gac_fail(GAC_E_ARG, "gac_chain_dp: bad overlap lists");
+        for (int64_t p = 0; p < n_pairs; ++p)
+            for (int64_t i = leaf_off[p]; i < leaf_off[p + 1]; ++i) {
+                if (ov_off[i + 1] < ov_off[i])
+                    return gac_fail(GAC_E_ARG, "gac_chain_dp: leaf %lld: bad overlap offsets", (long long)i);
+                for (int64_t k = ov_off[i]; k < ov_off[i + 1]; ++k) {
+                    const int32_t v = ov[k];
+                    if (v != -1 && (v < 0 || v >= pairs[p].n_nodes ||
+                                    node_b[2 * (node_off[p] + v) + 1] >= 0))
+                        return gac_fail(GAC_E_ARG, "gac_chain_dp: leaf %lld: bad overlap node",
+                                        (long long)i);
+                }
+            }
+    }
     HIPCHK(hipSetDevice(c->device));
     DpArgs a;
     dp_base_args(c, a);
@@ -1204,7 +1238,23 @@ extern "C" int gac_chain_dp(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq, c
     long long *d_ms = nullptr, *d_tot = nullptr, *d_total = nullptr;
     int32_t *d_score = nullptr, *d_node = nullptr, *d_path = nullptr, *d_pred = nullptr;
     int64_t *d_poff = nullptr;
+    long long *d_nw = nullptr;
+    int64_t *d_ovoff = nullptr;
+    int32_t *d_ov = nullptr;
     int rc = GAC_OK;
+    if (fast) {
+        std::vector<long long> nw0(nn, INT64_MIN / 4);
+        if ((rc = dev_upload(c, &d_nw, nw0.data(), nn)) != GAC_OK ||
+            (rc = dev_upload(c, &d_ovoff, ov_off, nl + 1)) != GAC_OK ||
+            (rc = dev_upload(c, &d_ov, nov ? ov : nullptr, nov ? nov : 1)) != GAC_OK) {
+            hipStreamSynchronize(c->stream);
+            hipFree(d_nw);
+            hipFree(d_ovoff);
+            hipFree(d_ov);
+            return rc;
+        }
+        hipStreamSynchronize(c->stream);  // (nw0 leaves scope)
+    }
     if ((rc = dev_upload(c, &d_pairs, pairs.data(), n_pairs)) == GAC_OK &&
         (rc = dev_upload(c, &d_na, node_a, nn)) == GAC_OK &&
         (rc = dev_upload(c, &d_nb, node_b, nn)) == GAC_OK &&
@@ -1230,10 +1280,15 @@ extern "C" int gac_chain_dp(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq, c
         a.path = d_path;
         a.lf_total = d_total;
         a.lf_pred = d_pred;
+        a.nd_nw = d_nw;
+        a.ov_off = d_ovoff;
+        a.ov = d_ov;
+        a.lin_k = lin_k;
+        a.min_entry = min_entry;
         // one wave per pair, every pair resident at once (largest first is
         // the caller's order; the grid covers them all)
         const int grid = (int)std::min<int64_t>(n_pairs, 1 << 20);
-        if (e == hipSuccess) e = launch_dp(a, grid, c->stream);
+        if (e == hipSuccess) e = fast ? launch_dp_fast(a, grid, c->stream) : launch_dp(a, grid, c->stream);
         if (e == hipSuccess)
             e = hipMemcpyAsync(total, d_total, nl * sizeof(long long), hipMemcpyDeviceToHost, c->stream);
         if (e == hipSuccess)
@@ -1254,6 +1309,9 @@ extern "C" int gac_chain_dp(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq, c
     hipFree(d_path);
     hipFree(d_total);
     hipFree(d_pred);
+    hipFree(d_nw);
+    hipFree(d_ovoff);
+    hipFree(d_ov);
     return rc;
 }
 

@@ -51,6 +51,18 @@ struct DpArgs {
     const int32_t *gap_tab;
     int32_t gap_len;
     int32_t m16[16];  // score matrix by 2-bit code [q * 4 + t] (T C A G)
+    // the exact fast DP (k_dp_fast; see gac_dp.hip): the linear gap-cost
+    // minorant s (dq + dt), s = lin_k / 1024, its per-node bound
+    // nd_nw[v] = max over the subtree's scored leaves of 1024 total + lin_k
+    // (qEnd + tEnd) (mutable), the smallest matrix entry, and per leaf the
+    // leaf nodes of its overlapping candidates, ov[ov_off[i] .. ov_off[i+1])
+    // (a -1 entry: too many, the leaf takes the reference search)
+    long long *nd_nw;
+    const int64_t *ov_off;  // [leaves + 1] (global)
+    const int32_t *ov;
+    long long lin_k;
+    int32_t min_entry;
+    int32_t pad;
 };
 
 // One overlapping adjacent block pair: left block ends at (lqe, lte), right
@@ -62,6 +74,7 @@ struct XoverJob {
 };
 
 hipError_t launch_dp(const DpArgs &a, int grid, hipStream_t s);
+hipError_t launch_dp_fast(const DpArgs &a, int grid, hipStream_t s);
 hipError_t launch_xover(const DpArgs &a, const XoverJob *jobs, int64_t n, int32_t *pos,
                         int32_t *adj, hipStream_t s);
 

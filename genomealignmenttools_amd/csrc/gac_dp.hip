@@ -272,6 +272,278 @@ hipError_t launch_dp(const DpArgs &a, int grid, hipStream_t s) {
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------ k_dp_fast --
+// The exact fast DP (host: pair_dp_fast, gac_axtchain.c), one wave per pair.
+// bestPredecessor's pruned DFS returns the first leaf in DFS order (= node
+// order of the pre-order layout) of the best score among the candidates it
+// does not prune, and its bounds are true upper bounds for every candidate
+// that does not overlap the lonely leaf (gapCalcCost is monotone, checked on
+// the host).  So unless an overlapping candidate is anomalous (its score
+// exceeds a bound at its own leaf node, chainConnect.c:61-105's negative
+// crossover adjustment), the answer is the maximum over all candidates, ties
+// to the smallest node -- found here in any order:
+//   A. the 64 previous leaves in target order (an LDS ring) that do not
+//      overlap the lonely one, scored with the corner gap cost, give a first
+//      best (the usual predecessor is a few leaves back);
+//   B. the window walk of k_dp, pruning by max score, corner gap and the
+//      linear bound of each subtree (all strict, so a subtree that could
+//      hold a tie with a smaller node stays open), an improvement being a
+//      greater score or an equal one at a smaller node;
+//   C. every overlapping candidate of the leaf (listed by the host) that
+//      could score at least the best while violating a bound at its leaf
+//      sends the leaf to k_dp's reference walk (best from 0, max-score and
+//      corner bounds, first strict improvement in DFS order).
+// Mutable node state is read and written by this wave only: workgroup-scope
+// atomics and fences (no L2 write-back per leaf, as an agent fence costs).
+constexpr int kGapLds = 1024;  // gap costs by distance < kGapLds in LDS, per kind
+
+__device__ __forceinline__ long long ld_wg(const long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void st_wg(long long *p, long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// k_dp_fast's LDS: the gap costs of short distances and the long-position
+// tables of the interpolation, so a gap cost never waits on memory
+struct DpGapLds {
+    int gap[3 * kGapLds];
+};
+
+// dp_gap_cost with the short distances from LDS (computing the longer ones
+// -- the interpolation's division -- measured slower than the L2-resident
+// table: 5.2 vs 4.4 s on a 230 k-leaf pair, r05dp2)
+__device__ __forceinline__ int dp_gap_lds(const DpArgs &a, const DpGapLds &G, int dq, int dt) {
+    if (dt < 0) dt = 0;
+    if (dq < 0) dq = 0;
+    const int which = dt == 0 ? 0 : (dq == 0 ? 1 : 2);
+    const int d = which == 0 ? dq : (which == 1 ? dt : dq + dt);
+    if (d < kGapLds) return G.gap[which * kGapLds + d];
+    return dp_gap_cost(a, dq, dt);
+}
+
+struct DpLeafCtx {
+    int lq, lqe, lt, lte;
+    long long ls;
+};
+
+// One window walk over the pair's nodes for the lonely leaf X.  FAST: the
+// linear bound and tie-to-smaller-node improvements (best/best_node come in
+// seeded); else the reference: max-score and corner bounds only, strict
+// improvements, best from 0.
+template <bool FAST>
+__device__ void dp_walk(const DpArgs &a, const DpSeq &S, const int *m, const DpGapLds &sg,
+                        const DpPair &P, const DpLeafCtx &X, long long kl, long long &best,
+                        int &best_node) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const long long *ms = a.nd_ms + P.node_off;
+    const long long *nwp = a.nd_nw + P.node_off;
+    const long long *tot = a.nd_tot + P.node_off;
+    const int4 *na = a.nd_a + P.node_off;
+    const int2 *nb = a.nd_b + P.node_off;
+    const int nn = P.n_nodes;
+    int p0 = 0;
+    while (p0 < nn) {
+        const int v = p0 + lane;
+        const bool in = v < nn;
+        long long M = 0, T = 0, NW = 0;
+        int4 A = make_int4(0, 0, 0, 0);
+        int2 B = make_int2(v + 1, 0);
+        if (in) {
+            A = na[v];
+            B = nb[v];
+            M = ld_wg(ms + v);
+            if (FAST) NW = ld_wg(nwp + v);
+            if (B.y < 0) T = ld_wg(tot + v);
+        }
+        const bool leaf = B.y < 0;
+        const long long m1 = M + X.ls;
+        const int gc = dp_gap_lds(a, sg, X.lq - A.x, X.lt - A.y);
+        const long long m2 = m1 - gc;
+        const long long key = m1 < m2 ? m1 : m2;
+        bool cand = false;
+        long long sc = 0;
+        if (in && leaf && A.z < X.lq && A.w < X.lt) {
+            cand = true;
+            // a leaf node's corner is its block's end: a candidate that does
+            // not overlap costs the corner gap just computed
+            const int dq = X.lq - A.x, dt = X.lt - A.y;
+            const int cost = (FAST && dq >= 0 && dt >= 0)
+                                 ? gc
+                                 : dp_connect_cost(a, S, m, A.z, A.x, A.y, X.lq, X.lqe, X.lt);
+            sc = T + X.ls - cost;
+        }
+        int nxt = v + 1;
+        if (in && !leaf) {
+            const int coord = B.y == 0 ? X.lq : X.lt;
+            nxt = coord > A.z ? v + 1 : A.w;
+        }
+        int se = v + 1;
+        int cur = 0;
+        for (;;) {
+            const bool pruned = key < best || (FAST && NW - kl < 1024 * best);
+            if (lane >= cur && in) se = pruned ? B.x : (leaf ? v + 1 : nxt);
+            int incl = se;
+#pragma unroll
+            for (int d = 1; d < kWave; d <<= 1) {
+                const int o = __shfl_up(incl, d, kWave);
+                if (lane >= d) incl = max(incl, o);
+            }
+            int excl = __shfl_up(incl, 1, kWave);
+            if (lane == 0) excl = 0;
+            const bool visited = in && excl <= v;
+            const bool better = sc > best || (FAST && sc == best && v < best_node);
+            const bool imp = visited && lane >= cur && cand && !pruned && better;
+            const unsigned long long bal = __ballot(imp);
+            if (!bal) break;
+            const int u = __builtin_ctzll(bal);
+            best = __shfl(sc, u, kWave);
+            best_node = p0 + u;
+            cur = u + 1;
+        }
+        int mx = in ? se : 0;
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) mx = max(mx, __shfl_xor(mx, d, kWave));
+        p0 = max(p0 + kWave, mx);
+    }
+}
+
+__global__ void __launch_bounds__(kWave) k_dp_fast(DpArgs a) {
+    __shared__ int s_m[16];
+    __shared__ DpGapLds s_gap;
+    __shared__ int4 r_box[kWave];  // the previous 64 leaves: {qs, qe, ts, te}
+    __shared__ long long r_tot[kWave];
+    __shared__ int r_node[kWave];
+    const int lane = threadIdx.x;
+    if (lane < 16) s_m[lane] = a.m16[lane];
+    for (int k = lane; k < 3 * kGapLds; k += kWave) {
+        const int which = k / kGapLds, d = k % kGapLds;
+        s_gap.gap[k] = which == 0 ? dp_gap_cost(a, d, 0)
+                                  : (which == 1 ? dp_gap_cost(a, 0, d)
+                                                : (d >= 2 ? dp_gap_cost(a, 1, d - 1) : 0));
+    }
+    __syncthreads();
+    for (int64_t pi = blockIdx.x; pi < a.n_pairs; pi += gridDim.x) {
+        const DpPair P = a.pairs[pi];
+        const DpSeq S = {P.tbase, P.qbase};
+        long long *ms = a.nd_ms + P.node_off;
+        long long *nwp = a.nd_nw + P.node_off;
+        long long *tot = a.nd_tot + P.node_off;
+        const int2 *nb = a.nd_b + P.node_off;
+        r_node[lane] = -1;
+        __syncthreads();
+        for (int i = 0; i < P.n_leaves; ++i) {
+            const int64_t li = P.leaf_off + i;
+            // every per-leaf record at once (one round trip, not one per stage)
+            const int4 L = a.lf[li];  // {qs, qe, ts, te}
+            const int node = a.lf_node[li];
+            const int64_t q0 = a.path_off[li], q1 = a.path_off[li + 1];
+            const int64_t o0 = a.ov_off[li], o1 = a.ov_off[li + 1];
+            DpLeafCtx X;
+            X.lq = L.x;
+            X.lqe = L.y;
+            X.lt = L.z;
+            X.lte = L.w;
+            X.ls = a.lf_score[li];
+            const long long kl = a.lin_k * ((long long)X.lq + X.lt) - 1024 * X.ls;
+            // ---- A: the ring's non-overlapping candidates
+            long long best = 0;
+            int best_node = -1;
+            {
+                const int4 bx = r_box[lane];
+                const int nd = r_node[lane];
+                long long sc = -1;
+                if (nd >= 0 && bx.x < X.lq && bx.z < X.lt) {
+                    const int dq = X.lq - bx.y, dt = X.lt - bx.w;
+                    if (dq >= 0 && dt >= 0) sc = r_tot[lane] + X.ls - dp_gap_lds(a, s_gap, dq, dt);
+                }
+                // max score, ties to the smaller node; > 0 only
+                long long bs = sc > 0 ? sc : -1;
+                int bn = sc > 0 ? nd : 0x7fffffff;
+#pragma unroll
+                for (int d = 32; d > 0; d >>= 1) {
+                    const long long os = __shfl_xor(bs, d, kWave);
+                    const int on = __shfl_xor(bn, d, kWave);
+                    if (os > bs || (os == bs && on < bn)) {
+                        bs = os;
+                        bn = on;
+                    }
+                }
+                if (bs > 0) {
+                    best = bs;
+                    best_node = bn;
+                }
+            }
+            // ---- B: the fast walk
+            dp_walk<true>(a, S, s_m, s_gap, P, X, kl, best, best_node);
+            // ---- C: anomalies among the overlapping candidates
+            bool fb = false;
+            {
+                const long long need = best > 0 ? best : 1;
+                const int lsize = X.lqe - X.lq;
+                for (int64_t k = o0 + lane; k < o1; k += kWave) {
+                    const int c = a.ov[k];
+                    if (c < 0) {
+                        fb = true;
+                        continue;
+                    }
+                    const int cpos = ~nb[c].y;
+                    const int4 cb = a.lf[P.leaf_off + cpos];  // {qs, qe, ts, te}
+                    const int dq = X.lq - cb.y, dt = X.lt - cb.w;
+                    const int ov = -(dq < dt ? dq : dt);
+                    if (ov >= lsize || ov >= cb.y - cb.x) continue;  // connect cost 1e8
+                    const long long tc = ld_wg(tot + c);
+                    const long long ub = tc + X.ls - dp_gap_lds(a, s_gap, dq + ov, dt + ov) -
+                                         (long long)ov * a.min_entry;
+                    if (ub < need) continue;
+                    const long long sc =
+                        tc + X.ls - dp_connect_cost(a, S, s_m, cb.x, cb.y, cb.w, X.lq, X.lqe, X.lt);
+                    if (sc < need) continue;
+                    const long long bc = tc + X.ls - dp_gap_lds(a, s_gap, dq, dt);
+                    const long long bl = 1024 * tc - a.lin_k * ((long long)dq + dt) + 1024 * X.ls;
+                    if (sc > bc || 1024 * sc > bl) fb = true;
+                }
+            }
+            if (__ballot(fb)) {
+                best = 0;
+                best_node = -1;
+                dp_walk<false>(a, S, s_m, s_gap, P, X, 0, best, best_node);
+            }
+            // ---- D: findBestPredecessors (chainBlock.c:289-297) + updateScoresOnWay
+            long long total = X.ls;
+            int pred = -1;
+            if (best > X.ls) {
+                total = best;
+                pred = best_node;
+            }
+            if (lane == 0) {
+                a.lf_total[li] = total;
+                a.lf_pred[li] = pred;
+                st_wg(tot + node, total);
+                r_box[i & (kWave - 1)] = L;
+                r_tot[i & (kWave - 1)] = total;
+                r_node[i & (kWave - 1)] = node;
+            }
+            const long long nwv = 1024 * total + a.lin_k * ((long long)X.lqe + X.lte);
+            for (int64_t k = q0 + lane; k < q1; k += kWave) {
+                const int u = a.path[k];
+                if (ld_wg(ms + u) < total) st_wg(ms + u, total);
+                if (ld_wg(nwp + u) < nwv) st_wg(nwp + u, nwv);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            __syncthreads();
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_dp_fast(const DpArgs &a, int grid, hipStream_t s) {
+    if (a.n_pairs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_dp_fast, dim3((unsigned)grid), dim3(kWave), 0, s, a);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------ k_xover ----
 // One wave per overlap: lane i scores overlap base k = base + i on both
 // blocks, d_k = left - right; the crossover is the first k where the prefix

@@ -2452,6 +2452,8 @@ typedef struct ax_gpair {
     int32_t *lf, *lsc, *lnode; /* [nl][4], [nl], [nl] */
     int64_t *poff;      /* [nl + 1], local */
     int32_t *path;
+    int64_t *ooff;      /* [nl + 1], local: overlapping candidates (fast DP) */
+    int32_t *ovl;
     /* peel */
     ax_chains pc;
     int32_t *xjob;      /* [nbk] global crossover job or -1 */
@@ -2568,6 +2570,34 @@ static void gpair_export(ax_gpair *G) {
     }
     free(end);
     free(dim);
+    G->ooff = NULL;
+    G->ovl = NULL;
+    if (dp_fast_enabled(w)) {
+        /* each leaf's overlapping candidates (dp_overlaps: leaf nodes; a
+         * single -1 past kOvCap sends the leaf to the reference search) */
+        enum { kOvCap = 1024 };
+        int32_t maxsz, buf[kOvCap];
+        dp_leaf_positions(w, &maxsz);
+        int64_t on = 0, ocap = nl + 64;
+        G->ooff = malloc((size_t)(nl + 1) * sizeof(int64_t));
+        G->ovl = malloc((size_t)ocap * sizeof(int32_t));
+        G->ooff[0] = 0;
+        for (int32_t i = 0; i < nl; ++i) {
+            w->cut_t = i;
+            int k = dp_overlaps(w, w->tord[i], i, maxsz, buf, kOvCap);
+            if (k < 0) {
+                buf[0] = -1;
+                k = 1;
+            }
+            if (on + k > ocap) {
+                ocap = 2 * (on + k) + 64;
+                G->ovl = realloc(G->ovl, (size_t)ocap * sizeof(int32_t));
+            }
+            memcpy(G->ovl + on, buf, (size_t)k * sizeof(int32_t));
+            on += k;
+            G->ooff[i + 1] = on;
+        }
+    }
 }
 
 static void gpair_free_export(ax_gpair *G) {
@@ -2578,8 +2608,10 @@ static void gpair_free_export(ax_gpair *G) {
     free(G->lnode);
     free(G->poff);
     free(G->path);
-    G->na = G->nb = G->lf = G->lsc = G->lnode = G->path = NULL;
-    G->poff = NULL;
+    free(G->ooff);
+    free(G->ovl);
+    G->na = G->nb = G->lf = G->lsc = G->lnode = G->path = G->ovl = NULL;
+    G->poff = G->ooff = NULL;
 }
 
 static void *gdp_thread(void *arg) {
@@ -2590,7 +2622,7 @@ static void *gdp_thread(void *arg) {
         if (k >= J->n_pairs)
             break;
         const int32_t p = J->order[k];
-        ax_gpair *G = &X->G[p];
+        ax_gpair *G = &X->G[k]; /* (by place in J->order: the job may be a subset) */
         ax_work *w = &G->w;
         ax_out *o = &J->out[p];
         const double t0 = gnow();
@@ -2625,7 +2657,7 @@ static void *gdp_thread(void *arg) {
                 o->coff = calloc(1, sizeof(int32_t));
                 continue;
             }
-            const int64_t lo = X->leaf_off[p];
+            const int64_t lo = X->leaf_off[k];
             for (int32_t i = 0; i < w->nl; ++i) {
                 const int32_t l = w->tord[i];
                 w->total[l] = (double)X->total[lo + i];
@@ -2673,7 +2705,7 @@ static void *gdp_thread(void *arg) {
         } else {
             if (!G->ok || w->err || w->nl == 0)
                 continue;
-            const int64_t x0 = X->xoff[p];
+            const int64_t x0 = X->xoff[k];
             for (int32_t j = 0; j < G->pc.nbk; ++j)
                 if (G->xjob[j] >= 0)
                     G->xjob[j] += (int32_t)x0;
@@ -2699,9 +2731,19 @@ static void gdp_phase(ax_gjob *X, int phase, int nt) {
     gac_run_threads(nt, gdp_thread, X);
 }
 
+/* the pairs J->order[0 .. J->n_pairs) (all of them, or the device's share
+ * of a hybrid run); arrays below are by place k in that list */
 static int axt_dp_gpu(ax_job *J, int nt) {
     const int64_t np = J->n_pairs;
     ax_gpair *G = calloc((size_t)(np ? np : 1), sizeof(ax_gpair));
+    int32_t *kt = malloc((size_t)(np ? np : 1) * sizeof(int32_t));
+    int32_t *kq = malloc((size_t)(np ? np : 1) * sizeof(int32_t));
+    uint8_t *ks = malloc((size_t)(np ? np : 1));
+    for (int64_t k = 0; k < np; ++k) {
+        kt[k] = J->in->t_seq[J->order[k]];
+        kq[k] = J->in->q_seq[J->order[k]];
+        ks[k] = J->in->q_strand[J->order[k]];
+    }
     ax_gjob X;
     memset(&X, 0, sizeof(X));
     X.J = J;
@@ -2715,12 +2757,16 @@ static int axt_dp_gpu(ax_job *J, int nt) {
     int64_t *node_off = malloc((size_t)(np + 1) * sizeof(int64_t));
     int64_t *leaf_off = malloc((size_t)(np + 1) * sizeof(int64_t));
     node_off[0] = leaf_off[0] = 0;
-    int64_t npath = 0;
+    int64_t npath = 0, novl = 0;
+    int fast = 1; /* every live pair exported its overlap lists */
     for (int64_t p = 0; p < np; ++p) {
         const int live = G[p].ok && !G[p].w.err && G[p].w.nl > 0;
         node_off[p + 1] = node_off[p] + (live ? G[p].w.nn : 0);
         leaf_off[p + 1] = leaf_off[p] + (live ? G[p].w.nl : 0);
         npath += live ? G[p].poff[G[p].w.nl] : 0;
+        if (live && !G[p].ooff)
+            fast = 0;
+        novl += live && G[p].ooff ? G[p].ooff[G[p].w.nl] : 0;
     }
     const int64_t nn = node_off[np], nl = leaf_off[np];
     int32_t *na = malloc((size_t)(nn ? nn : 1) * 16), *nb = malloc((size_t)(nn ? nn : 1) * 8);
@@ -2730,6 +2776,10 @@ static int axt_dp_gpu(ax_job *J, int nt) {
     int32_t *path = malloc((size_t)(npath ? npath : 1) * 4);
     int64_t *total = malloc((size_t)(nl ? nl : 1) * 8);
     int32_t *pred = malloc((size_t)(nl ? nl : 1) * 4);
+    int64_t *ooff = fast ? malloc((size_t)(nl + 1) * 8) : NULL;
+    int32_t *ovl = fast ? malloc((size_t)(novl ? novl : 1) * 4) : NULL;
+    if (ooff)
+        ooff[0] = 0;
     poff[0] = 0;
     for (int64_t p = 0; p < np; ++p) {
         const int64_t n0 = node_off[p], l0 = leaf_off[p], cn = node_off[p + 1] - n0,
@@ -2745,14 +2795,21 @@ static int axt_dp_gpu(ax_job *J, int nt) {
         memcpy(path + pb, G[p].path, (size_t)G[p].poff[cl] * 4);
         for (int64_t i = 0; i < cl; ++i)
             poff[l0 + i + 1] = pb + G[p].poff[i + 1];
+        if (ooff) {
+            const int64_t ob = ooff[l0];
+            memcpy(ovl + ob, G[p].ovl, (size_t)G[p].ooff[cl] * 4);
+            for (int64_t i = 0; i < cl; ++i)
+                ooff[l0 + i + 1] = ob + G[p].ooff[i + 1];
+        }
     }
-    for (int64_t p = 0; p < np; ++p)
-        if (leaf_off[p + 1] == leaf_off[p])
-            for (int64_t i = leaf_off[p]; i < leaf_off[p + 1]; ++i)
-                poff[i + 1] = poff[i];
     double t2 = gnow();
-    rc = gac_chain_dp(J->ctx, np, J->in->t_seq, J->in->q_seq, J->in->q_strand, node_off, na, nb,
-                      leaf_off, lf, lsc, lnode, poff, path, total, pred);
+    /* the exact fast DP (k_dp_fast) when the gap costs allow it, else the
+     * reference search (k_dp) */
+    rc = gac_chain_dp_ex(J->ctx, np, kt, kq, ks, node_off, na, nb,
+                         leaf_off, lf, lsc, lnode, poff, path, ooff, ovl,
+                         ooff ? J->e->lin_k : 0, J->e->min_entry, total, pred);
+    free(ooff);
+    free(ovl);
     double t3 = gnow();
     free(na);
     free(nb);
@@ -2780,12 +2837,12 @@ static int axt_dp_gpu(ax_job *J, int nt) {
         int32_t *xv[5], *xpos = malloc((size_t)(nx ? nx : 1) * 4), *xadj = malloc((size_t)(nx ? nx : 1) * 4);
         for (int f = 0; f < 5; ++f)
             xv[f] = malloc((size_t)(nx ? nx : 1) * 4);
-        for (int64_t p = 0; p < np; ++p)
+        for (int64_t p = 0; p < np; ++p) /* (p: place in J->order) */
             for (int32_t k = 0; k < G[p].nx; ++k) {
                 const int64_t g = xoff[p] + k;
-                xt[g] = J->in->t_seq[p];
-                xq[g] = J->in->q_seq[p];
-                xs[g] = J->in->q_strand[p] ? 1 : 0;
+                xt[g] = kt[p];
+                xq[g] = kq[p];
+                xs[g] = ks[p] ? 1 : 0;
                 for (int f = 0; f < 5; ++f)
                     xv[f][g] = G[p].xl[5 * k + f];
             }
@@ -2843,7 +2900,59 @@ static int axt_dp_gpu(ax_job *J, int nt) {
         free(w->xs);
     }
     free(G);
+    free(kt);
+    free(kq);
+    free(ks);
     return rc;
+}
+
+/* ---- the hybrid DP (the default): the device takes the smallest pairs
+ * (k_dp_fast, one wave per pair, every device pair at once) while host
+ * threads take the others (teams on the largest).  A device pair must end
+ * within the host's critical path, estimated from the largest pair at the
+ * team's rate; pairs are given to the device from the smallest up while
+ * their device time (leaves x the device's per-leaf time) fits 0.7 of it.
+ * GAC_AXT_DP=host: no device pairs; GAC_DP_GPU_MAX=n: device pairs of at
+ * most n leaves (0: none); GAC_DP_DEV_US / GAC_DP_HOST_US: the per-leaf
+ * times of the model.  Returns the first device place in `order`. */
+static int64_t dp_device_split(const int64_t *psize, const int32_t *order, int64_t np,
+                               const ax_env *e) {
+    const char *dpm = getenv("GAC_AXT_DP");
+    if ((dpm && strcmp(dpm, "host") == 0) || !e->fast || np == 0)
+        return np;
+    int64_t lmax;
+    const char *mx = getenv("GAC_DP_GPU_MAX");
+    if (mx && *mx) {
+        lmax = atoll(mx);
+    } else {
+        const char *dv = getenv("GAC_DP_DEV_US"), *hv = getenv("GAC_DP_HOST_US");
+        const double dev_us = dv && atof(dv) > 0 ? atof(dv) : 20.0;  /* k_dp_fast, r05dp3 */
+        const double host_us = hv && atof(hv) > 0 ? atof(hv) : 0.47; /* team, C4 (r04i) */
+        const double crit = (double)psize[order[0]] * host_us * 1e-6;
+        if (crit < 0.25) /* (small runs: the device's start-up costs more) */
+            return np;
+        lmax = (int64_t)(0.7 * crit / (dev_us * 1e-6));
+    }
+    if (lmax < 1024)
+        return np;
+    int64_t kd = np;
+    while (kd > 1 && psize[order[kd - 1]] <= lmax)
+        --kd;
+    return kd;
+}
+
+typedef struct dev_run {
+    ax_job J; /* the device's pairs */
+    int nt, rc;
+    double secs;
+} dev_run;
+
+static void *dev_runner(void *arg) {
+    dev_run *D = arg;
+    const double t0 = gnow();
+    D->rc = axt_dp_gpu(&D->J, D->nt);
+    D->secs = gnow() - t0;
+    return NULL;
 }
 
 static int thread_count(int req) {
@@ -3408,6 +3517,41 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
         rc = axt_dp_gpu(&J, nt);
         stage("kd-tree DP (device)", &tclock);
     } else {
+        /* the smallest pairs to the device, on a thread of their own (its
+         * host phases -- trees, peel, finish -- on 2 threads taken from the
+         * pool) */
+        const int64_t kd = dp_device_split(psize, order, np, &env);
+        int64_t np_host = np, nb_host = nb; /* the host's pairs and blocks */
+        int dev_threads = 0; /* the device side's host threads (taken from the pool) */
+        dev_run *D = NULL;
+        pthread_t dth;
+        int dev_started = 0;
+        if (kd < np) {
+            D = calloc(1, sizeof(dev_run));
+            memcpy(&D->J, &J, sizeof(J));
+            D->J.order = order + kd;
+            D->J.n_pairs = np - kd;
+            atomic_init(&D->J.next, 0);
+            const char *dtv = getenv("GAC_DP_DEV_THREADS"); /* (its host phases' threads) */
+            D->nt = dtv && atoi(dtv) > 0 ? atoi(dtv) : 2;
+            dev_threads = D->nt;
+            if (pthread_create(&dth, NULL, dev_runner, D) == 0)
+                dev_started = 1;
+            else
+                dev_runner(D);
+            int64_t dl = 0;
+            for (int64_t k = kd; k < np; ++k)
+                dl += psize[order[k]];
+            if (getenv("GAC_TIMING"))
+                fprintf(stderr, "[gac_axt_chain] hybrid DP: %lld of %lld pairs (%lld of %lld blocks, "
+                        "largest %lld) on the device\n", (long long)(np - kd), (long long)np,
+                        (long long)dl, (long long)nb, (long long)psize[order[kd]]);
+            nb_host = nb - dl;
+            np_host = kd;
+        }
+        J.n_pairs = np_host;
+        if (nt > np_host)
+            nt = np_host > 0 ? (int)np_host : 1;
         /* the pairs that would be the critical path on one thread -- over
          * 2^20 blocks and over 1.5x an even share of all blocks (C4: the
          * 11.5 M and 5 M block pairs of 50 M) -- each run as a team
@@ -3421,9 +3565,9 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
         const int64_t floor_ = mv && atoll(mv) > 0 ? atoll(mv) : (1 << 20);
         const char *sv = getenv("GAC_DP_SHARE"); /* (a team pair: over this many even shares) */
         const double mult = sv && atof(sv) > 0 ? atof(sv) : 1.5;
-        const int64_t even = (int64_t)(mult * (double)(nb / nthreads));
+        const int64_t even = (int64_t)(mult * (double)(nb_host / nthreads));
         const int64_t share = mv ? floor_ : (even > floor_ ? even : floor_);
-        while (team_on && big < np && psize[order[big]] > share && big < nthreads / 2)
+        while (team_on && big < np_host && psize[order[big]] > share && big < nthreads / 2)
             ++big;
         team_run *tr = big ? calloc((size_t)big, sizeof(team_run)) : NULL;
         int pool = nt;
@@ -3432,10 +3576,11 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
             for (int64_t k = 0; k < big; ++k)
                 sum += psize[order[k]];
             const char *pl = getenv("GAC_DP_POOL"); /* (threads beside the teams) */
-            pool = pl && atoi(pl) > 0 && atoi(pl) < nthreads ? atoi(pl)
-                                                             : (nthreads / 3 > 1 ? nthreads / 3 : 1);
-            if (pool > np - big) /* (no pool pairs left, e.g. an -nranks rank holding one big pair) */
-                pool = (int)(np - big);
+            pool = pl && atoi(pl) > 0 && atoi(pl) < nthreads
+                       ? atoi(pl)
+                       : (nthreads / 3 - dev_threads > 1 ? nthreads / 3 - dev_threads : 1);
+            if (pool > np_host - big) /* (no pool pairs left, e.g. an -nranks rank holding one big pair) */
+                pool = (int)(np_host - big);
             const int tt = nthreads - pool;
             int used = 0;
             /* each team in an L3 domain of its own, from the one this
@@ -3483,7 +3628,7 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
             }
             atomic_store(&J.next, big);
         }
-        if (big == 0 || np > big)
+        if (big == 0 || np_host > big)
             run_threads(pool, ax_thread, &J);
         for (int64_t k = 0; k < big; ++k)
             if (tr[k].started)
@@ -3493,6 +3638,17 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
             stage("kd-tree DP (teams on the largest pairs, beside the pool)", &tclock);
         else
             stage("kd-tree DP (threads)", &tclock);
+        if (D) {
+            if (dev_started)
+                pthread_join(dth, NULL);
+            if (getenv("GAC_TIMING"))
+                fprintf(stderr, "[gac_axt_chain] hybrid DP: the device's %lld pairs took %.3f s\n",
+                        (long long)D->J.n_pairs, D->secs);
+            if (D->rc != GAC_OK && rc == GAC_OK)
+                rc = D->rc;
+            free(D);
+            stage("kd-tree DP (the device's pairs joined)", &tclock);
+        }
     }
     if (getenv("GAC_TIMING")) {
         double sum = 0, mx = 0;

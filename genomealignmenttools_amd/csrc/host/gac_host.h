@@ -78,6 +78,17 @@ uint32_t gac_twobit_u32(const gac_twobit *tb, const uint8_t *p);
 int gac_is_twobit_file(const char *path);
 
 /* ---- host threads: GAC_THREADS, else OMP_NUM_THREADS, else gac_host_cpus() (<= 64) */
+/* gac_chain_dp (include/gachain.h) with the exact fast DP when ov_off is
+ * given: lin_k / 1024 = the linear minorant of the gap cost (0 <= s), the
+ * smallest matrix entry, and per leaf (global index) the leaf nodes of its
+ * overlapping candidates ov[ov_off[i] .. ov_off[i+1]) (-1: too many, the
+ * reference search).  Internal to libgachain (gac_axt_chain). */
+int gac_chain_dp_ex(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq, const int32_t *q_seq,
+                    const uint8_t *q_strand, const int64_t *node_off, const int32_t *node_a,
+                    const int32_t *node_b, const int64_t *leaf_off, const int32_t *leaf,
+                    const int32_t *leaf_score, const int32_t *leaf_node, const int64_t *path_off,
+                    const int32_t *path, const int64_t *ov_off, const int32_t *ov, int64_t lin_k,
+                    int32_t min_entry, int64_t *total, int32_t *pred);
 /* CPUs usable by this process: online CPUs narrowed by the affinity mask and
  * the cgroup CPU quota (cpu.max) */
 int gac_host_cpus(void);

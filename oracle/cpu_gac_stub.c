@@ -410,79 +410,178 @@ static int emu_connect(gac_ctx *c, int32_t ts, int32_t qs, int minus, int aqs, i
     return adj + emu_gap(c, dq, dt);
 }
 
-int gac_chain_dp(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq, const int32_t *q_seq,
-                 const uint8_t *q_strand, const int64_t *node_off, const int32_t *node_a,
-                 const int32_t *node_b, const int64_t *leaf_off, const int32_t *leaf,
-                 const int32_t *leaf_score, const int32_t *leaf_node, const int64_t *path_off,
-                 const int32_t *path, int64_t *total, int32_t *pred) {
+/* one window walk of k_dp / k_dp_fast (csrc/gac_dp.hip dp_walk), lane by
+ * lane: fast = the linear bound and ties to the smaller node (best seeded) */
+typedef struct emu_pair {
+    gac_ctx *c;
+    int32_t ts, qs;
+    uint8_t minus;
+    const int32_t *na, *nb;
+    long long *ms, *nw, *tot;
+    int nn;
+} emu_pair;
+
+static long long g_emu_windows[2], g_emu_walks[2];
+static void emu_walk(const emu_pair *E, int fast, int lq, int lqe, int lt, long long ls,
+                     long long kl, long long *best_io, int *node_io) {
+    long long best = *best_io;
+    int best_node = *node_io, p0 = 0;
+    const int nn = E->nn;
+    ++g_emu_walks[fast];
+    while (p0 < nn) {
+        ++g_emu_windows[fast];
+        long long key[64], sc[64], NW[64];
+        int cand[64], se[64], nxt[64], in[64], lf[64], end[64];
+        for (int lane = 0; lane < 64; ++lane) {
+            const int v = p0 + lane;
+            in[lane] = v < nn;
+            se[lane] = v + 1;
+            cand[lane] = 0;
+            lf[lane] = 0;
+            key[lane] = 0;
+            sc[lane] = 0;
+            NW[lane] = 0;
+            nxt[lane] = v + 1;
+            end[lane] = v + 1;
+            if (!in[lane])
+                continue;
+            const int32_t *A = E->na + 4 * v, *B = E->nb + 2 * v;
+            const long long m1 = E->ms[v] + ls;
+            const int gc = emu_gap(E->c, lq - A[0], lt - A[1]);
+            const long long m2 = m1 - gc;
+            key[lane] = m1 < m2 ? m1 : m2;
+            NW[lane] = fast ? E->nw[v] : 0;
+            lf[lane] = B[1] < 0;
+            end[lane] = B[0];
+            if (lf[lane] && A[2] < lq && A[3] < lt) {
+                cand[lane] = 1;
+                const int dq = lq - A[0], dt = lt - A[1];
+                const int cost = (fast && dq >= 0 && dt >= 0)
+                                     ? gc
+                                     : emu_connect(E->c, E->ts, E->qs, E->minus, A[2], A[0], A[1],
+                                                   lq, lqe, lt);
+                sc[lane] = E->tot[v] + ls - cost;
+            }
+            if (!lf[lane])
+                nxt[lane] = (B[1] == 0 ? lq : lt) > A[2] ? v + 1 : A[3];
+        }
+        int cur = 0;
+        for (;;) {
+            int pr[64];
+            for (int lane = 0; lane < 64; ++lane) {
+                pr[lane] = key[lane] < best || (fast && NW[lane] - kl < 1024 * best);
+                if (lane >= cur && in[lane])
+                    se[lane] = pr[lane] ? end[lane] : (lf[lane] ? p0 + lane + 1 : nxt[lane]);
+            }
+            int u = -1, pm = 0;
+            for (int lane = 0; lane < 64; ++lane) {
+                const int visited = in[lane] && pm <= p0 + lane;
+                const int better = sc[lane] > best || (fast && sc[lane] == best && p0 + lane < best_node);
+                if (u < 0 && visited && lane >= cur && cand[lane] && !pr[lane] && better)
+                    u = lane;
+                if (se[lane] > pm)
+                    pm = se[lane];
+            }
+            if (u < 0)
+                break;
+            best = sc[u];
+            best_node = p0 + u;
+            cur = u + 1;
+        }
+        int mx = 0;
+        for (int lane = 0; lane < 64; ++lane)
+            if (in[lane] && se[lane] > mx)
+                mx = se[lane];
+        p0 = p0 + 64 > mx ? p0 + 64 : mx;
+    }
+    *best_io = best;
+    *node_io = best_node;
+}
+
+int gac_chain_dp_ex(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq, const int32_t *q_seq,
+                    const uint8_t *q_strand, const int64_t *node_off, const int32_t *node_a,
+                    const int32_t *node_b, const int64_t *leaf_off, const int32_t *leaf,
+                    const int32_t *leaf_score, const int32_t *leaf_node, const int64_t *path_off,
+                    const int32_t *path, const int64_t *ov_off, const int32_t *ov, int64_t lin_k,
+                    int32_t min_entry, int64_t *total, int32_t *pred) {
     const int64_t NN = node_off[n_pairs];
+    const int fast = ov_off != NULL;
     long long *ms = calloc((size_t)(NN ? NN : 1), 8), *tot = calloc((size_t)(NN ? NN : 1), 8);
+    long long *nw = malloc((size_t)(NN ? NN : 1) * 8);
+    for (int64_t v = 0; v < NN; ++v)
+        nw[v] = INT64_MIN / 4;
     for (int64_t p = 0; p < n_pairs; ++p)
         for (int64_t i = leaf_off[p]; i < leaf_off[p + 1]; ++i)
             tot[node_off[p] + leaf_node[i]] = leaf_score[i];
     for (int64_t p = 0; p < n_pairs; ++p) {
         const int64_t o = node_off[p];
-        const int nn = (int)(node_off[p + 1] - o);
-        const int32_t *na = node_a + 4 * o, *nb = node_b + 2 * o;
+        emu_pair E = {c, t_seq[p], q_seq[p], q_strand[p], node_a + 4 * o, node_b + 2 * o,
+                      ms + o, nw + o, tot + o, (int)(node_off[p + 1] - o)};
+        /* k_dp_fast's ring: the previous 64 leaves */
+        int rbox[64][4], rnode[64];
+        long long rtot[64];
+        for (int k = 0; k < 64; ++k)
+            rnode[k] = -1;
         for (int64_t li = leaf_off[p]; li < leaf_off[p + 1]; ++li) {
-            const int lq = leaf[4 * li], lqe = leaf[4 * li + 1], lt = leaf[4 * li + 2];
+            const int i = (int)(li - leaf_off[p]);
+            const int lq = leaf[4 * li], lqe = leaf[4 * li + 1], lt = leaf[4 * li + 2],
+                      lte = leaf[4 * li + 3];
             const long long ls = leaf_score[li];
+            const long long kl = fast ? lin_k * ((long long)lq + lt) - 1024 * ls : 0;
             long long best = 0;
-            int best_node = -1, p0 = 0;
-            while (p0 < nn) {
-                long long key[64], sc[64];
-                int cand[64], se[64], nxt[64], in[64], lf[64], end[64];
-                for (int lane = 0; lane < 64; ++lane) {
-                    const int v = p0 + lane;
-                    in[lane] = v < nn;
-                    se[lane] = v + 1;
-                    cand[lane] = 0;
-                    lf[lane] = 0;
-                    key[lane] = 0;
-                    nxt[lane] = v + 1;
-                    end[lane] = v + 1;
-                    if (!in[lane])
+            int best_node = -1;
+            if (fast) {
+                /* A: the ring's non-overlapping candidates, max score, ties
+                 * to the smaller node, > 0 only */
+                for (int k = 0; k < 64; ++k) {
+                    if (rnode[k] < 0 || !(rbox[k][0] < lq && rbox[k][2] < lt))
                         continue;
-                    const int32_t *A = na + 4 * v, *B = nb + 2 * v;
-                    const long long m1 = ms[o + v] + ls;
-                    const long long m2 = m1 - emu_gap(c, lq - A[0], lt - A[1]);
-                    key[lane] = m1 < m2 ? m1 : m2;
-                    lf[lane] = B[1] < 0;
-                    end[lane] = B[0];
-                    if (lf[lane] && A[2] < lq && A[3] < lt) {
-                        cand[lane] = 1;
-                        sc[lane] = tot[o + v] + ls -
-                                   emu_connect(c, t_seq[p], q_seq[p], q_strand[p], A[2], A[0], A[1],
-                                               lq, lqe, lt);
+                    const int dq = lq - rbox[k][1], dt = lt - rbox[k][3];
+                    if (dq < 0 || dt < 0)
+                        continue;
+                    const long long sc = rtot[k] + ls - emu_gap(c, dq, dt);
+                    if (sc > 0 && (sc > best || (sc == best && rnode[k] < best_node))) {
+                        best = sc;
+                        best_node = rnode[k];
                     }
-                    if (!lf[lane])
-                        nxt[lane] = (B[1] == 0 ? lq : lt) > A[2] ? v + 1 : A[3];
                 }
-                int cur = 0;
-                for (;;) {
-                    for (int lane = cur; lane < 64; ++lane)
-                        if (in[lane])
-                            se[lane] = key[lane] < best ? end[lane] : (lf[lane] ? p0 + lane + 1 : nxt[lane]);
-                    int u = -1, pm = 0;
-                    for (int lane = 0; lane < 64; ++lane) {
-                        const int visited = in[lane] && pm <= p0 + lane;
-                        if (u < 0 && visited && lane >= cur && cand[lane] && !(key[lane] < best) &&
-                            sc[lane] > best)
-                            u = lane;
-                        if (se[lane] > pm)
-                            pm = se[lane];
-                    }
-                    if (u < 0)
+                /* B */
+                emu_walk(&E, 1, lq, lqe, lt, ls, kl, &best, &best_node);
+                /* C */
+                int fb = 0;
+                const long long need = best > 0 ? best : 1;
+                for (int64_t k = ov_off[li]; k < ov_off[li + 1] && !fb; ++k) {
+                    const int cn = ov[k];
+                    if (cn < 0) {
+                        fb = 1;
                         break;
-                    best = sc[u];
-                    best_node = p0 + u;
-                    cur = u + 1;
+                    }
+                    const int cpos = ~E.nb[2 * cn + 1];
+                    const int32_t *cb = leaf + 4 * (leaf_off[p] + cpos);
+                    const int dq = lq - cb[1], dt = lt - cb[3];
+                    const int ovl = -(dq < dt ? dq : dt);
+                    if (ovl >= lqe - lq || ovl >= cb[1] - cb[0])
+                        continue;
+                    const long long tc = tot[o + cn];
+                    const long long ub = tc + ls - emu_gap(c, dq + ovl, dt + ovl) - (long long)ovl * min_entry;
+                    if (ub < need)
+                        continue;
+                    const long long sc = tc + ls - emu_connect(c, t_seq[p], q_seq[p], q_strand[p], cb[0],
+                                                                cb[1], cb[3], lq, lqe, lt);
+                    if (sc < need)
+                        continue;
+                    const long long bc = tc + ls - emu_gap(c, dq, dt);
+                    const long long bl = 1024 * tc - lin_k * ((long long)dq + dt) + 1024 * ls;
+                    if (sc > bc || 1024 * sc > bl)
+                        fb = 1;
                 }
-                int mx = 0;
-                for (int lane = 0; lane < 64; ++lane)
-                    if (in[lane] && se[lane] > mx)
-                        mx = se[lane];
-                p0 = p0 + 64 > mx ? p0 + 64 : mx;
+                if (fb) {
+                    best = 0;
+                    best_node = -1;
+                    emu_walk(&E, 0, lq, lqe, lt, ls, 0, &best, &best_node);
+                }
+            } else {
+                emu_walk(&E, 0, lq, lqe, lt, ls, 0, &best, &best_node);
             }
             long long t = ls;
             int pr = -1;
@@ -493,12 +592,37 @@ int gac_chain_dp(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq, const int32_
             total[li] = t;
             pred[li] = pr;
             tot[o + leaf_node[li]] = t;
-            for (int64_t k = path_off[li]; k < path_off[li + 1]; ++k)
+            const long long nwv = 1024 * t + lin_k * ((long long)lqe + lte);
+            for (int64_t k = path_off[li]; k < path_off[li + 1]; ++k) {
                 if (ms[o + path[k]] < t)
                     ms[o + path[k]] = t;
+                if (nw[o + path[k]] < nwv)
+                    nw[o + path[k]] = nwv;
+            }
+            rbox[i & 63][0] = lq;
+            rbox[i & 63][1] = lqe;
+            rbox[i & 63][2] = lt;
+            rbox[i & 63][3] = lte;
+            rtot[i & 63] = t;
+            rnode[i & 63] = leaf_node[li];
         }
     }
     free(ms);
     free(tot);
+    free(nw);
+    if (getenv("GAC_EMU_STATS"))
+        fprintf(stderr, "[emu dp] fast walks %lld, %.2f windows each; reference walks %lld, %.2f windows each\n",
+                g_emu_walks[1], (double)g_emu_windows[1] / (g_emu_walks[1] ? g_emu_walks[1] : 1),
+                g_emu_walks[0], (double)g_emu_windows[0] / (g_emu_walks[0] ? g_emu_walks[0] : 1));
     return GAC_OK;
+}
+
+int gac_chain_dp(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq, const int32_t *q_seq,
+                 const uint8_t *q_strand, const int64_t *node_off, const int32_t *node_a,
+                 const int32_t *node_b, const int64_t *leaf_off, const int32_t *leaf,
+                 const int32_t *leaf_score, const int32_t *leaf_node, const int64_t *path_off,
+                 const int32_t *path, int64_t *total, int32_t *pred) {
+    return gac_chain_dp_ex(c, n_pairs, t_seq, q_seq, q_strand, node_off, node_a, node_b, leaf_off,
+                           leaf, leaf_score, leaf_node, path_off, path, NULL, NULL, 0, 0, total,
+                           pred);
 }

@@ -25,6 +25,10 @@ def line(path):
     e2e = d.get("scorechain_e2e", {})
     if e2e:
         out.append(f"sc_e2e {e2e.get('ms_per_step', 0):.0f}ms id={(e2e.get('parity_full') or {}).get('identical')}")
+    c3 = d.get("c3", {})
+    if c3:
+        out.append(f"c3 {c3.get('ms_per_step', 0):.0f}ms x{c3.get('speedup_vs_reference') or 0:.1f} "
+                   f"id={c3.get('identical')}" + (f" err={c3['error'][:80]}" if "error" in c3 else ""))
     c4 = d.get("c4", {})
     if c4:
         out.append(f"c4 {c4.get('ms_per_step', 0) / 1e3:.2f}s id={(c4.get('parity_full') or {}).get('identical')}")

@@ -18,7 +18,7 @@ in about a minute on the GPU box's host.
              chainCleaner -net= (about 12.5k suspects removed)
   C4-shaped: 24 x 21 chromosome pairs x 2 strands, power-law blocks per
              pair, 1.2 M PSL blocks (host and device DP) and 5 M PSL blocks
-             (host DP): axtChain -psl
+             (the default hybrid DP, and the device DP alone): axtChain -psl
 plus the edge cases the round-1 review listed: a custom -linearGap file on
 the device, zero-size terminal blocks, chainNet -rescore's subset-upload
 branch (a sequence missing from the 2bit), no partial fills at all, and a
@@ -27,6 +27,7 @@ clean exit status on failures while helper threads are live.
 import filecmp
 import json
 import os
+import re
 import subprocess
 
 import numpy as np
@@ -278,8 +279,10 @@ def test_c4_shaped_axtchain(tmp_path):
 @pytest.mark.timeout(1200)
 def test_c4_shaped_axtchain_5m_blocks(tmp_path):
     """The C4 shape at 5 M PSL blocks (a tenth of SURVEY §8(d)'s 50 M; the
-    reference takes about a minute here), the product's host DP, byte for
-    byte against the reference run in the same test."""
+    reference takes about a minute here), the product's default -- the
+    hybrid DP: the smaller pairs' kd-tree DP on the device (k_dp_fast), the
+    others on host threads -- and the device DP alone (GAC_AXT_DP=gpu), byte
+    for byte against the reference run in the same test."""
     from genomealignmenttools_amd import synth
     tg, qg, pairs, b = synth.psl_c4(7, 5_000_000, n_t=24, n_q=21, tsize=12_000_000,
                                     qsize=10_000_000)
@@ -290,9 +293,13 @@ def test_c4_shaped_axtchain_5m_blocks(tmp_path):
     synth.write_psl_c4(tg, qg, pairs, b, os.path.join(d, "in.psl"), 7)
     del tg, qg, b
     args = ["-linearGap=loose", "-psl", "in.psl", "t.2bit", "q.2bit"]
-    _run([_bin("axtChain")] + args + ["ours.chain"], cwd=d)
+    r = _run([_bin("axtChain")] + args + ["ours.chain"], cwd=d, env={"GAC_TIMING": "1"})
+    m = re.search(r"hybrid DP: (\d+) of (\d+) pairs \((\d+) of (\d+) blocks", r.stderr)
+    assert m and int(m.group(1)) > 0 and int(m.group(3)) > 100_000, r.stderr[-3000:]
+    _run([_bin("axtChain")] + args + ["dev.chain"], cwd=d, env={"GAC_AXT_DP": "gpu"})
     _run([_ref("axtChain")] + args + ["ref.chain"], cwd=d, timeout=900)
     _same(os.path.join(d, "ours.chain"), os.path.join(d, "ref.chain"))
+    _same(os.path.join(d, "dev.chain"), os.path.join(d, "ref.chain"))
 
 
 # ---------------------------------------------------------------- edge cases
@@ -455,7 +462,10 @@ def test_c4_fullscale_axtchain_vs_reference_sha(tmp_path):
     _run([os.path.join(PKG_DIR, "libexec", "gac_synth"), "c4", d, "-seed=7", "-blocks=50000000",
           "-threads=16"])
     args = ["-linearGap=loose", "-verbose=0", "-psl", "in.psl", "t.2bit", "q.2bit"]
-    _run([_bin("axtChain")] + args + ["one.chain"], cwd=d)
+    r = _run([_bin("axtChain")] + args + ["one.chain"], cwd=d, env={"GAC_TIMING": "1"})
+    # the default hybrid DP put a share of the pairs' leaves on the device
+    m = re.search(r"hybrid DP: (\d+) of (\d+) pairs \((\d+) of (\d+) blocks", r.stderr)
+    assert m and int(m.group(3)) > 1_000_000, r.stderr[-3000:]
     procs = [subprocess.Popen([_bin("axtChain")] + args + ["r3.chain", "-nranks=3", f"-rank={r}",
                                                            "-gpu=0"], cwd=d,
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
