@@ -49,12 +49,16 @@ hipError_t launch_relayout(const uint8_t *raw, const SeqDev *seqs, int nseq, int
 hipError_t launch_gap_table(const GapDev &g, const int32_t *small, int len, int32_t *tab,
                             hipStream_t s);
 hipError_t launch_nruns(const NPiece *p, int64_t n, uint32_t *nmask, hipStream_t s);
+hipError_t launch_build_index(const int32_t *bt, const int32_t *bq, const int32_t *bs, int64_t nb,
+                              const DChain *chains, int64_t n_chains, const int32_t *coff,
+                              const int32_t *tile_c0, int2 *tspan, uint32_t *bucket,
+                              hipStream_t s);
 hipError_t launch_build_flat(const int32_t *bt, const int32_t *bq, const int32_t *bs, int64_t nb,
                              const DChain *chains, int64_t n_chains, int32_t *coff,
                              int32_t *tile_c0, int4 *crun, const longlong2 *t_runs,
                              int64_t n_trun, const longlong2 *q_runs, int64_t n_qrun,
                              const int64_t *q_woff, int4 *blk, int2 *tspan, uint32_t *bucket,
-                             const UploadGaps &G, hipStream_t s);
+                             const UploadGaps &G, bool index, hipStream_t s);
 hipError_t launch_block_gaps_flat(const int32_t *coff, const int32_t *tile_c0, int64_t nb,
                                   int4 *blk, Blk12 *blk12, const UploadGaps &G, hipStream_t s);
 hipError_t launch_scatter(const SparseRun *runs, int64_t n, const uint64_t *compact,
@@ -247,6 +251,9 @@ struct gac_chainset {
     int32_t *d_coff = nullptr, *d_tile_c0 = nullptr;
     int4 *d_crun = nullptr;
     size_t cap_coff = 0, cap_tile_c0 = 0, cap_crun = 0;
+    // the window-search index (tspan, bucket) is built: at upload
+    // (GAC_UP_INDEX=eager) or at the first call that searches windows
+    bool idx_ready = false;
 };
 
 static void free_whole_plan(gac_chainset *cs) {
@@ -1643,11 +1650,18 @@ static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs)
     }();
     const bool gaps = fuse && c->scoring;
     const UploadGaps G = gaps ? upload_gaps(c, cs->blk12) : UploadGaps{};
+    // the window-search index only on demand: chainNet -rescore hands its
+    // windows over and whole chains need none (GAC_UP_INDEX=eager: now)
+    static const bool eager = [] {
+        const char *v = getenv("GAC_UP_INDEX");
+        return v && !strcmp(v, "eager");
+    }();
     if (e == hipSuccess && rc == GAC_OK)
         e = launch_build_flat(d_bt, d_bt + nb, d_bt + 2 * nb, (int64_t)nb, cs->chains, n, cs->d_coff,
                               cs->d_tile_c0, cs->d_crun, c->g[0].d_nrun, c->g[0].n_nrun,
                               c->g[1].d_nrun, c->g[1].n_nrun, c->g[1].d_woff, cs->blk, cs->tspan,
-                              cs->bucket, G, c->stream);
+                              cs->bucket, G, eager, c->stream);
+    cs->idx_ready = eager;
     if (e == hipSuccess && rc == GAC_OK && gaps) cs->gap_version = c->gap_version;
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     lap("device build + sync");
@@ -1809,6 +1823,19 @@ static int wait_status(gac_ctx *c, hipStream_t s, int32_t tag, int32_t st[4]) {
     }
 }
 
+// the set's window-search index (spans + bucket entries), built at the first
+// call that searches windows (stream-ordered before it)
+static int ensure_index(gac_ctx *c, const gac_chainset *cs_in, hipStream_t s) {
+    gac_chainset *cs = const_cast<gac_chainset *>(cs_in);
+    if (cs->idx_ready || (cs->n_blocks == 0 && cs->n_chains == 0)) return GAC_OK;
+    const int64_t nb = cs->n_blocks;
+    const int32_t *d_bt = cs->d_stage;
+    HIPCHK(launch_build_index(d_bt, d_bt + nb, d_bt + 2 * nb, nb, cs->chains, cs->n_chains,
+                              cs->d_coff, cs->d_tile_c0, cs->tspan, cs->bucket, s));
+    cs->idx_ready = true;
+    return GAC_OK;
+}
+
 // One call = k_plan, the tile map (k_tilemap_fused, or k_scan_agg + k_tilemap
 // above 1 M ranges), k_tile and the cross-tile fold (k_fold_tiles +
 // k_fold_super); the host waits only for the status words (pinned memory),
@@ -1883,6 +1910,7 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
     if (c->ws_last && c->ws_last != s) HIPCHK(hipStreamWaitEvent(s, c->ws_ev, 0));
     int rc = prepare_args(c, cs, n, flags, d_l, s, a_base);
     if (rc != GAC_OK || n == 0) return rc;
+    if (!d_wins && (rc = ensure_index(c, cs, s)) != GAC_OK) return rc;
     rc = score_device_split(c, a_base, d_ranges, d_wins, n, d_g, d_l, d_ali, s);
     if (hipEventRecord(c->ws_ev, s) == hipSuccess) c->ws_last = s;
     return rc;
@@ -2340,6 +2368,7 @@ extern "C" int gac_score_ranges(gac_ctx *c, const gac_chainset *cs, const gac_ra
         ScoreArgs a;
         int rc = prepare_args(c, cs, n, flags, local, s, a);
         if (rc != GAC_OK) return rc;
+        if ((rc = ensure_index(c, cs, s)) != GAC_OK) return rc;
         memcpy(c->h_small_in, ranges, (size_t)n * sizeof(Range));
         HIPCHK(launch_small(a, c->d_small_in, c->d_small_out, s));
         HIPCHK(hipStreamSynchronize(s));

@@ -357,7 +357,7 @@ __global__ void __launch_bounds__(256) k_chain_prep(const DChain *chains, int64_
     if (c == n_chains - 1) coff[n_chains] = (int32_t)nb;
     const int64_t span = (int64_t)ch.tend - ch.tstart;
     const int64_t nbk = span > 0 ? ((span - 1) >> ch.shift) + 1 : 0;
-    bucket[ch.idx_off + nbk] = (uint32_t)ch.nblk;
+    if (bucket) bucket[ch.idx_off + nbk] = (uint32_t)ch.nblk;  // (null: the index is built later)
     int4 r = make_int4(0, 0, 0, 0);
     if (ch.nblk > 0) {
         if (n_trun) runs_in(t_runs, n_trun, ch.tbase + ch.tstart, ch.tbase + ch.tend, &r.x, &r.y);
@@ -370,6 +370,17 @@ __global__ void __launch_bounds__(256) k_chain_prep(const DChain *chains, int64_
         }
     }
     crun[c] = r;
+}
+
+// one lane per chain: its bucket index's terminator (the lazy index build)
+__global__ void __launch_bounds__(256) k_bucket_term(const DChain *chains, int64_t n_chains,
+                                                     uint32_t *bucket) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_chains) return;
+    const DChain ch = chains[c];
+    const int64_t span = (int64_t)ch.tend - ch.tstart;
+    const int64_t nbk = span > 0 ? ((span - 1) >> ch.shift) + 1 : 0;
+    bucket[ch.idx_off + nbk] = (uint32_t)ch.nblk;
 }
 
 // one lane per 64-block tile: the chain holding its first block
@@ -418,7 +429,10 @@ __device__ __forceinline__ int block_gap(const UploadGaps &G, int t, int q, int 
 // for the buckets starting in [tEnd(k-1), tEnd(k))).  GAPS (the scoring is
 // set when the chains arrive): the gap costs and the 12-byte records too,
 // k_block_gaps_flat's pass folded in; otherwise gap 0 until it runs.
-template <bool GAPS>
+// MODE: 0 everything; 1 the records only (the window-search index -- spans
+// and buckets -- is built at the first call that searches windows: chainNet's
+// windows and whole chains never do); 2 the index only.
+template <bool GAPS, int MODE>
 __global__ void __launch_bounds__(256) k_build_flat(const int32_t *bt, const int32_t *bq,
                                                     const int32_t *bs, int64_t nb,
                                                     const DChain *chains, const int32_t *coff,
@@ -466,8 +480,8 @@ __global__ void __launch_bounds__(256) k_build_flat(const int32_t *bt, const int
         uint32_t val = 0;
         if (b >= nb) {
             if (b < nb + 8) {  // padding: a window search may read 8 past a chain
-                tspan[b] = make_int2(0x7fffffff, 0x7fffffff);
-                blk[b] = make_int4(0x7fffffff, 0, 0, 0);
+                if (MODE != 1) tspan[b] = make_int2(0x7fffffff, 0x7fffffff);
+                if (MODE != 2) blk[b] = make_int4(0x7fffffff, 0, 0, 0);
             }
         } else {
             int64_t tbase, idx_off, coff_c, coff_n;
@@ -486,7 +500,7 @@ __global__ void __launch_bounds__(256) k_build_flat(const int32_t *bt, const int
                 rr = crun ? crun[c] : make_int4(0, 0, 0, 0);
             }
             int flags = 0;  // (a block searches only the runs its chain's span meets)
-            if (!(GAC_UP_PROBE & 2) && z[i] > 0) {
+            if (MODE != 2 && !(GAC_UP_PROBE & 2) && z[i] > 0) {
                 if (rr.y > rr.x && span_meets(t_runs, rr.x, rr.y, tbase + t[i], tbase + t[i] + z[i]))
                     flags |= kTHasN;
                 if (rr.w > rr.z) {
@@ -496,12 +510,12 @@ __global__ void __launch_bounds__(256) k_build_flat(const int32_t *bt, const int
                 }
             }
             int cost = 0;
-            if (GAPS) {
+            if (GAPS && MODE != 2) {
                 if (b + 1 < coff_n) cost = block_gap(G, t[i], q[i], z[i], bt[b + 1], bq[b + 1]);
                 if (!(GAC_UP_PROBE & 4)) G.blk12[b] = blk12_of(t[i], q[i], z[i] | flags, cost);
             }
-            blk[b] = make_int4(t[i], q[i], z[i] | flags, cost);
-            if (!(GAC_UP_PROBE & 4)) tspan[b] = make_int2(t[i], t[i] + z[i]);
+            if (MODE != 2) blk[b] = make_int4(t[i], q[i], z[i] | flags, cost);
+            if (MODE != 1 && !(GAC_UP_PROBE & 4)) tspan[b] = make_int2(t[i], t[i] + z[i]);
             const int64_t k = b - coff_c;
             const int64_t span = (int64_t)tend - tstart;
             const int64_t nbk = span > 0 ? ((span - 1) >> shift) + 1 : 0;
@@ -509,8 +523,10 @@ __global__ void __launch_bounds__(256) k_build_flat(const int32_t *bt, const int
             const int64_t k0 = k ? ((int64_t)bt[b - 1] + bs[b - 1] - tstart + round) >> shift : 0;
             int64_t k1 = ((int64_t)t[i] + z[i] - tstart + round) >> shift;
             if (k1 > nbk) k1 = nbk;
-            if (!(GAC_UP_PROBE & 1) && k1 > k0) cnt = k1 - k0, dst = idx_off + k0, val = (uint32_t)k;
+            if (MODE != 1 && !(GAC_UP_PROBE & 1) && k1 > k0)
+                cnt = k1 - k0, dst = idx_off + k0, val = (uint32_t)k;
         }
+        if (MODE == 1) continue;  // (no bucket entries: uniform over the workgroup)
         // the wave's bucket entries, lane-strided: a block after a wide gap
         // owns many, and a loop per block left the other lanes idle.  Entry e
         // of the wave belongs to the last lane whose exclusive count is <= e.
@@ -2210,29 +2226,53 @@ hipError_t launch_gap_table(const GapDev &g, const int32_t *small, int len, int3
     return hipGetLastError();
 }
 
+// index: also the window-search index (spans, bucket entries and
+// terminators); without it launch_build_index builds them later
 hipError_t launch_build_flat(const int32_t *bt, const int32_t *bq, const int32_t *bs, int64_t nb,
                              const DChain *chains, int64_t n_chains, int32_t *coff,
                              int32_t *tile_c0, int4 *crun, const longlong2 *t_runs,
                              int64_t n_trun, const longlong2 *q_runs, int64_t n_qrun,
                              const int64_t *q_woff, int4 *blk, int2 *tspan, uint32_t *bucket,
-                             const UploadGaps &G, hipStream_t s) {
+                             const UploadGaps &G, bool index, hipStream_t s) {
     const int64_t ntiles = (nb + 63) >> 6;
     if (n_chains > 0) {
         hipLaunchKernelGGL(k_chain_prep, dim3((unsigned)((n_chains + 255) / 256)), dim3(256), 0, s,
                            chains, n_chains, nb, bq, bs, t_runs, n_trun, q_runs, n_qrun, q_woff,
-                           coff, crun, bucket);
+                           coff, crun, index ? bucket : nullptr);
         hipLaunchKernelGGL(k_tile_chain, dim3((unsigned)((ntiles + 1 + 255) / 256)), dim3(256), 0,
                            s, coff, n_chains, ntiles, tile_c0);
     }
     const int64_t g = (nb + 8 + 256 * kUpPer - 1) / (256 * kUpPer);
-    if (G.blk12)
-        hipLaunchKernelGGL(k_build_flat<true>, dim3((unsigned)g), dim3(256), 0, s, bt, bq, bs, nb,
-                           chains, coff, tile_c0, ntiles, (n_trun || n_qrun) ? crun : nullptr,
-                           t_runs, n_trun, q_runs, n_qrun, q_woff, blk, tspan, bucket, G);
-    else
-        hipLaunchKernelGGL(k_build_flat<false>, dim3((unsigned)g), dim3(256), 0, s, bt, bq, bs, nb,
-                           chains, coff, tile_c0, ntiles, (n_trun || n_qrun) ? crun : nullptr,
-                           t_runs, n_trun, q_runs, n_qrun, q_woff, blk, tspan, bucket, G);
+    int4 *cr = (n_trun || n_qrun) ? crun : nullptr;
+#define GAC_BUILD(GP, MD)                                                                         \
+    hipLaunchKernelGGL((k_build_flat<GP, MD>), dim3((unsigned)g), dim3(256), 0, s, bt, bq, bs, nb, \
+                       chains, coff, tile_c0, ntiles, cr, t_runs, n_trun, q_runs, n_qrun, q_woff,  \
+                       blk, tspan, bucket, G)
+    if (G.blk12) {
+        if (index) GAC_BUILD(true, 0);
+        else GAC_BUILD(true, 1);
+    } else {
+        if (index) GAC_BUILD(false, 0);
+        else GAC_BUILD(false, 1);
+    }
+#undef GAC_BUILD
+    return hipGetLastError();
+}
+
+// the window-search index of an uploaded set (coff / tile_c0 / chains as the
+// upload left them; bt/bq/bs the staged block arrays)
+hipError_t launch_build_index(const int32_t *bt, const int32_t *bq, const int32_t *bs, int64_t nb,
+                              const DChain *chains, int64_t n_chains, const int32_t *coff,
+                              const int32_t *tile_c0, int2 *tspan, uint32_t *bucket,
+                              hipStream_t s) {
+    const int64_t ntiles = (nb + 63) >> 6;
+    if (n_chains > 0)
+        hipLaunchKernelGGL(k_bucket_term, dim3((unsigned)((n_chains + 255) / 256)), dim3(256), 0, s,
+                           chains, n_chains, bucket);
+    const int64_t g = (nb + 8 + 256 * kUpPer - 1) / (256 * kUpPer);
+    hipLaunchKernelGGL((k_build_flat<false, 2>), dim3((unsigned)g), dim3(256), 0, s, bt, bq, bs, nb,
+                       chains, coff, tile_c0, ntiles, nullptr, nullptr, 0, nullptr, 0, nullptr,
+                       nullptr, tspan, bucket, UploadGaps{});
     return hipGetLastError();
 }
 
