@@ -1013,6 +1013,9 @@ static void run_job(int argc, char *argv[], ax_batch *B) {
     gac_axt_input ai = {nm, mt, mq, ms, moff, bt, bq, bs};
     gac_axt_chains *ch = NULL;
     gt_check(gac_axt_chain(ctx, mat, gap, &ai, (double)min_score, 0, details, &ch));
+    if (multi && getenv("GAC_TIMING")) /* (DESIGN §6's per-rank table) */
+        fprintf(stderr, "[rank %d/%d] %lld pairs, %lld blocks, %lld chains: chained in %.3f s\n",
+                rk.me, rk.n, (long long)nm, (long long)nb, (long long)ch->n_chains, wall() - t0);
     if (multi && rk.me > 0) { /* this rank's chains, sorted, to rank 0 */
         char part[4096], tmp[4096];
         gt_part_name(part, sizeof(part), out_path, rk.me, "");
@@ -1042,7 +1045,7 @@ static void run_job(int argc, char *argv[], ax_batch *B) {
         P0->off = ch->blk_off;
         P0->bt = ch->blk_t, P0->bq = ch->blk_q, P0->bs = ch->blk_size;
     }
-    if (multi) {
+    if (multi && !gt_ranks_solo()) {
         gt_ranks_wait(&rk, out_path);
         for (int r = 1; r < rk.n; ++r) {
             char part[4096];

@@ -130,8 +130,12 @@ static void *write_net(void *arg) {
                        : GAC_E_IO;
         if (mf && fclose(mf) != 0 && w->rc == GAC_OK)
             w->rc = GAC_E_IO;
-        if (w->rc == GAC_OK)
+        if (w->rc == GAC_OK) {
+            if (getenv("GAC_TIMING")) /* (the per-rank table of DESIGN §6) */
+                fprintf(stderr, "[rank %d/%d] %s part: %zu bytes\n", g_rk.me, g_rk.n,
+                        w->side == GAC_T ? "target net" : "query net", len);
             gt_ranks_place(&g_rk, w->path, buf, len);
+        }
         else
             snprintf(w->err, sizeof(w->err), "write error on %s", w->path);
         free(buf);
@@ -568,6 +572,18 @@ int main(int argc, char *argv[]) {
     else
         gt_check(gac_net_build(&in, &opt, &net));
     gt_stage("netting");
+    if (multi && getenv("GAC_TIMING")) { /* this rank's work (DESIGN §6's per-rank table) */
+        int64_t tb = 0, qb = 0;
+        for (int32_t k = 0; k < ts.names.n; ++k)
+            tb += tkeep[k] ? ts.size[k] : 0;
+        for (int32_t k = 0; k < qs.names.n; ++k)
+            qb += qkeep[k] ? qs.size[k] : 0;
+        fprintf(stderr, "[rank %d/%d] sides: %d target seqs (%lld bases), %d query seqs (%lld "
+                        "bases); %lld chain headers, %lld blocks parsed; fills: %lld target, %lld query\n",
+                g_rk.me, g_rk.n, tkept.n, (long long)tb, qkept.n, (long long)qb, (long long)c.n,
+                (long long)c.blk_off[c.n], (long long)gac_net_fill_count(net, GAC_T),
+                (long long)gac_net_fill_count(net, GAC_Q));
+    }
     gt_verbose(1, "Finishing nets\n");
 
     /* the two nets are independent files, written concurrently; the query

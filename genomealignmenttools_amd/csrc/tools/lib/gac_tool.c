@@ -864,12 +864,31 @@ void gt_ranks_clear_markers(const gt_ranks *rk, const char *path) {
     unlink(b);
 }
 
+/* GAC_RANK_SOLO=1 (measurement only: DESIGN §6's per-rank table): a rank
+ * runs by itself, as on a node where every rank has its own GPU and cores --
+ * its part goes to "<path>.solo<r>" and no rank waits for another */
+int gt_ranks_solo(void) {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("GAC_RANK_SOLO");
+        v = e && *e == '1';
+    }
+    return v;
+}
+
 void gt_ranks_place(const gt_ranks *rk, const char *path, const char *buf, size_t len) {
-    put_marker(path, "size", rk->me, (long long)len);
+    char solo[4096];
+    const int alone = gt_ranks_solo();
     off_t off = 0;
-    for (int r = 0; r < rk->me; ++r)
-        off += (off_t)get_marker(rk, path, "size", r);
-    const int fd = open(path, O_WRONLY | O_CREAT, 0666);
+    if (alone) {
+        snprintf(solo, sizeof(solo), "%s.solo%d", path, rk->me);
+        path = solo;
+    } else {
+        put_marker(path, "size", rk->me, (long long)len);
+        for (int r = 0; r < rk->me; ++r)
+            off += (off_t)get_marker(rk, path, "size", r);
+    }
+    const int fd = open(path, O_WRONLY | O_CREAT | (alone ? O_TRUNC : 0), 0666);
     if (fd < 0)
         gt_abort("Can't open %s to write: %s", path, strerror(errno));
     for (size_t done = 0; done < len;) {
@@ -880,10 +899,13 @@ void gt_ranks_place(const gt_ranks *rk, const char *path, const char *buf, size_
     }
     if (close(fd) != 0)
         gt_abort("close failed on %s", path);
-    put_marker(path, "done", rk->me, 1);
+    if (!alone)
+        put_marker(path, "done", rk->me, 1);
 }
 
 void gt_ranks_finish(const gt_ranks *rk, const char *path) {
+    if (gt_ranks_solo())
+        return;
     off_t total = 0;
     for (int r = 0; r < rk->n; ++r) {
         total += (off_t)get_marker(rk, path, "size", r);

@@ -140,6 +140,10 @@ void gt_ranks_append_parts(const gt_ranks *rk, const char *path, FILE *f);
  * before it calls this); rank 0 then waits for all parts (gt_ranks_finish).
  * gt_ranks_clear_markers removes this rank's stale markers at startup. */
 void gt_ranks_clear_markers(const gt_ranks *rk, const char *path);
+/* GAC_RANK_SOLO=1 (measurement only): ranks run alone, no rank waits for
+ * another; a part goes to "<path>.solo<r>" (chainNet) or is dropped
+ * (axtChain: rank 0 writes its own chains only) */
+int gt_ranks_solo(void);
 void gt_ranks_place(const gt_ranks *rk, const char *path, const char *buf, size_t len);
 void gt_ranks_finish(const gt_ranks *rk, const char *path);
 

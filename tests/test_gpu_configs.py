@@ -428,8 +428,9 @@ def _sha(*paths):
 @pytest.mark.timeout(900)
 def test_c5_fullscale_vs_reference_sha(tmp_path):
     """C5 at the bench's full size (5 M chains, 116 M blocks, all 455 x 66
-    sequences): bin/chainNet -rescore nets and bin/scoreChain's chains have
-    the sha256 of the reference's outputs on the same input
+    sequences): bin/chainNet -rescore nets -- one process, and eight ranks
+    (-nranks=8, the 8-GPU split) -- and bin/scoreChain's chains have the
+    sha256 of the reference's outputs on the same input
     (tests/golden/fullscale/c5.json; the reference takes ~45 min for the
     nets, so its outputs are pinned by hash)."""
     from genomealignmenttools_amd._lib import PKG_DIR
@@ -442,11 +443,27 @@ def test_c5_fullscale_vs_reference_sha(tmp_path):
           "-rescore", f"-tNibDir={p('t.2bit')}", f"-qNibDir={p('q.2bit')}", "-linearGap=loose"])
     _run([_bin("scoreChain"), p("in.chain"), p("t.2bit"), p("q.2bit"), p("o.sc.chain"),
           "-linearGap=loose"])
-    i, t, q, sc = _sha(p("in.chain"), p("o.t.net"), p("o.q.net"), p("o.sc.chain"))
+    # the 8-GPU split of the headline (bench.py --gpus 8): chainNet -nranks=8,
+    # every rank here on device 0 with 2 host threads
+    procs = [subprocess.Popen([_bin("chainNet"), p("in.chain"), p("t.sizes"), p("q.sizes"),
+                               p("r8.t.net"), p("r8.q.net"), "-rescore", f"-tNibDir={p('t.2bit')}",
+                               f"-qNibDir={p('q.2bit')}", "-linearGap=loose", "-nranks=8",
+                               f"-rank={r}", "-gpu=0"],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                              env=dict(os.environ, GAC_RANK_TOKEN="c5r8", GAC_THREADS="2"))
+             for r in range(8)]
+    for r, pr in enumerate(procs):
+        _, err = pr.communicate(timeout=600)
+        assert pr.returncode == 0, (r, err[-2000:])
+    i, t, q, sc, t8, q8 = _sha(p("in.chain"), p("o.t.net"), p("o.q.net"), p("o.sc.chain"),
+                               p("r8.t.net"), p("r8.q.net"))
     assert i == g["in_chain_sha256"], "generated input differs from the golden run's"
     assert t == g["chainnet_rescore"]["t_net_sha256"]
     assert q == g["chainnet_rescore"]["q_net_sha256"]
     assert sc == g["scorechain"]["chain_sha256"]
+    assert t8 == g["chainnet_rescore"]["t_net_sha256"]
+    assert q8 == g["chainnet_rescore"]["q_net_sha256"]
+    assert not [f for f in os.listdir(d) if ".gacpart" in f or ".gacsize" in f or ".gacdone" in f]
 
 
 @pytest.mark.timeout(900)
