@@ -1087,7 +1087,8 @@ def c3_leg(args, steps):
     res = {"workload": "configs[2]: chainCleaner -net= end to end (bin/chainCleaner) on C3: the "
                        "C2 chain set + 1000 planted chain-breaking loci",
            "ms_per_step": dt * 1e3, "steps": steps, **info, "removed_suspects": removed,
-           "tool_stages": [x.strip() for x in r.stderr.splitlines() if x.startswith("[")][-20:]}
+           "tool_stages": [x.strip() for x in r.stderr.splitlines()
+                           if x.startswith(("[stage]", "GPU:", "[gac_chains_upload]"))]}
     if os.path.exists(REF_CC_TOOL):
         ro = [p("ref.chain"), p("ref.bed")]
         for o in ro:

@@ -1884,19 +1884,33 @@ __device__ __forceinline__ uint32_t rev_nibbles(uint32_t v) {
     return ((v >> 2) & 0x33333333u) | ((v & 0x33333333u) << 2);
 }
 
-// one lane per plane word: one 8-byte load of the payload (every sequence
-// starts 8-byte aligned in the staging buffer, which is padded past its end).
-// A workgroup takes kRelPer runs of 256 words: the sequence search (a chain
-// of dependent scalar loads) is paid once per workgroup, not per 5 KB.
-constexpr int kRelPer = 8;
+// Two plane words per lane: one 16-byte load of the payload (every sequence
+// starts 8-byte aligned in the staging buffer, which is padded past its end),
+// one 16-byte plane store and one 8-byte N-mask store (round 4's lane per
+// word issued 8-byte accesses).  A workgroup takes kRelPer runs of 512
+// words: the sequence search (a chain of dependent scalar loads) is paid once
+// per workgroup.  A lane whose two words straddle a sequence start (rare)
+// builds each word from its own sequence.
+constexpr int kRelPer = 4;
+__device__ __forceinline__ int relayout_seq(const SeqDev *seqs, int nseq, int l, int64_t w) {
+    while (l + 1 < nseq && seqs[l + 1].word_off <= w) ++l;
+    return l;
+}
+
+__device__ __forceinline__ void relayout_word(const uint8_t *raw, const SeqDev &s, int64_t w,
+                                              uint32_t &p0, uint32_t &p1, uint32_t &pad) {
+    const int64_t base0 = (w - s.word_off) * 32;
+    const uint64_t x = *reinterpret_cast<const uint64_t *>(raw + s.byte_off + (base0 >> 2));
+    const int64_t valid = s.size - base0;  // > 0
+    pad = valid >= 32 ? 0u : ~((1u << valid) - 1u);  // padding scores 0 like an N
+    p0 = rev_nibbles(even_bits(x)) & ~pad;
+    p1 = rev_nibbles(even_bits(x >> 1)) & ~pad;
+}
+
 __global__ void __launch_bounds__(256) k_relayout(const uint8_t *raw, const SeqDev *seqs,
                                                   int nseq, int64_t nwords, uint2 *planes,
                                                   uint32_t *nmask) {
-    const int64_t W0 = (int64_t)blockIdx.x * blockDim.x * kRelPer;
-    // the sequence of the workgroup's first word: a search on workgroup-uniform
-    // values (scalar loads); each run then steps it forward, and the rare lanes
-    // past the next sequence start step further (sequences are mostly far
-    // longer than 256 words)
+    const int64_t W0 = (int64_t)blockIdx.x * blockDim.x * 2 * kRelPer;
     int lo = 0, hi = nseq - 1;
     while (lo < hi) {  // last seq with word_off <= W0
         const int mid = (lo + hi + 1) >> 1;
@@ -1904,21 +1918,38 @@ __global__ void __launch_bounds__(256) k_relayout(const uint8_t *raw, const SeqD
         else hi = mid - 1;
     }
     for (int r = 0; r < kRelPer; ++r) {
-        const int64_t w0 = W0 + r * (int64_t)blockDim.x, w = w0 + threadIdx.x;
+        const int64_t w0 = W0 + r * 2 * (int64_t)blockDim.x, w = w0 + 2 * threadIdx.x;
         if (w0 >= nwords) return;
         while (lo + 1 < nseq && seqs[lo + 1].word_off <= w0) ++lo;  // (uniform)
-        int l = lo;
-        if (l + 1 < nseq && seqs[l + 1].word_off < w0 + (int64_t)blockDim.x)
-            while (l + 1 < nseq && seqs[l + 1].word_off <= w) ++l;
         if (w >= nwords) return;
-        const SeqDev s = seqs[l];
-        const int64_t base0 = (w - s.word_off) * 32;
-        const uint64_t x = *reinterpret_cast<const uint64_t *>(raw + s.byte_off + (base0 >> 2));
-        const int64_t valid = s.size - base0;  // > 0
-        const uint32_t pad = valid >= 32 ? 0u : ~((1u << valid) - 1u);  // padding scores 0 like an N
-        const uint32_t p0 = rev_nibbles(even_bits(x)), p1 = rev_nibbles(even_bits(x >> 1));
-        planes[w] = make_uint2(p0 & ~pad, p1 & ~pad);
-        nmask[w] = pad;
+        const int l0 = relayout_seq(seqs, nseq, lo, w);
+        const SeqDev s = seqs[l0];
+        uint32_t a0, a1, ap, b0 = 0, b1 = 0, bp = 0xffffffffu;
+        const bool two = w + 1 < nwords;
+        if (two && (l0 + 1 >= nseq || seqs[l0 + 1].word_off > w + 1) &&
+            (w + 1 - s.word_off) * 32 < s.size) {  // both words in this sequence
+            const int64_t base0 = (w - s.word_off) * 32;
+            const u32x4a8 x = *reinterpret_cast<const u32x4a8 *>(raw + s.byte_off + (base0 >> 2));
+            const uint64_t x0 = (uint64_t)x.x | ((uint64_t)x.y << 32);
+            const uint64_t x1 = (uint64_t)x.z | ((uint64_t)x.w << 32);
+            const int64_t valid = s.size - base0 - 32;  // of the second word, > 0
+            bp = valid >= 32 ? 0u : ~((1u << valid) - 1u);
+            ap = 0;
+            a0 = rev_nibbles(even_bits(x0));
+            a1 = rev_nibbles(even_bits(x0 >> 1));
+            b0 = rev_nibbles(even_bits(x1)) & ~bp;
+            b1 = rev_nibbles(even_bits(x1 >> 1)) & ~bp;
+        } else {
+            relayout_word(raw, s, w, a0, a1, ap);
+            if (two) relayout_word(raw, seqs[relayout_seq(seqs, nseq, l0, w + 1)], w + 1, b0, b1, bp);
+        }
+        if (two) {
+            *reinterpret_cast<uint4 *>(planes + w) = make_uint4(a0, a1, b0, b1);
+            *reinterpret_cast<uint2 *>(nmask + w) = make_uint2(ap, bp);
+        } else {
+            planes[w] = make_uint2(a0, a1);
+            nmask[w] = ap;
+        }
     }
 }
 
@@ -2287,7 +2318,7 @@ hipError_t launch_block_gaps_flat(const int32_t *coff, const int32_t *tile_c0, i
 
 hipError_t launch_relayout(const uint8_t *raw, const SeqDev *seqs, int nseq, int64_t nwords,
                            uint2 *planes, uint32_t *nmask, hipStream_t s) {
-    const int64_t nb = (nwords + 256 * kRelPer - 1) / (256 * kRelPer);
+    const int64_t nb = (nwords + 512 * kRelPer - 1) / (512 * kRelPer);
     if (nb == 0) return hipSuccess;
     hipLaunchKernelGGL(k_relayout, dim3((unsigned)nb), dim3(256), 0, s, raw, seqs, nseq, nwords,
                        planes, nmask);

@@ -2467,6 +2467,7 @@ typedef struct ax_gjob {
     ax_gpair *G;
     int phase;
     _Atomic int64_t next;
+    double t_leaves, t_tree, t_export; /* (phase 1 laps summed over threads; racy, timing only) */
     /* device results */
     const int64_t *leaf_off, *xoff;
     const int64_t *total;
@@ -2646,9 +2647,16 @@ static void *gdp_thread(void *arg) {
             w->te = J->te + b0;
             w->score = J->score + b0;
             work_reserve(w, w->n);
+            const double ta = gnow();
             if (pair_leaves(w) > 0) {
+                const double tb = gnow();
                 pair_tree(w);
+                const double tc = gnow();
                 gpair_export(G);
+                const double td = gnow();
+                X->t_leaves += tb - ta; /* (phase laps, GAC_TIMING; summed over threads) */
+                X->t_tree += tc - tb;
+                X->t_export += td - tc;
             }
         } else if (X->phase == 2) {
             if (!G->ok || w->err)
@@ -2861,9 +2869,11 @@ static int axt_dp_gpu(ax_job *J, int nt) {
         }
         t6 = gnow();
         if (getenv("GAC_TIMING"))
-            fprintf(stderr, "[gac_axt_chain] device DP: trees %.3f s, gather %.3f s, gac_chain_dp "
-                            "%.3f s, peel %.3f s, %lld crossovers %.3f s, finish %.3f s\n",
-                    t1 - t, t2 - t1, t3 - t2, t4 - t3, (long long)nx, t5 - t4, t6 - t5);
+            fprintf(stderr, "[gac_axt_chain] device DP: trees %.3f s (thread-seconds: leaves %.3f, "
+                            "tree %.3f, export %.3f), gather %.3f s, gac_chain_dp %.3f s, peel %.3f s, "
+                            "%lld crossovers %.3f s, finish %.3f s\n",
+                    t1 - t, X.t_leaves, X.t_tree, X.t_export, t2 - t1, t3 - t2, t4 - t3,
+                    (long long)nx, t5 - t4, t6 - t5);
         free(xt);
         free(xq);
         free(xs);
