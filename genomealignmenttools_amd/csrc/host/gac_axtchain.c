@@ -2920,30 +2920,33 @@ static int axt_dp_gpu(ax_job *J, int nt) {
  * (k_dp_fast, one wave per pair, every device pair at once) while host
  * threads take the others (teams on the largest).  A device pair must end
  * within the host's critical path, estimated from the largest pair at the
- * team's rate; pairs are given to the device from the smallest up while
- * their device time (leaves x the device's per-leaf time) fits 0.7 of it.
- * GAC_AXT_DP=host: no device pairs; GAC_DP_GPU_MAX=n: device pairs of at
- * most n leaves (0: none); GAC_DP_DEV_US / GAC_DP_HOST_US: the per-leaf
- * times of the model.  Returns the first device place in `order`. */
+ * team's rate (its device time, leaves x the device's per-leaf time, within
+ * 0.7 of it), and is at most 5000 leaves: the device side's host work
+ * (export of paths and overlap lists, peel, finish) costs the host about
+ * as much per leaf as the DP it saves, so a larger share slows the run
+ * (r05multi: pairs up to 5000 leaves, 1.4 M of C4's 50 M blocks, is
+ * neutral; the model's 189 k-leaf bound is +0.5 s).  Pairs go to the
+ * device from the smallest up.  GAC_AXT_DP=host: no device pairs;
+ * GAC_DP_GPU_MAX=n: the leaf cap (0: none); GAC_DP_DEV_US /
+ * GAC_DP_HOST_US: the per-leaf times of the model.  Returns the first
+ * device place in `order`. */
 static int64_t dp_device_split(const int64_t *psize, const int32_t *order, int64_t np,
                                const ax_env *e) {
     const char *dpm = getenv("GAC_AXT_DP");
     if ((dpm && strcmp(dpm, "host") == 0) || !e->fast || np == 0)
         return np;
-    int64_t lmax;
+    const char *dv = getenv("GAC_DP_DEV_US"), *hv = getenv("GAC_DP_HOST_US");
+    const double dev_us = dv && atof(dv) > 0 ? atof(dv) : 20.0;  /* k_dp_fast, r05dp3 */
+    const double host_us = hv && atof(hv) > 0 ? atof(hv) : 0.47; /* team, C4 (r04i) */
+    const double crit = (double)psize[order[0]] * host_us * 1e-6;
+    if (crit < 0.25) /* (small runs: the device's start-up costs more) */
+        return np;
+    int64_t lmax = (int64_t)(0.7 * crit / (dev_us * 1e-6));
     const char *mx = getenv("GAC_DP_GPU_MAX");
-    if (mx && *mx) {
-        lmax = atoll(mx);
-    } else {
-        const char *dv = getenv("GAC_DP_DEV_US"), *hv = getenv("GAC_DP_HOST_US");
-        const double dev_us = dv && atof(dv) > 0 ? atof(dv) : 20.0;  /* k_dp_fast, r05dp3 */
-        const double host_us = hv && atof(hv) > 0 ? atof(hv) : 0.47; /* team, C4 (r04i) */
-        const double crit = (double)psize[order[0]] * host_us * 1e-6;
-        if (crit < 0.25) /* (small runs: the device's start-up costs more) */
-            return np;
-        lmax = (int64_t)(0.7 * crit / (dev_us * 1e-6));
-    }
-    if (lmax < 1024)
+    const int64_t cap = mx && *mx ? atoll(mx) : 5000;
+    if (cap < lmax)
+        lmax = cap;
+    if (lmax < 1)
         return np;
     int64_t kd = np;
     while (kd > 1 && psize[order[kd - 1]] <= lmax)
@@ -3528,11 +3531,11 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
         stage("kd-tree DP (device)", &tclock);
     } else {
         /* the smallest pairs to the device, on a thread of their own (its
-         * host phases -- trees, peel, finish -- on 2 threads taken from the
-         * pool) */
+         * host phases -- trees, peel, finish -- on 2 threads of its own,
+         * beside the host's: taking them from the pool was slower,
+         * r05multi hx2) */
         const int64_t kd = dp_device_split(psize, order, np, &env);
         int64_t np_host = np, nb_host = nb; /* the host's pairs and blocks */
-        int dev_threads = 0; /* the device side's host threads (taken from the pool) */
         dev_run *D = NULL;
         pthread_t dth;
         int dev_started = 0;
@@ -3544,7 +3547,6 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
             atomic_init(&D->J.next, 0);
             const char *dtv = getenv("GAC_DP_DEV_THREADS"); /* (its host phases' threads) */
             D->nt = dtv && atoi(dtv) > 0 ? atoi(dtv) : 2;
-            dev_threads = D->nt;
             if (pthread_create(&dth, NULL, dev_runner, D) == 0)
                 dev_started = 1;
             else
@@ -3588,7 +3590,7 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
             const char *pl = getenv("GAC_DP_POOL"); /* (threads beside the teams) */
             pool = pl && atoi(pl) > 0 && atoi(pl) < nthreads
                        ? atoi(pl)
-                       : (nthreads / 3 - dev_threads > 1 ? nthreads / 3 - dev_threads : 1);
+                       : (nthreads / 3 > 1 ? nthreads / 3 : 1);
             if (pool > np_host - big) /* (no pool pairs left, e.g. an -nranks rank holding one big pair) */
                 pool = (int)(np_host - big);
             const int tt = nthreads - pool;

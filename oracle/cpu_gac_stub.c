@@ -248,11 +248,9 @@ void gac_chains_free(gac_chainset *s) {
  * gac_axt_chain; chainNet's partial fills) */
 int gac_score_ranges(gac_ctx *c, const gac_chainset *s, const gac_range *r, int64_t n,
                      uint32_t flags, int64_t *g, int64_t *l, int32_t *ali) {
-    (void)flags;
-    (void)l;
     for (int64_t i = 0; i < n; ++i) {
         const int32_t k = r[i].chain, lo = r[i].t_start, hi = r[i].t_end;
-        int64_t sc = 0;
+        int64_t sc = 0, ls = 0, lm = 0; /* (local: chainCalcScoreLocal's running score, max) */
         int32_t a = 0, have = 0, pq = 0, pt = 0;
         for (int64_t b = s->off[k]; b < s->off[k + 1]; ++b) {
             const int32_t t0 = s->bt[b] > lo ? s->bt[b] : lo;
@@ -260,9 +258,16 @@ int gac_score_ranges(gac_ctx *c, const gac_chainset *s, const gac_range *r, int6
             if (t1 <= t0)
                 continue;
             const int32_t q0 = s->bq[b] + (t0 - s->bt[b]);
-            if (have)
-                sc -= gac_gap_cost(c->g, q0 - pq, t0 - pt);
-            sc += block_score(c, s->tseq[k], s->qseq[k], s->strand[k], t0, q0, t1 - t0);
+            if (have) {
+                const int gc = gac_gap_cost(c->g, q0 - pq, t0 - pt);
+                sc -= gc;
+                ls = ls - gc > 0 ? ls - gc : 0;
+            }
+            const int bsc = block_score(c, s->tseq[k], s->qseq[k], s->strand[k], t0, q0, t1 - t0);
+            sc += bsc;
+            ls += bsc;
+            if (ls > lm)
+                lm = ls;
             a += t1 - t0;
             pq = q0 + (t1 - t0);
             pt = t1;
@@ -270,8 +275,20 @@ int gac_score_ranges(gac_ctx *c, const gac_chainset *s, const gac_range *r, int6
         }
         g[i] = sc;
         ali[i] = a;
+        if ((flags & GAC_WANT_LOCAL) && l)
+            l[i] = lm;
     }
     return GAC_OK;
+}
+
+/* chains in host memory: a temporary set */
+int gac_score_ranges_host(gac_ctx *c, const gac_chainset_desc *d, const gac_range *r, int64_t n,
+                          uint32_t flags, int64_t *g, int64_t *l, int32_t *ali) {
+    gac_chainset *s = NULL;
+    gac_chains_upload(c, d, &s);
+    const int rc = gac_score_ranges(c, s, r, n, flags, g, l, ali);
+    gac_chains_free(s);
+    return rc;
 }
 
 /* windows: each one checked against chainSubsetOnT's walk (kent/src/lib/
