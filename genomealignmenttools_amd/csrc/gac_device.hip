@@ -33,6 +33,10 @@ hipError_t launch_combine(const ScoreArgs &a, int grid, hipStream_t s);
 hipError_t launch_small(const ScoreArgs &a, const Range *rin, SmallOut *out, hipStream_t s);
 hipError_t launch_small_host(const ScoreArgs &a, const RangeDesc *hin, const int4 *pool,
                              SmallOut *out, hipStream_t s);
+hipError_t launch_small_server(const ScoreArgs &a0, const ScoreArgs &a1, const Range *rin,
+                               const RangeDesc *hin, const int4 *pool, SmallOut *out,
+                               SmallMail *mail, SmallSync *sy, uint32_t last_done, uint64_t idle,
+                               hipStream_t s);
 struct SeqDev {
     int64_t byte_off;
     int64_t word_off;
@@ -136,8 +140,32 @@ struct Prof {
 
 constexpr size_t kStatusBytes = 128;  // status[0..8)
 
-// held by every entry point that uses a context (see gac_ctx::mu)
-#define CTX_LOCK(c) std::lock_guard<std::recursive_mutex> ctx_lock_((c)->mu)
+// held by every entry point that uses a context (see gac_ctx::mu); it also
+// parks the small-batch server (k_small_server) first, so that nothing else
+// runs beside a resident grid -- only the small-batch paths keep it
+#define CTX_LOCK(c) CtxLock ctx_lock_((c), true)
+#define CTX_LOCK_SMALL(c) CtxLock ctx_lock_((c), false)
+
+// the resident small-batch server of a context (GAC_SMALL_SERVER=1)
+struct SmallServer {
+    bool on = false;       // enabled for this context
+    bool running = false;  // a grid is resident (or exiting: mail->state 2)
+    hipStream_t st = nullptr;
+    SmallMail *mail = nullptr, *d_mail = nullptr;  // pinned, coherent
+    SmallSync *d_sync = nullptr;
+    Range *h_in = nullptr, *d_in = nullptr;        // pinned, coherent [kSmallMax]
+    RangeDesc *h_hq = nullptr, *d_hq = nullptr;    // pinned, coherent [kSmallMax]
+    int4 *h_pool = nullptr, *d_pool = nullptr;     // pinned, coherent, grown while parked
+    int64_t pool_cap = 0;
+    SmallOut *h_out = nullptr, *d_out = nullptr;   // pinned, coherent [kSmallMax]
+    uint32_t seq = 0;                  // the last request made (= completed: calls wait)
+    const gac_chainset *cs = nullptr;  // the set of kind-0 requests (nullptr: none)
+    uint32_t gap_version = 0;
+    int local = -1;
+    ScoreArgs a0, a1;                  // the resident grid's arguments
+    uint64_t idle = 2000000;           // exit after 20 ms without a request (100 MHz ticks)
+    int64_t launches = 0, requests = 0;
+};
 
 struct gac_ctx {
     // every entry point that touches the context's state holds this (the
@@ -211,6 +239,16 @@ struct gac_ctx {
     // device memory and orphans them (ctx = NULL), so a set freed after its
     // context (a kent-shim cache, a garbage-collected binding) is only deleted
     std::vector<gac_chainset *> sets;
+    SmallServer srv;
+};
+
+static void srv_park(gac_ctx *c);
+
+struct CtxLock {
+    std::lock_guard<std::recursive_mutex> g;
+    CtxLock(gac_ctx *c, bool park) : g(c->mu) {
+        if (park) srv_park(c);
+    }
 };
 
 struct gac_chainset {
@@ -341,6 +379,11 @@ extern "C" int gac_open(int device, gac_ctx **out) {
         const int m = atoi(v);
         c->small_max = m < 0 ? 0 : (m > kSmallMax ? kSmallMax : m);
     }
+    if (const char *v = getenv("GAC_SMALL_SERVER")) c->srv.on = v[0] == '1';
+    if (const char *v = getenv("GAC_SMALL_SERVER_IDLE_US")) {
+        const long long us = atoll(v);
+        if (us > 0 && us <= 10000000) c->srv.idle = (uint64_t)us * 100;
+    }
     lap("hipHostMalloc");
     *out = c;
     return GAC_OK;
@@ -357,9 +400,16 @@ static void free_genome(Genome &g) {
 
 static void free_set_memory(gac_chainset *cs);
 
+static void srv_free(gac_ctx *c);
+
 extern "C" void gac_close(gac_ctx *c) {
     if (!c) return;
     hipSetDevice(c->device);
+    {
+        std::lock_guard<std::recursive_mutex> g(c->mu);
+        srv_park(c);
+        srv_free(c);
+    }
     hipStreamSynchronize(c->stream);
     {
         CTX_LOCK(c);
@@ -1720,6 +1770,7 @@ extern "C" void gac_chains_free(gac_chainset *cs) {
         CTX_LOCK(c);
         free_set_memory(cs);
         c->sets.erase(std::remove(c->sets.begin(), c->sets.end(), cs), c->sets.end());
+        if (c->srv.cs == cs) c->srv.cs = nullptr;
     }
     delete cs;
 }
@@ -1900,6 +1951,180 @@ static int prepare_args(gac_ctx *c, const gac_chainset *cs, int64_t n, uint32_t 
 static int score_device_split(gac_ctx *c, const ScoreArgs &a_base, const Range *d_ranges,
                               const Window *d_wins, int64_t n, long long *d_g, long long *d_l,
                               int32_t *d_ali, hipStream_t s);
+
+// ------------------------------------------------ the small-batch server ----
+// k_small_server (gac_kernels.hip) keeps a grid resident between the calls of
+// a run of small batches (chainCleaner's replay loop), so a call costs a
+// mailbox round trip instead of a launch and a stream synchronisation.  Only
+// the small-batch entry points keep it running; every other entry point parks
+// it first (CTX_LOCK), and the grid exits by itself after `idle` without a
+// request.  Opt-in: GAC_SMALL_SERVER=1.
+static void srv_park(gac_ctx *c) {
+    SmallServer &v = c->srv;
+    if (!v.running) return;
+    __atomic_store_n(&v.mail->stop, 1u, __ATOMIC_RELEASE);
+    hipStreamSynchronize(v.st);
+    __atomic_store_n(&v.mail->stop, 0u, __ATOMIC_RELEASE);
+    v.running = false;
+}
+
+static void srv_free(gac_ctx *c) {
+    SmallServer &v = c->srv;
+    void *h[] = {v.mail, v.h_in, v.h_hq, v.h_pool, v.h_out};
+    for (void *p : h)
+        if (p) hipHostFree(p);
+    if (v.d_sync) hipFree(v.d_sync);
+    if (v.st) hipStreamDestroy(v.st);
+    const bool on = v.on;
+    const uint64_t idle = v.idle;
+    v = SmallServer();
+    v.on = on;
+    v.idle = idle;
+}
+
+static int srv_alloc(gac_ctx *c) {
+    SmallServer &v = c->srv;
+    if (v.mail) return GAC_OK;
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    HIPCHK(hipStreamCreateWithFlags(&v.st, hipStreamNonBlocking));
+    HIPCHK(hipHostMalloc((void **)&v.mail, sizeof(SmallMail), fl));
+    memset(v.mail, 0, sizeof(SmallMail));
+    HIPCHK(hipHostGetDevicePointer((void **)&v.d_mail, v.mail, 0));
+    HIPCHK(hipHostMalloc((void **)&v.h_in, kSmallMax * sizeof(Range), fl));
+    HIPCHK(hipHostGetDevicePointer((void **)&v.d_in, v.h_in, 0));
+    HIPCHK(hipHostMalloc((void **)&v.h_hq, kSmallMax * sizeof(RangeDesc), fl));
+    HIPCHK(hipHostGetDevicePointer((void **)&v.d_hq, v.h_hq, 0));
+    HIPCHK(hipHostMalloc((void **)&v.h_out, kSmallMax * sizeof(SmallOut), fl));
+    HIPCHK(hipHostGetDevicePointer((void **)&v.d_out, v.h_out, 0));
+    HIPCHK(hipMalloc((void **)&v.d_sync, sizeof(SmallSync)));
+    v.seq = 0;
+    return GAC_OK;
+}
+
+// the pool of host-planned window records: grown (while parked) to `need`
+static int srv_pool(gac_ctx *c, int64_t need) {
+    SmallServer &v = c->srv;
+    if (need <= v.pool_cap) return GAC_OK;
+    srv_park(c);
+    if (v.h_pool) hipHostFree(v.h_pool);
+    v.h_pool = nullptr;
+    v.pool_cap = 0;
+    const int64_t cap = std::max<int64_t>(need + need / 2, 1 << 16);
+    HIPCHK(hipHostMalloc((void **)&v.h_pool, cap * sizeof(int4),
+                         hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer((void **)&v.d_pool, v.h_pool, 0));
+    v.pool_cap = cap;
+    return GAC_OK;
+}
+
+static int srv_launch(gac_ctx *c) {
+    SmallServer &v = c->srv;
+    HIPCHK(hipMemsetAsync(v.d_sync, 0, sizeof(SmallSync), v.st));
+    __atomic_store_n(&v.mail->state, 1u, __ATOMIC_RELEASE);
+    __atomic_store_n(&v.mail->done, v.seq, __ATOMIC_RELEASE);
+    HIPCHK(launch_small_server(v.a0, v.a1, v.d_in, v.d_hq, v.d_pool, v.d_out, v.d_mail, v.d_sync,
+                               v.seq, v.idle, v.st));
+    v.running = true;
+    ++v.launches;
+    return GAC_OK;
+}
+
+// a resident grid for requests of this kind: kind 0 scores ranges of `cs`
+// (prepared like the k_small path: gaps, window index), kind 1 host-planned
+// descriptors (any grid with the same local flag takes them)
+static int srv_ensure(gac_ctx *c, const gac_chainset *cs, uint32_t flags) {
+    SmallServer &v = c->srv;
+    const int local = (flags & GAC_WANT_LOCAL) ? 1 : 0;
+    if (v.running && v.local == local && v.gap_version == c->gap_version && (!cs || v.cs == cs))
+        return GAC_OK;
+    srv_park(c);
+    int rc = srv_alloc(c);
+    if (rc != GAC_OK) return rc;
+    if (!cs) cs = v.cs;  // (a freed set is cleared from v.cs by gac_chains_free)
+    ScoreArgs a1;
+    memset(&a1, 0, sizeof(a1));
+    const Genome &T = c->g[0], &Q = c->g[1];
+    a1.t_planes = T.planes;
+    a1.t_nmask = T.nmask;
+    a1.t_woff = T.d_woff;
+    a1.q_planes = Q.planes;
+    a1.q_nmask = Q.nmask;
+    a1.q_woff = Q.d_woff;
+    a1.want_local = local;
+    a1.gap_len = c->gap_len;
+    a1.gap_tab = c->d_gap_tab;
+    a1.small_tab = c->d_small;
+    memcpy(a1.coef, c->coef, sizeof(a1.coef));
+    a1.sym = c->sym;
+    a1.gap = c->gap;
+    ScoreArgs a0 = a1;
+    if (cs) {
+        long long dummy = 0;
+        if ((rc = prepare_args(c, cs, 1, flags, &dummy, c->stream, a0)) != GAC_OK) return rc;
+        if ((rc = ensure_index(c, cs, c->stream)) != GAC_OK) return rc;
+        HIPCHK(hipStreamSynchronize(c->stream));  // (the gaps and the index, before the grid)
+    }
+    if ((rc = srv_pool(c, 1)) != GAC_OK) return rc;
+    v.a0 = a0;
+    v.a1 = a1;
+    v.cs = cs;
+    v.local = local;
+    v.gap_version = c->gap_version;
+    return srv_launch(c);
+}
+
+// one request: inputs already in the mailbox buffers; waits for the results
+static int srv_call(gac_ctx *c, uint32_t kind, int64_t n) {
+    SmallServer &v = c->srv;
+    __atomic_store_n(&v.mail->kind, kind, __ATOMIC_RELAXED);
+    __atomic_store_n(&v.mail->n, (uint32_t)n, __ATOMIC_RELAXED);
+    const uint32_t prev = v.seq;
+    uint32_t seq = prev + 1;  // (request numbers skip 0 and the exit word)
+    if (seq == 0 || seq == 0xffffffffu) seq = 1;
+    v.seq = seq;
+    __atomic_store_n(&v.mail->req, seq, __ATOMIC_RELEASE);
+    ++v.requests;
+    struct timespec t0;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (uint64_t it = 1;; ++it) {
+        if (__atomic_load_n(&v.mail->done, __ATOMIC_ACQUIRE) == seq) return GAC_OK;
+        if (__atomic_load_n(&v.mail->state, __ATOMIC_ACQUIRE) == 2u) {
+            // the grid left (idle) before it saw this request: once it has
+            // drained, a new one takes the request from the mailbox
+            HIPCHK(hipStreamSynchronize(v.st));
+            v.running = false;
+            if (__atomic_load_n(&v.mail->done, __ATOMIC_ACQUIRE) == seq) return GAC_OK;
+            v.seq = prev;
+            const int rc = srv_launch(c);
+            v.seq = seq;
+            if (rc != GAC_OK) return rc;
+            continue;
+        }
+        if ((it & 4095) == 0) {
+            struct timespec t1;
+            clock_gettime(CLOCK_MONOTONIC, &t1);
+            if ((t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec) > 10.0) {
+                srv_park(c);
+                return gac_fail(GAC_E_HIP, "small-batch server: no answer to request %u in 10 s",
+                                seq);
+            }
+            const hipError_t q = hipStreamQuery(v.st);
+            if (q != hipSuccess && q != hipErrorNotReady)
+                return gac_fail(GAC_E_HIP, "small-batch server failed: %s", hipGetErrorString(q));
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+static void srv_results(const gac_ctx *c, int64_t n, uint32_t flags, int64_t *global,
+                        int64_t *local, int32_t *ali) {
+    for (int64_t i = 0; i < n; ++i) {
+        const SmallOut o = c->srv.h_out[i];
+        global[i] = o.g;
+        ali[i] = o.ali;
+        if (flags & GAC_WANT_LOCAL) local[i] = o.l;
+    }
+}
 
 // d_wins non-null: the ranges come with their windows (gac_score_windows*),
 // d_ranges is ignored
@@ -2231,7 +2456,8 @@ extern "C" int gac_score_ranges_host(gac_ctx *c, const gac_chainset_desc *d, con
                                      int32_t *ali) {
     gac_clear_error();
     if (!c || !d) return gac_fail(GAC_E_ARG, "gac_score_ranges_host: NULL argument");
-    CTX_LOCK(c);
+    CTX_LOCK_SMALL(c);
+    if (!c->srv.on) srv_park(c);
     if (n < 0) return gac_fail(GAC_E_ARG, "negative range count");
     if (n == 0) return GAC_OK;
     if (!r || !global || !ali || ((flags & GAC_WANT_LOCAL) && !local))
@@ -2245,7 +2471,11 @@ extern "C" int gac_score_ranges_host(gac_ctx *c, const gac_chainset_desc *d, con
     if (d->blk_off[0] != 0 || d->blk_off[d->n_chains] != d->n_blocks)
         return gac_fail(GAC_E_ARG, "gac_score_ranges_host: blk_off must run from 0 to n_blocks");
     HIPCHK(hipSetDevice(c->device));
-    if (!c->h_hq) {
+    const bool srv = c->srv.on;  // the resident grid takes the batches
+    if (srv) {
+        const int rc = srv_ensure(c, nullptr, flags);
+        if (rc != GAC_OK) return rc;
+    } else if (!c->h_hq) {
         HIPCHK(hipHostMalloc((void **)&c->h_hq, kSmallMax * sizeof(RangeDesc), hipHostMallocMapped));
         HIPCHK(hipHostGetDevicePointer((void **)&c->d_hq, c->h_hq, 0));
     }
@@ -2296,7 +2526,12 @@ extern "C" int gac_score_ranges_host(gac_ctx *c, const gac_chainset_desc *d, con
             hi[k] = std::max(a0, e0);
             tot += hi[k] - lo[k];
         }
-        if (tot > c->pool_cap) {
+        if (srv) {
+            if (tot > c->srv.pool_cap) {  // (parks the grid to grow the pool)
+                int rc = srv_pool(c, tot);
+                if (rc != GAC_OK || (rc = srv_ensure(c, nullptr, flags)) != GAC_OK) return rc;
+            }
+        } else if (tot > c->pool_cap) {
             if (c->h_pool) hipHostFree(c->h_pool);
             c->h_pool = nullptr;
             c->pool_cap = 0;
@@ -2305,6 +2540,8 @@ extern "C" int gac_score_ranges_host(gac_ctx *c, const gac_chainset_desc *d, con
             HIPCHK(hipHostGetDevicePointer((void **)&c->d_pool, c->h_pool, 0));
             c->pool_cap = cap;
         }
+        RangeDesc *hq = srv ? c->srv.h_hq : c->h_hq;
+        int4 *pool = srv ? c->srv.h_pool : c->h_pool;
         int64_t j = 0;
         for (int64_t k = 0; k < m; ++k) {
             const gac_range &q = r[i0 + k];
@@ -2312,7 +2549,7 @@ extern "C" int gac_score_ranges_host(gac_ctx *c, const gac_chainset_desc *d, con
             if (ts < 0 || ts >= (int32_t)T.sizes.size() || qs < 0 || qs >= (int32_t)Q.sizes.size())
                 return gac_fail(GAC_E_ARG, "chain %d: sequence index out of range", q.chain);
             const int64_t tsize = T.sizes[ts], qsize = Q.sizes[qs];
-            RangeDesc &h = c->h_hq[k];
+            RangeDesc &h = hq[k];
             h.tbase = T.woff[ts] * 32;
             const int64_t qw = Q.woff[qs] * 32;
             h.qbase = d->q_strand[q.chain] ? ~(qw + qsize) : qw;
@@ -2330,8 +2567,14 @@ extern "C" int gac_score_ranges_host(gac_ctx *c, const gac_chainset_desc *d, con
                                     (long long)t, (long long)qq, (long long)z);
                 pt = t + z;
                 pq = qq + z;
-                c->h_pool[j] = make_int4((int)t, (int)qq, (int)z, 0);
+                pool[j] = make_int4((int)t, (int)qq, (int)z, 0);
             }
+        }
+        if (srv) {
+            const int rc = srv_call(c, 1, m);
+            if (rc != GAC_OK) return rc;
+            srv_results(c, m, flags, global + i0, local ? local + i0 : nullptr, ali + i0);
+            continue;
         }
         a.n = m;
         HIPCHK(launch_small_host(a, c->d_hq, c->d_pool, c->d_small_out, s));
@@ -2351,17 +2594,28 @@ extern "C" int gac_score_ranges(gac_ctx *c, const gac_chainset *cs, const gac_ra
                                 int32_t *ali) {
     gac_clear_error();
     if (!c) return gac_fail(GAC_E_ARG, "NULL context");
-    CTX_LOCK(c);
+    CTX_LOCK_SMALL(c);
     if (n < 0) return gac_fail(GAC_E_ARG, "negative range count");
     if (n == 0) return GAC_OK;
     if (!ranges || !global || !ali || ((flags & GAC_WANT_LOCAL) && !local))
         return gac_fail(GAC_E_ARG, "NULL buffer");
     if (!cs) return gac_fail(GAC_E_ARG, "NULL chainset");
+    if (n > c->small_max || !c->srv.on) srv_park(c);
     for (int64_t i = 0; i < n; ++i)
         if (ranges[i].chain < 0 || ranges[i].chain >= cs->n_chains)
             return gac_fail(GAC_E_ARG, "range %lld: chain %d out of range", (long long)i,
                             ranges[i].chain);
     HIPCHK(hipSetDevice(c->device));
+    if (n <= c->small_max && c->srv.on) {  // a request to the resident grid
+        if (!c->scoring) return gac_fail(GAC_E_STATE, "gac_set_scoring() not called");
+        if (cs->ctx != c) return gac_fail(GAC_E_ARG, "chainset does not belong to this context");
+        int rc = srv_ensure(c, cs, flags);
+        if (rc != GAC_OK) return rc;
+        memcpy(c->srv.h_in, ranges, (size_t)n * sizeof(Range));
+        if ((rc = srv_call(c, 0, n)) != GAC_OK) return rc;
+        srv_results(c, n, flags, global, local, ali);
+        return GAC_OK;
+    }
     if (n <= c->small_max) {
         // one launch; ranges in and results out through pinned host memory
         hipStream_t s = c->stream;

@@ -185,6 +185,25 @@ struct ScoreArgs {
 
 constexpr int kSmallMax = 256;  // ranges per small-batch call
 
+// k_small_server's mailbox, in pinned coherent host memory: the host writes
+// kind, n and the inputs, then req; the server writes done, and state = 2
+// when it exits (idle or stop)
+struct SmallMail {
+    uint32_t req;    // host: the request number (written last)
+    uint32_t kind;   // 0: Range batch of the uploaded set; 1: host-planned RangeDesc + pool
+    uint32_t n;      // ranges (<= kSmallMax)
+    uint32_t stop;   // host: 1 = exit now
+    uint32_t done;   // server: the last completed request
+    uint32_t state;  // server: 2 = exited
+    uint32_t pad[26];
+};
+// its device-side broadcast word and completion count (zeroed per launch)
+struct SmallSync {
+    uint32_t seq, cnt;
+    uint32_t pad[30];
+};
+constexpr int kSrvWaves = 256;  // resident server waves (64 workgroups)
+
 // One run of a sparse genome upload (bytes): its place in the staging layout
 // (8-byte aligned), its offset in the packed upload (8-byte aligned), length.
 struct SparseRun {

@@ -1787,11 +1787,9 @@ __global__ void __launch_bounds__(256) k_fold_super(ScoreArgs a) {
 // `pool`, records {tStart, qStart, size, 0}); the gaps are computed here from
 // the next record and every chunk takes the N-mask path (no upload flags).
 template <bool LOCAL, bool SYM, bool HOST>
-__global__ void __launch_bounds__(256) k_small(ScoreArgs a, const Range *rin, const RangeDesc *hin,
-                                               const int4 *pool, SmallOut *out) {
-    const int lane = threadIdx.x & 63;
-    const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (w >= a.n) return;
+__device__ __forceinline__ void small_range(const ScoreArgs &a, const Range *rin,
+                                            const RangeDesc *hin, const int4 *pool, SmallOut *out,
+                                            int64_t w, int lane) {
     const RangeDesc d = HOST ? hin[w] : plan_range(a, rin[w]);
     const bool minus = d.qbase < 0;
     long long gsum = 0, asum = 0;
@@ -1855,6 +1853,99 @@ __global__ void __launch_bounds__(256) k_small(ScoreArgs a, const Range *rin, co
         o.pad = 0;
         out[w] = o;
     }
+}
+
+template <bool LOCAL, bool SYM, bool HOST>
+__global__ void __launch_bounds__(256) k_small(ScoreArgs a, const Range *rin, const RangeDesc *hin,
+                                               const int4 *pool, SmallOut *out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (w >= a.n) return;
+    small_range<LOCAL, SYM, HOST>(a, rin, hin, pool, out, w, lane);
+}
+
+// ------------------------------------------------------ k_small_server ----
+// The small batches of a long run of on-demand calls (chainCleaner's replay
+// loop) without a launch per call: a resident grid of kSrvWaves waves takes
+// requests from a mailbox in pinned, coherent host memory (SmallMail).  Wave 0
+// polls the mailbox (system-scope loads, s_sleep between them) and
+// broadcasts a new request number through device memory (SmallSync.seq);
+// every wave scores ranges w, w + kSrvWaves, ... of it (k_small's body, the
+// request's kind selecting the uploaded set's ranges or host-planned
+// descriptors), makes its results visible to the host and counts itself in
+// SmallSync.cnt; the last wave publishes the request number in mail->done.
+// Every wave reaches the exit: wave 0 broadcasts kSrvExit when the host sets
+// mail->stop or no request arrives within `idle` ticks of the 100 MHz
+// real-time counter, and then marks the mailbox exited (state 2); the host
+// re-launches the grid for a request that finds it gone.
+constexpr uint32_t kSrvExit = 0xffffffffu;
+
+__device__ __forceinline__ uint32_t sys_load(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_store(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <bool LOCAL, bool SYM>
+__global__ void __launch_bounds__(256) k_small_server(ScoreArgs a0, ScoreArgs a1, const Range *rin,
+                                                      const RangeDesc *hin, const int4 *pool,
+                                                      SmallOut *out, SmallMail *mail,
+                                                      SmallSync *sy, uint32_t last_done,
+                                                      uint64_t idle) {
+    const int lane = threadIdx.x & 63;
+    const int wave = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int nw = (int)(((int64_t)gridDim.x * blockDim.x) >> 6);
+    uint32_t cur = last_done;
+    for (;;) {
+        uint32_t s;
+        if (wave == 0) {
+            uint64_t t0 = wall_clock64();
+            for (;;) {
+                const uint32_t r = sys_load(&mail->req);
+                if (sys_load(&mail->stop)) {
+                    s = kSrvExit;
+                    break;
+                }
+                if (r != cur) {
+                    s = r;
+                    break;
+                }
+                if (wall_clock64() - t0 > idle) {
+                    s = kSrvExit;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            __hip_atomic_store(&sy->seq, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            for (;;) {  // (0: the launch's zeroed word, never a request number)
+                s = __hip_atomic_load(&sy->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                if (s != cur && s != 0) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        if (s == kSrvExit) break;
+        const uint32_t kind = sys_load(&mail->kind), n = sys_load(&mail->n);
+        for (int64_t w = wave; w < (int64_t)n; w += nw) {
+            if (kind) small_range<LOCAL, SYM, true>(a1, nullptr, hin, pool, out, w, lane);
+            else small_range<LOCAL, SYM, false>(a0, rin, nullptr, nullptr, out, w, lane);
+        }
+        __threadfence_system();  // this wave's results, before it is counted
+        uint32_t old = 0;
+        if (lane == 0)
+            old = __hip_atomic_fetch_add(&sy->cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        old = __shfl(old, 0, 64);
+        if (old == (uint32_t)nw - 1) {  // the last wave: reset the count, publish
+            if (lane == 0) {
+                __hip_atomic_store(&sy->cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __threadfence_system();
+                sys_store(&mail->done, s);
+            }
+        }
+        cur = s;
+    }
+    if (wave == 0 && lane == 0) sys_store(&mail->state, 2u);
 }
 
 // ------------------------------------------------------------ genome -----
@@ -2146,6 +2237,21 @@ hipError_t launch_small(const ScoreArgs &a, const Range *rin, SmallOut *out, hip
 hipError_t launch_small_host(const ScoreArgs &a, const RangeDesc *hin, const int4 *pool,
                              SmallOut *out, hipStream_t s) {
     launch_small_t<true>(a, nullptr, hin, pool, out, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_small_server(const ScoreArgs &a0, const ScoreArgs &a1, const Range *rin,
+                               const RangeDesc *hin, const int4 *pool, SmallOut *out,
+                               SmallMail *mail, SmallSync *sy, uint32_t last_done, uint64_t idle,
+                               hipStream_t s) {
+    const dim3 g(kSrvWaves / kWavesPerWG), b(256);
+    if (a0.want_local) {
+        if (a0.sym) k_small_server<true, true><<<g, b, 0, s>>>(a0, a1, rin, hin, pool, out, mail, sy, last_done, idle);
+        else k_small_server<true, false><<<g, b, 0, s>>>(a0, a1, rin, hin, pool, out, mail, sy, last_done, idle);
+    } else {
+        if (a0.sym) k_small_server<false, true><<<g, b, 0, s>>>(a0, a1, rin, hin, pool, out, mail, sy, last_done, idle);
+        else k_small_server<false, false><<<g, b, 0, s>>>(a0, a1, rin, hin, pool, out, mail, sy, last_done, idle);
+    }
     return hipGetLastError();
 }
 

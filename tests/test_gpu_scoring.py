@@ -548,6 +548,55 @@ def test_small_batches_vs_oracle(case):
     assert np.array_equal(g3, og) and np.array_equal(l3, ol) and np.array_equal(a3, oa)
 
 
+@pytest.mark.parametrize("idle_us", [None, "300"])
+def test_small_batch_server(monkeypatch, idle_us):
+    """GAC_SMALL_SERVER=1: small batches go to a resident grid
+    (k_small_server) through a mailbox in pinned host memory instead of a
+    launch each.  Requests of both kinds (ranges of an uploaded set, ranges of
+    chains in host memory) interleaved, the local score switched off and on
+    (a new grid), a large batch in between (the grid parked), a freed set, and
+    -- with a 300 us idle limit and sleeps between calls -- grids that exit
+    and are re-launched under a waiting request: every result equals the
+    oracle's."""
+    import time
+    from genomealignmenttools_amd import synth
+    from genomealignmenttools_amd.gachain import GAC_Q, GAC_T
+    monkeypatch.setenv("GAC_SMALL_SERVER", "1")
+    if idle_us:
+        monkeypatch.setenv("GAC_SMALL_SERVER_IDLE_US", idle_us)
+    tg, qg, ca = synth.small_case(seed=23, n_chains=200, max_blocks=400, n_frac=0.05)
+    e, cs = _setup(None, tg, qg, ca)
+    orc = _oracle(tg, qg)
+    R = _ranges(ca, np.random.default_rng(23), per_chain=3)
+    og, ol, oa = orc.score_ranges(ca, R)
+    tix = np.array([e.seq_index(GAC_T, x) for x in ca.tname], np.int32)
+    qix = np.array([e.seq_index(GAC_Q, x) for x in ca.qname], np.int32)
+    arrs = (tix, qix, ca.qstrand, ca.blk_off, ca.blk_t, ca.blk_q, ca.blk_size)
+    g, l, a = _score_chunked(e, cs, R, True)
+    assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
+    for i in range(0, len(R), 50):
+        sl = slice(i, i + 50)
+        for fn in (lambda r: e.score_ranges(cs, r, want_local=True),
+                   lambda r: e.score_ranges_host(*arrs, r, want_local=True)):
+            g, l, a = fn(R[sl])
+            assert np.array_equal(g, og[sl]) and np.array_equal(l, ol[sl])
+            assert np.array_equal(a, oa[sl])
+            if idle_us and i % 200 == 0:
+                time.sleep(0.002)
+    g, _, a = _score_chunked(e, cs, R, False)
+    assert np.array_equal(g, og) and np.array_equal(a, oa)
+    g, l, a = e.score_ranges(cs, R, want_local=True)  # (parks the grid)
+    assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
+    g, l, a = e.score_ranges_host(*arrs, R[:256], want_local=True)
+    assert np.array_equal(g, og[:256]) and np.array_equal(l, ol[:256])
+    cs2 = e.upload_chain_arrays(*arrs)
+    cs.close()
+    g, l, a = _score_chunked(e, cs2, R, True)
+    assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
+    cs2.close()
+    e.close()
+
+
 def test_unfused_tile_map_path(monkeypatch):
     """Batches of more than 1 M ranges scan the plan-workgroup totals in a
     separate one-workgroup launch (k_scan_agg + k_tilemap); smaller ones fold

@@ -171,13 +171,14 @@ def _cleaner_outputs(opts):
     return files
 
 
-def _run_cleaner(case, tmp_path, net):
+def _run_cleaner(case, tmp_path, net, env=None):
     d = os.path.join(GOLDEN, "cleaner")
     opts = _cleaner_cases()["cases"][case]
     p = lambda x: os.path.join(d, x)
     cmd = [_bin("chainCleaner"), p("in.chain"), p("t.2bit"), p("q.2bit"), "out.chain", "out.bed"]
     cmd += [f"-net={p('in.net')}"] if net else [f"-tSizes={p('t.sizes')}", f"-qSizes={p('q.sizes')}"]
-    r = subprocess.run(cmd + opts, capture_output=True, text=True, timeout=600, cwd=tmp_path)
+    r = subprocess.run(cmd + opts, capture_output=True, text=True, timeout=600, cwd=tmp_path,
+                       env=dict(os.environ, **(env or {})))
     assert r.returncode == 0, r.stderr
     for f in _cleaner_outputs(opts):
         assert filecmp.cmp(tmp_path / f, os.path.join(d, case, f), shallow=False), (case, f)
@@ -187,6 +188,13 @@ def _run_cleaner(case, tmp_path, net):
 def test_chaincleaner_net(case, tmp_path):
     """chainCleaner -net=in.net: every output byte-identical to the reference."""
     _run_cleaner(case, tmp_path, net=True)
+
+
+@pytest.mark.parametrize("case", ["default", "pairs", "debug"])
+def test_chaincleaner_net_server(case, tmp_path):
+    """The same with the small-batch server (GAC_SMALL_SERVER=1: the replay
+    loop's on-demand batches go to a resident grid through a mailbox)."""
+    _run_cleaner(case, tmp_path, net=True, env={"GAC_SMALL_SERVER": "1"})
 
 
 @pytest.mark.parametrize("case", ["default", "lowfold"])
