@@ -36,7 +36,7 @@ hipError_t launch_small_host(const ScoreArgs &a, const RangeDesc *hin, const int
 hipError_t launch_small_server(const ScoreArgs &a0, const ScoreArgs &a1, const Range *rin,
                                const RangeDesc *hin, const int4 *pool, SmallOut *out,
                                SmallMail *mail, SmallSync *sy, uint32_t last_done, uint64_t idle,
-                               hipStream_t s);
+                               uint32_t trace, int wgs, hipStream_t s);
 struct SeqDev {
     int64_t byte_off;
     int64_t word_off;
@@ -146,7 +146,8 @@ constexpr size_t kStatusBytes = 128;  // status[0..8)
 #define CTX_LOCK(c) CtxLock ctx_lock_((c), true)
 #define CTX_LOCK_SMALL(c) CtxLock ctx_lock_((c), false)
 
-// the resident small-batch server of a context (GAC_SMALL_SERVER=1)
+// the resident small-batch server of a context (default; GAC_SMALL_SERVER=0
+// launches k_small per batch instead)
 struct SmallServer {
     bool on = false;       // enabled for this context
     bool running = false;  // a grid is resident (or exiting: mail->state 2)
@@ -165,6 +166,8 @@ struct SmallServer {
     ScoreArgs a0, a1;                  // the resident grid's arguments
     uint64_t idle = 2000000;           // exit after 20 ms without a request (100 MHz ticks)
     int64_t launches = 0, requests = 0;
+    unsigned in_fl = 0;  // hipHostMalloc flags of the inputs
+    int wgs = 16;        // workgroups of the grid (GAC_SRV_WGS, 1..kSrvWaves/4)
 };
 
 struct gac_ctx {
@@ -379,7 +382,12 @@ extern "C" int gac_open(int device, gac_ctx **out) {
         const int m = atoi(v);
         c->small_max = m < 0 ? 0 : (m > kSmallMax ? kSmallMax : m);
     }
-    if (const char *v = getenv("GAC_SMALL_SERVER")) c->srv.on = v[0] == '1';
+    c->srv.on = true;  // (GAC_SMALL_SERVER=0: a launch per small batch)
+    if (const char *v = getenv("GAC_SMALL_SERVER")) c->srv.on = v[0] != '0';
+    if (const char *v = getenv("GAC_SRV_WGS")) {
+        const int w = atoi(v);
+        if (w >= 1 && w <= kSrvWaves / kWavesPerWG) c->srv.wgs = w;
+    }
     if (const char *v = getenv("GAC_SMALL_SERVER_IDLE_US")) {
         const long long us = atoll(v);
         if (us > 0 && us <= 10000000) c->srv.idle = (uint64_t)us * 100;
@@ -408,6 +416,21 @@ extern "C" void gac_close(gac_ctx *c) {
     {
         std::lock_guard<std::recursive_mutex> g(c->mu);
         srv_park(c);
+        if (c->srv.launches && getenv("GAC_TIMING"))
+            fprintf(stderr, "[gac_close] small-batch server: %lld requests, %lld launches\n",
+                    (long long)c->srv.requests, (long long)c->srv.launches);
+        if (c->srv.d_sync && getenv("GAC_SRV_TRACE")) {  // (the last grid's phase sums)
+            SmallSync t;
+            if (hipMemcpy(&t, c->srv.d_sync, sizeof(t), hipMemcpyDeviceToHost) == hipSuccess &&
+                t.pad[15])
+                fprintf(stderr, "[gac_close] server phases (us after the poll saw the request, "
+                                "mean of %u): broadcast %.2f, all saw %.2f, "
+                                "work %.2f, fenced %.2f, done %.2f; polls %.1f\n",
+                        t.pad[15], 0.01 * t.pad[8] / t.pad[15], 0.01 * t.pad[9] / t.pad[15],
+                        0.01 * t.pad[11] / t.pad[15],
+                        0.01 * t.pad[12] / t.pad[15], 0.01 * t.pad[13] / t.pad[15],
+                        (double)t.pad[14] / t.pad[15]);
+        }
         srv_free(c);
     }
     hipStreamSynchronize(c->stream);
@@ -1958,7 +1981,10 @@ static int score_device_split(gac_ctx *c, const ScoreArgs &a_base, const Range *
 // mailbox round trip instead of a launch and a stream synchronisation.  Only
 // the small-batch entry points keep it running; every other entry point parks
 // it first (CTX_LOCK), and the grid exits by itself after `idle` without a
-// request.  Opt-in: GAC_SMALL_SERVER=1.
+// request.  On by default (GAC_SMALL_SERVER=0: a k_small launch per batch):
+// 16.5 vs 23.6 us per 20-range call of an uploaded set, 23.4 vs 30.6 for
+// host-held chains, chainCleaner's C3 loop 0.19 vs 0.27 s in its 10 k calls
+// (r05lat6).
 static void srv_park(gac_ctx *c) {
     SmallServer &v = c->srv;
     if (!v.running) return;
@@ -1977,26 +2003,35 @@ static void srv_free(gac_ctx *c) {
     if (v.st) hipStreamDestroy(v.st);
     const bool on = v.on;
     const uint64_t idle = v.idle;
+    const int wgs = v.wgs;
     v = SmallServer();
     v.on = on;
     v.idle = idle;
+    v.wgs = wgs;
 }
 
 static int srv_alloc(gac_ctx *c) {
     SmallServer &v = c->srv;
     if (v.mail) return GAC_OK;
     const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    // the inputs: coherent (uncached on the device) or, GAC_SRV_INPUT=nc,
+    // cached and invalidated by each workgroup's acquire fence per request
+    const char *iv = getenv("GAC_SRV_INPUT");
+    const unsigned fin = iv && strcmp(iv, "nc") == 0 ? (unsigned)hipHostMallocMapped : fl;
+    v.in_fl = fin;
     HIPCHK(hipStreamCreateWithFlags(&v.st, hipStreamNonBlocking));
     HIPCHK(hipHostMalloc((void **)&v.mail, sizeof(SmallMail), fl));
     memset(v.mail, 0, sizeof(SmallMail));
     HIPCHK(hipHostGetDevicePointer((void **)&v.d_mail, v.mail, 0));
-    HIPCHK(hipHostMalloc((void **)&v.h_in, kSmallMax * sizeof(Range), fl));
+    HIPCHK(hipHostMalloc((void **)&v.h_in, kSmallMax * sizeof(Range), fin));
     HIPCHK(hipHostGetDevicePointer((void **)&v.d_in, v.h_in, 0));
-    HIPCHK(hipHostMalloc((void **)&v.h_hq, kSmallMax * sizeof(RangeDesc), fl));
+    HIPCHK(hipHostMalloc((void **)&v.h_hq, kSmallMax * sizeof(RangeDesc), fin));
     HIPCHK(hipHostGetDevicePointer((void **)&v.d_hq, v.h_hq, 0));
     HIPCHK(hipHostMalloc((void **)&v.h_out, kSmallMax * sizeof(SmallOut), fl));
     HIPCHK(hipHostGetDevicePointer((void **)&v.d_out, v.h_out, 0));
-    HIPCHK(hipMalloc((void **)&v.d_sync, sizeof(SmallSync)));
+    // uncached device memory: the broadcast word and the count are polled
+    // by workgroups on every XCD, whose L2s are not coherent with each other
+    HIPCHK(hipExtMallocWithFlags((void **)&v.d_sync, sizeof(SmallSync), hipDeviceMallocUncached));
     v.seq = 0;
     return GAC_OK;
 }
@@ -2010,8 +2045,7 @@ static int srv_pool(gac_ctx *c, int64_t need) {
     v.h_pool = nullptr;
     v.pool_cap = 0;
     const int64_t cap = std::max<int64_t>(need + need / 2, 1 << 16);
-    HIPCHK(hipHostMalloc((void **)&v.h_pool, cap * sizeof(int4),
-                         hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostMalloc((void **)&v.h_pool, cap * sizeof(int4), v.in_fl));
     HIPCHK(hipHostGetDevicePointer((void **)&v.d_pool, v.h_pool, 0));
     v.pool_cap = cap;
     return GAC_OK;
@@ -2022,8 +2056,9 @@ static int srv_launch(gac_ctx *c) {
     HIPCHK(hipMemsetAsync(v.d_sync, 0, sizeof(SmallSync), v.st));
     __atomic_store_n(&v.mail->state, 1u, __ATOMIC_RELEASE);
     __atomic_store_n(&v.mail->done, v.seq, __ATOMIC_RELEASE);
+    static const uint32_t trace = getenv("GAC_SRV_TRACE") ? 1u : 0u;
     HIPCHK(launch_small_server(v.a0, v.a1, v.d_in, v.d_hq, v.d_pool, v.d_out, v.d_mail, v.d_sync,
-                               v.seq, v.idle, v.st));
+                               v.seq, v.idle, trace, v.wgs, v.st));
     v.running = true;
     ++v.launches;
     return GAC_OK;
@@ -2076,11 +2111,10 @@ static int srv_ensure(gac_ctx *c, const gac_chainset *cs, uint32_t flags) {
 // one request: inputs already in the mailbox buffers; waits for the results
 static int srv_call(gac_ctx *c, uint32_t kind, int64_t n) {
     SmallServer &v = c->srv;
-    __atomic_store_n(&v.mail->kind, kind, __ATOMIC_RELAXED);
-    __atomic_store_n(&v.mail->n, (uint32_t)n, __ATOMIC_RELAXED);
-    const uint32_t prev = v.seq;
-    uint32_t seq = prev + 1;  // (request numbers skip 0 and the exit word)
-    if (seq == 0 || seq == 0xffffffffu) seq = 1;
+    const uint32_t prev = v.seq;  // (the last request word; 20-bit numbers, never 0)
+    uint32_t num = ((prev & 0xfffffu) + 1) & 0xfffffu;
+    if (num == 0) num = 1;
+    const uint32_t seq = srv_word(num, kind, (uint32_t)n);
     v.seq = seq;
     __atomic_store_n(&v.mail->req, seq, __ATOMIC_RELEASE);
     ++v.requests;

@@ -188,21 +188,32 @@ constexpr int kSmallMax = 256;  // ranges per small-batch call
 // k_small_server's mailbox, in pinned coherent host memory: the host writes
 // kind, n and the inputs, then req; the server writes done, and state = 2
 // when it exits (idle or stop)
+// k_small_server's mailbox, in pinned coherent host memory: the host writes
+// kind, n and the inputs, then req; the server writes done, and state = 2
+// when it exits (idle or stop)
 struct SmallMail {
-    uint32_t req;    // host: the request number (written last)
-    uint32_t kind;   // 0: Range batch of the uploaded set; 1: host-planned RangeDesc + pool
-    uint32_t n;      // ranges (<= kSmallMax)
+    uint32_t req;    // host: the request word (written last, srv_word)
+    uint32_t kind;   // (unused)
+    uint32_t n;      // (unused)
     uint32_t stop;   // host: 1 = exit now
     uint32_t done;   // server: the last completed request
     uint32_t state;  // server: 2 = exited
     uint32_t pad[26];
 };
-// its device-side broadcast word and completion count (zeroed per launch)
+// its device-side copy for the other workgroups (the request number, kind
+// and range count, read from the mailbox by workgroup 0 only) and the
+// completion count: uncached device memory, zeroed per launch
 struct SmallSync {
-    uint32_t seq, cnt;
-    uint32_t pad[30];
+    uint32_t seq, kind, n, cnt;
+    uint32_t pad[28];  // (GAC_SRV_TRACE's phase words)
 };
-constexpr int kSrvWaves = 256;  // resident server waves (64 workgroups)
+constexpr int kSrvWaves = 256;  // resident server waves at most (64 workgroups)
+// the request word: bits 0-19 the request number (never 0), 20-28 the range
+// count (<= kSmallMax), 29 the kind (0: Range batch of the uploaded set; 1:
+// host-planned RangeDesc + pool); 0xffffffff (never a request) = exit
+__host__ __device__ constexpr uint32_t srv_word(uint32_t seq, uint32_t kind, uint32_t n) {
+    return (seq & 0xfffffu) | ((n & 0x1ffu) << 20) | ((kind & 1u) << 29);
+}
 
 // One run of a sparse genome upload (bytes): its place in the staging layout
 // (8-byte aligned), its offset in the packed upload (8-byte aligned), length.

@@ -1867,24 +1867,31 @@ __global__ void __launch_bounds__(256) k_small(ScoreArgs a, const Range *rin, co
 // ------------------------------------------------------ k_small_server ----
 // The small batches of a long run of on-demand calls (chainCleaner's replay
 // loop) without a launch per call: a resident grid of kSrvWaves waves takes
-// requests from a mailbox in pinned, coherent host memory (SmallMail).  Wave 0
-// polls the mailbox (system-scope loads, s_sleep between them) and
-// broadcasts a new request number through device memory (SmallSync.seq);
-// every wave scores ranges w, w + kSrvWaves, ... of it (k_small's body, the
-// request's kind selecting the uploaded set's ranges or host-planned
-// descriptors), makes its results visible to the host and counts itself in
-// SmallSync.cnt; the last wave publishes the request number in mail->done.
-// Every wave reaches the exit: wave 0 broadcasts kSrvExit when the host sets
-// mail->stop or no request arrives within `idle` ticks of the 100 MHz
-// real-time counter, and then marks the mailbox exited (state 2); the host
-// re-launches the grid for a request that finds it gone.
+// requests from a mailbox in pinned, coherent host memory (SmallMail).  One
+// lane of workgroup 0 polls the mailbox's request word (number, kind and
+// range count in 32 bits: srv_word; relaxed system-scope loads, s_sleep
+// between polls) and copies it to uncached device memory (SmallSync: the
+// XCDs' L2s are not coherent with each other, so a cached word could stay
+// stale in another XCD's L2); one lane of every other workgroup polls that copy
+// (relaxed, then one acquire fence) while its waves wait at a barrier.  Wave
+// w scores ranges w, w + kSrvWaves, ... (k_small's body; the kind selects the
+// uploaded set's ranges or host-planned descriptors).  A workgroup that wrote
+// results makes them visible to the host (one system-scope release) before
+// it counts itself in SmallSync.cnt; the last workgroup publishes the
+// request word in mail->done.  Measured (GAC_SRV_TRACE, r05lat2/5): every
+// workgroup reading the mailbox's kind and count from host memory cost ~38
+// us per request, one reader ~1.8 us; polling with acquire loads (a cache
+// invalidation per poll) or a cached copy was slower still.  (A 64-bit
+// request word hung the grid in r05lat3/4; the 32-bit words are what was
+// measured to work.)  Every wave reaches the exit: workgroup
+// 0 broadcasts kSrvExit when the host sets mail->stop or no request arrives
+// within `idle` ticks of the 100 MHz real-time counter, then marks the
+// mailbox exited (state 2); the host re-launches the grid for a request that
+// finds it gone.
 constexpr uint32_t kSrvExit = 0xffffffffu;
 
-__device__ __forceinline__ uint32_t sys_load(const uint32_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void sys_store(uint32_t *p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+__device__ __forceinline__ uint32_t sys_relaxed(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <bool LOCAL, bool SYM>
@@ -1892,60 +1899,95 @@ __global__ void __launch_bounds__(256) k_small_server(ScoreArgs a0, ScoreArgs a1
                                                       const RangeDesc *hin, const int4 *pool,
                                                       SmallOut *out, SmallMail *mail,
                                                       SmallSync *sy, uint32_t last_done,
-                                                      uint64_t idle) {
+                                                      uint64_t idle, uint32_t trace) {
+    __shared__ uint32_t s_req[3];
     const int lane = threadIdx.x & 63;
-    const int wave = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    const int nw = (int)(((int64_t)gridDim.x * blockDim.x) >> 6);
+    const int wave = (int)(blockIdx.x * kWavesPerWG + (threadIdx.x >> 6));
+    const int nw = (int)(gridDim.x * kWavesPerWG);
     uint32_t cur = last_done;
     for (;;) {
-        uint32_t s;
-        if (wave == 0) {
-            uint64_t t0 = wall_clock64();
-            for (;;) {
-                const uint32_t r = sys_load(&mail->req);
-                if (sys_load(&mail->stop)) {
-                    s = kSrvExit;
-                    break;
+        if (threadIdx.x == 0) {
+            uint32_t s, kind = 0, n = 0;
+            if (blockIdx.x == 0) {
+                const uint64_t t0 = wall_clock64();
+                uint32_t polls = 0;
+                for (;;) {
+                    ++polls;
+                    const uint32_t r = sys_relaxed(&mail->req);
+                    if (sys_relaxed(&mail->stop)) {
+                        s = kSrvExit;
+                        break;
+                    }
+                    if (r != cur) {
+                        s = r;
+                        break;
+                    }
+                    if (wall_clock64() - t0 > (long long)idle) {
+                        s = kSrvExit;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
                 }
-                if (r != cur) {
-                    s = r;
-                    break;
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                if (trace) {  // (GAC_SRV_TRACE: 10-ns ticks of the request's phases)
+                    sy->pad[0] = (uint32_t)wall_clock64();
+                    sy->pad[6] = polls;
                 }
-                if (wall_clock64() - t0 > idle) {
-                    s = kSrvExit;
-                    break;
+                __hip_atomic_store(&sy->seq, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                if (trace) sy->pad[1] = (uint32_t)wall_clock64();
+            } else {
+                for (;;) {  // (0: the launch's zeroed word, never a request word)
+                    s = __hip_atomic_load(&sy->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (s != cur && s != 0) break;
+                    __builtin_amdgcn_s_sleep(2);
                 }
-                __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // (inputs in host memory)
             }
-            __hip_atomic_store(&sy->seq, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            for (;;) {  // (0: the launch's zeroed word, never a request number)
-                s = __hip_atomic_load(&sy->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                if (s != cur && s != 0) break;
-                __builtin_amdgcn_s_sleep(2);
+            if (s != kSrvExit) {
+                kind = (s >> 29) & 1u;
+                n = (s >> 20) & 0x1ffu;
             }
+            s_req[0] = s;
+            s_req[1] = kind;
+            s_req[2] = n;
         }
+        __syncthreads();
+        const uint32_t s = s_req[0], kind = s_req[1], n = s_req[2];
         if (s == kSrvExit) break;
-        const uint32_t kind = sys_load(&mail->kind), n = sys_load(&mail->n);
+        if (trace && threadIdx.x == 0)
+            atomicMax(&sy->pad[2], (uint32_t)wall_clock64() - sy->pad[0]);
         for (int64_t w = wave; w < (int64_t)n; w += nw) {
             if (kind) small_range<LOCAL, SYM, true>(a1, nullptr, hin, pool, out, w, lane);
             else small_range<LOCAL, SYM, false>(a0, rin, nullptr, nullptr, out, w, lane);
         }
-        __threadfence_system();  // this wave's results, before it is counted
-        uint32_t old = 0;
-        if (lane == 0)
-            old = __hip_atomic_fetch_add(&sy->cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        old = __shfl(old, 0, 64);
-        if (old == (uint32_t)nw - 1) {  // the last wave: reset the count, publish
-            if (lane == 0) {
+        __syncthreads();  // (the workgroup's results are stored; s_req may be rewritten)
+        if (threadIdx.x == 0) {
+            if (trace) atomicMax(&sy->pad[4], (uint32_t)wall_clock64() - sy->pad[0]);
+            if ((int64_t)blockIdx.x * kWavesPerWG < (int64_t)n)
+                __threadfence_system();  // its results, before it is counted
+            if (trace) atomicMax(&sy->pad[5], (uint32_t)wall_clock64() - sy->pad[0]);
+            const uint32_t old =
+                __hip_atomic_fetch_add(&sy->cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (old == gridDim.x - 1) {  // the last workgroup: reset the count, publish
                 __hip_atomic_store(&sy->cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __threadfence_system();
-                sys_store(&mail->done, s);
+                __hip_atomic_store(&mail->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (trace) {  // per-request sums of the phase ends, then reset
+                    const uint32_t t = (uint32_t)wall_clock64() - sy->pad[0];
+                    atomicAdd(&sy->pad[8], sy->pad[1] - sy->pad[0]);
+                    atomicAdd(&sy->pad[9], sy->pad[2]);
+                    atomicAdd(&sy->pad[11], sy->pad[4]);
+                    atomicAdd(&sy->pad[12], sy->pad[5]);
+                    atomicAdd(&sy->pad[13], t);
+                    atomicAdd(&sy->pad[14], sy->pad[6]);
+                    atomicAdd(&sy->pad[15], 1u);
+                    sy->pad[2] = sy->pad[4] = sy->pad[5] = 0;
+                }
             }
         }
         cur = s;
     }
-    if (wave == 0 && lane == 0) sys_store(&mail->state, 2u);
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(&mail->state, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ------------------------------------------------------------ genome -----
@@ -2243,14 +2285,14 @@ hipError_t launch_small_host(const ScoreArgs &a, const RangeDesc *hin, const int
 hipError_t launch_small_server(const ScoreArgs &a0, const ScoreArgs &a1, const Range *rin,
                                const RangeDesc *hin, const int4 *pool, SmallOut *out,
                                SmallMail *mail, SmallSync *sy, uint32_t last_done, uint64_t idle,
-                               hipStream_t s) {
-    const dim3 g(kSrvWaves / kWavesPerWG), b(256);
+                               uint32_t trace, int wgs, hipStream_t s) {
+    const dim3 g((unsigned)wgs), b(256);
     if (a0.want_local) {
-        if (a0.sym) k_small_server<true, true><<<g, b, 0, s>>>(a0, a1, rin, hin, pool, out, mail, sy, last_done, idle);
-        else k_small_server<true, false><<<g, b, 0, s>>>(a0, a1, rin, hin, pool, out, mail, sy, last_done, idle);
+        if (a0.sym) k_small_server<true, true><<<g, b, 0, s>>>(a0, a1, rin, hin, pool, out, mail, sy, last_done, idle, trace);
+        else k_small_server<true, false><<<g, b, 0, s>>>(a0, a1, rin, hin, pool, out, mail, sy, last_done, idle, trace);
     } else {
-        if (a0.sym) k_small_server<false, true><<<g, b, 0, s>>>(a0, a1, rin, hin, pool, out, mail, sy, last_done, idle);
-        else k_small_server<false, false><<<g, b, 0, s>>>(a0, a1, rin, hin, pool, out, mail, sy, last_done, idle);
+        if (a0.sym) k_small_server<false, true><<<g, b, 0, s>>>(a0, a1, rin, hin, pool, out, mail, sy, last_done, idle, trace);
+        else k_small_server<false, false><<<g, b, 0, s>>>(a0, a1, rin, hin, pool, out, mail, sy, last_done, idle, trace);
     }
     return hipGetLastError();
 }

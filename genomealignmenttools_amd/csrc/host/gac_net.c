@@ -172,6 +172,11 @@ struct gac_net {
     /* pre-order fill index per side */
     nfill **order[2];
     int64_t n_order[2];
+    /* per side, by pre-order position: the parent fill's position (-1 at
+     * top level), filled by the first pass that chases the parent links
+     * (gac_net_get_fills with flags) and read by the output's "reached" pass */
+    int64_t *pord[2];
+    int pord_ok[2];
     int sides; /* bit 1 << side: side netted */
     atomic_int free_next; /* gac_net_free's worker cursor */
 };
@@ -996,6 +1001,8 @@ void gac_net_free(gac_net *n) {
     free(n->chroms[1]);
     free(n->order[0]);
     free(n->order[1]);
+    free(n->pord[0]);
+    free(n->pord[1]);
     free(n->chain_ali);
     free(n);
 }
@@ -1912,6 +1919,12 @@ static void *fills_thread(void *arg) {
 }
 
 static int64_t next_top_level(const gac_net *n, int side, int64_t i) {
+    if (n->pord_ok[side]) {
+        const int64_t *po = n->pord[side];
+        while (i < n->n_order[side] && po[i] >= 0)
+            ++i;
+        return i;
+    }
     while (i < n->n_order[side] && n->order[side][i]->pgap->pfill)
         ++i;
     return i;
@@ -1928,8 +1941,11 @@ static void *visible_thread(void *arg) {
             break;
         const int64_t a = next_top_level(n, side, r * J->per);
         const int64_t b = next_top_level(n, side, (r + 1) * J->per < nf ? (r + 1) * J->per : nf);
+        int64_t *po = n->pord[side];
         for (int64_t i = a; i < b; ++i) {
             const nfill *pf = n->order[side][i]->pgap->pfill;
+            if (po)
+                po[i] = pf ? pf->ord : -1;
             const int sz = J->ali ? J->ali[i] : 0;
             if ((!pf || (J->flags[pf->ord] & 2)) && sz >= n->opt.min_fill)
                 J->flags[i] |= 2;
@@ -1956,8 +1972,14 @@ int gac_net_get_fills(const gac_net *n, int side, int32_t *chain, int32_t *start
      * >= min_fill -- one pass in pre-order (parents precede children), in
      * parallel over runs that start at top-level fills (whole subtrees) */
     if (flags) {
+        /* (the parent positions are kept for the output's pass; the net is
+         * const to callers, this is a cache) */
+        gac_net *nm = (gac_net *)n;
+        if (!nm->pord[side])
+            nm->pord[side] = malloc((size_t)(nf ? nf : 1) * sizeof(int64_t));
         atomic_store(&J.next, 0);
         gac_run_threads(nt < nrun ? nt : (int)(nrun ? nrun : 1), visible_thread, &J);
+        nm->pord_ok[side] = 1;
     }
     gac_mark("get_fills: done");
     return GAC_OK;
@@ -2330,6 +2352,12 @@ static void *wreached_thread(void *arg) {
             return NULL;
         const int64_t a = next_top_level(J->n, J->side, r * per);
         const int64_t b = next_top_level(J->n, J->side, (r + 1) * per < J->nf ? (r + 1) * per : J->nf);
+        const int64_t *po = J->n->pord_ok[J->side] ? J->n->pord[J->side] : NULL;
+        if (po) {
+            for (int64_t i = a; i < b; ++i)
+                J->reached[i] = J->show[i] && (po[i] < 0 || J->reached[po[i]]);
+            continue;
+        }
         for (int64_t i = a; i < b; ++i) {
             const nfill *pf = J->ord[i]->pgap->pfill;
             J->reached[i] = J->show[i] && (!pf || J->reached[pf->ord]);

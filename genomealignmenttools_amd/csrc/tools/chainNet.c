@@ -679,9 +679,11 @@ int main(int argc, char *argv[]) {
             gt_stage("GPU fill rescoring");
             for (int64_t k = 0; k < nr; ++k)
                 tscores[rix[k]] = g[k];
-            free(g);
-            free(ali);
+            gac_mark("scores placed");
+            gt_free_late(g, (size_t)nr * 8);
+            gt_free_late(ali, (size_t)nr * 4);
             gt_device_close_async(&dev, ctx, pu.cs); /* overlaps writing the nets */
+            gac_mark("device close queued");
             pu.cs = NULL;
         } else if (nr) {
             if (pu.cs) {
@@ -762,15 +764,19 @@ int main(int argc, char *argv[]) {
             if (ctx)
                 gac_close(ctx);
         }
-        free(fc);
-        free(fs);
-        free(fe);
-        free(fl);
-        free(fa);
-        free(fw0);
-        free(fwn);
-        free(r);
-        free(rix);
+        /* (13 M-entry arrays: unmapping them here cost the target net's
+         * start tens of ms; their pages go after the nets are written) */
+        const size_t nfb = (size_t)(nf ? nf : 1);
+        gt_free_late(fc, nfb * 4);
+        gt_free_late(fs, nfb * 4);
+        gt_free_late(fe, nfb * 4);
+        gt_free_late(fl, nfb);
+        gt_free_late(fa, nfb * 4);
+        gt_free_late(fw0, nfb * 4);
+        gt_free_late(fwn, nfb * 4);
+        gt_free_late(r, nfb * sizeof(gac_window));
+        gt_free_late(rix, nfb * 8);
+        gac_mark("fill arrays released");
     }
     wo[0].tscores = tscores;
     write_net(&wo[0]);
@@ -795,6 +801,7 @@ int main(int argc, char *argv[]) {
      * they are freed on one core after the output is complete. */
     gac_net_free(net);
     gt_chains_drop_pages(&c);
+    gt_free_late_all();
     gt_stage("free nets and chains");
     gt_exit_ok();
 }

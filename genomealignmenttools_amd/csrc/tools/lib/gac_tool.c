@@ -623,6 +623,34 @@ void gt_chains_drop_pages(gt_chains *c) {
     gac_run_threads(J.n, drop_thread, &J);
 }
 
+static drop_job g_late;
+static int g_late_on = -1;
+
+void gt_free_late(void *p, size_t bytes) {
+    if (!p)
+        return;
+    if (g_late_on < 0) {
+        const char *e = getenv("GAC_LATE_FREE");
+        g_late_on = !(e && *e == '0');
+    }
+    if (!g_late_on || g_late.n == 16) {
+        free(p);
+        return;
+    }
+    g_late.p[g_late.n] = p;
+    g_late.len[g_late.n++] = bytes;
+}
+
+void gt_free_late_all(void) {
+    if (!g_late.n)
+        return;
+    atomic_init(&g_late.next, 0);
+    gac_run_threads(g_late.n, drop_thread, &g_late);
+    for (int k = 0; k < g_late.n; ++k)
+        free(g_late.p[k]);
+    g_late.n = 0;
+}
+
 void gt_exit_ok(void) {
     join_live_device();
     if (atomic_load(&g_aborting)) /* a helper is aborting: its exit status wins */

@@ -221,6 +221,12 @@ typedef struct gt_chains {
  * (madvise under the mm's read lock; the kernel's exit would free them on
  * one core).  The set must not be used afterwards. */
 void gt_chains_drop_pages(gt_chains *c);
+/* large temporary arrays released later, off the critical path: with
+ * GAC_LATE_FREE=1 (default) gt_free_late keeps them until gt_free_late_all,
+ * which drops their pages on all threads (madvise, read lock) and frees
+ * them; otherwise gt_free_late frees at once */
+void gt_free_late(void *p, size_t bytes);
+void gt_free_late_all(void);
 
 /* stop_below: stop after reading the first chain whose score is < stop_below
  * (that chain is read, like chainNet's loop, but not kept); pass -HUGE_VAL

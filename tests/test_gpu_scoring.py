@@ -548,11 +548,11 @@ def test_small_batches_vs_oracle(case):
     assert np.array_equal(g3, og) and np.array_equal(l3, ol) and np.array_equal(a3, oa)
 
 
-@pytest.mark.parametrize("idle_us", [None, "300"])
-def test_small_batch_server(monkeypatch, idle_us):
-    """GAC_SMALL_SERVER=1: small batches go to a resident grid
-    (k_small_server) through a mailbox in pinned host memory instead of a
-    launch each.  Requests of both kinds (ranges of an uploaded set, ranges of
+@pytest.mark.parametrize("server,idle_us", [("1", None), ("1", "300"), ("0", None)])
+def test_small_batch_server(monkeypatch, server, idle_us):
+    """Small batches go to a resident grid (k_small_server, the default)
+    through a mailbox in pinned host memory instead of a launch each
+    (GAC_SMALL_SERVER=0: a k_small launch each, checked the same way).  Requests of both kinds (ranges of an uploaded set, ranges of
     chains in host memory) interleaved, the local score switched off and on
     (a new grid), a large batch in between (the grid parked), a freed set, and
     -- with a 300 us idle limit and sleeps between calls -- grids that exit
@@ -561,7 +561,7 @@ def test_small_batch_server(monkeypatch, idle_us):
     import time
     from genomealignmenttools_amd import synth
     from genomealignmenttools_amd.gachain import GAC_Q, GAC_T
-    monkeypatch.setenv("GAC_SMALL_SERVER", "1")
+    monkeypatch.setenv("GAC_SMALL_SERVER", server)
     if idle_us:
         monkeypatch.setenv("GAC_SMALL_SERVER_IDLE_US", idle_us)
     tg, qg, ca = synth.small_case(seed=23, n_chains=200, max_blocks=400, n_frac=0.05)

@@ -191,10 +191,10 @@ def test_chaincleaner_net(case, tmp_path):
 
 
 @pytest.mark.parametrize("case", ["default", "pairs", "debug"])
-def test_chaincleaner_net_server(case, tmp_path):
-    """The same with the small-batch server (GAC_SMALL_SERVER=1: the replay
-    loop's on-demand batches go to a resident grid through a mailbox)."""
-    _run_cleaner(case, tmp_path, net=True, env={"GAC_SMALL_SERVER": "1"})
+def test_chaincleaner_net_launches(case, tmp_path):
+    """The same with a k_small launch per on-demand batch (GAC_SMALL_SERVER=0)
+    instead of the default resident small-batch server."""
+    _run_cleaner(case, tmp_path, net=True, env={"GAC_SMALL_SERVER": "0"})
 
 
 @pytest.mark.parametrize("case", ["default", "lowfold"])
