@@ -17,7 +17,7 @@ OBJDIR   := build/obj
 ARCH     := gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
             -Iinclude -I$(CSRC) -Wall -Wno-unused-result -Wno-unused-value $(HIPEXTRA)
-CFLAGS   := -O2 -std=gnu11 -fPIC -Wall -ffp-contract=off -Iinclude -I$(CSRC)
+CFLAGS   := -O2 -mpopcnt -std=gnu11 -fPIC -Wall -ffp-contract=off -Iinclude -I$(CSRC)
 
 HOST_SRC := $(wildcard $(CSRC)/host/*.c)
 HOST_OBJ := $(patsubst $(CSRC)/host/%.c,$(OBJDIR)/host/%.o,$(HOST_SRC))
@@ -118,7 +118,7 @@ cpu-axtchain: oracle/_build/axtChain_cpu
 oracle/_build/axtChain_cpu: $(CSRC)/tools/axtChain.c $(CSRC)/host/gac_axtchain.c \
 		$(CSRC)/host/gac_host.c oracle/cpu_gac_stub.c $(TOOL_LIB_SRC)
 	@mkdir -p oracle/_build
-	$(CC) -O2 -g -std=gnu11 -Wall -ffp-contract=off -Iinclude -I$(CSRC) -I$(CSRC)/host -I$(CSRC)/tools/lib $^ \
+	$(CC) -O2 -g -mpopcnt -std=gnu11 -Wall -ffp-contract=off -Iinclude -I$(CSRC) -I$(CSRC)/host -I$(CSRC)/tools/lib $^ \
 	    -o $@ -lz -lm -lpthread $(CPU_EXTRA)
 
 # chainNet -rescore on the same stand-in: the sparse genome upload's word
@@ -128,7 +128,7 @@ cpu-chainnet: oracle/_build/chainNet_cpu
 oracle/_build/chainNet_cpu: $(CSRC)/tools/chainNet.c $(CSRC)/host/gac_net.c \
 		$(CSRC)/host/gac_host.c oracle/cpu_gac_stub.c $(TOOL_LIB_SRC)
 	@mkdir -p oracle/_build
-	$(CC) -O2 -g -std=gnu11 -Wall -ffp-contract=off -Iinclude -I$(CSRC) -I$(CSRC)/host -I$(CSRC)/tools/lib $^ \
+	$(CC) -O2 -g -mpopcnt -std=gnu11 -Wall -ffp-contract=off -Iinclude -I$(CSRC) -I$(CSRC)/host -I$(CSRC)/tools/lib $^ \
 	    -o $@ -lz -lm -lpthread $(CPU_EXTRA)
 
 .PHONY: cpu-axtchain cpu-chainnet
