@@ -195,7 +195,38 @@ def init_ranks(args):
 
 def host_threads():
     v = os.environ.get("GAC_THREADS") or os.environ.get("OMP_NUM_THREADS")
-    return int(v) if v else len(os.sched_getaffinity(0))
+    return int(v) if v else usable_cpus()
+
+
+def usable_cpus(cpu_max="/sys/fs/cgroup/cpu.max"):
+    """The CPUs this process may use: its affinity mask narrowed by its
+    cgroup's CPU quota (gac_host_cpus in csrc/host/gac_host.c, the same rule)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open(cpu_max) as f:
+            q, per = f.read().split()[:2]
+        if q != "max" and int(q) > 0 and int(per) > 0:
+            n = min(n, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def rank_tool_threads(world, env, cpus):
+    """GAC_THREADS for the tool each of `world` ranks runs (N > 1): the
+    caller's GAC_THREADS / OMP_NUM_THREADS wins, except torch.distributed.run's
+    own default OMP_NUM_THREADS=1 (it sets it for every worker when the
+    launching environment has none; TORCHELASTIC_RUN_ID marks its workers),
+    which would run each rank's netting and parsing on one thread.  Else the
+    usable CPUs shared by the node's ranks: N ranks x all cores would
+    oversubscribe the host.  {} = leave the environment as it is."""
+    if world <= 1 or env.get("GAC_THREADS"):
+        return {}
+    omp = env.get("OMP_NUM_THREADS")
+    if omp and not (omp == "1" and env.get("TORCHELASTIC_RUN_ID")):
+        return {}
+    local_world = int(env.get("LOCAL_WORLD_SIZE", world))
+    return {"GAC_THREADS": str(max(1, cpus // local_world))}
 
 
 def host_cpu():
@@ -1172,13 +1203,10 @@ def main():
     run_id = f"{os.environ.get('TORCHELASTIC_RUN_ID', 'x')}-{os.environ.get('MASTER_PORT', '0')}"
     step_no = [0]
 
-    # host threads per rank: the launcher's GAC_THREADS / OMP_NUM_THREADS, else
-    # this process's cores shared by the node's ranks (N ranks x all cores
-    # would oversubscribe the host)
-    tool_threads = {}
-    if world > 1 and not (os.environ.get("GAC_THREADS") or os.environ.get("OMP_NUM_THREADS")):
-        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
-        tool_threads["GAC_THREADS"] = str(max(1, len(os.sched_getaffinity(0)) // local_world))
+    # host threads per rank (rank_tool_threads: the launcher's setting, not
+    # torch.distributed.run's OMP_NUM_THREADS=1 default, else this process's
+    # usable cores shared by the node's ranks)
+    tool_threads = rank_tool_threads(world, os.environ, usable_cpus())
 
     def step_env():
         step_no[0] += 1

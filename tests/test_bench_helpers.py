@@ -104,3 +104,25 @@ def test_full_parity_helper(tmp_path):
             assert len(res[k]["reference"]) == 64 and res[k]["same"] is False
         g = json.load(open(os.path.join(REPO, "tests", "golden", "fullscale", f"{which}.json")))
         assert g["info"]["seed"] in (7, 1234)
+
+
+def test_rank_tool_threads(tmp_path):
+    """N > 1: each rank's tool gets the node's usable CPUs shared by its
+    ranks -- also under torch.distributed.run's default OMP_NUM_THREADS=1,
+    which would otherwise run every rank's netting on one thread; a
+    launcher's own GAC_THREADS / OMP_NUM_THREADS is kept; the cgroup quota
+    narrows the CPU count."""
+    import bench
+    assert bench.rank_tool_threads(1, {}, 128) == {}
+    assert bench.rank_tool_threads(8, {}, 128) == {"GAC_THREADS": "16"}
+    tr = {"OMP_NUM_THREADS": "1", "TORCHELASTIC_RUN_ID": "x", "LOCAL_WORLD_SIZE": "4"}
+    assert bench.rank_tool_threads(8, tr, 128) == {"GAC_THREADS": "32"}
+    assert bench.rank_tool_threads(8, {"OMP_NUM_THREADS": "1"}, 128) == {}
+    assert bench.rank_tool_threads(8, {"OMP_NUM_THREADS": "12", "TORCHELASTIC_RUN_ID": "x"}, 128) == {}
+    assert bench.rank_tool_threads(8, {"GAC_THREADS": "3", **tr}, 128) == {}
+    assert bench.rank_tool_threads(8, {}, 4) == {"GAC_THREADS": "1"}
+    q = tmp_path / "cpu.max"
+    q.write_text("1600000 100000\n")
+    assert bench.usable_cpus(str(q)) == min(16, len(os.sched_getaffinity(0)))
+    q.write_text("max 100000\n")
+    assert bench.usable_cpus(str(q)) == len(os.sched_getaffinity(0))
