@@ -1673,41 +1673,123 @@ static int fast_block_line(lf *f, int *v, int *bw) {
     return 1;
 }
 
+/* A header line in the form chainWrite prints ("chain" and 11 or 12
+ * fields, one space apart, integer score of at most 15 digits, unsigned
+ * numbers of at most 9 digits, newline right after the last field) into
+ * chain c->n: 1 = parsed and the line consumed; 0 = anything else (the
+ * general lf_chop + need_num path reads it, with its messages). */
+static inline const char *fh_tok(const char *p, const char *end, const char **t, int *len) {
+    const char *q = p;
+    while (q < end && (unsigned char)*q > ' ')
+        ++q;
+    *t = p;
+    *len = (int)(q - p);
+    return q;
+}
+
+static inline const char *fh_num(const char *p, const char *end, int maxd, int64_t *v) {
+    int64_t x = 0;
+    const char *q = p;
+    while (q < end && (unsigned)(*q - '0') < 10u && q - p < maxd) {
+        x = x * 10 + (*q - '0');
+        ++q;
+    }
+    if (q == p || q >= end || (unsigned)(*q - '0') < 10u)
+        return NULL;
+    *v = x;
+    return q;
+}
+
+static int fast_header(lf *f, gt_chains *c) {
+    const char *p = f->cur, *end = f->end;
+    if (end - p < 32 || memcmp(p, "chain ", 6) != 0)
+        return 0;
+    p += 6;
+    int64_t num[13];
+    const char *tn = NULL, *qn = NULL;
+    int tl = 0, ql = 0, qminus = 0, nf = 1;
+    for (; nf < 13; ++nf) {
+        if (nf == 2 || nf == 4 || nf == 7 || nf == 9) { /* names and strands */
+            const char *t;
+            int len;
+            p = fh_tok(p, end, &t, &len);
+            if (len == 0)
+                return 0;
+            if (nf == 2)
+                tn = t, tl = len;
+            else if (nf == 7)
+                qn = t, ql = len;
+            else if (nf == 9)
+                qminus = t[0] == '-';
+        } else {
+            p = fh_num(p, end, nf == 1 ? 15 : 9, &num[nf]);
+            if (!p)
+                return 0;
+        }
+        if (p >= end)
+            return 0;
+        if (*p == '\n' && nf >= 11)
+            break;
+        if (*p != ' ')
+            return 0;
+        ++p;
+    }
+    if (nf == 13 || *p != '\n')
+        return 0;
+    const int64_t i = c->n;
+    c->score[i] = (double)num[1];
+    c->tname[i] = gt_names_add(&c->tnames, tn, (size_t)tl);
+    c->tsize[i] = (int)num[3];
+    c->id[i] = nf == 12 ? (int)num[12] : INT32_MIN; /* (chainIdNext later) */
+    c->tstart[i] = (int)num[5];
+    c->tend[i] = (int)num[6];
+    c->qname[i] = gt_names_add(&c->qnames, qn, (size_t)ql);
+    c->qsize[i] = (int)num[8];
+    c->qstrand[i] = (uint8_t)qminus;
+    c->qstart[i] = (int)num[10];
+    c->qend[i] = (int)num[11];
+    f->cur = (char *)p + 1;
+    ++f->line;
+    return 1;
+}
+
 /* parse one record; 0 = ok, 1 = end of chunk, -1 = error (f->msg) */
 static int parse_chain(chunk *k) {
     lf *f = &k->f;
     gt_chains *c = &k->c;
     char *row[13];
-    int wc = lf_chop(f, row, 13);
-    if (wc == 0)
-        return 1;
-    if (wc < 12)
-        LF_FAIL(f, "Expecting at least 12 words line \001 of \002");
-    if (strcmp(row[0], "chain") != 0)
-        LF_FAIL(f, "Expecting 'chain' line \001 of \002");
     chains_reserve(c);
     int64_t i = c->n;
-    int v;
-    c->score[i] = atof(row[1]);
-    c->tname[i] = gt_names_add(&c->tnames, row[2], strlen(row[2]));
-    if (need_num(f, row, 3, &v))
-        return -1;
-    c->tsize[i] = v;
-    if (wc >= 13) {
-        if (need_num(f, row, 12, &v))
+    if (!fast_header(f, c)) {
+        int wc = lf_chop(f, row, 13);
+        if (wc == 0)
+            return 1;
+        if (wc < 12)
+            LF_FAIL(f, "Expecting at least 12 words line \001 of \002");
+        if (strcmp(row[0], "chain") != 0)
+            LF_FAIL(f, "Expecting 'chain' line \001 of \002");
+        int v;
+        c->score[i] = atof(row[1]);
+        c->tname[i] = gt_names_add(&c->tnames, row[2], strlen(row[2]));
+        if (need_num(f, row, 3, &v))
             return -1;
-        c->id[i] = v;
-    } else {
-        c->id[i] = INT32_MIN; /* chainIdNext, assigned in file order later */
+        c->tsize[i] = v;
+        if (wc >= 13) {
+            if (need_num(f, row, 12, &v))
+                return -1;
+            c->id[i] = v;
+        } else {
+            c->id[i] = INT32_MIN; /* chainIdNext, assigned in file order later */
+        }
+        if (need_num(f, row, 5, &c->tstart[i]) || need_num(f, row, 6, &c->tend[i]))
+            return -1;
+        c->qname[i] = gt_names_add(&c->qnames, row[7], strlen(row[7]));
+        if (need_num(f, row, 8, &c->qsize[i]))
+            return -1;
+        c->qstrand[i] = row[9][0] == '-' ? 1 : 0;
+        if (need_num(f, row, 10, &c->qstart[i]) || need_num(f, row, 11, &c->qend[i]))
+            return -1;
     }
-    if (need_num(f, row, 5, &c->tstart[i]) || need_num(f, row, 6, &c->tend[i]))
-        return -1;
-    c->qname[i] = gt_names_add(&c->qnames, row[7], strlen(row[7]));
-    if (need_num(f, row, 8, &c->qsize[i]))
-        return -1;
-    c->qstrand[i] = row[9][0] == '-' ? 1 : 0;
-    if (need_num(f, row, 10, &c->qstart[i]) || need_num(f, row, 11, &c->qend[i]))
-        return -1;
     if (c->qstart[i] >= c->qend[i] || c->tstart[i] >= c->tend[i])
         LF_FAIL(f, "End before start line \001 of \002");
     if (c->qstart[i] < 0 || c->tstart[i] < 0)
