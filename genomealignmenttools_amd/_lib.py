@@ -192,6 +192,8 @@ _PROTOS = {
     "gac_net_get_fills": (
         C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "gac_net_get_fill_windows": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
+    "gac_net_rescore_windows": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                          C.c_void_p]),
     "gac_net_write": (
         C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_char_p, C.c_void_p, C.c_int32]),
     "gac_net_write_file": (

@@ -85,6 +85,24 @@ class Net:
                                                  _p(out["n_blocks"])))
         return out
 
+    def rescore_windows(self):
+        """gac_net_rescore_windows: the partial, printed target fills in
+        pre-order as gac_window records [n, 5] (chain, start, end, first
+        block, block count) and their pre-order positions."""
+        w = C.c_void_p()
+        pos = C.c_void_p()
+        n = C.c_int64()
+        check(lib().gac_net_rescore_windows(self.h, GAC_T, C.byref(w), C.byref(pos), C.byref(n)))
+        m = n.value
+        try:
+            win = np.ctypeslib.as_array(C.cast(w, C.POINTER(C.c_int32)), (max(m, 1) * 5,))
+            ps = np.ctypeslib.as_array(C.cast(pos, C.POINTER(C.c_int64)), (max(m, 1),))
+            return win[:m * 5].reshape(m, 5).copy(), ps[:m].copy()
+        finally:
+            libc = C.CDLL(None)
+            libc.free(w)
+            libc.free(pos)
+
     def write(self, side: int, path: str, t_scores: Optional[np.ndarray] = None,
               meta: Optional[List[str]] = None) -> None:
         meta = meta or []

@@ -2000,6 +2000,115 @@ int gac_net_get_fill_windows(const gac_net *n, int side, int32_t *first_block, i
     return GAC_OK;
 }
 
+/* gac_net_rescore_windows: per run of whole top-level subtrees (as the
+ * visibility pass), one read of each fill -- its parent position, its
+ * visibility and, when partial and printed, its record into the run's own
+ * buffer -- then the runs' buffers placed by a prefix sum and copied. */
+typedef struct rw_run {
+    gac_window *w;
+    int64_t *pos;
+    int64_t n, cap;
+} rw_run;
+
+typedef struct rw_job {
+    const gac_net *n;
+    int side;
+    uint8_t *vis;
+    int64_t *po;
+    int64_t per, nrun;
+    rw_run *runs;
+    gac_window *out;
+    int64_t *opos, *off;
+    _Atomic int64_t next;
+    int phase;
+} rw_job;
+
+static void *rw_thread(void *arg) {
+    rw_job *J = arg;
+    const gac_net *n = J->n;
+    const int side = J->side;
+    const int64_t nf = n->n_order[side];
+    for (;;) {
+        const int64_t r = atomic_fetch_add(&J->next, 1);
+        if (r >= J->nrun)
+            break;
+        rw_run *R = &J->runs[r];
+        if (J->phase == 1) {
+            if (R->n) {
+                memcpy(J->out + J->off[r], R->w, (size_t)R->n * sizeof(gac_window));
+                memcpy(J->opos + J->off[r], R->pos, (size_t)R->n * sizeof(int64_t));
+            }
+            free(R->w);
+            free(R->pos);
+            continue;
+        }
+        const int64_t a = next_top_level(n, side, r * J->per);
+        const int64_t b = next_top_level(n, side, (r + 1) * J->per < nf ? (r + 1) * J->per : nf);
+        for (int64_t i = a; i < b; ++i) {
+            if (i + 16 < b)
+                __builtin_prefetch(n->order[side][i + 16]);
+            const nfill *f = n->order[side][i];
+            const nfill *pf = f->pgap->pfill;
+            J->po[i] = pf ? pf->ord : -1;
+            const int sz = f->full ? full_size(n, f->chain) : f->ali;
+            const uint8_t v = (!pf || J->vis[pf->ord]) && sz >= n->opt.min_fill;
+            J->vis[i] = v;
+            if (!v || f->full)
+                continue;
+            if (R->n == R->cap) {
+                R->cap = R->cap ? 2 * R->cap : 4096;
+                R->w = realloc(R->w, (size_t)R->cap * sizeof(gac_window));
+                R->pos = realloc(R->pos, (size_t)R->cap * sizeof(int64_t));
+            }
+            R->w[R->n] = (gac_window){(int32_t)f->chain, f->start, f->end, f->wb0, f->wn};
+            R->pos[R->n++] = i;
+        }
+    }
+    return NULL;
+}
+
+int gac_net_rescore_windows(const gac_net *n, int side, gac_window **windows, int64_t **pos,
+                            int64_t *count) {
+    if (!n || side != GAC_T || !windows || !pos || !count)
+        return gac_fail(GAC_E_ARG, "gac_net_rescore_windows: bad argument (target side only)");
+    if (!(n->sides & (1 << side)))
+        return gac_fail(GAC_E_STATE, "gac_net_rescore_windows: side %d was not netted", side);
+    const int nt = gac_host_threads();
+    const int64_t nf = n->n_order[side];
+    gac_net *nm = (gac_net *)n; /* (the parent positions are a cache, as in get_fills) */
+    if (!nm->pord[side])
+        nm->pord[side] = malloc((size_t)(nf ? nf : 1) * sizeof(int64_t));
+    rw_job J;
+    memset(&J, 0, sizeof(J));
+    J.n = n;
+    J.side = side;
+    J.vis = malloc((size_t)(nf ? nf : 1));
+    J.po = nm->pord[side];
+    J.per = nf / (8 * (int64_t)nt) + 1;
+    J.nrun = (nf + J.per - 1) / J.per;
+    J.runs = calloc((size_t)(J.nrun ? J.nrun : 1), sizeof(rw_run));
+    atomic_init(&J.next, 0);
+    gac_run_threads(nt < J.nrun ? nt : (int)(J.nrun ? J.nrun : 1), rw_thread, &J);
+    nm->pord_ok[side] = 1;
+    J.off = malloc((size_t)(J.nrun + 1) * sizeof(int64_t));
+    J.off[0] = 0;
+    for (int64_t r = 0; r < J.nrun; ++r)
+        J.off[r + 1] = J.off[r] + J.runs[r].n;
+    const int64_t m = J.off[J.nrun];
+    J.out = malloc((size_t)(m ? m : 1) * sizeof(gac_window));
+    J.opos = malloc((size_t)(m ? m : 1) * sizeof(int64_t));
+    J.phase = 1;
+    atomic_store(&J.next, 0);
+    gac_run_threads(nt < J.nrun ? nt : (int)(J.nrun ? J.nrun : 1), rw_thread, &J);
+    free(J.runs);
+    free(J.off);
+    free(J.vis);
+    *windows = J.out;
+    *pos = J.opos;
+    *count = m;
+    return GAC_OK;
+}
+
 /* ------------------------------------------------------------ output */
 /* deferred scores (gac_net_write_begin): where each rescored fill's score
  * goes in a run's text */

@@ -349,43 +349,6 @@ static void *check_thread(void *arg) {
 
 /* chainNet -rescore's rescoring list: the target fills that are partial
  * (flag 1) and printed (flag 2), in fill order */
-typedef struct range_job {
-    const int32_t *fc, *fs, *fe, *fw0, *fwn;
-    const uint8_t *fl;
-    gac_window *r;
-    int64_t *rix;
-    int64_t nf;
-    int nt;
-    int64_t *cnt; /* [nt + 1]: per slice, then where its ranges start */
-    int phase;
-    _Atomic int next;
-} range_job;
-
-static void *range_thread(void *arg) {
-    range_job *J = arg;
-    for (int k; (k = atomic_fetch_add(&J->next, 1)) < J->nt;) {
-        const int64_t a = J->nf * k / J->nt, b = J->nf * (k + 1) / J->nt;
-        if (J->phase == 0) {
-            int64_t c = 0;
-            for (int64_t i = a; i < b; ++i)
-                c += (J->fl[i] & 3) == 3;
-            J->cnt[k] = c;
-            continue;
-        }
-        int64_t o = J->cnt[k];
-        for (int64_t i = a; i < b; ++i)
-            if ((J->fl[i] & 3) == 3) {
-                J->r[o].chain = J->fc[i];
-                J->r[o].t_start = J->fs[i];
-                J->r[o].t_end = J->fe[i];
-                J->r[o].first_block = J->fw0[i];
-                J->r[o].n_blocks = J->fwn[i];
-                J->rix[o++] = i;
-            }
-    }
-    return NULL;
-}
-
 int main(int argc, char *argv[]) {
     gt_stage("");
     int min_space = 25;
@@ -615,33 +578,13 @@ int main(int argc, char *argv[]) {
     int64_t *tscores = NULL;
     if (rescore) {
         const int64_t nf = gac_net_fill_count(net, GAC_T);
-        int32_t *fc = malloc((nf ? nf : 1) * 4), *fs = malloc((nf ? nf : 1) * 4),
-                *fe = malloc((nf ? nf : 1) * 4);
-        uint8_t *fl = malloc(nf ? nf : 1);
-        int32_t *fa = malloc((nf ? nf : 1) * 4);
-        int32_t *fw0 = malloc((nf ? nf : 1) * 4), *fwn = malloc((nf ? nf : 1) * 4);
-        gt_check(gac_net_get_fills(net, GAC_T, fc, fs, fe, fa, fl));
-        /* each fill's block window, found by the netting when it made the
-         * fill: the device reads it instead of searching the chain */
-        gt_check(gac_net_get_fill_windows(net, GAC_T, fw0, fwn));
-        gac_window *r = malloc((nf ? nf : 1) * sizeof(gac_window));
-        int64_t *rix = malloc((nf ? nf : 1) * 8);
+        /* the partial, printed target fills in pre-order with the window of
+         * blocks the netting found for each (the device reads it instead of
+         * searching the chain), in one pass over the fills */
+        gac_window *r = NULL;
+        int64_t *rix = NULL, nr = 0;
+        gt_check(gac_net_rescore_windows(net, GAC_T, &r, &rix, &nr));
         gac_mark("fill list: ranges");
-        /* the partial, printed fills in order: counted per slice, then
-         * placed, on all threads */
-        range_job RJ = {fc, fs, fe, fw0, fwn, fl, r, rix, nf, gt_threads(), NULL, 0, 0};
-        RJ.cnt = calloc((size_t)RJ.nt + 1, 8);
-        atomic_init(&RJ.next, 0);
-        gac_run_threads(RJ.nt, range_thread, &RJ);
-        for (int k = 0; k < RJ.nt; ++k) /* (exclusive prefix) */
-            RJ.cnt[k + 1] += RJ.cnt[k];
-        memmove(RJ.cnt + 1, RJ.cnt, (size_t)RJ.nt * 8);
-        RJ.cnt[0] = 0;
-        RJ.phase = 1;
-        atomic_init(&RJ.next, 0);
-        gac_run_threads(RJ.nt, range_thread, &RJ);
-        const int64_t nr = RJ.cnt[RJ.nt];
-        free(RJ.cnt);
         tscores = calloc(nf ? nf : 1, 8);
         /* GAC_DUMP_RANGES=FILE (measurement hook, one process only): the
          * rescored fills as gac_window records (int32 chain index in file
@@ -766,16 +709,9 @@ int main(int argc, char *argv[]) {
         }
         /* (13 M-entry arrays: unmapping them here cost the target net's
          * start tens of ms; their pages go after the nets are written) */
-        const size_t nfb = (size_t)(nf ? nf : 1);
-        gt_free_late(fc, nfb * 4);
-        gt_free_late(fs, nfb * 4);
-        gt_free_late(fe, nfb * 4);
-        gt_free_late(fl, nfb);
-        gt_free_late(fa, nfb * 4);
-        gt_free_late(fw0, nfb * 4);
-        gt_free_late(fwn, nfb * 4);
-        gt_free_late(r, nfb * sizeof(gac_window));
-        gt_free_late(rix, nfb * 8);
+        const size_t nrb = (size_t)(nr ? nr : 1);
+        gt_free_late(r, nrb * sizeof(gac_window));
+        gt_free_late(rix, nrb * 8);
         gac_mark("fill arrays released");
     }
     wo[0].tscores = tscores;

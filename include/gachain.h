@@ -439,6 +439,13 @@ int gac_net_get_fills(const gac_net *net, int side, int32_t *chain, int32_t *sta
  * n_blocks), recorded while netting.  side must be GAC_T. */
 int gac_net_get_fill_windows(const gac_net *net, int side, int32_t *first_block,
                              int32_t *n_blocks);
+/* The -rescore list in one pass: the target fills that are partial and
+ * printed (gac_net_get_fills flags == 3), in pre-order, as gac_window
+ * records (chain, start, end and their window) with each one's pre-order
+ * position in `pos` (for gac_net_write's t_scores).  *windows and *pos are
+ * malloc'ed (free them); *n = their count.  side must be GAC_T. */
+int gac_net_rescore_windows(const gac_net *net, int side, gac_window **windows, int64_t **pos,
+                            int64_t *n);
 /* Write one side's .net (outputNetSide) to path ("stdout" allowed) after the
  * n_meta '#' metadata lines.  t_scores (T side only, may be NULL): per fill
  * in gac_net_get_fills order, the rescored global score of partial fills

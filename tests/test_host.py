@@ -154,6 +154,13 @@ def test_net_fill_windows(case, monkeypatch):
         first, cnt = subset_windows(ca, f["chain"][part], f["start"][part], f["end"][part])
         assert np.array_equal(f["first_block"][part], first)
         assert np.array_equal(f["n_blocks"][part], cnt)
+        # chainNet -rescore's list in one pass: the partial printed fills
+        sel = np.nonzero(f["flags"] == 3)[0]
+        w, pos = net.rescore_windows()
+        assert np.array_equal(pos, sel)
+        want = np.stack([f["chain"][sel], f["start"][sel], f["end"][sel],
+                         f["first_block"][sel], f["n_blocks"][sel]], 1)
+        assert np.array_equal(w, want)
         net.close()
 
 
