@@ -16,23 +16,29 @@ def main():
     reps = int(sys.argv[1])
     specs = sys.argv[2:]
     variants = []
-    for sp in specs:
+    for sp in specs:  # tag:ENV=v,...  (@TOOL=path: another build's bin/chainNet)
         tag, _, kv = sp.partition(":")
         env = dict(os.environ)
+        tool = None
         for x in filter(None, kv.split(",")):
             k, _, v = x.partition("=")
-            env[k] = v
-        variants.append((tag, env))
+            if k == "@TOOL":
+                tool = v
+            else:
+                env[k] = v
+        variants.append((tag, env, tool))
     sys.argv = [sys.argv[0]]
     args = bench.parse()
     d, info = bench.c5_files(args)
     out = os.path.join(d, "ab")
     outs = [out + ".t.net", out + ".q.net"]
-    cmd = bench.tool_cmd(d, out, 1, 0)
-    bench.run_tool(cmd, outs)  # warm the page cache
-    times = {t: [] for t, _ in variants}
+    base = bench.tool_cmd(d, out, 1, 0)
+    cmd_of = lambda tool: [tool] + base[1:] if tool else base
+    bench.run_tool(base, outs)  # warm the page cache
+    times = {t: [] for t, _, _ in variants}
     for rep in range(reps):
-        for tag, env in variants:
+        for tag, env, tool in variants:
+            cmd = cmd_of(tool)
             for o in outs:
                 if os.path.exists(o):
                     os.remove(o)
@@ -40,8 +46,8 @@ def main():
             bench.run_tool(cmd, [], env=env)
             times[tag].append((time.perf_counter() - t0) * 1e3)
             print(f"{tag} rep {rep}: {times[tag][-1]:.0f} ms", flush=True)
-    for tag, env in variants:
-        r = bench.run_tool(cmd + ["-verbose=2"], outs, env=dict(env, GAC_TIMING="1"))
+    for tag, env, tool in variants:
+        r = bench.run_tool(cmd_of(tool) + ["-verbose=2"], outs, env=dict(env, GAC_TIMING="1"))
         par = bench.full_parity("c5", {"in_chain_sha256": os.path.join(d, "in.chain"),
                                        "chainnet_rescore.t_net_sha256": outs[0],
                                        "chainnet_rescore.q_net_sha256": outs[1]})
