@@ -918,17 +918,6 @@ void gac_obuf_printf(gac_obuf *o, const char *fmt, ...) {
     o->n += (size_t)k;
 }
 
-/* written run buffers handed back to the formatters (gac_obuf runs): their
- * pages are already faulted in, where a fresh buffer per run cost the kernel
- * a page clear per page of output (2.6 GB per C5 run) */
-#define PO_POOL 64
-typedef struct po_pool {
-    pthread_mutex_t mu;
-    char *p[PO_POOL];
-    size_t cap[PO_POOL];
-    int n;
-} po_pool;
-
 typedef struct po_job {
     int64_t nr;
     void (*fn)(FILE *, int64_t, void *);
@@ -936,37 +925,10 @@ typedef struct po_job {
     void *arg;
     char **buf;
     size_t *len;
-    size_t *cap; /* gac_obuf runs: the buffer's capacity (NULL: not pooled) */
-    po_pool *pool;
     _Atomic int *ready;
     _Atomic int64_t next;
     _Atomic int oom;
 } po_job;
-
-static void pool_take(po_pool *P, gac_obuf *o) {
-    if (!P)
-        return;
-    pthread_mutex_lock(&P->mu);
-    if (P->n) {
-        --P->n;
-        o->p = P->p[P->n];
-        o->cap = P->cap[P->n];
-    }
-    pthread_mutex_unlock(&P->mu);
-}
-
-static void pool_give(po_pool *P, char *p, size_t cap) {
-    if (P && p && cap >= (64u << 10)) {
-        pthread_mutex_lock(&P->mu);
-        if (P->n < PO_POOL) {
-            P->p[P->n] = p;
-            P->cap[P->n++] = cap;
-            p = NULL;
-        }
-        pthread_mutex_unlock(&P->mu);
-    }
-    free(p);
-}
 
 static void *po_thread(void *p) {
     po_job *J = p;
@@ -976,12 +938,9 @@ static void *po_thread(void *p) {
             break;
         if (J->fn_buf) {
             gac_obuf o = {NULL, 0, 0};
-            pool_take(J->pool, &o);
             J->fn_buf(&o, r, J->arg);
             J->buf[r] = o.p;
             J->len[r] = o.n;
-            if (J->cap)
-                J->cap[r] = o.cap;
             atomic_store_explicit(&J->ready[r], 1, memory_order_release);
             continue;
         }
@@ -1008,8 +967,6 @@ static int par_format(int64_t nr, void (*fn)(FILE *f, int64_t r, void *arg),
     J.arg = arg;
     J.buf = calloc((size_t)(nr > 0 ? nr : 1), sizeof(char *));
     J.len = calloc((size_t)(nr > 0 ? nr : 1), sizeof(size_t));
-    J.cap = NULL; /* (kept buffers: no pool) */
-    J.pool = NULL;
     J.ready = calloc((size_t)(nr > 0 ? nr : 1), sizeof(_Atomic int));
     atomic_init(&J.next, 0);
     atomic_init(&J.oom, 0);
@@ -1184,20 +1141,6 @@ static int par_output(FILE *out, int64_t nr, void (*fn)(FILE *f, int64_t r, void
     J.buf = calloc((size_t)nr, sizeof(char *));
     J.len = calloc((size_t)nr, sizeof(size_t));
     J.ready = calloc((size_t)nr, sizeof(_Atomic int));
-    po_pool pool;
-    J.cap = NULL;
-    J.pool = NULL;
-    static int pool_on = -1; /* (GAC_OUT_POOL=0: a fresh buffer per run) */
-    if (pool_on < 0) {
-        const char *e = getenv("GAC_OUT_POOL");
-        pool_on = !(e && *e == '0');
-    }
-    if (fn_buf && pool_on) {
-        pthread_mutex_init(&pool.mu, NULL);
-        pool.n = 0;
-        J.cap = calloc((size_t)nr, sizeof(size_t));
-        J.pool = &pool;
-    }
     atomic_init(&J.next, 0);
     atomic_init(&J.oom, 0);
     int nt = gac_host_threads() - 1;
@@ -1271,17 +1214,11 @@ static int par_output(FILE *out, int64_t nr, void (*fn)(FILE *f, int64_t r, void
         if (!bad && writev_all(fd, iov, k) != 0)
             bad = 1;
         for (int64_t x = r0; x < r; ++x)
-            pool_give(J.pool, J.buf[x], J.cap ? J.cap[x] : 0);
+            free(J.buf[x]);
     }
     for (int i = 0; i < nt; ++i)
         pthread_join(th[i], NULL);
     free(th);
-    if (J.pool) {
-        for (int k = 0; k < pool.n; ++k)
-            free(pool.p[k]);
-        pthread_mutex_destroy(&pool.mu);
-    }
-    free(J.cap);
     free(J.buf);
     free(J.len);
     free((void *)J.ready);
