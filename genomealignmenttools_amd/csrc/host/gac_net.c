@@ -1213,6 +1213,11 @@ typedef struct region {
 
 typedef struct big_net {
     net_task *t;
+    /* per chain of the task, in its order: span on this side and block
+     * count, gathered once (the chains of one side lie all over the input's
+     * arrays; the cut placement passes over them several times) */
+    int32_t *ss, *se;
+    int64_t *nbk;
     int64_t m;          /* chains netted sequentially first */
     sitem *spaces;      /* all spaces after the prefix */
     int64_t *lists;     /* region chain lists, back to back */
@@ -1304,12 +1309,9 @@ static int64_t upper_bound32(const int32_t *a, int64_t n, int32_t v) {
     return lo;
 }
 
-/* work of chain c inside [a, b): a region builds the block slice there and
- * scans the spaces its blocks reach */
-static int64_t chain_work_in(const gac_net *net, int side, int64_t c, int a, int b) {
-    int cs, ce;
-    chain_span(net, side, c, &cs, &ce);
-    const int64_t nb = net->in.blk_off[c + 1] - net->in.blk_off[c];
+/* work of a chain (span [cs, ce), nb blocks) inside [a, b): a region
+ * builds the block slice there and scans the spaces its blocks reach */
+static int64_t chain_work_in(int cs, int ce, int64_t nb, int a, int b) {
     const int64_t lo = cs > a ? cs : a, hi = ce < b ? ce : b;
     if (hi <= lo || ce <= cs)
         return 8;
@@ -1330,10 +1332,8 @@ static int32_t place_cuts(const gac_net *net, const big_net *B, const sitem *sp,
     int64_t *bin = calloc(NB, 8), tot = 0;
     const double scale = (double)NB / (size > 0 ? size : 1);
     for (int64_t i = 0; i < rest; ++i) {
-        const int64_t c = t->chains[B->m + i];
-        int cs, ce;
-        chain_span(net, t->side, c, &cs, &ce);
-        const int64_t w = 8 + (net->in.blk_off[c + 1] - net->in.blk_off[c]);
+        const int cs = B->ss[B->m + i], ce = B->se[B->m + i];
+        const int64_t w = 8 + B->nbk[B->m + i];
         int b0 = (int)(cs * scale), b1 = (int)((ce > cs ? ce - 1 : cs) * scale);
         b0 = b0 < 0 ? 0 : (b0 >= NB ? NB - 1 : b0);
         b1 = b1 < b0 ? b0 : (b1 >= NB ? NB - 1 : b1);
@@ -1374,12 +1374,11 @@ static int32_t place_cuts(const gac_net *net, const big_net *B, const sitem *sp,
     /* region work */
     int64_t *rw = calloc((size_t)nc + 1, 8), mx = 0;
     for (int64_t i = 0; i < rest; ++i) {
-        const int64_t c = t->chains[B->m + i];
-        int cs, ce;
-        chain_span(net, t->side, c, &cs, &ce);
+        const int cs = B->ss[B->m + i], ce = B->se[B->m + i];
         const int64_t a = upper_bound32(cuts, nc, cs), b = upper_bound32(cuts, nc, ce > cs ? ce - 1 : cs);
         for (int64_t r = a; r <= b; ++r)
-            rw[r] += chain_work_in(net, t->side, c, r ? cuts[r - 1] : 0, r < nc ? cuts[r] : size);
+            rw[r] += chain_work_in(cs, ce, B->nbk[B->m + i], r ? cuts[r - 1] : 0,
+                                   r < nc ? cuts[r] : size);
     }
     for (int32_t r = 0; r <= nc; ++r)
         mx = rw[r] > mx ? rw[r] : mx;
@@ -1398,6 +1397,22 @@ static void big_prefix(gac_net *n, nwork *w, big_net *B, int nthreads) {
     sp_init(w, c, 0, c->size, c->root);
     const int32_t want = 4 * nthreads;
     int32_t *cuts = malloc((size_t)want * 4);
+    B->ss = malloc((size_t)(t->n ? t->n : 1) * 4);
+    B->se = malloc((size_t)(t->n ? t->n : 1) * 4);
+    B->nbk = malloc((size_t)(t->n ? t->n : 1) * 8);
+    for (int64_t i = 0; i < t->n; ++i) {
+        const int64_t c = t->chains[i];
+        if (i + 8 < t->n) {
+            const int64_t d = t->chains[i + 8];
+            __builtin_prefetch(&n->in.blk_off[d]);
+            __builtin_prefetch(t->side == GAC_T ? &n->in.t_start[d] : &n->in.q_start[d]);
+        }
+        int cs, ce;
+        chain_span(n, t->side, c, &cs, &ce);
+        B->ss[i] = cs;
+        B->se[i] = ce;
+        B->nbk[i] = n->in.blk_off[c + 1] - n->in.blk_off[c];
+    }
     /* the prefix doubles from 8 chains until the regions balance: the
      * first chains leave one space over everything they did not reach */
     int64_t m = t->n < 8 ? t->n : 8, done = 0;
@@ -1437,13 +1452,12 @@ static void big_prefix(gac_net *n, nwork *w, big_net *B, int nthreads) {
     int64_t *cnt = calloc((size_t)nreg + 1, 8);
     int32_t *ra = malloc((size_t)(rest ? rest : 1) * 4), *rb = malloc((size_t)(rest ? rest : 1) * 4);
     for (int64_t i = 0; i < rest; ++i) {
-        int cs, ce;
-        chain_span(n, t->side, t->chains[m + i], &cs, &ce);
+        const int cs = B->ss[m + i], ce = B->se[m + i];
         ra[i] = (int32_t)upper_bound32(cuts, nreg - 1, cs);
         rb[i] = (int32_t)upper_bound32(cuts, nreg - 1, ce > cs ? ce - 1 : cs);
         for (int32_t r = ra[i]; r <= rb[i]; ++r) {
             ++cnt[r];
-            B->reg[r].work += chain_work_in(n, t->side, t->chains[m + i], r ? cuts[r - 1] : 0,
+            B->reg[r].work += chain_work_in(cs, ce, B->nbk[m + i], r ? cuts[r - 1] : 0,
                                             r < nreg - 1 ? cuts[r] : c->size);
         }
     }
@@ -1463,6 +1477,11 @@ static void big_prefix(gac_net *n, nwork *w, big_net *B, int nthreads) {
     free(ra);
     free(rb);
     free(cuts);
+    free(B->ss);
+    free(B->se);
+    free(B->nbk);
+    B->ss = B->se = NULL;
+    B->nbk = NULL;
 }
 
 static void net_region(gac_net *n, nwork *w, region *R) {
