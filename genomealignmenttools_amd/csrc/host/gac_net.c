@@ -26,6 +26,7 @@
 #include <sched.h>
 #include <stdint.h>
 #include <sys/mman.h>
+#include <pthread.h>
 #include <stdatomic.h>
 #include <math.h>
 #include <stdarg.h>
@@ -1218,6 +1219,7 @@ typedef struct big_net {
      * arrays; the cut placement passes over them several times) */
     int32_t *ss, *se;
     int64_t *nbk;
+    double t_start, t_gather, t_add, t_cut, t_reg; /* (GAC_TIMING laps of the prefix) */
     int64_t m;          /* chains netted sequentially first */
     sitem *spaces;      /* all spaces after the prefix */
     int64_t *lists;     /* region chain lists, back to back */
@@ -1329,20 +1331,28 @@ static int32_t place_cuts(const gac_net *net, const big_net *B, const sitem *sp,
     /* work density: each chain's blocks spread evenly over its span, on a
      * grid of 4096 bins */
     enum { NB = 4096 };
-    int64_t *bin = calloc(NB, 8), tot = 0;
+    int64_t *bin = calloc(NB + 1, 8), *dif = calloc(NB + 1, 8), tot = 0;
     const double scale = (double)NB / (size > 0 ? size : 1);
-    for (int64_t i = 0; i < rest; ++i) {
+    for (int64_t i = 0; i < rest; ++i) { /* (spread as a difference array) */
         const int cs = B->ss[B->m + i], ce = B->se[B->m + i];
         const int64_t w = 8 + B->nbk[B->m + i];
         int b0 = (int)(cs * scale), b1 = (int)((ce > cs ? ce - 1 : cs) * scale);
         b0 = b0 < 0 ? 0 : (b0 >= NB ? NB - 1 : b0);
         b1 = b1 < b0 ? b0 : (b1 >= NB ? NB - 1 : b1);
         const int64_t per = w / (b1 - b0 + 1);
-        for (int k = b0; k <= b1; ++k)
-            bin[k] += per;
+        dif[b0] += per;
+        dif[b1 + 1] -= per;
         bin[b0] += w - per * (b1 - b0 + 1);
         tot += w;
     }
+    {
+        int64_t run = 0;
+        for (int k = 0; k < NB; ++k) {
+            run += dif[k];
+            bin[k] += run;
+        }
+    }
+    free(dif);
     int32_t nc = 0;
     int64_t acc = 0;
     int k = 0;
@@ -1388,6 +1398,8 @@ static int32_t place_cuts(const gac_net *net, const big_net *B, const sitem *sp,
     return nc + 1;
 }
 
+static double mono_s(void);
+
 /* thread 0: the sequential prefix of a big side and its regions */
 static void big_prefix(gac_net *n, nwork *w, big_net *B, int nthreads) {
     net_task *t = B->t;
@@ -1397,6 +1409,7 @@ static void big_prefix(gac_net *n, nwork *w, big_net *B, int nthreads) {
     sp_init(w, c, 0, c->size, c->root);
     const int32_t want = 4 * nthreads;
     int32_t *cuts = malloc((size_t)want * 4);
+    B->t_start = mono_s();
     B->ss = malloc((size_t)(t->n ? t->n : 1) * 4);
     B->se = malloc((size_t)(t->n ? t->n : 1) * 4);
     B->nbk = malloc((size_t)(t->n ? t->n : 1) * 8);
@@ -1419,14 +1432,20 @@ static void big_prefix(gac_net *n, nwork *w, big_net *B, int nthreads) {
     sitem *sp = NULL;
     int64_t nsp = 0;
     int32_t nreg = 1;
+    double t_add = 0, t_cut = 0, t0 = mono_s();
+    const double t_gather = t0 - B->t_start;
     for (;;) {
+        double ta = mono_s();
         for (; done < m; ++done)
             add_chain(n, w, t->side, t->chains[done], c, INT32_MIN, INT32_MAX);
+        double tb = mono_s();
+        t_add += tb - ta;
         B->m = m;
         free(sp);
         sp = sp_all(w, c, &nsp);
         int64_t mx, tot;
         nreg = place_cuts(n, B, sp, nsp, want, c->size, cuts, &mx, &tot);
+        t_cut += mono_s() - tb;
         /* good enough: the largest region at most ~1/threads of the rest */
         if (m >= t->n || mx * nthreads <= tot * 5 / 4 || m >= t->n / 4)
             break;
@@ -1477,6 +1496,10 @@ static void big_prefix(gac_net *n, nwork *w, big_net *B, int nthreads) {
     free(ra);
     free(rb);
     free(cuts);
+    B->t_gather = t_gather;
+    B->t_add = t_add;
+    B->t_cut = t_cut;
+    B->t_reg = mono_s() - t0 - t_add - t_cut;
     free(B->ss);
     free(B->se);
     free(B->nbk);
@@ -1496,10 +1519,11 @@ typedef struct net_job {
     int64_t ntask;
     big_net *big;       /* big sides (split into regions) */
     int32_t nbig;
-    region **rq;        /* all regions, largest work first (after the prefixes) */
-    int64_t nrq;
-    _Atomic int64_t next, rnext;
-    _Atomic int ready;  /* the prefixes are done and rq is published */
+    region **rq;        /* the regions, each big side's largest work first, published per side */
+    int64_t nrq;        /* (capacity; the published count is rpub) */
+    _Atomic int64_t next, rnext, rpub;
+    pthread_mutex_t rmu; /* (publishing a side's regions) */
+    _Atomic int ready;  /* every prefix is done and every region published */
     _Atomic int wid;
     _Atomic int32_t bnext, bdone; /* big sides whose prefix was taken / is done */
     int nthreads;
@@ -1540,34 +1564,39 @@ static void *net_thread(void *arg) {
         if (b >= J->nbig)
             break;
         big_prefix(J->n, w, &J->big[b], J->nthreads);
+        /* its regions, largest work first, published at once: the other
+         * threads take them while the remaining prefixes run (round 4 waited
+         * for every prefix; at -nranks=8 that wait was most of the netting) */
+        big_net *B = &J->big[b];
+        region **tmp = malloc((size_t)(B->n_reg ? B->n_reg : 1) * sizeof(region *));
+        for (int32_t r = 0; r < B->n_reg; ++r)
+            tmp[r] = &B->reg[r];
+        qsort(tmp, (size_t)B->n_reg, sizeof(region *), region_cmp);
+        pthread_mutex_lock(&J->rmu);
+        const int64_t at = atomic_load(&J->rpub);
+        memcpy(J->rq + at, tmp, (size_t)B->n_reg * sizeof(region *));
+        atomic_store_explicit(&J->rpub, at + B->n_reg, memory_order_release);
+        pthread_mutex_unlock(&J->rmu);
+        free(tmp);
         if (atomic_fetch_add(&J->bdone, 1) + 1 < J->nbig)
             continue;
-        int64_t nr = 0;
-        for (int32_t k = 0; k < J->nbig; ++k)
-            nr += J->big[k].n_reg;
-        J->rq = malloc((size_t)(nr ? nr : 1) * sizeof(region *));
-        for (int32_t k = 0; k < J->nbig; ++k)
-            for (int32_t r = 0; r < J->big[k].n_reg; ++r)
-                J->rq[J->nrq++] = &J->big[k].reg[r];
-        qsort(J->rq, (size_t)J->nrq, sizeof(region *), region_cmp);
         J->prefix_s = mono_s() - J->t0;
         atomic_store_explicit(&J->ready, 1, memory_order_release);
     }
     for (;;) {
-        if (atomic_load_explicit(&J->ready, memory_order_acquire)) {
-            const int64_t k = atomic_fetch_add(&J->rnext, 1);
-            if (k < J->nrq) {
+        int64_t k = atomic_load(&J->rnext);
+        if (k < atomic_load_explicit(&J->rpub, memory_order_acquire)) {
+            if (atomic_compare_exchange_weak(&J->rnext, &k, k + 1))
                 net_region(J->n, w, J->rq[k]);
-                continue;
-            }
+            continue;
         }
-        const int64_t k = atomic_fetch_add(&J->next, 1);
-        if (k < J->ntask) {
-            net_small(J->n, w, &J->task[k]);
+        const int64_t t = atomic_fetch_add(&J->next, 1);
+        if (t < J->ntask) {
+            net_small(J->n, w, &J->task[t]);
             continue;
         }
         if (atomic_load_explicit(&J->ready, memory_order_acquire) &&
-            atomic_load(&J->rnext) >= J->nrq)
+            atomic_load(&J->rnext) >= atomic_load(&J->rpub))
             break;
         sched_yield();
     }
@@ -1731,12 +1760,14 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
     J2.ntask = nsmall;
     atomic_init(&J2.next, 0);
     atomic_init(&J2.rnext, 0);
+    atomic_init(&J2.rpub, 0);
+    pthread_mutex_init(&J2.rmu, NULL);
     atomic_init(&J2.ready, J.nbig == 0);
     atomic_init(&J2.wid, 0);
     atomic_init(&J2.bnext, 0);
     atomic_init(&J2.bdone, 0);
-    J2.rq = NULL;
-    J2.nrq = 0;
+    J2.nrq = (int64_t)J.nbig * 4 * n->n_w; /* (place_cuts makes at most 4 x threads regions) */
+    J2.rq = malloc((size_t)(J2.nrq ? J2.nrq : 1) * sizeof(region *));
     struct timespec t_add0, t_add1;
     clock_gettime(CLOCK_MONOTONIC, &t_add0);
     J2.t0 = mono_s();
@@ -1751,9 +1782,10 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
             int64_t mx = 0;
             for (int32_t r = 0; r < J.big[b].n_reg; ++r)
                 mx = J.big[b].reg[r].work > mx ? J.big[b].reg[r].work : mx;
-            fprintf(stderr, "[gac_net_build] side %d seq %d: %lld chains, %lld sequential, %d regions (largest work %lld)\n",
+            fprintf(stderr, "[gac_net_build] side %d seq %d: %lld chains, %lld sequential, %d regions (largest work %lld); prefix: gather %.3f, chains %.3f, cuts %.3f, regions %.3f s\n",
                     J.big[b].t->side, J.big[b].t->chrom, (long long)J.big[b].t->n,
-                    (long long)J.big[b].m, J.big[b].n_reg, (long long)mx);
+                    (long long)J.big[b].m, J.big[b].n_reg, (long long)mx, J.big[b].t_gather,
+                    J.big[b].t_add, J.big[b].t_cut, J.big[b].t_reg);
         }
     }
     for (int32_t b = 0; b < J.nbig; ++b) {
@@ -1763,6 +1795,7 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
     }
     free(J.big);
     free(J2.rq);
+    pthread_mutex_destroy(&J2.rmu);
     free(J.task);
     free(toff);
     free(qoff);
