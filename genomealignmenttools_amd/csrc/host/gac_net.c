@@ -2629,6 +2629,46 @@ static int net_write_f(const gac_net *n, int side, const int64_t *tscores, FILE 
     return (ferror(f) || wbad) ? GAC_E_IO : GAC_OK;
 }
 
+int gac_net_format(const gac_net *n, int side, const int64_t *tscores, const char *const *meta,
+                   int32_t n_meta, char ***bufs, size_t **lens, int64_t *nbufs) {
+    if (!n || (side != GAC_T && side != GAC_Q) || !bufs || !lens || !nbufs)
+        return gac_fail(GAC_E_ARG, "gac_net_format: bad argument");
+    if (!(n->sides & (1 << side)))
+        return gac_fail(GAC_E_STATE, "gac_net_format: side %d was not netted", side);
+    wjob J;
+    wjob_flags(&J, n, side, tscores);
+    const int64_t nr = (J.nf + J.per - 1) / J.per;
+    char **b = NULL;
+    size_t *l = NULL;
+    const int bad = gac_par_format_buf(nr, write_run, &J, &b, &l);
+    wjob_free_flags(&J);
+    if (bad) {
+        for (int64_t r = 0; r < nr; ++r)
+            free(b ? b[r] : NULL);
+        free(b);
+        free(l);
+        return gac_fail(GAC_E_IO, "gac_net_format: out of memory");
+    }
+    /* the '#' lines in front */
+    char **ob = malloc((size_t)(nr + 1) * sizeof(char *));
+    size_t *ol = malloc((size_t)(nr + 1) * sizeof(size_t));
+    gac_obuf m = {NULL, 0, 0};
+    for (int32_t i = 0; i < n_meta; ++i)
+        gac_obuf_printf(&m, "%s\n", meta[i]);
+    ob[0] = m.p;
+    ol[0] = m.n;
+    if (nr) {
+        memcpy(ob + 1, b, (size_t)nr * sizeof(char *));
+        memcpy(ol + 1, l, (size_t)nr * sizeof(size_t));
+    }
+    free(b);
+    free(l);
+    *bufs = ob;
+    *lens = ol;
+    *nbufs = nr + 1;
+    return GAC_OK;
+}
+
 /* ---- two-phase target net for -rescore (gac_net_write_begin/_end) */
 struct gac_net_wpre {
     wjob J;

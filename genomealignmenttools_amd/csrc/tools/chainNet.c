@@ -114,9 +114,36 @@ static void *write_net(void *arg) {
             snprintf(w->err, sizeof(w->err), "write error on %s", w->path);
         return NULL;
     }
+    if (g_rk.n > 1 && !w->pre) {
+        /* -nranks: this rank's part formatted on all threads into buffers and
+         * written in place from them (rank 0's part carries the '#' lines) */
+        const int m = g_rk.me == 0;
+        char **bufs = NULL;
+        size_t *lens = NULL;
+        int64_t nb = 0;
+        w->rc = gac_net_format(w->net, w->side, w->tscores,
+                               m ? (const char *const *)w->c->meta : NULL, m ? w->c->n_meta : 0,
+                               &bufs, &lens, &nb);
+        if (w->rc != GAC_OK) {
+            snprintf(w->err, sizeof(w->err), "%s", gac_last_error());
+            return NULL;
+        }
+        size_t len = 0;
+        for (int64_t k = 0; k < nb; ++k)
+            len += lens[k];
+        if (getenv("GAC_TIMING")) /* (the per-rank table of DESIGN §6) */
+            fprintf(stderr, "[rank %d/%d] %s part: %zu bytes\n", g_rk.me, g_rk.n,
+                    w->side == GAC_T ? "target net" : "query net", len);
+        gt_ranks_place_bufs(&g_rk, w->path, bufs, lens, nb);
+        for (int64_t k = 0; k < nb; ++k)
+            free(bufs[k]);
+        free(bufs);
+        free(lens);
+        return NULL;
+    }
     if (g_rk.n > 1) {
-        /* -nranks: this rank's part formatted in memory and written in place
-         * (rank 0's part carries the '#' lines) */
+        /* -nranks with the preformatted target net: formatted in memory and
+         * written in place (rank 0's part carries the '#' lines) */
         char *buf = NULL;
         size_t len = 0;
         FILE *mf = open_memstream(&buf, &len);

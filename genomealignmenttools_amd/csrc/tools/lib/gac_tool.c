@@ -12,6 +12,7 @@
 #include <string.h>
 #include <signal.h>
 #include <sys/stat.h>
+#include <sys/uio.h>
 #include <unistd.h>
 #include <sys/syscall.h>
 #include <pthread.h>
@@ -905,6 +906,15 @@ int gt_ranks_solo(void) {
 }
 
 void gt_ranks_place(const gt_ranks *rk, const char *path, const char *buf, size_t len) {
+    char *b = (char *)buf;
+    gt_ranks_place_bufs(rk, path, &b, &len, 1);
+}
+
+void gt_ranks_place_bufs(const gt_ranks *rk, const char *path, char *const *bufs,
+                         const size_t *lens, int64_t nb) {
+    size_t len = 0;
+    for (int64_t k = 0; k < nb; ++k)
+        len += lens[k];
     char solo[4096];
     const int alone = gt_ranks_solo();
     off_t off = 0;
@@ -919,11 +929,35 @@ void gt_ranks_place(const gt_ranks *rk, const char *path, const char *buf, size_
     const int fd = open(path, O_WRONLY | O_CREAT | (alone ? O_TRUNC : 0), 0666);
     if (fd < 0)
         gt_abort("Can't open %s to write: %s", path, strerror(errno));
-    for (size_t done = 0; done < len;) {
-        const ssize_t k = pwrite(fd, buf + done, len - done, off + (off_t)done);
-        if (k <= 0)
-            gt_abort("write error on %s: %s", path, strerror(errno));
-        done += (size_t)k;
+    for (int64_t k = 0; k < nb; ++k) { /* (pwritev of up to 256 buffers at a time) */
+        struct iovec iov[256];
+        int m = 0;
+        size_t bytes = 0;
+        for (; k < nb && m < 256; ++k)
+            if (lens[k]) {
+                iov[m].iov_base = bufs[k];
+                iov[m++].iov_len = lens[k];
+                bytes += lens[k];
+            }
+        --k;
+        size_t done = 0;
+        while (done < bytes) {
+            const ssize_t w = pwritev(fd, iov, m, off);
+            if (w <= 0)
+                gt_abort("write error on %s: %s", path, strerror(errno));
+            done += (size_t)w;
+            off += (off_t)w;
+            size_t skip = (size_t)w; /* (a short write: drop what went out) */
+            int i = 0;
+            while (i < m && skip >= iov[i].iov_len)
+                skip -= iov[i++].iov_len;
+            memmove(iov, iov + i, (size_t)(m - i) * sizeof(struct iovec));
+            m -= i;
+            if (m) {
+                iov[0].iov_base = (char *)iov[0].iov_base + skip;
+                iov[0].iov_len -= skip;
+            }
+        }
     }
     if (close(fd) != 0)
         gt_abort("close failed on %s", path);

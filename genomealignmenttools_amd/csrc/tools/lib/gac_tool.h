@@ -145,6 +145,9 @@ void gt_ranks_clear_markers(const gt_ranks *rk, const char *path);
  * (axtChain: rank 0 writes its own chains only) */
 int gt_ranks_solo(void);
 void gt_ranks_place(const gt_ranks *rk, const char *path, const char *buf, size_t len);
+/* the same for a part held as n buffers (the buffers are left to the caller) */
+void gt_ranks_place_bufs(const gt_ranks *rk, const char *path, char *const *bufs,
+                         const size_t *lens, int64_t n);
 void gt_ranks_finish(const gt_ranks *rk, const char *path);
 
 /* ---- options ---- */

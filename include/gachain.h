@@ -456,6 +456,13 @@ int gac_net_write(const gac_net *net, int side, const int64_t *t_scores, const c
  * chainNet -nranks formats a rank's part in memory, then writes it in place). */
 int gac_net_write_file(const gac_net *net, int side, const int64_t *t_scores, FILE *f,
                        const char *const *meta, int32_t n_meta);
+/* The same text formatted on all threads and returned as buffers (chainNet
+ * -nranks writes a rank's part in place from them, with no staging copy):
+ * *bufs[0 .. *nbufs) in order, malloc'ed (free each and the arrays), *lens
+ * their lengths; the n_meta '#' lines are the first buffer. */
+int gac_net_format(const gac_net *net, int side, const int64_t *t_scores,
+                   const char *const *meta, int32_t n_meta, char ***bufs, size_t **lens,
+                   int64_t *nbufs);
 /* The target net in two phases, for -rescore: _begin formats everything but
  * the rescored partial fills' scores (which fills print does not depend on
  * them when minScore <= 1: a rescored score is >= 1, chainNet.c:244-245),
