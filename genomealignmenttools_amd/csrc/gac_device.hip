@@ -3,6 +3,7 @@
 // There is deliberately no host fallback: every scoring entry point runs the
 // HIP kernels of gac_kernels.hip on a gfx950 device or returns an error.
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 #include <time.h>
 
 #include <stdint.h>
@@ -295,6 +296,7 @@ struct gac_chainset {
     // the window-search index (tspan, bucket) is built: at upload
     // (GAC_UP_INDEX=eager) or at the first call that searches windows
     bool idx_ready = false;
+    int64_t idx_n = 0;  // bucket entries of the index
 };
 
 static void free_whole_plan(gac_chainset *cs) {
@@ -1610,6 +1612,7 @@ static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs)
     const int64_t n = d->n_chains;
     const bool timing = getenv("GAC_TIMING") != nullptr;
     double t_lap = wall_s();
+    const double t_fill0 = t_lap;
     auto lap = [&](const char *what) {
         if (!timing) return;
         const double t = wall_s();
@@ -1619,9 +1622,24 @@ static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs)
     // (not value-initialised: upload_pass1 writes every field of every good
     // chain on its own thread, so the 64 B/chain are first touched in
     // parallel instead of zeroed on this thread -- 320 MB at C5)
+    // (an anonymous mapping of its own: from the heap, its free() at the end
+    // let glibc trim the heap top -- 0.11 s at axtChain's C4 chain scoring,
+    // r05c4t4 -- and the mapping comes back zeroed on first touch anyway)
     const size_t n_rec = (size_t)(n ? n : 1);
-    std::unique_ptr<DChain[]> ch(new DChain[n_rec]);
-    if (!n) memset(ch.get(), 0, sizeof(DChain));
+    struct MapArr {
+        DChain *p;
+        size_t bytes;
+        explicit MapArr(size_t k) : bytes(k * sizeof(DChain)) {
+            void *m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+            p = m == MAP_FAILED ? nullptr : (DChain *)m;
+        }
+        ~MapArr() {
+            if (p) munmap(p, bytes);
+        }
+        DChain *get() const { return p; }
+        DChain &operator[](size_t i) const { return p[i]; }
+    } ch(n_rec);
+    if (!ch.get()) return gac_fail(GAC_E_HIP, "gac_chains_upload: out of host memory");
     // tasks: contiguous chain ranges of about equal blocks + chains
     const int nt = std::max(1, std::min(64, gac_host_threads()));
     const int ntask = (int)std::min<int64_t>(std::max<int64_t>(n, 1), 8 * nt);
@@ -1692,8 +1710,16 @@ static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs)
     hipError_t e = ensure_buf((void **)&cs->chains, &cs->cap_chains, n_rec, sizeof(DChain));
     if (e == hipSuccess) e = ensure_buf((void **)&cs->blk, &cs->cap_blocks, nb + 8, sizeof(int4));
     if (e == hipSuccess) e = ensure_buf((void **)&cs->blk12, &cs->cap_blk12, nb + 8, sizeof(Blk12));
-    if (e == hipSuccess) e = ensure_buf((void **)&cs->tspan, &cs->cap_tspan, nb + 8, sizeof(int2));
-    if (e == hipSuccess)
+    // (the window-search index -- spans, bucket entries -- is allocated
+    // with the index itself: ensure_index, or here when it is built eagerly)
+    static const bool eager = [] {
+        const char *v = getenv("GAC_UP_INDEX");
+        return v && !strcmp(v, "eager");
+    }();
+    cs->idx_n = idx_n;
+    if (e == hipSuccess && eager)
+        e = ensure_buf((void **)&cs->tspan, &cs->cap_tspan, nb + 8, sizeof(int2));
+    if (e == hipSuccess && eager)
         e = ensure_buf((void **)&cs->bucket, &cs->cap_idx, (size_t)std::max<int64_t>(idx_n, 1), 4);
     if (e == hipSuccess)
         e = ensure_buf((void **)&cs->d_stage, &cs->cap_stage, std::max<size_t>(3 * nb, 1), 4);
@@ -1725,10 +1751,6 @@ static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs)
     const UploadGaps G = gaps ? upload_gaps(c, cs->blk12) : UploadGaps{};
     // the window-search index only on demand: chainNet -rescore hands its
     // windows over and whole chains need none (GAC_UP_INDEX=eager: now)
-    static const bool eager = [] {
-        const char *v = getenv("GAC_UP_INDEX");
-        return v && !strcmp(v, "eager");
-    }();
     if (e == hipSuccess && rc == GAC_OK)
         e = launch_build_flat(d_bt, d_bt + nb, d_bt + 2 * nb, (int64_t)nb, cs->chains, n, cs->d_coff,
                               cs->d_tile_c0, cs->d_crun, c->g[0].d_nrun, c->g[0].n_nrun,
@@ -1738,6 +1760,8 @@ static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs)
     if (e == hipSuccess && rc == GAC_OK && gaps) cs->gap_version = c->gap_version;
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     lap("device build + sync");
+    if (timing)
+        fprintf(stderr, "[gac_chains_upload] laps from the fill's start: %.3f s\n", wall_s() - t_fill0);
     if (rc != GAC_OK) return rc;
     if (e != hipSuccess) return gac_fail(GAC_E_HIP, "chain upload failed: %s", hipGetErrorString(e));
     return GAC_OK;
@@ -1746,17 +1770,25 @@ static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs)
 extern "C" int gac_chains_upload(gac_ctx *c, const gac_chainset_desc *d, gac_chainset **out) {
     gac_clear_error();
     if (!c || !d || !out) return gac_fail(GAC_E_ARG, "gac_chains_upload: NULL argument");
+    const double t_in = wall_s();
     CTX_LOCK(c);
+    if (getenv("GAC_TIMING"))
+        fprintf(stderr, "[gac_chains_upload] context lock          %.3f s\n", wall_s() - t_in);
     *out = nullptr;
     gac_chainset *cs = new gac_chainset();
     cs->ctx = c;
     c->sets.push_back(cs);
+    const double t_f = wall_s();
     const int rc = chains_fill(c, d, cs);
+    const double t_r = wall_s();
     if (rc != GAC_OK) {
         gac_chains_free(cs);
         return rc;
     }
     *out = cs;
+    if (getenv("GAC_TIMING"))
+        fprintf(stderr, "[gac_chains_upload] total                 %.3f s (before the fill %.3f, "
+                        "fill %.3f)\n", wall_s() - t_in, t_f - t_in, t_r - t_f);
     return GAC_OK;
 }
 
@@ -1903,6 +1935,8 @@ static int ensure_index(gac_ctx *c, const gac_chainset *cs_in, hipStream_t s) {
     gac_chainset *cs = const_cast<gac_chainset *>(cs_in);
     if (cs->idx_ready || (cs->n_blocks == 0 && cs->n_chains == 0)) return GAC_OK;
     const int64_t nb = cs->n_blocks;
+    HIPCHK(ensure_buf((void **)&cs->tspan, &cs->cap_tspan, (size_t)nb + 8, sizeof(int2)));
+    HIPCHK(ensure_buf((void **)&cs->bucket, &cs->cap_idx, (size_t)std::max<int64_t>(cs->idx_n, 1), 4));
     const int32_t *d_bt = cs->d_stage;
     HIPCHK(launch_build_index(d_bt, d_bt + nb, d_bt + 2 * nb, nb, cs->chains, cs->n_chains,
                               cs->d_coff, cs->d_tile_c0, cs->tspan, cs->bucket, s));
@@ -2097,6 +2131,8 @@ static int srv_ensure(gac_ctx *c, const gac_chainset *cs, uint32_t flags) {
         long long dummy = 0;
         if ((rc = prepare_args(c, cs, 1, flags, &dummy, c->stream, a0)) != GAC_OK) return rc;
         if ((rc = ensure_index(c, cs, c->stream)) != GAC_OK) return rc;
+        a0.tspan = cs->tspan;  // (allocated with the index)
+        a0.bucket = cs->bucket;
         HIPCHK(hipStreamSynchronize(c->stream));  // (the gaps and the index, before the grid)
     }
     if ((rc = srv_pool(c, 1)) != GAC_OK) return rc;
@@ -2170,6 +2206,8 @@ static int score_device(gac_ctx *c, const gac_chainset *cs, const Range *d_range
     int rc = prepare_args(c, cs, n, flags, d_l, s, a_base);
     if (rc != GAC_OK || n == 0) return rc;
     if (!d_wins && (rc = ensure_index(c, cs, s)) != GAC_OK) return rc;
+    a_base.tspan = cs->tspan;  // (allocated with the index)
+    a_base.bucket = cs->bucket;
     rc = score_device_split(c, a_base, d_ranges, d_wins, n, d_g, d_l, d_ali, s);
     if (hipEventRecord(c->ws_ev, s) == hipSuccess) c->ws_last = s;
     return rc;
@@ -2657,6 +2695,8 @@ extern "C" int gac_score_ranges(gac_ctx *c, const gac_chainset *cs, const gac_ra
         int rc = prepare_args(c, cs, n, flags, local, s, a);
         if (rc != GAC_OK) return rc;
         if ((rc = ensure_index(c, cs, s)) != GAC_OK) return rc;
+        a.tspan = cs->tspan;  // (allocated with the index)
+        a.bucket = cs->bucket;
         memcpy(c->h_small_in, ranges, (size_t)n * sizeof(Range));
         HIPCHK(launch_small(a, c->d_small_in, c->d_small_out, s));
         HIPCHK(hipStreamSynchronize(s));

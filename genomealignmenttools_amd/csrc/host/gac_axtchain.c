@@ -3742,15 +3742,18 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
         free(G.task);
         free(G.c0);
         free(G.x0);
+        stage("chains gathered for scoring", &tclock);
         gac_chainset_desc d = {nc, ct, cq, cs, coff, ncb, bt, bq, bs};
         gac_chainset *set = NULL;
         if (nc > 0) { /* whole chains: chainCalcScore of each (axtChain.c:300-305) */
             rc = gac_chains_upload(ctx, &d, &set);
+            stage("chains to HBM", &tclock);
             if (rc == GAC_OK)
                 rc = gac_score_chains(ctx, set, 0, gsc, NULL, gali);
+            stage("GPU chain scores", &tclock);
             gac_chains_free(set);
         }
-        stage("GPU chain scores", &tclock);
+        stage("chain set freed", &tclock);
         if (rc == GAC_OK) {
             /* minScore filter; slAddHead onto the master list (reversed),
              * then slSort(chainCmpScore) -- stable */
