@@ -15,6 +15,7 @@
 #include <atomic>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <memory>
 #include <vector>
@@ -1622,24 +1623,28 @@ static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs)
     // (not value-initialised: upload_pass1 writes every field of every good
     // chain on its own thread, so the 64 B/chain are first touched in
     // parallel instead of zeroed on this thread -- 320 MB at C5)
-    // (an anonymous mapping of its own: from the heap, its free() at the end
-    // let glibc trim the heap top -- 0.11 s at axtChain's C4 chain scoring,
-    // r05c4t4 -- and the mapping comes back zeroed on first touch anyway)
+    // (freed on a detached thread when the fill returns: freeing it here
+    // waited ~0.11 s at axtChain's C4 chain scoring -- glibc trimming the
+    // heap top behind other threads' unmapping, r05c4t4; a private mapping
+    // instead was slower still, r05c4t5)
     const size_t n_rec = (size_t)(n ? n : 1);
-    struct MapArr {
+    struct LateArr {
         DChain *p;
-        size_t bytes;
-        explicit MapArr(size_t k) : bytes(k * sizeof(DChain)) {
-            void *m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-            p = m == MAP_FAILED ? nullptr : (DChain *)m;
-        }
-        ~MapArr() {
-            if (p) munmap(p, bytes);
+        explicit LateArr(size_t k) : p((DChain *)malloc(k * sizeof(DChain))) {}
+        ~LateArr() {
+            DChain *q = p;
+            if (!q) return;
+            try {
+                std::thread([q] { free(q); }).detach();
+            } catch (...) {
+                free(q);
+            }
         }
         DChain *get() const { return p; }
         DChain &operator[](size_t i) const { return p[i]; }
     } ch(n_rec);
     if (!ch.get()) return gac_fail(GAC_E_HIP, "gac_chains_upload: out of host memory");
+    if (!n) memset(ch.get(), 0, sizeof(DChain));
     // tasks: contiguous chain ranges of about equal blocks + chains
     const int nt = std::max(1, std::min(64, gac_host_threads()));
     const int ntask = (int)std::min<int64_t>(std::max<int64_t>(n, 1), 8 * nt);
