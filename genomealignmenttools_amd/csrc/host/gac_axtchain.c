@@ -3172,6 +3172,39 @@ static double now_s(void) {
     return ts.tv_sec + 1e-9 * ts.tv_nsec;
 }
 
+/* free() of n blocks on a detached thread (the caller goes on; the frees
+ * unmap GBs at C4 scale) */
+typedef struct late_free {
+    int n;
+    void *p[];
+} late_free;
+
+static void *late_free_thread(void *arg) {
+    late_free *L = arg;
+    for (int i = 0; i < L->n; ++i)
+        free(L->p[i]);
+    free(L);
+    return NULL;
+}
+
+static void free_later(void *const *p, int n) {
+    late_free *L = malloc(sizeof(late_free) + (size_t)(n > 0 ? n : 1) * sizeof(void *));
+    if (!L) {
+        for (int i = 0; i < n; ++i)
+            free(p[i]);
+        return;
+    }
+    L->n = n;
+    memcpy(L->p, p, (size_t)n * sizeof(void *));
+    pthread_attr_t at;
+    pthread_attr_init(&at);
+    pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
+    pthread_t th;
+    if (pthread_create(&th, &at, late_free_thread, L) != 0)
+        late_free_thread(L);
+    pthread_attr_destroy(&at);
+}
+
 static void stage(const char *what, double *t) {
     static int on = -1;
     if (on < 0) {
@@ -3789,25 +3822,25 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
             run_threads(nthreads, out_thread, &O);
             free(k);
         }
-        free(ct);
-        free(cq);
-        free(cs);
-        free(cpair);
-        free(coff);
-        free(bt);
-        free(bq);
-        free(bs);
-        free(gsc);
-        free(gali);
+        /* the scoring set's host arrays and every pair's chains (GBs at C4):
+         * freed on a detached thread, off the caller's path */
+        void *big[] = {ct, cq, cs, cpair, coff, bt, bq, bs, gsc, gali};
+        free_later(big, (int)(sizeof(big) / sizeof(big[0])));
     }
-    for (int64_t p = 0; p < np; ++p) {
-        free(po[p].coff);
-        free(po[p].bt);
-        free(po[p].bq);
-        free(po[p].bs);
-        free(po[p].details);
+    {
+        void **pp = malloc((size_t)(5 * np + 1) * sizeof(void *));
+        int64_t k = 0;
+        for (int64_t p = 0; p < np; ++p) {
+            pp[k++] = po[p].coff;
+            pp[k++] = po[p].bt;
+            pp[k++] = po[p].bq;
+            pp[k++] = po[p].bs;
+            pp[k++] = po[p].details;
+        }
+        pp[k++] = po;
+        free_later(pp, (int)k);
+        free(pp);
     }
-    free(po);
     stage("filter + sort", &tclock);
     if (rc == GAC_OK)
         *out = R;
