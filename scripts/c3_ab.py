@@ -38,14 +38,14 @@ def main():
     for rep in range(reps):
         for tag, env in variants:
             outs = [p(f"{tag}.chain"), p(f"{tag}.bed")]
-            cmd = [bench.CC_TOOL, p("in.chain"), p("t.2bit"), p("q.2bit")] + outs + opts + ["-verbose=1"]
+            cmd = [bench.CC_TOOL, p("in.chain"), p("t.2bit"), p("q.2bit")] + outs + opts + ["-verbose=" + os.environ.get("C3_VERBOSE", "1")]
             e2 = dict(env, GAC_TIMING="1")
             t0 = time.perf_counter()
             r = bench.run_tool(cmd, outs, env=e2)
             dt = time.perf_counter() - t0
             same = all(filecmp.cmp(a, b, False) for a, b in zip(outs, ro))
             lines = [x.strip() for x in r.stderr.splitlines()
-                     if x.startswith(("GPU:", "[stage] 4.", "[stage] 1."))]
+                     if x.startswith(("GPU", "[stage] 4.", "[stage] 1."))]
             print(f"{tag} rep {rep}: {dt * 1e3:.0f} ms identical={same} | " + " | ".join(lines),
                   flush=True)
             if not same:
