@@ -744,6 +744,28 @@ typedef struct ax_part {
     int32_t *bt, *bq, *bs;
 } ax_part;
 
+/* rank 0's output: chain j of the merged order is chain[j] of part[j],
+ * written with id j + 1 (chainWrite order) */
+typedef struct ax_out {
+    const ax_part *parts;
+    int32_t *part;
+    int64_t *chain;
+    pair *const *ord;
+    const uint8_t *strand;
+    int32_t *tsize, *qsize; /* per pair */
+} ax_out;
+
+static void out_chain(FILE *f, int64_t j, void *arg) {
+    const ax_out *O = arg;
+    const ax_part *P = &O->parts[O->part[j]];
+    const int64_t c = O->chain[j];
+    const int32_t p = P->pair[c];
+    const int64_t b0 = P->off[c];
+    gt_write_chain_raw(f, P->score[c], O->ord[p]->tname, O->tsize[p], P->ts[c], P->te[c],
+                       O->ord[p]->qname, O->qsize[p], O->strand[p], P->qs[c], P->qe[c],
+                       (int32_t)(j + 1), P->bt + b0, P->bq + b0, P->bs + b0, P->off[c + 1] - b0);
+}
+
 static void lpt_deal(const int64_t *boff, int64_t np, int nranks, int32_t *owner) {
     int64_t *ix = malloc((size_t)(np ? np : 1) * 8), *load = calloc((size_t)nranks, 8);
     for (int64_t i = 0; i < np; ++i)
@@ -1054,8 +1076,21 @@ static void run_job(int argc, char *argv[], ax_batch *B) {
             unlink(part);
         }
     }
+    /* the merged order first (part, chain), then the text formatted on all
+     * threads in runs and written in order (ids = output positions) */
+    int64_t n_out = 0;
+    for (int r = 0; r < rk.n; ++r)
+        n_out += parts[r].n;
+    ax_out O = {parts, malloc((size_t)(n_out ? n_out : 1) * 4), malloc((size_t)(n_out ? n_out : 1) * 8),
+                ord, strand, NULL, NULL};
+    O.tsize = malloc((size_t)(np ? np : 1) * 4);
+    O.qsize = malloc((size_t)(np ? np : 1) * 4);
+    for (int64_t p = 0; p < np; ++p) {
+        O.tsize[p] = gac_genome_seq_size(ctx, GAC_T, tseq[p]);
+        O.qsize[p] = gac_genome_seq_size(ctx, GAC_Q, qseq[p]);
+    }
     int64_t *head = calloc((size_t)rk.n, 8);
-    for (int32_t id = 1;; ++id) {
+    for (int64_t j = 0;; ++j) {
         int best = -1;
         for (int r = 0; r < rk.n; ++r) {
             if (head[r] >= parts[r].n)
@@ -1070,16 +1105,16 @@ static void run_job(int argc, char *argv[], ax_batch *B) {
         }
         if (best < 0)
             break;
-        const ax_part *P = &parts[best];
-        const int64_t c = head[best]++;
-        const int32_t p = P->pair[c];
-        const int64_t b0 = P->off[c];
-        gt_write_chain_raw(f, P->score[c], ord[p]->tname, gac_genome_seq_size(ctx, GAC_T, tseq[p]),
-                           P->ts[c], P->te[c], ord[p]->qname, gac_genome_seq_size(ctx, GAC_Q, qseq[p]),
-                           strand[p], P->qs[c], P->qe[c], id, P->bt + b0, P->bq + b0, P->bs + b0,
-                           P->off[c + 1] - b0);
+        O.part[j] = best;
+        O.chain[j] = head[best]++;
     }
     free(head);
+    fflush(f);
+    gt_par_write(f, n_out, out_chain, &O);
+    free(O.part);
+    free(O.chain);
+    free(O.tsize);
+    free(O.qsize);
     gt_careful_close(f, out_path);
     gt_ranks_done(&rk);
     gt_verbose(2, "chaining + writing in %.3f s\n", wall() - t0);
