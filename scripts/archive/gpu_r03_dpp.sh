@@ -11,5 +11,5 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_scoring.py -m gpu -x -v --t
 tail -1 $out/gpu_tests.txt
 timeout -k 10 600 python -u bench.py --steps 2 --warmup 1 --no-c2 --no-cpu-baseline \
     --kernel-steps 20 --no-pmc > $out/bench.json 2> $out/bench.err || exit $?
-timeout -k 10 600 python3 scripts/pmc_ab.py $out scorechain ${PMC_SPECS:-default=} \
+timeout -k 10 600 python3 scripts/archive/pmc_ab.py $out scorechain ${PMC_SPECS:-default=} \
     > $out/pmc.log 2>&1 || exit $?

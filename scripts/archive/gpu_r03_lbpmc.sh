@@ -8,5 +8,5 @@ mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 600 python -u bench.py --steps 1 --warmup 0 --no-c2 --no-cpu-baseline \
     --no-kernel > $out/bench_gen.json 2> $out/bench_gen.err || exit $?
-timeout -k 10 900 python -u scripts/pmc_ab.py $out fills base=GAC_PLAN_LB=0 lb=GAC_PLAN_LB=1 \
+timeout -k 10 900 python -u scripts/archive/pmc_ab.py $out fills base=GAC_PLAN_LB=0 lb=GAC_PLAN_LB=1 \
     > $out/pmc_fills.txt 2>&1 || exit $?

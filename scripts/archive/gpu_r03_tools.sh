@@ -11,5 +11,5 @@ HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 timeout -k 10 400 python -u scripts/bench_tools.py axtchain --blocks 50000000 --seed 7 --no-ref \
     > $out/c4.json 2> $out/c4.err || exit $?
-timeout -k 10 400 python -u scripts/c3_probe.py $out/c3.txt > $out/c3.log 2>&1 || exit $?
+timeout -k 10 400 python -u scripts/archive/c3_probe.py $out/c3.txt > $out/c3.log 2>&1 || exit $?
 echo "tools ok"

@@ -1,5 +1,5 @@
 // Probe (analysis only): per-XCD set-associative LRU model of the 4 MiB L2s
-// for scripts/traffic_sim/sim.py.  Input: uint64 pairs {xcd, line} in issue
+// for scripts/archive/traffic_sim/sim.py.  Input: uint64 pairs {xcd, line} in issue
 // order; line >> 40 tags the region.  Prints the misses per region.
 // per-XCD set-associative LRU L2 simulator: input = uint64 keys sorted by (xcd, time);
 // each record: uint32 xcd, uint64 line. Reports misses per region (line>>40).
