@@ -740,6 +740,9 @@ int main(int argc, char *argv[]) {
         gt_free_late(r, nrb * sizeof(gac_window));
         gt_free_late(rix, nrb * 8);
         gac_mark("fill arrays released");
+        /* the block coordinates are read by nothing after the rescoring */
+        if (!multi)
+            gt_chains_drop_blocks_async(&c);
     }
     wo[0].tscores = tscores;
     write_net(&wo[0]);

@@ -599,6 +599,34 @@ static void *drop_thread(void *arg) {
     return NULL;
 }
 
+static void *drop_detached(void *arg) {
+    drop_thread(arg);
+    free(arg);
+    return NULL;
+}
+
+void gt_chains_drop_blocks_async(gt_chains *c) {
+    const char *e = getenv("GAC_EARLY_FREE");
+    if (e && *e == '0')
+        return;
+    drop_job *J = calloc(1, sizeof(drop_job));
+    if (!J)
+        return;
+    const size_t nb = (size_t)c->nb;
+    J->p[0] = c->bt, J->len[0] = nb * 4;
+    J->p[1] = c->bq, J->len[1] = nb * 4;
+    J->p[2] = c->bs, J->len[2] = nb * 4;
+    J->n = 3;
+    atomic_init(&J->next, 0);
+    pthread_t th;
+    pthread_attr_t at;
+    pthread_attr_init(&at);
+    pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
+    if (pthread_create(&th, &at, drop_detached, J) != 0)
+        free(J);
+    pthread_attr_destroy(&at);
+}
+
 void gt_chains_drop_pages(gt_chains *c) {
     const char *e = getenv("GAC_FREE_MADV");
     if (e && *e == '0')

@@ -224,6 +224,9 @@ typedef struct gt_chains {
  * (madvise under the mm's read lock; the kernel's exit would free them on
  * one core).  The set must not be used afterwards. */
 void gt_chains_drop_pages(gt_chains *c);
+/* the block arrays' pages dropped now on a detached thread (the caller no
+ * longer reads bt/bq/bs; the arrays stay allocated); GAC_EARLY_FREE=0: not */
+void gt_chains_drop_blocks_async(gt_chains *c);
 /* large temporary arrays released later, off the critical path: with
  * GAC_LATE_FREE=1 (default) gt_free_late keeps them until gt_free_late_all,
  * which drops their pages on all threads (madvise, read lock) and frees
