@@ -2264,24 +2264,55 @@ static char *put_int(char *p, int64_t v) {
                                   "25262728293031323334353637383940414243444546474849"
                                   "50515253545556575859606162636465666768697071727374"
                                   "75767778798081828384858687888990919293949596979899";
-    char tmp[24], *e = tmp + sizeof(tmp), *q = e;
     uint64_t u = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
-    while (u >= 100) { /* two digits per step */
-        const unsigned r = (unsigned)(u % 100);
-        u /= 100;
+    if (v < 0)
+        *p++ = '-';
+    /* the digit count first, then the digits straight into place, two per
+     * step (no staging copy: a variable-length memcpy is a library call per
+     * number, and the nets print ~150 M of them); 32-bit arithmetic when the
+     * value fits, as nearly all coordinates do */
+    static const uint32_t p10[10] = {0u,      10u,      100u,      1000u,      10000u,
+                                     100000u, 1000000u, 10000000u, 100000000u, 1000000000u};
+    if (u >> 32) {
+        int nd = 1;
+        for (uint64_t t = 10; nd < 20 && u >= t; t *= 10)
+            ++nd;
+        char *const e = p + nd;
+        char *q = e;
+        while (u >= 100) {
+            const unsigned r = (unsigned)(u % 100);
+            u /= 100;
+            q -= 2;
+            memcpy(q, dig2 + 2 * r, 2);
+        }
+        if (u >= 10) {
+            q -= 2;
+            memcpy(q, dig2 + 2 * u, 2);
+        } else {
+            *--q = (char)('0' + u);
+        }
+        return e;
+    }
+    uint32_t w = (uint32_t)u;
+    int nd = ((32 - __builtin_clz(w | 1)) * 1233) >> 12; /* floor(log10) or one less */
+    nd += (nd < 10 && w >= p10[nd]) ? 1 : 0;
+    if (nd == 0)
+        nd = 1;
+    char *const e = p + nd;
+    char *q = e;
+    while (w >= 100) {
+        const uint32_t r = w % 100;
+        w /= 100;
         q -= 2;
         memcpy(q, dig2 + 2 * r, 2);
     }
-    if (u >= 10) {
+    if (w >= 10) {
         q -= 2;
-        memcpy(q, dig2 + 2 * u, 2);
+        memcpy(q, dig2 + 2 * w, 2);
     } else {
-        *--q = (char)('0' + u);
+        *--q = (char)('0' + w);
     }
-    if (v < 0)
-        *p++ = '-';
-    memcpy(p, q, (size_t)(e - q));
-    return p + (e - q);
+    return e;
 }
 
 static char *put_str(char *p, const char *s) {

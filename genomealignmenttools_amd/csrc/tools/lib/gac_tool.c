@@ -13,6 +13,7 @@
 #include <signal.h>
 #include <sys/stat.h>
 #include <sys/uio.h>
+#include <sys/resource.h>
 #include <unistd.h>
 #include <sys/syscall.h>
 #include <pthread.h>
@@ -126,11 +127,20 @@ void gt_stage(const char *what) {
     clock_gettime(CLOCK_PROCESS_CPUTIME_ID, &cs);
     const double cpu = cs.tv_sec + 1e-9 * cs.tv_nsec;
     static double last_cpu = 0;
+    /* and its system time and page faults (first touches of new memory) */
+    struct rusage ru;
+    getrusage(RUSAGE_SELF, &ru);
+    const double sys = ru.ru_stime.tv_sec + 1e-6 * ru.ru_stime.tv_usec;
+    static double last_sys = 0;
+    static long last_flt = 0;
     if (last >= 0 && what && show)
-        fprintf(stderr, "[stage] %-32s %8.3f s  (cpu %.3f s, %.1f busy)\n", what, now - last,
-                cpu - last_cpu, now > last ? (cpu - last_cpu) / (now - last) : 0.0);
+        fprintf(stderr, "[stage] %-32s %8.3f s  (cpu %.3f s, %.1f busy; sys %.3f s, %ld faults)\n", what,
+                now - last, cpu - last_cpu, now > last ? (cpu - last_cpu) / (now - last) : 0.0,
+                sys - last_sys, ru.ru_minflt - last_flt);
     last = now;
     last_cpu = cpu;
+    last_sys = sys;
+    last_flt = ru.ru_minflt;
 }
 
 static double now_s(void) {
@@ -2239,24 +2249,55 @@ static char *put_int(char *p, int64_t v) {
                                   "25262728293031323334353637383940414243444546474849"
                                   "50515253545556575859606162636465666768697071727374"
                                   "75767778798081828384858687888990919293949596979899";
-    char tmp[24], *e = tmp + sizeof(tmp), *q = e;
     uint64_t u = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
-    while (u >= 100) { /* two digits per step */
-        const unsigned r = (unsigned)(u % 100);
-        u /= 100;
+    if (v < 0)
+        *p++ = '-';
+    /* the digit count first, then the digits straight into place, two per
+     * step (no staging copy: a variable-length memcpy is a library call per
+     * number, and the nets print ~150 M of them); 32-bit arithmetic when the
+     * value fits, as nearly all coordinates do */
+    static const uint32_t p10[10] = {0u,      10u,      100u,      1000u,      10000u,
+                                     100000u, 1000000u, 10000000u, 100000000u, 1000000000u};
+    if (u >> 32) {
+        int nd = 1;
+        for (uint64_t t = 10; nd < 20 && u >= t; t *= 10)
+            ++nd;
+        char *const e = p + nd;
+        char *q = e;
+        while (u >= 100) {
+            const unsigned r = (unsigned)(u % 100);
+            u /= 100;
+            q -= 2;
+            memcpy(q, dig2 + 2 * r, 2);
+        }
+        if (u >= 10) {
+            q -= 2;
+            memcpy(q, dig2 + 2 * u, 2);
+        } else {
+            *--q = (char)('0' + u);
+        }
+        return e;
+    }
+    uint32_t w = (uint32_t)u;
+    int nd = ((32 - __builtin_clz(w | 1)) * 1233) >> 12; /* floor(log10) or one less */
+    nd += (nd < 10 && w >= p10[nd]) ? 1 : 0;
+    if (nd == 0)
+        nd = 1;
+    char *const e = p + nd;
+    char *q = e;
+    while (w >= 100) {
+        const uint32_t r = w % 100;
+        w /= 100;
         q -= 2;
         memcpy(q, dig2 + 2 * r, 2);
     }
-    if (u >= 10) {
+    if (w >= 10) {
         q -= 2;
-        memcpy(q, dig2 + 2 * u, 2);
+        memcpy(q, dig2 + 2 * w, 2);
     } else {
-        *--q = (char)('0' + u);
+        *--q = (char)('0' + w);
     }
-    if (v < 0)
-        *p++ = '-';
-    memcpy(p, q, (size_t)(e - q));
-    return p + (e - q);
+    return e;
 }
 
 /* block lines "size\tdt\tdq" and the last "size", then the blank line

@@ -5,6 +5,7 @@ reference's sha256 (tests/golden/fullscale/c5.json) after each variant's last
 run; then one GAC_TIMING run per variant for its stage laps and marks.
 usage: c5_ab.py REPS tag:ENV=v,ENV2=v ..."""
 import os
+import resource
 import sys
 import time
 
@@ -42,10 +43,14 @@ def main():
             for o in outs:
                 if os.path.exists(o):
                     os.remove(o)
+            ru0 = resource.getrusage(resource.RUSAGE_CHILDREN)
             t0 = time.perf_counter()
             bench.run_tool(cmd, [], env=env)
             times[tag].append((time.perf_counter() - t0) * 1e3)
-            print(f"{tag} rep {rep}: {times[tag][-1]:.0f} ms", flush=True)
+            ru1 = resource.getrusage(resource.RUSAGE_CHILDREN)
+            print(f"{tag} rep {rep}: {times[tag][-1]:.0f} ms (user {ru1.ru_utime - ru0.ru_utime:.2f} s, "
+                  f"sys {ru1.ru_stime - ru0.ru_stime:.2f} s, minor faults "
+                  f"{ru1.ru_minflt - ru0.ru_minflt})", flush=True)
     for tag, env, tool in variants:
         r = bench.run_tool(cmd_of(tool) + ["-verbose=2"], outs, env=dict(env, GAC_TIMING="1"))
         par = bench.full_parity("c5", {"in_chain_sha256": os.path.join(d, "in.chain"),
