@@ -918,45 +918,6 @@ void gac_obuf_printf(gac_obuf *o, const char *fmt, ...) {
     o->n += (size_t)k;
 }
 
-/* Run buffers recycled between the writer and the formatters (par_output):
- * a run's buffer goes back to the pool once written, so after the first few
- * runs the formatters write into memory that is already mapped and large
- * enough -- no page faults, reallocations or unmaps per run (a C5 net is
- * ≈700 runs of 1-2 MB). */
-typedef struct obuf_pool {
-    pthread_mutex_t mu;
-    char *p[64];
-    size_t cap[64];
-    int n;
-} obuf_pool;
-
-static gac_obuf pool_get(obuf_pool *P) {
-    gac_obuf o = {NULL, 0, 0};
-    if (!P)
-        return o;
-    pthread_mutex_lock(&P->mu);
-    if (P->n > 0) {
-        --P->n;
-        o.p = P->p[P->n];
-        o.cap = P->cap[P->n];
-    }
-    pthread_mutex_unlock(&P->mu);
-    return o;
-}
-
-static void pool_put(obuf_pool *P, char *b, size_t cap) {
-    if (P && b) {
-        pthread_mutex_lock(&P->mu);
-        if (P->n < 64) {
-            P->p[P->n] = b;
-            P->cap[P->n++] = cap;
-            b = NULL;
-        }
-        pthread_mutex_unlock(&P->mu);
-    }
-    free(b);
-}
-
 typedef struct po_job {
     int64_t nr;
     void (*fn)(FILE *, int64_t, void *);
@@ -964,8 +925,6 @@ typedef struct po_job {
     void *arg;
     char **buf;
     size_t *len;
-    size_t *cap;     /* (with a pool) each run's buffer capacity */
-    obuf_pool *pool; /* NULL: the buffers are the caller's (par_format) */
     _Atomic int *ready;
     _Atomic int64_t next;
     _Atomic int oom;
@@ -978,12 +937,10 @@ static void *po_thread(void *p) {
         if (r >= J->nr)
             break;
         if (J->fn_buf) {
-            gac_obuf o = pool_get(J->pool);
+            gac_obuf o = {NULL, 0, 0};
             J->fn_buf(&o, r, J->arg);
             J->buf[r] = o.p;
             J->len[r] = o.n;
-            if (J->cap)
-                J->cap[r] = o.cap;
             atomic_store_explicit(&J->ready[r], 1, memory_order_release);
             continue;
         }
@@ -1010,8 +967,6 @@ static int par_format(int64_t nr, void (*fn)(FILE *f, int64_t r, void *arg),
     J.arg = arg;
     J.buf = calloc((size_t)(nr > 0 ? nr : 1), sizeof(char *));
     J.len = calloc((size_t)(nr > 0 ? nr : 1), sizeof(size_t));
-    J.cap = NULL;
-    J.pool = NULL;
     J.ready = calloc((size_t)(nr > 0 ? nr : 1), sizeof(_Atomic int));
     atomic_init(&J.next, 0);
     atomic_init(&J.oom, 0);
@@ -1186,16 +1141,6 @@ static int par_output(FILE *out, int64_t nr, void (*fn)(FILE *f, int64_t r, void
     J.buf = calloc((size_t)nr, sizeof(char *));
     J.len = calloc((size_t)nr, sizeof(size_t));
     J.ready = calloc((size_t)nr, sizeof(_Atomic int));
-    /* GAC_OBUF_POOL=0: a fresh buffer per run, freed once written */
-    const char *pe = getenv("GAC_OBUF_POOL");
-    obuf_pool pool;
-    const int pooled = fn_buf && !(pe && *pe == '0');
-    J.cap = pooled ? calloc((size_t)nr, sizeof(size_t)) : NULL;
-    J.pool = pooled ? &pool : NULL;
-    if (pooled) {
-        pthread_mutex_init(&pool.mu, NULL);
-        pool.n = 0;
-    }
     atomic_init(&J.next, 0);
     atomic_init(&J.oom, 0);
     int nt = gac_host_threads() - 1;
@@ -1268,22 +1213,12 @@ static int par_output(FILE *out, int64_t nr, void (*fn)(FILE *f, int64_t r, void
         }
         if (!bad && writev_all(fd, iov, k) != 0)
             bad = 1;
-        for (int64_t x = r0; x < r; ++x) {
-            if (J.pool)
-                pool_put(J.pool, J.buf[x], J.cap[x]);
-            else
-                free(J.buf[x]);
-        }
+        for (int64_t x = r0; x < r; ++x)
+            free(J.buf[x]);
     }
     for (int i = 0; i < nt; ++i)
         pthread_join(th[i], NULL);
     free(th);
-    if (J.pool) {
-        for (int k = 0; k < pool.n; ++k)
-            free(pool.p[k]);
-        pthread_mutex_destroy(&pool.mu);
-        free(J.cap);
-    }
     free(J.buf);
     free(J.len);
     free((void *)J.ready);
