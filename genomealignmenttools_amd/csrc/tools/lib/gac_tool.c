@@ -2036,49 +2036,11 @@ void gt_read_chains_keep(const char *path, gt_chains *c, double stop_below, int 
     read_chains(path, c, stop_below, keep_meta, tkeep, qkeep);
 }
 
-/* GAC_READ_MMAP=1: a large regular chain file is mapped instead of copied
- * (default: gt_slurp's parallel pread into the heap): the parse threads read the page
- * cache directly, 1.4 GB of copy and of fresh heap pages fewer at C5.  The
- * private writable mapping is followed by a zero page, so the text is
- * NUL-terminated and the parsers' over-reads stay in bounds as with
- * gt_slurp's padding.  *maplen = the mapping's length (0: a heap buffer). */
-static char *map_text(const char *path, size_t *len, size_t *maplen) {
-    *maplen = 0;
-    const char *e = getenv("GAC_READ_MMAP");
-    const size_t n = strlen(path);
-    if (!(e && *e == '1') || strcmp(path, "stdin") == 0 || (n > 3 && strcmp(path + n - 3, ".gz") == 0))
-        return gt_slurp(path, len);
-    const int fd = open(path, O_RDONLY);
-    struct stat st;
-    if (fd < 0 || fstat(fd, &st) != 0 || !S_ISREG(st.st_mode) || st.st_size <= (32 << 20)) {
-        if (fd >= 0)
-            close(fd);
-        return gt_slurp(path, len);
-    }
-    const size_t size = (size_t)st.st_size, pg = (size_t)sysconf(_SC_PAGESIZE);
-    const size_t total = (size + pg - 1) / pg * pg + pg;
-    char *base = mmap(NULL, total, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-    if (base == MAP_FAILED) {
-        close(fd);
-        return gt_slurp(path, len);
-    }
-    char *m = mmap(base, size, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_FIXED, fd, 0);
-    close(fd);
-    if (m == MAP_FAILED) {
-        munmap(base, total);
-        return gt_slurp(path, len);
-    }
-    *len = size;
-    *maplen = total;
-    return m;
-}
-
 typedef struct rc_free_job {
     chunk *K;
     int nk;
     void *cut;
     char *buf;
-    size_t maplen; /* buf is a mapping of this length (0: heap) */
 } rc_free_job;
 
 static void *rc_free_thread(void *arg) {
@@ -2087,10 +2049,7 @@ static void *rc_free_thread(void *arg) {
         gt_chains_free(&F->K[k].c);
     free(F->K);
     free(F->cut);
-    if (F->maplen)
-        munmap(F->buf, F->maplen);
-    else
-        free(F->buf);
+    free(F->buf);
     free(F);
     return NULL;
 }
@@ -2108,8 +2067,8 @@ static void read_chains(const char *path, gt_chains *c, double stop_below, int k
             t_mark = t_;                                                           \
         }                                                                          \
     } while (0)
-    size_t len, maplen;
-    char *buf = map_text(path, &len, &maplen);
+    size_t len;
+    char *buf = gt_slurp(path, &len);
     RC_LAP("read file");
     /* chunk boundaries at "\nchain": 8 chunks per thread, taken in order by
      * the threads as they finish (chain density varies along a file in score
@@ -2243,7 +2202,7 @@ static void read_chains(const char *path, gt_chains *c, double stop_below, int k
      * 0.2 s of page freeing on C5 at 5 M chains) are released off the
      * caller's path */
     rc_free_job *F = malloc(sizeof(*F));
-    *F = (rc_free_job){K, nk, cut, buf, maplen};
+    *F = (rc_free_job){K, nk, cut, buf};
     pthread_attr_t at;
     pthread_attr_init(&at);
     pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);

@@ -61,7 +61,7 @@ def main():
               f"{' '.join(f'{x:.0f}' for x in times[tag])}; nets identical {par['identical']}",
               flush=True)
         for line in r.stderr.splitlines():
-            if line.startswith(("[stage]", "[mark]", "[gac_net_build]", "[gt_read_chains]")):
+            if line.startswith(("[stage]", "[mark]", "[gac_net_build]")):
                 print("   " + line, flush=True)
 
 
