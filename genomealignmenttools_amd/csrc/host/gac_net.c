@@ -158,6 +158,9 @@ typedef struct nwork {
     /* scratch for reversed blocks */
     int32_t *rs, *re, *ros, *roe, *ro; /* ro: each block's other-side start */
     int64_t r_cap;
+    /* finishNet scratch: a gap's fill list gathered in one walk */
+    struct nfill **sf;
+    int64_t sf_cap;
     char pad[64]; /* keep workers' hot fields on separate cache lines */
 } nwork;
 
@@ -925,14 +928,19 @@ static void sort_gap_fills(nwork *w, ngap *g) {
         g->fills = NULL;
         return;
     }
+    /* one walk of the list (its fills are scattered over the arenas: every
+     * link is a miss) into the worker's scratch, then the exact array */
     int cnt = 0;
-    for (nfill *f = g->fill_head; f; f = f->next)
-        ++cnt;
+    for (nfill *f = g->fill_head; f; f = f->next) {
+        if (cnt == w->sf_cap) {
+            w->sf_cap = w->sf_cap ? 2 * w->sf_cap : 4096;
+            w->sf = realloc(w->sf, (size_t)w->sf_cap * sizeof(nfill *));
+        }
+        w->sf[cnt++] = f;
+    }
     g->n_fills = cnt;
     g->fills = arena_alloc(&w->ar, cnt * sizeof(nfill *));
-    cnt = 0;
-    for (nfill *f = g->fill_head; f; f = f->next)
-        g->fills[cnt++] = f;
+    memcpy(g->fills, w->sf, (size_t)cnt * sizeof(nfill *));
     const int32_t level = g->pfill ? g->pfill->level + 1 : 0;
     if (cnt <= 16) { /* fills of one gap are disjoint: starts are distinct */
         for (int i = 1; i < cnt; ++i) {
@@ -981,6 +989,7 @@ static void *free_worker(void *arg) {
         free(w->ros);
         free(w->roe);
         free(w->ro);
+        free(w->sf);
     }
 }
 
@@ -1055,8 +1064,9 @@ static void space_release(gac_net *n) {
         SDROP(w->q, (size_t)w->q_cap * sizeof(sitem));
         SDROP(w->it, (size_t)w->it_cap * sizeof(sitem));
         SDROP(w->cmb, (size_t)w->cmb_cap * sizeof(sitem));
+        SDROP(w->sf, (size_t)w->sf_cap * sizeof(nfill *));
         w->lf_cap = w->in_cap = 0;
-        w->q_cap = w->it_cap = w->cmb_cap = 0;
+        w->q_cap = w->it_cap = w->cmb_cap = w->sf_cap = 0;
     }
 #undef SDROP
     pthread_t th;
