@@ -181,6 +181,10 @@ struct gac_net {
      * (gac_net_get_fills with flags) and read by the output's "reached" pass */
     int64_t *pord[2];
     int pord_ok[2];
+    /* per side, ascending: the pre-order positions of the top-level fills
+     * (where the runs of whole subtrees may start), from finishNet */
+    int64_t *top[2];
+    int64_t n_top[2];
     int sides; /* bit 1 << side: side netted */
     atomic_int free_next; /* gac_net_free's worker cursor */
 };
@@ -1013,6 +1017,8 @@ void gac_net_free(gac_net *n) {
     free(n->order[1]);
     free(n->pord[0]);
     free(n->pord[1]);
+    free(n->top[0]);
+    free(n->top[1]);
     free(n->chain_ali);
     free(n);
 }
@@ -1926,6 +1932,10 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
         for (int64_t k = 0; k < nc; ++k)
             nspan += F.sk[k].n;
         splice_job SJ = {n, malloc((size_t)(nspan ? nspan : 1) * sizeof(ispan)), nspan, 0};
+        for (int side = 0; side < 2; ++side) {
+            n->top[side] = malloc((size_t)(nspan ? nspan : 1) * sizeof(int64_t));
+            n->n_top[side] = 0;
+        }
         {
             int64_t gidx = 0, used = 0, m = 0; /* GAP item; fills taken from its chunk's list */
             for (int64_t k = 0; k < nc; ++k) {
@@ -1934,6 +1944,8 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
                     sk_item *it = &F.sk[k].it[i];
                     if (!it->g) {
                         SJ.sp[m++] = (ispan){&it->f, n->n_order[side], 1, side};
+                        if (it->f->level == 0)
+                            n->top[side][n->n_top[side]++] = n->n_order[side];
                         ++n->n_order[side];
                         continue;
                     }
@@ -2051,6 +2063,18 @@ static void *fills_thread(void *arg) {
 }
 
 static int64_t next_top_level(const gac_net *n, int side, int64_t i) {
+    if (n->top[side]) { /* the first top-level position >= i */
+        const int64_t *t = n->top[side];
+        int64_t lo = 0, hi = n->n_top[side];
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (t[mid] < i)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        return lo < n->n_top[side] ? t[lo] : n->n_order[side];
+    }
     if (n->pord_ok[side]) {
         const int64_t *po = n->pord[side];
         while (i < n->n_order[side] && po[i] >= 0)
