@@ -120,8 +120,12 @@ static void *arena_alloc(arena *a, size_t sz) {
         a->bsize = bs;
         a->used = 0;
     }
-    void *p = a->blocks[a->n - 1] + a->used;
+    char *p = a->blocks[a->n - 1] + a->used;
     a->used += sz;
+    /* the next allocations land just past this one: fetch those lines for
+     * writing now (fresh arena memory: every new line is a miss) */
+    if (a->used + 512 <= a->bsize)
+        __builtin_prefetch(p + sz + 384, 1, 3);
     return p;
 }
 
@@ -2511,6 +2515,8 @@ typedef struct wjob {
     uint8_t *show;   /* passes its own filter */
     uint8_t *more;   /* a later sibling in its gap passes its filter */
     uint8_t *reached;/* printed: passes and every ancestor fill is printed */
+    uint16_t *lvl;   /* (no parent positions) nesting level, for the reached pass */
+    _Atomic int deep; /* a level >= 65535 seen: the reached pass chases parents */
     _Atomic int64_t next;
 } wjob;
 
@@ -2595,6 +2601,12 @@ static void *winfo_thread(void *arg) {
             }
             J->show[i] = (uint8_t)fill_info(J->n, J->side, J->tscore, J->ord[i], &J->score[i],
                                             &J->sub[i]);
+            if (J->lvl) {
+                const int32_t L = J->ord[i]->level;
+                J->lvl[i] = (uint16_t)(L < 65535 ? L : 65535);
+                if (L >= 65535)
+                    atomic_store(&J->deep, 1);
+            }
         }
     }
     return NULL;
@@ -2652,6 +2664,30 @@ static void *wreached_thread(void *arg) {
         if (po) {
             for (int64_t i = a; i < b; ++i)
                 J->reached[i] = J->show[i] && (po[i] < 0 || J->reached[po[i]]);
+            continue;
+        }
+        if (J->lvl && !atomic_load(&J->deep)) {
+            /* pre-order from a top-level fill: a fill's parent is the last
+             * fill before it one level up, so a stack of the last position
+             * per level replaces the parent links */
+            int64_t stk[256], *last = stk;
+            int cap = 256;
+            for (int64_t i = a; i < b; ++i) {
+                const int L = J->lvl[i];
+                if (L >= cap) {
+                    const int nc = L + 256;
+                    int64_t *q = malloc((size_t)nc * sizeof(int64_t));
+                    memcpy(q, last, (size_t)cap * sizeof(int64_t));
+                    if (last != stk)
+                        free(last);
+                    last = q;
+                    cap = nc;
+                }
+                last[L] = i;
+                J->reached[i] = J->show[i] && (L == 0 || J->reached[last[L - 1]]);
+            }
+            if (last != stk)
+                free(last);
             continue;
         }
         for (int64_t i = a; i < b; ++i) {
@@ -2716,6 +2752,9 @@ static void wjob_flags(wjob *J, const gac_net *n, int side, const int64_t *tscor
     J->show = malloc(m);
     J->more = malloc(m);
     J->reached = malloc(m);
+    /* (levels for the reached pass unless the parent positions are known) */
+    J->lvl = n->pord_ok[side] ? NULL : malloc(m * sizeof(uint16_t));
+    atomic_init(&J->deep, 0);
     const int nt = gac_host_threads();
     atomic_init(&J->next, 0);
     gac_run_threads(nt, winfo_thread, J);
@@ -2744,6 +2783,8 @@ static void wjob_free_flags(wjob *J) {
     free(J->show);
     free(J->more);
     free(J->reached);
+    free(J->lvl);
+    J->lvl = NULL;
     J->score = NULL;
     J->sub = NULL;
     J->show = J->more = J->reached = NULL;
