@@ -2515,8 +2515,9 @@ typedef struct wjob {
     uint8_t *show;   /* passes its own filter */
     uint8_t *more;   /* a later sibling in its gap passes its filter */
     uint8_t *reached;/* printed: passes and every ancestor fill is printed */
-    uint16_t *lvl;   /* (no parent positions) nesting level, for the reached pass */
-    _Atomic int deep; /* a level >= 65535 seen: the reached pass chases parents */
+    uint16_t *lvl;   /* nesting level, for the more and reached passes */
+    int32_t *pix;    /* index in its gap's fill list, for the more pass */
+    _Atomic int deep; /* a level >= 65535 seen: both passes chase links instead */
     _Atomic int64_t next;
 } wjob;
 
@@ -2601,12 +2602,11 @@ static void *winfo_thread(void *arg) {
             }
             J->show[i] = (uint8_t)fill_info(J->n, J->side, J->tscore, J->ord[i], &J->score[i],
                                             &J->sub[i]);
-            if (J->lvl) {
-                const int32_t L = J->ord[i]->level;
-                J->lvl[i] = (uint16_t)(L < 65535 ? L : 65535);
-                if (L >= 65535)
-                    atomic_store(&J->deep, 1);
-            }
+            const int32_t L = J->ord[i]->level;
+            J->lvl[i] = (uint16_t)(L < 65535 ? L : 65535);
+            J->pix[i] = J->ord[i]->pidx;
+            if (L >= 65535)
+                atomic_store(&J->deep, 1);
         }
     }
     return NULL;
@@ -2651,6 +2651,64 @@ static int net_write_f(const gac_net *n, int side, const int64_t *tscores, FILE 
 /* "reached" flags: a fill prints when it passes and every ancestor fill
  * prints; parents precede children in pre-order, so runs that start at
  * top-level fills (whole subtrees) are independent */
+/* The same flags from the levels, per run of whole top-level subtrees,
+ * scanning backwards: the fills of one gap are the fills of one level seen
+ * with their gap indices counting down to 0 (a gap's fills are consecutive at
+ * their level in pre-order, their subtrees in between), so a per-level
+ * "some later sibling shows" accumulator, reset whenever the index does not
+ * continue the count, replaces the walks of every gap's fill list.  Level 0
+ * (the root gaps, which span runs) is left to the roots' pass. */
+static void *wmore_lvl_thread(void *arg) {
+    wjob *J = arg;
+    const int64_t per = J->nf / (8 * (int64_t)gac_host_threads()) + 1;
+    for (;;) {
+        const int64_t r = atomic_fetch_add(&J->next, 1);
+        if (r * per >= J->nf)
+            return NULL;
+        const int64_t a = next_top_level(J->n, J->side, r * per);
+        const int64_t b = next_top_level(J->n, J->side, (r + 1) * per < J->nf ? (r + 1) * per : J->nf);
+        int32_t pbuf[256], *prev = pbuf;
+        uint8_t abuf[256], *acc = abuf;
+        int cap = 256;
+        for (int k = 0; k < cap; ++k)
+            prev[k] = INT32_MIN;
+        for (int64_t i = b - 1; i >= a; --i) {
+            const int L = J->lvl[i];
+            if (L == 0)
+                continue;
+            if (L >= cap) {
+                const int nc = L + 256;
+                int32_t *np = malloc((size_t)nc * sizeof(int32_t));
+                uint8_t *na = malloc((size_t)nc);
+                memcpy(np, prev, (size_t)cap * sizeof(int32_t));
+                memcpy(na, acc, (size_t)cap);
+                for (int k = cap; k < nc; ++k)
+                    np[k] = INT32_MIN;
+                if (prev != pbuf) {
+                    free(prev);
+                    free(acc);
+                }
+                prev = np;
+                acc = na;
+                cap = nc;
+            }
+            const int32_t p = J->pix[i];
+            if (prev[L] != INT32_MIN && p == prev[L] - 1) {
+                J->more[i] = acc[L];
+                acc[L] |= J->show[i];
+            } else {
+                J->more[i] = 0;
+                acc[L] = J->show[i];
+            }
+            prev[L] = p;
+        }
+        if (prev != pbuf) {
+            free(prev);
+            free(acc);
+        }
+    }
+}
+
 static void *wreached_thread(void *arg) {
     wjob *J = arg;
     const int64_t per = J->nf / (8 * (int64_t)gac_host_threads()) + 1;
@@ -2666,7 +2724,7 @@ static void *wreached_thread(void *arg) {
                 J->reached[i] = J->show[i] && (po[i] < 0 || J->reached[po[i]]);
             continue;
         }
-        if (J->lvl && !atomic_load(&J->deep)) {
+        if (!atomic_load(&J->deep)) {
             /* pre-order from a top-level fill: a fill's parent is the last
              * fill before it one level up, so a stack of the last position
              * per level replaces the parent links */
@@ -2752,15 +2810,15 @@ static void wjob_flags(wjob *J, const gac_net *n, int side, const int64_t *tscor
     J->show = malloc(m);
     J->more = malloc(m);
     J->reached = malloc(m);
-    /* (levels for the reached pass unless the parent positions are known) */
-    J->lvl = n->pord_ok[side] ? NULL : malloc(m * sizeof(uint16_t));
+    J->lvl = malloc(m * sizeof(uint16_t));
+    J->pix = malloc(m * sizeof(int32_t));
     atomic_init(&J->deep, 0);
     const int nt = gac_host_threads();
     atomic_init(&J->next, 0);
     gac_run_threads(nt, winfo_thread, J);
     gac_mark("flags: info done");
     atomic_store(&J->next, 0);
-    gac_run_threads(nt, wmore_thread, J);
+    gac_run_threads(nt, atomic_load(&J->deep) ? wmore_thread : wmore_lvl_thread, J);
     gac_mark("flags: more done");
     for (int32_t k = 0; k < n->n_chroms[side]; ++k) {
         const nchrom *c = &n->chroms[side][k];
@@ -2784,7 +2842,9 @@ static void wjob_free_flags(wjob *J) {
     free(J->more);
     free(J->reached);
     free(J->lvl);
+    free(J->pix);
     J->lvl = NULL;
+    J->pix = NULL;
     J->score = NULL;
     J->sub = NULL;
     J->show = J->more = J->reached = NULL;
