@@ -1774,6 +1774,13 @@ static inline const char *fh_num(const char *p, const char *end, int maxd, int64
 
 static int fast_header(lf *f, gt_chains *c) {
     const char *p = f->cur, *end = f->end;
+    /* the empty line chainWrite puts after every chain's blocks (lf_chop
+     * skips blank lines the same way, counting them) */
+    int64_t blank = 0;
+    while (p < end && *p == '\n') {
+        ++p;
+        ++blank;
+    }
     if (end - p < 32 || memcmp(p, "chain ", 6) != 0)
         return 0;
     p += 6;
@@ -1821,7 +1828,7 @@ static int fast_header(lf *f, gt_chains *c) {
     c->qstart[i] = (int)num[10];
     c->qend[i] = (int)num[11];
     f->cur = (char *)p + 1;
-    ++f->line;
+    f->line += blank + 1;
     return 1;
 }
 
