@@ -227,6 +227,31 @@ typedef struct sitem {
     ngap *gap;
 } sitem;
 
+/* Element moves inside a node or a gap's list: a few entries at a time,
+ * tens of millions of times per net -- inline loops, not memmove/memcpy
+ * library calls (the loop-to-call rewrite is off for these). */
+#define NO_LIBCALL __attribute__((optimize("no-tree-loop-distribute-patterns")))
+NO_LIBCALL static inline void move_i32(int32_t *a, int to, int from, int cnt) {
+    if (to > from)
+        for (int k = cnt - 1; k >= 0; --k)
+            a[to + k] = a[from + k];
+    else
+        for (int k = 0; k < cnt; ++k)
+            a[to + k] = a[from + k];
+}
+NO_LIBCALL static inline void move_ptr(void **a, int to, int from, int cnt) {
+    if (to > from)
+        for (int k = cnt - 1; k >= 0; --k)
+            a[to + k] = a[from + k];
+    else
+        for (int k = 0; k < cnt; ++k)
+            a[to + k] = a[from + k];
+}
+NO_LIBCALL static inline void copy_ptr(void **d, void *const *s, int64_t cnt) {
+    for (int64_t k = 0; k < cnt; ++k)
+        d[k] = s[k];
+}
+
 static int32_t sp_new_leaf(nwork *w) {
     int32_t i;
     if (w->lf_free >= 0) {
@@ -542,9 +567,9 @@ static void sp_replace(nwork *w, nchrom *c, int sstart, int send, const sitem *i
                                        : spkey(w->lf[l].start[1], w->lf[l].end[1]));
     if (tot <= SP_LF) {
         sleaf *L = &w->lf[l];
-        memmove(L->start + idx + m, L->start + idx + 1, (size_t)(n0 - idx - 1) * 4);
-        memmove(L->end + idx + m, L->end + idx + 1, (size_t)(n0 - idx - 1) * 4);
-        memmove(L->gap + idx + m, L->gap + idx + 1, (size_t)(n0 - idx - 1) * sizeof(ngap *));
+        move_i32(L->start, idx + m, idx + 1, n0 - idx - 1);
+        move_i32(L->end, idx + m, idx + 1, n0 - idx - 1);
+        move_ptr((void **)L->gap, idx + m, idx + 1, n0 - idx - 1);
         for (int k = 0; k < m; ++k) {
             L->start[idx + k] = it[k].start;
             L->end[idx + k] = it[k].end;
@@ -948,7 +973,7 @@ static void sort_gap_fills(nwork *w, ngap *g) {
     }
     g->n_fills = cnt;
     g->fills = arena_alloc(&w->ar, cnt * sizeof(nfill *));
-    memcpy(g->fills, w->sf, (size_t)cnt * sizeof(nfill *));
+    copy_ptr((void **)g->fills, (void *const *)w->sf, cnt);
     const int32_t level = g->pfill ? g->pfill->level + 1 : 0;
     if (cnt <= 16) { /* fills of one gap are disjoint: starts are distinct */
         for (int i = 1; i < cnt; ++i) {
@@ -2375,10 +2400,14 @@ static char *put_score(char *p, double v) {
     return p + sprintf(p, "%1.0f", v);
 }
 
+/* (the callers reserve room past the indentation: whole 16-byte stores) */
 static char *put_spaces(char *p, int k) {
-    while (k-- > 0)
-        *p++ = ' ';
-    return p;
+    static const char sp[16] = {' ', ' ', ' ', ' ', ' ', ' ', ' ', ' ',
+                                ' ', ' ', ' ', ' ', ' ', ' ', ' ', ' '};
+    char *const e = p + k;
+    for (; p < e; p += 16)
+        memcpy(p, sp, 16);
+    return e;
 }
 
 /* gap line at the given indentation (rOutputGap, chainNet.c:747-761) */
