@@ -277,7 +277,12 @@ static void partition(int32_t *a, int32_t n, const uint8_t *hit, int32_t *tmp) {
     for (int32_t i = 0; i < n; ++i)
         if (!hit[a[i]])
             tmp[k++] = a[i];
-    memcpy(a, tmp, (size_t)n * sizeof(int32_t));
+    if (n > 64) {
+        memcpy(a, tmp, (size_t)n * sizeof(int32_t));
+    } else { /* (most nodes are small: no library call per node) */
+        for (int32_t i = 0; i < n; ++i)
+            a[i] = tmp[i];
+    }
 }
 
 /* medianVal + splitList of one node (chainBlock.c:112-122, 92-110): the
@@ -3252,16 +3257,17 @@ static void *gather_thread(void *arg) {
         const int32_t k0 = (int32_t)G->task[3 * t + 1], k1 = (int32_t)G->task[3 * t + 2];
         const ax_out *o = &G->po[p];
         int64_t c = G->c0[p] + k0, x = G->x0[p] + o->coff[k0];
+        /* (the task's chains' blocks are one run of the pair's arrays) */
+        const int32_t r0 = o->coff[k0], r1 = o->coff[k1];
+        memcpy(G->bt + x, o->bt + r0, (size_t)(r1 - r0) * 4);
+        memcpy(G->bq + x, o->bq + r0, (size_t)(r1 - r0) * 4);
+        memcpy(G->bs + x, o->bs + r0, (size_t)(r1 - r0) * 4);
         for (int32_t k = k0; k < k1; ++k, ++c) {
             G->ct[c] = G->in->t_seq[p];
             G->cq[c] = G->in->q_seq[p];
             G->cs[c] = G->in->q_strand[p] ? 1 : 0;
             G->cpair[c] = (int32_t)p;
-            const int32_t b0 = o->coff[k], b1 = o->coff[k + 1];
-            memcpy(G->bt + x, o->bt + b0, (size_t)(b1 - b0) * 4);
-            memcpy(G->bq + x, o->bq + b0, (size_t)(b1 - b0) * 4);
-            memcpy(G->bs + x, o->bs + b0, (size_t)(b1 - b0) * 4);
-            x += b1 - b0;
+            x += o->coff[k + 1] - o->coff[k];
             G->coff[c + 1] = x;
         }
     }
