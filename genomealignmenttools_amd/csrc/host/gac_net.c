@@ -189,6 +189,7 @@ struct gac_net {
      * (where the runs of whole subtrees may start), from finishNet */
     int64_t *top[2];
     int64_t n_top[2];
+    int32_t *nlen[2]; /* [GAC_T] / [GAC_Q]: the sequence names' lengths */
     int sides; /* bit 1 << side: side netted */
     atomic_int free_next; /* gac_net_free's worker cursor */
 };
@@ -1048,6 +1049,8 @@ void gac_net_free(gac_net *n) {
     free(n->pord[1]);
     free(n->top[0]);
     free(n->top[1]);
+    free(n->nlen[0]);
+    free(n->nlen[1]);
     free(n->chain_ali);
     free(n);
 }
@@ -2022,6 +2025,13 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
     }
     /* the space index is netting-only: released now, on a detached thread */
     space_release(n);
+    for (int side = 0; side < 2; ++side) { /* (the writers' line-length check) */
+        const int32_t ns = side == GAC_T ? in->n_tseq : in->n_qseq;
+        const char *const *nm = side == GAC_T ? in->t_names : in->q_names;
+        n->nlen[side] = malloc((size_t)(ns > 0 ? ns : 1) * sizeof(int32_t));
+        for (int32_t k = 0; k < ns; ++k)
+            n->nlen[side][k] = (int32_t)strlen(nm[k]);
+    }
     /* aligned bases per chain (chainBaseCount), in parallel over chains */
     n->chain_ali = malloc((size_t)(in->n_chains ? in->n_chains : 1) * sizeof(int64_t));
     {
@@ -2415,7 +2425,8 @@ static void put_gap_line(const wctx *w, const nfill *parent, const ngap *g, int 
     const gac_net_input *in = &w->n->in;
     const int64_t c = parent->chain;
     const char *ochrom = w->side == GAC_Q ? in->t_names[in->t_seq[c]] : in->q_names[in->q_seq[c]];
-    if (strlen(ochrom) > 400 || depth > 400) {
+    const int olen = w->side == GAC_Q ? w->n->nlen[GAC_T][in->t_seq[c]] : w->n->nlen[GAC_Q][in->q_seq[c]];
+    if (olen > 400 || depth > 400) {
         gac_obuf_printf(w->o, "%*sgap %d %d %s %c %d %d\n", depth, "", g->start, g->end - g->start,
                   ochrom, in->q_strand[c] ? '-' : '+', g->o_start, g->o_end - g->o_start);
         return;
@@ -2471,8 +2482,9 @@ static void put_fill_line(const wctx *w, const nfill *f, int depth, double score
     const gac_net_input *in = &w->n->in;
     const int64_t c = f->chain;
     const char *ochrom = w->side == GAC_Q ? in->t_names[in->t_seq[c]] : in->q_names[in->q_seq[c]];
+    const int olen = w->side == GAC_Q ? w->n->nlen[GAC_T][in->t_seq[c]] : w->n->nlen[GAC_Q][in->q_seq[c]];
     const int deferred = w->marks && w->side == GAC_T && !f->full;
-    if (strlen(ochrom) > 400 || depth > 400 || !(score > -1e300 && score < 1e300)) {
+    if (olen > 400 || depth > 400 || !(score > -1e300 && score < 1e300)) {
         gac_obuf_printf(w->o, "%*sfill %d %d %s %c %d %d id %d score ", depth, "", f->start,
                   f->end - f->start, ochrom, in->q_strand[c] ? '-' : '+', f->o_start,
                   f->o_end - f->o_start, in->id[c]);
