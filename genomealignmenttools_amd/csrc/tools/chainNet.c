@@ -345,6 +345,7 @@ typedef struct check_job {
     const gt_chains *c;
     const gt_sizes *ts, *qs;
     int32_t *tix, *qix;
+    const int32_t *tmap, *qmap; /* the chain set's distinct names -> sizes rows */
     int64_t n;
     _Atomic int64_t next, first_bad;
 } check_job;
@@ -359,8 +360,8 @@ static void *check_thread(void *arg) {
         const int64_t b = a + 65536 < J->n ? a + 65536 : J->n;
         for (int64_t i = a; i < b; ++i) {
             int ok = i == 0 || c->score[i - 1] < 0 || c->score[i] <= c->score[i - 1];
-            J->qix[i] = gt_names_find(&J->qs->names, c->qnames.names[c->qname[i]]);
-            J->tix[i] = gt_names_find(&J->ts->names, c->tnames.names[c->tname[i]]);
+            J->qix[i] = J->qmap[c->qname[i]];
+            J->tix[i] = J->tmap[c->tname[i]];
             ok = ok && J->qix[i] >= 0 && J->qs->size[J->qix[i]] == c->qsize[i] && J->tix[i] >= 0 &&
                  J->ts->size[J->tix[i]] == c->tsize[i];
             if (!ok) {
@@ -492,7 +493,14 @@ int main(int argc, char *argv[]) {
     {
         /* in parallel; the first failing chain in file order is re-checked
          * serially for its message */
-        check_job cj = {&c, &ts, &qs, tix, qix, c.n, 0};
+        /* (each distinct name looked up once, not once per chain) */
+        int32_t *tmap = malloc((size_t)(c.tnames.n ? c.tnames.n : 1) * 4);
+        int32_t *qmap = malloc((size_t)(c.qnames.n ? c.qnames.n : 1) * 4);
+        for (int32_t k = 0; k < c.tnames.n; ++k)
+            tmap[k] = gt_names_find(&ts.names, c.tnames.names[k]);
+        for (int32_t k = 0; k < c.qnames.n; ++k)
+            qmap[k] = gt_names_find(&qs.names, c.qnames.names[k]);
+        check_job cj = {&c, &ts, &qs, tix, qix, tmap, qmap, c.n, 0};
         atomic_init(&cj.next, 0);
         atomic_init(&cj.first_bad, c.n);
         gac_run_threads(gt_threads(), check_thread, &cj);
@@ -512,6 +520,8 @@ int main(int argc, char *argv[]) {
             gt_abort("%s is %d in %s but %d in %s", tn, c.tsize[i], chain_file, ts.size[tix[i]],
                      tsizes_file);
         }
+        free(tmap);
+        free(qmap);
     }
     gt_stage("chain checks");
     runs_job rj = {&runs, &c, tnib, qnib};
