@@ -927,6 +927,7 @@ typedef struct po_job {
     size_t *len;
     _Atomic int *ready;
     _Atomic int64_t next;
+    _Atomic int64_t done; /* runs formatted (GAC_TIMING: a mark when all are) */
     _Atomic int oom;
 } po_job;
 
@@ -942,6 +943,8 @@ static void *po_thread(void *p) {
             J->buf[r] = o.p;
             J->len[r] = o.n;
             atomic_store_explicit(&J->ready[r], 1, memory_order_release);
+            if (atomic_fetch_add(&J->done, 1) + 1 == J->nr)
+                gac_mark("output: every run formatted");
             continue;
         }
         FILE *f = open_memstream(&J->buf[r], &J->len[r]);
@@ -969,6 +972,7 @@ static int par_format(int64_t nr, void (*fn)(FILE *f, int64_t r, void *arg),
     J.len = calloc((size_t)(nr > 0 ? nr : 1), sizeof(size_t));
     J.ready = calloc((size_t)(nr > 0 ? nr : 1), sizeof(_Atomic int));
     atomic_init(&J.next, 0);
+    atomic_init(&J.done, 0);
     atomic_init(&J.oom, 0);
     int nt = gac_host_threads();
     if (nt > nr)
@@ -1129,6 +1133,90 @@ int gac_par_format_buf(int64_t nr, void (*fn)(gac_obuf *o, int64_t r, void *arg)
     return par_format(nr, NULL, fn, arg, bufs, lens);
 }
 
+/* GAC_OUT_WRITERS=K (K > 1): the in-order loop below places each batch at
+ * its file offset and K threads write the batches with pwritev, so a file's
+ * writes are not one thread's copy into the page cache (the formatters can
+ * finish well before a single writer does).  Default 1: one writev loop. */
+typedef struct wbatch {
+    struct iovec iov[256];
+    int n;
+    off_t off;
+    char *owned[256]; /* run buffers to free once written */
+    int n_owned;
+} wbatch;
+
+typedef struct wpool {
+    int fd;
+    wbatch *q; /* ring */
+    int cap, head, tail, count, closing;
+    pthread_mutex_t mu;
+    pthread_cond_t can_put, can_take;
+    _Atomic int bad;
+} wpool;
+
+static int pwritev_all(int fd, struct iovec *iov, int n, off_t off) {
+    while (n > 0) {
+        const ssize_t w = pwritev(fd, iov, n, off);
+        if (w < 0) {
+            if (errno == EINTR)
+                continue;
+            return -1;
+        }
+        off += w;
+        size_t left = (size_t)w;
+        while (n > 0 && left >= iov->iov_len) {
+            left -= iov->iov_len;
+            ++iov;
+            --n;
+        }
+        if (n > 0) {
+            iov->iov_base = (char *)iov->iov_base + left;
+            iov->iov_len -= left;
+        }
+    }
+    return 0;
+}
+
+static void *wpool_thread(void *arg) {
+    wpool *P = arg;
+    wbatch b;
+    for (;;) {
+        pthread_mutex_lock(&P->mu);
+        while (P->count == 0 && !P->closing)
+            pthread_cond_wait(&P->can_take, &P->mu);
+        if (P->count == 0) {
+            pthread_mutex_unlock(&P->mu);
+            return NULL;
+        }
+        b = P->q[P->head];
+        P->head = (P->head + 1) % P->cap;
+        --P->count;
+        pthread_cond_signal(&P->can_put);
+        pthread_mutex_unlock(&P->mu);
+        if (!atomic_load(&P->bad) && pwritev_all(P->fd, b.iov, b.n, b.off) != 0)
+            atomic_store(&P->bad, 1);
+        for (int k = 0; k < b.n_owned; ++k)
+            free(b.owned[k]);
+    }
+}
+
+static void wpool_put(wpool *P, const wbatch *b) {
+    pthread_mutex_lock(&P->mu);
+    while (P->count == P->cap)
+        pthread_cond_wait(&P->can_put, &P->mu);
+    P->q[P->tail] = *b;
+    P->tail = (P->tail + 1) % P->cap;
+    ++P->count;
+    pthread_cond_signal(&P->can_take);
+    pthread_mutex_unlock(&P->mu);
+}
+
+static int out_writers(void) {
+    const char *e = getenv("GAC_OUT_WRITERS");
+    const int k = e && *e ? atoi(e) : 1;
+    return k < 1 ? 1 : (k > 8 ? 8 : k);
+}
+
 static int par_output(FILE *out, int64_t nr, void (*fn)(FILE *f, int64_t r, void *arg),
                       void (*fn_buf)(gac_obuf *o, int64_t r, void *arg), void *arg) {
     if (nr <= 0)
@@ -1142,6 +1230,7 @@ static int par_output(FILE *out, int64_t nr, void (*fn)(FILE *f, int64_t r, void
     J.len = calloc((size_t)nr, sizeof(size_t));
     J.ready = calloc((size_t)nr, sizeof(_Atomic int));
     atomic_init(&J.next, 0);
+    atomic_init(&J.done, 0);
     atomic_init(&J.oom, 0);
     int nt = gac_host_threads() - 1;
     if (nt < 1)
@@ -1188,6 +1277,62 @@ static int par_output(FILE *out, int64_t nr, void (*fn)(FILE *f, int64_t r, void
      * memory speed; stdio only for streams without a descriptor */
     const int fd = r < nr ? fileno(out) : -1;
     const int use_fd = fd >= 0 && fflush(out) == 0;
+    const int nw = use_fd ? out_writers() : 1;
+    if (nw > 1 && r < nr) {
+        off_t off = lseek(fd, 0, SEEK_CUR);
+        wpool P;
+        memset(&P, 0, sizeof(P));
+        P.fd = fd;
+        P.cap = 4 * nw;
+        P.q = malloc((size_t)P.cap * sizeof(wbatch));
+        pthread_mutex_init(&P.mu, NULL);
+        pthread_cond_init(&P.can_put, NULL);
+        pthread_cond_init(&P.can_take, NULL);
+        atomic_init(&P.bad, 0);
+        pthread_t wt[8];
+        int started = 0;
+        for (int i = 0; i < nw; ++i)
+            if (pthread_create(&wt[i], NULL, wpool_thread, &P) == 0)
+                ++started;
+        wbatch *b = malloc(sizeof(wbatch));
+        while (r < nr && off >= 0 && started > 0) {
+            wait_ready(&J.ready[r]);
+            b->n = b->n_owned = 0;
+            b->off = off;
+            size_t bytes = 0;
+            const int64_t r0 = r;
+            while (r < nr && b->n_owned < 256 && bytes < (8u << 20) &&
+                   (r == r0 || atomic_load_explicit(&J.ready[r], memory_order_acquire))) {
+                if (J.len[r]) {
+                    b->iov[b->n].iov_base = J.buf[r];
+                    b->iov[b->n].iov_len = J.len[r];
+                    bytes += J.len[r];
+                    ++b->n;
+                }
+                b->owned[b->n_owned++] = J.buf[r];
+                ++r;
+            }
+            off += (off_t)bytes;
+            wpool_put(&P, b);
+        }
+        pthread_mutex_lock(&P.mu);
+        P.closing = 1;
+        pthread_cond_broadcast(&P.can_take);
+        pthread_mutex_unlock(&P.mu);
+        for (int i = 0; i < started; ++i)
+            pthread_join(wt[i], NULL);
+        if (atomic_load(&P.bad) || off < 0 || started == 0 || lseek(fd, off, SEEK_SET) < 0)
+            bad = 1;
+        for (; r < nr; ++r) { /* (only after a failure above) */
+            wait_ready(&J.ready[r]);
+            free(J.buf[r]);
+        }
+        free(b);
+        free(P.q);
+        pthread_mutex_destroy(&P.mu);
+        pthread_cond_destroy(&P.can_put);
+        pthread_cond_destroy(&P.can_take);
+    }
     while (r < nr) {
         wait_ready(&J.ready[r]);
         if (!use_fd) {
