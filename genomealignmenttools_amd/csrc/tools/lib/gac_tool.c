@@ -18,6 +18,7 @@
 #include <sys/syscall.h>
 #include <pthread.h>
 #include <stdatomic.h>
+#include <malloc.h>
 #include <sys/mman.h>
 #include <time.h>
 #include <zlib.h>
@@ -2048,15 +2049,38 @@ typedef struct rc_free_job {
     int nk;
     void *cut;
     char *buf;
+    size_t len;
 } rc_free_job;
+
+/* pages of a large heap block dropped first (madvise runs under the mm's
+ * read lock; an munmap of populated pages holds the write lock while it
+ * frees them, stalling every other thread's page faults -- the netting's
+ * and the checks' first touches) */
+static void drop_free(void *p, size_t len) {
+    if (p && len > malloc_usable_size(p))
+        len = malloc_usable_size(p); /* (never past the block) */
+    if (p && len >= (1u << 20)) {
+        const uintptr_t pg = 4096;
+        const uintptr_t a = ((uintptr_t)p + pg - 1) & ~(pg - 1), b = ((uintptr_t)p + len) & ~(pg - 1);
+        if (b > a)
+            madvise((void *)a, b - a, MADV_DONTNEED);
+    }
+    free(p);
+}
 
 static void *rc_free_thread(void *arg) {
     rc_free_job *F = arg;
-    for (int k = 0; k < F->nk; ++k)
-        gt_chains_free(&F->K[k].c);
+    for (int k = 0; k < F->nk; ++k) {
+        gt_chains *c = &F->K[k].c;
+        drop_free(c->bt, (size_t)c->bcap * 4);
+        drop_free(c->bq, (size_t)c->bcap * 4);
+        drop_free(c->bs, (size_t)c->bcap * 4);
+        c->bt = c->bq = c->bs = NULL;
+        gt_chains_free(c);
+    }
     free(F->K);
     free(F->cut);
-    free(F->buf);
+    drop_free(F->buf, F->len + 17);
     free(F);
     return NULL;
 }
@@ -2209,7 +2233,7 @@ static void read_chains(const char *path, gt_chains *c, double stop_below, int k
      * 0.2 s of page freeing on C5 at 5 M chains) are released off the
      * caller's path */
     rc_free_job *F = malloc(sizeof(*F));
-    *F = (rc_free_job){K, nk, cut, buf};
+    *F = (rc_free_job){K, nk, cut, buf, len};
     pthread_attr_t at;
     pthread_attr_init(&at);
     pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
