@@ -1635,7 +1635,7 @@ static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs)
             DChain *q = p;
             if (!q) return;
             try {
-                std::thread([q] { gac_drop_free(q); }).detach();
+                std::thread([q] { free(q); }).detach();
             } catch (...) {
                 free(q);
             }

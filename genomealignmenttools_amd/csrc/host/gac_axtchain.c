@@ -3187,7 +3187,7 @@ typedef struct late_free {
 static void *late_free_thread(void *arg) {
     late_free *L = arg;
     for (int i = 0; i < L->n; ++i)
-        gac_drop_free(L->p[i]);
+        free(L->p[i]);
     free(L);
     return NULL;
 }

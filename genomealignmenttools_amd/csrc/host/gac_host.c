@@ -24,7 +24,6 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
-#include <malloc.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <sys/uio.h>
@@ -791,19 +790,6 @@ int gac_host_threads(void) {
     return n > 64 ? 64 : n;
 }
 
-void gac_drop_free(void *p) {
-    if (!p)
-        return;
-    const size_t len = malloc_usable_size(p);
-    if (len >= (1u << 20)) {
-        const uintptr_t pg = 4096;
-        const uintptr_t a = ((uintptr_t)p + pg - 1) & ~(pg - 1), b = ((uintptr_t)p + len) & ~(pg - 1);
-        if (b > a)
-            madvise((void *)a, b - a, MADV_DONTNEED);
-    }
-    free(p);
-}
-
 void gac_mark(const char *what) {
     static int on = -1;
     static double t0;
@@ -1210,7 +1196,7 @@ static void *wpool_thread(void *arg) {
         if (!atomic_load(&P->bad) && pwritev_all(P->fd, b.iov, b.n, b.off) != 0)
             atomic_store(&P->bad, 1);
         for (int k = 0; k < b.n_owned; ++k)
-            gac_drop_free(b.owned[k]);
+            free(b.owned[k]);
     }
 }
 
@@ -1373,7 +1359,7 @@ static int par_output(FILE *out, int64_t nr, void (*fn)(FILE *f, int64_t r, void
         if (!bad && writev_all(fd, iov, k) != 0)
             bad = 1;
         for (int64_t x = r0; x < r; ++x)
-            gac_drop_free(J.buf[x]);
+            free(J.buf[x]);
     }
     for (int i = 0; i < nt; ++i)
         pthread_join(th[i], NULL);

@@ -96,10 +96,6 @@ int gac_host_threads(void);
 /* GAC_TIMING: "[mark] <seconds since the first mark> <thread> <what>" on
  * stderr (timelines of overlapped phases; no-op otherwise) */
 void gac_mark(const char *what);
-/* free() of a large heap block with its pages dropped first (madvise, under
- * the mm's read lock): an munmap of populated pages holds the write lock
- * while it frees them and stalls every other thread's page faults */
-void gac_drop_free(void *p);
 /* gap tables with the same content (as gapCalcCost sees them) */
 int gac_gapcalc_same(const gac_gapcalc *a, const gac_gapcalc *b);
 /* deep copy, freed with gac_gapcalc_free */

@@ -2877,13 +2877,13 @@ static void wjob_flags(wjob *J, const gac_net *n, int side, const int64_t *tscor
 }
 
 static void wjob_free_flags(wjob *J) {
-    gac_drop_free(J->score);
-    gac_drop_free(J->sub);
-    gac_drop_free(J->show);
-    gac_drop_free(J->more);
-    gac_drop_free(J->reached);
-    gac_drop_free(J->lvl);
-    gac_drop_free(J->pix);
+    free(J->score);
+    free(J->sub);
+    free(J->show);
+    free(J->more);
+    free(J->reached);
+    free(J->lvl);
+    free(J->pix);
     J->lvl = NULL;
     J->pix = NULL;
     J->score = NULL;
