@@ -240,7 +240,7 @@ NO_LIBCALL static inline void move_i32(int32_t *a, int to, int from, int cnt) {
         for (int k = 0; k < cnt; ++k)
             a[to + k] = a[from + k];
 }
-NO_LIBCALL static inline void move_ptr(void **a, int to, int from, int cnt) {
+NO_LIBCALL static inline void move_gap(ngap **a, int to, int from, int cnt) {
     if (to > from)
         for (int k = cnt - 1; k >= 0; --k)
             a[to + k] = a[from + k];
@@ -248,7 +248,7 @@ NO_LIBCALL static inline void move_ptr(void **a, int to, int from, int cnt) {
         for (int k = 0; k < cnt; ++k)
             a[to + k] = a[from + k];
 }
-NO_LIBCALL static inline void copy_ptr(void **d, void *const *s, int64_t cnt) {
+NO_LIBCALL static inline void copy_fill(nfill **d, nfill *const *s, int64_t cnt) {
     for (int64_t k = 0; k < cnt; ++k)
         d[k] = s[k];
 }
@@ -570,7 +570,7 @@ static void sp_replace(nwork *w, nchrom *c, int sstart, int send, const sitem *i
         sleaf *L = &w->lf[l];
         move_i32(L->start, idx + m, idx + 1, n0 - idx - 1);
         move_i32(L->end, idx + m, idx + 1, n0 - idx - 1);
-        move_ptr((void **)L->gap, idx + m, idx + 1, n0 - idx - 1);
+        move_gap(L->gap, idx + m, idx + 1, n0 - idx - 1);
         for (int k = 0; k < m; ++k) {
             L->start[idx + k] = it[k].start;
             L->end[idx + k] = it[k].end;
@@ -974,7 +974,7 @@ static void sort_gap_fills(nwork *w, ngap *g) {
     }
     g->n_fills = cnt;
     g->fills = arena_alloc(&w->ar, cnt * sizeof(nfill *));
-    copy_ptr((void **)g->fills, (void *const *)w->sf, cnt);
+    copy_fill(g->fills, w->sf, cnt);
     const int32_t level = g->pfill ? g->pfill->level + 1 : 0;
     if (cnt <= 16) { /* fills of one gap are disjoint: starts are distinct */
         for (int i = 1; i < cnt; ++i) {
