@@ -170,6 +170,8 @@ struct SmallServer {
     int64_t launches = 0, requests = 0;
     unsigned in_fl = 0;  // hipHostMalloc flags of the inputs
     int wgs = 16;        // workgroups of the grid (GAC_SRV_WGS, 1..kSrvWaves/4)
+    bool wedged = false; // a grid did not exit within kParkSecs of its stop:
+                         // the server is not used again (no unbounded wait)
 };
 
 struct gac_ctx {
@@ -1371,7 +1373,33 @@ extern "C" int gac_chain_dp_ex(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq
         // one wave per pair, every pair resident at once (largest first is
         // the caller's order; the grid covers them all)
         const int grid = (int)std::min<int64_t>(n_pairs, 1 << 20);
+        // GAC_DP_PROF: k_dp_fast's per-phase cycle counters, to stderr
+        unsigned long long *d_prof = nullptr;
+        const char *dpprof = getenv("GAC_DP_PROF");
+        if (fast && dpprof && *dpprof && *dpprof != '0' && e == hipSuccess &&
+            (e = hipMalloc(&d_prof, kDpProf * sizeof(unsigned long long))) == hipSuccess)
+            e = hipMemsetAsync(d_prof, 0, kDpProf * sizeof(unsigned long long), c->stream);
+        a.prof = d_prof;
+        const double tk0 = wall_s();
         if (e == hipSuccess) e = fast ? launch_dp_fast(a, grid, c->stream) : launch_dp(a, grid, c->stream);
+        if (d_prof && e == hipSuccess) {
+            unsigned long long pv[kDpProf];
+            e = hipMemcpyAsync(pv, d_prof, sizeof(pv), hipMemcpyDeviceToHost, c->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+            if (e == hipSuccess) {
+                const double secs = wall_s() - tk0, L = pv[kPfLeaves] ? (double)pv[kPfLeaves] : 1.0;
+                fprintf(stderr,
+                        "[gac_chain_dp] k_dp_fast %.3f s, %llu pairs, %llu leaves, %llu fallbacks; per leaf: "
+                        "%.2f windows, %.3f fallback windows, %.3f windows with an overlapping candidate, "
+                        "%.2f overlap checks; cycles per leaf: load %.0f seed %.0f walk %.0f "
+                        "(node loads + bounds %.0f) anomalies %.0f fallback %.0f commit %.0f\n",
+                        secs, (unsigned long long)n_pairs, pv[kPfLeaves], pv[kPfFallbacks],
+                        pv[kPfWindows] / L, pv[kPfFbWindows] / L, pv[kPfXoverWin] / L, pv[kPfOvChecks] / L,
+                        pv[kPfCycLoad] / L, pv[kPfCycSeed] / L, pv[kPfCycWalk] / L, pv[kPfCycXover] / L,
+                        pv[kPfCycAnom] / L, pv[kPfCycFb] / L, pv[kPfCycCommit] / L);
+            }
+            hipFree(d_prof);
+        }
         if (e == hipSuccess)
             e = hipMemcpyAsync(total, d_total, nl * sizeof(long long), hipMemcpyDeviceToHost, c->stream);
         if (e == hipSuccess)
@@ -1630,10 +1658,17 @@ static int chains_fill(gac_ctx *c, const gac_chainset_desc *d, gac_chainset *cs)
     const size_t n_rec = (size_t)(n ? n : 1);
     struct LateArr {
         DChain *p;
-        explicit LateArr(size_t k) : p((DChain *)malloc(k * sizeof(DChain))) {}
+        size_t bytes;
+        explicit LateArr(size_t k) : p((DChain *)malloc(k * sizeof(DChain))), bytes(k * sizeof(DChain)) {}
         ~LateArr() {
             DChain *q = p;
             if (!q) return;
+            // only the tens-of-MB staging of C4/C5-sized sets goes to a
+            // thread: a small set (tests, re-uploads, loops) frees inline
+            if (bytes < ((size_t)16 << 20)) {
+                free(q);
+                return;
+            }
             try {
                 std::thread([q] { free(q); }).detach();
             } catch (...) {
@@ -2024,17 +2059,38 @@ static int score_device_split(gac_ctx *c, const ScoreArgs &a_base, const Range *
 // 16.5 vs 23.6 us per 20-range call of an uploaded set, 23.4 vs 30.6 for
 // host-held chains, chainCleaner's C3 loop 0.19 vs 0.27 s in its 10 k calls
 // (r05lat6).
+// (bounded: a grid that has not drained kParkSecs after its stop -- wedged,
+// or never scheduled -- is left behind, the server marked unusable, and the
+// caller gets an error instead of an unbounded hipStreamSynchronize)
+constexpr double kParkSecs = 10.0;
+
 static void srv_park(gac_ctx *c) {
     SmallServer &v = c->srv;
     if (!v.running) return;
     __atomic_store_n(&v.mail->stop, 1u, __ATOMIC_RELEASE);
-    hipStreamSynchronize(v.st);
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (uint64_t it = 1;; ++it) {
+        const hipError_t q = hipStreamQuery(v.st);
+        if (q != hipErrorNotReady) break;  // drained (or failed: reported by the next call)
+        if ((it & 1023) == 0) {
+            clock_gettime(CLOCK_MONOTONIC, &t1);
+            if ((t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec) > kParkSecs) {
+                v.wedged = true;
+                v.on = false;
+                v.running = false;
+                return;  // (stop stays set: the grid exits whenever it runs)
+            }
+        }
+        __builtin_ia32_pause();
+    }
     __atomic_store_n(&v.mail->stop, 0u, __ATOMIC_RELEASE);
     v.running = false;
 }
 
 static void srv_free(gac_ctx *c) {
     SmallServer &v = c->srv;
+    if (v.wedged) return;  // (a grid may still read these: left allocated)
     void *h[] = {v.mail, v.h_in, v.h_hq, v.h_pool, v.h_out};
     for (void *p : h)
         if (p) hipHostFree(p);
@@ -2108,6 +2164,7 @@ static int srv_launch(gac_ctx *c) {
 // descriptors (any grid with the same local flag takes them)
 static int srv_ensure(gac_ctx *c, const gac_chainset *cs, uint32_t flags) {
     SmallServer &v = c->srv;
+    if (v.wedged) return gac_fail(GAC_E_HIP, "small-batch server disabled: an earlier grid did not exit");
     const int local = (flags & GAC_WANT_LOCAL) ? 1 : 0;
     if (v.running && v.local == local && v.gap_version == c->gap_version && (!cs || v.cs == cs))
         return GAC_OK;
@@ -2179,9 +2236,9 @@ static int srv_call(gac_ctx *c, uint32_t kind, int64_t n) {
             struct timespec t1;
             clock_gettime(CLOCK_MONOTONIC, &t1);
             if ((t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec) > 10.0) {
-                srv_park(c);
-                return gac_fail(GAC_E_HIP, "small-batch server: no answer to request %u in 10 s",
-                                seq);
+                srv_park(c);  // (bounded)
+                return gac_fail(GAC_E_HIP, "small-batch server: no answer to request %u in 10 s%s",
+                                seq, v.wedged ? " (grid did not exit; server disabled)" : "");
             }
             const hipError_t q = hipStreamQuery(v.st);
             if (q != hipSuccess && q != hipErrorNotReady)

@@ -63,6 +63,16 @@ struct DpArgs {
     long long lin_k;
     int32_t min_entry;
     int32_t pad;
+    // GAC_DP_PROF: per-phase cycle counters of k_dp_fast (kDpProf slots,
+    // summed over pairs), or null
+    unsigned long long *prof;
+};
+
+// k_dp_fast's profile slots (GAC_DP_PROF)
+enum DpProf {
+    kPfLeaves, kPfWindows, kPfFbWindows, kPfFallbacks, kPfXoverWin, kPfOvChecks,
+    kPfCycLoad, kPfCycSeed, kPfCycWalk, kPfCycAnom, kPfCycFb, kPfCycCommit, kPfCycXover,
+    kDpProf
 };
 
 // One overlapping adjacent block pair: left block ends at (lqe, lte), right

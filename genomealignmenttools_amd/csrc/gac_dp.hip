@@ -107,6 +107,73 @@ __device__ __forceinline__ int dp_msc(const int *m, int q, int t) {
     return (q == 4 || t == 4) ? 0 : m[q * 4 + t];
 }
 
+// ------------------------------------------------------------ wave scans --
+// On DPP (row_shr 1/2/4/8 inside each 16-lane row, row_bcast15/31 across
+// rows, wave_shr:1 for the exclusive shift): VALU moves, no LDS round trip
+// per step as __shfl_up's ds_bpermute costs -- the walk runs a prefix max
+// per improvement round and window.
+template <int CTRL, int RM>
+__device__ __forceinline__ int dp_dpp(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, RM, 0xf, true);
+}
+
+// inclusive prefix max over the wave
+__device__ __forceinline__ int dp_wave_incl_max(int v, int lane) {
+    int o;
+    o = dp_dpp<0x111, 0xf>(v);
+    if ((lane & 15) >= 1) v = max(v, o);
+    o = dp_dpp<0x112, 0xf>(v);
+    if ((lane & 15) >= 2) v = max(v, o);
+    o = dp_dpp<0x114, 0xf>(v);
+    if ((lane & 15) >= 4) v = max(v, o);
+    o = dp_dpp<0x118, 0xf>(v);
+    if ((lane & 15) >= 8) v = max(v, o);
+    o = dp_dpp<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+    if (lane & 16) v = max(v, o);
+    o = dp_dpp<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
+    if (lane >= 32) v = max(v, o);
+    return v;
+}
+
+// the wave's maximum (int64) / minimum (int), in every lane: an inclusive
+// scan on DPP, then the last lane's value
+__device__ __forceinline__ long long dp_dpp64_max_step(long long v, long long o, bool ok) {
+    return ok && o > v ? o : v;
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ long long dp_dpp64(long long v) {
+    const unsigned long long u = (unsigned long long)v;
+    const uint32_t lo = (uint32_t)dp_dpp<CTRL, RM>((int)(uint32_t)u);
+    const uint32_t hi = (uint32_t)dp_dpp<CTRL, RM>((int)(uint32_t)(u >> 32));
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ long long dp_wave_max64(long long v, int lane) {
+    v = dp_dpp64_max_step(v, dp_dpp64<0x111, 0xf>(v), (lane & 15) >= 1);
+    v = dp_dpp64_max_step(v, dp_dpp64<0x112, 0xf>(v), (lane & 15) >= 2);
+    v = dp_dpp64_max_step(v, dp_dpp64<0x114, 0xf>(v), (lane & 15) >= 4);
+    v = dp_dpp64_max_step(v, dp_dpp64<0x118, 0xf>(v), (lane & 15) >= 8);
+    v = dp_dpp64_max_step(v, dp_dpp64<0x142, 0xa>(v), (lane & 16) != 0);
+    v = dp_dpp64_max_step(v, dp_dpp64<0x143, 0xc>(v), lane >= 32);
+    const unsigned long long u = (unsigned long long)v;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, kWave - 1);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), kWave - 1);
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ int dp_wave_min32(int v, int lane) {
+    return -__builtin_amdgcn_readlane(dp_wave_incl_max(-v, lane), kWave - 1);
+}
+
+// lane u's value (u wave-uniform)
+__device__ __forceinline__ long long dp_readlane64(long long v, int u) {
+    const unsigned long long x = (unsigned long long)v;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, u);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), u);
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+
+// the previous lane's value (lane 0: 0)
+__device__ __forceinline__ int dp_wave_shr1(int v) { return dp_dpp<0x138, 0xf>(v); }
+
 // cBlockFindCrossover (chainConnect.c:61-105), one lane: left block ends at
 // (lqe, lte), right block starts at (rqs, rts), `ov` overlapping bases.
 __device__ void dp_crossover(const DpArgs &a, const DpSeq &s, const int *m, int lqe, int lte,
@@ -296,6 +363,16 @@ hipError_t launch_dp(const DpArgs &a, int grid, hipStream_t s) {
 // Mutable node state is read and written by this wave only: workgroup-scope
 // atomics and fences (no L2 write-back per leaf, as an agent fence costs).
 constexpr int kGapLds = 1024;  // gap costs by distance < kGapLds in LDS, per kind
+constexpr int kLbOct = 22;     // octaves 2^10 .. 2^31 of the lower-bound grid
+constexpr int kLbN = 4 * kLbOct;
+
+// the lower-bound grid: point i = (4 + i % 4) << (i / 4 + 8) (>= kGapLds)
+__host__ __device__ inline int64_t dp_lb_point(int i) { return (int64_t)(4 + (i & 3)) << ((i >> 2) + 8); }
+// the last grid point <= d (d >= kGapLds)
+__device__ __forceinline__ int dp_lb_index(int d) {
+    const int e = 31 - __clz(d);               // d in [2^e, 2^(e+1)), e >= 10
+    return ((e - 10) << 2) + ((d >> (e - 2)) & 3);
+}
 
 __device__ __forceinline__ long long ld_wg(const long long *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -309,18 +386,68 @@ __device__ __forceinline__ void st_wg(long long *p, long long v) {
 // tables of the interpolation, so a gap cost never waits on memory
 struct DpGapLds {
     int gap[3 * kGapLds];
+    int lpos[kMaxLong];
+    double lval[3][kMaxLong];
+    // gapCalcCost's per-kind scalars (read with a per-lane kind: from the
+    // kernel arguments that was a vector load and a wait per gap cost)
+    int last_pos[3];
+    int small_size, long_count;
+    double last_val[3], last_slope[3];
+    // k_dp_fast's pruning bound past kGapLds: the cost at the grid point at
+    // or below d (4 points per octave, kLbOct octaves from kGapLds) -- a
+    // lower bound of gapCalcCost, which k_dp_fast only runs with when it is
+    // monotone in each distance (dp_fast_setup, host)
+    int lb[3][kLbN];
 };
 
-// dp_gap_cost with the short distances from LDS (computing the longer ones
-// -- the interpolation's division -- measured slower than the L2-resident
-// table: 5.2 vs 4.4 s on a 230 k-leaf pair, r05dp2)
+// interpolate (gapCalc.c:82-104) over the LDS copy of the long tables: the
+// first long position >= x by binary search (the reference's linear scan
+// stops at the same one), then its operation order
+__device__ __forceinline__ int dp_interp_lds(const DpGapLds &G, int n, int x, int which) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (G.lpos[mid] < x)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    const double *v = G.lval[which];
+    if (lo < n && G.lpos[lo] == x) return (int)v[lo];
+    // past the last position: the last two; (lo == 0, x below every long
+    // position, cannot happen: x >= smallSize here)
+    const int i = lo == n ? n - 1 : (lo < 1 ? 1 : lo);
+    const int p0 = G.lpos[i - 1];
+    const int ds = G.lpos[i] - p0;
+    const double dv = v[i] - v[i - 1];
+    const double prod = __dmul_rn(dv, (double)(x - p0));
+    return (int)__dadd_rn(v[i - 1], __ddiv_rn(prod, (double)ds));
+}
+
+// dp_gap_cost without a memory round trip: short distances from the LDS
+// table, the long ones by gapCalcCost's own branches (gapCalc.c:298-331) on
+// the LDS long tables (a table read from L2 was one more dependent round
+// trip per search window; r06dp1: 2.6 k cycles per window)
 __device__ __forceinline__ int dp_gap_lds(const DpArgs &a, const DpGapLds &G, int dq, int dt) {
     if (dt < 0) dt = 0;
     if (dq < 0) dq = 0;
     const int which = dt == 0 ? 0 : (dq == 0 ? 1 : 2);
     const int d = which == 0 ? dq : (which == 1 ? dt : dq + dt);
     if (d < kGapLds) return G.gap[which * kGapLds + d];
-    return dp_gap_cost(a, dq, dt);
+    if (d < G.small_size) return a.small_tab[which * G.small_size + d];
+    const int lp = G.last_pos[which];
+    if (d >= lp) return (int)__dadd_rn(G.last_val[which], __dmul_rn(G.last_slope[which], (double)(d - lp)));
+    return dp_interp_lds(G, G.long_count, d, which);
+}
+
+// a lower bound of dp_gap_lds (exact below kGapLds): what pruning needs
+__device__ __forceinline__ int dp_gap_lb(const DpGapLds &G, int dq, int dt) {
+    if (dt < 0) dt = 0;
+    if (dq < 0) dq = 0;
+    const int which = dt == 0 ? 0 : (dq == 0 ? 1 : 2);
+    const int d = which == 0 ? dq : (which == 1 ? dt : dq + dt);
+    if (d < kGapLds) return G.gap[which * kGapLds + d];
+    return G.lb[which][dp_lb_index(d)];
 }
 
 struct DpLeafCtx {
@@ -332,10 +459,15 @@ struct DpLeafCtx {
 // linear bound and tie-to-smaller-node improvements (best/best_node come in
 // seeded); else the reference: max-score and corner bounds only, strict
 // improvements, best from 0.
+// per-wave profile counters (GAC_DP_PROF; wave-uniform)
+struct DpPf {
+    unsigned long long v[kDpProf];
+};
+
 template <bool FAST>
 __device__ void dp_walk(const DpArgs &a, const DpSeq &S, const int *m, const DpGapLds &sg,
                         const DpPair &P, const DpLeafCtx &X, long long kl, long long &best,
-                        int &best_node) {
+                        int &best_node, DpPf &pf, bool prof) {
     const int lane = threadIdx.x & (kWave - 1);
     const long long *ms = a.nd_ms + P.node_off;
     const long long *nwp = a.nd_nw + P.node_off;
@@ -345,6 +477,12 @@ __device__ void dp_walk(const DpArgs &a, const DpSeq &S, const int *m, const DpG
     const int nn = P.n_nodes;
     int p0 = 0;
     while (p0 < nn) {
+        unsigned long long c0 = 0;
+        if (prof) {
+            __builtin_amdgcn_sched_barrier(0);
+            c0 = clock64();
+            __builtin_amdgcn_sched_barrier(0);
+        }
         const int v = p0 + lane;
         const bool in = v < nn;
         long long M = 0, T = 0, NW = 0;
@@ -355,22 +493,36 @@ __device__ void dp_walk(const DpArgs &a, const DpSeq &S, const int *m, const DpG
             B = nb[v];
             M = ld_wg(ms + v);
             if (FAST) NW = ld_wg(nwp + v);
-            if (B.y < 0) T = ld_wg(tot + v);
+            T = ld_wg(tot + v);  // (every node has a slot: no wait on B first)
         }
         const bool leaf = B.y < 0;
         const long long m1 = M + X.ls;
-        const int gc = dp_gap_lds(a, sg, X.lq - A.x, X.lt - A.y);
+        // FAST: the bound with the gap cost's lower bound (looser, still
+        // true); the reference walk needs bestPredecessor's exact one
+        const int gc = FAST ? dp_gap_lb(sg, X.lq - A.x, X.lt - A.y) : dp_gap_lds(a, sg, X.lq - A.x, X.lt - A.y);
         const long long m2 = m1 - gc;
         const long long key = m1 < m2 ? m1 : m2;
         bool cand = false;
         long long sc = 0;
+        if (prof) {
+            // (the bounds of the window's nodes are ready: their loads and
+            // gap costs done)
+            volatile long long sink = key;
+            (void)sink;
+            __builtin_amdgcn_sched_barrier(0);
+            pf.v[kPfCycXover] += clock64() - c0;
+            __builtin_amdgcn_sched_barrier(0);
+            ++pf.v[FAST ? kPfWindows : kPfFbWindows];
+            if (__ballot(in && leaf && A.z < X.lq && A.w < X.lt && (X.lq < A.x || X.lt < A.y)))
+                ++pf.v[kPfXoverWin];
+        }
         if (in && leaf && A.z < X.lq && A.w < X.lt) {
             cand = true;
             // a leaf node's corner is its block's end: a candidate that does
             // not overlap costs the corner gap just computed
             const int dq = X.lq - A.x, dt = X.lt - A.y;
             const int cost = (FAST && dq >= 0 && dt >= 0)
-                                 ? gc
+                                 ? dp_gap_lds(a, sg, dq, dt)
                                  : dp_connect_cost(a, S, m, A.z, A.x, A.y, X.lq, X.lqe, X.lt);
             sc = T + X.ls - cost;
         }
@@ -381,31 +533,26 @@ __device__ void dp_walk(const DpArgs &a, const DpSeq &S, const int *m, const DpG
         }
         int se = v + 1;
         int cur = 0;
+        int incl;
         for (;;) {
             const bool pruned = key < best || (FAST && NW - kl < 1024 * best);
             if (lane >= cur && in) se = pruned ? B.x : (leaf ? v + 1 : nxt);
-            int incl = se;
-#pragma unroll
-            for (int d = 1; d < kWave; d <<= 1) {
-                const int o = __shfl_up(incl, d, kWave);
-                if (lane >= d) incl = max(incl, o);
-            }
-            int excl = __shfl_up(incl, 1, kWave);
-            if (lane == 0) excl = 0;
+            incl = dp_wave_incl_max(se, lane);
+            const int excl = dp_wave_shr1(incl);
             const bool visited = in && excl <= v;
             const bool better = sc > best || (FAST && sc == best && v < best_node);
             const bool imp = visited && lane >= cur && cand && !pruned && better;
             const unsigned long long bal = __ballot(imp);
             if (!bal) break;
             const int u = __builtin_ctzll(bal);
-            best = __shfl(sc, u, kWave);
+            best = dp_readlane64(sc, u);
             best_node = p0 + u;
             cur = u + 1;
         }
-        int mx = in ? se : 0;
-#pragma unroll
-        for (int d = 32; d > 0; d >>= 1) mx = max(mx, __shfl_xor(mx, d, kWave));
-        p0 = max(p0 + kWave, mx);
+        // the next visited node after the window: past every skip interval
+        // that reaches beyond it (they nest) -- the last lane's prefix max
+        // (lanes past the pair's end only push it past the end too)
+        p0 = max(p0 + kWave, __builtin_amdgcn_readlane(incl, kWave - 1));
     }
 }
 
@@ -423,7 +570,38 @@ __global__ void __launch_bounds__(kWave) k_dp_fast(DpArgs a) {
                                   : (which == 1 ? dp_gap_cost(a, 0, d)
                                                 : (d >= 2 ? dp_gap_cost(a, 1, d - 1) : 0));
     }
+    if (lane < kMaxLong) {
+        s_gap.lpos[lane] = a.gap.long_pos[lane];
+        for (int w = 0; w < 3; ++w) s_gap.lval[w][lane] = a.gap.long_val[w][lane];
+    }
+    for (int k = lane; k < 3 * kLbN; k += kWave) {
+        const int which = k / kLbN, i = k % kLbN;
+        const int64_t x = dp_lb_point(i);
+        const int d = x > 0x7fffffff ? 0x7fffffff : (int)x;
+        s_gap.lb[which][i] = which == 0 ? dp_gap_cost(a, d, 0)
+                                        : (which == 1 ? dp_gap_cost(a, 0, d) : dp_gap_cost(a, 1, d - 1));
+    }
+    if (lane < 3) {
+        s_gap.last_pos[lane] = a.gap.last_pos[lane];
+        s_gap.last_val[lane] = a.gap.last_val[lane];
+        s_gap.last_slope[lane] = a.gap.last_slope[lane];
+    }
+    if (lane == 0) {
+        s_gap.small_size = a.gap.small_size;
+        s_gap.long_count = a.gap.long_count;
+    }
     __syncthreads();
+    const bool prof = a.prof != nullptr;
+    DpPf pf;
+    for (int k = 0; k < kDpProf; ++k) pf.v[k] = 0;
+    unsigned long long ck = prof ? clock64() : 0;
+    // GAC_DP_PROF: the cycles since the last lap into slot k
+#define DP_LAP(k)                        \
+    if (prof) {                          \
+        const unsigned long long t_ = clock64(); \
+        pf.v[k] += t_ - ck;              \
+        ck = t_;                         \
+    }
     for (int64_t pi = blockIdx.x; pi < a.n_pairs; pi += gridDim.x) {
         const DpPair P = a.pairs[pi];
         const DpSeq S = {P.tbase, P.qbase};
@@ -433,20 +611,44 @@ __global__ void __launch_bounds__(kWave) k_dp_fast(DpArgs a) {
         const int2 *nb = a.nd_b + P.node_off;
         r_node[lane] = -1;
         __syncthreads();
+        // every per-leaf record at once, the next leaf's loaded while this
+        // one is searched (software pipelined: no round trip of its own)
+        int4 nL = make_int4(0, 0, 0, 0);
+        int n_node = 0, n_ls = 0;
+        int64_t n_q1 = 0, n_o1 = 0, q1 = 0, o1 = 0;
+        if (P.n_leaves > 0) {
+            const int64_t l0 = P.leaf_off;
+            nL = a.lf[l0];
+            n_node = a.lf_node[l0];
+            n_ls = a.lf_score[l0];
+            q1 = a.path_off[l0];
+            o1 = a.ov_off[l0];
+            n_q1 = a.path_off[l0 + 1];
+            n_o1 = a.ov_off[l0 + 1];
+        }
         for (int i = 0; i < P.n_leaves; ++i) {
             const int64_t li = P.leaf_off + i;
-            // every per-leaf record at once (one round trip, not one per stage)
-            const int4 L = a.lf[li];  // {qs, qe, ts, te}
-            const int node = a.lf_node[li];
-            const int64_t q0 = a.path_off[li], q1 = a.path_off[li + 1];
-            const int64_t o0 = a.ov_off[li], o1 = a.ov_off[li + 1];
+            const int4 L = nL;  // {qs, qe, ts, te}
+            const int node = n_node;
+            const int64_t q0 = q1, o0 = o1;
+            q1 = n_q1;
+            o1 = n_o1;
             DpLeafCtx X;
             X.lq = L.x;
             X.lqe = L.y;
             X.lt = L.z;
             X.lte = L.w;
-            X.ls = a.lf_score[li];
+            X.ls = n_ls;
+            if (i + 1 < P.n_leaves) {
+                nL = a.lf[li + 1];
+                n_node = a.lf_node[li + 1];
+                n_ls = a.lf_score[li + 1];
+                n_q1 = a.path_off[li + 2];
+                n_o1 = a.ov_off[li + 2];
+            }
             const long long kl = a.lin_k * ((long long)X.lq + X.lt) - 1024 * X.ls;
+            if (prof) ++pf.v[kPfLeaves];
+            DP_LAP(kPfCycLoad)
             // ---- A: the ring's non-overlapping candidates
             long long best = 0;
             int best_node = -1;
@@ -459,29 +661,22 @@ __global__ void __launch_bounds__(kWave) k_dp_fast(DpArgs a) {
                     if (dq >= 0 && dt >= 0) sc = r_tot[lane] + X.ls - dp_gap_lds(a, s_gap, dq, dt);
                 }
                 // max score, ties to the smaller node; > 0 only
-                long long bs = sc > 0 ? sc : -1;
-                int bn = sc > 0 ? nd : 0x7fffffff;
-#pragma unroll
-                for (int d = 32; d > 0; d >>= 1) {
-                    const long long os = __shfl_xor(bs, d, kWave);
-                    const int on = __shfl_xor(bn, d, kWave);
-                    if (os > bs || (os == bs && on < bn)) {
-                        bs = os;
-                        bn = on;
-                    }
-                }
+                const long long bs = dp_wave_max64(sc > 0 ? sc : -1, lane);
                 if (bs > 0) {
                     best = bs;
-                    best_node = bn;
+                    best_node = dp_wave_min32(sc == bs ? nd : 0x7fffffff, lane);
                 }
             }
+            DP_LAP(kPfCycSeed)
             // ---- B: the fast walk
-            dp_walk<true>(a, S, s_m, s_gap, P, X, kl, best, best_node);
+            dp_walk<true>(a, S, s_m, s_gap, P, X, kl, best, best_node, pf, prof);
+            DP_LAP(kPfCycWalk)
             // ---- C: anomalies among the overlapping candidates
             bool fb = false;
             {
                 const long long need = best > 0 ? best : 1;
                 const int lsize = X.lqe - X.lq;
+                if (prof) pf.v[kPfOvChecks] += o1 - o0;
                 for (int64_t k = o0 + lane; k < o1; k += kWave) {
                     const int c = a.ov[k];
                     if (c < 0) {
@@ -505,10 +700,13 @@ __global__ void __launch_bounds__(kWave) k_dp_fast(DpArgs a) {
                     if (sc > bc || 1024 * sc > bl) fb = true;
                 }
             }
+            DP_LAP(kPfCycAnom)
             if (__ballot(fb)) {
                 best = 0;
                 best_node = -1;
-                dp_walk<false>(a, S, s_m, s_gap, P, X, 0, best, best_node);
+                if (prof) ++pf.v[kPfFallbacks];
+                dp_walk<false>(a, S, s_m, s_gap, P, X, 0, best, best_node, pf, prof);
+                DP_LAP(kPfCycFb)
             }
             // ---- D: findBestPredecessors (chainBlock.c:289-297) + updateScoresOnWay
             long long total = X.ls;
@@ -533,8 +731,16 @@ __global__ void __launch_bounds__(kWave) k_dp_fast(DpArgs a) {
             }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
             __syncthreads();
+            DP_LAP(kPfCycCommit)
         }
         __syncthreads();
+    }
+#undef DP_LAP
+    if (prof && lane < kDpProf) {
+        unsigned long long v = 0;
+        for (int k = 0; k < kDpProf; ++k)
+            if (k == lane) v = pf.v[k];
+        atomicAdd(a.prof + lane, v);
     }
 }
 

@@ -2580,8 +2580,15 @@ static void gpair_export(ax_gpair *G) {
     G->ovl = NULL;
     if (dp_fast_enabled(w)) {
         /* each leaf's overlapping candidates (dp_overlaps: leaf nodes; a
-         * single -1 past kOvCap sends the leaf to the reference search) */
+         * single -1 past the cap sends the leaf to the reference search;
+         * GAC_DP_OVCAP lowers the cap -- a test hook for that path) */
         enum { kOvCap = 1024 };
+        static int ov_cap = -1;
+        if (ov_cap < 0) {
+            const char *oc = getenv("GAC_DP_OVCAP");
+            const int v = oc && *oc ? atoi(oc) : kOvCap;
+            ov_cap = v >= 0 && v <= kOvCap ? v : kOvCap;
+        }
         int32_t maxsz, buf[kOvCap];
         dp_leaf_positions(w, &maxsz);
         int64_t on = 0, ocap = nl + 64;
@@ -2590,7 +2597,7 @@ static void gpair_export(ax_gpair *G) {
         G->ooff[0] = 0;
         for (int32_t i = 0; i < nl; ++i) {
             w->cut_t = i;
-            int k = dp_overlaps(w, w->tord[i], i, maxsz, buf, kOvCap);
+            int k = dp_overlaps(w, w->tord[i], i, maxsz, buf, ov_cap);
             if (k < 0) {
                 buf[0] = -1;
                 k = 1;

@@ -1162,6 +1162,10 @@ static int pwritev_all(int fd, struct iovec *iov, int n, off_t off) {
                 continue;
             return -1;
         }
+        if (w == 0) { /* (no progress with bytes left: an error, not a spin) */
+            errno = EIO;
+            return -1;
+        }
         off += w;
         size_t left = (size_t)w;
         while (n > 0 && left >= iov->iov_len) {

@@ -184,7 +184,8 @@ struct gac_net {
      * top level), filled by the first pass that chases the parent links
      * (gac_net_get_fills with flags) and read by the output's "reached" pass */
     int64_t *pord[2];
-    int pord_ok[2];
+    int pord_ok[2];          /* (set once, release/acquire: never rebuilt) */
+    pthread_mutex_t pord_mu; /* the first build of pord (callers share a const net) */
     /* per side, ascending: the pre-order positions of the top-level fills
      * (where the runs of whole subtrees may start), from finishNet */
     int64_t *top[2];
@@ -1047,6 +1048,7 @@ void gac_net_free(gac_net *n) {
     free(n->order[1]);
     free(n->pord[0]);
     free(n->pord[1]);
+    pthread_mutex_destroy(&n->pord_mu);
     free(n->top[0]);
     free(n->top[1]);
     free(n->nlen[0]);
@@ -1762,6 +1764,8 @@ static int net_build(const gac_net_input *in, const gac_net_opts *opt, int sides
                      const uint8_t *t_keep, const uint8_t *q_keep, gac_net **out) {
     *out = NULL;
     gac_net *n = calloc(1, sizeof(*n));
+    if (n)
+        pthread_mutex_init(&n->pord_mu, NULL);
     n->in = *in;
     n->opt = *opt;
     n->sides = sides;
@@ -2066,6 +2070,7 @@ typedef struct gf_job {
     int64_t per;
     _Atomic int64_t next;
     int32_t *wb0, *wn; /* gac_net_get_fill_windows */
+    int64_t *po;       /* the parent positions being built (NULL: built) */
 } gf_job;
 
 static void *fills_thread(void *arg) {
@@ -2114,7 +2119,7 @@ static int64_t next_top_level(const gac_net *n, int side, int64_t i) {
         }
         return lo < n->n_top[side] ? t[lo] : n->n_order[side];
     }
-    if (n->pord_ok[side]) {
+    if (__atomic_load_n(&n->pord_ok[side], __ATOMIC_ACQUIRE)) {
         const int64_t *po = n->pord[side];
         while (i < n->n_order[side] && po[i] >= 0)
             ++i;
@@ -2136,7 +2141,7 @@ static void *visible_thread(void *arg) {
             break;
         const int64_t a = next_top_level(n, side, r * J->per);
         const int64_t b = next_top_level(n, side, (r + 1) * J->per < nf ? (r + 1) * J->per : nf);
-        int64_t *po = n->pord[side];
+        int64_t *po = J->po;
         for (int64_t i = a; i < b; ++i) {
             const nfill *pf = n->order[side][i]->pgap->pfill;
             if (po)
@@ -2168,13 +2173,19 @@ int gac_net_get_fills(const gac_net *n, int side, int32_t *chain, int32_t *start
      * parallel over runs that start at top-level fills (whole subtrees) */
     if (flags) {
         /* (the parent positions are kept for the output's pass; the net is
-         * const to callers, this is a cache) */
+         * const to callers, this is a cache: built once, under pord_mu, and
+         * never written again -- a later pass gets po = NULL) */
         gac_net *nm = (gac_net *)n;
-        if (!nm->pord[side])
+        pthread_mutex_lock(&nm->pord_mu);
+        const int build = !__atomic_load_n(&nm->pord_ok[side], __ATOMIC_ACQUIRE);
+        if (build && !nm->pord[side])
             nm->pord[side] = malloc((size_t)(nf ? nf : 1) * sizeof(int64_t));
+        J.po = build ? nm->pord[side] : NULL;
         atomic_store(&J.next, 0);
         gac_run_threads(nt < nrun ? nt : (int)(nrun ? nrun : 1), visible_thread, &J);
-        nm->pord_ok[side] = 1;
+        if (build)
+            __atomic_store_n(&nm->pord_ok[side], 1, __ATOMIC_RELEASE);
+        pthread_mutex_unlock(&nm->pord_mu);
     }
     gac_mark("get_fills: done");
     return GAC_OK;
@@ -2244,7 +2255,8 @@ static void *rw_thread(void *arg) {
                 __builtin_prefetch(n->order[side][i + 16]);
             const nfill *f = n->order[side][i];
             const nfill *pf = f->pgap->pfill;
-            J->po[i] = pf ? pf->ord : -1;
+            if (J->po)
+                J->po[i] = pf ? pf->ord : -1;
             const int sz = f->full ? full_size(n, f->chain) : f->ali;
             const uint8_t v = (!pf || J->vis[pf->ord]) && sz >= n->opt.min_fill;
             J->vis[i] = v;
@@ -2271,20 +2283,24 @@ int gac_net_rescore_windows(const gac_net *n, int side, gac_window **windows, in
     const int nt = gac_host_threads();
     const int64_t nf = n->n_order[side];
     gac_net *nm = (gac_net *)n; /* (the parent positions are a cache, as in get_fills) */
-    if (!nm->pord[side])
+    pthread_mutex_lock(&nm->pord_mu);
+    const int build = !__atomic_load_n(&nm->pord_ok[side], __ATOMIC_ACQUIRE);
+    if (build && !nm->pord[side])
         nm->pord[side] = malloc((size_t)(nf ? nf : 1) * sizeof(int64_t));
     rw_job J;
     memset(&J, 0, sizeof(J));
     J.n = n;
     J.side = side;
     J.vis = malloc((size_t)(nf ? nf : 1));
-    J.po = nm->pord[side];
+    J.po = build ? nm->pord[side] : NULL;
     J.per = nf / (8 * (int64_t)nt) + 1;
     J.nrun = (nf + J.per - 1) / J.per;
     J.runs = calloc((size_t)(J.nrun ? J.nrun : 1), sizeof(rw_run));
     atomic_init(&J.next, 0);
     gac_run_threads(nt < J.nrun ? nt : (int)(J.nrun ? J.nrun : 1), rw_thread, &J);
-    nm->pord_ok[side] = 1;
+    if (build)
+        __atomic_store_n(&nm->pord_ok[side], 1, __ATOMIC_RELEASE);
+    pthread_mutex_unlock(&nm->pord_mu);
     J.off = malloc((size_t)(J.nrun + 1) * sizeof(int64_t));
     J.off[0] = 0;
     for (int64_t r = 0; r < J.nrun; ++r)
@@ -2759,7 +2775,7 @@ static void *wreached_thread(void *arg) {
             return NULL;
         const int64_t a = next_top_level(J->n, J->side, r * per);
         const int64_t b = next_top_level(J->n, J->side, (r + 1) * per < J->nf ? (r + 1) * per : J->nf);
-        const int64_t *po = J->n->pord_ok[J->side] ? J->n->pord[J->side] : NULL;
+        const int64_t *po = __atomic_load_n(&J->n->pord_ok[J->side], __ATOMIC_ACQUIRE) ? J->n->pord[J->side] : NULL;
         if (po) {
             for (int64_t i = a; i < b; ++i)
                 J->reached[i] = J->show[i] && (po[i] < 0 || J->reached[po[i]]);

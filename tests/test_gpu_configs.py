@@ -302,6 +302,33 @@ def test_c4_shaped_axtchain_5m_blocks(tmp_path):
     _same(os.path.join(d, "dev.chain"), os.path.join(d, "ref.chain"))
 
 
+@pytest.mark.timeout(900)
+def test_device_dp_fallbacks(tmp_path):
+    """k_dp_fast's two ways back to the reference walk, on the device: the
+    anomaly check (an overlapping candidate whose crossover beats its bound,
+    chainConnect.c:61-105) on a C4-shaped set dense with overlaps, and the
+    overlap lists' cap (GAC_DP_OVCAP=0: every leaf with an overlapping
+    candidate gets a -1 entry) -- both against the reference's chains, with
+    the kernel's own count of fallbacks (GAC_DP_PROF) asserted non-zero."""
+    synth = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                         "genomealignmenttools_amd", "libexec", "gac_synth")
+    d = str(tmp_path)
+    subprocess.run([synth, "c4", d, "-blocks=200000", "-nt=2", "-nq=2", "-tsize=3000000",
+                    "-qsize=2500000", "-threads=4"], check=True, timeout=300, capture_output=True)
+    args = ["-linearGap=loose", "-psl", "in.psl", "t.2bit", "q.2bit"]
+    _run([_ref("axtChain")] + args + ["ref.chain"], cwd=d, timeout=600)
+    counts = []
+    for cap in ("", "0"):
+        out = "dev%s.chain" % cap
+        r = _run([_bin("axtChain")] + args + [out], cwd=d,
+                 env={"GAC_AXT_DP": "gpu", "GAC_DP_PROF": "1", "GAC_DP_OVCAP": cap})
+        m = re.search(r"k_dp_fast .*?(\d+) leaves, (\d+) fallbacks", r.stderr)
+        assert m, r.stderr[-2000:]
+        counts.append(int(m.group(2)))
+        _same(os.path.join(d, out), os.path.join(d, "ref.chain"))
+    assert counts[0] > 0 and counts[1] > counts[0], counts
+
+
 # ---------------------------------------------------------------- edge cases
 def _synth(seed):
     return os.path.join(GOLDEN, f"synth{seed}")
