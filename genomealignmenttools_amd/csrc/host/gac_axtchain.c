@@ -2936,8 +2936,10 @@ static int axt_dp_gpu(ax_job *J, int nt) {
  * 0.7 of it), and is at most 5000 leaves: the device side's host work
  * (export of paths and overlap lists, peel, finish) costs the host about
  * as much per leaf as the DP it saves, so a larger share slows the run
- * (r05multi: pairs up to 5000 leaves, 1.4 M of C4's 50 M blocks, is
- * neutral; the model's 189 k-leaf bound is +0.5 s).  Pairs go to the
+ * (r06split1, C4 at 50 M blocks, the round-6 kernel: host only 8.89 /
+ * 9.43 s; pairs up to 5000 leaves, 2.8 % of the blocks, 8.98 / 9.06 s; up
+ * to 50 k leaves, 17.6 %, 8.92 / 9.06 s; the model's 187 k-leaf bound,
+ * 29 %, 9.66 / 9.93 s).  Pairs go to the
  * device from the smallest up.  GAC_AXT_DP=host: no device pairs;
  * GAC_DP_GPU_MAX=n: the leaf cap (0: none); GAC_DP_DEV_US /
  * GAC_DP_HOST_US: the per-leaf times of the model.  Returns the first
@@ -2948,14 +2950,14 @@ static int64_t dp_device_split(const int64_t *psize, const int32_t *order, int64
     if ((dpm && strcmp(dpm, "host") == 0) || !e->fast || np == 0)
         return np;
     const char *dv = getenv("GAC_DP_DEV_US"), *hv = getenv("GAC_DP_HOST_US");
-    const double dev_us = dv && atof(dv) > 0 ? atof(dv) : 20.0;  /* k_dp_fast, r05dp3 */
+    const double dev_us = dv && atof(dv) > 0 ? atof(dv) : 14.0;  /* k_dp_fast, r06dp */
     const double host_us = hv && atof(hv) > 0 ? atof(hv) : 0.47; /* team, C4 (r04i) */
     const double crit = (double)psize[order[0]] * host_us * 1e-6;
     if (crit < 0.25) /* (small runs: the device's start-up costs more) */
         return np;
     int64_t lmax = (int64_t)(0.7 * crit / (dev_us * 1e-6));
     const char *mx = getenv("GAC_DP_GPU_MAX");
-    const int64_t cap = mx && *mx ? atoll(mx) : 5000;
+    const int64_t cap = mx && *mx ? atoll(mx) : 50000;
     if (cap < lmax)
         lmax = cap;
     if (lmax < 1)
