@@ -75,6 +75,7 @@ REF_TOOL = os.path.join(REPO, "oracle", "_ref", "chainNet")
 SC_TOOL = os.path.join(PKG, "bin", "scoreChain")
 AXT_TOOL = os.path.join(PKG, "bin", "axtChain")
 REF_SC_TOOL = os.path.join(REPO, "oracle", "_ref", "scoreChain")
+REF_AXT_TOOL = os.path.join(REPO, "oracle", "_ref", "axtChain")
 SAMPLE_TARGETS = ("chr21", "chr22")
 # all-cores baseline: the reference split by target chromosome, one process
 # per sequence, run side by side (how the reference is parallelised on a
@@ -102,6 +103,8 @@ def parse():
     p.add_argument("--no-c4", action="store_true", help="skip the axtChain C4 leg")
     p.add_argument("--c4-blocks", type=int, default=50_000_000)
     p.add_argument("--c4-steps", type=int, default=1)
+    p.add_argument("--no-c4-ref", action="store_true",
+                   help="skip the reference axtChain timed on a C4 pair subset")
     p.add_argument("--no-kernel", action="store_true", help="skip the kernel/roofline legs")
     p.add_argument("--no-scorechain", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -997,7 +1000,51 @@ def c4_leg(args, dist, world, rank, local, barrier, step_env):
         res["parity_full"] = full_parity("c4", {"in_psl_sha256": p("in.psl"),
                                                 "axtchain.chain_sha256": out})
     os.remove(out)
+    if world == 1 and not args.no_c4_ref:
+        try:
+            res["reference_on_box"] = c4_ref_sample(d)
+        except Exception as ex:  # (reported, never fatal)
+            res["reference_on_box"] = {"error": str(ex)[:300]}
     return res
+
+
+def c4_ref_sample(d):
+    """The reference axtChain (oracle/_ref, one process, test
+    infrastructure) timed on this host on a pair subset of C4: the PSL
+    records whose target is chr4 (42 of the 1008 seqPairs, ~0.33 M of the
+    50 M blocks), with ours on the same file and the two outputs compared.
+    The reference's whole-C4 time (1287 s, build container) is dominated by
+    the 11.5 M-block pair, whose DP cost grows faster than linearly, so this
+    sample's per-block rate overstates the reference's whole-set rate."""
+    if not os.path.exists(REF_AXT_TOOL):
+        return {"error": f"{REF_AXT_TOOL} not built (make ref)"}
+    p = lambda x: os.path.join(d, x)
+    sample = p("sample_chr4.psl")
+    if not os.path.exists(sample):
+        with open(sample + ".tmp", "w") as f:
+            subprocess.run(["awk", "-F\t", '$14=="chr4"', p("in.psl")], stdout=f, check=True,
+                           timeout=600)
+        os.replace(sample + ".tmp", sample)
+    blocks = 0
+    with open(sample) as f:
+        for line in f:
+            blocks += int(line.split("\t", 18)[17])
+    args_ = ["-linearGap=loose", "-verbose=0", "-psl", sample, p("t.2bit"), p("q.2bit")]
+    t0 = time.perf_counter()
+    run_tool([REF_AXT_TOOL] + args_ + [p("sample.ref.chain")], [])
+    t_ref = time.perf_counter() - t0
+    run_tool([AXT_TOOL] + args_ + [p("sample.ours.chain")], [])  # (warm)
+    t0 = time.perf_counter()
+    run_tool([AXT_TOOL] + args_ + [p("sample.ours.chain")], [])
+    t_ours = time.perf_counter() - t0
+    same = filecmp.cmp(p("sample.ref.chain"), p("sample.ours.chain"), shallow=False)
+    for x in ("sample.ref.chain", "sample.ours.chain"):
+        os.remove(p(x))
+    return {"sample": "C4 PSL records with target chr4 (every query, both strands)",
+            "blocks": blocks, "reference_seconds": t_ref, "ours_seconds": t_ours,
+            "reference_Mblocks_per_s": blocks / t_ref / 1e6, "identical": same,
+            "cores": 1, "kind": "reference (oracle/_ref/axtChain), this host",
+            "cpu_model": host_cpu()["cpu_model"]}
 
 
 def c2_leg(args, steps, warmup):
