@@ -214,6 +214,15 @@ _PROTOS = {
     "gac_prof_enable": (C.c_int, [C.c_void_p, C.c_int]),
     "gac_prof_read": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "gac_prof_reset": (C.c_int, [C.c_void_p]),
+    "gac_comm_open": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double,
+                                C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
+    "gac_comm_backend": (C.c_int, [C.c_void_p]),
+    "gac_comm_init_seconds": (C.c_double, [C.c_void_p]),
+    "gac_allgather": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
+    "gac_allgatherv": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p),
+                                 C.POINTER(C.c_size_t)]),
+    "gac_comm_barrier": (C.c_int, [C.c_void_p]),
+    "gac_comm_close": (None, [C.c_void_p]),
 }
 
 EXPORTED = tuple(_PROTOS)

@@ -475,6 +475,37 @@ int gac_net_write_begin(const gac_net *net, int side, const char *const *meta, i
 int gac_net_write_end(gac_net_wpre *w, const int64_t *t_scores, FILE *f);
 void gac_net_write_free(gac_net_wpre *w);
 
+/* ---- the -nranks collective (gac_allgather) ---------------
+ * One process per GPU of one node.  A communicator joins `nranks` processes
+ * through a rendezvous prefix: a path the ranks share and that is unique to
+ * the run (the tools use their output path plus the run's GAC_RANK_TOKEN);
+ * the host backend keeps its part and barrier files next to it.
+ *   GAC_COMM_RCCL  ncclAllGather over xGMI (librccl loaded at run time; the
+ *                  unique id passes through the rendezvous files), `device`
+ *                  = this rank's GPU; RCCL refuses two ranks on one device.
+ *   GAC_COMM_HOST  part files in the node's page cache, no device.
+ *   GAC_COMM_AUTO  GAC_COMM=rccl|host if set, else RCCL when device >= 0.
+ * A wait gives up after timeout_s seconds (<= 0: 600) or when alive(peer,
+ * user) returns 0 (NULL: no check), with GAC_E_STATE.  Every rank must make
+ * the same calls in the same order. */
+typedef struct gac_comm gac_comm;
+#define GAC_COMM_AUTO 0
+#define GAC_COMM_HOST 1
+#define GAC_COMM_RCCL 2
+int gac_comm_open(const char *rendezvous, int nranks, int rank, int device, int backend,
+                  double timeout_s, int (*alive)(int rank, void *user), void *user,
+                  gac_comm **out);
+int gac_comm_backend(const gac_comm *comm); /* GAC_COMM_HOST / GAC_COMM_RCCL */
+double gac_comm_init_seconds(const gac_comm *comm); /* RCCL set-up time (0: host) */
+/* ncclAllGather: `bytes` from every rank; recv holds nranks * bytes, rank r's
+ * part at r * bytes.  Host buffers, synchronous. */
+int gac_allgather(gac_comm *comm, const void *send, size_t bytes, void *recv);
+/* parts of any size: *recv = malloc'd concatenation in rank order (free()),
+ * counts[0 .. nranks) = each rank's bytes */
+int gac_allgatherv(gac_comm *comm, const void *send, size_t bytes, void **recv, size_t *counts);
+int gac_comm_barrier(gac_comm *comm);
+void gac_comm_close(gac_comm *comm);
+
 /* ---- device memory helpers (for callers without their own allocator) ---- */
 int gac_dev_alloc(gac_ctx *ctx, size_t bytes, void **dptr);
 int gac_dev_free(gac_ctx *ctx, void *dptr);
