@@ -7,6 +7,7 @@
 #include <limits.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <stdatomic.h>
 #include <string.h>
 
 #include "gac_tool.h"
@@ -62,16 +63,36 @@ void gt_lines_free(gt_lines *l) {
 }
 
 /* ------------------------------------------------------------ net tree */
+/* Every line is classified and parsed as a fill/gap line on all threads
+ * first (pre_line); the tree is then built by the reference's recursion in
+ * one serial pass that only reads those records.  A line the fast parse
+ * cannot settle (or an error) goes through fill_from_line as before, which
+ * aborts with the reference's message at the same point of the serial
+ * pass. */
+typedef struct pre_line {
+    int32_t lead;    /* leading spaces */
+    uint8_t real;    /* lineFileNextReal keeps it */
+    uint8_t ok;      /* fill record parsed (else: fill_from_line decides) */
+    gt_fill f;
+} pre_line;
+
 typedef struct reader {
     const gt_lines *l;
     int64_t pos;
     const char *what;
     gt_netset *ns;
+    const pre_line *pre; /* NULL: parse lines as they come */
 } reader;
 
 /* lineFileNextReal: skip blank lines and lines whose first non-blank is '#' */
 static char *next_real(reader *r) {
     while (r->pos < r->l->n) {
+        if (r->pre) {
+            const int64_t i = r->pos++;
+            if (r->pre[i].real)
+                return r->l->line[i];
+            continue;
+        }
         char *s = r->l->line[r->pos++];
         const char *p = s;
         while (isspace((unsigned char)*p))
@@ -93,6 +114,15 @@ static int32_t need_num(reader *r, char **w, int i) {
 
 /* cnFillFromLine (chainNet.c:86-150): the fields chainCleaner uses */
 static int32_t fill_from_line(reader *r, char *line) {
+    if (r->pre && r->pre[r->pos - 1].ok) { /* (parsed on the threads) */
+        gt_netset *ns = r->ns;
+        if (ns->nf == ns->fcap) {
+            ns->fcap = ns->fcap ? ns->fcap * 2 : 4096;
+            ns->fills = realloc(ns->fills, (size_t)ns->fcap * sizeof(gt_fill));
+        }
+        ns->fills[ns->nf] = r->pre[r->pos - 1].f;
+        return (int32_t)ns->nf++;
+    }
     char *w[64];
     char *copy = strdup(line);
     int wc = gac_chop_white(copy, w, 64);
@@ -134,6 +164,94 @@ static int lead_spaces(const char *s) {
     return d;
 }
 
+/* need_num's test on a token: the whole token is a decimal long (strtol) */
+static int tok_num(const char *t, int len, int32_t *v) {
+    char b[64];
+    if (len <= 0 || len >= (int)sizeof(b))
+        return 0;
+    memcpy(b, t, (size_t)len);
+    b[len] = 0;
+    char *end;
+    const long x = strtol(b, &end, 10);
+    if (*end != 0)
+        return 0;
+    *v = (int32_t)x;
+    return 1;
+}
+
+/* fill_from_line's fields without the copy: 1 = parsed exactly as it
+ * would; 0 = let fill_from_line handle it (errors, odd tokens) */
+static int fast_fill(const char *line, gt_fill *f) {
+    const char *w[64];
+    int wl[64], wc = 0;
+    const char *p = line;
+    while (wc < 64) { /* gac_chop_white */
+        while (*p && isspace((unsigned char)*p))
+            ++p;
+        if (*p == 0)
+            break;
+        w[wc] = p;
+        while (*p && !isspace((unsigned char)*p))
+            ++p;
+        wl[wc] = (int)(p - w[wc]);
+        ++wc;
+    }
+    if (wc < 7)
+        return 0;
+    memset(f, 0, sizeof(*f));
+    f->child = f->next = -1;
+    int32_t v;
+    if (!tok_num(w[1], wl[1], &f->tstart) || !tok_num(w[2], wl[2], &f->tsize) ||
+        !tok_num(w[5], wl[5], &v) || !tok_num(w[6], wl[6], &v))
+        return 0;
+    for (int i = 7; i < wc; i += 2) {
+        if (i + 1 >= wc)
+            break;
+        if (wl[i] == 5 && memcmp(w[i], "score", 5) == 0) {
+            char b[64];
+            if (wl[i + 1] >= (int)sizeof(b))
+                return 0;
+            memcpy(b, w[i + 1], (size_t)wl[i + 1]);
+            b[wl[i + 1]] = 0;
+            f->score = atof(b);
+        } else if (wl[i] == 4 && memcmp(w[i], "type", 4) == 0) {
+        } else {
+            if (!tok_num(w[i + 1], wl[i + 1], &v))
+                return 0;
+            if (wl[i] == 2 && memcmp(w[i], "id", 2) == 0)
+                f->chain_id = v;
+        }
+    }
+    return 1;
+}
+
+typedef struct pre_job {
+    const gt_lines *l;
+    pre_line *pre;
+    int64_t per;
+    _Atomic int64_t next;
+} pre_job;
+
+static void *pre_thread(void *arg) {
+    pre_job *J = arg;
+    for (;;) {
+        const int64_t a = atomic_fetch_add(&J->next, 1) * J->per;
+        if (a >= J->l->n)
+            return NULL;
+        const int64_t b = a + J->per < J->l->n ? a + J->per : J->l->n;
+        for (int64_t i = a; i < b; ++i) {
+            const char *s = J->l->line[i];
+            pre_line *x = &J->pre[i];
+            const char *q = s;
+            while (isspace((unsigned char)*q))
+                ++q;
+            x->real = *q != 0 && *q != '#';
+            x->lead = lead_spaces(s);
+            x->ok = x->real && x->lead > 0 && fast_fill(s, &x->f);
+        }
+    }
+}
+
 /* cnFillRead (chainNet.c:152-178) */
 static int32_t read_list(reader *r) {
     int depth = 0;
@@ -142,7 +260,7 @@ static int32_t read_list(reader *r) {
         char *line = next_real(r);
         if (!line)
             break;
-        const int d = lead_spaces(line);
+        const int d = r->pre ? r->pre[r->pos - 1].lead : lead_spaces(line);
         if (fill < 0)
             depth = d;
         if (d < depth) {
@@ -167,7 +285,15 @@ static int32_t read_list(reader *r) {
 
 void gt_net_parse(const gt_lines *l, const char *what, gt_netset *ns) {
     memset(ns, 0, sizeof(*ns));
-    reader r = {l, 0, what, ns};
+    reader r = {l, 0, what, ns, NULL};
+    pre_line *pre = NULL;
+    if (l->n >= 65536 && !getenv("GAC_NET_PARSE_SERIAL")) {
+        pre = malloc((size_t)l->n * sizeof(pre_line));
+        pre_job J = {l, pre, 8192, 0};
+        atomic_init(&J.next, 0);
+        gac_run_threads(gt_threads(), pre_thread, &J);
+        r.pre = pre;
+    }
     char *line;
     while ((line = next_real(&r)) != NULL) {
         if (strncmp(line, "net ", 4) != 0)
@@ -187,6 +313,7 @@ void gt_net_parse(const gt_lines *l, const char *what, gt_netset *ns) {
         free(copy);
         n->first = read_list(&r);
     }
+    free(pre);
 }
 
 void gt_netset_free(gt_netset *ns) {
