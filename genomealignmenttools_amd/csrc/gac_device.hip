@@ -1392,11 +1392,13 @@ extern "C" int gac_chain_dp_ex(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq
                         "[gac_chain_dp] k_dp_fast %.3f s, %llu pairs, %llu leaves, %llu fallbacks; per leaf: "
                         "%.2f windows, %.3f fallback windows, %.3f windows with an overlapping candidate, "
                         "%.2f overlap checks; cycles per leaf: load %.0f seed %.0f walk %.0f "
-                        "(node loads + bounds %.0f) anomalies %.0f fallback %.0f commit %.0f\n",
+                        "(node loads + bounds %.0f) anomalies %.0f fallback %.0f commit %.0f; next windows: %.2f per leaf, "
+                        "%.3f contiguous\n",
                         secs, (unsigned long long)n_pairs, pv[kPfLeaves], pv[kPfFallbacks],
                         pv[kPfWindows] / L, pv[kPfFbWindows] / L, pv[kPfXoverWin] / L, pv[kPfOvChecks] / L,
                         pv[kPfCycLoad] / L, pv[kPfCycSeed] / L, pv[kPfCycWalk] / L, pv[kPfCycXover] / L,
-                        pv[kPfCycAnom] / L, pv[kPfCycFb] / L, pv[kPfCycCommit] / L);
+                        pv[kPfCycAnom] / L, pv[kPfCycFb] / L, pv[kPfCycCommit] / L, pv[kPfNextWin] / L,
+                        pv[kPfNextWin] ? (double)pv[kPfNextSeq] / pv[kPfNextWin] : 0.0);
             }
             hipFree(d_prof);
         }

@@ -72,7 +72,7 @@ struct DpArgs {
 enum DpProf {
     kPfLeaves, kPfWindows, kPfFbWindows, kPfFallbacks, kPfXoverWin, kPfOvChecks,
     kPfCycLoad, kPfCycSeed, kPfCycWalk, kPfCycAnom, kPfCycFb, kPfCycCommit, kPfCycXover,
-    kDpProf
+    kPfNextWin, kPfNextSeq, kDpProf
 };
 
 // One overlapping adjacent block pair: left block ends at (lqe, lte), right

@@ -552,7 +552,12 @@ __device__ void dp_walk(const DpArgs &a, const DpSeq &S, const int *m, const DpG
         // the next visited node after the window: past every skip interval
         // that reaches beyond it (they nest) -- the last lane's prefix max
         // (lanes past the pair's end only push it past the end too)
-        p0 = max(p0 + kWave, __builtin_amdgcn_readlane(incl, kWave - 1));
+        const int nx = max(p0 + kWave, __builtin_amdgcn_readlane(incl, kWave - 1));
+        if (prof && nx < nn) {  // (the walk goes on: contiguously, or by a jump)
+            ++pf.v[kPfNextWin];
+            if (nx == p0 + kWave) ++pf.v[kPfNextSeq];
+        }
+        p0 = nx;
     }
 }
 
