@@ -21,7 +21,7 @@ CFLAGS   := -O2 -mpopcnt -std=gnu11 -fPIC -Wall -ffp-contract=off -Iinclude -I$(
 
 HOST_SRC := $(wildcard $(CSRC)/host/*.c)
 HOST_OBJ := $(patsubst $(CSRC)/host/%.c,$(OBJDIR)/host/%.o,$(HOST_SRC))
-HIP_SRC  := $(CSRC)/gac_kernels.hip $(CSRC)/gac_dp.hip $(CSRC)/gac_device.hip $(CSRC)/gac_comm.hip
+HIP_SRC  := $(CSRC)/gac_kernels.hip $(CSRC)/gac_dp.hip $(CSRC)/gac_dptree.hip $(CSRC)/gac_device.hip $(CSRC)/gac_comm.hip
 HIP_OBJ  := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRC))
 HDRS     := include/gachain.h $(CSRC)/gac_kernels.h $(CSRC)/gac_dp.h $(wildcard $(CSRC)/host/*.h)
 

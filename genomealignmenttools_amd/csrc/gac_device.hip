@@ -1224,6 +1224,42 @@ static int dev_upload(gac_ctx *c, T **d, const void *h, size_t n) {
     return GAC_OK;
 }
 
+// k_dp_fast (fast) or k_dp over a.n_pairs pairs; GAC_DP_PROF: k_dp_fast's
+// per-phase cycle counters, summed over pairs, to stderr
+static hipError_t dp_launch(gac_ctx *c, DpArgs &a, int grid, bool fast) {
+    unsigned long long *d_prof = nullptr;
+    hipError_t e = hipSuccess;
+    const char *dpprof = getenv("GAC_DP_PROF");
+    if (fast && dpprof && *dpprof && *dpprof != '0' &&
+        (e = hipMalloc(&d_prof, kDpProf * sizeof(unsigned long long))) == hipSuccess)
+        e = hipMemsetAsync(d_prof, 0, kDpProf * sizeof(unsigned long long), c->stream);
+    a.prof = d_prof;
+    const double tk0 = wall_s();
+    if (e == hipSuccess) e = fast ? launch_dp_fast(a, grid, c->stream) : launch_dp(a, grid, c->stream);
+    if (d_prof && e == hipSuccess) {
+        unsigned long long pv[kDpProf];
+        e = hipMemcpyAsync(pv, d_prof, sizeof(pv), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e == hipSuccess) {
+            const double secs = wall_s() - tk0, L = pv[kPfLeaves] ? (double)pv[kPfLeaves] : 1.0;
+            fprintf(stderr,
+                    "[gac_chain_dp] k_dp_fast %.3f s, %llu pairs, %llu leaves, %llu fallbacks; per leaf: "
+                    "%.2f windows, %.3f fallback windows, %.3f windows with an overlapping candidate, "
+                    "%.2f overlap checks; cycles per leaf: load %.0f seed %.0f walk %.0f "
+                    "(node loads + bounds %.0f) anomalies %.0f fallback %.0f commit %.0f; next windows: %.2f per leaf, "
+                    "%.3f contiguous\n",
+                    secs, (unsigned long long)a.n_pairs, pv[kPfLeaves], pv[kPfFallbacks],
+                    pv[kPfWindows] / L, pv[kPfFbWindows] / L, pv[kPfXoverWin] / L, pv[kPfOvChecks] / L,
+                    pv[kPfCycLoad] / L, pv[kPfCycSeed] / L, pv[kPfCycWalk] / L, pv[kPfCycXover] / L,
+                    pv[kPfCycAnom] / L, pv[kPfCycFb] / L, pv[kPfCycCommit] / L, pv[kPfNextWin] / L,
+                    pv[kPfNextWin] ? (double)pv[kPfNextSeq] / pv[kPfNextWin] : 0.0);
+        }
+        hipFree(d_prof);
+        a.prof = nullptr;
+    }
+    return e;
+}
+
 extern "C" int gac_chain_dp(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq, const int32_t *q_seq,
                             const uint8_t *q_strand, const int64_t *node_off,
                             const int32_t *node_a, const int32_t *node_b, const int64_t *leaf_off,
@@ -1373,35 +1409,7 @@ extern "C" int gac_chain_dp_ex(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq
         // one wave per pair, every pair resident at once (largest first is
         // the caller's order; the grid covers them all)
         const int grid = (int)std::min<int64_t>(n_pairs, 1 << 20);
-        // GAC_DP_PROF: k_dp_fast's per-phase cycle counters, to stderr
-        unsigned long long *d_prof = nullptr;
-        const char *dpprof = getenv("GAC_DP_PROF");
-        if (fast && dpprof && *dpprof && *dpprof != '0' && e == hipSuccess &&
-            (e = hipMalloc(&d_prof, kDpProf * sizeof(unsigned long long))) == hipSuccess)
-            e = hipMemsetAsync(d_prof, 0, kDpProf * sizeof(unsigned long long), c->stream);
-        a.prof = d_prof;
-        const double tk0 = wall_s();
-        if (e == hipSuccess) e = fast ? launch_dp_fast(a, grid, c->stream) : launch_dp(a, grid, c->stream);
-        if (d_prof && e == hipSuccess) {
-            unsigned long long pv[kDpProf];
-            e = hipMemcpyAsync(pv, d_prof, sizeof(pv), hipMemcpyDeviceToHost, c->stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-            if (e == hipSuccess) {
-                const double secs = wall_s() - tk0, L = pv[kPfLeaves] ? (double)pv[kPfLeaves] : 1.0;
-                fprintf(stderr,
-                        "[gac_chain_dp] k_dp_fast %.3f s, %llu pairs, %llu leaves, %llu fallbacks; per leaf: "
-                        "%.2f windows, %.3f fallback windows, %.3f windows with an overlapping candidate, "
-                        "%.2f overlap checks; cycles per leaf: load %.0f seed %.0f walk %.0f "
-                        "(node loads + bounds %.0f) anomalies %.0f fallback %.0f commit %.0f; next windows: %.2f per leaf, "
-                        "%.3f contiguous\n",
-                        secs, (unsigned long long)n_pairs, pv[kPfLeaves], pv[kPfFallbacks],
-                        pv[kPfWindows] / L, pv[kPfFbWindows] / L, pv[kPfXoverWin] / L, pv[kPfOvChecks] / L,
-                        pv[kPfCycLoad] / L, pv[kPfCycSeed] / L, pv[kPfCycWalk] / L, pv[kPfCycXover] / L,
-                        pv[kPfCycAnom] / L, pv[kPfCycFb] / L, pv[kPfCycCommit] / L, pv[kPfNextWin] / L,
-                        pv[kPfNextWin] ? (double)pv[kPfNextSeq] / pv[kPfNextWin] : 0.0);
-            }
-            hipFree(d_prof);
-        }
+        if (e == hipSuccess) e = dp_launch(c, a, grid, fast);
         if (e == hipSuccess)
             e = hipMemcpyAsync(total, d_total, nl * sizeof(long long), hipMemcpyDeviceToHost, c->stream);
         if (e == hipSuccess)
@@ -1426,6 +1434,302 @@ extern "C" int gac_chain_dp_ex(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq
     hipFree(d_ovoff);
     hipFree(d_ov);
     return rc;
+}
+
+// device allocations of one call, freed together (after a stream sync)
+namespace {
+struct DevBufs {
+    std::vector<void *> p;
+    hipError_t e = hipSuccess;
+    template <class T>
+    T *take(int64_t n) {
+        void *q = nullptr;
+        if (e == hipSuccess) e = hipMalloc(&q, (size_t)(n > 0 ? n : 1) * sizeof(T));
+        if (q) p.push_back(q);
+        return (T *)q;
+    }
+    ~DevBufs() {
+        for (void *q : p) hipFree(q);
+    }
+};
+}  // namespace
+
+// chainBlocks' DP for n_pairs pairs from their blocks: the leaves, kd-trees,
+// update paths and overlap lists built on the device (gac_dptree.hip), then
+// k_dp_fast (fast) or k_dp; see include/gachain.h
+extern "C" int gac_chain_dp_blocks(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq,
+                                   const int32_t *q_seq, const uint8_t *q_strand,
+                                   const int64_t *blk_off, const int32_t *box, const int32_t *score,
+                                   int fast, int64_t lin_k, int32_t min_entry, int32_t ov_cap,
+                                   int64_t *leaf_off, int32_t *tord, int64_t *total, int32_t *pred) {
+    gac_clear_error();
+    if (!c || n_pairs < 0 || (n_pairs && (!t_seq || !q_seq || !q_strand || !blk_off || !leaf_off)))
+        return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: bad argument");
+    if (!c->scoring) return gac_fail(GAC_E_STATE, "gac_chain_dp_blocks before gac_set_scoring");
+    CTX_LOCK(c);
+    if (!c->g[0].final || !c->g[1].final)
+        return gac_fail(GAC_E_STATE, "load both genomes before gac_chain_dp_blocks");
+    if (n_pairs == 0) return GAC_OK;
+    if (n_pairs >= (1LL << 30)) return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: too many pairs");
+    const int64_t P = n_pairs, B = blk_off[P];
+    if (blk_off[0] != 0 || B < 0 || B > 0x7fffffffLL)
+        return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: bad block offsets");
+    for (int64_t p = 0; p < P; ++p)
+        if (blk_off[p + 1] < blk_off[p])
+            return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: pair %lld: block offsets descend",
+                            (long long)p);
+    if (B && (!box || !score || !tord || !total || !pred))
+        return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: NULL array");
+    if (fast && lin_k < 0) return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: bad lin_k");
+    if (B == 0) {
+        for (int64_t p = 0; p <= P; ++p) leaf_off[p] = 0;
+        return GAC_OK;
+    }
+    const bool timing = getenv("GAC_TIMING") != nullptr;
+    const double t0 = wall_s();
+    std::vector<DpPair> pairs(P);
+    std::vector<int2> sizes(P);
+    for (int64_t p = 0; p < P; ++p) {
+        int rc = pair_bases(c, t_seq[p], q_seq[p], q_strand[p], pairs[p].tbase, pairs[p].qbase);
+        if (rc != GAC_OK) return rc;
+        sizes[p] = make_int2(c->g[0].sizes[t_seq[p]], c->g[1].sizes[q_seq[p]]);
+    }
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    DevBufs M;
+    DtTree t;
+    memset(&t, 0, sizeof(t));
+    t.P = P;
+    t.B = B;
+    t.fast = fast ? 1 : 0;
+    t.ov_cap = ov_cap;
+    int bits = 0;
+    while ((1LL << bits) <= P) ++bits;
+    t.end_bit = 31 + bits;
+    int64_t *d_blk_off = M.take<int64_t>(P + 1);
+    int2 *d_sizes = M.take<int2>(P);
+    int4 *d_box = M.take<int4>(B);
+    int32_t *d_score = M.take<int32_t>(B);
+    unsigned long long *d_keys = M.take<unsigned long long>(2 * B);
+    int32_t *d_vals = M.take<int32_t>(2 * B);
+    int64_t *d_leaf_off = M.take<int64_t>(P + 1);
+    int32_t *d_err = M.take<int32_t>(1);
+    t.tpos = M.take<int32_t>(B);
+    t.qpos = M.take<int32_t>(B);
+    t.posd = M.take<int32_t>(B);
+    long long *d_total = M.take<long long>(B);
+    int32_t *d_pred = M.take<int32_t>(B);
+    if (M.e != hipSuccess)
+        return gac_fail(GAC_E_HIP, "gac_chain_dp_blocks: hipMalloc: %s", hipGetErrorString(M.e));
+    size_t b_sort = 0;
+    HIPCHK(dt_sort_pairs(nullptr, b_sort, d_keys, d_keys + B, d_vals, d_vals + B, B, t.end_bit, s));
+    void *d_tmp = M.take<uint8_t>((int64_t)b_sort);
+    HIPCHK(M.e);
+    HIPCHK(hipMemcpyAsync(d_blk_off, blk_off, (P + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_sizes, sizes.data(), P * sizeof(int2), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_box, box, B * sizeof(int4), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_score, score, B * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(d_err, 0, sizeof(int32_t), s));
+    // ---- leaves in target order, per-pair leaf offsets
+    HIPCHK(launch_dt_keys(P, B, d_blk_off, d_sizes, d_box, d_keys, d_vals, d_err, s));
+    HIPCHK(dt_sort_pairs(d_tmp, b_sort, d_keys, d_keys + B, d_vals, d_vals + B, B, t.end_bit, s));
+    HIPCHK(launch_dt_leaf_off(P, B, d_keys + B, d_leaf_off, s));
+    int32_t h_err = 0;
+    HIPCHK(hipMemcpyAsync(leaf_off, d_leaf_off, (P + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&h_err, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const double t1 = wall_s();
+    if (h_err & 1) {  // the first bad block, as a serial check reports it
+        for (int64_t p = 0; p < P; ++p)
+            for (int64_t g = blk_off[p]; g < blk_off[p + 1]; ++g) {
+                const int32_t *b = box + 4 * g;
+                if (b[0] < 0 || b[0] > b[1] || b[1] > sizes[p].y || b[2] < 0 || b[2] > b[3] ||
+                    b[3] > sizes[p].x)
+                    return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: pair %lld block %lld (%d-%d, %d-%d) "
+                                    "outside its sequences", (long long)p, (long long)(g - blk_off[p]),
+                                    b[0], b[1], b[2], b[3]);
+            }
+        return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: a block outside its sequences");
+    }
+    const int64_t L = leaf_off[P];
+    if (L == 0) {
+        for (int64_t g = 0; g < B; ++g) {
+            total[g] = score[g];
+            pred[g] = -1;
+        }
+        return GAC_OK;
+    }
+    std::vector<int64_t> node_off(P + 1);
+    int64_t maxnl = 0;
+    node_off[0] = 0;
+    for (int64_t p = 0; p < P; ++p) {
+        const int64_t nl = leaf_off[p + 1] - leaf_off[p];
+        maxnl = std::max(maxnl, nl);
+        node_off[p + 1] = node_off[p] + (nl ? 2 * nl - 1 : 0);
+        pairs[p].node_off = node_off[p];
+        pairs[p].leaf_off = leaf_off[p];
+        pairs[p].n_nodes = (int32_t)(node_off[p + 1] - node_off[p]);
+        pairs[p].n_leaves = (int32_t)nl;
+    }
+    const int64_t N = node_off[P];
+    int levels = 0;
+    for (int64_t n = maxnl; n > 1; n -= n / 2) ++levels;
+    t.L = L;
+    t.N = N;
+    t.blk_off = d_blk_off;
+    t.box = d_box;
+    t.score = d_score;
+    t.keys = d_keys + B;
+    t.tord = d_vals + B;
+    t.leaf_off = d_leaf_off;
+    int64_t *d_node_off = M.take<int64_t>(P + 1);
+    t.node_off = d_node_off;
+    t.pidx = M.take<int32_t>(L);
+    t.key2 = M.take<unsigned long long>(2 * L);
+    t.val2 = M.take<int32_t>(2 * L);
+    t.ql = M.take<int32_t>(L);
+    t.tl = M.take<int32_t>(L);
+    t.spare = M.take<int32_t>(L);
+    t.sstart = M.take<int32_t>(L);
+    t.slen = M.take<int32_t>(L);
+    t.snode = M.take<int32_t>(L);
+    t.flag = M.take<int32_t>(L);
+    t.excl = M.take<int32_t>(L);
+    t.ndep = M.take<int32_t>(N);
+    t.ndl = M.take<int32_t>(N);
+    t.qbox = M.take<int4>(L);
+    t.qtp = M.take<int32_t>(L);
+    t.msz = M.take<int32_t>(P);
+    t.over = M.take<uint8_t>(L);
+    t.pcnt = M.take<long long>(L + 1);
+    t.ocnt = M.take<long long>(L + 1);
+    t.err = d_err;
+    t.na = M.take<int4>(N);
+    t.nb = M.take<int2>(N);
+    t.tot = M.take<long long>(N);
+    t.ms = M.take<long long>(N);
+    t.nw = M.take<long long>(N);
+    t.lf = M.take<int4>(L);
+    t.lsc = M.take<int32_t>(L);
+    t.lnode = M.take<int32_t>(L);
+    t.poff = M.take<long long>(L + 1);
+    t.ooff = M.take<long long>(L + 1);
+    long long *d_lf_total = M.take<long long>(L);
+    int32_t *d_lf_pred = M.take<int32_t>(L);
+    int32_t *d_out_tord = M.take<int32_t>(L);
+    DpPair *d_pairs = M.take<DpPair>(P);
+    if (M.e != hipSuccess)
+        return gac_fail(GAC_E_HIP, "gac_chain_dp_blocks: hipMalloc: %s", hipGetErrorString(M.e));
+    size_t need = b_sort, b = 0;
+    HIPCHK(dt_sort_pairs(nullptr, b, t.key2, t.key2 + L, t.val2, t.val2 + L, L, t.end_bit, s));
+    need = std::max(need, b);
+    HIPCHK(dt_scan32(nullptr, b, t.flag, t.excl, L, s));
+    need = std::max(need, b);
+    HIPCHK(dt_scan64(nullptr, b, t.pcnt, t.poff, L + 1, s));
+    need = std::max(need, b);
+    t.tmp = need > b_sort ? M.take<uint8_t>((int64_t)need) : d_tmp;
+    t.tmp_bytes = need;
+    HIPCHK(M.e);
+    HIPCHK(hipMemcpyAsync(d_node_off, node_off.data(), (P + 1) * sizeof(int64_t),
+                          hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_pairs, pairs.data(), P * sizeof(DpPair), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(t.pcnt, 0, (L + 1) * sizeof(long long), s));
+    HIPCHK(hipMemsetAsync(t.ocnt, 0, (L + 1) * sizeof(long long), s));
+    // ---- query order, the trees, path and overlap counts
+    HIPCHK(launch_dt_tree(t, levels, s));
+    long long n_path = 0, n_ov = 0;
+    HIPCHK(hipMemcpyAsync(&n_path, t.poff + L, sizeof(long long), hipMemcpyDeviceToHost, s));
+    if (fast) HIPCHK(hipMemcpyAsync(&n_ov, t.ooff + L, sizeof(long long), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&h_err, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (h_err)
+        return gac_fail(GAC_E_HIP, "gac_chain_dp_blocks: device tree build failed (%d)", h_err);
+    int32_t *d_path = M.take<int32_t>(n_path);
+    int32_t *d_ov = M.take<int32_t>(n_ov);
+    if (M.e != hipSuccess)
+        return gac_fail(GAC_E_HIP, "gac_chain_dp_blocks: hipMalloc: %s", hipGetErrorString(M.e));
+    HIPCHK(launch_dt_lists(t, d_path, d_ov, s));
+    HIPCHK(hipMemcpyAsync(&h_err, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (h_err)
+        return gac_fail(GAC_E_HIP, "gac_chain_dp_blocks: device path build failed (%d)", h_err);
+    const double t2 = wall_s();
+    // ---- the DP
+    DpArgs a;
+    dp_base_args(c, a);
+    a.n_pairs = P;
+    a.pairs = d_pairs;
+    a.nd_ms = t.ms;
+    a.nd_tot = t.tot;
+    a.nd_a = t.na;
+    a.nd_b = t.nb;
+    a.lf = t.lf;
+    a.lf_score = t.lsc;
+    a.lf_node = t.lnode;
+    a.path_off = (const int64_t *)t.poff;
+    a.path = d_path;
+    a.lf_total = d_lf_total;
+    a.lf_pred = d_lf_pred;
+    a.nd_nw = fast ? t.nw : nullptr;
+    a.ov_off = fast ? (const int64_t *)t.ooff : nullptr;
+    a.ov = fast ? d_ov : nullptr;
+    a.lin_k = lin_k;
+    a.min_entry = min_entry;
+    const int grid = (int)std::min<int64_t>(P, 1 << 20);
+    HIPCHK(dp_launch(c, a, grid, fast != 0));
+    {
+        // the DP runs for seconds beside the host's own DP threads: wait
+        // without spinning a core (hipStreamSynchronize may busy-wait)
+        hipEvent_t done;
+        HIPCHK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+        hipError_t e = hipEventRecord(done, s);
+        while (e == hipSuccess && (e = hipEventQuery(done)) == hipErrorNotReady) {
+            const struct timespec nap = {0, 500000};
+            nanosleep(&nap, nullptr);
+            e = hipSuccess;
+        }
+        hipEventDestroy(done);
+        HIPCHK(e);
+    }
+    const double t3 = wall_s();
+    if (const char *dd = getenv("GAC_DT_DUMP")) {  // (debug: the built arrays, raw)
+        auto dump = [&](const char *name, const void *d, size_t bytes) {
+            std::vector<char> h(bytes);
+            if (hipMemcpy(h.data(), d, bytes, hipMemcpyDeviceToHost) != hipSuccess) return;
+            std::string f = std::string(dd) + "/" + name;
+            if (FILE *o = fopen(f.c_str(), "wb")) {
+                fwrite(h.data(), 1, bytes, o);
+                fclose(o);
+            }
+        };
+        dump("leaf_off", d_leaf_off, (P + 1) * 8);
+        dump("lf", t.lf, L * 16);
+        dump("lnode", t.lnode, L * 4);
+        dump("na", t.na, N * 16);
+        dump("nb", t.nb, N * 8);
+        dump("poff", t.poff, (L + 1) * 8);
+        dump("path", d_path, n_path * 4);
+        if (fast) dump("ooff", t.ooff, (L + 1) * 8);
+        if (fast) dump("ov", d_ov, n_ov * 4);
+        dump("lf_total", d_lf_total, L * 8);
+        dump("lf_pred", d_lf_pred, L * 4);
+    }
+    HIPCHK(launch_dt_out(t, d_lf_total, d_lf_pred, d_out_tord, d_total, d_pred, s));
+    HIPCHK(hipMemcpyAsync(tord, d_out_tord, L * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(total, d_total, B * sizeof(long long), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(pred, d_pred, B * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&h_err, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (h_err)
+        return gac_fail(GAC_E_HIP, "gac_chain_dp_blocks: a predecessor is not a leaf (%d)", h_err);
+    if (timing)
+        fprintf(stderr,
+                "[gac_chain_dp_blocks] %lld pairs, %lld blocks, %lld leaves, %d levels, %lld path "
+                "nodes, %lld overlap entries: upload + leaves %.3f s, trees + paths + overlaps %.3f s, "
+                "%s %.3f s, results %.3f s\n",
+                (long long)P, (long long)B, (long long)L, levels, n_path, n_ov, t1 - t0, t2 - t1,
+                fast ? "k_dp_fast" : "k_dp", t3 - t2, wall_s() - t3);
+    return GAC_OK;
 }
 
 extern "C" int gac_crossovers(gac_ctx *c, int64_t n, const int32_t *t_seq, const int32_t *q_seq,

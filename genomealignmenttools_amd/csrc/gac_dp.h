@@ -1,8 +1,9 @@
 // gac_dp.h -- device layout of axtChain's chaining kernels (gac_dp.hip):
 // the kd-tree DP (k_dp) and the crossover batch (k_xover).  gfx950 only.
 //
-// Per pair, the host-built kd-tree (kdBuild, kent/src/lib/chainBlock.c:124-
-// 164) in pre-order with the hi child first, as structure-of-arrays:
+// Per pair, the kd-tree (kdBuild, kent/src/lib/chainBlock.c:124-164; built
+// on the host, or on the device by gac_dptree.hip) in pre-order with the hi
+// child first, as structure-of-arrays:
 //   nd_a[v] = {maxQ, maxT, cut, lo}        internal node
 //             {qEnd, tEnd, qStart, tStart} leaf node
 //   nd_b[v] = {end of v's subtree, dim (0 = q, 1 = t) | ~leaf position}
@@ -82,6 +83,69 @@ struct XoverJob {
     int32_t lqe, lte, rqs, rts;
     int32_t ov, pad;
 };
+
+// The DP's per-pair inputs built on the device from the pairs' blocks
+// (gac_dptree.hip, gac_chain_dp_blocks): P pairs, B packed blocks (pair p's
+// [blk_off[p], blk_off[p+1]), box = {qs, qe, ts, te}), L leaves, N nodes.
+// The arrays after `tord` come out in the DpArgs layout above.
+struct DtTree {
+    int64_t P, B, L, N;
+    int end_bit;  // radix sort key bits: 31 + bit length of P
+    int fast;     // k_dp_fast: overlap lists too
+    int32_t ov_cap;
+    const int64_t *blk_off;  // [P + 1]
+    const int4 *box;         // [B]
+    const int32_t *score;    // [B]
+    const unsigned long long *keys;  // [B] sorted (pair, tStart) keys
+    const int32_t *tord;     // [B] blocks in that order: the first L are the leaves
+    const int64_t *leaf_off; // [P + 1]
+    const int64_t *node_off; // [P + 1]
+    // scratch
+    int32_t *pidx, *tpos, *qpos, *posd;  // [L], [B], [B], [B]
+    unsigned long long *key2;            // [2L]
+    int32_t *val2;                       // [2L]
+    int32_t *ql, *tl, *spare;            // [L]
+    int32_t *sstart, *slen, *snode;      // [L]
+    int32_t *flag, *excl;                // [L]
+    int32_t *ndep, *ndl;                 // [N]
+    int4 *qbox;                          // [L]
+    int32_t *qtp;                        // [L]
+    int32_t *msz;                        // [P]
+    uint8_t *over;                       // [L]
+    long long *pcnt, *ocnt;              // [L + 1]
+    int32_t *err;
+    void *tmp;
+    size_t tmp_bytes;
+    // out (DpArgs inputs)
+    int4 *na;           // [N]
+    int2 *nb;           // [N]
+    long long *tot, *ms, *nw;  // [N]
+    int4 *lf;           // [L]
+    int32_t *lsc, *lnode;      // [L]
+    long long *poff, *ooff;    // [L + 1]
+};
+
+hipError_t dt_sort_pairs(void *tmp, size_t &tmp_bytes, const unsigned long long *kin,
+                         unsigned long long *kout, const int32_t *vin, int32_t *vout, int64_t n,
+                         int end_bit, hipStream_t s);
+hipError_t dt_scan32(void *tmp, size_t &tmp_bytes, const int32_t *in, int32_t *out, int64_t n,
+                     hipStream_t s);
+hipError_t dt_scan64(void *tmp, size_t &tmp_bytes, const long long *in, long long *out, int64_t n,
+                     hipStream_t s);
+hipError_t launch_dt_keys(int64_t P, int64_t B, const int64_t *blk_off, const int2 *sizes,
+                          const int4 *box, unsigned long long *keys, int32_t *vals, int32_t *err,
+                          hipStream_t s);
+hipError_t launch_dt_leaf_off(int64_t P, int64_t B, const unsigned long long *keys,
+                              int64_t *leaf_off, hipStream_t s);
+// leaves in query order, the tree (levels = splits of the largest pair),
+// path counts and offsets, overlap counts and offsets (t.fast)
+hipError_t launch_dt_tree(const DtTree &t, int levels, hipStream_t s);
+// the paths and overlap lists into arrays of poff[L] / ooff[L] entries
+hipError_t launch_dt_lists(const DtTree &t, int32_t *path, int32_t *ov, hipStream_t s);
+// per packed block: totalScore, best predecessor (a block of its pair, or
+// -1); per leaf: the target order as pair-local blocks
+hipError_t launch_dt_out(const DtTree &t, const long long *lf_total, const int32_t *lf_pred,
+                         int32_t *out_tord, long long *total, int32_t *pred, hipStream_t s);
 
 hipError_t launch_dp(const DpArgs &a, int grid, hipStream_t s);
 hipError_t launch_dp_fast(const DpArgs &a, int grid, hipStream_t s);

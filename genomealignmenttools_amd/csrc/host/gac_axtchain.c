@@ -165,6 +165,7 @@ typedef struct ax_work {
     int32_t cut_t;   /* fast searches see only leaves with tpos < cut_t */
     long long fallbacks;
     int team, team_batch; /* > 1: this pair's DP on that many threads (pair_dp_team) */
+    int pred_blk;         /* pred holds blocks, not nodes (gac_chain_dp_blocks' results) */
     /* crossover scratch */
     uint8_t *xs;
     int32_t xcap;
@@ -1898,7 +1899,7 @@ static void pair_peel(ax_work *w, const ax_pairinfo *pi, FILE *details, ax_chain
                         w->qs[lf], w->qe[lf] - w->qs[lf]);
             if (w->pred[lf] < 0)
                 break;
-            const int32_t pl = w->nodes[w->pred[lf]].leaf;
+            const int32_t pl = w->pred_blk ? w->pred[lf] : w->nodes[w->pred[lf]].leaf;
             if (details)
                 fprintf(details, " gap %d\t%d\n", w->ts[lf] - w->te[pl], w->qs[lf] - w->qe[pl]);
             lf = pl;
@@ -2473,6 +2474,14 @@ typedef struct ax_gjob {
     int phase;
     _Atomic int64_t next;
     double t_leaves, t_tree, t_export; /* (phase 1 laps summed over threads; racy, timing only) */
+    /* the DP's inputs built on the device (gac_chain_dp_blocks): the pairs'
+     * blocks packed at boff[k] (phase 1), the results by packed block */
+    int dev_tree;
+    const int64_t *boff;
+    int32_t *box, *bscore;
+    const int32_t *tord;
+    const int64_t *btotal;
+    const int32_t *bpred;
     /* device results */
     const int64_t *leaf_off, *xoff;
     const int64_t *total;
@@ -2658,6 +2667,23 @@ static void *gdp_thread(void *arg) {
             w->ts = J->ts + b0;
             w->te = J->te + b0;
             w->score = J->score + b0;
+            if (X->dev_tree) { /* only what peel and finish use; the blocks packed */
+                const size_t c = (size_t)w->n + 16;
+                w->total = malloc(c * sizeof(double));
+                w->pred = malloc(c * sizeof(int32_t));
+                w->hit = malloc(c);
+                w->tord = malloc(c * sizeof(int32_t));
+                int32_t *bx = X->box + 4 * X->boff[k], *bs = X->bscore + X->boff[k];
+                for (int32_t i = 0; i < w->n; ++i) {
+                    bx[4 * i] = w->qs[i];
+                    bx[4 * i + 1] = w->qe[i];
+                    bx[4 * i + 2] = w->ts[i];
+                    bx[4 * i + 3] = w->te[i];
+                    bs[i] = w->score[i];
+                }
+                G->t0 += gnow() - t0;
+                continue;
+            }
             work_reserve(w, w->n);
             const double ta = gnow();
             if (pair_leaves(w) > 0) {
@@ -2673,12 +2699,22 @@ static void *gdp_thread(void *arg) {
         } else if (X->phase == 2) {
             if (!G->ok || w->err)
                 continue;
+            if (X->dev_tree) {
+                const int64_t lo = X->leaf_off[k], bo = X->boff[k];
+                w->nl = (int32_t)(X->leaf_off[k + 1] - lo);
+                memcpy(w->tord, X->tord + lo, (size_t)w->nl * sizeof(int32_t));
+                for (int32_t i = 0; i < w->n; ++i) {
+                    w->total[i] = (double)X->btotal[bo + i];
+                    w->pred[i] = X->bpred[bo + i];
+                }
+                w->pred_blk = 1;
+            }
             if (w->nl == 0) {
                 o->coff = calloc(1, sizeof(int32_t));
                 continue;
             }
             const int64_t lo = X->leaf_off[k];
-            for (int32_t i = 0; i < w->nl; ++i) {
+            for (int32_t i = 0; i < w->nl && !X->dev_tree; ++i) {
                 const int32_t l = w->tord[i];
                 w->total[l] = (double)X->total[lo + i];
                 w->pred[l] = X->pred[lo + i];
@@ -2751,6 +2787,155 @@ static void gdp_phase(ax_gjob *X, int phase, int nt) {
     gac_run_threads(nt, gdp_thread, X);
 }
 
+/* the peel, the crossovers of the peeled chains (one gac_crossovers batch)
+ * and the finish of the device pairs (phases 2 and 3), X->leaf_off and the
+ * DP's results set; returns the crossovers' rc.  *nxo: crossover count */
+static int gdp_finish(ax_gjob *X, int nt, const int32_t *kt, const int32_t *kq, const uint8_t *ks,
+                      int64_t *nxo) {
+    ax_job *J = X->J;
+    ax_gpair *G = X->G;
+    const int64_t np = J->n_pairs;
+    gdp_phase(X, 2, nt);
+    int64_t *xoff = malloc((size_t)(np + 1) * sizeof(int64_t));
+    xoff[0] = 0;
+    for (int64_t p = 0; p < np; ++p)
+        xoff[p + 1] = xoff[p] + G[p].nx;
+    const int64_t nx = xoff[np];
+    int32_t *xt = malloc((size_t)(nx ? nx : 1) * 4), *xq = malloc((size_t)(nx ? nx : 1) * 4);
+    uint8_t *xs = malloc((size_t)(nx ? nx : 1));
+    int32_t *xv[5], *xpos = malloc((size_t)(nx ? nx : 1) * 4), *xadj = malloc((size_t)(nx ? nx : 1) * 4);
+    for (int f = 0; f < 5; ++f)
+        xv[f] = malloc((size_t)(nx ? nx : 1) * 4);
+    for (int64_t p = 0; p < np; ++p) /* (p: place in J->order) */
+        for (int32_t k = 0; k < G[p].nx; ++k) {
+            const int64_t g = xoff[p] + k;
+            xt[g] = kt[p];
+            xq[g] = kq[p];
+            xs[g] = ks[p] ? 1 : 0;
+            for (int f = 0; f < 5; ++f)
+                xv[f][g] = G[p].xl[5 * k + f];
+        }
+    const int rc = gac_crossovers(J->ctx, nx, xt, xq, xs, xv[0], xv[1], xv[2], xv[3], xv[4], xpos, xadj);
+    if (rc == GAC_OK) {
+        X->xoff = xoff;
+        X->xpos = xpos;
+        X->xadj = xadj;
+        X->xlqe = xv[0];
+        X->xlte = xv[1];
+        X->xrqs = xv[2];
+        X->xrts = xv[3];
+        X->xov = xv[4];
+        gdp_phase(X, 3, nt);
+    }
+    free(xt);
+    free(xq);
+    free(xs);
+    free(xpos);
+    free(xadj);
+    for (int f = 0; f < 5; ++f)
+        free(xv[f]);
+    free(xoff);
+    *nxo = nx;
+    return rc;
+}
+
+static void gdp_free_pairs(ax_gpair *G, int64_t np) {
+    for (int64_t p = 0; p < np; ++p) {
+        ax_work *w = &G[p].w;
+        gpair_free_export(&G[p]);
+        free(G[p].pc.cblk);
+        free(G[p].pc.cstart);
+        free(G[p].xjob);
+        free(G[p].xl);
+        free(w->total);
+        free(w->pred);
+        free(w->hit);
+        free(w->tord);
+        free(w->qord);
+        free(w->tmp);
+        free(w->nodes);
+        free(w->lnode);
+        free(w->qpos);
+        free(w->tpos);
+        free(w->tbox);
+        free(w->qbox);
+        free(w->qtp);
+        free(w->bnd);
+        free(w->xs);
+    }
+    free(G);
+}
+
+/* the device pairs with every input of the DP built on the device
+ * (gac_chain_dp_blocks: leaves, kd-trees, update paths, overlap lists): the
+ * host packs the pairs' blocks (phase 1) and peels and finishes (phases 2,
+ * 3).  GAC_DP_DEVTREE=0: the round-5 path (trees, paths and overlap lists
+ * built and exported on host threads, gac_chain_dp_ex) */
+static int axt_dp_gpu_devtree(ax_job *J, int nt, ax_gjob *X, int32_t *kt, int32_t *kq, uint8_t *ks) {
+    const int64_t np = J->n_pairs;
+    ax_gpair *G = X->G;
+    const double t = gnow();
+    int64_t *boff = malloc((size_t)(np + 1) * sizeof(int64_t));
+    boff[0] = 0;
+    for (int64_t k = 0; k < np; ++k)
+        boff[k + 1] = boff[k] + (J->poff[J->order[k] + 1] - J->poff[J->order[k]]);
+    const int64_t nb = boff[np];
+    X->dev_tree = 1;
+    X->boff = boff;
+    X->box = malloc((size_t)(nb ? nb : 1) * 4 * sizeof(int32_t));
+    X->bscore = malloc((size_t)(nb ? nb : 1) * sizeof(int32_t));
+    gdp_phase(X, 1, nt);
+    const double t1 = gnow();
+    int rc = GAC_OK;
+    for (int64_t k = 0; k < np && rc == GAC_OK; ++k)
+        if (!G[k].ok)
+            rc = gac_fail(GAC_E_ARG, "pair %d: no host sequence", J->order[k]);
+    /* the fast DP when the gap costs allow it (as dp_fast_enabled) */
+    const char *fv = getenv("GAC_DP_FAST");
+    const int fast = J->e->fast && !(fv && *fv == '0');
+    static int ov_cap = -1; /* (GAC_DP_OVCAP: the test hook of gpair_export) */
+    if (ov_cap < 0) {
+        const char *oc = getenv("GAC_DP_OVCAP");
+        const int v = oc && *oc ? atoi(oc) : 1024;
+        ov_cap = v >= 0 && v <= 1024 ? v : 1024;
+    }
+    int64_t *leaf_off = malloc((size_t)(np + 1) * sizeof(int64_t));
+    int32_t *tord = malloc((size_t)(nb ? nb : 1) * sizeof(int32_t));
+    int64_t *btotal = malloc((size_t)(nb ? nb : 1) * sizeof(int64_t));
+    int32_t *bpred = malloc((size_t)(nb ? nb : 1) * sizeof(int32_t));
+    if (rc == GAC_OK)
+        rc = gac_chain_dp_blocks(J->ctx, np, kt, kq, ks, boff, X->box, X->bscore, fast,
+                                 fast ? J->e->lin_k : 0, J->e->min_entry, ov_cap, leaf_off, tord,
+                                 btotal, bpred);
+    free(X->box);
+    free(X->bscore);
+    X->box = X->bscore = NULL;
+    const double t2 = gnow();
+    int64_t nx = 0;
+    if (rc == GAC_OK) {
+        X->leaf_off = leaf_off;
+        X->tord = tord;
+        X->btotal = btotal;
+        X->bpred = bpred;
+        rc = gdp_finish(X, nt, kt, kq, ks, &nx);
+    }
+    const double t3 = gnow();
+    if (getenv("GAC_TIMING"))
+        fprintf(stderr, "[gac_axt_chain] device DP (device-built trees): pack %.3f s, "
+                        "gac_chain_dp_blocks %.3f s, peel + %lld crossovers + finish %.3f s\n",
+                t1 - t, t2 - t1, (long long)nx, t3 - t2);
+    free(leaf_off);
+    free(tord);
+    free(btotal);
+    free(bpred);
+    free(boff);
+    gdp_free_pairs(G, np);
+    free(kt);
+    free(kq);
+    free(ks);
+    return rc;
+}
+
 /* the pairs J->order[0 .. J->n_pairs) (all of them, or the device's share
  * of a hybrid run); arrays below are by place k in that list */
 static int axt_dp_gpu(ax_job *J, int nt) {
@@ -2771,6 +2956,9 @@ static int axt_dp_gpu(ax_job *J, int nt) {
     atomic_init(&X.next, 0);
     int rc = GAC_OK;
     double t = gnow();
+    const char *dtv = getenv("GAC_DP_DEVTREE");
+    if (!(dtv && *dtv == '0'))
+        return axt_dp_gpu_devtree(J, nt, &X, kt, kq, ks);
     gdp_phase(&X, 1, nt);
     double t1 = gnow();
     /* gather the pairs' trees */
@@ -2839,89 +3027,23 @@ static int axt_dp_gpu(ax_job *J, int nt) {
     free(poff);
     free(path);
     free(node_off);
-    int64_t *xoff = NULL;
-    double t4 = t3, t5 = t3, t6 = t3;
     if (rc == GAC_OK) {
         X.leaf_off = leaf_off;
         X.total = total;
         X.pred = pred;
-        gdp_phase(&X, 2, nt);
-        t4 = gnow();
-        xoff = malloc((size_t)(np + 1) * sizeof(int64_t));
-        xoff[0] = 0;
-        for (int64_t p = 0; p < np; ++p)
-            xoff[p + 1] = xoff[p] + G[p].nx;
-        const int64_t nx = xoff[np];
-        int32_t *xt = malloc((size_t)(nx ? nx : 1) * 4), *xq = malloc((size_t)(nx ? nx : 1) * 4);
-        uint8_t *xs = malloc((size_t)(nx ? nx : 1));
-        int32_t *xv[5], *xpos = malloc((size_t)(nx ? nx : 1) * 4), *xadj = malloc((size_t)(nx ? nx : 1) * 4);
-        for (int f = 0; f < 5; ++f)
-            xv[f] = malloc((size_t)(nx ? nx : 1) * 4);
-        for (int64_t p = 0; p < np; ++p) /* (p: place in J->order) */
-            for (int32_t k = 0; k < G[p].nx; ++k) {
-                const int64_t g = xoff[p] + k;
-                xt[g] = kt[p];
-                xq[g] = kq[p];
-                xs[g] = ks[p] ? 1 : 0;
-                for (int f = 0; f < 5; ++f)
-                    xv[f][g] = G[p].xl[5 * k + f];
-            }
-        rc = gac_crossovers(J->ctx, nx, xt, xq, xs, xv[0], xv[1], xv[2], xv[3], xv[4], xpos, xadj);
-        t5 = gnow();
-        if (rc == GAC_OK) {
-            X.xoff = xoff;
-            X.xpos = xpos;
-            X.xadj = xadj;
-            X.xlqe = xv[0];
-            X.xlte = xv[1];
-            X.xrqs = xv[2];
-            X.xrts = xv[3];
-            X.xov = xv[4];
-            gdp_phase(&X, 3, nt);
-        }
-        t6 = gnow();
+        int64_t nx = 0;
+        rc = gdp_finish(&X, nt, kt, kq, ks, &nx);
         if (getenv("GAC_TIMING"))
             fprintf(stderr, "[gac_axt_chain] device DP: trees %.3f s (thread-seconds: leaves %.3f, "
-                            "tree %.3f, export %.3f), gather %.3f s, gac_chain_dp %.3f s, peel %.3f s, "
-                            "%lld crossovers %.3f s, finish %.3f s\n",
-                    t1 - t, X.t_leaves, X.t_tree, X.t_export, t2 - t1, t3 - t2, t4 - t3,
-                    (long long)nx, t5 - t4, t6 - t5);
-        free(xt);
-        free(xq);
-        free(xs);
-        free(xpos);
-        free(xadj);
-        for (int f = 0; f < 5; ++f)
-            free(xv[f]);
+                            "tree %.3f, export %.3f), gather %.3f s, gac_chain_dp %.3f s, peel + "
+                            "%lld crossovers + finish %.3f s\n",
+                    t1 - t, X.t_leaves, X.t_tree, X.t_export, t2 - t1, t3 - t2, (long long)nx,
+                    gnow() - t3);
     }
-    free(xoff);
     free(leaf_off);
     free(total);
     free(pred);
-    for (int64_t p = 0; p < np; ++p) {
-        ax_work *w = &G[p].w;
-        gpair_free_export(&G[p]);
-        free(G[p].pc.cblk);
-        free(G[p].pc.cstart);
-        free(G[p].xjob);
-        free(G[p].xl);
-        free(w->total);
-        free(w->pred);
-        free(w->hit);
-        free(w->tord);
-        free(w->qord);
-        free(w->tmp);
-        free(w->nodes);
-        free(w->lnode);
-        free(w->qpos);
-        free(w->tpos);
-        free(w->tbox);
-        free(w->qbox);
-        free(w->qtp);
-        free(w->bnd);
-        free(w->xs);
-    }
-    free(G);
+    gdp_free_pairs(G, np);
     free(kt);
     free(kq);
     free(ks);
@@ -2929,21 +3051,21 @@ static int axt_dp_gpu(ax_job *J, int nt) {
 }
 
 /* ---- the hybrid DP (the default): the device takes the smallest pairs
- * (k_dp_fast, one wave per pair, every device pair at once) while host
- * threads take the others (teams on the largest).  A device pair must end
- * within the host's critical path, estimated from the largest pair at the
- * team's rate (its device time, leaves x the device's per-leaf time, within
- * 0.7 of it), and is at most 5000 leaves: the device side's host work
- * (export of paths and overlap lists, peel, finish) costs the host about
- * as much per leaf as the DP it saves, so a larger share slows the run
- * (r06split1, C4 at 50 M blocks, the round-6 kernel: host only 8.89 /
- * 9.43 s; pairs up to 5000 leaves, 2.8 % of the blocks, 8.98 / 9.06 s; up
- * to 50 k leaves, 17.6 %, 8.92 / 9.06 s; the model's 187 k-leaf bound,
- * 29 %, 9.66 / 9.93 s).  Pairs go to the
- * device from the smallest up.  GAC_AXT_DP=host: no device pairs;
- * GAC_DP_GPU_MAX=n: the leaf cap (0: none); GAC_DP_DEV_US /
- * GAC_DP_HOST_US: the per-leaf times of the model.  Returns the first
- * device place in `order`. */
+ * (gac_chain_dp_blocks: their leaves, kd-trees, update paths and overlap
+ * lists built on the device, then k_dp_fast, one wave per pair, every device
+ * pair at once) while host threads take the others (teams on the largest).
+ * A device pair must end within the host's critical path, estimated from the
+ * largest pair at the team's rate (its device time, leaves x the device's
+ * per-leaf time, within 0.7 of it), and is at most 200 k leaves.  With the
+ * inputs built on the device the device's host work is the pack, peel and
+ * finish only (C4 at 50 M blocks, r06dt2/r06dt3: 14.8 M blocks' trees +
+ * paths + overlap lists 0.03 s of GPU, vs 1.7 s on two host threads built
+ * and exported on the host (GAC_DP_DEVTREE=0); the device's 979 pairs done in
+ * 3.4-3.5 s inside the largest pair's 7 s; wall 8.60 / 8.67 s vs host-only
+ * 8.62 / 8.86 s).  Pairs go to the device from the smallest up.
+ * GAC_AXT_DP=host: no device pairs; GAC_DP_GPU_MAX=n: the leaf cap (0:
+ * none); GAC_DP_DEV_US / GAC_DP_HOST_US: the per-leaf times of the model.
+ * Returns the first device place in `order`. */
 static int64_t dp_device_split(const int64_t *psize, const int32_t *order, int64_t np,
                                const ax_env *e) {
     const char *dpm = getenv("GAC_AXT_DP");
@@ -2957,7 +3079,7 @@ static int64_t dp_device_split(const int64_t *psize, const int32_t *order, int64
         return np;
     int64_t lmax = (int64_t)(0.7 * crit / (dev_us * 1e-6));
     const char *mx = getenv("GAC_DP_GPU_MAX");
-    const int64_t cap = mx && *mx ? atoll(mx) : 50000;
+    const int64_t cap = mx && *mx ? atoll(mx) : 200000;
     if (cap < lmax)
         lmax = cap;
     if (lmax < 1)
@@ -3639,6 +3761,18 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
             pool = pl && atoi(pl) > 0 && atoi(pl) < nthreads
                        ? atoi(pl)
                        : (nthreads / 3 > 1 ? nthreads / 3 : 1);
+            /* the device's share relieves the pool: the pool shrinks with
+             * its blocks (the threads it gives up run the device's host
+             * phases -- pack, peel, finish -- beside it); the teams keep
+             * theirs (r06dt3: C4, cap 200 k, pool 5 -> 3: 8.60 / 8.67 s vs
+             * host-only 8.62 / 8.86 s; cap 50 k with the pool at 3: 9.39 s) */
+            if (D && !(pl && atoi(pl) > 0) && nb - sum > 0) {
+                const int64_t all = nb - sum, now = nb_host - sum > 0 ? nb_host - sum : 0;
+                int p2 = (int)((pool * now + all - 1) / all);
+                p2 = p2 < 2 ? 2 : p2;
+                if (p2 < pool)
+                    pool = p2;
+            }
             if (pool > np_host - big) /* (no pool pairs left, e.g. an -nranks rank holding one big pair) */
                 pool = (int)(np_host - big);
             const int tt = nthreads - pool;

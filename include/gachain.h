@@ -291,6 +291,34 @@ int gac_chain_dp(gac_ctx *ctx, int64_t n_pairs, const int32_t *t_seq, const int3
                  const int32_t *leaf_score, const int32_t *leaf_node, const int64_t *path_off,
                  const int32_t *path, int64_t *total, int32_t *pred);
 
+/* chainBlocks' kd-tree DP for n_pairs seqPairs straight from their blocks,
+ * every input of the DP built on the device:
+ *   the leaf list (kent/src/lib/chainBlock.c:400-420: blocks with tStart !=
+ *     tEnd, slSort by tStart over the slAddHead-built list) and its query
+ *     order (kdTreeMake :166-205),
+ *   the kd-trees (kdBuild :124-164, splitList/medianVal :92-122),
+ *   the update paths (updateScoresOnWay :265-279) and, for the exact fast
+ *     DP, each leaf's overlapping candidates,
+ * then findBestPredecessors (:281-300) as in gac_chain_dp.  Blocks of pair p
+ * are [blk_off[p], blk_off[p+1]) in the caller's list order (axtChain's order
+ * after removeExactOverlaps), box[4g..] = {qStart, qEnd, tStart, tEnd} in
+ * the pair's strand coordinates, score[g] = axtScoreUngapped.
+ * fast != 0: the exact fast search (k_dp_fast) with the linear gap-cost
+ * minorant lin_k / 1024 and the smallest matrix entry min_entry; ov_cap
+ * (<= 1024): more overlapping candidates than this send a leaf to the
+ * reference search order.  fast == 0: the reference search (k_dp).
+ * Out: leaf_off[n_pairs + 1] (the leaves of pair p are [leaf_off[p],
+ * leaf_off[p+1])), tord[leaf] = the pair-local block of each leaf in target
+ * order, and per block total[g] = totalScore (score for a non-leaf) and
+ * pred[g] = the best predecessor as a pair-local block, or -1.  A block
+ * outside its sequences is GAC_E_ARG.  Uses the context's scoring setup and
+ * genomes. */
+int gac_chain_dp_blocks(gac_ctx *ctx, int64_t n_pairs, const int32_t *t_seq,
+                        const int32_t *q_seq, const uint8_t *q_strand, const int64_t *blk_off,
+                        const int32_t *box, const int32_t *score, int fast, int64_t lin_k,
+                        int32_t min_entry, int32_t ov_cap, int64_t *leaf_off, int32_t *tord,
+                        int64_t *total, int32_t *pred);
+
 /* cBlockFindCrossover (kent/src/lib/chainConnect.c:61-105) of n overlapping
  * block pairs on the device (one wave per pair, a prefix-sum / first-maximum
  * scan): left block ending at (lqe, lte), right block starting at (rqs, rts),

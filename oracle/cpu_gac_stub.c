@@ -643,3 +643,319 @@ int gac_chain_dp(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq, const int32_
                            leaf, leaf_score, leaf_node, path_off, path, NULL, NULL, 0, 0, total,
                            pred);
 }
+
+/* gac_chain_dp_blocks: the device build of gac_dptree.hip restated kernel by
+ * kernel as sequential loops (every kernel is a per-element map or scatter,
+ * so a loop in any order gives the device's result), then the emulated DP
+ * above -- the level-synchronous kd-tree build is checked here, on CPU,
+ * against the reference's chains by the axtChain_cpu tests */
+typedef struct dt_key {
+    unsigned long long k;
+    int64_t r;
+    int32_t v;
+} dt_key;
+
+static int dt_key_cmp(const void *a, const void *b) {
+    const dt_key *x = a, *y = b;
+    if (x->k != y->k)
+        return x->k < y->k ? -1 : 1;
+    return (x->r > y->r) - (x->r < y->r);
+}
+
+int gac_chain_dp_blocks(gac_ctx *c, int64_t P, const int32_t *t_seq, const int32_t *q_seq,
+                        const uint8_t *q_strand, const int64_t *blk_off, const int32_t *box,
+                        const int32_t *score, int fast, int64_t lin_k, int32_t min_entry,
+                        int32_t ov_cap, int64_t *leaf_off, int32_t *tord_out, int64_t *total,
+                        int32_t *pred) {
+    const int64_t B = blk_off[P];
+    dt_key *k1 = malloc((size_t)(B ? B : 1) * sizeof(dt_key));
+    for (int64_t p = 0, r = 0; p < P; ++p)
+        for (int64_t j = blk_off[p]; j < blk_off[p + 1]; ++j, ++r) {
+            const int64_t g = blk_off[p] + (blk_off[p + 1] - 1 - r); /* (k_dt_keys) */
+            const int32_t *b = box + 4 * g;
+            if (b[0] < 0 || b[0] > b[1] || b[1] > c->s[1].sizes[q_seq[p]] || b[2] < 0 ||
+                b[2] > b[3] || b[3] > c->s[0].sizes[t_seq[p]]) {
+                fprintf(stderr, "stub: bad block p %lld g %lld: %d %d %d %d sizes t %d q %d\n", (long long)p, (long long)g, b[0], b[1], b[2], b[3], c->s[0].sizes[t_seq[p]], c->s[1].sizes[q_seq[p]]);
+                free(k1);
+                return GAC_E_ARG;
+            }
+            k1[r] = (dt_key){b[2] != b[3] ? ((unsigned long long)p << 31) | (unsigned)b[2]
+                                          : ((unsigned long long)P << 31), r, (int32_t)g};
+        }
+    qsort(k1, (size_t)B, sizeof(dt_key), dt_key_cmp);
+    for (int64_t p = 0, r = 0; p <= P; ++p) {
+        while (r < B && k1[r].k < ((unsigned long long)p << 31))
+            ++r;
+        leaf_off[p] = r;
+    }
+    const int64_t L = leaf_off[P];
+    int64_t *node_off = malloc((size_t)(P + 1) * 8), maxnl = 0;
+    node_off[0] = 0;
+    for (int64_t p = 0; p < P; ++p) {
+        const int64_t nl = leaf_off[p + 1] - leaf_off[p];
+        maxnl = nl > maxnl ? nl : maxnl;
+        node_off[p + 1] = node_off[p] + (nl ? 2 * nl - 1 : 0);
+    }
+    const int64_t N = node_off[P];
+    int32_t *tord = malloc((size_t)(L + 1) * 4), *pidx = malloc((size_t)(L + 1) * 4);
+    int32_t *tpos = malloc((size_t)(B + 1) * 4), *qpos = malloc((size_t)(B + 1) * 4),
+            *posd = malloc((size_t)(B + 1) * 4);
+    int32_t *lf = malloc((size_t)(L + 1) * 16), *lsc = malloc((size_t)(L + 1) * 4);
+    int32_t *ql = malloc((size_t)(L + 1) * 4), *tl = malloc((size_t)(L + 1) * 4),
+            *spare = malloc((size_t)(L + 1) * 4);
+    int32_t *ss = malloc((size_t)(L + 1) * 4), *sl = malloc((size_t)(L + 1) * 4),
+            *sn = malloc((size_t)(L + 1) * 4), *flag = malloc((size_t)(L + 1) * 4),
+            *excl = malloc((size_t)(L + 1) * 4);
+    int32_t *qbox = malloc((size_t)(L + 1) * 16), *qtp = malloc((size_t)(L + 1) * 4),
+            *lnode = malloc((size_t)(L + 1) * 4);
+    int32_t *na = calloc((size_t)(N + 1), 16), *nb = calloc((size_t)(N + 1), 8),
+            *ndep = malloc((size_t)(N + 1) * 4), *ndl = malloc((size_t)(N + 1) * 4);
+    dt_key *k2 = malloc((size_t)(L + 1) * sizeof(dt_key));
+    for (int64_t i = 0; i < L; ++i) { /* k_dt_tinit */
+        const int32_t g = k1[i].v, p = (int32_t)(k1[i].k >> 31);
+        tord[i] = g;
+        pidx[i] = p;
+        tpos[g] = (int32_t)i;
+        memcpy(lf + 4 * i, box + 4 * (int64_t)g, 16);
+        lsc[i] = score[g];
+        k2[i] = (dt_key){((unsigned long long)p << 31) | (unsigned)box[4 * (int64_t)g], i, g};
+        tl[i] = g;
+        ss[i] = (int32_t)leaf_off[p];
+        sl[i] = (int32_t)(leaf_off[p + 1] - leaf_off[p]);
+        sn[i] = 0;
+    }
+    qsort(k2, (size_t)L, sizeof(dt_key), dt_key_cmp);
+    for (int64_t k = 0; k < L; ++k) { /* k_dt_qinit */
+        const int32_t g = k2[k].v;
+        ql[k] = g;
+        qpos[g] = (int32_t)k;
+        memcpy(qbox + 4 * k, box + 4 * (int64_t)g, 16);
+        qtp[k] = tpos[g];
+    }
+    int levels = 0;
+    for (int64_t n = maxnl; n > 1; n -= n / 2)
+        ++levels;
+    for (int d = 0; d < levels; ++d) {
+        const int dim = d & 1;
+        int32_t *D = dim ? tl : ql, *O = dim ? ql : tl;
+        for (int64_t i = 0; i < L; ++i)
+            if (sl[i] >= 2)
+                posd[D[i]] = (int32_t)i;
+        for (int64_t i = 0; i < L; ++i)
+            flag[i] = sl[i] >= 2 && posd[O[i]] < ss[i] + (sl[i] >> 1);
+        for (int64_t i = 0, run = 0; i < L; ++i) {
+            excl[i] = (int32_t)run;
+            run += flag[i];
+        }
+        for (int64_t i = 0; i < L; ++i) { /* k_dt_split */
+            const int32_t s = ss[i], len = sl[i], e = O[i];
+            if (len < 2) {
+                spare[i] = e;
+                continue;
+            }
+            const int32_t half = len >> 1, hb = excl[i] - excl[s];
+            spare[flag[i] ? s + hb : s + half + ((int32_t)i - s - hb)] = e;
+            const int32_t v = sn[i], lo = v + 2 * (len - half);
+            if (i == s) {
+                const int32_t *bb = box + 4 * (int64_t)D[s + half - 1];
+                const int64_t nv = node_off[pidx[i]] + v;
+                na[4 * nv + 2] = dim ? bb[2] : bb[0];
+                na[4 * nv + 3] = lo;
+                nb[2 * nv] = v + 2 * len - 1;
+                nb[2 * nv + 1] = dim;
+                ndep[nv] = d;
+                ndl[nv] = lo - v;
+            }
+            if ((int32_t)i - s < half) {
+                sl[i] = half;
+                sn[i] = lo;
+            } else {
+                ss[i] = s + half;
+                sl[i] = len - half;
+                sn[i] = v + 1;
+            }
+        }
+        if (dim)
+            ql = spare;
+        else
+            tl = spare;
+        spare = O;
+    }
+    for (int64_t i = 0; i < L; ++i) { /* k_dt_leafnodes */
+        const int32_t g = ql[i];
+        if (sl[i] != 1 || tl[i] != g) {
+            fprintf(stderr, "gac_chain_dp_blocks (CPU stand-in): bad leaf segment at %lld\n", (long long)i);
+            abort();
+        }
+        const int64_t nv = node_off[pidx[i]] + sn[i];
+        const int32_t *b = box + 4 * (int64_t)g;
+        na[4 * nv] = b[1];
+        na[4 * nv + 1] = b[3];
+        na[4 * nv + 2] = b[0];
+        na[4 * nv + 3] = b[2];
+        nb[2 * nv] = sn[i] + 1;
+        nb[2 * nv + 1] = ~(int32_t)(tpos[g] - leaf_off[pidx[i]]);
+        ndep[nv] = -1;
+        lnode[tpos[g]] = sn[i];
+    }
+    for (int d = levels - 1; d >= 0; --d) /* k_dt_max */
+        for (int64_t v = 0; v < N; ++v)
+            if (ndep[v] == d) {
+                const int32_t *a = na + 4 * (v + ndl[v]), *b = na + 4 * (v + 1);
+                na[4 * v] = a[0] > b[0] ? a[0] : b[0];
+                na[4 * v + 1] = a[1] > b[1] ? a[1] : b[1];
+            }
+    /* k_dt_path */
+    int64_t *poff = malloc((size_t)(L + 1) * 8), pcap = L * 24 + 64, np_ = 0;
+    int32_t *path = malloc((size_t)pcap * 4);
+    for (int64_t i = 0; i < L; ++i) {
+        poff[i] = np_;
+        const int64_t base = node_off[pidx[i]];
+        int32_t st[64];
+        int sp = 0;
+        st[sp++] = 0;
+        while (sp > 0) {
+            const int32_t v = st[--sp];
+            if (np_ == pcap) {
+                pcap *= 2;
+                path = realloc(path, (size_t)pcap * 4);
+            }
+            path[np_++] = v;
+            if (nb[2 * (base + v) + 1] >= 0) {
+                const int32_t coord = nb[2 * (base + v) + 1] == 0 ? lf[4 * i] : lf[4 * i + 2];
+                const int32_t cut = na[4 * (base + v) + 2];
+                if (sp + 2 > 64)
+                    abort();
+                if (coord <= cut)
+                    st[sp++] = na[4 * (base + v) + 3];
+                if (coord >= cut)
+                    st[sp++] = v + 1;
+            }
+        }
+    }
+    poff[L] = np_;
+    /* k_dt_maxsz + k_dt_ovl */
+    int64_t *ooff = NULL;
+    int32_t *ov = NULL;
+    if (fast) {
+        int32_t *msz = calloc((size_t)(P + 1), 4);
+        for (int64_t i = 0; i < L; ++i)
+            if (lf[4 * i + 3] - lf[4 * i + 2] > msz[pidx[i]])
+                msz[pidx[i]] = lf[4 * i + 3] - lf[4 * i + 2];
+        int64_t ocap = L + 64, no = 0;
+        ooff = malloc((size_t)(L + 1) * 8);
+        ov = malloc((size_t)ocap * 4);
+        int32_t *buf = malloc(1025 * 4);
+        for (int64_t i = 0; i < L; ++i) {
+            ooff[i] = no;
+            const int32_t p = pidx[i], lq = lf[4 * i], lt = lf[4 * i + 2], m = msz[p];
+            const int64_t lo_i = leaf_off[p];
+            int n = 0, ovf = 0;
+            for (int64_t j = i - 1; j >= lo_i && !ovf; --j) {
+                const int32_t *b = lf + 4 * j;
+                if (!(b[2] > lt - m))
+                    break;
+                if (b[2] >= lt || b[0] >= lq)
+                    continue;
+                if (lq - b[1] >= 0 && lt - b[3] >= 0)
+                    continue;
+                if (n == ov_cap)
+                    ovf = 1;
+                else
+                    buf[n++] = lnode[j];
+            }
+            for (int64_t j = (int64_t)qpos[tord[i]] - 1; j >= lo_i && !ovf; --j) {
+                const int32_t *b = qbox + 4 * j;
+                if (!(b[0] > lq - m))
+                    break;
+                if (b[2] >= lt || b[0] >= lq || qtp[j] >= i)
+                    continue;
+                const int32_t dq = lq - b[1], dt = lt - b[3];
+                if ((dq >= 0 && dt >= 0) || dt < 0)
+                    continue;
+                if (n == ov_cap)
+                    ovf = 1;
+                else
+                    buf[n++] = lnode[qtp[j]];
+            }
+            if (ovf) {
+                buf[0] = -1;
+                n = 1;
+            }
+            if (no + n > ocap) {
+                ocap = 2 * (no + n) + 64;
+                ov = realloc(ov, (size_t)ocap * 4);
+            }
+            memcpy(ov + no, buf, (size_t)n * 4);
+            no += n;
+        }
+        ooff[L] = no;
+        free(buf);
+        free(msz);
+    }
+    int64_t *lt_ = malloc((size_t)(L + 1) * 8);
+    int32_t *lp = malloc((size_t)(L + 1) * 4);
+    const int rc = gac_chain_dp_ex(c, P, t_seq, q_seq, q_strand, node_off, na, nb, leaf_off, lf, lsc,
+                                   lnode, poff, path, ooff, ov, fast ? lin_k : 0, min_entry, lt_, lp);
+    if (getenv("GAC_DT_DUMP")) { /* (debug: as the device's dump) */
+        const char *dd = getenv("GAC_DT_DUMP");
+        const struct { const char *n; const void *p; size_t b; } F[] = {
+            {"leaf_off", leaf_off, (size_t)(P + 1) * 8}, {"lf", lf, (size_t)L * 16},
+            {"lnode", lnode, (size_t)L * 4}, {"na", na, (size_t)N * 16}, {"nb", nb, (size_t)N * 8},
+            {"poff", poff, (size_t)(L + 1) * 8}, {"path", path, (size_t)poff[L] * 4},
+            {"ooff", ooff, fast ? (size_t)(L + 1) * 8 : 0}, {"ov", ov, fast ? (size_t)ooff[L] * 4 : 0},
+            {"lf_total", lt_, (size_t)L * 8}, {"lf_pred", lp, (size_t)L * 4}};
+        for (size_t k = 0; k < sizeof(F) / sizeof(F[0]); ++k) {
+            char fn[4096];
+            snprintf(fn, sizeof(fn), "%s/%s", dd, F[k].n);
+            FILE *o = fopen(fn, "wb");
+            if (o) {
+                fwrite(F[k].p, 1, F[k].b, o);
+                fclose(o);
+            }
+        }
+    }
+    for (int64_t g = 0; g < B; ++g) { /* k_dt_out_init + k_dt_out */
+        total[g] = score[g];
+        pred[g] = -1;
+    }
+    for (int64_t i = 0; i < L; ++i) {
+        const int32_t g = tord[i], p = pidx[i];
+        tord_out[i] = (int32_t)(g - blk_off[p]);
+        total[g] = lt_[i];
+        pred[g] = lp[i] < 0 ? -1
+                            : (int32_t)(tord[leaf_off[p] + ~nb[2 * (node_off[p] + lp[i]) + 1]] - blk_off[p]);
+    }
+    free(k1);
+    free(k2);
+    free(node_off);
+    free(tord);
+    free(pidx);
+    free(tpos);
+    free(qpos);
+    free(posd);
+    free(lf);
+    free(lsc);
+    free(ql);
+    free(tl);
+    free(spare);
+    free(ss);
+    free(sl);
+    free(sn);
+    free(flag);
+    free(excl);
+    free(qbox);
+    free(qtp);
+    free(lnode);
+    free(na);
+    free(nb);
+    free(ndep);
+    free(ndl);
+    free(poff);
+    free(path);
+    free(ooff);
+    free(ov);
+    free(lt_);
+    free(lp);
+    return rc;
+}

@@ -15,6 +15,9 @@ for i in $(seq 1 ${REPS:-2}); do
     case $mode in
       host) env="GAC_AXT_DP=host" ;;
       default) env="" ;;
+      gpu) env="GAC_AXT_DP=gpu" ;;
+      dt0_*) env="GAC_DP_DEVTREE=0 GAC_DP_GPU_MAX=${mode#dt0_}" ;;
+      us*_*) u=${mode%%_*}; env="GAC_DP_DEV_US=${u#us} GAC_DP_GPU_MAX=${mode#*_}" ;;
       *) env="GAC_DP_GPU_MAX=$mode" ;;
     esac
     t0=$(date +%s%N)
@@ -23,6 +26,8 @@ for i in $(seq 1 ${REPS:-2}); do
     ms=$(( ($(date +%s%N) - t0) / 1000000 ))
     sha=$(sha256sum $d/o.chain | cut -c1-16)
     split=$(grep -o "hybrid DP: [^)]*)" $out/${mode}_$i.err | head -1)
+    dev=$(grep -o "device's [0-9]* pairs took [0-9.]* s" $out/${mode}_$i.err | head -1)
+    split="$split $dev"
     echo "$mode rep $i: wall $ms ms sha $sha $split" | tee -a $out/summary.txt
     rm -f $d/o.chain
   done

@@ -214,3 +214,38 @@ def test_axtchain_block_past_sequence_end(tool, side, tmp_path):
                             text=True, timeout=300)
         assert rr.returncode == 255
         assert r.stderr.strip().splitlines()[-1] == rr.stderr.strip().splitlines()[-1]
+
+
+@pytest.mark.parametrize("env", [{}, {"GAC_DP_FAST": "0"}, {"GAC_DP_OVCAP": "0"}])
+def test_device_built_dp_inputs_cpu(tool, env, tmp_path):
+    """gac_chain_dp_blocks (the kd-tree DP's leaves, trees, update paths and
+    overlap lists built level-synchronously on the device, gac_dptree.hip) as
+    its kernel-by-kernel CPU restatement in the stand-in: GAC_AXT_DP=gpu on
+    the golden axtChain cases and a C4-shaped set, with the fast search, the
+    reference search (GAC_DP_FAST=0) and every overlapping leaf sent to the
+    reference order (GAC_DP_OVCAP=0), equal to the reference's chains."""
+    base = dict(os.environ, GAC_AXT_DP="gpu", GAC_THREADS="2", **env)
+    with open(os.path.join(GOLDEN, "axtchain", "cases.json")) as f:
+        cases = json.load(f)
+    for seed in (5, 6):
+        d = os.path.join(GOLDEN, "axtchain", f"s{seed}")
+        for case in ("loose", "medium0", "axt"):
+            opts = cases[case]
+            inp = "in.psl" if "-psl" in opts else "in.axt.gz"
+            out = tmp_path / f"{case}{seed}.chain"
+            subprocess.run([tool] + opts + [os.path.join(d, inp), os.path.join(d, "t.2bit"),
+                                            os.path.join(d, "q.2bit"), str(out)],
+                           env=base, check=True, capture_output=True, timeout=300)
+            assert filecmp.cmp(out, os.path.join(d, f"{case}.chain"), shallow=False), (case, seed)
+    ref = os.path.join(ROOT, "oracle", "_ref", "axtChain")
+    if not os.path.exists(ref):
+        return
+    synth = os.path.join(ROOT, "genomealignmenttools_amd", "libexec", "gac_synth")
+    subprocess.run([synth, "c4", str(tmp_path), "-blocks=100000", "-nt=4", "-nq=4", "-tsize=3000000",
+                    "-qsize=2500000", "-threads=4"], check=True, timeout=300, capture_output=True)
+    args = ["-linearGap=loose", "-psl", "in.psl", "t.2bit", "q.2bit"]
+    subprocess.run([tool] + args + ["dev.chain"], cwd=tmp_path, env=base, check=True,
+                   capture_output=True, timeout=600)
+    subprocess.run([ref] + args + ["ref.chain"], cwd=tmp_path, check=True, timeout=600,
+                   capture_output=True)
+    assert filecmp.cmp(tmp_path / "dev.chain", tmp_path / "ref.chain", shallow=False)
