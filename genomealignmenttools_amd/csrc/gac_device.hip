@@ -1235,7 +1235,16 @@ static hipError_t dp_launch(gac_ctx *c, DpArgs &a, int grid, bool fast) {
         e = hipMemsetAsync(d_prof, 0, kDpProf * sizeof(unsigned long long), c->stream);
     a.prof = d_prof;
     const double tk0 = wall_s();
-    if (e == hipSuccess) e = fast ? launch_dp_fast(a, grid, c->stream) : launch_dp(a, grid, c->stream);
+    // GAC_DP_WAVES=4/8/16: k_dp_spec, that many waves per pair
+    static int waves = -1;
+    if (waves < 0) {
+        const char *wv = getenv("GAC_DP_WAVES");
+        waves = wv && *wv ? atoi(wv) : 1;
+        if (waves != 4 && waves != 8 && waves != 16) waves = 1;
+    }
+    if (e == hipSuccess)
+        e = !fast ? launch_dp(a, grid, c->stream)
+                  : (waves > 1 ? launch_dp_spec(a, grid, waves, c->stream) : launch_dp_fast(a, grid, c->stream));
     if (d_prof && e == hipSuccess) {
         unsigned long long pv[kDpProf];
         e = hipMemcpyAsync(pv, d_prof, sizeof(pv), hipMemcpyDeviceToHost, c->stream);
@@ -1253,6 +1262,13 @@ static hipError_t dp_launch(gac_ctx *c, DpArgs &a, int grid, bool fast) {
                     pv[kPfCycLoad] / L, pv[kPfCycSeed] / L, pv[kPfCycWalk] / L, pv[kPfCycXover] / L,
                     pv[kPfCycAnom] / L, pv[kPfCycFb] / L, pv[kPfCycCommit] / L, pv[kPfNextWin] / L,
                     pv[kPfNextWin] ? (double)pv[kPfNextSeq] / pv[kPfNextWin] : 0.0);
+            if (waves > 1)
+                fprintf(stderr, "[gac_chain_dp] k_dp_spec, %d waves per pair: per leaf %.0f cycles searching, "
+                        "%.0f waiting for its turn, in order: %.0f the leaves since the snapshot, %.0f "
+                        "anomalies, %.0f commit; then %.0f publishing; %.3f of the leaves "
+                        "searched beside earlier ones\n", waves, pv[kPfCycWalk] / L, pv[kPfCycLoad] / L,
+                        pv[kPfCycSeed] / L, pv[kPfCycAnom] / L, pv[kPfCycCommit] / L, pv[kPfCycFb] / L,
+                        pv[kPfXoverWin] / L);
         }
         hipFree(d_prof);
         a.prof = nullptr;
@@ -1675,6 +1691,7 @@ extern "C" int gac_chain_dp_blocks(gac_ctx *c, int64_t n_pairs, const int32_t *t
     a.ov = fast ? d_ov : nullptr;
     a.lin_k = lin_k;
     a.min_entry = min_entry;
+    a.err = d_err;
     const int grid = (int)std::min<int64_t>(P, 1 << 20);
     HIPCHK(dp_launch(c, a, grid, fast != 0));
     {
@@ -1721,7 +1738,9 @@ extern "C" int gac_chain_dp_blocks(gac_ctx *c, int64_t n_pairs, const int32_t *t
     HIPCHK(hipMemcpyAsync(&h_err, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     if (h_err)
-        return gac_fail(GAC_E_HIP, "gac_chain_dp_blocks: a predecessor is not a leaf (%d)", h_err);
+        return gac_fail(GAC_E_HIP, "gac_chain_dp_blocks: %s (%d)",
+                        (h_err & 32) ? "the DP's in-order commit stalled" : "a predecessor is not a leaf",
+                        h_err);
     if (timing)
         fprintf(stderr,
                 "[gac_chain_dp_blocks] %lld pairs, %lld blocks, %lld leaves, %d levels, %lld path "

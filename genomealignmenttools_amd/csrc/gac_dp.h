@@ -67,6 +67,9 @@ struct DpArgs {
     // GAC_DP_PROF: per-phase cycle counters of k_dp_fast (kDpProf slots,
     // summed over pairs), or null
     unsigned long long *prof;
+    // k_dp_spec: set (32) when a wave gave up waiting for its turn (a
+    // watchdog: the kernel then ends instead of spinning), or null
+    int32_t *err;
 };
 
 // k_dp_fast's profile slots (GAC_DP_PROF)
@@ -149,6 +152,9 @@ hipError_t launch_dt_out(const DtTree &t, const long long *lf_total, const int32
 
 hipError_t launch_dp(const DpArgs &a, int grid, hipStream_t s);
 hipError_t launch_dp_fast(const DpArgs &a, int grid, hipStream_t s);
+// k_dp_fast with `waves` (4, 8, 16) waves per pair searching consecutive
+// leaves at once, committed in order (k_dp_spec)
+hipError_t launch_dp_spec(const DpArgs &a, int grid, int waves, hipStream_t s);
 hipError_t launch_xover(const DpArgs &a, const XoverJob *jobs, int64_t n, int32_t *pos,
                         int32_t *adj, hipStream_t s);
 

@@ -561,6 +561,42 @@ __device__ void dp_walk(const DpArgs &a, const DpSeq &S, const int *m, const DpG
     }
 }
 
+// k_dp_fast's step C (the host's dp_anomaly): one of the leaf's overlapping
+// candidates ov[o0 .. o1) (leaf nodes; -1: too many listed) could score at
+// least `best` while violating a bound at its own leaf -- the leaf then takes
+// the reference search order.  Wave-uniform result.
+__device__ __forceinline__ bool dp_anomaly_check(const DpArgs &a, const DpSeq &S, const int *m,
+                                                 const DpGapLds &sg, const DpPair &P,
+                                                 const DpLeafCtx &X, const int2 *nb,
+                                                 const long long *tot, int64_t o0, int64_t o1,
+                                                 long long best) {
+    const int lane = threadIdx.x & (kWave - 1);
+    bool fb = false;
+    const long long need = best > 0 ? best : 1;
+    const int lsize = X.lqe - X.lq;
+    for (int64_t k = o0 + lane; k < o1; k += kWave) {
+        const int c = a.ov[k];
+        if (c < 0) {
+            fb = true;
+            continue;
+        }
+        const int cpos = ~nb[c].y;
+        const int4 cb = a.lf[P.leaf_off + cpos];  // {qs, qe, ts, te}
+        const int dq = X.lq - cb.y, dt = X.lt - cb.w;
+        const int ov = -(dq < dt ? dq : dt);
+        if (ov >= lsize || ov >= cb.y - cb.x) continue;  // connect cost 1e8
+        const long long tc = ld_wg(tot + c);
+        const long long ub = tc + X.ls - dp_gap_lds(a, sg, dq + ov, dt + ov) - (long long)ov * a.min_entry;
+        if (ub < need) continue;
+        const long long sc = tc + X.ls - dp_connect_cost(a, S, m, cb.x, cb.y, cb.w, X.lq, X.lqe, X.lt);
+        if (sc < need) continue;
+        const long long bc = tc + X.ls - dp_gap_lds(a, sg, dq, dt);
+        const long long bl = 1024 * tc - a.lin_k * ((long long)dq + dt) + 1024 * X.ls;
+        if (sc > bc || 1024 * sc > bl) fb = true;
+    }
+    return __ballot(fb) != 0;
+}
+
 __global__ void __launch_bounds__(kWave) k_dp_fast(DpArgs a) {
     __shared__ int s_m[16];
     __shared__ DpGapLds s_gap;
@@ -677,36 +713,10 @@ __global__ void __launch_bounds__(kWave) k_dp_fast(DpArgs a) {
             dp_walk<true>(a, S, s_m, s_gap, P, X, kl, best, best_node, pf, prof);
             DP_LAP(kPfCycWalk)
             // ---- C: anomalies among the overlapping candidates
-            bool fb = false;
-            {
-                const long long need = best > 0 ? best : 1;
-                const int lsize = X.lqe - X.lq;
-                if (prof) pf.v[kPfOvChecks] += o1 - o0;
-                for (int64_t k = o0 + lane; k < o1; k += kWave) {
-                    const int c = a.ov[k];
-                    if (c < 0) {
-                        fb = true;
-                        continue;
-                    }
-                    const int cpos = ~nb[c].y;
-                    const int4 cb = a.lf[P.leaf_off + cpos];  // {qs, qe, ts, te}
-                    const int dq = X.lq - cb.y, dt = X.lt - cb.w;
-                    const int ov = -(dq < dt ? dq : dt);
-                    if (ov >= lsize || ov >= cb.y - cb.x) continue;  // connect cost 1e8
-                    const long long tc = ld_wg(tot + c);
-                    const long long ub = tc + X.ls - dp_gap_lds(a, s_gap, dq + ov, dt + ov) -
-                                         (long long)ov * a.min_entry;
-                    if (ub < need) continue;
-                    const long long sc =
-                        tc + X.ls - dp_connect_cost(a, S, s_m, cb.x, cb.y, cb.w, X.lq, X.lqe, X.lt);
-                    if (sc < need) continue;
-                    const long long bc = tc + X.ls - dp_gap_lds(a, s_gap, dq, dt);
-                    const long long bl = 1024 * tc - a.lin_k * ((long long)dq + dt) + 1024 * X.ls;
-                    if (sc > bc || 1024 * sc > bl) fb = true;
-                }
-            }
+            if (prof) pf.v[kPfOvChecks] += o1 - o0;
+            const bool fb = dp_anomaly_check(a, S, s_m, s_gap, P, X, nb, tot, o0, o1, best);
             DP_LAP(kPfCycAnom)
-            if (__ballot(fb)) {
+            if (fb) {
                 best = 0;
                 best_node = -1;
                 if (prof) ++pf.v[kPfFallbacks];
@@ -747,6 +757,281 @@ __global__ void __launch_bounds__(kWave) k_dp_fast(DpArgs a) {
             if (k == lane) v = pf.v[k];
         atomicAdd(a.prof + lane, v);
     }
+}
+
+// ------------------------------------------------------------ k_dp_spec --
+// k_dp_fast with W waves per pair, searching W consecutive leaves (target
+// order) at once and committing them in order -- the device form of the
+// host's searcher/committer team (pair_dp_team).  Wave w takes leaves w,
+// w + W, ...; leaf i:
+//   1. snapshot c0 = the count of committed leaves (every leaf < c0 has its
+//      total and its update path's bounds in the tree);
+//   2. seed from the ring's leaves in [c0 - 64 + W, c0) (slots no commit in
+//      flight can overwrite) and run the fast walk on the tree as it is:
+//      its bounds include every leaf < c0, so the walk's best is the exact
+//      maximum over the candidates < c0 (ties to the smaller node), joined
+//      by at most some of [c0, i) with totals <= their final ones;
+//   3. wait for its turn (c = i), then score the leaves [c0, i) exactly from
+//      the ring (final totals now) and keep the better of each: the maximum
+//      over every candidate < i, as findBestPredecessors' in-order search;
+//   4. the anomaly check on final totals (k_dp_fast's step C) and, when it
+//      fires, the reference-order walk on the final tree;
+//   5. commit (total, update path, ring slot) and release c = i + 1.
+// Bounds only grow, so a walk on a tree that lacks some of [c0, i) prunes
+// only subtrees whose leaves < c0 cannot reach its best: steps 2-3 give the
+// exact result without searching again.
+// k_dp_spec's in-order turns: wait until *c == i (LDS, polled with a nap);
+// false after seconds without progress (err |= 32: the kernel then ends)
+__device__ __forceinline__ bool dp_spec_wait(const int *c, int i, int32_t *err) {
+    for (unsigned spin = 0; ; ++spin) {
+        const int v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (v == i) return true;
+        __builtin_amdgcn_s_sleep(2);
+        if (spin > (1u << 26)) {
+            if (err && (threadIdx.x & (kWave - 1)) == 0) atomicOr(err, 32);
+            return false;
+        }
+    }
+}
+// the same, then an acquire of what the publisher released before *c = i
+__device__ __forceinline__ bool dp_spec_acquire(const int *c, int i, int32_t *err) {
+    if (!dp_spec_wait(c, i, err)) return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    return true;
+}
+
+template <int W>
+__global__ void __launch_bounds__(kWave * W) k_dp_spec(DpArgs a) {
+    __shared__ int s_m[16];
+    __shared__ DpGapLds s_gap;
+    __shared__ int4 r_box[kWave];  // the last 64 committed leaves: {qs, qe, ts, te}
+    __shared__ long long r_tot[kWave];
+    __shared__ int r_node[kWave];
+    __shared__ int r_leaf[kWave];
+    __shared__ int s_commit;  // leaves committed (their ring slots written)
+    __shared__ int s_vis;     // leaves whose tree updates are visible (<= s_commit)
+    const int tid = threadIdx.x, lane = tid & (kWave - 1);
+    const int nt = kWave * W;
+    if (tid < 16) s_m[tid] = a.m16[tid];
+    for (int k = tid; k < 3 * kGapLds; k += nt) {
+        const int which = k / kGapLds, d = k % kGapLds;
+        s_gap.gap[k] = which == 0 ? dp_gap_cost(a, d, 0)
+                                  : (which == 1 ? dp_gap_cost(a, 0, d)
+                                                : (d >= 2 ? dp_gap_cost(a, 1, d - 1) : 0));
+    }
+    if (tid < kMaxLong) {
+        s_gap.lpos[tid] = a.gap.long_pos[tid];
+        for (int w = 0; w < 3; ++w) s_gap.lval[w][tid] = a.gap.long_val[w][tid];
+    }
+    for (int k = tid; k < 3 * kLbN; k += nt) {
+        const int which = k / kLbN, i = k % kLbN;
+        const int64_t x = dp_lb_point(i);
+        const int d = x > 0x7fffffff ? 0x7fffffff : (int)x;
+        s_gap.lb[which][i] = which == 0 ? dp_gap_cost(a, d, 0)
+                                        : (which == 1 ? dp_gap_cost(a, 0, d) : dp_gap_cost(a, 1, d - 1));
+    }
+    if (tid < 3) {
+        s_gap.last_pos[tid] = a.gap.last_pos[tid];
+        s_gap.last_val[tid] = a.gap.last_val[tid];
+        s_gap.last_slope[tid] = a.gap.last_slope[tid];
+    }
+    if (tid == 0) {
+        s_gap.small_size = a.gap.small_size;
+        s_gap.long_count = a.gap.long_count;
+    }
+    const int wave = tid / kWave;
+    const bool prof = a.prof != nullptr;
+    DpPf pf;
+    for (int k = 0; k < kDpProf; ++k) pf.v[k] = 0;
+    for (int64_t pi = blockIdx.x; pi < a.n_pairs; pi += gridDim.x) {
+        const DpPair P = a.pairs[pi];
+        const DpSeq S = {P.tbase, P.qbase};
+        long long *ms = a.nd_ms + P.node_off;
+        long long *nwp = a.nd_nw + P.node_off;
+        long long *tot = a.nd_tot + P.node_off;
+        const int2 *nb = a.nd_b + P.node_off;
+        __syncthreads();  // (the previous pair's waves are done with the ring)
+        if (tid < kWave) {
+            r_node[tid] = -1;
+            r_leaf[tid] = -1;
+        }
+        if (tid == 0) s_commit = s_vis = 0;
+        __syncthreads();
+        for (int i = wave; i < P.n_leaves; i += W) {
+            const int64_t li = P.leaf_off + i;
+            const int4 L = a.lf[li];  // {qs, qe, ts, te}
+            const int node = a.lf_node[li];
+            DpLeafCtx X;
+            X.lq = L.x;
+            X.lqe = L.y;
+            X.lt = L.z;
+            X.lte = L.w;
+            X.ls = a.lf_score[li];
+            const int64_t q0 = a.path_off[li], q1 = a.path_off[li + 1];
+            const int64_t o0 = a.ov_off[li], o1 = a.ov_off[li + 1];
+            const long long kl = a.lin_k * ((long long)X.lq + X.lt) - 1024 * X.ls;
+            // the update path's first 64 nodes now, off the in-order section
+            const int pu = q0 + lane < q1 ? a.path[q0 + lane] : -1;
+            if (prof) ++pf.v[kPfLeaves];
+            // ---- 1-2: snapshot, seed, fast walk
+            unsigned long long ck = prof ? clock64() : 0;
+            const int c0 = __hip_atomic_load(&s_vis, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            long long best = 0;
+            int best_node = -1;
+            {
+                const int j = r_leaf[lane];
+                long long sc = -1;
+                int nd = 0x7fffffff;
+                if (j >= 0 && j >= c0 - kWave + W && j < c0) {  // (-1: a slot not written yet)
+                    const int4 bx = r_box[lane];
+                    nd = r_node[lane];
+                    if (bx.x < X.lq && bx.z < X.lt) {
+                        const int dq = X.lq - bx.y, dt = X.lt - bx.w;
+                        if (dq >= 0 && dt >= 0) sc = r_tot[lane] + X.ls - dp_gap_lds(a, s_gap, dq, dt);
+                    }
+                }
+                const long long bs = dp_wave_max64(sc > 0 ? sc : -1, lane);
+                if (bs > 0) {
+                    best = bs;
+                    best_node = dp_wave_min32(sc == bs ? nd : 0x7fffffff, lane);
+                }
+            }
+            dp_walk<true>(a, S, s_m, s_gap, P, X, kl, best, best_node, pf, prof);
+            if (prof) {  // (slots: search, wait, in-order section)
+                const unsigned long long t_ = clock64();
+                pf.v[kPfCycWalk] += t_ - ck;
+                ck = t_;
+            }
+            // ---- 3: in order; the leaves committed since the snapshot
+            if (!dp_spec_wait(&s_commit, i, a.err)) return;
+            if (prof) {
+                const unsigned long long t_ = clock64();
+                pf.v[kPfCycLoad] += t_ - ck;
+                ck = t_;
+            }
+            if (c0 < i) {
+                if (prof) ++pf.v[kPfXoverWin];  // (counts the leaves searched beside earlier ones)
+                long long sc = -1;
+                int nd = 0x7fffffff;
+                if (lane < i - c0) {
+                    const int slot = (c0 + lane) & (kWave - 1);
+                    const int4 bx = r_box[slot];  // {qs, qe, ts, te}
+                    if (bx.x < X.lq && bx.z < X.lt) {
+                        nd = r_node[slot];
+                        const int dq = X.lq - bx.y, dt = X.lt - bx.w;
+                        const int cost = (dq >= 0 && dt >= 0)
+                                             ? dp_gap_lds(a, s_gap, dq, dt)
+                                             : dp_connect_cost(a, S, s_m, bx.x, bx.y, bx.w, X.lq, X.lqe, X.lt);
+                        sc = r_tot[slot] + X.ls - cost;
+                    }
+                }
+                const long long bs = dp_wave_max64(sc, lane);
+                if (bs > 0) {
+                    const int bn = dp_wave_min32(sc == bs ? nd : 0x7fffffff, lane);
+                    if (bs > best || (bs == best && bn < best_node)) {
+                        best = bs;
+                        best_node = bn;
+                    }
+                }
+            }
+            if (prof) {
+                const unsigned long long t_ = clock64();
+                pf.v[kPfCycSeed] += t_ - ck;  // (spec: the leaves since the snapshot)
+                ck = t_;
+            }
+            // ---- 4: anomalies on final totals (the earlier leaves' tree
+            // updates visible first), the reference walk if one fires
+            if (prof) pf.v[kPfOvChecks] += o1 - o0;
+            if (o1 > o0 && !dp_spec_acquire(&s_vis, i, a.err)) return;
+            if (dp_anomaly_check(a, S, s_m, s_gap, P, X, nb, tot, o0, o1, best)) {
+                best = 0;
+                best_node = -1;
+                if (prof) ++pf.v[kPfFallbacks];
+                dp_walk<false>(a, S, s_m, s_gap, P, X, 0, best, best_node, pf, prof);
+            }
+            if (prof) {
+                const unsigned long long t_ = clock64();
+                pf.v[kPfCycAnom] += t_ - ck;  // (spec: anomaly check + fallback)
+                ck = t_;
+            }
+            // ---- 5: commit
+            long long total = X.ls;
+            int pred = -1;
+            if (best > X.ls) {
+                total = best;
+                pred = best_node;
+            }
+#ifdef GAC_DP_SPEC_CHECK
+            if (pred < -1 || pred >= P.n_nodes || node < 0 || node >= P.n_nodes) {
+                if (a.err && lane == 0) atomicOr(a.err, pred < -1 || pred >= P.n_nodes ? 64 : 128);
+                pred = -1;
+                if (node < 0 || node >= P.n_nodes) return;
+            }
+            for (int64_t k = q0 + lane; k < q1; k += kWave)
+                if (a.path[k] < 0 || a.path[k] >= P.n_nodes) {
+                    if (a.err) atomicOr(a.err, 256);
+                    return;
+                }
+#endif
+            const long long nwv = 1024 * total + a.lin_k * ((long long)X.lqe + X.lte);
+            // (GAC_DP_SPEC_LDST: a load and a store, as k_dp_fast; else an
+            // atomic max with no return -- no round trip before the fence;
+            // the other waves' walks may read either value: bounds only grow)
+            for (int64_t k = q0 + lane; k < q1; k += kWave) {
+                const int u = k < q0 + kWave ? pu : a.path[k];
+#ifdef GAC_DP_SPEC_LDST
+                if (ld_wg(ms + u) < total) st_wg(ms + u, total);
+                if (ld_wg(nwp + u) < nwv) st_wg(nwp + u, nwv);
+#else
+                __hip_atomic_fetch_max(ms + u, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_max(nwp + u, nwv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+            }
+            if (lane == 0) {
+                a.lf_total[li] = total;
+                a.lf_pred[li] = pred;
+                st_wg(tot + node, total);
+                const int slot = i & (kWave - 1);
+                r_box[slot] = L;
+                r_tot[slot] = total;
+                r_node[slot] = node;
+                r_leaf[slot] = i;
+                // the next leaf's turn needs the ring only: an LDS-only
+                // release (the tree updates are still in flight)
+                __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __hip_atomic_store(&s_commit, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            if (prof) {
+                const unsigned long long t_ = clock64();
+                pf.v[kPfCycCommit] += t_ - ck;
+                ck = t_;
+            }
+            // then the tree updates land and are published in order
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (!dp_spec_wait(&s_vis, i, a.err)) return;
+            if (lane == 0)
+                __hip_atomic_store(&s_vis, i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (prof) pf.v[kPfCycFb] += clock64() - ck;  // (spec: publishing the tree updates)
+        }
+    }
+    if (prof && lane < kDpProf) {
+        unsigned long long v = 0;
+        for (int k = 0; k < kDpProf; ++k)
+            if (k == lane) v = pf.v[k];
+        atomicAdd(a.prof + lane, v);
+    }
+}
+
+hipError_t launch_dp_spec(const DpArgs &a, int grid, int waves, hipStream_t s) {
+    if (a.n_pairs == 0) return hipSuccess;
+    switch (waves) {
+    case 4: hipLaunchKernelGGL(k_dp_spec<4>, dim3((unsigned)grid), dim3(kWave * 4), 0, s, a); break;
+    case 8: hipLaunchKernelGGL(k_dp_spec<8>, dim3((unsigned)grid), dim3(kWave * 8), 0, s, a); break;
+    case 16: hipLaunchKernelGGL(k_dp_spec<16>, dim3((unsigned)grid), dim3(kWave * 16), 0, s, a); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_dp_fast(const DpArgs &a, int grid, hipStream_t s) {
