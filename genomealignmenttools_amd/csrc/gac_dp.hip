@@ -82,8 +82,9 @@ __device__ __forceinline__ int dp_gap_cost(const DpArgs &a, int dq, int dt) {
 __device__ __forceinline__ int dp_code(const uint2 *planes, const uint32_t *nmask, int64_t g) {
     const int64_t w = g >> 5;
     const int s = (int)(g & 31);
-    if ((nmask[w] >> s) & 1u) return 4;
+    const uint32_t nm = nmask[w];  // (both loads in flight at once)
     const uint2 p = planes[w];
+    if ((nm >> s) & 1u) return 4;
     return (int)(((p.x >> s) & 1u) | (((p.y >> s) & 1u) << 1));
 }
 
@@ -780,6 +781,96 @@ __global__ void __launch_bounds__(kWave) k_dp_fast(DpArgs a) {
 // Bounds only grow, so a walk on a tree that lacks some of [c0, i) prunes
 // only subtrees whose leaves < c0 cannot reach its best: steps 2-3 give the
 // exact result without searching again.
+// cBlockFindCrossover's adjustment (chainConnect.c:61-105) with the whole
+// wave (arguments wave-uniform): lane k scores overlap base k of both blocks
+// (left - right), the best crossover is where the prefix sum peaks (k_xover)
+__device__ long long dp_crossover_adj_wave(const DpArgs &a, const DpSeq &S, const int *m, int lqe,
+                                           int lte, int rqs, int rts, int ov) {
+    const int lane = threadIdx.x & (kWave - 1);
+    long long carry = 0, lsum = 0, bestv = 0;
+    for (int base = 0; base < ov; base += kWave) {
+        const int k = base + lane;
+        long long d = 0, l = 0;
+        if (k < ov) {
+            l = dp_msc(m, dp_qcode(a, S, lqe - ov + k), dp_tcode(a, S, lte - ov + k));
+            d = l - dp_msc(m, dp_qcode(a, S, rqs + k), dp_tcode(a, S, rts + k));
+        }
+        long long incl = d;
+#pragma unroll
+        for (int sh = 1; sh < kWave; sh <<= 1) {
+            const long long o = __shfl_up(incl, sh, kWave);
+            if (lane >= sh) incl += o;
+        }
+        const long long mx = dp_wave_max64(k < ov ? carry + incl : (long long)INT64_MIN, lane);
+        bestv = mx > bestv ? mx : bestv;
+        carry += dp_readlane64(incl, kWave - 1);
+        long long ls = l;
+#pragma unroll
+        for (int sh = 32; sh > 0; sh >>= 1) ls += __shfl_xor(ls, sh, kWave);
+        lsum += ls;
+    }
+    return lsum - bestv;
+}
+
+// k_dp_spec: fold the candidates among committed leaves [j0, j1) (their ring
+// slots) into (best, best_node), exactly: a bound first (an overlapping one's
+// crossover costs at least ov * min_entry), the exact cost only where the
+// bound can reach the best, an overlap's crossover on the whole wave
+__device__ void dp_spec_fold(const DpArgs &a, const DpSeq &S, const int *m, const DpGapLds &sg,
+                             const DpLeafCtx &X, const int4 *r_box, const long long *r_tot,
+                             const int *r_node, int j0, int j1, long long &best, int &best_node) {
+    const int lane = threadIdx.x & (kWave - 1);
+    for (int jb = j0; jb < j1; jb += kWave) {
+        const int j = jb + lane;
+        long long sc = -1;
+        int nd = 0x7fffffff;
+        bool need_x = false;  // an overlap whose bound reaches the best
+        int4 bx = make_int4(0, 0, 0, 0);
+        long long tj = 0;
+        if (j < j1) {
+            const int slot = j & (kWave - 1);
+            bx = r_box[slot];  // {qs, qe, ts, te}
+            if (bx.x < X.lq && bx.z < X.lt) {
+                tj = r_tot[slot];
+                const int dq = X.lq - bx.y, dt = X.lt - bx.w;
+                if (dq >= 0 && dt >= 0) {
+                    sc = tj + X.ls - dp_gap_lds(a, sg, dq, dt);
+                    nd = r_node[slot];
+                } else {
+                    const int ov = -(dq < dt ? dq : dt);
+                    nd = r_node[slot];
+                    if (ov < X.lqe - X.lq && ov < bx.y - bx.x) {
+                        const long long ub = tj + X.ls - dp_gap_lds(a, sg, dq + ov, dt + ov) -
+                                             (long long)ov * a.min_entry;
+                        need_x = ub > 0 && ub >= best;
+                    } else {  // (cost 1e8: no crossover)
+                        sc = tj + X.ls - dp_connect_cost(a, S, m, bx.x, bx.y, bx.w, X.lq, X.lqe, X.lt);
+                    }
+                }
+            }
+        }
+        unsigned long long need = __ballot(need_x);
+        while (need) {  // (rare: one overlap at a time, on the whole wave)
+            const int u = __builtin_ctzll(need);
+            need &= need - 1;
+            const int uqs = __shfl(bx.x, u), uqe = __shfl(bx.y, u), ute = __shfl(bx.w, u);
+            const int dq = X.lq - uqe, dt = X.lt - ute, ov = -(dq < dt ? dq : dt);
+            const long long adj = dp_crossover_adj_wave(a, S, m, uqe, ute, X.lq, X.lt, ov);
+            const long long s_u = dp_readlane64(tj, u) + X.ls - adj - dp_gap_lds(a, sg, dq + ov, dt + ov);
+            (void)uqs;
+            if (lane == u) sc = s_u;
+        }
+        const long long bs = dp_wave_max64(sc, lane);
+        if (bs > 0) {
+            const int bn = dp_wave_min32(sc == bs ? nd : 0x7fffffff, lane);
+            if (bs > best || (bs == best && bn < best_node)) {
+                best = bs;
+                best_node = bn;
+            }
+        }
+    }
+}
+
 // k_dp_spec's in-order turns: wait until *c == i (LDS, polled with a nap);
 // false after seconds without progress (err |= 32: the kernel then ends)
 __device__ __forceinline__ bool dp_spec_wait(const int *c, int i, int32_t *err) {
@@ -904,36 +995,35 @@ __global__ void __launch_bounds__(kWave * W) k_dp_spec(DpArgs a) {
                 ck = t_;
             }
             // ---- 3: in order; the leaves committed since the snapshot
-            if (!dp_spec_wait(&s_commit, i, a.err)) return;
-            if (prof) {
-                const unsigned long long t_ = clock64();
-                pf.v[kPfCycLoad] += t_ - ck;
-                ck = t_;
-            }
-            if (c0 < i) {
-                if (prof) ++pf.v[kPfXoverWin];  // (counts the leaves searched beside earlier ones)
-                long long sc = -1;
-                int nd = 0x7fffffff;
-                if (lane < i - c0) {
-                    const int slot = (c0 + lane) & (kWave - 1);
-                    const int4 bx = r_box[slot];  // {qs, qe, ts, te}
-                    if (bx.x < X.lq && bx.z < X.lt) {
-                        nd = r_node[slot];
-                        const int dq = X.lq - bx.y, dt = X.lt - bx.w;
-                        const int cost = (dq >= 0 && dt >= 0)
-                                             ? dp_gap_lds(a, s_gap, dq, dt)
-                                             : dp_connect_cost(a, S, s_m, bx.x, bx.y, bx.w, X.lq, X.lqe, X.lt);
-                        sc = r_tot[slot] + X.ls - cost;
+            // ---- 3: until its turn, the leaves committed since the
+            // snapshot folded in as they commit (final totals, from the ring)
+            {
+                int done = c0;
+                for (unsigned spin = 0;; ++spin) {
+                    const int c = __hip_atomic_load(&s_commit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if (c > done) {
+                        if (prof) {
+                            const unsigned long long t_ = clock64();
+                            pf.v[kPfCycLoad] += t_ - ck;
+                            ck = t_;
+                        }
+                        dp_spec_fold(a, S, s_m, s_gap, X, r_box, r_tot, r_node, done, c, best, best_node);
+                        if (prof) {
+                            const unsigned long long t_ = clock64();
+                            pf.v[c == i ? kPfCycSeed : kPfCycLoad] += t_ - ck;
+                            ck = t_;
+                        }
+                        done = c;
+                    }
+                    if (c == i) break;
+                    __builtin_amdgcn_s_sleep(2);
+                    if (spin > (1u << 26)) {  // (seconds without a commit: end, reported)
+                        if (a.err && lane == 0) atomicOr(a.err, 32);
+                        return;
                     }
                 }
-                const long long bs = dp_wave_max64(sc, lane);
-                if (bs > 0) {
-                    const int bn = dp_wave_min32(sc == bs ? nd : 0x7fffffff, lane);
-                    if (bs > best || (bs == best && bn < best_node)) {
-                        best = bs;
-                        best_node = bn;
-                    }
-                }
+                if (prof && c0 < i) ++pf.v[kPfXoverWin];
             }
             if (prof) {
                 const unsigned long long t_ = clock64();
