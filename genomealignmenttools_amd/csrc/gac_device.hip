@@ -1235,16 +1235,31 @@ static hipError_t dp_launch(gac_ctx *c, DpArgs &a, int grid, bool fast) {
         e = hipMemsetAsync(d_prof, 0, kDpProf * sizeof(unsigned long long), c->stream);
     a.prof = d_prof;
     const double tk0 = wall_s();
-    // GAC_DP_WAVES=4/8/16: k_dp_spec, that many waves per pair
+    // k_dp_spec with 16 waves per pair (GAC_DP_WAVES=4/8/16; 1: k_dp_fast,
+    // one wave per pair -- 7.2x slower on the C4-shaped set, r06spec7)
     static int waves = -1;
     if (waves < 0) {
         const char *wv = getenv("GAC_DP_WAVES");
-        waves = wv && *wv ? atoi(wv) : 1;
+        waves = wv && *wv ? atoi(wv) : 16;
         if (waves != 4 && waves != 8 && waves != 16) waves = 1;
     }
+    // (k_dp_spec's watchdog flag: the caller's, or one of our own)
+    int32_t *d_err_own = nullptr;
+    if (e == hipSuccess && fast && waves > 1 && !a.err &&
+        (e = hipMalloc(&d_err_own, sizeof(int32_t))) == hipSuccess &&
+        (e = hipMemsetAsync(d_err_own, 0, sizeof(int32_t), c->stream)) == hipSuccess)
+        a.err = d_err_own;
     if (e == hipSuccess)
         e = !fast ? launch_dp(a, grid, c->stream)
                   : (waves > 1 ? launch_dp_spec(a, grid, waves, c->stream) : launch_dp_fast(a, grid, c->stream));
+    if (d_err_own) {
+        int32_t h = 0;
+        if (e == hipSuccess) e = hipMemcpyAsync(&h, d_err_own, sizeof(h), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e == hipSuccess && h) e = hipErrorLaunchTimeOut;  // (the in-order commit stalled)
+        hipFree(d_err_own);
+        a.err = nullptr;
+    }
     if (d_prof && e == hipSuccess) {
         unsigned long long pv[kDpProf];
         e = hipMemcpyAsync(pv, d_prof, sizeof(pv), hipMemcpyDeviceToHost, c->stream);
@@ -1252,12 +1267,13 @@ static hipError_t dp_launch(gac_ctx *c, DpArgs &a, int grid, bool fast) {
         if (e == hipSuccess) {
             const double secs = wall_s() - tk0, L = pv[kPfLeaves] ? (double)pv[kPfLeaves] : 1.0;
             fprintf(stderr,
-                    "[gac_chain_dp] k_dp_fast %.3f s, %llu pairs, %llu leaves, %llu fallbacks; per leaf: "
+                    "[gac_chain_dp] %s %.3f s, %llu pairs, %llu leaves, %llu fallbacks; per leaf: "
                     "%.2f windows, %.3f fallback windows, %.3f windows with an overlapping candidate, "
                     "%.2f overlap checks; cycles per leaf: load %.0f seed %.0f walk %.0f "
                     "(node loads + bounds %.0f) anomalies %.0f fallback %.0f commit %.0f; next windows: %.2f per leaf, "
                     "%.3f contiguous\n",
-                    secs, (unsigned long long)a.n_pairs, pv[kPfLeaves], pv[kPfFallbacks],
+                    waves > 1 ? "k_dp_spec" : "k_dp_fast", secs, (unsigned long long)a.n_pairs,
+                    pv[kPfLeaves], pv[kPfFallbacks],
                     pv[kPfWindows] / L, pv[kPfFbWindows] / L, pv[kPfXoverWin] / L, pv[kPfOvChecks] / L,
                     pv[kPfCycLoad] / L, pv[kPfCycSeed] / L, pv[kPfCycWalk] / L, pv[kPfCycXover] / L,
                     pv[kPfCycAnom] / L, pv[kPfCycFb] / L, pv[kPfCycCommit] / L, pv[kPfNextWin] / L,

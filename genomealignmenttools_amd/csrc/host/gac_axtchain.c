@@ -3052,17 +3052,16 @@ static int axt_dp_gpu(ax_job *J, int nt) {
 
 /* ---- the hybrid DP (the default): the device takes the smallest pairs
  * (gac_chain_dp_blocks: their leaves, kd-trees, update paths and overlap
- * lists built on the device, then k_dp_fast, one wave per pair, every device
- * pair at once) while host threads take the others (teams on the largest).
- * A device pair must end within the host's critical path, estimated from the
+ * lists built on the device, then k_dp_spec, 16 waves per pair searching
+ * consecutive leaves and committing them in order, every device pair at
+ * once) while host threads take the others (teams on the largest).  A
+ * device pair must end within the host's critical path, estimated from the
  * largest pair at the team's rate (its device time, leaves x the device's
- * per-leaf time, within 0.7 of it), and is at most 200 k leaves.  With the
- * inputs built on the device the device's host work is the pack, peel and
- * finish only (C4 at 50 M blocks, r06dt2/r06dt3: 14.8 M blocks' trees +
- * paths + overlap lists 0.03 s of GPU, vs 1.7 s on two host threads built
- * and exported on the host (GAC_DP_DEVTREE=0); the device's 979 pairs done in
- * 3.4-3.5 s inside the largest pair's 7 s; wall 8.60 / 8.67 s vs host-only
- * 8.62 / 8.86 s).  Pairs go to the device from the smallest up.
+ * per-leaf time, within 0.7 of it), and is at most 1 M leaves.  C4 at 50 M
+ * blocks (r06sp16): the device's 1000 pairs, 23.1 M blocks (46 %), done in
+ * 3.7 s inside the largest pair's 7 s on its host team; wall 9.23 / 8.79 s vs
+ * host-only 8.97 / 8.91 s -- the wall is that one pair's team, which no
+ * device share shortens.  Pairs go to the device from the smallest up.
  * GAC_AXT_DP=host: no device pairs; GAC_DP_GPU_MAX=n: the leaf cap (0:
  * none); GAC_DP_DEV_US / GAC_DP_HOST_US: the per-leaf times of the model.
  * Returns the first device place in `order`. */
@@ -3072,14 +3071,14 @@ static int64_t dp_device_split(const int64_t *psize, const int32_t *order, int64
     if ((dpm && strcmp(dpm, "host") == 0) || !e->fast || np == 0)
         return np;
     const char *dv = getenv("GAC_DP_DEV_US"), *hv = getenv("GAC_DP_HOST_US");
-    const double dev_us = dv && atof(dv) > 0 ? atof(dv) : 14.0;  /* k_dp_fast, r06dp */
+    const double dev_us = dv && atof(dv) > 0 ? atof(dv) : 4.0;  /* k_dp_spec x 16, r06sp16 */
     const double host_us = hv && atof(hv) > 0 ? atof(hv) : 0.47; /* team, C4 (r04i) */
     const double crit = (double)psize[order[0]] * host_us * 1e-6;
     if (crit < 0.25) /* (small runs: the device's start-up costs more) */
         return np;
     int64_t lmax = (int64_t)(0.7 * crit / (dev_us * 1e-6));
     const char *mx = getenv("GAC_DP_GPU_MAX");
-    const int64_t cap = mx && *mx ? atoll(mx) : 200000;
+    const int64_t cap = mx && *mx ? atoll(mx) : 1000000;
     if (cap < lmax)
         lmax = cap;
     if (lmax < 1)

@@ -16,7 +16,7 @@ for w in ${WAVES:-1 4 8 16}; do
   ( cd $d && GAC_AXT_DP=gpu GAC_DP_WAVES=$w GAC_DP_PROF=1 GAC_TIMING=1 timeout -k 10 200 $B/axtChain $args w$w.chain ) > $out/w$w.err 2>&1
   rc=$?
   same=$(cmp -s $d/host.chain $d/w$w.chain && echo same || echo DIFF)
-  echo "waves $w rc $rc $same $(grep -o 'k_dp_fast [0-9.]* s, [0-9]* pairs, [0-9]* leaves, [0-9]* fallbacks' $out/w$w.err) $(grep -o 'k_dp[_a-z]* [0-9.]* s, results' $out/w$w.err)" | tee -a $out/summary.txt
+  echo "waves $w rc $rc $same $(grep -o 'k_dp_[a-z]* [0-9.]* s, [0-9]* pairs, [0-9]* leaves, [0-9]* fallbacks' $out/w$w.err) $(grep -o 'k_dp[_a-z]* [0-9.]* s, results' $out/w$w.err)" | tee -a $out/summary.txt
   [ $rc -eq 0 ] || exit $rc
 done
 rm -rf $d

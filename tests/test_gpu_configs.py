@@ -304,7 +304,7 @@ def test_c4_shaped_axtchain_5m_blocks(tmp_path):
 
 @pytest.mark.timeout(900)
 def test_device_dp_fallbacks(tmp_path):
-    """k_dp_fast's two ways back to the reference walk, on the device: the
+    """k_dp_spec's and k_dp_fast's two ways back to the reference walk, on the device: the
     anomaly check (an overlapping candidate whose crossover beats its bound,
     chainConnect.c:61-105) on a C4-shaped set dense with overlaps, and the
     overlap lists' cap (GAC_DP_OVCAP=0: every leaf with an overlapping
@@ -318,15 +318,19 @@ def test_device_dp_fallbacks(tmp_path):
     args = ["-linearGap=loose", "-psl", "in.psl", "t.2bit", "q.2bit"]
     _run([_ref("axtChain")] + args + ["ref.chain"], cwd=d, timeout=600)
     counts = []
-    for cap in ("", "0"):
-        out = "dev%s.chain" % cap
-        r = _run([_bin("axtChain")] + args + [out], cwd=d,
-                 env={"GAC_AXT_DP": "gpu", "GAC_DP_PROF": "1", "GAC_DP_OVCAP": cap})
-        m = re.search(r"k_dp_fast .*?(\d+) leaves, (\d+) fallbacks", r.stderr)
-        assert m, r.stderr[-2000:]
-        counts.append(int(m.group(2)))
-        _same(os.path.join(d, out), os.path.join(d, "ref.chain"))
+    # k_dp_spec (16 waves per pair, the default) and k_dp_fast (one wave)
+    for waves in ("16", "1"):
+        for cap in ("", "0"):
+            out = "dev%s_%s.chain" % (cap, waves)
+            r = _run([_bin("axtChain")] + args + [out], cwd=d,
+                     env={"GAC_AXT_DP": "gpu", "GAC_DP_PROF": "1", "GAC_DP_OVCAP": cap,
+                          "GAC_DP_WAVES": waves})
+            m = re.search(r"(k_dp_(?:fast|spec)) .*?(\d+) leaves, (\d+) fallbacks", r.stderr)
+            assert m and m.group(1) == ("k_dp_spec" if waves == "16" else "k_dp_fast"), r.stderr[-2000:]
+            counts.append(int(m.group(3)))
+            _same(os.path.join(d, out), os.path.join(d, "ref.chain"))
     assert counts[0] > 0 and counts[1] > counts[0], counts
+    assert counts[2:] == counts[:2], counts
 
 
 # ---------------------------------------------------------------- edge cases
