@@ -1224,6 +1224,18 @@ static int dev_upload(gac_ctx *c, T **d, const void *h, size_t n) {
     return GAC_OK;
 }
 
+// the fast DP's waves per pair: k_dp_spec with 16 (GAC_DP_WAVES=4/8/16; 1:
+// k_dp_fast, one wave per pair -- 7.2x slower on the C4-shaped set, r06spec7)
+static int dp_waves() {
+    static int waves = -1;
+    if (waves < 0) {
+        const char *wv = getenv("GAC_DP_WAVES");
+        int w = wv && *wv ? atoi(wv) : 16;
+        waves = (w == 4 || w == 8 || w == 16) ? w : 1;
+    }
+    return waves;
+}
+
 // k_dp_fast (fast) or k_dp over a.n_pairs pairs; GAC_DP_PROF: k_dp_fast's
 // per-phase cycle counters, summed over pairs, to stderr
 static hipError_t dp_launch(gac_ctx *c, DpArgs &a, int grid, bool fast) {
@@ -1235,14 +1247,7 @@ static hipError_t dp_launch(gac_ctx *c, DpArgs &a, int grid, bool fast) {
         e = hipMemsetAsync(d_prof, 0, kDpProf * sizeof(unsigned long long), c->stream);
     a.prof = d_prof;
     const double tk0 = wall_s();
-    // k_dp_spec with 16 waves per pair (GAC_DP_WAVES=4/8/16; 1: k_dp_fast,
-    // one wave per pair -- 7.2x slower on the C4-shaped set, r06spec7)
-    static int waves = -1;
-    if (waves < 0) {
-        const char *wv = getenv("GAC_DP_WAVES");
-        waves = wv && *wv ? atoi(wv) : 16;
-        if (waves != 4 && waves != 8 && waves != 16) waves = 1;
-    }
+    const int waves = dp_waves();
     // (k_dp_spec's watchdog flag: the caller's, or one of our own)
     int32_t *d_err_own = nullptr;
     if (e == hipSuccess && fast && waves > 1 && !a.err &&
@@ -1763,7 +1768,7 @@ extern "C" int gac_chain_dp_blocks(gac_ctx *c, int64_t n_pairs, const int32_t *t
                 "nodes, %lld overlap entries: upload + leaves %.3f s, trees + paths + overlaps %.3f s, "
                 "%s %.3f s, results %.3f s\n",
                 (long long)P, (long long)B, (long long)L, levels, n_path, n_ov, t1 - t0, t2 - t1,
-                fast ? "k_dp_fast" : "k_dp", t3 - t2, wall_s() - t3);
+                !fast ? "k_dp" : (dp_waves() > 1 ? "k_dp_spec" : "k_dp_fast"), t3 - t2, wall_s() - t3);
     return GAC_OK;
 }
 

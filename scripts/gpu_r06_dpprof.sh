@@ -13,7 +13,7 @@ d=/tmp/c4p
 $S c4 $d -seed=7 -blocks=1000000 -threads=16 > /dev/null || exit 1
 cd $d
 for w in 16 1; do
-  GAC_AXT_DP=gpu GAC_DP_WAVES=$w GAC_TIMING=1 HSA_ENABLE_SDMA=0 timeout -k 10 300 \
+  GAC_AXT_DP=gpu GAC_DP_WAVES=$w GAC_TIMING=1 GAC_PROFILE_EXIT=1 HSA_ENABLE_SDMA=0 timeout -k 10 300 \
     rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$out/w$w -o run -- \
     $X -linearGap=loose -psl in.psl t.2bit q.2bit w$w.chain > $GRAFT_REPO_ROOT/$out/w$w.err 2>&1 || exit $?
 done
