@@ -566,6 +566,12 @@ static uint8_t *g_cused = NULL;
 static int64_t g_cslots = 0, g_cn = 0;
 static int64_t g_gpu_calls = 0, g_gpu_ranges = 0, g_uploads = 0;
 static int64_t g_host_chains = 0, g_host_blocks = 0; /* (modified chains' blocks handed over) */
+/* GAC_CLEANER_SPEC=0: no speculative keys, no prefetch at a list's first
+ * pass (round 5's batching) */
+static int g_spec = 1;
+static int g_lookahead = 8;             /* lists whose keys one first-pass batch holds */
+static int64_t g_calls_site[3];         /* scoring calls: list batches, later passes, tests */
+static int g_site = 2;
 static double g_gpu_s = 0; /* wall time inside the scoring calls */
 
 static double wall_s(void) {
@@ -685,6 +691,7 @@ static void score_keys(state *S, const qkey *in, int64_t n) {
         ++n0;
     }
     const double t0 = wall_s();
+    ++g_calls_site[g_site];
     if (n0) {
         gt_check(gac_score_ranges(S->ctx, S->cs_base, rb, n0, GAC_WANT_LOCAL, g, l, a));
         ++g_gpu_calls;
@@ -768,16 +775,51 @@ static int break_keys(const state *S, const cbrk *b, qkey *out) {
     return 4;
 }
 
-/* keys of every break of a list (singles) and of its valid adjacent pairs */
+/* Speculative keys of break x (prev: its upstream neighbour): when the
+ * breaks before it are removed, test_and_remove hands each removed suspect's
+ * left fill to its downstream neighbour (d->Lfs = b->Lfs when d's left fill
+ * is b's right fill, cascading down a run of such links), so x is then
+ * tested with its fill starting at an upstream break's Lfs.  Those keys
+ * (the fill and the left fill; the suspect and the right fill keep theirs)
+ * for up to kSpecDepth removed predecessors, scored in the pass's batch
+ * instead of one call per removal (chainCleaner.c:1191-1398's update of the
+ * neighbours, 1452-1631's loop). */
+enum { kSpecDepth = 3 };
+
+static int spec_keys(const state *S, int32_t x, qkey *out) {
+    int n = 0;
+    const cbrk *cur = &g_brk[x];
+    const int32_t ik = ich_of(S, cur->chain_id);
+    if (ik < 0)
+        return 0;
+    const int32_t rfe = g_brk[x].Rfe, se = g_brk[x].se;
+    for (int32_t p = g_brk[x].prev, k = 0; p >= 0 && k < kSpecDepth; ++k) {
+        const cbrk *P = &g_brk[p];
+        if (!(P->chain_id == cur->chain_id && P->parent_id == cur->parent_id && cur->Lfs == P->Rfs &&
+              cur->Lfe == P->Rfe))
+            break;
+        out[n++] = make_key(S, ik, P->Lfs, rfe);
+        out[n++] = make_key(S, ik, P->Lfs, se);
+        cur = P;
+        p = P->prev;
+    }
+    return n;
+}
+
+/* keys of every break of a list (singles, with their speculative keys) and
+ * of its valid adjacent pairs */
 static void list_keys(const state *S, int32_t head, int pairs, int singles, qkey **q, int64_t *n,
                       int64_t *cap) {
     for (int32_t b = head; b >= 0; b = g_brk[b].next) {
-        if (*n + 8 > *cap) {
+        if (*n + 8 + 2 * kSpecDepth > *cap) {
             *cap = *cap ? *cap * 2 : 1024;
             *q = realloc(*q, (size_t)*cap * sizeof(qkey));
         }
-        if (singles)
+        if (singles) {
             *n += break_keys(S, &g_brk[b], *q + *n);
+            if (g_spec)
+                *n += spec_keys(S, b, *q + *n);
+        }
         const int32_t d = g_brk[b].next;
         if (pairs && d >= 0 && valid_pair(&g_brk[b], &g_brk[d])) {
             cbrk p = g_brk[b]; /* newBreakPair without the list / asserts */
@@ -1048,8 +1090,14 @@ static void loop_breaks(state *S, int32_t head) {
     for (;;) {
         for (;;) {
             ++total;
-            if (!first_pass)
+            /* (a list's first pass was batched with every list's before the
+             * loop; chains modified by the lists since then change keys: one
+             * call for those too) */
+            if (!first_pass) {
+                g_site = 1;
                 prefetch_list(S, head, 0, 1);
+                g_site = 2;
+            }
             first_pass = 0;
             int any_single = 0;
             for (int32_t b = head; b >= 0;) {
@@ -1074,7 +1122,9 @@ static void loop_breaks(state *S, int32_t head) {
         int any_pair = 0;
         if (doPairs) {
             ++total;
+            g_site = 1;
             prefetch_list(S, head, 1, 0);
+            g_site = 2;
             for (int32_t b = head; b >= 0 && g_brk[b].next >= 0;) {
                 const int32_t u = b, d = g_brk[b].next, after = g_brk[d].next,
                               before = g_brk[b].prev;
@@ -1219,6 +1269,13 @@ static void write_sorted(FILE *f, int64_t j, void *arg) {
 }
 
 int main(int argc, char *argv[]) {
+    {
+        const char *sv = getenv("GAC_CLEANER_SPEC");
+        g_spec = !(sv && *sv == '0');
+        const char *lv = getenv("GAC_CLEANER_LOOKAHEAD");
+        if (lv && atoi(lv) > 0)
+            g_lookahead = atoi(lv);
+    }
     gt_stage("");
     gt_options(&argc, argv, k_opts);
     if (argc != 6)
@@ -1498,12 +1555,27 @@ int main(int argc, char *argv[]) {
         int64_t nq = 0, capq = 0;
         for (int32_t oi = 0; oi < no; ++oi)
             list_keys(&S, bh_head[order[oi]], doPairs, 1, &q, &nq, &capq);
+        g_site = 0;
         score_keys(&S, q, nq);
-        free(q);
+        g_site = 2;
         gt_verbose(2, "scored %lld sub-chains of %lld breaks in one batch\n",
                    (long long)g_gpu_ranges, (long long)g_nbrk);
-        for (int32_t oi = no - 1; oi >= 0; --oi) /* hashElListHash: traversal reversed */
+        for (int32_t oi = no - 1; oi >= 0; --oi) { /* hashElListHash: traversal reversed */
+            /* the next lists' keys as the chains are now (the lists before
+             * them modified their breaking chains): one batch for
+             * g_lookahead lists; a key a later list changes is scored when
+             * it is met */
+            if (g_spec && (no - 1 - oi) % g_lookahead == 0) {
+                nq = 0;
+                for (int32_t oj = oi; oj >= 0 && oj > oi - g_lookahead; --oj)
+                    list_keys(&S, bh_head[order[oj]], 0, 1, &q, &nq, &capq);
+                g_site = 0;
+                score_keys(&S, q, nq);
+                g_site = 2;
+            }
             loop_breaks(&S, bh_head[order[oi]]);
+        }
+        free(q);
         free(order);
     }
     gt_careful_close(g_bed, out_bed);
@@ -1576,6 +1648,8 @@ int main(int argc, char *argv[]) {
                (long long)g_gpu_calls, (long long)g_gpu_ranges, (long long)g_uploads, g_gpu_s);
     gt_verbose(2, "GPU: modified chains handed over %lld times, %lld blocks\n",
                (long long)g_host_chains, (long long)g_host_blocks);
+    gt_verbose(2, "GPU: scoring calls by site: %lld list batches, %lld later passes, %lld tests\n",
+               (long long)g_calls_site[0], (long long)g_calls_site[1], (long long)g_calls_site[2]);
     gt_verbose(1, "\nALL DONE. New chains are in %s. Deleted suspects in %s\n", out_chain, out_bed);
     gac_chains_free(S.cs_base);
     gac_close(S.ctx);
