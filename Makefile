@@ -144,3 +144,14 @@ variant: $(HOST_OBJ)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/$(NAME)/libgachain.so \
 	    build/variants/$(NAME)/*.o $(HOST_OBJ) -Wl,-soname,libgachain.so
 .PHONY: variant
+
+# chainCleaner on the same stand-in (CPU profiling of its host loop)
+cpu-chaincleaner: oracle/_build/chainCleaner_cpu
+
+oracle/_build/chainCleaner_cpu: $(CSRC)/tools/chainCleaner.c $(CSRC)/host/gac_net.c \
+		$(CSRC)/host/gac_host.c oracle/cpu_gac_stub.c $(TOOL_LIB_SRC)
+	@mkdir -p oracle/_build
+	$(CC) -O2 -g -mpopcnt -std=gnu11 -Wall -ffp-contract=off -Iinclude -I$(CSRC) -I$(CSRC)/host -I$(CSRC)/tools/lib $^ \
+	    -o $@ -lz -lm -lpthread $(CPU_EXTRA)
+
+.PHONY: cpu-chaincleaner

@@ -567,9 +567,14 @@ static int64_t g_cslots = 0, g_cn = 0;
 static int64_t g_gpu_calls = 0, g_gpu_ranges = 0, g_uploads = 0;
 static int64_t g_host_chains = 0, g_host_blocks = 0; /* (modified chains' blocks handed over) */
 /* GAC_CLEANER_SPEC=0: no speculative keys, no prefetch at a list's first
- * pass (round 5's batching) */
+ * pass (round 5's batching); GAC_CLEANER_LOOKAHEAD=n: n lists per first-pass
+ * batch (C3, profiles/r06c3b: 1 list 3208 calls, 8 lists 3672, 32 lists
+ * 4141 -- keys of later lists go stale as the lists before them modify
+ * chains) */
 static int g_spec = 1;
-static int g_lookahead = 8;             /* lists whose keys one first-pass batch holds */
+static int g_lookahead = 1;             /* lists whose keys one first-pass batch holds */
+static int64_t g_miss[4][2];            /* test-time misses by key (S F L R) x (original, modified) */
+static double g_t_remove = 0, g_t_keys = 0; /* (timing: block removal, key making) */
 static int64_t g_calls_site[3];         /* scoring calls: list batches, later passes, tests */
 static int g_site = 2;
 static double g_gpu_s = 0; /* wall time inside the scoring calls */
@@ -636,11 +641,12 @@ static const sres *cache_get(qkey k) {
     return NULL;
 }
 
-static qkey make_key(const state *S, int32_t ix, int32_t s, int32_t e) {
+/* cur: the current subset of [s, e) when the caller has it, else NULL */
+static qkey make_key_cur(const state *S, int32_t ix, int32_t s, int32_t e, const subchain *pc) {
     const ichain *x = &S->ich[ix];
     int32_t ver = 0;
     if (x->version) {
-        const subchain cur = subset(S, ix, s, e);
+        const subchain cur = pc ? *pc : subset(S, ix, s, e);
         const int64_t ci = x->ci, b0 = S->c.blk_off[ci];
         const subchain org = subset_of(S->c.bt + b0, S->c.bq + b0, S->c.bs + b0,
                                        (int32_t)(S->c.blk_off[ci + 1] - b0), S->c.tstart[ci],
@@ -650,6 +656,10 @@ static qkey make_key(const state *S, int32_t ix, int32_t s, int32_t e) {
             ver = x->version;
     }
     return (qkey){ix, ver, s, e};
+}
+
+static qkey make_key(const state *S, int32_t ix, int32_t s, int32_t e) {
+    return make_key_cur(S, ix, s, e, NULL);
 }
 
 static int qkey_cmp(const void *a, const void *b) {
@@ -949,7 +959,16 @@ static int test_and_remove(state *S, cbrk *b, int32_t up, int32_t down, int *upd
         gt_abort("ERROR: broken chain %d has no block in its fill %d-%d (suspect %d-%d)\n",
                  b->chain_id, b->Lfs, b->Rfe, b->ss, b->se);
     qkey k[4];
-    break_keys(S, b, k);
+    const double tk0 = wall_s();
+    /* break_keys with the subsets just taken */
+    k[0] = make_key_cur(S, ib, b->ss, b->se, &sS);
+    k[1] = make_key_cur(S, ik, b->Lfs, b->Rfe, &sF);
+    k[2] = make_key_cur(S, ik, b->Lfs, b->se, &sL);
+    k[3] = make_key_cur(S, ik, b->ss, b->Rfe, &sR);
+    g_t_keys += wall_s() - tk0;
+    for (int j = 0; j < 4; ++j)
+        if (!cache_get(k[j]))
+            ++g_miss[j][k[j].version != 0];
     score_keys(S, k, 4);
     const sres rS = *cache_get(k[0]), rF = *cache_get(k[1]), rL = *cache_get(k[2]),
                rR = *cache_get(k[3]);
@@ -1038,7 +1057,9 @@ static int test_and_remove(state *S, cbrk *b, int32_t up, int32_t down, int *upd
         o.qstart = sS.qs;
         o.qend = sS.qe;
     }
+    const double tr0 = wall_s();
     remove_blocks(S, ib, b->ss, b->se);
+    g_t_remove += wall_s() - tr0;
     o.id = ++g_max_chain_id;
     if (g_dict)
         fprintf(g_dict, "%d\t%d\n", o.id, S->c.id[x->ci]);
@@ -1650,6 +1671,12 @@ int main(int argc, char *argv[]) {
                (long long)g_host_chains, (long long)g_host_blocks);
     gt_verbose(2, "GPU: scoring calls by site: %lld list batches, %lld later passes, %lld tests\n",
                (long long)g_calls_site[0], (long long)g_calls_site[1], (long long)g_calls_site[2]);
+    gt_verbose(2, "host: %.3f s removing suspects' blocks, %.3f s making tests' keys\n", g_t_remove,
+               g_t_keys);
+    gt_verbose(2, "GPU: keys a test missed (original / modified): suspect %lld/%lld fill %lld/%lld "
+               "left %lld/%lld right %lld/%lld\n", (long long)g_miss[0][0], (long long)g_miss[0][1],
+               (long long)g_miss[1][0], (long long)g_miss[1][1], (long long)g_miss[2][0],
+               (long long)g_miss[2][1], (long long)g_miss[3][0], (long long)g_miss[3][1]);
     gt_verbose(1, "\nALL DONE. New chains are in %s. Deleted suspects in %s\n", out_chain, out_bed);
     gac_chains_free(S.cs_base);
     gac_close(S.ctx);

@@ -44,7 +44,7 @@ def main():
                                + ["-verbose=2"], capture_output=True, text=True, env=env, timeout=300)
             dt = time.perf_counter() - t0
             assert x.returncode == 0, x.stderr[-2000:]
-            lines = [ln for ln in x.stderr.splitlines() if ln.startswith(("GPU:", "[stage] 4", "[stage] 1"))]
+            lines = [ln for ln in x.stderr.splitlines() if ln.startswith(("GPU:", "host:", "[stage] 4", "[stage] 1"))]
             same_ref = (filecmp.cmp(outs[0], ref[0], False) and filecmp.cmp(outs[1], ref[1], False)
                         if os.path.exists(ref[1]) else None)
             res["runs"].append({"spec": spec, "rep": r, "wall_s": dt, "identical_to_reference": same_ref,
