@@ -427,6 +427,10 @@ typedef struct ichain {
     int32_t nb;
     int32_t version;  /* bumped by every chainRemoveBlocks */
     int rescore;      /* in chainId2NeedsRescoring */
+    /* the blocks removed so far, ascending in t (disjoint: tEnd ascends too):
+     * a sub-chain has its original content unless one of them is in it */
+    int32_t *rm_s, *rm_e;
+    int32_t rm_n, rm_cap;
 } ichain;
 
 typedef struct state {
@@ -572,6 +576,7 @@ static int64_t g_host_chains = 0, g_host_blocks = 0; /* (modified chains' blocks
  * 4141 -- keys of later lists go stale as the lists before them modify
  * chains) */
 static int g_spec = 1;
+static int g_check_keys = 0;             /* GAC_CLEANER_CHECK_KEYS=1 (tests) */
 static int g_lookahead = 1;             /* lists whose keys one first-pass batch holds */
 static int64_t g_miss[4][2];            /* test-time misses by key (S F L R) x (original, modified) */
 static double g_t_remove = 0, g_t_keys = 0; /* (timing: block removal, key making) */
@@ -646,14 +651,46 @@ static qkey make_key_cur(const state *S, int32_t ix, int32_t s, int32_t e, const
     const ichain *x = &S->ich[ix];
     int32_t ver = 0;
     if (x->version) {
-        const subchain cur = pc ? *pc : subset(S, ix, s, e);
-        const int64_t ci = x->ci, b0 = S->c.blk_off[ci];
-        const subchain org = subset_of(S->c.bt + b0, S->c.bq + b0, S->c.bs + b0,
-                                       (int32_t)(S->c.blk_off[ci + 1] - b0), S->c.tstart[ci],
-                                       S->c.tend[ci], s, e);
-        /* the current selection is a subset of the original one */
-        if (cur.easy || cur.nb != org.nb)
+        const int64_t ci = x->ci;
+        /* a whole-chain selection (chainSubsetOnT's easy case, the original
+         * bounds) follows every version; else the current selection -- a
+         * subset of the original one (blocks only ever go) -- differs from
+         * it iff a removed block is in [s, e): tEnd > s and tStart < e */
+        if (s <= S->c.tstart[ci] && e >= S->c.tend[ci]) {
             ver = x->version;
+        } else {
+            int32_t lo = 0, hi = x->rm_n; /* first removed block with tEnd > s */
+            while (lo < hi) {
+                const int32_t m = (lo + hi) >> 1;
+                if (x->rm_e[m] > s)
+                    hi = m;
+                else
+                    lo = m + 1;
+            }
+            if (lo < x->rm_n && x->rm_s[lo] < e)
+                ver = x->version;
+        }
+        if (g_check_keys) { /* (test hook: the rule as counts of the two selections) */
+            const subchain cur = pc ? *pc : subset(S, ix, s, e);
+            const int64_t b0 = S->c.blk_off[ci];
+            const subchain org = subset_of(S->c.bt + b0, S->c.bq + b0, S->c.bs + b0,
+                                           (int32_t)(S->c.blk_off[ci + 1] - b0), S->c.tstart[ci],
+                                           S->c.tend[ci], s, e);
+            if ((cur.easy || cur.nb != org.nb) != (ver != 0)) {
+                for (int32_t k = 0; k < x->rm_n; ++k)
+                    if (x->rm_e[k] > s - 1000 && x->rm_s[k] < e + 1000)
+                        fprintf(stderr, "removed[%d] = [%d, %d)\n", k, x->rm_s[k], x->rm_e[k]);
+                for (int32_t k = 0; k < org.nb; ++k)
+                    fprintf(stderr, "org block %d: [%d, %d)\n", org.b0 + k, S->c.bt[b0 + org.b0 + k],
+                            S->c.bt[b0 + org.b0 + k] + S->c.bs[b0 + org.b0 + k]);
+                fprintf(stderr, "rm_n %d sorted check:", x->rm_n);
+                for (int32_t k = 1; k < x->rm_n; ++k)
+                    if (x->rm_s[k] < x->rm_e[k - 1]) fprintf(stderr, " bad@%d [%d,%d) [%d,%d)", k, x->rm_s[k-1], x->rm_e[k-1], x->rm_s[k], x->rm_e[k]);
+                fprintf(stderr, "\n");
+                gt_abort("key version rule: chain %d [%d, %d): counts %d/%d, easy %d, version %d\n",
+                         (int)S->c.id[ci], s, e, cur.nb, org.nb, cur.easy, ver);
+            }
+        }
     }
     return (qkey){ix, ver, s, e};
 }
@@ -924,6 +961,28 @@ static void remove_blocks(state *S, int32_t ix, int32_t ts, int32_t te) {
      * (tested non-empty before) rule that out */
     must_assert(last > first + 1, "chainRemoveBlocks: blocks between the boundaries");
     const int32_t gone = last - first - 1, tail = x->nb - last;
+    /* the removed run into the sorted removed list */
+    if (x->rm_n + gone > x->rm_cap) {
+        x->rm_cap = 2 * (x->rm_n + gone) + 16;
+        x->rm_s = realloc(x->rm_s, (size_t)x->rm_cap * 4);
+        x->rm_e = realloc(x->rm_e, (size_t)x->rm_cap * 4);
+    }
+    {
+        /* merged from the back (the run may straddle blocks removed before:
+         * they lay between its blocks in the chain) */
+        int32_t i = x->rm_n - 1, j = gone - 1, o = x->rm_n + gone - 1;
+        while (j >= 0) {
+            const int32_t js = x->bt[first + 1 + j];
+            if (i >= 0 && x->rm_s[i] > js) {
+                x->rm_s[o] = x->rm_s[i];
+                x->rm_e[o--] = x->rm_e[i--];
+            } else {
+                x->rm_s[o] = js;
+                x->rm_e[o--] = js + x->bs[first + 1 + j--];
+            }
+        }
+        x->rm_n += gone;
+    }
     memmove(x->bt + first + 1, x->bt + last, (size_t)tail * 4);
     memmove(x->bq + first + 1, x->bq + last, (size_t)tail * 4);
     memmove(x->bs + first + 1, x->bs + last, (size_t)tail * 4);
@@ -1293,6 +1352,8 @@ int main(int argc, char *argv[]) {
     {
         const char *sv = getenv("GAC_CLEANER_SPEC");
         g_spec = !(sv && *sv == '0');
+        const char *ck = getenv("GAC_CLEANER_CHECK_KEYS");
+        g_check_keys = ck && *ck == '1';
         const char *lv = getenv("GAC_CLEANER_LOOKAHEAD");
         if (lv && atoi(lv) > 0)
             g_lookahead = atoi(lv);
