@@ -1491,40 +1491,34 @@ struct DevBufs {
 };
 }  // namespace
 
-// chainBlocks' DP for n_pairs pairs from their blocks: the leaves, kd-trees,
-// update paths and overlap lists built on the device (gac_dptree.hip), then
-// k_dp_fast (fast) or k_dp; see include/gachain.h
-extern "C" int gac_chain_dp_blocks(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq,
-                                   const int32_t *q_seq, const uint8_t *q_strand,
-                                   const int64_t *blk_off, const int32_t *box, const int32_t *score,
-                                   int fast, int64_t lin_k, int32_t min_entry, int32_t ov_cap,
-                                   int64_t *leaf_off, int32_t *tord, int64_t *total, int32_t *pred) {
-    gac_clear_error();
-    if (!c || n_pairs < 0 || (n_pairs && (!t_seq || !q_seq || !q_strand || !blk_off || !leaf_off)))
-        return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: bad argument");
-    if (!c->scoring) return gac_fail(GAC_E_STATE, "gac_chain_dp_blocks before gac_set_scoring");
-    CTX_LOCK(c);
-    if (!c->g[0].final || !c->g[1].final)
-        return gac_fail(GAC_E_STATE, "load both genomes before gac_chain_dp_blocks");
-    if (n_pairs == 0) return GAC_OK;
-    if (n_pairs >= (1LL << 30)) return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: too many pairs");
-    const int64_t P = n_pairs, B = blk_off[P];
-    if (blk_off[0] != 0 || B < 0 || B > 0x7fffffffLL)
-        return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: bad block offsets");
-    for (int64_t p = 0; p < P; ++p)
-        if (blk_off[p + 1] < blk_off[p])
-            return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: pair %lld: block offsets descend",
-                            (long long)p);
-    if (B && (!box || !score || !tord || !total || !pred))
-        return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: NULL array");
-    if (fast && lin_k < 0) return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: bad lin_k");
-    if (B == 0) {
-        for (int64_t p = 0; p <= P; ++p) leaf_off[p] = 0;
-        return GAC_OK;
-    }
+// the device build's set-up shared by gac_chain_dp_blocks and gac_kd_trees:
+// uploads, leaves in target order and leaf offsets (leaf_off, host), node
+// offsets, every array of the build; u.t.L == 0: no leaves (nothing else set)
+namespace {
+struct DtSetup {
+    DtTree t;
+    std::vector<DpPair> pairs;
+    std::vector<int64_t> node_off;
+    int levels = 0;
+    int64_t *d_leaf_off = nullptr;
+    int32_t *d_err = nullptr;
+    long long *d_total = nullptr, *d_lf_total = nullptr;
+    int32_t *d_pred = nullptr, *d_lf_pred = nullptr, *d_out_tord = nullptr;
+    DpPair *d_pairs = nullptr;
+    double t0 = 0, t1 = 0;
+};
+}  // namespace
+
+static int dt_setup(gac_ctx *c, const char *who, int64_t P, const int32_t *t_seq,
+                    const int32_t *q_seq, const uint8_t *q_strand, const int64_t *blk_off,
+                    const int32_t *box, const int32_t *score, int fast, int32_t ov_cap,
+                    int64_t *leaf_off, DevBufs &M, DtSetup &u) {
+    const int64_t B = blk_off[P];
+    u.t0 = wall_s();
     const bool timing = getenv("GAC_TIMING") != nullptr;
-    const double t0 = wall_s();
-    std::vector<DpPair> pairs(P);
+    (void)timing;
+    std::vector<DpPair> &pairs = u.pairs;
+    pairs.resize(P);
     std::vector<int2> sizes(P);
     for (int64_t p = 0; p < P; ++p) {
         int rc = pair_bases(c, t_seq[p], q_seq[p], q_strand[p], pairs[p].tbase, pairs[p].qbase);
@@ -1533,8 +1527,7 @@ extern "C" int gac_chain_dp_blocks(gac_ctx *c, int64_t n_pairs, const int32_t *t
     }
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
-    DevBufs M;
-    DtTree t;
+    DtTree &t = u.t;
     memset(&t, 0, sizeof(t));
     t.P = P;
     t.B = B;
@@ -1549,15 +1542,15 @@ extern "C" int gac_chain_dp_blocks(gac_ctx *c, int64_t n_pairs, const int32_t *t
     int32_t *d_score = M.take<int32_t>(B);
     unsigned long long *d_keys = M.take<unsigned long long>(2 * B);
     int32_t *d_vals = M.take<int32_t>(2 * B);
-    int64_t *d_leaf_off = M.take<int64_t>(P + 1);
-    int32_t *d_err = M.take<int32_t>(1);
+    int64_t *d_leaf_off = u.d_leaf_off = M.take<int64_t>(P + 1);
+    int32_t *d_err = u.d_err = M.take<int32_t>(1);
     t.tpos = M.take<int32_t>(B);
     t.qpos = M.take<int32_t>(B);
     t.posd = M.take<int32_t>(B);
-    long long *d_total = M.take<long long>(B);
-    int32_t *d_pred = M.take<int32_t>(B);
+    u.d_total = M.take<long long>(B);
+    u.d_pred = M.take<int32_t>(B);
     if (M.e != hipSuccess)
-        return gac_fail(GAC_E_HIP, "gac_chain_dp_blocks: hipMalloc: %s", hipGetErrorString(M.e));
+        return gac_fail(GAC_E_HIP, "%s: hipMalloc: %s", who, hipGetErrorString(M.e));
     size_t b_sort = 0;
     HIPCHK(dt_sort_pairs(nullptr, b_sort, d_keys, d_keys + B, d_vals, d_vals + B, B, t.end_bit, s));
     void *d_tmp = M.take<uint8_t>((int64_t)b_sort);
@@ -1565,7 +1558,10 @@ extern "C" int gac_chain_dp_blocks(gac_ctx *c, int64_t n_pairs, const int32_t *t
     HIPCHK(hipMemcpyAsync(d_blk_off, blk_off, (P + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(d_sizes, sizes.data(), P * sizeof(int2), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(d_box, box, B * sizeof(int4), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(d_score, score, B * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    if (score)
+        HIPCHK(hipMemcpyAsync(d_score, score, B * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    else
+        HIPCHK(hipMemsetAsync(d_score, 0, B * sizeof(int32_t), s));
     HIPCHK(hipMemsetAsync(d_err, 0, sizeof(int32_t), s));
     // ---- leaves in target order, per-pair leaf offsets
     HIPCHK(launch_dt_keys(P, B, d_blk_off, d_sizes, d_box, d_keys, d_vals, d_err, s));
@@ -1576,27 +1572,24 @@ extern "C" int gac_chain_dp_blocks(gac_ctx *c, int64_t n_pairs, const int32_t *t
     HIPCHK(hipMemcpyAsync(&h_err, d_err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     const double t1 = wall_s();
+    (void)t1;
     if (h_err & 1) {  // the first bad block, as a serial check reports it
         for (int64_t p = 0; p < P; ++p)
             for (int64_t g = blk_off[p]; g < blk_off[p + 1]; ++g) {
                 const int32_t *b = box + 4 * g;
                 if (b[0] < 0 || b[0] > b[1] || b[1] > sizes[p].y || b[2] < 0 || b[2] > b[3] ||
                     b[3] > sizes[p].x)
-                    return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: pair %lld block %lld (%d-%d, %d-%d) "
-                                    "outside its sequences", (long long)p, (long long)(g - blk_off[p]),
+                    return gac_fail(GAC_E_ARG, "%s: pair %lld block %lld (%d-%d, %d-%d) "
+                                    "outside its sequences", who, (long long)p, (long long)(g - blk_off[p]),
                                     b[0], b[1], b[2], b[3]);
             }
-        return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: a block outside its sequences");
+        return gac_fail(GAC_E_ARG, "%s: a block outside its sequences", who);
     }
     const int64_t L = leaf_off[P];
-    if (L == 0) {
-        for (int64_t g = 0; g < B; ++g) {
-            total[g] = score[g];
-            pred[g] = -1;
-        }
-        return GAC_OK;
-    }
-    std::vector<int64_t> node_off(P + 1);
+    u.t1 = t1;
+    if (L == 0) return GAC_OK;
+    std::vector<int64_t> &node_off = u.node_off;
+    node_off.resize(P + 1);
     int64_t maxnl = 0;
     node_off[0] = 0;
     for (int64_t p = 0; p < P; ++p) {
@@ -1609,7 +1602,8 @@ extern "C" int gac_chain_dp_blocks(gac_ctx *c, int64_t n_pairs, const int32_t *t
         pairs[p].n_leaves = (int32_t)nl;
     }
     const int64_t N = node_off[P];
-    int levels = 0;
+    int &levels = u.levels;
+    levels = 0;
     for (int64_t n = maxnl; n > 1; n -= n / 2) ++levels;
     t.L = L;
     t.N = N;
@@ -1651,12 +1645,12 @@ extern "C" int gac_chain_dp_blocks(gac_ctx *c, int64_t n_pairs, const int32_t *t
     t.lnode = M.take<int32_t>(L);
     t.poff = M.take<long long>(L + 1);
     t.ooff = M.take<long long>(L + 1);
-    long long *d_lf_total = M.take<long long>(L);
-    int32_t *d_lf_pred = M.take<int32_t>(L);
-    int32_t *d_out_tord = M.take<int32_t>(L);
-    DpPair *d_pairs = M.take<DpPair>(P);
+    u.d_lf_total = M.take<long long>(L);
+    u.d_lf_pred = M.take<int32_t>(L);
+    u.d_out_tord = M.take<int32_t>(L);
+    DpPair *d_pairs = u.d_pairs = M.take<DpPair>(P);
     if (M.e != hipSuccess)
-        return gac_fail(GAC_E_HIP, "gac_chain_dp_blocks: hipMalloc: %s", hipGetErrorString(M.e));
+        return gac_fail(GAC_E_HIP, "%s: hipMalloc: %s", who, hipGetErrorString(M.e));
     size_t need = b_sort, b = 0;
     HIPCHK(dt_sort_pairs(nullptr, b, t.key2, t.key2 + L, t.val2, t.val2 + L, L, t.end_bit, s));
     need = std::max(need, b);
@@ -1672,6 +1666,65 @@ extern "C" int gac_chain_dp_blocks(gac_ctx *c, int64_t n_pairs, const int32_t *t
     HIPCHK(hipMemcpyAsync(d_pairs, pairs.data(), P * sizeof(DpPair), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(t.pcnt, 0, (L + 1) * sizeof(long long), s));
     HIPCHK(hipMemsetAsync(t.ocnt, 0, (L + 1) * sizeof(long long), s));
+    return GAC_OK;
+}
+
+// chainBlocks' DP for n_pairs pairs from their blocks: the leaves, kd-trees,
+// update paths and overlap lists built on the device (gac_dptree.hip), then
+// k_dp_fast (fast) or k_dp; see include/gachain.h
+extern "C" int gac_chain_dp_blocks(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq,
+                                   const int32_t *q_seq, const uint8_t *q_strand,
+                                   const int64_t *blk_off, const int32_t *box, const int32_t *score,
+                                   int fast, int64_t lin_k, int32_t min_entry, int32_t ov_cap,
+                                   int64_t *leaf_off, int32_t *tord, int64_t *total, int32_t *pred) {
+    gac_clear_error();
+    if (!c || n_pairs < 0 || (n_pairs && (!t_seq || !q_seq || !q_strand || !blk_off || !leaf_off)))
+        return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: bad argument");
+    if (!c->scoring) return gac_fail(GAC_E_STATE, "gac_chain_dp_blocks before gac_set_scoring");
+    CTX_LOCK(c);
+    if (!c->g[0].final || !c->g[1].final)
+        return gac_fail(GAC_E_STATE, "load both genomes before gac_chain_dp_blocks");
+    if (n_pairs == 0) return GAC_OK;
+    if (n_pairs >= (1LL << 30)) return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: too many pairs");
+    const int64_t P = n_pairs, B = blk_off[P];
+    if (blk_off[0] != 0 || B < 0 || B > 0x7fffffffLL)
+        return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: bad block offsets");
+    for (int64_t p = 0; p < P; ++p)
+        if (blk_off[p + 1] < blk_off[p])
+            return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: pair %lld: block offsets descend",
+                            (long long)p);
+    if (B && (!box || !score || !tord || !total || !pred))
+        return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: NULL array");
+    if (fast && lin_k < 0) return gac_fail(GAC_E_ARG, "gac_chain_dp_blocks: bad lin_k");
+    if (B == 0) {
+        for (int64_t p = 0; p <= P; ++p) leaf_off[p] = 0;
+        return GAC_OK;
+    }
+    const bool timing = getenv("GAC_TIMING") != nullptr;
+    DevBufs M;
+    DtSetup u;
+    int rc0 = dt_setup(c, "gac_chain_dp_blocks", P, t_seq, q_seq, q_strand, blk_off, box, score, fast,
+                       ov_cap, leaf_off, M, u);
+    if (rc0 != GAC_OK) return rc0;
+    const double t0 = u.t0, t1 = u.t1;
+    if (u.t.L == 0) {
+        for (int64_t g = 0; g < B; ++g) {
+            total[g] = score[g];
+            pred[g] = -1;
+        }
+        return GAC_OK;
+    }
+    DtTree &t = u.t;
+    hipStream_t s = c->stream;
+    const int64_t L = t.L;
+    const int levels = u.levels;
+    int32_t *d_err = u.d_err;
+    long long *d_total = u.d_total, *d_lf_total = u.d_lf_total;
+    int32_t *d_pred = u.d_pred, *d_lf_pred = u.d_lf_pred, *d_out_tord = u.d_out_tord;
+    DpPair *d_pairs = u.d_pairs;
+    int64_t *d_leaf_off = u.d_leaf_off;
+    const int64_t N = t.N;
+    int32_t h_err = 0;
     // ---- query order, the trees, path and overlap counts
     HIPCHK(launch_dt_tree(t, levels, s));
     long long n_path = 0, n_ov = 0;
@@ -1769,6 +1822,80 @@ extern "C" int gac_chain_dp_blocks(gac_ctx *c, int64_t n_pairs, const int32_t *t
                 "%s %.3f s, results %.3f s\n",
                 (long long)P, (long long)B, (long long)L, levels, n_path, n_ov, t1 - t0, t2 - t1,
                 !fast ? "k_dp" : (dp_waves() > 1 ? "k_dp_spec" : "k_dp_fast"), t3 - t2, wall_s() - t3);
+    return GAC_OK;
+}
+
+// kdTreeMake for n_pairs pairs on the device (gac_dptree.hip's build), out
+// in the host DP's layout, per pair into the caller's buffers; see
+// include/gachain.h
+extern "C" int gac_kd_trees(gac_ctx *c, int64_t n_pairs, const int32_t *t_seq, const int32_t *q_seq,
+                            const uint8_t *q_strand, const int64_t *blk_off, const int32_t *box,
+                            int64_t *leaf_off, int32_t *const *tord, int32_t *const *qord,
+                            int32_t *const *lnode, int32_t *const *nodes) {
+    gac_clear_error();
+    if (!c || n_pairs < 0 || (n_pairs && (!t_seq || !q_seq || !q_strand || !blk_off || !leaf_off)))
+        return gac_fail(GAC_E_ARG, "gac_kd_trees: bad argument");
+    CTX_LOCK(c);
+    if (!c->g[0].final || !c->g[1].final)
+        return gac_fail(GAC_E_STATE, "load both genomes before gac_kd_trees");
+    if (n_pairs == 0) return GAC_OK;
+    if (n_pairs >= (1LL << 30)) return gac_fail(GAC_E_ARG, "gac_kd_trees: too many pairs");
+    const int64_t P = n_pairs, B = blk_off[P];
+    if (blk_off[0] != 0 || B < 0 || B > 0x7fffffffLL)
+        return gac_fail(GAC_E_ARG, "gac_kd_trees: bad block offsets");
+    for (int64_t p = 0; p < P; ++p)
+        if (blk_off[p + 1] < blk_off[p])
+            return gac_fail(GAC_E_ARG, "gac_kd_trees: pair %lld: block offsets descend", (long long)p);
+    if (B && (!box || !tord || !qord || !lnode || !nodes))
+        return gac_fail(GAC_E_ARG, "gac_kd_trees: NULL array");
+    if (B == 0) {
+        for (int64_t p = 0; p <= P; ++p) leaf_off[p] = 0;
+        return GAC_OK;
+    }
+    const double t0 = wall_s();
+    DevBufs M;
+    DtSetup u;
+    int rc = dt_setup(c, "gac_kd_trees", P, t_seq, q_seq, q_strand, blk_off, box, nullptr, 0, 0,
+                      leaf_off, M, u);
+    if (rc != GAC_OK) return rc;
+    hipStream_t s = c->stream;
+    DtTree &t = u.t;
+    if (t.L == 0) {
+        for (int64_t p = 0; p < P; ++p)
+            for (int64_t g = 0; g < blk_off[p + 1] - blk_off[p]; ++g) lnode[p][g] = -1;
+        return GAC_OK;
+    }
+    int32_t *d_nodes = M.take<int32_t>(6 * t.N);
+    int32_t *d_qord = M.take<int32_t>(t.L);
+    int32_t *d_lnode_blk = M.take<int32_t>(B);
+    if (M.e != hipSuccess)
+        return gac_fail(GAC_E_HIP, "gac_kd_trees: hipMalloc: %s", hipGetErrorString(M.e));
+    HIPCHK(launch_dt_build(t, u.levels, s));
+    HIPCHK(launch_dt_host(t, d_nodes, u.d_out_tord, d_qord, d_lnode_blk, s));
+    int32_t h_err = 0;
+    HIPCHK(hipMemcpyAsync(&h_err, u.d_err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (h_err) return gac_fail(GAC_E_HIP, "gac_kd_trees: device tree build failed (%d)", h_err);
+    const double t1 = wall_s();
+    for (int64_t p = 0; p < P; ++p) {
+        const int64_t nl = leaf_off[p + 1] - leaf_off[p], nb = blk_off[p + 1] - blk_off[p];
+        if (nl) {
+            HIPCHK(hipMemcpyAsync(tord[p], u.d_out_tord + leaf_off[p], nl * sizeof(int32_t),
+                                  hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(qord[p], d_qord + leaf_off[p], nl * sizeof(int32_t),
+                                  hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(nodes[p], d_nodes + 6 * u.node_off[p],
+                                  (2 * nl - 1) * 6 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        }
+        if (nb)
+            HIPCHK(hipMemcpyAsync(lnode[p], d_lnode_blk + blk_off[p], nb * sizeof(int32_t),
+                                  hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    if (getenv("GAC_TIMING"))
+        fprintf(stderr, "[gac_kd_trees] %lld pairs, %lld blocks, %lld leaves, %d levels: build %.3f s, "
+                        "results %.3f s\n", (long long)P, (long long)B, (long long)t.L, u.levels,
+                t1 - t0, wall_s() - t1);
     return GAC_OK;
 }
 

@@ -140,9 +140,16 @@ hipError_t launch_dt_keys(int64_t P, int64_t B, const int64_t *blk_off, const in
                           hipStream_t s);
 hipError_t launch_dt_leaf_off(int64_t P, int64_t B, const unsigned long long *keys,
                               int64_t *leaf_off, hipStream_t s);
-// leaves in query order, the tree (levels = splits of the largest pair),
-// path counts and offsets, overlap counts and offsets (t.fast)
+// leaves in query order and the tree (levels = splits of the largest pair)
+hipError_t launch_dt_build(const DtTree &t, int levels, hipStream_t s);
+// launch_dt_build, then path counts and offsets, overlap counts and offsets
+// (t.fast)
 hipError_t launch_dt_tree(const DtTree &t, int levels, hipStream_t s);
+// the built trees in the host DP's layout (6 int32 per node: lo, hi, leaf,
+// cut, maxQ, maxT), the target / query orders of the leaves as pair-local
+// blocks, each block's leaf node (-1: none)
+hipError_t launch_dt_host(const DtTree &t, int32_t *nodes, int32_t *out_t, int32_t *out_q,
+                          int32_t *out_lnode, hipStream_t s);
 // the paths and overlap lists into arrays of poff[L] / ooff[L] entries
 hipError_t launch_dt_lists(const DtTree &t, int32_t *path, int32_t *ov, hipStream_t s);
 // per packed block: totalScore, best predecessor (a block of its pair, or

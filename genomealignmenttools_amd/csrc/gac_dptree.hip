@@ -372,6 +372,50 @@ __global__ void __launch_bounds__(kDtThreads)
     pred[g] = (int32_t)(tord[leaf_off[p] + ~pl] - b0);
 }
 
+// the tree in the host's node layout (host/gac_axtchain.c ax_node: lo, hi,
+// leaf, cut, maxQ, maxT; a leaf node: qStart, tStart, its block, 0, qEnd,
+// tEnd), node ids and blocks local to the pair
+__global__ void __launch_bounds__(kDtThreads)
+    k_dt_host_nodes(int64_t P, int64_t N, const int64_t *node_off, const int64_t *leaf_off,
+                    const int64_t *blk_off, const int32_t *tord, const int4 *na, const int2 *nb,
+                    const int32_t *ndep, int32_t *out) {
+    const int64_t v = dt_id();
+    if (v >= N) return;
+    const int64_t p = dt_pair_of(node_off, P, v);
+    const int32_t vl = (int32_t)(v - node_off[p]);
+    const int4 a = na[v];
+    const int2 b = nb[v];
+    int32_t *o = out + 6 * v;
+    if (ndep[v] >= 0) {
+        o[0] = a.w;
+        o[1] = vl + 1;
+        o[2] = -1;
+        o[3] = a.z;
+    } else {
+        o[0] = a.z;
+        o[1] = a.w;
+        o[2] = (int32_t)(tord[leaf_off[p] + ~b.y] - blk_off[p]);
+        o[3] = 0;
+    }
+    o[4] = a.x;
+    o[5] = a.y;
+}
+
+// per leaf position: the target and query orders as pair-local blocks; per
+// block: its leaf node (-1: not a leaf)
+__global__ void __launch_bounds__(kDtThreads)
+    k_dt_host_lists(int64_t L, const int32_t *pidx, const int64_t *blk_off, const int32_t *tord,
+                    const int32_t *qord, const int32_t *lnode, int32_t *out_t, int32_t *out_q,
+                    int32_t *out_lnode) {
+    const int64_t i = dt_id();
+    if (i >= L) return;
+    const int64_t b0 = blk_off[pidx[i]];
+    const int32_t g = tord[i];
+    out_t[i] = (int32_t)(g - b0);
+    out_q[i] = (int32_t)(qord[i] - b0);
+    out_lnode[g] = lnode[i];
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ launchers
@@ -407,7 +451,7 @@ hipError_t launch_dt_leaf_off(int64_t P, int64_t B, const unsigned long long *ke
     return hipGetLastError();
 }
 
-hipError_t launch_dt_tree(const DtTree &t, int levels, hipStream_t s) {
+hipError_t launch_dt_build(const DtTree &t, int levels, hipStream_t s) {
     const int64_t L = t.L, N = t.N;
     if (L == 0) return hipSuccess;
     const dim3 gl = dt_grid(L), bl(kDtThreads);
@@ -448,6 +492,15 @@ hipError_t launch_dt_tree(const DtTree &t, int levels, hipStream_t s) {
                        t.tot, t.err);
     for (int d = levels - 1; d >= 0; --d)
         hipLaunchKernelGGL(k_dt_max, dt_grid(N), bl, 0, s, N, d, t.ndep, t.ndl, t.na);
+    return hipGetLastError();
+}
+
+hipError_t launch_dt_tree(const DtTree &t, int levels, hipStream_t s) {
+    hipError_t e = launch_dt_build(t, levels, s);
+    const int64_t L = t.L;
+    if (e != hipSuccess || L == 0) return e;
+    const dim3 gl = dt_grid(L), bl(kDtThreads);
+    size_t b;
     hipLaunchKernelGGL(k_dt_path, gl, bl, 0, s, L, 0, t.lf, t.pidx, t.node_off, t.na, t.nb,
                        t.pcnt, nullptr, nullptr, t.err);
     b = t.tmp_bytes;
@@ -486,6 +539,18 @@ hipError_t launch_dt_out(const DtTree &t, const long long *lf_total, const int32
         hipLaunchKernelGGL(k_dt_out, dt_grid(t.L), dim3(kDtThreads), 0, s, t.L, t.tord, t.pidx,
                            t.blk_off, t.leaf_off, t.node_off, t.nb, lf_total, lf_pred, out_tord,
                            total, pred, t.err);
+    return hipGetLastError();
+}
+
+hipError_t launch_dt_host(const DtTree &t, int32_t *nodes, int32_t *out_t, int32_t *out_q,
+                          int32_t *out_lnode, hipStream_t s) {
+    if (t.B) hipMemsetAsync(out_lnode, 0xff, t.B * sizeof(int32_t), s);
+    if (t.N)
+        hipLaunchKernelGGL(k_dt_host_nodes, dt_grid(t.N), dim3(kDtThreads), 0, s, t.P, t.N,
+                           t.node_off, t.leaf_off, t.blk_off, t.tord, t.na, t.nb, t.ndep, nodes);
+    if (t.L)
+        hipLaunchKernelGGL(k_dt_host_lists, dt_grid(t.L), dim3(kDtThreads), 0, s, t.L, t.pidx,
+                           t.blk_off, t.tord, t.val2 + t.L, t.lnode, out_t, out_q, out_lnode);
     return hipGetLastError();
 }
 

@@ -141,6 +141,14 @@ typedef struct ax_out { /* one pair's result */
     double secs; /* wall time of this pair's chaining */
 } ax_out;
 
+/* a pair's leaves and kd-tree built on the device (gac_kd_trees) for the
+ * host DP: the arrays are adopted by the pair's ax_work */
+typedef struct ax_pre {
+    int32_t nl;
+    int32_t *tord, *qord, *lnode; /* [n] */
+    int32_t *nodes;               /* [2 n][6]: ax_node */
+} ax_pre;
+
 typedef struct ax_work {
     const ax_env *e;
     ax_seq q, t;
@@ -166,6 +174,7 @@ typedef struct ax_work {
     long long fallbacks;
     int team, team_batch; /* > 1: this pair's DP on that many threads (pair_dp_team) */
     int pred_blk;         /* pred holds blocks, not nodes (gac_chain_dp_blocks' results) */
+    ax_pre *pre;          /* this pair's leaves and tree, built on the device (or NULL) */
     /* crossover scratch */
     uint8_t *xs;
     int32_t xcap;
@@ -2114,6 +2123,20 @@ static void pair_finish_team(ax_work *w, ax_chains *pc, ax_out *out) {
     pc->cblk = pc->cstart = NULL;
 }
 
+/* pair_leaves + pair_tree from the device's build (gac_kd_trees; the arrays
+ * were adopted by run_pair): the totals and the bounds to start from */
+static int32_t pair_prebuilt(ax_work *w) {
+    w->nl = w->pre->nl;
+    for (int32_t i = 0; i < w->n; ++i) {
+        w->total[i] = w->score[i];
+        w->pred[i] = -1;
+    }
+    w->nn = w->nl ? 2 * w->nl - 1 : 0;
+    for (int32_t v = 0; v < w->nn; ++v)
+        w->bnd[v] = (ax_bound){0.0, INT64_MIN / 4};
+    return w->nl;
+}
+
 static double mono_s(void) {
     struct timespec t;
     clock_gettime(CLOCK_MONOTONIC, &t);
@@ -2125,12 +2148,13 @@ static void chain_pair(ax_work *w, const ax_pairinfo *pi, FILE *details, ax_out 
     /* GAC_TIMING: the phases of pairs of over a million blocks */
     const int tm = w->n > (1 << 20) && getenv("GAC_TIMING");
     double t0 = tm ? mono_s() : 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
-    if (pair_leaves(w) == 0) {
+    if ((w->pre ? pair_prebuilt(w) : pair_leaves(w)) == 0) {
         out->coff = calloc(1, sizeof(int32_t));
         return;
     }
     if (tm) t1 = mono_s();
-    pair_tree(w);
+    if (!w->pre)
+        pair_tree(w);
     if (tm) t2 = mono_s();
     pair_dp_host(w);
     if (w->err)
@@ -2313,6 +2337,17 @@ static void run_pair(ax_job *J, ax_work *w, int32_t p) {
     w->te = J->te + b0;
     w->score = J->score + b0;
     work_reserve(w, n);
+    if (w->pre) { /* the device's leaves and tree become this pair's arrays */
+        free(w->tord);
+        free(w->qord);
+        free(w->lnode);
+        free(w->nodes);
+        w->tord = w->pre->tord;
+        w->qord = w->pre->qord;
+        w->lnode = w->pre->lnode;
+        w->nodes = (ax_node *)w->pre->nodes;
+        w->cap_n = 0; /* (not reusable at work_reserve's sizes) */
+    }
     char *dbuf = NULL;
     size_t dlen = 0;
     FILE *df = J->want_details ? open_memstream(&dbuf, &dlen) : NULL;
@@ -2353,6 +2388,7 @@ static void work_free(ax_work *w) {
 typedef struct team_run {
     ax_job *J;
     const ax_env *env;
+    ax_pre *pre; /* the pair's leaves and tree built on the device, or NULL */
     int32_t p;
     int team, batch, started, pin;
     cpu_set_t cpus; /* (pin) the L3 domain the team runs in */
@@ -2422,6 +2458,7 @@ static void *team_runner(void *arg) {
     w.e = R->env;
     w.team = R->team;
     w.team_batch = R->batch;
+    w.pre = R->pre;
     run_pair(R->J, &w, R->p);
     work_free(&w);
     return NULL;
@@ -3089,6 +3126,97 @@ static int64_t dp_device_split(const int64_t *psize, const int32_t *order, int64
     return kd;
 }
 
+/* gac_kd_trees for the team pairs order[0 .. big): their blocks packed on
+ * nt threads, each pair's arrays allocated here and adopted by its team
+ * (run_pair); NULL (and *rc) when the device build fails */
+typedef struct tt_pack {
+    const ax_job *J;
+    const int32_t *order;
+    const int64_t *boff; /* [big + 1] */
+    int32_t *box;
+    int64_t big;
+    _Atomic int64_t next; /* slices of 1 M packed blocks */
+} tt_pack;
+
+static void *tt_pack_thread(void *arg) {
+    tt_pack *T = arg;
+    const int64_t nb = T->boff[T->big];
+    for (;;) {
+        const int64_t c0 = atomic_fetch_add(&T->next, 1) << 20;
+        if (c0 >= nb)
+            return NULL;
+        const int64_t c1 = c0 + (1 << 20) < nb ? c0 + (1 << 20) : nb;
+        int64_t k = 0;
+        while (T->boff[k + 1] <= c0)
+            ++k;
+        for (int64_t g = c0; g < c1; ++g) {
+            while (T->boff[k + 1] <= g)
+                ++k;
+            const int64_t b = T->J->poff[T->order[k]] + (g - T->boff[k]);
+            int32_t *x = T->box + 4 * g;
+            x[0] = T->J->qs[b];
+            x[1] = T->J->qe[b];
+            x[2] = T->J->ts[b];
+            x[3] = T->J->te[b];
+        }
+    }
+}
+
+static ax_pre *team_trees(ax_job *J, const int32_t *order, int64_t big, int nt, int *rc) {
+    int64_t *boff = malloc((size_t)(big + 1) * sizeof(int64_t));
+    boff[0] = 0;
+    for (int64_t k = 0; k < big; ++k)
+        boff[k + 1] = boff[k] + (J->poff[order[k] + 1] - J->poff[order[k]]);
+    const int64_t nb = boff[big];
+    int32_t *box = malloc((size_t)(nb ? nb : 1) * 4 * sizeof(int32_t));
+    int32_t *kt = malloc((size_t)big * sizeof(int32_t)), *kq = malloc((size_t)big * sizeof(int32_t));
+    uint8_t *ks = malloc((size_t)big);
+    ax_pre *pre = calloc((size_t)big, sizeof(ax_pre));
+    int32_t **tord = malloc((size_t)big * sizeof(int32_t *)), **qord = malloc((size_t)big * sizeof(int32_t *));
+    int32_t **lnode = malloc((size_t)big * sizeof(int32_t *)), **nodes = malloc((size_t)big * sizeof(int32_t *));
+    for (int64_t k = 0; k < big; ++k) {
+        const int32_t p = order[k];
+        const int64_t n = boff[k + 1] - boff[k];
+        kt[k] = J->in->t_seq[p];
+        kq[k] = J->in->q_seq[p];
+        ks[k] = J->in->q_strand[p] ? 1 : 0;
+        /* (sized as work_reserve sizes them: + 16) */
+        pre[k].tord = tord[k] = malloc((size_t)(n + 16) * sizeof(int32_t));
+        pre[k].qord = qord[k] = malloc((size_t)(n + 16) * sizeof(int32_t));
+        pre[k].lnode = lnode[k] = malloc((size_t)(n + 16) * sizeof(int32_t));
+        pre[k].nodes = nodes[k] = malloc((size_t)(2 * n + 32) * 6 * sizeof(int32_t));
+    }
+    tt_pack T = {J, order, boff, box, big, 0};
+    gac_run_threads(nt, tt_pack_thread, &T);
+    int64_t *leaf_off = malloc((size_t)(big + 1) * sizeof(int64_t));
+    const int r = gac_kd_trees(J->ctx, big, kt, kq, ks, boff, box, leaf_off, tord, qord, lnode, nodes);
+    if (r == GAC_OK) {
+        for (int64_t k = 0; k < big; ++k)
+            pre[k].nl = (int32_t)(leaf_off[k + 1] - leaf_off[k]);
+    } else {
+        *rc = r;
+        for (int64_t k = 0; k < big; ++k) {
+            free(pre[k].tord);
+            free(pre[k].qord);
+            free(pre[k].lnode);
+            free(pre[k].nodes);
+        }
+        free(pre);
+        pre = NULL;
+    }
+    free(leaf_off);
+    free(boff);
+    free(box);
+    free(kt);
+    free(kq);
+    free(ks);
+    free(tord);
+    free(qord);
+    free(lnode);
+    free(nodes);
+    return pre;
+}
+
 typedef struct dev_run {
     ax_job J; /* the device's pairs */
     int nt, rc;
@@ -3716,10 +3844,6 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
             atomic_init(&D->J.next, 0);
             const char *dtv = getenv("GAC_DP_DEV_THREADS"); /* (its host phases' threads) */
             D->nt = dtv && atoi(dtv) > 0 ? atoi(dtv) : 2;
-            if (pthread_create(&dth, NULL, dev_runner, D) == 0)
-                dev_started = 1;
-            else
-                dev_runner(D);
             int64_t dl = 0;
             for (int64_t k = kd; k < np; ++k)
                 dl += psize[order[k]];
@@ -3750,6 +3874,27 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
         const int64_t share = mv ? floor_ : (even > floor_ ? even : floor_);
         while (team_on && big < np_host && psize[order[big]] > share && big < nthreads / 2)
             ++big;
+        /* the team pairs' leaves and kd-trees built on the device first
+         * (gac_kd_trees, ~0.1 s for C4's 20 M team blocks, vs ~0.5 s of the
+         * largest team's critical path on its threads); then the device
+         * takes its own pairs.  GAC_DP_TEAMTREE=0: built on the teams */
+        ax_pre *pre = NULL;
+        {
+            const char *ttv = getenv("GAC_DP_TEAMTREE");
+            if (big && !(ttv && *ttv == '0') && !(dpm && strcmp(dpm, "host") == 0)) {
+                const double tp0 = now_s();
+                pre = team_trees(&J, order, big, nthreads, &rc);
+                if (getenv("GAC_TIMING"))
+                    fprintf(stderr, "[gac_axt_chain] the %lld team pairs' leaves and kd-trees on the "
+                            "device: %.3f s\n", (long long)big, now_s() - tp0);
+            }
+        }
+        if (D) {
+            if (pthread_create(&dth, NULL, dev_runner, D) == 0)
+                dev_started = 1;
+            else
+                dev_runner(D);
+        }
         team_run *tr = big ? calloc((size_t)big, sizeof(team_run)) : NULL;
         int pool = nt;
         if (big) {
@@ -3799,6 +3944,7 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
                     t = tt - used > 2 ? tt - used : 2;
                 used += t;
                 tr[k].J = &J;
+                tr[k].pre = pre ? &pre[k] : NULL;
                 tr[k].p = order[k];
                 tr[k].team = t;
                 if (nd >= 2 && k < nd && dom[(d0 + k) % nd].n >= t) {
@@ -3827,6 +3973,7 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
             if (tr[k].started)
                 pthread_join(tr[k].th, NULL);
         free(tr);
+        free(pre); /* (its arrays went to the teams' work) */
         if (big)
             stage("kd-tree DP (teams on the largest pairs, beside the pool)", &tclock);
         else

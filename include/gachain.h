@@ -313,6 +313,22 @@ int gac_chain_dp(gac_ctx *ctx, int64_t n_pairs, const int32_t *t_seq, const int3
  * pred[g] = the best predecessor as a pair-local block, or -1.  A block
  * outside its sequences is GAC_E_ARG.  Uses the context's scoring setup and
  * genomes. */
+/* kdTreeMake (kent/src/lib/chainBlock.c:166-205: the leaf lists and
+ * kdBuild :124-164) for n_pairs seqPairs on the device -- the build of
+ * gac_chain_dp_blocks -- for a caller that runs the DP itself.  Blocks as in
+ * gac_chain_dp_blocks.  Out: leaf_off[n_pairs + 1], and per pair p into the
+ * caller's buffers: tord[p][leaf] / qord[p][leaf] = the pair-local blocks of
+ * its leaves in target / query order (at most blk_off[p+1] - blk_off[p]
+ * each), lnode[p][block] = the leaf node of each block (-1: tStart ==
+ * tEnd, not a leaf), nodes[p][6 v ..] = node v of the pair's 2 n - 1 (n =
+ * its leaves) in pre-order with the hi child first: {lo, hi, -1, cut, maxQ,
+ * maxT} for an internal node, {qStart, tStart, block, 0, qEnd, tEnd} for a
+ * leaf node. */
+int gac_kd_trees(gac_ctx *ctx, int64_t n_pairs, const int32_t *t_seq, const int32_t *q_seq,
+                 const uint8_t *q_strand, const int64_t *blk_off, const int32_t *box,
+                 int64_t *leaf_off, int32_t *const *tord, int32_t *const *qord,
+                 int32_t *const *lnode, int32_t *const *nodes);
+
 int gac_chain_dp_blocks(gac_ctx *ctx, int64_t n_pairs, const int32_t *t_seq,
                         const int32_t *q_seq, const uint8_t *q_strand, const int64_t *blk_off,
                         const int32_t *box, const int32_t *score, int fast, int64_t lin_k,

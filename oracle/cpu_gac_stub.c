@@ -959,3 +959,89 @@ int gac_chain_dp_blocks(gac_ctx *c, int64_t P, const int32_t *t_seq, const int32
     free(lp);
     return rc;
 }
+
+/* gac_kd_trees: kdTreeMake (chainBlock.c:166-205) restated recursively --
+ * the leaf sorts of gac_chain_dp_blocks' stand-in above, then kdBuild
+ * (:124-164) in pre-order with the hi child first -- into the host layout */
+typedef struct stub_kd {
+    const int32_t *box; /* the pair's blocks */
+    int32_t *nodes, *lnode, *hit, *tmp;
+    int32_t nn;
+} stub_kd;
+
+static int32_t stub_kd_build(stub_kd *K, int32_t *Q, int32_t *T, int32_t n, int dim) {
+    const int32_t id = K->nn++;
+    int32_t *nd = K->nodes + 6 * id;
+    if (n == 1) {
+        const int32_t l = Q[0];
+        const int32_t *b = K->box + 4 * l;
+        nd[0] = b[0], nd[1] = b[2], nd[2] = l, nd[3] = 0, nd[4] = b[1], nd[5] = b[3];
+        K->lnode[l] = id;
+        return id;
+    }
+    const int32_t half = n / 2;
+    int32_t *D = dim == 0 ? Q : T, *O = dim == 0 ? T : Q;
+    for (int32_t i = 0; i < n; ++i)
+        K->hit[D[i]] = i < half;
+    int32_t k = 0;
+    for (int32_t i = 0; i < n; ++i)
+        if (K->hit[O[i]])
+            K->tmp[k++] = O[i];
+    for (int32_t i = 0; i < n; ++i)
+        if (!K->hit[O[i]])
+            K->tmp[k++] = O[i];
+    memcpy(O, K->tmp, (size_t)n * 4);
+    const int32_t *mb = K->box + 4 * D[half - 1];
+    const int32_t cut = dim == 0 ? mb[0] : mb[2];
+    const int32_t hi = stub_kd_build(K, Q + half, T + half, n - half, 1 - dim);
+    const int32_t lo = stub_kd_build(K, Q, T, half, 1 - dim);
+    nd = K->nodes + 6 * id;
+    const int32_t *a = K->nodes + 6 * lo, *b = K->nodes + 6 * hi;
+    nd[0] = lo, nd[1] = hi, nd[2] = -1, nd[3] = cut;
+    nd[4] = a[4] > b[4] ? a[4] : b[4];
+    nd[5] = a[5] > b[5] ? a[5] : b[5];
+    return id;
+}
+
+int gac_kd_trees(gac_ctx *c, int64_t P, const int32_t *t_seq, const int32_t *q_seq,
+                 const uint8_t *q_strand, const int64_t *blk_off, const int32_t *box,
+                 int64_t *leaf_off, int32_t *const *tord, int32_t *const *qord,
+                 int32_t *const *lnode, int32_t *const *nodes) {
+    (void)c, (void)t_seq, (void)q_seq, (void)q_strand;
+    leaf_off[0] = 0;
+    for (int64_t p = 0; p < P; ++p) {
+        const int64_t b0 = blk_off[p];
+        const int32_t nb = (int32_t)(blk_off[p + 1] - b0);
+        const int32_t *bx = box + 4 * b0;
+        dt_key *k = malloc((size_t)(nb ? nb : 1) * sizeof(dt_key));
+        int32_t nl = 0;
+        for (int32_t r = 0; r < nb; ++r) { /* reverse input order (slAddHead) */
+            const int32_t g = nb - 1 - r;
+            lnode[p][g] = -1;
+            if (bx[4 * g + 2] != bx[4 * g + 3])
+                k[nl++] = (dt_key){(unsigned long long)(uint32_t)bx[4 * g + 2], r, g};
+        }
+        qsort(k, (size_t)nl, sizeof(dt_key), dt_key_cmp);
+        for (int32_t i = 0; i < nl; ++i)
+            tord[p][i] = k[i].v;
+        for (int32_t i = 0; i < nl; ++i)
+            k[i] = (dt_key){(unsigned long long)(uint32_t)bx[4 * tord[p][i]], i, tord[p][i]};
+        qsort(k, (size_t)nl, sizeof(dt_key), dt_key_cmp);
+        for (int32_t i = 0; i < nl; ++i)
+            qord[p][i] = k[i].v;
+        free(k);
+        leaf_off[p + 1] = leaf_off[p] + nl;
+        if (!nl)
+            continue;
+        stub_kd K = {bx, nodes[p], lnode[p], calloc((size_t)nb, 4), malloc((size_t)nl * 4), 0};
+        int32_t *Q = malloc((size_t)nl * 4), *T = malloc((size_t)nl * 4);
+        memcpy(Q, qord[p], (size_t)nl * 4);
+        memcpy(T, tord[p], (size_t)nl * 4);
+        stub_kd_build(&K, Q, T, nl, 0);
+        free(Q);
+        free(T);
+        free(K.hit);
+        free(K.tmp);
+    }
+    return GAC_OK;
+}

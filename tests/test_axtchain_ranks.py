@@ -249,3 +249,28 @@ def test_device_built_dp_inputs_cpu(tool, env, tmp_path):
     subprocess.run([ref] + args + ["ref.chain"], cwd=tmp_path, check=True, timeout=600,
                    capture_output=True)
     assert filecmp.cmp(tmp_path / "dev.chain", tmp_path / "ref.chain", shallow=False)
+
+
+@pytest.mark.parametrize("teamtree", ["1", "0"])
+def test_team_pairs_device_trees_cpu(tool, teamtree, tmp_path):
+    """The team pairs' leaves and kd-trees from gac_kd_trees (here its CPU
+    restatement in the stand-in: kdTreeMake recursively), adopted by the
+    host teams' DP (GAC_DP_TEAMTREE=1, the default) or built on the teams'
+    threads (=0): a C4-shaped set with several team pairs (GAC_DP_TEAM_MIN),
+    equal to the reference's chains."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "axtChain")
+    if not os.path.exists(ref):
+        pytest.skip("reference axtChain not built (make ref)")
+    synth = os.path.join(ROOT, "genomealignmenttools_amd", "libexec", "gac_synth")
+    subprocess.run([synth, "c4", str(tmp_path), "-blocks=120000", "-nt=4", "-nq=4", "-tsize=3000000",
+                    "-qsize=2500000", "-threads=4"], check=True, timeout=300, capture_output=True)
+    args = ["-linearGap=loose", "-psl", "in.psl", "t.2bit", "q.2bit"]
+    env = dict(os.environ, GAC_DP_TEAMTREE=teamtree, GAC_DP_TEAM_MIN="5000", GAC_THREADS="8",
+               GAC_TIMING="1")
+    r = subprocess.run([tool] + args + ["ours.chain"], cwd=tmp_path, env=env, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert ("team pairs' leaves and kd-trees on the device" in r.stderr) == (teamtree == "1")
+    subprocess.run([ref] + args + ["ref.chain"], cwd=tmp_path, check=True, timeout=600,
+                   capture_output=True)
+    assert filecmp.cmp(tmp_path / "ours.chain", tmp_path / "ref.chain", shallow=False)
