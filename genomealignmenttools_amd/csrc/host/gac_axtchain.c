@@ -139,6 +139,8 @@ typedef struct ax_out { /* one pair's result */
     int err;
     char msg[512];
     double secs; /* wall time of this pair's chaining */
+    int64_t *gsc; /* [n_chains]: chainCalcScore of each chain (score_pairs) */
+    int scored;
 } ax_out;
 
 /* a pair's leaves and kd-tree built on the device (gac_kd_trees) for the
@@ -3494,7 +3496,6 @@ typedef struct gather_job {
     const gac_axt_input *in;
     int32_t *ct, *cq;
     uint8_t *cs;
-    int32_t *cpair;
     int64_t *coff;
     int32_t *bt, *bq, *bs;
     int64_t *c0, *x0; /* per pair: first chain, first block */
@@ -3524,19 +3525,21 @@ static void *gather_thread(void *arg) {
             G->ct[c] = G->in->t_seq[p];
             G->cq[c] = G->in->q_seq[p];
             G->cs[c] = G->in->q_strand[p] ? 1 : 0;
-            G->cpair[c] = (int32_t)p;
             x += o->coff[k + 1] - o->coff[k];
             G->coff[c + 1] = x;
         }
     }
 }
 
-/* the kept chains in output order (parallel over chains) */
+/* the kept chains in output order (parallel over chains), copied from each
+ * pair's own arrays: chain i of the whole list is chain i - c0[p] of pair
+ * p = cpair[i] */
 typedef struct out_job {
     gac_axt_chains *R;
     const struct dkey *k;
-    const int64_t *coff, *gsc;
-    const int32_t *cpair, *bt, *bq, *bs;
+    const ax_out *po;
+    const int64_t *c0, *gsc;
+    const int32_t *cpair;
     int64_t nk;
     _Atomic int64_t next;
 } out_job;
@@ -3550,19 +3553,117 @@ static void *out_thread(void *arg) {
             return NULL;
         const int64_t j1 = j0 + 1024 < O->nk ? j0 + 1024 : O->nk;
         for (int64_t j = j0; j < j1; ++j) {
-            const int32_t i = O->k[j].v;
-            const int64_t b0 = O->coff[i], b1 = O->coff[i + 1], o = R->blk_off[j];
+            const int32_t i = O->k[j].v, p = O->cpair[i];
+            const ax_out *po = &O->po[p];
+            const int32_t c = (int32_t)(i - O->c0[p]);
+            const int64_t b0 = po->coff[c], b1 = po->coff[c + 1], o = R->blk_off[j];
             R->score[j] = (double)O->gsc[i];
-            R->pair[j] = O->cpair[i];
-            R->t_start[j] = O->bt[b0];
-            R->q_start[j] = O->bq[b0];
-            R->t_end[j] = O->bt[b1 - 1] + O->bs[b1 - 1];
-            R->q_end[j] = O->bq[b1 - 1] + O->bs[b1 - 1];
-            memcpy(R->blk_t + o, O->bt + b0, (size_t)(b1 - b0) * 4);
-            memcpy(R->blk_q + o, O->bq + b0, (size_t)(b1 - b0) * 4);
-            memcpy(R->blk_size + o, O->bs + b0, (size_t)(b1 - b0) * 4);
+            R->pair[j] = p;
+            R->t_start[j] = po->bt[b0];
+            R->q_start[j] = po->bq[b0];
+            R->t_end[j] = po->bt[b1 - 1] + po->bs[b1 - 1];
+            R->q_end[j] = po->bq[b1 - 1] + po->bs[b1 - 1];
+            memcpy(R->blk_t + o, po->bt + b0, (size_t)(b1 - b0) * 4);
+            memcpy(R->blk_q + o, po->bq + b0, (size_t)(b1 - b0) * 4);
+            memcpy(R->blk_size + o, po->bs + b0, (size_t)(b1 - b0) * 4);
         }
     }
+}
+
+/* chainCalcScore of every chain of the pairs sel[0 .. ns) (axtChain.c:300-305):
+ * their chains gathered into one set (pairs in parallel, disjoint slots from
+ * prefix sums over the selection), one upload, one GPU batch; each pair's
+ * scores to its po[p].gsc.  Called for the pairs that are done while the
+ * teams still run (the pool's and the device's), then for the rest, so that
+ * only the last pairs' scoring is on the critical path. */
+static int score_pairs(gac_ctx *ctx, ax_out *po, const gac_axt_input *in, int64_t np,
+                       const int32_t *sel, int64_t ns, int nthreads, double *tclock) {
+    int64_t nc = 0, ncb = 0, ntask = 0;
+    for (int64_t s = 0; s < ns; ++s) {
+        const ax_out *o = &po[sel[s]];
+        nc += o->n_chains;
+        ncb += o->coff ? o->coff[o->n_chains] : 0;
+        ntask += (o->n_chains + 4095) / 4096;
+    }
+    for (int64_t s = 0; s < ns; ++s) { /* (a pair without chains: nothing to score) */
+        ax_out *o = &po[sel[s]];
+        o->scored = 1;
+        o->gsc = malloc((size_t)(o->n_chains ? o->n_chains : 1) * 8);
+    }
+    if (nc == 0)
+        return GAC_OK;
+    int32_t *ct = malloc((size_t)nc * 4), *cq = malloc((size_t)nc * 4);
+    uint8_t *cs = malloc((size_t)nc);
+    int64_t *coff = malloc((size_t)(nc + 1) * 8);
+    int32_t *bt = malloc((size_t)(ncb ? ncb : 1) * 4), *bq = malloc((size_t)(ncb ? ncb : 1) * 4),
+            *bs = malloc((size_t)(ncb ? ncb : 1) * 4);
+    int64_t *gsc = malloc((size_t)nc * 8);
+    int32_t *gali = malloc((size_t)nc * 4);
+    gather_job G;
+    memset(&G, 0, sizeof(G));
+    G.po = po, G.in = in, G.ct = ct, G.cq = cq, G.cs = cs, G.coff = coff;
+    G.bt = bt, G.bq = bq, G.bs = bs, G.np = np;
+    G.c0 = malloc((size_t)(np + 1) * 8); /* (set for the selected pairs only) */
+    G.x0 = malloc((size_t)(np + 1) * 8);
+    G.task = malloc((size_t)(ntask ? ntask : 1) * 3 * sizeof(int64_t));
+    int64_t c = 0, x = 0;
+    for (int64_t s = 0; s < ns; ++s) {
+        const int32_t p = sel[s];
+        G.c0[p] = c;
+        G.x0[p] = x;
+        c += po[p].n_chains;
+        x += po[p].coff ? po[p].coff[po[p].n_chains] : 0;
+        for (int32_t k = 0; k < po[p].n_chains; k += 4096) {
+            G.task[3 * G.ntask] = p;
+            G.task[3 * G.ntask + 1] = k;
+            G.task[3 * G.ntask + 2] = k + 4096 < po[p].n_chains ? k + 4096 : po[p].n_chains;
+            ++G.ntask;
+        }
+    }
+    coff[0] = 0;
+    atomic_init(&G.next, 0);
+    run_threads(nthreads < G.ntask ? nthreads : (int)(G.ntask ? G.ntask : 1), gather_thread, &G);
+    free(G.task);
+    stage("chains gathered for scoring", tclock);
+    gac_chainset_desc d = {nc, ct, cq, cs, coff, ncb, bt, bq, bs};
+    gac_chainset *set = NULL;
+    int rc = gac_chains_upload(ctx, &d, &set);
+    stage("chains to HBM", tclock);
+    if (rc == GAC_OK)
+        rc = gac_score_chains(ctx, set, 0, gsc, NULL, gali);
+    stage("GPU chain scores", tclock);
+    gac_chains_free(set);
+    if (rc == GAC_OK)
+        for (int64_t s = 0; s < ns; ++s) {
+            const int32_t p = sel[s];
+            memcpy(po[p].gsc, gsc + G.c0[p], (size_t)po[p].n_chains * 8);
+        }
+    free(G.c0);
+    free(G.x0);
+    /* (GBs at C4: freed on a detached thread, off the caller's path) */
+    void *big[] = {ct, cq, cs, coff, bt, bq, bs, gsc, gali};
+    free_later(big, (int)(sizeof(big) / sizeof(big[0])));
+    return rc;
+}
+
+/* score_pairs of the pairs not scored yet, unless one of them failed (the
+ * caller reports the first pair's error) */
+static int score_rest(gac_ctx *ctx, ax_out *po, const gac_axt_input *in, int64_t np,
+                      const int32_t *cand, int64_t ncand, int nthreads, double *tclock) {
+    int32_t *sel = malloc((size_t)(ncand ? ncand : 1) * 4);
+    int64_t ns = 0;
+    for (int64_t k = 0; k < ncand; ++k) {
+        const int32_t p = cand ? cand[k] : (int32_t)k;
+        if (po[p].err) {
+            free(sel);
+            return GAC_OK;
+        }
+        if (!po[p].scored)
+            sel[ns++] = p;
+    }
+    const int rc = ns ? score_pairs(ctx, po, in, np, sel, ns, nthreads, tclock) : GAC_OK;
+    free(sel);
+    return rc;
 }
 
 void gac_axt_chains_free(gac_axt_chains *c) {
@@ -3969,6 +4070,22 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
         }
         if (big == 0 || np_host > big)
             run_threads(pool, ax_thread, &J);
+        if (big) {
+            /* the pool's and the device's pairs scored while the teams run
+             * (GAC_AXT_SCORE_EARLY=0: every pair's chains in one batch after
+             * the teams) */
+            const char *ev = getenv("GAC_AXT_SCORE_EARLY");
+            if (!(ev && *ev == '0')) {
+                if (D && dev_started) {
+                    pthread_join(dth, NULL);
+                    dev_started = 0;
+                }
+                stage("kd-tree DP (the pool's and the device's pairs)", &tclock);
+                if (rc == GAC_OK && (!D || D->rc == GAC_OK))
+                    rc = score_rest(ctx, po, in, np, order + big, np - big,
+                                    pool + (D ? D->nt : 0), &tclock);
+            }
+        }
         for (int64_t k = 0; k < big; ++k)
             if (tr[k].started)
                 pthread_join(tr[k].th, NULL);
@@ -4027,61 +4144,25 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
     }
     gac_axt_chains *R = NULL;
     if (rc == GAC_OK) {
-        /* ---- chainCalcScore of every chain: one GPU batch */
-        int64_t nc = 0, ncb = 0;
-        for (int64_t p = 0; p < np; ++p) {
-            nc += po[p].n_chains;
-            ncb += po[p].coff ? po[p].coff[po[p].n_chains] : 0;
-        }
-        int32_t *ct = malloc((size_t)(nc ? nc : 1) * 4), *cq = malloc((size_t)(nc ? nc : 1) * 4);
-        uint8_t *cs = malloc((size_t)(nc ? nc : 1));
-        int32_t *cpair = malloc((size_t)(nc ? nc : 1) * 4);
-        int64_t *coff = malloc((size_t)(nc + 1) * 8);
-        int32_t *bt = malloc((size_t)(ncb ? ncb : 1) * 4), *bq = malloc((size_t)(ncb ? ncb : 1) * 4),
-                *bs = malloc((size_t)(ncb ? ncb : 1) * 4);
-        int64_t *gsc = malloc((size_t)(nc ? nc : 1) * 8);
-        int32_t *gali = malloc((size_t)(nc ? nc : 1) * 4);
-        /* every pair's chains into the set, pairs in parallel (disjoint
-         * slots from prefix sums over the pairs) */
-        gather_job G;
-        memset(&G, 0, sizeof(G));
-        G.po = po, G.in = in, G.ct = ct, G.cq = cq, G.cs = cs, G.cpair = cpair, G.coff = coff;
-        G.bt = bt, G.bq = bq, G.bs = bs, G.np = np;
-        G.c0 = malloc((size_t)(np + 1) * 8);
-        G.x0 = malloc((size_t)(np + 1) * 8);
-        G.c0[0] = G.x0[0] = 0;
-        int64_t nt_ = 0;
-        for (int64_t p = 0; p < np; ++p) {
-            G.c0[p + 1] = G.c0[p] + po[p].n_chains;
-            G.x0[p + 1] = G.x0[p] + (po[p].coff ? po[p].coff[po[p].n_chains] : 0);
-            nt_ += (po[p].n_chains + 4095) / 4096;
-        }
-        G.task = malloc((size_t)(nt_ ? nt_ : 1) * 3 * sizeof(int64_t));
+        /* ---- chainCalcScore of every chain not scored yet: one GPU batch
+         * (score_pairs) */
+        rc = score_rest(ctx, po, in, np, NULL, np, nthreads, &tclock);
+        int64_t nc = 0;
+        int64_t *c0 = malloc((size_t)(np + 1) * 8);
+        c0[0] = 0;
         for (int64_t p = 0; p < np; ++p)
-            for (int32_t k = 0; k < po[p].n_chains; k += 4096) {
-                G.task[3 * G.ntask] = p;
-                G.task[3 * G.ntask + 1] = k;
-                G.task[3 * G.ntask + 2] = k + 4096 < po[p].n_chains ? k + 4096 : po[p].n_chains;
-                ++G.ntask;
+            c0[p + 1] = c0[p] + po[p].n_chains;
+        nc = c0[np];
+        int32_t *cpair = malloc((size_t)(nc ? nc : 1) * 4);
+        int64_t *gsc = malloc((size_t)(nc ? nc : 1) * 8);
+        if (rc == GAC_OK)
+            for (int64_t p = 0; p < np; ++p) {
+                for (int64_t i = c0[p]; i < c0[p + 1]; ++i)
+                    cpair[i] = (int32_t)p;
+                if (po[p].n_chains)
+                    memcpy(gsc + c0[p], po[p].gsc, (size_t)po[p].n_chains * 8);
             }
-        coff[0] = 0;
-        atomic_init(&G.next, 0);
-        run_threads(nthreads < G.ntask ? nthreads : (int)(G.ntask ? G.ntask : 1), gather_thread, &G);
-        free(G.task);
-        free(G.c0);
-        free(G.x0);
-        stage("chains gathered for scoring", &tclock);
-        gac_chainset_desc d = {nc, ct, cq, cs, coff, ncb, bt, bq, bs};
-        gac_chainset *set = NULL;
-        if (nc > 0) { /* whole chains: chainCalcScore of each (axtChain.c:300-305) */
-            rc = gac_chains_upload(ctx, &d, &set);
-            stage("chains to HBM", &tclock);
-            if (rc == GAC_OK)
-                rc = gac_score_chains(ctx, set, 0, gsc, NULL, gali);
-            stage("GPU chain scores", &tclock);
-            gac_chains_free(set);
-        }
-        stage("chain set freed", &tclock);
+        stage("scores in list order", &tclock);
         if (rc == GAC_OK) {
             /* minScore filter; slAddHead onto the master list (reversed),
              * then slSort(chainCmpScore) -- stable */
@@ -4102,30 +4183,31 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
             R->q_start = malloc((size_t)(nk ? nk : 1) * 4);
             R->q_end = malloc((size_t)(nk ? nk : 1) * 4);
             R->blk_off = malloc((size_t)(nk + 1) * 8);
-            int64_t tb = 0;
-            for (int64_t j = 0; j < nk; ++j)
-                tb += coff[k[j].v + 1] - coff[k[j].v];
+            R->blk_off[0] = 0;
+            for (int64_t j = 0; j < nk; ++j) {
+                const int32_t i = k[j].v, p = cpair[i], c = (int32_t)(i - c0[p]);
+                R->blk_off[j + 1] = R->blk_off[j] + (po[p].coff[c + 1] - po[p].coff[c]);
+            }
+            const int64_t tb = R->blk_off[nk];
             R->n_blocks = tb;
             R->blk_t = malloc((size_t)(tb ? tb : 1) * 4);
             R->blk_q = malloc((size_t)(tb ? tb : 1) * 4);
             R->blk_size = malloc((size_t)(tb ? tb : 1) * 4);
-            R->blk_off[0] = 0;
-            for (int64_t j = 0; j < nk; ++j)
-                R->blk_off[j + 1] = R->blk_off[j] + (coff[k[j].v + 1] - coff[k[j].v]);
-            out_job O = {R, k, coff, gsc, cpair, bt, bq, bs, nk, 0};
+            out_job O = {R, k, po, c0, gsc, cpair, nk, 0};
             atomic_init(&O.next, 0);
             run_threads(nthreads, out_thread, &O);
             free(k);
         }
-        /* the scoring set's host arrays and every pair's chains (GBs at C4):
-         * freed on a detached thread, off the caller's path */
-        void *big[] = {ct, cq, cs, cpair, coff, bt, bq, bs, gsc, gali};
+        void *big[] = {c0, cpair, gsc};
         free_later(big, (int)(sizeof(big) / sizeof(big[0])));
     }
+    /* every pair's chains (GBs at C4): freed on a detached thread, off the
+     * caller's path */
     {
-        void **pp = malloc((size_t)(5 * np + 1) * sizeof(void *));
+        void **pp = malloc((size_t)(6 * np + 1) * sizeof(void *));
         int64_t k = 0;
         for (int64_t p = 0; p < np; ++p) {
+            pp[k++] = po[p].gsc;
             pp[k++] = po[p].coff;
             pp[k++] = po[p].bt;
             pp[k++] = po[p].bq;

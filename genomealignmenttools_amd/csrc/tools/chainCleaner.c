@@ -1712,10 +1712,11 @@ int main(int argc, char *argv[]) {
         for (int32_t m = 0; m < S.c.n_meta; ++m)
             fprintf(f, "%s\n", S.c.meta[m]);
         sortkey *k = malloc((size_t)(g_nout ? g_nout : 1) * sizeof(sortkey));
+        /* the score as written ("%1.0f") and read back: printf rounds the
+         * exact binary value to the nearest integer, ties to even, which is
+         * nearbyint in the default rounding mode (no string round trip) */
         for (int64_t i = 0; i < g_nout; ++i) {
-            char buf[400];
-            snprintf(buf, sizeof(buf), "%1.0f", g_out[i].score);
-            k[i].score = atof(buf);
+            k[i].score = nearbyint(g_out[i].score);
             k[i].rank = g_nout - 1 - i;
         }
         qsort(k, (size_t)g_nout, sizeof(sortkey), sortkey_cmp);

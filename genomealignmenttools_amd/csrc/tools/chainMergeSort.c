@@ -147,11 +147,11 @@ static void heap_remove(qheap *q, cursor *e) { /* removeFromQuickHeapByElem */
         heap_balance(q, n);
 }
 
-/* the %1.0f text of a score, re-read with atof (a temp file round trip) */
+/* the %1.0f text of a score, re-read with atof (a temp file round trip):
+ * printf rounds the exact value to the nearest integer, ties to even --
+ * nearbyint in the default rounding mode, at any magnitude */
 static double printed(double s) {
-    char b[64];
-    snprintf(b, sizeof(b), "%1.0f", s);
-    return atof(b);
+    return nearbyint(s);
 }
 
 /* chainMergeSort(fileCount, files, out, level): intermediate outputs keep

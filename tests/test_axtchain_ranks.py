@@ -251,13 +251,15 @@ def test_device_built_dp_inputs_cpu(tool, env, tmp_path):
     assert filecmp.cmp(tmp_path / "dev.chain", tmp_path / "ref.chain", shallow=False)
 
 
-@pytest.mark.parametrize("teamtree", ["1", "0"])
-def test_team_pairs_device_trees_cpu(tool, teamtree, tmp_path):
+@pytest.mark.parametrize("teamtree,early", [("1", "1"), ("0", "1"), ("1", "0")])
+def test_team_pairs_device_trees_cpu(tool, teamtree, early, tmp_path):
     """The team pairs' leaves and kd-trees from gac_kd_trees (here its CPU
     restatement in the stand-in: kdTreeMake recursively), adopted by the
     host teams' DP (GAC_DP_TEAMTREE=1, the default) or built on the teams'
     threads (=0): a C4-shaped set with several team pairs (GAC_DP_TEAM_MIN),
-    equal to the reference's chains."""
+    equal to the reference's chains.  The pool's pairs' chains are scored
+    while the teams run (GAC_AXT_SCORE_EARLY=1, the default) or with the
+    teams' in one batch (=0)."""
     ref = os.path.join(ROOT, "oracle", "_ref", "axtChain")
     if not os.path.exists(ref):
         pytest.skip("reference axtChain not built (make ref)")
@@ -266,11 +268,12 @@ def test_team_pairs_device_trees_cpu(tool, teamtree, tmp_path):
                     "-qsize=2500000", "-threads=4"], check=True, timeout=300, capture_output=True)
     args = ["-linearGap=loose", "-psl", "in.psl", "t.2bit", "q.2bit"]
     env = dict(os.environ, GAC_DP_TEAMTREE=teamtree, GAC_DP_TEAM_MIN="5000", GAC_THREADS="8",
-               GAC_TIMING="1")
+               GAC_TIMING="1", GAC_AXT_SCORE_EARLY=early)
     r = subprocess.run([tool] + args + ["ours.chain"], cwd=tmp_path, env=env, capture_output=True,
                        text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     assert ("team pairs' leaves and kd-trees on the device" in r.stderr) == (teamtree == "1")
+    assert r.stderr.count("GPU chain scores") == (2 if early == "1" else 1)
     subprocess.run([ref] + args + ["ref.chain"], cwd=tmp_path, check=True, timeout=600,
                    capture_output=True)
     assert filecmp.cmp(tmp_path / "ours.chain", tmp_path / "ref.chain", shallow=False)
