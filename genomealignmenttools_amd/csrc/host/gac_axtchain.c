@@ -774,10 +774,17 @@ static void *rs_scatter(void *arg) {
     return NULL;
 }
 
+static int radix_sort16_any(void *a, int64_t n, int nt, uint64_t any);
+
 static int radix_sort16(void *a, int64_t n, int nt) { /* -1, unsorted: a key < 0 as int64 */
     uint64_t any = 0;
     for (int64_t i = 0; i < n; ++i)
         any |= rs_key((const uint8_t *)a + 16 * i);
+    return radix_sort16_any(a, n, nt, any);
+}
+
+/* any: the OR of every key (the bits the passes cover) */
+static int radix_sort16_any(void *a, int64_t n, int nt, uint64_t any) {
     if (any >> 63)
         return -1;
     if (n < 2 || any == 0)
@@ -896,28 +903,106 @@ static void par_sort16(void *a, int64_t n, int (*cmp)(const void *, const void *
  * scores are integral (sums of integer block scores and gap costs), so
  * (max - k) is an exact unsigned key for radix_sort16 (stable: ties stay in
  * rank order); other keys take the comparator sort */
-static void sort_desc16(dkey *k, int64_t n, int nt) {
+/* slices [n c / nt, n (c + 1) / nt) of a loop on nt threads (one slice,
+ * inline, below 2^18 iterations) */
+typedef struct pfor {
+    void (*fn)(void *ctx, int c, int64_t a, int64_t b);
+    void *ctx;
+    int64_t n;
+    int nt;
+    _Atomic int next;
+} pfor;
+
+static void *pfor_thread(void *arg) {
+    pfor *P = arg;
+    for (int c; (c = atomic_fetch_add(&P->next, 1)) < P->nt;)
+        P->fn(P->ctx, c, P->n * c / P->nt, P->n * (c + 1) / P->nt);
+    return NULL;
+}
+
+static int par_for(int64_t n, int nt, void (*fn)(void *, int, int64_t, int64_t), void *ctx) {
+    nt = nt > 256 ? 256 : nt;
+    if (nt <= 1 || n < (1 << 18)) {
+        fn(ctx, 0, 0, n);
+        return 1;
+    }
+    pfor P = {fn, ctx, n, nt, 0};
+    atomic_init(&P.next, 0);
+    gac_run_threads(nt, pfor_thread, &P);
+    return nt;
+}
+
+typedef struct sd16 {
+    dkey *k;
+    int64_t m;
+    double mx[256];
+    int bad[256], any[256];
+    uint64_t bits[256];
+} sd16;
+
+static void sd16_scan(void *arg, int c, int64_t a, int64_t b) {
+    sd16 *S = arg;
     double mx = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        const double x = k[i].k;
+    S->bad[c] = 0;
+    S->any[c] = a < b;
+    for (int64_t i = a; i < b; ++i) {
+        const double x = S->k[i].k;
         if (!(x > -4.0e15 && x < 4.0e15) || (double)(int64_t)x != x) {
+            S->bad[c] = 1;
+            return;
+        }
+        if (i == a || x > mx)
+            mx = x;
+    }
+    S->mx[c] = mx;
+}
+
+static void sd16_to_u(void *arg, int c, int64_t a, int64_t b) {
+    sd16 *S = arg;
+    uint64_t o = 0;
+    for (int64_t i = a; i < b; ++i) {
+        const uint64_t u = (uint64_t)(S->m - (int64_t)S->k[i].k);
+        memcpy(&S->k[i].k, &u, 8);
+        o |= u;
+    }
+    S->bits[c] = o;
+}
+
+static void sd16_from_u(void *arg, int c, int64_t a, int64_t b) {
+    sd16 *S = arg;
+    (void)c;
+    for (int64_t i = a; i < b; ++i) {
+        uint64_t u;
+        memcpy(&u, &S->k[i].k, 8);
+        S->k[i].k = (double)(S->m - (int64_t)u);
+    }
+}
+
+static void sort_desc16(dkey *k, int64_t n, int nt) {
+    sd16 *S = malloc(sizeof(sd16));
+    S->k = k;
+    const int ns = par_for(n, nt, sd16_scan, S);
+    int have = 0;
+    double mx = 0;
+    for (int c = 0; c < ns; ++c) {
+        if (S->bad[c]) {
+            free(S);
             par_sort16(k, n, dkey_cmp_desc, nt);
             return;
         }
-        if (i == 0 || x > mx)
-            mx = x;
+        if (S->any[c] && (!have || S->mx[c] > mx)) {
+            mx = S->mx[c];
+            have = 1;
+        }
     }
-    const int64_t m = (int64_t)mx;
-    for (int64_t i = 0; i < n; ++i) {
-        const uint64_t u = (uint64_t)(m - (int64_t)k[i].k);
-        memcpy(&k[i].k, &u, 8);
-    }
-    radix_sort16(k, n, nt);
-    for (int64_t i = 0; i < n; ++i) {
-        uint64_t u;
-        memcpy(&u, &k[i].k, 8);
-        k[i].k = (double)(m - (int64_t)u);
-    }
+    S->m = (int64_t)mx;
+    const int nu = par_for(n, nt, sd16_to_u, S);
+    uint64_t any = 0;
+    for (int c = 0; c < nu; ++c)
+        any |= S->bits[c];
+    radix_sort16_any(k, n, nt, any);
+    par_for(n, nt, sd16_from_u, S);
+    free(S);
 }
 
 typedef struct ax_cb {
@@ -1880,19 +1965,50 @@ typedef struct ax_chains {
     int32_t nc, nbk;
 } ax_chains;
 
+typedef struct peel_keys {
+    const ax_work *w;
+    dkey *dk;
+} peel_keys;
+
+static void peel_keys_fn(void *arg, int c, int64_t a, int64_t b) {
+    const peel_keys *K = arg;
+    (void)c;
+    for (int64_t i = a; i < b; ++i)
+        K->dk[i] = (dkey){K->w->total[K->w->tord[i]], (int32_t)i, K->w->tord[i]};
+}
+
 static void pair_peel(ax_work *w, const ax_pairinfo *pi, FILE *details, ax_chains *pc) {
     const int32_t nb = w->n, nl = w->nl;
+    const int tm = nb > (1 << 20) && getenv("GAC_TIMING");
+    const double t0 = tm ? mono_s() : 0;
     /* in totalScore order */
     dkey *dk = malloc((size_t)nl * sizeof(dkey));
-    for (int32_t i = 0; i < nl; ++i)
-        dk[i] = (dkey){w->total[w->tord[i]], i, w->tord[i]};
+    peel_keys K = {w, dk};
+    par_for(nl, w->team > 1 ? w->team : 1, peel_keys_fn, &K);
     sort_desc16(dk, nl, w->team > 1 ? w->team : 1);
+    const double t1 = tm ? mono_s() : 0;
     for (int32_t i = 0; i < nb; ++i)
         w->hit[i] = 0;
     int32_t *cblk = malloc((size_t)nl * sizeof(int32_t));
     int32_t *cstart = malloc((size_t)(nl + 1) * sizeof(int32_t));
     int32_t nc = 0, nbk = 0;
     for (int32_t i = 0; i < nl; ++i) {
+        /* (the chain starts come in score order, at random leaves: their
+         * flags, predecessors and the predecessors' nodes prefetched) */
+        if (i + 32 < nl) {
+            const int32_t f = dk[i + 32].v;
+            __builtin_prefetch(&w->hit[f]);
+            __builtin_prefetch(&w->pred[f]);
+        }
+        if (i + 16 < nl) {
+            const int32_t f = w->pred[dk[i + 16].v];
+            if (f >= 0) {
+                if (w->pred_blk)
+                    __builtin_prefetch(&w->hit[f]);
+                else
+                    __builtin_prefetch(&w->nodes[f]);
+            }
+        }
         const int32_t leaf = dk[i].v;
         if (w->hit[leaf])
             continue;
@@ -1927,6 +2043,9 @@ static void pair_peel(ax_work *w, const ax_pairinfo *pi, FILE *details, ax_chain
     }
     cstart[nc] = nbk;
     free(dk);
+    if (tm)
+        fprintf(stderr, "[gac_axt_chain] peel of %d leaves: keys + sort %.3f s, walk %.3f s (%d "
+                "chains)\n", nl, t1 - t0, mono_s() - t1, nc);
     pc->cblk = cblk;
     pc->cstart = cstart;
     pc->nc = nc;
@@ -2016,6 +2135,14 @@ static void *fin_thread(void *arg) {
         const int32_t b = a + 256 < F->n ? a + 256 : F->n;
         for (int32_t r = a; r < b; ++r) {
             if (F->phase == 0) { /* scoreBlocks of chain r */
+                if (r + 4 < F->n) { /* (the blocks are at random places) */
+                    const int32_t k4 = cblk[cstart[r + 4]];
+                    __builtin_prefetch(&w->score[k4]);
+                    __builtin_prefetch(&w->qs[k4]);
+                    __builtin_prefetch(&w->qe[k4]);
+                    __builtin_prefetch(&w->ts[k4]);
+                    __builtin_prefetch(&w->te[k4]);
+                }
                 double sc = 0;
                 for (int32_t j = cstart[r]; j < cstart[r + 1]; ++j) {
                     sc += w->score[cblk[j]];
@@ -2024,6 +2151,20 @@ static void *fin_thread(void *arg) {
                 }
                 F->ck[r] = (dkey){sc, r, r};
             } else if (F->phase == 1) { /* overlap removal of the r-th chain */
+                /* (chains in score order, at random places: the chain's
+                 * start, first block and its coordinates prefetched) */
+                if (r + 8 < F->n)
+                    __builtin_prefetch(&cstart[F->ck[r + 8].v]);
+                if (r + 4 < F->n)
+                    __builtin_prefetch(&cblk[cstart[F->ck[r + 4].v]]);
+                if (r + 2 < F->n) {
+                    const int32_t j2 = cstart[F->ck[r + 2].v], k2 = cblk[j2];
+                    __builtin_prefetch(&w->qs[k2]);
+                    __builtin_prefetch(&w->qe[k2]);
+                    __builtin_prefetch(&w->ts[k2]);
+                    __builtin_prefetch(&w->te[k2]);
+                    __builtin_prefetch(&F->cb[j2], 1);
+                }
                 const int32_t c = F->ck[r].v, b0 = cstart[c], b1 = cstart[c + 1];
                 for (int32_t j = b0; j < b1; ++j) {
                     const int32_t k = cblk[j];
@@ -2036,6 +2177,8 @@ static void *fin_thread(void *arg) {
                     ++m;
                 F->cnt[r] = m;
             } else { /* copy the r-th chain's blocks out */
+                if (r + 4 < F->n && F->head[r + 4] >= 0)
+                    __builtin_prefetch(&F->cb[F->head[r + 4]]);
                 int32_t o = F->pos[r];
                 for (int32_t x = F->head[r]; x >= 0; x = F->cb[x].next, ++o) {
                     F->out->bt[o] = F->cb[x].ts;
@@ -2073,11 +2216,15 @@ static void pair_finish_team(ax_work *w, ax_chains *pc, ax_out *out) {
         F.tw[t].xcap = 0;
         F.tw[t].err = 0;
     }
+    const int tm = w->n > (1 << 20) && getenv("GAC_TIMING");
+    double tf[5] = {tm ? mono_s() : 0, 0, 0, 0, 0};
     F.ck = malloc((size_t)(nc ? nc : 1) * sizeof(dkey));
     F.phase = 0;
     gac_run_threads(nt, fin_thread, &F);
+    if (tm) tf[1] = mono_s();
     if (F.err_at < 0) {
         sort_desc16(F.ck, nc, nt);
+        if (tm) tf[2] = mono_s();
         F.cb = malloc((size_t)(nbk ? nbk : 1) * sizeof(ax_cb));
         F.head = malloc((size_t)(nc ? nc : 1) * sizeof(int32_t));
         F.cnt = malloc((size_t)(nc ? nc : 1) * sizeof(int32_t));
@@ -2086,6 +2233,7 @@ static void pair_finish_team(ax_work *w, ax_chains *pc, ax_out *out) {
         atomic_store(&F.next, 0);
         atomic_store(&F.wid, 0);
         gac_run_threads(nt, fin_thread, &F);
+        if (tm) tf[3] = mono_s();
     }
     if (F.err_at >= 0) {
         w->err = 1;
@@ -2110,6 +2258,12 @@ static void pair_finish_team(ax_work *w, ax_chains *pc, ax_out *out) {
         atomic_store(&F.next, 0);
         atomic_store(&F.wid, 0);
         gac_run_threads(nt, fin_thread, &F);
+        if (tm) {
+            tf[4] = mono_s();
+            fprintf(stderr, "[gac_axt_chain] finish of %d chains (%d threads): scores %.3f, sort "
+                    "%.3f, overlaps %.3f, copy-out %.3f s\n", nc, nt, tf[1] - tf[0],
+                    tf[2] - tf[1], tf[3] - tf[2], tf[4] - tf[3]);
+        }
     }
     for (int t = 0; t < nt; ++t)
         free(F.tw[t].xs);
@@ -2393,6 +2547,7 @@ typedef struct team_run {
     ax_pre *pre; /* the pair's leaves and tree built on the device, or NULL */
     int32_t p;
     int team, batch, started, pin;
+    _Atomic int done; /* (its pair's chains are in J->out) */
     cpu_set_t cpus; /* (pin) the L3 domain the team runs in */
     pthread_t th;
 } team_run;
@@ -2463,6 +2618,7 @@ static void *team_runner(void *arg) {
     w.pre = R->pre;
     run_pair(R->J, &w, R->p);
     work_free(&w);
+    atomic_store_explicit(&R->done, 1, memory_order_release);
     return NULL;
 }
 
@@ -3646,6 +3802,41 @@ static int score_pairs(gac_ctx *ctx, ax_out *po, const gac_axt_input *in, int64_
     return rc;
 }
 
+/* every chain's pair and score in list order (pairs in input order), in
+ * slices of the chain list */
+typedef struct list_job {
+    const ax_out *po;
+    const int64_t *c0;
+    int64_t np, nc;
+    int32_t *cpair;
+    int64_t *gsc;
+    _Atomic int64_t next;
+} list_job;
+
+static void *list_thread(void *arg) {
+    list_job *L = arg;
+    for (;;) {
+        const int64_t a = atomic_fetch_add(&L->next, 1 << 16);
+        if (a >= L->nc)
+            return NULL;
+        const int64_t b = a + (1 << 16) < L->nc ? a + (1 << 16) : L->nc;
+        int64_t lo = 0, hi = L->np - 1; /* the pair of chain a: last p with c0[p] <= a */
+        while (lo < hi) {
+            const int64_t m = (lo + hi + 1) >> 1;
+            if (L->c0[m] <= a)
+                lo = m;
+            else
+                hi = m - 1;
+        }
+        for (int64_t i = a, p = lo; i < b; ++i) {
+            while (L->c0[p + 1] <= i)
+                ++p;
+            L->cpair[i] = (int32_t)p;
+            L->gsc[i] = L->po[p].gsc[i - L->c0[p]];
+        }
+    }
+}
+
 /* score_pairs of the pairs not scored yet, unless one of them failed (the
  * caller reports the first pair's error) */
 static int score_rest(gac_ctx *ctx, ax_out *po, const gac_axt_input *in, int64_t np,
@@ -4081,9 +4272,15 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
                     dev_started = 0;
                 }
                 stage("kd-tree DP (the pool's and the device's pairs)", &tclock);
+                /* with the teams that are done by now (the smaller ones) */
+                int32_t *cand = malloc((size_t)np * 4);
+                int64_t ncand = 0;
+                for (int64_t k = 0; k < np; ++k)
+                    if (k >= big || atomic_load_explicit(&tr[k].done, memory_order_acquire))
+                        cand[ncand++] = order[k];
                 if (rc == GAC_OK && (!D || D->rc == GAC_OK))
-                    rc = score_rest(ctx, po, in, np, order + big, np - big,
-                                    pool + (D ? D->nt : 0), &tclock);
+                    rc = score_rest(ctx, po, in, np, cand, ncand, pool + (D ? D->nt : 0), &tclock);
+                free(cand);
             }
         }
         for (int64_t k = 0; k < big; ++k)
@@ -4155,13 +4352,11 @@ int gac_axt_chain(gac_ctx *ctx, const int32_t mat[16], const gac_gapcalc *g,
         nc = c0[np];
         int32_t *cpair = malloc((size_t)(nc ? nc : 1) * 4);
         int64_t *gsc = malloc((size_t)(nc ? nc : 1) * 8);
-        if (rc == GAC_OK)
-            for (int64_t p = 0; p < np; ++p) {
-                for (int64_t i = c0[p]; i < c0[p + 1]; ++i)
-                    cpair[i] = (int32_t)p;
-                if (po[p].n_chains)
-                    memcpy(gsc + c0[p], po[p].gsc, (size_t)po[p].n_chains * 8);
-            }
+        if (rc == GAC_OK) {
+            list_job L = {po, c0, np, nc, cpair, gsc, 0};
+            atomic_init(&L.next, 0);
+            run_threads(nthreads, list_thread, &L);
+        }
         stage("scores in list order", &tclock);
         if (rc == GAC_OK) {
             /* minScore filter; slAddHead onto the master list (reversed),

@@ -17,6 +17,7 @@ for i in $(seq 1 ${REPS:-2}); do
       default) env="" ;;
       gpu) env="GAC_AXT_DP=gpu" ;;
       tt0) env="GAC_DP_TEAMTREE=0" ;;
+      early0) env="GAC_AXT_SCORE_EARLY=0" ;;
       hosttt) env="GAC_DP_GPU_MAX=0" ;;
       dt0_*) env="GAC_DP_DEVTREE=0 GAC_DP_GPU_MAX=${mode#dt0_}" ;;
       us*_*) u=${mode%%_*}; env="GAC_DP_DEV_US=${u#us} GAC_DP_GPU_MAX=${mode#*_}" ;;
