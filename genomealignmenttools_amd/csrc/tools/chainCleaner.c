@@ -553,8 +553,8 @@ static void write_subchain(FILE *f, const state *S, int32_t ix, const subchain *
 
 /* ================================================================ GPU scores
  * Cached by (chain, content version, s, e).  A range of a chain that lost
- * blocks selects the same blocks as in the original chain unless a removed
- * block falls inside it: such ranges keep version 0. */
+ * blocks selects the original blocks minus the removed ones inside it; the
+ * content version is their count (0: the original selection). */
 typedef struct sres {
     int64_t g, l;
     int32_t ali;
@@ -650,14 +650,17 @@ static const sres *cache_get(qkey k) {
 static qkey make_key_cur(const state *S, int32_t ix, int32_t s, int32_t e, const subchain *pc) {
     const ichain *x = &S->ich[ix];
     int32_t ver = 0;
-    if (x->version) {
+    if (x->rm_n) {
         const int64_t ci = x->ci;
-        /* a whole-chain selection (chainSubsetOnT's easy case, the original
-         * bounds) follows every version; else the current selection -- a
-         * subset of the original one (blocks only ever go) -- differs from
-         * it iff a removed block is in [s, e): tEnd > s and tStart < e */
+        /* the key's version is the number of removed blocks the selection
+         * would hold: blocks only ever go, so the current selection is the
+         * original one minus those, and equal counts at two times mean the
+         * same blocks (a key stays valid across removals elsewhere in the
+         * chain).  A whole-chain selection (chainSubsetOnT's easy case, the
+         * original bounds) holds every removed block; else those with
+         * tEnd > s and tStart < e (the removed list is sorted and disjoint) */
         if (s <= S->c.tstart[ci] && e >= S->c.tend[ci]) {
-            ver = x->version;
+            ver = x->rm_n;
         } else {
             int32_t lo = 0, hi = x->rm_n; /* first removed block with tEnd > s */
             while (lo < hi) {
@@ -667,8 +670,15 @@ static qkey make_key_cur(const state *S, int32_t ix, int32_t s, int32_t e, const
                 else
                     lo = m + 1;
             }
-            if (lo < x->rm_n && x->rm_s[lo] < e)
-                ver = x->version;
+            int32_t l2 = lo, h2 = x->rm_n; /* first from there with tStart >= e */
+            while (l2 < h2) {
+                const int32_t m = (l2 + h2) >> 1;
+                if (x->rm_s[m] >= e)
+                    h2 = m;
+                else
+                    l2 = m + 1;
+            }
+            ver = l2 - lo;
         }
         if (g_check_keys) { /* (test hook: the rule as counts of the two selections) */
             const subchain cur = pc ? *pc : subset(S, ix, s, e);
@@ -676,7 +686,7 @@ static qkey make_key_cur(const state *S, int32_t ix, int32_t s, int32_t e, const
             const subchain org = subset_of(S->c.bt + b0, S->c.bq + b0, S->c.bs + b0,
                                            (int32_t)(S->c.blk_off[ci + 1] - b0), S->c.tstart[ci],
                                            S->c.tend[ci], s, e);
-            if ((cur.easy || cur.nb != org.nb) != (ver != 0)) {
+            if ((cur.easy ? x->rm_n : org.nb - cur.nb) != ver) {
                 for (int32_t k = 0; k < x->rm_n; ++k)
                     if (x->rm_e[k] > s - 1000 && x->rm_s[k] < e + 1000)
                         fprintf(stderr, "removed[%d] = [%d, %d)\n", k, x->rm_s[k], x->rm_e[k]);
@@ -750,7 +760,8 @@ static void score_keys(state *S, const qkey *in, int64_t n) {
         int32_t ns = 0;
         int64_t nbk = 0;
         for (int64_t i = n0; i < m; ++i) {
-            must_assert(q[i].version == S->ich[q[i].ich].version, "key of the current version");
+            must_assert(q[i].version == make_key(S, q[i].ich, q[i].s, q[i].e).version,
+                        "key of the current blocks");
             if (ns == 0 || sel[ns - 1] != q[i].ich) {
                 sel[ns++] = q[i].ich;
                 nbk += S->ich[q[i].ich].nb;
