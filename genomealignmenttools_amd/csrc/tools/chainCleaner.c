@@ -1585,6 +1585,14 @@ int main(int argc, char *argv[]) {
                          interest.key[order[oi]]);
         free(order);
     }
+    /* the first pass's keys of every list (and its pairs), made while the
+     * device may still be opening: host work only */
+    int32_t *border = malloc((size_t)(breakhash.n ? breakhash.n : 1) * 4);
+    const int32_t nborder = gt_khash_order(&breakhash, border);
+    qkey *q0 = NULL;
+    int64_t nq0 = 0, capq0 = 0;
+    for (int32_t oi = 0; oi < nborder; ++oi)
+        list_keys(&S, bh_head[border[oi]], sdata_file ? 0 : doPairs, 1, &q0, &nq0, &capq0);
     S.ctx = gt_device_join(&dev);
     {
         const size_t nn = (size_t)(S.nich ? S.nich : 1);
@@ -1641,13 +1649,11 @@ int main(int argc, char *argv[]) {
         doPairs = 0;
     }
     {
-        int32_t *order = malloc((size_t)(breakhash.n ? breakhash.n : 1) * 4);
-        const int32_t no = gt_khash_order(&breakhash, order);
+        int32_t *order = border;
+        const int32_t no = nborder;
         /* the first pass over every list (and its pairs) in one batch */
-        qkey *q = NULL;
-        int64_t nq = 0, capq = 0;
-        for (int32_t oi = 0; oi < no; ++oi)
-            list_keys(&S, bh_head[order[oi]], doPairs, 1, &q, &nq, &capq);
+        qkey *q = q0;
+        int64_t nq = nq0, capq = capq0;
         g_site = 0;
         score_keys(&S, q, nq);
         g_site = 2;
