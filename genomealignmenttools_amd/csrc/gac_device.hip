@@ -30,6 +30,8 @@ int plan_grid(int64_t n);
 int persistent_blocks_per_cu(int which, int sym);
 hipError_t launch_plan(const ScoreArgs &a, hipStream_t s);
 hipError_t launch_tilemap(const ScoreArgs &a, hipStream_t s);
+hipError_t launch_plan_lb(const ScoreArgs &a, hipStream_t s);
+bool plan_lb();
 hipError_t launch_tile(const ScoreArgs &a, int grid, hipStream_t s);
 hipError_t launch_combine(const ScoreArgs &a, int grid, hipStream_t s);
 hipError_t launch_small(const ScoreArgs &a, const Range *rin, SmallOut *out, hipStream_t s);
@@ -140,7 +142,7 @@ struct Prof {
 
 }  // namespace
 
-constexpr size_t kStatusBytes = 128;  // status[0..8)
+constexpr size_t kStatusBytes = 128;  // status[0..9) (see ScoreArgs::status)
 
 // held by every entry point that uses a context (see gac_ctx::mu); it also
 // parks the small-batch server (k_small_server) first, so that nothing else
@@ -203,6 +205,7 @@ struct gac_ctx {
     int32_t *pb0 = nullptr;                  // [ws_n]
     int32_t *agg = nullptr;                  // [plan workgroups]
     int32_t *plan_off = nullptr;             // [plan workgroups]
+    unsigned long long *lbflag = nullptr;    // [plan workgroups] k_plan_lb's look-back words
     int32_t *gflat = nullptr;                // [ws_n]
     int32_t *status = nullptr;               // [8]
     int64_t ws_tiles = 0;
@@ -449,7 +452,7 @@ extern "C" void gac_close(gac_ctx *c) {
     }
     free_genome(c->g[0]);
     free_genome(c->g[1]);
-    void *bufs[] = {c->d_small,  c->d_gap_tab, c->rdesc,    c->nblk,     c->goff, c->pb0, c->agg, c->plan_off, c->gflat,
+    void *bufs[] = {c->d_small,  c->d_gap_tab, c->rdesc,    c->nblk,     c->goff, c->pb0, c->agg, c->plan_off, c->lbflag, c->gflat,
                     c->status,   c->tile_r0,  c->sum_head, c->sum_tail,
                     c->sup_head, c->sup_tail, c->sup_tail_r,
                     c->d_ranges, c->d_g,      c->d_l,      c->d_ali};
@@ -2357,10 +2360,11 @@ static int ensure_ws(gac_ctx *c, int64_t n, int64_t max_tiles, hipStream_t s) {
     }
     if (n > c->ws_n) {
         int64_t cap = n + n / 2 + 1024;
-        void *bufs[] = {c->rdesc, c->nblk, c->goff, c->pb0, c->agg, c->plan_off, c->gflat};
+        void *bufs[] = {c->rdesc, c->nblk, c->goff, c->pb0, c->agg, c->plan_off, c->lbflag, c->gflat, c->lbflag};
         for (void *p : bufs)
             if (p) hipFree(p);
         c->rdesc = nullptr;
+        c->lbflag = nullptr;
         c->nblk = c->goff = c->pb0 = c->plan_off = c->gflat = nullptr;
         c->agg = nullptr;
         const int64_t G = plan_grid(cap) + 2;
@@ -2371,6 +2375,12 @@ static int ensure_ws(gac_ctx *c, int64_t n, int64_t max_tiles, hipStream_t s) {
         HIPCHK(hipMalloc(&c->gflat, cap * 4));
         HIPCHK(hipMalloc(&c->agg, G * 4));
         HIPCHK(hipMalloc(&c->plan_off, G * 4));
+        HIPCHK(hipMalloc(&c->lbflag, G * 8));
+        HIPCHK(hipMemsetAsync(c->lbflag, 0, G * 8, s));  // (no tag: "not yet")
+        // (this memset returns success but leaves hipErrorInvalidValue as the
+        // thread's last error on this runtime, which the next launch check
+        // would report as its own: consumed here; r06lbdbg)
+        (void)hipGetLastError();
         c->ws_n = cap;
     }
     if (!c->status) {
@@ -2771,6 +2781,7 @@ static int score_device_split(gac_ctx *c, const ScoreArgs &a_base, const Range *
         a.pb0 = c->pb0;
         a.agg = c->agg;
         a.plan_off = c->plan_off;
+        a.lbflag = c->lbflag;
         a.gflat = c->gflat;
         a.status = c->status;
         a.tile_r0 = c->tile_r0;
@@ -2785,8 +2796,12 @@ static int score_device_split(gac_ctx *c, const ScoreArgs &a_base, const Range *
         a.cap_tiles = (int32_t)(c->ws_tiles < INT32_MAX ? c->ws_tiles : INT32_MAX);
         {
             PROF_BEGIN(GAC_K_PLAN);
-            HIPCHK(launch_plan(a, s));
-            HIPCHK(launch_tilemap(a, s));
+            if (plan_lb()) {
+                HIPCHK(launch_plan_lb(a, s));
+            } else {
+                HIPCHK(launch_plan(a, s));
+                HIPCHK(launch_tilemap(a, s));
+            }
             PROF_END(GAC_K_PLAN);
         }
         {

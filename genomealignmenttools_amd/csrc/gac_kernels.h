@@ -155,9 +155,11 @@ struct ScoreArgs {
     int32_t *sup_tail_r; // [U]   that range, or -1
     int32_t *agg;        // [G]   window blocks of each plan workgroup (k_plan; saturated)
     int32_t *plan_off;   // [G+1] flat offset of plan workgroup w
-    int32_t *status;     // [8]   W (flat blocks, saturated), T (tiles), 1 = workspace too
+    unsigned long long *lbflag;  // [G] k_plan_lb's look-back words {value, call tag, state}
+    int32_t *status;     // [32]  W (flat blocks, saturated), T (tiles), 1 = workspace too
                          //       small; status[5]: a window lay outside its chain (k_plan<true>,
-                         //       published to host_status[3] and cleared)
+                         //       published to host_status[3] and cleared); status[8]:
+                         //       k_plan_lb's workgroup tickets (re-armed by the last one)
     int32_t *host_status;  // pinned host words: status[0..4) + call_tag (k_scan_agg)
     int32_t call_tag;
     int32_t cap_tiles;   // tile_r0 / sum_head / sum_tail capacity

@@ -835,10 +835,11 @@ __device__ long long scan_totals(const ScoreArgs &a, int G, long long *s_wsum) {
 // call's sequence number, straight into the host's pinned status words: the
 // host learns whether the workspace sufficed as soon as this kernel ends,
 // while k_tilemap / k_tile / the folds still run.
-__device__ __forceinline__ void publish_status(const ScoreArgs &a, long long W) {
+// bad: a window lay outside its chain (k_plan<true> sets status[5], read
+// here and cleared for the next call; k_plan_lb carries it in its words)
+__device__ __forceinline__ void publish_status(const ScoreArgs &a, long long W, int32_t bad) {
     const long long T = (W + kTileBlocks - 1) / kTileBlocks;
     const bool over = W >= 0x7fffffffLL || T > a.cap_tiles;
-    const int32_t bad = a.status[5];  // (k_plan<true>; cleared for the next call)
     const int32_t st[4] = {(int32_t)W, (int32_t)T, over ? 1 : 0, bad};
     for (int k = 0; k < 4; ++k) {
         a.status[k] = k == 3 ? 0 : st[k];
@@ -853,7 +854,7 @@ __global__ void __launch_bounds__(kPlanWG) k_scan_agg(ScoreArgs a) {
     __shared__ long long s_wsum[kPlanWG / kWave];
     const int G = (int)((a.n + kPlanWG - 1) / kPlanWG);
     const long long W = scan_totals(a, G, s_wsum);
-    if (threadIdx.x == 0) publish_status(a, W);
+    if (threadIdx.x == 0) publish_status(a, W, a.status[5]);
 }
 
 // ------------------------------------------------------------ k_tilemap --
@@ -906,7 +907,7 @@ __global__ void __launch_bounds__(kPlanWG) k_tilemap_fused(ScoreArgs a) {
         pre += s_part[1][k];
     }
     const long long W = tot > 0x7fffffffLL ? 0x7fffffffLL : tot;
-    if (w == 0 && tid == 0) publish_status(a, W);
+    if (w == 0 && tid == 0) publish_status(a, W, a.status[5]);
     const long long T = (W + kTileBlocks - 1) / kTileBlocks;
     if (W >= 0x7fffffffLL || T > a.cap_tiles) return;  // the host grows the workspace, reruns
     if (tid == 0) a.plan_off[w] = (int32_t)pre;
@@ -919,6 +920,146 @@ __global__ void __launch_bounds__(kPlanWG) k_tilemap_fused(ScoreArgs a) {
         const int64_t end = (int64_t)g + nb;
         for (int64_t t = ((int64_t)g + kTileBlocks - 1) / kTileBlocks; t * kTileBlocks < end; ++t)
             a.tile_r0[t] = (int32_t)i;
+    }
+}
+
+// ------------------------------------------------------------ k_plan_lb --
+// k_plan, k_scan_agg and k_tilemap as ONE pass (a single-pass scan with
+// decoupled look-back): a workgroup takes a ticket (tickets follow the order
+// the chip started the workgroups, so every workgroup it waits for is already
+// running), plans its 256 ranges, publishes its window-block total, adds up
+// its predecessors' words back to the first one holding an inclusive prefix,
+// publishes its own inclusive prefix, and writes gflat and its tiles'
+// tile_r0 straight away.  A word is self-contained -- {state, call tag, bad
+// window seen, value} in 64 bits -- so the words need no ordering against
+// other memory: relaxed agent-scope atomics (coherent across the XCDs' L2s,
+// no L2 write-back or invalidate per workgroup; a release/acquire pair per
+// word cost 28 ms per 13 M-window call, r06lb).  The tag makes an earlier
+// call's words read as "not yet", so nothing is cleared per call.  The last
+// ticket publishes {W, T, overflow, bad} (publish_status) and re-arms the
+// ticket counter.  Saves the per-range goff and agg round trip through HBM
+// and two launches (C5 fills, 13.2 M windows: k_plan + k_scan_agg +
+// k_tilemap = 0.25 + 0.07 + 0.04 ms, r06final).
+constexpr unsigned long long kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbBad = 1ull << 31;
+constexpr unsigned long long kLbTagMask = 0x3fffffffull << 32;
+
+__device__ __forceinline__ unsigned long long lb_word(long long v, int32_t tag, bool bad,
+                                                      unsigned long long state) {
+    const unsigned long long sv = (unsigned long long)(v < 0x7fffffffLL ? v : 0x7fffffffLL);
+    return state | ((unsigned long long)(tag & 0x3fffffff) << 32) | (bad ? kLbBad : 0ull) | sv;
+}
+
+// ranges per k_plan_lb workgroup: kLbSlabs slabs of 256 (fewer workgroups,
+// so fewer look-back words per range; r06lb3: one slab per workgroup took
+// 0.64 ms for the 13.2 M C5 fills against 0.36 ms for the three launches)
+constexpr int kLbSlabs = 8;
+constexpr int kLbRanges = kLbSlabs * kPlanWG;
+int plan_lb_grid(int64_t n) { return (int)((n + kLbRanges - 1) / kLbRanges); }
+
+template <bool WIN>
+__global__ void __launch_bounds__(kPlanWG, 8) k_plan_lb(ScoreArgs a) {
+    __shared__ long long s_wsum[kPlanWG / kWave];
+    __shared__ int s_ticket, s_bad;
+    __shared__ long long s_pre;
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        s_ticket = __hip_atomic_fetch_add(&a.status[8], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_bad = 0;
+    }
+    __syncthreads();
+    const int w = s_ticket;
+    const int64_t i0 = (int64_t)w * kLbRanges + tid;
+    int nbk[kLbSlabs];
+    long long exk[kLbSlabs];
+    long long agg = 0;
+#pragma unroll
+    for (int k = 0; k < kLbSlabs; ++k) {
+        const int64_t i = i0 + (int64_t)k * kPlanWG;
+        int nb = 0;
+        if (i < a.n) {
+            bool bad = false;
+            const RangeDesc d = WIN ? plan_window(a, a.wins[i], bad) : plan_range(a, a.ranges[i]);
+            if (WIN && bad) s_bad = 1;
+            a.rdesc[i] = d;
+            a.nblk[i] = nb = d.nblk;
+            a.pb0[i] = d.b0;
+            if (nb == 0) {
+                a.out_g[i] = 0;
+                a.out_ali[i] = 0;
+                if (a.want_local) a.out_l[i] = 0;
+            }
+        }
+        nbk[k] = nb;
+    }
+#pragma unroll
+    for (int k = 0; k < kLbSlabs; ++k) {  // slab by slab: range order
+        long long tot;
+        exk[k] = agg + wg_exclusive_scan(nbk[k], s_wsum, tot);  // (its barriers order s_bad)
+        agg += tot;
+    }
+    if (tid < kWave) {  // wave 0: the look-back, 64 predecessors' words per load
+        unsigned long long *F = a.lbflag;
+        const unsigned long long tagbits = (unsigned long long)(a.call_tag & 0x3fffffff) << 32;
+        bool bad = s_bad != 0;
+        long long pre = 0;
+        if (tid == 0)
+            __hip_atomic_store(&F[w], lb_word(agg, a.call_tag, bad, w == 0 ? kLbInc : kLbAgg),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (w > 0) {
+            for (int j = w - 1;;) {
+                // lane k: the word of workgroup j - k (before workgroup 0: an
+                // inclusive zero)
+                const int q = j - tid;
+                const unsigned long long f =
+                    q >= 0 ? __hip_atomic_load(&F[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           : (kLbInc | tagbits);
+                const bool ok = (f & kLbTagMask) == tagbits && (f >> 62) != 0;
+                const bool inc = ok && (f >> 62) == 2;
+                const unsigned long long incs = __ballot(inc);
+                const unsigned long long oks = __ballot(ok);
+                // the words up to the nearest inclusive one (all 64 if none)
+                const int upto = incs ? __builtin_ctzll(incs) : kWave - 1;
+                const unsigned long long need = upto == kWave - 1 ? ~0ull : ((2ull << upto) - 1);
+                if ((oks & need) != need) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                const bool mine = tid <= upto;
+                pre += wave_sum(mine ? (long long)(f & 0x7fffffffull) : 0ll);
+                bad = bad || __ballot(mine && (f & kLbBad)) != 0ull;
+                if (incs) break;
+                j -= kWave;
+            }
+            if (pre > 0x7fffffffLL) pre = 0x7fffffffLL;
+            if (tid == 0)
+                __hip_atomic_store(&F[w], lb_word(pre + agg, a.call_tag, bad, kLbInc),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (tid == 0) {
+            s_pre = pre;
+            if (w == (int)gridDim.x - 1) {  // every predecessor's word is in: W is known
+                const long long W = pre + agg;
+                __hip_atomic_store(&a.status[8], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                publish_status(a, W > 0x7fffffffLL ? 0x7fffffffLL : W, bad ? 1 : 0);
+            }
+        }
+    }
+    __syncthreads();
+    const long long pre = s_pre;
+#pragma unroll
+    for (int k = 0; k < kLbSlabs; ++k) {
+        const int64_t i = i0 + (int64_t)k * kPlanWG;
+        if (i >= a.n) break;
+        const int nb = nbk[k];
+        const long long g = pre + exk[k];
+        a.gflat[i] = (int32_t)(g < 0x7fffffffLL ? g : 0x7fffffffLL);
+        if (nb > 0 && g + nb < 0x7fffffffLL) {
+            // (tiles past the workspace are left out; the last ticket's status
+            // words tell k_tile, the folds and the host to grow it and rerun)
+            const int64_t end = g + nb, cap = a.cap_tiles;
+            for (int64_t t = (g + kTileBlocks - 1) / kTileBlocks; t * kTileBlocks < end && t < cap; ++t)
+                a.tile_r0[t] = (int32_t)i;
+        }
     }
 }
 
@@ -2194,6 +2335,22 @@ hipError_t launch_plan(const ScoreArgs &a, hipStream_t s) {
         hipLaunchKernelGGL(k_plan<true>, dim3((unsigned)plan_grid(a.n)), dim3(kPlanWG), 0, s, a);
     else
         hipLaunchKernelGGL(k_plan<false>, dim3((unsigned)plan_grid(a.n)), dim3(kPlanWG), 0, s, a);
+    return hipGetLastError();
+}
+
+// GAC_PLAN_LB=1: the single-pass k_plan_lb instead of k_plan + the tile map
+// (opt-in: see DESIGN 4.4 for its A/Bs)
+// (read per call, like GAC_UNFUSED_MAP: the tests switch paths in one process)
+bool plan_lb() {
+    const char *e = getenv("GAC_PLAN_LB");
+    return e && e[0] == '1';
+}
+
+hipError_t launch_plan_lb(const ScoreArgs &a, hipStream_t s) {
+    if (a.wins)
+        hipLaunchKernelGGL(k_plan_lb<true>, dim3((unsigned)plan_lb_grid(a.n)), dim3(kPlanWG), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_plan_lb<false>, dim3((unsigned)plan_lb_grid(a.n)), dim3(kPlanWG), 0, s, a);
     return hipGetLastError();
 }
 

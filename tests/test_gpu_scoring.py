@@ -598,20 +598,26 @@ def test_small_batch_server(monkeypatch, server, idle_us):
 
 
 def test_unfused_tile_map_path(monkeypatch):
-    """Batches of more than 1 M ranges scan the plan-workgroup totals in a
-    separate one-workgroup launch (k_scan_agg + k_tilemap); smaller ones fold
-    that scan into k_tilemap_fused.  Both give the oracle's scores
-    (GAC_UNFUSED_MAP forces the large-batch path on a small batch)."""
+    """The planning of a batch has three forms: k_plan followed by
+    k_tilemap_fused (the default up to 1 M ranges) or by k_scan_agg +
+    k_tilemap (GAC_UNFUSED_MAP forces the large-batch form on a small
+    batch), and the single pass k_plan_lb (GAC_PLAN_LB=1: plan + scan with
+    decoupled look-back + tile map).  All give the oracle's scores, and the
+    look-back's tagged words of one call never leak into the next."""
     from genomealignmenttools_amd import synth
     tg, qg, ca = synth.small_case(seed=31, n_chains=300, max_blocks=500)
     e, cs = _setup(None, tg, qg, ca)
     R = _ranges(ca, np.random.default_rng(31), per_chain=6)
     og, ol, oa = _oracle(tg, qg).score_ranges(ca, R)
-    g, l, a = e.score_ranges(cs, R, want_local=True)
-    assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
-    monkeypatch.setenv("GAC_UNFUSED_MAP", "1")
-    g, l, a = e.score_ranges(cs, R, want_local=True)
-    assert np.array_equal(g, og) and np.array_equal(l, ol) and np.array_equal(a, oa)
+    for env in ({"GAC_PLAN_LB": "1"}, {}, {"GAC_UNFUSED_MAP": "1"}, {"GAC_PLAN_LB": "1"}):
+        monkeypatch.delenv("GAC_PLAN_LB", raising=False)
+        monkeypatch.delenv("GAC_UNFUSED_MAP", raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        for n in (len(R), 257, 1):  # several plan workgroups, one partial, one range
+            g, l, a = e.score_ranges(cs, R[:n], want_local=True)
+            assert np.array_equal(g, og[:n]) and np.array_equal(l, ol[:n]), (env, n)
+            assert np.array_equal(a, oa[:n]), (env, n)
 
 
 @pytest.mark.parametrize("want_local", [False, True])
